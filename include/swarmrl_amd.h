@@ -1,0 +1,195 @@
+/*
+ * swarmrl_amd.h -- C ABI of the MI355X active-Brownian swarm engine.
+ *
+ * This is the drop-in boundary that replaces the ESPResSo calls made by
+ * SwarmRL's engine adapter (reference: swarmrl/engine/espresso.py).  Every
+ * entry point below names the reference call site it stands in for.  The
+ * ABI uses only plain C types and pointers: no torch, no HIP types (a HIP
+ * stream is passed as `void*`).  All functions return SWARM_OK (0) or an
+ * error code; the message of the last error on the calling thread is
+ * returned by swarm_last_error().  No C++ exception crosses this boundary.
+ *
+ * Error codes map onto the Python exceptions the reference raises:
+ *   SWARM_EINVAL    -> ValueError   (bad configuration, espresso.py:180-182, 252-288)
+ *   SWARM_ESTATE    -> RuntimeError (mutation after first integrate, espresso.py:300-305)
+ *   SWARM_EDEVICE   -> RuntimeError (HIP runtime failure)
+ *   SWARM_ECAPACITY -> ValueError   (size beyond what this build supports)
+ *
+ * Units: simulation units of the reference (espresso.py:211-234):
+ * length 1 um, time 1 s, energy 293 K * k_B.
+ *
+ * State representation (identical in the CPU oracle and on the GPU):
+ *   position  : per axis a uint32 fraction of the box (q * L / 2^32) plus an
+ *               int32 image counter; unwrapped x = (img + q / 2^32) * L.
+ *   orientation (2-D): uint32 angle, theta = a * 2 pi / 2^32.
+ * Index g = env * n_particles + i.  Device arrays are axis-major [3][E*N].
+ */
+#ifndef SWARMRL_AMD_H
+#define SWARMRL_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SWARM_MAX_SPECIES 16
+#define SWARM_MAX_CONES 16
+#define SWARM_MAX_DETECTED_TYPES 8
+
+#define SWARM_OK 0
+#define SWARM_EINVAL 1
+#define SWARM_ESTATE 2
+#define SWARM_EDEVICE 3
+#define SWARM_ECAPACITY 4
+
+/* Physical parameters of one engine (all envs share them).
+ * Mirrors MDParams (espresso.py:30-88) after unit conversion, plus the
+ * per-particle friction/mass registered by add_colloid_on_point
+ * (espresso.py:376-413).  A "species" is one distinct
+ * (radius, gamma_t, gamma_r, mass, rinertia) combination. */
+typedef struct swarm_params {
+  int32_t n_dims;   /* 2 (3-D is not implemented in this build) */
+  int32_t periodic; /* MDParams.periodic (espresso.py:270) */
+  double box[3];    /* box_l (espresso.py:267) */
+  double time_step; /* system.time_step (espresso.py:268) */
+  double kT;        /* Brownian thermostat kT (espresso.py:1171, 1179-1184) */
+  double wca_epsilon; /* WCA epsilon (espresso.py:814-819) */
+  uint64_t seed;    /* thermostat seed (espresso.py:1183) */
+  int32_t n_species;
+  int32_t reserved0;
+  double radius[SWARM_MAX_SPECIES];
+  double gamma_t[SWARM_MAX_SPECIES];  /* 6 pi eta r  (espresso.py:108-113) */
+  double gamma_r[SWARM_MAX_SPECIES];  /* 8 pi eta r^3 */
+  double mass[SWARM_MAX_SPECIES];     /* used for the BD thermal velocity */
+  double rinertia[SWARM_MAX_SPECIES]; /* used for the BD thermal omega */
+} swarm_params_t;
+
+/* Raw device pointers of the SoA state, for zero-copy consumers. */
+typedef struct swarm_device_views {
+  uint32_t *q;        /* [3][E*N] */
+  int32_t *img;       /* [3][E*N] */
+  uint32_t *ang;      /* [E*N]    */
+  float *f_swim;      /* [E*N]    */
+  float *torque_z;    /* [E*N]    */
+  float *f_ext;       /* [3][E*N] */
+  float *vel;         /* [3][E*N] (written by the last sub-step of a run) */
+  float *omega_z;     /* [E*N]    */
+  uint8_t *species;   /* [N]      */
+  int32_t n_envs;
+  int32_t n_particles;
+} swarm_device_views_t;
+
+/* Vision-cone parameters (SubdividedVisionCones,
+ * swarmrl/observables/subdivided_vision_cones.py:25-60). */
+typedef struct swarm_vision_params {
+  float vision_range;
+  float vision_half_angle;
+  int32_t n_cones;
+  int32_t n_types;                       /* len(detected_types) */
+  int32_t detected_types[SWARM_MAX_DETECTED_TYPES];
+  float rims[SWARM_MAX_CONES + 1];       /* -a + k*2a/n, computed in fp32 */
+} swarm_vision_params_t;
+
+typedef struct swarm_engine swarm_engine_t;
+
+/* Thread-local message of the last failing call. */
+const char *swarm_last_error(void);
+
+/* Engine construction: replaces espressomd.System(...) + _init_system +
+ * part.add for all particles (espresso.py:192-196, 236-288, 415-441).
+ * `species` is [n_particles]: index into the per-species arrays of params. */
+int swarm_engine_create(const swarm_params_t *params, int32_t n_envs,
+                        int32_t n_particles, const int32_t *species,
+                        swarm_engine_t **out);
+void swarm_engine_destroy(swarm_engine_t *e);
+
+/* Bind all later launches to a HIP stream (hipStream_t as void*). */
+int swarm_engine_set_stream(swarm_engine_t *e, void *hip_stream);
+
+/* Initial state from host fp64 arrays pos[E][N][3] (unwrapped) and
+ * dir[E][N][3]; replaces part.add(pos=...) + _rotate_colloid_to_2d
+ * (espresso.py:428-449). */
+int swarm_engine_upload_state(swarm_engine_t *e, const double *pos,
+                              const double *director);
+
+/* Exact state transfer in the engine's own number format (host arrays):
+ * q/img [3][E*N], ang [E*N].  Used for checkpoints and bit-exact parity. */
+int swarm_engine_upload_raw(swarm_engine_t *e, const uint32_t *q,
+                            const int32_t *img, const uint32_t *ang);
+int swarm_engine_download_raw(swarm_engine_t *e, uint32_t *q, int32_t *img,
+                              uint32_t *ang);
+
+/* Synchronous copy of the state to host fp64 arrays [E][N][3]; replaces
+ * the particle property getters used by get_particle_data and the Colloid
+ * snapshot (espresso.py:1216-1225, 1320-1336).  Any pointer may be NULL. */
+int swarm_engine_download_state(swarm_engine_t *e, double *pos_unwrapped,
+                                double *director, double *velocity);
+
+/* Per-particle swim force and z-torque [E*N]; replaces
+ * coll.swimming = {"f_swim": ...} and coll.ext_torque = ...
+ * (espresso.py:1228-1235).  on_device != 0: the pointers are device
+ * pointers read asynchronously on the engine stream. */
+int swarm_engine_set_actions(swarm_engine_t *e, const float *f_swim,
+                             const float *torque_z, int32_t on_device);
+
+/* Per-particle external force [E*N][3] (host); replaces p.ext_force. */
+int swarm_engine_set_external_force(swarm_engine_t *e, const double *f_ext);
+
+/* new_direction handling of manage_forces in 2-D: rotate about +-z so the
+ * director equals dir (espresso.py:1236-1249).  dir [E*N][3], mask [E*N]. */
+int swarm_engine_set_directors(swarm_engine_t *e, const double *dir,
+                               const uint8_t *mask);
+
+/* Steepest-descent overlap removal (espresso.py:1161-1168): n_steps of
+ * dp = clamp(gamma * F, -max_disp, max_disp) per free coordinate. */
+int swarm_engine_remove_overlap(swarm_engine_t *e, int32_t n_steps,
+                                double gamma, double max_displacement);
+
+/* n_steps Brownian-dynamics sub-steps with WCA pair forces; replaces
+ * system.integrator.run(k, reuse_forces=True, recalc_forces=False)
+ * (espresso.py:1304-1306).  Asynchronous on the engine stream. */
+int swarm_engine_integrate(swarm_engine_t *e, int32_t n_steps);
+
+/* Total number of BD sub-steps integrated so far (the noise counter). */
+int64_t swarm_engine_step_count(const swarm_engine_t *e);
+
+int swarm_engine_device_views(swarm_engine_t *e, swarm_device_views_t *v);
+
+/* Vision cones for n_agents agents (indices into [0,N), device int32),
+ * radii[N] device fp32 (radius of the SEEN colloid by list position,
+ * subdivided_vision_cones.py:199-203); out device fp32
+ * [E][n_agents][n_cones][n_types].  Replaces
+ * SubdividedVisionCones.compute_observable (subdivided_vision_cones.py:241-258).
+ * types[N] device int32: particle type of every colloid. */
+int swarm_vision_cone(swarm_engine_t *e, const swarm_vision_params_t *vp,
+                      const int32_t *agent_idx, int32_t n_agents,
+                      const float *radii, const int32_t *types, float *out);
+
+/* Distances to a source for the concentration-field observable and the
+ * gradient-sensing task (concentration_field.py:84-108,
+ * gradient_sensing.py:92-126): for agent a of env e,
+ *   p      = unwrapped_pos / box_scale (fp64),
+ *   d_cur  = || fp32(source/box_scale - p) ||,
+ *   d_prev = same for the history position,
+ * then (if update_history) history <- current.  History is kept as raw
+ * engine coordinates hist_q/hist_img [3][E*n_agents] (device).
+ * init_only != 0: only copy the current positions into the history. */
+int swarm_field_distance(swarm_engine_t *e, const int32_t *agent_idx,
+                         int32_t n_agents, const double source[3],
+                         const double box_scale[3], uint32_t *hist_q,
+                         int32_t *hist_img, float *d_cur, float *d_prev,
+                         int32_t update_history, int32_t init_only);
+
+/* Parity helper: all pairs (i<j) of env `env` closer than `cutoff`
+ * (minimum image if periodic) as int32 [max_pairs][2] (host), count in
+ * *n_pairs; returns SWARM_ECAPACITY if more than max_pairs. */
+int swarm_engine_neighbor_pairs(swarm_engine_t *e, int32_t env, double cutoff,
+                                int32_t *pairs, int32_t max_pairs,
+                                int32_t *n_pairs);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SWARMRL_AMD_H */

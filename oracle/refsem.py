@@ -1,0 +1,197 @@
+"""
+Plain numpy (fp64) restatement of the reference's semantics on the hot path.
+
+TEST INFRASTRUCTURE ONLY.  The reference (/root/reference, pure Python over
+jax/pint/h5py/espressomd) cannot be imported in this image
+(ModuleNotFoundError: jax) and never travels to the GPU box,
+so its behaviour is restated here from its source text, function by
+function, with the file:line it follows.  These restatements are pinned by
+the reference's own known-answer tests (tests/test_oracle_kat.py) and then
+used to check the C oracle's number formats on random inputs.
+"""
+
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+
+# --------------------------------------------------------- schedule (a1)
+def schedule(steps_per_slice: int, steps_per_write: int, calls, write_chunk_size: int):
+    """
+    Restates EspressoMD.integrate's bookkeeping (espresso.py:1251-1308)
+    including _update_traj_holder/_write_traj_chunk_to_file cadence.
+    ``calls`` is a list of n_slices per integrate() call.  Returns one dict
+    per call with step/slice/write indices, traj-holder length and the
+    numbers of manage_forces / calc_reward / integrator.run invocations.
+    """
+    step_idx = slice_idx = write_idx = 0
+    holder = 0
+    out = []
+    n_manage = n_reward = 0
+    runs = []
+    for n_slices in calls:
+        old = slice_idx
+        while step_idx < steps_per_slice * (old + n_slices):
+            if step_idx == steps_per_write * write_idx:
+                holder += 1
+                write_idx += 1
+                if holder >= write_chunk_size:
+                    holder = 0
+            if step_idx == steps_per_slice * slice_idx:
+                slice_idx += 1
+                n_manage += 1
+            to_write = steps_per_write * write_idx - step_idx
+            to_slice = steps_per_slice * slice_idx - step_idx
+            k = min(to_write, to_slice)
+            runs.append(k)
+            n_reward += 1
+            step_idx += k
+        out.append(dict(step_idx=step_idx, slice_idx=slice_idx, write_idx=write_idx,
+                        traj_len=holder, n_manage=n_manage, n_reward=n_reward,
+                        runs=list(runs)))
+    return out
+
+
+# ------------------------------------------------------ placement (a3 init)
+def placement(n, init_radius, center, seed, n_calls_before=0):
+    """
+    add_colloids 2-D placement (espresso.py:91-105, 521-533): per colloid
+    r = R sqrt(U), theta = 2 pi U, then director angle 2 pi U; the director
+    goes through vector_from_angles / angles_from_vector (utils.py:24-34).
+    """
+    rng = np.random.default_rng(seed)
+    pos = np.zeros((n, 3))
+    dirs = np.zeros((n, 3))
+    for i in range(n):
+        r = init_radius * np.sqrt(rng.random())
+        th = 2 * np.pi * rng.random()
+        pos[i] = r * np.array([np.cos(th), np.sin(th), 0]) + center
+        pos[i, 2] = 0
+        a = 2 * np.pi * rng.random()
+        d = np.array([np.sin(np.pi / 2) * np.cos(a), np.sin(np.pi / 2) * np.sin(a),
+                      np.cos(np.pi / 2)])
+        d = d / np.linalg.norm(d)
+        phi = np.arctan2(d[1], d[0])
+        dirs[i] = [np.cos(phi), np.sin(phi), 0.0]
+    return pos, dirs
+
+
+# ----------------------------------------------------------- units (a3)
+K_B = 1.380649e-23
+SIM_ENERGY = 293 * K_B                       # espresso.py:223
+SIM_MASS = SIM_ENERGY / (1e-6) ** 2          # sim_energy / sim_velocity^2
+SIM_DYN_VISC = SIM_MASS / (1e-6 * 1.0)       # sim_mass / (sim_length sim_time)
+
+
+def friction(eta_si, radius_um):
+    """espresso.py:108-113 in simulation units."""
+    eta = eta_si / SIM_DYN_VISC
+    return 6 * np.pi * eta * radius_um, 8 * np.pi * eta * radius_um**3
+
+
+# ------------------------------------------------------- signed angle (a10)
+def signed_angle(my_director, other_director):
+    """calc_signed_angle_between_directors (utils.py:297-332), fp64."""
+    my = np.asarray(my_director, dtype=float)
+    ot = np.asarray(other_director, dtype=float)
+    my = my / np.linalg.norm(my)
+    ot = ot / np.linalg.norm(ot)
+    angle = np.arccos(np.clip(np.dot(ot, my), -1.0, 1.0))
+    orth = np.dot(ot, np.array([-my[1], my[0], my[2]]))
+    return angle * (1 if orth >= 0 else -1)
+
+
+# -------------------------------------------------------- vision cone (a10)
+def vision_cones(positions, directors, types, radii, vision_range, half_angle, n_cones,
+                 detected_types=None, particle_type=0):
+    """
+    SubdividedVisionCones.compute_observable (subdivided_vision_cones.py:
+    105-258) in fp64: for each agent (type == particle_type), sum over ALL
+    colloids j (the `c is not index` filter never removes anything, line 232)
+    of in_range * min(1, 2 r_j / d) * type_mask * in_cone; the self term is
+    NaN-masked to 0 (d = 0 gives NaN angles).
+    """
+    positions = np.asarray(positions, dtype=float)
+    directors = np.asarray(directors, dtype=float)
+    types = np.asarray(types)
+    if detected_types is None:
+        seen = []
+        for t in types:
+            if t not in seen:
+                seen.append(t)
+        detected_types = np.sort(seen)
+    detected_types = np.asarray(detected_types)
+    rims = -half_angle + np.arange(n_cones + 1) * half_angle * 2 / n_cones
+    agents = [i for i, t in enumerate(types) if t == particle_type]
+    out = []
+    for i in agents:
+        acc = np.zeros((n_cones, len(detected_types)))
+        for j in range(len(positions)):
+            dist = positions[j] - positions[i]
+            d = np.linalg.norm(dist)
+            if not d < vision_range or d == 0.0:
+                continue
+            amp = min(1.0, 2 * radii[j] / d)
+            col = np.nonzero(detected_types == types[j])[0]
+            if len(col) == 0:
+                continue
+            ang = signed_angle(directors[i], dist / d)
+            for k in range(n_cones):
+                if rims[k] < ang < rims[k + 1]:
+                    acc[k, col[0]] += amp
+        out.append(acc)
+    return out
+
+
+# ------------------------------------------- concentration / gradient (a11/12)
+def field_distance(pos, source, box_length):
+    """|| fp32(source/L - pos/L) || as the reference computes it
+    (concentration_field.py:100-101; gradient_sensing.py:110-111)."""
+    diff = np.asarray(source, dtype=float) / box_length - np.asarray(pos, dtype=float) / box_length
+    d32 = diff.astype(np.float32)
+    return np.float32(np.sqrt(np.sum(d32.astype(np.float64) ** 2)))
+
+
+def concentration_observable(cur, prev, source, box_length, decay_fn, scale):
+    """scale * (f(d_cur) - f(d_prev)) (concentration_field.py:102-104)."""
+    dc = field_distance(cur, source, box_length)
+    dp = field_distance(prev, source, box_length)
+    return scale * (decay_fn(dc) - decay_fn(dp))
+
+
+def gradient_reward(cur, prev, source, box_length, decay_fn, scale):
+    """clip(scale * (f(d_cur) - f(d_prev)), 0, inf) (gradient_sensing.py:108-121)."""
+    return max(0.0, float(concentration_observable(cur, prev, source, box_length, decay_fn,
+                                                   scale)))
+
+
+# --------------------------------------------------- BD, deterministic (a3)
+def bd_free_deterministic(pos0, theta0, f_swim, torque_z, gamma_t, gamma_r, dt, n_steps):
+    """kT = 0, no pair forces: x += f d(theta)/gamma_t dt, theta += tau/gamma_r dt."""
+    pos = np.array(pos0, dtype=float)
+    th = np.array(theta0, dtype=float)
+    for _ in range(n_steps):
+        d = np.stack([np.cos(th), np.sin(th)], axis=-1)
+        pos[:, :2] += (np.asarray(f_swim)[:, None] * d) / gamma_t * dt
+        th = th + np.asarray(torque_z) / gamma_r * dt
+    return pos, th
+
+
+def wca_force(r_vec, r_i, r_j, eps):
+    """ESPResSo WCA (espresso.py:814-819): sigma = (r_i + r_j) 2^(-1/6)."""
+    sig = (r_i + r_j) * 2 ** (-1 / 6)
+    r = np.linalg.norm(r_vec)
+    if r >= (r_i + r_j):
+        return np.zeros_like(r_vec)
+    s6 = (sig / r) ** 6
+    return 48 * eps / r**2 * (s6 * s6 - 0.5 * s6) * r_vec
+
+
+def expected_msd_2d(kT, gamma_t, t):
+    return 4 * kT / gamma_t * t
+
+
+def expected_orientation_corr(kT, gamma_r, t):
+    return math.exp(-kT / gamma_r * t)

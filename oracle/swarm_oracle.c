@@ -1,0 +1,730 @@
+/*
+ * swarm_oracle.c -- CPU restatement of the SwarmRL rollout hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this code, and only as the checker
+ * (or the timed CPU comparator).  The product (swarmrl_amd/) never links or
+ * calls it.
+ *
+ * What it restates (reference = /root/reference, read as text):
+ *   - overdamped Brownian dynamics with swim force and torque, as configured
+ *     by swarmrl/engine/espresso.py:1179-1186 (thermostat), 376-389 and
+ *     108-113 (per-particle friction 6 pi eta r / 8 pi eta r^3), 431-449
+ *     (2-D: z fixed, rotation about lab z only), 1228-1235 (f_swim along the
+ *     director, ext_torque);
+ *   - the WCA pair force set up at espresso.py:814-819
+ *     (sigma = (r_i + r_j) 2^(-1/6), cutoff = r_i + r_j, epsilon);
+ *   - steepest-descent overlap removal, espresso.py:1161-1168
+ *     (f_max = 0, gamma, max_displacement, n steps);
+ *   - SubdividedVisionCones, swarmrl/observables/subdivided_vision_cones.py:
+ *     105-203 with calc_signed_angle_between_directors,
+ *     swarmrl/utils/utils.py:297-332;
+ *   - the distance part of ConcentrationField
+ *     (swarmrl/observables/concentration_field.py:84-108) and GradientSensing
+ *     (swarmrl/tasks/searching/gradient_sensing.py:92-126).
+ *
+ * The BD/WCA arithmetic of ESPResSo itself is third-party code that is not
+ * in /root/reference (pinned only as ESPResSo dc87ede3..., see
+ * .github/workflows/espresso.yml:24).  Its documented algorithm is restated
+ * here; its Philox noise stream is unknowable, so the noise below is this
+ * project's own counter-based stream (Philox4x32-10 keyed by seed/env,
+ * counter = particle id / step / tag) -- noisy trajectories are pinned
+ * statistically, deterministic (kT = 0) ones by the reference's tests.
+ *
+ * Number formats (shared spec with the GPU path):
+ *   position  = uint32 fraction of the box + int32 image counter,
+ *   angle     = uint32 turn fraction,
+ *   WCA force = sum of per-pair fp32 forces in int64 fixed point (2^-24),
+ *   vision    = sum of per-colloid fp32 amplitudes in int64 fixed point
+ *               (2^-32),
+ * so every sum is exact and independent of neighbour order.  Build with
+ * -ffp-contract=off: every fp32 operation below is rounded separately.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/swarmrl_amd.h"
+
+/* ------------------------------------------------------------------ */
+/* Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11 "Parallel random   */
+/* numbers: as easy as 1, 2, 3").                                      */
+/* ------------------------------------------------------------------ */
+void or_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2],
+                      uint32_t out[4]) {
+  uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+  uint32_t k0 = key_in[0], k1 = key_in[1];
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    uint32_t n1 = (uint32_t)p1;
+    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    uint32_t n3 = (uint32_t)p0;
+    c0 = n0;
+    c1 = n1;
+    c2 = n2;
+    c3 = n3;
+  }
+  out[0] = c0;
+  out[1] = c1;
+  out[2] = c2;
+  out[3] = c3;
+}
+
+/* ------------------------------------------------------------------ */
+/* Elementary functions with a fixed operation sequence (cephes        */
+/* single-precision polynomials) so CPU and GPU round identically.      */
+/* ------------------------------------------------------------------ */
+static float f_from_bits(uint32_t b) {
+  float f;
+  memcpy(&f, &b, 4);
+  return f;
+}
+static uint32_t bits_from_f(float f) {
+  uint32_t b;
+  memcpy(&b, &f, 4);
+  return b;
+}
+
+/* natural log for normal x > 0 */
+float or_logf(float x) {
+  uint32_t b = bits_from_f(x);
+  int e = (int)((b >> 23) & 0xffu) - 126;
+  float m = f_from_bits((b & 0x007fffffu) | 0x3f000000u); /* [0.5, 1) */
+  if (m < 0.70710678118654752440f) {
+    e -= 1;
+    m = m + m;
+    m = m - 1.0f;
+  } else {
+    m = m - 1.0f;
+  }
+  float z = m * m;
+  float y = 7.0376836292e-2f;
+  y = y * m;
+  y = y + -1.1514610310e-1f;
+  y = y * m;
+  y = y + 1.1676998740e-1f;
+  y = y * m;
+  y = y + -1.2420140846e-1f;
+  y = y * m;
+  y = y + 1.4249322787e-1f;
+  y = y * m;
+  y = y + -1.6668057665e-1f;
+  y = y * m;
+  y = y + 2.0000714765e-1f;
+  y = y * m;
+  y = y + -2.4999993993e-1f;
+  y = y * m;
+  y = y + 3.3333331174e-1f;
+  y = y * m;
+  y = y * z;
+  float fe = (float)e;
+  y = y + -2.12194440e-4f * fe;
+  y = y + -0.5f * z;
+  float r = m + y;
+  r = r + 0.693359375f * fe;
+  return r;
+}
+
+/* sin and cos of the angle a * 2 pi / 2^32 */
+void or_sincos_turn(uint32_t a, float *s_out, float *c_out) {
+  uint32_t b = a + 0x20000000u; /* shift by 1/8 turn */
+  uint32_t quad = b >> 30;
+  int32_t rem = (int32_t)(b & 0x3FFFFFFFu) - 0x20000000; /* [-2^29, 2^29) */
+  float x = (float)rem * 1.46291807926715968e-09f;      /* 2 pi / 2^32 */
+  float z = x * x;
+  float sp = -1.9515295891e-4f;
+  sp = sp * z;
+  sp = sp + 8.3321608736e-3f;
+  sp = sp * z;
+  sp = sp + -1.6666654611e-1f;
+  sp = sp * z;
+  sp = sp * x;
+  float s = sp + x;
+  float cp = 2.443315711809948e-5f;
+  cp = cp * z;
+  cp = cp + -1.388731625493765e-3f;
+  cp = cp * z;
+  cp = cp + 4.166664568298827e-2f;
+  cp = cp * z;
+  cp = cp * z;
+  float c = cp - 0.5f * z;
+  c = c + 1.0f;
+  float so, co;
+  switch (quad) {
+  case 0:
+    so = s;
+    co = c;
+    break;
+  case 1:
+    so = c;
+    co = -s;
+    break;
+  case 2:
+    so = -s;
+    co = -c;
+    break;
+  default:
+    so = -c;
+    co = s;
+    break;
+  }
+  *s_out = so;
+  *c_out = co;
+}
+
+static float asinf_small(float a) { /* |a| <= 0.5 */
+  float z = a * a;
+  float p = 4.2163199048e-2f;
+  p = p * z;
+  p = p + 2.4181311049e-2f;
+  p = p * z;
+  p = p + 4.5470025998e-2f;
+  p = p * z;
+  p = p + 7.4953002686e-2f;
+  p = p * z;
+  p = p + 1.6666752422e-1f;
+  p = p * z;
+  p = p * a;
+  return p + a;
+}
+
+float or_acosf(float x) {
+  if (x < -0.5f) {
+    float t = 1.0f + x;
+    t = 0.5f * t;
+    return 3.14159265358979323846f - 2.0f * asinf_small(sqrtf(t));
+  }
+  if (x > 0.5f) {
+    float t = 1.0f - x;
+    t = 0.5f * t;
+    return 2.0f * asinf_small(sqrtf(t));
+  }
+  return 1.57079632679489661923f - asinf_small(x);
+}
+
+/* calc_signed_angle_between_directors, utils.py:297-332, in fp32 */
+float or_signed_angle(const float my[3], const float other[3]) {
+  float nm = sqrtf(my[0] * my[0] + my[1] * my[1] + my[2] * my[2]);
+  float m0 = my[0] / nm, m1 = my[1] / nm, m2 = my[2] / nm;
+  float no = sqrtf(other[0] * other[0] + other[1] * other[1] +
+                   other[2] * other[2]);
+  float o0 = other[0] / no, o1 = other[1] / no, o2 = other[2] / no;
+  float dot = o0 * m0 + o1 * m1 + o2 * m2;
+  dot = fminf(fmaxf(dot, -1.0f), 1.0f);
+  float ang = or_acosf(dot);
+  float orth = o0 * (-m1) + o1 * m0 + o2 * m2;
+  return orth >= 0.0f ? ang : -ang;
+}
+
+/* Four standard normals for (seed, env, particle id, step, tag):
+ * Box-Muller on the two 32-bit pairs of one Philox4x32-10 block. */
+void or_normals4(uint64_t seed, uint32_t env, uint32_t id, uint64_t step,
+                 uint32_t tag, float out[4]) {
+  uint32_t ctr[4] = {id, (uint32_t)step, (uint32_t)(step >> 32), tag};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32) ^ env};
+  uint32_t r[4];
+  or_philox4x32_10(ctr, key, r);
+  for (int p = 0; p < 2; ++p) {
+    float u = (float)(r[2 * p] >> 9) + 0.5f;
+    u = u * 1.1920928955078125e-07f; /* 2^-23 : u in (0, 1) */
+    float l = or_logf(u);
+    float rad = sqrtf(-2.0f * l);
+    float s, c;
+    or_sincos_turn(r[2 * p + 1], &s, &c);
+    out[2 * p] = rad * c;
+    out[2 * p + 1] = rad * s;
+  }
+}
+
+/* ------------------------------------------------------------------ */
+/* Derived fp32 constants (same derivation as swarm_engine.hip).       */
+/* ------------------------------------------------------------------ */
+typedef struct {
+  float sx[3], inv_sx[3];
+  float mob_dt[SWARM_MAX_SPECIES], sig_t[SWARM_MAX_SPECIES];
+  float rot_dt[SWARM_MAX_SPECIES], sig_r[SWARM_MAX_SPECIES];
+  float inv_gt[SWARM_MAX_SPECIES], inv_gr[SWARM_MAX_SPECIES];
+  float sig_v[SWARM_MAX_SPECIES], sig_w[SWARM_MAX_SPECIES];
+  float cut2[SWARM_MAX_SPECIES][SWARM_MAX_SPECIES];
+  float sig6[SWARM_MAX_SPECIES][SWARM_MAX_SPECIES];
+  float eps24;
+  double rc_max;
+} derived_t;
+
+#define TWO32 4294967296.0
+#define TWO_PI 6.283185307179586476925
+#define ANG_INV_SCALE 683565275.57643158f /* 2^32 / (2 pi) */
+
+static void derive(const swarm_params_t *p, derived_t *d) {
+  memset(d, 0, sizeof(*d));
+  for (int a = 0; a < 3; ++a) {
+    double L = p->box[a];
+    d->sx[a] = (float)(L / TWO32);
+    d->inv_sx[a] = (float)(TWO32 / L);
+  }
+  double kT = p->kT, dt = p->time_step;
+  for (int s = 0; s < p->n_species; ++s) {
+    double gt = p->gamma_t[s], gr = p->gamma_r[s];
+    d->mob_dt[s] = (float)(dt / gt);
+    d->rot_dt[s] = (float)(dt / gr);
+    d->sig_t[s] = (float)sqrt(2.0 * kT * dt / gt);
+    d->sig_r[s] = (float)sqrt(2.0 * kT * dt / gr);
+    d->inv_gt[s] = (float)(1.0 / gt);
+    d->inv_gr[s] = (float)(1.0 / gr);
+    d->sig_v[s] = p->mass[s] > 0.0 ? (float)sqrt(kT / p->mass[s]) : 0.0f;
+    d->sig_w[s] = p->rinertia[s] > 0.0 ? (float)sqrt(kT / p->rinertia[s]) : 0.0f;
+  }
+  d->rc_max = 0.0;
+  for (int s = 0; s < p->n_species; ++s)
+    for (int t = 0; t < p->n_species; ++t) {
+      double rc = p->radius[s] + p->radius[t];
+      double rc2 = rc * rc;
+      d->cut2[s][t] = (float)rc2;
+      d->sig6[s][t] = (float)(rc2 * rc2 * rc2 * 0.5);
+      if (rc > d->rc_max)
+        d->rc_max = rc;
+    }
+  d->eps24 = (float)(24.0 * p->wca_epsilon);
+}
+
+static int32_t f2i32(float v) {
+  v = fminf(fmaxf(v, -2147483520.0f), 2147483520.0f);
+  return (int32_t)lrintf(v);
+}
+static int64_t f2fix24(float v) {
+  v = v * 16777216.0f;
+  v = fminf(fmaxf(v, -4.611686018427387904e18f), 4.611686018427387904e18f);
+  return (int64_t)llrintf(v);
+}
+
+/* displacement j - i along axis a, fp32 sim units */
+static float pair_disp(const swarm_params_t *p, const derived_t *d,
+                       const uint32_t *q, const int32_t *img, int n, int a,
+                       int i, int j) {
+  if (p->periodic) {
+    int32_t dq = (int32_t)(q[a * n + j] - q[a * n + i]);
+    return (float)dq * d->sx[a];
+  }
+  int64_t dq = ((int64_t)(img[a * n + j] - img[a * n + i]) * (int64_t)4294967296LL) +
+               ((int64_t)q[a * n + j] - (int64_t)q[a * n + i]);
+  return (float)dq * d->sx[a];
+}
+
+/* WCA force on i from j accumulated in 2^-24 fixed point */
+static void wca_pair(const derived_t *d, int si, int sj, float rx, float ry,
+                     int64_t *ax, int64_t *ay) {
+  float r2 = rx * rx + ry * ry;
+  if (r2 < d->cut2[si][sj] && r2 > 0.0f) {
+    float ir2 = 1.0f / r2;
+    float ir6 = ir2 * ir2;
+    ir6 = ir6 * ir2;
+    float s6 = d->sig6[si][sj] * ir6;
+    float t = 2.0f * s6;
+    t = t - 1.0f;
+    float fr = d->eps24 * s6;
+    fr = fr * t;
+    fr = fr * ir2;
+    *ax += f2fix24(-fr * rx);
+    *ay += f2fix24(-fr * ry);
+  }
+}
+
+/* cell index of particle i (2-D), grid ncx x ncy (powers of two) */
+static int cell_of(const swarm_params_t *p, const uint32_t *q, const int32_t *img,
+                   int n, int i, int lx, int ly) {
+  int c[2];
+  int lg[2] = {lx, ly};
+  for (int a = 0; a < 2; ++a) {
+    int nc = 1 << lg[a];
+    int v = lg[a] == 0 ? 0 : (int)(q[a * n + i] >> (32 - lg[a]));
+    if (!p->periodic) {
+      if (img[a * n + i] < 0)
+        v = 0;
+      else if (img[a * n + i] > 0)
+        v = nc - 1;
+    }
+    c[a] = v;
+  }
+  return c[1] * (1 << lx) + c[0];
+}
+
+static int ilog2_floor(double v) {
+  int l = 0;
+  while ((double)(1 << (l + 1)) <= v && l < 20)
+    ++l;
+  return l;
+}
+
+/* cell grid: power-of-two cells per axis, cell side >= rc_max and at most
+ * max(n, 64) cells in total (same rule as the GPU path). */
+void or_cell_grid(const swarm_params_t *p, int n, double cutoff, int *lx,
+                  int *ly) {
+  int l[2];
+  for (int a = 0; a < 2; ++a) {
+    double m = cutoff > 0.0 ? p->box[a] / cutoff : 1024.0;
+    l[a] = m >= 1.0 ? ilog2_floor(m) : 0;
+    if (l[a] > 15)
+      l[a] = 15;
+  }
+  int cap = n > 64 ? n : 64;
+  while ((1 << (l[0] + l[1])) > cap) {
+    if (l[0] >= l[1] && l[0] > 0)
+      l[0]--;
+    else if (l[1] > 0)
+      l[1]--;
+    else
+      break;
+  }
+  *lx = l[0];
+  *ly = l[1];
+}
+
+/* Neighbour candidate iteration helper: builds a cell list (counting sort). */
+typedef struct {
+  int lx, ly, ncell;
+  int *start; /* ncell + 1 */
+  int *list;  /* n */
+  int *cell;  /* n */
+} celllist_t;
+
+static void cl_build(celllist_t *cl, const swarm_params_t *p, const uint32_t *q,
+                     const int32_t *img, int n) {
+  memset(cl->start, 0, sizeof(int) * (size_t)(cl->ncell + 1));
+  for (int i = 0; i < n; ++i) {
+    cl->cell[i] = cell_of(p, q, img, n, i, cl->lx, cl->ly);
+    cl->start[cl->cell[i] + 1]++;
+  }
+  for (int c = 0; c < cl->ncell; ++c)
+    cl->start[c + 1] += cl->start[c];
+  int *fill = (int *)malloc(sizeof(int) * (size_t)cl->ncell);
+  memcpy(fill, cl->start, sizeof(int) * (size_t)cl->ncell);
+  for (int i = 0; i < n; ++i)
+    cl->list[fill[cl->cell[i]]++] = i;
+  free(fill);
+}
+
+/* total WCA forces (int64 fixed point) for all particles */
+static void wca_forces(const swarm_params_t *p, const derived_t *d, int n,
+                       const uint32_t *q, const int32_t *img,
+                       const uint8_t *species, int64_t *acc, celllist_t *cl) {
+  memset(acc, 0, sizeof(int64_t) * 2 * (size_t)n);
+  if (!cl) { /* brute force */
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        if (j == i)
+          continue;
+        float rx = pair_disp(p, d, q, img, n, 0, i, j);
+        float ry = pair_disp(p, d, q, img, n, 1, i, j);
+        wca_pair(d, species[i], species[j], rx, ry, &acc[i], &acc[n + i]);
+      }
+    return;
+  }
+  cl_build(cl, p, q, img, n);
+  int ncx = 1 << cl->lx, ncy = 1 << cl->ly;
+  for (int i = 0; i < n; ++i) {
+    int c = cl->cell[i];
+    int cx = c % ncx, cy = c / ncx;
+    int lox = ncx >= 3 ? -1 : 0, hix = ncx >= 3 ? 1 : ncx - 1;
+    int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+    for (int oy = loy; oy <= hiy; ++oy)
+      for (int ox = lox; ox <= hix; ++ox) {
+        int x = cx + ox, y = cy + oy;
+        if (p->periodic) {
+          x = (x + ncx) % ncx;
+          y = (y + ncy) % ncy;
+        } else if (x < 0 || x >= ncx || y < 0 || y >= ncy)
+          continue;
+        int cc = y * ncx + x;
+        for (int k = cl->start[cc]; k < cl->start[cc + 1]; ++k) {
+          int j = cl->list[k];
+          if (j == i)
+            continue;
+          float rx = pair_disp(p, d, q, img, n, 0, i, j);
+          float ry = pair_disp(p, d, q, img, n, 1, i, j);
+          wca_pair(d, species[i], species[j], rx, ry, &acc[i], &acc[n + i]);
+        }
+      }
+  }
+}
+
+static void advance(uint32_t *q, int32_t *img, int32_t dq) {
+  uint32_t old = *q;
+  uint32_t nq = old + (uint32_t)dq;
+  if (dq > 0 && nq < old)
+    *img += 1;
+  else if (dq < 0 && nq > old)
+    *img -= 1;
+  *q = nq;
+}
+
+static int cl_alloc(celllist_t *cl, const swarm_params_t *p, const derived_t *d,
+                    int n) {
+  or_cell_grid(p, n, d->rc_max, &cl->lx, &cl->ly);
+  cl->ncell = 1 << (cl->lx + cl->ly);
+  cl->start = (int *)malloc(sizeof(int) * (size_t)(cl->ncell + 1));
+  cl->list = (int *)malloc(sizeof(int) * (size_t)n);
+  cl->cell = (int *)malloc(sizeof(int) * (size_t)n);
+  return cl->start && cl->list && cl->cell;
+}
+static void cl_free(celllist_t *cl) {
+  free(cl->start);
+  free(cl->list);
+  free(cl->cell);
+}
+
+/*
+ * n_steps Brownian-dynamics sub-steps of ONE env (2-D).
+ * q/img: [3][n], ang: [n]; f_swim, torque_z: [n]; f_ext: [3][n] or NULL.
+ * vel/omega (NULL allowed) receive the BD velocity of the last sub-step.
+ * step0: global step index of the first sub-step (noise counter).
+ * use_cells: 0 = O(n^2) pair search, 1 = cell list (same result).
+ */
+int or_bd_run(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
+              uint32_t *ang, const uint8_t *species, const float *f_swim,
+              const float *torque_z, const float *f_ext, uint64_t step0,
+              int n_steps, uint32_t env, float *vel, float *omega,
+              int use_cells) {
+  if (p->n_dims != 2)
+    return SWARM_EINVAL;
+  derived_t d;
+  derive(p, &d);
+  int64_t *acc = (int64_t *)malloc(sizeof(int64_t) * 2 * (size_t)(n > 0 ? n : 1));
+  celllist_t cl;
+  int have_cl = use_cells && cl_alloc(&cl, p, &d, n);
+  const int noisy = p->kT > 0.0;
+  for (int s = 0; s < n_steps; ++s) {
+    uint64_t step = step0 + (uint64_t)s;
+    wca_forces(p, &d, n, q, img, species, acc, have_cl ? &cl : NULL);
+    for (int i = 0; i < n; ++i) {
+      int sp = species[i];
+      float sn, cs;
+      or_sincos_turn(ang[i], &sn, &cs);
+      float fx = (float)acc[i] * 5.9604644775390625e-08f;
+      float fy = (float)acc[n + i] * 5.9604644775390625e-08f;
+      if (f_ext) {
+        fx = fx + f_ext[i];
+        fy = fy + f_ext[n + i];
+      }
+      fx = fx + f_swim[i] * cs;
+      fy = fy + f_swim[i] * sn;
+      float dx = fx * d.mob_dt[sp];
+      float dy = fy * d.mob_dt[sp];
+      float dth = torque_z[i] * d.rot_dt[sp];
+      if (noisy) {
+        float g[4];
+        or_normals4(p->seed, env, (uint32_t)i, step, 0u, g);
+        dx = dx + d.sig_t[sp] * g[0];
+        dy = dy + d.sig_t[sp] * g[1];
+        dth = dth + d.sig_r[sp] * g[2];
+      }
+      advance(&q[i], &img[i], f2i32(dx * d.inv_sx[0]));
+      advance(&q[n + i], &img[n + i], f2i32(dy * d.inv_sx[1]));
+      ang[i] = ang[i] + (uint32_t)f2i32(dth * ANG_INV_SCALE);
+      if (s == n_steps - 1) {
+        float vx = fx * d.inv_gt[sp], vy = fy * d.inv_gt[sp];
+        float w = torque_z[i] * d.inv_gr[sp];
+        if (noisy) {
+          float g[4];
+          or_normals4(p->seed, env, (uint32_t)i, step, 1u, g);
+          vx = vx + d.sig_v[sp] * g[0];
+          vy = vy + d.sig_v[sp] * g[1];
+          w = w + d.sig_w[sp] * g[2];
+        }
+        if (vel) {
+          vel[i] = vx;
+          vel[n + i] = vy;
+          vel[2 * n + i] = 0.0f;
+        }
+        if (omega)
+          omega[i] = w;
+      }
+    }
+  }
+  if (have_cl)
+    cl_free(&cl);
+  free(acc);
+  return SWARM_OK;
+}
+
+/*
+ * Steepest descent (espresso.py:1161-1168): per step F = WCA + ext + swim,
+ * dp = clamp(gamma F, -max_disp, max_disp) per free coordinate; stops early
+ * once every force is exactly zero (later steps would not move anything).
+ * Returns the number of steps executed.
+ */
+int or_sd_run(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
+              uint32_t *ang, const uint8_t *species, const float *f_swim,
+              const float *torque_z, const float *f_ext, int n_steps,
+              double gamma, double max_disp, int use_cells) {
+  derived_t d;
+  derive(p, &d);
+  const float g = (float)gamma, md = (float)max_disp;
+  int64_t *acc = (int64_t *)malloc(sizeof(int64_t) * 2 * (size_t)(n > 0 ? n : 1));
+  celllist_t cl;
+  int have_cl = use_cells && cl_alloc(&cl, p, &d, n);
+  int s;
+  for (s = 0; s < n_steps; ++s) {
+    wca_forces(p, &d, n, q, img, species, acc, have_cl ? &cl : NULL);
+    int any = 0;
+    for (int i = 0; i < n; ++i) {
+      float sn, cs;
+      or_sincos_turn(ang[i], &sn, &cs);
+      float fx = (float)acc[i] * 5.9604644775390625e-08f;
+      float fy = (float)acc[n + i] * 5.9604644775390625e-08f;
+      if (f_ext) {
+        fx = fx + f_ext[i];
+        fy = fy + f_ext[n + i];
+      }
+      fx = fx + f_swim[i] * cs;
+      fy = fy + f_swim[i] * sn;
+      float tz = torque_z[i];
+      if (fx != 0.0f || fy != 0.0f || tz != 0.0f)
+        any = 1;
+      float px = fminf(fmaxf(g * fx, -md), md);
+      float py = fminf(fmaxf(g * fy, -md), md);
+      float pa = fminf(fmaxf(g * tz, -md), md);
+      advance(&q[i], &img[i], f2i32(px * d.inv_sx[0]));
+      advance(&q[n + i], &img[n + i], f2i32(py * d.inv_sx[1]));
+      ang[i] = ang[i] + (uint32_t)f2i32(pa * ANG_INV_SCALE);
+    }
+    if (!any)
+      break;
+  }
+  if (have_cl)
+    cl_free(&cl);
+  free(acc);
+  return s;
+}
+
+/*
+ * Vision cones of ONE env, O(n_agents * n): out[a][k][t] (fp32).
+ * radii[n]: radius of the seen colloid by list position; types[n]: type of
+ * every colloid; det[n_types]: detected types; rims[n_cones + 1].
+ */
+void or_vision_cone(const swarm_params_t *p, int n, const uint32_t *q,
+                    const int32_t *img, const uint32_t *ang, const int *agents,
+                    int n_agents, const float *radii, const int *types,
+                    float vision_range, int n_cones, const float *rims,
+                    int n_types, const int *det, float *out) {
+  derived_t d;
+  derive(p, &d);
+  int64_t acc[SWARM_MAX_CONES * SWARM_MAX_DETECTED_TYPES];
+  for (int ai = 0; ai < n_agents; ++ai) {
+    int i = agents[ai];
+    memset(acc, 0, sizeof(acc));
+    float sn, cs;
+    or_sincos_turn(ang[i], &sn, &cs);
+    float nm = sqrtf(cs * cs + sn * sn);
+    float mx = cs / nm, my = sn / nm;
+    for (int j = 0; j < n; ++j) {
+      if (j == i)
+        continue;
+      int ti = -1;
+      for (int t = 0; t < n_types; ++t)
+        if (det[t] == types[j])
+          ti = t;
+      if (ti < 0)
+        continue;
+      /* unwrapped difference, no minimum image (subdivided_vision_cones.py:116) */
+      float dd[2];
+      int far = 0;
+      for (int a = 0; a < 2; ++a) {
+        int64_t dq = ((int64_t)(img[a * n + j] - img[a * n + i]) * (int64_t)4294967296LL) +
+                     ((int64_t)q[a * n + j] - (int64_t)q[a * n + i]);
+        if (dq < -2147483647LL || dq > 2147483647LL)
+          far = 1; /* more than half a box away: never within vision_range */
+        dd[a] = (float)dq * d.sx[a];
+      }
+      if (far)
+        continue;
+      float dist2 = dd[0] * dd[0] + dd[1] * dd[1];
+      float dist = sqrtf(dist2);
+      if (!(dist < vision_range) || dist == 0.0f)
+        continue;
+      float amp = (2.0f * radii[j]) / dist;
+      amp = fminf(1.0f, amp);
+      float ux = dd[0] / dist, uy = dd[1] / dist;
+      float dot = ux * mx + uy * my;
+      dot = fminf(fmaxf(dot, -1.0f), 1.0f);
+      float an = or_acosf(dot);
+      float orth = ux * (-my) + uy * mx;
+      if (orth < 0.0f)
+        an = -an;
+      for (int k = 0; k < n_cones; ++k)
+        if (rims[k] < an && an < rims[k + 1])
+          acc[k * n_types + ti] += (int64_t)llrintf(amp * 4294967296.0f);
+    }
+    for (int k = 0; k < n_cones * n_types; ++k)
+      out[(size_t)ai * (size_t)(n_cones * n_types) + (size_t)k] =
+          (float)acc[k] * 2.3283064365386963e-10f;
+  }
+}
+
+/* unwrapped position along axis a, fp64 */
+static double unwrap(const swarm_params_t *p, const uint32_t *q,
+                     const int32_t *img, int n, int a, int i) {
+  return ((double)img[a * n + i] + (double)q[a * n + i] * (1.0 / TWO32)) *
+         p->box[a];
+}
+
+/* Field distances of ONE env (see swarm_field_distance in the C ABI).
+ * hist_q / hist_img: [3][n_agents]. */
+void or_field_distance(const swarm_params_t *p, int n, const uint32_t *q,
+                       const int32_t *img, const int *agents, int n_agents,
+                       const double source[3], const double box_scale[3],
+                       uint32_t *hist_q, int32_t *hist_img, float *d_cur,
+                       float *d_prev, int update_history) {
+  double src[3];
+  for (int a = 0; a < 3; ++a)
+    src[a] = source[a] / box_scale[a];
+  for (int ai = 0; ai < n_agents; ++ai) {
+    int i = agents[ai];
+    float cur[3], prev[3];
+    for (int a = 0; a < 3; ++a) {
+      double pc = a < 2 ? unwrap(p, q, img, n, a, i) / box_scale[a] : 0.0 / box_scale[a];
+      double hp = a < 2 ? ((double)hist_img[a * n_agents + ai] +
+                           (double)hist_q[a * n_agents + ai] * (1.0 / TWO32)) *
+                              p->box[a] / box_scale[a]
+                        : 0.0 / box_scale[a];
+      cur[a] = (float)(src[a] - pc);
+      prev[a] = (float)(src[a] - hp);
+    }
+    d_cur[ai] = sqrtf(cur[0] * cur[0] + cur[1] * cur[1] + cur[2] * cur[2]);
+    d_prev[ai] = sqrtf(prev[0] * prev[0] + prev[1] * prev[1] + prev[2] * prev[2]);
+    if (update_history)
+      for (int a = 0; a < 3; ++a) {
+        hist_q[a * n_agents + ai] = q[a * n + i];
+        hist_img[a * n_agents + ai] = img[a * n + i];
+      }
+  }
+}
+
+/* All pairs i<j closer than cutoff (minimum image if periodic). */
+int or_neighbor_pairs(const swarm_params_t *p, int n, const uint32_t *q,
+                      const int32_t *img, double cutoff, int *pairs,
+                      int max_pairs) {
+  derived_t d;
+  derive(p, &d);
+  float c2 = (float)(cutoff * cutoff);
+  int np = 0;
+  for (int i = 0; i < n; ++i)
+    for (int j = i + 1; j < n; ++j) {
+      float rx = pair_disp(p, &d, q, img, n, 0, i, j);
+      float ry = pair_disp(p, &d, q, img, n, 1, i, j);
+      if (rx * rx + ry * ry < c2) {
+        if (np < max_pairs) {
+          pairs[2 * np] = i;
+          pairs[2 * np + 1] = j;
+        }
+        np++;
+      }
+    }
+  return np;
+}

@@ -1,0 +1,147 @@
+"""
+Actor-critic agent (reference: swarmrl/agents/actor_critic.py:20-216).
+
+calc_action: observable -> network -> action table -> trajectory append;
+calc_reward: task (+ intrinsic) + external -> trajectory append (called by
+the engine after every integration chunk).  With a SwarmView the whole slice
+stays on the GPU: the observable is a HIP kernel, the policy a torch MLP,
+the action table a device gather, and the trajectory holds device tensors.
+"""
+
+import numpy as np
+import torch
+
+from swarmrl_amd.agents.agent import Agent
+from swarmrl_amd.engine.swarm_view import DeviceActions, is_view
+from swarmrl_amd.losses.proximal_policy_loss import ProximalPolicyLoss
+from swarmrl_amd.utils.colloid_utils import TrajectoryInformation
+
+
+class ActorCriticAgent(Agent):
+    """Class to handle the actor-critic RL protocol."""
+
+    def __init__(
+        self,
+        particle_type: int,
+        network,
+        task,
+        observable,
+        actions: dict,
+        loss=None,
+        train: bool = True,
+        intrinsic_reward=None,
+    ):
+        self.network = network
+        self.particle_type = particle_type
+        self.task = task
+        self.observable = observable
+        self.actions = actions
+        self.train = train
+        self.loss = loss if loss is not None else ProximalPolicyLoss()
+        self.intrinsic_reward = intrinsic_reward
+        self.trajectory = TrajectoryInformation(particle_type=self.particle_type)
+        self._tables = None
+
+    def __name__(self) -> str:
+        return "ActorCriticAgent"
+
+    def supports_device(self) -> bool:
+        ok = getattr(self.observable, "supports_device", False) and getattr(
+            self.task, "supports_device", False
+        )
+        if self.intrinsic_reward is not None:
+            ok = ok and getattr(self.intrinsic_reward, "supports_device", False)
+        return bool(ok) and hasattr(self.network, "compute_action")
+
+    # ----------------------------------------------------------- training
+    def update_agent(self) -> tuple:
+        rewards = self.trajectory.rewards
+        killed = self.trajectory.killed
+        self.loss.compute_loss(network=self.network, episode_data=self.trajectory)
+        if self.intrinsic_reward:
+            self.intrinsic_reward.update(self.trajectory)
+        self.reset_trajectory()
+        return rewards, killed
+
+    def reset_agent(self, colloids):
+        self.observable.initialize(colloids)
+        self.task.initialize(colloids)
+
+    def reset_trajectory(self):
+        self.task.kill_switch = False
+        self.trajectory = TrajectoryInformation(particle_type=self.particle_type)
+
+    def initialize_network(self):
+        self.network.reinitialize_network()
+
+    def save_agent(self, directory: str):
+        self.network.export_model(
+            filename=f"{self.__name__()}_{self.particle_type}", directory=directory
+        )
+
+    def restore_agent(self, directory: str):
+        self.network.restore_model_state(
+            filename=f"{self.__name__()}_{self.particle_type}", directory=directory
+        )
+
+    # ------------------------------------------------------------- acting
+    def _action_tables(self, device):
+        if self._tables is None or self._tables[0] != device:
+            acts = list(self.actions.values())
+            f = torch.tensor([float(a.force) for a in acts], dtype=torch.float32, device=device)
+            tz = torch.tensor(
+                [0.0 if a.torque is None else float(np.asarray(a.torque, dtype=float)[2])
+                 for a in acts],
+                dtype=torch.float32, device=device,
+            )
+            has_dir = any(a.new_direction is not None for a in acts)
+            self._tables = (device, f, tz, has_dir)
+        return self._tables
+
+    def calc_action(self, colloids):
+        state_description = self.observable.compute_observable(colloids)
+        if is_view(colloids):
+            E = colloids.n_envs
+            A = int(state_description.shape[1])
+            flat = state_description.reshape(E * A, -1)
+            idx, logp = self.network.compute_action(observables=flat)
+            idx = idx.reshape(E, A)
+            logp = logp.reshape(E, A)
+            _, ftab, ttab, has_dir = self._action_tables(colloids.device)
+            new_dir = None
+            mask = None
+            if has_dir:
+                acts = list(self.actions.values())
+                host_idx = idx.cpu().numpy()
+                new_dir = np.zeros((E, A, 3))
+                mask = np.zeros((E, A), dtype=bool)
+                for k, a in enumerate(acts):
+                    if a.new_direction is not None:
+                        sel = host_idx == k
+                        new_dir[sel] = a.new_direction
+                        mask[sel] = True
+            chosen = DeviceActions(ftab[idx], ttab[idx], new_dir, mask)
+            if self.train:
+                self.trajectory.features.append(state_description)
+                self.trajectory.actions.append(idx)
+                self.trajectory.log_probs.append(logp)
+                self.trajectory.killed = self.task.kill_switch
+            return chosen
+        action_indices, log_probs = self.network.compute_action(observables=state_description)
+        chosen_actions = np.take(list(self.actions.values()), action_indices, axis=-1)
+        if self.train:
+            self.trajectory.features.append(state_description)
+            self.trajectory.actions.append(action_indices)
+            self.trajectory.log_probs.append(log_probs)
+            self.trajectory.killed = self.task.kill_switch
+        return chosen_actions
+
+    def calc_reward(self, colloids, external_reward: float = 0.0):
+        rewards = self.task(colloids)
+        if self.intrinsic_reward:
+            rewards = rewards + self.intrinsic_reward.compute_reward(episode_data=self.trajectory)
+        rewards = rewards + external_reward
+        if self.train:
+            self.trajectory.rewards.append(rewards)
+        self.kill_switch = self.task.kill_switch
+        return rewards

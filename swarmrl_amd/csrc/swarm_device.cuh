@@ -1,0 +1,212 @@
+// swarm_device.cuh -- device arithmetic shared by the engine kernels.
+//
+// Every function here fixes its fp32 operation sequence (the file is compiled
+// with -ffp-contract=off), so a kernel result is a deterministic function of
+// its inputs and is reproduced bit for bit by the CPU oracle (oracle/), which
+// restates the same number formats independently.  See DESIGN.md "Number
+// formats".
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace swarm {
+
+// ---------------------------------------------------------------- Philox
+// Philox4x32-10 (Salmon et al., SC'11).  Key = (seed lo, seed hi ^ env),
+// counter = (particle id, step lo, step hi, stream tag).
+struct u32x4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c.z;
+    u32x4 n;
+    n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+    n.y = (uint32_t)p1;
+    n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+    n.w = (uint32_t)p0;
+    c = n;
+  }
+  return c;
+}
+
+// ------------------------------------------------- elementary functions
+// Correctly rounded fp32 square root.  hipcc (ROCm 7.2) lowers sqrtf and
+// __fsqrt_rn to the bare v_sqrt_f32 (<= 1 ulp); the host's sqrtf is IEEE
+// exact.  Refine the hardware value by testing its two neighbours with an
+// exact-residual FMA (the sequence LLVM emits for correctly rounded sqrt).
+__device__ __forceinline__ float sqrt_rn(float x) {
+  if (!(x > 0.0f) || x == __builtin_inff()) return __builtin_sqrtf(x);
+  const bool tiny = x < 1.2621774483536189e-29f;  // 2^-96: keep clear of denormals
+  const float xs = tiny ? x * 4294967296.0f : x;
+  float s = __builtin_amdgcn_sqrtf(xs);
+  const uint32_t si = __float_as_uint(s);
+  const float s_dn = __uint_as_float(si - 1u);
+  const float s_up = __uint_as_float(si + 1u);
+  const float r_dn = __builtin_fmaf(-s_dn, s, xs);
+  const float r_up = __builtin_fmaf(-s_up, s, xs);
+  s = (r_dn <= 0.0f) ? s_dn : s;
+  s = (r_up > 0.0f) ? s_up : s;
+  return tiny ? s * 1.52587890625e-05f : s;  // * 2^-16
+}
+
+__device__ __forceinline__ float logf_fixed(float x) {
+  const uint32_t b = __float_as_uint(x);
+  int e = (int)((b >> 23) & 0xffu) - 126;
+  float m = __uint_as_float((b & 0x007fffffu) | 0x3f000000u);
+  if (m < 0.70710678118654752440f) {
+    e -= 1;
+    m = m + m;
+    m = m - 1.0f;
+  } else {
+    m = m - 1.0f;
+  }
+  const float z = m * m;
+  float y = 7.0376836292e-2f;
+  y = y * m;
+  y = y + -1.1514610310e-1f;
+  y = y * m;
+  y = y + 1.1676998740e-1f;
+  y = y * m;
+  y = y + -1.2420140846e-1f;
+  y = y * m;
+  y = y + 1.4249322787e-1f;
+  y = y * m;
+  y = y + -1.6668057665e-1f;
+  y = y * m;
+  y = y + 2.0000714765e-1f;
+  y = y * m;
+  y = y + -2.4999993993e-1f;
+  y = y * m;
+  y = y + 3.3333331174e-1f;
+  y = y * m;
+  y = y * z;
+  const float fe = (float)e;
+  y = y + -2.12194440e-4f * fe;
+  y = y + -0.5f * z;
+  float r = m + y;
+  r = r + 0.693359375f * fe;
+  return r;
+}
+
+// sin/cos of a * 2 pi / 2^32
+__device__ __forceinline__ void sincos_turn(uint32_t a, float* s_out, float* c_out) {
+  const uint32_t b = a + 0x20000000u;
+  const uint32_t quad = b >> 30;
+  const int32_t rem = (int32_t)(b & 0x3FFFFFFFu) - 0x20000000;
+  const float x = (float)rem * 1.46291807926715968e-09f;
+  const float z = x * x;
+  float sp = -1.9515295891e-4f;
+  sp = sp * z;
+  sp = sp + 8.3321608736e-3f;
+  sp = sp * z;
+  sp = sp + -1.6666654611e-1f;
+  sp = sp * z;
+  sp = sp * x;
+  const float s = sp + x;
+  float cp = 2.443315711809948e-5f;
+  cp = cp * z;
+  cp = cp + -1.388731625493765e-3f;
+  cp = cp * z;
+  cp = cp + 4.166664568298827e-2f;
+  cp = cp * z;
+  cp = cp * z;
+  float c = cp - 0.5f * z;
+  c = c + 1.0f;
+  // quadrant rotation without divergent branches
+  const bool swap = (quad & 1u) != 0u;
+  float so = swap ? c : s;
+  float co = swap ? s : c;
+  if (quad == 1u) co = -co;
+  if (quad == 2u) {
+    so = -so;
+    co = -co;
+  }
+  if (quad == 3u) so = -so;
+  *s_out = so;
+  *c_out = co;
+}
+
+__device__ __forceinline__ float asinf_small(float a) {
+  const float z = a * a;
+  float p = 4.2163199048e-2f;
+  p = p * z;
+  p = p + 2.4181311049e-2f;
+  p = p * z;
+  p = p + 4.5470025998e-2f;
+  p = p * z;
+  p = p + 7.4953002686e-2f;
+  p = p * z;
+  p = p + 1.6666752422e-1f;
+  p = p * z;
+  p = p * a;
+  return p + a;
+}
+
+__device__ __forceinline__ float acosf_fixed(float x) {
+  if (x < -0.5f) {
+    float t = 1.0f + x;
+    t = 0.5f * t;
+    return 3.14159265358979323846f - 2.0f * asinf_small(sqrt_rn(t));
+  }
+  if (x > 0.5f) {
+    float t = 1.0f - x;
+    t = 0.5f * t;
+    return 2.0f * asinf_small(sqrt_rn(t));
+  }
+  return 1.57079632679489661923f - asinf_small(x);
+}
+
+// Four standard normals (two Box-Muller pairs of one Philox block).
+__device__ __forceinline__ void normals4(uint32_t k0, uint32_t k1, uint32_t id,
+                                         uint64_t step, uint32_t tag, float g[4]) {
+  u32x4 c;
+  c.x = id;
+  c.y = (uint32_t)step;
+  c.z = (uint32_t)(step >> 32);
+  c.w = tag;
+  const u32x4 r = philox4x32_10(c, k0, k1);
+  const uint32_t ru[2] = {r.x, r.z};
+  const uint32_t ra[2] = {r.y, r.w};
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    float u = (float)(ru[p] >> 9) + 0.5f;
+    u = u * 1.1920928955078125e-07f;
+    const float l = logf_fixed(u);
+    const float rad = sqrt_rn(-2.0f * l);
+    float s, c2;
+    sincos_turn(ra[p], &s, &c2);
+    g[2 * p] = rad * c2;
+    g[2 * p + 1] = rad * s;
+  }
+}
+
+// --------------------------------------------------- fixed-point helpers
+__device__ __forceinline__ int32_t f2i32(float v) {
+  v = fminf(fmaxf(v, -2147483520.0f), 2147483520.0f);
+  return __float2int_rn(v);
+}
+
+__device__ __forceinline__ int64_t f2fix24(float v) {
+  v = v * 16777216.0f;
+  v = fminf(fmaxf(v, -4.611686018427387904e18f), 4.611686018427387904e18f);
+  return __float2ll_rn(v);
+}
+
+__device__ __forceinline__ void advance(uint32_t& q, int32_t& img, int32_t dq) {
+  const uint32_t old = q;
+  const uint32_t nq = old + (uint32_t)dq;
+  img += (dq > 0 && nq < old) ? 1 : 0;
+  img -= (dq < 0 && nq > old) ? 1 : 0;
+  q = nq;
+}
+
+}  // namespace swarm

@@ -1,0 +1,1072 @@
+// swarm_engine.hip -- MI355X (gfx950) active-Brownian swarm engine.
+//
+// Implements the C ABI of include/swarmrl_amd.h.  The per-step hot path of
+// the reference (ESPResSo Brownian dynamics + WCA via a cell system, driven by
+// swarmrl/engine/espresso.py:1251-1308) runs here as hand-written HIP:
+//
+//   k_bd_block      one workgroup (<=1024 threads) per environment; the whole
+//                   env's state lives in registers, a cell list is rebuilt in
+//                   LDS every sub-step (counting sort), n sub-steps per launch.
+//                   Also runs steepest descent (espresso.py:1161-1168).
+//   k_grid_build    per-env cell list in global memory (for the observables).
+//   k_vision        SubdividedVisionCones, one thread per (env, agent).
+//   k_field         ConcentrationField / GradientSensing distances + history.
+//   k_pairs         neighbour pairs (parity helper).
+//
+// Number formats: positions are uint32 box fractions + int32
+// image counters, angles uint32 turn fractions, pair sums int64 fixed point,
+// so results are independent of neighbour order and bit-identical to the
+// CPU oracle.  Compile with -ffp-contract=off.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/swarmrl_amd.h"
+#include "swarm_device.cuh"
+
+namespace {
+
+constexpr int kMaxSpecies = SWARM_MAX_SPECIES;
+constexpr double kTwo32 = 4294967296.0;
+constexpr double kTwoPi = 6.283185307179586476925;
+constexpr float kAngInvScale = 683565275.57643158f;  // 2^32 / (2 pi)
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                        \
+  do {                                                                       \
+    hipError_t _e = (expr);                                                  \
+    if (_e != hipSuccess)                                                    \
+      return fail(SWARM_EDEVICE, std::string(#expr ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+// fp32 constants derived from swarm_params_t (same derivation as the oracle).
+struct Derived {
+  float sx[3], inv_sx[3];
+  float mob_dt[kMaxSpecies], sig_t[kMaxSpecies];
+  float rot_dt[kMaxSpecies], sig_r[kMaxSpecies];
+  float inv_gt[kMaxSpecies], inv_gr[kMaxSpecies];
+  float sig_v[kMaxSpecies], sig_w[kMaxSpecies];
+  float cut2[kMaxSpecies * kMaxSpecies];
+  float sig6[kMaxSpecies * kMaxSpecies];
+  float eps24;
+  int32_t n_species;
+  uint32_t key0, key1;
+  int32_t noisy;
+  int32_t periodic;
+  double rc_max;
+};
+
+void derive(const swarm_params_t& p, Derived& d) {
+  std::memset(&d, 0, sizeof(d));
+  for (int a = 0; a < 3; ++a) {
+    d.sx[a] = (float)(p.box[a] / kTwo32);
+    d.inv_sx[a] = (float)(kTwo32 / p.box[a]);
+  }
+  const double kT = p.kT, dt = p.time_step;
+  for (int s = 0; s < p.n_species; ++s) {
+    const double gt = p.gamma_t[s], gr = p.gamma_r[s];
+    d.mob_dt[s] = (float)(dt / gt);
+    d.rot_dt[s] = (float)(dt / gr);
+    d.sig_t[s] = (float)std::sqrt(2.0 * kT * dt / gt);
+    d.sig_r[s] = (float)std::sqrt(2.0 * kT * dt / gr);
+    d.inv_gt[s] = (float)(1.0 / gt);
+    d.inv_gr[s] = (float)(1.0 / gr);
+    d.sig_v[s] = p.mass[s] > 0.0 ? (float)std::sqrt(kT / p.mass[s]) : 0.0f;
+    d.sig_w[s] = p.rinertia[s] > 0.0 ? (float)std::sqrt(kT / p.rinertia[s]) : 0.0f;
+  }
+  d.rc_max = 0.0;
+  for (int s = 0; s < p.n_species; ++s)
+    for (int t = 0; t < p.n_species; ++t) {
+      const double rc = p.radius[s] + p.radius[t];
+      const double rc2 = rc * rc;
+      d.cut2[s * kMaxSpecies + t] = (float)rc2;
+      d.sig6[s * kMaxSpecies + t] = (float)(rc2 * rc2 * rc2 * 0.5);
+      d.rc_max = std::max(d.rc_max, rc);
+    }
+  d.eps24 = (float)(24.0 * p.wca_epsilon);
+  d.n_species = p.n_species;
+  d.key0 = (uint32_t)p.seed;
+  d.key1 = (uint32_t)(p.seed >> 32);
+  d.noisy = p.kT > 0.0 ? 1 : 0;
+  d.periodic = p.periodic;
+}
+
+int ilog2_floor(double v) {
+  int l = 0;
+  while ((double)(1 << (l + 1)) <= v && l < 20) ++l;
+  return l;
+}
+
+// Power-of-two cell grid with side >= cutoff and at most max(n, 64) cells
+// (identical rule in oracle/swarm_oracle.c:or_cell_grid).
+void cell_grid(const swarm_params_t& p, int n, double cutoff, int* lx, int* ly) {
+  int l[2];
+  for (int a = 0; a < 2; ++a) {
+    const double m = cutoff > 0.0 ? p.box[a] / cutoff : 1024.0;
+    l[a] = m >= 1.0 ? ilog2_floor(m) : 0;
+    if (l[a] > 15) l[a] = 15;
+  }
+  const int cap = n > 64 ? n : 64;
+  while ((1 << (l[0] + l[1])) > cap) {
+    if (l[0] >= l[1] && l[0] > 0)
+      l[0]--;
+    else if (l[1] > 0)
+      l[1]--;
+    else
+      break;
+  }
+  *lx = l[0];
+  *ly = l[1];
+}
+
+struct DevState {
+  uint32_t* q;      // [3][M]
+  int32_t* img;     // [3][M]
+  uint32_t* ang;    // [M]
+  float* f_swim;    // [M]
+  float* torque_z;  // [M]
+  float* f_ext;     // [3][M]
+  float* vel;       // [3][M]
+  float* omega;     // [M]
+  uint8_t* species; // [N]
+  int32_t n;        // particles per env
+  int32_t m;        // E * N
+};
+
+// ------------------------------------------------------------ block scan
+// Exclusive scan of data[0..n) in LDS by the whole block; data[n] = total.
+__device__ void block_exclusive_scan(int32_t* data, int n, int32_t* wave_sums) {
+  const int T = blockDim.x;
+  const int tid = threadIdx.x;
+  const int per = (n + T - 1) / T;
+  const int lo = min(tid * per, n), hi = min(lo + per, n);
+  int32_t local = 0;
+  for (int k = lo; k < hi; ++k) local += data[k];
+  // inclusive wave scan of local
+  const int lane = tid & 63, wave = tid >> 6;
+  int32_t v = local;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t o = __shfl_up(v, off, 64);
+    if (lane >= off) v += o;
+  }
+  if (lane == 63) wave_sums[wave] = v;
+  __syncthreads();
+  if (wave == 0) {
+    const int nw = (T + 63) >> 6;
+    int32_t w = lane < nw ? wave_sums[lane] : 0;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int32_t o = __shfl_up(w, off, 64);
+      if (lane >= off) w += o;
+    }
+    if (lane < nw) wave_sums[lane] = w;  // inclusive
+  }
+  __syncthreads();
+  int32_t run = v - local + (wave > 0 ? wave_sums[wave - 1] : 0);
+  for (int k = lo; k < hi; ++k) {
+    const int32_t c = data[k];
+    data[k] = run;
+    run += c;
+  }
+  if (tid == T - 1) data[n] = run;
+}
+
+__device__ __forceinline__ int cell_index(uint32_t qx, uint32_t qy, int lx, int ly) {
+  const int cx = lx == 0 ? 0 : (int)(qx >> (32 - lx));
+  const int cy = ly == 0 ? 0 : (int)(qy >> (32 - ly));
+  return (cy << lx) | cx;
+}
+
+// -------------------------------------------------------------- BD / SD
+// One workgroup per env.  Template MAXP = particles held per thread.
+template <int MAXP>
+__global__ __launch_bounds__(1024) void k_bd_block(const Derived* __restrict__ dglob,
+                                                   DevState st, int n_steps,
+                                                   uint64_t* __restrict__ step_ctr,
+                                                   uint32_t* __restrict__ arrive, int lx,
+                                                   int ly, int sd_mode, float sd_gamma,
+                                                   float sd_maxd, int32_t* sd_done) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int e = blockIdx.x;
+  const int T = blockDim.x;
+  const int tid = threadIdx.x;
+  const int N = st.n;
+  const int ncell = 1 << (lx + ly);
+  const int cnt_words = (ncell + 1 + 3) & ~3;
+
+  Derived* d = reinterpret_cast<Derived*>(smem);
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem + ((sizeof(Derived) + 15) & ~15));
+  int32_t* cnt = wave_sums + 16;
+  uint32_t* sqx = reinterpret_cast<uint32_t*>(cnt + cnt_words);
+  uint32_t* sqy = sqx + N;
+  uint32_t* sinf = sqy + N;
+
+  // derived constants -> LDS
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(dglob);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(d);
+    for (int k = tid; k < (int)(sizeof(Derived) / 4); k += T) dst[k] = src[k];
+  }
+
+  uint32_t qx[MAXP], qy[MAXP], an[MAXP];
+  int32_t ix[MAXP], iy[MAXP];
+  int sp[MAXP];
+  float fs[MAXP], tz[MAXP], fex[MAXP], fey[MAXP];
+  const size_t M = (size_t)st.m;
+#pragma unroll
+  for (int k = 0; k < MAXP; ++k) {
+    const int i = tid + k * T;
+    if (i < N) {
+      const size_t g = (size_t)e * N + i;
+      qx[k] = st.q[g];
+      qy[k] = st.q[M + g];
+      ix[k] = st.img[g];
+      iy[k] = st.img[M + g];
+      an[k] = st.ang[g];
+      sp[k] = st.species[i];
+      fs[k] = st.f_swim[g];
+      tz[k] = st.torque_z[g];
+      fex[k] = st.f_ext[g];
+      fey[k] = st.f_ext[M + g];
+    }
+  }
+  __syncthreads();
+
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const float isx0 = d->inv_sx[0], isx1 = d->inv_sx[1];
+  const int ncx = 1 << lx, ncy = 1 << ly;
+  const int lox = ncx >= 3 ? -1 : 0, hix = ncx >= 3 ? 1 : ncx - 1;
+  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+  const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
+  const bool noisy = d->noisy != 0;
+  // The noise counter lives in device memory so a captured hipGraph replays
+  // with fresh noise; the last workgroup to finish advances it (below).
+  const uint64_t step0 = sd_mode ? 0ull : *step_ctr;
+  int steps_done = 0;
+
+  for (int s = 0; s < n_steps; ++s) {
+    const uint64_t step = step0 + (uint64_t)s;
+    for (int c = tid; c < cnt_words; c += T) cnt[c] = 0;
+    __syncthreads();
+    int cell[MAXP], slot[MAXP];
+#pragma unroll
+    for (int k = 0; k < MAXP; ++k) {
+      const int i = tid + k * T;
+      if (i < N) {
+        cell[k] = cell_index(qx[k], qy[k], lx, ly);
+        slot[k] = atomicAdd(&cnt[cell[k]], 1);
+      }
+    }
+    __syncthreads();
+    block_exclusive_scan(cnt, ncell, wave_sums);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < MAXP; ++k) {
+      const int i = tid + k * T;
+      if (i < N) {
+        const int pos = cnt[cell[k]] + slot[k];
+        sqx[pos] = qx[k];
+        sqy[pos] = qy[k];
+        sinf[pos] = (uint32_t)i | ((uint32_t)sp[k] << 24);
+      }
+    }
+    __syncthreads();
+
+    int any = 0;
+#pragma unroll
+    for (int k = 0; k < MAXP; ++k) {
+      const int i = tid + k * T;
+      if (i < N) {
+        int64_t ax = 0, ay = 0;
+        const int cx = cell[k] & (ncx - 1), cy = cell[k] >> lx;
+        const int si = sp[k];
+        for (int oy = loy; oy <= hiy; ++oy) {
+          const int y = (cy + oy + ncy) & (ncy - 1);
+          for (int ox = lox; ox <= hix; ++ox) {
+            const int x = (cx + ox + ncx) & (ncx - 1);
+            const int cc = (y << lx) | x;
+            const int jb = cnt[cc], je = cnt[cc + 1];
+            for (int jj = jb; jj < je; ++jj) {
+              const uint32_t inf = sinf[jj];
+              if ((int)(inf & 0xFFFFFFu) == i) continue;
+              const int sj = (int)(inf >> 24);
+              const float rx = (float)(int32_t)(sqx[jj] - qx[k]) * sx0;
+              const float ry = (float)(int32_t)(sqy[jj] - qy[k]) * sx1;
+              const float r2 = rx * rx + ry * ry;
+              if (r2 < d->cut2[si * kMaxSpecies + sj] && r2 > 0.0f) {
+                const float ir2 = 1.0f / r2;
+                float ir6 = ir2 * ir2;
+                ir6 = ir6 * ir2;
+                const float s6 = d->sig6[si * kMaxSpecies + sj] * ir6;
+                float t = 2.0f * s6;
+                t = t - 1.0f;
+                float fr = d->eps24 * s6;
+                fr = fr * t;
+                fr = fr * ir2;
+                ax += swarm::f2fix24(-fr * rx);
+                ay += swarm::f2fix24(-fr * ry);
+              }
+            }
+          }
+        }
+        float sn, cs;
+        swarm::sincos_turn(an[k], &sn, &cs);
+        float fx = (float)ax * 5.9604644775390625e-08f;
+        float fy = (float)ay * 5.9604644775390625e-08f;
+        fx = fx + fex[k];
+        fy = fy + fey[k];
+        fx = fx + fs[k] * cs;
+        fy = fy + fs[k] * sn;
+        if (sd_mode) {
+          if (fx != 0.0f || fy != 0.0f || tz[k] != 0.0f) any = 1;
+          const float px = fminf(fmaxf(sd_gamma * fx, -sd_maxd), sd_maxd);
+          const float py = fminf(fmaxf(sd_gamma * fy, -sd_maxd), sd_maxd);
+          const float pa = fminf(fmaxf(sd_gamma * tz[k], -sd_maxd), sd_maxd);
+          swarm::advance(qx[k], ix[k], swarm::f2i32(px * isx0));
+          swarm::advance(qy[k], iy[k], swarm::f2i32(py * isx1));
+          an[k] = an[k] + (uint32_t)swarm::f2i32(pa * kAngInvScale);
+        } else {
+          float dx = fx * d->mob_dt[si];
+          float dy = fy * d->mob_dt[si];
+          float dth = tz[k] * d->rot_dt[si];
+          if (noisy) {
+            float g[4];
+            swarm::normals4(k0, k1, (uint32_t)i, step, 0u, g);
+            dx = dx + d->sig_t[si] * g[0];
+            dy = dy + d->sig_t[si] * g[1];
+            dth = dth + d->sig_r[si] * g[2];
+          }
+          swarm::advance(qx[k], ix[k], swarm::f2i32(dx * isx0));
+          swarm::advance(qy[k], iy[k], swarm::f2i32(dy * isx1));
+          an[k] = an[k] + (uint32_t)swarm::f2i32(dth * kAngInvScale);
+          if (s == n_steps - 1) {
+            float vx = fx * d->inv_gt[si], vy = fy * d->inv_gt[si];
+            float w = tz[k] * d->inv_gr[si];
+            if (noisy) {
+              float g[4];
+              swarm::normals4(k0, k1, (uint32_t)i, step, 1u, g);
+              vx = vx + d->sig_v[si] * g[0];
+              vy = vy + d->sig_v[si] * g[1];
+              w = w + d->sig_w[si] * g[2];
+            }
+            const size_t gi = (size_t)e * N + i;
+            st.vel[gi] = vx;
+            st.vel[M + gi] = vy;
+            st.vel[2 * M + gi] = 0.0f;
+            st.omega[gi] = w;
+          }
+        }
+      }
+    }
+    ++steps_done;
+    if (sd_mode) {
+      if (!__syncthreads_or(any)) break;
+    } else {
+      __syncthreads();
+    }
+  }
+
+#pragma unroll
+  for (int k = 0; k < MAXP; ++k) {
+    const int i = tid + k * T;
+    if (i < N) {
+      const size_t g = (size_t)e * N + i;
+      st.q[g] = qx[k];
+      st.q[M + g] = qy[k];
+      st.img[g] = ix[k];
+      st.img[M + g] = iy[k];
+      st.ang[g] = an[k];
+    }
+  }
+  if (sd_mode && tid == 0 && sd_done) sd_done[e] = steps_done;
+  if (!sd_mode && tid == 0) {
+    // every block read *step_ctr before reaching this point
+    const uint32_t ticket = atomicAdd(arrive, 1u);
+    if (ticket == gridDim.x - 1) {
+      *step_ctr = step0 + (uint64_t)n_steps;
+      *arrive = 0u;
+    }
+  }
+}
+
+// ------------------------------------------------- global per-env grid
+// Counting sort of every env into cells (side >= cutoff), written to global
+// memory: start[E][ncell+1], sorted particle index order[E][N].
+__global__ __launch_bounds__(1024) void k_grid_build(DevState st, int lx, int ly,
+                                                     int32_t* __restrict__ start,
+                                                     int32_t* __restrict__ order) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const int ncell = 1 << (lx + ly);
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
+  int32_t* cnt = wave_sums + 16;
+  for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
+  __syncthreads();
+  const size_t M = (size_t)st.m;
+  for (int i = tid; i < N; i += T) {
+    const size_t g = (size_t)e * N + i;
+    atomicAdd(&cnt[cell_index(st.q[g], st.q[M + g], lx, ly)], 1);
+  }
+  __syncthreads();
+  block_exclusive_scan(cnt, ncell, wave_sums);
+  __syncthreads();
+  int32_t* so = start + (size_t)e * (ncell + 1);
+  for (int c = tid; c <= ncell; c += T) so[c] = cnt[c];
+  __syncthreads();
+  for (int i = tid; i < N; i += T) {
+    const size_t g = (size_t)e * N + i;
+    const int pos = atomicAdd(&cnt[cell_index(st.q[g], st.q[M + g], lx, ly)], 1);
+    order[(size_t)e * N + pos] = i;
+  }
+}
+
+// ---------------------------------------------------------- vision cone
+__global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __restrict__ d,
+                                                swarm_vision_params_t vp, int lx, int ly,
+                                                const int32_t* __restrict__ start,
+                                                const int32_t* __restrict__ order,
+                                                const int32_t* __restrict__ agents, int n_agents,
+                                                const float* __restrict__ radii,
+                                                const int32_t* __restrict__ types,
+                                                float* __restrict__ out, int n_envs) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_envs * n_agents) return;
+  const int e = t / n_agents, ai = t - e * n_agents;
+  const int N = st.n;
+  const size_t M = (size_t)st.m;
+  const int i = agents[ai];
+  const size_t gi = (size_t)e * N + i;
+  const uint32_t qxi = st.q[gi], qyi = st.q[M + gi];
+  const int32_t ixi = st.img[gi], iyi = st.img[M + gi];
+  float sn, cs;
+  swarm::sincos_turn(st.ang[gi], &sn, &cs);
+  const float nm = swarm::sqrt_rn(cs * cs + sn * sn);
+  const float mx = cs / nm, my = sn / nm;
+  const int nb = vp.n_cones * vp.n_types;
+  int64_t acc[SWARM_MAX_CONES * 2];  // host guarantees nb <= 32
+  for (int k = 0; k < SWARM_MAX_CONES * 2; ++k) acc[k] = 0;
+  const int ncell = 1 << (lx + ly);
+  const int ncx = 1 << lx, ncy = 1 << ly;
+  const int lox = ncx >= 3 ? -1 : 0, hix = ncx >= 3 ? 1 : ncx - 1;
+  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+  const int cc0 = cell_index(qxi, qyi, lx, ly);
+  const int cx = cc0 & (ncx - 1), cy = cc0 >> lx;
+  const int32_t* so = start + (size_t)e * (ncell + 1);
+  const int32_t* oo = order + (size_t)e * N;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  float* o = out + (size_t)t * nb;
+  for (int oy = loy; oy <= hiy; ++oy) {
+    const int y = (cy + oy + ncy) & (ncy - 1);
+    for (int ox = lox; ox <= hix; ++ox) {
+      const int x = (cx + ox + ncx) & (ncx - 1);
+      const int cc = (y << lx) | x;
+      for (int jj = so[cc]; jj < so[cc + 1]; ++jj) {
+        const int j = oo[jj];
+        if (j == i) continue;
+        const int tj = types[j];
+        int ti = -1;
+        for (int tt = 0; tt < vp.n_types; ++tt)
+          if (vp.detected_types[tt] == tj) ti = tt;
+        if (ti < 0) continue;
+        const size_t gj = (size_t)e * N + j;
+        const int64_t dqx = ((int64_t)(st.img[gj] - ixi) * (int64_t)4294967296LL) +
+                            ((int64_t)st.q[gj] - (int64_t)qxi);
+        const int64_t dqy = ((int64_t)(st.img[M + gj] - iyi) * (int64_t)4294967296LL) +
+                            ((int64_t)st.q[M + gj] - (int64_t)qyi);
+        // unwrapped separations beyond half a box are never within range
+        // (vision_range < L/2): skip them and convert the rest from int32,
+        // whose conversion is a single exact-rounding instruction.
+        if (dqx < -2147483647LL || dqx > 2147483647LL || dqy < -2147483647LL ||
+            dqy > 2147483647LL)
+          continue;
+        const float dx = (float)(int32_t)dqx * sx0, dy = (float)(int32_t)dqy * sx1;
+        const float dist = swarm::sqrt_rn(dx * dx + dy * dy);
+        if (!(dist < vp.vision_range) || dist == 0.0f) continue;
+        float amp = (2.0f * radii[j]) / dist;
+        amp = fminf(1.0f, amp);
+        const float ux = dx / dist, uy = dy / dist;
+        float dot = ux * mx + uy * my;
+        dot = fminf(fmaxf(dot, -1.0f), 1.0f);
+        float an = swarm::acosf_fixed(dot);
+        const float orth = ux * (-my) + uy * mx;
+        if (orth < 0.0f) an = -an;
+        const int64_t fixed = __float2ll_rn(amp * 4294967296.0f);
+        for (int k = 0; k < vp.n_cones; ++k)
+          if (vp.rims[k] < an && an < vp.rims[k + 1]) acc[k * vp.n_types + ti] += fixed;
+      }
+    }
+  }
+  for (int k = 0; k < nb; ++k) o[k] = (float)acc[k] * 2.3283064365386963e-10f;
+}
+
+// ------------------------------------------------------- field distance
+__global__ __launch_bounds__(256) void k_field(DevState st, const double* __restrict__ box,
+                                               const int32_t* __restrict__ agents, int n_agents,
+                                               double s0, double s1, double s2,
+                                               double b0, double b1, double b2,
+                                               uint32_t* __restrict__ hq, int32_t* __restrict__ himg,
+                                               float* __restrict__ d_cur, float* __restrict__ d_prev,
+                                               int update, int init_only, int n_envs) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int A = n_agents * n_envs;
+  if (t >= A) return;
+  const int e = t / n_agents, ai = t - e * n_agents;
+  const int N = st.n;
+  const size_t M = (size_t)st.m;
+  const size_t gi = (size_t)e * N + agents[ai];
+  const double inv32 = 1.0 / 4294967296.0;
+  if (!init_only) {
+    const double src[3] = {s0 / b0, s1 / b1, s2 / b2};
+    const double bs[3] = {b0, b1, b2};
+    float cur[3], prev[3];
+    for (int a = 0; a < 3; ++a) {
+      double pc, hp;
+      if (a < 2) {
+        pc = ((double)st.img[a * M + gi] + (double)st.q[a * M + gi] * inv32) * box[a] / bs[a];
+        hp = ((double)himg[(size_t)a * A + t] + (double)hq[(size_t)a * A + t] * inv32) * box[a] / bs[a];
+      } else {
+        pc = 0.0 / bs[a];
+        hp = 0.0 / bs[a];
+      }
+      cur[a] = (float)(src[a] - pc);
+      prev[a] = (float)(src[a] - hp);
+    }
+    d_cur[t] = swarm::sqrt_rn(cur[0] * cur[0] + cur[1] * cur[1] + cur[2] * cur[2]);
+    d_prev[t] = swarm::sqrt_rn(prev[0] * prev[0] + prev[1] * prev[1] + prev[2] * prev[2]);
+  }
+  if (update || init_only) {
+    for (int a = 0; a < 3; ++a) {
+      hq[(size_t)a * A + t] = a < 2 ? st.q[a * M + gi] : 0u;
+      himg[(size_t)a * A + t] = a < 2 ? st.img[a * M + gi] : 0;
+    }
+  }
+}
+
+// --------------------------------------------------------- pair listing
+__global__ __launch_bounds__(256) void k_pairs(DevState st, const Derived* __restrict__ d,
+                                               int env, float cut2, int lx, int ly,
+                                               const int32_t* __restrict__ start,
+                                               const int32_t* __restrict__ order,
+                                               int32_t* __restrict__ pairs, int max_pairs,
+                                               int32_t* __restrict__ count) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int N = st.n;
+  if (i >= N) return;
+  const size_t M = (size_t)st.m;
+  const size_t gi = (size_t)env * N + i;
+  const uint32_t qxi = st.q[gi], qyi = st.q[M + gi];
+  const int ncell = 1 << (lx + ly);
+  const int ncx = 1 << lx, ncy = 1 << ly;
+  const int lox = ncx >= 3 ? -1 : 0, hix = ncx >= 3 ? 1 : ncx - 1;
+  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+  const int cc0 = cell_index(qxi, qyi, lx, ly);
+  const int cx = cc0 & (ncx - 1), cy = cc0 >> lx;
+  const int32_t* so = start + (size_t)env * (ncell + 1);
+  const int32_t* oo = order + (size_t)env * N;
+  for (int oy = loy; oy <= hiy; ++oy) {
+    const int y = (cy + oy + ncy) & (ncy - 1);
+    for (int ox = lox; ox <= hix; ++ox) {
+      const int x = (cx + ox + ncx) & (ncx - 1);
+      const int cc = (y << lx) | x;
+      for (int jj = so[cc]; jj < so[cc + 1]; ++jj) {
+        const int j = oo[jj];
+        if (j <= i) continue;
+        const size_t gj = (size_t)env * N + j;
+        const float rx = (float)(int32_t)(st.q[gj] - qxi) * d->sx[0];
+        const float ry = (float)(int32_t)(st.q[M + gj] - qyi) * d->sx[1];
+        if (rx * rx + ry * ry < cut2) {
+          const int slot = atomicAdd(count, 1);
+          if (slot < max_pairs) {
+            pairs[2 * slot] = i;
+            pairs[2 * slot + 1] = j;
+          }
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// =================================================================== C ABI
+struct swarm_engine {
+  swarm_params_t params;
+  Derived derived;
+  int32_t n_envs = 0, n = 0;
+  hipStream_t stream = nullptr;
+  int device = 0;
+  DevState st{};
+  Derived* d_derived = nullptr;
+  double* d_box = nullptr;
+  int32_t* d_sd_done = nullptr;
+  uint64_t* d_step = nullptr;
+  uint32_t* d_arrive = nullptr;
+  // observable grid scratch
+  int32_t* d_start = nullptr;
+  size_t start_cap = 0;
+  int32_t* d_order = nullptr;
+  int32_t* d_count = nullptr;
+  int32_t* d_pairs = nullptr;
+  size_t pairs_cap = 0;
+  int lx = 0, ly = 0;  // WCA grid
+  void* allocs[16] = {};
+  int n_allocs = 0;
+};
+
+namespace {
+
+template <typename T>
+int dev_alloc(swarm_engine* e, T** p, size_t count) {
+  void* v = nullptr;
+  HIP_TRY(hipMalloc(&v, std::max<size_t>(count, 1) * sizeof(T)));
+  HIP_TRY(hipMemsetAsync(v, 0, std::max<size_t>(count, 1) * sizeof(T), e->stream));
+  e->allocs[e->n_allocs++] = v;
+  *p = reinterpret_cast<T*>(v);
+  return SWARM_OK;
+}
+
+size_t bd_lds_bytes(int n, int lx, int ly) {
+  const int ncell = 1 << (lx + ly);
+  const int cnt_words = (ncell + 1 + 3) & ~3;
+  return ((sizeof(Derived) + 15) & ~(size_t)15) + 16 * 4 + (size_t)cnt_words * 4 +
+         3 * (size_t)n * 4;
+}
+
+constexpr size_t kMaxLds = 160 * 1024;
+
+int block_threads(int n) {
+  int t = ((n + 63) / 64) * 64;
+  return std::min(std::max(t, 64), 1024);
+}
+
+// Best effort: ROCm admits dynamic LDS up to the device limit at launch; the
+// attribute is only a hint here and a refusal is not an error (a launch that
+// really exceeds the limit fails at hipGetLastError after the launch).
+int set_lds_attributes() {
+  static bool done = false;
+  if (done) return SWARM_OK;
+  const void* fns[] = {reinterpret_cast<const void*>(&k_bd_block<1>),
+                       reinterpret_cast<const void*>(&k_bd_block<2>),
+                       reinterpret_cast<const void*>(&k_bd_block<4>),
+                       reinterpret_cast<const void*>(&k_bd_block<8>),
+                       reinterpret_cast<const void*>(&k_grid_build)};
+  for (const void* f : fns)
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+  (void)hipGetLastError();
+  done = true;
+  return SWARM_OK;
+}
+
+template <int MAXP>
+int launch_bd(swarm_engine* e, int n_steps, int sd_mode, float g, float md) {
+  const int T = block_threads(e->n);
+  const size_t lds = bd_lds_bytes(e->n, e->lx, e->ly);
+  hipLaunchKernelGGL(k_bd_block<MAXP>, dim3(e->n_envs), dim3(T), lds, e->stream,
+                     e->d_derived, e->st, n_steps, e->d_step, e->d_arrive, e->lx, e->ly,
+                     sd_mode, g, md, e->d_sd_done);
+  HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+
+int run_bd(swarm_engine* e, int n_steps, int sd_mode, float g, float md) {
+  const int T = block_threads(e->n);
+  const int maxp = (e->n + T - 1) / T;
+  if (maxp <= 1) return launch_bd<1>(e, n_steps, sd_mode, g, md);
+  if (maxp <= 2) return launch_bd<2>(e, n_steps, sd_mode, g, md);
+  if (maxp <= 4) return launch_bd<4>(e, n_steps, sd_mode, g, md);
+  if (maxp <= 8) return launch_bd<8>(e, n_steps, sd_mode, g, md);
+  return fail(SWARM_ECAPACITY, "more than 8192 particles per env are not supported by this build");
+}
+
+int ensure_grid_scratch(swarm_engine* e, int lx, int ly) {
+  const size_t need = (size_t)e->n_envs * ((size_t)(1 << (lx + ly)) + 1);
+  if (need > e->start_cap) {
+    if (e->d_start) HIP_TRY(hipFree(e->d_start));
+    HIP_TRY(hipMalloc(&e->d_start, need * sizeof(int32_t)));
+    e->start_cap = need;
+  }
+  return SWARM_OK;
+}
+
+int build_grid(swarm_engine* e, int lx, int ly) {
+  int rc = ensure_grid_scratch(e, lx, ly);
+  if (rc) return rc;
+  const int ncell = 1 << (lx + ly);
+  const size_t lds = 16 * 4 + (size_t)(ncell + 1) * 4;
+  if (lds > kMaxLds) return fail(SWARM_ECAPACITY, "observable cell grid too large");
+  hipLaunchKernelGGL(k_grid_build, dim3(e->n_envs), dim3(1024), lds, e->stream, e->st, lx, ly,
+                     e->d_start, e->d_order);
+  HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+
+void to_fixed(double x, double L, uint32_t* q, int32_t* img) {
+  const double u = x / L;
+  double fl = std::floor(u);
+  double qd = std::nearbyint((u - fl) * kTwo32);
+  if (qd >= kTwo32) {
+    qd -= kTwo32;
+    fl += 1.0;
+  }
+  *q = (uint32_t)qd;
+  *img = (int32_t)fl;
+}
+
+// host copy of swarm::sincos_turn (same fp32 operation sequence)
+void host_sincos_turn(uint32_t a, float* s_out, float* c_out) {
+  const uint32_t b = a + 0x20000000u;
+  const uint32_t quad = b >> 30;
+  const int32_t rem = (int32_t)(b & 0x3FFFFFFFu) - 0x20000000;
+  const float x = (float)rem * 1.46291807926715968e-09f;
+  const float z = x * x;
+  float sp = -1.9515295891e-4f;
+  sp = sp * z;
+  sp = sp + 8.3321608736e-3f;
+  sp = sp * z;
+  sp = sp + -1.6666654611e-1f;
+  sp = sp * z;
+  sp = sp * x;
+  const float s = sp + x;
+  float cp = 2.443315711809948e-5f;
+  cp = cp * z;
+  cp = cp + -1.388731625493765e-3f;
+  cp = cp * z;
+  cp = cp + 4.166664568298827e-2f;
+  cp = cp * z;
+  cp = cp * z;
+  float c = cp - 0.5f * z;
+  c = c + 1.0f;
+  float so, co;
+  switch (quad) {
+    case 0: so = s; co = c; break;
+    case 1: so = c; co = -s; break;
+    case 2: so = -s; co = -c; break;
+    default: so = -c; co = s; break;
+  }
+  *s_out = so;
+  *c_out = co;
+}
+
+uint32_t angle_fixed(double dx, double dy) {
+  const double phi = std::atan2(dy, dx);
+  const int64_t a = (int64_t)std::nearbyint(phi / kTwoPi * kTwo32);
+  return (uint32_t)(a & 0xFFFFFFFFLL);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* swarm_last_error(void) { return g_err.c_str(); }
+
+int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_particles,
+                        const int32_t* species, swarm_engine_t** out) {
+  if (!params || !out) return fail(SWARM_EINVAL, "null argument");
+  *out = nullptr;
+  if (params->n_dims != 2)
+    return fail(SWARM_EINVAL, "only n_dims == 2 is implemented in this build");
+  if (!params->periodic)
+    return fail(SWARM_EINVAL, "non-periodic boxes are not implemented on the GPU in this build");
+  if (n_envs < 1 || n_particles < 1) return fail(SWARM_EINVAL, "n_envs and n_particles must be >= 1");
+  if (params->n_species < 1 || params->n_species > kMaxSpecies)
+    return fail(SWARM_EINVAL, "n_species out of range");
+  for (int a = 0; a < 2; ++a)
+    if (!(params->box[a] > 0.0)) return fail(SWARM_EINVAL, "box lengths must be positive");
+  if (!(params->time_step > 0.0)) return fail(SWARM_EINVAL, "time_step must be positive");
+  for (int s = 0; s < params->n_species; ++s)
+    if (!(params->gamma_t[s] > 0.0) || !(params->gamma_r[s] > 0.0) || !(params->radius[s] >= 0.0))
+      return fail(SWARM_EINVAL, "friction coefficients must be positive");
+  if (n_particles > 8192)
+    return fail(SWARM_ECAPACITY, "more than 8192 particles per env are not supported by this build");
+  for (int i = 0; i < n_particles; ++i)
+    if (species[i] < 0 || species[i] >= params->n_species)
+      return fail(SWARM_EINVAL, "species index out of range");
+
+  swarm_engine* e = new swarm_engine();
+  e->params = *params;
+  derive(*params, e->derived);
+  e->n_envs = n_envs;
+  e->n = n_particles;
+  if (hipGetDevice(&e->device) != hipSuccess) {
+    delete e;
+    return fail(SWARM_EDEVICE, "no HIP device");
+  }
+  cell_grid(*params, n_particles, e->derived.rc_max, &e->lx, &e->ly);
+  if (bd_lds_bytes(n_particles, e->lx, e->ly) > kMaxLds) {
+    delete e;
+    return fail(SWARM_ECAPACITY, "env does not fit the LDS-resident integrator");
+  }
+  const size_t M = (size_t)n_envs * n_particles;
+  int rc = SWARM_OK;
+  rc = rc ? rc : dev_alloc(e, &e->st.q, 3 * M);
+  rc = rc ? rc : dev_alloc(e, &e->st.img, 3 * M);
+  rc = rc ? rc : dev_alloc(e, &e->st.ang, M);
+  rc = rc ? rc : dev_alloc(e, &e->st.f_swim, M);
+  rc = rc ? rc : dev_alloc(e, &e->st.torque_z, M);
+  rc = rc ? rc : dev_alloc(e, &e->st.f_ext, 3 * M);
+  rc = rc ? rc : dev_alloc(e, &e->st.vel, 3 * M);
+  rc = rc ? rc : dev_alloc(e, &e->st.omega, M);
+  rc = rc ? rc : dev_alloc(e, &e->st.species, (size_t)n_particles);
+  rc = rc ? rc : dev_alloc(e, &e->d_derived, 1);
+  rc = rc ? rc : dev_alloc(e, &e->d_box, 3);
+  rc = rc ? rc : dev_alloc(e, &e->d_sd_done, (size_t)n_envs);
+  rc = rc ? rc : dev_alloc(e, &e->d_order, M);
+  rc = rc ? rc : dev_alloc(e, &e->d_count, 1);
+  rc = rc ? rc : dev_alloc(e, &e->d_step, 1);
+  rc = rc ? rc : dev_alloc(e, &e->d_arrive, 1);
+  rc = rc ? rc : set_lds_attributes();
+  if (rc) {
+    swarm_engine_destroy(e);
+    return rc;
+  }
+  e->st.n = n_particles;
+  e->st.m = (int32_t)M;
+  std::vector<uint8_t> sp(n_particles);
+  for (int i = 0; i < n_particles; ++i) sp[i] = (uint8_t)species[i];
+  if (hipMemcpy(e->st.species, sp.data(), sp.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(e->d_derived, &e->derived, sizeof(Derived), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(e->d_box, params->box, 3 * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
+    swarm_engine_destroy(e);
+    return fail(SWARM_EDEVICE, "initial upload failed");
+  }
+  *out = e;
+  return SWARM_OK;
+}
+
+void swarm_engine_destroy(swarm_engine_t* e) {
+  if (!e) return;
+  (void)hipDeviceSynchronize();
+  for (int k = 0; k < e->n_allocs; ++k) (void)hipFree(e->allocs[k]);
+  if (e->d_start) (void)hipFree(e->d_start);
+  if (e->d_pairs) (void)hipFree(e->d_pairs);
+  delete e;
+}
+
+int swarm_engine_set_stream(swarm_engine_t* e, void* stream) {
+  if (!e) return fail(SWARM_EINVAL, "null engine");
+  e->stream = reinterpret_cast<hipStream_t>(stream);
+  return SWARM_OK;
+}
+
+int swarm_engine_upload_raw(swarm_engine_t* e, const uint32_t* q, const int32_t* img,
+                            const uint32_t* ang) {
+  if (!e || !q || !img || !ang) return fail(SWARM_EINVAL, "null argument");
+  const size_t M = (size_t)e->st.m;
+  HIP_TRY(hipMemcpyAsync(e->st.q, q, 3 * M * sizeof(uint32_t), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->st.img, img, 3 * M * sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->st.ang, ang, M * sizeof(uint32_t), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return SWARM_OK;
+}
+
+int swarm_engine_download_raw(swarm_engine_t* e, uint32_t* q, int32_t* img, uint32_t* ang) {
+  if (!e) return fail(SWARM_EINVAL, "null engine");
+  const size_t M = (size_t)e->st.m;
+  if (q) HIP_TRY(hipMemcpyAsync(q, e->st.q, 3 * M * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  if (img) HIP_TRY(hipMemcpyAsync(img, e->st.img, 3 * M * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+  if (ang) HIP_TRY(hipMemcpyAsync(ang, e->st.ang, M * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return SWARM_OK;
+}
+
+int swarm_engine_upload_state(swarm_engine_t* e, const double* pos, const double* director) {
+  if (!e || !pos || !director) return fail(SWARM_EINVAL, "null argument");
+  const size_t M = (size_t)e->st.m;
+  std::vector<uint32_t> q(3 * M, 0u), ang(M);
+  std::vector<int32_t> img(3 * M, 0);
+  for (size_t g = 0; g < M; ++g) {
+    for (int a = 0; a < 2; ++a) to_fixed(pos[3 * g + a], e->params.box[a], &q[a * M + g], &img[a * M + g]);
+    ang[g] = angle_fixed(director[3 * g + 0], director[3 * g + 1]);
+  }
+  return swarm_engine_upload_raw(e, q.data(), img.data(), ang.data());
+}
+
+int swarm_engine_download_state(swarm_engine_t* e, double* pos, double* director, double* velocity) {
+  if (!e) return fail(SWARM_EINVAL, "null engine");
+  const size_t M = (size_t)e->st.m;
+  std::vector<uint32_t> q(3 * M), ang(M);
+  std::vector<int32_t> img(3 * M);
+  std::vector<float> vel(velocity ? 3 * M : 0);
+  HIP_TRY(hipMemcpyAsync(q.data(), e->st.q, 3 * M * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(img.data(), e->st.img, 3 * M * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(ang.data(), e->st.ang, M * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  if (velocity)
+    HIP_TRY(hipMemcpyAsync(vel.data(), e->st.vel, 3 * M * sizeof(float), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  for (size_t g = 0; g < M; ++g) {
+    if (pos) {
+      for (int a = 0; a < 2; ++a)
+        pos[3 * g + a] = ((double)img[a * M + g] + (double)q[a * M + g] / kTwo32) * e->params.box[a];
+      pos[3 * g + 2] = 0.0;
+    }
+    if (director) {
+      float so, co;
+      host_sincos_turn(ang[g], &so, &co);
+      director[3 * g + 0] = co;
+      director[3 * g + 1] = so;
+      director[3 * g + 2] = 0.0;
+    }
+    if (velocity)
+      for (int a = 0; a < 3; ++a) velocity[3 * g + a] = vel[a * M + g];
+  }
+  return SWARM_OK;
+}
+
+int swarm_engine_set_actions(swarm_engine_t* e, const float* f_swim, const float* torque_z,
+                             int32_t on_device) {
+  if (!e || !f_swim || !torque_z) return fail(SWARM_EINVAL, "null argument");
+  const size_t M = (size_t)e->st.m;
+  const hipMemcpyKind kind = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  HIP_TRY(hipMemcpyAsync(e->st.f_swim, f_swim, M * sizeof(float), kind, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->st.torque_z, torque_z, M * sizeof(float), kind, e->stream));
+  if (!on_device) HIP_TRY(hipStreamSynchronize(e->stream));
+  return SWARM_OK;
+}
+
+int swarm_engine_set_external_force(swarm_engine_t* e, const double* f_ext) {
+  if (!e || !f_ext) return fail(SWARM_EINVAL, "null argument");
+  const size_t M = (size_t)e->st.m;
+  std::vector<float> f(3 * M);
+  for (size_t g = 0; g < M; ++g)
+    for (int a = 0; a < 3; ++a) f[a * M + g] = (float)f_ext[3 * g + a];
+  HIP_TRY(hipMemcpyAsync(e->st.f_ext, f.data(), 3 * M * sizeof(float), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return SWARM_OK;
+}
+
+int swarm_engine_set_directors(swarm_engine_t* e, const double* dir, const uint8_t* mask) {
+  if (!e || !dir || !mask) return fail(SWARM_EINVAL, "null argument");
+  const size_t M = (size_t)e->st.m;
+  std::vector<uint32_t> ang(M);
+  HIP_TRY(hipMemcpyAsync(ang.data(), e->st.ang, M * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  for (size_t g = 0; g < M; ++g)
+    if (mask[g]) ang[g] = angle_fixed(dir[3 * g + 0], dir[3 * g + 1]);
+  HIP_TRY(hipMemcpyAsync(e->st.ang, ang.data(), M * sizeof(uint32_t), hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return SWARM_OK;
+}
+
+int swarm_engine_remove_overlap(swarm_engine_t* e, int32_t n_steps, double gamma, double max_disp) {
+  if (!e) return fail(SWARM_EINVAL, "null engine");
+  if (n_steps <= 0) return SWARM_OK;
+  return run_bd(e, n_steps, 1, (float)gamma, (float)max_disp);
+}
+
+int swarm_engine_integrate(swarm_engine_t* e, int32_t n_steps) {
+  if (!e) return fail(SWARM_EINVAL, "null engine");
+  if (n_steps < 0) return fail(SWARM_EINVAL, "n_steps must be >= 0");
+  if (n_steps == 0) return SWARM_OK;
+  return run_bd(e, n_steps, 0, 0.0f, 0.0f);
+}
+
+int64_t swarm_engine_step_count(const swarm_engine_t* e) {
+  if (!e) return -1;
+  uint64_t v = 0;
+  if (hipMemcpyAsync(&v, e->d_step, sizeof(v), hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+      hipStreamSynchronize(e->stream) != hipSuccess)
+    return -1;
+  return (int64_t)v;
+}
+
+int swarm_engine_device_views(swarm_engine_t* e, swarm_device_views_t* v) {
+  if (!e || !v) return fail(SWARM_EINVAL, "null argument");
+  v->q = e->st.q;
+  v->img = e->st.img;
+  v->ang = e->st.ang;
+  v->f_swim = e->st.f_swim;
+  v->torque_z = e->st.torque_z;
+  v->f_ext = e->st.f_ext;
+  v->vel = e->st.vel;
+  v->omega_z = e->st.omega;
+  v->species = e->st.species;
+  v->n_envs = e->n_envs;
+  v->n_particles = e->n;
+  return SWARM_OK;
+}
+
+int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const int32_t* agent_idx,
+                      int32_t n_agents, const float* radii, const int32_t* types, float* out) {
+  if (!e || !vp || !agent_idx || !radii || !types || !out) return fail(SWARM_EINVAL, "null argument");
+  if (vp->n_cones < 1 || vp->n_cones > SWARM_MAX_CONES || vp->n_types < 1 ||
+      vp->n_types > SWARM_MAX_DETECTED_TYPES || vp->n_cones * vp->n_types > 2 * SWARM_MAX_CONES)
+    return fail(SWARM_ECAPACITY, "n_cones * n_types exceeds this build's limit (32)");
+  if (n_agents <= 0) return SWARM_OK;
+  if (!(2.0 * vp->vision_range < std::min(e->params.box[0], e->params.box[1])))
+    return fail(SWARM_EINVAL, "vision_range must be below half the box length");
+  int lx, ly;
+  cell_grid(e->params, e->n, (double)vp->vision_range, &lx, &ly);
+  int rc = build_grid(e, lx, ly);
+  if (rc) return rc;
+  const int total = n_agents * e->n_envs;
+  hipLaunchKernelGGL(k_vision, dim3((total + 255) / 256), dim3(256), 0, e->stream, e->st,
+                     e->d_derived, *vp, lx, ly, e->d_start, e->d_order, agent_idx, n_agents, radii,
+                     types, out, e->n_envs);
+  HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+
+int swarm_field_distance(swarm_engine_t* e, const int32_t* agent_idx, int32_t n_agents,
+                         const double source[3], const double box_scale[3], uint32_t* hist_q,
+                         int32_t* hist_img, float* d_cur, float* d_prev, int32_t update_history,
+                         int32_t init_only) {
+  if (!e || !agent_idx || !hist_q || !hist_img) return fail(SWARM_EINVAL, "null argument");
+  if (!init_only && (!d_cur || !d_prev || !source || !box_scale)) return fail(SWARM_EINVAL, "null argument");
+  if (n_agents <= 0) return SWARM_OK;
+  const int total = n_agents * e->n_envs;
+  const double s[3] = {source ? source[0] : 0.0, source ? source[1] : 0.0, source ? source[2] : 0.0};
+  const double b[3] = {box_scale ? box_scale[0] : 1.0, box_scale ? box_scale[1] : 1.0,
+                       box_scale ? box_scale[2] : 1.0};
+  hipLaunchKernelGGL(k_field, dim3((total + 255) / 256), dim3(256), 0, e->stream, e->st, e->d_box,
+                     agent_idx, n_agents, s[0], s[1], s[2], b[0], b[1], b[2], hist_q, hist_img,
+                     d_cur, d_prev, update_history, init_only, e->n_envs);
+  HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+
+int swarm_engine_neighbor_pairs(swarm_engine_t* e, int32_t env, double cutoff, int32_t* pairs,
+                                int32_t max_pairs, int32_t* n_pairs) {
+  if (!e || !pairs || !n_pairs) return fail(SWARM_EINVAL, "null argument");
+  if (env < 0 || env >= e->n_envs) return fail(SWARM_EINVAL, "env out of range");
+  if (!(2.0 * cutoff < std::min(e->params.box[0], e->params.box[1])))
+    return fail(SWARM_EINVAL, "cutoff must be below half the box length");
+  int lx, ly;
+  cell_grid(e->params, e->n, cutoff, &lx, &ly);
+  int rc = build_grid(e, lx, ly);
+  if (rc) return rc;
+  if ((size_t)max_pairs > e->pairs_cap) {
+    if (e->d_pairs) HIP_TRY(hipFree(e->d_pairs));
+    HIP_TRY(hipMalloc(&e->d_pairs, 2 * (size_t)std::max(max_pairs, 1) * sizeof(int32_t)));
+    e->pairs_cap = (size_t)max_pairs;
+  }
+  HIP_TRY(hipMemsetAsync(e->d_count, 0, sizeof(int32_t), e->stream));
+  const float c2 = (float)(cutoff * cutoff);
+  hipLaunchKernelGGL(k_pairs, dim3((e->n + 255) / 256), dim3(256), 0, e->stream, e->st,
+                     e->d_derived, env, c2, lx, ly, e->d_start, e->d_order, e->d_pairs, max_pairs,
+                     e->d_count);
+  HIP_TRY(hipGetLastError());
+  int32_t cnt = 0;
+  HIP_TRY(hipMemcpyAsync(&cnt, e->d_count, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  *n_pairs = cnt;
+  const int32_t got = std::min(cnt, max_pairs);
+  if (got > 0)
+    HIP_TRY(hipMemcpy(pairs, e->d_pairs, 2 * (size_t)got * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (cnt > max_pairs) return fail(SWARM_ECAPACITY, "more pairs than max_pairs");
+  return SWARM_OK;
+}
+
+}  // extern "C"

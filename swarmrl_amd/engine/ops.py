@@ -1,0 +1,244 @@
+"""
+Thin Python wrappers over the observable entry points of the C ABI.
+
+Both call forms of the reference observables/tasks run through the HIP
+kernels:
+  * batched: a ``SwarmView`` of a live engine -> device tensors [E, A, ...];
+  * list:    a Python list of ``Colloid`` objects (the reference contract,
+             e.g. its unit tests) -> the points are uploaded into a small
+             scratch engine with a power-of-two virtual box (exact for
+             integer coordinates) and the same kernels run on it.
+There is no CPU implementation of these computations in the product.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Dict, Tuple
+
+import numpy as np
+import torch
+
+from swarmrl_amd import _capi
+
+_TWO32 = 4294967296.0
+
+
+def to_fixed_host(x: np.ndarray, L: float) -> Tuple[np.ndarray, np.ndarray]:
+    """Same rounding as to_fixed() in swarm_engine.hip (fp64, ties to even)."""
+    u = np.asarray(x, dtype=np.float64) / L
+    fl = np.floor(u)
+    qd = np.rint((u - fl) * _TWO32)
+    wrap = qd >= _TWO32
+    qd = np.where(wrap, qd - _TWO32, qd)
+    fl = np.where(wrap, fl + 1.0, fl)
+    return qd.astype(np.uint64).astype(np.uint32), fl.astype(np.int32)
+
+
+def vision_params(vision_range, half_angle, n_cones, detected_types) -> _capi.SwarmVisionParams:
+    """Pack SubdividedVisionCones parameters; rims in the reference's fp32 order
+    (-a + ((k * a) * 2) / n, subdivided_vision_cones.py:145-148)."""
+    det = [int(t) for t in detected_types]
+    if len(det) > _capi.SWARM_MAX_DETECTED_TYPES:
+        raise ValueError("too many detected types for this build")
+    if n_cones > _capi.SWARM_MAX_CONES:
+        raise ValueError("too many cones for this build")
+    vp = _capi.SwarmVisionParams()
+    vp.vision_range = float(vision_range)
+    vp.vision_half_angle = float(half_angle)
+    vp.n_cones = int(n_cones)
+    vp.n_types = len(det)
+    for i, t in enumerate(det):
+        vp.detected_types[i] = t
+    a = np.float32(half_angle)
+    k = np.arange(n_cones + 1, dtype=np.float32)
+    rims = -a + ((k * a) * np.float32(2)) / np.float32(n_cones)
+    for i, r in enumerate(rims.astype(np.float32)):
+        vp.rims[i] = float(r)
+    return vp
+
+
+def vision_cone(native, n_envs: int, agent_idx: torch.Tensor, radii: torch.Tensor,
+                types: torch.Tensor, vp: _capi.SwarmVisionParams) -> torch.Tensor:
+    """[E, A, n_cones, n_types] fp32 device tensor (k_vision)."""
+    A = int(agent_idx.numel())
+    out = torch.empty((n_envs, A, vp.n_cones, vp.n_types), dtype=torch.float32,
+                      device=agent_idx.device)
+    if A == 0:
+        return out
+    native.bind_stream()
+    native.call(
+        "swarm_vision_cone", ctypes.byref(vp), agent_idx.data_ptr(), A, radii.data_ptr(),
+        types.data_ptr(), out.data_ptr(),
+    )
+    return out
+
+
+def field_distance(native, n_envs: int, agent_idx: torch.Tensor, source, box_scale,
+                   hist_q: torch.Tensor, hist_img: torch.Tensor, update: bool,
+                   init_only: bool = False):
+    """(d_cur, d_prev) fp32 [E, A] device tensors (k_field); updates the history."""
+    A = int(agent_idx.numel())
+    dev = agent_idx.device
+    d_cur = torch.empty((n_envs, A), dtype=torch.float32, device=dev)
+    d_prev = torch.empty((n_envs, A), dtype=torch.float32, device=dev)
+    if A == 0:
+        return d_cur, d_prev
+    src = (ctypes.c_double * 3)(*[float(v) for v in np.asarray(source, dtype=float)[:3]])
+    bs = (ctypes.c_double * 3)(*[float(v) for v in np.asarray(box_scale, dtype=float)[:3]])
+    native.bind_stream()
+    native.call(
+        "swarm_field_distance", agent_idx.data_ptr(), A, ctypes.cast(src, ctypes.c_void_p),
+        ctypes.cast(bs, ctypes.c_void_p), hist_q.data_ptr(), hist_img.data_ptr(),
+        d_cur.data_ptr(), d_prev.data_ptr(), 1 if update else 0, 1 if init_only else 0,
+    )
+    return d_cur, d_prev
+
+
+# ------------------------------------------------------------ list path
+class _PointsEngine:
+    """A scratch single-env engine that holds an arbitrary point set."""
+
+    def __init__(self, n: int, box: float):
+        from swarmrl_amd.engine.swarm_engine import _NativeEngine
+
+        _capi.require_gpu()
+        p = _capi.SwarmParams()
+        p.n_dims = 2
+        p.periodic = 1
+        for a in range(3):
+            p.box[a] = box
+        p.time_step = 1.0
+        p.kT = 0.0
+        p.wca_epsilon = 0.0
+        p.n_species = 1
+        p.radius[0] = 0.0
+        p.gamma_t[0] = 1.0
+        p.gamma_r[0] = 1.0
+        self.native = _NativeEngine(p, 1, np.zeros(n, dtype=np.int32))
+        self.n = n
+        self.box = box
+
+    def upload(self, pos: np.ndarray, director: np.ndarray):
+        pos = np.ascontiguousarray(pos, dtype=np.float64).reshape(self.n, 3)
+        director = np.ascontiguousarray(director, dtype=np.float64).reshape(self.n, 3)
+        self.native.bind_stream()
+        self.native.call("swarm_engine_upload_state", pos.ctypes.data, director.ctypes.data)
+
+
+_points_cache: Dict[tuple, _PointsEngine] = {}
+
+
+def virtual_box(extent: float) -> float:
+    """Power-of-two box comfortably larger than every coordinate/range."""
+    return float(2.0 ** max(4, math.ceil(math.log2(max(extent, 1.0) * 4.0 + 1.0))))
+
+
+def points_engine(n: int, box: float) -> _PointsEngine:
+    key = (n, box, torch.cuda.current_device())
+    eng = _points_cache.get(key)
+    if eng is None:
+        if len(_points_cache) > 32:
+            _points_cache.clear()
+        eng = _PointsEngine(n, box)
+        _points_cache[key] = eng
+    return eng
+
+
+def list_vision_cone(positions: np.ndarray, directors: np.ndarray, types: np.ndarray,
+                     agent_indices, radii: np.ndarray, vision_range: float,
+                     half_angle: float, n_cones: int, detected_types) -> np.ndarray:
+    """Vision cones for a Colloid list: [A, n_cones, n_types] (numpy fp32)."""
+    positions = np.asarray(positions, dtype=np.float64)
+    n = len(positions)
+    extent = float(np.max(np.abs(positions[:, :2]))) + float(vision_range)
+    eng = points_engine(n, virtual_box(extent))
+    eng.upload(positions, directors)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    agent_t = torch.as_tensor(np.asarray(agent_indices, dtype=np.int32), device=dev)
+    radii_t = torch.as_tensor(np.asarray(radii, dtype=np.float32), device=dev)
+    types_t = torch.as_tensor(np.asarray(types, dtype=np.int32), device=dev)
+    vp = vision_params(vision_range, half_angle, n_cones, detected_types)
+    out = vision_cone(eng.native, 1, agent_t, radii_t, types_t, vp)
+    return out[0].cpu().numpy()
+
+
+def list_field_distance(cur_scaled: np.ndarray, prev_scaled: np.ndarray,
+                        source_scaled: np.ndarray):
+    """
+    Distances for the list path: positions and source are already divided by
+    the box (fp64, as the reference does); returns fp32 numpy (d_cur, d_prev).
+    """
+    cur_scaled = np.asarray(cur_scaled, dtype=np.float64).reshape(-1, 3)
+    prev_scaled = np.asarray(prev_scaled, dtype=np.float64).reshape(-1, 3)
+    A = len(cur_scaled)
+    if A == 0:
+        return np.zeros(0, np.float32), np.zeros(0, np.float32)
+    src = np.asarray(source_scaled, dtype=np.float64).reshape(3)
+    extent = max(
+        float(np.max(np.abs(cur_scaled[:, :2]))), float(np.max(np.abs(prev_scaled[:, :2]))), 1.0
+    )
+    L = virtual_box(extent)
+    eng = points_engine(A, L)
+    dirs = np.zeros((A, 3))
+    dirs[:, 0] = 1.0
+    pos = cur_scaled.copy()
+    pos[:, 2] = 0.0
+    eng.upload(pos, dirs)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    hq = np.zeros((3, A), dtype=np.uint32)
+    hi = np.zeros((3, A), dtype=np.int32)
+    for a in range(2):
+        hq[a], hi[a] = to_fixed_host(prev_scaled[:, a], L)
+    hq_t = torch.as_tensor(hq.view(np.int32), device=dev)
+    hi_t = torch.as_tensor(hi, device=dev)
+    agent_t = torch.arange(A, dtype=torch.int32, device=dev)
+    if np.any(cur_scaled[:, 2] != 0) or np.any(prev_scaled[:, 2] != 0):
+        raise NotImplementedError("positions off the z = 0 plane are not supported (2-D build)")
+    # the kernel scales engine coordinates by box[a] / box_scale[a]; the
+    # engine already holds scaled coordinates, so box_scale = 1.
+    d_cur, d_prev = field_distance(eng.native, 1, agent_t, src, np.ones(3), hq_t, hi_t,
+                                   update=False)
+    return d_cur[0].cpu().numpy(), d_prev[0].cpu().numpy()
+
+
+# ------------------------------------------------- history initialisation
+def engine_of(colloids):
+    """The SwarmEngine behind a list of engine particle handles, else None."""
+    if isinstance(colloids, (list, tuple)) and len(colloids) > 0:
+        eng = getattr(colloids[0], "_engine", None)
+        if eng is not None and all(getattr(c, "_engine", None) is eng for c in colloids):
+            return eng
+    return None
+
+
+def snapshot_history(engine, p_type: int):
+    """
+    Raw engine coordinates (q [3, E*A] uint32, img [3, E*A] int32) of the
+    agents of one type, taken now: from the registry before the first
+    integrate (exactly what upload_state will convert), else from the device.
+    """
+    types = np.asarray(engine._types_list, dtype=np.int64)
+    idx = np.nonzero(types == int(p_type))[0]
+    E, N = engine.n_envs, engine.n_particles
+    A = len(idx)
+    hq = np.zeros((3, E, A), dtype=np.uint32)
+    hi = np.zeros((3, E, A), dtype=np.int32)
+    if engine._native is None:
+        pos = np.stack([np.stack(v) for v in engine._pos])  # [E, N, 3]
+        for a in range(2):
+            q, im = to_fixed_host(pos[:, idx, a], float(engine._box[a]))
+            hq[a], hi[a] = q, im
+    else:
+        raw = engine.get_raw_state()
+        hq[:] = raw["q"].reshape(3, E, N)[:, :, idx]
+        hi[:] = raw["img"].reshape(3, E, N)[:, :, idx]
+    return hq.reshape(3, E * A), hi.reshape(3, E * A)
+
+
+def history_tensors(hq: np.ndarray, hi: np.ndarray, device):
+    return (
+        torch.as_tensor(np.ascontiguousarray(hq).view(np.int32), device=device).clone(),
+        torch.as_tensor(np.ascontiguousarray(hi), device=device).clone(),
+    )

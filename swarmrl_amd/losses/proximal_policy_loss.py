@@ -1,0 +1,72 @@
+"""
+PPO loss (reference: swarmrl/losses/proximal_policy_loss.py:23-170), in torch.
+
+loss = sum(-min(r A, clip(r, 1-eps, 1+eps) A)) - c_H * entropy
+       + 0.5 * sum(huber(V, returns)),   r = exp(log p_new(a) - log p_old(a)),
+advantages/returns from GAE on the episode's rewards and predicted values;
+n_epochs gradient steps per episode.
+"""
+
+import torch
+import torch.nn.functional as F
+
+from swarmrl_amd.sampling_strategies.gumbel_distribution import GumbelDistribution
+from swarmrl_amd.value_functions.generalized_advantage_estimate import GAE
+
+
+class Loss:
+    def compute_loss(self, network, episode_data):
+        raise NotImplementedError
+
+
+def _stack(items, device):
+    out = []
+    for x in items:
+        out.append(torch.as_tensor(x, device=device))
+    return torch.stack(out)
+
+
+class ProximalPolicyLoss(Loss):
+    def __init__(self, value_function: GAE = None, sampling_strategy=None, n_epochs: int = 20,
+                 epsilon: float = 0.2, entropy_coefficient: float = 0.01):
+        self.value_function = value_function if value_function is not None else GAE()
+        self.sampling_strategy = sampling_strategy or GumbelDistribution()
+        self.n_epochs = n_epochs
+        self.epsilon = epsilon
+        self.entropy_coefficient = entropy_coefficient
+        self.eps = 1e-8
+
+    def _calculate_loss(self, network, feature_data, action_indices, rewards, old_log_probs):
+        obs_ndim = feature_data.ndim - 2
+        new_logits, predicted_values = network(feature_data, obs_ndim=obs_ndim)
+        predicted_values = predicted_values.squeeze(-1)
+        with torch.no_grad():
+            advantages, returns = self.value_function(rewards=rewards, values=predicted_values)
+        new_probabilities = torch.softmax(new_logits, dim=-1)
+        entropy = self.sampling_strategy.compute_entropy(new_probabilities)
+        chosen = torch.gather(new_probabilities, -1, action_indices.unsqueeze(-1)).squeeze(-1)
+        chosen_log_probs = torch.log(chosen + self.eps)
+        ratio = torch.exp(chosen_log_probs - old_log_probs)
+        total_critic_loss = F.huber_loss(predicted_values, returns, reduction="sum", delta=1.0)
+        clipped = -torch.minimum(
+            ratio * advantages, torch.clamp(ratio, 1 - self.epsilon, 1 + self.epsilon) * advantages
+        )
+        actor_loss = clipped.sum()
+        return actor_loss - self.entropy_coefficient * entropy + 0.5 * total_critic_loss
+
+    def compute_loss(self, network, episode_data):
+        dev = network.device
+        old_log_probs = _stack(episode_data.log_probs, dev).float()
+        features = _stack(episode_data.features, dev).float()
+        actions = _stack(episode_data.actions, dev).long()
+        rewards = _stack(episode_data.rewards, dev).float()
+        # device path: [T, E, A, ...] -> merge env and agent axes
+        if actions.ndim == 3:
+            T, E, A = actions.shape
+            actions = actions.reshape(T, E * A)
+            old_log_probs = old_log_probs.reshape(T, E * A)
+            features = features.reshape(T, E * A, *features.shape[3:])
+            rewards = rewards.reshape(rewards.shape[0], E * A)
+        for _ in range(self.n_epochs):
+            loss = self._calculate_loss(network, features, actions, rewards, old_log_probs)
+            network.update_model(loss)

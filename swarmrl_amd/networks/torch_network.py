@@ -1,0 +1,125 @@
+"""
+Actor-critic network on PyTorch-ROCm (reference: swarmrl/networks/flax_network.py).
+
+``TorchModel.compute_action`` mirrors FlaxModel.compute_action
+(flax_network.py:153-195): logits, values = model(obs); Gumbel sampling;
+log_probs = log(softmax(logits) + 1e-8); exploration; gather the chosen
+log-prob.  Observables of shape (n_agents, ...) are flattened per agent.
+With a device tensor input everything stays on the GPU (no host sync).
+"""
+
+import os
+
+import numpy as np
+import torch
+from torch import nn
+
+from swarmrl_amd.exploration_policies.random_exploration import RandomExploration
+from swarmrl_amd.sampling_strategies.gumbel_distribution import GumbelDistribution
+
+
+class ActorCriticMLP(nn.Module):
+    """Dense(hidden) -> ReLU -> {Dense(n_actions) logits, Dense(1) value}
+    (the network of CI/espresso_tests/integration_tests/test_rl_trainers.py:17-26)."""
+
+    def __init__(self, input_dim: int, n_actions: int = 4, hidden: int = 128):
+        super().__init__()
+        self.hidden = nn.Linear(input_dim, hidden)
+        self.actor = nn.Linear(hidden, n_actions)
+        self.critic = nn.Linear(hidden, 1)
+
+    def forward(self, x):
+        h = torch.relu(self.hidden(x))
+        return self.actor(h), self.critic(h)
+
+
+class TorchModel:
+    """Network wrapper with the FlaxModel surface used by the agents."""
+
+    def __init__(
+        self,
+        torch_model: nn.Module,
+        input_shape: tuple = None,
+        optimizer=None,
+        exploration_policy=RandomExploration(probability=0.0),
+        sampling_strategy=GumbelDistribution(),
+        rng_key: int = None,
+        deployment_mode: bool = False,
+        device=None,
+        learning_rate: float = 1e-3,
+    ):
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) \
+                if torch.cuda.is_available() else torch.device("cpu")
+        self.device = torch.device(device)
+        if rng_key is not None:
+            torch.manual_seed(int(rng_key))
+        self.model = torch_model.to(self.device)
+        self.input_shape = input_shape
+        self.sampling_strategy = sampling_strategy
+        self.exploration_policy = exploration_policy
+        self.deployment_mode = deployment_mode
+        if optimizer is None:
+            optimizer = lambda params: torch.optim.Adam(params, lr=learning_rate)  # noqa: E731
+        self._optimizer_factory = optimizer
+        self.optimizer = None if deployment_mode else optimizer(self.model.parameters())
+        self.epoch_count = 0
+        self.generator = None
+
+    def reinitialize_network(self):
+        for m in self.model.modules():
+            if hasattr(m, "reset_parameters"):
+                m.reset_parameters()
+        self.optimizer = self._optimizer_factory(self.model.parameters())
+
+    def __call__(self, features: torch.Tensor, obs_ndim: int = 1):
+        """Forward over features (..., n_agents, *obs); the trailing obs_ndim
+        dims are flattened per agent.  Returns (logits, values)."""
+        lead = features.shape[: features.ndim - obs_ndim]
+        return self.model(features.reshape(*lead, -1).to(torch.float32))
+
+    @torch.no_grad()
+    def compute_action(self, observables):
+        """(indices, log_probs) for every agent; tensors in -> tensors out."""
+        host = not isinstance(observables, torch.Tensor)
+        if host:
+            obs = torch.as_tensor(np.asarray(observables, dtype=np.float32), device=self.device)
+        else:
+            obs = observables.to(torch.float32)
+        obs = obs.reshape(obs.shape[0], -1)
+        logits, _ = self.model(obs)
+        indices = self.sampling_strategy(logits, generator=self.generator)
+        eps = 1e-8
+        log_probs = torch.log(torch.softmax(logits, dim=-1) + eps)
+        indices = self.exploration_policy(indices, logits.shape[-1], generator=self.generator)
+        chosen = torch.gather(log_probs, 1, indices.reshape(-1, 1)).reshape(-1)
+        if host:
+            return indices.cpu().numpy(), chosen.cpu().numpy()
+        return indices, chosen
+
+    def update_model(self, loss: torch.Tensor):
+        self.optimizer.zero_grad(set_to_none=True)
+        loss.backward()
+        self.optimizer.step()
+        self.epoch_count += 1
+
+    def export_model(self, filename: str = "model", directory: str = "Models"):
+        os.makedirs(directory, exist_ok=True)
+        torch.save(
+            {
+                "model": self.model.state_dict(),
+                "optimizer": self.optimizer.state_dict() if self.optimizer else None,
+                "epoch": self.epoch_count,
+            },
+            os.path.join(directory, filename + ".pt"),
+        )
+
+    def restore_model_state(self, filename, directory):
+        state = torch.load(os.path.join(directory, filename + ".pt"), weights_only=True,
+                           map_location=self.device)
+        self.model.load_state_dict(state["model"])
+        if self.optimizer is not None and state["optimizer"] is not None:
+            self.optimizer.load_state_dict(state["optimizer"])
+        self.epoch_count = int(state["epoch"])
+
+

@@ -1,0 +1,5 @@
+from swarmrl_amd.observables.concentration_field import ConcentrationField
+from swarmrl_amd.observables.observable import Observable
+from swarmrl_amd.observables.subdivided_vision_cones import SubdividedVisionCones
+
+__all__ = ["Observable", "ConcentrationField", "SubdividedVisionCones"]

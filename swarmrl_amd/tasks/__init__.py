@@ -1,0 +1,4 @@
+from swarmrl_amd.tasks import searching
+from swarmrl_amd.tasks.task import Task
+
+__all__ = ["Task", "searching"]

@@ -1,0 +1,56 @@
+"""Device arithmetic (swarm_device.cuh) is bit-identical to the host's:
+correctly rounded sqrt, the fixed-sequence log/acos/sincos polynomials and
+the Philox/Box-Muller normals."""
+
+import ctypes
+import math
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(x, a):
+    import torch  # noqa: F401  (HIP runtime first)
+
+    lib_path = ROOT / "tests" / "csrc" / "libdevmath.so"
+    if not lib_path.exists():
+        import __graft_entry__ as g
+
+        g.build()
+    lib = ctypes.CDLL(str(lib_path))
+    n = len(x)
+    out = np.zeros(9 * n, np.float32)
+    rc = lib.devmath_selftest(x.ctypes.data_as(ctypes.c_void_p), a.ctypes.data_as(ctypes.c_void_p),
+                              ctypes.c_int(n), out.ctypes.data_as(ctypes.c_void_p))
+    assert rc == 0
+    return out
+
+
+def test_device_math_bit_exact(oracle_mod):
+    rng = np.random.default_rng(0)
+    n = 1 << 18
+    # sqrt over many binades, including tiny values
+    x = np.concatenate([
+        rng.random(n // 2).astype(np.float32),
+        (10.0 ** rng.uniform(-35, 30, n // 2)).astype(np.float32),
+    ])
+    x = np.clip(x, np.float32(1e-37), None).astype(np.float32)
+    a = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    out = _run(x, a)
+    o_sqrt, o_log, o_acos = out[:n], out[n:2 * n], out[2 * n:3 * n]
+    o_sin, o_cos = out[3 * n:4 * n], out[4 * n:5 * n]
+    g = out[5 * n:].reshape(n, 4)
+    assert np.array_equal(o_sqrt, np.sqrt(x))  # numpy sqrt is IEEE correctly rounded
+    sub = np.arange(0, n, 97)
+    for i in sub[:3000]:
+        if x[i] < 1.0:
+            assert o_log[i] == np.float32(oracle_mod.logf(float(x[i]))), i
+            assert o_acos[i] == np.float32(oracle_mod.acosf(float(x[i] * np.float32(2) - np.float32(1)))), i
+        s, c = oracle_mod.sincos_turn(int(a[i]))
+        assert o_sin[i] == np.float32(s) and o_cos[i] == np.float32(c), i
+        assert np.array_equal(g[i], oracle_mod.normals4(42, 0, int(i), 7, 0)), i
+    assert math.isfinite(float(o_log[0]))
