@@ -1,0 +1,280 @@
+#!/usr/bin/env python
+"""
+bench.py -- agent-steps/s of the 4096-colloid WCA + vision-cone rollout.
+
+One step = one RL slice for every agent of every env on every rank:
+vision-cone observable (HIP) -> actor-critic MLP + Gumbel sampling (torch) ->
+action table -> 100 Brownian-dynamics sub-steps with WCA (HIP) -> gradient-
+sensing reward (HIP + torch) -> device trajectory ring buffers.  The slice is
+captured once into a HIP graph and replayed.  With N > 1 ranks (one process
+per GPU, RCCL) every rank runs its own envs (seed 42 + env id) and the
+trajectory buffers are all-gathered at the end of each episode.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement".
+"""
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "agent-steps/sec, 4096-colloid WCA+vision-cone rollout @1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+BYTES_PER_PARTICLE_SUBSTEP = 40
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--colloids", type=int, default=4096)
+    ap.add_argument("--envs-per-gpu", type=int, default=1)
+    ap.add_argument("--episode-length", type=int, default=20)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-slices", type=int, default=12)
+    ap.add_argument("--bd-reps", type=int, default=20)
+    return ap.parse_args()
+
+
+def build_workload(args, env_seed, device):
+    import torch
+
+    from swarmrl_amd.actions import Action
+    from swarmrl_amd.agents import ActorCriticAgent
+    from swarmrl_amd.engine import MDParams, SwarmEngine
+    from swarmrl_amd.force_functions import ForceFunction
+    from swarmrl_amd.networks import ActorCriticMLP, TorchModel
+    from swarmrl_amd.observables import SubdividedVisionCones
+    from swarmrl_amd.rollout import EpisodeRecorder
+    from swarmrl_amd.tasks.searching import GradientSensing
+    from swarmrl_amd.units import UnitRegistry
+
+    N, E = args.colloids, args.envs_per_gpu
+    L = 2.0 * math.sqrt(N * 1.0**2 / 0.1)  # area fraction 0.1 in the placement disc
+    ureg = UnitRegistry()
+    params = MDParams(
+        ureg=ureg,
+        box_length=ureg.Quantity([L, L, L], "micrometer"),
+        time_step=ureg.Quantity(1e-3, "second"),
+        time_slice=ureg.Quantity(0.1, "second"),
+        # trajectory output (a "next" row) stays outside the timed slices
+        write_interval=ureg.Quantity(1e4, "second"),
+    )
+    eng = SwarmEngine(params, n_dims=2, seed=env_seed, n_envs=E,
+                      out_folder=f"/tmp/swarm_bench_{os.getpid()}")
+    eng.add_colloids(N, ureg.Quantity(1.0, "micrometer"),
+                     ureg.Quantity(np.array([L / 2, L / 2, 0.0]), "micrometer"),
+                     ureg.Quantity(L / 2, "micrometer"))
+    observable = SubdividedVisionCones(10.0, np.pi / 2, 3, radii=[1.0] * N)
+    task = GradientSensing(source=np.array([L / 2, L / 2, 0.0]), decay_function=lambda d: 1 - d,
+                           box_length=np.array([L, L, L]), reward_scale_factor=10)
+    torch.manual_seed(env_seed)
+    net = TorchModel(ActorCriticMLP(3, 4, 128), input_shape=(3,), device=device)
+    actions = {
+        "RotateClockwise": Action(torque=np.array([0.0, 0.0, 10.0])),
+        "Translate": Action(force=10.0),
+        "RotateCounterClockwise": Action(torque=np.array([0.0, 0.0, -10.0])),
+        "DoNothing": Action(),
+    }
+    agent = ActorCriticAgent(0, net, task, observable, actions, train=False)
+    agent.recorder = EpisodeRecorder(args.episode_length, E, N, (3, 1), device)
+    ff = ForceFunction({"0": agent})
+    agent.reset_agent(eng.colloids)
+    return eng, ff, agent
+
+
+def time_bd_kernel(eng, reps):
+    """Average duration of the fused 100-sub-step BD kernel (HIP events on
+    the stream the kernel is launched on)."""
+    import torch
+
+    stream = torch.cuda.current_stream()
+    start = torch.cuda.Event(enable_timing=True)
+    stop = torch.cuda.Event(enable_timing=True)
+    eng._run(eng.params.steps_per_slice)
+    start.record(stream)
+    for _ in range(reps):
+        eng._run(eng.params.steps_per_slice)
+    stop.record(stream)
+    stop.synchronize()
+    return start.elapsed_time(stop) / reps
+
+
+def cpu_baseline(args):
+    """The CPU oracle (C restatement) + torch-CPU policy on one 4096-colloid
+    env, one thread, for a bounded number of slices."""
+    import torch
+
+    from oracle import oracle
+
+    torch_threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        N = args.colloids
+        L = 2.0 * math.sqrt(N / 0.1)
+        box = [L, L, L]
+        rng = np.random.default_rng(42)
+        r = L / 2 * np.sqrt(rng.random(N))
+        th = 2 * np.pi * rng.random(N)
+        pos = np.stack([L / 2 + r * np.cos(th), L / 2 + r * np.sin(th), np.zeros(N)], 1)
+        a = 2 * np.pi * rng.random(N)
+        dirs = np.stack([np.cos(a), np.sin(a), np.zeros(N)], 1)
+        gt = 6 * np.pi * (1e-3 / 4.0453e-3)
+        gr = 8 * np.pi * (1e-3 / 4.0453e-3)
+        kT = 300.0 / 293.0
+        p = oracle.make_params(box, 1e-3, kT, kT, 42, [(1.0, gt, gr, 1.0358e-6, 4.143e-7)])
+        st = oracle.state_from_positions(pos, dirs, box)
+        sp = np.zeros(N, np.uint8)
+        st, _ = oracle.sd_run(p, st, sp, 1000)
+        agents = np.arange(N)
+        hist = oracle.history_from_state(st, agents)
+        net = torch.nn.Sequential(torch.nn.Linear(3, 128), torch.nn.ReLU(), torch.nn.Linear(128, 5))
+        ftab = np.array([0.0, 10.0, 0.0, 0.0], np.float32)
+        ttab = np.array([10.0, 0.0, -10.0, 0.0], np.float32)
+        src = np.array([L / 2, L / 2, 0.0])
+        t0 = time.perf_counter()
+        for s in range(args.cpu_sample_slices):
+            obs = oracle.vision_cone(p, st, agents, np.ones(N, np.float32), np.zeros(N, np.int32),
+                                     10.0, np.pi / 2, 3, [0])
+            with torch.no_grad():
+                logits = net(torch.as_tensor(obs.reshape(N, 3)))[:, :4]
+                u = torch.rand(logits.shape)
+                idx = torch.argmax(logits - torch.log(-torch.log(u)), dim=-1).numpy()
+                torch.log(torch.softmax(logits, -1) + 1e-8)
+            st, _, _ = oracle.bd_run(p, st, sp, ftab[idx], ttab[idx], 100, step0=100 * s)
+            dc, dp = oracle.field_distance(p, st, agents, src, np.array(box), hist)
+            np.clip(10 * ((1 - dc) - (1 - dp)), 0, None)
+        dt = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(torch_threads)
+    return {
+        "value": N * args.cpu_sample_slices / dt,
+        "unit": "agent-steps/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{args.cpu_sample_slices} slices x {N} colloids (1 env, 100 sub-steps each, "
+                  f"O(N^2) vision cone as in the reference) on 1 host core, {dt:.1f} s",
+    }
+
+
+def main():
+    args = parse_args()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+
+    from swarmrl_amd.rollout import gather_episode
+
+    E = args.envs_per_gpu
+    eng, ff, agent = build_workload(args, 42 + rank * E, device)
+    eng.integrate(1, ff)  # setup, overlap removal, first slice (eager)
+
+    def one_slice():
+        eng.integrate(1, ff)
+
+    graph = None
+    if not args.no_graph:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                one_slice()
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            one_slice()
+
+    def step():
+        if graph is not None:
+            graph.replay()
+        else:
+            one_slice()
+
+    T = args.episode_length
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step()
+        if world > 1 and (k + 1) % T == 0:
+            gather_episode(agent.recorder)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    bd_ms = time_bd_kernel(eng, args.bd_reps)
+    N = args.colloids
+    agent_steps = N * E * world * args.steps
+    value = agent_steps / elapsed
+    achieved = BYTES_PER_PARTICLE_SUBSTEP * N * eng.params.steps_per_slice * E / (bd_ms * 1e-3) / 1e9
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "agent-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 (uint32 fixed-point positions)",
+        "data": "synthetic: seeded disc placement (area fraction 0.1), random-init actor-critic",
+        "config": {
+            "workload": "4096-colloid WCA+vision-cone rollout",
+            "colloids_per_env": N,
+            "envs_per_gpu": E,
+            "substeps_per_slice": eng.params.steps_per_slice,
+            "episode_length": T,
+            "policy": "MLP 3-128-(4+1), Gumbel sampling",
+            "task": "GradientSensing (find centre)",
+            "parallelism": f"episode-parallel, {world} process(es), RCCL all-gather per episode",
+            "hip_graph": graph is not None,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_bd_block (100 fused BD+WCA sub-steps)",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel_ms": bd_ms,
+            "bytes_per_launch": BYTES_PER_PARTICLE_SUBSTEP * N * eng.params.steps_per_slice * E,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

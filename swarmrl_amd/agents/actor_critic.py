@@ -41,6 +41,9 @@ class ActorCriticAgent(Agent):
         self.intrinsic_reward = intrinsic_reward
         self.trajectory = TrajectoryInformation(particle_type=self.particle_type)
         self._tables = None
+        # optional device ring buffers (swarmrl_amd.rollout.EpisodeRecorder):
+        # graph-capturable recording of the batched path
+        self.recorder = None
 
     def __name__(self) -> str:
         return "ActorCriticAgent"
@@ -121,6 +124,8 @@ class ActorCriticAgent(Agent):
                         new_dir[sel] = a.new_direction
                         mask[sel] = True
             chosen = DeviceActions(ftab[idx], ttab[idx], new_dir, mask)
+            if self.recorder is not None:
+                self.recorder.record_action(state_description, idx, logp)
             if self.train:
                 self.trajectory.features.append(state_description)
                 self.trajectory.actions.append(idx)
@@ -141,6 +146,8 @@ class ActorCriticAgent(Agent):
         if self.intrinsic_reward:
             rewards = rewards + self.intrinsic_reward.compute_reward(episode_data=self.trajectory)
         rewards = rewards + external_reward
+        if self.recorder is not None and is_view(colloids):
+            self.recorder.record_reward(rewards)
         if self.train:
             self.trajectory.rewards.append(rewards)
         self.kill_switch = self.task.kill_switch

@@ -4,10 +4,10 @@
 // the reference (ESPResSo Brownian dynamics + WCA via a cell system, driven by
 // swarmrl/engine/espresso.py:1251-1308) runs here as hand-written HIP:
 //
-//   k_bd_block      one workgroup (<=1024 threads) per environment; the whole
-//                   env's state lives in registers, a cell list is rebuilt in
-//                   LDS every sub-step (counting sort), n sub-steps per launch.
-//                   Also runs steepest descent (espresso.py:1161-1168).
+//   integrator      swarm_integrator.cuh: per window k_cluster_build ->
+//                   k_cluster_run -> k_check (cluster-parallel Brownian
+//                   dynamics + WCA, exact fallback to the global path);
+//                   k_global also runs steepest descent (espresso.py:1161-1168).
 //   k_grid_build    per-env cell list in global memory (for the observables).
 //   k_vision        SubdividedVisionCones, one thread per (env, agent).
 //   k_field         ConcentrationField / GradientSensing distances + history.
@@ -28,13 +28,23 @@
 
 #include "../../include/swarmrl_amd.h"
 #include "swarm_device.cuh"
+#include "swarm_integrator.cuh"
 
 namespace {
+
+using swarm::Derived;
+using swarm::DevState;
+using swarm::Scratch;
+using swarm::cell_index;
+using swarm::block_exclusive_scan;
 
 constexpr int kMaxSpecies = SWARM_MAX_SPECIES;
 constexpr double kTwo32 = 4294967296.0;
 constexpr double kTwoPi = 6.283185307179586476925;
-constexpr float kAngInvScale = 683565275.57643158f;  // 2^32 / (2 pi)
+// Verlet-style skin of the cluster decomposition (performance only: results
+// do not depend on it).  2 um keeps inter-cluster approaches below the cutoff
+// over a 100-step slice a ~5-sigma event at the reference's defaults.
+constexpr double kSkin = 2.0;
 
 thread_local std::string g_err;
 
@@ -49,23 +59,6 @@ int fail(int code, const std::string& msg) {
     if (_e != hipSuccess)                                                    \
       return fail(SWARM_EDEVICE, std::string(#expr ": ") + hipGetErrorString(_e)); \
   } while (0)
-
-// fp32 constants derived from swarm_params_t (same derivation as the oracle).
-struct Derived {
-  float sx[3], inv_sx[3];
-  float mob_dt[kMaxSpecies], sig_t[kMaxSpecies];
-  float rot_dt[kMaxSpecies], sig_r[kMaxSpecies];
-  float inv_gt[kMaxSpecies], inv_gr[kMaxSpecies];
-  float sig_v[kMaxSpecies], sig_w[kMaxSpecies];
-  float cut2[kMaxSpecies * kMaxSpecies];
-  float sig6[kMaxSpecies * kMaxSpecies];
-  float eps24;
-  int32_t n_species;
-  uint32_t key0, key1;
-  int32_t noisy;
-  int32_t periodic;
-  double rc_max;
-};
 
 void derive(const swarm_params_t& p, Derived& d) {
   std::memset(&d, 0, sizeof(d));
@@ -94,6 +87,13 @@ void derive(const swarm_params_t& p, Derived& d) {
       d.sig6[s * kMaxSpecies + t] = (float)(rc2 * rc2 * rc2 * 0.5);
       d.rc_max = std::max(d.rc_max, rc);
     }
+  for (int s = 0; s < p.n_species; ++s)
+    for (int t = 0; t < p.n_species; ++t) {
+      const double r = p.radius[s] + p.radius[t] + kSkin;
+      d.nb2[s * kMaxSpecies + t] = (float)(r * r);
+    }
+  d.skin = (float)kSkin;
+  d.rc_max_f = (float)d.rc_max;
   d.eps24 = (float)(24.0 * p.wca_epsilon);
   d.n_species = p.n_species;
   d.key0 = (uint32_t)p.seed;
@@ -128,277 +128,6 @@ void cell_grid(const swarm_params_t& p, int n, double cutoff, int* lx, int* ly) 
   }
   *lx = l[0];
   *ly = l[1];
-}
-
-struct DevState {
-  uint32_t* q;      // [3][M]
-  int32_t* img;     // [3][M]
-  uint32_t* ang;    // [M]
-  float* f_swim;    // [M]
-  float* torque_z;  // [M]
-  float* f_ext;     // [3][M]
-  float* vel;       // [3][M]
-  float* omega;     // [M]
-  uint8_t* species; // [N]
-  int32_t n;        // particles per env
-  int32_t m;        // E * N
-};
-
-// ------------------------------------------------------------ block scan
-// Exclusive scan of data[0..n) in LDS by the whole block; data[n] = total.
-__device__ void block_exclusive_scan(int32_t* data, int n, int32_t* wave_sums) {
-  const int T = blockDim.x;
-  const int tid = threadIdx.x;
-  const int per = (n + T - 1) / T;
-  const int lo = min(tid * per, n), hi = min(lo + per, n);
-  int32_t local = 0;
-  for (int k = lo; k < hi; ++k) local += data[k];
-  // inclusive wave scan of local
-  const int lane = tid & 63, wave = tid >> 6;
-  int32_t v = local;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int32_t o = __shfl_up(v, off, 64);
-    if (lane >= off) v += o;
-  }
-  if (lane == 63) wave_sums[wave] = v;
-  __syncthreads();
-  if (wave == 0) {
-    const int nw = (T + 63) >> 6;
-    int32_t w = lane < nw ? wave_sums[lane] : 0;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int32_t o = __shfl_up(w, off, 64);
-      if (lane >= off) w += o;
-    }
-    if (lane < nw) wave_sums[lane] = w;  // inclusive
-  }
-  __syncthreads();
-  int32_t run = v - local + (wave > 0 ? wave_sums[wave - 1] : 0);
-  for (int k = lo; k < hi; ++k) {
-    const int32_t c = data[k];
-    data[k] = run;
-    run += c;
-  }
-  if (tid == T - 1) data[n] = run;
-}
-
-__device__ __forceinline__ int cell_index(uint32_t qx, uint32_t qy, int lx, int ly) {
-  const int cx = lx == 0 ? 0 : (int)(qx >> (32 - lx));
-  const int cy = ly == 0 ? 0 : (int)(qy >> (32 - ly));
-  return (cy << lx) | cx;
-}
-
-// -------------------------------------------------------------- BD / SD
-// One workgroup per env.  Template MAXP = particles held per thread.
-template <int MAXP>
-__global__ __launch_bounds__(1024) void k_bd_block(const Derived* __restrict__ dglob,
-                                                   DevState st, int n_steps,
-                                                   uint64_t* __restrict__ step_ctr,
-                                                   uint32_t* __restrict__ arrive, int lx,
-                                                   int ly, int sd_mode, float sd_gamma,
-                                                   float sd_maxd, int32_t* sd_done) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int e = blockIdx.x;
-  const int T = blockDim.x;
-  const int tid = threadIdx.x;
-  const int N = st.n;
-  const int ncell = 1 << (lx + ly);
-  const int cnt_words = (ncell + 1 + 3) & ~3;
-
-  Derived* d = reinterpret_cast<Derived*>(smem);
-  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem + ((sizeof(Derived) + 15) & ~15));
-  int32_t* cnt = wave_sums + 16;
-  uint32_t* sqx = reinterpret_cast<uint32_t*>(cnt + cnt_words);
-  uint32_t* sqy = sqx + N;
-  uint32_t* sinf = sqy + N;
-
-  // derived constants -> LDS
-  {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(dglob);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(d);
-    for (int k = tid; k < (int)(sizeof(Derived) / 4); k += T) dst[k] = src[k];
-  }
-
-  uint32_t qx[MAXP], qy[MAXP], an[MAXP];
-  int32_t ix[MAXP], iy[MAXP];
-  int sp[MAXP];
-  float fs[MAXP], tz[MAXP], fex[MAXP], fey[MAXP];
-  const size_t M = (size_t)st.m;
-#pragma unroll
-  for (int k = 0; k < MAXP; ++k) {
-    const int i = tid + k * T;
-    if (i < N) {
-      const size_t g = (size_t)e * N + i;
-      qx[k] = st.q[g];
-      qy[k] = st.q[M + g];
-      ix[k] = st.img[g];
-      iy[k] = st.img[M + g];
-      an[k] = st.ang[g];
-      sp[k] = st.species[i];
-      fs[k] = st.f_swim[g];
-      tz[k] = st.torque_z[g];
-      fex[k] = st.f_ext[g];
-      fey[k] = st.f_ext[M + g];
-    }
-  }
-  __syncthreads();
-
-  const float sx0 = d->sx[0], sx1 = d->sx[1];
-  const float isx0 = d->inv_sx[0], isx1 = d->inv_sx[1];
-  const int ncx = 1 << lx, ncy = 1 << ly;
-  const int lox = ncx >= 3 ? -1 : 0, hix = ncx >= 3 ? 1 : ncx - 1;
-  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
-  const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
-  const bool noisy = d->noisy != 0;
-  // The noise counter lives in device memory so a captured hipGraph replays
-  // with fresh noise; the last workgroup to finish advances it (below).
-  const uint64_t step0 = sd_mode ? 0ull : *step_ctr;
-  int steps_done = 0;
-
-  for (int s = 0; s < n_steps; ++s) {
-    const uint64_t step = step0 + (uint64_t)s;
-    for (int c = tid; c < cnt_words; c += T) cnt[c] = 0;
-    __syncthreads();
-    int cell[MAXP], slot[MAXP];
-#pragma unroll
-    for (int k = 0; k < MAXP; ++k) {
-      const int i = tid + k * T;
-      if (i < N) {
-        cell[k] = cell_index(qx[k], qy[k], lx, ly);
-        slot[k] = atomicAdd(&cnt[cell[k]], 1);
-      }
-    }
-    __syncthreads();
-    block_exclusive_scan(cnt, ncell, wave_sums);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < MAXP; ++k) {
-      const int i = tid + k * T;
-      if (i < N) {
-        const int pos = cnt[cell[k]] + slot[k];
-        sqx[pos] = qx[k];
-        sqy[pos] = qy[k];
-        sinf[pos] = (uint32_t)i | ((uint32_t)sp[k] << 24);
-      }
-    }
-    __syncthreads();
-
-    int any = 0;
-#pragma unroll
-    for (int k = 0; k < MAXP; ++k) {
-      const int i = tid + k * T;
-      if (i < N) {
-        int64_t ax = 0, ay = 0;
-        const int cx = cell[k] & (ncx - 1), cy = cell[k] >> lx;
-        const int si = sp[k];
-        for (int oy = loy; oy <= hiy; ++oy) {
-          const int y = (cy + oy + ncy) & (ncy - 1);
-          for (int ox = lox; ox <= hix; ++ox) {
-            const int x = (cx + ox + ncx) & (ncx - 1);
-            const int cc = (y << lx) | x;
-            const int jb = cnt[cc], je = cnt[cc + 1];
-            for (int jj = jb; jj < je; ++jj) {
-              const uint32_t inf = sinf[jj];
-              if ((int)(inf & 0xFFFFFFu) == i) continue;
-              const int sj = (int)(inf >> 24);
-              const float rx = (float)(int32_t)(sqx[jj] - qx[k]) * sx0;
-              const float ry = (float)(int32_t)(sqy[jj] - qy[k]) * sx1;
-              const float r2 = rx * rx + ry * ry;
-              if (r2 < d->cut2[si * kMaxSpecies + sj] && r2 > 0.0f) {
-                const float ir2 = 1.0f / r2;
-                float ir6 = ir2 * ir2;
-                ir6 = ir6 * ir2;
-                const float s6 = d->sig6[si * kMaxSpecies + sj] * ir6;
-                float t = 2.0f * s6;
-                t = t - 1.0f;
-                float fr = d->eps24 * s6;
-                fr = fr * t;
-                fr = fr * ir2;
-                ax += swarm::f2fix24(-fr * rx);
-                ay += swarm::f2fix24(-fr * ry);
-              }
-            }
-          }
-        }
-        float sn, cs;
-        swarm::sincos_turn(an[k], &sn, &cs);
-        float fx = (float)ax * 5.9604644775390625e-08f;
-        float fy = (float)ay * 5.9604644775390625e-08f;
-        fx = fx + fex[k];
-        fy = fy + fey[k];
-        fx = fx + fs[k] * cs;
-        fy = fy + fs[k] * sn;
-        if (sd_mode) {
-          if (fx != 0.0f || fy != 0.0f || tz[k] != 0.0f) any = 1;
-          const float px = fminf(fmaxf(sd_gamma * fx, -sd_maxd), sd_maxd);
-          const float py = fminf(fmaxf(sd_gamma * fy, -sd_maxd), sd_maxd);
-          const float pa = fminf(fmaxf(sd_gamma * tz[k], -sd_maxd), sd_maxd);
-          swarm::advance(qx[k], ix[k], swarm::f2i32(px * isx0));
-          swarm::advance(qy[k], iy[k], swarm::f2i32(py * isx1));
-          an[k] = an[k] + (uint32_t)swarm::f2i32(pa * kAngInvScale);
-        } else {
-          float dx = fx * d->mob_dt[si];
-          float dy = fy * d->mob_dt[si];
-          float dth = tz[k] * d->rot_dt[si];
-          if (noisy) {
-            float g[4];
-            swarm::normals4(k0, k1, (uint32_t)i, step, 0u, g);
-            dx = dx + d->sig_t[si] * g[0];
-            dy = dy + d->sig_t[si] * g[1];
-            dth = dth + d->sig_r[si] * g[2];
-          }
-          swarm::advance(qx[k], ix[k], swarm::f2i32(dx * isx0));
-          swarm::advance(qy[k], iy[k], swarm::f2i32(dy * isx1));
-          an[k] = an[k] + (uint32_t)swarm::f2i32(dth * kAngInvScale);
-          if (s == n_steps - 1) {
-            float vx = fx * d->inv_gt[si], vy = fy * d->inv_gt[si];
-            float w = tz[k] * d->inv_gr[si];
-            if (noisy) {
-              float g[4];
-              swarm::normals4(k0, k1, (uint32_t)i, step, 1u, g);
-              vx = vx + d->sig_v[si] * g[0];
-              vy = vy + d->sig_v[si] * g[1];
-              w = w + d->sig_w[si] * g[2];
-            }
-            const size_t gi = (size_t)e * N + i;
-            st.vel[gi] = vx;
-            st.vel[M + gi] = vy;
-            st.vel[2 * M + gi] = 0.0f;
-            st.omega[gi] = w;
-          }
-        }
-      }
-    }
-    ++steps_done;
-    if (sd_mode) {
-      if (!__syncthreads_or(any)) break;
-    } else {
-      __syncthreads();
-    }
-  }
-
-#pragma unroll
-  for (int k = 0; k < MAXP; ++k) {
-    const int i = tid + k * T;
-    if (i < N) {
-      const size_t g = (size_t)e * N + i;
-      st.q[g] = qx[k];
-      st.q[M + g] = qy[k];
-      st.img[g] = ix[k];
-      st.img[M + g] = iy[k];
-      st.ang[g] = an[k];
-    }
-  }
-  if (sd_mode && tid == 0 && sd_done) sd_done[e] = steps_done;
-  if (!sd_mode && tid == 0) {
-    // every block read *step_ctr before reaching this point
-    const uint32_t ticket = atomicAdd(arrive, 1u);
-    if (ticket == gridDim.x - 1) {
-      *step_ctr = step0 + (uint64_t)n_steps;
-      *arrive = 0u;
-    }
-  }
 }
 
 // ------------------------------------------------- global per-env grid
@@ -608,9 +337,9 @@ struct swarm_engine {
   hipStream_t stream = nullptr;
   int device = 0;
   DevState st{};
+  Scratch sc{};
   Derived* d_derived = nullptr;
   double* d_box = nullptr;
-  int32_t* d_sd_done = nullptr;
   uint64_t* d_step = nullptr;
   uint32_t* d_arrive = nullptr;
   // observable grid scratch
@@ -620,8 +349,10 @@ struct swarm_engine {
   int32_t* d_count = nullptr;
   int32_t* d_pairs = nullptr;
   size_t pairs_cap = 0;
-  int lx = 0, ly = 0;  // WCA grid
-  void* allocs[16] = {};
+  int lxg = 0, lyg = 0;  // global-path grid: cell side >= rc_max
+  int lxb = 0, lyb = 0;  // cluster-build grid: cell side >= rc_max + skin
+  bool cluster_path = false;
+  void* allocs[48] = {};
   int n_allocs = 0;
 };
 
@@ -637,57 +368,68 @@ int dev_alloc(swarm_engine* e, T** p, size_t count) {
   return SWARM_OK;
 }
 
-size_t bd_lds_bytes(int n, int lx, int ly) {
-  const int ncell = 1 << (lx + ly);
-  const int cnt_words = (ncell + 1 + 3) & ~3;
-  return ((sizeof(Derived) + 15) & ~(size_t)15) + 16 * 4 + (size_t)cnt_words * 4 +
-         3 * (size_t)n * 4;
-}
-
 constexpr size_t kMaxLds = 160 * 1024;
 
-int block_threads(int n) {
-  int t = ((n + 63) / 64) * 64;
-  return std::min(std::max(t, 64), 1024);
+size_t global_lds_bytes(int lx, int ly) { return (16 + (size_t)(1 << (lx + ly)) + 1) * 4; }
+
+size_t build_lds_bytes(int n, int lx, int ly) {
+  const int ncell = 1 << (lx + ly);
+  return (16 + 16 + 68 + 68 + (size_t)((ncell + 1 + 3) & ~3) + 3 * (size_t)n) * 4;
 }
 
-// Best effort: ROCm admits dynamic LDS up to the device limit at launch; the
-// attribute is only a hint here and a refusal is not an error (a launch that
-// really exceeds the limit fails at hipGetLastError after the launch).
-int set_lds_attributes() {
+size_t check_lds_bytes(int lx, int ly) {
+  return (16 + 16 + 1024 + (size_t)(1 << (lx + ly)) + 1) * 4;
+}
+
+// ROCm admits dynamic LDS up to the device limit at launch; this attribute
+// is only a hint, a refusal is not an error (a launch that really exceeds the
+// limit fails at hipGetLastError after the launch).
+void set_lds_attributes() {
   static bool done = false;
-  if (done) return SWARM_OK;
-  const void* fns[] = {reinterpret_cast<const void*>(&k_bd_block<1>),
-                       reinterpret_cast<const void*>(&k_bd_block<2>),
-                       reinterpret_cast<const void*>(&k_bd_block<4>),
-                       reinterpret_cast<const void*>(&k_bd_block<8>),
+  if (done) return;
+  const void* fns[] = {reinterpret_cast<const void*>(&swarm::k_global),
+                       reinterpret_cast<const void*>(&swarm::k_cluster_build),
+                       reinterpret_cast<const void*>(&swarm::k_check),
                        reinterpret_cast<const void*>(&k_grid_build)};
   for (const void* f : fns)
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
   (void)hipGetLastError();
   done = true;
-  return SWARM_OK;
 }
 
-template <int MAXP>
-int launch_bd(swarm_engine* e, int n_steps, int sd_mode, float g, float md) {
-  const int T = block_threads(e->n);
-  const size_t lds = bd_lds_bytes(e->n, e->lx, e->ly);
-  hipLaunchKernelGGL(k_bd_block<MAXP>, dim3(e->n_envs), dim3(T), lds, e->stream,
-                     e->d_derived, e->st, n_steps, e->d_step, e->d_arrive, e->lx, e->ly,
-                     sd_mode, g, md, e->d_sd_done);
+int launch_global(swarm_engine* e, int n_steps, int sd_mode, float g, float md) {
+  hipLaunchKernelGGL(swarm::k_global, dim3(e->n_envs), dim3(1024),
+                     global_lds_bytes(e->lxg, e->lyg), e->stream, e->d_derived, e->st, e->sc,
+                     n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg, sd_mode, g, md);
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
 }
 
-int run_bd(swarm_engine* e, int n_steps, int sd_mode, float g, float md) {
-  const int T = block_threads(e->n);
-  const int maxp = (e->n + T - 1) / T;
-  if (maxp <= 1) return launch_bd<1>(e, n_steps, sd_mode, g, md);
-  if (maxp <= 2) return launch_bd<2>(e, n_steps, sd_mode, g, md);
-  if (maxp <= 4) return launch_bd<4>(e, n_steps, sd_mode, g, md);
-  if (maxp <= 8) return launch_bd<8>(e, n_steps, sd_mode, g, md);
-  return fail(SWARM_ECAPACITY, "more than 8192 particles per env are not supported by this build");
+// One integration window: cluster build -> cluster run -> check/fallback.
+int launch_window(swarm_engine* e, int n_steps) {
+  hipLaunchKernelGGL(swarm::k_cluster_build, dim3(e->n_envs), dim3(1024),
+                     build_lds_bytes(e->n, e->lxb, e->lyb), e->stream, e->d_derived, e->st,
+                     e->sc, e->lxb, e->lyb);
+  HIP_TRY(hipGetLastError());
+  const long waves = (long)e->n_envs * e->sc.wmax;
+  hipLaunchKernelGGL(swarm::k_cluster_run, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+                     e->stream, e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(swarm::k_check, dim3(e->n_envs), dim3(1024),
+                     check_lds_bytes(e->lxg, e->lyg), e->stream, e->d_derived, e->st, e->sc,
+                     n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg);
+  HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+
+int run_bd(swarm_engine* e, int n_steps) {
+  while (n_steps > 0) {
+    const int w = std::min(n_steps, swarm::kMaxWindow);
+    const int rc = e->cluster_path ? launch_window(e, w) : launch_global(e, w, 0, 0.0f, 0.0f);
+    if (rc) return rc;
+    n_steps -= w;
+  }
+  return SWARM_OK;
 }
 
 int ensure_grid_scratch(swarm_engine* e, int lx, int ly) {
@@ -788,8 +530,8 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   for (int s = 0; s < params->n_species; ++s)
     if (!(params->gamma_t[s] > 0.0) || !(params->gamma_r[s] > 0.0) || !(params->radius[s] >= 0.0))
       return fail(SWARM_EINVAL, "friction coefficients must be positive");
-  if (n_particles > 8192)
-    return fail(SWARM_ECAPACITY, "more than 8192 particles per env are not supported by this build");
+  if (n_particles > (1 << 20))
+    return fail(SWARM_ECAPACITY, "more than 2^20 particles per env are not supported");
   for (int i = 0; i < n_particles; ++i)
     if (species[i] < 0 || species[i] >= params->n_species)
       return fail(SWARM_EINVAL, "species index out of range");
@@ -803,11 +545,16 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     delete e;
     return fail(SWARM_EDEVICE, "no HIP device");
   }
-  cell_grid(*params, n_particles, e->derived.rc_max, &e->lx, &e->ly);
-  if (bd_lds_bytes(n_particles, e->lx, e->ly) > kMaxLds) {
+  cell_grid(*params, n_particles, e->derived.rc_max, &e->lxg, &e->lyg);
+  cell_grid(*params, n_particles, e->derived.rc_max + kSkin, &e->lxb, &e->lyb);
+  if (check_lds_bytes(e->lxg, e->lyg) > kMaxLds) {
     delete e;
-    return fail(SWARM_ECAPACITY, "env does not fit the LDS-resident integrator");
+    return fail(SWARM_ECAPACITY, "env cell grid does not fit the LDS of one workgroup");
   }
+  // the cluster path needs the build workgroup's LDS and a non-degenerate
+  // build grid; otherwise every window runs on the global path
+  e->cluster_path = build_lds_bytes(n_particles, e->lxb, e->lyb) <= kMaxLds &&
+                    (1 << e->lxb) >= 3 && (1 << e->lyb) >= 3;
   const size_t M = (size_t)n_envs * n_particles;
   int rc = SWARM_OK;
   rc = rc ? rc : dev_alloc(e, &e->st.q, 3 * M);
@@ -821,12 +568,30 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->st.species, (size_t)n_particles);
   rc = rc ? rc : dev_alloc(e, &e->d_derived, 1);
   rc = rc ? rc : dev_alloc(e, &e->d_box, 3);
-  rc = rc ? rc : dev_alloc(e, &e->d_sd_done, (size_t)n_envs);
   rc = rc ? rc : dev_alloc(e, &e->d_order, M);
   rc = rc ? rc : dev_alloc(e, &e->d_count, 1);
   rc = rc ? rc : dev_alloc(e, &e->d_step, 1);
   rc = rc ? rc : dev_alloc(e, &e->d_arrive, 1);
-  rc = rc ? rc : set_lds_attributes();
+  // integrator scratch
+  const int S = 2 * n_particles + 64 * 66;
+  e->sc.S = S;
+  e->sc.wmax = S / 64;
+  rc = rc ? rc : dev_alloc(e, &e->sc.sqx, M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.sqy, M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.sidx, M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.bq, 2 * M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.bimg, 2 * M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.bang, M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.root, M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.slot_of, M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.ncount, M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.nbr_tmp, M * swarm::kNbMax);
+  rc = rc ? rc : dev_alloc(e, &e->sc.perm, (size_t)n_envs * S);
+  rc = rc ? rc : dev_alloc(e, &e->sc.nbr, (size_t)n_envs * S * 4);
+  rc = rc ? rc : dev_alloc(e, &e->sc.disp, M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.env_waves, (size_t)n_envs);
+  rc = rc ? rc : dev_alloc(e, &e->sc.fallback, (size_t)n_envs);
+  set_lds_attributes();
   if (rc) {
     swarm_engine_destroy(e);
     return rc;
@@ -963,14 +728,14 @@ int swarm_engine_set_directors(swarm_engine_t* e, const double* dir, const uint8
 int swarm_engine_remove_overlap(swarm_engine_t* e, int32_t n_steps, double gamma, double max_disp) {
   if (!e) return fail(SWARM_EINVAL, "null engine");
   if (n_steps <= 0) return SWARM_OK;
-  return run_bd(e, n_steps, 1, (float)gamma, (float)max_disp);
+  return launch_global(e, n_steps, 1, (float)gamma, (float)max_disp);
 }
 
 int swarm_engine_integrate(swarm_engine_t* e, int32_t n_steps) {
   if (!e) return fail(SWARM_EINVAL, "null engine");
   if (n_steps < 0) return fail(SWARM_EINVAL, "n_steps must be >= 0");
   if (n_steps == 0) return SWARM_OK;
-  return run_bd(e, n_steps, 0, 0.0f, 0.0f);
+  return run_bd(e, n_steps);
 }
 
 int64_t swarm_engine_step_count(const swarm_engine_t* e) {

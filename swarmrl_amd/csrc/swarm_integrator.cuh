@@ -1,0 +1,681 @@
+// swarm_integrator.cuh -- Brownian dynamics + WCA integrator kernels.
+//
+// One integration window (<= kMaxWindow sub-steps, normally one RL slice of
+// 100) is three launches:
+//
+//   k_cluster_build  one workgroup per env: cell list (side >= rc + skin),
+//                    neighbour lists, union-find connected components
+//                    ("clusters") of the rc+skin graph, and a packing of the
+//                    clusters into 64-lane wave slots that never straddle a
+//                    wave.  Also snapshots the window-start state.
+//   k_cluster_run    one wave per 64 slots, one lane per particle: all
+//                    sub-steps of the window with no block or grid barrier;
+//                    neighbour positions move lane-to-lane (ds_bpermute).
+//                    Tracks every particle's maximum displacement D.
+//   k_check          one workgroup per env: exact validity test of the
+//                    decomposition (no pair of different clusters can have
+//                    come within the WCA cutoff: d0 >= rc + D_i + D_j for all
+//                    such pairs), and, if it failed (or the build flagged a
+//                    cluster > 64 / a neighbour-list overflow), re-runs the
+//                    env from the snapshot with the global per-sub-step
+//                    algorithm.  Advances the device noise counter.
+//
+// Both paths call the same pair_force() / bd_step() functions and sum pair
+// forces in int64 fixed point, so the result is independent of the
+// decomposition and bit-identical to the CPU oracle.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/swarmrl_amd.h"
+#include "swarm_device.cuh"
+
+namespace swarm {
+
+constexpr int kMaxSpecies = SWARM_MAX_SPECIES;
+constexpr int kNbMax = 15;        // neighbours per particle inside a window
+constexpr int kMaxWindow = 128;   // sub-steps per cluster window
+constexpr float kAngInvScale = 683565275.57643158f;  // 2^32 / (2 pi)
+
+// fp32 constants derived from swarm_params_t (same derivation as the oracle).
+struct Derived {
+  float sx[3], inv_sx[3];
+  float mob_dt[kMaxSpecies], sig_t[kMaxSpecies];
+  float rot_dt[kMaxSpecies], sig_r[kMaxSpecies];
+  float inv_gt[kMaxSpecies], inv_gr[kMaxSpecies];
+  float sig_v[kMaxSpecies], sig_w[kMaxSpecies];
+  float cut2[kMaxSpecies * kMaxSpecies];
+  float sig6[kMaxSpecies * kMaxSpecies];
+  float nb2[kMaxSpecies * kMaxSpecies];  // (r_i + r_j + skin)^2: cluster links
+  float eps24;
+  float skin;
+  float rc_max_f;
+  int32_t n_species;
+  uint32_t key0, key1;
+  int32_t noisy;
+  int32_t periodic;
+  double rc_max;
+};
+
+struct DevState {
+  uint32_t* q;       // [3][M]
+  int32_t* img;      // [3][M]
+  uint32_t* ang;     // [M]
+  float* f_swim;     // [M]
+  float* torque_z;   // [M]
+  float* f_ext;      // [3][M]
+  float* vel;        // [3][M]
+  float* omega;      // [M]
+  uint8_t* species;  // [N]
+  int32_t n;         // particles per env
+  int32_t m;         // E * N
+};
+
+struct Scratch {
+  uint32_t* sqx;      // [M] positions sorted by cell
+  uint32_t* sqy;      // [M]
+  int32_t* sidx;      // [M] particle index of a sorted entry
+  uint32_t* bq;       // [2][M] window-start snapshot
+  int32_t* bimg;      // [2][M]
+  uint32_t* bang;     // [M]
+  int32_t* root;      // [M] cluster id (root particle)
+  int32_t* slot_of;   // [M] wave slot of a particle
+  int32_t* ncount;    // [M] neighbour count
+  int32_t* nbr_tmp;   // [M][kNbMax] neighbour particle indices
+  int32_t* perm;      // [E][S] particle of a slot (-1: idle lane)
+  uint32_t* nbr;      // [E][S][4] packed: byte 0 count, bytes 1..15 lanes
+  float* disp;        // [M] max displacement over the window
+  int32_t* env_waves; // [E]
+  int32_t* fallback;  // [E]
+  int32_t S;          // slots per env
+  int32_t wmax;       // S / 64
+};
+
+// ---------------------------------------------------------------- helpers
+__device__ __forceinline__ int cell_index(uint32_t qx, uint32_t qy, int lx, int ly) {
+  const int cx = lx == 0 ? 0 : (int)(qx >> (32 - lx));
+  const int cy = ly == 0 ? 0 : (int)(qy >> (32 - ly));
+  return (cy << lx) | cx;
+}
+
+// Exclusive scan of data[0..n) in LDS by the whole block; data[n] = total.
+__device__ inline void block_exclusive_scan(int32_t* data, int n, int32_t* wave_sums) {
+  const int T = blockDim.x;
+  const int tid = threadIdx.x;
+  const int per = (n + T - 1) / T;
+  const int lo = min(tid * per, n), hi = min(lo + per, n);
+  int32_t local = 0;
+  for (int k = lo; k < hi; ++k) local += data[k];
+  const int lane = tid & 63, wave = tid >> 6;
+  int32_t v = local;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t o = __shfl_up(v, off, 64);
+    if (lane >= off) v += o;
+  }
+  if (lane == 63) wave_sums[wave] = v;
+  __syncthreads();
+  if (wave == 0) {
+    const int nw = (T + 63) >> 6;
+    int32_t w = lane < nw ? wave_sums[lane] : 0;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int32_t o = __shfl_up(w, off, 64);
+      if (lane >= off) w += o;
+    }
+    if (lane < nw) wave_sums[lane] = w;
+  }
+  __syncthreads();
+  int32_t run = v - local + (wave > 0 ? wave_sums[wave - 1] : 0);
+  for (int k = lo; k < hi; ++k) {
+    const int32_t c = data[k];
+    data[k] = run;
+    run += c;
+  }
+  if (tid == T - 1) data[n] = run;
+}
+
+// WCA force on i from j (r = x_j - x_i), accumulated in 2^-24 fixed point.
+__device__ __forceinline__ void pair_force(const Derived* __restrict__ d, int si, int sj,
+                                           float rx, float ry, int64_t& ax, int64_t& ay) {
+  const float r2 = rx * rx + ry * ry;
+  if (r2 < d->cut2[si * kMaxSpecies + sj] && r2 > 0.0f) {
+    const float ir2 = 1.0f / r2;
+    float ir6 = ir2 * ir2;
+    ir6 = ir6 * ir2;
+    const float s6 = d->sig6[si * kMaxSpecies + sj] * ir6;
+    float t = 2.0f * s6;
+    t = t - 1.0f;
+    float fr = d->eps24 * s6;
+    fr = fr * t;
+    fr = fr * ir2;
+    ax += f2fix24(-fr * rx);
+    ay += f2fix24(-fr * ry);
+  }
+}
+
+struct PState {
+  uint32_t qx, qy, an;
+  int32_t ix, iy;
+};
+
+// One Brownian-dynamics sub-step of one particle from its summed WCA force.
+__device__ __forceinline__ void bd_step(const Derived* __restrict__ d, PState& p, int si,
+                                        int64_t ax, int64_t ay, float fs, float tz, float fex,
+                                        float fey, uint32_t k0, uint32_t k1, uint32_t id,
+                                        uint64_t step, bool last, float* vx, float* vy,
+                                        float* w) {
+  float sn, cs;
+  sincos_turn(p.an, &sn, &cs);
+  float fx = (float)ax * 5.9604644775390625e-08f;
+  float fy = (float)ay * 5.9604644775390625e-08f;
+  fx = fx + fex;
+  fy = fy + fey;
+  fx = fx + fs * cs;
+  fy = fy + fs * sn;
+  float dx = fx * d->mob_dt[si];
+  float dy = fy * d->mob_dt[si];
+  float dth = tz * d->rot_dt[si];
+  const bool noisy = d->noisy != 0;
+  if (noisy) {
+    float g[4];
+    normals4(k0, k1, id, step, 0u, g);
+    dx = dx + d->sig_t[si] * g[0];
+    dy = dy + d->sig_t[si] * g[1];
+    dth = dth + d->sig_r[si] * g[2];
+  }
+  advance(p.qx, p.ix, f2i32(dx * d->inv_sx[0]));
+  advance(p.qy, p.iy, f2i32(dy * d->inv_sx[1]));
+  p.an = p.an + (uint32_t)f2i32(dth * kAngInvScale);
+  if (last) {
+    float v0 = fx * d->inv_gt[si], v1 = fy * d->inv_gt[si];
+    float om = tz * d->inv_gr[si];
+    if (noisy) {
+      float g[4];
+      normals4(k0, k1, id, step, 1u, g);
+      v0 = v0 + d->sig_v[si] * g[0];
+      v1 = v1 + d->sig_v[si] * g[1];
+      om = om + d->sig_w[si] * g[2];
+    }
+    *vx = v0;
+    *vy = v1;
+    *w = om;
+  }
+}
+
+// One steepest-descent step of one particle (espresso.py:1163-1168).
+__device__ __forceinline__ bool sd_step(const Derived* __restrict__ d, PState& p, int64_t ax,
+                                        int64_t ay, float fs, float tz, float fex, float fey,
+                                        float g, float md) {
+  float sn, cs;
+  sincos_turn(p.an, &sn, &cs);
+  float fx = (float)ax * 5.9604644775390625e-08f;
+  float fy = (float)ay * 5.9604644775390625e-08f;
+  fx = fx + fex;
+  fy = fy + fey;
+  fx = fx + fs * cs;
+  fy = fy + fs * sn;
+  const bool any = fx != 0.0f || fy != 0.0f || tz != 0.0f;
+  const float px = fminf(fmaxf(g * fx, -md), md);
+  const float py = fminf(fmaxf(g * fy, -md), md);
+  const float pa = fminf(fmaxf(g * tz, -md), md);
+  advance(p.qx, p.ix, f2i32(px * d->inv_sx[0]));
+  advance(p.qy, p.iy, f2i32(py * d->inv_sx[1]));
+  p.an = p.an + (uint32_t)f2i32(pa * kAngInvScale);
+  return any;
+}
+
+// ------------------------------------------------------- global path
+// All sub-steps of env e by one workgroup: per sub-step a counting sort into
+// cells of side >= rc_max (counts in LDS, sorted copy in global scratch), then
+// every particle sums its pair forces over the 3x3 cells and is advanced.
+// Spill-free: no per-thread particle arrays.
+__device__ void block_global_run(const Derived* __restrict__ d, const DevState& st,
+                                 const Scratch& sc, int e, int n_steps, uint64_t step0, int lx,
+                                 int ly, bool sd_mode, float g, float md, int32_t* cnt,
+                                 int32_t* wave_sums) {
+  const int T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int ncell = 1 << (lx + ly);
+  const int ncx = 1 << lx, ncy = 1 << ly;
+  const int lox = ncx >= 3 ? -1 : 0, hix = ncx >= 3 ? 1 : ncx - 1;
+  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+  const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  for (int s = 0; s < n_steps; ++s) {
+    for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
+    __syncthreads();
+    for (int i = tid; i < N; i += T)
+      atomicAdd(&cnt[cell_index(st.q[base + i], st.q[M + base + i], lx, ly)], 1);
+    __syncthreads();
+    block_exclusive_scan(cnt, ncell, wave_sums);
+    __syncthreads();
+    for (int i = tid; i < N; i += T) {
+      const uint32_t qx = st.q[base + i], qy = st.q[M + base + i];
+      const int pos = atomicAdd(&cnt[cell_index(qx, qy, lx, ly)], 1);
+      sc.sqx[base + pos] = qx;
+      sc.sqy[base + pos] = qy;
+      sc.sidx[base + pos] = i;
+    }
+    __syncthreads();  // cell c now spans [c ? cnt[c-1] : 0, cnt[c])
+    int any = 0;
+    for (int i = tid; i < N; i += T) {
+      const size_t gi = base + i;
+      PState p;
+      p.qx = st.q[gi];
+      p.qy = st.q[M + gi];
+      p.ix = st.img[gi];
+      p.iy = st.img[M + gi];
+      p.an = st.ang[gi];
+      const int si = st.species[i];
+      int64_t ax = 0, ay = 0;
+      const int c0 = cell_index(p.qx, p.qy, lx, ly);
+      const int cx = c0 & (ncx - 1), cy = c0 >> lx;
+      for (int oy = loy; oy <= hiy; ++oy) {
+        const int y = (cy + oy + ncy) & (ncy - 1);
+        for (int ox = lox; ox <= hix; ++ox) {
+          const int x = (cx + ox + ncx) & (ncx - 1);
+          const int cc = (y << lx) | x;
+          const int jb = cc ? cnt[cc - 1] : 0, je = cnt[cc];
+          for (int jj = jb; jj < je; ++jj) {
+            const int j = sc.sidx[base + jj];
+            if (j == i) continue;
+            const float rx = (float)(int32_t)(sc.sqx[base + jj] - p.qx) * sx0;
+            const float ry = (float)(int32_t)(sc.sqy[base + jj] - p.qy) * sx1;
+            pair_force(d, si, st.species[j], rx, ry, ax, ay);
+          }
+        }
+      }
+      const float fs = st.f_swim[gi], tz = st.torque_z[gi];
+      const float fex = st.f_ext[gi], fey = st.f_ext[M + gi];
+      if (sd_mode) {
+        any |= sd_step(d, p, ax, ay, fs, tz, fex, fey, g, md) ? 1 : 0;
+      } else {
+        float vx, vy, w;
+        const bool last = s == n_steps - 1;
+        bd_step(d, p, si, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
+                last, &vx, &vy, &w);
+        if (last) {
+          st.vel[gi] = vx;
+          st.vel[M + gi] = vy;
+          st.vel[2 * M + gi] = 0.0f;
+          st.omega[gi] = w;
+        }
+      }
+      st.q[gi] = p.qx;
+      st.q[M + gi] = p.qy;
+      st.img[gi] = p.ix;
+      st.img[M + gi] = p.iy;
+      st.ang[gi] = p.an;
+    }
+    if (sd_mode) {
+      if (!__syncthreads_or(any)) break;
+    } else {
+      __syncthreads();
+    }
+  }
+}
+
+// Advance the device noise counter once every workgroup of the launch has
+// read it (the last arriving workgroup does it).
+__device__ __forceinline__ void advance_counter(uint64_t* step_ctr, uint32_t* arrive,
+                                                uint64_t step0, int n_steps) {
+  if (threadIdx.x == 0) {
+    const uint32_t ticket = atomicAdd(arrive, 1u);
+    if (ticket == gridDim.x - 1) {
+      *step_ctr = step0 + (uint64_t)n_steps;
+      *arrive = 0u;
+    }
+  }
+}
+
+// Global-path launch: n_steps sub-steps (or SD steps) of every env.
+__global__ __launch_bounds__(1024) void k_global(const Derived* __restrict__ d, DevState st,
+                                                 Scratch sc, int n_steps,
+                                                 uint64_t* __restrict__ step_ctr,
+                                                 uint32_t* __restrict__ arrive, int lx, int ly,
+                                                 int sd_mode, float g, float md) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
+  int32_t* cnt = wave_sums + 16;
+  const uint64_t step0 = sd_mode ? 0ull : *step_ctr;
+  block_global_run(d, st, sc, blockIdx.x, n_steps, step0, lx, ly, sd_mode != 0, g, md, cnt,
+                   wave_sums);
+  if (!sd_mode) advance_counter(step_ctr, arrive, step0, n_steps);
+}
+
+// ------------------------------------------------------ cluster build
+__device__ __forceinline__ int uf_find(volatile int32_t* parent, int x) {
+  while (true) {
+    const int p = parent[x];
+    if (p == x) return x;
+    x = p;
+  }
+}
+
+__device__ __forceinline__ void uf_union(int32_t* parent, int a, int b) {
+  while (true) {
+    a = uf_find(parent, a);
+    b = uf_find(parent, b);
+    if (a == b) return;
+    if (a < b) {
+      const int t = a;
+      a = b;
+      b = t;
+    }
+    // hook the larger root under the smaller one: no cycles can form
+    if (atomicCAS(&parent[a], a, b) == a) return;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_cluster_build(const Derived* __restrict__ d,
+                                                        DevState st, Scratch sc, int lx,
+                                                        int ly) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int ncell = 1 << (lx + ly);
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);  // 16
+  int32_t* misc = wave_sums + 16;                          // 16
+  int32_t* classcnt = misc + 16;                           // 68
+  int32_t* wavebase = classcnt + 68;                       // 68
+  int32_t* cnt = wavebase + 68;                            // ncell + 1 (padded)
+  int32_t* parent = cnt + ((ncell + 1 + 3) & ~3);
+  int32_t* csz = parent + N;
+  int32_t* cbase = csz + N;
+  const int S = sc.S;
+
+  for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
+  for (int k = tid; k < 68; k += T) classcnt[k] = 0;
+  if (tid < 16) misc[tid] = 0;
+  for (int i = tid; i < N; i += T) {
+    parent[i] = i;
+    csz[i] = 0;
+    const size_t gi = base + i;
+    sc.bq[gi] = st.q[gi];
+    sc.bq[M + gi] = st.q[M + gi];
+    sc.bimg[gi] = st.img[gi];
+    sc.bimg[M + gi] = st.img[M + gi];
+    sc.bang[gi] = st.ang[gi];
+  }
+  for (int k = tid; k < S; k += T) sc.perm[(size_t)e * S + k] = -1;
+  __syncthreads();
+
+  // cell sort (side >= rc_max + skin)
+  for (int i = tid; i < N; i += T)
+    atomicAdd(&cnt[cell_index(st.q[base + i], st.q[M + base + i], lx, ly)], 1);
+  __syncthreads();
+  block_exclusive_scan(cnt, ncell, wave_sums);
+  __syncthreads();
+  for (int i = tid; i < N; i += T) {
+    const uint32_t qx = st.q[base + i], qy = st.q[M + base + i];
+    const int pos = atomicAdd(&cnt[cell_index(qx, qy, lx, ly)], 1);
+    sc.sqx[base + pos] = qx;
+    sc.sqy[base + pos] = qy;
+    sc.sidx[base + pos] = i;
+  }
+  __syncthreads();
+
+  // neighbours within r_i + r_j + skin, union of the pairs
+  const int ncx = 1 << lx, ncy = 1 << ly;
+  const int lox = ncx >= 3 ? -1 : 0, hix = ncx >= 3 ? 1 : ncx - 1;
+  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  for (int i = tid; i < N; i += T) {
+    const uint32_t qx = st.q[base + i], qy = st.q[M + base + i];
+    const int si = st.species[i];
+    const int c0 = cell_index(qx, qy, lx, ly);
+    const int cx = c0 & (ncx - 1), cy = c0 >> lx;
+    int nc = 0;
+    for (int oy = loy; oy <= hiy; ++oy) {
+      const int y = (cy + oy + ncy) & (ncy - 1);
+      for (int ox = lox; ox <= hix; ++ox) {
+        const int x = (cx + ox + ncx) & (ncx - 1);
+        const int cc = (y << lx) | x;
+        const int jb = cc ? cnt[cc - 1] : 0, je = cnt[cc];
+        for (int jj = jb; jj < je; ++jj) {
+          const int j = sc.sidx[base + jj];
+          if (j == i) continue;
+          const float rx = (float)(int32_t)(sc.sqx[base + jj] - qx) * sx0;
+          const float ry = (float)(int32_t)(sc.sqy[base + jj] - qy) * sx1;
+          if (rx * rx + ry * ry < d->nb2[si * kMaxSpecies + st.species[j]]) {
+            if (nc < kNbMax)
+              sc.nbr_tmp[(base + i) * kNbMax + nc] = j;
+            else
+              misc[0] = 1;  // neighbour overflow -> global path for this env
+            ++nc;
+            if (i < j) uf_union(parent, i, j);
+          }
+        }
+      }
+    }
+    sc.ncount[base + i] = nc < kNbMax ? nc : kNbMax;
+  }
+  __syncthreads();
+  for (int i = tid; i < N; i += T) parent[i] = uf_find(parent, i);
+  __syncthreads();
+  for (int i = tid; i < N; i += T) sc.slot_of[base + i] = atomicAdd(&csz[parent[i]], 1);
+  __syncthreads();
+  for (int i = tid; i < N; i += T) {
+    if (parent[i] != i) continue;
+    const int s = csz[i];
+    if (s > 64)
+      misc[0] = 1;  // cluster wider than a wave -> global path for this env
+    else
+      cbase[i] = atomicAdd(&classcnt[s], 1);
+  }
+  __syncthreads();
+  if (misc[0]) {
+    if (tid == 0) {
+      sc.fallback[e] = 1;
+      sc.env_waves[e] = 0;
+    }
+    return;
+  }
+  if (tid < 64) {
+    const int s = tid + 1;
+    const int per = 64 / s;
+    int32_t w = (classcnt[s] + per - 1) / per;
+    const int32_t own = w;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int32_t o = __shfl_up(w, off, 64);
+      if (tid >= off) w += o;
+    }
+    wavebase[s] = w - own;
+    if (tid == 63) misc[1] = w;
+  }
+  __syncthreads();
+  for (int i = tid; i < N; i += T) {
+    if (parent[i] != i) continue;
+    const int s = csz[i];
+    const int per = 64 / s;
+    const int r = cbase[i];
+    cbase[i] = (wavebase[s] + r / per) * 64 + (r % per) * s;
+  }
+  __syncthreads();
+  for (int i = tid; i < N; i += T) {
+    const int root = parent[i];
+    const int slot = cbase[root] + sc.slot_of[base + i];
+    sc.slot_of[base + i] = slot;
+    sc.perm[(size_t)e * S + slot] = i;
+    sc.root[base + i] = root;
+  }
+  __syncthreads();
+  for (int i = tid; i < N; i += T) {
+    const int slot = sc.slot_of[base + i];
+    const int nc = sc.ncount[base + i];
+    uint32_t wds[4] = {(uint32_t)nc, 0u, 0u, 0u};
+    for (int k = 0; k < nc; ++k) {
+      const int j = sc.nbr_tmp[(base + i) * kNbMax + k];
+      const uint32_t lane = (uint32_t)(sc.slot_of[base + j] & 63);
+      const int b = k + 1;
+      wds[b >> 2] |= lane << ((b & 3) * 8);
+    }
+    uint32_t* out = sc.nbr + ((size_t)e * S + slot) * 4;
+    out[0] = wds[0];
+    out[1] = wds[1];
+    out[2] = wds[2];
+    out[3] = wds[3];
+  }
+  if (tid == 0) {
+    sc.env_waves[e] = misc[1];
+    sc.fallback[e] = 0;
+  }
+}
+
+// -------------------------------------------------------- cluster run
+__device__ __forceinline__ uint32_t nb_lane(const uint32_t (&w)[4], int b) {
+  return (w[b >> 2] >> ((b & 3) * 8)) & 0xffu;
+}
+
+__global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__ d, DevState st,
+                                                     Scratch sc, int n_envs, int n_steps,
+                                                     const uint64_t* __restrict__ step_ctr) {
+  const int lane = threadIdx.x & 63;
+  const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int e = gw / sc.wmax;
+  const int w = gw - e * sc.wmax;
+  if (e >= n_envs) return;
+  if (sc.fallback[e] != 0 || w >= sc.env_waves[e]) return;
+  const int N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int slot = w * 64 + lane;
+  const int i = sc.perm[(size_t)e * sc.S + slot];
+  const bool active = i >= 0;
+  PState p = {0u, 0u, 0u, 0, 0};
+  int si = 0;
+  float fs = 0.0f, tz = 0.0f, fex = 0.0f, fey = 0.0f;
+  uint32_t nw[4] = {0u, 0u, 0u, 0u};
+  const size_t gi = base + (active ? i : 0);
+  if (active) {
+    p.qx = st.q[gi];
+    p.qy = st.q[M + gi];
+    p.ix = st.img[gi];
+    p.iy = st.img[M + gi];
+    p.an = st.ang[gi];
+    si = st.species[i];
+    fs = st.f_swim[gi];
+    tz = st.torque_z[gi];
+    fex = st.f_ext[gi];
+    fey = st.f_ext[M + gi];
+    const uint32_t* nb = sc.nbr + ((size_t)e * sc.S + slot) * 4;
+    nw[0] = nb[0];
+    nw[1] = nb[1];
+    nw[2] = nb[2];
+    nw[3] = nb[3];
+  }
+  const int cnt = (int)(nw[0] & 0xffu);
+  int kmax = cnt;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) kmax = max(kmax, __shfl_xor(kmax, off, 64));
+  const uint64_t step0 = *step_ctr;
+  const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const uint32_t q0x = p.qx, q0y = p.qy;
+  float dmax2 = 0.0f;
+  float vx = 0.0f, vy = 0.0f, om = 0.0f;
+  for (int s = 0; s < n_steps; ++s) {
+    int64_t ax = 0, ay = 0;
+#pragma unroll
+    for (int k = 0; k < kNbMax; ++k) {
+      if (k < kmax) {  // wave-uniform
+        const int src = k < cnt ? (int)nb_lane(nw, k + 1) : lane;
+        const uint32_t oqx = (uint32_t)__shfl((int)p.qx, src, 64);
+        const uint32_t oqy = (uint32_t)__shfl((int)p.qy, src, 64);
+        const int osp = __shfl(si, src, 64);
+        if (k < cnt) {
+          const float rx = (float)(int32_t)(oqx - p.qx) * sx0;
+          const float ry = (float)(int32_t)(oqy - p.qy) * sx1;
+          pair_force(d, si, osp, rx, ry, ax, ay);
+        }
+      }
+    }
+    if (active) {
+      bd_step(d, p, si, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
+              s == n_steps - 1, &vx, &vy, &om);
+      const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
+      const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
+      dmax2 = fmaxf(dmax2, ddx * ddx + ddy * ddy);
+    }
+  }
+  if (active) {
+    st.q[gi] = p.qx;
+    st.q[M + gi] = p.qy;
+    st.img[gi] = p.ix;
+    st.img[M + gi] = p.iy;
+    st.ang[gi] = p.an;
+    st.vel[gi] = vx;
+    st.vel[M + gi] = vy;
+    st.vel[2 * M + gi] = 0.0f;
+    st.omega[gi] = om;
+    sc.disp[gi] = sqrt_rn(dmax2);
+  }
+}
+
+// ---------------------------------------------------------------- check
+__global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, DevState st,
+                                                Scratch sc, int n_steps,
+                                                uint64_t* __restrict__ step_ctr,
+                                                uint32_t* __restrict__ arrive, int lx, int ly) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  constexpr int kMaxMovers = 1024;
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);  // 16
+  int32_t* misc = wave_sums + 16;                          // 16
+  int32_t* movers = misc + 16;                             // kMaxMovers
+  int32_t* cnt = movers + kMaxMovers;                      // global-path cell counts
+  const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const uint64_t step0 = *step_ctr;
+  if (tid < 16) misc[tid] = 0;
+  __syncthreads();
+  const bool flagged_build = sc.fallback[e] != 0;
+  if (!flagged_build) {
+    const float half = 0.5f * d->skin;
+    for (int i = tid; i < N; i += T) {
+      if (!(sc.disp[base + i] < half)) {
+        const int k = atomicAdd(&misc[0], 1);
+        if (k < kMaxMovers) movers[k] = i;
+      }
+    }
+    __syncthreads();
+    const int nm = misc[0];
+    if (nm > kMaxMovers) {
+      if (tid == 0) misc[1] = 1;
+    } else if (nm > 0) {
+      // exact test of every (mover, other-cluster particle) pair at the
+      // window-start positions: d0 < rc + D_i + D_j could have interacted
+      const float rc = d->rc_max_f;
+      const float sx0 = d->sx[0], sx1 = d->sx[1];
+      const long total = (long)nm * N;
+      for (long t = tid; t < total; t += T) {
+        const int m = movers[t / N];
+        const int j = (int)(t % N);
+        if (sc.root[base + j] == sc.root[base + m]) continue;
+        const float rx = (float)(int32_t)(sc.bq[base + j] - sc.bq[base + m]) * sx0;
+        const float ry = (float)(int32_t)(sc.bq[M + base + j] - sc.bq[M + base + m]) * sx1;
+        const float lim = rc + sc.disp[base + m] + sc.disp[base + j] + 1e-3f;
+        if (rx * rx + ry * ry < lim * lim) misc[1] = 1;
+      }
+    }
+    __syncthreads();
+  }
+  const bool rerun = flagged_build || misc[1] != 0;
+  if (rerun) {
+    for (int i = tid; i < N; i += T) {
+      const size_t gi = base + i;
+      st.q[gi] = sc.bq[gi];
+      st.q[M + gi] = sc.bq[M + gi];
+      st.img[gi] = sc.bimg[gi];
+      st.img[M + gi] = sc.bimg[M + gi];
+      st.ang[gi] = sc.bang[gi];
+    }
+    if (tid == 0) sc.fallback[e] = 2;  // diagnostics: env re-run on the global path
+    __syncthreads();
+    block_global_run(d, st, sc, e, n_steps, step0, lx, ly, false, 0.0f, 0.0f, cnt, wave_sums);
+  }
+  advance_counter(step_ctr, arrive, step0, n_steps);
+}
+
+}  // namespace swarm

@@ -233,3 +233,51 @@ def _disc(rng, n, L):
     a = 2 * np.pi * rng.random(n)
     dirs = np.stack([np.cos(a), np.sin(a), np.zeros(n)], 1)
     return pos, dirs
+
+
+@pytest.mark.parametrize("force", [40.0, 400.0])
+def test_fast_swimmers_cross_skin_bit_exact(force):
+    """Swimmers faster than skin / window exercise the decomposition check and
+    the global-path re-run; results must stay bit-exact."""
+    from gpu_harness import Harness, random_state, species_list
+
+    rng = np.random.default_rng(9)
+    box = [150.0, 150.0, 150.0]
+    n = 1500
+    E = 2
+    sp = np.zeros(n, int)
+    h = Harness(box, 1e-3, 1.0239, 1.0239, 11, species_list()[:1], sp, n_envs=E)
+    states = [random_state(rng, n, box) for _ in range(E)]
+    states = [oracle.sd_run(h.op, s, sp, 300)[0] for s in states]
+    h.upload(states)
+    f = np.full(E * n, force, np.float32)
+    t = rng.normal(size=E * n).astype(np.float32) * 5
+    h.set_actions(f, t)
+    for _ in range(2):
+        h.integrate(100)
+    got = h.download()
+    for e in range(E):
+        ref = states[e]
+        for k in range(2):
+            ref, _, _ = oracle.bd_run(h.op, ref, sp, f[e * n:(e + 1) * n], t[e * n:(e + 1) * n],
+                                      100, step0=100 * k, env=e)
+        _eq(got[e], ref)
+
+
+def test_long_run_is_windowed_bit_exact():
+    """integrate(n) longer than one window (128 sub-steps) splits into windows."""
+    from gpu_harness import Harness, random_state, species_list
+
+    rng = np.random.default_rng(10)
+    box = [100.0, 100.0, 100.0]
+    n = 800
+    sp = np.zeros(n, int)
+    h = Harness(box, 1e-3, 1.0239, 1.0239, 12, species_list()[:1], sp)
+    st = oracle.sd_run(h.op, random_state(rng, n, box), sp, 300)[0]
+    h.upload([st])
+    f = np.full(n, 10.0, np.float32)
+    t = np.zeros(n, np.float32)
+    h.set_actions(f, t)
+    h.integrate(300)
+    ref, _, _ = oracle.bd_run(h.op, st, sp, f, t, 300)
+    _eq(h.download()[0], ref)
