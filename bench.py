@@ -54,7 +54,6 @@ def build_workload(args, env_seed, device):
     from swarmrl_amd.force_functions import ForceFunction
     from swarmrl_amd.networks import ActorCriticMLP, TorchModel
     from swarmrl_amd.observables import SubdividedVisionCones
-    from swarmrl_amd.rollout import EpisodeRecorder
     from swarmrl_amd.tasks.searching import GradientSensing
     from swarmrl_amd.units import UnitRegistry
 
@@ -85,8 +84,7 @@ def build_workload(args, env_seed, device):
         "RotateCounterClockwise": Action(torque=np.array([0.0, 0.0, -10.0])),
         "DoNothing": Action(),
     }
-    agent = ActorCriticAgent(0, net, task, observable, actions, train=False)
-    agent.recorder = EpisodeRecorder(args.episode_length, E, N, (3, 1), device)
+    agent = ActorCriticAgent(0, net, task, observable, actions, train=True)
     ff = ForceFunction({"0": agent})
     agent.reset_agent(eng.colloids)
     return eng, ff, agent
@@ -179,7 +177,7 @@ def main():
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
 
-    from swarmrl_amd.rollout import gather_episode
+    from swarmrl_amd.rollout import gather_trajectory
 
     E = args.envs_per_gpu
     eng, ff, agent = build_workload(args, 42 + rank * E, device)
@@ -188,36 +186,55 @@ def main():
     def one_slice():
         eng.integrate(1, ff)
 
-    graph = None
+    T = args.episode_length
+    slice_graph = episode_graph = None
     if not args.no_graph:
+        # One graph per slice (for step counts that are not a multiple of T)
+        # and one per episode: the episode graph's T slices write T distinct
+        # trajectory tensors, so replaying it records a whole episode with no
+        # copies (agent.trajectory holds references to those tensors).
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(2):
                 one_slice()
         torch.cuda.current_stream().wait_stream(side)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        slice_graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(slice_graph):
             one_slice()
+        agent.reset_trajectory()
+        episode_graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(episode_graph, pool=slice_graph.pool()):
+            for _ in range(T):
+                one_slice()
+    else:
+        agent.reset_trajectory()
 
-    def step():
-        if graph is not None:
-            graph.replay()
-        else:
-            one_slice()
+    def run(n_steps, timed):
+        k = 0
+        while k < n_steps:
+            if episode_graph is not None and n_steps - k >= T:
+                episode_graph.replay()
+                k += T
+                if timed and world > 1:
+                    gather_trajectory(agent.trajectory)
+            elif slice_graph is not None:
+                slice_graph.replay()
+                k += 1
+            else:
+                one_slice()
+                k += 1
+                if timed and world > 1 and len(agent.trajectory.actions) >= T:
+                    gather_trajectory(agent.trajectory)
+                    agent.reset_trajectory()
 
-    T = args.episode_length
-    for _ in range(args.warmup):
-        step()
+    run(args.warmup, False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step()
-        if world > 1 and (k + 1) % T == 0:
-            gather_episode(agent.recorder)
+    run(args.steps, True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -254,7 +271,7 @@ def main():
             "policy": "MLP 3-128-(4+1), Gumbel sampling",
             "task": "GradientSensing (find centre)",
             "parallelism": f"episode-parallel, {world} process(es), RCCL all-gather per episode",
-            "hip_graph": graph is not None,
+            "hip_graph": episode_graph is not None,
         },
         "roofline": {
             "bound": "hbm",

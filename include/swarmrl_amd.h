@@ -128,8 +128,10 @@ int swarm_engine_download_state(swarm_engine_t *e, double *pos_unwrapped,
 
 /* Per-particle swim force and z-torque [E*N]; replaces
  * coll.swimming = {"f_swim": ...} and coll.ext_torque = ...
- * (espresso.py:1228-1235).  on_device != 0: the pointers are device
- * pointers read asynchronously on the engine stream. */
+ * (espresso.py:1228-1235).  on_device = 0: host arrays (copied);
+ * 1: device arrays copied on the engine stream; 2: device arrays BOUND
+ * (zero copy): later launches read them directly, so the caller keeps them
+ * alive and unchanged until the next set_actions call. */
 int swarm_engine_set_actions(swarm_engine_t *e, const float *f_swim,
                              const float *torque_z, int32_t on_device);
 
@@ -180,6 +182,16 @@ int swarm_field_distance(swarm_engine_t *e, const int32_t *agent_idx,
                          const double box_scale[3], uint32_t *hist_q,
                          int32_t *hist_img, float *d_cur, float *d_prev,
                          int32_t update_history, int32_t init_only);
+
+/* Fused field observable / reward for an affine decay f(d) = a + b d:
+ * out[e][a] = scale * (f(d_cur) - f(d_prev)) (concentration_field.py:
+ * 102-104), clipped at 0 when clip_at_zero (gradient_sensing.py:117-118);
+ * the history is updated.  Distances as in swarm_field_distance. */
+int swarm_field_transform(swarm_engine_t *e, const int32_t *agent_idx,
+                          int32_t n_agents, const double source[3],
+                          const double box_scale[3], uint32_t *hist_q,
+                          int32_t *hist_img, float decay_a, float decay_b,
+                          float scale, int32_t clip_at_zero, float *out);
 
 /* Parity helper: all pairs (i<j) of env `env` closer than `cutoff`
  * (minimum image if periodic) as int32 [max_pairs][2] (host), count in

@@ -107,6 +107,11 @@ _SIGNATURES = {
         ctypes.c_int,
         [_P, _P, ctypes.c_int32, _P, _P, _P, _P, _P, _P, ctypes.c_int32, ctypes.c_int32],
     ),
+    "swarm_field_transform": (
+        ctypes.c_int,
+        [_P, _P, ctypes.c_int32, _P, _P, _P, _P, ctypes.c_float, ctypes.c_float,
+         ctypes.c_float, ctypes.c_int32, _P],
+    ),
     "swarm_engine_neighbor_pairs": (
         ctypes.c_int,
         [_P, ctypes.c_int32, ctypes.c_double, _P, ctypes.c_int32, _P],

@@ -162,6 +162,8 @@ __global__ __launch_bounds__(1024) void k_grid_build(DevState st, int lx, int ly
 }
 
 // ---------------------------------------------------------- vision cone
+// NB = bins held in registers (>= n_cones * n_types), statically indexed.
+template <int NB>
 __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __restrict__ d,
                                                 swarm_vision_params_t vp, int lx, int ly,
                                                 const int32_t* __restrict__ start,
@@ -184,8 +186,9 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
   const float nm = swarm::sqrt_rn(cs * cs + sn * sn);
   const float mx = cs / nm, my = sn / nm;
   const int nb = vp.n_cones * vp.n_types;
-  int64_t acc[SWARM_MAX_CONES * 2];  // host guarantees nb <= 32
-  for (int k = 0; k < SWARM_MAX_CONES * 2; ++k) acc[k] = 0;
+  int64_t acc[NB];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) acc[k] = 0;
   const int ncell = 1 << (lx + ly);
   const int ncx = 1 << lx, ncy = 1 << ly;
   const int lox = ncx >= 3 ? -1 : 0, hix = ncx >= 3 ? 1 : ncx - 1;
@@ -232,12 +235,17 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
         const float orth = ux * (-my) + uy * mx;
         if (orth < 0.0f) an = -an;
         const int64_t fixed = __float2ll_rn(amp * 4294967296.0f);
+        int bin = -1;
         for (int k = 0; k < vp.n_cones; ++k)
-          if (vp.rims[k] < an && an < vp.rims[k + 1]) acc[k * vp.n_types + ti] += fixed;
+          if (vp.rims[k] < an && an < vp.rims[k + 1]) bin = k * vp.n_types + ti;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[b] += (b == bin) ? fixed : 0;
       }
     }
   }
-  for (int k = 0; k < nb; ++k) o[k] = (float)acc[k] * 2.3283064365386963e-10f;
+#pragma unroll
+  for (int k = 0; k < NB; ++k)
+    if (k < nb) o[k] = (float)acc[k] * 2.3283064365386963e-10f;
 }
 
 // ------------------------------------------------------- field distance
@@ -247,7 +255,9 @@ __global__ __launch_bounds__(256) void k_field(DevState st, const double* __rest
                                                double b0, double b1, double b2,
                                                uint32_t* __restrict__ hq, int32_t* __restrict__ himg,
                                                float* __restrict__ d_cur, float* __restrict__ d_prev,
-                                               int update, int init_only, int n_envs) {
+                                               int update, int init_only, int n_envs,
+                                               int mode, float fa, float fb, float fscale,
+                                               float* __restrict__ out) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int A = n_agents * n_envs;
   if (t >= A) return;
@@ -272,8 +282,21 @@ __global__ __launch_bounds__(256) void k_field(DevState st, const double* __rest
       cur[a] = (float)(src[a] - pc);
       prev[a] = (float)(src[a] - hp);
     }
-    d_cur[t] = swarm::sqrt_rn(cur[0] * cur[0] + cur[1] * cur[1] + cur[2] * cur[2]);
-    d_prev[t] = swarm::sqrt_rn(prev[0] * prev[0] + prev[1] * prev[1] + prev[2] * prev[2]);
+    const float dc = swarm::sqrt_rn(cur[0] * cur[0] + cur[1] * cur[1] + cur[2] * cur[2]);
+    const float dp = swarm::sqrt_rn(prev[0] * prev[0] + prev[1] * prev[1] + prev[2] * prev[2]);
+    if (mode == 0) {
+      d_cur[t] = dc;
+      d_prev[t] = dp;
+    } else {
+      // affine decay f(d) = fa + fb * d; value = scale * (f(d_cur) - f(d_prev))
+      // (concentration_field.py:102-104); mode 2 clips at 0
+      // (gradient_sensing.py:117-118; NaN propagates as in torch.clamp)
+      const float fc = fa + fb * dc;
+      const float fp = fa + fb * dp;
+      float v = fscale * (fc - fp);
+      if (mode == 2) v = v < 0.0f ? 0.0f : v;
+      out[t] = v;
+    }
   }
   if (update || init_only) {
     for (int a = 0; a < 3; ++a) {
@@ -352,6 +375,8 @@ struct swarm_engine {
   int lxg = 0, lyg = 0;  // global-path grid: cell side >= rc_max
   int lxb = 0, lyb = 0;  // cluster-build grid: cell side >= rc_max + skin
   bool cluster_path = false;
+  float* own_f_swim = nullptr;
+  float* own_torque_z = nullptr;
   void* allocs[48] = {};
   int n_allocs = 0;
 };
@@ -565,6 +590,8 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->st.f_ext, 3 * M);
   rc = rc ? rc : dev_alloc(e, &e->st.vel, 3 * M);
   rc = rc ? rc : dev_alloc(e, &e->st.omega, M);
+  e->own_f_swim = e->st.f_swim;
+  e->own_torque_z = e->st.torque_z;
   rc = rc ? rc : dev_alloc(e, &e->st.species, (size_t)n_particles);
   rc = rc ? rc : dev_alloc(e, &e->d_derived, 1);
   rc = rc ? rc : dev_alloc(e, &e->d_box, 3);
@@ -694,6 +721,15 @@ int swarm_engine_set_actions(swarm_engine_t* e, const float* f_swim, const float
                              int32_t on_device) {
   if (!e || !f_swim || !torque_z) return fail(SWARM_EINVAL, "null argument");
   const size_t M = (size_t)e->st.m;
+  if (on_device == 2) {
+    // bind: later launches read the caller's buffers directly (zero copy);
+    // the caller keeps them alive and unchanged until the next set_actions
+    e->st.f_swim = const_cast<float*>(f_swim);
+    e->st.torque_z = const_cast<float*>(torque_z);
+    return SWARM_OK;
+  }
+  e->st.f_swim = e->own_f_swim;
+  e->st.torque_z = e->own_torque_z;
   const hipMemcpyKind kind = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
   HIP_TRY(hipMemcpyAsync(e->st.f_swim, f_swim, M * sizeof(float), kind, e->stream));
   HIP_TRY(hipMemcpyAsync(e->st.torque_z, torque_z, M * sizeof(float), kind, e->stream));
@@ -777,9 +813,20 @@ int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const 
   int rc = build_grid(e, lx, ly);
   if (rc) return rc;
   const int total = n_agents * e->n_envs;
-  hipLaunchKernelGGL(k_vision, dim3((total + 255) / 256), dim3(256), 0, e->stream, e->st,
-                     e->d_derived, *vp, lx, ly, e->d_start, e->d_order, agent_idx, n_agents, radii,
-                     types, out, e->n_envs);
+  const int nb = vp->n_cones * vp->n_types;
+  const dim3 grid((total + 255) / 256), block(256);
+#define SWARM_VISION(NBV)                                                                   \
+  hipLaunchKernelGGL(k_vision<NBV>, grid, block, 0, e->stream, e->st, e->d_derived, *vp, lx, ly, \
+                     e->d_start, e->d_order, agent_idx, n_agents, radii, types, out, e->n_envs)
+  if (nb <= 4)
+    SWARM_VISION(4);
+  else if (nb <= 8)
+    SWARM_VISION(8);
+  else if (nb <= 16)
+    SWARM_VISION(16);
+  else
+    SWARM_VISION(32);
+#undef SWARM_VISION
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
 }
@@ -797,7 +844,24 @@ int swarm_field_distance(swarm_engine_t* e, const int32_t* agent_idx, int32_t n_
                        box_scale ? box_scale[2] : 1.0};
   hipLaunchKernelGGL(k_field, dim3((total + 255) / 256), dim3(256), 0, e->stream, e->st, e->d_box,
                      agent_idx, n_agents, s[0], s[1], s[2], b[0], b[1], b[2], hist_q, hist_img,
-                     d_cur, d_prev, update_history, init_only, e->n_envs);
+                     d_cur, d_prev, update_history, init_only, e->n_envs, 0, 0.0f, 0.0f, 0.0f,
+                     nullptr);
+  HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+
+int swarm_field_transform(swarm_engine_t* e, const int32_t* agent_idx, int32_t n_agents,
+                          const double source[3], const double box_scale[3], uint32_t* hist_q,
+                          int32_t* hist_img, float decay_a, float decay_b, float scale,
+                          int32_t clip_at_zero, float* out) {
+  if (!e || !agent_idx || !hist_q || !hist_img || !source || !box_scale || !out)
+    return fail(SWARM_EINVAL, "null argument");
+  if (n_agents <= 0) return SWARM_OK;
+  const int total = n_agents * e->n_envs;
+  hipLaunchKernelGGL(k_field, dim3((total + 255) / 256), dim3(256), 0, e->stream, e->st, e->d_box,
+                     agent_idx, n_agents, source[0], source[1], source[2], box_scale[0],
+                     box_scale[1], box_scale[2], hist_q, hist_img, nullptr, nullptr, 1, 0,
+                     e->n_envs, clip_at_zero ? 2 : 1, decay_a, decay_b, scale, out);
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
 }

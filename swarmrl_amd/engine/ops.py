@@ -242,3 +242,43 @@ def history_tensors(hq: np.ndarray, hi: np.ndarray, device):
         torch.as_tensor(np.ascontiguousarray(hq).view(np.int32), device=device).clone(),
         torch.as_tensor(np.ascontiguousarray(hi), device=device).clone(),
     )
+
+
+# ------------------------------------------------ fused affine field tasks
+def affine_coefficients(decay_fn):
+    """
+    (a, b) if decay_fn(d) == a + b * d exactly in fp32 on probe values (the
+    reference's decay functions, e.g. ``1 - d`` or ``-1 * d``), else None.
+    Affine decays run fused inside the HIP field kernel.
+    """
+    try:
+        probe = torch.tensor([0.0, 1.0, 2.0, 0.3712, 123.5, 7.25e-3], dtype=torch.float32)
+        y = decay_fn(probe)
+        if not isinstance(y, torch.Tensor) or y.shape != probe.shape or y.dtype != torch.float32:
+            return None
+        a = y[0]
+        b = y[1] - y[0]
+        if not torch.equal(a + b * probe, y):
+            return None
+        return float(a), float(b)
+    except Exception:
+        return None
+
+
+def field_transform(native, n_envs: int, agent_idx: torch.Tensor, source, box_scale,
+                    hist_q: torch.Tensor, hist_img: torch.Tensor, a: float, b: float,
+                    scale: float, clip: bool) -> torch.Tensor:
+    """scale * (f(d_cur) - f(d_prev)) [E, A] for affine f (k_field, fused)."""
+    A = int(agent_idx.numel())
+    out = torch.empty((n_envs, A), dtype=torch.float32, device=agent_idx.device)
+    if A == 0:
+        return out
+    src = (ctypes.c_double * 3)(*[float(v) for v in np.asarray(source, dtype=float)[:3]])
+    bs = (ctypes.c_double * 3)(*[float(v) for v in np.asarray(box_scale, dtype=float)[:3]])
+    native.bind_stream()
+    native.call(
+        "swarm_field_transform", agent_idx.data_ptr(), A, ctypes.cast(src, ctypes.c_void_p),
+        ctypes.cast(bs, ctypes.c_void_p), hist_q.data_ptr(), hist_img.data_ptr(), float(a),
+        float(b), float(scale), 1 if clip else 0, out.data_ptr(),
+    )
+    return out

@@ -647,11 +647,13 @@ class SwarmEngine(Engine):
     def apply_device_actions(self, actions: DeviceActions):
         """Write per-particle actions from device tensors [E, N]."""
         E, N = self.n_envs, self.n_particles
-        f = actions.f_swim.to(torch.float32).reshape(E * N).contiguous()
-        t = actions.torque_z.to(torch.float32).reshape(E * N).contiguous()
+        f = actions.f_swim.to(torch.float32).expand(E, N).reshape(E * N).contiguous()
+        t = actions.torque_z.to(torch.float32).expand(E, N).reshape(E * N).contiguous()
+        # bind (zero copy): the engine reads these buffers until the next
+        # set_actions; keep them alive until then
         self._actions_keepalive = (f, t)
         self._native.bind_stream()
-        self._native.call("swarm_engine_set_actions", f.data_ptr(), t.data_ptr(), 1)
+        self._native.call("swarm_engine_set_actions", f.data_ptr(), t.data_ptr(), 2)
         if actions.new_direction is not None:
             nd = np.broadcast_to(np.asarray(actions.new_direction, dtype=float), (E, N, 3))
             mask = actions.new_direction_mask

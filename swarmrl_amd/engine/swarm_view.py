@@ -99,6 +99,10 @@ class SwarmView:
             self._type_index[int(p_type)] = idx
         return idx
 
+    def covers_all(self, p_type: int) -> bool:
+        """True when every particle has this type (indices == arange(N))."""
+        return bool(np.all(self.engine._types_host == int(p_type)))
+
     def positions(self) -> torch.Tensor:
         """Unwrapped positions, float64 [E, N, 3]."""
         box = self.engine._box

@@ -63,6 +63,14 @@ class ForceFunction:
 
     def _calc_action_device(self, view) -> DeviceActions:
         E, N = view.n_envs, view.n_particles
+        if len(self.agents) == 1:
+            agent_type, agent = next(iter(self.agents.items()))
+            if view.covers_all(int(agent_type)):
+                # one agent acts on every colloid: its [E, N] actions are the
+                # merged actions (no scatter needed)
+                acts = agent.calc_action(colloids=view)
+                self.kill_switch = bool(agent.kill_switch)
+                return acts
         f = torch.zeros((E, N), dtype=torch.float32, device=view.device)
         tz = torch.zeros((E, N), dtype=torch.float32, device=view.device)
         new_dir = None

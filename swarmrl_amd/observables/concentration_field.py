@@ -44,6 +44,7 @@ class ConcentrationField(Observable):
         self._observable_shape = (3,)
         self._dev_hist = None  # (engine id, hist_q, hist_img)
         self._pending = None
+        self._affine = None
 
     # ------------------------------------------------------------ init
     def initialize(self, colloids):
@@ -108,6 +109,13 @@ class ConcentrationField(Observable):
                 raise ValueError(f"{type(self).__name__} was initialised for another engine")
             agents = view.indices_of_type(self.particle_type)
             _, hq, hi = self._dev_hist
+            if self._affine is None:
+                self._affine = ops.affine_coefficients(self.decay_fn) or False
+            if self._affine:
+                return ops.field_transform(
+                    view.engine._native, view.n_envs, agents, self._source_raw, self.box_length,
+                    hq, hi, self._affine[0], self._affine[1], float(self.scale_factor), False,
+                ).unsqueeze(-1)
             d_cur, d_prev = ops.field_distance(
                 view.engine._native, view.n_envs, agents, self._source_raw, self.box_length,
                 hq, hi, update=True,

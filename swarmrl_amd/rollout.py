@@ -81,3 +81,27 @@ def gather_episode(recorder: EpisodeRecorder, group=None) -> Dict[str, torch.Ten
 def shard_envs(total_envs: int, rank: int, world: int):
     """Env ids owned by a rank: e with e mod world == rank."""
     return [e for e in range(total_envs) if e % world == rank]
+
+
+def gather_trajectory(trajectory, group=None) -> Dict[str, torch.Tensor]:
+    """
+    Stack an agent's device trajectory (lists of [E, A, ...] tensors, one entry
+    per slice) into [T, E, ...] tensors and all-gather them along the env axis
+    -> [T, world * E, ...] on every rank.
+    """
+    bufs = {
+        "features": torch.stack(list(trajectory.features)),
+        "actions": torch.stack(list(trajectory.actions)),
+        "log_probs": torch.stack(list(trajectory.log_probs)),
+        "rewards": torch.stack(list(trajectory.rewards)),
+    }
+    if not (dist.is_available() and dist.is_initialized()):
+        return bufs
+    world = dist.get_world_size(group)
+    out = {}
+    for name, t in bufs.items():
+        t = t.contiguous()
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t, group=group)
+        out[name] = torch.cat(parts, dim=1)
+    return out

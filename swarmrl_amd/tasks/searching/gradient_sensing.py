@@ -37,6 +37,7 @@ class GradientSensing(Task):
         self._historic_positions = {}
         self._dev_hist = None
         self._pending = None
+        self._affine = None
 
     def initialize(self, colloids):
         """Store the starting positions of particle_type colloids (lines 60-79)."""
@@ -95,6 +96,14 @@ class GradientSensing(Task):
                 raise ValueError("GradientSensing was not initialised for this engine")
             agents = view.indices_of_type(self.particle_type)
             _, hq, hi = self._dev_hist
+            if self._affine is None:
+                self._affine = ops.affine_coefficients(self.decay_fn) or False
+            if self._affine:
+                return ops.field_transform(
+                    view.engine._native, view.n_envs, agents, self._source_raw, self.box_length,
+                    hq, hi, self._affine[0], self._affine[1], float(self.reward_scale_factor),
+                    True,
+                )
             d_cur, d_prev = ops.field_distance(
                 view.engine._native, view.n_envs, agents, self._source_raw, self.box_length,
                 hq, hi, update=True,
