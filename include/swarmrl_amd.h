@@ -153,6 +153,13 @@ int swarm_engine_remove_overlap(swarm_engine_t *e, int32_t n_steps,
  * (espresso.py:1304-1306).  Asynchronous on the engine stream. */
 int swarm_engine_integrate(swarm_engine_t *e, int32_t n_steps);
 
+/* Diagnostics of the last integration window, per env (host arrays [E],
+ * either may be NULL): fallback 0 = cluster path, 1 = flagged by the build
+ * (cluster > 64 lanes or neighbour overflow), 2 = re-run on the global path;
+ * waves = 64-lane waves the env's clusters were packed into. */
+int swarm_engine_window_stats(swarm_engine_t *e, int32_t *fallback,
+                              int32_t *waves);
+
 /* Total number of BD sub-steps integrated so far (the noise counter). */
 int64_t swarm_engine_step_count(const swarm_engine_t *e);
 

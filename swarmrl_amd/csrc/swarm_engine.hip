@@ -38,6 +38,16 @@ using swarm::Scratch;
 using swarm::cell_index;
 using swarm::block_exclusive_scan;
 
+struct VisionSorted {
+  uint32_t* qx;
+  uint32_t* qy;
+  int32_t* ix;
+  int32_t* iy;
+  int32_t* tslot;
+  float* rad;
+  int32_t* idx;
+};
+
 constexpr int kMaxSpecies = SWARM_MAX_SPECIES;
 constexpr double kTwo32 = 4294967296.0;
 constexpr double kTwoPi = 6.283185307179586476925;
@@ -161,24 +171,63 @@ __global__ __launch_bounds__(1024) void k_grid_build(DevState st, int lx, int ly
   }
 }
 
+// Vision grid: counting sort of every env into cells of side >= vision range,
+// writing cell-sorted SoA copies (position, image, detected-type slot, radius,
+// particle index) so a candidate cell is one contiguous run.
+__global__ __launch_bounds__(1024) void k_vision_grid(DevState st, swarm_vision_params_t vp,
+                                                      int lx, int ly,
+                                                      const float* __restrict__ radii,
+                                                      const int32_t* __restrict__ types,
+                                                      int32_t* __restrict__ start, VisionSorted vs) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const int ncell = 1 << (lx + ly);
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
+  int32_t* cnt = wave_sums + 16;
+  for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
+  __syncthreads();
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  for (int i = tid; i < N; i += T)
+    atomicAdd(&cnt[cell_index(st.q[base + i], st.q[M + base + i], lx, ly)], 1);
+  __syncthreads();
+  block_exclusive_scan(cnt, ncell, wave_sums);
+  __syncthreads();
+  int32_t* so = start + (size_t)e * (ncell + 1);
+  for (int c = tid; c <= ncell; c += T) so[c] = cnt[c];
+  __syncthreads();
+  for (int i = tid; i < N; i += T) {
+    const size_t g = base + i;
+    const uint32_t qx = st.q[g], qy = st.q[M + g];
+    const size_t pos = base + atomicAdd(&cnt[cell_index(qx, qy, lx, ly)], 1);
+    const int tj = types[i];
+    int ti = -1;
+    for (int tt = 0; tt < vp.n_types; ++tt)
+      if (vp.detected_types[tt] == tj) ti = tt;
+    vs.qx[pos] = qx;
+    vs.qy[pos] = qy;
+    vs.ix[pos] = st.img[g];
+    vs.iy[pos] = st.img[M + g];
+    vs.tslot[pos] = ti;
+    vs.rad[pos] = radii[i];
+    vs.idx[pos] = i;
+  }
+}
+
 // ---------------------------------------------------------- vision cone
 // NB = bins held in registers (>= n_cones * n_types), statically indexed.
 template <int NB>
 __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __restrict__ d,
                                                 swarm_vision_params_t vp, int lx, int ly,
-                                                const int32_t* __restrict__ start,
-                                                const int32_t* __restrict__ order,
+                                                const int32_t* __restrict__ start, VisionSorted vs,
                                                 const int32_t* __restrict__ agents, int n_agents,
-                                                const float* __restrict__ radii,
-                                                const int32_t* __restrict__ types,
                                                 float* __restrict__ out, int n_envs) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_envs * n_agents) return;
   const int e = t / n_agents, ai = t - e * n_agents;
   const int N = st.n;
-  const size_t M = (size_t)st.m;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int i = agents[ai];
-  const size_t gi = (size_t)e * N + i;
+  const size_t gi = base + i;
   const uint32_t qxi = st.q[gi], qyi = st.q[M + gi];
   const int32_t ixi = st.img[gi], iyi = st.img[M + gi];
   float sn, cs;
@@ -196,27 +245,24 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
   const int cc0 = cell_index(qxi, qyi, lx, ly);
   const int cx = cc0 & (ncx - 1), cy = cc0 >> lx;
   const int32_t* so = start + (size_t)e * (ncell + 1);
-  const int32_t* oo = order + (size_t)e * N;
   const float sx0 = d->sx[0], sx1 = d->sx[1];
-  float* o = out + (size_t)t * nb;
+  const float R = vp.vision_range;
+  // conservative pre-test on dist^2 (the exact test below is on fp32 sqrt)
+  const float R2pad = R * R * 1.0001f;
   for (int oy = loy; oy <= hiy; ++oy) {
     const int y = (cy + oy + ncy) & (ncy - 1);
     for (int ox = lox; ox <= hix; ++ox) {
       const int x = (cx + ox + ncx) & (ncx - 1);
       const int cc = (y << lx) | x;
-      for (int jj = so[cc]; jj < so[cc + 1]; ++jj) {
-        const int j = oo[jj];
-        if (j == i) continue;
-        const int tj = types[j];
-        int ti = -1;
-        for (int tt = 0; tt < vp.n_types; ++tt)
-          if (vp.detected_types[tt] == tj) ti = tt;
+      const int jb = so[cc], je = so[cc + 1];
+      for (int jj = jb; jj < je; ++jj) {
+        const size_t p = base + jj;
+        const int ti = vs.tslot[p];
         if (ti < 0) continue;
-        const size_t gj = (size_t)e * N + j;
-        const int64_t dqx = ((int64_t)(st.img[gj] - ixi) * (int64_t)4294967296LL) +
-                            ((int64_t)st.q[gj] - (int64_t)qxi);
-        const int64_t dqy = ((int64_t)(st.img[M + gj] - iyi) * (int64_t)4294967296LL) +
-                            ((int64_t)st.q[M + gj] - (int64_t)qyi);
+        const int64_t dqx = ((int64_t)(vs.ix[p] - ixi) * (int64_t)4294967296LL) +
+                            ((int64_t)vs.qx[p] - (int64_t)qxi);
+        const int64_t dqy = ((int64_t)(vs.iy[p] - iyi) * (int64_t)4294967296LL) +
+                            ((int64_t)vs.qy[p] - (int64_t)qyi);
         // unwrapped separations beyond half a box are never within range
         // (vision_range < L/2): skip them and convert the rest from int32,
         // whose conversion is a single exact-rounding instruction.
@@ -224,9 +270,12 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
             dqy > 2147483647LL)
           continue;
         const float dx = (float)(int32_t)dqx * sx0, dy = (float)(int32_t)dqy * sx1;
-        const float dist = swarm::sqrt_rn(dx * dx + dy * dy);
-        if (!(dist < vp.vision_range) || dist == 0.0f) continue;
-        float amp = (2.0f * radii[j]) / dist;
+        const float dist2 = dx * dx + dy * dy;
+        if (!(dist2 < R2pad) || dist2 == 0.0f) continue;
+        if (vs.idx[p] == i) continue;
+        const float dist = swarm::sqrt_rn(dist2);
+        if (!(dist < R)) continue;
+        float amp = (2.0f * vs.rad[p]) / dist;
         amp = fminf(1.0f, amp);
         const float ux = dx / dist, uy = dy / dist;
         float dot = ux * mx + uy * my;
@@ -243,6 +292,7 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
       }
     }
   }
+  float* o = out + (size_t)t * nb;
 #pragma unroll
   for (int k = 0; k < NB; ++k)
     if (k < nb) o[k] = (float)acc[k] * 2.3283064365386963e-10f;
@@ -375,6 +425,7 @@ struct swarm_engine {
   int lxg = 0, lyg = 0;  // global-path grid: cell side >= rc_max
   int lxb = 0, lyb = 0;  // cluster-build grid: cell side >= rc_max + skin
   bool cluster_path = false;
+  VisionSorted vs{};
   float* own_f_swim = nullptr;
   float* own_torque_z = nullptr;
   void* allocs[48] = {};
@@ -415,7 +466,8 @@ void set_lds_attributes() {
   const void* fns[] = {reinterpret_cast<const void*>(&swarm::k_global),
                        reinterpret_cast<const void*>(&swarm::k_cluster_build),
                        reinterpret_cast<const void*>(&swarm::k_check),
-                       reinterpret_cast<const void*>(&k_grid_build)};
+                       reinterpret_cast<const void*>(&k_grid_build),
+                       reinterpret_cast<const void*>(&k_vision_grid)};
   for (const void* f : fns)
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
   (void)hipGetLastError();
@@ -618,6 +670,13 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->sc.disp, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.env_waves, (size_t)n_envs);
   rc = rc ? rc : dev_alloc(e, &e->sc.fallback, (size_t)n_envs);
+  e->vs.qx = e->sc.sqx;  // the observables run between integration windows
+  e->vs.qy = e->sc.sqy;
+  e->vs.idx = e->sc.sidx;
+  rc = rc ? rc : dev_alloc(e, &e->vs.ix, M);
+  rc = rc ? rc : dev_alloc(e, &e->vs.iy, M);
+  rc = rc ? rc : dev_alloc(e, &e->vs.tslot, M);
+  rc = rc ? rc : dev_alloc(e, &e->vs.rad, M);
   set_lds_attributes();
   if (rc) {
     swarm_engine_destroy(e);
@@ -774,6 +833,19 @@ int swarm_engine_integrate(swarm_engine_t* e, int32_t n_steps) {
   return run_bd(e, n_steps);
 }
 
+int swarm_engine_window_stats(swarm_engine_t* e, int32_t* fallback, int32_t* waves) {
+  if (!e) return fail(SWARM_EINVAL, "null engine");
+  const size_t E = (size_t)e->n_envs;
+  if (fallback)
+    HIP_TRY(hipMemcpyAsync(fallback, e->sc.fallback, E * sizeof(int32_t), hipMemcpyDeviceToHost,
+                           e->stream));
+  if (waves)
+    HIP_TRY(hipMemcpyAsync(waves, e->sc.env_waves, E * sizeof(int32_t), hipMemcpyDeviceToHost,
+                           e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return SWARM_OK;
+}
+
 int64_t swarm_engine_step_count(const swarm_engine_t* e) {
   if (!e) return -1;
   uint64_t v = 0;
@@ -810,14 +882,22 @@ int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const 
     return fail(SWARM_EINVAL, "vision_range must be below half the box length");
   int lx, ly;
   cell_grid(e->params, e->n, (double)vp->vision_range, &lx, &ly);
-  int rc = build_grid(e, lx, ly);
+  int rc = ensure_grid_scratch(e, lx, ly);
   if (rc) return rc;
+  {
+    const int ncell = 1 << (lx + ly);
+    const size_t lds = 16 * 4 + (size_t)(ncell + 1) * 4;
+    if (lds > kMaxLds) return fail(SWARM_ECAPACITY, "observable cell grid too large");
+    hipLaunchKernelGGL(k_vision_grid, dim3(e->n_envs), dim3(1024), lds, e->stream, e->st, *vp,
+                       lx, ly, radii, types, e->d_start, e->vs);
+    HIP_TRY(hipGetLastError());
+  }
   const int total = n_agents * e->n_envs;
   const int nb = vp->n_cones * vp->n_types;
   const dim3 grid((total + 255) / 256), block(256);
 #define SWARM_VISION(NBV)                                                                   \
   hipLaunchKernelGGL(k_vision<NBV>, grid, block, 0, e->stream, e->st, e->d_derived, *vp, lx, ly, \
-                     e->d_start, e->d_order, agent_idx, n_agents, radii, types, out, e->n_envs)
+                     e->d_start, e->vs, agent_idx, n_agents, out, e->n_envs)
   if (nb <= 4)
     SWARM_VISION(4);
   else if (nb <= 8)

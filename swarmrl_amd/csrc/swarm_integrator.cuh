@@ -137,17 +137,18 @@ __device__ inline void block_exclusive_scan(int32_t* data, int n, int32_t* wave_
 }
 
 // WCA force on i from j (r = x_j - x_i), accumulated in 2^-24 fixed point.
-__device__ __forceinline__ void pair_force(const Derived* __restrict__ d, int si, int sj,
-                                           float rx, float ry, int64_t& ax, int64_t& ay) {
+// cut2 = (r_i + r_j)^2, sig6 = sigma^6, eps24 = 24 epsilon (Derived tables).
+__device__ __forceinline__ void pair_force(float cut2, float sig6, float eps24, float rx,
+                                           float ry, int64_t& ax, int64_t& ay) {
   const float r2 = rx * rx + ry * ry;
-  if (r2 < d->cut2[si * kMaxSpecies + sj] && r2 > 0.0f) {
+  if (r2 < cut2 && r2 > 0.0f) {
     const float ir2 = 1.0f / r2;
     float ir6 = ir2 * ir2;
     ir6 = ir6 * ir2;
-    const float s6 = d->sig6[si * kMaxSpecies + sj] * ir6;
+    const float s6 = sig6 * ir6;
     float t = 2.0f * s6;
     t = t - 1.0f;
-    float fr = d->eps24 * s6;
+    float fr = eps24 * s6;
     fr = fr * t;
     fr = fr * ir2;
     ax += f2fix24(-fr * rx);
@@ -160,12 +161,48 @@ struct PState {
   int32_t ix, iy;
 };
 
+// Per-colloid constants, read once per launch (not per sub-step).
+struct PConst {
+  float mob_dt, sig_t, rot_dt, sig_r, inv_gt, inv_gr, sig_v, sig_w;
+  float inv_sx0, inv_sx1;
+  bool noisy;
+};
+
+__device__ __forceinline__ PConst load_pconst(const Derived* __restrict__ d, int si) {
+  PConst c;
+  c.mob_dt = d->mob_dt[si];
+  c.sig_t = d->sig_t[si];
+  c.rot_dt = d->rot_dt[si];
+  c.sig_r = d->sig_r[si];
+  c.inv_gt = d->inv_gt[si];
+  c.inv_gr = d->inv_gr[si];
+  c.sig_v = d->sig_v[si];
+  c.sig_w = d->sig_w[si];
+  c.inv_sx0 = d->inv_sx[0];
+  c.inv_sx1 = d->inv_sx[1];
+  c.noisy = d->noisy != 0;
+  return c;
+}
+
+// Pair tables staged in LDS by the whole block (call before any early exit).
+struct PairTables {
+  float cut2[kMaxSpecies * kMaxSpecies];
+  float sig6[kMaxSpecies * kMaxSpecies];
+};
+
+__device__ __forceinline__ void stage_pair_tables(const Derived* __restrict__ d, PairTables* t) {
+  for (int k = threadIdx.x; k < kMaxSpecies * kMaxSpecies; k += blockDim.x) {
+    t->cut2[k] = d->cut2[k];
+    t->sig6[k] = d->sig6[k];
+  }
+  __syncthreads();
+}
+
 // One Brownian-dynamics sub-step of one particle from its summed WCA force.
-__device__ __forceinline__ void bd_step(const Derived* __restrict__ d, PState& p, int si,
-                                        int64_t ax, int64_t ay, float fs, float tz, float fex,
-                                        float fey, uint32_t k0, uint32_t k1, uint32_t id,
-                                        uint64_t step, bool last, float* vx, float* vy,
-                                        float* w) {
+__device__ __forceinline__ void bd_step(const PConst& c, PState& p, int64_t ax, int64_t ay,
+                                        float fs, float tz, float fex, float fey, uint32_t k0,
+                                        uint32_t k1, uint32_t id, uint64_t step, bool last,
+                                        float* vx, float* vy, float* w) {
   float sn, cs;
   sincos_turn(p.an, &sn, &cs);
   float fx = (float)ax * 5.9604644775390625e-08f;
@@ -174,29 +211,28 @@ __device__ __forceinline__ void bd_step(const Derived* __restrict__ d, PState& p
   fy = fy + fey;
   fx = fx + fs * cs;
   fy = fy + fs * sn;
-  float dx = fx * d->mob_dt[si];
-  float dy = fy * d->mob_dt[si];
-  float dth = tz * d->rot_dt[si];
-  const bool noisy = d->noisy != 0;
-  if (noisy) {
+  float dx = fx * c.mob_dt;
+  float dy = fy * c.mob_dt;
+  float dth = tz * c.rot_dt;
+  if (c.noisy) {
     float g[4];
     normals4(k0, k1, id, step, 0u, g);
-    dx = dx + d->sig_t[si] * g[0];
-    dy = dy + d->sig_t[si] * g[1];
-    dth = dth + d->sig_r[si] * g[2];
+    dx = dx + c.sig_t * g[0];
+    dy = dy + c.sig_t * g[1];
+    dth = dth + c.sig_r * g[2];
   }
-  advance(p.qx, p.ix, f2i32(dx * d->inv_sx[0]));
-  advance(p.qy, p.iy, f2i32(dy * d->inv_sx[1]));
+  advance(p.qx, p.ix, f2i32(dx * c.inv_sx0));
+  advance(p.qy, p.iy, f2i32(dy * c.inv_sx1));
   p.an = p.an + (uint32_t)f2i32(dth * kAngInvScale);
   if (last) {
-    float v0 = fx * d->inv_gt[si], v1 = fy * d->inv_gt[si];
-    float om = tz * d->inv_gr[si];
-    if (noisy) {
+    float v0 = fx * c.inv_gt, v1 = fy * c.inv_gt;
+    float om = tz * c.inv_gr;
+    if (c.noisy) {
       float g[4];
       normals4(k0, k1, id, step, 1u, g);
-      v0 = v0 + d->sig_v[si] * g[0];
-      v1 = v1 + d->sig_v[si] * g[1];
-      om = om + d->sig_w[si] * g[2];
+      v0 = v0 + c.sig_v * g[0];
+      v1 = v1 + c.sig_v * g[1];
+      om = om + c.sig_w * g[2];
     }
     *vx = v0;
     *vy = v1;
@@ -205,9 +241,9 @@ __device__ __forceinline__ void bd_step(const Derived* __restrict__ d, PState& p
 }
 
 // One steepest-descent step of one particle (espresso.py:1163-1168).
-__device__ __forceinline__ bool sd_step(const Derived* __restrict__ d, PState& p, int64_t ax,
-                                        int64_t ay, float fs, float tz, float fex, float fey,
-                                        float g, float md) {
+__device__ __forceinline__ bool sd_step(const PConst& c, PState& p, int64_t ax, int64_t ay,
+                                        float fs, float tz, float fex, float fey, float g,
+                                        float md) {
   float sn, cs;
   sincos_turn(p.an, &sn, &cs);
   float fx = (float)ax * 5.9604644775390625e-08f;
@@ -220,8 +256,8 @@ __device__ __forceinline__ bool sd_step(const Derived* __restrict__ d, PState& p
   const float px = fminf(fmaxf(g * fx, -md), md);
   const float py = fminf(fmaxf(g * fy, -md), md);
   const float pa = fminf(fmaxf(g * tz, -md), md);
-  advance(p.qx, p.ix, f2i32(px * d->inv_sx[0]));
-  advance(p.qy, p.iy, f2i32(py * d->inv_sx[1]));
+  advance(p.qx, p.ix, f2i32(px * c.inv_sx0));
+  advance(p.qy, p.iy, f2i32(py * c.inv_sx1));
   p.an = p.an + (uint32_t)f2i32(pa * kAngInvScale);
   return any;
 }
@@ -234,7 +270,7 @@ __device__ __forceinline__ bool sd_step(const Derived* __restrict__ d, PState& p
 __device__ void block_global_run(const Derived* __restrict__ d, const DevState& st,
                                  const Scratch& sc, int e, int n_steps, uint64_t step0, int lx,
                                  int ly, bool sd_mode, float g, float md, int32_t* cnt,
-                                 int32_t* wave_sums) {
+                                 int32_t* wave_sums, const PairTables* pt) {
   const int T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly);
@@ -243,6 +279,7 @@ __device__ void block_global_run(const Derived* __restrict__ d, const DevState& 
   const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
   const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
   const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const float eps24 = d->eps24;
   for (int s = 0; s < n_steps; ++s) {
     for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
     __syncthreads();
@@ -283,19 +320,21 @@ __device__ void block_global_run(const Derived* __restrict__ d, const DevState& 
             if (j == i) continue;
             const float rx = (float)(int32_t)(sc.sqx[base + jj] - p.qx) * sx0;
             const float ry = (float)(int32_t)(sc.sqy[base + jj] - p.qy) * sx1;
-            pair_force(d, si, st.species[j], rx, ry, ax, ay);
+            const int pk = si * kMaxSpecies + st.species[j];
+            pair_force(pt->cut2[pk], pt->sig6[pk], eps24, rx, ry, ax, ay);
           }
         }
       }
       const float fs = st.f_swim[gi], tz = st.torque_z[gi];
       const float fex = st.f_ext[gi], fey = st.f_ext[M + gi];
+      const PConst pc = load_pconst(d, si);
       if (sd_mode) {
-        any |= sd_step(d, p, ax, ay, fs, tz, fex, fey, g, md) ? 1 : 0;
+        any |= sd_step(pc, p, ax, ay, fs, tz, fex, fey, g, md) ? 1 : 0;
       } else {
         float vx, vy, w;
         const bool last = s == n_steps - 1;
-        bd_step(d, p, si, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
-                last, &vx, &vy, &w);
+        bd_step(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s, last,
+                &vx, &vy, &w);
         if (last) {
           st.vel[gi] = vx;
           st.vel[M + gi] = vy;
@@ -337,11 +376,13 @@ __global__ __launch_bounds__(1024) void k_global(const Derived* __restrict__ d, 
                                                  uint32_t* __restrict__ arrive, int lx, int ly,
                                                  int sd_mode, float g, float md) {
   extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ PairTables pt;
+  stage_pair_tables(d, &pt);
   int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
   int32_t* cnt = wave_sums + 16;
   const uint64_t step0 = sd_mode ? 0ull : *step_ctr;
   block_global_run(d, st, sc, blockIdx.x, n_steps, step0, lx, ly, sd_mode != 0, g, md, cnt,
-                   wave_sums);
+                   wave_sums, &pt);
   if (!sd_mode) advance_counter(step_ctr, arrive, step0, n_steps);
 }
 
@@ -533,6 +574,8 @@ __device__ __forceinline__ uint32_t nb_lane(const uint32_t (&w)[4], int b) {
 __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__ d, DevState st,
                                                      Scratch sc, int n_envs, int n_steps,
                                                      const uint64_t* __restrict__ step_ctr) {
+  __shared__ PairTables pt;
+  stage_pair_tables(d, &pt);
   const int lane = threadIdx.x & 63;
   const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const int e = gw / sc.wmax;
@@ -573,6 +616,10 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
   const uint64_t step0 = *step_ctr;
   const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
   const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const float eps24 = d->eps24;
+  const PConst pc = load_pconst(d, si);
+  const float* cut2_row = pt.cut2 + si * kMaxSpecies;
+  const float* sig6_row = pt.sig6 + si * kMaxSpecies;
   const uint32_t q0x = p.qx, q0y = p.qy;
   float dmax2 = 0.0f;
   float vx = 0.0f, vy = 0.0f, om = 0.0f;
@@ -588,12 +635,12 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
         if (k < cnt) {
           const float rx = (float)(int32_t)(oqx - p.qx) * sx0;
           const float ry = (float)(int32_t)(oqy - p.qy) * sx1;
-          pair_force(d, si, osp, rx, ry, ax, ay);
+          pair_force(cut2_row[osp], sig6_row[osp], eps24, rx, ry, ax, ay);
         }
       }
     }
     if (active) {
-      bd_step(d, p, si, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
+      bd_step(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
               s == n_steps - 1, &vx, &vy, &om);
       const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
       const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
@@ -625,6 +672,8 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
   int32_t* misc = wave_sums + 16;                          // 16
   int32_t* movers = misc + 16;                             // kMaxMovers
   int32_t* cnt = movers + kMaxMovers;                      // global-path cell counts
+  __shared__ PairTables pt;
+  stage_pair_tables(d, &pt);
   const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const uint64_t step0 = *step_ctr;
@@ -673,7 +722,8 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
     }
     if (tid == 0) sc.fallback[e] = 2;  // diagnostics: env re-run on the global path
     __syncthreads();
-    block_global_run(d, st, sc, e, n_steps, step0, lx, ly, false, 0.0f, 0.0f, cnt, wave_sums);
+    block_global_run(d, st, sc, e, n_steps, step0, lx, ly, false, 0.0f, 0.0f, cnt, wave_sums,
+                     &pt);
   }
   advance_counter(step_ctr, arrive, step0, n_steps);
 }

@@ -505,7 +505,9 @@ class SwarmEngine(Engine):
 
     @property
     def device(self):
-        return torch.device("cuda", torch.cuda.current_device())
+        if torch.cuda.is_available():
+            return torch.device("cuda", torch.cuda.current_device())
+        return torch.device("cpu")
 
     def _kT(self) -> float:
         return (self.params.temperature * self.ureg.boltzmann_constant).m_as("sim_energy")
@@ -815,6 +817,14 @@ class SwarmEngine(Engine):
         self._native.bind_stream()
         self._native.call("swarm_engine_upload_raw", q.ctypes.data, img.ctypes.data, ang.ctypes.data)
         self._host_cache = None
+
+    def window_stats(self) -> dict:
+        """Per-env diagnostics of the last integration window (see C ABI)."""
+        fb = np.zeros(self.n_envs, np.int32)
+        w = np.zeros(self.n_envs, np.int32)
+        self._native.bind_stream()
+        self._native.call("swarm_engine_window_stats", fb.ctypes.data, w.ctypes.data)
+        return {"fallback": fb, "waves": w}
 
     def step_count(self) -> int:
         self._native.bind_stream()

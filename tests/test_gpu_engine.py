@@ -1,0 +1,298 @@
+"""
+GPU tests through the product's Python surface (the SwarmRL-compatible API):
+reference known answers, device path == list path, a full PPO training run,
+and size-independent statistics of the noisy dynamics at full size.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import refsem
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    from swarmrl_amd import _capi
+
+    _capi.require_gpu()
+    torch.cuda.set_device(0)
+
+
+def _params(ureg, **kw):
+    from swarmrl_amd.engine import MDParams
+
+    return MDParams(ureg=ureg, **kw)
+
+
+# ------------------------------------------------ reference unit-test KATs
+def test_vision_cone_kat_product_list_path():
+    from swarmrl_amd.components import Colloid
+    from swarmrl_amd.observables import SubdividedVisionCones
+
+    vc = SubdividedVisionCones(vision_range=10, vision_half_angle=np.pi / 2, n_cones=3,
+                               radii=[1, 2, 3, 4, 1], particle_type=0)
+    cols = [
+        Colloid(np.array([0, 0, 0]), np.array([0, 1.0, 0]), 0, np.array([0, 0, 0]), 0),
+        Colloid(np.array([0, 5, 0]), np.array([1.0, 0, 0]), 1, np.array([0, 0, 0]), 0),
+        Colloid(np.array([0, 8, 0]), np.array([1.0, 0, 0]), 2, np.array([0, 0, 0]), 1),
+        Colloid(np.array([-7, 8, 0]), np.array([0.0, 1.0, 0]), 3, np.array([0, 0, 0]), 1),
+        Colloid(np.array([1, 1, 0]), np.array([0.0, 1.0, 0]), 4, np.array([0, 0, 0]), 0),
+    ]
+    obs = vc.compute_observable(cols)[0]
+    assert obs[0, 0] == 1.0
+    assert obs[1, 0] == 0.8
+    assert obs[2, 0] == 0.0
+    assert obs[0, 1] == 0.0
+    assert obs[1, 1] == 0.75
+    assert obs[2, 1] == 0.0
+
+
+def test_concentration_field_kat_product():
+    from swarmrl_amd.components import Colloid
+    from swarmrl_amd.observables import ConcentrationField
+
+    ob = ConcentrationField(source=np.array([0.5, 0.5, 0.0]), decay_fn=lambda x: -1 * x,
+                            box_length=np.array([1.0, 1.0, 1.0]), particle_type=0)
+    old = [Colloid(np.array([0.0, 0.0, 0.0]), np.array([0.0, 1.0, 0]), 0, 0),
+           Colloid(np.array([0.0, 1.0, 0.0]), np.array([0.0, 1.0, 0]), 1, 0),
+           Colloid(np.array([1.0, 1.0, 0.0]), np.array([0.0, 1.0, 0]), 2, 0)]
+    ob.initialize(old)
+    assert list(ob._historic_positions.keys()) == ["0", "1", "2"]
+    np.testing.assert_array_equal(ob._historic_positions["1"], [0.0, 1.0, 0.0])
+    assert ob.scale_factor == 100.0
+    new = [Colloid(np.array([1.0, 0.0, 0.0]), np.array([0.0, 1.0, 0]), 0, 0),
+           Colloid(np.array([1.0, 1.0, 0.0]), np.array([0.0, 1.0, 0]), 1, 0),
+           Colloid(np.array([0.0, 1.0, 0.0]), np.array([0.0, 1.0, 0]), 2, 0)]
+    obs = ob.compute_observable(new)
+    expect = np.array([
+        -100 * (np.linalg.norm(n.pos - ob.source) - np.linalg.norm(o.pos - ob.source))
+        for n, o in zip(new, old)
+    ]).reshape(-1, 1)
+    np.testing.assert_array_equal(obs, expect)
+    with pytest.raises(ValueError):
+        ConcentrationField(np.zeros(3), lambda x: x, np.ones(3)).compute_observable(new)
+
+
+def test_gradient_sensing_kat_product():
+    from swarmrl_amd.components import Colloid
+    from swarmrl_amd.tasks.searching import GradientSensing
+
+    task = GradientSensing(source=np.array([0.5, 0.5, 0.0]), decay_function=lambda x: 1 - x,
+                           box_length=np.array([1.0, 1.0, 1.0]), particle_type=0,
+                           reward_scale_factor=1)
+    old = [Colloid(np.array([0.0, 0.0, 0.0]), np.array([0.0, 1.0, 0]), 0, 0),
+           Colloid(np.array([0.0, 0.6, 0.0]), np.array([0.0, 1.0, 0]), 1, 0),
+           Colloid(np.array([1.0, 0.0, 0.0]), np.array([0.0, 1.0, 0]), 2, 0)]
+    task.initialize(old)
+    new = [Colloid(np.array([0.2, 0.2, 0.0]), np.array([0.0, 1.0, 0]), 0, 0),
+           Colloid(np.array([0.0, 1.0, 0.0]), np.array([0.0, 1.0, 0]), 1, 0),
+           Colloid(np.array([0.0, 1.0, 0.0]), np.array([0.0, 1.0, 0]), 2, 0)]
+    r = task(new)
+    d1 = np.linalg.norm(new[0].pos - task.source)
+    d0 = np.linalg.norm(old[0].pos - task.source)
+    assert r[0] > 0 and r[0] == pytest.approx((1 - d1) - (1 - d0), rel=1e-6)
+    assert r[1] == 0.0
+    assert r[2] == 0.0
+
+
+# ------------------------------------------------------ engine semantics
+def _engine(ureg, tmp_path, n, L, seed=42, n_envs=1, **kw):
+    from swarmrl_amd.engine import SwarmEngine
+
+    p = _params(ureg, box_length=ureg.Quantity([L, L, L], "micrometer"), **kw)
+    eng = SwarmEngine(p, n_dims=2, seed=seed, out_folder=tmp_path, write_chunk_size=1,
+                      n_envs=n_envs)
+    eng.add_colloids(n, ureg.Quantity(1.0, "micrometer"),
+                     ureg.Quantity(np.array([L / 2, L / 2, 0.0]), "micrometer"),
+                     ureg.Quantity(L / 2 - 2, "micrometer"), type_colloid=1)
+    return eng
+
+
+def test_kt0_drift_and_velocity_kat(tmp_path):
+    """test_espresso.py:89-111 in 2-D: rotate to a fixed director, then
+    ConstForce(1.234): v = F d / gamma_t and x = x0 + t v (rtol 2e-6)."""
+    from swarmrl_amd.agents import dummy_models
+    from swarmrl_amd.force_functions import ForceFunction
+    from swarmrl_amd.units import UnitRegistry
+
+    ureg = UnitRegistry()
+    eng = _engine(ureg, tmp_path, 5, 1000.0,
+                  fluid_dyn_viscosity=ureg.Quantity(8.9e-3, "pascal * second"),
+                  WCA_epsilon=ureg.Quantity(1e-20, "joule"),
+                  temperature=ureg.Quantity(0, "kelvin"),
+                  time_step=ureg.Quantity(0.01, "second"),
+                  time_slice=ureg.Quantity(0.1, "second"),
+                  write_interval=ureg.Quantity(0.1, "second"))
+    old = eng.get_particle_data()
+    direc = np.array([1 / np.sqrt(2), 1 / np.sqrt(2), 0])
+    eng.integrate(1, ForceFunction({"1": dummy_models.ToConstDirection(direc)}))
+    eng.system.time = 0.0
+    for d in eng.get_particle_data()["Directors"]:
+        np.testing.assert_array_almost_equal(d, direc)
+    force = 1.234
+    eng.integrate(10, ForceFunction({"1": dummy_models.ConstForce(force)}))
+    new = eng.get_particle_data()
+    gt, _ = eng.get_friction_coefficients(1)
+    for v in new["Velocities"]:
+        np.testing.assert_array_almost_equal(v, force * direc / gt)
+    np.testing.assert_allclose(old["Unwrapped_Positions"] + eng.system.time * force * direc / gt,
+                               new["Unwrapped_Positions"], rtol=2e-6)
+    eng.finalize()
+
+
+def test_isotropic_2d_rotation_and_set_direction(tmp_path):
+    """test_espresso_2d.py:29-92."""
+    from swarmrl_amd.agents import dummy_models
+    from swarmrl_amd.force_functions import ForceFunction
+    from swarmrl_amd.units import UnitRegistry
+
+    ureg = UnitRegistry()
+    eng = _engine(ureg, tmp_path, 14, 1000.0,
+                  fluid_dyn_viscosity=ureg.Quantity(8.9e-4, "pascal * second"),
+                  WCA_epsilon=ureg.Quantity(1e-20, "joule"),
+                  temperature=ureg.Quantity(300, "kelvin"),
+                  time_step=ureg.Quantity(0.05, "second"),
+                  time_slice=ureg.Quantity(0.1, "second"),
+                  write_interval=ureg.Quantity(0.1, "second"))
+    d0 = eng.get_particle_data()["Directors"]
+    np.testing.assert_allclose(eng.get_particle_data()["Unwrapped_Positions"][:, 2], 0)
+    eng.integrate(10, ForceFunction({"1": dummy_models.ConstForce(force=0)}))
+    d1 = eng.get_particle_data()["Directors"]
+    np.testing.assert_array_almost_equal(d1[:, 2], 0)
+    assert not np.allclose(d0, d1, atol=1e-6)
+    orientation = np.array([1 / np.sqrt(2), 1 / np.sqrt(2), 0])
+    eng.manage_forces(ForceFunction({"1": dummy_models.ToConstDirection(orientation)}))
+    for d in eng.get_particle_data()["Directors"]:
+        np.testing.assert_array_almost_equal(d, orientation)
+
+
+def test_device_path_equals_list_path(tmp_path, monkeypatch):
+    """The batched SwarmView path and the reference list-of-Colloid path give
+    bit-identical engine states (same actions, same kernels)."""
+    from swarmrl_amd.agents import dummy_models
+    from swarmrl_amd.engine import SwarmEngine
+    from swarmrl_amd.force_functions import ForceFunction
+    from swarmrl_amd.units import UnitRegistry
+
+    states = []
+    for use_device in (True, False):
+        ureg = UnitRegistry()
+        eng = _engine(ureg, tmp_path / str(use_device), 300, 120.0)
+        if not use_device:
+            monkeypatch.setattr(SwarmEngine, "_device_capable", staticmethod(lambda fm: False))
+        ff = ForceFunction({"1": dummy_models.ConstForceAndTorque(4.0, np.array([0, 0, 3.0]))})
+        eng.integrate(3, ff)
+        states.append(eng.get_raw_state())
+        monkeypatch.undo()
+    for k in ("q", "img", "ang"):
+        assert np.array_equal(states[0][k], states[1][k])
+
+
+def test_observables_device_vs_list(tmp_path):
+    from swarmrl_amd.components import Colloid
+    from swarmrl_amd.observables import SubdividedVisionCones
+    from swarmrl_amd.units import UnitRegistry
+    from swarmrl_amd.agents import dummy_models
+    from swarmrl_amd.force_functions import ForceFunction
+
+    ureg = UnitRegistry()
+    n = 500
+    eng = _engine(ureg, tmp_path, n, 150.0)
+    eng.integrate(1, ForceFunction({"1": dummy_models.ConstForce(5.0)}))
+    vc = SubdividedVisionCones(12.0, 1.1, 4, radii=[1.0] * n, particle_type=1)
+    dev = vc.compute_observable(eng.swarm_view())[0].cpu().numpy()
+    data = eng.get_particle_data()
+    cols = [Colloid(data["Unwrapped_Positions"][i], data["Directors"][i], i, None, 1)
+            for i in range(n)]
+    lst = np.stack(vc.compute_observable(cols))
+    # the list path re-quantises fp64 positions into a virtual box: equal up
+    # to fp32 rounding, except a colloid exactly on a cone rim
+    bad = np.abs(dev - lst) > 1e-5
+    assert bad.sum() <= 2
+
+
+def test_ppo_training_device_path(tmp_path):
+    """ContinuousTrainer + ActorCriticAgent (vision cones, gradient sensing,
+    PPO) entirely on the device path."""
+    from swarmrl_amd.actions import Action
+    from swarmrl_amd.agents import ActorCriticAgent
+    from swarmrl_amd.networks import ActorCriticMLP, TorchModel
+    from swarmrl_amd.observables import SubdividedVisionCones
+    from swarmrl_amd.tasks.searching import GradientSensing
+    from swarmrl_amd.trainers import ContinuousTrainer
+    from swarmrl_amd.units import UnitRegistry
+
+    ureg = UnitRegistry()
+    n, L = 200, 100.0
+    eng = _engine(ureg, tmp_path, n, L, n_envs=2,
+                  time_slice=ureg.Quantity(0.1, "second"),
+                  write_interval=ureg.Quantity(1.0, "second"))
+    net = TorchModel(ActorCriticMLP(3, 4, 32), input_shape=(3,), rng_key=3)
+    before = [p.detach().clone() for p in net.model.parameters()]
+    actions = {"a": Action(torque=np.array([0, 0, 10.0])), "b": Action(force=10.0),
+               "c": Action(torque=np.array([0, 0, -10.0])), "d": Action()}
+    agent = ActorCriticAgent(
+        1, net, GradientSensing(np.array([L / 2, L / 2, 0]), lambda d: 1 - d,
+                                np.array([L, L, L]), 10, particle_type=1),
+        SubdividedVisionCones(10.0, np.pi / 2, 3, [1.0] * n, particle_type=1), actions)
+    agent.loss.n_epochs = 3
+    trainer = ContinuousTrainer([agent])
+    rewards = trainer.perform_rl_training(eng, n_episodes=3, episode_length=4)
+    assert rewards.shape == (4,) and np.all(np.isfinite(rewards))
+    after = list(net.model.parameters())
+    assert any(not torch.equal(a, b) for a, b in zip(after, before))
+
+
+# --------------------------------------------------- statistics, full size
+def test_free_diffusion_statistics_4096(tmp_path):
+    """MSD = 4 D_t t and <cos dtheta> = exp(-D_r t) at 4096 colloids x 2 envs."""
+    from swarmrl_amd.agents import dummy_models
+    from swarmrl_amd.force_functions import ForceFunction
+    from swarmrl_amd.units import UnitRegistry
+
+    ureg = UnitRegistry()
+    n = 4096
+    L = 2 * np.sqrt(n / 0.1)
+    # 1e-26 J ~ 2.5e-6 sim energy: no repulsion (1e-20 J would be ~2.5 kT)
+    eng = _engine(ureg, tmp_path, n, L, n_envs=2,
+                  WCA_epsilon=ureg.Quantity(1e-26, "joule"),
+                  write_interval=ureg.Quantity(100.0, "second"))
+    ff = ForceFunction({"1": dummy_models.ConstForce(0.0)})
+    eng.integrate(1, ff)
+    p0 = eng.get_particle_data()
+    eng.integrate(10, ff)  # t = 1 s
+    p1 = eng.get_particle_data()
+    gt, gr = eng.get_friction_coefficients(1)
+    kT = eng._kT()
+    t = 1.0
+    disp = p1["Unwrapped_Positions"] - p0["Unwrapped_Positions"]
+    msd = np.mean(np.sum(disp[..., :2] ** 2, axis=-1))
+    assert msd == pytest.approx(refsem.expected_msd_2d(kT, gt, t), rel=0.04)
+    cosd = np.mean(np.sum(p0["Directors"] * p1["Directors"], axis=-1))
+    assert cosd == pytest.approx(refsem.expected_orientation_corr(kT, gr, t), abs=0.02)
+    # the two envs are independent replicas (own placement, own noise)
+    assert not np.allclose(disp[0], disp[1])
+
+
+def test_wca_slows_self_diffusion(tmp_path):
+    """Property check at full size: with WCA on, collisions reduce the MSD
+    below the free value (the reference's epsilon = k_B 300 K)."""
+    from swarmrl_amd.agents import dummy_models
+    from swarmrl_amd.force_functions import ForceFunction
+    from swarmrl_amd.units import UnitRegistry
+
+    ureg = UnitRegistry()
+    n = 4096
+    L = 2 * np.sqrt(n / 0.3)  # area fraction 0.3
+    eng = _engine(ureg, tmp_path, n, L, write_interval=ureg.Quantity(100.0, "second"))
+    ff = ForceFunction({"1": dummy_models.ConstForce(0.0)})
+    eng.integrate(1, ff)
+    p0 = eng.get_particle_data()
+    eng.integrate(10, ff)
+    p1 = eng.get_particle_data()
+    gt, _ = eng.get_friction_coefficients(1)
+    msd = np.mean(np.sum((p1["Unwrapped_Positions"] - p0["Unwrapped_Positions"])[:, :2] ** 2, 1))
+    assert msd < 0.95 * refsem.expected_msd_2d(eng._kT(), gt, 1.0)
