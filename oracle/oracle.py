@@ -66,7 +66,7 @@ def lib():
         L.or_sincos_turn.argtypes = [ctypes.c_uint32, _P, _P]
         L.or_signed_angle.restype = ctypes.c_float
         L.or_signed_angle.argtypes = [_P, _P]
-        L.or_normals4.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+        L.or_normals3.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_uint64, ctypes.c_uint32, _P]
         L.or_bd_run.restype = ctypes.c_int
         L.or_bd_run.argtypes = [ctypes.POINTER(Params), ctypes.c_int, _P, _P, _P, _P, _P, _P,
@@ -257,9 +257,10 @@ def philox(ctr, key):
     return list(o)
 
 
-def normals4(seed, env, pid, step, tag):
-    out = np.zeros(4, np.float32)
-    lib().or_normals4(int(seed), int(env), int(pid), int(step), int(tag), _ptr(out))
+def normals3(seed, env, pid, step, tag):
+    """Three standard normals of one Philox block (swarm_oracle.c or_normals3)."""
+    out = np.zeros(3, np.float32)
+    lib().or_normals3(int(seed), int(env), int(pid), int(step), int(tag), _ptr(out))
     return out
 
 

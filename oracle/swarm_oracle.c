@@ -106,29 +106,21 @@ float or_logf(float x) {
   }
   float z = m * m;
   float y = 7.0376836292e-2f;
-  y = y * m;
-  y = y + -1.1514610310e-1f;
-  y = y * m;
-  y = y + 1.1676998740e-1f;
-  y = y * m;
-  y = y + -1.2420140846e-1f;
-  y = y * m;
-  y = y + 1.4249322787e-1f;
-  y = y * m;
-  y = y + -1.6668057665e-1f;
-  y = y * m;
-  y = y + 2.0000714765e-1f;
-  y = y * m;
-  y = y + -2.4999993993e-1f;
-  y = y * m;
-  y = y + 3.3333331174e-1f;
+  y = fmaf(y, m, -1.1514610310e-1f);
+  y = fmaf(y, m, 1.1676998740e-1f);
+  y = fmaf(y, m, -1.2420140846e-1f);
+  y = fmaf(y, m, 1.4249322787e-1f);
+  y = fmaf(y, m, -1.6668057665e-1f);
+  y = fmaf(y, m, 2.0000714765e-1f);
+  y = fmaf(y, m, -2.4999993993e-1f);
+  y = fmaf(y, m, 3.3333331174e-1f);
   y = y * m;
   y = y * z;
   float fe = (float)e;
-  y = y + -2.12194440e-4f * fe;
-  y = y + -0.5f * z;
+  y = fmaf(-2.12194440e-4f, fe, y);
+  y = fmaf(-0.5f, z, y);
   float r = m + y;
-  r = r + 0.693359375f * fe;
+  r = fmaf(0.693359375f, fe, r);
   return r;
 }
 
@@ -140,22 +132,16 @@ void or_sincos_turn(uint32_t a, float *s_out, float *c_out) {
   float x = (float)rem * 1.46291807926715968e-09f;      /* 2 pi / 2^32 */
   float z = x * x;
   float sp = -1.9515295891e-4f;
+  sp = fmaf(sp, z, 8.3321608736e-3f);
+  sp = fmaf(sp, z, -1.6666654611e-1f);
   sp = sp * z;
-  sp = sp + 8.3321608736e-3f;
-  sp = sp * z;
-  sp = sp + -1.6666654611e-1f;
-  sp = sp * z;
-  sp = sp * x;
-  float s = sp + x;
+  float s = fmaf(sp, x, x);
   float cp = 2.443315711809948e-5f;
+  cp = fmaf(cp, z, -1.388731625493765e-3f);
+  cp = fmaf(cp, z, 4.166664568298827e-2f);
   cp = cp * z;
-  cp = cp + -1.388731625493765e-3f;
-  cp = cp * z;
-  cp = cp + 4.166664568298827e-2f;
-  cp = cp * z;
-  cp = cp * z;
-  float c = cp - 0.5f * z;
-  c = c + 1.0f;
+  float h = fmaf(-0.5f, z, 1.0f);
+  float c = fmaf(cp, z, h);
   float so, co;
   switch (quad) {
   case 0:
@@ -182,17 +168,12 @@ void or_sincos_turn(uint32_t a, float *s_out, float *c_out) {
 static float asinf_small(float a) { /* |a| <= 0.5 */
   float z = a * a;
   float p = 4.2163199048e-2f;
+  p = fmaf(p, z, 2.4181311049e-2f);
+  p = fmaf(p, z, 4.5470025998e-2f);
+  p = fmaf(p, z, 7.4953002686e-2f);
+  p = fmaf(p, z, 1.6666752422e-1f);
   p = p * z;
-  p = p + 2.4181311049e-2f;
-  p = p * z;
-  p = p + 4.5470025998e-2f;
-  p = p * z;
-  p = p + 7.4953002686e-2f;
-  p = p * z;
-  p = p + 1.6666752422e-1f;
-  p = p * z;
-  p = p * a;
-  return p + a;
+  return fmaf(p, a, a);
 }
 
 float or_acosf(float x) {
@@ -223,24 +204,28 @@ float or_signed_angle(const float my[3], const float other[3]) {
   return orth >= 0.0f ? ang : -ang;
 }
 
-/* Four standard normals for (seed, env, particle id, step, tag):
- * Box-Muller on the two 32-bit pairs of one Philox4x32-10 block. */
-void or_normals4(uint64_t seed, uint32_t env, uint32_t id, uint64_t step,
-                 uint32_t tag, float out[4]) {
+/* Three standard normals for (seed, env, particle id, step, tag): a full
+ * Box-Muller pair from Philox words 0/1, the cosine leg of words 2/3. */
+static float bm_radius(uint32_t r) {
+  float u = (float)(r >> 9) + 0.5f;
+  u = u * 1.1920928955078125e-07f; /* 2^-23 : u in (0, 1) */
+  return sqrtf(-2.0f * or_logf(u));
+}
+
+void or_normals3(uint64_t seed, uint32_t env, uint32_t id, uint64_t step,
+                 uint32_t tag, float out[3]) {
   uint32_t ctr[4] = {id, (uint32_t)step, (uint32_t)(step >> 32), tag};
   uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32) ^ env};
   uint32_t r[4];
   or_philox4x32_10(ctr, key, r);
-  for (int p = 0; p < 2; ++p) {
-    float u = (float)(r[2 * p] >> 9) + 0.5f;
-    u = u * 1.1920928955078125e-07f; /* 2^-23 : u in (0, 1) */
-    float l = or_logf(u);
-    float rad = sqrtf(-2.0f * l);
-    float s, c;
-    or_sincos_turn(r[2 * p + 1], &s, &c);
-    out[2 * p] = rad * c;
-    out[2 * p + 1] = rad * s;
-  }
+  float rad0 = bm_radius(r[0]);
+  float rad1 = bm_radius(r[2]);
+  float s0, c0, s1, c1;
+  or_sincos_turn(r[1], &s0, &c0);
+  or_sincos_turn(r[3], &s1, &c1);
+  out[0] = rad0 * c0;
+  out[1] = rad0 * s0;
+  out[2] = rad1 * c1;
 }
 
 /* ------------------------------------------------------------------ */
@@ -518,8 +503,8 @@ int or_bd_run(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
       float dy = fy * d.mob_dt[sp];
       float dth = torque_z[i] * d.rot_dt[sp];
       if (noisy) {
-        float g[4];
-        or_normals4(p->seed, env, (uint32_t)i, step, 0u, g);
+        float g[3];
+        or_normals3(p->seed, env, (uint32_t)i, step, 0u, g);
         dx = dx + d.sig_t[sp] * g[0];
         dy = dy + d.sig_t[sp] * g[1];
         dth = dth + d.sig_r[sp] * g[2];
@@ -531,8 +516,8 @@ int or_bd_run(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
         float vx = fx * d.inv_gt[sp], vy = fy * d.inv_gt[sp];
         float w = torque_z[i] * d.inv_gr[sp];
         if (noisy) {
-          float g[4];
-          or_normals4(p->seed, env, (uint32_t)i, step, 1u, g);
+          float g[3];
+          or_normals3(p->seed, env, (uint32_t)i, step, 1u, g);
           vx = vx + d.sig_v[sp] * g[0];
           vy = vy + d.sig_v[sp] * g[1];
           w = w + d.sig_w[sp] * g[2];

@@ -58,6 +58,22 @@ __device__ __forceinline__ float sqrt_rn(float x) {
   return tiny ? s * 1.52587890625e-05f : s;  // * 2^-16
 }
 
+// Correctly rounded sqrt for a positive normal finite x (the Box-Muller
+// radius -2 ln u >= 1.19e-7): no special-case or denormal branch.
+__device__ __forceinline__ float sqrt_pos(float x) {
+  float s = __builtin_amdgcn_sqrtf(x);
+  const uint32_t si = __float_as_uint(s);
+  const float s_dn = __uint_as_float(si - 1u);
+  const float s_up = __uint_as_float(si + 1u);
+  const float r_dn = __builtin_fmaf(-s_dn, s, x);
+  const float r_up = __builtin_fmaf(-s_up, s, x);
+  s = (r_dn <= 0.0f) ? s_dn : s;
+  s = (r_up > 0.0f) ? s_up : s;
+  return s;
+}
+
+// Polynomials below are Horner chains of fused multiply-adds: one rounding
+// per step, reproduced by C fmaf() in the oracle.
 __device__ __forceinline__ float logf_fixed(float x) {
   const uint32_t b = __float_as_uint(x);
   int e = (int)((b >> 23) & 0xffu) - 126;
@@ -71,29 +87,21 @@ __device__ __forceinline__ float logf_fixed(float x) {
   }
   const float z = m * m;
   float y = 7.0376836292e-2f;
-  y = y * m;
-  y = y + -1.1514610310e-1f;
-  y = y * m;
-  y = y + 1.1676998740e-1f;
-  y = y * m;
-  y = y + -1.2420140846e-1f;
-  y = y * m;
-  y = y + 1.4249322787e-1f;
-  y = y * m;
-  y = y + -1.6668057665e-1f;
-  y = y * m;
-  y = y + 2.0000714765e-1f;
-  y = y * m;
-  y = y + -2.4999993993e-1f;
-  y = y * m;
-  y = y + 3.3333331174e-1f;
+  y = __builtin_fmaf(y, m, -1.1514610310e-1f);
+  y = __builtin_fmaf(y, m, 1.1676998740e-1f);
+  y = __builtin_fmaf(y, m, -1.2420140846e-1f);
+  y = __builtin_fmaf(y, m, 1.4249322787e-1f);
+  y = __builtin_fmaf(y, m, -1.6668057665e-1f);
+  y = __builtin_fmaf(y, m, 2.0000714765e-1f);
+  y = __builtin_fmaf(y, m, -2.4999993993e-1f);
+  y = __builtin_fmaf(y, m, 3.3333331174e-1f);
   y = y * m;
   y = y * z;
   const float fe = (float)e;
-  y = y + -2.12194440e-4f * fe;
-  y = y + -0.5f * z;
+  y = __builtin_fmaf(-2.12194440e-4f, fe, y);
+  y = __builtin_fmaf(-0.5f, z, y);
   float r = m + y;
-  r = r + 0.693359375f * fe;
+  r = __builtin_fmaf(0.693359375f, fe, r);
   return r;
 }
 
@@ -105,22 +113,16 @@ __device__ __forceinline__ void sincos_turn(uint32_t a, float* s_out, float* c_o
   const float x = (float)rem * 1.46291807926715968e-09f;
   const float z = x * x;
   float sp = -1.9515295891e-4f;
+  sp = __builtin_fmaf(sp, z, 8.3321608736e-3f);
+  sp = __builtin_fmaf(sp, z, -1.6666654611e-1f);
   sp = sp * z;
-  sp = sp + 8.3321608736e-3f;
-  sp = sp * z;
-  sp = sp + -1.6666654611e-1f;
-  sp = sp * z;
-  sp = sp * x;
-  const float s = sp + x;
+  const float s = __builtin_fmaf(sp, x, x);
   float cp = 2.443315711809948e-5f;
+  cp = __builtin_fmaf(cp, z, -1.388731625493765e-3f);
+  cp = __builtin_fmaf(cp, z, 4.166664568298827e-2f);
   cp = cp * z;
-  cp = cp + -1.388731625493765e-3f;
-  cp = cp * z;
-  cp = cp + 4.166664568298827e-2f;
-  cp = cp * z;
-  cp = cp * z;
-  float c = cp - 0.5f * z;
-  c = c + 1.0f;
+  const float h = __builtin_fmaf(-0.5f, z, 1.0f);
+  const float c = __builtin_fmaf(cp, z, h);
   // quadrant rotation without divergent branches
   const bool swap = (quad & 1u) != 0u;
   float so = swap ? c : s;
@@ -138,17 +140,12 @@ __device__ __forceinline__ void sincos_turn(uint32_t a, float* s_out, float* c_o
 __device__ __forceinline__ float asinf_small(float a) {
   const float z = a * a;
   float p = 4.2163199048e-2f;
+  p = __builtin_fmaf(p, z, 2.4181311049e-2f);
+  p = __builtin_fmaf(p, z, 4.5470025998e-2f);
+  p = __builtin_fmaf(p, z, 7.4953002686e-2f);
+  p = __builtin_fmaf(p, z, 1.6666752422e-1f);
   p = p * z;
-  p = p + 2.4181311049e-2f;
-  p = p * z;
-  p = p + 4.5470025998e-2f;
-  p = p * z;
-  p = p + 7.4953002686e-2f;
-  p = p * z;
-  p = p + 1.6666752422e-1f;
-  p = p * z;
-  p = p * a;
-  return p + a;
+  return __builtin_fmaf(p, a, a);
 }
 
 __device__ __forceinline__ float acosf_fixed(float x) {
@@ -165,28 +162,30 @@ __device__ __forceinline__ float acosf_fixed(float x) {
   return 1.57079632679489661923f - asinf_small(x);
 }
 
-// Four standard normals (two Box-Muller pairs of one Philox block).
-__device__ __forceinline__ void normals4(uint32_t k0, uint32_t k1, uint32_t id,
-                                         uint64_t step, uint32_t tag, float g[4]) {
+// Three standard normals from one Philox block: a full Box-Muller pair from
+// words (x, y) and the cosine leg of a second pair from (z, w).
+__device__ __forceinline__ float bm_radius(uint32_t r) {
+  float u = (float)(r >> 9) + 0.5f;
+  u = u * 1.1920928955078125e-07f;  // 2^-23: u in (0, 1)
+  return sqrt_pos(-2.0f * logf_fixed(u));
+}
+
+__device__ __forceinline__ void normals3(uint32_t k0, uint32_t k1, uint32_t id,
+                                         uint64_t step, uint32_t tag, float g[3]) {
   u32x4 c;
   c.x = id;
   c.y = (uint32_t)step;
   c.z = (uint32_t)(step >> 32);
   c.w = tag;
   const u32x4 r = philox4x32_10(c, k0, k1);
-  const uint32_t ru[2] = {r.x, r.z};
-  const uint32_t ra[2] = {r.y, r.w};
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    float u = (float)(ru[p] >> 9) + 0.5f;
-    u = u * 1.1920928955078125e-07f;
-    const float l = logf_fixed(u);
-    const float rad = sqrt_rn(-2.0f * l);
-    float s, c2;
-    sincos_turn(ra[p], &s, &c2);
-    g[2 * p] = rad * c2;
-    g[2 * p + 1] = rad * s;
-  }
+  const float rad0 = bm_radius(r.x);
+  const float rad1 = bm_radius(r.z);
+  float s0, c0, s1, c1;
+  sincos_turn(r.y, &s0, &c0);
+  sincos_turn(r.w, &s1, &c1);
+  g[0] = rad0 * c0;
+  g[1] = rad0 * s0;
+  g[2] = rad1 * c1;
 }
 
 // --------------------------------------------------- fixed-point helpers
@@ -197,8 +196,16 @@ __device__ __forceinline__ int32_t f2i32(float v) {
 
 __device__ __forceinline__ int64_t f2fix24(float v) {
   v = v * 16777216.0f;
+  // |v| < 2^31 (force below 128): one int32 conversion, same value
+  if (__builtin_expect(fabsf(v) < 2147483520.0f, 1)) return (int64_t)__float2int_rn(v);
   v = fminf(fmaxf(v, -4.611686018427387904e18f), 4.611686018427387904e18f);
   return __float2ll_rn(v);
+}
+
+// int64 -> fp32 round-to-nearest; int32-range values take one conversion.
+__device__ __forceinline__ float i64_to_f32(int64_t a) {
+  if (__builtin_expect(a == (int64_t)(int32_t)a, 1)) return (float)(int32_t)a;
+  return (float)a;
 }
 
 __device__ __forceinline__ void advance(uint32_t& q, int32_t& img, int32_t dq) {

@@ -214,16 +214,21 @@ __global__ __launch_bounds__(1024) void k_vision_grid(DevState st, swarm_vision_
 }
 
 // ---------------------------------------------------------- vision cone
-// NB = bins held in registers (>= n_cones * n_types), statically indexed.
-template <int NB>
+// One group of G lanes per (env, agent): the candidates of the 3x3 cell
+// stencil form one flat index range that the G lanes split; each lane keeps
+// NB bins (>= n_cones * n_types) of 2^-32 fixed-point amplitude in
+// registers, and the group adds them with xor-shuffles.  Integer sums make
+// the result independent of G and of the visiting order.
+template <int NB, int G>
 __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __restrict__ d,
                                                 swarm_vision_params_t vp, int lx, int ly,
                                                 const int32_t* __restrict__ start, VisionSorted vs,
                                                 const int32_t* __restrict__ agents, int n_agents,
                                                 float* __restrict__ out, int n_envs) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_envs * n_agents) return;
-  const int e = t / n_agents, ai = t - e * n_agents;
+  const int grp = t / G, sub = t & (G - 1);
+  if (grp >= n_envs * n_agents) return;  // whole groups only (G divides 64)
+  const int e = grp / n_agents, ai = grp - e * n_agents;
   const int N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int i = agents[ai];
@@ -249,50 +254,67 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
   const float R = vp.vision_range;
   // conservative pre-test on dist^2 (the exact test below is on fp32 sqrt)
   const float R2pad = R * R * 1.0001f;
-  for (int oy = loy; oy <= hiy; ++oy) {
-    const int y = (cy + oy + ncy) & (ncy - 1);
-    for (int ox = lox; ox <= hix; ++ox) {
+  int skip = sub;  // offset of this lane's next flat index past the current cell
+#pragma unroll
+  for (int r = 0; r < 9; ++r) {
+    const int oy = r / 3 - 1, ox = r % 3 - 1;
+    int jb = 0, je = 0;
+    if (oy >= loy && oy <= hiy && ox >= lox && ox <= hix) {
+      const int y = (cy + oy + ncy) & (ncy - 1);
       const int x = (cx + ox + ncx) & (ncx - 1);
       const int cc = (y << lx) | x;
-      const int jb = so[cc], je = so[cc + 1];
-      for (int jj = jb; jj < je; ++jj) {
-        const size_t p = base + jj;
-        const int ti = vs.tslot[p];
-        if (ti < 0) continue;
-        const int64_t dqx = ((int64_t)(vs.ix[p] - ixi) * (int64_t)4294967296LL) +
-                            ((int64_t)vs.qx[p] - (int64_t)qxi);
-        const int64_t dqy = ((int64_t)(vs.iy[p] - iyi) * (int64_t)4294967296LL) +
-                            ((int64_t)vs.qy[p] - (int64_t)qyi);
-        // unwrapped separations beyond half a box are never within range
-        // (vision_range < L/2): skip them and convert the rest from int32,
-        // whose conversion is a single exact-rounding instruction.
-        if (dqx < -2147483647LL || dqx > 2147483647LL || dqy < -2147483647LL ||
-            dqy > 2147483647LL)
-          continue;
-        const float dx = (float)(int32_t)dqx * sx0, dy = (float)(int32_t)dqy * sx1;
-        const float dist2 = dx * dx + dy * dy;
-        if (!(dist2 < R2pad) || dist2 == 0.0f) continue;
-        if (vs.idx[p] == i) continue;
-        const float dist = swarm::sqrt_rn(dist2);
-        if (!(dist < R)) continue;
-        float amp = (2.0f * vs.rad[p]) / dist;
-        amp = fminf(1.0f, amp);
-        const float ux = dx / dist, uy = dy / dist;
-        float dot = ux * mx + uy * my;
-        dot = fminf(fmaxf(dot, -1.0f), 1.0f);
-        float an = swarm::acosf_fixed(dot);
-        const float orth = ux * (-my) + uy * mx;
-        if (orth < 0.0f) an = -an;
-        const int64_t fixed = __float2ll_rn(amp * 4294967296.0f);
-        int bin = -1;
-        for (int k = 0; k < vp.n_cones; ++k)
-          if (vp.rims[k] < an && an < vp.rims[k + 1]) bin = k * vp.n_types + ti;
+      jb = so[cc];
+      je = so[cc + 1];
+    }
+    int jj = jb + skip;
+    for (; jj < je; jj += G) {
+      const size_t p = base + jj;
+      const int ti = vs.tslot[p];
+      if (ti < 0) continue;
+      const int64_t dqx = ((int64_t)(vs.ix[p] - ixi) * (int64_t)4294967296LL) +
+                          ((int64_t)vs.qx[p] - (int64_t)qxi);
+      const int64_t dqy = ((int64_t)(vs.iy[p] - iyi) * (int64_t)4294967296LL) +
+                          ((int64_t)vs.qy[p] - (int64_t)qyi);
+      // unwrapped separations beyond half a box are never within range
+      // (vision_range < L/2): skip them and convert the rest from int32,
+      // whose conversion is a single exact-rounding instruction.
+      if (dqx < -2147483647LL || dqx > 2147483647LL || dqy < -2147483647LL ||
+          dqy > 2147483647LL)
+        continue;
+      const float dx = (float)(int32_t)dqx * sx0, dy = (float)(int32_t)dqy * sx1;
+      const float dist2 = dx * dx + dy * dy;
+      if (!(dist2 < R2pad) || dist2 == 0.0f) continue;
+      if (vs.idx[p] == i) continue;
+      const float dist = swarm::sqrt_rn(dist2);
+      if (!(dist < R)) continue;
+      float amp = (2.0f * vs.rad[p]) / dist;
+      amp = fminf(1.0f, amp);
+      const float ux = dx / dist, uy = dy / dist;
+      float dot = ux * mx + uy * my;
+      dot = fminf(fmaxf(dot, -1.0f), 1.0f);
+      float an = swarm::acosf_fixed(dot);
+      const float orth = ux * (-my) + uy * mx;
+      if (orth < 0.0f) an = -an;
+      const int64_t fixed = __float2ll_rn(amp * 4294967296.0f);
+      int bin = -1;
+      for (int k = 0; k < vp.n_cones; ++k)
+        if (vp.rims[k] < an && an < vp.rims[k + 1]) bin = k * vp.n_types + ti;
 #pragma unroll
-        for (int b = 0; b < NB; ++b) acc[b] += (b == bin) ? fixed : 0;
-      }
+      for (int b = 0; b < NB; ++b) acc[b] += (b == bin) ? fixed : 0;
+    }
+    skip = jj - je;
+  }
+#pragma unroll
+  for (int off = G / 2; off > 0; off >>= 1) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)acc[b], off, 64);
+      const int32_t hi = __shfl_xor((int)(acc[b] >> 32), off, 64);
+      acc[b] += (int64_t)(((uint64_t)(uint32_t)hi << 32) | lo);
     }
   }
-  float* o = out + (size_t)t * nb;
+  if (sub != 0) return;
+  float* o = out + (size_t)grp * nb;
 #pragma unroll
   for (int k = 0; k < NB; ++k)
     if (k < nb) o[k] = (float)acc[k] * 2.3283064365386963e-10f;
@@ -448,10 +470,7 @@ constexpr size_t kMaxLds = 160 * 1024;
 
 size_t global_lds_bytes(int lx, int ly) { return (16 + (size_t)(1 << (lx + ly)) + 1) * 4; }
 
-size_t build_lds_bytes(int n, int lx, int ly) {
-  const int ncell = 1 << (lx + ly);
-  return (16 + 16 + 68 + 68 + (size_t)((ncell + 1 + 3) & ~3) + 3 * (size_t)n) * 4;
-}
+size_t build_lds_bytes(int n, int lx, int ly) { return swarm::build_lds_words(n, lx, ly) * 4; }
 
 size_t check_lds_bytes(int lx, int ly) {
   return (16 + 16 + 1024 + (size_t)(1 << (lx + ly)) + 1) * 4;
@@ -489,8 +508,13 @@ int launch_window(swarm_engine* e, int n_steps) {
                      e->sc, e->lxb, e->lyb);
   HIP_TRY(hipGetLastError());
   const long waves = (long)e->n_envs * e->sc.wmax;
-  hipLaunchKernelGGL(swarm::k_cluster_run, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
-                     e->stream, e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step);
+  const dim3 run_grid((unsigned)((waves + 3) / 4)), run_block(256);
+  if (e->params.n_species > 1)
+    hipLaunchKernelGGL(swarm::k_cluster_run<true>, run_grid, run_block, 0, e->stream,
+                       e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step);
+  else
+    hipLaunchKernelGGL(swarm::k_cluster_run<false>, run_grid, run_block, 0, e->stream,
+                       e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(swarm::k_check, dim3(e->n_envs), dim3(1024),
                      check_lds_bytes(e->lxg, e->lyg), e->stream, e->d_derived, e->st, e->sc,
@@ -624,13 +648,16 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   }
   cell_grid(*params, n_particles, e->derived.rc_max, &e->lxg, &e->lyg);
   cell_grid(*params, n_particles, e->derived.rc_max + kSkin, &e->lxb, &e->lyb);
-  if (check_lds_bytes(e->lxg, e->lyg) > kMaxLds) {
+  // static LDS of the kernels: pair tables (k_global, k_check, k_cluster_run)
+  // and the link table of k_cluster_build
+  constexpr size_t kStaticLds = sizeof(swarm::PairTables);
+  if (check_lds_bytes(e->lxg, e->lyg) + kStaticLds > kMaxLds) {
     delete e;
     return fail(SWARM_ECAPACITY, "env cell grid does not fit the LDS of one workgroup");
   }
   // the cluster path needs the build workgroup's LDS and a non-degenerate
   // build grid; otherwise every window runs on the global path
-  e->cluster_path = build_lds_bytes(n_particles, e->lxb, e->lyb) <= kMaxLds &&
+  e->cluster_path = build_lds_bytes(n_particles, e->lxb, e->lyb) + kStaticLds <= kMaxLds &&
                     (1 << e->lxb) >= 3 && (1 << e->lyb) >= 3;
   const size_t M = (size_t)n_envs * n_particles;
   int rc = SWARM_OK;
@@ -892,20 +919,31 @@ int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const 
                        lx, ly, radii, types, e->d_start, e->vs);
     HIP_TRY(hipGetLastError());
   }
-  const int total = n_agents * e->n_envs;
+  const long total = (long)n_agents * e->n_envs;
   const int nb = vp->n_cones * vp->n_types;
-  const dim3 grid((total + 255) / 256), block(256);
-#define SWARM_VISION(NBV)                                                                   \
-  hipLaunchKernelGGL(k_vision<NBV>, grid, block, 0, e->stream, e->st, e->d_derived, *vp, lx, ly, \
-                     e->d_start, e->vs, agent_idx, n_agents, out, e->n_envs)
-  if (nb <= 4)
-    SWARM_VISION(4);
-  else if (nb <= 8)
-    SWARM_VISION(8);
-  else if (nb <= 16)
-    SWARM_VISION(16);
-  else
-    SWARM_VISION(32);
+  // lanes per agent: enough threads to give every SIMD a few waves
+  const int G = total >= (1L << 18) ? 1 : total >= (1L << 16) ? 4 : 16;
+  const dim3 grid((unsigned)((total * G + 255) / 256)), block(256);
+#define SWARM_VISION(NBV, GV)                                                              \
+  hipLaunchKernelGGL((k_vision<NBV, GV>), grid, block, 0, e->stream, e->st, e->d_derived, *vp, \
+                     lx, ly, e->d_start, e->vs, agent_idx, n_agents, out, e->n_envs)
+#define SWARM_VISION_G(NBV) \
+  if (G == 1)               \
+    SWARM_VISION(NBV, 1);   \
+  else if (G == 4)          \
+    SWARM_VISION(NBV, 4);   \
+  else                      \
+    SWARM_VISION(NBV, 16)
+  if (nb <= 4) {
+    SWARM_VISION_G(4);
+  } else if (nb <= 8) {
+    SWARM_VISION_G(8);
+  } else if (nb <= 16) {
+    SWARM_VISION_G(16);
+  } else {
+    SWARM_VISION_G(32);
+  }
+#undef SWARM_VISION_G
 #undef SWARM_VISION
   HIP_TRY(hipGetLastError());
   return SWARM_OK;

@@ -205,8 +205,8 @@ __device__ __forceinline__ void bd_step(const PConst& c, PState& p, int64_t ax, 
                                         float* vx, float* vy, float* w) {
   float sn, cs;
   sincos_turn(p.an, &sn, &cs);
-  float fx = (float)ax * 5.9604644775390625e-08f;
-  float fy = (float)ay * 5.9604644775390625e-08f;
+  float fx = i64_to_f32(ax) * 5.9604644775390625e-08f;
+  float fy = i64_to_f32(ay) * 5.9604644775390625e-08f;
   fx = fx + fex;
   fy = fy + fey;
   fx = fx + fs * cs;
@@ -215,8 +215,8 @@ __device__ __forceinline__ void bd_step(const PConst& c, PState& p, int64_t ax, 
   float dy = fy * c.mob_dt;
   float dth = tz * c.rot_dt;
   if (c.noisy) {
-    float g[4];
-    normals4(k0, k1, id, step, 0u, g);
+    float g[3];
+    normals3(k0, k1, id, step, 0u, g);
     dx = dx + c.sig_t * g[0];
     dy = dy + c.sig_t * g[1];
     dth = dth + c.sig_r * g[2];
@@ -228,8 +228,8 @@ __device__ __forceinline__ void bd_step(const PConst& c, PState& p, int64_t ax, 
     float v0 = fx * c.inv_gt, v1 = fy * c.inv_gt;
     float om = tz * c.inv_gr;
     if (c.noisy) {
-      float g[4];
-      normals4(k0, k1, id, step, 1u, g);
+      float g[3];
+      normals3(k0, k1, id, step, 1u, g);
       v0 = v0 + c.sig_v * g[0];
       v1 = v1 + c.sig_v * g[1];
       om = om + c.sig_w * g[2];
@@ -246,8 +246,8 @@ __device__ __forceinline__ bool sd_step(const PConst& c, PState& p, int64_t ax, 
                                         float md) {
   float sn, cs;
   sincos_turn(p.an, &sn, &cs);
-  float fx = (float)ax * 5.9604644775390625e-08f;
-  float fy = (float)ay * 5.9604644775390625e-08f;
+  float fx = i64_to_f32(ax) * 5.9604644775390625e-08f;
+  float fy = i64_to_f32(ay) * 5.9604644775390625e-08f;
   fx = fx + fex;
   fy = fy + fey;
   fx = fx + fs * cs;
@@ -410,10 +410,18 @@ __device__ __forceinline__ void uf_union(int32_t* parent, int a, int b) {
   }
 }
 
+// LDS words of k_cluster_build: 168 fixed + cell counts + parent[N] + 3 N
+// (cell-sorted positions / ids, later cluster sizes, bases and slots).
+__host__ __device__ inline size_t build_lds_words(int n, int lx, int ly) {
+  const int ncell = 1 << (lx + ly);
+  return 16 + 16 + 68 + 68 + (size_t)((ncell + 1 + 3) & ~3) + 4 * (size_t)n;
+}
+
 __global__ __launch_bounds__(1024) void k_cluster_build(const Derived* __restrict__ d,
                                                         DevState st, Scratch sc, int lx,
                                                         int ly) {
   extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ float nb2[kMaxSpecies * kMaxSpecies];
   const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly);
@@ -422,17 +430,23 @@ __global__ __launch_bounds__(1024) void k_cluster_build(const Derived* __restric
   int32_t* classcnt = misc + 16;                           // 68
   int32_t* wavebase = classcnt + 68;                       // 68
   int32_t* cnt = wavebase + 68;                            // ncell + 1 (padded)
-  int32_t* parent = cnt + ((ncell + 1 + 3) & ~3);
-  int32_t* csz = parent + N;
-  int32_t* cbase = csz + N;
+  int32_t* parent = cnt + ((ncell + 1 + 3) & ~3);          // N
+  // phase A (cell sort + neighbour search): sorted positions and ids
+  uint32_t* lqx = reinterpret_cast<uint32_t*>(parent + N);
+  uint32_t* lqy = lqx + N;
+  int32_t* lid = reinterpret_cast<int32_t*>(lqy + N);  // particle | species << 24
+  // phase B (clusters -> wave slots) reuses the same words
+  int32_t* csz = reinterpret_cast<int32_t*>(lqx);
+  int32_t* cbase = reinterpret_cast<int32_t*>(lqy);
+  int32_t* lslot = lid;
   const int S = sc.S;
 
+  for (int k = tid; k < kMaxSpecies * kMaxSpecies; k += T) nb2[k] = d->nb2[k];
   for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
   for (int k = tid; k < 68; k += T) classcnt[k] = 0;
   if (tid < 16) misc[tid] = 0;
   for (int i = tid; i < N; i += T) {
     parent[i] = i;
-    csz[i] = 0;
     const size_t gi = base + i;
     sc.bq[gi] = st.q[gi];
     sc.bq[M + gi] = st.q[M + gi];
@@ -443,7 +457,7 @@ __global__ __launch_bounds__(1024) void k_cluster_build(const Derived* __restric
   for (int k = tid; k < S; k += T) sc.perm[(size_t)e * S + k] = -1;
   __syncthreads();
 
-  // cell sort (side >= rc_max + skin)
+  // cell sort into LDS (side >= rc_max + skin)
   for (int i = tid; i < N; i += T)
     atomicAdd(&cnt[cell_index(st.q[base + i], st.q[M + base + i], lx, ly)], 1);
   __syncthreads();
@@ -452,9 +466,9 @@ __global__ __launch_bounds__(1024) void k_cluster_build(const Derived* __restric
   for (int i = tid; i < N; i += T) {
     const uint32_t qx = st.q[base + i], qy = st.q[M + base + i];
     const int pos = atomicAdd(&cnt[cell_index(qx, qy, lx, ly)], 1);
-    sc.sqx[base + pos] = qx;
-    sc.sqy[base + pos] = qy;
-    sc.sidx[base + pos] = i;
+    lqx[pos] = qx;
+    lqy[pos] = qy;
+    lid[pos] = i | ((int32_t)st.species[i] << 24);
   }
   __syncthreads();
 
@@ -465,9 +479,10 @@ __global__ __launch_bounds__(1024) void k_cluster_build(const Derived* __restric
   const float sx0 = d->sx[0], sx1 = d->sx[1];
   for (int i = tid; i < N; i += T) {
     const uint32_t qx = st.q[base + i], qy = st.q[M + base + i];
-    const int si = st.species[i];
+    const float* nb2_row = nb2 + (int)st.species[i] * kMaxSpecies;
     const int c0 = cell_index(qx, qy, lx, ly);
     const int cx = c0 & (ncx - 1), cy = c0 >> lx;
+    int32_t* out = sc.nbr_tmp + (base + i) * kNbMax;
     int nc = 0;
     for (int oy = loy; oy <= hiy; ++oy) {
       const int y = (cy + oy + ncy) & (ncy - 1);
@@ -476,13 +491,13 @@ __global__ __launch_bounds__(1024) void k_cluster_build(const Derived* __restric
         const int cc = (y << lx) | x;
         const int jb = cc ? cnt[cc - 1] : 0, je = cnt[cc];
         for (int jj = jb; jj < je; ++jj) {
-          const int j = sc.sidx[base + jj];
-          if (j == i) continue;
-          const float rx = (float)(int32_t)(sc.sqx[base + jj] - qx) * sx0;
-          const float ry = (float)(int32_t)(sc.sqy[base + jj] - qy) * sx1;
-          if (rx * rx + ry * ry < d->nb2[si * kMaxSpecies + st.species[j]]) {
+          const int packed = lid[jj];
+          const int j = packed & 0xffffff;
+          const float rx = (float)(int32_t)(lqx[jj] - qx) * sx0;
+          const float ry = (float)(int32_t)(lqy[jj] - qy) * sx1;
+          if (j != i && rx * rx + ry * ry < nb2_row[packed >> 24]) {
             if (nc < kNbMax)
-              sc.nbr_tmp[(base + i) * kNbMax + nc] = j;
+              out[nc] = j;
             else
               misc[0] = 1;  // neighbour overflow -> global path for this env
             ++nc;
@@ -494,9 +509,12 @@ __global__ __launch_bounds__(1024) void k_cluster_build(const Derived* __restric
     sc.ncount[base + i] = nc < kNbMax ? nc : kNbMax;
   }
   __syncthreads();
-  for (int i = tid; i < N; i += T) parent[i] = uf_find(parent, i);
+  for (int i = tid; i < N; i += T) {
+    parent[i] = uf_find(parent, i);
+    csz[i] = 0;
+  }
   __syncthreads();
-  for (int i = tid; i < N; i += T) sc.slot_of[base + i] = atomicAdd(&csz[parent[i]], 1);
+  for (int i = tid; i < N; i += T) lslot[i] = atomicAdd(&csz[parent[i]], 1);
   __syncthreads();
   for (int i = tid; i < N; i += T) {
     if (parent[i] != i) continue;
@@ -538,27 +556,29 @@ __global__ __launch_bounds__(1024) void k_cluster_build(const Derived* __restric
   __syncthreads();
   for (int i = tid; i < N; i += T) {
     const int root = parent[i];
-    const int slot = cbase[root] + sc.slot_of[base + i];
+    const int slot = cbase[root] + lslot[i];
+    lslot[i] = slot;
     sc.slot_of[base + i] = slot;
     sc.perm[(size_t)e * S + slot] = i;
     sc.root[base + i] = root;
   }
   __syncthreads();
   for (int i = tid; i < N; i += T) {
-    const int slot = sc.slot_of[base + i];
+    const int slot = lslot[i];
     const int nc = sc.ncount[base + i];
+    const int32_t* nb = sc.nbr_tmp + (base + i) * kNbMax;
+    int32_t js[kNbMax];
+#pragma unroll
+    for (int k = 0; k < kNbMax; ++k) js[k] = k < nc ? nb[k] : i;
     uint32_t wds[4] = {(uint32_t)nc, 0u, 0u, 0u};
-    for (int k = 0; k < nc; ++k) {
-      const int j = sc.nbr_tmp[(base + i) * kNbMax + k];
-      const uint32_t lane = (uint32_t)(sc.slot_of[base + j] & 63);
+#pragma unroll
+    for (int k = 0; k < kNbMax; ++k) {
+      const uint32_t lane = k < nc ? (uint32_t)(lslot[js[k]] & 63) : 0u;
       const int b = k + 1;
       wds[b >> 2] |= lane << ((b & 3) * 8);
     }
-    uint32_t* out = sc.nbr + ((size_t)e * S + slot) * 4;
-    out[0] = wds[0];
-    out[1] = wds[1];
-    out[2] = wds[2];
-    out[3] = wds[3];
+    uint4* out = reinterpret_cast<uint4*>(sc.nbr + ((size_t)e * S + slot) * 4);
+    *out = make_uint4(wds[0], wds[1], wds[2], wds[3]);
   }
   if (tid == 0) {
     sc.env_waves[e] = misc[1];
@@ -571,6 +591,8 @@ __device__ __forceinline__ uint32_t nb_lane(const uint32_t (&w)[4], int b) {
   return (w[b >> 2] >> ((b & 3) * 8)) & 0xffu;
 }
 
+// kMulti = false: one species, so the pair constants are wave-uniform scalars.
+template <bool kMulti>
 __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__ d, DevState st,
                                                      Scratch sc, int n_envs, int n_steps,
                                                      const uint64_t* __restrict__ step_ctr) {
@@ -620,6 +642,7 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
   const PConst pc = load_pconst(d, si);
   const float* cut2_row = pt.cut2 + si * kMaxSpecies;
   const float* sig6_row = pt.sig6 + si * kMaxSpecies;
+  const float cut2_0 = d->cut2[0], sig6_0 = d->sig6[0];
   const uint32_t q0x = p.qx, q0y = p.qy;
   float dmax2 = 0.0f;
   float vx = 0.0f, vy = 0.0f, om = 0.0f;
@@ -631,11 +654,14 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
         const int src = k < cnt ? (int)nb_lane(nw, k + 1) : lane;
         const uint32_t oqx = (uint32_t)__shfl((int)p.qx, src, 64);
         const uint32_t oqy = (uint32_t)__shfl((int)p.qy, src, 64);
-        const int osp = __shfl(si, src, 64);
+        const int osp = kMulti ? __shfl(si, src, 64) : 0;
         if (k < cnt) {
           const float rx = (float)(int32_t)(oqx - p.qx) * sx0;
           const float ry = (float)(int32_t)(oqy - p.qy) * sx1;
-          pair_force(cut2_row[osp], sig6_row[osp], eps24, rx, ry, ax, ay);
+          if (kMulti)
+            pair_force(cut2_row[osp], sig6_row[osp], eps24, rx, ry, ax, ay);
+          else
+            pair_force(cut2_0, sig6_0, eps24, rx, ry, ax, ay);
         }
       }
     }

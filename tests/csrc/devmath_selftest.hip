@@ -16,9 +16,12 @@ __global__ void k_math(const float* x, const uint32_t* a, int n, float* o_sqrt, 
   swarm::sincos_turn(a[i], &s, &c);
   o_sin[i] = s;
   o_cos[i] = c;
-  float g[4];
-  swarm::normals4(42u, 0u, (uint32_t)i, 7ull, 0u, g);
-  for (int k = 0; k < 4; ++k) o_g[4 * i + k] = g[k];
+  float g[3];
+  swarm::normals3(42u, 0u, (uint32_t)i, 7ull, 0u, g);
+  for (int k = 0; k < 3; ++k) o_g[3 * i + k] = g[k];
+  // branchless sqrt on the Box-Muller radius range [1.19e-7, 33.3]
+  const float xp = 1.1920929e-07f + x[i] * 40.0f;
+  o_g[3 * (size_t)n + i] = swarm::sqrt_pos(xp > 0.0f ? xp : 1.0f);
 }
 
 extern "C" int devmath_selftest(const float* x, const uint32_t* a, int n, float* out) {

@@ -43,8 +43,12 @@ def test_device_math_bit_exact(oracle_mod):
     out = _run(x, a)
     o_sqrt, o_log, o_acos = out[:n], out[n:2 * n], out[2 * n:3 * n]
     o_sin, o_cos = out[3 * n:4 * n], out[4 * n:5 * n]
-    g = out[5 * n:].reshape(n, 4)
+    g = out[5 * n:8 * n].reshape(n, 3)
+    o_sqrtp = out[8 * n:]
     assert np.array_equal(o_sqrt, np.sqrt(x))  # numpy sqrt is IEEE correctly rounded
+    xp = (np.float32(1.1920929e-07) + x * np.float32(40.0)).astype(np.float32)
+    bm = xp < np.float32(41.0)  # the radius range sqrt_pos serves (x < 1 part)
+    assert np.array_equal(o_sqrtp[bm], np.sqrt(xp[bm]))
     sub = np.arange(0, n, 97)
     for i in sub[:3000]:
         if x[i] < 1.0:
@@ -52,5 +56,5 @@ def test_device_math_bit_exact(oracle_mod):
             assert o_acos[i] == np.float32(oracle_mod.acosf(float(x[i] * np.float32(2) - np.float32(1)))), i
         s, c = oracle_mod.sincos_turn(int(a[i]))
         assert o_sin[i] == np.float32(s) and o_cos[i] == np.float32(c), i
-        assert np.array_equal(g[i], oracle_mod.normals4(42, 0, int(i), 7, 0)), i
+        assert np.array_equal(g[i], oracle_mod.normals3(42, 0, int(i), 7, 0)), i
     assert math.isfinite(float(o_log[0]))

@@ -53,6 +53,11 @@ def run(E, kT, eps, label, reps=20, force=10.0):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1:  # e.g. "64,1" -> E=64 with noise; "256,0" -> kT=0
+        for spec in sys.argv[1:]:
+            E, noisy = (int(x) for x in spec.split(","))
+            run(E, 1.0239 if noisy else 0.0, 1.0239, f"kT{'>' if noisy else '='}0, WCA")
+        sys.exit(0)
     for E in [1, 64, 256]:
         run(E, 1.0239, 1.0239, "kT>0, WCA")
         run(E, 0.0, 1.0239, "kT=0, WCA")
