@@ -26,7 +26,10 @@ SWARM_ESTATE = 2
 SWARM_EDEVICE = 3
 SWARM_ECAPACITY = 4
 
-_LIB_PATH = pathlib.Path(__file__).resolve().parent / "libswarmrl_amd.so"
+# SWARMRL_AMD_LIB selects another build of the same library (e.g. the
+# profiling variants tools/build_variants.sh makes); default: in-tree build.
+_LIB_PATH = pathlib.Path(os.environ.get(
+    "SWARMRL_AMD_LIB", pathlib.Path(__file__).resolve().parent / "libswarmrl_amd.so"))
 
 
 class SwarmParams(ctypes.Structure):
@@ -97,6 +100,7 @@ _SIGNATURES = {
         [_P, ctypes.c_int32, ctypes.c_double, ctypes.c_double],
     ),
     "swarm_engine_integrate": (ctypes.c_int, [_P, ctypes.c_int32]),
+    "swarm_engine_prebuild": (ctypes.c_int, [_P, _P, ctypes.c_int32]),
     "swarm_engine_step_count": (ctypes.c_int64, [_P]),
     "swarm_engine_window_stats": (ctypes.c_int, [_P, _P, _P]),
     "swarm_engine_device_views": (ctypes.c_int, [_P, ctypes.POINTER(SwarmDeviceViews)]),

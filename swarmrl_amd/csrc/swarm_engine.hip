@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -448,9 +449,16 @@ struct swarm_engine {
   int lxb = 0, lyb = 0;  // cluster-build grid: cell side >= rc_max + skin
   bool cluster_path = false;
   VisionSorted vs{};
+  // latency-bound windows read their normals from a table (k_noise)
+  bool noise_table = false;
+  float* d_noise = nullptr;
+  // swarm_engine_prebuild: the next window's build (and noise table) were
+  // launched ahead on another stream from the current positions
+  bool prebuilt = false;
+  int prebuilt_noise_steps = 0;
   float* own_f_swim = nullptr;
   float* own_torque_z = nullptr;
-  void* allocs[48] = {};
+  void* allocs[64] = {};
   int n_allocs = 0;
 };
 
@@ -501,20 +509,53 @@ int launch_global(swarm_engine* e, int n_steps, int sd_mode, float g, float md) 
   return SWARM_OK;
 }
 
-// One integration window: cluster build -> cluster run -> check/fallback.
-int launch_window(swarm_engine* e, int n_steps) {
+// Cluster build (+ noise table for n_noise sub-steps) of the next window.
+int launch_build(swarm_engine* e, hipStream_t stream, int n_noise) {
   hipLaunchKernelGGL(swarm::k_cluster_build, dim3(e->n_envs), dim3(1024),
-                     build_lds_bytes(e->n, e->lxb, e->lyb), e->stream, e->d_derived, e->st,
-                     e->sc, e->lxb, e->lyb);
+                     build_lds_bytes(e->n, e->lxb, e->lyb), stream, e->d_derived, e->st, e->sc,
+                     e->lxb, e->lyb);
   HIP_TRY(hipGetLastError());
+  if (e->noise_table && n_noise > 0) {
+    const long ts = (long)e->n_envs * e->sc.S;
+    hipLaunchKernelGGL(swarm::k_noise, dim3((unsigned)((ts + 255) / 256), (unsigned)n_noise),
+                       dim3(256), 0, stream, e->d_derived, e->sc, e->n_envs, e->d_step,
+                       e->d_noise);
+    HIP_TRY(hipGetLastError());
+  }
+  return SWARM_OK;
+}
+
+// One integration window: cluster build -> cluster run -> check/fallback.
+// use_prebuilt: the build (and noise for prebuilt_noise_steps) ran already.
+int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt) {
+  if (!use_prebuilt) {
+    const int rc = launch_build(e, e->stream, n_steps);
+    if (rc) return rc;
+  } else if (e->noise_table && n_steps > e->prebuilt_noise_steps) {
+    const long ts = (long)e->n_envs * e->sc.S;
+    hipLaunchKernelGGL(swarm::k_noise, dim3((unsigned)((ts + 255) / 256), (unsigned)n_steps),
+                       dim3(256), 0, e->stream, e->d_derived, e->sc, e->n_envs, e->d_step,
+                       e->d_noise);
+    HIP_TRY(hipGetLastError());
+  }
   const long waves = (long)e->n_envs * e->sc.wmax;
   const dim3 run_grid((unsigned)((waves + 3) / 4)), run_block(256);
-  if (e->params.n_species > 1)
-    hipLaunchKernelGGL(swarm::k_cluster_run<true>, run_grid, run_block, 0, e->stream,
-                       e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step);
-  else
-    hipLaunchKernelGGL(swarm::k_cluster_run<false>, run_grid, run_block, 0, e->stream,
-                       e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step);
+#define SWARM_RUN(MULTI, TABLE)                                                              \
+  hipLaunchKernelGGL((swarm::k_cluster_run<MULTI, TABLE>), run_grid, run_block, 0, e->stream, \
+                     e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise)
+  const bool multi = e->params.n_species > 1;
+  if (e->noise_table) {
+    if (multi)
+      SWARM_RUN(true, true);
+    else
+      SWARM_RUN(false, true);
+  } else {
+    if (multi)
+      SWARM_RUN(true, false);
+    else
+      SWARM_RUN(false, false);
+  }
+#undef SWARM_RUN
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(swarm::k_check, dim3(e->n_envs), dim3(1024),
                      check_lds_bytes(e->lxg, e->lyg), e->stream, e->d_derived, e->st, e->sc,
@@ -524,10 +565,13 @@ int launch_window(swarm_engine* e, int n_steps) {
 }
 
 int run_bd(swarm_engine* e, int n_steps) {
+  bool pre = e->prebuilt;
+  e->prebuilt = false;
   while (n_steps > 0) {
     const int w = std::min(n_steps, swarm::kMaxWindow);
-    const int rc = e->cluster_path ? launch_window(e, w) : launch_global(e, w, 0, 0.0f, 0.0f);
+    const int rc = e->cluster_path ? launch_window(e, w, pre) : launch_global(e, w, 0, 0.0f, 0.0f);
     if (rc) return rc;
+    pre = false;
     n_steps -= w;
   }
   return SWARM_OK;
@@ -697,9 +741,21 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->sc.disp, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.env_waves, (size_t)n_envs);
   rc = rc ? rc : dev_alloc(e, &e->sc.fallback, (size_t)n_envs);
-  e->vs.qx = e->sc.sqx;  // the observables run between integration windows
-  e->vs.qy = e->sc.sqy;
-  e->vs.idx = e->sc.sidx;
+  rc = rc ? rc : dev_alloc(e, &e->vs.qx, M);
+  rc = rc ? rc : dev_alloc(e, &e->vs.qy, M);
+  rc = rc ? rc : dev_alloc(e, &e->vs.idx, M);
+  // noise table for latency-bound windows: few envs fill few SIMDs, so the
+  // normals are better produced chip-wide ahead of the run.  Override with
+  // SWARMRL_AMD_NOISE_TABLE=0|1.
+  {
+    const char* ov = std::getenv("SWARMRL_AMD_NOISE_TABLE");
+    bool want = (long)n_envs * n_particles <= 32768;
+    if (ov && ov[0] == '0') want = false;
+    if (ov && ov[0] == '1') want = true;
+    e->noise_table = want && e->derived.noisy && e->cluster_path;
+    if (e->noise_table)
+      rc = rc ? rc : dev_alloc(e, &e->d_noise, (size_t)swarm::kMaxWindow * 3 * n_envs * S);
+  }
   rc = rc ? rc : dev_alloc(e, &e->vs.ix, M);
   rc = rc ? rc : dev_alloc(e, &e->vs.iy, M);
   rc = rc ? rc : dev_alloc(e, &e->vs.tslot, M);
@@ -741,6 +797,7 @@ int swarm_engine_set_stream(swarm_engine_t* e, void* stream) {
 
 int swarm_engine_upload_raw(swarm_engine_t* e, const uint32_t* q, const int32_t* img,
                             const uint32_t* ang) {
+  if (e) e->prebuilt = false;
   if (!e || !q || !img || !ang) return fail(SWARM_EINVAL, "null argument");
   const size_t M = (size_t)e->st.m;
   HIP_TRY(hipMemcpyAsync(e->st.q, q, 3 * M * sizeof(uint32_t), hipMemcpyHostToDevice, e->stream));
@@ -849,6 +906,7 @@ int swarm_engine_set_directors(swarm_engine_t* e, const double* dir, const uint8
 
 int swarm_engine_remove_overlap(swarm_engine_t* e, int32_t n_steps, double gamma, double max_disp) {
   if (!e) return fail(SWARM_EINVAL, "null engine");
+  e->prebuilt = false;
   if (n_steps <= 0) return SWARM_OK;
   return launch_global(e, n_steps, 1, (float)gamma, (float)max_disp);
 }
@@ -858,6 +916,19 @@ int swarm_engine_integrate(swarm_engine_t* e, int32_t n_steps) {
   if (n_steps < 0) return fail(SWARM_EINVAL, "n_steps must be >= 0");
   if (n_steps == 0) return SWARM_OK;
   return run_bd(e, n_steps);
+}
+
+int swarm_engine_prebuild(swarm_engine_t* e, void* stream, int32_t n_steps_hint) {
+  if (!e) return fail(SWARM_EINVAL, "null engine");
+  if (n_steps_hint < 0) return fail(SWARM_EINVAL, "n_steps_hint must be >= 0");
+  if (!e->cluster_path) return SWARM_OK;  // the global path has no build step
+  const int n_noise = std::min<int>(n_steps_hint, swarm::kMaxWindow);
+  const int rc = launch_build(e, stream ? reinterpret_cast<hipStream_t>(stream) : e->stream,
+                              n_noise);
+  if (rc) return rc;
+  e->prebuilt = true;
+  e->prebuilt_noise_steps = e->noise_table ? n_noise : 0;
+  return SWARM_OK;
 }
 
 int swarm_engine_window_stats(swarm_engine_t* e, int32_t* fallback, int32_t* waves) {

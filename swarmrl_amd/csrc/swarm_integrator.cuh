@@ -7,15 +7,19 @@
 //                    neighbour lists, union-find connected components
 //                    ("clusters") of the rc+skin graph, and a packing of the
 //                    clusters into 64-lane wave slots that never straddle a
-//                    wave.  Also snapshots the window-start state.
+//                    wave.  Depends on positions only, so it may run ahead
+//                    (swarm_engine_prebuild) while the slice's actions are
+//                    being computed.
 //   k_cluster_run    one wave per 64 slots, one lane per particle: all
 //                    sub-steps of the window with no block or grid barrier;
 //                    neighbour positions move lane-to-lane (ds_bpermute).
-//                    Tracks every particle's maximum displacement D.
+//                    Snapshots the window-start state and tracks every
+//                    particle's maximum displacement D.
 //   k_check          one workgroup per env: exact validity test of the
-//                    decomposition (no pair of different clusters can have
-//                    come within the WCA cutoff: d0 >= rc + D_i + D_j for all
-//                    such pairs), and, if it failed (or the build flagged a
+//                    decomposition (no pair that is not a listed neighbour
+//                    pair can have come within the WCA cutoff:
+//                    d0 >= rc + D_i + D_j for every such pair with a mover,
+//                    D >= skin / 2), and, if it failed (or the build flagged a
 //                    cluster > 64 / a neighbour-list overflow), re-runs the
 //                    env from the snapshot with the global per-sub-step
 //                    algorithm.  Advances the device noise counter.
@@ -199,10 +203,13 @@ __device__ __forceinline__ void stage_pair_tables(const Derived* __restrict__ d,
 }
 
 // One Brownian-dynamics sub-step of one particle from its summed WCA force.
+// kTable: the step's three normals come precomputed in gt (k_noise).
+template <bool kTable = false>
 __device__ __forceinline__ void bd_step(const PConst& c, PState& p, int64_t ax, int64_t ay,
                                         float fs, float tz, float fex, float fey, uint32_t k0,
                                         uint32_t k1, uint32_t id, uint64_t step, bool last,
-                                        float* vx, float* vy, float* w) {
+                                        float* vx, float* vy, float* w,
+                                        const float* gt = nullptr) {
   float sn, cs;
   sincos_turn(p.an, &sn, &cs);
   float fx = i64_to_f32(ax) * 5.9604644775390625e-08f;
@@ -216,7 +223,13 @@ __device__ __forceinline__ void bd_step(const PConst& c, PState& p, int64_t ax, 
   float dth = tz * c.rot_dt;
   if (c.noisy) {
     float g[3];
-    normals3(k0, k1, id, step, 0u, g);
+    if (kTable) {
+      g[0] = gt[0];
+      g[1] = gt[1];
+      g[2] = gt[2];
+    } else {
+      normals3(k0, k1, id, step, 0u, g);
+    }
     dx = dx + c.sig_t * g[0];
     dy = dy + c.sig_t * g[1];
     dth = dth + c.sig_r * g[2];
@@ -445,15 +458,7 @@ __global__ __launch_bounds__(1024) void k_cluster_build(const Derived* __restric
   for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
   for (int k = tid; k < 68; k += T) classcnt[k] = 0;
   if (tid < 16) misc[tid] = 0;
-  for (int i = tid; i < N; i += T) {
-    parent[i] = i;
-    const size_t gi = base + i;
-    sc.bq[gi] = st.q[gi];
-    sc.bq[M + gi] = st.q[M + gi];
-    sc.bimg[gi] = st.img[gi];
-    sc.bimg[M + gi] = st.img[M + gi];
-    sc.bang[gi] = st.ang[gi];
-  }
+  for (int i = tid; i < N; i += T) parent[i] = i;
   for (int k = tid; k < S; k += T) sc.perm[(size_t)e * S + k] = -1;
   __syncthreads();
 
@@ -591,11 +596,34 @@ __device__ __forceinline__ uint32_t nb_lane(const uint32_t (&w)[4], int b) {
   return (w[b >> 2] >> ((b & 3) * 8)) & 0xffu;
 }
 
+// Noise table for latency-bound windows (few waves per SIMD): the normals of
+// every (sub-step, wave slot) computed by the whole chip ahead of the run,
+// table[(s * 3 + c) * (E * S) + e * S + slot].
+__global__ __launch_bounds__(256) void k_noise(const Derived* __restrict__ d, Scratch sc,
+                                               int n_envs, const uint64_t* __restrict__ step_ctr,
+                                               float* __restrict__ table) {
+  const long ts = (long)n_envs * sc.S;
+  const long gs = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gs >= ts) return;
+  const int e = (int)(gs / sc.S);
+  const int i = sc.perm[gs];
+  if (i < 0 || sc.fallback[e] != 0) return;
+  const int s = blockIdx.y;
+  float g[3];
+  normals3(d->key0, d->key1 ^ (uint32_t)e, (uint32_t)i, *step_ctr + (uint64_t)s, 0u, g);
+  float* o = table + (size_t)s * 3 * ts + gs;
+  o[0] = g[0];
+  o[ts] = g[1];
+  o[2 * ts] = g[2];
+}
+
 // kMulti = false: one species, so the pair constants are wave-uniform scalars.
-template <bool kMulti>
+// kTable: read the normals from k_noise's table (prefetched one step ahead).
+template <bool kMulti, bool kTable>
 __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__ d, DevState st,
                                                      Scratch sc, int n_envs, int n_steps,
-                                                     const uint64_t* __restrict__ step_ctr) {
+                                                     const uint64_t* __restrict__ step_ctr,
+                                                     const float* __restrict__ table) {
   __shared__ PairTables pt;
   stage_pair_tables(d, &pt);
   const int lane = threadIdx.x & 63;
@@ -630,6 +658,13 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
     nw[1] = nb[1];
     nw[2] = nb[2];
     nw[3] = nb[3];
+    // window-start snapshot for k_check's exact test and re-run (taken here,
+    // not by the build, so a build may run ahead of the slice's actions)
+    sc.bq[gi] = p.qx;
+    sc.bq[M + gi] = p.qy;
+    sc.bimg[gi] = p.ix;
+    sc.bimg[M + gi] = p.iy;
+    sc.bang[gi] = p.an;
   }
   const int cnt = (int)(nw[0] & 0xffu);
   int kmax = cnt;
@@ -646,8 +681,24 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
   const uint32_t q0x = p.qx, q0y = p.qy;
   float dmax2 = 0.0f;
   float vx = 0.0f, vy = 0.0f, om = 0.0f;
+  const long ts = (long)n_envs * sc.S;
+  const float* tcol = table + (size_t)e * sc.S + slot;
+  float gn[3] = {0.0f, 0.0f, 0.0f};
+  if (kTable && active) {
+    gn[0] = tcol[0];
+    gn[1] = tcol[ts];
+    gn[2] = tcol[2 * ts];
+  }
   for (int s = 0; s < n_steps; ++s) {
+    float gt[3] = {gn[0], gn[1], gn[2]};
+    if (kTable && active && s + 1 < n_steps) {
+      const float* nx = tcol + (size_t)(s + 1) * 3 * ts;
+      gn[0] = nx[0];
+      gn[1] = nx[ts];
+      gn[2] = nx[2 * ts];
+    }
     int64_t ax = 0, ay = 0;
+#ifndef SWARM_ABLATE_NO_PAIRS
 #pragma unroll
     for (int k = 0; k < kNbMax; ++k) {
       if (k < kmax) {  // wave-uniform
@@ -665,9 +716,18 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
         }
       }
     }
+#endif
+#ifdef SWARM_ABLATE_NO_BD
     if (active) {
-      bd_step(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
-              s == n_steps - 1, &vx, &vy, &om);
+      p.qx += (uint32_t)ax;
+      p.qy += (uint32_t)ay + gt[0];
+    }
+    if (false) {
+#else
+    if (active) {
+#endif
+      bd_step<kTable>(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i,
+                      step0 + (uint64_t)s, s == n_steps - 1, &vx, &vy, &om, gt);
       const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
       const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
       dmax2 = fmaxf(dmax2, ddx * ddx + ddy * ddy);
@@ -719,26 +779,39 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
     if (nm > kMaxMovers) {
       if (tid == 0) misc[1] = 1;
     } else if (nm > 0) {
-      // exact test of every (mover, other-cluster particle) pair at the
-      // window-start positions: d0 < rc + D_i + D_j could have interacted
+      // exact test of every (mover, non-neighbour) pair at the window-start
+      // positions: d0 < rc + D_i + D_j could have interacted without its
+      // force being computed.  Same-cluster pairs count too: a cluster links
+      // particles through chains, so two of its members need not be listed
+      // neighbours of each other.
       const float rc = d->rc_max_f;
       const float sx0 = d->sx[0], sx1 = d->sx[1];
       const long total = (long)nm * N;
       for (long t = tid; t < total; t += T) {
         const int m = movers[t / N];
         const int j = (int)(t % N);
-        if (sc.root[base + j] == sc.root[base + m]) continue;
+        if (j == m) continue;
         const float rx = (float)(int32_t)(sc.bq[base + j] - sc.bq[base + m]) * sx0;
         const float ry = (float)(int32_t)(sc.bq[M + base + j] - sc.bq[M + base + m]) * sx1;
         const float lim = rc + sc.disp[base + m] + sc.disp[base + j] + 1e-3f;
-        if (rx * rx + ry * ry < lim * lim) misc[1] = 1;
+        if (rx * rx + ry * ry < lim * lim) {
+          bool listed = false;
+          if (sc.root[base + j] == sc.root[base + m]) {
+            const int nc = sc.ncount[base + m];
+            const int32_t* nb = sc.nbr_tmp + (base + m) * kNbMax;
+            for (int k = 0; k < nc; ++k) listed |= nb[k] == j;
+          }
+          if (!listed) misc[1] = 1;
+        }
       }
     }
     __syncthreads();
   }
   const bool rerun = flagged_build || misc[1] != 0;
   if (rerun) {
-    for (int i = tid; i < N; i += T) {
+    // a flagged env was skipped by k_cluster_run: its state is the window
+    // start already; otherwise restore the snapshot k_cluster_run took
+    for (int i = tid; i < N && !flagged_build; i += T) {
       const size_t gi = base + i;
       st.q[gi] = sc.bq[gi];
       st.q[M + gi] = sc.bq[M + gi];

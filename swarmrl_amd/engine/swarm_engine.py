@@ -248,6 +248,11 @@ class SwarmEngine(Engine):
         self._host_cache = None
         self._view = None
         self._type_index_cache = {}
+        # device path: prepare each window's build on a side stream while
+        # the force model computes the slice's actions (see _prebuild)
+        self.overlap_build = True
+        self._side_stream = None
+        self._prebuild_pending = None
         self.traj_holder = None
         self.write_idx = 0
         self.slice_idx = 0
@@ -718,7 +723,25 @@ class SwarmEngine(Engine):
             self._set_new_directions(new_dir, mask)
 
     # ---------------------------------------------------------- integrate
+    def _prebuild(self, n_steps: int):
+        """
+        Fork the next window's position-only preparation (cluster build,
+        noise table) onto a side stream so it overlaps the observable and
+        policy kernels of manage_forces; _run joins it.  Positions cannot
+        change in between (espresso.py:1253-1306), see swarm_engine_prebuild.
+        """
+        main = torch.cuda.current_stream()
+        if self._side_stream is None:
+            self._side_stream = torch.cuda.Stream(device=main.device)
+        side = self._side_stream
+        side.wait_stream(main)
+        self._native.call("swarm_engine_prebuild", ctypes.c_void_p(side.cuda_stream), int(n_steps))
+        self._prebuild_pending = side
+
     def _run(self, n_steps: int):
+        if self._prebuild_pending is not None:
+            torch.cuda.current_stream().wait_stream(self._prebuild_pending)
+            self._prebuild_pending = None
         self._native.bind_stream()
         self._native.call("swarm_engine_integrate", int(n_steps))
         self.system.time += n_steps * self._time_step
@@ -752,6 +775,10 @@ class SwarmEngine(Engine):
 
             if self.step_idx == self.params.steps_per_slice * self.slice_idx:
                 self.slice_idx += 1
+                if device_path and self.overlap_build:
+                    self._prebuild(min(
+                        self.params.steps_per_write_interval * self.write_idx - self.step_idx,
+                        self.params.steps_per_slice * self.slice_idx - self.step_idx))
                 self.manage_forces(force_model)
 
             steps_to_next_write = (

@@ -77,6 +77,13 @@ class Harness:
         self.native.bind_stream()
         self.native.call("swarm_engine_integrate", int(n))
 
+    def prebuild(self, n_hint, stream=None):
+        """swarm_engine_prebuild on `stream` (a torch stream; default current)."""
+        import torch
+
+        st = stream if stream is not None else torch.cuda.current_stream()
+        self.native.call("swarm_engine_prebuild", ctypes.c_void_p(st.cuda_stream), int(n_hint))
+
     def sd(self, n, gamma=0.1, maxd=0.1):
         self.native.bind_stream()
         self.native.call("swarm_engine_remove_overlap", int(n), float(gamma), float(maxd))

@@ -26,8 +26,13 @@ def _eq(a, b):
         assert np.array_equal(a[k], b[k]), k
 
 
-def test_bd_parity_dilute_multi_chunk():
+@pytest.mark.parametrize("table", ["0", "1"])
+def test_bd_parity_dilute_multi_chunk(table, monkeypatch):
+    """Both noise paths: normals computed in the run kernel (table=0) and
+    read from the chip-wide k_noise table (table=1)."""
     from gpu_harness import Harness, random_state, species_list
+
+    monkeypatch.setenv("SWARMRL_AMD_NOISE_TABLE", table)
 
     rng = np.random.default_rng(1)
     box = [120.0, 120.0, 120.0]
@@ -203,8 +208,11 @@ def test_field_distance_parity():
         assert np.array_equal(hq_host[:, e], hists[e]["q"])
 
 
-def test_full_size_4096_slice_bit_exact():
-    """BASELINE workload size: 4096 colloids, 100 sub-steps, vs the oracle."""
+@pytest.mark.parametrize("table", ["0", "1"])
+def test_full_size_4096_slice_bit_exact(table, monkeypatch):
+    """BASELINE workload size: 4096 colloids, 100 sub-steps, vs the oracle,
+    with the in-kernel (table=0) and the precomputed (table=1) normals."""
+    monkeypatch.setenv("SWARMRL_AMD_NOISE_TABLE", table)
     from gpu_harness import Harness, species_list
 
     rng = np.random.default_rng(8)
@@ -281,3 +289,45 @@ def test_long_run_is_windowed_bit_exact():
     h.integrate(300)
     ref, _, _ = oracle.bd_run(h.op, st, sp, f, t, 300)
     _eq(h.download()[0], ref)
+
+
+@pytest.mark.parametrize("hint", [100, 37])
+def test_prebuild_on_side_stream_bit_exact(hint):
+    """swarm_engine_prebuild on a side stream, joined before integrate, gives
+    the oracle trajectory; a hint shorter than the window makes integrate top
+    up the noise table; an upload after a prebuild discards it."""
+    from gpu_harness import Harness, species_list
+
+    rng = np.random.default_rng(21)
+    n = 2048
+    L = 2 * np.sqrt(n / 0.1)
+    box = [L, L, L]
+    pos, dirs = _disc(rng, n, L)
+    st = oracle.state_from_positions(pos, dirs, box)
+    h = Harness(box, 1e-3, 1.0239, 1.0239, 5, species_list()[:1], np.zeros(n, int))
+    h.upload([st])
+    h.sd(300)
+    st, _ = oracle.sd_run(h.op, st, np.zeros(n), 300)
+    f = rng.choice([0.0, 10.0], n).astype(np.float32)
+    t = rng.choice([-10.0, 0.0, 10.0], n).astype(np.float32)
+    side = torch.cuda.Stream()
+    step = 0
+    for _ in range(3):
+        side.wait_stream(torch.cuda.current_stream())
+        h.prebuild(hint, side)
+        h.set_actions(f, t)
+        torch.cuda.current_stream().wait_stream(side)
+        h.integrate(100)
+        st, _, _ = oracle.bd_run(h.op, st, np.zeros(n), f, t, 100, step0=step)
+        step += 100
+        _eq(h.download()[0], st)
+    # prebuild from the current positions, then replace them: must not be used
+    h.prebuild(hint)
+    pos2, dirs2 = _disc(rng, n, L)
+    st2 = oracle.state_from_positions(pos2, dirs2, box)
+    h.upload([st2])
+    h.sd(300)  # steepest descent sees the swim forces / torques set above
+    st2, _ = oracle.sd_run(h.op, st2, np.zeros(n), 300, f_swim=f, torque_z=t)
+    h.integrate(100)
+    st2, _, _ = oracle.bd_run(h.op, st2, np.zeros(n), f, t, 100, step0=step)
+    _eq(h.download()[0], st2)

@@ -54,9 +54,16 @@ def run(E, kT, eps, label, reps=20, force=10.0):
 
 if __name__ == "__main__":
     if len(sys.argv) > 1:  # e.g. "64,1" -> E=64 with noise; "256,0" -> kT=0
-        for spec in sys.argv[1:]:
-            E, noisy = (int(x) for x in spec.split(","))
-            run(E, 1.0239 if noisy else 0.0, 1.0239, f"kT{'>' if noisy else '='}0, WCA")
+        import os
+        for spec in sys.argv[1:]:  # "E,noisy[,table]" with table 0/1 (default: auto)
+            parts = spec.split(",")
+            E, noisy = int(parts[0]), int(parts[1])
+            if len(parts) > 2:
+                os.environ["SWARMRL_AMD_NOISE_TABLE"] = parts[2]
+            else:
+                os.environ.pop("SWARMRL_AMD_NOISE_TABLE", None)
+            run(E, 1.0239 if noisy else 0.0, 1.0239,
+                f"kT{'>' if noisy else '='}0, WCA, table={parts[2] if len(parts) > 2 else 'auto'}")
         sys.exit(0)
     for E in [1, 64, 256]:
         run(E, 1.0239, 1.0239, "kT>0, WCA")
