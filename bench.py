@@ -33,14 +33,17 @@ BYTES_PER_PARTICLE_SUBSTEP = 40
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--colloids", type=int, default=4096)
-    ap.add_argument("--envs-per-gpu", type=int, default=1)
+    ap.add_argument("--envs-per-gpu", type=int, default=1,
+                    help="headline: one env (4096 colloids) per GPU, as BASELINE's north star")
+    ap.add_argument("--batched-envs", type=int, default=64,
+                    help="also report envs-per-GPU batching in 'batched' (0: off)")
     ap.add_argument("--episode-length", type=int, default=20)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-slices", type=int, default=12)
+    ap.add_argument("--cpu-sample-slices", type=int, default=100)
     ap.add_argument("--bd-reps", type=int, default=20)
     return ap.parse_args()
 
@@ -90,21 +93,50 @@ def build_workload(args, env_seed, device):
     return eng, ff, agent
 
 
-def time_bd_kernel(eng, reps):
-    """Average duration of the fused 100-sub-step BD kernel (HIP events on
-    the stream the kernel is launched on)."""
+def time_run_kernel(eng, reps):
+    """Average duration (ms) of k_cluster_run, the dominant kernel: HIP events
+    recorded by the engine around each launch on the stream it runs on
+    (swarm_engine_profile), over `reps` eager 100-sub-step windows."""
+    import ctypes
+
     import torch
 
-    stream = torch.cuda.current_stream()
-    start = torch.cuda.Event(enable_timing=True)
-    stop = torch.cuda.Event(enable_timing=True)
+    nat = eng._native
+    ms = ctypes.c_double()
+    cnt = ctypes.c_int32()
     eng._run(eng.params.steps_per_slice)
-    start.record(stream)
+    torch.cuda.synchronize()
+    nat.call("swarm_engine_profile", 1, ctypes.byref(ms), ctypes.byref(cnt))
     for _ in range(reps):
         eng._run(eng.params.steps_per_slice)
-    stop.record(stream)
-    stop.synchronize()
-    return start.elapsed_time(stop) / reps
+    nat.call("swarm_engine_profile", 0, ctypes.byref(ms), ctypes.byref(cnt))
+    if cnt.value == 0:  # global path only (no cluster windows): whole windows
+        start = torch.cuda.Event(enable_timing=True)
+        stop = torch.cuda.Event(enable_timing=True)
+        start.record()
+        for _ in range(reps):
+            eng._run(eng.params.steps_per_slice)
+        stop.record()
+        stop.synchronize()
+        return start.elapsed_time(stop) / reps, "k_global (100 sub-steps)"
+    return ms.value / cnt.value, "k_cluster_run (100 fused BD+WCA sub-steps)"
+
+
+def pmc_traffic(kernel_prefix, E, N):
+    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3
+    PMC summary (profiles/, separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE
+    x2 per MI355X_MICROARCH.md), when it was collected on this workload."""
+    path = os.path.join(ROOT, "profiles", "r1_traffic.json")
+    try:
+        with open(path) as f:
+            rows = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    for r in rows:
+        if r.get("kernel", "").startswith(kernel_prefix) and r.get("envs") == E and \
+                r.get("colloids") == N:
+            return float(r["bytes_per_launch"]), f"profiles/{r['source']}"
+    return None, None
 
 
 def cpu_baseline(args):
@@ -164,23 +196,17 @@ def cpu_baseline(args):
     }
 
 
-def main():
-    args = parse_args()
+def measure(args, E, rank, world, device):
+    """Build, capture and time one workload of E envs per GPU; returns the
+    timing and roofline numbers (all ranks)."""
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
-
     from swarmrl_amd.rollout import gather_trajectory
 
-    E = args.envs_per_gpu
-    eng, ff, agent = build_workload(args, 42 + rank * E, device)
+    args_e = argparse.Namespace(**vars(args))
+    args_e.envs_per_gpu = E
+    eng, ff, agent = build_workload(args_e, 42 + rank * E, device)
     eng.integrate(1, ff)  # setup, overlap removal, first slice (eager)
 
     def one_slice():
@@ -244,19 +270,65 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    bd_ms = time_bd_kernel(eng, args.bd_reps)
+    kernel_ms, kernel = time_run_kernel(eng, args.bd_reps)
     N = args.colloids
-    agent_steps = N * E * world * args.steps
-    value = agent_steps / elapsed
-    achieved = BYTES_PER_PARTICLE_SUBSTEP * N * eng.params.steps_per_slice * E / (bd_ms * 1e-3) / 1e9
+    sub = eng.params.steps_per_slice
+    bytes_per_launch = BYTES_PER_PARTICLE_SUBSTEP * N * sub * E
+    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic("k_cluster_run", E, N)
+    out = {
+        "E": E,
+        "value": N * E * world * args.steps / elapsed,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "hip_graph": episode_graph is not None,
+        "roofline": {
+            "bound": "hbm",
+            "kernel": kernel,
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel_ms": kernel_ms,
+            "bytes_per_launch": bytes_per_launch,
+            "algorithmic_bytes": f"{BYTES_PER_PARTICLE_SUBSTEP} B per colloid-sub-step "
+                                 f"(SURVEY 8d) x {N} colloids x {sub} sub-steps x {E} env(s)",
+        },
+    }
+    if traffic_src:
+        out["roofline"]["traffic_source"] = traffic_src
+    del eng, ff, agent, slice_graph, episode_graph
+    torch.cuda.synchronize()
+    return out
+
+
+def main():
+    args = parse_args()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+
+    E = args.envs_per_gpu
+    head = measure(args, E, rank, world, device)
+    batched = None
+    if args.batched_envs > 0 and args.batched_envs != E:
+        batched = measure(args, args.batched_envs, rank, world, device)
+    N = args.colloids
     line = {
         "metric": METRIC,
-        "value": value,
+        "value": head["value"],
         "unit": "agent-steps/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": head["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -266,25 +338,24 @@ def main():
             "workload": "4096-colloid WCA+vision-cone rollout",
             "colloids_per_env": N,
             "envs_per_gpu": E,
-            "substeps_per_slice": eng.params.steps_per_slice,
-            "episode_length": T,
+            "substeps_per_slice": 100,
+            "episode_length": args.episode_length,
             "policy": "MLP 3-128-(4+1), Gumbel sampling",
             "task": "GradientSensing (find centre)",
-            "parallelism": f"episode-parallel, {world} process(es), RCCL all-gather per episode",
-            "hip_graph": episode_graph is not None,
+            "parallelism": f"episode-parallel, {world} process(es), one env per GPU, "
+                           f"RCCL all-gather per episode",
+            "hip_graph": head["hip_graph"],
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": "k_bd_block (100 fused BD+WCA sub-steps)",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
-            "kernel_ms": bd_ms,
-            "bytes_per_launch": BYTES_PER_PARTICLE_SUBSTEP * N * eng.params.steps_per_slice * E,
-        },
+        "roofline": head["roofline"],
     }
+    if batched is not None:
+        line["batched"] = {
+            "envs_per_gpu": batched["E"],
+            "value": batched["value"],
+            "unit": "agent-steps/s",
+            "ms_per_step": batched["ms_per_step"],
+            "roofline": batched["roofline"],
+        }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:

@@ -172,12 +172,19 @@ int swarm_engine_prebuild(swarm_engine_t *e, void *stream, int32_t n_steps_hint)
 int swarm_engine_window_stats(swarm_engine_t *e, int32_t *fallback,
                               int32_t *waves);
 
+/* Kernel timing for measurement (bench.py roofline): returns the summed
+ * duration (ms) and count of the k_cluster_run launches recorded since the
+ * previous call (HIP events on the engine stream; waits for them), then
+ * enables (1) or disables (0) recording.  Not for use under graph capture. */
+int swarm_engine_profile(swarm_engine_t *e, int32_t enable, double *run_ms,
+                         int32_t *launches);
+
 /* Total number of BD sub-steps integrated so far (the noise counter). */
 int64_t swarm_engine_step_count(const swarm_engine_t *e);
 
 int swarm_engine_device_views(swarm_engine_t *e, swarm_device_views_t *v);
 
-/* Vision cones for n_agents agents (indices into [0,N), device int32),
+/* Vision cones for n_agents agents (distinct indices into [0,N), device int32),
  * radii[N] device fp32 (radius of the SEEN colloid by list position,
  * subdivided_vision_cones.py:199-203); out device fp32
  * [E][n_agents][n_cones][n_types].  Replaces

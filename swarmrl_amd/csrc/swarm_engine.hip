@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/swarmrl_amd.h"
@@ -39,14 +40,11 @@ using swarm::Scratch;
 using swarm::cell_index;
 using swarm::block_exclusive_scan;
 
+// Cell-sorted 32-byte record of one particle for the observables, read as
+// two 16-byte loads: {qx, qy, ix, iy}, {radius bits, particle, type slot, 0}.
 struct VisionSorted {
-  uint32_t* qx;
-  uint32_t* qy;
-  int32_t* ix;
-  int32_t* iy;
-  int32_t* tslot;
-  float* rad;
-  int32_t* idx;
+  uint4* rec;          // [E * N][2]
+  int32_t* agent_row;  // [N] row of a particle in the agent list, -1 if none
 };
 
 constexpr int kMaxSpecies = SWARM_MAX_SPECIES;
@@ -173,12 +171,14 @@ __global__ __launch_bounds__(1024) void k_grid_build(DevState st, int lx, int ly
 }
 
 // Vision grid: counting sort of every env into cells of side >= vision range,
-// writing cell-sorted SoA copies (position, image, detected-type slot, radius,
-// particle index) so a candidate cell is one contiguous run.
+// writing cell-sorted records so a candidate cell is one contiguous run; the
+// env-0 workgroup also inverts the agent list (agent_row).
 __global__ __launch_bounds__(1024) void k_vision_grid(DevState st, swarm_vision_params_t vp,
                                                       int lx, int ly,
                                                       const float* __restrict__ radii,
                                                       const int32_t* __restrict__ types,
+                                                      const int32_t* __restrict__ agents,
+                                                      int n_agents,
                                                       int32_t* __restrict__ start, VisionSorted vs) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
@@ -186,7 +186,11 @@ __global__ __launch_bounds__(1024) void k_vision_grid(DevState st, swarm_vision_
   int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
   int32_t* cnt = wave_sums + 16;
   for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
+  if (e == 0)
+    for (int i = tid; i < N; i += T) vs.agent_row[i] = -1;
   __syncthreads();
+  if (e == 0)
+    for (int a = tid; a < n_agents; a += T) vs.agent_row[agents[a]] = a;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   for (int i = tid; i < N; i += T)
     atomicAdd(&cnt[cell_index(st.q[base + i], st.q[M + base + i], lx, ly)], 1);
@@ -204,40 +208,40 @@ __global__ __launch_bounds__(1024) void k_vision_grid(DevState st, swarm_vision_
     int ti = -1;
     for (int tt = 0; tt < vp.n_types; ++tt)
       if (vp.detected_types[tt] == tj) ti = tt;
-    vs.qx[pos] = qx;
-    vs.qy[pos] = qy;
-    vs.ix[pos] = st.img[g];
-    vs.iy[pos] = st.img[M + g];
-    vs.tslot[pos] = ti;
-    vs.rad[pos] = radii[i];
-    vs.idx[pos] = i;
+    vs.rec[2 * pos] = make_uint4(qx, qy, (uint32_t)st.img[g], (uint32_t)st.img[M + g]);
+    vs.rec[2 * pos + 1] = make_uint4(__float_as_uint(radii[i]), (uint32_t)i, (uint32_t)ti, 0u);
   }
 }
 
 // ---------------------------------------------------------- vision cone
-// One group of G lanes per (env, agent): the candidates of the 3x3 cell
-// stencil form one flat index range that the G lanes split; each lane keeps
-// NB bins (>= n_cones * n_types) of 2^-32 fixed-point amplitude in
-// registers, and the group adds them with xor-shuffles.  Integer sums make
-// the result independent of G and of the visiting order.
+// One group of G lanes per cell-sorted particle (neighbouring groups share
+// candidate cells, so their record loads coalesce); groups of particles
+// that are not agents exit.  The candidates of the 3x3 cell stencil form one
+// flat index range that the G lanes split; each lane keeps NB bins
+// (>= n_cones * n_types) of 2^-32 fixed-point amplitude in registers, and
+// the group adds them with xor-shuffles.  Integer sums make the result
+// independent of G and of the visiting order.
 template <int NB, int G>
 __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __restrict__ d,
                                                 swarm_vision_params_t vp, int lx, int ly,
                                                 const int32_t* __restrict__ start, VisionSorted vs,
-                                                const int32_t* __restrict__ agents, int n_agents,
-                                                float* __restrict__ out, int n_envs) {
+                                                int n_agents, float* __restrict__ out,
+                                                int n_envs) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int grp = t / G, sub = t & (G - 1);
-  if (grp >= n_envs * n_agents) return;  // whole groups only (G divides 64)
-  const int e = grp / n_agents, ai = grp - e * n_agents;
   const int N = st.n;
-  const size_t M = (size_t)st.m, base = (size_t)e * N;
-  const int i = agents[ai];
-  const size_t gi = base + i;
-  const uint32_t qxi = st.q[gi], qyi = st.q[M + gi];
-  const int32_t ixi = st.img[gi], iyi = st.img[M + gi];
+  if (grp >= n_envs * N) return;  // whole groups only (G divides 64)
+  const int e = grp / N, ps = grp - e * N;
+  const size_t base = (size_t)e * N;
+  const uint4 own0 = vs.rec[2 * (base + ps)];
+  const uint4 own1 = vs.rec[2 * (base + ps) + 1];
+  const int i = (int)own1.y;
+  const int row = vs.agent_row[i];
+  if (row < 0) return;
+  const uint32_t qxi = own0.x, qyi = own0.y;
+  const int32_t ixi = (int32_t)own0.z, iyi = (int32_t)own0.w;
   float sn, cs;
-  swarm::sincos_turn(st.ang[gi], &sn, &cs);
+  swarm::sincos_turn(st.ang[base + i], &sn, &cs);
   const float nm = swarm::sqrt_rn(cs * cs + sn * sn);
   const float mx = cs / nm, my = sn / nm;
   const int nb = vp.n_cones * vp.n_types;
@@ -269,13 +273,11 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
     }
     int jj = jb + skip;
     for (; jj < je; jj += G) {
-      const size_t p = base + jj;
-      const int ti = vs.tslot[p];
-      if (ti < 0) continue;
-      const int64_t dqx = ((int64_t)(vs.ix[p] - ixi) * (int64_t)4294967296LL) +
-                          ((int64_t)vs.qx[p] - (int64_t)qxi);
-      const int64_t dqy = ((int64_t)(vs.iy[p] - iyi) * (int64_t)4294967296LL) +
-                          ((int64_t)vs.qy[p] - (int64_t)qyi);
+      const uint4 c0 = vs.rec[2 * (base + jj)];
+      const int64_t dqx = ((int64_t)((int32_t)c0.z - ixi) * (int64_t)4294967296LL) +
+                          ((int64_t)c0.x - (int64_t)qxi);
+      const int64_t dqy = ((int64_t)((int32_t)c0.w - iyi) * (int64_t)4294967296LL) +
+                          ((int64_t)c0.y - (int64_t)qyi);
       // unwrapped separations beyond half a box are never within range
       // (vision_range < L/2): skip them and convert the rest from int32,
       // whose conversion is a single exact-rounding instruction.
@@ -285,10 +287,12 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
       const float dx = (float)(int32_t)dqx * sx0, dy = (float)(int32_t)dqy * sx1;
       const float dist2 = dx * dx + dy * dy;
       if (!(dist2 < R2pad) || dist2 == 0.0f) continue;
-      if (vs.idx[p] == i) continue;
+      const uint4 c1 = vs.rec[2 * (base + jj) + 1];
+      const int ti = (int)c1.z;
+      if (ti < 0 || (int)c1.y == i) continue;
       const float dist = swarm::sqrt_rn(dist2);
       if (!(dist < R)) continue;
-      float amp = (2.0f * vs.rad[p]) / dist;
+      float amp = (2.0f * __uint_as_float(c1.x)) / dist;
       amp = fminf(1.0f, amp);
       const float ux = dx / dist, uy = dy / dist;
       float dot = ux * mx + uy * my;
@@ -315,7 +319,7 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
     }
   }
   if (sub != 0) return;
-  float* o = out + (size_t)grp * nb;
+  float* o = out + ((size_t)e * n_agents + row) * nb;
 #pragma unroll
   for (int k = 0; k < NB; ++k)
     if (k < nb) o[k] = (float)acc[k] * 2.3283064365386963e-10f;
@@ -456,6 +460,9 @@ struct swarm_engine {
   // launched ahead on another stream from the current positions
   bool prebuilt = false;
   int prebuilt_noise_steps = 0;
+  // swarm_engine_profile: HIP events around every k_cluster_run launch
+  bool profile = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
   float* own_f_swim = nullptr;
   float* own_torque_z = nullptr;
   void* allocs[64] = {};
@@ -544,6 +551,12 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt) {
   hipLaunchKernelGGL((swarm::k_cluster_run<MULTI, TABLE>), run_grid, run_block, 0, e->stream, \
                      e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise)
   const bool multi = e->params.n_species > 1;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  if (e->profile) {
+    HIP_TRY(hipEventCreate(&ev0));
+    HIP_TRY(hipEventCreate(&ev1));
+    HIP_TRY(hipEventRecord(ev0, e->stream));
+  }
   if (e->noise_table) {
     if (multi)
       SWARM_RUN(true, true);
@@ -557,6 +570,10 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt) {
   }
 #undef SWARM_RUN
   HIP_TRY(hipGetLastError());
+  if (e->profile) {
+    HIP_TRY(hipEventRecord(ev1, e->stream));
+    e->prof_events.emplace_back(ev0, ev1);
+  }
   hipLaunchKernelGGL(swarm::k_check, dim3(e->n_envs), dim3(1024),
                      check_lds_bytes(e->lxg, e->lyg), e->stream, e->d_derived, e->st, e->sc,
                      n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg);
@@ -741,9 +758,8 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->sc.disp, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.env_waves, (size_t)n_envs);
   rc = rc ? rc : dev_alloc(e, &e->sc.fallback, (size_t)n_envs);
-  rc = rc ? rc : dev_alloc(e, &e->vs.qx, M);
-  rc = rc ? rc : dev_alloc(e, &e->vs.qy, M);
-  rc = rc ? rc : dev_alloc(e, &e->vs.idx, M);
+  rc = rc ? rc : dev_alloc(e, &e->vs.rec, 2 * M);
+  rc = rc ? rc : dev_alloc(e, &e->vs.agent_row, (size_t)n_particles);
   // noise table for latency-bound windows: few envs fill few SIMDs, so the
   // normals are better produced chip-wide ahead of the run.  Override with
   // SWARMRL_AMD_NOISE_TABLE=0|1.
@@ -756,10 +772,6 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     if (e->noise_table)
       rc = rc ? rc : dev_alloc(e, &e->d_noise, (size_t)swarm::kMaxWindow * 3 * n_envs * S);
   }
-  rc = rc ? rc : dev_alloc(e, &e->vs.ix, M);
-  rc = rc ? rc : dev_alloc(e, &e->vs.iy, M);
-  rc = rc ? rc : dev_alloc(e, &e->vs.tslot, M);
-  rc = rc ? rc : dev_alloc(e, &e->vs.rad, M);
   set_lds_attributes();
   if (rc) {
     swarm_engine_destroy(e);
@@ -783,6 +795,10 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
 void swarm_engine_destroy(swarm_engine_t* e) {
   if (!e) return;
   (void)hipDeviceSynchronize();
+  for (auto& pr : e->prof_events) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
   for (int k = 0; k < e->n_allocs; ++k) (void)hipFree(e->allocs[k]);
   if (e->d_start) (void)hipFree(e->d_start);
   if (e->d_pairs) (void)hipFree(e->d_pairs);
@@ -918,6 +934,24 @@ int swarm_engine_integrate(swarm_engine_t* e, int32_t n_steps) {
   return run_bd(e, n_steps);
 }
 
+int swarm_engine_profile(swarm_engine_t* e, int32_t enable, double* run_ms, int32_t* launches) {
+  if (!e) return fail(SWARM_EINVAL, "null engine");
+  double total = 0.0;
+  for (auto& pr : e->prof_events) {
+    float ms = 0.0f;
+    HIP_TRY(hipEventSynchronize(pr.second));
+    HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+    total += ms;
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  if (run_ms) *run_ms = total;
+  if (launches) *launches = (int32_t)e->prof_events.size();
+  e->prof_events.clear();
+  e->profile = enable != 0;
+  return SWARM_OK;
+}
+
 int swarm_engine_prebuild(swarm_engine_t* e, void* stream, int32_t n_steps_hint) {
   if (!e) return fail(SWARM_EINVAL, "null engine");
   if (n_steps_hint < 0) return fail(SWARM_EINVAL, "n_steps_hint must be >= 0");
@@ -987,17 +1021,17 @@ int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const 
     const size_t lds = 16 * 4 + (size_t)(ncell + 1) * 4;
     if (lds > kMaxLds) return fail(SWARM_ECAPACITY, "observable cell grid too large");
     hipLaunchKernelGGL(k_vision_grid, dim3(e->n_envs), dim3(1024), lds, e->stream, e->st, *vp,
-                       lx, ly, radii, types, e->d_start, e->vs);
+                       lx, ly, radii, types, agent_idx, n_agents, e->d_start, e->vs);
     HIP_TRY(hipGetLastError());
   }
-  const long total = (long)n_agents * e->n_envs;
+  const long total = (long)e->n * e->n_envs;  // one group per sorted particle
   const int nb = vp->n_cones * vp->n_types;
   // lanes per agent: enough threads to give every SIMD a few waves
   const int G = total >= (1L << 18) ? 1 : total >= (1L << 16) ? 4 : 16;
   const dim3 grid((unsigned)((total * G + 255) / 256)), block(256);
 #define SWARM_VISION(NBV, GV)                                                              \
   hipLaunchKernelGGL((k_vision<NBV, GV>), grid, block, 0, e->stream, e->st, e->d_derived, *vp, \
-                     lx, ly, e->d_start, e->vs, agent_idx, n_agents, out, e->n_envs)
+                     lx, ly, e->d_start, e->vs, n_agents, out, e->n_envs)
 #define SWARM_VISION_G(NBV) \
   if (G == 1)               \
     SWARM_VISION(NBV, 1);   \

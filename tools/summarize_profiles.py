@@ -1,0 +1,65 @@
+"""
+Summarize a profiles/profile_round.sh run into committed files:
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --stats (copied)
+  profiles/<tag>_bench.json         the bench line of the traced run
+  profiles/<tag>_pmc_summary.csv    per-kernel, per-grid averages of FETCH_SIZE,
+                                    WRITE_SIZE, SQ_INSTS_VALU, SQ_WAVES
+  profiles/<tag>_traffic.json       per-launch HBM bytes of k_cluster_run by
+                                    env count (FETCH_SIZE x 2 + WRITE_SIZE,
+                                    MI355X_MICROARCH.md gfx950 correction)
+Usage: python tools/summarize_profiles.py <tag> [colloids]
+"""
+import collections
+import csv
+import re
+import json
+import os
+import shutil
+import sys
+
+tag = sys.argv[1]
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+S = 2 * N + 64 * 66  # wave slots per env (swarm_engine.hip)
+src = f"gpurun_out/prof_{tag}"
+dst = "profiles"
+shutil.copy(f"{src}/trace/run_kernel_stats.csv", f"{dst}/{tag}_kernel_stats.csv")
+for line in open(f"{src}/trace_bench.log"):
+    if line.startswith("{"):
+        with open(f"{dst}/{tag}_bench.json", "w") as f:
+            f.write(line)
+
+acc = collections.defaultdict(lambda: collections.defaultdict(list))
+for sub in ("fetch", "write", "valu"):
+    path = f"{src}/{sub}/run_counter_collection.csv"
+    if not os.path.exists(path):
+        continue
+    for r in csv.DictReader(open(path)):
+        name = re.sub(r"\(anonymous namespace\)::", "", r["Kernel_Name"])
+        name = re.sub(r"^void ", "", name).split("(")[0][:80]
+        key = (name, int(r["Grid_Size"]))
+        acc[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+names = ["FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "SQ_WAVES"]
+with open(f"{dst}/{tag}_pmc_summary.csv", "w", newline="") as f:
+    w = csv.writer(f)
+    w.writerow(["kernel", "grid_size", "dispatches"] + [f"mean_{n}" for n in names])
+    for (k, g), cs in sorted(acc.items()):
+        n = max(len(v) for v in cs.values())
+        w.writerow([k, g, n] + [f"{sum(cs[c]) / len(cs[c]):.1f}" if cs.get(c) else "" for c in names])
+
+traffic = []
+for (k, g), cs in acc.items():
+    if "k_cluster_run" not in k or not cs.get("FETCH_SIZE") or not cs.get("WRITE_SIZE"):
+        continue
+    E = round(g / S)
+    fetch_kb = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"])
+    write_kb = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"])
+    traffic.append({
+        "kernel": k, "envs": E, "colloids": N,
+        "fetch_size_kb": fetch_kb, "write_size_kb": write_kb,
+        # FETCH_SIZE/WRITE_SIZE are in KB; FETCH_SIZE reads half the bytes on gfx950
+        "bytes_per_launch": (2 * fetch_kb + write_kb) * 1024.0,
+        "source": f"{tag}_pmc_summary.csv",
+    })
+with open(f"{dst}/{tag}_traffic.json", "w") as f:
+    json.dump(traffic, f, indent=1)
+print(json.dumps(traffic, indent=1))
