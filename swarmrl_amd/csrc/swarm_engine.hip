@@ -740,7 +740,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->d_step, 1);
   rc = rc ? rc : dev_alloc(e, &e->d_arrive, 1);
   // integrator scratch
-  const int S = 2 * n_particles + 64 * 66;
+  const int S = swarm::slots_per_env(n_particles);
   e->sc.S = S;
   e->sc.wmax = S / 64;
   rc = rc ? rc : dev_alloc(e, &e->sc.sqx, M);
@@ -754,7 +754,8 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->sc.ncount, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.nbr_tmp, M * swarm::kNbMax);
   rc = rc ? rc : dev_alloc(e, &e->sc.perm, (size_t)n_envs * S);
-  rc = rc ? rc : dev_alloc(e, &e->sc.nbr, (size_t)n_envs * S * 4);
+  rc = rc ? rc : dev_alloc(e, &e->sc.pairs, (size_t)n_envs * (S / 64) * swarm::kPairsPerWave);
+  rc = rc ? rc : dev_alloc(e, &e->sc.wave_npairs, (size_t)n_envs * (S / 64));
   rc = rc ? rc : dev_alloc(e, &e->sc.disp, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.env_waves, (size_t)n_envs);
   rc = rc ? rc : dev_alloc(e, &e->sc.fallback, (size_t)n_envs);

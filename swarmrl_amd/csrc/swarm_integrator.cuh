@@ -40,6 +40,11 @@ namespace swarm {
 constexpr int kMaxSpecies = SWARM_MAX_SPECIES;
 constexpr int kNbMax = 15;        // neighbours per particle inside a window
 constexpr int kMaxWindow = 128;   // sub-steps per cluster window
+constexpr int kPairsPerWave = 256;  // neighbour pairs of one 64-lane wave (4 passes)
+
+// Wave slots per env: every cluster packs into one wave, worst case 2 N
+// slots plus per-size-class rounding.
+__host__ __device__ inline int slots_per_env(int n) { return 2 * n + 64 * 66; }
 constexpr float kAngInvScale = 683565275.57643158f;  // 2^32 / (2 pi)
 
 // fp32 constants derived from swarm_params_t (same derivation as the oracle).
@@ -88,7 +93,8 @@ struct Scratch {
   int32_t* ncount;    // [M] neighbour count
   int32_t* nbr_tmp;   // [M][kNbMax] neighbour particle indices
   int32_t* perm;      // [E][S] particle of a slot (-1: idle lane)
-  uint32_t* nbr;      // [E][S][4] packed: byte 0 count, bytes 1..15 lanes
+  uint32_t* pairs;    // [E][wmax][kPairsPerWave]: lane a | lane b << 6 | species pair << 12
+  int32_t* wave_npairs;  // [E][wmax]
   float* disp;        // [M] max displacement over the window
   int32_t* env_waves; // [E]
   int32_t* fallback;  // [E]
@@ -423,11 +429,14 @@ __device__ __forceinline__ void uf_union(int32_t* parent, int a, int b) {
   }
 }
 
-// LDS words of k_cluster_build: 168 fixed + cell counts + parent[N] + 3 N
-// (cell-sorted positions / ids, later cluster sizes, bases and slots).
+// LDS words of k_cluster_build: 168 fixed + per-wave pair counters + cell
+// counts + parent[N] + 3 N (cell-sorted positions / ids, later cluster
+// sizes, bases and slots).
 __host__ __device__ inline size_t build_lds_words(int n, int lx, int ly) {
   const int ncell = 1 << (lx + ly);
-  return 16 + 16 + 68 + 68 + (size_t)((ncell + 1 + 3) & ~3) + 4 * (size_t)n;
+  const int wmax = slots_per_env(n) / 64;
+  return 16 + 16 + 68 + 68 + (size_t)((wmax + 3) & ~3) + (size_t)((ncell + 1 + 3) & ~3) +
+         4 * (size_t)n;
 }
 
 __global__ __launch_bounds__(1024) void k_cluster_build(const Derived* __restrict__ d,
@@ -442,7 +451,9 @@ __global__ __launch_bounds__(1024) void k_cluster_build(const Derived* __restric
   int32_t* misc = wave_sums + 16;                          // 16
   int32_t* classcnt = misc + 16;                           // 68
   int32_t* wavebase = classcnt + 68;                       // 68
-  int32_t* cnt = wavebase + 68;                            // ncell + 1 (padded)
+  const int wmax = sc.wmax;
+  int32_t* wave_np = wavebase + 68;                        // wmax (padded)
+  int32_t* cnt = wave_np + ((wmax + 3) & ~3);              // ncell + 1 (padded)
   int32_t* parent = cnt + ((ncell + 1 + 3) & ~3);          // N
   // phase A (cell sort + neighbour search): sorted positions and ids
   uint32_t* lqx = reinterpret_cast<uint32_t*>(parent + N);
@@ -457,6 +468,7 @@ __global__ __launch_bounds__(1024) void k_cluster_build(const Derived* __restric
   for (int k = tid; k < kMaxSpecies * kMaxSpecies; k += T) nb2[k] = d->nb2[k];
   for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
   for (int k = tid; k < 68; k += T) classcnt[k] = 0;
+  for (int k = tid; k < wmax; k += T) wave_np[k] = 0;
   if (tid < 16) misc[tid] = 0;
   for (int i = tid; i < N; i += T) parent[i] = i;
   for (int k = tid; k < S; k += T) sc.perm[(size_t)e * S + k] = -1;
@@ -568,32 +580,42 @@ __global__ __launch_bounds__(1024) void k_cluster_build(const Derived* __restric
     sc.root[base + i] = root;
   }
   __syncthreads();
+  // neighbour pairs of every wave, each once (from its lower index); the two
+  // particles share a cluster and therefore a wave
   for (int i = tid; i < N; i += T) {
     const int slot = lslot[i];
+    const int wv = slot >> 6;
     const int nc = sc.ncount[base + i];
     const int32_t* nb = sc.nbr_tmp + (base + i) * kNbMax;
-    int32_t js[kNbMax];
-#pragma unroll
-    for (int k = 0; k < kNbMax; ++k) js[k] = k < nc ? nb[k] : i;
-    uint32_t wds[4] = {(uint32_t)nc, 0u, 0u, 0u};
-#pragma unroll
-    for (int k = 0; k < kNbMax; ++k) {
-      const uint32_t lane = k < nc ? (uint32_t)(lslot[js[k]] & 63) : 0u;
-      const int b = k + 1;
-      wds[b >> 2] |= lane << ((b & 3) * 8);
+    const int si = st.species[i];
+    uint32_t* pw = sc.pairs + ((size_t)e * wmax + wv) * kPairsPerWave;
+    for (int k = 0; k < nc; ++k) {
+      const int j = nb[k];
+      if (j < i) continue;
+      const int idx = atomicAdd(&wave_np[wv], 1);
+      if (idx < kPairsPerWave)
+        pw[idx] = (uint32_t)(slot & 63) | ((uint32_t)(lslot[j] & 63) << 6) |
+                  ((uint32_t)(si * kMaxSpecies + st.species[j]) << 12);
+      else
+        misc[2] = 1;  // pair overflow -> global path for this env
     }
-    uint4* out = reinterpret_cast<uint4*>(sc.nbr + ((size_t)e * S + slot) * 4);
-    *out = make_uint4(wds[0], wds[1], wds[2], wds[3]);
   }
+  __syncthreads();
+  for (int w = tid; w < misc[1]; w += T)
+    sc.wave_npairs[(size_t)e * wmax + w] = min(wave_np[w], kPairsPerWave);
   if (tid == 0) {
-    sc.env_waves[e] = misc[1];
-    sc.fallback[e] = 0;
+    sc.env_waves[e] = misc[2] ? 0 : misc[1];
+    sc.fallback[e] = misc[2] ? 1 : 0;
   }
 }
 
 // -------------------------------------------------------- cluster run
-__device__ __forceinline__ uint32_t nb_lane(const uint32_t (&w)[4], int b) {
-  return (w[b >> 2] >> ((b & 3) * 8)) & 0xffu;
+// Orders one wave's LDS accesses (DS operations of a wave execute in order;
+// this keeps the compiler from moving them across).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Noise table for latency-bound windows (few waves per SIMD): the normals of
@@ -625,8 +647,10 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
                                                      const uint64_t* __restrict__ step_ctr,
                                                      const float* __restrict__ table) {
   __shared__ PairTables pt;
+  __shared__ uint2 lpos[4][64];                  // positions of the block's 4 waves
+  __shared__ unsigned long long lacc[4][2][64];  // int64 force sums (x, y)
   stage_pair_tables(d, &pt);
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const int e = gw / sc.wmax;
   const int w = gw - e * sc.wmax;
@@ -640,7 +664,6 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
   PState p = {0u, 0u, 0u, 0, 0};
   int si = 0;
   float fs = 0.0f, tz = 0.0f, fex = 0.0f, fey = 0.0f;
-  uint32_t nw[4] = {0u, 0u, 0u, 0u};
   const size_t gi = base + (active ? i : 0);
   if (active) {
     p.qx = st.q[gi];
@@ -653,11 +676,6 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
     tz = st.torque_z[gi];
     fex = st.f_ext[gi];
     fey = st.f_ext[M + gi];
-    const uint32_t* nb = sc.nbr + ((size_t)e * sc.S + slot) * 4;
-    nw[0] = nb[0];
-    nw[1] = nb[1];
-    nw[2] = nb[2];
-    nw[3] = nb[3];
     // window-start snapshot for k_check's exact test and re-run (taken here,
     // not by the build, so a build may run ahead of the slice's actions)
     sc.bq[gi] = p.qx;
@@ -666,17 +684,21 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
     sc.bimg[M + gi] = p.iy;
     sc.bang[gi] = p.an;
   }
-  const int cnt = (int)(nw[0] & 0xffu);
-  int kmax = cnt;
+  // this wave's neighbour pairs: one per lane and pass (wave-uniform count)
+  const int np = sc.wave_npairs[(size_t)e * sc.wmax + w];
+  const int npass = (np + 63) >> 6;
+  const uint32_t* pw = sc.pairs + ((size_t)e * sc.wmax + w) * kPairsPerWave;
+  uint32_t pr[kPairsPerWave / 64];
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) kmax = max(kmax, __shfl_xor(kmax, off, 64));
+  for (int q = 0; q < kPairsPerWave / 64; ++q)
+    pr[q] = q * 64 + lane < np ? pw[q * 64 + lane] : 0xffffffffu;
+  lacc[wv][0][lane] = 0ull;
+  lacc[wv][1][lane] = 0ull;
   const uint64_t step0 = *step_ctr;
   const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
   const float sx0 = d->sx[0], sx1 = d->sx[1];
   const float eps24 = d->eps24;
   const PConst pc = load_pconst(d, si);
-  const float* cut2_row = pt.cut2 + si * kMaxSpecies;
-  const float* sig6_row = pt.sig6 + si * kMaxSpecies;
   const float cut2_0 = d->cut2[0], sig6_0 = d->sig6[0];
   const uint32_t q0x = p.qx, q0y = p.qy;
   float dmax2 = 0.0f;
@@ -699,22 +721,36 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
     }
     int64_t ax = 0, ay = 0;
 #ifndef SWARM_ABLATE_NO_PAIRS
+    if (npass > 0) {  // wave-uniform
+      lpos[wv][lane] = make_uint2(p.qx, p.qy);
+      wave_lds_sync();
 #pragma unroll
-    for (int k = 0; k < kNbMax; ++k) {
-      if (k < kmax) {  // wave-uniform
-        const int src = k < cnt ? (int)nb_lane(nw, k + 1) : lane;
-        const uint32_t oqx = (uint32_t)__shfl((int)p.qx, src, 64);
-        const uint32_t oqy = (uint32_t)__shfl((int)p.qy, src, 64);
-        const int osp = kMulti ? __shfl(si, src, 64) : 0;
-        if (k < cnt) {
-          const float rx = (float)(int32_t)(oqx - p.qx) * sx0;
-          const float ry = (float)(int32_t)(oqy - p.qy) * sx1;
-          if (kMulti)
-            pair_force(cut2_row[osp], sig6_row[osp], eps24, rx, ry, ax, ay);
-          else
-            pair_force(cut2_0, sig6_0, eps24, rx, ry, ax, ay);
+      for (int q = 0; q < kPairsPerWave / 64; ++q) {
+        if (q < npass && pr[q] != 0xffffffffu) {
+          const int a = (int)(pr[q] & 63u), b = (int)((pr[q] >> 6) & 63u);
+          const uint2 pa = lpos[wv][a], pb = lpos[wv][b];
+          const float rx = (float)(int32_t)(pb.x - pa.x) * sx0;
+          const float ry = (float)(int32_t)(pb.y - pa.y) * sx1;
+          int64_t fx = 0, fy = 0;  // on a; b receives exactly the negation
+          if (kMulti) {
+            const int sp = (int)((pr[q] >> 12) & 255u);
+            pair_force(pt.cut2[sp], pt.sig6[sp], eps24, rx, ry, fx, fy);
+          } else {
+            pair_force(cut2_0, sig6_0, eps24, rx, ry, fx, fy);
+          }
+          if ((fx | fy) != 0) {
+            atomicAdd(&lacc[wv][0][a], (unsigned long long)fx);
+            atomicAdd(&lacc[wv][1][a], (unsigned long long)fy);
+            atomicAdd(&lacc[wv][0][b], (unsigned long long)(-fx));
+            atomicAdd(&lacc[wv][1][b], (unsigned long long)(-fy));
+          }
         }
       }
+      wave_lds_sync();
+      ax = (int64_t)lacc[wv][0][lane];
+      ay = (int64_t)lacc[wv][1][lane];
+      lacc[wv][0][lane] = 0ull;
+      lacc[wv][1][lane] = 0ull;
     }
 #endif
 #ifdef SWARM_ABLATE_NO_BD
