@@ -226,6 +226,21 @@ int swarm_engine_neighbor_pairs(swarm_engine_t *e, int32_t env, double cutoff,
                                 int32_t *pairs, int32_t max_pairs,
                                 int32_t *n_pairs);
 
+/* Fused action sampling for the device rollout path (all pointers device):
+ * per agent a < n, over logits [n][k] fp32 (k <= 64):
+ *   idx  = argmax_j(logits_j - log(-log u_j))     gumbel_distribution.py:37-40
+ *   idx  = RandomExploration(idx) when explore_p > 0 (random_exploration.py:54-71)
+ *   logp = log(softmax(logits)_idx + 1e-8)         flax_network.py:185-192
+ *   out_f = f_table[idx], out_t = t_table[idx]     actor_critic.py:159-184
+ * u from Philox4x32-10 keyed by seed; state = 2 uint64 of device memory
+ * (call counter, arrival ticket; zero-initialise once), advanced on every
+ * call so graph replays draw fresh numbers.  Asynchronous on `stream`
+ * (hipStream_t, NULL = default stream). */
+int swarm_sample_actions(const float *logits, int32_t n, int32_t k, uint64_t seed,
+                         uint64_t *state, float explore_p, const float *f_table,
+                         const float *t_table, int64_t *out_idx, float *out_logp,
+                         float *out_f, float *out_t, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -107,10 +107,16 @@ class ActorCriticAgent(Agent):
             E = colloids.n_envs
             A = int(state_description.shape[1])
             flat = state_description.reshape(E * A, -1)
-            idx, logp = self.network.compute_action(observables=flat)
+            _, ftab, ttab, has_dir = self._action_tables(colloids.device)
+            fused = getattr(self.network, "fused_sampling_ok", None)
+            if fused is not None and fused(flat):
+                idx, logp, f_act, t_act = self.network.compute_action_fused(flat, ftab, ttab)
+                f_act, t_act = f_act.reshape(E, A), t_act.reshape(E, A)
+            else:
+                idx, logp = self.network.compute_action(observables=flat)
+                f_act = t_act = None
             idx = idx.reshape(E, A)
             logp = logp.reshape(E, A)
-            _, ftab, ttab, has_dir = self._action_tables(colloids.device)
             new_dir = None
             mask = None
             if has_dir:
@@ -123,7 +129,9 @@ class ActorCriticAgent(Agent):
                         sel = host_idx == k
                         new_dir[sel] = a.new_direction
                         mask[sel] = True
-            chosen = DeviceActions(ftab[idx], ttab[idx], new_dir, mask)
+            if f_act is None:
+                f_act, t_act = ftab[idx], ttab[idx]
+            chosen = DeviceActions(f_act, t_act, new_dir, mask)
             if self.recorder is not None:
                 self.recorder.record_action(state_description, idx, logp)
             if self.train:
@@ -145,7 +153,8 @@ class ActorCriticAgent(Agent):
         rewards = self.task(colloids)
         if self.intrinsic_reward:
             rewards = rewards + self.intrinsic_reward.compute_reward(episode_data=self.trajectory)
-        rewards = rewards + external_reward
+        if not (isinstance(external_reward, (int, float)) and external_reward == 0):
+            rewards = rewards + external_reward
         if self.recorder is not None and is_view(colloids):
             self.recorder.record_reward(rewards)
         if self.train:

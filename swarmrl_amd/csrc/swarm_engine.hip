@@ -31,6 +31,7 @@
 #include "../../include/swarmrl_amd.h"
 #include "swarm_device.cuh"
 #include "swarm_integrator.cuh"
+#include "swarm_policy.cuh"
 
 namespace {
 
@@ -1123,3 +1124,21 @@ int swarm_engine_neighbor_pairs(swarm_engine_t* e, int32_t env, double cutoff, i
 }
 
 }  // extern "C"
+
+int swarm_sample_actions(const float* logits, int32_t n, int32_t k, uint64_t seed,
+                         uint64_t* state, float explore_p, const float* f_table,
+                         const float* t_table, int64_t* out_idx, float* out_logp, float* out_f,
+                         float* out_t, void* stream) {
+  if (!logits || !state || !f_table || !t_table || !out_idx || !out_logp || !out_f || !out_t)
+    return fail(SWARM_EINVAL, "null argument");
+  if (k < 1 || k > swarm::kMaxActions) return fail(SWARM_ECAPACITY, "1 <= k <= 64 actions");
+  if (!(explore_p >= 0.0f && explore_p <= 1.0f))
+    return fail(SWARM_EINVAL, "exploration probability must be in [0, 1]");
+  if (n <= 0) return SWARM_OK;
+  hipLaunchKernelGGL(swarm::k_sample_actions, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), logits, n, k, (uint32_t)seed,
+                     (uint32_t)(seed >> 32), reinterpret_cast<unsigned long long*>(state),
+                     explore_p, f_table, t_table, out_idx, out_logp, out_f, out_t);
+  HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}

@@ -282,3 +282,26 @@ def field_transform(native, n_envs: int, agent_idx: torch.Tensor, source, box_sc
         float(b), float(scale), 1 if clip else 0, out.data_ptr(),
     )
     return out
+
+
+def sample_actions(logits: torch.Tensor, seed: int, state: torch.Tensor, explore_p: float,
+                   f_table: torch.Tensor, t_table: torch.Tensor):
+    """
+    Fused Gumbel-max sampling + exploration + log(softmax + 1e-8) of the
+    chosen action + action-table lookup (swarm_sample_actions, one kernel on
+    the current stream).  logits [n, k] fp32 (device); state: int64[2] device
+    counter buffer.  Returns (idx int64 [n], log_prob [n], f_swim [n], torque_z [n]).
+    """
+    logits = logits.contiguous()
+    n, k = logits.shape
+    dev = logits.device
+    idx = torch.empty(n, dtype=torch.int64, device=dev)
+    logp = torch.empty(n, dtype=torch.float32, device=dev)
+    f = torch.empty(n, dtype=torch.float32, device=dev)
+    t = torch.empty(n, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _capi.check(_capi.lib().swarm_sample_actions(
+        logits.data_ptr(), n, k, ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), state.data_ptr(),
+        ctypes.c_float(explore_p), f_table.data_ptr(), t_table.data_ptr(), idx.data_ptr(),
+        logp.data_ptr(), f.data_ptr(), t.data_ptr(), ctypes.c_void_p(stream)))
+    return idx, logp, f, t

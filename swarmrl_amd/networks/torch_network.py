@@ -32,6 +32,12 @@ class ActorCriticMLP(nn.Module):
         h = torch.relu(self.hidden(x))
         return self.actor(h), self.critic(h)
 
+    def logits(self, x):
+        """Actor head only (the rollout never reads the value); the hidden
+        layer's bias + ReLU run in the GEMM epilogue."""
+        h = torch._addmm_activation(self.hidden.bias, x, self.hidden.weight.t())
+        return self.actor(h)
+
 
 class TorchModel:
     """Network wrapper with the FlaxModel surface used by the agents."""
@@ -65,6 +71,10 @@ class TorchModel:
         self.optimizer = None if deployment_mode else optimizer(self.model.parameters())
         self.epoch_count = 0
         self.generator = None
+        # fused device sampling (swarm_sample_actions): Philox seed drawn from
+        # torch's generator, call counter in device memory
+        self._fused_seed = int(torch.randint(0, 2**62, (1,)).item())
+        self._fused_state = None
 
     def reinitialize_network(self):
         for m in self.model.modules():
@@ -96,6 +106,31 @@ class TorchModel:
         if host:
             return indices.cpu().numpy(), chosen.cpu().numpy()
         return indices, chosen
+
+    def fused_sampling_ok(self, observables) -> bool:
+        """The one-kernel sampling path applies: stock Gumbel sampling and
+        random exploration, device tensors, the HIP library present."""
+        return (isinstance(observables, torch.Tensor) and observables.is_cuda
+                and type(self.sampling_strategy) is GumbelDistribution
+                and type(self.exploration_policy) is RandomExploration)
+
+    @torch.no_grad()
+    def compute_action_fused(self, observables: torch.Tensor, f_table: torch.Tensor,
+                             t_table: torch.Tensor):
+        """compute_action + action-table lookup in one sampling kernel:
+        returns (indices, log_probs, f_swim, torque_z) device tensors."""
+        from swarmrl_amd.engine import ops
+
+        obs = observables.to(torch.float32)
+        obs = obs.reshape(obs.shape[0], -1)
+        if hasattr(self.model, "logits"):
+            logits = self.model.logits(obs)
+        else:
+            logits, _ = self.model(obs)
+        if self._fused_state is None or self._fused_state.device != logits.device:
+            self._fused_state = torch.zeros(2, dtype=torch.int64, device=logits.device)
+        return ops.sample_actions(logits.float(), self._fused_seed, self._fused_state,
+                                  float(self.exploration_policy.probability), f_table, t_table)
 
     def update_model(self, loss: torch.Tensor):
         self.optimizer.zero_grad(set_to_none=True)
