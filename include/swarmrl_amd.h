@@ -179,6 +179,10 @@ int swarm_engine_window_stats(swarm_engine_t *e, int32_t *fallback,
 int swarm_engine_profile(swarm_engine_t *e, int32_t enable, double *run_ms,
                          int32_t *launches);
 
+/* Diagnostics: 32 shader-clock stamps of the last cluster build's phases
+ * (env 0), filled only by builds compiled with -DSWARM_PHASE_TIMING. */
+int swarm_engine_debug_phases(swarm_engine_t *e, uint64_t *out32);
+
 /* Total number of BD sub-steps integrated so far (the noise counter). */
 int64_t swarm_engine_step_count(const swarm_engine_t *e);
 

@@ -486,7 +486,15 @@ constexpr size_t kMaxLds = 160 * 1024;
 
 size_t global_lds_bytes(int lx, int ly) { return (16 + (size_t)(1 << (lx + ly)) + 1) * 4; }
 
-size_t build_lds_bytes(int n, int lx, int ly) { return swarm::build_lds_words(n, lx, ly) * 4; }
+// Pair-list capacity of the cluster build: up to 3 N pairs (mean degree 6),
+// at least N, within the LDS left after the other arrays of k_cluster_build.
+int build_pair_cap(int n) {
+  const size_t fixed = swarm::build_lds_words(n, 0) * 4;
+  const size_t room = fixed < kMaxLds ? (kMaxLds - fixed) / 4 : 0;
+  return (int)std::min<size_t>(room, 3 * (size_t)n);
+}
+
+size_t build_lds_bytes(int n, int pair_cap) { return swarm::build_lds_words(n, pair_cap) * 4; }
 
 size_t check_lds_bytes(int lx, int ly) {
   return (16 + 16 + 1024 + (size_t)(1 << (lx + ly)) + 1) * 4;
@@ -500,6 +508,7 @@ void set_lds_attributes() {
   if (done) return;
   const void* fns[] = {reinterpret_cast<const void*>(&swarm::k_global),
                        reinterpret_cast<const void*>(&swarm::k_cluster_build),
+                       reinterpret_cast<const void*>(&swarm::k_build_sort),
                        reinterpret_cast<const void*>(&swarm::k_check),
                        reinterpret_cast<const void*>(&k_grid_build),
                        reinterpret_cast<const void*>(&k_vision_grid)};
@@ -519,9 +528,15 @@ int launch_global(swarm_engine* e, int n_steps, int sd_mode, float g, float md) 
 
 // Cluster build (+ noise table for n_noise sub-steps) of the next window.
 int launch_build(swarm_engine* e, hipStream_t stream, int n_noise) {
+  const int ncb = 1 << (e->lxb + e->lyb);
+  hipLaunchKernelGGL(swarm::k_build_sort, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4, stream,
+                     e->st, e->sc, e->lxb, e->lyb);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(swarm::k_build_pairs, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
+                     dim3(256), 0, stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb);
+  HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(swarm::k_cluster_build, dim3(e->n_envs), dim3(1024),
-                     build_lds_bytes(e->n, e->lxb, e->lyb), stream, e->d_derived, e->st, e->sc,
-                     e->lxb, e->lyb);
+                     build_lds_bytes(e->n, e->sc.pair_cap), stream, e->st, e->sc);
   HIP_TRY(hipGetLastError());
   if (e->noise_table && n_noise > 0) {
     const long ts = (long)e->n_envs * e->sc.S;
@@ -719,7 +734,9 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   }
   // the cluster path needs the build workgroup's LDS and a non-degenerate
   // build grid; otherwise every window runs on the global path
-  e->cluster_path = build_lds_bytes(n_particles, e->lxb, e->lyb) + kStaticLds <= kMaxLds &&
+  e->sc.pair_cap = build_pair_cap(n_particles);
+  e->cluster_path = e->sc.pair_cap >= n_particles && n_particles < 65536 &&
+                    (size_t)(16 + (1 << (e->lxb + e->lyb)) + 1) * 4 <= kMaxLds &&
                     (1 << e->lxb) >= 3 && (1 << e->lyb) >= 3;
   const size_t M = (size_t)n_envs * n_particles;
   int rc = SWARM_OK;
@@ -752,11 +769,15 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->sc.bang, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.root, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.slot_of, M);
-  rc = rc ? rc : dev_alloc(e, &e->sc.ncount, M);
-  rc = rc ? rc : dev_alloc(e, &e->sc.nbr_tmp, M * swarm::kNbMax);
   rc = rc ? rc : dev_alloc(e, &e->sc.perm, (size_t)n_envs * S);
   rc = rc ? rc : dev_alloc(e, &e->sc.pairs, (size_t)n_envs * (S / 64) * swarm::kPairsPerWave);
+  rc = rc ? rc : dev_alloc(e, &e->sc.bsq, 2 * M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.bsid, M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.bcstart, (size_t)n_envs * ((1 << (e->lxb + e->lyb)) + 1));
+  rc = rc ? rc : dev_alloc(e, &e->sc.gplist, (size_t)n_envs * std::max(e->sc.pair_cap, 1));
+  rc = rc ? rc : dev_alloc(e, &e->sc.gnpairs, (size_t)n_envs);
   rc = rc ? rc : dev_alloc(e, &e->sc.wave_npairs, (size_t)n_envs * (S / 64));
+  rc = rc ? rc : dev_alloc(e, &e->sc.phase, 32);
   rc = rc ? rc : dev_alloc(e, &e->sc.disp, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.env_waves, (size_t)n_envs);
   rc = rc ? rc : dev_alloc(e, &e->sc.fallback, (size_t)n_envs);
@@ -951,6 +972,13 @@ int swarm_engine_profile(swarm_engine_t* e, int32_t enable, double* run_ms, int3
   if (launches) *launches = (int32_t)e->prof_events.size();
   e->prof_events.clear();
   e->profile = enable != 0;
+  return SWARM_OK;
+}
+
+int swarm_engine_debug_phases(swarm_engine_t* e, uint64_t* out32) {
+  if (!e || !out32) return fail(SWARM_EINVAL, "null argument");
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipMemcpy(out32, e->sc.phase, 32 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return SWARM_OK;
 }
 

@@ -38,7 +38,6 @@
 namespace swarm {
 
 constexpr int kMaxSpecies = SWARM_MAX_SPECIES;
-constexpr int kNbMax = 15;        // neighbours per particle inside a window
 constexpr int kMaxWindow = 128;   // sub-steps per cluster window
 constexpr int kPairsPerWave = 256;  // neighbour pairs of one 64-lane wave (4 passes)
 
@@ -90,17 +89,34 @@ struct Scratch {
   uint32_t* bang;     // [M]
   int32_t* root;      // [M] cluster id (root particle)
   int32_t* slot_of;   // [M] wave slot of a particle
-  int32_t* ncount;    // [M] neighbour count
-  int32_t* nbr_tmp;   // [M][kNbMax] neighbour particle indices
   int32_t* perm;      // [E][S] particle of a slot (-1: idle lane)
   uint32_t* pairs;    // [E][wmax][kPairsPerWave]: lane a | lane b << 6 | species pair << 12
   int32_t* wave_npairs;  // [E][wmax]
   float* disp;        // [M] max displacement over the window
   int32_t* env_waves; // [E]
   int32_t* fallback;  // [E]
+  // cluster build (k_build_sort -> k_build_pairs -> k_cluster_build)
+  uint32_t* bsq;      // [2][M] cell-sorted positions (x, y)
+  int32_t* bsid;      // [M] particle | species << 24 of a sorted entry
+  int32_t* bcstart;   // [E][ncb + 1] first sorted entry of every cell, [ncb] = N
+  uint32_t* gplist;   // [E][pair_cap] neighbour pairs i | j << 16, i < j
+  int32_t* gnpairs;   // [E] pairs found (may exceed pair_cap: overflow)
+  int32_t pair_cap;   // pairs per env
   int32_t S;          // slots per env
   int32_t wmax;       // S / 64
+  uint64_t* phase;    // [32] build phase stamps (SWARM_PHASE_TIMING builds only)
 };
+
+#ifdef SWARM_PHASE_TIMING
+#define SWARM_STAMP(k)                                                    \
+  do {                                                                    \
+    if (blockIdx.x == 0 && threadIdx.x == 0) sc.phase[k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define SWARM_STAMP(k) \
+  do {                 \
+  } while (0)
+#endif
 
 // ---------------------------------------------------------------- helpers
 __device__ __forceinline__ int cell_index(uint32_t qx, uint32_t qy, int lx, int ly) {
@@ -406,11 +422,16 @@ __global__ __launch_bounds__(1024) void k_global(const Derived* __restrict__ d, 
 }
 
 // ------------------------------------------------------ cluster build
+// Concurrent union-find on LDS: find with path halving (a lane only ever
+// points a node at one of its ancestors), union hooks the larger root under
+// the smaller with CAS, so no cycle can form.
 __device__ __forceinline__ int uf_find(volatile int32_t* parent, int x) {
   while (true) {
     const int p = parent[x];
     if (p == x) return x;
-    x = p;
+    const int gp = parent[p];
+    if (gp != p) parent[x] = gp;
+    x = gp;
   }
 }
 
@@ -424,112 +445,161 @@ __device__ __forceinline__ void uf_union(int32_t* parent, int a, int b) {
       a = b;
       b = t;
     }
-    // hook the larger root under the smaller one: no cycles can form
     if (atomicCAS(&parent[a], a, b) == a) return;
   }
 }
 
-// LDS words of k_cluster_build: 168 fixed + per-wave pair counters + cell
-// counts + parent[N] + 3 N (cell-sorted positions / ids, later cluster
-// sizes, bases and slots).
-__host__ __device__ inline size_t build_lds_words(int n, int lx, int ly) {
-  const int ncell = 1 << (lx + ly);
+// LDS words of k_cluster_build: 168 fixed + per-wave pair counters +
+// parent[N] + 3 N (cluster sizes, bases, slots) + the env's pair list.
+__host__ __device__ inline size_t build_lds_words(int n, int pair_cap) {
   const int wmax = slots_per_env(n) / 64;
-  return 16 + 16 + 68 + 68 + (size_t)((wmax + 3) & ~3) + (size_t)((ncell + 1 + 3) & ~3) +
-         4 * (size_t)n;
+  return 16 + 16 + 68 + 68 + (size_t)((wmax + 3) & ~3) + 4 * (size_t)n + (size_t)pair_cap;
 }
 
-__global__ __launch_bounds__(1024) void k_cluster_build(const Derived* __restrict__ d,
-                                                        DevState st, Scratch sc, int lx,
-                                                        int ly) {
+// Build step 1, one workgroup per env: counting sort into cells of side
+// >= rc_max + skin (global arrays for the chip-wide pair search).
+__global__ __launch_bounds__(1024) void k_build_sort(DevState st, Scratch sc, int lx, int ly) {
   extern __shared__ __align__(16) unsigned char smem[];
-  __shared__ float nb2[kMaxSpecies * kMaxSpecies];
   const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly);
-  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);  // 16
-  int32_t* misc = wave_sums + 16;                          // 16
-  int32_t* classcnt = misc + 16;                           // 68
-  int32_t* wavebase = classcnt + 68;                       // 68
-  const int wmax = sc.wmax;
-  int32_t* wave_np = wavebase + 68;                        // wmax (padded)
-  int32_t* cnt = wave_np + ((wmax + 3) & ~3);              // ncell + 1 (padded)
-  int32_t* parent = cnt + ((ncell + 1 + 3) & ~3);          // N
-  // phase A (cell sort + neighbour search): sorted positions and ids
-  uint32_t* lqx = reinterpret_cast<uint32_t*>(parent + N);
-  uint32_t* lqy = lqx + N;
-  int32_t* lid = reinterpret_cast<int32_t*>(lqy + N);  // particle | species << 24
-  // phase B (clusters -> wave slots) reuses the same words
-  int32_t* csz = reinterpret_cast<int32_t*>(lqx);
-  int32_t* cbase = reinterpret_cast<int32_t*>(lqy);
-  int32_t* lslot = lid;
-  const int S = sc.S;
-
-  for (int k = tid; k < kMaxSpecies * kMaxSpecies; k += T) nb2[k] = d->nb2[k];
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
+  int32_t* cnt = wave_sums + 16;
+  SWARM_STAMP(0);
   for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
-  for (int k = tid; k < 68; k += T) classcnt[k] = 0;
-  for (int k = tid; k < wmax; k += T) wave_np[k] = 0;
-  if (tid < 16) misc[tid] = 0;
-  for (int i = tid; i < N; i += T) parent[i] = i;
-  for (int k = tid; k < S; k += T) sc.perm[(size_t)e * S + k] = -1;
+  for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
+  if (tid == 0) sc.gnpairs[e] = 0;
   __syncthreads();
-
-  // cell sort into LDS (side >= rc_max + skin)
   for (int i = tid; i < N; i += T)
     atomicAdd(&cnt[cell_index(st.q[base + i], st.q[M + base + i], lx, ly)], 1);
   __syncthreads();
   block_exclusive_scan(cnt, ncell, wave_sums);
   __syncthreads();
+  int32_t* cs = sc.bcstart + (size_t)e * (ncell + 1);
+  for (int c = tid; c <= ncell; c += T) cs[c] = cnt[c];
+  __syncthreads();
   for (int i = tid; i < N; i += T) {
     const uint32_t qx = st.q[base + i], qy = st.q[M + base + i];
-    const int pos = atomicAdd(&cnt[cell_index(qx, qy, lx, ly)], 1);
-    lqx[pos] = qx;
-    lqy[pos] = qy;
-    lid[pos] = i | ((int32_t)st.species[i] << 24);
+    const size_t pos = base + atomicAdd(&cnt[cell_index(qx, qy, lx, ly)], 1);
+    sc.bsq[pos] = qx;
+    sc.bsq[M + pos] = qy;
+    sc.bsid[pos] = i | ((int32_t)st.species[i] << 24);
   }
-  __syncthreads();
+  SWARM_STAMP(1);
+}
 
-  // neighbours within r_i + r_j + skin, union of the pairs
+// Build step 2, chip-wide (grid.y = env, one thread per sorted entry): every
+// pair within r_i + r_j + skin once (i < j).  A stencil row (cells x-1..x+1)
+// is one contiguous sorted range, plus a wrap range at the grid edge.  Pass
+// 0 counts, one atomic per wave reserves the space, pass 1 writes.
+__global__ __launch_bounds__(256) void k_build_pairs(const Derived* __restrict__ d, DevState st,
+                                                     Scratch sc, int lx, int ly) {
+  __shared__ float nb2[kMaxSpecies * kMaxSpecies];
+  for (int k = threadIdx.x; k < kMaxSpecies * kMaxSpecies; k += blockDim.x) nb2[k] = d->nb2[k];
+  __syncthreads();
+  const int e = blockIdx.y, N = st.n;
+  const int ps = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = ps < N;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int ncell = 1 << (lx + ly);
+  const int32_t* cs = sc.bcstart + (size_t)e * (ncell + 1);
   const int ncx = 1 << lx, ncy = 1 << ly;
-  const int lox = ncx >= 3 ? -1 : 0, hix = ncx >= 3 ? 1 : ncx - 1;
   const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
   const float sx0 = d->sx[0], sx1 = d->sx[1];
-  for (int i = tid; i < N; i += T) {
-    const uint32_t qx = st.q[base + i], qy = st.q[M + base + i];
-    const float* nb2_row = nb2 + (int)st.species[i] * kMaxSpecies;
-    const int c0 = cell_index(qx, qy, lx, ly);
-    const int cx = c0 & (ncx - 1), cy = c0 >> lx;
-    int32_t* out = sc.nbr_tmp + (base + i) * kNbMax;
-    int nc = 0;
-    for (int oy = loy; oy <= hiy; ++oy) {
-      const int y = (cy + oy + ncy) & (ncy - 1);
-      for (int ox = lox; ox <= hix; ++ox) {
-        const int x = (cx + ox + ncx) & (ncx - 1);
-        const int cc = (y << lx) | x;
-        const int jb = cc ? cnt[cc - 1] : 0, je = cnt[cc];
+  int pk = 0, i = 0;
+  uint32_t qx = 0, qy = 0;
+  if (valid) {
+    pk = sc.bsid[base + ps];
+    i = pk & 0xffffff;
+    qx = sc.bsq[base + ps];
+    qy = sc.bsq[M + base + ps];
+  }
+  const float* nb2_row = nb2 + (pk >> 24) * kMaxSpecies;
+  const int c0 = cell_index(qx, qy, lx, ly);
+  const int cx = c0 & (ncx - 1), cy = c0 >> lx;
+  const int xa = ncx >= 3 ? max(cx - 1, 0) : 0;
+  const int xb = ncx >= 3 ? min(cx + 1, ncx - 1) : ncx - 1;
+  const int xw = ncx >= 3 ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
+  uint32_t* out = sc.gplist + (size_t)e * sc.pair_cap;
+  int my_off = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    int found = 0;
+    for (int oy = loy; oy <= hiy && valid; ++oy) {
+      const int row = ((cy + oy + ncy) & (ncy - 1)) << lx;
+#pragma unroll
+      for (int part = 0; part < 2; ++part) {
+        if (part == 1 && xw < 0) continue;
+        const int c_lo = row | (part == 0 ? xa : xw), c_hi = row | (part == 0 ? xb : xw);
+        const int jb = cs[c_lo], je = cs[c_hi + 1];
         for (int jj = jb; jj < je; ++jj) {
-          const int packed = lid[jj];
+          const int packed = sc.bsid[base + jj];
           const int j = packed & 0xffffff;
-          const float rx = (float)(int32_t)(lqx[jj] - qx) * sx0;
-          const float ry = (float)(int32_t)(lqy[jj] - qy) * sx1;
-          if (j != i && rx * rx + ry * ry < nb2_row[packed >> 24]) {
-            if (nc < kNbMax)
-              out[nc] = j;
-            else
-              misc[0] = 1;  // neighbour overflow -> global path for this env
-            ++nc;
-            if (i < j) uf_union(parent, i, j);
+          const float rx = (float)(int32_t)(sc.bsq[base + jj] - qx) * sx0;
+          const float ry = (float)(int32_t)(sc.bsq[M + base + jj] - qy) * sx1;
+          if (i < j && rx * rx + ry * ry < nb2_row[packed >> 24]) {
+            if (pass == 1) {
+              const int k = my_off + found;
+              if (k < sc.pair_cap) out[k] = (uint32_t)i | ((uint32_t)j << 16);
+            }
+            ++found;
           }
         }
       }
     }
-    sc.ncount[base + i] = nc < kNbMax ? nc : kNbMax;
+    if (pass == 0) {  // wave prefix sum, one atomic per wave
+      const int lane = threadIdx.x & 63;
+      int v = found;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(v, off, 64);
+        if (lane >= off) v += o;
+      }
+      int wbase = 0;
+      if (lane == 63) wbase = atomicAdd(&sc.gnpairs[e], v);
+      wbase = __shfl(wbase, 63, 64);
+      my_off = wbase + v - found;
+    }
   }
-  __syncthreads();
+}
+
+// Build step 3, one workgroup per env: union-find over the pair list
+// (connected components = clusters), packing of the clusters into 64-lane
+// wave slots that never straddle a wave, per-wave pair lists.
+__global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t base = (size_t)e * N;
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);  // 16
+  int32_t* misc = wave_sums + 16;                          // 16: 0 flag, 1 waves
+  int32_t* classcnt = misc + 16;                           // 68
+  int32_t* wavebase = classcnt + 68;                       // 68
+  const int wmax = sc.wmax;
+  int32_t* wave_np = wavebase + 68;                        // wmax (padded)
+  int32_t* parent = wave_np + ((wmax + 3) & ~3);           // N
+  int32_t* csz = parent + N;                               // N
+  int32_t* cbase = csz + N;                                // N
+  int32_t* lslot = cbase + N;                              // N
+  uint32_t* plist = reinterpret_cast<uint32_t*>(lslot + N);  // pair_cap
+  const int S = sc.S;
+  SWARM_STAMP(2);
+  const int found = sc.gnpairs[e];
+  const int npairs = min(found, sc.pair_cap);
+  for (int k = tid; k < 68; k += T) classcnt[k] = 0;
+  for (int k = tid; k < wmax; k += T) wave_np[k] = 0;
+  if (tid < 16) misc[tid] = found > sc.pair_cap ? 1 : 0;  // overflow -> global path
   for (int i = tid; i < N; i += T) {
-    parent[i] = uf_find(parent, i);
+    parent[i] = i;
     csz[i] = 0;
   }
+  for (int k = tid; k < npairs; k += T) plist[k] = sc.gplist[(size_t)e * sc.pair_cap + k];
+  __syncthreads();
+  for (int k = tid; k < npairs; k += T) {
+    const uint32_t pr = plist[k];
+    uf_union(parent, (int)(pr & 0xffffu), (int)(pr >> 16));
+  }
+  __syncthreads();
+  SWARM_STAMP(3);
+  for (int i = tid; i < N; i += T) parent[i] = uf_find(parent, i);
   __syncthreads();
   for (int i = tid; i < N; i += T) lslot[i] = atomicAdd(&csz[parent[i]], 1);
   __syncthreads();
@@ -542,6 +612,7 @@ __global__ __launch_bounds__(1024) void k_cluster_build(const Derived* __restric
       cbase[i] = atomicAdd(&classcnt[s], 1);
   }
   __syncthreads();
+  SWARM_STAMP(4);
   if (misc[0]) {
     if (tid == 0) {
       sc.fallback[e] = 1;
@@ -580,27 +651,23 @@ __global__ __launch_bounds__(1024) void k_cluster_build(const Derived* __restric
     sc.root[base + i] = root;
   }
   __syncthreads();
-  // neighbour pairs of every wave, each once (from its lower index); the two
-  // particles share a cluster and therefore a wave
-  for (int i = tid; i < N; i += T) {
-    const int slot = lslot[i];
-    const int wv = slot >> 6;
-    const int nc = sc.ncount[base + i];
-    const int32_t* nb = sc.nbr_tmp + (base + i) * kNbMax;
-    const int si = st.species[i];
-    uint32_t* pw = sc.pairs + ((size_t)e * wmax + wv) * kPairsPerWave;
-    for (int k = 0; k < nc; ++k) {
-      const int j = nb[k];
-      if (j < i) continue;
-      const int idx = atomicAdd(&wave_np[wv], 1);
-      if (idx < kPairsPerWave)
-        pw[idx] = (uint32_t)(slot & 63) | ((uint32_t)(lslot[j] & 63) << 6) |
-                  ((uint32_t)(si * kMaxSpecies + st.species[j]) << 12);
-      else
-        misc[2] = 1;  // pair overflow -> global path for this env
-    }
+  SWARM_STAMP(5);
+  // per-wave pair lists (both particles of a pair share a cluster, so a wave)
+  for (int k = tid; k < npairs; k += T) {
+    const uint32_t pr = plist[k];
+    const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
+    const int si = lslot[i], sj = lslot[j];
+    const int wv = si >> 6;
+    const int idx = atomicAdd(&wave_np[wv], 1);
+    if (idx < kPairsPerWave)
+      sc.pairs[((size_t)e * wmax + wv) * kPairsPerWave + idx] =
+          (uint32_t)(si & 63) | ((uint32_t)(sj & 63) << 6) |
+          ((uint32_t)(st.species[i] * kMaxSpecies + st.species[j]) << 12);
+    else
+      misc[2] = 1;  // a wave with more than kPairsPerWave pairs
   }
   __syncthreads();
+  SWARM_STAMP(6);
   for (int w = tid; w < misc[1]; w += T)
     sc.wave_npairs[(size_t)e * wmax + w] = min(wave_np[w], kPairsPerWave);
   if (tid == 0) {
@@ -832,10 +899,16 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
         const float lim = rc + sc.disp[base + m] + sc.disp[base + j] + 1e-3f;
         if (rx * rx + ry * ry < lim * lim) {
           bool listed = false;
-          if (sc.root[base + j] == sc.root[base + m]) {
-            const int nc = sc.ncount[base + m];
-            const int32_t* nb = sc.nbr_tmp + (base + m) * kNbMax;
-            for (int k = 0; k < nc; ++k) listed |= nb[k] == j;
+          if (sc.root[base + j] == sc.root[base + m]) {  // same wave: search its pairs
+            const int sm = sc.slot_of[base + m], sj = sc.slot_of[base + j];
+            const int wv = sm >> 6;
+            const uint32_t lm = (uint32_t)(sm & 63), lj = (uint32_t)(sj & 63);
+            const uint32_t* pw = sc.pairs + ((size_t)e * sc.wmax + wv) * kPairsPerWave;
+            const int np = sc.wave_npairs[(size_t)e * sc.wmax + wv];
+            for (int k = 0; k < np; ++k) {
+              const uint32_t a = pw[k] & 63u, b = (pw[k] >> 6) & 63u;
+              listed |= (a == lm && b == lj) || (a == lj && b == lm);
+            }
           }
           if (!listed) misc[1] = 1;
         }

@@ -1,0 +1,31 @@
+"""Phase timing of k_cluster_build (needs the PHASE_TIMING variant library):
+SWARMRL_AMD_LIB=tools/_variants/libswarmrl_amd_PHASE_TIMING.so python tools/build_phases.py"""
+import ctypes
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+sys.path.insert(0, "tools")
+from ablate_integrator import disc_states  # noqa: E402
+
+sys.path.insert(0, "tests")
+from gpu_harness import Harness, species_list  # noqa: E402
+
+torch.cuda.set_device(0)
+n = 4096
+L = 2 * np.sqrt(n / 0.1)
+rng = np.random.default_rng(1)
+h = Harness([L, L, L], 1e-3, 1.0239, 1.0239, 42, species_list()[:1], np.zeros(n, int))
+h.upload(disc_states(rng, n, L, 1))
+h.sd(1000)
+h.set_actions(rng.choice([0.0, 10.0], n).astype(np.float32),
+              rng.choice([-10.0, 0.0, 10.0], n).astype(np.float32))
+for rep in range(5):
+    h.integrate(100)
+    out = np.zeros(32, np.uint64)
+    h.native.call("swarm_engine_debug_phases", out.ctypes.data)
+    k = int(np.max(np.nonzero(out)[0])) + 1
+    d = np.diff(out[:k].astype(np.int64))
+    print("phase cycles:", " ".join(f"{x:6d}" for x in d), " total", int(out[k - 1]) - int(out[0]))

@@ -2,9 +2,9 @@
 #   _nopairs: run kernel without the neighbour loop; _nobd: without the BD update.
 set -e
 cd "$(dirname "$0")/.."
-for v in NO_PAIRS NO_BD; do
+for v in NO_PAIRS NO_BD PHASE_TIMING; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off \
-    -DSWARM_ABLATE_$v swarmrl_amd/csrc/swarm_engine.hip -o /tmp/libswarmrl_amd_$v.so &
+    -DSWARM_$v -DSWARM_ABLATE_$v swarmrl_amd/csrc/swarm_engine.hip -o /tmp/libswarmrl_amd_$v.so &
 done
 wait
-mkdir -p tools/_variants && cp /tmp/libswarmrl_amd_NO_*.so tools/_variants/
+mkdir -p tools/_variants && cp /tmp/libswarmrl_amd_*.so tools/_variants/
