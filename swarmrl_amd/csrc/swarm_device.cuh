@@ -123,16 +123,12 @@ __device__ __forceinline__ void sincos_turn(uint32_t a, float* s_out, float* c_o
   cp = cp * z;
   const float h = __builtin_fmaf(-0.5f, z, 1.0f);
   const float c = __builtin_fmaf(cp, z, h);
-  // quadrant rotation without divergent branches
+  // quadrant rotation: a swap and two sign flips on the float bits (exact)
   const bool swap = (quad & 1u) != 0u;
-  float so = swap ? c : s;
-  float co = swap ? s : c;
-  if (quad == 1u) co = -co;
-  if (quad == 2u) {
-    so = -so;
-    co = -co;
-  }
-  if (quad == 3u) so = -so;
+  const float so0 = swap ? c : s;
+  const float co0 = swap ? s : c;
+  const float so = __uint_as_float(__float_as_uint(so0) ^ ((quad >> 1) << 31));
+  const float co = __uint_as_float(__float_as_uint(co0) ^ (((quad ^ (quad >> 1)) & 1u) << 31));
   *s_out = so;
   *c_out = co;
 }
@@ -202,18 +198,19 @@ __device__ __forceinline__ int64_t f2fix24(float v) {
   return __float2ll_rn(v);
 }
 
-// int64 -> fp32 round-to-nearest; int32-range values take one conversion.
+// int64 -> fp32 round-to-nearest; when every lane's value fits int32 (the
+// common case, a wave-uniform test) one conversion instruction.
 __device__ __forceinline__ float i64_to_f32(int64_t a) {
-  if (__builtin_expect(a == (int64_t)(int32_t)a, 1)) return (float)(int32_t)a;
+  if (__all(a == (int64_t)(int32_t)a)) return (float)(int32_t)a;
   return (float)a;
 }
 
+// q + dq with the box crossing carried into the image counter: the high
+// word of the 64-bit sum (q zero-extended, dq sign-extended) is -1, 0 or +1.
 __device__ __forceinline__ void advance(uint32_t& q, int32_t& img, int32_t dq) {
-  const uint32_t old = q;
-  const uint32_t nq = old + (uint32_t)dq;
-  img += (dq > 0 && nq < old) ? 1 : 0;
-  img -= (dq < 0 && nq > old) ? 1 : 0;
-  q = nq;
+  const int64_t sum = (int64_t)(uint64_t)q + (int64_t)dq;
+  img += (int32_t)(sum >> 32);
+  q = (uint32_t)sum;
 }
 
 }  // namespace swarm

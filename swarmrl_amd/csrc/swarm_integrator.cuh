@@ -182,6 +182,34 @@ __device__ __forceinline__ void pair_force(float cut2, float sig6, float eps24, 
   }
 }
 
+// Branch-free pair_force for the run kernel's pair passes: the force on the
+// first particle in 2^-24 fixed point, or zero out of range (r2 = 0 for an
+// empty slot that names one particle twice).  In-range values equal
+// pair_force's; the int32 conversion is taken when every lane fits.
+__device__ __forceinline__ void pair_fix_sel(float cut2, float sig6, float eps24, float rx,
+                                             float ry, int64_t& fx, int64_t& fy) {
+  const float r2 = rx * rx + ry * ry;
+  const bool in = r2 < cut2 && r2 > 0.0f;
+  const float ir2 = 1.0f / (in ? r2 : 1.0f);
+  float ir6 = ir2 * ir2;
+  ir6 = ir6 * ir2;
+  const float s6 = sig6 * ir6;
+  float t = 2.0f * s6;
+  t = t - 1.0f;
+  float fr = eps24 * s6;
+  fr = fr * t;
+  fr = fr * ir2;
+  const float vx = (in ? -fr * rx : 0.0f) * 16777216.0f;
+  const float vy = (in ? -fr * ry : 0.0f) * 16777216.0f;
+  if (__all(fabsf(vx) < 2147483520.0f && fabsf(vy) < 2147483520.0f)) {
+    fx = (int64_t)__float2int_rn(vx);
+    fy = (int64_t)__float2int_rn(vy);
+  } else {
+    fx = __float2ll_rn(fminf(fmaxf(vx, -4.611686018427387904e18f), 4.611686018427387904e18f));
+    fy = __float2ll_rn(fminf(fmaxf(vy, -4.611686018427387904e18f), 4.611686018427387904e18f));
+  }
+}
+
 struct PState {
   uint32_t qx, qy, an;
   int32_t ix, iy;
@@ -231,9 +259,14 @@ __device__ __forceinline__ void bd_step(const PConst& c, PState& p, int64_t ax, 
                                         float fs, float tz, float fex, float fey, uint32_t k0,
                                         uint32_t k1, uint32_t id, uint64_t step, bool last,
                                         float* vx, float* vy, float* w,
-                                        const float* gt = nullptr) {
+                                        const float* gt = nullptr, const float* dir = nullptr) {
   float sn, cs;
-  sincos_turn(p.an, &sn, &cs);
+  if (dir) {  // director of this sub-step, computed ahead by the caller
+    sn = dir[0];
+    cs = dir[1];
+  } else {
+    sincos_turn(p.an, &sn, &cs);
+  }
   float fx = i64_to_f32(ax) * 5.9604644775390625e-08f;
   float fy = i64_to_f32(ay) * 5.9604644775390625e-08f;
   fx = fx + fex;
@@ -778,7 +811,18 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
     gn[1] = tcol[ts];
     gn[2] = tcol[2 * ts];
   }
+#ifdef SWARM_PHASE_TIMING
+  const bool stamp = e == 0 && w == sc.env_waves[e] - 1 && lane == 0;
+  uint64_t t_pairs = 0, t_read = 0, t_bd = 0, t0s = 0, t1s = 0;
+#endif
   for (int s = 0; s < n_steps; ++s) {
+#ifdef SWARM_PHASE_TIMING
+    if (stamp) t0s = t1s = __builtin_amdgcn_s_memtime();
+#endif
+    // the director depends on the angle only: off the force chain, it can
+    // fill the LDS latencies of the pair section
+    float dir[2];
+    sincos_turn(p.an, &dir[0], &dir[1]);
     float gt[3] = {gn[0], gn[1], gn[2]};
     if (kTable && active && s + 1 < n_steps) {
       const float* nx = tcol + (size_t)(s + 1) * 3 * ts;
@@ -793,31 +837,44 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
       wave_lds_sync();
 #pragma unroll
       for (int q = 0; q < kPairsPerWave / 64; ++q) {
-        if (q < npass && pr[q] != 0xffffffffu) {
-          const int a = (int)(pr[q] & 63u), b = (int)((pr[q] >> 6) & 63u);
+        if (q < npass) {  // wave-uniform; an empty slot names the lane twice
+          const uint32_t e_ = pr[q];
+          const int a = e_ == 0xffffffffu ? lane : (int)(e_ & 63u);
+          const int b = e_ == 0xffffffffu ? lane : (int)((e_ >> 6) & 63u);
           const uint2 pa = lpos[wv][a], pb = lpos[wv][b];
           const float rx = (float)(int32_t)(pb.x - pa.x) * sx0;
           const float ry = (float)(int32_t)(pb.y - pa.y) * sx1;
-          int64_t fx = 0, fy = 0;  // on a; b receives exactly the negation
+          int64_t fx, fy;  // on a; b receives exactly the negation
           if (kMulti) {
-            const int sp = (int)((pr[q] >> 12) & 255u);
-            pair_force(pt.cut2[sp], pt.sig6[sp], eps24, rx, ry, fx, fy);
+            const int sp = (int)((e_ >> 12) & 255u);
+            pair_fix_sel(pt.cut2[sp], pt.sig6[sp], eps24, rx, ry, fx, fy);
           } else {
-            pair_force(cut2_0, sig6_0, eps24, rx, ry, fx, fy);
+            pair_fix_sel(cut2_0, sig6_0, eps24, rx, ry, fx, fy);
           }
-          if ((fx | fy) != 0) {
-            atomicAdd(&lacc[wv][0][a], (unsigned long long)fx);
-            atomicAdd(&lacc[wv][1][a], (unsigned long long)fy);
-            atomicAdd(&lacc[wv][0][b], (unsigned long long)(-fx));
-            atomicAdd(&lacc[wv][1][b], (unsigned long long)(-fy));
-          }
+          atomicAdd(&lacc[wv][0][a], (unsigned long long)fx);
+          atomicAdd(&lacc[wv][1][a], (unsigned long long)fy);
+          atomicAdd(&lacc[wv][0][b], (unsigned long long)(-fx));
+          atomicAdd(&lacc[wv][1][b], (unsigned long long)(-fy));
         }
       }
       wave_lds_sync();
+#ifdef SWARM_PHASE_TIMING
+      if (stamp) {
+        t1s = __builtin_amdgcn_s_memtime();
+        t_pairs += t1s - t0s;
+      }
+#endif
       ax = (int64_t)lacc[wv][0][lane];
       ay = (int64_t)lacc[wv][1][lane];
       lacc[wv][0][lane] = 0ull;
       lacc[wv][1][lane] = 0ull;
+#ifdef SWARM_PHASE_TIMING
+      if (stamp) {
+        const uint64_t t2 = __builtin_amdgcn_s_memtime();
+        t_read += t2 - t1s;
+        t1s = t2;
+      }
+#endif
     }
 #endif
 #ifdef SWARM_ABLATE_NO_BD
@@ -830,12 +887,24 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
     if (active) {
 #endif
       bd_step<kTable>(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i,
-                      step0 + (uint64_t)s, s == n_steps - 1, &vx, &vy, &om, gt);
+                      step0 + (uint64_t)s, s == n_steps - 1, &vx, &vy, &om, gt, dir);
       const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
       const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
       dmax2 = fmaxf(dmax2, ddx * ddx + ddy * ddy);
     }
+#ifdef SWARM_PHASE_TIMING
+    if (stamp) t_bd += __builtin_amdgcn_s_memtime() - t1s;
+#endif
   }
+#ifdef SWARM_PHASE_TIMING
+  if (stamp) {
+    sc.phase[16] = t_pairs;
+    sc.phase[17] = t_read;
+    sc.phase[18] = t_bd;
+    sc.phase[19] = (uint64_t)n_steps;
+    sc.phase[20] = (uint64_t)npass;
+  }
+#endif
   if (active) {
     st.q[gi] = p.qx;
     st.q[M + gi] = p.qy;

@@ -26,6 +26,10 @@ for rep in range(5):
     h.integrate(100)
     out = np.zeros(32, np.uint64)
     h.native.call("swarm_engine_debug_phases", out.ctypes.data)
-    k = int(np.max(np.nonzero(out)[0])) + 1
+    if out[19]:
+        ns = int(out[19])
+        print(f"run (wave 0, npass {int(out[20])}): cycles/sub-step pairs {int(out[16]) // ns} "
+              f"read-back {int(out[17]) // ns} bd {int(out[18]) // ns}")
+    k = int(np.max(np.nonzero(out[:16])[0])) + 1
     d = np.diff(out[:k].astype(np.int64))
     print("phase cycles:", " ".join(f"{x:6d}" for x in d), " total", int(out[k - 1]) - int(out[0]))
