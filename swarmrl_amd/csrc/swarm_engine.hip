@@ -453,6 +453,7 @@ struct swarm_engine {
   int lxg = 0, lyg = 0;  // global-path grid: cell side >= rc_max
   int lxb = 0, lyb = 0;  // cluster-build grid: cell side >= rc_max + skin
   bool cluster_path = false;
+  bool big_build = false;  // k_cluster_build<true>: cluster arrays in global memory
   VisionSorted vs{};
   // latency-bound windows read their normals from a table (k_noise)
   bool noise_table = false;
@@ -487,12 +488,18 @@ constexpr size_t kMaxLds = 160 * 1024;
 size_t global_lds_bytes(int lx, int ly) { return (16 + (size_t)(1 << (lx + ly)) + 1) * 4; }
 
 // Pair-list capacity of the cluster build: up to 3 N pairs (mean degree 6),
-// at least N, within the LDS left after the other arrays of k_cluster_build.
-int build_pair_cap(int n) {
+// at least N, within the LDS left after the other arrays of k_cluster_build;
+// 3 N in global memory for the large-N variant.
+int build_pair_cap(int n, bool big) {
+  if (big) return 3 * n;
   const size_t fixed = swarm::build_lds_words(n, 0) * 4;
   const size_t room = fixed < kMaxLds ? (kMaxLds - fixed) / 4 : 0;
   return (int)std::min<size_t>(room, 3 * (size_t)n);
 }
+
+// The LDS build needs room for at least N pairs; beyond that, the large-N
+// variant keeps only the union-find forest in LDS.
+bool build_is_big(int n) { return swarm::build_lds_words(n, n) * 4 > kMaxLds; }
 
 size_t build_lds_bytes(int n, int pair_cap) { return swarm::build_lds_words(n, pair_cap) * 4; }
 
@@ -507,7 +514,8 @@ void set_lds_attributes() {
   static bool done = false;
   if (done) return;
   const void* fns[] = {reinterpret_cast<const void*>(&swarm::k_global),
-                       reinterpret_cast<const void*>(&swarm::k_cluster_build),
+                       reinterpret_cast<const void*>(&swarm::k_cluster_build<false>),
+                       reinterpret_cast<const void*>(&swarm::k_cluster_build<true>),
                        reinterpret_cast<const void*>(&swarm::k_build_sort),
                        reinterpret_cast<const void*>(&swarm::k_check),
                        reinterpret_cast<const void*>(&k_grid_build),
@@ -535,8 +543,12 @@ int launch_build(swarm_engine* e, hipStream_t stream, int n_noise) {
   hipLaunchKernelGGL(swarm::k_build_pairs, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
                      dim3(256), 0, stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(swarm::k_cluster_build, dim3(e->n_envs), dim3(1024),
-                     build_lds_bytes(e->n, e->sc.pair_cap), stream, e->st, e->sc);
+  if (e->big_build)
+    hipLaunchKernelGGL(swarm::k_cluster_build<true>, dim3(e->n_envs), dim3(1024),
+                       swarm::build_lds_words_big(e->n) * 4, stream, e->st, e->sc);
+  else
+    hipLaunchKernelGGL(swarm::k_cluster_build<false>, dim3(e->n_envs), dim3(1024),
+                       build_lds_bytes(e->n, e->sc.pair_cap), stream, e->st, e->sc);
   HIP_TRY(hipGetLastError());
   if (e->noise_table && n_noise > 0) {
     const long ts = (long)e->n_envs * e->sc.S;
@@ -734,8 +746,10 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   }
   // the cluster path needs the build workgroup's LDS and a non-degenerate
   // build grid; otherwise every window runs on the global path
-  e->sc.pair_cap = build_pair_cap(n_particles);
+  e->big_build = build_is_big(n_particles);
+  e->sc.pair_cap = build_pair_cap(n_particles, e->big_build);
   e->cluster_path = e->sc.pair_cap >= n_particles && n_particles < 65536 &&
+                    swarm::build_lds_words_big(n_particles) * 4 <= kMaxLds &&
                     (size_t)(16 + (1 << (e->lxb + e->lyb)) + 1) * 4 <= kMaxLds &&
                     (1 << e->lxb) >= 3 && (1 << e->lyb) >= 3;
   const size_t M = (size_t)n_envs * n_particles;
@@ -776,6 +790,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->sc.bcstart, (size_t)n_envs * ((1 << (e->lxb + e->lyb)) + 1));
   rc = rc ? rc : dev_alloc(e, &e->sc.gplist, (size_t)n_envs * std::max(e->sc.pair_cap, 1));
   rc = rc ? rc : dev_alloc(e, &e->sc.gnpairs, (size_t)n_envs);
+  if (e->big_build) rc = rc ? rc : dev_alloc(e, &e->sc.gclus, 3 * M);
   rc = rc ? rc : dev_alloc(e, &e->sc.wave_npairs, (size_t)n_envs * (S / 64));
   rc = rc ? rc : dev_alloc(e, &e->sc.phase, 32);
   rc = rc ? rc : dev_alloc(e, &e->sc.disp, M);

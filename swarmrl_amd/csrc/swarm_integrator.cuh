@@ -101,6 +101,7 @@ struct Scratch {
   int32_t* bcstart;   // [E][ncb + 1] first sorted entry of every cell, [ncb] = N
   uint32_t* gplist;   // [E][pair_cap] neighbour pairs i | j << 16, i < j
   int32_t* gnpairs;   // [E] pairs found (may exceed pair_cap: overflow)
+  int32_t* gclus;     // [3][M] cluster sizes / bases / slots (large-N build only)
   int32_t pair_cap;   // pairs per env
   int32_t S;          // slots per env
   int32_t wmax;       // S / 64
@@ -595,9 +596,18 @@ __global__ __launch_bounds__(256) void k_build_pairs(const Derived* __restrict__
   }
 }
 
+// LDS words of the large-N variant: the union-find forest only.
+__host__ __device__ inline size_t build_lds_words_big(int n) {
+  const int wmax = slots_per_env(n) / 64;
+  return 16 + 16 + 68 + 68 + (size_t)((wmax + 3) & ~3) + (size_t)n;
+}
+
 // Build step 3, one workgroup per env: union-find over the pair list
 // (connected components = clusters), packing of the clusters into 64-lane
-// wave slots that never straddle a wave, per-wave pair lists.
+// wave slots that never straddle a wave, per-wave pair lists.  kBig: the
+// cluster sizes, bases, slots and the pair list stay in global memory (N
+// too large for them in LDS); the forest is always in LDS.
+template <bool kBig>
 __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
@@ -609,10 +619,12 @@ __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc)
   const int wmax = sc.wmax;
   int32_t* wave_np = wavebase + 68;                        // wmax (padded)
   int32_t* parent = wave_np + ((wmax + 3) & ~3);           // N
-  int32_t* csz = parent + N;                               // N
-  int32_t* cbase = csz + N;                                // N
-  int32_t* lslot = cbase + N;                              // N
-  uint32_t* plist = reinterpret_cast<uint32_t*>(lslot + N);  // pair_cap
+  const size_t M = (size_t)st.m;
+  int32_t* csz = kBig ? sc.gclus + base : parent + N;              // N
+  int32_t* cbase = kBig ? sc.gclus + M + base : parent + 2 * N;    // N
+  int32_t* lslot = kBig ? sc.gclus + 2 * M + base : parent + 3 * N;  // N
+  uint32_t* plist = kBig ? sc.gplist + (size_t)e * sc.pair_cap
+                         : reinterpret_cast<uint32_t*>(parent + 4 * N);  // pair_cap
   const int S = sc.S;
   SWARM_STAMP(2);
   const int found = sc.gnpairs[e];
@@ -624,7 +636,8 @@ __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc)
     parent[i] = i;
     csz[i] = 0;
   }
-  for (int k = tid; k < npairs; k += T) plist[k] = sc.gplist[(size_t)e * sc.pair_cap + k];
+  if (!kBig)
+    for (int k = tid; k < npairs; k += T) plist[k] = sc.gplist[(size_t)e * sc.pair_cap + k];
   __syncthreads();
   for (int k = tid; k < npairs; k += T) {
     const uint32_t pr = plist[k];

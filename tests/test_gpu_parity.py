@@ -331,3 +331,32 @@ def test_prebuild_on_side_stream_bit_exact(hint):
     h.integrate(100)
     st2, _, _ = oracle.bd_run(h.op, st2, np.zeros(n), f, t, 100, step0=step)
     _eq(h.download()[0], st2)
+
+
+def test_c5_16384_large_build_bit_exact():
+    """C5 size (16 384 colloids): the large-N cluster build (cluster arrays in
+    global memory) integrates a slice bit-exactly and without fallback."""
+    import ctypes
+
+    from gpu_harness import Harness, species_list
+
+    rng = np.random.default_rng(16)
+    n = 16384
+    L = 2 * np.sqrt(n / 0.1)
+    box = [L, L, L]
+    pos, dirs = _disc(rng, n, L)
+    st = oracle.state_from_positions(pos, dirs, box)
+    h = Harness(box, 1e-3, 1.0239, 1.0239, 3, species_list()[:1], np.zeros(n, int))
+    h.upload([st])
+    h.sd(300)
+    st, _ = oracle.sd_run(h.op, st, np.zeros(n), 300)
+    f = rng.choice([0.0, 10.0], n).astype(np.float32)
+    t = rng.choice([-10.0, 0.0, 10.0], n).astype(np.float32)
+    h.set_actions(f, t)
+    h.integrate(100)
+    ref, _, _ = oracle.bd_run(h.op, st, np.zeros(n), f, t, 100)
+    _eq(h.download()[0], ref)
+    fb = np.zeros(1, np.int32)
+    w = np.zeros(1, np.int32)
+    h.native.call("swarm_engine_window_stats", fb.ctypes.data, w.ctypes.data)
+    assert fb[0] == 0 and w[0] > 0, (fb, w)
