@@ -230,6 +230,16 @@ int swarm_engine_neighbor_pairs(swarm_engine_t *e, int32_t env, double cutoff,
                                 int32_t *pairs, int32_t max_pairs,
                                 int32_t *n_pairs);
 
+/* Pairwise scaled distances for ParticleSensing / SpeciesSearch
+ * (particle_sensing.py:95-121, species_search.py:97-130): for every env e,
+ * agent a < n_agents and sensed column m in [m0, m0 + mc),
+ *   out[e][m - m0][a] = || (fp32(x_sensed[m]) - fp32(x_agent[a])) / box_scale ||
+ * with unwrapped positions (no minimum image, as the reference).  Indices
+ * are device int32 into [0, N); out is device fp32 [E][mc][n_agents]. */
+int swarm_pair_distances(swarm_engine_t *e, const int32_t *agent_idx, int32_t n_agents,
+                         const int32_t *sensed_idx, int32_t m0, int32_t mc,
+                         const double box_scale[3], float *out);
+
 /* Fused action sampling for the device rollout path (all pointers device):
  * per agent a < n, over logits [n][k] fp32 (k <= 64):
  *   idx  = argmax_j(logits_j - log(-log u_j))     gumbel_distribution.py:37-40

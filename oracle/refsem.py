@@ -168,6 +168,26 @@ def gradient_reward(cur, prev, source, box_length, decay_fn, scale):
 
 
 # --------------------------------------------------- BD, deterministic (a3)
+def pair_field(positions, types, agent_indices, sensing_type, box_length, decay_fn):
+    """
+    particle_sensing.py:95-121 / species_search.py:97-130 in numpy fp32:
+    d = ||(x_j - x_i) / L|| over the sensed colloids (colloid order); the
+    first M - 1 non-zero distances, padded with index 0 when fewer
+    (jnp.nonzero(..., size=M - 1), fill 0); field = decay(d).sum().
+    """
+    pos = np.asarray(positions, dtype=np.float32)
+    box = np.asarray(box_length, dtype=np.float32)
+    test = pos[[j for j, t in enumerate(types) if t == sensing_type]]
+    m = len(test)
+    out = []
+    for i in agent_indices:
+        d = np.linalg.norm((test - pos[i]) / box, axis=-1).astype(np.float32)
+        nz = np.nonzero(d)[0][: m - 1]
+        idx = np.concatenate([nz, np.zeros(max(0, m - 1 - len(nz)), dtype=int)])
+        out.append(np.float32(np.sum(decay_fn(d[idx]), dtype=np.float32)))
+    return np.array(out, dtype=np.float32)
+
+
 def bd_free_deterministic(pos0, theta0, f_swim, torque_z, gamma_t, gamma_r, dt, n_steps):
     """kT = 0, no pair forces: x += f d(theta)/gamma_t dt, theta += tau/gamma_r dt."""
     pos = np.array(pos0, dtype=float)

@@ -103,6 +103,11 @@ _SIGNATURES = {
     "swarm_engine_prebuild": (ctypes.c_int, [_P, _P, ctypes.c_int32]),
     "swarm_engine_profile": (ctypes.c_int, [_P, ctypes.c_int32, _P, _P]),
     "swarm_engine_debug_phases": (ctypes.c_int, [_P, _P]),
+    "swarm_pair_distances": (
+        ctypes.c_int,
+        [_P, _P, ctypes.c_int32, _P, ctypes.c_int32, ctypes.c_int32,
+         ctypes.POINTER(ctypes.c_double), _P],
+    ),
     "swarm_sample_actions": (
         ctypes.c_int,
         [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, _P, ctypes.c_float, _P, _P, _P,

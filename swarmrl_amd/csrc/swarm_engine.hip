@@ -326,6 +326,51 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
     if (k < nb) o[k] = (float)acc[k] * 2.3283064365386963e-10f;
 }
 
+// ------------------------------------------------ pairwise field distances
+// For ParticleSensing / SpeciesSearch (particle_sensing.py:95-121,
+// species_search.py:97-130): d = || fp32(x_j) - fp32(x_i) || / L per agent
+// i and sensed colloid j (unwrapped positions, no minimum image), written
+// [E][mc][A] for sensed columns m0 .. m0 + mc - 1.  The sensed positions of
+// the block's column tile are staged in LDS once and read by all agents.
+__global__ __launch_bounds__(256) void k_pair_dist(DevState st, const double* __restrict__ box,
+                                                   const int32_t* __restrict__ agents,
+                                                   int n_agents,
+                                                   const int32_t* __restrict__ sensed, int m0,
+                                                   int mc, float b0, float b1, float b2,
+                                                   float* __restrict__ out) {
+  __shared__ float tile[256][3];
+  const int e = blockIdx.z;
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  const int N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const double inv32 = 1.0 / 4294967296.0;
+  float xi[3] = {0.0f, 0.0f, 0.0f};
+  if (a < n_agents) {
+    const size_t gi = base + agents[a];
+    for (int k = 0; k < 2; ++k)
+      xi[k] = (float)(((double)st.img[k * M + gi] + (double)st.q[k * M + gi] * inv32) * box[k]);
+  }
+  const int c0 = blockIdx.y * 256;
+  const int cn = min(256, mc - c0);
+  if (threadIdx.x < cn) {
+    const size_t gj = base + sensed[m0 + c0 + threadIdx.x];
+    for (int k = 0; k < 2; ++k)
+      tile[threadIdx.x][k] =
+          (float)(((double)st.img[k * M + gj] + (double)st.q[k * M + gj] * inv32) * box[k]);
+    tile[threadIdx.x][2] = 0.0f;
+  }
+  __syncthreads();
+  if (a >= n_agents) return;
+  const size_t A = (size_t)n_agents;
+  float* o = out + ((size_t)e * mc + c0) * A + a;
+  for (int c = 0; c < cn; ++c) {
+    const float dx = (tile[c][0] - xi[0]) / b0;
+    const float dy = (tile[c][1] - xi[1]) / b1;
+    const float dz = (tile[c][2] - xi[2]) / b2;
+    o[(size_t)c * A] = swarm::sqrt_rn(dx * dx + dy * dy + dz * dz);
+  }
+}
+
 // ------------------------------------------------------- field distance
 __global__ __launch_bounds__(256) void k_field(DevState st, const double* __restrict__ box,
                                                const int32_t* __restrict__ agents, int n_agents,
@@ -1130,6 +1175,22 @@ int swarm_field_transform(swarm_engine_t* e, const int32_t* agent_idx, int32_t n
                      agent_idx, n_agents, source[0], source[1], source[2], box_scale[0],
                      box_scale[1], box_scale[2], hist_q, hist_img, nullptr, nullptr, 1, 0,
                      e->n_envs, clip_at_zero ? 2 : 1, decay_a, decay_b, scale, out);
+  HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+
+int swarm_pair_distances(swarm_engine_t* e, const int32_t* agent_idx, int32_t n_agents,
+                         const int32_t* sensed_idx, int32_t m0, int32_t mc,
+                         const double box_scale[3], float* out) {
+  if (!e || !agent_idx || !sensed_idx || !box_scale || !out)
+    return fail(SWARM_EINVAL, "null argument");
+  if (m0 < 0 || mc < 0) return fail(SWARM_EINVAL, "negative sensed range");
+  if (n_agents <= 0 || mc == 0) return SWARM_OK;
+  const dim3 grid((unsigned)((n_agents + 255) / 256), (unsigned)((mc + 255) / 256),
+                  (unsigned)e->n_envs);
+  hipLaunchKernelGGL(k_pair_dist, grid, dim3(256), 0, e->stream, e->st, e->d_box, agent_idx,
+                     n_agents, sensed_idx, m0, mc, (float)box_scale[0], (float)box_scale[1],
+                     (float)box_scale[2], out);
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
 }

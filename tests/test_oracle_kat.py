@@ -296,3 +296,35 @@ def test_placement_restatement_draw_order():
     np.testing.assert_allclose(pos[0, :2], [50 + r * np.cos(th), 50 + r * np.sin(th)])
     np.testing.assert_allclose(dirs[0, :2], [np.cos(2 * np.pi * u[2]), np.sin(2 * np.pi * u[2])],
                                atol=1e-12)
+
+
+def test_refsem_pair_field_reference_kats():
+    """particle_sensing / species_search KATs (test_particle_sensing.py:46-121,
+    test_species_search.py:46-118): fields -2 and -sqrt(2)-1 for the unit
+    triangle with decay -x; approaching colloid 1 to (0, 0.5) gives +0.5."""
+    from oracle import refsem
+
+    pos = np.array([[0.0, 0.0, 0.0], [0.0, 1.0, 0.0], [1.0, 0.0, 0.0]])
+    f = refsem.pair_field(pos, [0, 0, 0], [0, 1, 2], 0, np.ones(3), lambda x: -1 * x)
+    assert f[0] == -2.0
+    assert f[1] == pytest.approx(-np.sqrt(2) - 1.0)
+    assert f[2] == pytest.approx(-np.sqrt(2) - 1.0)
+    pos2 = pos.copy()
+    pos2[1, 1] = 0.5
+    f2 = refsem.pair_field(pos2, [0, 0, 0], [0, 1, 2], 0, np.ones(3), lambda x: -1 * x)
+    assert f2[0] - f[0] == 0.5
+
+
+def test_refsem_pair_field_nonzero_size_quirk():
+    """jnp.nonzero(size=M-1): an agent that is not sensed keeps only the first
+    M-1 sensed colloids; coincident colloids pad with column 0."""
+    from oracle import refsem
+
+    pos = np.array([[0.0, 0.0, 0.0], [0.0, 1.0, 0.0], [2.0, 0.0, 0.0], [0.0, 0.0, 0.0]])
+    types = [0, 1, 1, 0]
+    # agent 0 (type 0) senses type 1: d = [1, 2] -> only the first (M-1 = 1)
+    f = refsem.pair_field(pos, types, [0], 1, np.ones(3), lambda x: x)
+    assert f[0] == 1.0
+    # sensing type 0 from agent 0: d = [0 (self), 0 (coincident)] -> pad with col 0
+    f = refsem.pair_field(pos, types, [0], 0, np.ones(3), lambda x: x + 10)
+    assert f[0] == 10.0
