@@ -246,14 +246,32 @@ int swarm_pair_distances(swarm_engine_t *e, const int32_t *agent_idx, int32_t n_
  *   idx  = RandomExploration(idx) when explore_p > 0 (random_exploration.py:54-71)
  *   logp = log(softmax(logits)_idx + 1e-8)         flax_network.py:185-192
  *   out_f = f_table[idx], out_t = t_table[idx]     actor_critic.py:159-184
- * u from Philox4x32-10 keyed by seed; state = 2 uint64 of device memory
- * (call counter, arrival ticket; zero-initialise once), advanced on every
- * call so graph replays draw fresh numbers.  Asynchronous on `stream`
- * (hipStream_t, NULL = default stream). */
+ * u from Philox4x32-10 keyed by seed; state = n_state >= ceil(n / 64) uint64
+ * call counters of device memory (one per group of 64 agents; zero-initialise
+ * once), advanced on every call so graph replays draw fresh numbers.
+ * Asynchronous on `stream` (hipStream_t, NULL = default stream).
+ * Replaces the jnp sampling chain of FlaxModel.compute_action. */
 int swarm_sample_actions(const float *logits, int32_t n, int32_t k, uint64_t seed,
-                         uint64_t *state, float explore_p, const float *f_table,
-                         const float *t_table, int64_t *out_idx, float *out_logp,
-                         float *out_f, float *out_t, void *stream);
+                         uint64_t *state, int32_t n_state, float explore_p,
+                         const float *f_table, const float *t_table, int64_t *out_idx,
+                         float *out_logp, float *out_f, float *out_t, void *stream);
+
+/* The whole rollout policy of FlaxModel.compute_action
+ * (networks/flax_network.py:153-195) for the reference's actor-critic MLP
+ * (Dense(hidden) -> ReLU -> Dense(k), CI/espresso_tests/integration_tests/
+ * test_rl_trainers.py:17-26) in one launch:
+ *   logits = W2 relu(W1 obs_a + b1) + b2        (fp32; torch Linear layouts
+ *            W1 [hidden][d_in], W2 [k][hidden], read in place)
+ * followed by exactly the sampling of swarm_sample_actions (same counters,
+ * same bits for the same logits).  obs [n][d_in]; d_in <= 16, hidden <= 256,
+ * k <= 16.  out_logits [n][k] is optional (NULL: not written).  The critic
+ * head is not evaluated (the rollout does not read it). */
+int swarm_policy_mlp_sample(const float *obs, int32_t n, int32_t d_in, const float *w1,
+                            const float *b1, int32_t hidden, const float *w2, const float *b2,
+                            int32_t k, uint64_t seed, uint64_t *state, int32_t n_state,
+                            float explore_p, const float *f_table, const float *t_table,
+                            int64_t *out_idx, float *out_logp, float *out_f, float *out_t,
+                            float *out_logits, void *stream);
 
 #ifdef __cplusplus
 }

@@ -110,8 +110,13 @@ _SIGNATURES = {
     ),
     "swarm_sample_actions": (
         ctypes.c_int,
-        [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, _P, ctypes.c_float, _P, _P, _P,
-         _P, _P, _P, _P],
+        [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, _P, ctypes.c_int32,
+         ctypes.c_float, _P, _P, _P, _P, _P, _P, _P],
+    ),
+    "swarm_policy_mlp_sample": (
+        ctypes.c_int,
+        [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_int32, _P, _P, ctypes.c_int32,
+         ctypes.c_uint64, _P, ctypes.c_int32, ctypes.c_float, _P, _P, _P, _P, _P, _P, _P, _P],
     ),
     "swarm_engine_step_count": (ctypes.c_int64, [_P]),
     "swarm_engine_window_stats": (ctypes.c_int, [_P, _P, _P]),

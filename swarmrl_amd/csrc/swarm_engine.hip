@@ -1230,19 +1230,72 @@ int swarm_engine_neighbor_pairs(swarm_engine_t* e, int32_t env, double cutoff, i
 }  // extern "C"
 
 int swarm_sample_actions(const float* logits, int32_t n, int32_t k, uint64_t seed,
-                         uint64_t* state, float explore_p, const float* f_table,
-                         const float* t_table, int64_t* out_idx, float* out_logp, float* out_f,
-                         float* out_t, void* stream) {
+                         uint64_t* state, int32_t n_state, float explore_p,
+                         const float* f_table, const float* t_table, int64_t* out_idx,
+                         float* out_logp, float* out_f, float* out_t, void* stream) {
   if (!logits || !state || !f_table || !t_table || !out_idx || !out_logp || !out_f || !out_t)
     return fail(SWARM_EINVAL, "null argument");
   if (k < 1 || k > swarm::kMaxActions) return fail(SWARM_ECAPACITY, "1 <= k <= 64 actions");
   if (!(explore_p >= 0.0f && explore_p <= 1.0f))
     return fail(SWARM_EINVAL, "exploration probability must be in [0, 1]");
   if (n <= 0) return SWARM_OK;
+  if (n_state < (n + 63) / 64) return fail(SWARM_EINVAL, "state needs ceil(n / 64) counters");
   hipLaunchKernelGGL(swarm::k_sample_actions, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), logits, n, k, (uint32_t)seed,
                      (uint32_t)(seed >> 32), reinterpret_cast<unsigned long long*>(state),
                      explore_p, f_table, t_table, out_idx, out_logp, out_f, out_t);
+  HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+
+int swarm_policy_mlp_sample(const float* obs, int32_t n, int32_t d_in, const float* w1,
+                            const float* b1, int32_t hidden, const float* w2, const float* b2,
+                            int32_t k, uint64_t seed, uint64_t* state, int32_t n_state,
+                            float explore_p, const float* f_table, const float* t_table,
+                            int64_t* out_idx, float* out_logp, float* out_f, float* out_t,
+                            float* out_logits, void* stream) {
+  if (!obs || !w1 || !b1 || !w2 || !b2 || !state || !f_table || !t_table || !out_idx ||
+      !out_logp || !out_f || !out_t)
+    return fail(SWARM_EINVAL, "null argument");
+  if (d_in < 1 || d_in > swarm::kMlpMaxIn) return fail(SWARM_ECAPACITY, "1 <= d_in <= 16");
+  if (hidden < 1 || hidden > swarm::kMlpMaxHidden)
+    return fail(SWARM_ECAPACITY, "1 <= hidden <= 256");
+  if (k < 1 || k > swarm::kMlpMaxActions) return fail(SWARM_ECAPACITY, "1 <= k <= 16 actions");
+  if (!(explore_p >= 0.0f && explore_p <= 1.0f))
+    return fail(SWARM_EINVAL, "exploration probability must be in [0, 1]");
+  if (n <= 0) return SWARM_OK;
+  if (n_state < (n + 63) / 64) return fail(SWARM_EINVAL, "state needs ceil(n / 64) counters");
+  // lanes per agent: enough waves to cover the SIMDs when agents are few
+  const int G = n <= 16384 ? 4 : (n <= 65536 ? 2 : 1);
+  const bool small_in = d_in <= 4, small_k = k <= 4;
+  const unsigned blocks = (unsigned)(((long)n * G + 255) / 256);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  auto* st = reinterpret_cast<unsigned long long*>(state);
+#define SWARM_MLP(GG, DD, KK)                                                                   \
+  hipLaunchKernelGGL((swarm::k_policy_mlp_sample<GG, DD, KK>), dim3(blocks), dim3(256),        \
+                     (size_t)(hidden * swarm::MlpRow<DD, KK>::kStride + KK) * sizeof(float), s, \
+                     obs, n, d_in, w1, b1, hidden, w2, b2, k, k0, k1, st, explore_p, f_table,  \
+                     t_table, out_idx, out_logp, out_f, out_t, out_logits)
+#define SWARM_MLP_G(GG)                 \
+  do {                                  \
+    if (small_in && small_k)            \
+      SWARM_MLP(GG, 4, 4);              \
+    else if (small_in)                  \
+      SWARM_MLP(GG, 4, 16);             \
+    else if (small_k)                   \
+      SWARM_MLP(GG, 16, 4);             \
+    else                                \
+      SWARM_MLP(GG, 16, 16);            \
+  } while (0)
+  if (G == 4)
+    SWARM_MLP_G(4);
+  else if (G == 2)
+    SWARM_MLP_G(2);
+  else
+    SWARM_MLP_G(1);
+#undef SWARM_MLP_G
+#undef SWARM_MLP
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
 }

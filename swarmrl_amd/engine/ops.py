@@ -284,13 +284,27 @@ def field_transform(native, n_envs: int, agent_idx: torch.Tensor, source, box_sc
     return out
 
 
+def counter_state(state, n: int, device):
+    """Device call counters of the sampling kernels: one int64 per group of
+    64 agents (grown, never shrunk; new groups start at zero)."""
+    need = max(1, (n + 63) // 64)
+    if state is None or state.device != device:
+        return torch.zeros(need, dtype=torch.int64, device=device)
+    if state.numel() < need:
+        grown = torch.zeros(need, dtype=torch.int64, device=device)
+        grown[: state.numel()] = state
+        return grown
+    return state
+
+
 def sample_actions(logits: torch.Tensor, seed: int, state: torch.Tensor, explore_p: float,
                    f_table: torch.Tensor, t_table: torch.Tensor):
     """
     Fused Gumbel-max sampling + exploration + log(softmax + 1e-8) of the
     chosen action + action-table lookup (swarm_sample_actions, one kernel on
-    the current stream).  logits [n, k] fp32 (device); state: int64[2] device
-    counter buffer.  Returns (idx int64 [n], log_prob [n], f_swim [n], torque_z [n]).
+    the current stream).  logits [n, k] fp32 (device); state: int64 device
+    counters, at least ceil(n / 64) (counter_state).  Returns
+    (idx int64 [n], log_prob [n], f_swim [n], torque_z [n]).
     """
     logits = logits.contiguous()
     n, k = logits.shape
@@ -302,6 +316,36 @@ def sample_actions(logits: torch.Tensor, seed: int, state: torch.Tensor, explore
     stream = torch.cuda.current_stream(dev).cuda_stream
     _capi.check(_capi.lib().swarm_sample_actions(
         logits.data_ptr(), n, k, ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), state.data_ptr(),
-        ctypes.c_float(explore_p), f_table.data_ptr(), t_table.data_ptr(), idx.data_ptr(),
-        logp.data_ptr(), f.data_ptr(), t.data_ptr(), ctypes.c_void_p(stream)))
+        int(state.numel()), ctypes.c_float(explore_p), f_table.data_ptr(), t_table.data_ptr(),
+        idx.data_ptr(), logp.data_ptr(), f.data_ptr(), t.data_ptr(), ctypes.c_void_p(stream)))
+    return idx, logp, f, t
+
+
+def policy_mlp_sample(obs: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor,
+                      b2: torch.Tensor, seed: int, state: torch.Tensor, explore_p: float,
+                      f_table: torch.Tensor, t_table: torch.Tensor, want_logits: bool = False):
+    """
+    The rollout policy in one kernel (swarm_policy_mlp_sample): actor logits
+    W2 relu(W1 obs + b1) + b2 from the torch Linear weights in place, then the
+    sampling of sample_actions (same counters and bits).  obs [n, d_in] fp32
+    device.  Returns (idx, log_prob, f_swim, torque_z[, logits]).
+    """
+    obs = obs.contiguous()
+    n, d_in = obs.shape
+    hidden, k = int(w1.shape[0]), int(w2.shape[0])
+    dev = obs.device
+    idx = torch.empty(n, dtype=torch.int64, device=dev)
+    logp = torch.empty(n, dtype=torch.float32, device=dev)
+    f = torch.empty(n, dtype=torch.float32, device=dev)
+    t = torch.empty(n, dtype=torch.float32, device=dev)
+    logits = torch.empty(n, k, dtype=torch.float32, device=dev) if want_logits else None
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _capi.check(_capi.lib().swarm_policy_mlp_sample(
+        obs.data_ptr(), n, d_in, w1.data_ptr(), b1.data_ptr(), hidden, w2.data_ptr(),
+        b2.data_ptr(), k, ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), state.data_ptr(),
+        int(state.numel()), ctypes.c_float(explore_p), f_table.data_ptr(), t_table.data_ptr(),
+        idx.data_ptr(), logp.data_ptr(), f.data_ptr(), t.data_ptr(),
+        logits.data_ptr() if want_logits else None, ctypes.c_void_p(stream)))
+    if want_logits:
+        return idx, logp, f, t, logits
     return idx, logp, f, t

@@ -38,6 +38,11 @@ class ActorCriticMLP(nn.Module):
         h = torch._addmm_activation(self.hidden.bias, x, self.hidden.weight.t())
         return self.actor(h)
 
+    def rollout_layers(self):
+        """(W1, b1, W2, b2) of the actor path, for the one-kernel rollout
+        policy (swarm_policy_mlp_sample)."""
+        return (self.hidden.weight, self.hidden.bias, self.actor.weight, self.actor.bias)
+
 
 class TorchModel:
     """Network wrapper with the FlaxModel surface used by the agents."""
@@ -123,14 +128,31 @@ class TorchModel:
 
         obs = observables.to(torch.float32)
         obs = obs.reshape(obs.shape[0], -1)
+        p = float(self.exploration_policy.probability)
+        self._fused_state = ops.counter_state(self._fused_state, obs.shape[0], obs.device)
+        layers = self._mlp_layers(obs.shape[1], int(f_table.numel()))
+        if layers is not None:  # stock MLP: network + sampling in one kernel
+            return ops.policy_mlp_sample(obs, *layers, self._fused_seed, self._fused_state, p,
+                                         f_table, t_table)
         if hasattr(self.model, "logits"):
             logits = self.model.logits(obs)
         else:
             logits, _ = self.model(obs)
-        if self._fused_state is None or self._fused_state.device != logits.device:
-            self._fused_state = torch.zeros(2, dtype=torch.int64, device=logits.device)
-        return ops.sample_actions(logits.float(), self._fused_seed, self._fused_state,
-                                  float(self.exploration_policy.probability), f_table, t_table)
+        return ops.sample_actions(logits.float(), self._fused_seed, self._fused_state, p,
+                                  f_table, t_table)
+
+    def _mlp_layers(self, d_in: int, k: int):
+        """The actor weights when the one-kernel policy applies (fp32 device
+        parameters within swarm_policy_mlp_sample's limits), else None."""
+        get = getattr(self.model, "rollout_layers", None)
+        if get is None:
+            return None
+        w1, b1, w2, b2 = get()
+        ok = all(t.dtype == torch.float32 and t.is_cuda and t.is_contiguous()
+                 for t in (w1, b1, w2, b2))
+        ok = ok and w1.shape[1] == d_in and w2.shape[0] == k and w2.shape[1] == w1.shape[0]
+        ok = ok and d_in <= 16 and w1.shape[0] <= 256 and k <= 16
+        return (w1, b1, w2, b2) if ok else None
 
     def update_model(self, loss: torch.Tensor):
         self.optimizer.zero_grad(set_to_none=True)
