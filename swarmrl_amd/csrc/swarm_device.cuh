@@ -198,11 +198,17 @@ __device__ __forceinline__ int64_t f2fix24(float v) {
   return __float2ll_rn(v);
 }
 
-// int64 -> fp32 round-to-nearest; when every lane's value fits int32 (the
-// common case, a wave-uniform test) one conversion instruction.
+// int64 -> fp32 round-to-nearest.  |a| < 2^53 (every realistic force sum):
+// hi * 2^32 + lo is exact in fp64, so one fp64 -> fp32 rounding gives the
+// correctly rounded value in four branch-free instructions; larger values
+// (never in practice) take the generic conversion behind a wave-uniform
+// branch.
 __device__ __forceinline__ float i64_to_f32(int64_t a) {
-  if (__all(a == (int64_t)(int32_t)a)) return (float)(int32_t)a;
-  return (float)a;
+  const double d = fma((double)(int32_t)(a >> 32), 4294967296.0, (double)(uint32_t)a);
+  float r = (float)d;
+  const bool big = a >= (int64_t)9007199254740992LL || a <= -(int64_t)9007199254740992LL;
+  if (__builtin_expect(__any(big), 0)) r = big ? (float)a : r;
+  return r;
 }
 
 // q + dq with the box crossing carried into the image counter: the high

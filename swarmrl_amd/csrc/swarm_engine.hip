@@ -817,7 +817,18 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->d_step, 1);
   rc = rc ? rc : dev_alloc(e, &e->d_arrive, 1);
   // integrator scratch
-  const int S = swarm::slots_per_env(n_particles);
+  // latency-bound launches (few envs x particles fill few SIMDs): one pair
+  // pass per wave and sub-step (k_cluster_build), normals from a table
+  // (k_noise).  Overrides: SWARMRL_AMD_ONE_PASS / SWARMRL_AMD_NOISE_TABLE=0|1.
+  const bool latency_bound = (long)n_envs * n_particles <= 32768;
+  {
+    const char* ov = std::getenv("SWARMRL_AMD_ONE_PASS");
+    bool want = latency_bound;
+    if (ov && ov[0] == '0') want = false;
+    if (ov && ov[0] == '1') want = true;
+    e->sc.one_pass = want ? 1 : 0;
+  }
+  const int S = swarm::slots_per_env(n_particles, e->sc.one_pass != 0);
   e->sc.S = S;
   e->sc.wmax = S / 64;
   rc = rc ? rc : dev_alloc(e, &e->sc.sqx, M);
@@ -848,7 +859,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   // SWARMRL_AMD_NOISE_TABLE=0|1.
   {
     const char* ov = std::getenv("SWARMRL_AMD_NOISE_TABLE");
-    bool want = (long)n_envs * n_particles <= 32768;
+    bool want = latency_bound;
     if (ov && ov[0] == '0') want = false;
     if (ov && ov[0] == '1') want = true;
     e->noise_table = want && e->derived.noisy && e->cluster_path;

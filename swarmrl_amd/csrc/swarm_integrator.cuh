@@ -42,8 +42,12 @@ constexpr int kMaxWindow = 128;   // sub-steps per cluster window
 constexpr int kPairsPerWave = 256;  // neighbour pairs of one 64-lane wave (4 passes)
 
 // Wave slots per env: every cluster packs into one wave, worst case 2 N
-// slots plus per-size-class rounding.
-__host__ __device__ inline int slots_per_env(int n) { return 2 * n + 64 * 66; }
+// slots plus per-size-class rounding.  One-pass packing (latency-bound
+// launches, see k_cluster_build) reserves up to 2 s lanes for a cluster of
+// s particles: worst case 4 N.
+__host__ __device__ inline int slots_per_env(int n, bool one_pass = false) {
+  return (one_pass ? 4 : 2) * n + 64 * 66;
+}
 constexpr float kAngInvScale = 683565275.57643158f;  // 2^32 / (2 pi)
 
 // fp32 constants derived from swarm_params_t (same derivation as the oracle).
@@ -103,6 +107,7 @@ struct Scratch {
   int32_t* gnpairs;   // [E] pairs found (may exceed pair_cap: overflow)
   int32_t* gclus;     // [3][M] cluster sizes / bases / slots (large-N build only)
   int32_t pair_cap;   // pairs per env
+  int32_t one_pass;   // 1: pack clusters so that a wave has <= 64 pairs
   int32_t S;          // slots per env
   int32_t wmax;       // S / 64
   uint64_t* phase;    // [32] build phase stamps (SWARM_PHASE_TIMING builds only)
@@ -486,7 +491,7 @@ __device__ __forceinline__ void uf_union(int32_t* parent, int a, int b) {
 // LDS words of k_cluster_build: 168 fixed + per-wave pair counters +
 // parent[N] + 3 N (cluster sizes, bases, slots) + the env's pair list.
 __host__ __device__ inline size_t build_lds_words(int n, int pair_cap) {
-  const int wmax = slots_per_env(n) / 64;
+  const int wmax = slots_per_env(n, true) / 64;  // either packing
   return 16 + 16 + 68 + 68 + (size_t)((wmax + 3) & ~3) + 4 * (size_t)n + (size_t)pair_cap;
 }
 
@@ -598,7 +603,7 @@ __global__ __launch_bounds__(256) void k_build_pairs(const Derived* __restrict__
 
 // LDS words of the large-N variant: the union-find forest only.
 __host__ __device__ inline size_t build_lds_words_big(int n) {
-  const int wmax = slots_per_env(n) / 64;
+  const int wmax = slots_per_env(n, true) / 64;  // either packing
   return 16 + 16 + 68 + 68 + (size_t)((wmax + 3) & ~3) + (size_t)n;
 }
 
@@ -635,6 +640,7 @@ __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc)
   for (int i = tid; i < N; i += T) {
     parent[i] = i;
     csz[i] = 0;
+    cbase[i] = 0;  // pair count of a cluster (one-pass packing), then its base
   }
   if (!kBig)
     for (int k = tid; k < npairs; k += T) plist[k] = sc.gplist[(size_t)e * sc.pair_cap + k];
@@ -648,14 +654,23 @@ __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc)
   for (int i = tid; i < N; i += T) parent[i] = uf_find(parent, i);
   __syncthreads();
   for (int i = tid; i < N; i += T) lslot[i] = atomicAdd(&csz[parent[i]], 1);
+  if (sc.one_pass)
+    for (int k = tid; k < npairs; k += T) atomicAdd(&cbase[parent[plist[k] & 0xffffu]], 1);
   __syncthreads();
+  // Lanes reserved per cluster (its packing class w): its size s, or with
+  // one-pass packing max(s, min(pairs, 64, 2 s)), so that the clusters of a
+  // wave have at most 64 pairs (one pair pass per sub-step) unless a cluster
+  // is denser than 2 pairs per particle.  Results do not depend on it.
   for (int i = tid; i < N; i += T) {
     if (parent[i] != i) continue;
     const int s = csz[i];
-    if (s > 64)
+    if (s > 64) {
       misc[0] = 1;  // cluster wider than a wave -> global path for this env
-    else
-      cbase[i] = atomicAdd(&classcnt[s], 1);
+    } else {
+      const int w = sc.one_pass ? max(s, min(min(cbase[i], 64), 2 * s)) : s;
+      csz[i] = w;
+      cbase[i] = atomicAdd(&classcnt[w], 1);
+    }
   }
   __syncthreads();
   SWARM_STAMP(4);

@@ -19,7 +19,17 @@ import sys
 
 tag = sys.argv[1]
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
-S = 2 * N + 64 * 66  # wave slots per env (swarm_engine.hip)
+
+
+def envs_of_grid(g):
+    """Envs of a k_cluster_run launch of g threads: ceil(E * wmax / 4) blocks
+    of 256, wmax = slots_per_env / 64 (dense: 2 N, one-pass: 4 N slots)."""
+    for E in range(1, 4097):
+        for slots in (2 * N + 64 * 66, 4 * N + 64 * 66):
+            if (E * (slots // 64) + 3) // 4 * 256 == g:
+                return E
+    return None
+
 src = f"gpurun_out/prof_{tag}"
 dst = "profiles"
 shutil.copy(f"{src}/trace/run_kernel_stats.csv", f"{dst}/{tag}_kernel_stats.csv")
@@ -50,7 +60,7 @@ traffic = []
 for (k, g), cs in acc.items():
     if "k_cluster_run" not in k or not cs.get("FETCH_SIZE") or not cs.get("WRITE_SIZE"):
         continue
-    E = round(g / S)
+    E = envs_of_grid(g)
     fetch_kb = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"])
     write_kb = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"])
     traffic.append({
