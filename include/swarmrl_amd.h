@@ -154,16 +154,21 @@ int swarm_engine_remove_overlap(swarm_engine_t *e, int32_t n_steps,
 int swarm_engine_integrate(swarm_engine_t *e, int32_t n_steps);
 
 /* Launch the next integration window's position-only preparation (cluster
- * decomposition, and the noise table for min(n_steps_hint, 128) sub-steps
- * when the engine uses one) on `stream` (a hipStream_t; NULL = engine
- * stream), so it can overlap the observable and policy work that produces
- * the slice's actions (espresso.py:1253-1306: manage_forces precedes
- * integrator.run and cannot change positions).  The caller orders `stream`
- * after the last position change and the engine stream after `stream`
- * (events); the next swarm_engine_integrate consumes the preparation.  Any
- * position change in between (upload, remove_overlap) discards it.  No-op
- * for engines on the global path. */
+ * decomposition) on `stream` (a hipStream_t; NULL = engine stream), so it
+ * can overlap the observable and policy work that produces the slice's
+ * actions (espresso.py:1253-1306: manage_forces precedes integrator.run and
+ * cannot change positions).  The caller orders `stream` after the last
+ * position change and the engine stream after `stream` (events); the next
+ * swarm_engine_integrate consumes the preparation.  Any position change in
+ * between (upload, remove_overlap) discards it.  No-op for engines on the
+ * global path.  n_steps_hint is unused (kept for the noise variant below). */
 int swarm_engine_prebuild(swarm_engine_t *e, void *stream, int32_t n_steps_hint);
+
+/* Same contract for the noise table of latency-bound engines: the normals
+ * of the next min(n_steps_hint, 128) sub-steps, computed on `stream` (it
+ * depends on the step counter only, so it may run beside the build).  No-op
+ * for engines without a noise table. */
+int swarm_engine_prebuild_noise(swarm_engine_t *e, void *stream, int32_t n_steps_hint);
 
 /* Diagnostics of the last integration window, per env (host arrays [E],
  * either may be NULL): fallback 0 = cluster path, 1 = flagged by the build

@@ -218,16 +218,95 @@ __global__ __launch_bounds__(1024) void k_vision_grid(DevState st, swarm_vision_
 // One group of G lanes per cell-sorted particle (neighbouring groups share
 // candidate cells, so their record loads coalesce); groups of particles
 // that are not agents exit.  The candidates of the 3x3 cell stencil form one
-// flat index range that the G lanes split; each lane keeps NB bins
-// (>= n_cones * n_types) of 2^-32 fixed-point amplitude in registers, and
-// the group adds them with xor-shuffles.  Integer sums make the result
-// independent of G and of the visiting order.
+// flat index range that the G lanes split.  Two phases, so that the lanes of
+// a wave stay converged: a cheap range test over the candidates appends the
+// hits to a per-lane list in LDS, and the cone arithmetic (sqrt, divisions,
+// acos) then runs over the hits only, four at a time; a full list is drained
+// early.  Each lane keeps NB bins (>= n_cones * n_types) of 2^-32
+// fixed-point amplitude in registers, and the group adds them with
+// xor-shuffles.  Integer sums make the result independent of G, of the
+// visiting order and of the phase split.
+constexpr int kVisionHits = 16;  // per-lane hit list (LDS, [kVisionHits][256])
+
+struct VisionLane {
+  uint32_t qxi, qyi;
+  int32_t ixi, iyi;
+  int i;
+  float mx, my, sx0, sx1, R;
+};
+
+// The in-range test of one candidate record (shared by both phases).
+__device__ __forceinline__ bool vision_offsets(const VisionLane& L, const uint4& c0, float* dx,
+                                               float* dy) {
+  const int64_t dqx = ((int64_t)((int32_t)c0.z - L.ixi) * (int64_t)4294967296LL) +
+                      ((int64_t)c0.x - (int64_t)L.qxi);
+  const int64_t dqy = ((int64_t)((int32_t)c0.w - L.iyi) * (int64_t)4294967296LL) +
+                      ((int64_t)c0.y - (int64_t)L.qyi);
+  // unwrapped separations beyond half a box are never within range
+  // (vision_range < L/2): skip them and convert the rest from int32, whose
+  // conversion is a single exact-rounding instruction.
+  if (dqx < -2147483647LL || dqx > 2147483647LL || dqy < -2147483647LL || dqy > 2147483647LL)
+    return false;
+  *dx = (float)(int32_t)dqx * L.sx0;
+  *dy = (float)(int32_t)dqy * L.sx1;
+  const float dist2 = *dx * *dx + *dy * *dy;
+  // conservative pre-test on dist^2 (the exact test is on the fp32 sqrt)
+  return dist2 < L.R * L.R * 1.0001f && dist2 != 0.0f;
+}
+
+template <int NB>
+__device__ __forceinline__ void vision_hit(const VisionLane& L, const swarm_vision_params_t& vp,
+                                           const uint4& c0, const uint4& c1, int64_t* acc) {
+  float dx, dy;
+  if (!vision_offsets(L, c0, &dx, &dy)) return;
+  const int ti = (int)c1.z;
+  if (ti < 0 || (int)c1.y == L.i) return;
+  const float dist = swarm::sqrt_rn(dx * dx + dy * dy);
+  if (!(dist < L.R)) return;
+  float amp = (2.0f * __uint_as_float(c1.x)) / dist;
+  amp = fminf(1.0f, amp);
+  const float ux = dx / dist, uy = dy / dist;
+  float dot = ux * L.mx + uy * L.my;
+  dot = fminf(fmaxf(dot, -1.0f), 1.0f);
+  float an = swarm::acosf_fixed(dot);
+  const float orth = ux * (-L.my) + uy * L.mx;
+  if (orth < 0.0f) an = -an;
+  const int64_t fixed = __float2ll_rn(amp * 4294967296.0f);
+  int bin = -1;
+  for (int k = 0; k < vp.n_cones; ++k)
+    if (vp.rims[k] < an && an < vp.rims[k + 1]) bin = k * vp.n_types + ti;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) acc[b] += (b == bin) ? fixed : 0;
+}
+
+// Cone arithmetic over a lane's listed hits, records fetched four at a time.
+template <int NB>
+__device__ __forceinline__ void vision_drain(const VisionLane& L, const swarm_vision_params_t& vp,
+                                             const uint4* __restrict__ rec, size_t base,
+                                             const uint32_t (*hits)[256], int nh, int64_t* acc) {
+  for (int k0 = 0; __any(k0 < nh); k0 += 4) {  // over the active lanes' longest list
+    uint4 c0[4], c1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (k0 + u < nh) {
+        const size_t jj = base + hits[k0 + u][threadIdx.x];
+        c0[u] = rec[2 * jj];
+        c1[u] = rec[2 * jj + 1];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (k0 + u < nh) vision_hit<NB>(L, vp, c0[u], c1[u], acc);
+  }
+}
+
 template <int NB, int G>
 __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __restrict__ d,
                                                 swarm_vision_params_t vp, int lx, int ly,
                                                 const int32_t* __restrict__ start, VisionSorted vs,
                                                 int n_agents, float* __restrict__ out,
                                                 int n_envs) {
+  __shared__ uint32_t hits[kVisionHits][256];
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int grp = t / G, sub = t & (G - 1);
   const int N = st.n;
@@ -236,15 +315,22 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
   const size_t base = (size_t)e * N;
   const uint4 own0 = vs.rec[2 * (base + ps)];
   const uint4 own1 = vs.rec[2 * (base + ps) + 1];
-  const int i = (int)own1.y;
-  const int row = vs.agent_row[i];
+  VisionLane L;
+  L.i = (int)own1.y;
+  const int row = vs.agent_row[L.i];
   if (row < 0) return;
-  const uint32_t qxi = own0.x, qyi = own0.y;
-  const int32_t ixi = (int32_t)own0.z, iyi = (int32_t)own0.w;
+  L.qxi = own0.x;
+  L.qyi = own0.y;
+  L.ixi = (int32_t)own0.z;
+  L.iyi = (int32_t)own0.w;
   float sn, cs;
-  swarm::sincos_turn(st.ang[base + i], &sn, &cs);
+  swarm::sincos_turn(st.ang[base + L.i], &sn, &cs);
   const float nm = swarm::sqrt_rn(cs * cs + sn * sn);
-  const float mx = cs / nm, my = sn / nm;
+  L.mx = cs / nm;
+  L.my = sn / nm;
+  L.sx0 = d->sx[0];
+  L.sx1 = d->sx[1];
+  L.R = vp.vision_range;
   const int nb = vp.n_cones * vp.n_types;
   int64_t acc[NB];
 #pragma unroll
@@ -253,15 +339,12 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
   const int ncx = 1 << lx, ncy = 1 << ly;
   const int lox = ncx >= 3 ? -1 : 0, hix = ncx >= 3 ? 1 : ncx - 1;
   const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
-  const int cc0 = cell_index(qxi, qyi, lx, ly);
+  const int cc0 = cell_index(L.qxi, L.qyi, lx, ly);
   const int cx = cc0 & (ncx - 1), cy = cc0 >> lx;
   const int32_t* so = start + (size_t)e * (ncell + 1);
-  const float sx0 = d->sx[0], sx1 = d->sx[1];
-  const float R = vp.vision_range;
-  // conservative pre-test on dist^2 (the exact test below is on fp32 sqrt)
-  const float R2pad = R * R * 1.0001f;
+  int nh = 0;
   int skip = sub;  // offset of this lane's next flat index past the current cell
-#pragma unroll
+#pragma unroll 1
   for (int r = 0; r < 9; ++r) {
     const int oy = r / 3 - 1, ox = r % 3 - 1;
     int jb = 0, je = 0;
@@ -274,42 +357,16 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
     }
     int jj = jb + skip;
     for (; jj < je; jj += G) {
-      const uint4 c0 = vs.rec[2 * (base + jj)];
-      const int64_t dqx = ((int64_t)((int32_t)c0.z - ixi) * (int64_t)4294967296LL) +
-                          ((int64_t)c0.x - (int64_t)qxi);
-      const int64_t dqy = ((int64_t)((int32_t)c0.w - iyi) * (int64_t)4294967296LL) +
-                          ((int64_t)c0.y - (int64_t)qyi);
-      // unwrapped separations beyond half a box are never within range
-      // (vision_range < L/2): skip them and convert the rest from int32,
-      // whose conversion is a single exact-rounding instruction.
-      if (dqx < -2147483647LL || dqx > 2147483647LL || dqy < -2147483647LL ||
-          dqy > 2147483647LL)
-        continue;
-      const float dx = (float)(int32_t)dqx * sx0, dy = (float)(int32_t)dqy * sx1;
-      const float dist2 = dx * dx + dy * dy;
-      if (!(dist2 < R2pad) || dist2 == 0.0f) continue;
-      const uint4 c1 = vs.rec[2 * (base + jj) + 1];
-      const int ti = (int)c1.z;
-      if (ti < 0 || (int)c1.y == i) continue;
-      const float dist = swarm::sqrt_rn(dist2);
-      if (!(dist < R)) continue;
-      float amp = (2.0f * __uint_as_float(c1.x)) / dist;
-      amp = fminf(1.0f, amp);
-      const float ux = dx / dist, uy = dy / dist;
-      float dot = ux * mx + uy * my;
-      dot = fminf(fmaxf(dot, -1.0f), 1.0f);
-      float an = swarm::acosf_fixed(dot);
-      const float orth = ux * (-my) + uy * mx;
-      if (orth < 0.0f) an = -an;
-      const int64_t fixed = __float2ll_rn(amp * 4294967296.0f);
-      int bin = -1;
-      for (int k = 0; k < vp.n_cones; ++k)
-        if (vp.rims[k] < an && an < vp.rims[k + 1]) bin = k * vp.n_types + ti;
-#pragma unroll
-      for (int b = 0; b < NB; ++b) acc[b] += (b == bin) ? fixed : 0;
+      float dx, dy;
+      if (vision_offsets(L, vs.rec[2 * (base + jj)], &dx, &dy)) hits[nh++][threadIdx.x] = jj;
+      if (__any(nh == kVisionHits)) {  // a full list: drain every lane's
+        vision_drain<NB>(L, vp, vs.rec, base, hits, nh, acc);
+        nh = 0;
+      }
     }
     skip = jj - je;
   }
+  vision_drain<NB>(L, vp, vs.rec, base, hits, nh, acc);
 #pragma unroll
   for (int off = G / 2; off > 0; off >>= 1) {
 #pragma unroll
@@ -506,6 +563,8 @@ struct swarm_engine {
   // swarm_engine_prebuild: the next window's build (and noise table) were
   // launched ahead on another stream from the current positions
   bool prebuilt = false;
+  // swarm_engine_prebuild_noise: the next window's noise table for this many
+  // sub-steps was launched ahead (on a stream of the caller's)
   int prebuilt_noise_steps = 0;
   // swarm_engine_profile: HIP events around every k_cluster_run launch
   bool profile = false;
@@ -579,8 +638,18 @@ int launch_global(swarm_engine* e, int n_steps, int sd_mode, float g, float md) 
   return SWARM_OK;
 }
 
-// Cluster build (+ noise table for n_noise sub-steps) of the next window.
-int launch_build(swarm_engine* e, hipStream_t stream, int n_noise) {
+// Noise table (latency-bound windows) for n sub-steps from the current
+// step counter.
+int launch_noise(swarm_engine* e, hipStream_t stream, int n) {
+  const long M = (long)e->n_envs * e->n;
+  hipLaunchKernelGGL(swarm::k_noise, dim3((unsigned)((M + 255) / 256), (unsigned)n), dim3(256), 0,
+                     stream, e->d_derived, e->st, e->d_step, e->d_noise);
+  HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+
+// Cluster build of the next window.
+int launch_build(swarm_engine* e, hipStream_t stream) {
   const int ncb = 1 << (e->lxb + e->lyb);
   hipLaunchKernelGGL(swarm::k_build_sort, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4, stream,
                      e->st, e->sc, e->lxb, e->lyb);
@@ -595,28 +664,20 @@ int launch_build(swarm_engine* e, hipStream_t stream, int n_noise) {
     hipLaunchKernelGGL(swarm::k_cluster_build<false>, dim3(e->n_envs), dim3(1024),
                        build_lds_bytes(e->n, e->sc.pair_cap), stream, e->st, e->sc);
   HIP_TRY(hipGetLastError());
-  if (e->noise_table && n_noise > 0) {
-    const long ts = (long)e->n_envs * e->sc.S;
-    hipLaunchKernelGGL(swarm::k_noise, dim3((unsigned)((ts + 255) / 256), (unsigned)n_noise),
-                       dim3(256), 0, stream, e->d_derived, e->sc, e->n_envs, e->d_step,
-                       e->d_noise);
-    HIP_TRY(hipGetLastError());
-  }
   return SWARM_OK;
 }
 
 // One integration window: cluster build -> cluster run -> check/fallback.
-// use_prebuilt: the build (and noise for prebuilt_noise_steps) ran already.
-int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt) {
+// use_prebuilt: the build ran already; noise_ready: the noise table holds
+// this many sub-steps from the current counter.
+int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_ready) {
   if (!use_prebuilt) {
-    const int rc = launch_build(e, e->stream, n_steps);
+    const int rc = launch_build(e, e->stream);
     if (rc) return rc;
-  } else if (e->noise_table && n_steps > e->prebuilt_noise_steps) {
-    const long ts = (long)e->n_envs * e->sc.S;
-    hipLaunchKernelGGL(swarm::k_noise, dim3((unsigned)((ts + 255) / 256), (unsigned)n_steps),
-                       dim3(256), 0, e->stream, e->d_derived, e->sc, e->n_envs, e->d_step,
-                       e->d_noise);
-    HIP_TRY(hipGetLastError());
+  }
+  if (e->noise_table && n_steps > noise_ready) {
+    const int rc = launch_noise(e, e->stream, n_steps);
+    if (rc) return rc;
   }
   const long waves = (long)e->n_envs * e->sc.wmax;
   const dim3 run_grid((unsigned)((waves + 3) / 4)), run_block(256);
@@ -656,12 +717,16 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt) {
 
 int run_bd(swarm_engine* e, int n_steps) {
   bool pre = e->prebuilt;
+  int noise_ready = e->prebuilt_noise_steps;
   e->prebuilt = false;
+  e->prebuilt_noise_steps = 0;
   while (n_steps > 0) {
     const int w = std::min(n_steps, swarm::kMaxWindow);
-    const int rc = e->cluster_path ? launch_window(e, w, pre) : launch_global(e, w, 0, 0.0f, 0.0f);
+    const int rc = e->cluster_path ? launch_window(e, w, pre, noise_ready)
+                                   : launch_global(e, w, 0, 0.0f, 0.0f);
     if (rc) return rc;
     pre = false;
+    noise_ready = 0;
     n_steps -= w;
   }
   return SWARM_OK;
@@ -817,13 +882,15 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->d_step, 1);
   rc = rc ? rc : dev_alloc(e, &e->d_arrive, 1);
   // integrator scratch
-  // latency-bound launches (few envs x particles fill few SIMDs): one pair
-  // pass per wave and sub-step (k_cluster_build), normals from a table
-  // (k_noise).  Overrides: SWARMRL_AMD_ONE_PASS / SWARMRL_AMD_NOISE_TABLE=0|1.
+  // One pair pass per wave and sub-step (k_cluster_build): the run kernel
+  // lasts as long as its slowest waves, at any env count.  Latency-bound
+  // launches (few envs x particles fill few SIMDs) also read their normals
+  // from a table (k_noise).  Overrides: SWARMRL_AMD_ONE_PASS /
+  // SWARMRL_AMD_NOISE_TABLE=0|1.
   const bool latency_bound = (long)n_envs * n_particles <= 32768;
   {
     const char* ov = std::getenv("SWARMRL_AMD_ONE_PASS");
-    bool want = latency_bound;
+    bool want = true;
     if (ov && ov[0] == '0') want = false;
     if (ov && ov[0] == '1') want = true;
     e->sc.one_pass = want ? 1 : 0;
@@ -864,7 +931,8 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     if (ov && ov[0] == '1') want = true;
     e->noise_table = want && e->derived.noisy && e->cluster_path;
     if (e->noise_table)
-      rc = rc ? rc : dev_alloc(e, &e->d_noise, (size_t)swarm::kMaxWindow * 3 * n_envs * S);
+      rc = rc ? rc : dev_alloc(e, &e->d_noise, (size_t)swarm::kMaxWindow * 3 * M);
+
   }
   set_lds_attributes();
   if (rc) {
@@ -907,7 +975,7 @@ int swarm_engine_set_stream(swarm_engine_t* e, void* stream) {
 
 int swarm_engine_upload_raw(swarm_engine_t* e, const uint32_t* q, const int32_t* img,
                             const uint32_t* ang) {
-  if (e) e->prebuilt = false;
+  if (e) e->prebuilt = false, e->prebuilt_noise_steps = 0;
   if (!e || !q || !img || !ang) return fail(SWARM_EINVAL, "null argument");
   const size_t M = (size_t)e->st.m;
   HIP_TRY(hipMemcpyAsync(e->st.q, q, 3 * M * sizeof(uint32_t), hipMemcpyHostToDevice, e->stream));
@@ -1017,6 +1085,7 @@ int swarm_engine_set_directors(swarm_engine_t* e, const double* dir, const uint8
 int swarm_engine_remove_overlap(swarm_engine_t* e, int32_t n_steps, double gamma, double max_disp) {
   if (!e) return fail(SWARM_EINVAL, "null engine");
   e->prebuilt = false;
+  e->prebuilt_noise_steps = 0;
   if (n_steps <= 0) return SWARM_OK;
   return launch_global(e, n_steps, 1, (float)gamma, (float)max_disp);
 }
@@ -1057,12 +1126,20 @@ int swarm_engine_prebuild(swarm_engine_t* e, void* stream, int32_t n_steps_hint)
   if (!e) return fail(SWARM_EINVAL, "null engine");
   if (n_steps_hint < 0) return fail(SWARM_EINVAL, "n_steps_hint must be >= 0");
   if (!e->cluster_path) return SWARM_OK;  // the global path has no build step
-  const int n_noise = std::min<int>(n_steps_hint, swarm::kMaxWindow);
-  const int rc = launch_build(e, stream ? reinterpret_cast<hipStream_t>(stream) : e->stream,
-                              n_noise);
+  const int rc = launch_build(e, stream ? reinterpret_cast<hipStream_t>(stream) : e->stream);
   if (rc) return rc;
   e->prebuilt = true;
-  e->prebuilt_noise_steps = e->noise_table ? n_noise : 0;
+  return SWARM_OK;
+}
+
+int swarm_engine_prebuild_noise(swarm_engine_t* e, void* stream, int32_t n_steps_hint) {
+  if (!e) return fail(SWARM_EINVAL, "null engine");
+  if (n_steps_hint < 0) return fail(SWARM_EINVAL, "n_steps_hint must be >= 0");
+  if (!e->noise_table || n_steps_hint == 0) return SWARM_OK;
+  const int n = std::min<int>(n_steps_hint, swarm::kMaxWindow);
+  const int rc = launch_noise(e, stream ? reinterpret_cast<hipStream_t>(stream) : e->stream, n);
+  if (rc) return rc;
+  e->prebuilt_noise_steps = n;
   return SWARM_OK;
 }
 

@@ -492,50 +492,82 @@ __device__ __forceinline__ void uf_union(int32_t* parent, int a, int b) {
 // parent[N] + 3 N (cluster sizes, bases, slots) + the env's pair list.
 __host__ __device__ inline size_t build_lds_words(int n, int pair_cap) {
   const int wmax = slots_per_env(n, true) / 64;  // either packing
-  return 16 + 16 + 68 + 68 + (size_t)((wmax + 3) & ~3) + 4 * (size_t)n + (size_t)pair_cap;
+  return 16 + 16 + 3 * 68 + (size_t)((wmax + 3) & ~3) + 4 * (size_t)n + (size_t)pair_cap;
 }
 
 // Build step 1, one workgroup per env: counting sort into cells of side
 // >= rc_max + skin (global arrays for the chip-wide pair search).
 __global__ __launch_bounds__(1024) void k_build_sort(DevState st, Scratch sc, int lx, int ly) {
   extern __shared__ __align__(16) unsigned char smem[];
+  constexpr int CH = 4;  // particles per thread kept in registers across the scan
   const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly);
   int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
   int32_t* cnt = wave_sums + 16;
   SWARM_STAMP(0);
+  // all loads of the cached particles first (one memory latency, not CH)
+  uint32_t cqx[CH], cqy[CH];
+  int32_t cid[CH];
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int i = tid + k * T;
+    const bool ok = i < N;
+    cqx[k] = ok ? st.q[base + i] : 0u;
+    cqy[k] = ok ? st.q[M + base + i] : 0u;
+    cid[k] = ok ? (i | ((int32_t)st.species[i] << 24)) : -1;
+  }
   for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
-  for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
   if (tid == 0) sc.gnpairs[e] = 0;
   __syncthreads();
-  for (int i = tid; i < N; i += T)
+  SWARM_STAMP(1);
+#pragma unroll
+  for (int k = 0; k < CH; ++k)
+    if (cid[k] >= 0) atomicAdd(&cnt[cell_index(cqx[k], cqy[k], lx, ly)], 1);
+  for (int i = tid + CH * T; i < N; i += T)
     atomicAdd(&cnt[cell_index(st.q[base + i], st.q[M + base + i], lx, ly)], 1);
   __syncthreads();
+  SWARM_STAMP(2);
   block_exclusive_scan(cnt, ncell, wave_sums);
   __syncthreads();
+  SWARM_STAMP(3);
   int32_t* cs = sc.bcstart + (size_t)e * (ncell + 1);
   for (int c = tid; c <= ncell; c += T) cs[c] = cnt[c];
-  __syncthreads();
-  for (int i = tid; i < N; i += T) {
+  __syncthreads();  // cnt is read above and incremented below
+  SWARM_STAMP(4);
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    if (cid[k] < 0) continue;
+    const size_t pos = base + atomicAdd(&cnt[cell_index(cqx[k], cqy[k], lx, ly)], 1);
+    sc.bsq[pos] = cqx[k];
+    sc.bsq[M + pos] = cqy[k];
+    sc.bsid[pos] = cid[k];
+  }
+  for (int i = tid + CH * T; i < N; i += T) {
     const uint32_t qx = st.q[base + i], qy = st.q[M + base + i];
     const size_t pos = base + atomicAdd(&cnt[cell_index(qx, qy, lx, ly)], 1);
     sc.bsq[pos] = qx;
     sc.bsq[M + pos] = qy;
     sc.bsid[pos] = i | ((int32_t)st.species[i] << 24);
   }
-  SWARM_STAMP(1);
+  // idle wave slots of the next run (k_cluster_build writes the used ones);
+  // last, so the stores drain in the shadow of the scatter
+  for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
+  SWARM_STAMP(5);
 }
 
 // Build step 2, chip-wide (grid.y = env, one thread per sorted entry): every
 // pair within r_i + r_j + skin once (i < j).  A stencil row (cells x-1..x+1)
-// is one contiguous sorted range, plus a wrap range at the grid edge.  Pass
-// 0 counts, one atomic per wave reserves the space, pass 1 writes.
+// is one contiguous sorted range, plus a wrap range at the grid edge.  The
+// six range bounds are loaded together and candidates four at a time (a few
+// memory latencies per thread, not one per candidate); up to kKeep pairs per
+// thread stay in registers, one atomic per wave reserves the output, and a
+// wave with a denser thread rescans to write.
 __global__ __launch_bounds__(256) void k_build_pairs(const Derived* __restrict__ d, DevState st,
                                                      Scratch sc, int lx, int ly) {
+  constexpr int kKeep = 8;
   __shared__ float nb2[kMaxSpecies * kMaxSpecies];
   for (int k = threadIdx.x; k < kMaxSpecies * kMaxSpecies; k += blockDim.x) nb2[k] = d->nb2[k];
-  __syncthreads();
   const int e = blockIdx.y, N = st.n;
   const int ps = blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = ps < N;
@@ -553,50 +585,89 @@ __global__ __launch_bounds__(256) void k_build_pairs(const Derived* __restrict__
     qx = sc.bsq[base + ps];
     qy = sc.bsq[M + base + ps];
   }
-  const float* nb2_row = nb2 + (pk >> 24) * kMaxSpecies;
   const int c0 = cell_index(qx, qy, lx, ly);
   const int cx = c0 & (ncx - 1), cy = c0 >> lx;
   const int xa = ncx >= 3 ? max(cx - 1, 0) : 0;
   const int xb = ncx >= 3 ? min(cx + 1, ncx - 1) : ncx - 1;
   const int xw = ncx >= 3 ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
-  uint32_t* out = sc.gplist + (size_t)e * sc.pair_cap;
-  int my_off = 0;
-  for (int pass = 0; pass < 2; ++pass) {
-    int found = 0;
-    for (int oy = loy; oy <= hiy && valid; ++oy) {
-      const int row = ((cy + oy + ncy) & (ncy - 1)) << lx;
+  int rb[6], re[6];
 #pragma unroll
-      for (int part = 0; part < 2; ++part) {
-        if (part == 1 && xw < 0) continue;
-        const int c_lo = row | (part == 0 ? xa : xw), c_hi = row | (part == 0 ? xb : xw);
-        const int jb = cs[c_lo], je = cs[c_hi + 1];
-        for (int jj = jb; jj < je; ++jj) {
-          const int packed = sc.bsid[base + jj];
-          const int j = packed & 0xffffff;
-          const float rx = (float)(int32_t)(sc.bsq[base + jj] - qx) * sx0;
-          const float ry = (float)(int32_t)(sc.bsq[M + base + jj] - qy) * sx1;
-          if (i < j && rx * rx + ry * ry < nb2_row[packed >> 24]) {
-            if (pass == 1) {
-              const int k = my_off + found;
-              if (k < sc.pair_cap) out[k] = (uint32_t)i | ((uint32_t)j << 16);
-            }
-            ++found;
-          }
+  for (int r = 0; r < 6; ++r) {
+    const int oy = loy + (r >> 1), part = r & 1;
+    const bool use = valid && oy <= hiy && (part == 0 || xw >= 0);
+    const int row = ((cy + oy + ncy) & (ncy - 1)) << lx;
+    const int c_lo = row | (part == 0 ? xa : xw), c_hi = row | (part == 0 ? xb : xw);
+    rb[r] = use ? cs[c_lo] : 0;
+    re[r] = use ? cs[c_hi + 1] : 0;
+  }
+  __syncthreads();  // nb2
+  const float* nb2_row = nb2 + (pk >> 24) * kMaxSpecies;
+  int found = 0;
+  uint32_t keep[kKeep];
+#pragma unroll
+  for (int v = 0; v < kKeep; ++v) keep[v] = 0u;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    for (int jj0 = rb[r]; jj0 < re[r]; jj0 += 4) {
+      int pk4[4];
+      uint32_t x4[4], y4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int jj = jj0 + u;
+        const bool ok = jj < re[r];
+        pk4[u] = ok ? sc.bsid[base + jj] : -1;
+        x4[u] = ok ? sc.bsq[base + jj] : 0u;
+        y4[u] = ok ? sc.bsq[M + base + jj] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (pk4[u] < 0) continue;
+        const int j = pk4[u] & 0xffffff;
+        const float rx = (float)(int32_t)(x4[u] - qx) * sx0;
+        const float ry = (float)(int32_t)(y4[u] - qy) * sx1;
+        if (i < j && rx * rx + ry * ry < nb2_row[pk4[u] >> 24]) {
+#pragma unroll
+          for (int v = 0; v < kKeep; ++v) keep[v] = found == v ? (uint32_t)j : keep[v];
+          ++found;
         }
       }
     }
-    if (pass == 0) {  // wave prefix sum, one atomic per wave
-      const int lane = threadIdx.x & 63;
-      int v = found;
+  }
+  // wave prefix sum, one atomic per wave
+  const int lane = threadIdx.x & 63;
+  int v = found;
 #pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const int o = __shfl_up(v, off, 64);
-        if (lane >= off) v += o;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(v, off, 64);
+    if (lane >= off) v += o;
+  }
+  int wbase = 0;
+  if (lane == 63) wbase = atomicAdd(&sc.gnpairs[e], v);
+  wbase = __shfl(wbase, 63, 64);
+  const int my_off = wbase + v - found;
+  uint32_t* out = sc.gplist + (size_t)e * sc.pair_cap;
+  if (!__any(found > kKeep)) {
+#pragma unroll
+    for (int u = 0; u < kKeep; ++u) {
+      const int k = my_off + u;
+      if (u < found && k < sc.pair_cap) out[k] = (uint32_t)i | (keep[u] << 16);
+    }
+    return;
+  }
+  // a lane found more than kKeep pairs: rescan and write in order
+  int w = 0;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    for (int jj = rb[r]; jj < re[r]; ++jj) {
+      const int packed = sc.bsid[base + jj];
+      const int j = packed & 0xffffff;
+      const float rx = (float)(int32_t)(sc.bsq[base + jj] - qx) * sx0;
+      const float ry = (float)(int32_t)(sc.bsq[M + base + jj] - qy) * sx1;
+      if (i < j && rx * rx + ry * ry < nb2_row[packed >> 24]) {
+        const int k = my_off + w;
+        if (k < sc.pair_cap) out[k] = (uint32_t)i | ((uint32_t)j << 16);
+        ++w;
       }
-      int wbase = 0;
-      if (lane == 63) wbase = atomicAdd(&sc.gnpairs[e], v);
-      wbase = __shfl(wbase, 63, 64);
-      my_off = wbase + v - found;
     }
   }
 }
@@ -604,7 +675,7 @@ __global__ __launch_bounds__(256) void k_build_pairs(const Derived* __restrict__
 // LDS words of the large-N variant: the union-find forest only.
 __host__ __device__ inline size_t build_lds_words_big(int n) {
   const int wmax = slots_per_env(n, true) / 64;  // either packing
-  return 16 + 16 + 68 + 68 + (size_t)((wmax + 3) & ~3) + (size_t)n;
+  return 16 + 16 + 3 * 68 + (size_t)((wmax + 3) & ~3) + (size_t)n;
 }
 
 // Build step 3, one workgroup per env: union-find over the pair list
@@ -621,8 +692,9 @@ __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc)
   int32_t* misc = wave_sums + 16;                          // 16: 0 flag, 1 waves
   int32_t* classcnt = misc + 16;                           // 68
   int32_t* wavebase = classcnt + 68;                       // 68
+  int32_t* freebase = wavebase + 68;                       // 68
   const int wmax = sc.wmax;
-  int32_t* wave_np = wavebase + 68;                        // wmax (padded)
+  int32_t* wave_np = freebase + 68;                        // wmax (padded)
   int32_t* parent = wave_np + ((wmax + 3) & ~3);           // N
   const size_t M = (size_t)st.m;
   int32_t* csz = kBig ? sc.gclus + base : parent + N;              // N
@@ -631,7 +703,7 @@ __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc)
   uint32_t* plist = kBig ? sc.gplist + (size_t)e * sc.pair_cap
                          : reinterpret_cast<uint32_t*>(parent + 4 * N);  // pair_cap
   const int S = sc.S;
-  SWARM_STAMP(2);
+  SWARM_STAMP(6);
   const int found = sc.gnpairs[e];
   const int npairs = min(found, sc.pair_cap);
   for (int k = tid; k < 68; k += T) classcnt[k] = 0;
@@ -642,15 +714,24 @@ __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc)
     csz[i] = 0;
     cbase[i] = 0;  // pair count of a cluster (one-pass packing), then its base
   }
-  if (!kBig)
-    for (int k = tid; k < npairs; k += T) plist[k] = sc.gplist[(size_t)e * sc.pair_cap + k];
+  if (!kBig) {  // pair list into LDS, four loads in flight per thread
+    const uint32_t* gp = sc.gplist + (size_t)e * sc.pair_cap;
+    for (int k0 = tid; k0 < npairs; k0 += 4 * T) {
+      uint32_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = k0 + u * T < npairs ? gp[k0 + u * T] : 0u;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (k0 + u * T < npairs) plist[k0 + u * T] = v[u];
+    }
+  }
   __syncthreads();
   for (int k = tid; k < npairs; k += T) {
     const uint32_t pr = plist[k];
     uf_union(parent, (int)(pr & 0xffffu), (int)(pr >> 16));
   }
   __syncthreads();
-  SWARM_STAMP(3);
+  SWARM_STAMP(7);
   for (int i = tid; i < N; i += T) parent[i] = uf_find(parent, i);
   __syncthreads();
   for (int i = tid; i < N; i += T) lslot[i] = atomicAdd(&csz[parent[i]], 1);
@@ -673,7 +754,7 @@ __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc)
     }
   }
   __syncthreads();
-  SWARM_STAMP(4);
+  SWARM_STAMP(8);
   if (misc[0]) {
     if (tid == 0) {
       sc.fallback[e] = 1;
@@ -681,26 +762,73 @@ __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc)
     }
     return;
   }
+  // Waves per class.  The tail lanes a class leaves free in its waves
+  // (64 - per * w in a full wave, more in its last one) take the singletons
+  // first; only the rest of them get waves of their own (fewer, fuller
+  // waves: the run kernel's cost is per wave).
   if (tid < 64) {
-    const int s = tid + 1;
-    const int per = 64 / s;
-    int32_t w = (classcnt[s] + per - 1) / per;
-    const int32_t own = w;
+    const int w = tid + 1;
+    const int per = 64 / w;
+    const int cnt = classcnt[w];
+    int32_t nw = (cnt + per - 1) / per;
+    int32_t fl = 0;
+    if (w >= 2 && nw > 0) fl = (nw - 1) * (64 - per * w) + (64 - (cnt - (nw - 1) * per) * w);
+    int32_t f = fl;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-      const int32_t o = __shfl_up(w, off, 64);
-      if (tid >= off) w += o;
+      const int32_t o = __shfl_up(f, off, 64);
+      if (tid >= off) f += o;
     }
-    wavebase[s] = w - own;
-    if (tid == 63) misc[1] = w;
+    freebase[w] = f - fl;
+    const int32_t F = __shfl(f, 63, 64);
+    if (w == 1) nw = (max(cnt - F, 0) + 63) / 64;
+    int32_t v = nw;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int32_t o = __shfl_up(v, off, 64);
+      if (tid >= off) v += o;
+    }
+    wavebase[w] = v - nw;
+    if (tid == 63) {
+      misc[1] = v;
+      misc[3] = F;
+      freebase[65] = F;
+    }
   }
   __syncthreads();
+  const int nfree = misc[3];
   for (int i = tid; i < N; i += T) {
     if (parent[i] != i) continue;
     const int s = csz[i];
-    const int per = 64 / s;
     const int r = cbase[i];
-    cbase[i] = (wavebase[s] + r / per) * 64 + (r % per) * s;
+    if (s == 1 && r < nfree) {
+      // the class v whose free-lane range holds r (largest v >= 2 with
+      // freebase[v] <= r; its range is non-empty), then wave j and lane
+      int lo = 2, hi = 64;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (freebase[mid] <= r) lo = mid; else hi = mid - 1;
+      }
+      const int v = lo, per = 64 / v;
+      const int nw = (classcnt[v] + per - 1) / per;
+      const int ffull = 64 - per * v;
+      const int t = r - freebase[v];
+      int j, lane;
+      if (t < (nw - 1) * ffull) {
+        j = t / ffull;
+        lane = per * v + t % ffull;
+      } else {
+        j = nw - 1;
+        lane = (classcnt[v] - (nw - 1) * per) * v + (t - (nw - 1) * ffull);
+      }
+      cbase[i] = (wavebase[v] + j) * 64 + lane;
+    } else if (s == 1) {
+      const int r2 = r - nfree;
+      cbase[i] = (wavebase[1] + r2 / 64) * 64 + r2 % 64;
+    } else {
+      const int per = 64 / s;
+      cbase[i] = (wavebase[s] + r / per) * 64 + (r % per) * s;
+    }
   }
   __syncthreads();
   for (int i = tid; i < N; i += T) {
@@ -712,7 +840,7 @@ __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc)
     sc.root[base + i] = root;
   }
   __syncthreads();
-  SWARM_STAMP(5);
+  SWARM_STAMP(9);
   // per-wave pair lists (both particles of a pair share a cluster, so a wave)
   for (int k = tid; k < npairs; k += T) {
     const uint32_t pr = plist[k];
@@ -728,7 +856,7 @@ __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc)
       misc[2] = 1;  // a wave with more than kPairsPerWave pairs
   }
   __syncthreads();
-  SWARM_STAMP(6);
+  SWARM_STAMP(10);
   for (int w = tid; w < misc[1]; w += T)
     sc.wave_npairs[(size_t)e * wmax + w] = min(wave_np[w], kPairsPerWave);
   if (tid == 0) {
@@ -747,24 +875,24 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // Noise table for latency-bound windows (few waves per SIMD): the normals of
-// every (sub-step, wave slot) computed by the whole chip ahead of the run,
-// table[(s * 3 + c) * (E * S) + e * S + slot].
-__global__ __launch_bounds__(256) void k_noise(const Derived* __restrict__ d, Scratch sc,
-                                               int n_envs, const uint64_t* __restrict__ step_ctr,
+// every (sub-step, particle) computed by the whole chip ahead of the run,
+// table[(s * 3 + c) * M + e * N + i].  Indexed by particle, not wave slot,
+// so it does not wait for the cluster build (it runs on its own stream).
+__global__ __launch_bounds__(256) void k_noise(const Derived* __restrict__ d, DevState st,
+                                               const uint64_t* __restrict__ step_ctr,
                                                float* __restrict__ table) {
-  const long ts = (long)n_envs * sc.S;
-  const long gs = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gs >= ts) return;
-  const int e = (int)(gs / sc.S);
-  const int i = sc.perm[gs];
-  if (i < 0 || sc.fallback[e] != 0) return;
+  const long M = st.m;
+  const long gi = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi >= M) return;
+  const int e = (int)(gi / st.n);
+  const int i = (int)(gi - (long)e * st.n);
   const int s = blockIdx.y;
   float g[3];
   normals3(d->key0, d->key1 ^ (uint32_t)e, (uint32_t)i, *step_ctr + (uint64_t)s, 0u, g);
-  float* o = table + (size_t)s * 3 * ts + gs;
+  float* o = table + (size_t)s * 3 * M + gi;
   o[0] = g[0];
-  o[ts] = g[1];
-  o[2 * ts] = g[2];
+  o[M] = g[1];
+  o[2 * M] = g[2];
 }
 
 // kMulti = false: one species, so the pair constants are wave-uniform scalars.
@@ -831,8 +959,8 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
   const uint32_t q0x = p.qx, q0y = p.qy;
   float dmax2 = 0.0f;
   float vx = 0.0f, vy = 0.0f, om = 0.0f;
-  const long ts = (long)n_envs * sc.S;
-  const float* tcol = table + (size_t)e * sc.S + slot;
+  const long ts = (long)M;
+  const float* tcol = table + gi;
   float gn[3] = {0.0f, 0.0f, 0.0f};
   if (kTable && active) {
     gn[0] = tcol[0];

@@ -736,11 +736,17 @@ class SwarmEngine(Engine):
         side = self._side_stream
         side.wait_stream(main)
         self._native.call("swarm_engine_prebuild", ctypes.c_void_p(side.cuda_stream), int(n_steps))
-        self._prebuild_pending = side
+        self._prebuild_pending = (side,)
 
     def _run(self, n_steps: int):
         if self._prebuild_pending is not None:
-            torch.cuda.current_stream().wait_stream(self._prebuild_pending)
+            # The noise table (latency-bound engines) runs on the main stream
+            # after the policy kernels, ahead of the join: the build usually
+            # finishes later, and a third stream would add a graph join.
+            self._native.bind_stream()
+            self._native.call("swarm_engine_prebuild_noise", None, int(n_steps))
+            for st in self._prebuild_pending:
+                torch.cuda.current_stream().wait_stream(st)
             self._prebuild_pending = None
         self._native.bind_stream()
         self._native.call("swarm_engine_integrate", int(n_steps))

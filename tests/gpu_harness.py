@@ -77,12 +77,16 @@ class Harness:
         self.native.bind_stream()
         self.native.call("swarm_engine_integrate", int(n))
 
-    def prebuild(self, n_hint, stream=None):
-        """swarm_engine_prebuild on `stream` (a torch stream; default current)."""
+    def prebuild(self, n_hint, stream=None, noise_stream=None):
+        """swarm_engine_prebuild on `stream` and swarm_engine_prebuild_noise on
+        `noise_stream` (torch streams; default: both on the current stream)."""
         import torch
 
         st = stream if stream is not None else torch.cuda.current_stream()
+        ns = noise_stream if noise_stream is not None else st
         self.native.call("swarm_engine_prebuild", ctypes.c_void_p(st.cuda_stream), int(n_hint))
+        self.native.call("swarm_engine_prebuild_noise", ctypes.c_void_p(ns.cuda_stream),
+                         int(n_hint))
 
     def sd(self, n, gamma=0.1, maxd=0.1):
         self.native.bind_stream()

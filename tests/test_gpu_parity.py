@@ -310,13 +310,15 @@ def test_prebuild_on_side_stream_bit_exact(hint):
     st, _ = oracle.sd_run(h.op, st, np.zeros(n), 300)
     f = rng.choice([0.0, 10.0], n).astype(np.float32)
     t = rng.choice([-10.0, 0.0, 10.0], n).astype(np.float32)
-    side = torch.cuda.Stream()
+    side, side2 = torch.cuda.Stream(), torch.cuda.Stream()
     step = 0
     for _ in range(3):
         side.wait_stream(torch.cuda.current_stream())
-        h.prebuild(hint, side)
+        side2.wait_stream(torch.cuda.current_stream())
+        h.prebuild(hint, side, side2)
         h.set_actions(f, t)
         torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.current_stream().wait_stream(side2)
         h.integrate(100)
         st, _, _ = oracle.bd_run(h.op, st, np.zeros(n), f, t, 100, step0=step)
         step += 100
@@ -360,3 +362,32 @@ def test_c5_16384_large_build_bit_exact():
     w = np.zeros(1, np.int32)
     h.native.call("swarm_engine_window_stats", fb.ctypes.data, w.ctypes.data)
     assert fb[0] == 0 and w[0] > 0, (fb, w)
+
+
+@pytest.mark.parametrize("E,n,box_len", [(1, 2000, 90.0), (20, 4096, 200.0), (64, 4096, 160.0)])
+def test_vision_cone_parity_lane_variants_and_dense(E, n, box_len):
+    """The vision kernel's 16/4/1 lanes-per-agent variants (by envs x
+    particles) and dense neighbourhoods (more in-range hits per lane than its
+    LDS hit list holds, so the list is drained mid-scan), bit-exact against
+    the oracle on the first and last env."""
+    from gpu_harness import Harness, random_state, species_list
+    from swarmrl_amd.engine import ops
+
+    rng = np.random.default_rng(60 + E)
+    box = [box_len, box_len, box_len]
+    types = rng.integers(0, 2, n)
+    h = Harness(box, 1e-3, 0.0, 1.0, 0, species_list(), np.zeros(n, int), n_envs=E)
+    states = [random_state(rng, n, box) for _ in range(E)]
+    h.upload(states)
+    agents = np.nonzero(types == 1)[0].astype(np.int32)
+    radii = (0.5 + rng.random(n)).astype(np.float32)
+    dev = torch.device("cuda", 0)
+    vp = ops.vision_params(12.0, 1.0, 3, [0, 1])
+    out = ops.vision_cone(h.native, E, torch.as_tensor(agents, device=dev),
+                          torch.as_tensor(radii, device=dev),
+                          torch.as_tensor(types.astype(np.int32), device=dev), vp)
+    out = out.cpu().numpy()
+    for e in sorted({0, E - 1}):
+        ref = oracle.vision_cone(h.op, states[e], agents, radii, types, 12.0, 1.0, 3, [0, 1])
+        assert np.array_equal(out[e], ref)
+        assert np.count_nonzero(ref) > len(agents)
