@@ -22,6 +22,8 @@
  *   position  : per axis a uint32 fraction of the box (q * L / 2^32) plus an
  *               int32 image counter; unwrapped x = (img + q / 2^32) * L.
  *   orientation (2-D): uint32 angle, theta = a * 2 pi / 2^32.
+ *   orientation (3-D): fp32 unit director [3], rotated each sub-step by
+ *               the rotation vector (Rodrigues) and renormalised.
  * Index g = env * n_particles + i.  Device arrays are axis-major [3][E*N].
  */
 #ifndef SWARMRL_AMD_H
@@ -49,7 +51,7 @@ extern "C" {
  * (espresso.py:376-413).  A "species" is one distinct
  * (radius, gamma_t, gamma_r, mass, rinertia) combination. */
 typedef struct swarm_params {
-  int32_t n_dims;   /* 2 (3-D is not implemented in this build) */
+  int32_t n_dims;   /* 2 or 3 (espresso.py:143-152, n_dims) */
   int32_t periodic; /* MDParams.periodic (espresso.py:270) */
   double box[3];    /* box_l (espresso.py:267) */
   double time_step; /* system.time_step (espresso.py:268) */
@@ -78,7 +80,34 @@ typedef struct swarm_device_views {
   uint8_t *species;   /* [N]      */
   int32_t n_envs;
   int32_t n_particles;
+  int32_t n_dims;
+  int32_t reserved0;
+  float *dir3;        /* [3][E*N] 3-D directors */
+  float *torque_xy;   /* [2][E*N] 3-D torque x, y */
+  float *omega_xy;    /* [2][E*N] 3-D angular velocity x, y */
 } swarm_device_views_t;
+
+/* A confining or user wall (espresso.py:667-800): a WCA constraint with
+ * sigma = r_particle * 2^(-1/6), cutoff = r_particle (the wall type has
+ * radius 0) and the engine's epsilon, acting on every particle.
+ *   kind 0 = espressomd.shapes.Wall: dist = n . x_folded - offset
+ *            (add_confining_walls, espresso.py:683-697);
+ *   kind 1 = the vertical Rhomboid of add_walls (espresso.py:765-784):
+ *            corner + s a + t b (s, t in [0, 1]), a and b in the xy plane,
+ *            spanning the whole box in z; distance in the xy plane.
+ * A particle on or inside a wall (dist <= 0) is a constraint violation:
+ * it is counted (swarm_engine_wall_violations) and gets no wall force. */
+typedef struct swarm_wall {
+  int32_t kind;
+  int32_t reserved;
+  double normal[3]; /* kind 0 */
+  double offset;    /* kind 0 */
+  double corner[3]; /* kind 1 */
+  double a[3];      /* kind 1 */
+  double b[3];      /* kind 1 */
+} swarm_wall_t;
+
+#define SWARM_MAX_WALLS 16
 
 /* Vision-cone parameters (SubdividedVisionCones,
  * swarmrl/observables/subdivided_vision_cones.py:25-60). */
@@ -138,10 +167,32 @@ int swarm_engine_set_actions(swarm_engine_t *e, const float *f_swim,
 /* Per-particle external force [E*N][3] (host); replaces p.ext_force. */
 int swarm_engine_set_external_force(swarm_engine_t *e, const double *f_ext);
 
-/* new_direction handling of manage_forces in 2-D: rotate about +-z so the
- * director equals dir (espresso.py:1236-1249).  dir [E*N][3], mask [E*N]. */
+/* new_direction handling of manage_forces (espresso.py:1236-1249): in 2-D
+ * rotate about +-z so the director equals dir; in 3-D set the director to
+ * dir (normalised).  dir [E*N][3], mask [E*N]. */
 int swarm_engine_set_directors(swarm_engine_t *e, const double *dir,
                                const uint8_t *mask);
+
+/* 3-D only: the x and y components of the lab-frame torque [2][E*N]
+ * (the z component is set_actions' torque_z); replaces coll.ext_torque =
+ * action.torque (espresso.py:1230-1235).  on_device as in set_actions
+ * (0 host, 1 device copy; binding is not offered). */
+int swarm_engine_set_torque_xy(swarm_engine_t *e, const float *torque_xy,
+                               int32_t on_device);
+
+/* 3-D directors in the engine's own format (host fp32 [3][E*N]), for
+ * checkpoints and bit-exact parity. */
+int swarm_engine_upload_directors(swarm_engine_t *e, const float *dir3);
+int swarm_engine_download_directors(swarm_engine_t *e, float *dir3);
+
+/* Walls (see swarm_wall_t); replaces add_confining_walls / add_walls
+ * (espresso.py:667-800).  Replaces any previous set; n_walls <= 16. */
+int swarm_engine_set_walls(swarm_engine_t *e, const swarm_wall_t *walls,
+                           int32_t n_walls);
+
+/* Number of (particle, sub-step) wall contacts with dist <= 0 since the
+ * engine was created (ESPResSo raises for those; synchronous). */
+int swarm_engine_wall_violations(swarm_engine_t *e, uint64_t *count);
 
 /* Steepest-descent overlap removal (espresso.py:1161-1168): n_steps of
  * dp = clamp(gamma * F, -max_disp, max_disp) per free coordinate. */

@@ -48,6 +48,36 @@ class Params(ctypes.Structure):
     ]
 
 
+MAX_WALLS = 16
+
+
+class Wall(ctypes.Structure):
+    """swarm_wall_t (declared independently of the product binding)."""
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("normal", ctypes.c_double * 3),
+        ("offset", ctypes.c_double),
+        ("corner", ctypes.c_double * 3),
+        ("a", ctypes.c_double * 3),
+        ("b", ctypes.c_double * 3),
+    ]
+
+
+def make_walls(walls):
+    """walls: list of dicts {'kind': 0, 'normal', 'offset'} or {'kind': 1,
+    'corner', 'a', 'b'} -> (ctypes array, count)."""
+    arr = (Wall * max(1, len(walls)))()
+    for k, w in enumerate(walls):
+        arr[k].kind = int(w["kind"])
+        for key in ("normal", "corner", "a", "b"):
+            if key in w:
+                for a in range(3):
+                    getattr(arr[k], key)[a] = float(w[key][a])
+        arr[k].offset = float(w.get("offset", 0.0))
+    return arr, len(walls)
+
+
 _lib = None
 _P = ctypes.c_void_p
 
@@ -85,6 +115,19 @@ def lib():
         L.or_neighbor_pairs.argtypes = [ctypes.POINTER(Params), ctypes.c_int, _P, _P,
                                         ctypes.c_double, _P, ctypes.c_int]
         L.or_cell_grid.argtypes = [ctypes.POINTER(Params), ctypes.c_int, ctypes.c_double, _P, _P]
+        L.or_bd_run_walls.restype = ctypes.c_int
+        L.or_bd_run_walls.argtypes = L.or_bd_run.argtypes + [_P, ctypes.c_int, _P]
+        L.or_sd_run_walls.restype = ctypes.c_int
+        L.or_sd_run_walls.argtypes = L.or_sd_run.argtypes + [_P, ctypes.c_int]
+        L.or_bd_run3.restype = ctypes.c_int
+        L.or_bd_run3.argtypes = [ctypes.POINTER(Params), ctypes.c_int, _P, _P, _P, _P, _P, _P,
+                                 _P, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, _P, _P,
+                                 _P, ctypes.c_int, _P]
+        L.or_sd_run3.restype = ctypes.c_int
+        L.or_sd_run3.argtypes = [ctypes.POINTER(Params), ctypes.c_int, _P, _P, _P, _P, _P, _P,
+                                 _P, ctypes.c_int, ctypes.c_double, ctypes.c_double, _P,
+                                 ctypes.c_int]
+        L.or_rotate_director.argtypes = [_P, ctypes.c_float, ctypes.c_float, ctypes.c_float]
         _lib = L
     return _lib
 
@@ -140,26 +183,47 @@ def state_from_positions(pos, dirs, box):
     return {"q": q, "img": img, "ang": ang}
 
 
-def unwrapped(state, box):
+def state3_from_positions(pos, dirs, box):
+    """3-D: pos/dirs (N, 3) fp64 -> {'q' [3,N] u32, 'img' [3,N] i32,
+    'dir' [3,N] f32 (normalised), 'ang' [N] u32 (unused, 0)}."""
+    pos = np.asarray(pos, dtype=float)
+    n = len(pos)
+    q = np.zeros((3, n), np.uint32)
+    img = np.zeros((3, n), np.int32)
+    for a in range(3):
+        q[a], img[a] = to_fixed(pos[:, a], box[a])
+    d = np.asarray(dirs, dtype=float)
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).T.astype(np.float32)
+    return {"q": q, "img": img, "dir": np.ascontiguousarray(d), "ang": np.zeros(n, np.uint32)}
+
+
+def unwrapped(state, box, dims=None):
     q, img = state["q"], state["img"]
     out = np.zeros((q.shape[1], 3))
-    for a in range(2):
+    if dims is None:
+        dims = 3 if "dir" in state else 2
+    for a in range(dims):
         out[:, a] = (img[a].astype(np.float64) + q[a].astype(np.float64) / TWO32) * box[a]
     return out
 
 
 def _copy_state(state):
-    return {
+    out = {
         "q": np.ascontiguousarray(state["q"], dtype=np.uint32).copy(),
         "img": np.ascontiguousarray(state["img"], dtype=np.int32).copy(),
         "ang": np.ascontiguousarray(state["ang"], dtype=np.uint32).copy(),
     }
+    if "dir" in state:
+        out["dir"] = np.ascontiguousarray(state["dir"], dtype=np.float32).copy()
+    return out
 
 
 # ------------------------------------------------------------- dynamics
 def bd_run(params, state, species, f_swim, torque_z, n_steps, step0=0, env=0, f_ext=None,
-           use_cells=True):
-    """n_steps BD sub-steps of one env; returns (new_state, vel [3,N], omega [N])."""
+           use_cells=True, walls=None, violations=None):
+    """n_steps BD sub-steps of one env; returns (new_state, vel [3,N], omega [N]).
+    walls: list of wall dicts (make_walls); violations: 1-element uint64
+    array that receives the added count of wall contacts."""
     st = _copy_state(state)
     n = st["ang"].shape[0]
     sp = np.ascontiguousarray(species, dtype=np.uint8)
@@ -168,25 +232,75 @@ def bd_run(params, state, species, f_swim, torque_z, n_steps, step0=0, env=0, f_
     fe = None if f_ext is None else np.ascontiguousarray(f_ext, dtype=np.float32)
     vel = np.zeros((3, n), np.float32)
     om = np.zeros(n, np.float32)
-    rc = lib().or_bd_run(ctypes.byref(params), n, _ptr(st["q"]), _ptr(st["img"]),
-                         _ptr(st["ang"]), _ptr(sp), _ptr(fs), _ptr(tz), _ptr(fe), int(step0),
-                         int(n_steps), int(env), _ptr(vel), _ptr(om), 1 if use_cells else 0)
+    wa, nw = make_walls(walls or [])
+    viol = np.zeros(1, np.uint64) if violations is None else violations
+    rc = lib().or_bd_run_walls(ctypes.byref(params), n, _ptr(st["q"]), _ptr(st["img"]),
+                               _ptr(st["ang"]), _ptr(sp), _ptr(fs), _ptr(tz), _ptr(fe),
+                               int(step0), int(n_steps), int(env), _ptr(vel), _ptr(om),
+                               1 if use_cells else 0, ctypes.cast(wa, _P), nw, _ptr(viol))
     if rc != 0:
         raise ValueError(f"or_bd_run failed ({rc})")
     return st, vel, om
 
 
+def bd_run3(params, state, species, f_swim, torque, n_steps, step0=0, env=0, f_ext=None,
+            walls=None, violations=None):
+    """3-D: n_steps BD sub-steps of one env (state with 'dir' [3,N]); torque
+    [3,N] lab frame.  Returns (new_state, vel [3,N], omega [3,N])."""
+    st = _copy_state(state)
+    n = st["q"].shape[1]
+    sp = np.ascontiguousarray(species, dtype=np.uint8)
+    fs = np.ascontiguousarray(f_swim, dtype=np.float32)
+    tq = np.ascontiguousarray(torque, dtype=np.float32).reshape(3, n)
+    fe = None if f_ext is None else np.ascontiguousarray(f_ext, dtype=np.float32)
+    vel = np.zeros((3, n), np.float32)
+    om = np.zeros((3, n), np.float32)
+    wa, nw = make_walls(walls or [])
+    viol = np.zeros(1, np.uint64) if violations is None else violations
+    rc = lib().or_bd_run3(ctypes.byref(params), n, _ptr(st["q"]), _ptr(st["img"]),
+                          _ptr(st["dir"]), _ptr(sp), _ptr(fs), _ptr(tq), _ptr(fe), int(step0),
+                          int(n_steps), int(env), _ptr(vel), _ptr(om), ctypes.cast(wa, _P), nw,
+                          _ptr(viol))
+    if rc != 0:
+        raise ValueError(f"or_bd_run3 failed ({rc})")
+    return st, vel, om
+
+
+def sd_run3(params, state, species, n_steps, gamma=0.1, max_disp=0.1, f_swim=None,
+            torque=None, f_ext=None, walls=None):
+    st = _copy_state(state)
+    n = st["q"].shape[1]
+    sp = np.ascontiguousarray(species, dtype=np.uint8)
+    fs = np.zeros(n, np.float32) if f_swim is None else np.ascontiguousarray(f_swim, np.float32)
+    tq = np.zeros((3, n), np.float32) if torque is None else \
+        np.ascontiguousarray(torque, np.float32).reshape(3, n)
+    fe = None if f_ext is None else np.ascontiguousarray(f_ext, dtype=np.float32)
+    wa, nw = make_walls(walls or [])
+    steps = lib().or_sd_run3(ctypes.byref(params), n, _ptr(st["q"]), _ptr(st["img"]),
+                             _ptr(st["dir"]), _ptr(sp), _ptr(fs), _ptr(tq), _ptr(fe),
+                             int(n_steps), float(gamma), float(max_disp), ctypes.cast(wa, _P), nw)
+    return st, steps
+
+
+def rotate_director(v, phi):
+    out = np.ascontiguousarray(v, dtype=np.float32).copy()
+    lib().or_rotate_director(_ptr(out), float(phi[0]), float(phi[1]), float(phi[2]))
+    return out
+
+
 def sd_run(params, state, species, n_steps, gamma=0.1, max_disp=0.1, f_swim=None,
-           torque_z=None, f_ext=None, use_cells=True):
+           torque_z=None, f_ext=None, use_cells=True, walls=None):
     st = _copy_state(state)
     n = st["ang"].shape[0]
     sp = np.ascontiguousarray(species, dtype=np.uint8)
     fs = np.zeros(n, np.float32) if f_swim is None else np.ascontiguousarray(f_swim, np.float32)
     tz = np.zeros(n, np.float32) if torque_z is None else np.ascontiguousarray(torque_z, np.float32)
     fe = None if f_ext is None else np.ascontiguousarray(f_ext, dtype=np.float32)
-    steps = lib().or_sd_run(ctypes.byref(params), n, _ptr(st["q"]), _ptr(st["img"]),
-                            _ptr(st["ang"]), _ptr(sp), _ptr(fs), _ptr(tz), _ptr(fe),
-                            int(n_steps), float(gamma), float(max_disp), 1 if use_cells else 0)
+    wa, nw = make_walls(walls or [])
+    steps = lib().or_sd_run_walls(ctypes.byref(params), n, _ptr(st["q"]), _ptr(st["img"]),
+                                  _ptr(st["ang"]), _ptr(sp), _ptr(fs), _ptr(tz), _ptr(fe),
+                                  int(n_steps), float(gamma), float(max_disp),
+                                  1 if use_cells else 0, ctypes.cast(wa, _P), nw)
     return st, steps
 
 

@@ -78,6 +78,37 @@ def placement(n, init_radius, center, seed, n_calls_before=0):
     return pos, dirs
 
 
+def placement3(n, init_radius, center, seed):
+    """
+    add_colloids 3-D placement (espresso.py:91-105, 521-529): per colloid
+    r = R cbrt(U), direction from get_random_angles (theta = arccos(2U - 1),
+    phi = 2 pi U, utils.py:19-27) for the position, then again for the
+    director.
+    """
+    rng = np.random.default_rng(seed)
+    pos = np.zeros((n, 3))
+    dirs = np.zeros((n, 3))
+
+    def unit(theta, phi):
+        return np.array([np.sin(theta) * np.cos(phi), np.sin(theta) * np.sin(phi),
+                         np.cos(theta)])
+
+    for i in range(n):
+        r = init_radius * np.cbrt(rng.random())
+        th = np.arccos(2.0 * rng.random() - 1)
+        ph = 2.0 * np.pi * rng.random()
+        pos[i] = r * unit(th, ph) + center
+        th = np.arccos(2.0 * rng.random() - 1)
+        ph = 2.0 * np.pi * rng.random()
+        dirs[i] = unit(th, ph)
+    return pos, dirs
+
+
+def wall_distance_plane(x, normal, offset):
+    """espressomd.shapes.Wall: dist = n . x - offset (folded position)."""
+    return float(np.dot(normal, x) - offset)
+
+
 # ----------------------------------------------------------- units (a3)
 K_B = 1.380649e-23
 SIM_ENERGY = 293 * K_B                       # espresso.py:223

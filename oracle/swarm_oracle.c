@@ -241,6 +241,11 @@ typedef struct {
   float sig6[SWARM_MAX_SPECIES][SWARM_MAX_SPECIES];
   float eps24;
   double rc_max;
+  /* walls (espresso.py:667-800), see swarm_wall_t */
+  int n_walls;
+  int wkind[SWARM_MAX_WALLS];
+  float wp[SWARM_MAX_WALLS][8]; /* plane: n0 n1 n2 off; slab: o0 o1 a0 a1 b0 b1 la lb */
+  float wcut2[SWARM_MAX_SPECIES], wsig6[SWARM_MAX_SPECIES];
 } derived_t;
 
 #define TWO32 4294967296.0
@@ -277,6 +282,36 @@ static void derive(const swarm_params_t *p, derived_t *d) {
         d->rc_max = rc;
     }
   d->eps24 = (float)(24.0 * p->wca_epsilon);
+  for (int s = 0; s < p->n_species; ++s) {
+    double rc2 = p->radius[s] * p->radius[s];
+    d->wcut2[s] = (float)rc2;
+    d->wsig6[s] = (float)(rc2 * rc2 * rc2 * 0.5);
+  }
+}
+
+/* wall table in fp32 (same derivation as the engine's set_walls) */
+static void derive_walls(derived_t *d, const swarm_wall_t *w, int n_walls) {
+  d->n_walls = n_walls;
+  for (int k = 0; k < n_walls; ++k) {
+    d->wkind[k] = w[k].kind;
+    float *o = d->wp[k];
+    if (w[k].kind == 0) {
+      for (int a = 0; a < 3; ++a)
+        o[a] = (float)w[k].normal[a];
+      o[3] = (float)w[k].offset;
+    } else {
+      double la = sqrt(w[k].a[0] * w[k].a[0] + w[k].a[1] * w[k].a[1]);
+      double lb = sqrt(w[k].b[0] * w[k].b[0] + w[k].b[1] * w[k].b[1]);
+      o[0] = (float)w[k].corner[0];
+      o[1] = (float)w[k].corner[1];
+      o[2] = (float)(w[k].a[0] / la);
+      o[3] = (float)(w[k].a[1] / la);
+      o[4] = (float)(w[k].b[0] / lb);
+      o[5] = (float)(w[k].b[1] / lb);
+      o[6] = (float)la;
+      o[7] = (float)lb;
+    }
+  }
 }
 
 static int32_t f2i32(float v) {
@@ -318,6 +353,59 @@ static void wca_pair(const derived_t *d, int si, int sj, float rx, float ry,
     fr = fr * ir2;
     *ax += f2fix24(-fr * rx);
     *ay += f2fix24(-fr * ry);
+  }
+}
+
+/* WCA force of every wall on a particle of species sp at the folded
+ * position (x, y, z), added to acc[0..dims) in 2^-24 fixed point
+ * (ShapeBasedConstraint + WCA, espresso.py:667-800, 814-819). */
+static void wall_forces(const derived_t *d, int sp, float x, float y, float z, int dims,
+                        int64_t *ax, int64_t *ay, int64_t *az, uint64_t *viol) {
+  for (int k = 0; k < d->n_walls; ++k) {
+    const float *w = d->wp[k];
+    float vx, vy, vz, r2;
+    if (d->wkind[k] == 0) {
+      float dist = w[0] * x + w[1] * y;
+      dist = dist + w[2] * z;
+      dist = dist - w[3];
+      if (!(dist > 0.0f)) {
+        ++*viol;
+        continue;
+      }
+      vx = w[0] * dist;
+      vy = w[1] * dist;
+      vz = w[2] * dist;
+      r2 = dist * dist;
+    } else {
+      float px = x - w[0], py = y - w[1];
+      float u = px * w[2] + py * w[3];
+      float t = px * w[4] + py * w[5];
+      float du = u - fminf(fmaxf(u, 0.0f), w[6]);
+      float dt = t - fminf(fmaxf(t, 0.0f), w[7]);
+      if (du == 0.0f && dt == 0.0f) {
+        ++*viol;
+        continue;
+      }
+      vx = du * w[2] + dt * w[4];
+      vy = du * w[3] + dt * w[5];
+      vz = 0.0f;
+      r2 = vx * vx + vy * vy;
+    }
+    if (r2 < d->wcut2[sp]) {
+      float ir2 = 1.0f / r2;
+      float ir6 = ir2 * ir2;
+      ir6 = ir6 * ir2;
+      float s6 = d->wsig6[sp] * ir6;
+      float t = 2.0f * s6;
+      t = t - 1.0f;
+      float fr = d->eps24 * s6;
+      fr = fr * t;
+      fr = fr * ir2;
+      *ax += f2fix24(fr * vx);
+      *ay += f2fix24(fr * vy);
+      if (dims == 3)
+        *az += f2fix24(fr * vz);
+    }
   }
 }
 
@@ -471,15 +559,18 @@ static void cl_free(celllist_t *cl) {
  * step0: global step index of the first sub-step (noise counter).
  * use_cells: 0 = O(n^2) pair search, 1 = cell list (same result).
  */
-int or_bd_run(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
-              uint32_t *ang, const uint8_t *species, const float *f_swim,
-              const float *torque_z, const float *f_ext, uint64_t step0,
-              int n_steps, uint32_t env, float *vel, float *omega,
-              int use_cells) {
+int or_bd_run_walls(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
+                    uint32_t *ang, const uint8_t *species, const float *f_swim,
+                    const float *torque_z, const float *f_ext, uint64_t step0,
+                    int n_steps, uint32_t env, float *vel, float *omega,
+                    int use_cells, const swarm_wall_t *walls, int n_walls,
+                    uint64_t *violations) {
   if (p->n_dims != 2)
     return SWARM_EINVAL;
   derived_t d;
   derive(p, &d);
+  derive_walls(&d, walls, n_walls);
+  uint64_t viol = 0;
   int64_t *acc = (int64_t *)malloc(sizeof(int64_t) * 2 * (size_t)(n > 0 ? n : 1));
   celllist_t cl;
   int have_cl = use_cells && cl_alloc(&cl, p, &d, n);
@@ -490,6 +581,9 @@ int or_bd_run(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
     for (int i = 0; i < n; ++i) {
       int sp = species[i];
       float sn, cs;
+      if (d.n_walls)
+        wall_forces(&d, sp, (float)q[i] * d.sx[0], (float)q[n + i] * d.sx[1], 0.0f, 2,
+                    &acc[i], &acc[n + i], NULL, &viol);
       or_sincos_turn(ang[i], &sn, &cs);
       float fx = (float)acc[i] * 5.9604644775390625e-08f;
       float fy = (float)acc[n + i] * 5.9604644775390625e-08f;
@@ -535,7 +629,18 @@ int or_bd_run(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
   if (have_cl)
     cl_free(&cl);
   free(acc);
+  if (violations)
+    *violations += viol;
   return SWARM_OK;
+}
+
+int or_bd_run(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
+              uint32_t *ang, const uint8_t *species, const float *f_swim,
+              const float *torque_z, const float *f_ext, uint64_t step0,
+              int n_steps, uint32_t env, float *vel, float *omega,
+              int use_cells) {
+  return or_bd_run_walls(p, n, q, img, ang, species, f_swim, torque_z, f_ext, step0,
+                         n_steps, env, vel, omega, use_cells, NULL, 0, NULL);
 }
 
 /*
@@ -544,12 +649,15 @@ int or_bd_run(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
  * once every force is exactly zero (later steps would not move anything).
  * Returns the number of steps executed.
  */
-int or_sd_run(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
-              uint32_t *ang, const uint8_t *species, const float *f_swim,
-              const float *torque_z, const float *f_ext, int n_steps,
-              double gamma, double max_disp, int use_cells) {
+int or_sd_run_walls(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
+                    uint32_t *ang, const uint8_t *species, const float *f_swim,
+                    const float *torque_z, const float *f_ext, int n_steps,
+                    double gamma, double max_disp, int use_cells,
+                    const swarm_wall_t *walls, int n_walls) {
   derived_t d;
   derive(p, &d);
+  derive_walls(&d, walls, n_walls);
+  uint64_t viol = 0;
   const float g = (float)gamma, md = (float)max_disp;
   int64_t *acc = (int64_t *)malloc(sizeof(int64_t) * 2 * (size_t)(n > 0 ? n : 1));
   celllist_t cl;
@@ -560,6 +668,9 @@ int or_sd_run(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
     int any = 0;
     for (int i = 0; i < n; ++i) {
       float sn, cs;
+      if (d.n_walls)
+        wall_forces(&d, species[i], (float)q[i] * d.sx[0], (float)q[n + i] * d.sx[1], 0.0f,
+                    2, &acc[i], &acc[n + i], NULL, &viol);
       or_sincos_turn(ang[i], &sn, &cs);
       float fx = (float)acc[i] * 5.9604644775390625e-08f;
       float fy = (float)acc[n + i] * 5.9604644775390625e-08f;
@@ -584,6 +695,212 @@ int or_sd_run(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
   }
   if (have_cl)
     cl_free(&cl);
+  free(acc);
+  return s;
+}
+
+int or_sd_run(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
+              uint32_t *ang, const uint8_t *species, const float *f_swim,
+              const float *torque_z, const float *f_ext, int n_steps,
+              double gamma, double max_disp, int use_cells) {
+  return or_sd_run_walls(p, n, q, img, ang, species, f_swim, torque_z, f_ext, n_steps, gamma,
+                         max_disp, use_cells, NULL, 0);
+}
+
+/* ------------------------------------------------------------------ */
+/* 3-D (espresso.py:415-426: rotation about all three axes, no fixed    */
+/* coordinate).  Pair search is O(n^2): sums are exact, so the GPU's     */
+/* cell lists give the same bits.                                        */
+/* ------------------------------------------------------------------ */
+static void wca_pair3(const derived_t *d, int si, int sj, float rx, float ry, float rz,
+                      int64_t *ax, int64_t *ay, int64_t *az) {
+  float r2 = rx * rx + ry * ry;
+  r2 = r2 + rz * rz;
+  if (r2 < d->cut2[si][sj] && r2 > 0.0f) {
+    float ir2 = 1.0f / r2;
+    float ir6 = ir2 * ir2;
+    ir6 = ir6 * ir2;
+    float s6 = d->sig6[si][sj] * ir6;
+    float t = 2.0f * s6;
+    t = t - 1.0f;
+    float fr = d->eps24 * s6;
+    fr = fr * t;
+    fr = fr * ir2;
+    *ax += f2fix24(-fr * rx);
+    *ay += f2fix24(-fr * ry);
+    *az += f2fix24(-fr * rz);
+  }
+}
+
+static void wca_forces3(const swarm_params_t *p, const derived_t *d, int n, const uint32_t *q,
+                        const int32_t *img, const uint8_t *species, int64_t *acc) {
+  memset(acc, 0, sizeof(int64_t) * 3 * (size_t)n);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      if (j == i)
+        continue;
+      float rx = pair_disp(p, d, q, img, n, 0, i, j);
+      float ry = pair_disp(p, d, q, img, n, 1, i, j);
+      float rz = pair_disp(p, d, q, img, n, 2, i, j);
+      wca_pair3(d, species[i], species[j], rx, ry, rz, &acc[i], &acc[n + i], &acc[2 * n + i]);
+    }
+}
+
+/* Rotate the unit director v by the rotation vector (px, py, pz) (Rodrigues,
+ * angle = |p|) and renormalise. */
+void or_rotate_director(float v[3], float px, float py, float pz) {
+  float th2 = px * px + py * py;
+  th2 = th2 + pz * pz;
+  if (!(th2 > 0.0f))
+    return;
+  float th = sqrtf(th2);
+  float kx = px / th, ky = py / th, kz = pz / th;
+  float sn, cs;
+  or_sincos_turn((uint32_t)f2i32(th * ANG_INV_SCALE), &sn, &cs);
+  float kd = kx * v[0] + ky * v[1];
+  kd = kd + kz * v[2];
+  float cx = ky * v[2] - kz * v[1];
+  float cy = kz * v[0] - kx * v[2];
+  float cz = kx * v[1] - ky * v[0];
+  float kdo = kd * (1.0f - cs);
+  float n0 = v[0] * cs + cx * sn;
+  float n1 = v[1] * cs + cy * sn;
+  float n2 = v[2] * cs + cz * sn;
+  n0 = n0 + kx * kdo;
+  n1 = n1 + ky * kdo;
+  n2 = n2 + kz * kdo;
+  float nn = n0 * n0 + n1 * n1;
+  nn = nn + n2 * n2;
+  float nm = sqrtf(nn);
+  v[0] = n0 / nm;
+  v[1] = n1 / nm;
+  v[2] = n2 / nm;
+}
+
+/*
+ * n_steps 3-D Brownian-dynamics sub-steps of ONE env.  q/img [3][n];
+ * dir [3][n] fp32 unit directors; torque [3][n] lab frame; f_ext [3][n] or
+ * NULL; vel/omega [3][n] (NULL allowed): BD velocity and angular velocity of
+ * the last sub-step.  Noise tags: 0 translation, 2 rotation, 1 velocity,
+ * 3 angular velocity.
+ */
+int or_bd_run3(const swarm_params_t *p, int n, uint32_t *q, int32_t *img, float *dir,
+               const uint8_t *species, const float *f_swim, const float *torque,
+               const float *f_ext, uint64_t step0, int n_steps, uint32_t env, float *vel,
+               float *omega, const swarm_wall_t *walls, int n_walls, uint64_t *violations) {
+  if (p->n_dims != 3)
+    return SWARM_EINVAL;
+  derived_t d;
+  derive(p, &d);
+  derive_walls(&d, walls, n_walls);
+  uint64_t viol = 0;
+  int64_t *acc = (int64_t *)malloc(sizeof(int64_t) * 3 * (size_t)(n > 0 ? n : 1));
+  const int noisy = p->kT > 0.0;
+  for (int s = 0; s < n_steps; ++s) {
+    uint64_t step = step0 + (uint64_t)s;
+    wca_forces3(p, &d, n, q, img, species, acc);
+    for (int i = 0; i < n; ++i) {
+      int sp = species[i];
+      if (d.n_walls)
+        wall_forces(&d, sp, (float)q[i] * d.sx[0], (float)q[n + i] * d.sx[1],
+                    (float)q[2 * n + i] * d.sx[2], 3, &acc[i], &acc[n + i], &acc[2 * n + i],
+                    &viol);
+      float f[3], dq[3], ph[3], v[3] = {dir[i], dir[n + i], dir[2 * n + i]};
+      for (int a = 0; a < 3; ++a) {
+        f[a] = (float)acc[a * n + i] * 5.9604644775390625e-08f;
+        if (f_ext)
+          f[a] = f[a] + f_ext[a * n + i];
+        f[a] = f[a] + f_swim[i] * v[a];
+        dq[a] = f[a] * d.mob_dt[sp];
+        ph[a] = torque[a * n + i] * d.rot_dt[sp];
+      }
+      if (noisy) {
+        float g[3], h[3];
+        or_normals3(p->seed, env, (uint32_t)i, step, 0u, g);
+        or_normals3(p->seed, env, (uint32_t)i, step, 2u, h);
+        for (int a = 0; a < 3; ++a) {
+          dq[a] = dq[a] + d.sig_t[sp] * g[a];
+          ph[a] = ph[a] + d.sig_r[sp] * h[a];
+        }
+      }
+      for (int a = 0; a < 3; ++a)
+        advance(&q[a * n + i], &img[a * n + i], f2i32(dq[a] * d.inv_sx[a]));
+      or_rotate_director(v, ph[0], ph[1], ph[2]);
+      dir[i] = v[0];
+      dir[n + i] = v[1];
+      dir[2 * n + i] = v[2];
+      if (s == n_steps - 1) {
+        float vv[3], ww[3];
+        for (int a = 0; a < 3; ++a) {
+          vv[a] = f[a] * d.inv_gt[sp];
+          ww[a] = torque[a * n + i] * d.inv_gr[sp];
+        }
+        if (noisy) {
+          float g[3], h[3];
+          or_normals3(p->seed, env, (uint32_t)i, step, 1u, g);
+          or_normals3(p->seed, env, (uint32_t)i, step, 3u, h);
+          for (int a = 0; a < 3; ++a) {
+            vv[a] = vv[a] + d.sig_v[sp] * g[a];
+            ww[a] = ww[a] + d.sig_w[sp] * h[a];
+          }
+        }
+        for (int a = 0; a < 3; ++a) {
+          if (vel)
+            vel[a * n + i] = vv[a];
+          if (omega)
+            omega[a * n + i] = ww[a];
+        }
+      }
+    }
+  }
+  free(acc);
+  if (violations)
+    *violations += viol;
+  return SWARM_OK;
+}
+
+/* 3-D steepest descent: dp = clamp(gamma F) per coordinate, rotation by the
+ * rotation vector clamp(gamma tau) (espresso.py:1161-1168). */
+int or_sd_run3(const swarm_params_t *p, int n, uint32_t *q, int32_t *img, float *dir,
+               const uint8_t *species, const float *f_swim, const float *torque,
+               const float *f_ext, int n_steps, double gamma, double max_disp,
+               const swarm_wall_t *walls, int n_walls) {
+  derived_t d;
+  derive(p, &d);
+  derive_walls(&d, walls, n_walls);
+  uint64_t viol = 0;
+  const float g = (float)gamma, md = (float)max_disp;
+  int64_t *acc = (int64_t *)malloc(sizeof(int64_t) * 3 * (size_t)(n > 0 ? n : 1));
+  int s;
+  for (s = 0; s < n_steps; ++s) {
+    wca_forces3(p, &d, n, q, img, species, acc);
+    int any = 0;
+    for (int i = 0; i < n; ++i) {
+      int sp = species[i];
+      if (d.n_walls)
+        wall_forces(&d, sp, (float)q[i] * d.sx[0], (float)q[n + i] * d.sx[1],
+                    (float)q[2 * n + i] * d.sx[2], 3, &acc[i], &acc[n + i], &acc[2 * n + i],
+                    &viol);
+      float v[3] = {dir[i], dir[n + i], dir[2 * n + i]}, pr[3];
+      for (int a = 0; a < 3; ++a) {
+        float f = (float)acc[a * n + i] * 5.9604644775390625e-08f;
+        if (f_ext)
+          f = f + f_ext[a * n + i];
+        f = f + f_swim[i] * v[a];
+        if (f != 0.0f || torque[a * n + i] != 0.0f)
+          any = 1;
+        float dp = fminf(fmaxf(g * f, -md), md);
+        pr[a] = fminf(fmaxf(g * torque[a * n + i], -md), md);
+        advance(&q[a * n + i], &img[a * n + i], f2i32(dp * d.inv_sx[a]));
+      }
+      or_rotate_director(v, pr[0], pr[1], pr[2]);
+      dir[i] = v[0];
+      dir[n + i] = v[1];
+      dir[2 * n + i] = v[2];
+    }
+    if (!any)
+      break;
+  }
   free(acc);
   return s;
 }
@@ -673,8 +990,8 @@ void or_field_distance(const swarm_params_t *p, int n, const uint32_t *q,
     int i = agents[ai];
     float cur[3], prev[3];
     for (int a = 0; a < 3; ++a) {
-      double pc = a < 2 ? unwrap(p, q, img, n, a, i) / box_scale[a] : 0.0 / box_scale[a];
-      double hp = a < 2 ? ((double)hist_img[a * n_agents + ai] +
+      double pc = a < p->n_dims ? unwrap(p, q, img, n, a, i) / box_scale[a] : 0.0 / box_scale[a];
+      double hp = a < p->n_dims ? ((double)hist_img[a * n_agents + ai] +
                            (double)hist_q[a * n_agents + ai] * (1.0 / TWO32)) *
                               p->box[a] / box_scale[a]
                         : 0.0 / box_scale[a];

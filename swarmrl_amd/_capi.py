@@ -64,6 +64,26 @@ class SwarmDeviceViews(ctypes.Structure):
         ("species", ctypes.c_void_p),
         ("n_envs", ctypes.c_int32),
         ("n_particles", ctypes.c_int32),
+        ("n_dims", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
+        ("dir3", ctypes.c_void_p),
+        ("torque_xy", ctypes.c_void_p),
+        ("omega_xy", ctypes.c_void_p),
+    ]
+
+
+SWARM_MAX_WALLS = 16
+
+
+class SwarmWall(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("normal", ctypes.c_double * 3),
+        ("offset", ctypes.c_double),
+        ("corner", ctypes.c_double * 3),
+        ("a", ctypes.c_double * 3),
+        ("b", ctypes.c_double * 3),
     ]
 
 
@@ -135,6 +155,11 @@ _SIGNATURES = {
         [_P, _P, ctypes.c_int32, _P, _P, _P, _P, ctypes.c_float, ctypes.c_float,
          ctypes.c_float, ctypes.c_int32, _P],
     ),
+    "swarm_engine_set_torque_xy": (ctypes.c_int, [_P, _P, ctypes.c_int32]),
+    "swarm_engine_upload_directors": (ctypes.c_int, [_P, _P]),
+    "swarm_engine_download_directors": (ctypes.c_int, [_P, _P]),
+    "swarm_engine_set_walls": (ctypes.c_int, [_P, _P, ctypes.c_int32]),
+    "swarm_engine_wall_violations": (ctypes.c_int, [_P, _P]),
     "swarm_engine_neighbor_pairs": (
         ctypes.c_int,
         [_P, ctypes.c_int32, ctypes.c_double, _P, ctypes.c_int32, _P],

@@ -31,6 +31,7 @@
 #include "../../include/swarmrl_amd.h"
 #include "swarm_device.cuh"
 #include "swarm_integrator.cuh"
+#include "swarm_integrator3.cuh"
 #include "swarm_policy.cuh"
 
 namespace {
@@ -110,6 +111,11 @@ void derive(const swarm_params_t& p, Derived& d) {
   d.key1 = (uint32_t)(p.seed >> 32);
   d.noisy = p.kT > 0.0 ? 1 : 0;
   d.periodic = p.periodic;
+  for (int s = 0; s < p.n_species; ++s) {  // walls: WCA with a radius-0 wall type
+    const double rc2 = p.radius[s] * p.radius[s];
+    d.wcut2[s] = (float)rc2;
+    d.wsig6[s] = (float)(rc2 * rc2 * rc2 * 0.5);
+  }
 }
 
 int ilog2_floor(double v) {
@@ -138,6 +144,27 @@ void cell_grid(const swarm_params_t& p, int n, double cutoff, int* lx, int* ly) 
   }
   *lx = l[0];
   *ly = l[1];
+}
+
+// 3-D: the same rule over three axes (3-D global path).
+void cell_grid3(const swarm_params_t& p, int n, double cutoff, int* lx, int* ly, int* lz) {
+  int l[3];
+  for (int a = 0; a < 3; ++a) {
+    const double m = cutoff > 0.0 ? p.box[a] / cutoff : 1024.0;
+    l[a] = m >= 1.0 ? ilog2_floor(m) : 0;
+    if (l[a] > 10) l[a] = 10;
+  }
+  const int cap = std::min(n > 64 ? n : 64, 8192);  // counts fit the default 64 KB of LDS
+  while ((1 << (l[0] + l[1] + l[2])) > cap) {
+    int k = 0;
+    for (int a = 1; a < 3; ++a)
+      if (l[a] > l[k]) k = a;
+    if (l[k] == 0) break;
+    l[k]--;
+  }
+  *lx = l[0];
+  *ly = l[1];
+  *lz = l[2];
 }
 
 // ------------------------------------------------- global per-env grid
@@ -404,17 +431,17 @@ __global__ __launch_bounds__(256) void k_pair_dist(DevState st, const double* __
   float xi[3] = {0.0f, 0.0f, 0.0f};
   if (a < n_agents) {
     const size_t gi = base + agents[a];
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < st.dims; ++k)
       xi[k] = (float)(((double)st.img[k * M + gi] + (double)st.q[k * M + gi] * inv32) * box[k]);
   }
   const int c0 = blockIdx.y * 256;
   const int cn = min(256, mc - c0);
   if (threadIdx.x < cn) {
     const size_t gj = base + sensed[m0 + c0 + threadIdx.x];
-    for (int k = 0; k < 2; ++k)
+    tile[threadIdx.x][2] = 0.0f;
+    for (int k = 0; k < st.dims; ++k)
       tile[threadIdx.x][k] =
           (float)(((double)st.img[k * M + gj] + (double)st.q[k * M + gj] * inv32) * box[k]);
-    tile[threadIdx.x][2] = 0.0f;
   }
   __syncthreads();
   if (a >= n_agents) return;
@@ -452,7 +479,7 @@ __global__ __launch_bounds__(256) void k_field(DevState st, const double* __rest
     float cur[3], prev[3];
     for (int a = 0; a < 3; ++a) {
       double pc, hp;
-      if (a < 2) {
+      if (a < st.dims) {
         pc = ((double)st.img[a * M + gi] + (double)st.q[a * M + gi] * inv32) * box[a] / bs[a];
         hp = ((double)himg[(size_t)a * A + t] + (double)hq[(size_t)a * A + t] * inv32) * box[a] / bs[a];
       } else {
@@ -480,8 +507,8 @@ __global__ __launch_bounds__(256) void k_field(DevState st, const double* __rest
   }
   if (update || init_only) {
     for (int a = 0; a < 3; ++a) {
-      hq[(size_t)a * A + t] = a < 2 ? st.q[a * M + gi] : 0u;
-      himg[(size_t)a * A + t] = a < 2 ? st.img[a * M + gi] : 0;
+      hq[(size_t)a * A + t] = a < st.dims ? st.q[a * M + gi] : 0u;
+      himg[(size_t)a * A + t] = a < st.dims ? st.img[a * M + gi] : 0;
     }
   }
 }
@@ -552,7 +579,7 @@ struct swarm_engine {
   int32_t* d_count = nullptr;
   int32_t* d_pairs = nullptr;
   size_t pairs_cap = 0;
-  int lxg = 0, lyg = 0;  // global-path grid: cell side >= rc_max
+  int lxg = 0, lyg = 0, lzg = 0;  // global-path grid: cell side >= rc_max (lzg: 3-D)
   int lxb = 0, lyb = 0;  // cluster-build grid: cell side >= rc_max + skin
   bool cluster_path = false;
   bool big_build = false;  // k_cluster_build<true>: cluster arrays in global memory
@@ -631,6 +658,14 @@ void set_lds_attributes() {
 }
 
 int launch_global(swarm_engine* e, int n_steps, int sd_mode, float g, float md) {
+  if (e->params.n_dims == 3) {
+    hipLaunchKernelGGL(swarm::k_global3, dim3(e->n_envs), dim3(1024),
+                       (16 + (size_t)(1 << (e->lxg + e->lyg + e->lzg)) + 1) * 4, e->stream,
+                       e->d_derived, e->st, e->sc, n_steps, e->d_step, e->d_arrive, e->lxg,
+                       e->lyg, e->lzg, sd_mode, g, md);
+    HIP_TRY(hipGetLastError());
+    return SWARM_OK;
+  }
   hipLaunchKernelGGL(swarm::k_global, dim3(e->n_envs), dim3(1024),
                      global_lds_bytes(e->lxg, e->lyg), e->stream, e->d_derived, e->st, e->sc,
                      n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg, sd_mode, g, md);
@@ -817,14 +852,14 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
                         const int32_t* species, swarm_engine_t** out) {
   if (!params || !out) return fail(SWARM_EINVAL, "null argument");
   *out = nullptr;
-  if (params->n_dims != 2)
-    return fail(SWARM_EINVAL, "only n_dims == 2 is implemented in this build");
+  if (params->n_dims != 2 && params->n_dims != 3)
+    return fail(SWARM_EINVAL, "n_dims must be 2 or 3");
   if (!params->periodic)
     return fail(SWARM_EINVAL, "non-periodic boxes are not implemented on the GPU in this build");
   if (n_envs < 1 || n_particles < 1) return fail(SWARM_EINVAL, "n_envs and n_particles must be >= 1");
   if (params->n_species < 1 || params->n_species > kMaxSpecies)
     return fail(SWARM_EINVAL, "n_species out of range");
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < params->n_dims; ++a)
     if (!(params->box[a] > 0.0)) return fail(SWARM_EINVAL, "box lengths must be positive");
   if (!(params->time_step > 0.0)) return fail(SWARM_EINVAL, "time_step must be positive");
   for (int s = 0; s < params->n_species; ++s)
@@ -845,7 +880,11 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     delete e;
     return fail(SWARM_EDEVICE, "no HIP device");
   }
-  cell_grid(*params, n_particles, e->derived.rc_max, &e->lxg, &e->lyg);
+  const bool three_d = params->n_dims == 3;
+  if (three_d)
+    cell_grid3(*params, n_particles, e->derived.rc_max, &e->lxg, &e->lyg, &e->lzg);
+  else
+    cell_grid(*params, n_particles, e->derived.rc_max, &e->lxg, &e->lyg);
   cell_grid(*params, n_particles, e->derived.rc_max + kSkin, &e->lxb, &e->lyb);
   // static LDS of the kernels: pair tables (k_global, k_check, k_cluster_run)
   // and the link table of k_cluster_build
@@ -858,7 +897,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   // build grid; otherwise every window runs on the global path
   e->big_build = build_is_big(n_particles);
   e->sc.pair_cap = build_pair_cap(n_particles, e->big_build);
-  e->cluster_path = e->sc.pair_cap >= n_particles && n_particles < 65536 &&
+  e->cluster_path = !three_d && e->sc.pair_cap >= n_particles && n_particles < 65536 &&
                     swarm::build_lds_words_big(n_particles) * 4 <= kMaxLds &&
                     (size_t)(16 + (1 << (e->lxb + e->lyb)) + 1) * 4 <= kMaxLds &&
                     (1 << e->lxb) >= 3 && (1 << e->lyb) >= 3;
@@ -900,6 +939,11 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   e->sc.wmax = S / 64;
   rc = rc ? rc : dev_alloc(e, &e->sc.sqx, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.sqy, M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.sqz, M);
+  rc = rc ? rc : dev_alloc(e, &e->st.dir3, 3 * M);
+  rc = rc ? rc : dev_alloc(e, &e->st.torque_xy, 2 * M);
+  rc = rc ? rc : dev_alloc(e, &e->st.omega_xy, 2 * M);
+  rc = rc ? rc : dev_alloc(e, &e->st.wall_viol, 1);
   rc = rc ? rc : dev_alloc(e, &e->sc.sidx, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.bq, 2 * M);
   rc = rc ? rc : dev_alloc(e, &e->sc.bimg, 2 * M);
@@ -941,6 +985,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   }
   e->st.n = n_particles;
   e->st.m = (int32_t)M;
+  e->st.dims = params->n_dims;
   std::vector<uint8_t> sp(n_particles);
   for (int i = 0; i < n_particles; ++i) sp[i] = (uint8_t)species[i];
   if (hipMemcpy(e->st.species, sp.data(), sp.size(), hipMemcpyHostToDevice) != hipSuccess ||
@@ -1000,9 +1045,20 @@ int swarm_engine_upload_state(swarm_engine_t* e, const double* pos, const double
   const size_t M = (size_t)e->st.m;
   std::vector<uint32_t> q(3 * M, 0u), ang(M);
   std::vector<int32_t> img(3 * M, 0);
+  const int D = e->params.n_dims;
+  std::vector<float> d3(D == 3 ? 3 * M : 0);
   for (size_t g = 0; g < M; ++g) {
-    for (int a = 0; a < 2; ++a) to_fixed(pos[3 * g + a], e->params.box[a], &q[a * M + g], &img[a * M + g]);
+    for (int a = 0; a < D; ++a) to_fixed(pos[3 * g + a], e->params.box[a], &q[a * M + g], &img[a * M + g]);
     ang[g] = angle_fixed(director[3 * g + 0], director[3 * g + 1]);
+    if (D == 3) {
+      const double* v = director + 3 * g;
+      const double nm = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+      for (int a = 0; a < 3; ++a) d3[a * M + g] = (float)(nm > 0.0 ? v[a] / nm : (a == 2));
+    }
+  }
+  if (D == 3) {
+    const int rc = swarm_engine_upload_directors(e, d3.data());
+    if (rc) return rc;
   }
   return swarm_engine_upload_raw(e, q.data(), img.data(), ang.data());
 }
@@ -1013,6 +1069,11 @@ int swarm_engine_download_state(swarm_engine_t* e, double* pos, double* director
   std::vector<uint32_t> q(3 * M), ang(M);
   std::vector<int32_t> img(3 * M);
   std::vector<float> vel(velocity ? 3 * M : 0);
+  const int D = e->params.n_dims;
+  std::vector<float> d3(D == 3 && director ? 3 * M : 0);
+  if (!d3.empty())
+    HIP_TRY(hipMemcpyAsync(d3.data(), e->st.dir3, 3 * M * sizeof(float), hipMemcpyDeviceToHost,
+                           e->stream));
   HIP_TRY(hipMemcpyAsync(q.data(), e->st.q, 3 * M * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipMemcpyAsync(img.data(), e->st.img, 3 * M * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipMemcpyAsync(ang.data(), e->st.ang, M * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
@@ -1021,11 +1082,14 @@ int swarm_engine_download_state(swarm_engine_t* e, double* pos, double* director
   HIP_TRY(hipStreamSynchronize(e->stream));
   for (size_t g = 0; g < M; ++g) {
     if (pos) {
-      for (int a = 0; a < 2; ++a)
-        pos[3 * g + a] = ((double)img[a * M + g] + (double)q[a * M + g] / kTwo32) * e->params.box[a];
-      pos[3 * g + 2] = 0.0;
+      for (int a = 0; a < 3; ++a)
+        pos[3 * g + a] = a < D ? ((double)img[a * M + g] + (double)q[a * M + g] / kTwo32) *
+                                     e->params.box[a]
+                               : 0.0;
     }
-    if (director) {
+    if (director && D == 3) {
+      for (int a = 0; a < 3; ++a) director[3 * g + a] = d3[a * M + g];
+    } else if (director) {
       float so, co;
       host_sincos_turn(ang[g], &so, &co);
       director[3 * g + 0] = co;
@@ -1072,6 +1136,20 @@ int swarm_engine_set_external_force(swarm_engine_t* e, const double* f_ext) {
 int swarm_engine_set_directors(swarm_engine_t* e, const double* dir, const uint8_t* mask) {
   if (!e || !dir || !mask) return fail(SWARM_EINVAL, "null argument");
   const size_t M = (size_t)e->st.m;
+  if (e->params.n_dims == 3) {  // coll.director = new_direction (espresso.py:1238-1239)
+    std::vector<float> d3(3 * M);
+    HIP_TRY(hipMemcpyAsync(d3.data(), e->st.dir3, 3 * M * sizeof(float), hipMemcpyDeviceToHost,
+                           e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    for (size_t g = 0; g < M; ++g) {
+      if (!mask[g]) continue;
+      const double* v = dir + 3 * g;
+      const double nm = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+      if (!(nm > 0.0)) return fail(SWARM_EINVAL, "new_direction must be non-zero");
+      for (int a = 0; a < 3; ++a) d3[a * M + g] = (float)(v[a] / nm);
+    }
+    return swarm_engine_upload_directors(e, d3.data());
+  }
   std::vector<uint32_t> ang(M);
   HIP_TRY(hipMemcpyAsync(ang.data(), e->st.ang, M * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1178,12 +1256,17 @@ int swarm_engine_device_views(swarm_engine_t* e, swarm_device_views_t* v) {
   v->species = e->st.species;
   v->n_envs = e->n_envs;
   v->n_particles = e->n;
+  v->n_dims = e->params.n_dims;
+  v->dir3 = e->st.dir3;
+  v->torque_xy = e->st.torque_xy;
+  v->omega_xy = e->st.omega_xy;
   return SWARM_OK;
 }
 
 int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const int32_t* agent_idx,
                       int32_t n_agents, const float* radii, const int32_t* types, float* out) {
   if (!e || !vp || !agent_idx || !radii || !types || !out) return fail(SWARM_EINVAL, "null argument");
+  if (e->params.n_dims != 2) return fail(SWARM_EINVAL, "the vision-cone kernel is 2-D only");
   if (vp->n_cones < 1 || vp->n_cones > SWARM_MAX_CONES || vp->n_types < 1 ||
       vp->n_types > SWARM_MAX_DETECTED_TYPES || vp->n_cones * vp->n_types > 2 * SWARM_MAX_CONES)
     return fail(SWARM_ECAPACITY, "n_cones * n_types exceeds this build's limit (32)");
@@ -1287,6 +1370,7 @@ int swarm_engine_neighbor_pairs(swarm_engine_t* e, int32_t env, double cutoff, i
                                 int32_t max_pairs, int32_t* n_pairs) {
   if (!e || !pairs || !n_pairs) return fail(SWARM_EINVAL, "null argument");
   if (env < 0 || env >= e->n_envs) return fail(SWARM_EINVAL, "env out of range");
+  if (e->params.n_dims != 2) return fail(SWARM_EINVAL, "neighbor_pairs is 2-D only");
   if (!(2.0 * cutoff < std::min(e->params.box[0], e->params.box[1])))
     return fail(SWARM_EINVAL, "cutoff must be below half the box length");
   int lx, ly;
@@ -1312,6 +1396,77 @@ int swarm_engine_neighbor_pairs(swarm_engine_t* e, int32_t env, double cutoff, i
   if (got > 0)
     HIP_TRY(hipMemcpy(pairs, e->d_pairs, 2 * (size_t)got * sizeof(int32_t), hipMemcpyDeviceToHost));
   if (cnt > max_pairs) return fail(SWARM_ECAPACITY, "more pairs than max_pairs");
+  return SWARM_OK;
+}
+
+int swarm_engine_set_torque_xy(swarm_engine_t* e, const float* torque_xy, int32_t on_device) {
+  if (!e || !torque_xy) return fail(SWARM_EINVAL, "null argument");
+  const size_t M = (size_t)e->st.m;
+  const hipMemcpyKind kind = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  HIP_TRY(hipMemcpyAsync(e->st.torque_xy, torque_xy, 2 * M * sizeof(float), kind, e->stream));
+  if (!on_device) HIP_TRY(hipStreamSynchronize(e->stream));
+  return SWARM_OK;
+}
+
+int swarm_engine_upload_directors(swarm_engine_t* e, const float* dir3) {
+  if (!e || !dir3) return fail(SWARM_EINVAL, "null argument");
+  const size_t M = (size_t)e->st.m;
+  HIP_TRY(hipMemcpyAsync(e->st.dir3, dir3, 3 * M * sizeof(float), hipMemcpyHostToDevice,
+                         e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return SWARM_OK;
+}
+
+int swarm_engine_download_directors(swarm_engine_t* e, float* dir3) {
+  if (!e || !dir3) return fail(SWARM_EINVAL, "null argument");
+  const size_t M = (size_t)e->st.m;
+  HIP_TRY(hipMemcpyAsync(dir3, e->st.dir3, 3 * M * sizeof(float), hipMemcpyDeviceToHost,
+                         e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return SWARM_OK;
+}
+
+int swarm_engine_set_walls(swarm_engine_t* e, const swarm_wall_t* walls, int32_t n_walls) {
+  if (!e) return fail(SWARM_EINVAL, "null engine");
+  if (n_walls < 0 || n_walls > SWARM_MAX_WALLS) return fail(SWARM_ECAPACITY, "0 <= n_walls <= 16");
+  if (n_walls > 0 && !walls) return fail(SWARM_EINVAL, "null walls");
+  Derived& d = e->derived;
+  d.n_walls = n_walls;
+  for (int k = 0; k < n_walls; ++k) {
+    const swarm_wall_t& w = walls[k];
+    float* o = d.wp[k];
+    d.wkind[k] = w.kind;
+    if (w.kind == 0) {
+      for (int a = 0; a < 3; ++a) o[a] = (float)w.normal[a];
+      o[3] = (float)w.offset;
+    } else if (w.kind == 1) {
+      const double la = std::sqrt(w.a[0] * w.a[0] + w.a[1] * w.a[1]);
+      const double lb = std::sqrt(w.b[0] * w.b[0] + w.b[1] * w.b[1]);
+      if (!(la > 0.0) || !(lb > 0.0)) return fail(SWARM_EINVAL, "degenerate wall");
+      o[0] = (float)w.corner[0];
+      o[1] = (float)w.corner[1];
+      o[2] = (float)(w.a[0] / la);
+      o[3] = (float)(w.a[1] / la);
+      o[4] = (float)(w.b[0] / lb);
+      o[5] = (float)(w.b[1] / lb);
+      o[6] = (float)la;
+      o[7] = (float)lb;
+    } else {
+      return fail(SWARM_EINVAL, "wall kind must be 0 (plane) or 1 (slab)");
+    }
+  }
+  HIP_TRY(hipMemcpyAsync(e->d_derived, &e->derived, sizeof(Derived), hipMemcpyHostToDevice,
+                         e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return SWARM_OK;
+}
+
+int swarm_engine_wall_violations(swarm_engine_t* e, uint64_t* count) {
+  if (!e || !count) return fail(SWARM_EINVAL, "null argument");
+  unsigned long long v = 0;
+  HIP_TRY(hipMemcpyAsync(&v, e->st.wall_viol, sizeof(v), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  *count = v;
   return SWARM_OK;
 }
 

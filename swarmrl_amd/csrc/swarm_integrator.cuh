@@ -68,6 +68,11 @@ struct Derived {
   int32_t noisy;
   int32_t periodic;
   double rc_max;
+  // walls (swarm_engine_set_walls): plane n0 n1 n2 off | slab o0 o1 a0 a1 b0 b1 la lb
+  int32_t n_walls;
+  int32_t wkind[SWARM_MAX_WALLS];
+  float wp[SWARM_MAX_WALLS][8];
+  float wcut2[kMaxSpecies], wsig6[kMaxSpecies];  // wall WCA per species (radius 0 wall)
 };
 
 struct DevState {
@@ -82,11 +87,18 @@ struct DevState {
   uint8_t* species;  // [N]
   int32_t n;         // particles per env
   int32_t m;         // E * N
+  int32_t dims;      // 2 or 3
+  // 3-D only
+  float* dir3;       // [3][M] unit directors
+  float* torque_xy;  // [2][M] (z: torque_z)
+  float* omega_xy;   // [2][M] (z: omega)
+  unsigned long long* wall_viol;  // [1] wall contacts with dist <= 0
 };
 
 struct Scratch {
   uint32_t* sqx;      // [M] positions sorted by cell
   uint32_t* sqy;      // [M]
+  uint32_t* sqz;      // [M] (3-D global path)
   int32_t* sidx;      // [M] particle index of a sorted entry
   uint32_t* bq;       // [2][M] window-start snapshot
   int32_t* bimg;      // [2][M]
@@ -213,6 +225,61 @@ __device__ __forceinline__ void pair_fix_sel(float cut2, float sig6, float eps24
   } else {
     fx = __float2ll_rn(fminf(fmaxf(vx, -4.611686018427387904e18f), 4.611686018427387904e18f));
     fy = __float2ll_rn(fminf(fmaxf(vy, -4.611686018427387904e18f), 4.611686018427387904e18f));
+  }
+}
+
+// WCA force of every wall on a particle of species si at the folded
+// position (x, y, z) in 2^-24 fixed point (same operation sequence as
+// oracle/swarm_oracle.c:wall_forces); contacts with dist <= 0 are counted.
+template <int D>
+__device__ __forceinline__ void wall_forces(const Derived* __restrict__ d, int si, float x, float y,
+                                            float z, int64_t& ax, int64_t& ay, int64_t& az,
+                                            unsigned long long* viol) {
+  const int nw = d->n_walls;
+  for (int k = 0; k < nw; ++k) {
+    const float* w = d->wp[k];
+    float vx, vy, vz, r2;
+    if (d->wkind[k] == 0) {
+      float dist = w[0] * x + w[1] * y;
+      dist = dist + w[2] * z;
+      dist = dist - w[3];
+      if (!(dist > 0.0f)) {
+        atomicAdd(viol, 1ull);
+        continue;
+      }
+      vx = w[0] * dist;
+      vy = w[1] * dist;
+      vz = w[2] * dist;
+      r2 = dist * dist;
+    } else {
+      const float px = x - w[0], py = y - w[1];
+      const float u = px * w[2] + py * w[3];
+      const float t = px * w[4] + py * w[5];
+      const float du = u - fminf(fmaxf(u, 0.0f), w[6]);
+      const float dt = t - fminf(fmaxf(t, 0.0f), w[7]);
+      if (du == 0.0f && dt == 0.0f) {
+        atomicAdd(viol, 1ull);
+        continue;
+      }
+      vx = du * w[2] + dt * w[4];
+      vy = du * w[3] + dt * w[5];
+      vz = 0.0f;
+      r2 = vx * vx + vy * vy;
+    }
+    if (r2 < d->wcut2[si]) {
+      const float ir2 = 1.0f / r2;
+      float ir6 = ir2 * ir2;
+      ir6 = ir6 * ir2;
+      const float s6 = d->wsig6[si] * ir6;
+      float t = 2.0f * s6;
+      t = t - 1.0f;
+      float fr = d->eps24 * s6;
+      fr = fr * t;
+      fr = fr * ir2;
+      ax += f2fix24(fr * vx);
+      ay += f2fix24(fr * vy);
+      if (D == 3) az += f2fix24(fr * vz);
+    }
   }
 }
 
@@ -398,6 +465,11 @@ __device__ void block_global_run(const Derived* __restrict__ d, const DevState& 
             pair_force(pt->cut2[pk], pt->sig6[pk], eps24, rx, ry, ax, ay);
           }
         }
+      }
+      if (d->n_walls) {
+        int64_t az = 0;
+        wall_forces<2>(d, si, (float)p.qx * sx0, (float)p.qy * sx1, 0.0f, ax, ay, az,
+                       st.wall_viol);
       }
       const float fs = st.f_swim[gi], tz = st.torque_z[gi];
       const float fex = st.f_ext[gi], fey = st.f_ext[M + gi];
@@ -956,6 +1028,7 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
   const float eps24 = d->eps24;
   const PConst pc = load_pconst(d, si);
   const float cut2_0 = d->cut2[0], sig6_0 = d->sig6[0];
+  const int nwalls = d->n_walls;
   const uint32_t q0x = p.qx, q0y = p.qy;
   float dmax2 = 0.0f;
   float vx = 0.0f, vy = 0.0f, om = 0.0f;
@@ -1042,6 +1115,11 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
 #else
     if (active) {
 #endif
+      if (nwalls) {  // wave-uniform
+        int64_t az = 0;
+        wall_forces<2>(d, si, (float)p.qx * sx0, (float)p.qy * sx1, 0.0f, ax, ay, az,
+                       st.wall_viol);
+      }
       bd_step<kTable>(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i,
                       step0 + (uint64_t)s, s == n_steps - 1, &vx, &vy, &om, gt, dir);
       const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;

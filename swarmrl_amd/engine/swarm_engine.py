@@ -83,15 +83,23 @@ class MDParams:
 def _get_random_start_pos(
     init_radius: float, init_center: np.ndarray, dim: int, rng: np.random.Generator
 ):
-    """Uniform point in a disc (espresso.py:91-105; 2-D branch)."""
+    """Uniform point in a disc (2-D) or ball (3-D), espresso.py:91-105."""
     if dim == 2:
         r = init_radius * np.sqrt(rng.random())
         theta = 2 * np.pi * rng.random()
         pos = r * np.array([np.cos(theta), np.sin(theta), 0])
         assert init_center[2] == 0.0
+    elif dim == 3:
+        r = init_radius * np.cbrt(rng.random())
+        pos = r * _vector_from_angles(*_get_random_angles(rng))
     else:
-        raise ValueError("Random position finder only implemented for 2d in this build")
+        raise ValueError("Random position finder only implemented for 2d and 3d")
     return pos + init_center
+
+
+def _get_random_angles(rng: np.random.Generator):
+    """utils.get_random_angles (utils.py:19-21): uniform on the sphere."""
+    return np.arccos(2.0 * rng.random() - 1), 2.0 * np.pi * rng.random()
 
 
 def _calc_friction_coefficients(dyn_visc: float, radius: float):
@@ -121,6 +129,7 @@ class _SystemState:
 
     def __init__(self):
         self.time = 0.0
+        self.constraints = []  # wall shapes (espressomd.constraints analogue)
 
 
 class _Particle:
@@ -212,11 +221,6 @@ class SwarmEngine(Engine):
         self.rng = np.random.default_rng(self.seed)
         if n_dims not in [2, 3]:
             raise ValueError("Only 2d and 3d are allowed")
-        if n_dims == 3:
-            raise NotImplementedError(
-                "3-D dynamics are not implemented in this build of the MI355X engine "
-                "(2-D only, see DESIGN.md)"
-            )
         self.n_dims = n_dims
         if int(n_envs) < 1:
             raise ValueError("n_envs must be >= 1")
@@ -244,6 +248,7 @@ class SwarmEngine(Engine):
         self._species_keys: typing.List[tuple] = []
         self._species_of: typing.List[int] = []
         self._ext_force = None
+        self._walls = []  # swarm_wall_t dicts (add_confining_walls / add_walls)
         self._native: _NativeEngine = None
         self._host_cache = None
         self._view = None
@@ -412,6 +417,14 @@ class SwarmEngine(Engine):
         init_pos = np.array(init_position.m_as("sim_length"), dtype=float)
         init_direction = np.asarray(init_direction, dtype=float)
         init_direction = init_direction / np.linalg.norm(init_direction)
+        if self.n_dims == 3:  # espresso.py:415-426
+            handle = self._register_particle(
+                [init_pos] * self.n_envs, [init_direction] * self.n_envs, type_colloid, key
+            )
+            self.colloid_radius_register.update(
+                {type_colloid: {"radius": radius_simunits, "aspect_ratio": aspect_ratio}}
+            )
+            return handle
         init_pos[2] = 0
         theta, phi = _angles_from_vector(init_direction)
         if abs(theta - np.pi / 2) > 10e-6:
@@ -465,6 +478,11 @@ class SwarmEngine(Engine):
             for e in range(self.n_envs):
                 rng = self._env_rngs[e]
                 start_pos = _get_random_start_pos(init_rad, init_center, self.n_dims, rng)
+                if self.n_dims == 3:  # espresso.py:526-529
+                    d = _vector_from_angles(*_get_random_angles(rng))
+                    positions.append(np.array(start_pos, dtype=float))
+                    directions.append(d / np.linalg.norm(d))
+                    continue
                 start_angle = 2 * np.pi * rng.random()
                 init_direction = _vector_from_angles(np.pi / 2, start_angle)
                 init_direction = init_direction / np.linalg.norm(init_direction)
@@ -489,6 +507,68 @@ class SwarmEngine(Engine):
             self._native.bind_stream()
             ext = np.ascontiguousarray(self._ext_force.reshape(-1, 3))
             self._native.call("swarm_engine_set_external_force", ext.ctypes.data)
+
+    def add_confining_walls(self, wall_type: int):
+        """WCA walls on the box faces (espresso.py:667-704): x = 0, x = L_x,
+        y = 0, y = L_y (and z in 3-D), interacting with every particle."""
+        self._check_already_initialised()
+        if wall_type in self.colloid_radius_register.keys():
+            raise ValueError(
+                f"wall type {wall_type} is already taken by other system component. "
+                "Choose a new one"
+            )
+        L = self._box
+        normals = [([1, 0, 0], 0.0), ([-1, 0, 0], -L[0]), ([0, 1, 0], 0.0), ([0, -1, 0], -L[1])]
+        if self.n_dims == 3:
+            normals += [([0, 0, 1], 0.0), ([0, 0, -1], -L[2])]
+        for n, off in normals:
+            self._add_wall({"kind": 0, "normal": n, "offset": off})
+        self.colloid_radius_register.update({wall_type: {"radius": 0.0, "aspect_ratio": 1.0}})
+
+    def add_walls(self, wall_start_point: Quantity, wall_end_point: Quantity, wall_type: int,
+                  wall_thickness: Quantity):
+        """Rectangular walls from start to end points of the given thickness,
+        spanning the box in z (espresso.py:706-800, Rhomboid constraints)."""
+        start = np.asarray(wall_start_point.m_as("sim_length"), dtype=float)
+        end = np.asarray(wall_end_point.m_as("sim_length"), dtype=float)
+        thickness = float(wall_thickness.m_as("sim_length"))
+        if len(start) != len(end):
+            raise ValueError(
+                " Please double check your walls. There are more or less "
+                f" starting points {len(start)} than "
+                f" end points {len(end)}. They should be equal."
+            )
+        self._check_already_initialised()
+        if wall_type in self.colloid_radius_register.keys():
+            if self.colloid_radius_register[wall_type] != 0.0:
+                raise ValueError(
+                    f" The chosen type {wall_type} is already taken"
+                    "and used with a different radius "
+                    f"{self.colloid_radius_register[wall_type]['radius']}."
+                    " Choose a new combination"
+                )
+        z_height = self._box[2]
+        for k in range(len(start)):
+            a = np.array([end[k, 0] - start[k, 0], end[k, 1] - start[k, 1], 0.0])
+            c = np.array([0.0, 0.0, z_height])
+            b = np.cross(a / np.linalg.norm(a), c / np.linalg.norm(c)) * thickness
+            corner = [start[k, 0] - b[0] / 2, start[k, 1] - b[1] / 2, 0.0]
+            self._add_wall({"kind": 1, "corner": corner, "a": a, "b": b})
+        self.colloid_radius_register.update({wall_type: {"radius": 0.0, "aspect_ratio": 1.0}})
+
+    def _add_wall(self, wall: dict):
+        if len(self._walls) >= _capi.SWARM_MAX_WALLS:
+            raise ValueError(f"at most {_capi.SWARM_MAX_WALLS} walls are supported")
+        self._walls.append(wall)
+        self.system.constraints.append(wall)
+
+    def wall_violations(self) -> int:
+        """Wall contacts with distance <= 0 so far (ESPResSo raises on those)."""
+        if self._native is None:
+            return 0
+        v = np.zeros(1, np.uint64)
+        self._native.call("swarm_engine_wall_violations", v.ctypes.data)
+        return int(v[0])
 
     def get_friction_coefficients(self, type: int):
         """espresso.py:1038-1052."""
@@ -555,6 +635,17 @@ class SwarmEngine(Engine):
         if self._ext_force is not None:
             ext = np.ascontiguousarray(self._ext_force.reshape(-1, 3))
             self._native.call("swarm_engine_set_external_force", ext.ctypes.data)
+        if self._walls:
+            arr = (_capi.SwarmWall * len(self._walls))()
+            for k, w in enumerate(self._walls):
+                arr[k].kind = w["kind"]
+                for key in ("normal", "corner", "a", "b"):
+                    if key in w:
+                        for a in range(3):
+                            getattr(arr[k], key)[a] = float(w[key][a])
+                arr[k].offset = float(w.get("offset", 0.0))
+            self._native.call("swarm_engine_set_walls", ctypes.cast(arr, ctypes.c_void_p),
+                              len(self._walls))
 
         self._types_host = np.asarray(self._types_list, dtype=np.int32)
         self._types_device = torch.as_tensor(self._types_host, device=self.device)
@@ -669,7 +760,16 @@ class SwarmEngine(Engine):
             self._set_new_directions(nd, np.broadcast_to(mask, (E, N)))
 
     def _set_new_directions(self, new_dir: np.ndarray, mask: np.ndarray):
-        """2-D branch of espresso.py:1236-1249: rotate about +-z if angle > 1e-6."""
+        """espresso.py:1236-1249: 3-D sets the director; 2-D rotates about +-z
+        if the angle exceeds 1e-6."""
+        if self.n_dims == 3:
+            nd = np.ascontiguousarray(new_dir.reshape(-1, 3), dtype=float)
+            m = np.ascontiguousarray(mask.reshape(-1), dtype=np.uint8)
+            if m.any():
+                self._native.bind_stream()
+                self._native.call("swarm_engine_set_directors", nd.ctypes.data, m.ctypes.data)
+                self._host_cache = None
+            return
         old = self._host()["dir"]
         nd = np.ascontiguousarray(new_dir.reshape(-1, 3), dtype=float)
         dots = np.einsum("ij,ij->i", nd, old.reshape(-1, 3))
@@ -708,17 +808,22 @@ class SwarmEngine(Engine):
         N = self.n_particles
         f = np.zeros(N, dtype=np.float32)
         tz = np.zeros(N, dtype=np.float32)
+        txy = np.zeros((2, N), dtype=np.float32)
         new_dir = np.zeros((1, N, 3))
         mask = np.zeros((1, N), dtype=bool)
         for i, action in enumerate(actions):
             f[i] = action.force
             if action.torque is not None:
-                tz[i] = np.asarray(action.torque, dtype=float)[2]
+                tq = np.asarray(action.torque, dtype=float)
+                tz[i] = tq[2]
+                txy[:, i] = tq[:2]
             if action.new_direction is not None:
                 new_dir[0, i] = action.new_direction
                 mask[0, i] = True
         self._native.bind_stream()
         self._native.call("swarm_engine_set_actions", f.ctypes.data, tz.ctypes.data, 0)
+        if self.n_dims == 3:
+            self._native.call("swarm_engine_set_torque_xy", txy.ctypes.data, 0)
         if mask.any():
             self._set_new_directions(new_dir, mask)
 

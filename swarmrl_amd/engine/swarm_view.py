@@ -84,6 +84,9 @@ class SwarmView:
         self.q = wrap_device_pointer(views.q, (3, E, N), torch.uint32, dev)
         self.img = wrap_device_pointer(views.img, (3, E, N), torch.int32, dev)
         self.ang = wrap_device_pointer(views.ang, (E, N), torch.uint32, dev)
+        self.n_dims = int(engine.n_dims)
+        self.dir3 = (wrap_device_pointer(views.dir3, (3, E, N), torch.float32, dev)
+                     if self.n_dims == 3 else None)
         self.types = engine._types_device
         self.radii = engine._radii_device
         self.ids = np.arange(N)
@@ -110,11 +113,15 @@ class SwarmView:
         pos = (self.img.to(torch.float64) + qf / _TWO32)
         pos = pos * torch.as_tensor(box, dtype=torch.float64, device=self.device).view(3, 1, 1)
         out = pos.permute(1, 2, 0).contiguous()
-        out[..., 2] = 0.0
+        if self.n_dims == 2:
+            out[..., 2] = 0.0
         return out
 
     def directors(self) -> torch.Tensor:
-        """Directors, float32 [E, N, 3] (torch sin/cos of the stored angle)."""
+        """Directors, float32 [E, N, 3] (2-D: torch sin/cos of the stored
+        angle; 3-D: the stored unit vectors)."""
+        if self.n_dims == 3:
+            return self.dir3.permute(1, 2, 0).contiguous()
         a = (self.ang.to(torch.int64) & 0xFFFFFFFF).to(torch.float64) * (2.0 * math.pi / _TWO32)
         d = torch.stack([torch.cos(a), torch.sin(a), torch.zeros_like(a)], dim=-1)
         return d.to(torch.float32)

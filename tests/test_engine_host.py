@@ -154,8 +154,6 @@ def test_engine_validation_errors():
     ureg = UnitRegistry()
     with pytest.raises(ValueError):
         SwarmEngine(MDParams(ureg=ureg), n_dims=4)
-    with pytest.raises(NotImplementedError):
-        SwarmEngine(MDParams(ureg=ureg), n_dims=3)
     with pytest.raises(ValueError):
         SwarmEngine(MDParams(ureg=ureg, time_slice=ureg.Quantity(0.10005, "second")), n_dims=2)
     eng = SwarmEngine(MDParams(ureg=ureg), n_dims=2)
@@ -191,3 +189,55 @@ def test_trajectory_chunks_written(fake_backend, tmp_path):
     assert traj["Unwrapped_Positions"].shape == (7, 1, 3)
     assert traj["Times"].shape == (7, 1, 1)
     np.testing.assert_allclose(traj["Times"][:, 0, 0], 0.2 * np.arange(7), atol=1e-12)
+
+
+def test_placement_3d_matches_reference_draw_order(fake_backend, tmp_path):
+    """3-D add_colloids (espresso.py:91-105, 521-529): r = R cbrt(U), two
+    get_random_angles draws per colloid (position, then director)."""
+    ureg = UnitRegistry()
+    params = MDParams(ureg=ureg, box_length=ureg.Quantity(3 * [100.0], "micrometer"))
+    eng = SwarmEngine(params, n_dims=3, seed=11, out_folder=tmp_path)
+    center = np.array([50.0, 50.0, 50.0])
+    eng.add_colloids(7, ureg.Quantity(1.0, "micrometer"),
+                     ureg.Quantity(center, "micrometer"), ureg.Quantity(20.0, "micrometer"))
+    pos, dirs = refsem.placement3(7, 20.0, center, 11)
+    h = eng._host()
+    np.testing.assert_allclose(h["pos"][0], pos, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(h["dir"][0], dirs, rtol=0, atol=1e-12)
+
+
+def test_walls_registration_and_errors(fake_backend, tmp_path):
+    """add_confining_walls / add_walls (espresso.py:667-800): type checks,
+    2 * n_dims constraints for the box faces, one slab per wall segment, and
+    the wall table handed to the engine at setup."""
+    ureg = UnitRegistry()
+    params = MDParams(ureg=ureg, box_length=ureg.Quantity(3 * [10.0], "micrometer"))
+    eng = SwarmEngine(params, n_dims=3, out_folder=tmp_path)
+    eng.add_colloids(5, ureg.Quantity(1.0, "micrometer"),
+                     ureg.Quantity(np.array(3 * [5.0]), "micrometer"),
+                     ureg.Quantity(4.0, "micrometer"), type_colloid=1)
+    with pytest.raises(ValueError):
+        eng.add_confining_walls(1)
+    eng.add_confining_walls(2)
+    assert len(eng.system.constraints) == 2 * eng.n_dims
+    faces = [(w["normal"], w["offset"]) for w in eng._walls]
+    assert ([-1, 0, 0], -10.0) in faces and ([0, 0, 1], 0.0) in faces
+
+    eng2 = SwarmEngine(MDParams(ureg=ureg, box_length=ureg.Quantity(3 * [100.0], "micrometer")),
+                       n_dims=2, out_folder=tmp_path)
+    eng2.add_colloids(5, ureg.Quantity(1.0, "micrometer"),
+                      ureg.Quantity(np.array([50.0, 50.0, 0.0]), "micrometer"),
+                      ureg.Quantity(4.0, "micrometer"), type_colloid=1)
+    start = ureg.Quantity(np.array([[40, 40], [40, 40], [60, 60], [60, 60]]), "micrometer")
+    end = ureg.Quantity(np.array([[40, 60], [60, 40], [40, 60], [60, 40]]), "micrometer")
+    with pytest.raises(ValueError):
+        eng2.add_walls(start, end, 1, ureg.Quantity(2, "micrometer"))
+    eng2.add_walls(start, end, 2, ureg.Quantity(2, "micrometer"))
+    assert len(eng2.system.constraints) == 4
+    w0 = eng2._walls[0]  # start (40, 40) -> end (40, 60), thickness 2
+    np.testing.assert_allclose(w0["a"], [0, 20, 0])
+    np.testing.assert_allclose(w0["b"], [2, 0, 0])
+    np.testing.assert_allclose(w0["corner"], [39, 40, 0])
+    eng2.integrate(1, ForceFunction({"1": dummy_models.ConstForce(1.0)}))
+    names = [c[0] for c in fake_backend.instances[-1].calls]
+    assert "swarm_engine_set_walls" in names
