@@ -89,7 +89,7 @@ def test_bd3_statistics():
     from gpu_harness import Harness, random_state3
 
     rng = np.random.default_rng(33)
-    n = 20000
+    n = 8000
     box = [400.0, 400.0, 400.0]
     gt, gr = 4.6595, 6.2126
     kT = 1.0239
