@@ -329,6 +329,21 @@ int swarm_policy_mlp_sample(const float *obs, int32_t n, int32_t d_in, const flo
                             int64_t *out_idx, float *out_logp, float *out_f, float *out_t,
                             float *out_logits, void *stream);
 
+/* Neighbour reductions for the classical agents (all pointers device):
+ * get_colloids_in_vision of bechinger_models.py:156-171 (range + cone) and
+ * lymburn_model.py:113-125 (range only, half_angle < 0), fused with the
+ * sums those agents take over the neighbours it returns.  pos, dir and vel
+ * [E][N][3] fp64 (pos unwrapped; vel may be NULL), types [N];
+ * candidates: j != agent with bit types[j] set in cand_type_mask.  Per env
+ * e and agent a, out[e][a][12] (fp64) = {count, sum 1/(2 pi |d|), sum d (3),
+ * sum |d|^2, sum dir_j (3), sum v_j (3)} with d = x_j - x_agent.
+ * Asynchronous on `stream`. */
+int swarm_neighbor_reduce(const double *pos, const double *dir, const double *vel,
+                          const int32_t *types, int32_t n_envs, int32_t n,
+                          const int32_t *agent_idx, int32_t n_agents,
+                          uint32_t cand_type_mask, double vision_range,
+                          double half_angle, double *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -246,3 +246,93 @@ def expected_msd_2d(kT, gamma_t, t):
 
 def expected_orientation_corr(kT, gamma_r, t):
     return math.exp(-kT / gamma_r * t)
+
+
+# ------------------------------------------ classical agents (rank 4, 8f)
+def colloids_in_vision(my_pos, my_dir, others_pos, vision_half_angle=np.pi,
+                       vision_range=np.inf, cone=True):
+    """bechinger_models.py:156-171 / lymburn_model.py:113-125: indices of
+    others within range (and, with cone, acos(d/|d| . dir) < half angle)."""
+    out = []
+    for k, p in enumerate(others_pos):
+        d = p - my_pos
+        dn = np.linalg.norm(d)
+        if not dn < vision_range:
+            continue
+        if cone and not np.arccos(np.dot(d / dn, my_dir)) < vision_half_angle:
+            continue
+        out.append(k)
+    return out
+
+
+def lavergne_forces(pos, dirs, types, half_angle, act_force, threshold, acts_on):
+    """bechinger_models.py:29-50: per colloid the swim force (0 if off)."""
+    f = np.zeros(len(pos))
+    for i in range(len(pos)):
+        if types[i] not in acts_on:
+            continue
+        others = [j for j in range(len(pos)) if j != i]
+        vis = colloids_in_vision(pos[i], dirs[i], pos[others], half_angle)
+        perception = sum(1 / (2 * np.pi * np.linalg.norm(pos[i] - pos[others[k]])) for k in vis)
+        if perception >= threshold:
+            f[i] = act_force
+    return f
+
+
+def baeuerle_actions(pos, dirs, types, act_force, act_torque, r_pos, r_orient, half_angle,
+                     dev, acts_on):
+    """bechinger_models.py:81-153: (force, torque_z) per colloid."""
+    f = np.zeros(len(pos))
+    tz = np.zeros(len(pos))
+    for i in range(len(pos)):
+        if types[i] not in acts_on:
+            continue
+        others = [j for j in range(len(pos)) if j != i]
+        vp = colloids_in_vision(pos[i], dirs[i], pos[others], half_angle, r_pos)
+        if len(vp) == 0:
+            continue
+        com = np.mean(np.stack([pos[others[k]] for k in vp]), axis=0)
+        to_com = com - pos[i]
+        to_com_angle = np.arctan2(to_com[1], to_com[0])
+        vo = colloids_in_vision(pos[i], dirs[i], pos[others], half_angle, r_orient)
+        if len(vo) == 0:
+            continue
+        mo = np.mean(np.stack([dirs[others[k]] for k in vo] + [dirs[i]]), axis=0)
+        mo /= np.linalg.norm(mo)
+        choices = [to_com_angle + dev, to_com_angle - dev]
+        devs = [np.arccos(np.dot(np.array([np.cos(a), np.sin(a), 0]), mo)) for a in choices]
+        target = choices[np.argmin(devs)]
+        diff = target - np.arctan2(dirs[i][1], dirs[i][0])
+        if diff >= np.pi:
+            diff -= 2 * np.pi
+        if diff <= -np.pi:
+            diff += 2 * np.pi
+        f[i] = act_force
+        tz[i] = np.sin(diff) * act_torque
+    return f, tz
+
+
+def lymburn_actions(pos, vel, types, K, r_colls, r_pred, home, speed, pred_type):
+    """lymburn_model.py:55-110: (force magnitude, direction) per non-predator."""
+    out = []
+    pred = [j for j in range(len(pos)) if types[j] == pred_type]
+    for i in range(len(pos)):
+        if types[i] == pred_type:
+            continue
+        others = [j for j in range(len(pos)) if j != i and types[j] != pred_type]
+        vis = [others[k] for k in colloids_in_vision(pos[i], None, pos[others], vision_range=r_colls,
+                                                     cone=False)]
+        pv = [pred[k] for k in colloids_in_vision(pos[i], None, pos[pred], vision_range=r_pred,
+                                                  cone=False)] if pred else []
+        fa, fr = np.zeros(3), np.zeros(3)
+        if vis:
+            fa = np.sum(vel[vis] - vel[i], axis=0)
+            fr = np.sum(pos[vis] - pos[i], axis=0) / np.linalg.norm(pos[vis] - pos[i])
+        fh = home - pos[i]
+        fp = np.zeros(3)
+        if pv:
+            fp = np.sum(pos[i] - pos[pv], axis=0) / np.linalg.norm(pos[i] - pos[pv])
+        ff = -vel[i] * (np.abs(vel[i]) - speed) / speed
+        F = K["K_a"] * fa + K["K_r"] * fr + K["K_h"] * fh + K["K_p"] * fp + K["K_f"] * ff
+        out.append((np.linalg.norm(F), F / np.linalg.norm(F)))
+    return out

@@ -160,6 +160,11 @@ _SIGNATURES = {
     "swarm_engine_download_directors": (ctypes.c_int, [_P, _P]),
     "swarm_engine_set_walls": (ctypes.c_int, [_P, _P, ctypes.c_int32]),
     "swarm_engine_wall_violations": (ctypes.c_int, [_P, _P]),
+    "swarm_neighbor_reduce": (
+        ctypes.c_int,
+        [_P, _P, _P, _P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32, ctypes.c_uint32,
+         ctypes.c_double, ctypes.c_double, _P, _P],
+    ),
     "swarm_engine_neighbor_pairs": (
         ctypes.c_int,
         [_P, ctypes.c_int32, ctypes.c_double, _P, ctypes.c_int32, _P],

@@ -410,6 +410,87 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
     if (k < nb) o[k] = (float)acc[k] * 2.3283064365386963e-10f;
 }
 
+// ------------------------------------------- neighbour reductions (fp64)
+// For the classical neighbour-rule agents (bechinger_models.py:156-171
+// get_colloids_in_vision; lymburn_model.py:113-125): per agent i and every
+// candidate j != i whose type bit is set in cand_mask, with d = x_j - x_i,
+// |d| < range and (half_angle >= 0) acos(d/|d| . dir_i) < half_angle:
+//   out[0] = count, out[1] = sum 1/(2 pi |d|), out[2..4] = sum d,
+//   out[5] = sum |d|^2, out[6..8] = sum dir_j, out[9..11] = sum v_j.
+// fp64 like the reference's numpy; candidates staged in LDS tiles.
+constexpr int kNbOut = 12;
+
+__global__ __launch_bounds__(256) void k_neighbor_reduce(
+    const double* __restrict__ pos, const double* __restrict__ dir, const double* __restrict__ vel,
+    const int32_t* __restrict__ types, int n, const int32_t* __restrict__ agents, int n_agents,
+    uint32_t cand_mask, double range, double half_angle, double* __restrict__ out) {
+  __shared__ double tp[256][3], td[256][3], tv[256][3];
+  __shared__ int32_t tid_[256];
+  const int e = blockIdx.y;
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = a < n_agents;
+  const size_t base = (size_t)e * n;
+  int i = -1;
+  double xi[3] = {0.0, 0.0, 0.0}, mi[3] = {0.0, 0.0, 0.0};
+  if (valid) {
+    i = agents[a];
+    for (int k = 0; k < 3; ++k) {
+      xi[k] = pos[(base + i) * 3 + k];
+      mi[k] = dir[(base + i) * 3 + k];
+    }
+  }
+  double acc[kNbOut];
+#pragma unroll
+  for (int k = 0; k < kNbOut; ++k) acc[k] = 0.0;
+  for (int j0 = 0; j0 < n; j0 += 256) {
+    const int j = j0 + (int)threadIdx.x;
+    __syncthreads();
+    if (j < n) {
+      const bool ok = (cand_mask >> (types[j] & 31)) & 1u;
+      tid_[threadIdx.x] = ok ? j : -1;
+      for (int k = 0; k < 3; ++k) {
+        tp[threadIdx.x][k] = pos[(base + j) * 3 + k];
+        td[threadIdx.x][k] = dir[(base + j) * 3 + k];
+        tv[threadIdx.x][k] = vel ? vel[(base + j) * 3 + k] : 0.0;
+      }
+    } else {
+      tid_[threadIdx.x] = -1;
+    }
+    __syncthreads();
+    if (!valid) continue;
+    const int cn = min(256, n - j0);
+    for (int c = 0; c < cn; ++c) {
+      const int jj = tid_[c];
+      if (jj < 0 || jj == i) continue;
+      const double dx = tp[c][0] - xi[0], dy = tp[c][1] - xi[1], dz = tp[c][2] - xi[2];
+      const double d2 = dx * dx + dy * dy + dz * dz;
+      const double dn = sqrt(d2);
+      if (!(dn < range)) continue;
+      if (half_angle >= 0.0) {
+        const double dot = (dx / dn) * mi[0] + (dy / dn) * mi[1] + (dz / dn) * mi[2];
+        if (!(acos(dot) < half_angle)) continue;
+      }
+      acc[0] += 1.0;
+      acc[1] += 1.0 / (2.0 * 3.14159265358979323846 * dn);
+      acc[2] += dx;
+      acc[3] += dy;
+      acc[4] += dz;
+      acc[5] += d2;
+      acc[6] += td[c][0];
+      acc[7] += td[c][1];
+      acc[8] += td[c][2];
+      acc[9] += tv[c][0];
+      acc[10] += tv[c][1];
+      acc[11] += tv[c][2];
+    }
+  }
+  if (valid) {
+    double* o = out + ((size_t)e * n_agents + a) * kNbOut;
+#pragma unroll
+    for (int k = 0; k < kNbOut; ++k) o[k] = acc[k];
+  }
+}
+
 // ------------------------------------------------ pairwise field distances
 // For ParticleSensing / SpeciesSearch (particle_sensing.py:95-121,
 // species_search.py:97-130): d = || fp32(x_j) - fp32(x_i) || / L per agent
@@ -1539,6 +1620,21 @@ int swarm_policy_mlp_sample(const float* obs, int32_t n, int32_t d_in, const flo
     SWARM_MLP_G(1);
 #undef SWARM_MLP_G
 #undef SWARM_MLP
+  HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+
+int swarm_neighbor_reduce(const double* pos, const double* dir, const double* vel,
+                          const int32_t* types, int32_t n_envs, int32_t n,
+                          const int32_t* agent_idx, int32_t n_agents, uint32_t cand_type_mask,
+                          double vision_range, double half_angle, double* out, void* stream) {
+  if (!pos || !dir || !types || !agent_idx || !out) return fail(SWARM_EINVAL, "null argument");
+  if (n_envs < 1 || n < 0 || n_agents < 0) return fail(SWARM_EINVAL, "bad sizes");
+  if (n_agents == 0) return SWARM_OK;
+  const dim3 grid((unsigned)((n_agents + 255) / 256), (unsigned)n_envs);
+  hipLaunchKernelGGL(k_neighbor_reduce, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     pos, dir, vel, types, n, agent_idx, n_agents, cand_type_mask, vision_range,
+                     half_angle, out);
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
 }

@@ -349,3 +349,38 @@ def policy_mlp_sample(obs: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2:
     if want_logits:
         return idx, logp, f, t, logits
     return idx, logp, f, t
+
+
+NB_COUNT, NB_PERCEPTION, NB_SUM_D, NB_SUM_D2, NB_SUM_DIR, NB_SUM_V = 0, 1, 2, 5, 6, 9
+
+
+def neighbor_reduce(pos: torch.Tensor, directors: torch.Tensor, velocities, types: torch.Tensor,
+                    agent_idx: torch.Tensor, cand_types, vision_range: float,
+                    half_angle: float) -> torch.Tensor:
+    """
+    Neighbour sums of the classical agents (swarm_neighbor_reduce, one HIP
+    kernel): pos [E, N, 3] fp64, directors / velocities [E, N, 3] (velocities
+    may be None), types [N] int32, agent_idx [A] int32 (all device).  Returns
+    fp64 [E, A, 12]: count, sum 1/(2 pi |d|), sum d (3), sum |d|^2, sum
+    dir_j (3), sum v_j (3) over the candidates (types in cand_types, not the
+    agent) within vision_range and, for half_angle >= 0, inside the cone.
+    """
+    E, N = int(pos.shape[0]), int(pos.shape[1])
+    dev = pos.device
+    pos = pos.to(torch.float64).contiguous()
+    dirs = directors.to(torch.float64).contiguous()
+    vel = None if velocities is None else velocities.to(torch.float64).contiguous()
+    A = int(agent_idx.numel())
+    out = torch.empty((E, A, 12), dtype=torch.float64, device=dev)
+    mask = 0
+    for t in cand_types:
+        if not 0 <= int(t) < 32:
+            raise ValueError("particle types must be in [0, 32) for the neighbour kernel")
+        mask |= 1 << int(t)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _capi.check(_capi.lib().swarm_neighbor_reduce(
+        pos.data_ptr(), dirs.data_ptr(), None if vel is None else vel.data_ptr(),
+        types.to(torch.int32).contiguous().data_ptr(), E, N,
+        agent_idx.to(torch.int32).contiguous().data_ptr(), A, ctypes.c_uint32(mask),
+        float(vision_range), float(half_angle), out.data_ptr(), ctypes.c_void_p(stream)))
+    return out

@@ -126,6 +126,13 @@ class SwarmView:
         d = torch.stack([torch.cos(a), torch.sin(a), torch.zeros_like(a)], dim=-1)
         return d.to(torch.float32)
 
+    def velocities(self) -> torch.Tensor:
+        """BD velocities of the last sub-step, float32 [E, N, 3]."""
+        v = self.engine._device_views()
+        vel = wrap_device_pointer(v.vel, (3, self.n_envs, self.n_particles), torch.float32,
+                                  self.device)
+        return vel.permute(1, 2, 0).contiguous()
+
     def __len__(self):
         return self.n_particles
 
