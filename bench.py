@@ -133,7 +133,7 @@ def pmc_traffic(kernel_prefix, E, N):
     except (OSError, ValueError):
         return None, None
     for r in rows:
-        if r.get("kernel", "").startswith(kernel_prefix) and r.get("envs") == E and \
+        if kernel_prefix in r.get("kernel", "") and r.get("envs") == E and \
                 r.get("colloids") == N:
             return float(r["bytes_per_launch"]), f"profiles/{r['source']}"
     return None, None
