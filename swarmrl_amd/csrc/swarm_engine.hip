@@ -370,8 +370,12 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
   const int cx = cc0 & (ncx - 1), cy = cc0 >> lx;
   const int32_t* so = start + (size_t)e * (ncell + 1);
   int nh = 0;
-  int skip = sub;  // offset of this lane's next flat index past the current cell
-#pragma unroll 1
+  // the 3x3 candidate cells as one flat index range [0, total): all 18
+  // bounds loaded together, then candidates four at a time per lane (their
+  // record loads in flight together), a lane taking f = sub, sub + G, ...
+  int jbs[9], pre[10];
+  pre[0] = 0;
+#pragma unroll
   for (int r = 0; r < 9; ++r) {
     const int oy = r / 3 - 1, ox = r % 3 - 1;
     int jb = 0, je = 0;
@@ -382,16 +386,32 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
       jb = so[cc];
       je = so[cc + 1];
     }
-    int jj = jb + skip;
-    for (; jj < je; jj += G) {
-      float dx, dy;
-      if (vision_offsets(L, vs.rec[2 * (base + jj)], &dx, &dy)) hits[nh++][threadIdx.x] = jj;
-      if (__any(nh == kVisionHits)) {  // a full list: drain every lane's
-        vision_drain<NB>(L, vp, vs.rec, base, hits, nh, acc);
-        nh = 0;
-      }
+    jbs[r] = jb;
+    pre[r + 1] = pre[r] + (je - jb);
+  }
+  const int total = pre[9];
+  for (int f0 = sub; f0 < total; f0 += 4 * G) {
+    uint4 c0[4];
+    int jj[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int f = f0 + u * G;
+      int j = jbs[0] + f;
+#pragma unroll
+      for (int r = 1; r < 9; ++r) j = f >= pre[r] ? jbs[r] + (f - pre[r]) : j;
+      jj[u] = j;
+      if (f < total) c0[u] = vs.rec[2 * (base + j)];
     }
-    skip = jj - je;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float dx, dy;
+      if (f0 + u * G < total && vision_offsets(L, c0[u], &dx, &dy))
+        hits[nh++][threadIdx.x] = jj[u];
+    }
+    if (__any(nh > kVisionHits - 4)) {  // no room for four more: drain every lane's
+      vision_drain<NB>(L, vp, vs.rec, base, hits, nh, acc);
+      nh = 0;
+    }
   }
   vision_drain<NB>(L, vp, vs.rec, base, hits, nh, acc);
 #pragma unroll
@@ -1014,6 +1034,14 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     if (ov && ov[0] == '0') want = false;
     if (ov && ov[0] == '1') want = true;
     e->sc.one_pass = want ? 1 : 0;
+  }
+  // fewer, fuller waves only pay when the waves compete for the SIMDs; a
+  // latency-bound launch has SIMDs to spare and a shorter build is worth more
+  e->sc.fill_singletons = latency_bound ? 0 : 1;
+  {
+    const char* ov = std::getenv("SWARMRL_AMD_FILL_SINGLETONS");
+    if (ov && ov[0] == '0') e->sc.fill_singletons = 0;
+    if (ov && ov[0] == '1') e->sc.fill_singletons = 1;
   }
   const int S = swarm::slots_per_env(n_particles, e->sc.one_pass != 0);
   e->sc.S = S;

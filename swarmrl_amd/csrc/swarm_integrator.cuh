@@ -120,6 +120,7 @@ struct Scratch {
   int32_t* gclus;     // [3][M] cluster sizes / bases / slots (large-N build only)
   int32_t pair_cap;   // pairs per env
   int32_t one_pass;   // 1: pack clusters so that a wave has <= 64 pairs
+  int32_t fill_singletons;  // 1: singletons take the tail lanes of the other classes
   int32_t S;          // slots per env
   int32_t wmax;       // S / 64
   uint64_t* phase;    // [32] build phase stamps (SWARM_PHASE_TIMING builds only)
@@ -852,7 +853,7 @@ __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc)
       if (tid >= off) f += o;
     }
     freebase[w] = f - fl;
-    const int32_t F = __shfl(f, 63, 64);
+    const int32_t F = sc.fill_singletons ? __shfl(f, 63, 64) : 0;
     if (w == 1) nw = (max(cnt - F, 0) + 63) / 64;
     int32_t v = nw;
 #pragma unroll
