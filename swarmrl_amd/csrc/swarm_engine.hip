@@ -694,6 +694,15 @@ struct swarm_engine {
   // swarm_engine_prebuild_noise: the next window's noise table for this many
   // sub-steps was launched ahead (on a stream of the caller's)
   int prebuilt_noise_steps = 0;
+  // Latency-bound engines run k_cluster_run_wide: one block per CU, and
+  // (noise_blocks > 0) the next window's noise table filled beside the run;
+  // next_table_ready: the last window did that (the table's first step and
+  // length are checked on the device, this flag only skips k_noise).
+  bool wide_run = false;
+  // k_build_env: the whole build in one LDS-resident workgroup per env
+  bool env_build = false;
+  int noise_blocks = 0;
+  bool next_table_ready = false;
   // swarm_engine_profile: HIP events around every k_cluster_run launch
   bool profile = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
@@ -749,11 +758,14 @@ void set_lds_attributes() {
                        reinterpret_cast<const void*>(&swarm::k_cluster_build<false>),
                        reinterpret_cast<const void*>(&swarm::k_cluster_build<true>),
                        reinterpret_cast<const void*>(&swarm::k_build_sort),
+                       reinterpret_cast<const void*>(&swarm::k_build_env),
                        reinterpret_cast<const void*>(&swarm::k_check),
                        reinterpret_cast<const void*>(&k_grid_build),
-                       reinterpret_cast<const void*>(&k_vision_grid)};
+                       reinterpret_cast<const void*>(&k_vision_grid),
+                       reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<false>),
+                       reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<true>)};
   for (const void* f : fns)
-    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
   (void)hipGetLastError();
   done = true;
 }
@@ -787,6 +799,13 @@ int launch_noise(swarm_engine* e, hipStream_t stream, int n) {
 // Cluster build of the next window.
 int launch_build(swarm_engine* e, hipStream_t stream) {
   const int ncb = 1 << (e->lxb + e->lyb);
+  if (e->env_build) {
+    hipLaunchKernelGGL(swarm::k_build_env, dim3(e->n_envs), dim3(1024),
+                       build_lds_bytes(e->n, e->sc.pair_cap), stream, e->d_derived, e->st, e->sc,
+                       e->lxb, e->lyb);
+    HIP_TRY(hipGetLastError());
+    return SWARM_OK;
+  }
   hipLaunchKernelGGL(swarm::k_build_sort, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4, stream,
                      e->st, e->sc, e->lxb, e->lyb);
   HIP_TRY(hipGetLastError());
@@ -811,15 +830,11 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
     const int rc = launch_build(e, e->stream);
     if (rc) return rc;
   }
-  if (e->noise_table && n_steps > noise_ready) {
+  if (e->noise_table && !e->next_table_ready && n_steps > noise_ready) {
     const int rc = launch_noise(e, e->stream, n_steps);
     if (rc) return rc;
   }
   const long waves = (long)e->n_envs * e->sc.wmax;
-  const dim3 run_grid((unsigned)((waves + 3) / 4)), run_block(256);
-#define SWARM_RUN(MULTI, TABLE)                                                              \
-  hipLaunchKernelGGL((swarm::k_cluster_run<MULTI, TABLE>), run_grid, run_block, 0, e->stream, \
-                     e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise)
   const bool multi = e->params.n_species > 1;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   if (e->profile) {
@@ -827,18 +842,38 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
     HIP_TRY(hipEventCreate(&ev1));
     HIP_TRY(hipEventRecord(ev0, e->stream));
   }
-  if (e->noise_table) {
+  if (e->wide_run) {
+    // dynamic LDS beyond half a CU's keeps one block (4 run waves) per CU
+    const dim3 grid((unsigned)(e->noise_blocks + (waves + 3) / 4));
+    const size_t lds = 96 * 1024;
     if (multi)
-      SWARM_RUN(true, true);
+      hipLaunchKernelGGL(swarm::k_cluster_run_wide<true>, grid, dim3(1024), lds, e->stream,
+                         e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise,
+                         e->noise_blocks);
     else
-      SWARM_RUN(false, true);
+      hipLaunchKernelGGL(swarm::k_cluster_run_wide<false>, grid, dim3(1024), lds, e->stream,
+                         e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise,
+                         e->noise_blocks);
+    e->next_table_ready = e->noise_blocks > 0;
   } else {
-    if (multi)
-      SWARM_RUN(true, false);
-    else
-      SWARM_RUN(false, false);
-  }
+    const dim3 run_grid((unsigned)((waves + 3) / 4)), run_block(256);
+#define SWARM_RUN(MULTI, TABLE)                                                              \
+  hipLaunchKernelGGL((swarm::k_cluster_run<MULTI, TABLE>), run_grid, run_block, 0, e->stream, \
+                     e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise)
+    if (e->noise_table) {
+      if (multi)
+        SWARM_RUN(true, true);
+      else
+        SWARM_RUN(false, true);
+    } else {
+      if (multi)
+        SWARM_RUN(true, false);
+      else
+        SWARM_RUN(false, false);
+    }
 #undef SWARM_RUN
+    e->next_table_ready = false;
+  }
   HIP_TRY(hipGetLastError());
   if (e->profile) {
     HIP_TRY(hipEventRecord(ev1, e->stream));
@@ -1019,7 +1054,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->d_box, 3);
   rc = rc ? rc : dev_alloc(e, &e->d_order, M);
   rc = rc ? rc : dev_alloc(e, &e->d_count, 1);
-  rc = rc ? rc : dev_alloc(e, &e->d_step, 1);
+  rc = rc ? rc : dev_alloc(e, &e->d_step, swarm::kCtlWords);
   rc = rc ? rc : dev_alloc(e, &e->d_arrive, 1);
   // integrator scratch
   // One pair pass per wave and sub-step (k_cluster_build): the run kernel
@@ -1084,7 +1119,30 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     if (ov && ov[0] == '1') want = true;
     e->noise_table = want && e->derived.noisy && e->cluster_path;
     if (e->noise_table)
-      rc = rc ? rc : dev_alloc(e, &e->d_noise, (size_t)swarm::kMaxWindow * 3 * M);
+      rc = rc ? rc : dev_alloc(e, &e->d_noise, 2 * swarm::noise_table_words(M));
+    // the one-launch build (one CU per env) for throughput-bound engines
+    // when its sort region fits below the pair list; latency-bound ones keep
+    // the three-launch build, whose pair search spreads over the chip
+    // (one env: 42 us for the three launches, 52 us for k_build_env)
+    {
+      const int wm = S / 64;
+      const size_t below = 16 + 16 + 3 * 68 + (size_t)((wm + 3) & ~3) + 4 * (size_t)n_particles;
+      e->env_build = e->cluster_path && !e->big_build && !latency_bound &&
+                     swarm::build_env_sort_words(n_particles, 1 << (e->lxb + e->lyb)) <= below;
+      const char* ob = std::getenv("SWARMRL_AMD_ENV_BUILD");
+      if (ob && ob[0] == '0') e->env_build = false;
+      if (ob && ob[0] == '1')
+        e->env_build = e->cluster_path && !e->big_build &&
+                       swarm::build_env_sort_words(n_particles, 1 << (e->lxb + e->lyb)) <= below;
+    }
+    // one block per CU for latency-bound runs; beside a run of up to 8192
+    // particles, 64 CUs produce the next window's table in its shadow
+    e->wide_run = e->noise_table;
+    e->noise_blocks = e->wide_run && M <= 8192 ? 64 : 0;
+    const char* ow = std::getenv("SWARMRL_AMD_WIDE_RUN");
+    if (ow && ow[0] == '0') e->wide_run = false, e->noise_blocks = 0;
+    const char* on = std::getenv("SWARMRL_AMD_WIDE_NOISE");
+    if (on && on[0] == '0') e->noise_blocks = 0;
 
   }
   set_lds_attributes();
@@ -1323,6 +1381,7 @@ int swarm_engine_prebuild_noise(swarm_engine_t* e, void* stream, int32_t n_steps
   if (!e) return fail(SWARM_EINVAL, "null engine");
   if (n_steps_hint < 0) return fail(SWARM_EINVAL, "n_steps_hint must be >= 0");
   if (!e->noise_table || n_steps_hint == 0) return SWARM_OK;
+  if (e->next_table_ready) return SWARM_OK;  // filled beside the last run
   const int n = std::min<int>(n_steps_hint, swarm::kMaxWindow);
   const int rc = launch_noise(e, stream ? reinterpret_cast<hipStream_t>(stream) : e->stream, n);
   if (rc) return rc;

@@ -95,6 +95,14 @@ struct DevState {
   unsigned long long* wall_viol;  // [1] wall contacts with dist <= 0
 };
 
+// Device control block (uint64 words): step counter, window counter, and
+// the two noise tables' first step / length (by window parity, see k_noise).
+constexpr int kCtlStep = 0, kCtlWin = 1, kCtlTStep = 2, kCtlTLen = 4, kCtlWords = 8;
+
+__device__ __forceinline__ int window_parity(const uint64_t* ctl) {
+  return (int)(ctl[kCtlWin] & 1ull);  // written by earlier launches only
+}
+
 struct Scratch {
   uint32_t* sqx;      // [M] positions sorted by cell
   uint32_t* sqy;      // [M]
@@ -382,6 +390,44 @@ __device__ __forceinline__ void bd_step(const PConst& c, PState& p, int64_t ax, 
   }
 }
 
+// bd_step without the rotation, for the cluster run (which updates the
+// angle, and the next sub-step's director, while the force sums are in
+// flight): same operation sequence for the translation and velocities.
+__device__ __forceinline__ void bd_translate(const PConst& c, PState& p, int64_t ax, int64_t ay,
+                                             float fs, float tz, float fex, float fey,
+                                             uint32_t k0, uint32_t k1, uint32_t id, uint64_t step,
+                                             bool last, float* vx, float* vy, float* w,
+                                             const float* g, float sn, float cs) {
+  float fx = i64_to_f32(ax) * 5.9604644775390625e-08f;
+  float fy = i64_to_f32(ay) * 5.9604644775390625e-08f;
+  fx = fx + fex;
+  fy = fy + fey;
+  fx = fx + fs * cs;
+  fy = fy + fs * sn;
+  float dx = fx * c.mob_dt;
+  float dy = fy * c.mob_dt;
+  if (c.noisy) {
+    dx = dx + c.sig_t * g[0];
+    dy = dy + c.sig_t * g[1];
+  }
+  advance(p.qx, p.ix, f2i32(dx * c.inv_sx0));
+  advance(p.qy, p.iy, f2i32(dy * c.inv_sx1));
+  if (last) {
+    float v0 = fx * c.inv_gt, v1 = fy * c.inv_gt;
+    float om = tz * c.inv_gr;
+    if (c.noisy) {
+      float gv[3];
+      normals3(k0, k1, id, step, 1u, gv);
+      v0 = v0 + c.sig_v * gv[0];
+      v1 = v1 + c.sig_v * gv[1];
+      om = om + c.sig_w * gv[2];
+    }
+    *vx = v0;
+    *vy = v1;
+    *w = om;
+  }
+}
+
 // One steepest-descent step of one particle (espresso.py:1163-1168).
 __device__ __forceinline__ bool sd_step(const PConst& c, PState& p, int64_t ax, int64_t ay,
                                         float fs, float tz, float fex, float fey, float g,
@@ -510,7 +556,8 @@ __device__ __forceinline__ void advance_counter(uint64_t* step_ctr, uint32_t* ar
   if (threadIdx.x == 0) {
     const uint32_t ticket = atomicAdd(arrive, 1u);
     if (ticket == gridDim.x - 1) {
-      *step_ctr = step0 + (uint64_t)n_steps;
+      step_ctr[kCtlStep] = step0 + (uint64_t)n_steps;
+      step_ctr[kCtlWin] += 1ull;  // window counter (noise table parity)
       *arrive = 0u;
     }
   }
@@ -537,7 +584,13 @@ __global__ __launch_bounds__(1024) void k_global(const Derived* __restrict__ d, 
 // Concurrent union-find on LDS: find with path halving (a lane only ever
 // points a node at one of its ancestors), union hooks the larger root under
 // the smaller with CAS, so no cycle can form.
-__device__ __forceinline__ int uf_find(volatile int32_t* parent, int x) {
+// The forest always lives in LDS: typed LDS pointers give ds_* operations
+// (a generic volatile pointer compiles to flat accesses that wait on both
+// the vector-memory and the LDS counters).
+typedef __attribute__((address_space(3))) int32_t lds_i32;
+
+__device__ __forceinline__ int uf_find(int32_t* parent_g, int x) {
+  volatile lds_i32* parent = (volatile lds_i32*)(parent_g);
   while (true) {
     const int p = parent[x];
     if (p == x) return x;
@@ -756,10 +809,12 @@ __host__ __device__ inline size_t build_lds_words_big(int n) {
 // wave slots that never straddle a wave, per-wave pair lists.  kBig: the
 // cluster sizes, bases, slots and the pair list stay in global memory (N
 // too large for them in LDS); the forest is always in LDS.
-template <bool kBig>
-__global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
+// kCopy: the pair list (found pairs) is copied from sc.gplist into LDS;
+// otherwise (!kBig) it is in LDS already (k_build_env).
+template <bool kBig, bool kCopy>
+__device__ __forceinline__ void cluster_build_env(const DevState& st, const Scratch& sc, int e,
+                                                  unsigned char* smem, int found) {
+  const int T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t base = (size_t)e * N;
   int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);  // 16
   int32_t* misc = wave_sums + 16;                          // 16: 0 flag, 1 waves
@@ -777,7 +832,6 @@ __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc)
                          : reinterpret_cast<uint32_t*>(parent + 4 * N);  // pair_cap
   const int S = sc.S;
   SWARM_STAMP(6);
-  const int found = sc.gnpairs[e];
   const int npairs = min(found, sc.pair_cap);
   for (int k = tid; k < 68; k += T) classcnt[k] = 0;
   for (int k = tid; k < wmax; k += T) wave_np[k] = 0;
@@ -787,7 +841,7 @@ __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc)
     csz[i] = 0;
     cbase[i] = 0;  // pair count of a cluster (one-pass packing), then its base
   }
-  if (!kBig) {  // pair list into LDS, four loads in flight per thread
+  if (!kBig && kCopy) {  // pair list into LDS, four loads in flight per thread
     const uint32_t* gp = sc.gplist + (size_t)e * sc.pair_cap;
     for (int k0 = tid; k0 < npairs; k0 += 4 * T) {
       uint32_t v[4];
@@ -938,6 +992,192 @@ __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc)
   }
 }
 
+template <bool kBig>
+__global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  cluster_build_env<kBig, !kBig>(st, sc, blockIdx.x, smem, sc.gnpairs[blockIdx.x]);
+}
+
+// Words of k_build_env's sort/search region (wave sums, cell ends, sorted
+// x, y, id), which must fit below the pair list of the build's LDS layout.
+__host__ __device__ inline size_t build_env_sort_words(int n, int ncell) {
+  return 16 + (size_t)((ncell + 2) & ~1) + 3 * (size_t)n;
+}
+
+// The whole build of one env in one workgroup, LDS-resident (no global
+// intermediates, one launch): counting sort of the positions into cells of
+// side >= rc_max + skin, the pair search over the sorted LDS copy (every pair
+// within r_i + r_j + skin once, straight into the LDS pair list), then
+// union-find and packing (cluster_build_env).  Same pair set as
+// k_build_sort -> k_build_pairs -> k_cluster_build, in one launch and without
+// their global round trips.
+__global__ __launch_bounds__(1024) void k_build_env(const Derived* __restrict__ d, DevState st,
+                                                    Scratch sc, int lx, int ly) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ float nb2[kMaxSpecies * kMaxSpecies];
+  __shared__ int32_t npair;
+  constexpr int CH = 4;   // particles per thread kept in registers across the scan
+  constexpr int kKeep = 8;
+  const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int ncell = 1 << (lx + ly);
+  const int ncx = 1 << lx, ncy = 1 << ly;
+  int32_t* ws = reinterpret_cast<int32_t*>(smem);
+  int32_t* cnt = ws + 16;  // counts, then exclusive starts, then cell ends
+  // sorted positions as (x, y) pairs (one 8-byte LDS read per candidate),
+  // then the ids; cnt padded to 8-byte alignment
+  uint2* lq = reinterpret_cast<uint2*>(cnt + ((ncell + 2) & ~1));
+  int32_t* lid = reinterpret_cast<int32_t*>(lq + N);
+  const int wmax = sc.wmax;
+  uint32_t* plist = reinterpret_cast<uint32_t*>(smem) +
+                    (16 + 16 + 3 * 68 + ((wmax + 3) & ~3) + 4 * (size_t)N);
+  SWARM_STAMP(0);
+  uint32_t cqx[CH], cqy[CH];
+  int32_t cid[CH];
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int i = tid + k * T;
+    const bool ok = i < N;
+    cqx[k] = ok ? st.q[base + i] : 0u;
+    cqy[k] = ok ? st.q[M + base + i] : 0u;
+    cid[k] = ok ? (i | ((int32_t)st.species[i] << 24)) : -1;
+  }
+  for (int k = tid; k < kMaxSpecies * kMaxSpecies; k += T) nb2[k] = d->nb2[k];
+  for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
+  if (tid == 0) npair = 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < CH; ++k)
+    if (cid[k] >= 0) atomicAdd(&cnt[cell_index(cqx[k], cqy[k], lx, ly)], 1);
+  for (int i = tid + CH * T; i < N; i += T)
+    atomicAdd(&cnt[cell_index(st.q[base + i], st.q[M + base + i], lx, ly)], 1);
+  __syncthreads();
+  block_exclusive_scan(cnt, ncell, ws);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    if (cid[k] < 0) continue;
+    const int pos = atomicAdd(&cnt[cell_index(cqx[k], cqy[k], lx, ly)], 1);
+    lq[pos] = make_uint2(cqx[k], cqy[k]);
+    lid[pos] = cid[k];
+  }
+  for (int i = tid + CH * T; i < N; i += T) {
+    const uint32_t qx = st.q[base + i], qy = st.q[M + base + i];
+    const int pos = atomicAdd(&cnt[cell_index(qx, qy, lx, ly)], 1);
+    lq[pos] = make_uint2(qx, qy);
+    lid[pos] = i | ((int32_t)st.species[i] << 24);
+  }
+  // idle wave slots of the next run (the packing writes the used ones)
+  for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
+  __syncthreads();  // cnt[c] = end of cell c = start of cell c + 1
+  SWARM_STAMP(1);
+  // pair search: a stencil row (cells x-1..x+1) is one contiguous sorted
+  // range, plus a wrap range at the grid edge
+  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const int lane = tid & 63;
+  for (int ps0 = 0; ps0 < N; ps0 += T) {  // uniform trip count: whole waves
+    const int ps = ps0 + tid;
+    const bool valid = ps < N;
+    int pk = 0, i = 0;
+    uint32_t qx = 0, qy = 0;
+    if (valid) {
+      pk = lid[ps];
+      i = pk & 0xffffff;
+      const uint2 q = lq[ps];
+      qx = q.x;
+      qy = q.y;
+    }
+    const int c0 = cell_index(qx, qy, lx, ly);
+    const int cx = c0 & (ncx - 1), cy = c0 >> lx;
+    const int xa = ncx >= 3 ? max(cx - 1, 0) : 0;
+    const int xb = ncx >= 3 ? min(cx + 1, ncx - 1) : ncx - 1;
+    const int xw = ncx >= 3 ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
+    int rb[6], re[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const int oy = loy + (r >> 1), part = r & 1;
+      const bool use = valid && oy <= hiy && (part == 0 || xw >= 0);
+      const int row = ((cy + oy + ncy) & (ncy - 1)) << lx;
+      const int c_lo = row | (part == 0 ? xa : xw), c_hi = row | (part == 0 ? xb : xw);
+      rb[r] = use ? (c_lo > 0 ? cnt[c_lo - 1] : 0) : 0;
+      re[r] = use ? cnt[c_hi] : 0;
+    }
+    const float* nb2_row = nb2 + (pk >> 24) * kMaxSpecies;
+    int found = 0;
+    uint32_t keep[kKeep];
+#pragma unroll
+    for (int v = 0; v < kKeep; ++v) keep[v] = 0u;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      for (int jj0 = rb[r]; jj0 < re[r]; jj0 += 4) {  // four candidates' loads in flight
+        int pk4[4];
+        uint32_t x4[4], y4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int jj = min(jj0 + u, N - 1);
+          pk4[u] = jj0 + u < re[r] ? lid[jj] : -1;
+          const uint2 q = lq[jj];
+          x4[u] = q.x;
+          y4[u] = q.y;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (pk4[u] < 0) continue;
+          const int j = pk4[u] & 0xffffff;
+          const float rx = (float)(int32_t)(x4[u] - qx) * sx0;
+          const float ry = (float)(int32_t)(y4[u] - qy) * sx1;
+          if (i < j && rx * rx + ry * ry < nb2_row[pk4[u] >> 24]) {
+#pragma unroll
+            for (int v = 0; v < kKeep; ++v) keep[v] = found == v ? (uint32_t)j : keep[v];
+            ++found;
+          }
+        }
+      }
+    }
+    // wave prefix sum, one LDS atomic per wave
+    int v = found;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int o = __shfl_up(v, off, 64);
+      if (lane >= off) v += o;
+    }
+    int wbase = 0;
+    if (lane == 63) wbase = atomicAdd(&npair, v);
+    wbase = __shfl(wbase, 63, 64);
+    const int my_off = wbase + v - found;
+    if (!__any(found > kKeep)) {
+#pragma unroll
+      for (int u = 0; u < kKeep; ++u) {
+        const int k = my_off + u;
+        if (u < found && k < sc.pair_cap) plist[k] = (uint32_t)i | (keep[u] << 16);
+      }
+    } else {  // a lane found more than kKeep pairs: rescan and write in order
+      int w = 0;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        for (int jj = rb[r]; jj < re[r]; ++jj) {
+          const int pkj = lid[jj];
+          const int j = pkj & 0xffffff;
+          const uint2 q = lq[jj];
+          const float rx = (float)(int32_t)(q.x - qx) * sx0;
+          const float ry = (float)(int32_t)(q.y - qy) * sx1;
+          if (i < j && rx * rx + ry * ry < nb2_row[pkj >> 24]) {
+            const int k = my_off + w;
+            if (k < sc.pair_cap) plist[k] = (uint32_t)i | ((uint32_t)j << 16);
+            ++w;
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  SWARM_STAMP(2);
+  const int found = npair;
+  __syncthreads();  // the sort region is reused by the union-find arrays
+  cluster_build_env<false, false>(st, sc, e, smem, found);
+}
+
 // -------------------------------------------------------- cluster run
 // Orders one wave's LDS accesses (DS operations of a wave execute in order;
 // this keeps the compiler from moving them across).
@@ -948,43 +1188,65 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // Noise table for latency-bound windows (few waves per SIMD): the normals of
-// every (sub-step, particle) computed by the whole chip ahead of the run,
+// every (sub-step, particle) computed ahead of the run,
 // table[(s * 3 + c) * M + e * N + i].  Indexed by particle, not wave slot,
 // so it does not wait for the cluster build.  Step-major on purpose: the
 // 3 x 4 B x M of one sub-step are read by every wave in the same few
 // microseconds, so 32 particles share a 128-B line and the lines stay hot in
 // L2 (each XCD's L2 fetches its own copy: rocprof FETCH ~ 8 x the table).
 // Particle-major layouts (one line per lane) measured 8-20 % slower.
-__global__ __launch_bounds__(256) void k_noise(const Derived* __restrict__ d, DevState st,
-                                               const uint64_t* __restrict__ step_ctr,
-                                               float* __restrict__ table) {
+// Two tables, by window parity: the wide run kernel fills the next window's
+// on otherwise idle CUs while it reads this one's.  The control block
+// records each table's first step and length; a run whose window does not
+// match its table draws the normals itself.
+__host__ __device__ inline size_t noise_table_words(size_t M) { return (size_t)kMaxWindow * 3 * M; }
+
+__device__ __forceinline__ void noise_entry(const Derived* __restrict__ d, const DevState& st,
+                                            uint64_t step_start, float* __restrict__ table,
+                                            long gi, int s) {
   const long M = st.m;
-  const long gi = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gi >= M) return;
   const int e = (int)(gi / st.n);
   const int i = (int)(gi - (long)e * st.n);
-  const int s = blockIdx.y;
   float g[3];
-  normals3(d->key0, d->key1 ^ (uint32_t)e, (uint32_t)i, *step_ctr + (uint64_t)s, 0u, g);
+  normals3(d->key0, d->key1 ^ (uint32_t)e, (uint32_t)i, step_start + (uint64_t)s, 0u, g);
   float* o = table + (size_t)s * 3 * M + gi;
   o[0] = g[0];
   o[M] = g[1];
   o[2 * M] = g[2];
 }
 
+// This window's table (grid.y = sub-steps) from the current step counter.
+__global__ __launch_bounds__(256) void k_noise(const Derived* __restrict__ d, DevState st,
+                                               uint64_t* __restrict__ ctl,
+                                               float* __restrict__ tables) {
+  const long M = st.m;
+  const int par = window_parity(ctl);
+  const uint64_t step0 = ctl[kCtlStep];
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    ctl[kCtlTStep + par] = step0;
+    ctl[kCtlTLen + par] = gridDim.y;
+  }
+  const long gi = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi >= M) return;
+  noise_entry(d, st, step0, tables + par * noise_table_words(M), gi, blockIdx.y);
+}
+
+#ifndef SWARM_NOISE_AHEAD
+#define SWARM_NOISE_AHEAD 1
+#endif
+constexpr int kAhead = SWARM_NOISE_AHEAD;  // sub-steps of table reads in flight
+
+// One wave of the cluster run: all n_steps sub-steps of the particles in
+// its 64 slots.  kTable: the normals come from this window's noise table
+// (prefetched one sub-step ahead), else they are drawn here.
 // kMulti = false: one species, so the pair constants are wave-uniform scalars.
-// kTable: read the normals from k_noise's table (prefetched one step ahead).
 template <bool kMulti, bool kTable>
-__global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__ d, DevState st,
-                                                     Scratch sc, int n_envs, int n_steps,
-                                                     const uint64_t* __restrict__ step_ctr,
-                                                     const float* __restrict__ table) {
-  __shared__ PairTables pt;
-  __shared__ uint2 lpos[4][64];                  // positions of the block's 4 waves
-  __shared__ unsigned long long lacc[4][2][64];  // int64 force sums (x, y)
-  stage_pair_tables(d, &pt);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+__device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const DevState& st,
+                                         const Scratch& sc, int n_envs, int n_steps,
+                                         uint64_t step0, const float* __restrict__ table,
+                                         int gw, int lane, uint2* lpos_w,
+                                         unsigned long long* lacc_x, unsigned long long* lacc_y,
+                                         const PairTables& pt) {
   const int e = gw / sc.wmax;
   const int w = gw - e * sc.wmax;
   if (e >= n_envs) return;
@@ -1025,9 +1287,8 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
 #pragma unroll
   for (int q = 0; q < kPairsPerWave / 64; ++q)
     pr[q] = q * 64 + lane < np ? pw[q * 64 + lane] : 0xffffffffu;
-  lacc[wv][0][lane] = 0ull;
-  lacc[wv][1][lane] = 0ull;
-  const uint64_t step0 = *step_ctr;
+  lacc_x[lane] = 0ull;
+  lacc_y[lane] = 0ull;
   const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
   const float sx0 = d->sx[0], sx1 = d->sx[1];
   const float eps24 = d->eps24;
@@ -1039,35 +1300,53 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
   float vx = 0.0f, vy = 0.0f, om = 0.0f;
   const long ts = (long)M;
   const float* tcol = table + gi;
-  float gn[3] = {0.0f, 0.0f, 0.0f};
-  if (kTable && active) {
-    gn[0] = tcol[0];
-    gn[1] = tcol[ts];
-    gn[2] = tcol[2 * ts];
+  // normals of the next kAhead sub-steps in flight (register ring)
+  float gn[kAhead][3];
+#pragma unroll
+  for (int k = 0; k < kAhead; ++k) {
+    gn[k][0] = gn[k][1] = gn[k][2] = 0.0f;
+    if (kTable && active && k < n_steps) {
+      const float* nx = tcol + (size_t)k * 3 * ts;
+      gn[k][0] = nx[0];
+      gn[k][1] = nx[ts];
+      gn[k][2] = nx[2 * ts];
+    }
   }
 #ifdef SWARM_PHASE_TIMING
   const bool stamp = e == 0 && w == sc.env_waves[e] - 1 && lane == 0;
   uint64_t t_pairs = 0, t_read = 0, t_bd = 0, t0s = 0, t1s = 0;
 #endif
+  // The rotation and the director do not depend on the forces: each
+  // sub-step turns the angle and computes the next sub-step's director while
+  // its force sums are in flight in LDS (software-pipelined director).
+  float dir[2];
+  sincos_turn(p.an, &dir[0], &dir[1]);
   for (int s = 0; s < n_steps; ++s) {
 #ifdef SWARM_PHASE_TIMING
     if (stamp) t0s = t1s = __builtin_amdgcn_s_memtime();
 #endif
-    // the director depends on the angle only: off the force chain, it can
-    // fill the LDS latencies of the pair section
-    float dir[2];
-    sincos_turn(p.an, &dir[0], &dir[1]);
-    float gt[3] = {gn[0], gn[1], gn[2]};
-    if (kTable && active && s + 1 < n_steps) {
-      const float* nx = tcol + (size_t)(s + 1) * 3 * ts;
-      gn[0] = nx[0];
-      gn[1] = nx[ts];
-      gn[2] = nx[2 * ts];
+    float gt[3] = {gn[0][0], gn[0][1], gn[0][2]};
+#pragma unroll
+    for (int k = 0; k + 1 < kAhead; ++k) {
+      gn[k][0] = gn[k + 1][0];
+      gn[k][1] = gn[k + 1][1];
+      gn[k][2] = gn[k + 1][2];
     }
+#ifdef SWARM_ABLATE_NO_TABLE
+    if (false) {
+#else
+    if (kTable && active && s + kAhead < n_steps) {
+#endif
+      const float* nx = tcol + (size_t)(s + kAhead) * 3 * ts;
+      gn[kAhead - 1][0] = nx[0];
+      gn[kAhead - 1][1] = nx[ts];
+      gn[kAhead - 1][2] = nx[2 * ts];
+    }
+    if (!kTable && active && pc.noisy) normals3(k0, k1, (uint32_t)i, step0 + (uint64_t)s, 0u, gt);
     int64_t ax = 0, ay = 0;
 #ifndef SWARM_ABLATE_NO_PAIRS
     if (npass > 0) {  // wave-uniform
-      lpos[wv][lane] = make_uint2(p.qx, p.qy);
+      lpos_w[lane] = make_uint2(p.qx, p.qy);
       wave_lds_sync();
 #pragma unroll
       for (int q = 0; q < kPairsPerWave / 64; ++q) {
@@ -1075,7 +1354,7 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
           const uint32_t e_ = pr[q];
           const int a = e_ == 0xffffffffu ? lane : (int)(e_ & 63u);
           const int b = e_ == 0xffffffffu ? lane : (int)((e_ >> 6) & 63u);
-          const uint2 pa = lpos[wv][a], pb = lpos[wv][b];
+          const uint2 pa = lpos_w[a], pb = lpos_w[b];
           const float rx = (float)(int32_t)(pb.x - pa.x) * sx0;
           const float ry = (float)(int32_t)(pb.y - pa.y) * sx1;
           int64_t fx, fy;  // on a; b receives exactly the negation
@@ -1085,12 +1364,25 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
           } else {
             pair_fix_sel(cut2_0, sig6_0, eps24, rx, ry, fx, fy);
           }
-          atomicAdd(&lacc[wv][0][a], (unsigned long long)fx);
-          atomicAdd(&lacc[wv][1][a], (unsigned long long)fy);
-          atomicAdd(&lacc[wv][0][b], (unsigned long long)(-fx));
-          atomicAdd(&lacc[wv][1][b], (unsigned long long)(-fy));
+          atomicAdd(&lacc_x[a], (unsigned long long)fx);
+          atomicAdd(&lacc_y[a], (unsigned long long)fy);
+          atomicAdd(&lacc_x[b], (unsigned long long)(-fx));
+          atomicAdd(&lacc_y[b], (unsigned long long)(-fy));
         }
       }
+    }
+#endif
+    // rotation (bd_step's sequence) and the next director, between the
+    // force-sum atomics and their read-back
+    __builtin_amdgcn_sched_barrier(0);
+    float dth = tz * pc.rot_dt;
+    if (pc.noisy) dth = dth + pc.sig_r * gt[2];
+    const uint32_t an_next = p.an + (uint32_t)f2i32(dth * kAngInvScale);
+    float dnext[2];
+    sincos_turn(an_next, &dnext[0], &dnext[1]);
+    __builtin_amdgcn_sched_barrier(0);
+#ifndef SWARM_ABLATE_NO_PAIRS
+    if (npass > 0) {
       wave_lds_sync();
 #ifdef SWARM_PHASE_TIMING
       if (stamp) {
@@ -1098,10 +1390,10 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
         t_pairs += t1s - t0s;
       }
 #endif
-      ax = (int64_t)lacc[wv][0][lane];
-      ay = (int64_t)lacc[wv][1][lane];
-      lacc[wv][0][lane] = 0ull;
-      lacc[wv][1][lane] = 0ull;
+      ax = (int64_t)lacc_x[lane];
+      ay = (int64_t)lacc_y[lane];
+      lacc_x[lane] = 0ull;
+      lacc_y[lane] = 0ull;
 #ifdef SWARM_PHASE_TIMING
       if (stamp) {
         const uint64_t t2 = __builtin_amdgcn_s_memtime();
@@ -1125,12 +1417,15 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
         wall_forces<2>(d, si, (float)p.qx * sx0, (float)p.qy * sx1, 0.0f, ax, ay, az,
                        st.wall_viol);
       }
-      bd_step<kTable>(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i,
-                      step0 + (uint64_t)s, s == n_steps - 1, &vx, &vy, &om, gt, dir);
+      bd_translate(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
+                   s == n_steps - 1, &vx, &vy, &om, gt, dir[0], dir[1]);
       const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
       const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
       dmax2 = fmaxf(dmax2, ddx * ddx + ddy * ddy);
     }
+    p.an = an_next;
+    dir[0] = dnext[0];
+    dir[1] = dnext[1];
 #ifdef SWARM_PHASE_TIMING
     if (stamp) t_bd += __builtin_amdgcn_s_memtime() - t1s;
 #endif
@@ -1158,6 +1453,79 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
   }
 }
 
+// Throughput launch: 256-thread blocks, 4 waves each.
+template <bool kMulti, bool kTable>
+__global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__ d, DevState st,
+                                                     Scratch sc, int n_envs, int n_steps,
+                                                     const uint64_t* __restrict__ ctl,
+                                                     const float* __restrict__ tables) {
+  __shared__ PairTables pt;
+  __shared__ uint2 lpos[4][64];                  // positions of the block's 4 waves
+  __shared__ unsigned long long lacc[4][2][64];  // int64 force sums (x, y)
+  stage_pair_tables(d, &pt);
+  const int par = window_parity(ctl);
+  const uint64_t step0 = ctl[kCtlStep];
+  const bool table_ok = kTable && ctl[kCtlTStep + par] == step0 &&
+                        (uint64_t)n_steps <= ctl[kCtlTLen + par];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  // a table that does not cover this window (the device check; the host
+  // normally guarantees it) -> the normals are drawn in the kernel
+  if (table_ok)
+    run_wave<kMulti, true>(d, st, sc, n_envs, n_steps, step0,
+                           tables + par * noise_table_words(st.m), gw, lane, lpos[wv],
+                           lacc[wv][0], lacc[wv][1], pt);
+  else
+    run_wave<kMulti, false>(d, st, sc, n_envs, n_steps, step0, nullptr, gw, lane, lpos[wv],
+                            lacc[wv][0], lacc[wv][1], pt);
+}
+
+// Latency-bound launch (few envs x particles: the run's waves fill few
+// SIMDs): 1024-thread blocks whose dynamic LDS (set by the host) keeps one
+// block per CU.  Blocks [0, nnb) fill the NEXT window's noise table
+// (kMaxWindow sub-steps from this window's end) on CUs the run leaves idle,
+// so no noise kernel sits between the policy and the run; the other blocks
+// run with waves 0-3 only, one wave per SIMD.
+template <bool kMulti>
+__global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __restrict__ d,
+                                                           DevState st, Scratch sc, int n_envs,
+                                                           int n_steps, uint64_t* __restrict__ ctl,
+                                                           float* __restrict__ tables,
+                                                           int n_noise_blocks) {
+  __shared__ PairTables pt;
+  __shared__ uint2 lpos[4][64];
+  __shared__ unsigned long long lacc[4][2][64];
+  stage_pair_tables(d, &pt);
+  const int par = window_parity(ctl);
+  const uint64_t step0 = ctl[kCtlStep];
+  const size_t M = (size_t)st.m;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (b < n_noise_blocks) {
+    const uint64_t start = step0 + (uint64_t)n_steps;
+    if (b == 0 && tid == 0) {
+      ctl[kCtlTStep + (par ^ 1)] = start;
+      ctl[kCtlTLen + (par ^ 1)] = (uint64_t)kMaxWindow;
+    }
+    float* t = tables + (par ^ 1) * noise_table_words(M);
+    const long total = (long)kMaxWindow * (long)M;
+    for (long k = (long)b * blockDim.x + tid; k < total; k += (long)n_noise_blocks * blockDim.x) {
+      const int s = (int)(k / (long)M);
+      noise_entry(d, st, start, t, k - (long)s * (long)M, s);
+    }
+    return;
+  }
+  const int lane = tid & 63, wv = tid >> 6;
+  if (wv >= 4) return;
+  const int gw = (b - n_noise_blocks) * 4 + wv;
+  const bool table_ok = ctl[kCtlTStep + par] == step0 && (uint64_t)n_steps <= ctl[kCtlTLen + par];
+  if (table_ok)
+    run_wave<kMulti, true>(d, st, sc, n_envs, n_steps, step0, tables + par * noise_table_words(M),
+                           gw, lane, lpos[wv], lacc[wv][0], lacc[wv][1], pt);
+  else
+    run_wave<kMulti, false>(d, st, sc, n_envs, n_steps, step0, nullptr, gw, lane, lpos[wv],
+                            lacc[wv][0], lacc[wv][1], pt);
+}
+
 // ---------------------------------------------------------------- check
 __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, DevState st,
                                                 Scratch sc, int n_steps,
@@ -1173,7 +1541,7 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
   stage_pair_tables(d, &pt);
   const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
-  const uint64_t step0 = *step_ctr;
+  const uint64_t step0 = step_ctr[kCtlStep];
   if (tid < 16) misc[tid] = 0;
   __syncthreads();
   const bool flagged_build = sc.fallback[e] != 0;

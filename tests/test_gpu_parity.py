@@ -208,11 +208,19 @@ def test_field_distance_parity():
         assert np.array_equal(hq_host[:, e], hists[e]["q"])
 
 
-@pytest.mark.parametrize("table", ["0", "1"])
-def test_full_size_4096_slice_bit_exact(table, monkeypatch):
-    """BASELINE workload size: 4096 colloids, 100 sub-steps, vs the oracle,
-    with the in-kernel (table=0) and the precomputed (table=1) normals."""
+@pytest.mark.parametrize("table,wide,env_build", [
+    ("0", "0", "0"),  # normals drawn in the run kernel
+    ("1", "0", "0"),  # k_noise table, 256-thread run blocks
+    ("1", "1", "0"),  # default latency-bound path: wide run, next table beside the run
+    ("1", "1", "1"),  # ... with the one-launch LDS build (k_build_env)
+])
+def test_full_size_4096_slice_bit_exact(table, wide, env_build, monkeypatch):
+    """BASELINE workload size: 4096 colloids, windows of 100, 37 and 100
+    sub-steps (the second and third read noise tables filled beside the
+    previous run), vs the oracle, for every run/noise/build variant."""
     monkeypatch.setenv("SWARMRL_AMD_NOISE_TABLE", table)
+    monkeypatch.setenv("SWARMRL_AMD_WIDE_RUN", wide)
+    monkeypatch.setenv("SWARMRL_AMD_ENV_BUILD", env_build)
     from gpu_harness import Harness, species_list
 
     rng = np.random.default_rng(8)
@@ -226,12 +234,16 @@ def test_full_size_4096_slice_bit_exact(table, monkeypatch):
     h.sd(1000)
     st, _ = oracle.sd_run(h.op, st, np.zeros(n), 1000)
     _eq(h.download()[0], st)
-    f = rng.choice([0.0, 10.0], n).astype(np.float32)
-    t = rng.choice([-10.0, 0.0, 10.0], n).astype(np.float32)
-    h.set_actions(f, t)
-    h.integrate(100)
-    ref, _, _ = oracle.bd_run(h.op, st, np.zeros(n), f, t, 100)
-    _eq(h.download()[0], ref)
+    step = 0
+    for nsteps in (100, 37, 100):
+        f = rng.choice([0.0, 10.0], n).astype(np.float32)
+        t = rng.choice([-10.0, 0.0, 10.0], n).astype(np.float32)
+        h.set_actions(f, t)
+        h.integrate(nsteps)
+        st, vel, _ = oracle.bd_run(h.op, st, np.zeros(n), f, t, nsteps, step0=step)
+        step += nsteps
+        _eq(h.download()[0], st)
+        assert np.array_equal(h.velocities(), vel)
 
 
 def _disc(rng, n, L):
