@@ -55,7 +55,14 @@ constexpr double kTwoPi = 6.283185307179586476925;
 // Verlet-style skin of the cluster decomposition (performance only: results
 // do not depend on it).  2 um keeps inter-cluster approaches below the cutoff
 // over a 100-step slice a ~5-sigma event at the reference's defaults.
-constexpr double kSkin = 2.0;
+// Verlet skin of the cluster decomposition (um): pairs closer than
+// r_i + r_j + skin at the window start share a cluster.  Results do not
+// depend on it; SWARMRL_AMD_SKIN overrides it for tuning.
+double skin_um() {
+  const char* ov = std::getenv("SWARMRL_AMD_SKIN");
+  const double v = ov ? std::atof(ov) : 0.0;
+  return v > 0.0 ? v : 2.0;
+}
 
 thread_local std::string g_err;
 
@@ -100,10 +107,10 @@ void derive(const swarm_params_t& p, Derived& d) {
     }
   for (int s = 0; s < p.n_species; ++s)
     for (int t = 0; t < p.n_species; ++t) {
-      const double r = p.radius[s] + p.radius[t] + kSkin;
+      const double r = p.radius[s] + p.radius[t] + skin_um();
       d.nb2[s * kMaxSpecies + t] = (float)(r * r);
     }
-  d.skin = (float)kSkin;
+  d.skin = (float)skin_um();
   d.rc_max_f = (float)d.rc_max;
   d.eps24 = (float)(24.0 * p.wca_epsilon);
   d.n_species = p.n_species;
@@ -726,7 +733,11 @@ int dev_alloc(swarm_engine* e, T** p, size_t count) {
 
 constexpr size_t kMaxLds = 160 * 1024;
 
-size_t global_lds_bytes(int lx, int ly) { return (16 + (size_t)(1 << (lx + ly)) + 1) * 4; }
+// k_global: wave sums, cell counts and (2-D, N <= 4096) the register-resident
+// path's sorted copy
+size_t global_lds_bytes(int lx, int ly, int n, int dims) {
+  return (16 + (size_t)(1 << (lx + ly)) + 1 + swarm::global_lds_extra_words(n, dims, 1 << (lx + ly))) * 4;
+}
 
 // Pair-list capacity of the cluster build: up to 3 N pairs (mean degree 6),
 // at least N, within the LDS left after the other arrays of k_cluster_build;
@@ -744,8 +755,9 @@ bool build_is_big(int n) { return swarm::build_lds_words(n, n) * 4 > kMaxLds; }
 
 size_t build_lds_bytes(int n, int pair_cap) { return swarm::build_lds_words(n, pair_cap) * 4; }
 
-size_t check_lds_bytes(int lx, int ly) {
-  return (16 + 16 + 1024 + (size_t)(1 << (lx + ly)) + 1) * 4;
+size_t check_lds_bytes(int lx, int ly, int n, int dims) {
+  return (16 + 16 + 1024 + (size_t)(1 << (lx + ly)) + 1 + swarm::global_lds_extra_words(n, dims, 1 << (lx + ly))) *
+         4;
 }
 
 // ROCm admits dynamic LDS up to the device limit at launch; this attribute
@@ -780,7 +792,7 @@ int launch_global(swarm_engine* e, int n_steps, int sd_mode, float g, float md) 
     return SWARM_OK;
   }
   hipLaunchKernelGGL(swarm::k_global, dim3(e->n_envs), dim3(1024),
-                     global_lds_bytes(e->lxg, e->lyg), e->stream, e->d_derived, e->st, e->sc,
+                     global_lds_bytes(e->lxg, e->lyg, e->n, e->params.n_dims), e->stream, e->d_derived, e->st, e->sc,
                      n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg, sd_mode, g, md);
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
@@ -880,7 +892,7 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
     e->prof_events.emplace_back(ev0, ev1);
   }
   hipLaunchKernelGGL(swarm::k_check, dim3(e->n_envs), dim3(1024),
-                     check_lds_bytes(e->lxg, e->lyg), e->stream, e->d_derived, e->st, e->sc,
+                     check_lds_bytes(e->lxg, e->lyg, e->n, e->params.n_dims), e->stream, e->d_derived, e->st, e->sc,
                      n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg);
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
@@ -1021,11 +1033,11 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     cell_grid3(*params, n_particles, e->derived.rc_max, &e->lxg, &e->lyg, &e->lzg);
   else
     cell_grid(*params, n_particles, e->derived.rc_max, &e->lxg, &e->lyg);
-  cell_grid(*params, n_particles, e->derived.rc_max + kSkin, &e->lxb, &e->lyb);
+  cell_grid(*params, n_particles, e->derived.rc_max + skin_um(), &e->lxb, &e->lyb);
   // static LDS of the kernels: pair tables (k_global, k_check, k_cluster_run)
   // and the link table of k_cluster_build
   constexpr size_t kStaticLds = sizeof(swarm::PairTables);
-  if (check_lds_bytes(e->lxg, e->lyg) + kStaticLds > kMaxLds) {
+  if (check_lds_bytes(e->lxg, e->lyg, n_particles, params->n_dims) + kStaticLds > kMaxLds) {
     delete e;
     return fail(SWARM_ECAPACITY, "env cell grid does not fit the LDS of one workgroup");
   }
@@ -1364,6 +1376,9 @@ int swarm_engine_debug_phases(swarm_engine_t* e, uint64_t* out32) {
   if (!e || !out32) return fail(SWARM_EINVAL, "null argument");
   HIP_TRY(hipStreamSynchronize(e->stream));
   HIP_TRY(hipMemcpy(out32, e->sc.phase, 32 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+#ifdef SWARM_PHASE_TIMING
+  HIP_TRY(hipMemcpyFromSymbol(out32 + 24, HIP_SYMBOL(swarm::g_global_phase), 3 * sizeof(uint64_t)));
+#endif
   return SWARM_OK;
 }
 

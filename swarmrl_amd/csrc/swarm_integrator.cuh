@@ -549,6 +549,174 @@ __device__ void block_global_run(const Derived* __restrict__ d, const DevState& 
   }
 }
 
+#ifdef SWARM_PHASE_TIMING
+__device__ unsigned long long g_global_phase[4];  // cycles: sort, forces+step, steps
+#endif
+
+// LDS words the register-resident global path needs after the cell counts
+// (sorted positions as uint2 + ids), 0 when it does not apply (3-D, or more
+// than kGlobalCH particles per thread of a 1024-thread block).
+constexpr int kGlobalCH = 4;
+__host__ __device__ inline size_t global_lds_extra_words(int n, int dims, int ncell) {
+  const size_t extra = 8 * (size_t)n + 2;
+  // k_check's layout (the larger): 16 + 16 + 1024 + ncell + 1 words first,
+  // and 4 KB of static LDS beside it
+  const bool fits = (16 + 16 + 1024 + (size_t)ncell + 1 + extra) * 4 + 4096 <= 160 * 1024;
+  return dims == 2 && n <= kGlobalCH * 1024 && fits ? extra : 0;
+}
+
+// The global path with the particle state and the per-sub-step cell sort in
+// LDS (up to kGlobalCH particles per thread): same pair_force / bd_step /
+// sd_step sequence and int64 force sums as block_global_run, so the same
+// bits, but no global round trip inside a sub-step (it is the exact re-run
+// of an env whose cluster window failed k_check, and the overlap removal).
+// lsq: 8 N + 2 LDS words after cnt[ncell + 1].
+__device__ __forceinline__ void block_global_run_lds(const Derived* __restrict__ d, const DevState& st, int e,
+                                     int n_steps, uint64_t step0, int lx, int ly, bool sd_mode,
+                                     float g, float md, int32_t* cnt, int32_t* wave_sums,
+                                     int32_t* lsq, const PairTables* pt) {
+  const int T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int ncell = 1 << (lx + ly);
+  const int ncx = 1 << lx, ncy = 1 << ly;
+  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+  const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const float eps24 = d->eps24;
+  uint2* sq = reinterpret_cast<uint2*>(lsq + ((reinterpret_cast<uintptr_t>(lsq) >> 2) & 1));
+  int32_t* sid = reinterpret_cast<int32_t*>(sq + N);
+  // particle state by particle index (the forces, velocities and species
+  // are re-read from global memory, L1-resident, where used)
+  uint32_t* lqx = reinterpret_cast<uint32_t*>(sid + N);
+  uint32_t* lqy = lqx + N;
+  int32_t* lix = reinterpret_cast<int32_t*>(lqy + N);
+  int32_t* liy = lix + N;
+  uint32_t* lan = reinterpret_cast<uint32_t*>(liy + N);
+  for (int i = tid; i < N; i += T) {
+    const size_t gi = base + i;
+    lqx[i] = st.q[gi];
+    lqy[i] = st.q[M + gi];
+    lix[i] = st.img[gi];
+    liy[i] = st.img[M + gi];
+    lan[i] = st.ang[gi];
+  }
+  __syncthreads();
+#ifdef SWARM_PHASE_TIMING
+  uint64_t t_sort = 0, t_force = 0, tA = 0;
+#endif
+  for (int s = 0; s < n_steps; ++s) {
+#ifdef SWARM_PHASE_TIMING
+    if (tid == 0) tA = __builtin_amdgcn_s_memtime();
+#endif
+    for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
+    __syncthreads();
+    for (int i = tid; i < N; i += T) atomicAdd(&cnt[cell_index(lqx[i], lqy[i], lx, ly)], 1);
+    __syncthreads();
+    block_exclusive_scan(cnt, ncell, wave_sums);
+    __syncthreads();
+    for (int i = tid; i < N; i += T) {
+      const uint32_t qx = lqx[i], qy = lqy[i];
+      const int pos = atomicAdd(&cnt[cell_index(qx, qy, lx, ly)], 1);
+      sq[pos] = make_uint2(qx, qy);
+      sid[pos] = i | ((int)st.species[i] << 24);
+    }
+    __syncthreads();  // cell c now spans [c ? cnt[c-1] : 0, cnt[c])
+#ifdef SWARM_PHASE_TIMING
+    if (tid == 0) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      t_sort += t - tA;
+      tA = t;
+    }
+#endif
+    int any = 0;
+    // sorted order: the lanes of a wave take neighbouring particles, so their
+    // candidate ranges (a stencil row = one contiguous sorted range, plus a
+    // wrap range at the grid edge) are alike and the loops stay converged
+    for (int ps = tid; ps < N; ps += T) {
+      const int pki = sid[ps];
+      const int i = pki & 0xffffff, sik = pki >> 24;
+      const size_t gi = base + i;
+      PState pp = {lqx[i], lqy[i], lan[i], lix[i], liy[i]};
+      const float fs = st.f_swim[gi], tz = st.torque_z[gi];
+      const float fex = st.f_ext[gi], fey = st.f_ext[M + gi];
+      int64_t ax = 0, ay = 0;
+      const int c0 = cell_index(pp.qx, pp.qy, lx, ly);
+      const int cx = c0 & (ncx - 1), cy = c0 >> lx;
+      const int xa = ncx >= 3 ? max(cx - 1, 0) : 0;
+      const int xb = ncx >= 3 ? min(cx + 1, ncx - 1) : ncx - 1;
+      const int xw = ncx >= 3 ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
+      for (int oy = loy; oy <= hiy; ++oy) {
+        const int row = ((cy + oy + ncy) & (ncy - 1)) << lx;
+#pragma unroll
+        for (int part = 0; part < 2; ++part) {
+          if (part == 1 && xw < 0) continue;
+          const int c_lo = row | (part == 0 ? xa : xw), c_hi = row | (part == 0 ? xb : xw);
+          const int jb = c_lo ? cnt[c_lo - 1] : 0, je = cnt[c_hi];
+          for (int jj = jb; jj < je; ++jj) {
+            const int pj = sid[jj];
+            if ((pj & 0xffffff) == i) continue;
+            const uint2 qj = sq[jj];
+            const float rx = (float)(int32_t)(qj.x - pp.qx) * sx0;
+            const float ry = (float)(int32_t)(qj.y - pp.qy) * sx1;
+            const int pk = sik * kMaxSpecies + (pj >> 24);
+            pair_force(pt->cut2[pk], pt->sig6[pk], eps24, rx, ry, ax, ay);
+          }
+        }
+      }
+      if (d->n_walls) {
+        int64_t az = 0;
+        wall_forces<2>(d, sik, (float)pp.qx * sx0, (float)pp.qy * sx1, 0.0f, ax, ay, az,
+                       st.wall_viol);
+      }
+      const PConst pc = load_pconst(d, sik);
+      if (sd_mode) {
+        any |= sd_step(pc, pp, ax, ay, fs, tz, fex, fey, g, md) ? 1 : 0;
+      } else {
+        float vx, vy, w;
+        const bool last = s == n_steps - 1;
+        bd_step(pc, pp, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
+                last, &vx, &vy, &w);
+        if (last) {
+          st.vel[gi] = vx;
+          st.vel[M + gi] = vy;
+          st.vel[2 * M + gi] = 0.0f;
+          st.omega[gi] = w;
+        }
+      }
+      lqx[i] = pp.qx;  // the sort of the next sub-step reads lqx/lqy after a barrier
+      lqy[i] = pp.qy;
+      lix[i] = pp.ix;
+      liy[i] = pp.iy;
+      lan[i] = pp.an;
+    }
+#ifdef SWARM_PHASE_TIMING
+    __syncthreads();
+    if (tid == 0) t_force += __builtin_amdgcn_s_memtime() - tA;
+#endif
+    if (sd_mode) {
+      if (!__syncthreads_or(any)) break;
+    } else {
+      __syncthreads();
+    }
+  }
+#ifdef SWARM_PHASE_TIMING
+  if (tid == 0) {
+    g_global_phase[0] = t_sort;
+    g_global_phase[1] = t_force;
+    g_global_phase[2] = (uint64_t)n_steps;
+  }
+#endif
+  __syncthreads();
+  for (int i = tid; i < N; i += T) {
+    const size_t gi = base + i;
+    st.q[gi] = lqx[i];
+    st.q[M + gi] = lqy[i];
+    st.img[gi] = lix[i];
+    st.img[M + gi] = liy[i];
+    st.ang[gi] = lan[i];
+  }
+}
+
 // Advance the device noise counter once every workgroup of the launch has
 // read it (the last arriving workgroup does it).
 __device__ __forceinline__ void advance_counter(uint64_t* step_ctr, uint32_t* arrive,
@@ -575,8 +743,12 @@ __global__ __launch_bounds__(1024) void k_global(const Derived* __restrict__ d, 
   int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
   int32_t* cnt = wave_sums + 16;
   const uint64_t step0 = sd_mode ? 0ull : *step_ctr;
-  block_global_run(d, st, sc, blockIdx.x, n_steps, step0, lx, ly, sd_mode != 0, g, md, cnt,
-                   wave_sums, &pt);
+  if (global_lds_extra_words(st.n, st.dims, 1 << (lx + ly)) && blockDim.x == 1024)
+    block_global_run_lds(d, st, blockIdx.x, n_steps, step0, lx, ly, sd_mode != 0, g, md, cnt,
+                         wave_sums, cnt + (1 << (lx + ly)) + 1, &pt);
+  else
+    block_global_run(d, st, sc, blockIdx.x, n_steps, step0, lx, ly, sd_mode != 0, g, md, cnt,
+                     wave_sums, &pt);
   if (!sd_mode) advance_counter(step_ctr, arrive, step0, n_steps);
 }
 
@@ -1606,8 +1778,12 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
     }
     if (tid == 0) sc.fallback[e] = 2;  // diagnostics: env re-run on the global path
     __syncthreads();
-    block_global_run(d, st, sc, e, n_steps, step0, lx, ly, false, 0.0f, 0.0f, cnt, wave_sums,
-                     &pt);
+    if (global_lds_extra_words(N, st.dims, 1 << (lx + ly)))
+      block_global_run_lds(d, st, e, n_steps, step0, lx, ly, false, 0.0f, 0.0f, cnt, wave_sums,
+                           cnt + (1 << (lx + ly)) + 1, &pt);
+    else
+      block_global_run(d, st, sc, e, n_steps, step0, lx, ly, false, 0.0f, 0.0f, cnt, wave_sums,
+                       &pt);
   }
   advance_counter(step_ctr, arrive, step0, n_steps);
 }

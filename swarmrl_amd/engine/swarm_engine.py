@@ -17,6 +17,7 @@ integrator raise NotImplementedError.
 from __future__ import annotations
 
 import ctypes
+import os
 import logging
 import pathlib
 import typing
@@ -255,7 +256,7 @@ class SwarmEngine(Engine):
         self._type_index_cache = {}
         # device path: prepare each window's build on a side stream while
         # the force model computes the slice's actions (see _prebuild)
-        self.overlap_build = True
+        self.overlap_build = os.environ.get("SWARMRL_AMD_OVERLAP_BUILD", "1") != "0"
         self._side_stream = None
         self._prebuild_pending = None
         self.traj_holder = None

@@ -1,5 +1,5 @@
 """Per-window fallback statistics of the bench workload (GPU):
-python tools/fallback_stats.py [envs] [slices]"""
+python tools/fallback_stats.py [envs] [slices] [seed]"""
 import argparse
 import sys
 
@@ -11,9 +11,10 @@ import bench  # noqa: E402
 
 E = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 S = int(sys.argv[2]) if len(sys.argv) > 2 else 60
+SEED = int(sys.argv[3]) if len(sys.argv) > 3 else 42
 ns = argparse.Namespace(colloids=4096, envs_per_gpu=E)
 torch.cuda.set_device(0)
-eng, ff, agent = bench.build_workload(ns, 42, torch.device("cuda", 0))
+eng, ff, agent = bench.build_workload(ns, SEED, torch.device("cuda", 0))
 flagged = rerun = 0
 waves = []
 for s in range(S):
