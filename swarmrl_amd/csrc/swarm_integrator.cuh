@@ -32,6 +32,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/swarmrl_amd.h"
 #include "swarm_device.cuh"
 
@@ -228,7 +230,7 @@ __device__ __forceinline__ void pair_fix_sel(float cut2, float sig6, float eps24
   fr = fr * ir2;
   const float vx = (in ? -fr * rx : 0.0f) * 16777216.0f;
   const float vy = (in ? -fr * ry : 0.0f) * 16777216.0f;
-  if (__all(fabsf(vx) < 2147483520.0f && fabsf(vy) < 2147483520.0f)) {
+  if (__builtin_expect(__all(fabsf(vx) < 2147483520.0f && fabsf(vy) < 2147483520.0f), 1)) {
     fx = (int64_t)__float2int_rn(vx);
     fy = (int64_t)__float2int_rn(vy);
   } else {
@@ -1403,16 +1405,11 @@ __global__ __launch_bounds__(256) void k_noise(const Derived* __restrict__ d, De
   noise_entry(d, st, step0, tables + par * noise_table_words(M), gi, blockIdx.y);
 }
 
-#ifndef SWARM_NOISE_AHEAD
-#define SWARM_NOISE_AHEAD 1
-#endif
-constexpr int kAhead = SWARM_NOISE_AHEAD;  // sub-steps of table reads in flight
-
 // One wave of the cluster run: all n_steps sub-steps of the particles in
 // its 64 slots.  kTable: the normals come from this window's noise table
 // (prefetched one sub-step ahead), else they are drawn here.
 // kMulti = false: one species, so the pair constants are wave-uniform scalars.
-template <bool kMulti, bool kTable>
+template <bool kMulti, bool kTable, bool kWalls>
 __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const DevState& st,
                                          const Scratch& sc, int n_envs, int n_steps,
                                          uint64_t step0, const float* __restrict__ table,
@@ -1466,23 +1463,16 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
   const float eps24 = d->eps24;
   const PConst pc = load_pconst(d, si);
   const float cut2_0 = d->cut2[0], sig6_0 = d->sig6[0];
-  const int nwalls = d->n_walls;
   const uint32_t q0x = p.qx, q0y = p.qy;
   float dmax2 = 0.0f;
   float vx = 0.0f, vy = 0.0f, om = 0.0f;
   const long ts = (long)M;
   const float* tcol = table + gi;
-  // normals of the next kAhead sub-steps in flight (register ring)
-  float gn[kAhead][3];
-#pragma unroll
-  for (int k = 0; k < kAhead; ++k) {
-    gn[k][0] = gn[k][1] = gn[k][2] = 0.0f;
-    if (kTable && active && k < n_steps) {
-      const float* nx = tcol + (size_t)k * 3 * ts;
-      gn[k][0] = nx[0];
-      gn[k][1] = nx[ts];
-      gn[k][2] = nx[2 * ts];
-    }
+  float gn[3] = {0.0f, 0.0f, 0.0f};
+  if (kTable) {  // idle lanes read particle 0's (never stored)
+    gn[0] = tcol[0];
+    gn[1] = tcol[ts];
+    gn[2] = tcol[2 * ts];
   }
 #ifdef SWARM_PHASE_TIMING
   const bool stamp = e == 0 && w == sc.env_waves[e] - 1 && lane == 0;
@@ -1491,38 +1481,32 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
   // The rotation and the director do not depend on the forces: each
   // sub-step turns the angle and computes the next sub-step's director while
   // its force sums are in flight in LDS (software-pipelined director).
+  // A lone wave pays for every taken branch, so the sub-step is branch-lean:
+  // the pass count (0, 1 or up to 4) and the last sub-step (velocities) are
+  // compile-time variants, and idle lanes compute along (never stored).
   float dir[2];
   sincos_turn(p.an, &dir[0], &dir[1]);
-  for (int s = 0; s < n_steps; ++s) {
+  auto substep = [&](const int s, auto last_t, auto pass_t) __attribute__((always_inline)) {
+    constexpr bool kLast = decltype(last_t)::value;
+    constexpr int kPass = decltype(pass_t)::value;  // 0, 1, or 4: up to npass
 #ifdef SWARM_PHASE_TIMING
     if (stamp) t0s = t1s = __builtin_amdgcn_s_memtime();
 #endif
-    float gt[3] = {gn[0][0], gn[0][1], gn[0][2]};
-#pragma unroll
-    for (int k = 0; k + 1 < kAhead; ++k) {
-      gn[k][0] = gn[k + 1][0];
-      gn[k][1] = gn[k + 1][1];
-      gn[k][2] = gn[k + 1][2];
+    float gt[3] = {gn[0], gn[1], gn[2]};
+    if (kTable && !kLast) {  // the next sub-step's normals, one sub-step ahead
+      const float* nx = tcol + (size_t)(s + 1) * 3 * ts;
+      gn[0] = nx[0];
+      gn[1] = nx[ts];
+      gn[2] = nx[2 * ts];
     }
-#ifdef SWARM_ABLATE_NO_TABLE
-    if (false) {
-#else
-    if (kTable && active && s + kAhead < n_steps) {
-#endif
-      const float* nx = tcol + (size_t)(s + kAhead) * 3 * ts;
-      gn[kAhead - 1][0] = nx[0];
-      gn[kAhead - 1][1] = nx[ts];
-      gn[kAhead - 1][2] = nx[2 * ts];
-    }
-    if (!kTable && active && pc.noisy) normals3(k0, k1, (uint32_t)i, step0 + (uint64_t)s, 0u, gt);
+    if (!kTable && pc.noisy) normals3(k0, k1, (uint32_t)i, step0 + (uint64_t)s, 0u, gt);
     int64_t ax = 0, ay = 0;
-#ifndef SWARM_ABLATE_NO_PAIRS
-    if (npass > 0) {  // wave-uniform
+    if (kPass > 0) {
       lpos_w[lane] = make_uint2(p.qx, p.qy);
       wave_lds_sync();
 #pragma unroll
-      for (int q = 0; q < kPairsPerWave / 64; ++q) {
-        if (q < npass) {  // wave-uniform; an empty slot names the lane twice
+      for (int q = 0; q < (kPass == 1 ? 1 : kPairsPerWave / 64); ++q) {
+        if (kPass == 1 || q < npass) {  // wave-uniform; an empty slot names the lane twice
           const uint32_t e_ = pr[q];
           const int a = e_ == 0xffffffffu ? lane : (int)(e_ & 63u);
           const int b = e_ == 0xffffffffu ? lane : (int)((e_ >> 6) & 63u);
@@ -1543,7 +1527,6 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
         }
       }
     }
-#endif
     // rotation (bd_step's sequence) and the next director, between the
     // force-sum atomics and their read-back
     __builtin_amdgcn_sched_barrier(0);
@@ -1551,10 +1534,10 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     if (pc.noisy) dth = dth + pc.sig_r * gt[2];
     const uint32_t an_next = p.an + (uint32_t)f2i32(dth * kAngInvScale);
     float dnext[2];
-    sincos_turn(an_next, &dnext[0], &dnext[1]);
+    if (!kLast) sincos_turn(an_next, &dnext[0], &dnext[1]);
     __builtin_amdgcn_sched_barrier(0);
-#ifndef SWARM_ABLATE_NO_PAIRS
-    if (npass > 0) {
+    __asm__ volatile("" ::: "memory");  // keep the read-back after the director
+    if (kPass > 0) {
       wave_lds_sync();
 #ifdef SWARM_PHASE_TIMING
       if (stamp) {
@@ -1574,34 +1557,35 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
       }
 #endif
     }
-#endif
-#ifdef SWARM_ABLATE_NO_BD
-    if (active) {
-      p.qx += (uint32_t)ax;
-      p.qy += (uint32_t)ay + gt[0];
+    if (kWalls && active) {  // contacts of real particles only
+      int64_t az = 0;
+      wall_forces<2>(d, si, (float)p.qx * sx0, (float)p.qy * sx1, 0.0f, ax, ay, az,
+                     st.wall_viol);
     }
-    if (false) {
-#else
-    if (active) {
-#endif
-      if (nwalls) {  // wave-uniform
-        int64_t az = 0;
-        wall_forces<2>(d, si, (float)p.qx * sx0, (float)p.qy * sx1, 0.0f, ax, ay, az,
-                       st.wall_viol);
-      }
-      bd_translate(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
-                   s == n_steps - 1, &vx, &vy, &om, gt, dir[0], dir[1]);
-      const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
-      const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
-      dmax2 = fmaxf(dmax2, ddx * ddx + ddy * ddy);
-    }
+    bd_translate(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s, kLast,
+                 &vx, &vy, &om, gt, dir[0], dir[1]);
+    const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
+    const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
+    dmax2 = fmaxf(dmax2, ddx * ddx + ddy * ddy);
     p.an = an_next;
-    dir[0] = dnext[0];
-    dir[1] = dnext[1];
+    if (!kLast) {
+      dir[0] = dnext[0];
+      dir[1] = dnext[1];
+    }
 #ifdef SWARM_PHASE_TIMING
     if (stamp) t_bd += __builtin_amdgcn_s_memtime() - t1s;
 #endif
-  }
+  };
+  auto run_steps = [&](auto pass_t) __attribute__((always_inline)) {
+    for (int s = 0; s < n_steps - 1; ++s) substep(s, std::false_type{}, pass_t);
+    substep(n_steps - 1, std::true_type{}, pass_t);  // velocities of the last sub-step
+  };
+  if (npass == 0)
+    run_steps(std::integral_constant<int, 0>{});
+  else if (npass == 1)
+    run_steps(std::integral_constant<int, 1>{});
+  else
+    run_steps(std::integral_constant<int, 4>{});
 #ifdef SWARM_PHASE_TIMING
   if (stamp) {
     sc.phase[16] = t_pairs;
@@ -1625,6 +1609,34 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
   }
 }
 
+// Uniform dispatch to the compile-time variants: normals from a table
+// (table != null) or drawn here; walls or none.
+template <bool kMulti>
+__device__ __forceinline__ void run_wave_dispatch(const Derived* __restrict__ d, const DevState& st,
+                                                  const Scratch& sc, int n_envs, int n_steps,
+                                                  uint64_t step0, const float* __restrict__ table,
+                                                  int gw, int lane, uint2* lpos_w,
+                                                  unsigned long long* lacc_x,
+                                                  unsigned long long* lacc_y,
+                                                  const PairTables& pt) {
+  const bool walls = d->n_walls != 0;
+  if (table) {
+    if (walls)
+      run_wave<kMulti, true, true>(d, st, sc, n_envs, n_steps, step0, table, gw, lane, lpos_w,
+                                   lacc_x, lacc_y, pt);
+    else
+      run_wave<kMulti, true, false>(d, st, sc, n_envs, n_steps, step0, table, gw, lane, lpos_w,
+                                    lacc_x, lacc_y, pt);
+  } else {
+    if (walls)
+      run_wave<kMulti, false, true>(d, st, sc, n_envs, n_steps, step0, nullptr, gw, lane, lpos_w,
+                                    lacc_x, lacc_y, pt);
+    else
+      run_wave<kMulti, false, false>(d, st, sc, n_envs, n_steps, step0, nullptr, gw, lane,
+                                     lpos_w, lacc_x, lacc_y, pt);
+  }
+}
+
 // Throughput launch: 256-thread blocks, 4 waves each.
 template <bool kMulti, bool kTable>
 __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__ d, DevState st,
@@ -1643,13 +1655,9 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
   const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   // a table that does not cover this window (the device check; the host
   // normally guarantees it) -> the normals are drawn in the kernel
-  if (table_ok)
-    run_wave<kMulti, true>(d, st, sc, n_envs, n_steps, step0,
-                           tables + par * noise_table_words(st.m), gw, lane, lpos[wv],
-                           lacc[wv][0], lacc[wv][1], pt);
-  else
-    run_wave<kMulti, false>(d, st, sc, n_envs, n_steps, step0, nullptr, gw, lane, lpos[wv],
-                            lacc[wv][0], lacc[wv][1], pt);
+  run_wave_dispatch<kMulti>(d, st, sc, n_envs, n_steps, step0,
+                            table_ok ? tables + par * noise_table_words(st.m) : nullptr, gw, lane,
+                            lpos[wv], lacc[wv][0], lacc[wv][1], pt);
 }
 
 // Latency-bound launch (few envs x particles: the run's waves fill few
@@ -1690,12 +1698,9 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
   if (wv >= 4) return;
   const int gw = (b - n_noise_blocks) * 4 + wv;
   const bool table_ok = ctl[kCtlTStep + par] == step0 && (uint64_t)n_steps <= ctl[kCtlTLen + par];
-  if (table_ok)
-    run_wave<kMulti, true>(d, st, sc, n_envs, n_steps, step0, tables + par * noise_table_words(M),
-                           gw, lane, lpos[wv], lacc[wv][0], lacc[wv][1], pt);
-  else
-    run_wave<kMulti, false>(d, st, sc, n_envs, n_steps, step0, nullptr, gw, lane, lpos[wv],
-                            lacc[wv][0], lacc[wv][1], pt);
+  run_wave_dispatch<kMulti>(d, st, sc, n_envs, n_steps, step0,
+                            table_ok ? tables + par * noise_table_words(M) : nullptr, gw, lane,
+                            lpos[wv], lacc[wv][0], lacc[wv][1], pt);
 }
 
 // ---------------------------------------------------------------- check
