@@ -21,12 +21,19 @@ tag = sys.argv[1]
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 
 
-def envs_of_grid(g):
-    """Envs of a k_cluster_run launch of g threads: ceil(E * wmax / 4) blocks
-    of 256, wmax = slots_per_env / 64 (dense: 2 N, one-pass: 4 N slots)."""
+def envs_of_grid(g, wide):
+    """Envs of a run launch of g threads: ceil(E * wmax / 4) blocks of 256
+    (k_cluster_run), or of 1024 after 64 noise blocks when E * N <= 8192
+    (k_cluster_run_wide); wmax = slots_per_env / 64 (dense: 2 N, one-pass:
+    4 N slots)."""
     for E in range(1, 4097):
         for slots in (2 * N + 64 * 66, 4 * N + 64 * 66):
-            if (E * (slots // 64) + 3) // 4 * 256 == g:
+            blocks = (E * (slots // 64) + 3) // 4
+            if wide:
+                nnb = 64 if E * N <= 8192 else 0
+                if (nnb + blocks) * 1024 == g:
+                    return E
+            elif blocks * 256 == g:
                 return E
     return None
 
@@ -60,7 +67,7 @@ traffic = []
 for (k, g), cs in acc.items():
     if "k_cluster_run" not in k or not cs.get("FETCH_SIZE") or not cs.get("WRITE_SIZE"):
         continue
-    E = envs_of_grid(g)
+    E = envs_of_grid(g, "wide" in k)
     fetch_kb = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"])
     write_kb = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"])
     traffic.append({
