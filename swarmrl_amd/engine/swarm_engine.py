@@ -840,19 +840,31 @@ class SwarmEngine(Engine):
         if self._side_stream is None:
             self._side_stream = torch.cuda.Stream(device=main.device)
         side = self._side_stream
+        if self.n_envs * self.n_particles > 32768:
+            # Throughput-bound engines: the observables outlast the build, and
+            # in a captured graph the branch captured first after a fork keeps
+            # the launch queue (the other pays the cross-queue latencies,
+            # DESIGN.md section 6): fork here, launch the build in _run.
+            fork = torch.cuda.Event()
+            fork.record(main)
+            self._prebuild_pending = (side, fork, int(n_steps))
+            return
         side.wait_stream(main)
         self._native.call("swarm_engine_prebuild", ctypes.c_void_p(side.cuda_stream), int(n_steps))
-        self._prebuild_pending = (side,)
+        self._prebuild_pending = (side, None, 0)
 
     def _run(self, n_steps: int):
         if self._prebuild_pending is not None:
             # The noise table (latency-bound engines) runs on the main stream
             # after the policy kernels, ahead of the join: the build usually
             # finishes later, and a third stream would add a graph join.
+            side, fork, hint = self._prebuild_pending
+            if fork is not None:  # deferred build (throughput-bound engines)
+                side.wait_event(fork)
+                self._native.call("swarm_engine_prebuild", ctypes.c_void_p(side.cuda_stream), hint)
             self._native.bind_stream()
             self._native.call("swarm_engine_prebuild_noise", None, int(n_steps))
-            for st in self._prebuild_pending:
-                torch.cuda.current_stream().wait_stream(st)
+            torch.cuda.current_stream().wait_stream(side)
             self._prebuild_pending = None
         self._native.bind_stream()
         self._native.call("swarm_engine_integrate", int(n_steps))
