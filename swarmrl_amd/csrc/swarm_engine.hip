@@ -756,8 +756,11 @@ bool build_is_big(int n) { return swarm::build_lds_words(n, n) * 4 > kMaxLds; }
 size_t build_lds_bytes(int n, int pair_cap) { return swarm::build_lds_words(n, pair_cap) * 4; }
 
 size_t check_lds_bytes(int lx, int ly, int n, int dims) {
-  return (16 + 16 + 1024 + (size_t)(1 << (lx + ly)) + 1 + swarm::global_lds_extra_words(n, dims, 1 << (lx + ly))) *
-         4;
+  // the global-path re-run region (cell counts + LDS path) or the big
+  // clusters' positions and force sums, after 16 + 16 + 1024 words
+  const size_t rerun = (size_t)(1 << (lx + ly)) + 1 + swarm::global_lds_extra_words(n, dims, 1 << (lx + ly));
+  const size_t big = 6 * (size_t)swarm::kBigMax + 2;  // uint2 positions, 2 x u64 sums
+  return (16 + 16 + 1024 + std::max(rerun, big)) * 4;
 }
 
 // ROCm admits dynamic LDS up to the device limit at launch; this attribute
@@ -1119,6 +1122,10 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->sc.disp, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.env_waves, (size_t)n_envs);
   rc = rc ? rc : dev_alloc(e, &e->sc.fallback, (size_t)n_envs);
+  rc = rc ? rc : dev_alloc(e, &e->sc.big_list, (size_t)n_envs * swarm::kBigMax);
+  rc = rc ? rc : dev_alloc(e, &e->sc.big_pairs, (size_t)n_envs * swarm::kBigPairs);
+  rc = rc ? rc : dev_alloc(e, &e->sc.big_n, (size_t)n_envs);
+  rc = rc ? rc : dev_alloc(e, &e->sc.big_np, (size_t)n_envs);
   rc = rc ? rc : dev_alloc(e, &e->vs.rec, 2 * M);
   rc = rc ? rc : dev_alloc(e, &e->vs.agent_row, (size_t)n_particles);
   // noise table for latency-bound windows: few envs fill few SIMDs, so the

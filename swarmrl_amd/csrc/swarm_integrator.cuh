@@ -42,6 +42,11 @@ namespace swarm {
 constexpr int kMaxSpecies = SWARM_MAX_SPECIES;
 constexpr int kMaxWindow = 128;   // sub-steps per cluster window
 constexpr int kPairsPerWave = 256;  // neighbour pairs of one 64-lane wave (4 passes)
+// Clusters wider than a wave ("big" clusters) run in k_check's workgroup, one
+// member per thread: up to kBigMax members and kBigPairs pairs per env.
+constexpr int kBigMax = 1024;
+constexpr int kBigPairs = 4096;
+constexpr int kBigMark = -0x40000000;  // cbase of a big cluster's root
 
 // Wave slots per env: every cluster packs into one wave, worst case 2 N
 // slots plus per-size-class rounding.  One-pass packing (latency-bound
@@ -121,6 +126,10 @@ struct Scratch {
   float* disp;        // [M] max displacement over the window
   int32_t* env_waves; // [E]
   int32_t* fallback;  // [E]
+  int32_t* big_list;  // [E][kBigMax] particles of the env's big clusters (member order)
+  uint32_t* big_pairs;  // [E][kBigPairs] member a | member b << 10 | species pair << 20
+  int32_t* big_n;     // [E] members
+  int32_t* big_np;    // [E] pairs
   // cluster build (k_build_sort -> k_build_pairs -> k_cluster_build)
   uint32_t* bsq;      // [2][M] cell-sorted positions (x, y)
   int32_t* bsid;      // [M] particle | species << 24 of a sorted entry
@@ -1009,7 +1018,7 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   const int npairs = min(found, sc.pair_cap);
   for (int k = tid; k < 68; k += T) classcnt[k] = 0;
   for (int k = tid; k < wmax; k += T) wave_np[k] = 0;
-  if (tid < 16) misc[tid] = found > sc.pair_cap ? 1 : 0;  // overflow -> global path
+  if (tid < 16) misc[tid] = tid == 0 && found > sc.pair_cap ? 1 : 0;  // overflow -> global path
   for (int i = tid; i < N; i += T) {
     parent[i] = i;
     csz[i] = 0;
@@ -1046,8 +1055,9 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   for (int i = tid; i < N; i += T) {
     if (parent[i] != i) continue;
     const int s = csz[i];
-    if (s > 64) {
-      misc[0] = 1;  // cluster wider than a wave -> global path for this env
+    if (s > 64) {  // wider than a wave: a big cluster, run by k_check's workgroup
+      atomicAdd(&misc[4], s);
+      cbase[i] = kBigMark;
     } else {
       const int w = sc.one_pass ? max(s, min(min(cbase[i], 64), 2 * s)) : s;
       csz[i] = w;
@@ -1056,10 +1066,14 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   }
   __syncthreads();
   SWARM_STAMP(8);
+  if (tid == 0 && misc[4] > min(kBigMax, (int)blockDim.x)) misc[0] = 1;  // -> global path
+  __syncthreads();
   if (misc[0]) {
     if (tid == 0) {
       sc.fallback[e] = 1;
       sc.env_waves[e] = 0;
+      sc.big_n[e] = 0;
+      sc.big_np[e] = 0;
     }
     return;
   }
@@ -1102,6 +1116,7 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
     if (parent[i] != i) continue;
     const int s = csz[i];
     const int r = cbase[i];
+    if (r == kBigMark) continue;
     if (s == 1 && r < nfree) {
       // the class v whose free-lane range holds r (largest v >= 2 with
       // freebase[v] <= r; its range is non-empty), then wave j and lane
@@ -1134,10 +1149,17 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   __syncthreads();
   for (int i = tid; i < N; i += T) {
     const int root = parent[i];
-    const int slot = cbase[root] + lslot[i];
+    int slot;
+    if (cbase[root] == kBigMark) {  // big-cluster member m: slot -1 - m
+      const int m = atomicAdd(&misc[5], 1);
+      sc.big_list[(size_t)e * kBigMax + m] = i;
+      slot = -1 - m;
+    } else {
+      slot = cbase[root] + lslot[i];
+      sc.perm[(size_t)e * S + slot] = i;
+    }
     lslot[i] = slot;
     sc.slot_of[base + i] = slot;
-    sc.perm[(size_t)e * S + slot] = i;
     sc.root[base + i] = root;
   }
   __syncthreads();
@@ -1147,12 +1169,21 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
     const uint32_t pr = plist[k];
     const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
     const int si = lslot[i], sj = lslot[j];
+    const uint32_t spp = (uint32_t)(st.species[i] * kMaxSpecies + st.species[j]);
+    if (si < 0) {  // a big cluster's pair (both members of it)
+      const int idx = atomicAdd(&misc[6], 1);
+      if (idx < kBigPairs)
+        sc.big_pairs[(size_t)e * kBigPairs + idx] =
+            (uint32_t)(-1 - si) | ((uint32_t)(-1 - sj) << 10) | (spp << 20);
+      else
+        misc[2] = 1;  // -> global path
+      continue;
+    }
     const int wv = si >> 6;
     const int idx = atomicAdd(&wave_np[wv], 1);
     if (idx < kPairsPerWave)
       sc.pairs[((size_t)e * wmax + wv) * kPairsPerWave + idx] =
-          (uint32_t)(si & 63) | ((uint32_t)(sj & 63) << 6) |
-          ((uint32_t)(st.species[i] * kMaxSpecies + st.species[j]) << 12);
+          (uint32_t)(si & 63) | ((uint32_t)(sj & 63) << 6) | (spp << 12);
     else
       misc[2] = 1;  // a wave with more than kPairsPerWave pairs
   }
@@ -1163,6 +1194,8 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   if (tid == 0) {
     sc.env_waves[e] = misc[2] ? 0 : misc[1];
     sc.fallback[e] = misc[2] ? 1 : 0;
+    sc.big_n[e] = misc[5];
+    sc.big_np[e] = min(misc[6], kBigPairs);
   }
 }
 
@@ -1703,6 +1736,107 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
                             lpos[wv], lacc[wv][0], lacc[wv][1], pt);
 }
 
+// The env's big clusters (wider than a wave) for the window, by k_check's
+// workgroup: one member per thread, the clusters' pairs spread over the
+// threads; per sub-step the members publish their positions, every pair's
+// force goes to both members' int64 sums (LDS atomics, as in the run
+// kernel), then the members take the Brownian step (bd_step, normals drawn
+// here: the same numbers as the noise table).  Writes the window-start
+// snapshot, the final state, velocities and displacements like the run
+// kernel, so k_check's exact test covers the members too.
+// lds: 6 * kBigMax + 2 words (uint2 positions, two u64 force sums).
+__device__ void run_big_clusters(const Derived* __restrict__ d, const DevState& st,
+                                 const Scratch& sc, int e, int n_steps, uint64_t step0,
+                                 int32_t* lds, const PairTables* pt) {
+  const int T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int nm = sc.big_n[e], np = sc.big_np[e];
+  uint2* lp = reinterpret_cast<uint2*>(lds + ((reinterpret_cast<uintptr_t>(lds) >> 2) & 1));
+  unsigned long long* ax = reinterpret_cast<unsigned long long*>(lp + kBigMax);
+  unsigned long long* ay = ax + kBigMax;
+  const bool mem = tid < nm;
+  const int i = mem ? sc.big_list[(size_t)e * kBigMax + tid] : 0;
+  const size_t gi = base + i;
+  PState p = {st.q[gi], st.q[M + gi], st.ang[gi], st.img[gi], st.img[M + gi]};
+  const int si = st.species[i];
+  const float fs = st.f_swim[gi], tz = st.torque_z[gi];
+  const float fex = st.f_ext[gi], fey = st.f_ext[M + gi];
+  const PConst pc = load_pconst(d, si);
+  if (mem) {
+    sc.bq[gi] = p.qx;
+    sc.bq[M + gi] = p.qy;
+    sc.bimg[gi] = p.ix;
+    sc.bimg[M + gi] = p.iy;
+    sc.bang[gi] = p.an;
+  }
+  const uint32_t q0x = p.qx, q0y = p.qy;
+  constexpr int kPer = kBigPairs / 1024;  // pairs per thread (blockDim 1024)
+  uint32_t pr[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int k = tid + u * T;
+    pr[u] = k < np ? sc.big_pairs[(size_t)e * kBigPairs + k] : 0u;  // 0: member 0 twice
+  }
+  const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const float eps24 = d->eps24;
+  float dmax2 = 0.0f, vx = 0.0f, vy = 0.0f, om = 0.0f;
+  if (mem) {
+    ax[tid] = 0ull;
+    ay[tid] = 0ull;
+  }
+  for (int s = 0; s < n_steps; ++s) {
+    if (mem) lp[tid] = make_uint2(p.qx, p.qy);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int a = (int)(pr[u] & 1023u), b = (int)((pr[u] >> 10) & 1023u);
+      const int sp = (int)(pr[u] >> 20);
+      const uint2 pa = lp[a], pb = lp[b];
+      const float rx = (float)(int32_t)(pb.x - pa.x) * sx0;
+      const float ry = (float)(int32_t)(pb.y - pa.y) * sx1;
+      int64_t fx, fy;  // zero for an empty slot (a == b: r = 0)
+      pair_fix_sel(pt->cut2[sp], pt->sig6[sp], eps24, rx, ry, fx, fy);
+      if (a != b) {
+        atomicAdd(&ax[a], (unsigned long long)fx);
+        atomicAdd(&ay[a], (unsigned long long)fy);
+        atomicAdd(&ax[b], (unsigned long long)(-fx));
+        atomicAdd(&ay[b], (unsigned long long)(-fy));
+      }
+    }
+    __syncthreads();
+    if (mem) {
+      int64_t fxs = (int64_t)ax[tid], fys = (int64_t)ay[tid];
+      ax[tid] = 0ull;
+      ay[tid] = 0ull;
+      if (d->n_walls) {
+        int64_t az = 0;
+        wall_forces<2>(d, si, (float)p.qx * sx0, (float)p.qy * sx1, 0.0f, fxs, fys, az,
+                       st.wall_viol);
+      }
+      bd_step(pc, p, fxs, fys, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
+              s == n_steps - 1, &vx, &vy, &om);
+      const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
+      const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
+      dmax2 = fmaxf(dmax2, ddx * ddx + ddy * ddy);
+    }
+  }
+  if (mem) {
+    st.q[gi] = p.qx;
+    st.q[M + gi] = p.qy;
+    st.img[gi] = p.ix;
+    st.img[M + gi] = p.iy;
+    st.ang[gi] = p.an;
+    st.vel[gi] = vx;
+    st.vel[M + gi] = vy;
+    st.vel[2 * M + gi] = 0.0f;
+    st.omega[gi] = om;
+    sc.disp[gi] = sqrt_rn(dmax2);
+  }
+  __threadfence();
+  __syncthreads();
+}
+
 // ---------------------------------------------------------------- check
 __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, DevState st,
                                                 Scratch sc, int n_steps,
@@ -1722,6 +1856,8 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
   if (tid < 16) misc[tid] = 0;
   __syncthreads();
   const bool flagged_build = sc.fallback[e] != 0;
+  if (!flagged_build && sc.big_n[e] > 0)
+    run_big_clusters(d, st, sc, e, n_steps, step0, cnt, &pt);
   if (!flagged_build) {
     const float half = 0.5f * d->skin;
     for (int i = tid; i < N; i += T) {
@@ -1752,8 +1888,16 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
         const float lim = rc + sc.disp[base + m] + sc.disp[base + j] + 1e-3f;
         if (rx * rx + ry * ry < lim * lim) {
           bool listed = false;
-          if (sc.root[base + j] == sc.root[base + m]) {  // same wave: search its pairs
-            const int sm = sc.slot_of[base + m], sj = sc.slot_of[base + j];
+          const int sm = sc.slot_of[base + m], sj = sc.slot_of[base + j];
+          if (sc.root[base + j] == sc.root[base + m] && sm < 0) {  // same big cluster
+            const uint32_t bm = (uint32_t)(-1 - sm), bj = (uint32_t)(-1 - sj);
+            const uint32_t* bp = sc.big_pairs + (size_t)e * kBigPairs;
+            const int np = sc.big_np[e];
+            for (int k = 0; k < np; ++k) {
+              const uint32_t a = bp[k] & 1023u, b = (bp[k] >> 10) & 1023u;
+              listed |= (a == bm && b == bj) || (a == bj && b == bm);
+            }
+          } else if (sc.root[base + j] == sc.root[base + m]) {  // same wave: its pairs
             const int wv = sm >> 6;
             const uint32_t lm = (uint32_t)(sm & 63), lj = (uint32_t)(sj & 63);
             const uint32_t* pw = sc.pairs + ((size_t)e * sc.wmax + wv) * kPairsPerWave;

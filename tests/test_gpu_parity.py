@@ -403,3 +403,46 @@ def test_vision_cone_parity_lane_variants_and_dense(E, n, box_len):
         ref = oracle.vision_cone(h.op, states[e], agents, radii, types, 12.0, 1.0, 3, [0, 1])
         assert np.array_equal(out[e], ref)
         assert np.count_nonzero(ref) > len(agents)
+
+
+def test_big_clusters_run_in_check_bit_exact():
+    """Clusters wider than a wave (three 10 x 10 patches at 2.5 um spacing:
+    100 colloids each, within r_c + skin of their neighbours) run in k_check's
+    workgroup instead of sending the env to the global path: bit-exact
+    against the oracle over several windows, without a global-path re-run."""
+    from gpu_harness import Harness, species_list
+
+    rng = np.random.default_rng(21)
+    box = [200.0, 200.0, 200.0]
+    pts = []
+    for cx, cy in ((40.0, 40.0), (120.0, 60.0), (80.0, 150.0)):
+        for gx in range(10):
+            for gy in range(10):
+                pts.append((cx + 2.5 * gx, cy + 2.5 * gy))
+    n_free = 700
+    while len(pts) < 300 + n_free:
+        p = rng.random(2) * 200.0
+        if min((p[0] - q[0]) ** 2 + (p[1] - q[1]) ** 2 for q in pts) > 16.0:
+            pts.append((p[0], p[1]))
+    n = len(pts)
+    pos = np.zeros((n, 3))
+    pos[:, :2] = pts
+    a = 2 * np.pi * rng.random(n)
+    dirs = np.stack([np.cos(a), np.sin(a), np.zeros(n)], 1)
+    st = oracle.state_from_positions(pos, dirs, box)
+    h = Harness(box, 1e-3, 1.0239, 1.0239, 5, species_list()[:1], np.zeros(n, int))
+    h.upload([st])
+    step = 0
+    for nsteps in (100, 60):
+        f = rng.choice([0.0, 5.0], n).astype(np.float32)
+        t = rng.choice([-5.0, 0.0, 5.0], n).astype(np.float32)
+        h.set_actions(f, t)
+        h.integrate(nsteps)
+        st, vel, _ = oracle.bd_run(h.op, st, np.zeros(n), f, t, nsteps, step0=step)
+        step += nsteps
+        _eq(h.download()[0], st)
+        assert np.array_equal(h.velocities(), vel)
+        fb = np.zeros(1, np.int32)
+        w = np.zeros(1, np.int32)
+        h.native.call("swarm_engine_window_stats", fb.ctypes.data, w.ctypes.data)
+        assert fb[0] == 0 and w[0] > 0, (fb, w)
