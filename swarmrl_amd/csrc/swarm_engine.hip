@@ -1477,8 +1477,15 @@ int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const 
   }
   const long total = (long)e->n * e->n_envs;  // one group per sorted particle
   const int nb = vp->n_cones * vp->n_types;
-  // lanes per agent: enough threads to give every SIMD a few waves
-  const int G = total >= (1L << 18) ? 1 : total >= (1L << 16) ? 4 : 16;
+  // lanes per agent: enough threads to give every SIMD a few waves, few
+  // enough that the lanes of a wave stay busy (measured, tools/vision_time.py:
+  // 64 x 4096 agents 107 -> 93 us with G = 4 instead of 1; G = 1 never wins
+  // on this device, it stays for SWARMRL_AMD_VISION_G=1)
+  int G = total >= (1L << 15) ? 4 : 16;
+  if (const char* og = std::getenv("SWARMRL_AMD_VISION_G")) {
+    const int v = std::atoi(og);
+    if (v == 1 || v == 4 || v == 16) G = v;
+  }
   const dim3 grid((unsigned)((total * G + 255) / 256)), block(256);
 #define SWARM_VISION(NBV, GV)                                                              \
   hipLaunchKernelGGL((k_vision<NBV, GV>), grid, block, 0, e->stream, e->st, e->d_derived, *vp, \

@@ -191,6 +191,27 @@ def test_device_path_equals_list_path(tmp_path, monkeypatch):
         assert np.array_equal(states[0][k], states[1][k])
 
 
+@pytest.mark.parametrize("n_envs,n", [(1, 300), (12, 3000)])
+def test_prebuild_overlap_equals_serial(tmp_path, n_envs, n):
+    """The build forked on a side stream (latency-bound engines: launched
+    first; throughput-bound ones, E x N > 32768: forked first, launched after
+    the observables) gives the same bits as the serial single-stream slice."""
+    from swarmrl_amd.agents import dummy_models
+    from swarmrl_amd.force_functions import ForceFunction
+    from swarmrl_amd.units import UnitRegistry
+
+    states = []
+    for overlap in (True, False):
+        ureg = UnitRegistry()
+        eng = _engine(ureg, tmp_path / str(overlap), n, 2.0 * np.sqrt(n / 0.1), n_envs=n_envs)
+        eng.overlap_build = overlap
+        ff = ForceFunction({"1": dummy_models.ConstForceAndTorque(4.0, np.array([0, 0, 3.0]))})
+        eng.integrate(3, ff)
+        states.append(eng.get_raw_state())
+    for k in ("q", "img", "ang"):
+        assert np.array_equal(states[0][k], states[1][k])
+
+
 def test_observables_device_vs_list(tmp_path):
     from swarmrl_amd.components import Colloid
     from swarmrl_amd.observables import SubdividedVisionCones

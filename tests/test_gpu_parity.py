@@ -376,14 +376,18 @@ def test_c5_16384_large_build_bit_exact():
     assert fb[0] == 0 and w[0] > 0, (fb, w)
 
 
-@pytest.mark.parametrize("E,n,box_len", [(1, 2000, 90.0), (20, 4096, 200.0), (64, 4096, 160.0)])
-def test_vision_cone_parity_lane_variants_and_dense(E, n, box_len):
+@pytest.mark.parametrize("E,n,box_len,lanes", [(1, 2000, 90.0, None), (20, 4096, 200.0, None),
+                                               (64, 4096, 160.0, None), (64, 4096, 160.0, "1")])
+def test_vision_cone_parity_lane_variants_and_dense(E, n, box_len, lanes, monkeypatch):
     """The vision kernel's 16/4/1 lanes-per-agent variants (by envs x
-    particles) and dense neighbourhoods (more in-range hits per lane than its
-    LDS hit list holds, so the list is drained mid-scan), bit-exact against
-    the oracle on the first and last env."""
+    particles; 1 lane only by override) and dense neighbourhoods (more
+    in-range hits per lane than its LDS hit list holds, so the list is
+    drained mid-scan), bit-exact against the oracle on the first and last env."""
     from gpu_harness import Harness, random_state, species_list
     from swarmrl_amd.engine import ops
+
+    if lanes:
+        monkeypatch.setenv("SWARMRL_AMD_VISION_G", lanes)
 
     rng = np.random.default_rng(60 + E)
     box = [box_len, box_len, box_len]
