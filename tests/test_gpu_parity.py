@@ -450,3 +450,35 @@ def test_big_clusters_run_in_check_bit_exact():
         w = np.zeros(1, np.int32)
         h.native.call("swarm_engine_window_stats", fb.ctypes.data, w.ctypes.data)
         assert fb[0] == 0 and w[0] > 0, (fb, w)
+
+
+def test_c4_size_8_envs_x_1024_bit_exact():
+    """SURVEY config C4 per GPU (8 envs x 1024 colloids, area fraction 0.1):
+    the latency-bound wide run with its next-window noise, three windows,
+    bit-exact on every env."""
+    from gpu_harness import Harness, species_list
+
+    rng = np.random.default_rng(31)
+    n, E = 1024, 8
+    L = 2 * np.sqrt(n / 0.1)
+    box = [L, L, L]
+    states = []
+    for _ in range(E):
+        pos, dirs = _disc(rng, n, L)
+        states.append(oracle.state_from_positions(pos, dirs, box))
+    h = Harness(box, 1e-3, 1.0239, 1.0239, 42, species_list()[:1], np.zeros(n, int), n_envs=E)
+    h.upload(states)
+    h.sd(500)
+    states = [oracle.sd_run(h.op, s, np.zeros(n), 500)[0] for s in states]
+    step = 0
+    for nsteps in (100, 100, 50):
+        f = rng.choice([0.0, 10.0], E * n).astype(np.float32)
+        t = rng.choice([-10.0, 0.0, 10.0], E * n).astype(np.float32)
+        h.set_actions(f, t)
+        h.integrate(nsteps)
+        got = h.download()
+        for e in range(E):
+            states[e], _, _ = oracle.bd_run(h.op, states[e], np.zeros(n), f[e * n:(e + 1) * n],
+                                            t[e * n:(e + 1) * n], nsteps, step0=step, env=e)
+            _eq(got[e], states[e])
+        step += nsteps
