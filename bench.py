@@ -119,7 +119,10 @@ def time_run_kernel(eng, reps):
         stop.record()
         stop.synchronize()
         return start.elapsed_time(stop) / reps, "k_global (100 sub-steps)"
-    return ms.value / cnt.value, "k_cluster_run (100 fused BD+WCA sub-steps)"
+    wide = eng.n_envs * eng.n_particles <= 32768  # latency-bound engines
+    name = ("k_cluster_run_wide (100 fused BD+WCA sub-steps; the next window's noise table "
+            "filled beside them)" if wide else "k_cluster_run (100 fused BD+WCA sub-steps)")
+    return ms.value / cnt.value, name
 
 
 def pmc_traffic(kernel_prefix, E, N):
