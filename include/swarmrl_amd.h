@@ -329,6 +329,36 @@ int swarm_policy_mlp_sample(const float *obs, int32_t n, int32_t d_in, const flo
                             int64_t *out_idx, float *out_logp, float *out_f, float *out_t,
                             float *out_logits, void *stream);
 
+/* The gradient of one PPO epoch -- ProximalPolicyLoss._calculate_loss
+ * differentiated by jax.value_and_grad (swarmrl/losses/
+ * proximal_policy_loss.py:62-138, :160-168) with its GAE value function
+ * (value_functions/generalized_advantage_estimate.py:42-72) -- for the
+ * actor-critic MLP Dense(hidden) -> ReLU -> {Dense(k) logits, Dense(1)
+ * value}.  Samples are T time slices x S agent columns, sample t * S + col:
+ * x [T*S][d_in], actions [T*S] (int64), old_logp [T*S], rewards [T][S].
+ * Parameters in torch Linear layouts: w1 [hidden][d_in], b1 [hidden],
+ * wa [k][hidden], ba [k], wc [1][hidden], bc [1].  Writes grad =
+ * d loss / d params, concatenated as w1 | b1 | wa | ba | wc | bc
+ * (hidden*d_in + hidden + k*hidden + k + hidden + 1 floats).  The loss:
+ *   sum -min(r A, clip(r, 1 - clip_eps, 1 + clip_eps) A)
+ *   - entropy_coef * sum -(p + 1e-8) log(p + 1e-8)
+ *   + 0.5 * sum huber(V, R)
+ * with r = exp(log(p_a + 1e-8) - old_logp), A the GAE advantages
+ * normalised by mean and population std (+ fp32 eps) and held constant,
+ * R = A_raw + V differentiated through V as in the reference.
+ * d_in <= 32, hidden <= 256, k <= 16, T*S < 2^31.  workspace: device
+ * memory of at least swarm_ppo_workspace_bytes(T, S, d_in, hidden, k)
+ * bytes.  Deterministic (fixed reduction order).  Asynchronous on
+ * `stream`. */
+int64_t swarm_ppo_workspace_bytes(int32_t T, int32_t S, int32_t d_in, int32_t hidden,
+                                  int32_t k);
+int swarm_ppo_epoch_grad(const float *x, int32_t T, int32_t S, int32_t d_in,
+                         const int64_t *actions, const float *old_logp, const float *rewards,
+                         const float *w1, const float *b1, int32_t hidden, const float *wa,
+                         const float *ba, int32_t k, const float *wc, const float *bc,
+                         float gamma, float lambda, float clip_eps, float entropy_coef,
+                         void *workspace, int64_t workspace_bytes, float *grad, void *stream);
+
 /* Neighbour reductions for the classical agents (all pointers device):
  * get_colloids_in_vision of bechinger_models.py:156-171 (range + cone) and
  * lymburn_model.py:113-125 (range only, half_angle < 0), fused with the

@@ -139,6 +139,16 @@ _SIGNATURES = {
         [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_int32, _P, _P, ctypes.c_int32,
          ctypes.c_uint64, _P, ctypes.c_int32, ctypes.c_float, _P, _P, _P, _P, _P, _P, _P, _P],
     ),
+    "swarm_ppo_workspace_bytes": (
+        ctypes.c_int64,
+        [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32],
+    ),
+    "swarm_ppo_epoch_grad": (
+        ctypes.c_int,
+        [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, _P, _P, _P, ctypes.c_int32,
+         _P, _P, ctypes.c_int32, _P, _P, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+         ctypes.c_float, _P, ctypes.c_int64, _P, _P],
+    ),
     "swarm_engine_step_count": (ctypes.c_int64, [_P]),
     "swarm_engine_window_stats": (ctypes.c_int, [_P, _P, _P]),
     "swarm_engine_device_views": (ctypes.c_int, [_P, ctypes.POINTER(SwarmDeviceViews)]),

@@ -33,6 +33,7 @@
 #include "swarm_integrator.cuh"
 #include "swarm_integrator3.cuh"
 #include "swarm_policy.cuh"
+#include "swarm_ppo.cuh"
 
 namespace {
 
@@ -1736,6 +1737,99 @@ int swarm_policy_mlp_sample(const float* obs, int32_t n, int32_t d_in, const flo
     SWARM_MLP_G(1);
 #undef SWARM_MLP_G
 #undef SWARM_MLP
+  HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+
+namespace {
+struct PpoWorkspace {
+  size_t values, adv, dv, stats, partial, total;
+};
+PpoWorkspace ppo_workspace(long n, int d, int hidden, int k) {
+  PpoWorkspace w;
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  w.values = 0;
+  w.adv = up(w.values + (size_t)n * 4);
+  w.dv = up(w.adv + (size_t)n * 4);
+  w.stats = up(w.dv + (size_t)n * 4);
+  w.partial = up(w.stats + 2 * sizeof(double));
+  w.total = up(w.partial + (size_t)swarm::kPpoBlocks * swarm::ppo_grad_size(d, hidden, k) * 4);
+  return w;
+}
+}  // namespace
+
+int64_t swarm_ppo_workspace_bytes(int32_t T, int32_t S, int32_t d_in, int32_t hidden,
+                                  int32_t k) {
+  if (T < 1 || S < 1 || d_in < 1 || hidden < 1 || k < 1) return -1;
+  return (int64_t)ppo_workspace((long)T * S, d_in, hidden, k).total;
+}
+
+int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
+                         const int64_t* actions, const float* old_logp, const float* rewards,
+                         const float* w1, const float* b1, int32_t hidden, const float* wa,
+                         const float* ba, int32_t k, const float* wc, const float* bc,
+                         float gamma, float lambda, float clip_eps, float entropy_coef,
+                         void* workspace, int64_t workspace_bytes, float* grad, void* stream) {
+  if (!x || !actions || !old_logp || !rewards || !w1 || !b1 || !wa || !ba || !wc || !bc ||
+      !workspace || !grad)
+    return fail(SWARM_EINVAL, "null argument");
+  if (T < 1 || S < 1) return fail(SWARM_EINVAL, "T, S >= 1");
+  if ((long)T * S > INT32_MAX) return fail(SWARM_ECAPACITY, "T x S < 2^31 samples");
+  if (d_in < 1 || d_in > swarm::kPpoMaxIn) return fail(SWARM_ECAPACITY, "1 <= d_in <= 32");
+  if (hidden < 1 || hidden > swarm::kPpoMaxHidden)
+    return fail(SWARM_ECAPACITY, "1 <= hidden <= 256");
+  if (k < 1 || k > swarm::kPpoMaxK) return fail(SWARM_ECAPACITY, "1 <= k <= 16 actions");
+  const int n = T * S;
+  const PpoWorkspace ws = ppo_workspace(n, d_in, hidden, k);
+  if (workspace_bytes < (int64_t)ws.total)
+    return fail(SWARM_EINVAL, "workspace smaller than swarm_ppo_workspace_bytes");
+  char* base = static_cast<char*>(workspace);
+  float* values = reinterpret_cast<float*>(base + ws.values);
+  float* adv = reinterpret_cast<float*>(base + ws.adv);
+  float* dv = reinterpret_cast<float*>(base + ws.dv);
+  double* stats = reinterpret_cast<double*>(base + ws.stats);
+  float* partial = reinterpret_cast<float*>(base + ws.partial);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipMemsetAsync(stats, 0, 2 * sizeof(double), s));
+  hipLaunchKernelGGL(swarm::k_ppo_values, dim3((unsigned)((n + 255) / 256)), dim3(256),
+                     (size_t)hidden * (d_in + 2) * sizeof(float), s, x, n, d_in, w1, b1, hidden,
+                     wc, bc, values);
+  hipLaunchKernelGGL(swarm::k_ppo_gae, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, s,
+                     rewards, values, T, S, gamma, lambda, adv, dv, stats);
+  const int HB = hidden <= 64 ? 64 : (hidden <= 128 ? 128 : 256);
+  const long tiles = ((long)n + swarm::PpoTile<256>::kTile - 1) / swarm::PpoTile<256>::kTile;
+  // every block writes its partial row; the reduce reads exactly the rows written
+  const int blocks = (int)std::min<long>(tiles, swarm::kPpoBlocks);
+#define SWARM_PPO(HH, DD, KK)                                                                  \
+  hipLaunchKernelGGL((swarm::k_ppo_grads<HH, DD, KK>), dim3((unsigned)blocks), dim3(HH), 0, s, \
+                     x, n, d_in, w1, b1, hidden, wa, ba, k, wc, bc, actions, old_logp, adv,   \
+                     dv, stats, clip_eps, entropy_coef, partial)
+#define SWARM_PPO_H(HH)                          \
+  do {                                           \
+    if (d_in <= 4 && k <= 4)                     \
+      SWARM_PPO(HH, 4, 4);                       \
+    else if (d_in <= 4)                          \
+      SWARM_PPO(HH, 4, 16);                      \
+    else if (d_in <= 16 && k <= 4)               \
+      SWARM_PPO(HH, 16, 4);                      \
+    else if (d_in <= 16)                         \
+      SWARM_PPO(HH, 16, 16);                     \
+    else if (k <= 4)                             \
+      SWARM_PPO(HH, 32, 4);                      \
+    else                                         \
+      SWARM_PPO(HH, 32, 16);                     \
+  } while (0)
+  if (HB == 64)
+    SWARM_PPO_H(64);
+  else if (HB == 128)
+    SWARM_PPO_H(128);
+  else
+    SWARM_PPO_H(256);
+#undef SWARM_PPO_H
+#undef SWARM_PPO
+  const int size = swarm::ppo_grad_size(d_in, hidden, k);
+  hipLaunchKernelGGL(swarm::k_ppo_reduce, dim3((unsigned)((size + 63) / 64)), dim3(256), 0, s,
+                     partial, blocks, size, grad);
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
 }

@@ -351,6 +351,48 @@ def policy_mlp_sample(obs: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2:
     return idx, logp, f, t
 
 
+_PPO_WS: Dict[Tuple[int, int], torch.Tensor] = {}
+
+
+def ppo_epoch_grad(features: torch.Tensor, actions: torch.Tensor, old_logp: torch.Tensor,
+                   rewards: torch.Tensor, layers, gamma: float, lambda_: float,
+                   clip_eps: float, entropy_coef: float) -> torch.Tensor:
+    """
+    The gradient of one PPO epoch (swarm_ppo_epoch_grad): features [T, S, d]
+    fp32, actions [T, S] int64, old_logp / rewards [T, S] fp32 (all device),
+    layers = (w1, b1, wa, ba, wc, bc) of the actor-critic MLP in torch
+    layouts.  Returns the flat gradient w1 | b1 | wa | ba | wc | bc (fp32).
+    """
+    T, S = int(actions.shape[0]), int(actions.shape[1])
+    x = features.reshape(T * S, -1).to(torch.float32).contiguous()
+    d_in = int(x.shape[1])
+    w1, b1, wa, ba, wc, bc = layers
+    hidden, k = int(w1.shape[0]), int(wa.shape[0])
+    dev = x.device
+    lib = _capi.lib()
+    nbytes = int(lib.swarm_ppo_workspace_bytes(T, S, d_in, hidden, k))
+    if nbytes < 0:
+        raise ValueError("bad PPO sizes")
+    key = (dev.index or 0, nbytes)
+    ws = _PPO_WS.get(key)
+    if ws is None:
+        _PPO_WS.clear()
+        ws = _PPO_WS[key] = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    grad = torch.empty(hidden * d_in + hidden + k * hidden + k + hidden + 1,
+                       dtype=torch.float32, device=dev)
+    acts = actions.to(torch.int64).contiguous()
+    olp = old_logp.to(torch.float32).contiguous()
+    rew = rewards.to(torch.float32).contiguous()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _capi.check(lib.swarm_ppo_epoch_grad(
+        x.data_ptr(), T, S, d_in, acts.data_ptr(), olp.data_ptr(), rew.data_ptr(),
+        w1.data_ptr(), b1.data_ptr(), hidden, wa.data_ptr(), ba.data_ptr(), k, wc.data_ptr(),
+        bc.data_ptr(), ctypes.c_float(gamma), ctypes.c_float(lambda_), ctypes.c_float(clip_eps),
+        ctypes.c_float(entropy_coef), ws.data_ptr(), nbytes, grad.data_ptr(),
+        ctypes.c_void_p(stream)))
+    return grad
+
+
 NB_COUNT, NB_PERCEPTION, NB_SUM_D, NB_SUM_D2, NB_SUM_DIR, NB_SUM_V = 0, 1, 2, 5, 6, 9
 
 

@@ -4,11 +4,19 @@ PPO loss (reference: swarmrl/losses/proximal_policy_loss.py:23-170), in torch.
 loss = sum(-min(r A, clip(r, 1-eps, 1+eps) A)) - c_H * entropy
        + 0.5 * sum(huber(V, returns)),   r = exp(log p_new(a) - log p_old(a)),
 advantages/returns from GAE on the episode's rewards and predicted values;
-n_epochs gradient steps per episode.
+n_epochs gradient steps per episode.  On the GPU, for the stock
+actor-critic MLP, each epoch's gradient comes from the fused kernels of
+swarm_ppo_epoch_grad (csrc/swarm_ppo.cuh) and torch's optimizer takes the
+step; otherwise torch autograd differentiates _calculate_loss.
 """
+
+import os
 
 import torch
 import torch.nn.functional as F
+
+from swarmrl_amd.engine import ops
+from swarmrl_amd.sampling_strategies.sampling_strategy import SamplingStrategy
 
 from swarmrl_amd.sampling_strategies.gumbel_distribution import GumbelDistribution
 from swarmrl_amd.value_functions.generalized_advantage_estimate import GAE
@@ -40,8 +48,10 @@ class ProximalPolicyLoss(Loss):
         obs_ndim = feature_data.ndim - 2
         new_logits, predicted_values = network(feature_data, obs_ndim=obs_ndim)
         predicted_values = predicted_values.squeeze(-1)
-        with torch.no_grad():
-            advantages, returns = self.value_function(rewards=rewards, values=predicted_values)
+        # as in the reference (:101-124), only the normalised advantages are
+        # held constant: the returns R = A + V stay differentiable in V
+        advantages, returns = self.value_function(rewards=rewards, values=predicted_values)
+        advantages = advantages.detach()
         new_probabilities = torch.softmax(new_logits, dim=-1)
         entropy = self.sampling_strategy.compute_entropy(new_probabilities)
         chosen = torch.gather(new_probabilities, -1, action_indices.unsqueeze(-1)).squeeze(-1)
@@ -67,6 +77,33 @@ class ProximalPolicyLoss(Loss):
             old_log_probs = old_log_probs.reshape(T, E * A)
             features = features.reshape(T, E * A, *features.shape[3:])
             rewards = rewards.reshape(rewards.shape[0], E * A)
+        layers = self._fused_layers(network, features, actions)
         for _ in range(self.n_epochs):
+            if layers is not None:
+                grad = ops.ppo_epoch_grad(features, actions, old_log_probs, rewards, layers,
+                                          self.value_function.gamma,
+                                          self.value_function.lambda_, self.epsilon,
+                                          self.entropy_coefficient)
+                network.apply_gradients(layers, grad)
+                continue
             loss = self._calculate_loss(network, features, actions, rewards, old_log_probs)
             network.update_model(loss)
+
+    def _fused_layers(self, network, features, actions):
+        """The network's layers when the epoch gradient runs as the fused
+        device kernels (swarm_ppo_epoch_grad): stock GAE and entropy, the
+        actor-critic MLP on the GPU, [T, S, ...] samples; else None (the
+        torch autograd path).  SWARMRL_AMD_FUSED_PPO=0 forces the torch path."""
+        if os.environ.get("SWARMRL_AMD_FUSED_PPO", "1") == "0" or not features.is_cuda:
+            return None
+        if type(self.value_function) is not GAE or actions.ndim != 2:
+            return None
+        if type(self.sampling_strategy).compute_entropy is not SamplingStrategy.compute_entropy:
+            return None
+        get = getattr(network, "ppo_layers", None)
+        if get is None:
+            return None
+        d_in = 1
+        for n in features.shape[2:]:
+            d_in *= int(n)
+        return get(d_in)

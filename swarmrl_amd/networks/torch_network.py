@@ -43,6 +43,12 @@ class ActorCriticMLP(nn.Module):
         policy (swarm_policy_mlp_sample)."""
         return (self.hidden.weight, self.hidden.bias, self.actor.weight, self.actor.bias)
 
+    def ppo_layers(self):
+        """(W1, b1, Wa, ba, Wc, bc), the order of the fused PPO gradient
+        (swarm_ppo_epoch_grad)."""
+        return (self.hidden.weight, self.hidden.bias, self.actor.weight, self.actor.bias,
+                self.critic.weight, self.critic.bias)
+
 
 class TorchModel:
     """Network wrapper with the FlaxModel surface used by the agents."""
@@ -153,6 +159,35 @@ class TorchModel:
         ok = ok and w1.shape[1] == d_in and w2.shape[0] == k and w2.shape[1] == w1.shape[0]
         ok = ok and d_in <= 16 and w1.shape[0] <= 256 and k <= 16
         return (w1, b1, w2, b2) if ok else None
+
+    def ppo_layers(self, d_in: int):
+        """The actor-critic weights when the fused PPO gradient applies (fp32
+        contiguous device parameters within swarm_ppo_epoch_grad's limits and
+        every trainable parameter among them), else None."""
+        get = getattr(self.model, "ppo_layers", None)
+        if get is None or self.optimizer is None:
+            return None
+        layers = get()
+        w1, b1, wa, ba, wc, bc = layers
+        ok = all(t.dtype == torch.float32 and t.is_cuda and t.is_contiguous() for t in layers)
+        ok = ok and w1.shape[1] == d_in and wa.shape[1] == w1.shape[0]
+        ok = ok and tuple(wc.shape) == (1, w1.shape[0]) and bc.numel() == 1
+        ok = ok and d_in <= 32 and w1.shape[0] <= 256 and wa.shape[0] <= 16
+        ids = {id(t) for t in layers}
+        ok = ok and all(id(p) in ids for p in self.model.parameters() if p.requires_grad)
+        return layers if ok else None
+
+    def apply_gradients(self, layers, flat_grad: torch.Tensor):
+        """One optimizer step with the gradient given as the concatenation of
+        the layers' gradients (the layout of swarm_ppo_epoch_grad)."""
+        self.optimizer.zero_grad(set_to_none=True)
+        off = 0
+        for t in layers:
+            n = t.numel()
+            t.grad = flat_grad[off:off + n].view_as(t)
+            off += n
+        self.optimizer.step()
+        self.epoch_count += 1
 
     def update_model(self, loss: torch.Tensor):
         self.optimizer.zero_grad(set_to_none=True)
