@@ -1743,7 +1743,7 @@ int swarm_policy_mlp_sample(const float* obs, int32_t n, int32_t d_in, const flo
 
 namespace {
 struct PpoWorkspace {
-  size_t values, adv, dv, stats, partial, total;
+  size_t values, adv, dv, stats, table, partial, total;
 };
 PpoWorkspace ppo_workspace(long n, int d, int hidden, int k) {
   PpoWorkspace w;
@@ -1752,7 +1752,9 @@ PpoWorkspace ppo_workspace(long n, int d, int hidden, int k) {
   w.adv = up(w.values + (size_t)n * 4);
   w.dv = up(w.adv + (size_t)n * 4);
   w.stats = up(w.dv + (size_t)n * 4);
-  w.partial = up(w.stats + 2 * sizeof(double));
+  w.table = up(w.stats + 2 * sizeof(double));
+  // unit rows: at most 256 units x PpoTable<32, 16>::kStride floats
+  w.partial = up(w.table + (size_t)swarm::kPpoMaxHidden * swarm::PpoTable<32, 16>::kStride * 4);
   w.total = up(w.partial + (size_t)swarm::kPpoBlocks * swarm::ppo_grad_size(d, hidden, k) * 4);
   return w;
 }
@@ -1789,24 +1791,39 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
   float* dv = reinterpret_cast<float*>(base + ws.dv);
   double* stats = reinterpret_cast<double*>(base + ws.stats);
   float* partial = reinterpret_cast<float*>(base + ws.partial);
+  float* table = reinterpret_cast<float*>(base + ws.table);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   HIP_TRY(hipMemsetAsync(stats, 0, 2 * sizeof(double), s));
-  hipLaunchKernelGGL(swarm::k_ppo_values, dim3((unsigned)((n + 255) / 256)), dim3(256),
-                     (size_t)hidden * (d_in + 2) * sizeof(float), s, x, n, d_in, w1, b1, hidden,
-                     wc, bc, values);
-  hipLaunchKernelGGL(swarm::k_ppo_gae, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, s,
-                     rewards, values, T, S, gamma, lambda, adv, dv, stats);
   const int HB = hidden <= 64 ? 64 : (hidden <= 128 ? 128 : 256);
-  const long tiles = ((long)n + swarm::PpoTile<256>::kTile - 1) / swarm::PpoTile<256>::kTile;
+  const long tiles = ((long)n + 63) / 64;
   // every block writes its partial row; the reduce reads exactly the rows written
   const int blocks = (int)std::min<long>(tiles, swarm::kPpoBlocks);
-#define SWARM_PPO(HH, DD, KK)                                                                  \
-  hipLaunchKernelGGL((swarm::k_ppo_grads<HH, DD, KK>), dim3((unsigned)blocks), dim3(HH), 0, s, \
-                     x, n, d_in, w1, b1, hidden, wa, ba, k, wc, bc, actions, old_logp, adv,   \
-                     dv, stats, clip_eps, entropy_coef, partial)
+  const unsigned vblocks = (unsigned)((n + 255) / 256);
+  // pack the unit rows, V of every sample, GAE + dL/dV, then the gradients
+#define SWARM_PPO(HH, DD, KK)                                                                 \
+  do {                                                                                        \
+    using Tb = swarm::PpoTable<DD, KK>;                                                       \
+    hipLaunchKernelGGL((swarm::k_ppo_pack<DD, KK>),                                           \
+                       dim3((unsigned)((HH * Tb::kStride + 255) / 256)), dim3(256), 0, s, w1, \
+                       b1, d_in, hidden, wa, k, wc, HH, table);                               \
+    hipLaunchKernelGGL((swarm::k_ppo_values<DD, KK>), dim3(vblocks), dim3(256), 0, s, x, n,   \
+                       d_in, table, hidden, bc, values);                                      \
+    hipLaunchKernelGGL(swarm::k_ppo_gae, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, s,  \
+                       rewards, values, T, S, gamma, lambda, adv, dv, stats);                 \
+    const void* fn = reinterpret_cast<const void*>(&swarm::k_ppo_grads<HH, DD, KK>);          \
+    const int lds = swarm::ppo_grads_lds_floats<HH, KK>() * (int)sizeof(float);               \
+    if (lds > 65536)                                                                          \
+      (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);         \
+    hipLaunchKernelGGL((swarm::k_ppo_grads<HH, DD, KK>), dim3((unsigned)blocks), dim3(HH),    \
+                       (size_t)lds, s, x, n, d_in, w1, b1, hidden, wa, ba, k, wc, bc,         \
+                       actions, old_logp, adv, dv, stats, table, clip_eps, entropy_coef,      \
+                       partial);                                                              \
+  } while (0)
 #define SWARM_PPO_H(HH)                          \
   do {                                           \
-    if (d_in <= 4 && k <= 4)                     \
+    if (d_in == 1 && k <= 4)                     \
+      SWARM_PPO(HH, 1, 4);                       \
+    else if (d_in <= 4 && k <= 4)                \
       SWARM_PPO(HH, 4, 4);                       \
     else if (d_in <= 4)                          \
       SWARM_PPO(HH, 4, 16);                      \
@@ -1828,7 +1845,7 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
 #undef SWARM_PPO_H
 #undef SWARM_PPO
   const int size = swarm::ppo_grad_size(d_in, hidden, k);
-  hipLaunchKernelGGL(swarm::k_ppo_reduce, dim3((unsigned)((size + 63) / 64)), dim3(256), 0, s,
+  hipLaunchKernelGGL(swarm::k_ppo_reduce, dim3((unsigned)((size + 63) / 64)), dim3(1024), 0, s,
                      partial, blocks, size, grad);
   HIP_TRY(hipGetLastError());
   return SWARM_OK;

@@ -38,38 +38,73 @@ namespace swarm {
 constexpr int kPpoMaxIn = 32;
 constexpr int kPpoMaxK = 16;
 constexpr int kPpoMaxHidden = 256;
-constexpr int kPpoBlocks = 512;  // grad blocks: 2 per CU (LDS-limited)
+constexpr int kPpoBlocks = 1024;  // grad blocks: 4 per CU
 
 // Gradient layout (floats): W1 [H][D] | b1 [H] | Wa [K][H] | ba [K] | Wc [H] | bc
 __host__ __device__ inline int ppo_grad_size(int d, int h, int k) {
   return h * d + h + k * h + k + h + 1;
 }
 
-// V of every sample (one thread per sample, hidden layer + critic in LDS).
+// Per-unit parameter rows, the wave-uniform operands of the sample-major
+// loops (one scalar-load row per unit): [Wa[:, u], Wc[u], 0 ... | W1[u, :], b1[u], 0 ...]
+template <int D, int K>
+struct PpoTable {
+  static constexpr int kHeads = (K + 1 + 7) / 8 * 8;
+  static constexpr int kW1 = kHeads;
+  static constexpr int kB1 = kHeads + D;
+  static constexpr int kStride = kHeads + (D + 1 + 7) / 8 * 8;
+};
+
+// rows = hidden rounded up to the grads block (zero rows past hidden)
+template <int D, int K>
+__global__ __launch_bounds__(256) void k_ppo_pack(const float* __restrict__ w1,
+                                                  const float* __restrict__ b1, int d,
+                                                  int hidden, const float* __restrict__ wa,
+                                                  int k, const float* __restrict__ wc, int rows,
+                                                  float* __restrict__ table) {
+  using Tb = PpoTable<D, K>;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= rows * Tb::kStride) return;
+  const int u = t / Tb::kStride, col = t - u * Tb::kStride;
+  float v = 0.0f;
+  if (u < hidden) {
+    if (col < k)
+      v = wa[(size_t)col * hidden + u];
+    else if (col == K)
+      v = wc[u];
+    else if (col >= Tb::kW1 && col < Tb::kW1 + d)
+      v = w1[(size_t)u * d + (col - Tb::kW1)];
+    else if (col == Tb::kB1)
+      v = b1[u];
+  }
+  table[t] = v;
+}
+
+// V of every sample: one thread per sample, its features in registers, the
+// unit rows wave-uniform scalar loads.
+template <int D, int K>
 __global__ __launch_bounds__(256) void k_ppo_values(const float* __restrict__ x, int n, int d,
-                                                    const float* __restrict__ w1,
-                                                    const float* __restrict__ b1, int hidden,
-                                                    const float* __restrict__ wc,
+                                                    const float* __restrict__ table, int hidden,
                                                     const float* __restrict__ bc,
                                                     float* __restrict__ values) {
-  extern __shared__ float sv[];  // w1 [hidden][d] | b1 [hidden] | wc [hidden]
-  float* sw1 = sv;
-  float* sb1 = sv + hidden * d;
-  float* swc = sb1 + hidden;
-  for (int t = threadIdx.x; t < hidden * d; t += blockDim.x) sw1[t] = w1[t];
-  for (int t = threadIdx.x; t < hidden; t += blockDim.x) {
-    sb1[t] = b1[t];
-    swc[t] = wc[t];
-  }
-  __syncthreads();
+  using Tb = PpoTable<D, K>;
   const long s = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
-  const float* xs = x + (size_t)s * d;
+  float xs[D];
+  const float* xp = x + (size_t)s * d;
+#pragma unroll
+  for (int c = 0; c < D; ++c) {
+    const float v = xp[min(c, d - 1)];
+    xs[c] = c < d ? v : 0.0f;
+  }
   float v = bc[0];
+#pragma unroll 4
   for (int j = 0; j < hidden; ++j) {
-    float h = sb1[j];
-    for (int c = 0; c < d; ++c) h = fmaf(sw1[j * d + c], xs[c], h);
-    v = fmaf(swc[j], fmaxf(h, 0.0f), v);
+    const float* row = table + (size_t)j * Tb::kStride;
+    float h = row[Tb::kB1];
+#pragma unroll
+    for (int c = 0; c < D; ++c) h = fmaf(row[Tb::kW1 + c], xs[c], h);
+    v = fmaf(row[K], fmaxf(h, 0.0f), v);
   }
   values[s] = v;
 }
@@ -130,14 +165,35 @@ __global__ __launch_bounds__(256) void k_ppo_gae(const float* __restrict__ rewar
   }
 }
 
-template <int HB>
-struct PpoTile {
-  static constexpr int kTile = HB == 256 ? 32 : 64;  // samples per tile (LDS < 64 KB)
-  static constexpr int kPer = HB / kTile;             // threads per sample for the heads
+// Value of lane l of a wave (v_readlane: wave-uniform result).
+__device__ __forceinline__ float lane_value(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+template <int K>
+struct PpoHeads {
+  static constexpr int kP = K + 1;                  // logits + value
+  static constexpr int kRow = (K + 1 + 3) / 4 * 4;  // a sample's dL/d(heads) row in LDS
 };
 
-// Per-block parameter gradients; blockDim = HB >= hidden.
-// partial: [gridDim.x][ppo_grad_size(d, hidden, k)].
+template <int HB, int K>
+__host__ __device__ constexpr int ppo_grads_lds_floats() {
+  // per-wave H transpose [64][65] | head partials of waves 1.. [K+1][64] |
+  // dL/d(logits, value) [64][kRow]
+  return (HB / 64) * 64 * 65 + (HB / 64 - 1) * (K + 1) * 64 + 64 * PpoHeads<K>::kRow;
+}
+
+// Per-block parameter gradients; blockDim = HB >= hidden, dynamic LDS
+// ppo_grads_lds_floats<HB, K>() floats.  partial: [gridDim.x][ppo_grad_size].
+// Tiles of 64 samples, lane = sample within every wave:
+//   A  thread j (unit j): h_sj for the tile's 64 samples into registers, the
+//      sample's features broadcast by v_readlane; each wave also writes its
+//      64 x 64 block of H to LDS, transposed
+//   B  wave w, lane s: the heads' partial sums over units 64w..64w+63 (H row
+//      from LDS, the unit's weights broadcast from the owning lane); wave 0
+//      adds the other waves' partials (fixed order) and forms dL/dz, dL/dV
+//   C  thread j: gradient accumulation over the 64 samples, dL/dz of each
+//      broadcast by v_readlane
 template <int HB, int D, int K>
 __global__ __launch_bounds__(HB) void k_ppo_grads(
     const float* __restrict__ x, int n, int d, const float* __restrict__ w1,
@@ -145,143 +201,170 @@ __global__ __launch_bounds__(HB) void k_ppo_grads(
     const float* __restrict__ ba, int k, const float* __restrict__ wc,
     const float* __restrict__ bc, const int64_t* __restrict__ actions,
     const float* __restrict__ old_logp, const float* __restrict__ adv,
-    const float* __restrict__ dvalue, const double* __restrict__ stats, float clip_eps,
-    float c_ent, float* __restrict__ partial) {
-  constexpr int kTile = PpoTile<HB>::kTile, kPer = PpoTile<HB>::kPer;
-  __shared__ float sx[kTile][D];
-  __shared__ float sh[kTile][HB + 1];
-  __shared__ float sz[kTile][K + 1];  // dL/d(logits, value) per sample
-  __shared__ float swo[K + 1][HB];    // [Wa; Wc] columns
-  const int j = threadIdx.x;
+    const float* __restrict__ dvalue, const double* __restrict__ stats,
+    const float* __restrict__ table, float clip_eps, float c_ent, float* __restrict__ partial) {
+  constexpr int W = HB / 64, KP = K + 1, kTab = PpoTable<D, K>::kStride;
+  extern __shared__ float ppo_lds[];
+  const int j = threadIdx.x, lane = j & 63, w = j >> 6;
+  float* sh = ppo_lds + w * 64 * 65;          // this wave's H block, [sample][unit]
+  float* red = ppo_lds + W * 64 * 65;         // [W - 1][KP][64]
+  float* sz = red + (W - 1) * KP * 64;        // [64][kRow]
+  constexpr int kRow = PpoHeads<K>::kRow;
   const bool unit = j < hidden;
-  float w1j[D], woj[K + 1];
+  float w1j[D], woj[KP];
 #pragma unroll
   for (int c = 0; c < D; ++c) w1j[c] = unit && c < d ? w1[(size_t)j * d + c] : 0.0f;
   const float b1j = unit ? b1[j] : 0.0f;
 #pragma unroll
-  for (int q = 0; q < K + 1; ++q) {
+  for (int q = 0; q < KP; ++q)
     woj[q] = !unit ? 0.0f : (q < k ? wa[(size_t)q * hidden + j] : (q == K ? wc[j] : 0.0f));
-    swo[q][j] = woj[q];
-  }
-  float bo[K + 1];
+  float bo[KP];
 #pragma unroll
-  for (int q = 0; q < K + 1; ++q) bo[q] = q < k ? ba[q] : (q == K ? bc[0] : 0.0f);
+  for (int q = 0; q < KP; ++q) bo[q] = q < k ? ba[q] : (q == K ? bc[0] : 0.0f);
   // normalised advantages (A - mean) / (std + eps): population std, fp32 eps
   const double mean = stats[0] / (double)n;
   const double var = fmax(stats[1] / (double)n - mean * mean, 0.0);
   const float a_mean = (float)mean;
   const float a_den = (float)sqrt(var) + 1.1920928955078125e-07f;
-  float gw1[D], gwo[K + 1], gb1 = 0.0f, gbo = 0.0f;
+  float gw1[D], gwo[KP], gbias[KP], gb1 = 0.0f;
 #pragma unroll
   for (int c = 0; c < D; ++c) gw1[c] = 0.0f;
 #pragma unroll
-  for (int q = 0; q < K + 1; ++q) gwo[q] = 0.0f;
-  const long tiles = ((long)n + kTile - 1) / kTile;
+  for (int q = 0; q < KP; ++q) gwo[q] = gbias[q] = 0.0f;
+  const long tiles = ((long)n + 63) / 64;
   for (long tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-    const long s0 = tile * kTile;
-    __syncthreads();  // the previous tile's readers are done
-    for (int t = j; t < kTile * D; t += HB) {
-      const int s = t / D, c = t - s * D;
-      sx[s][c] = s0 + s < n && c < d ? x[(size_t)(s0 + s) * d + c] : 0.0f;
-    }
-    __syncthreads();
-    if (unit) {
-      for (int s = 0; s < kTile; ++s) {
-        float h = b1j;
-#pragma unroll
-        for (int c = 0; c < D; ++c) h = fmaf(w1j[c], sx[s][c], h);
-        sh[s][j] = fmaxf(h, 0.0f);
-      }
-    }
-    __syncthreads();
+    const long si = tile * 64 + lane;
+    const bool valid = si < n;
+    float xr[D];
     {
-      // heads: kPer threads per sample split the hidden units
-      const int s = j / kPer, part = j - s * kPer;
-      float acc[K + 1];
+      // clamped loads and a select, no branches (a feature c >= d meets a
+      // zero weight; a sample past n has dL/dz = 0 below, so adds nothing)
+      const float* xs = x + (size_t)min(si, (long)n - 1) * d;
 #pragma unroll
-      for (int q = 0; q < K + 1; ++q) acc[q] = 0.0f;
-      for (int u = part; u < hidden; u += kPer) {
-        const float h = sh[s][u];
-#pragma unroll
-        for (int q = 0; q < K + 1; ++q) acc[q] = fmaf(swo[q][u], h, acc[q]);
+      for (int c = 0; c < D; ++c) {
+        const float v = xs[min(c, d - 1)];
+        xr[c] = c < d ? v : 0.0f;
       }
+    }
+    // A: hidden activations of the 64 samples, features broadcast by v_readlane
+    float hs[64];
 #pragma unroll
-      for (int o = 1; o < kPer; o <<= 1) {
+    for (int s = 0; s < 64; ++s) {
+      float h = b1j;
 #pragma unroll
-        for (int q = 0; q < K + 1; ++q) acc[q] += __shfl_xor(acc[q], o, 64);
+      for (int c = 0; c < D; ++c) h = fmaf(w1j[c], lane_value(xr[c], s), h);
+      hs[s] = fmaxf(h, 0.0f);
+      sh[s * 65 + lane] = hs[s];
+    }
+    __syncthreads();
+    // B: heads, lane = sample, this wave's 64 units
+    float acc[KP];
+#pragma unroll
+    for (int q = 0; q < KP; ++q) acc[q] = 0.0f;
+    {
+      // the unit's head weights: one wave-uniform row of the packed table
+      const float* row = table + (size_t)__builtin_amdgcn_readfirstlane(w) * 64 * kTab;
+#pragma unroll 4
+      for (int u = 0; u < 64; ++u) {
+        const float h = sh[lane * 65 + u];
+#pragma unroll
+        for (int q = 0; q < KP; ++q) acc[q] = fmaf(row[u * kTab + q], h, acc[q]);
       }
-      const long si = s0 + s;
-      if (part == 0) {
-        float g[K + 1];
+    }
+    if (w > 0) {
 #pragma unroll
-        for (int q = 0; q < K + 1; ++q) g[q] = 0.0f;
-        if (si < n) {
-          float z[K], p[K];
+      for (int q = 0; q < KP; ++q) red[((w - 1) * KP + q) * 64 + lane] = acc[q];
+    }
+    __syncthreads();
+    if (w == 0) {
 #pragma unroll
-          for (int q = 0; q < K; ++q) z[q] = acc[q] + bo[q];
-          float m = z[0];
+      for (int ww = 1; ww < W; ++ww) {
 #pragma unroll
-          for (int q = 1; q < K; ++q)
-            if (q < k) m = fmaxf(m, z[q]);
-          float sum = 0.0f;
+        for (int q = 0; q < KP; ++q) acc[q] += red[((ww - 1) * KP + q) * 64 + lane];
+      }
+      float g[KP];
 #pragma unroll
-          for (int q = 0; q < K; ++q) {
-            p[q] = q < k ? expf(z[q] - m) : 0.0f;
-            sum += p[q];
-          }
-          const int a = (int)actions[si];
-          float pa = 0.0f;
+      for (int q = 0; q < KP; ++q) g[q] = 0.0f;
+      if (valid) {
+        float p[K];
+        float m = acc[0] + bo[0];
 #pragma unroll
-          for (int q = 0; q < K; ++q) {
-            p[q] = p[q] / sum;
-            pa = q == a ? p[q] : pa;
-          }
-          // -min(r A, clip(r, 1 - eps, 1 + eps) A): a tie splits the gradient
-          // evenly between the two arguments, clip passes it on its closed range
-          const float A = (adv[si] - a_mean) / a_den;
-          const float r = expf(logf(pa + 1e-8f) - old_logp[si]);
-          const float lo = 1.0f - clip_eps, hi = 1.0f + clip_eps;
-          const float rc = fminf(fmaxf(r, lo), hi);
-          const float t1 = r * A, t2 = rc * A;
-          const float w1st = t1 < t2 ? 1.0f : (t1 > t2 ? 0.0f : 0.5f);
-          const float in = (r >= lo && r <= hi) ? 1.0f : 0.0f;
-          const float d_r = -A * (w1st + (1.0f - w1st) * in);
-          const float d_pa = d_r * r / (pa + 1e-8f);
-          // entropy term: + c_ent sum_q (p_q + eps) log(p_q + eps)
-          float dp[K], pdp = 0.0f;
+        for (int q = 1; q < K; ++q)
+          if (q < k) m = fmaxf(m, acc[q] + bo[q]);
+        float sum = 0.0f;
 #pragma unroll
-          for (int q = 0; q < K; ++q) {
-            dp[q] = q < k ? c_ent * (logf(p[q] + 1e-8f) + 1.0f) + (q == a ? d_pa : 0.0f) : 0.0f;
-            pdp = fmaf(p[q], dp[q], pdp);
-          }
+        for (int q = 0; q < K; ++q) {
+          p[q] = q < k ? expf(acc[q] + bo[q] - m) : 0.0f;
+          sum += p[q];
+        }
+        const int a = (int)actions[si];
+        float pa = 0.0f;
 #pragma unroll
-          for (int q = 0; q < K; ++q) g[q] = p[q] * (dp[q] - pdp);
-          g[K] = dvalue[si];
+        for (int q = 0; q < K; ++q) {
+          p[q] = p[q] / sum;
+          pa = q == a ? p[q] : pa;
+        }
+        // -min(r A, clip(r, 1 - eps, 1 + eps) A): a tie splits the gradient
+        // evenly between the two arguments, clip passes it on its closed range
+        const float A = (adv[si] - a_mean) / a_den;
+        const float r = expf(logf(pa + 1e-8f) - old_logp[si]);
+        const float lo = 1.0f - clip_eps, hi = 1.0f + clip_eps;
+        const float rc = fminf(fmaxf(r, lo), hi);
+        const float t1 = r * A, t2 = rc * A;
+        const float w1st = t1 < t2 ? 1.0f : (t1 > t2 ? 0.0f : 0.5f);
+        const float in = (r >= lo && r <= hi) ? 1.0f : 0.0f;
+        const float d_r = -A * (w1st + (1.0f - w1st) * in);
+        const float d_pa = d_r * r / (pa + 1e-8f);
+        // entropy term: + c_ent sum_q (p_q + eps) log(p_q + eps)
+        float dp[K], pdp = 0.0f;
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+          dp[q] = q < k ? c_ent * (logf(p[q] + 1e-8f) + 1.0f) + (q == a ? d_pa : 0.0f) : 0.0f;
+          pdp = fmaf(p[q], dp[q], pdp);
         }
 #pragma unroll
-        for (int q = 0; q < K + 1; ++q) sz[s][q] = g[q];
+        for (int q = 0; q < K; ++q) g[q] = p[q] * (dp[q] - pdp);
+        g[K] = dvalue[si];
+      }
+#pragma unroll
+      for (int q = 0; q < KP; ++q) {
+        sz[lane * kRow + q] = g[q];
+        gbias[q] += g[q];
       }
     }
     __syncthreads();
-    // back through the layers: thread j sums its unit's gradients
-    if (unit) {
-      for (int s = 0; s < kTile; ++s) {
-        const float h = sh[s][j];
-        float dh = 0.0f;
+    float gq[KP];
 #pragma unroll
-        for (int q = 0; q < K + 1; ++q) {
-          const float gq = sz[s][q];
-          gwo[q] = fmaf(gq, h, gwo[q]);
-          dh = fmaf(woj[q], gq, dh);
-        }
-        dh = h > 0.0f ? dh : 0.0f;
-        gb1 += dh;
+    for (int q = 0; q < KP; ++q) gq[q] = sz[lane * kRow + q];
+    // broadcast the features again in C rather than keep phase A's 64 x D
+    // uniform copies alive (they would spill the SGPR file)
 #pragma unroll
-        for (int c = 0; c < D; ++c) gw1[c] = fmaf(dh, sx[s][c], gw1[c]);
+    for (int c = 0; c < D; ++c) asm volatile("" : "+v"(xr[c]));
+    // C: thread j sums its unit's gradients over the 64 samples, dL/dz of
+    // each broadcast by v_readlane
+#pragma unroll
+    for (int s = 0; s < 64; ++s) {
+      const float h = hs[s];
+      float dh = 0.0f;
+#pragma unroll
+      for (int q = 0; q < KP; ++q) {
+        const float g = lane_value(gq[q], s);
+        gwo[q] = fmaf(g, h, gwo[q]);
+        dh = fmaf(woj[q], g, dh);
       }
+      dh = h > 0.0f ? dh : 0.0f;
+      gb1 += dh;
+#pragma unroll
+      for (int c = 0; c < D; ++c) gw1[c] = fmaf(dh, lane_value(xr[c], s), gw1[c]);
     }
-    if (j <= K) {
-      for (int s = 0; s < kTile; ++s) gbo += sz[s][j];
+  }
+  // output-bias gradients: wave 0's per-lane sums, reduced across the wave
+  if (w == 0) {
+#pragma unroll
+    for (int q = 0; q < KP; ++q) {
+      float v = gbias[q];
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      gbias[q] = v;
     }
   }
   float* out = partial + (size_t)blockIdx.x * ppo_grad_size(d, hidden, k);
@@ -297,26 +380,34 @@ __global__ __launch_bounds__(HB) void k_ppo_grads(
       if (q < k) out[o_wa + q * hidden + j] = gwo[q];
     out[o_wc + j] = gwo[K];
   }
-  if (j < k) out[o_ba + j] = gbo;
-  if (j == K) out[o_bc] = gbo;
+  if (j == 0) {
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+      if (q < k) out[o_ba + q] = gbias[q];
+    out[o_bc] = gbias[K];
+  }
 }
 
-// Sum of the block partials, fp64 in a fixed order.  Workgroup 256 = 64
-// parameters x 4 block strides.
-__global__ __launch_bounds__(256) void k_ppo_reduce(const float* __restrict__ partial,
-                                                    int n_blocks, int size,
-                                                    float* __restrict__ grad) {
-  __shared__ double red[4][64];
+// Sum of the block partials, fp64 in a fixed order.  Workgroup 1024 = 64
+// parameters x 16 block strides.
+__global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ partial,
+                                                     int n_blocks, int size,
+                                                     float* __restrict__ grad) {
+  __shared__ double red[16][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int p = blockIdx.x * 64 + lane;
   double acc = 0.0;
   if (p < size) {
-    for (int b = w; b < n_blocks; b += 4) acc += (double)partial[(size_t)b * size + p];
+#pragma unroll 8
+    for (int b = w; b < n_blocks; b += 16) acc += (double)partial[(size_t)b * size + p];
   }
   red[w][lane] = acc;
   __syncthreads();
-  if (w == 0 && p < size)
-    grad[p] = (float)(((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
+  if (w == 0 && p < size) {
+    double t = 0.0;
+    for (int i = 0; i < 16; ++i) t += red[i][lane];
+    grad[p] = (float)t;
+  }
 }
 
 }  // namespace swarm

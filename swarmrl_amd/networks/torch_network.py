@@ -77,7 +77,10 @@ class TorchModel:
         self.exploration_policy = exploration_policy
         self.deployment_mode = deployment_mode
         if optimizer is None:
-            optimizer = lambda params: torch.optim.Adam(params, lr=learning_rate)  # noqa: E731
+            # optax.adam of the reference; on the GPU one fused launch per step
+            fused = self.device.type == "cuda"
+            optimizer = lambda params: torch.optim.Adam(  # noqa: E731
+                params, lr=learning_rate, fused=fused)
         self._optimizer_factory = optimizer
         self.optimizer = None if deployment_mode else optimizer(self.model.parameters())
         self.epoch_count = 0
