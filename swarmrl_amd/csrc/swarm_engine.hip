@@ -1743,16 +1743,17 @@ int swarm_policy_mlp_sample(const float* obs, int32_t n, int32_t d_in, const flo
 
 namespace {
 struct PpoWorkspace {
-  size_t values, adv, dv, stats, table, partial, total;
+  size_t values, adv, dv, stats, spart, table, partial, total;
 };
-PpoWorkspace ppo_workspace(long n, int d, int hidden, int k) {
+PpoWorkspace ppo_workspace(long n, long S, int d, int hidden, int k) {
   PpoWorkspace w;
   auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
   w.values = 0;
   w.adv = up(w.values + (size_t)n * 4);
   w.dv = up(w.adv + (size_t)n * 4);
   w.stats = up(w.dv + (size_t)n * 4);
-  w.table = up(w.stats + 2 * sizeof(double));
+  w.spart = up(w.stats + 2 * sizeof(double));
+  w.table = up(w.spart + (size_t)((S + 255) / 256) * 2 * sizeof(double));
   // unit rows: at most 256 units x PpoTable<32, 16>::kStride floats
   w.partial = up(w.table + (size_t)swarm::kPpoMaxHidden * swarm::PpoTable<32, 16>::kStride * 4);
   w.total = up(w.partial + (size_t)swarm::kPpoBlocks * swarm::ppo_grad_size(d, hidden, k) * 4);
@@ -1763,7 +1764,7 @@ PpoWorkspace ppo_workspace(long n, int d, int hidden, int k) {
 int64_t swarm_ppo_workspace_bytes(int32_t T, int32_t S, int32_t d_in, int32_t hidden,
                                   int32_t k) {
   if (T < 1 || S < 1 || d_in < 1 || hidden < 1 || k < 1) return -1;
-  return (int64_t)ppo_workspace((long)T * S, d_in, hidden, k).total;
+  return (int64_t)ppo_workspace((long)T * S, S, d_in, hidden, k).total;
 }
 
 int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
@@ -1782,7 +1783,7 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
     return fail(SWARM_ECAPACITY, "1 <= hidden <= 256");
   if (k < 1 || k > swarm::kPpoMaxK) return fail(SWARM_ECAPACITY, "1 <= k <= 16 actions");
   const int n = T * S;
-  const PpoWorkspace ws = ppo_workspace(n, d_in, hidden, k);
+  const PpoWorkspace ws = ppo_workspace(n, S, d_in, hidden, k);
   if (workspace_bytes < (int64_t)ws.total)
     return fail(SWARM_EINVAL, "workspace smaller than swarm_ppo_workspace_bytes");
   char* base = static_cast<char*>(workspace);
@@ -1792,13 +1793,14 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
   double* stats = reinterpret_cast<double*>(base + ws.stats);
   float* partial = reinterpret_cast<float*>(base + ws.partial);
   float* table = reinterpret_cast<float*>(base + ws.table);
+  double* spart = reinterpret_cast<double*>(base + ws.spart);
+  const int gae_blocks = (S + 255) / 256;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  HIP_TRY(hipMemsetAsync(stats, 0, 2 * sizeof(double), s));
   const int HB = hidden <= 64 ? 64 : (hidden <= 128 ? 128 : 256);
   const long tiles = ((long)n + 63) / 64;
   // every block writes its partial row; the reduce reads exactly the rows written
   const int blocks = (int)std::min<long>(tiles, swarm::kPpoBlocks);
-  const unsigned vblocks = (unsigned)((n + 255) / 256);
+  const unsigned vblocks = (unsigned)(((n + 1) / 2 + 255) / 256);
   // pack the unit rows, V of every sample, GAE + dL/dV, then the gradients
 #define SWARM_PPO(HH, DD, KK)                                                                 \
   do {                                                                                        \
@@ -1808,8 +1810,9 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
                        b1, d_in, hidden, wa, k, wc, HH, table);                               \
     hipLaunchKernelGGL((swarm::k_ppo_values<DD, KK>), dim3(vblocks), dim3(256), 0, s, x, n,   \
                        d_in, table, hidden, bc, values);                                      \
-    hipLaunchKernelGGL(swarm::k_ppo_gae, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, s,  \
-                       rewards, values, T, S, gamma, lambda, adv, dv, stats);                 \
+    hipLaunchKernelGGL(swarm::k_ppo_gae, dim3((unsigned)gae_blocks), dim3(256), 0, s, rewards, \
+                       values, T, S, gamma, lambda, adv, dv, spart);                          \
+    hipLaunchKernelGGL(swarm::k_ppo_stats, dim3(1), dim3(256), 0, s, spart, gae_blocks, stats); \
     const void* fn = reinterpret_cast<const void*>(&swarm::k_ppo_grads<HH, DD, KK>);          \
     const int lds = swarm::ppo_grads_lds_floats<HH, KK>() * (int)sizeof(float);               \
     if (lds > 65536)                                                                          \

@@ -11,7 +11,8 @@
 //   k_ppo_values  V = critic(relu(W1 x + b1)) of every sample
 //   k_ppo_gae     per agent column: the generalized advantages and returns
 //                 (generalized_advantage_estimate.py:42-72), the sum and sum
-//                 of squares of the advantages (fp64, for their
+//                 of squares of the advantages (fp64 block partials summed
+//                 in a fixed order by k_ppo_stats, for their
 //                 normalisation), and dL/dV of the critic term -- which, as
 //                 in the reference, differentiates the returns too
 //                 (R = A + V is built from the predicted values; only the
@@ -80,44 +81,51 @@ __global__ __launch_bounds__(256) void k_ppo_pack(const float* __restrict__ w1,
   table[t] = v;
 }
 
-// V of every sample: one thread per sample, its features in registers, the
-// unit rows wave-uniform scalar loads.
+typedef float ppo_f2 __attribute__((ext_vector_type(2)));
+
+// V of every sample: one thread per two adjacent samples (packed fp32 FMAs,
+// v_pk_fma_f32), their features in registers, the unit rows wave-uniform
+// scalar loads.
 template <int D, int K>
 __global__ __launch_bounds__(256) void k_ppo_values(const float* __restrict__ x, int n, int d,
                                                     const float* __restrict__ table, int hidden,
                                                     const float* __restrict__ bc,
                                                     float* __restrict__ values) {
   using Tb = PpoTable<D, K>;
-  const long s = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long s = 2 * ((long)blockIdx.x * blockDim.x + threadIdx.x);
   if (s >= n) return;
-  float xs[D];
-  const float* xp = x + (size_t)s * d;
+  const long s1 = min(s + 1, (long)n - 1);  // an odd n pairs the last sample with itself
+  ppo_f2 xs[D];
+  const float* xa = x + (size_t)s * d;
+  const float* xb = x + (size_t)s1 * d;
 #pragma unroll
   for (int c = 0; c < D; ++c) {
-    const float v = xp[min(c, d - 1)];
-    xs[c] = c < d ? v : 0.0f;
+    const float va = xa[min(c, d - 1)], vb = xb[min(c, d - 1)];
+    xs[c] = c < d ? ppo_f2{va, vb} : ppo_f2{0.0f, 0.0f};
   }
-  float v = bc[0];
+  ppo_f2 v = bc[0];
 #pragma unroll 4
   for (int j = 0; j < hidden; ++j) {
     const float* row = table + (size_t)j * Tb::kStride;
-    float h = row[Tb::kB1];
+    ppo_f2 h = row[Tb::kB1];
 #pragma unroll
-    for (int c = 0; c < D; ++c) h = fmaf(row[Tb::kW1 + c], xs[c], h);
-    v = fmaf(row[K], fmaxf(h, 0.0f), v);
+    for (int c = 0; c < D; ++c) h = __builtin_elementwise_fma((ppo_f2)row[Tb::kW1 + c], xs[c], h);
+    h = __builtin_elementwise_max(h, (ppo_f2)0.0f);
+    v = __builtin_elementwise_fma((ppo_f2)row[K], h, v);
   }
-  values[s] = v;
+  values[s] = v.x;
+  if (s + 1 < n) values[s + 1] = v.y;
 }
 
 // One thread per agent column of the T x S sample grid (sample t * S + col).
 // adv: raw advantages; dv: dL/dV = 0.5 huber'(V - R) minus the returns'
 // dependence on later values, dR_t/dV_u = gamma (1 - lambda) (gamma
-// lambda)^(u-1-t) for u > t; stats[0..1] += sum A, sum A^2.
+// lambda)^(u-1-t) for u > t; part[2 block + 0..1] = the block's sum A, sum A^2.
 __global__ __launch_bounds__(256) void k_ppo_gae(const float* __restrict__ rewards,
                                                  const float* __restrict__ values, int T, int S,
                                                  float gamma, float lambda,
                                                  float* __restrict__ adv, float* __restrict__ dv,
-                                                 double* __restrict__ stats) {
+                                                 double* __restrict__ part) {
   __shared__ double red[2][4];
   const int col = blockIdx.x * blockDim.x + threadIdx.x;
   double s1 = 0.0, s2 = 0.0;
@@ -160,8 +168,33 @@ __global__ __launch_bounds__(256) void k_ppo_gae(const float* __restrict__ rewar
       a += red[0][w];
       b += red[1][w];
     }
-    atomicAdd(&stats[0], a);
-    atomicAdd(&stats[1], b);
+    part[2 * blockIdx.x] = a;
+    part[2 * blockIdx.x + 1] = b;
+  }
+}
+
+// stats[0..1] = the sums of the GAE blocks' partials, in a fixed order.
+__global__ __launch_bounds__(256) void k_ppo_stats(const double* __restrict__ part,
+                                                   int n_part, double* __restrict__ stats) {
+  __shared__ double red[2][256];
+  double a = 0.0, b = 0.0;
+  for (int i = threadIdx.x; i < n_part; i += 256) {
+    a += part[2 * i];
+    b += part[2 * i + 1];
+  }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + o];
+      red[1][threadIdx.x] += red[1][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    stats[0] = red[0][0];
+    stats[1] = red[1][0];
   }
 }
 
