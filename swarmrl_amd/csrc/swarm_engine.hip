@@ -1796,55 +1796,54 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
   double* spart = reinterpret_cast<double*>(base + ws.spart);
   const int gae_blocks = (S + 255) / 256;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int HB = hidden <= 64 ? 64 : (hidden <= 128 ? 128 : 256);
+  const int NW = hidden <= 128 ? 1 : 2;  // waves of 128 units
   const long tiles = ((long)n + 63) / 64;
   // every block writes its partial row; the reduce reads exactly the rows written
   const int blocks = (int)std::min<long>(tiles, swarm::kPpoBlocks);
   const unsigned vblocks = (unsigned)(((n + 1) / 2 + 255) / 256);
   // pack the unit rows, V of every sample, GAE + dL/dV, then the gradients
-#define SWARM_PPO(HH, DD, KK)                                                                 \
+#define SWARM_PPO(NN, DD, KK)                                                                 \
   do {                                                                                        \
     using Tb = swarm::PpoTable<DD, KK>;                                                       \
     hipLaunchKernelGGL((swarm::k_ppo_pack<DD, KK>),                                           \
-                       dim3((unsigned)((HH * Tb::kStride + 255) / 256)), dim3(256), 0, s, w1, \
-                       b1, d_in, hidden, wa, k, wc, HH, table);                               \
+                       dim3((unsigned)((128 * NN * Tb::kStride + 255) / 256)), dim3(256), 0, \
+                       s, w1, b1, d_in, hidden, wa, k, wc, 128 * NN, table);                  \
     hipLaunchKernelGGL((swarm::k_ppo_values<DD, KK>), dim3(vblocks), dim3(256), 0, s, x, n,   \
                        d_in, table, hidden, bc, values);                                      \
     hipLaunchKernelGGL(swarm::k_ppo_gae, dim3((unsigned)gae_blocks), dim3(256), 0, s, rewards, \
                        values, T, S, gamma, lambda, adv, dv, spart);                          \
     hipLaunchKernelGGL(swarm::k_ppo_stats, dim3(1), dim3(256), 0, s, spart, gae_blocks, stats); \
-    const void* fn = reinterpret_cast<const void*>(&swarm::k_ppo_grads<HH, DD, KK>);          \
-    const int lds = swarm::ppo_grads_lds_floats<HH, KK>() * (int)sizeof(float);               \
+    const void* fn = reinterpret_cast<const void*>(&swarm::k_ppo_grads<NN, DD, KK>);          \
+    const int lds = swarm::ppo_grads_lds_floats<NN, KK>() * (int)sizeof(float);               \
     if (lds > 65536)                                                                          \
       (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);         \
-    hipLaunchKernelGGL((swarm::k_ppo_grads<HH, DD, KK>), dim3((unsigned)blocks), dim3(HH),    \
+    hipLaunchKernelGGL((swarm::k_ppo_grads<NN, DD, KK>), dim3((unsigned)blocks),             \
+                       dim3(64 * NN),                                                         \
                        (size_t)lds, s, x, n, d_in, w1, b1, hidden, wa, ba, k, wc, bc,         \
                        actions, old_logp, adv, dv, stats, table, clip_eps, entropy_coef,      \
                        partial);                                                              \
   } while (0)
-#define SWARM_PPO_H(HH)                          \
+#define SWARM_PPO_H(NN)                          \
   do {                                           \
     if (d_in == 1 && k <= 4)                     \
-      SWARM_PPO(HH, 1, 4);                       \
+      SWARM_PPO(NN, 1, 4);                       \
     else if (d_in <= 4 && k <= 4)                \
-      SWARM_PPO(HH, 4, 4);                       \
+      SWARM_PPO(NN, 4, 4);                       \
     else if (d_in <= 4)                          \
-      SWARM_PPO(HH, 4, 16);                      \
+      SWARM_PPO(NN, 4, 16);                      \
     else if (d_in <= 16 && k <= 4)               \
-      SWARM_PPO(HH, 16, 4);                      \
+      SWARM_PPO(NN, 16, 4);                      \
     else if (d_in <= 16)                         \
-      SWARM_PPO(HH, 16, 16);                     \
+      SWARM_PPO(NN, 16, 16);                     \
     else if (k <= 4)                             \
-      SWARM_PPO(HH, 32, 4);                      \
+      SWARM_PPO(NN, 32, 4);                      \
     else                                         \
-      SWARM_PPO(HH, 32, 16);                     \
+      SWARM_PPO(NN, 32, 16);                     \
   } while (0)
-  if (HB == 64)
-    SWARM_PPO_H(64);
-  else if (HB == 128)
-    SWARM_PPO_H(128);
+  if (NW == 1)
+    SWARM_PPO_H(1);
   else
-    SWARM_PPO_H(256);
+    SWARM_PPO_H(2);
 #undef SWARM_PPO_H
 #undef SWARM_PPO
   const int size = swarm::ppo_grad_size(d_in, hidden, k);

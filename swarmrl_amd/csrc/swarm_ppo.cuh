@@ -39,7 +39,7 @@ namespace swarm {
 constexpr int kPpoMaxIn = 32;
 constexpr int kPpoMaxK = 16;
 constexpr int kPpoMaxHidden = 256;
-constexpr int kPpoBlocks = 1024;  // grad blocks: 4 per CU
+constexpr int kPpoBlocks = 2048;  // grad blocks (one or two waves each)
 
 // Gradient layout (floats): W1 [H][D] | b1 [H] | Wa [K][H] | ba [K] | Wc [H] | bc
 __host__ __device__ inline int ppo_grad_size(int d, int h, int k) {
@@ -209,26 +209,31 @@ struct PpoHeads {
   static constexpr int kRow = (K + 1 + 3) / 4 * 4;  // a sample's dL/d(heads) row in LDS
 };
 
-template <int HB, int K>
+template <int NW, int K>
 __host__ __device__ constexpr int ppo_grads_lds_floats() {
-  // per-wave H transpose [64][65] | head partials of waves 1.. [K+1][64] |
-  // dL/d(logits, value) [64][kRow]
-  return (HB / 64) * 64 * 65 + (HB / 64 - 1) * (K + 1) * 64 + 64 * PpoHeads<K>::kRow;
+  // per-wave H half-block transpose [64][65] | head partials of waves 1..
+  // [K+1][64] | dL/d(logits, value) [64][kRow]
+  return NW * 64 * 65 + (NW - 1) * (K + 1) * 64 + 64 * PpoHeads<K>::kRow;
 }
 
-// Per-block parameter gradients; blockDim = HB >= hidden, dynamic LDS
-// ppo_grads_lds_floats<HB, K>() floats.  partial: [gridDim.x][ppo_grad_size].
-// Tiles of 64 samples, lane = sample within every wave:
-//   A  thread j (unit j): h_sj for the tile's 64 samples into registers, the
-//      sample's features broadcast by v_readlane; each wave also writes its
-//      64 x 64 block of H to LDS, transposed
-//   B  wave w, lane s: the heads' partial sums over units 64w..64w+63 (H row
-//      from LDS, the unit's weights broadcast from the owning lane); wave 0
-//      adds the other waves' partials (fixed order) and forms dL/dz, dL/dV
-//   C  thread j: gradient accumulation over the 64 samples, dL/dz of each
-//      broadcast by v_readlane
-template <int HB, int D, int K>
-__global__ __launch_bounds__(HB) void k_ppo_grads(
+__device__ __forceinline__ ppo_f2 ppo_splat(float v) { return ppo_f2{v, v}; }
+
+// Per-block parameter gradients; NW waves, each owning 128 hidden units --
+// thread (w, lane) holds units u0 = 128 w + lane and u1 = u0 + 64 as the two
+// halves of packed fp32 registers, so every broadcast operand feeds a
+// v_pk_fma_f32 for two units.  Dynamic LDS ppo_grads_lds_floats<NW, K>()
+// floats; partial: [gridDim.x][ppo_grad_size].  Tiles of 64 samples:
+//   A  h of both units for the tile's 64 samples into registers, each
+//      sample's features broadcast from its lane by v_readlane
+//   B  lane = sample: the heads' partial sums over the wave's 128 units, H
+//      transposed through LDS one 64-unit half at a time, the unit's head
+//      weights one scalar-load row of the packed table; wave 0 adds the other
+//      waves' partials (fixed order) and forms dL/dz, dL/dV of its lane's
+//      sample
+//   C  gradient accumulation over the 64 samples, dL/dz of each broadcast by
+//      v_readlane
+template <int NW, int D, int K>
+__global__ __launch_bounds__(64 * NW) void k_ppo_grads(
     const float* __restrict__ x, int n, int d, const float* __restrict__ w1,
     const float* __restrict__ b1, int hidden, const float* __restrict__ wa,
     const float* __restrict__ ba, int k, const float* __restrict__ wc,
@@ -236,21 +241,27 @@ __global__ __launch_bounds__(HB) void k_ppo_grads(
     const float* __restrict__ old_logp, const float* __restrict__ adv,
     const float* __restrict__ dvalue, const double* __restrict__ stats,
     const float* __restrict__ table, float clip_eps, float c_ent, float* __restrict__ partial) {
-  constexpr int W = HB / 64, KP = K + 1, kTab = PpoTable<D, K>::kStride;
+  constexpr int KP = K + 1, kTab = PpoTable<D, K>::kStride, kRow = PpoHeads<K>::kRow;
   extern __shared__ float ppo_lds[];
-  const int j = threadIdx.x, lane = j & 63, w = j >> 6;
-  float* sh = ppo_lds + w * 64 * 65;          // this wave's H block, [sample][unit]
-  float* red = ppo_lds + W * 64 * 65;         // [W - 1][KP][64]
-  float* sz = red + (W - 1) * KP * 64;        // [64][kRow]
-  constexpr int kRow = PpoHeads<K>::kRow;
-  const bool unit = j < hidden;
-  float w1j[D], woj[KP];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  float* sh = ppo_lds + w * 64 * 65;   // this wave's H half-block, [sample][unit]
+  float* red = ppo_lds + NW * 64 * 65; // [NW - 1][KP][64]
+  float* sz = red + (NW - 1) * KP * 64;
+  const int u0 = 128 * w + lane, u1 = u0 + 64;
+  const bool in0 = u0 < hidden, in1 = u1 < hidden;
+  ppo_f2 w1p[D], wop[KP];
 #pragma unroll
-  for (int c = 0; c < D; ++c) w1j[c] = unit && c < d ? w1[(size_t)j * d + c] : 0.0f;
-  const float b1j = unit ? b1[j] : 0.0f;
+  for (int c = 0; c < D; ++c)
+    w1p[c] = ppo_f2{in0 && c < d ? w1[(size_t)u0 * d + c] : 0.0f,
+                    in1 && c < d ? w1[(size_t)u1 * d + c] : 0.0f};
+  const ppo_f2 b1p{in0 ? b1[u0] : 0.0f, in1 ? b1[u1] : 0.0f};
 #pragma unroll
-  for (int q = 0; q < KP; ++q)
-    woj[q] = !unit ? 0.0f : (q < k ? wa[(size_t)q * hidden + j] : (q == K ? wc[j] : 0.0f));
+  for (int q = 0; q < KP; ++q) {
+    const float* col = q < k ? wa + (size_t)q * hidden : wc;
+    const bool live = q < k || q == K;
+    wop[q] = ppo_f2{live && in0 ? col[u0] : 0.0f, live && in1 ? col[u1] : 0.0f};
+  }
   float bo[KP];
 #pragma unroll
   for (int q = 0; q < KP; ++q) bo[q] = q < k ? ba[q] : (q == K ? bc[0] : 0.0f);
@@ -259,11 +270,16 @@ __global__ __launch_bounds__(HB) void k_ppo_grads(
   const double var = fmax(stats[1] / (double)n - mean * mean, 0.0);
   const float a_mean = (float)mean;
   const float a_den = (float)sqrt(var) + 1.1920928955078125e-07f;
-  float gw1[D], gwo[KP], gbias[KP], gb1 = 0.0f;
+  ppo_f2 gw1p[D], gwop[KP], gb1p = ppo_splat(0.0f);
+  float gbias[KP];
 #pragma unroll
-  for (int c = 0; c < D; ++c) gw1[c] = 0.0f;
+  for (int c = 0; c < D; ++c) gw1p[c] = ppo_splat(0.0f);
 #pragma unroll
-  for (int q = 0; q < KP; ++q) gwo[q] = gbias[q] = 0.0f;
+  for (int q = 0; q < KP; ++q) {
+    gwop[q] = ppo_splat(0.0f);
+    gbias[q] = 0.0f;
+  }
+  const float* rows = table + (size_t)wu * 128 * kTab;
   const long tiles = ((long)n + 63) / 64;
   for (long tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const long si = tile * 64 + lane;
@@ -279,24 +295,27 @@ __global__ __launch_bounds__(HB) void k_ppo_grads(
         xr[c] = c < d ? v : 0.0f;
       }
     }
-    // A: hidden activations of the 64 samples, features broadcast by v_readlane
-    float hs[64];
+    // A: hidden activations of both units for the 64 samples
+    ppo_f2 hs[64];
 #pragma unroll
     for (int s = 0; s < 64; ++s) {
-      float h = b1j;
+      ppo_f2 h = b1p;
 #pragma unroll
-      for (int c = 0; c < D; ++c) h = fmaf(w1j[c], lane_value(xr[c], s), h);
-      hs[s] = fmaxf(h, 0.0f);
-      sh[s * 65 + lane] = hs[s];
+      for (int c = 0; c < D; ++c)
+        h = __builtin_elementwise_fma(w1p[c], ppo_splat(lane_value(xr[c], s)), h);
+      hs[s] = __builtin_elementwise_max(h, ppo_splat(0.0f));
     }
-    __syncthreads();
-    // B: heads, lane = sample, this wave's 64 units
+    // B: heads, lane = sample, the wave's units one 64-unit half at a time
     float acc[KP];
 #pragma unroll
     for (int q = 0; q < KP; ++q) acc[q] = 0.0f;
-    {
-      // the unit's head weights: one wave-uniform row of the packed table
-      const float* row = table + (size_t)__builtin_amdgcn_readfirstlane(w) * 64 * kTab;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if (half) __syncthreads();  // the first half's readers are done
+#pragma unroll
+      for (int s = 0; s < 64; ++s) sh[s * 65 + lane] = half ? hs[s].y : hs[s].x;
+      __syncthreads();
+      const float* row = rows + (size_t)half * 64 * kTab;
 #pragma unroll 4
       for (int u = 0; u < 64; ++u) {
         const float h = sh[lane * 65 + u];
@@ -304,20 +323,20 @@ __global__ __launch_bounds__(HB) void k_ppo_grads(
         for (int q = 0; q < KP; ++q) acc[q] = fmaf(row[u * kTab + q], h, acc[q]);
       }
     }
-    if (w > 0) {
+    if (NW > 1 && w > 0) {
 #pragma unroll
       for (int q = 0; q < KP; ++q) red[((w - 1) * KP + q) * 64 + lane] = acc[q];
     }
-    __syncthreads();
+    if (NW > 1) __syncthreads();
+    float g[KP];
+#pragma unroll
+    for (int q = 0; q < KP; ++q) g[q] = 0.0f;
     if (w == 0) {
 #pragma unroll
-      for (int ww = 1; ww < W; ++ww) {
+      for (int ww = 1; ww < NW; ++ww) {
 #pragma unroll
         for (int q = 0; q < KP; ++q) acc[q] += red[((ww - 1) * KP + q) * 64 + lane];
       }
-      float g[KP];
-#pragma unroll
-      for (int q = 0; q < KP; ++q) g[q] = 0.0f;
       if (valid) {
         float p[K];
         float m = acc[0] + bo[0];
@@ -360,36 +379,40 @@ __global__ __launch_bounds__(HB) void k_ppo_grads(
         g[K] = dvalue[si];
       }
 #pragma unroll
-      for (int q = 0; q < KP; ++q) {
-        sz[lane * kRow + q] = g[q];
-        gbias[q] += g[q];
+      for (int q = 0; q < KP; ++q) gbias[q] += g[q];
+      if (NW > 1) {
+#pragma unroll
+        for (int q = 0; q < KP; ++q) sz[lane * kRow + q] = g[q];
       }
     }
-    __syncthreads();
-    float gq[KP];
+    if (NW > 1) {
+      __syncthreads();
 #pragma unroll
-    for (int q = 0; q < KP; ++q) gq[q] = sz[lane * kRow + q];
+      for (int q = 0; q < KP; ++q) g[q] = sz[lane * kRow + q];
+    }
     // broadcast the features again in C rather than keep phase A's 64 x D
     // uniform copies alive (they would spill the SGPR file)
 #pragma unroll
     for (int c = 0; c < D; ++c) asm volatile("" : "+v"(xr[c]));
-    // C: thread j sums its unit's gradients over the 64 samples, dL/dz of
-    // each broadcast by v_readlane
+    // C: both units' gradients over the 64 samples, dL/dz of each broadcast
 #pragma unroll
     for (int s = 0; s < 64; ++s) {
-      const float h = hs[s];
-      float dh = 0.0f;
+      const ppo_f2 h = hs[s];
+      ppo_f2 dh = ppo_splat(0.0f);
 #pragma unroll
       for (int q = 0; q < KP; ++q) {
-        const float g = lane_value(gq[q], s);
-        gwo[q] = fmaf(g, h, gwo[q]);
-        dh = fmaf(woj[q], g, dh);
+        const ppo_f2 gs = ppo_splat(lane_value(g[q], s));
+        gwop[q] = __builtin_elementwise_fma(gs, h, gwop[q]);
+        dh = __builtin_elementwise_fma(wop[q], gs, dh);
       }
-      dh = h > 0.0f ? dh : 0.0f;
-      gb1 += dh;
+      dh.x = h.x > 0.0f ? dh.x : 0.0f;
+      dh.y = h.y > 0.0f ? dh.y : 0.0f;
+      gb1p += dh;
 #pragma unroll
-      for (int c = 0; c < D; ++c) gw1[c] = fmaf(dh, lane_value(xr[c], s), gw1[c]);
+      for (int c = 0; c < D; ++c)
+        gw1p[c] = __builtin_elementwise_fma(dh, ppo_splat(lane_value(xr[c], s)), gw1p[c]);
     }
+    if (NW > 1) __syncthreads();  // sz and red are rewritten next tile
   }
   // output-bias gradients: wave 0's per-lane sums, reduced across the wave
   if (w == 0) {
@@ -403,17 +426,21 @@ __global__ __launch_bounds__(HB) void k_ppo_grads(
   float* out = partial + (size_t)blockIdx.x * ppo_grad_size(d, hidden, k);
   const int o_b1 = hidden * d, o_wa = o_b1 + hidden, o_ba = o_wa + k * hidden;
   const int o_wc = o_ba + k, o_bc = o_wc + hidden;
-  if (unit) {
 #pragma unroll
-    for (int c = 0; c < D; ++c)
-      if (c < d) out[j * d + c] = gw1[c];
-    out[o_b1 + j] = gb1;
+  for (int half = 0; half < 2; ++half) {
+    const int u = half ? u1 : u0;
+    if (u < hidden) {
 #pragma unroll
-    for (int q = 0; q < K; ++q)
-      if (q < k) out[o_wa + q * hidden + j] = gwo[q];
-    out[o_wc + j] = gwo[K];
+      for (int c = 0; c < D; ++c)
+        if (c < d) out[u * d + c] = half ? gw1p[c].y : gw1p[c].x;
+      out[o_b1 + u] = half ? gb1p.y : gb1p.x;
+#pragma unroll
+      for (int q = 0; q < K; ++q)
+        if (q < k) out[o_wa + q * hidden + u] = half ? gwop[q].y : gwop[q].x;
+      out[o_wc + u] = half ? gwop[K].y : gwop[K].x;
+    }
   }
-  if (j == 0) {
+  if (threadIdx.x == 0) {
 #pragma unroll
     for (int q = 0; q < K; ++q)
       if (q < k) out[o_ba + q] = gbias[q];
