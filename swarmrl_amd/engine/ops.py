@@ -356,12 +356,14 @@ _PPO_WS: Dict[Tuple[int, int], torch.Tensor] = {}
 
 def ppo_epoch_grad(features: torch.Tensor, actions: torch.Tensor, old_logp: torch.Tensor,
                    rewards: torch.Tensor, layers, gamma: float, lambda_: float,
-                   clip_eps: float, entropy_coef: float) -> torch.Tensor:
+                   clip_eps: float, entropy_coef: float, out: torch.Tensor = None) -> torch.Tensor:
     """
     The gradient of one PPO epoch (swarm_ppo_epoch_grad): features [T, S, d]
     fp32, actions [T, S] int64, old_logp / rewards [T, S] fp32 (all device),
     layers = (w1, b1, wa, ba, wc, bc) of the actor-critic MLP in torch
-    layouts.  Returns the flat gradient w1 | b1 | wa | ba | wc | bc (fp32).
+    layouts.  Returns the flat gradient w1 | b1 | wa | ba | wc | bc (fp32),
+    written into `out` when given.  Inputs already fp32/int64 and contiguous
+    are used in place (no copies: the launches can be graph-captured).
     """
     T, S = int(actions.shape[0]), int(actions.shape[1])
     x = features.reshape(T * S, -1).to(torch.float32).contiguous()
@@ -378,8 +380,10 @@ def ppo_epoch_grad(features: torch.Tensor, actions: torch.Tensor, old_logp: torc
     if ws is None:
         _PPO_WS.clear()
         ws = _PPO_WS[key] = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    grad = torch.empty(hidden * d_in + hidden + k * hidden + k + hidden + 1,
-                       dtype=torch.float32, device=dev)
+    size = hidden * d_in + hidden + k * hidden + k + hidden + 1
+    grad = out if out is not None else torch.empty(size, dtype=torch.float32, device=dev)
+    if grad.numel() != size or grad.dtype != torch.float32 or not grad.is_contiguous():
+        raise ValueError("out must be a contiguous fp32 tensor of the gradient's size")
     acts = actions.to(torch.int64).contiguous()
     olp = old_logp.to(torch.float32).contiguous()
     rew = rewards.to(torch.float32).contiguous()

@@ -78,6 +78,10 @@ class ProximalPolicyLoss(Loss):
             features = features.reshape(T, E * A, *features.shape[3:])
             rewards = rewards.reshape(rewards.shape[0], E * A)
         layers = self._fused_layers(network, features, actions)
+        if layers is not None:
+            features = features.reshape(features.shape[0], features.shape[1], -1).contiguous()
+            if self._graph_epochs(network, layers, features, actions, old_log_probs, rewards):
+                return
         for _ in range(self.n_epochs):
             if layers is not None:
                 grad = ops.ppo_epoch_grad(features, actions, old_log_probs, rewards, layers,
@@ -88,6 +92,68 @@ class ProximalPolicyLoss(Loss):
                 continue
             loss = self._calculate_loss(network, features, actions, rewards, old_log_probs)
             network.update_model(loss)
+
+    def _graph_epochs(self, network, layers, features, actions, old_log_probs, rewards):
+        """
+        The n_epochs fused steps (gradient kernels + the optimizer's step) as
+        one captured HIP graph, replayed per episode with the episode's data
+        copied into the graph's input buffers: the epochs are launch-bound at
+        small sizes (E = 1: ~100 us of host work per epoch).  Needs an
+        optimizer whose every param group is capturable (the default fused
+        Adam is) and state already initialised (the first episode runs
+        eagerly).  Recaptured when shapes, learning rates or the optimizer's
+        state tensors change.  SWARMRL_AMD_PPO_GRAPH=0 disables it.
+        Returns False when the eager loop should run instead.
+        """
+        opt = getattr(network, "optimizer", None)
+        if os.environ.get("SWARMRL_AMD_PPO_GRAPH", "1") == "0" or opt is None:
+            return False
+        if not all(g.get("capturable", False) for g in opt.param_groups):
+            return False
+        states = [opt.state.get(p, {}) for p in layers]
+        if not all(states) or any(p.grad is None for p in layers):
+            return False  # optimizer state not initialised yet: first episode is eager
+        sig = (id(network), id(opt), tuple(features.shape), tuple(actions.shape),
+               tuple(float(g["lr"]) for g in opt.param_groups),
+               tuple(t.data_ptr() for st in states for t in st.values()
+                     if isinstance(t, torch.Tensor)),
+               tuple(p.data_ptr() for p in layers), self.n_epochs,
+               self.value_function.gamma, self.value_function.lambda_, self.epsilon,
+               self.entropy_coefficient)
+        cache = getattr(self, "_ppo_graph", None)
+        if cache is None or cache["sig"] != sig:
+            cache = None
+            self._ppo_graph = None
+            x = features.clone()
+            act = actions.to(torch.int64).clone()
+            olp = old_log_probs.to(torch.float32).clone()
+            rew = rewards.to(torch.float32).clone()
+            grad = torch.zeros(sum(p.numel() for p in layers), dtype=torch.float32,
+                               device=features.device)
+            off = 0
+            for p in layers:
+                p.grad = grad[off:off + p.numel()].view_as(p)
+                off += p.numel()
+            args = (x, act, olp, rew, layers, self.value_function.gamma,
+                    self.value_function.lambda_, self.epsilon, self.entropy_coefficient)
+            ops.ppo_epoch_grad(*args, out=grad)  # sizes the workspace outside the capture
+            torch.cuda.synchronize(features.device)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                for _ in range(self.n_epochs):
+                    ops.ppo_epoch_grad(*args, out=grad)
+                    opt.step()
+            cache = self._ppo_graph = {"sig": sig, "graph": graph, "inputs": (x, act, olp, rew),
+                                       "grad": grad}
+        x, act, olp, rew = cache["inputs"]
+        x.copy_(features)
+        act.copy_(actions)
+        olp.copy_(old_log_probs)
+        rew.copy_(rewards)
+        cache["graph"].replay()
+        if hasattr(network, "epoch_count"):
+            network.epoch_count += self.n_epochs
+        return True
 
     def _fused_layers(self, network, features, actions):
         """The network's layers when the epoch gradient runs as the fused

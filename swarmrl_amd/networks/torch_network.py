@@ -77,10 +77,11 @@ class TorchModel:
         self.exploration_policy = exploration_policy
         self.deployment_mode = deployment_mode
         if optimizer is None:
-            # optax.adam of the reference; on the GPU one fused launch per step
+            # optax.adam of the reference; on the GPU one fused launch per step,
+            # capturable so the fused PPO epochs can run as one graph
             fused = self.device.type == "cuda"
             optimizer = lambda params: torch.optim.Adam(  # noqa: E731
-                params, lr=learning_rate, fused=fused)
+                params, lr=learning_rate, fused=fused, capturable=fused)
         self._optimizer_factory = optimizer
         self.optimizer = None if deployment_mode else optimizer(self.model.parameters())
         self.epoch_count = 0

@@ -143,3 +143,38 @@ def test_compute_loss_fused_equals_torch_path(monkeypatch):
     for a, b in zip(*steps):
         # SGD: the parameter change is lr x the summed gradients of the two epochs
         assert (a - b).norm().item() <= 1e-3 * b.norm().item() + 1e-7
+
+
+def test_graph_epochs_equal_eager(monkeypatch):
+    """Three episodes of compute_loss with the default (fused, capturable)
+    Adam: the captured-graph epochs (episode 1 eager, 2 captured + replayed,
+    3 replayed) end on bit-identical parameters to the eager loop."""
+    from swarmrl_amd.losses.proximal_policy_loss import ProximalPolicyLoss
+    from swarmrl_amd.networks.torch_network import ActorCriticMLP, TorchModel
+
+    dev = torch.device("cuda", 0)
+    T, E, A, d = 20, 1, 300, 4
+
+    def episode(seed):
+        g = torch.Generator().manual_seed(seed)
+
+        class Episode:
+            features = [f.to(dev) for f in torch.randn(T, E, A, d, generator=g)]
+            actions = [a.to(dev) for a in torch.randint(0, 4, (T, E, A), generator=g)]
+            rewards = [r.to(dev) for r in torch.randn(T, E, A, generator=g)]
+            log_probs = [lp.to(dev) for lp in -1.386 + 0.3 * torch.randn(T, E, A, generator=g)]
+        return Episode()
+
+    finals = []
+    for graph in ("1", "0"):
+        monkeypatch.setenv("SWARMRL_AMD_PPO_GRAPH", graph)
+        torch.manual_seed(0)
+        model = TorchModel(ActorCriticMLP(d, 4, 128), input_shape=(d,), device=dev)
+        loss = ProximalPolicyLoss(n_epochs=5)
+        for ep in range(3):
+            loss.compute_loss(model, episode(100 + ep))
+        assert (getattr(loss, "_ppo_graph", None) is not None) == (graph == "1")
+        assert model.epoch_count == 15
+        finals.append([p.detach().clone() for p in model.model.ppo_layers()])
+    for a, b in zip(*finals):
+        assert torch.equal(a, b)
