@@ -44,6 +44,8 @@ def parse_args():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-slices", type=int, default=100)
+    ap.add_argument("--cpu-all-core-slices", type=int, default=10,
+                    help="slices per env of the all-cores CPU baseline (0: skip it)")
     ap.add_argument("--bd-reps", type=int, default=20)
     return ap.parse_args()
 
@@ -142,60 +144,111 @@ def pmc_traffic(kernel_prefix, E, N):
     return None, None
 
 
-def cpu_baseline(args):
-    """The CPU oracle (C restatement) + torch-CPU policy on one 4096-colloid
-    env, one thread, for a bounded number of slices."""
+def _cpu_env(N, slices, seed, barrier=None):
+    """One env of the CPU baseline: the CPU oracle (C restatement) + the
+    torch-CPU policy on one thread.  Returns (agent-steps, t_start, t_end)
+    of the timed loop (after setup; `barrier` lines up concurrent workers)."""
     import torch
 
     from oracle import oracle
 
-    torch_threads = torch.get_num_threads()
     torch.set_num_threads(1)
+    L = 2.0 * math.sqrt(N / 0.1)
+    box = [L, L, L]
+    rng = np.random.default_rng(seed)
+    r = L / 2 * np.sqrt(rng.random(N))
+    th = 2 * np.pi * rng.random(N)
+    pos = np.stack([L / 2 + r * np.cos(th), L / 2 + r * np.sin(th), np.zeros(N)], 1)
+    a = 2 * np.pi * rng.random(N)
+    dirs = np.stack([np.cos(a), np.sin(a), np.zeros(N)], 1)
+    gt = 6 * np.pi * (1e-3 / 4.0453e-3)
+    gr = 8 * np.pi * (1e-3 / 4.0453e-3)
+    kT = 300.0 / 293.0
+    p = oracle.make_params(box, 1e-3, kT, kT, seed, [(1.0, gt, gr, 1.0358e-6, 4.143e-7)])
+    st = oracle.state_from_positions(pos, dirs, box)
+    sp = np.zeros(N, np.uint8)
+    st, _ = oracle.sd_run(p, st, sp, 1000)
+    agents = np.arange(N)
+    hist = oracle.history_from_state(st, agents)
+    net = torch.nn.Sequential(torch.nn.Linear(3, 128), torch.nn.ReLU(), torch.nn.Linear(128, 5))
+    ftab = np.array([0.0, 10.0, 0.0, 0.0], np.float32)
+    ttab = np.array([10.0, 0.0, -10.0, 0.0], np.float32)
+    src = np.array([L / 2, L / 2, 0.0])
+    if barrier is not None:
+        barrier.wait()
+    t0 = time.time()
+    for s in range(slices):
+        obs = oracle.vision_cone(p, st, agents, np.ones(N, np.float32), np.zeros(N, np.int32),
+                                 10.0, np.pi / 2, 3, [0])
+        with torch.no_grad():
+            logits = net(torch.as_tensor(obs.reshape(N, 3)))[:, :4]
+            u = torch.rand(logits.shape)
+            idx = torch.argmax(logits - torch.log(-torch.log(u)), dim=-1).numpy()
+            torch.log(torch.softmax(logits, -1) + 1e-8)
+        st, _, _ = oracle.bd_run(p, st, sp, ftab[idx], ttab[idx], 100, step0=100 * s)
+        dc, dp = oracle.field_distance(p, st, agents, src, np.array(box), hist)
+        np.clip(10 * ((1 - dc) - (1 - dp)), 0, None)
+    return N * slices, t0, time.time()
+
+
+_POOL_BARRIER = None
+
+
+def _pool_init(barrier):
+    global _POOL_BARRIER
+    _POOL_BARRIER = barrier
+
+
+def _pool_env(job):
+    N, slices, seed = job
+    return _cpu_env(N, slices, seed, _POOL_BARRIER)
+
+
+def cpu_baseline(args):
+    """The CPU oracle + torch-CPU policy on one 4096-colloid env, one
+    thread, for a bounded number of slices."""
+    import torch
+
+    torch_threads = torch.get_num_threads()
     try:
-        N = args.colloids
-        L = 2.0 * math.sqrt(N / 0.1)
-        box = [L, L, L]
-        rng = np.random.default_rng(42)
-        r = L / 2 * np.sqrt(rng.random(N))
-        th = 2 * np.pi * rng.random(N)
-        pos = np.stack([L / 2 + r * np.cos(th), L / 2 + r * np.sin(th), np.zeros(N)], 1)
-        a = 2 * np.pi * rng.random(N)
-        dirs = np.stack([np.cos(a), np.sin(a), np.zeros(N)], 1)
-        gt = 6 * np.pi * (1e-3 / 4.0453e-3)
-        gr = 8 * np.pi * (1e-3 / 4.0453e-3)
-        kT = 300.0 / 293.0
-        p = oracle.make_params(box, 1e-3, kT, kT, 42, [(1.0, gt, gr, 1.0358e-6, 4.143e-7)])
-        st = oracle.state_from_positions(pos, dirs, box)
-        sp = np.zeros(N, np.uint8)
-        st, _ = oracle.sd_run(p, st, sp, 1000)
-        agents = np.arange(N)
-        hist = oracle.history_from_state(st, agents)
-        net = torch.nn.Sequential(torch.nn.Linear(3, 128), torch.nn.ReLU(), torch.nn.Linear(128, 5))
-        ftab = np.array([0.0, 10.0, 0.0, 0.0], np.float32)
-        ttab = np.array([10.0, 0.0, -10.0, 0.0], np.float32)
-        src = np.array([L / 2, L / 2, 0.0])
-        t0 = time.perf_counter()
-        for s in range(args.cpu_sample_slices):
-            obs = oracle.vision_cone(p, st, agents, np.ones(N, np.float32), np.zeros(N, np.int32),
-                                     10.0, np.pi / 2, 3, [0])
-            with torch.no_grad():
-                logits = net(torch.as_tensor(obs.reshape(N, 3)))[:, :4]
-                u = torch.rand(logits.shape)
-                idx = torch.argmax(logits - torch.log(-torch.log(u)), dim=-1).numpy()
-                torch.log(torch.softmax(logits, -1) + 1e-8)
-            st, _, _ = oracle.bd_run(p, st, sp, ftab[idx], ttab[idx], 100, step0=100 * s)
-            dc, dp = oracle.field_distance(p, st, agents, src, np.array(box), hist)
-            np.clip(10 * ((1 - dc) - (1 - dp)), 0, None)
-        dt = time.perf_counter() - t0
+        steps, t0, t1 = _cpu_env(args.colloids, args.cpu_sample_slices, 42)
     finally:
         torch.set_num_threads(torch_threads)
+    dt = t1 - t0
     return {
-        "value": N * args.cpu_sample_slices / dt,
+        "value": steps / dt,
         "unit": "agent-steps/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"{args.cpu_sample_slices} slices x {N} colloids (1 env, 100 sub-steps each, "
-                  f"O(N^2) vision cone as in the reference) on 1 host core, {dt:.1f} s",
+        "sample": f"{args.cpu_sample_slices} slices x {args.colloids} colloids (1 env, 100 "
+                  f"sub-steps each, O(N^2) vision cone as in the reference) on 1 host core, "
+                  f"{dt:.1f} s",
+    }
+
+
+def cpu_baseline_all_cores(args):
+    """The same CPU baseline with one env per host core (independent envs,
+    the reference's episode parallelism), all running at once: worker
+    processes (spawned, not forked from this GPU process) line up on a
+    barrier; value = all their agent-steps / (last end - first start)."""
+    import multiprocessing as mp
+
+    cores = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    cores = max(1, min(cores, 16, os.cpu_count() or 1))
+    ctx = mp.get_context("spawn")
+    barrier = ctx.Barrier(cores)
+    jobs = [(args.colloids, args.cpu_all_core_slices, 42 + i) for i in range(cores)]
+    with ctx.Pool(cores, initializer=_pool_init, initargs=(barrier,)) as pool:
+        res = pool.map(_pool_env, jobs, chunksize=1)
+    steps = sum(r[0] for r in res)
+    dt = max(r[2] for r in res) - min(r[1] for r in res)
+    return {
+        "value": steps / dt,
+        "unit": "agent-steps/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"{cores} envs x {args.cpu_all_core_slices} slices x {args.colloids} colloids, "
+                  f"one env per core in concurrent processes, {dt:.1f} s",
     }
 
 
@@ -361,6 +414,8 @@ def main():
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args)
+        if args.cpu_all_core_slices > 0:
+            line["cpu_baseline_all_cores"] = cpu_baseline_all_cores(args)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
