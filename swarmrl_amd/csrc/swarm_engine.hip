@@ -1743,7 +1743,7 @@ int swarm_policy_mlp_sample(const float* obs, int32_t n, int32_t d_in, const flo
 
 namespace {
 struct PpoWorkspace {
-  size_t values, adv, dv, stats, spart, table, partial, total;
+  size_t values, adv, dv, spart, table, partial, total;
 };
 PpoWorkspace ppo_workspace(long n, long S, int d, int hidden, int k) {
   PpoWorkspace w;
@@ -1751,8 +1751,7 @@ PpoWorkspace ppo_workspace(long n, long S, int d, int hidden, int k) {
   w.values = 0;
   w.adv = up(w.values + (size_t)n * 4);
   w.dv = up(w.adv + (size_t)n * 4);
-  w.stats = up(w.dv + (size_t)n * 4);
-  w.spart = up(w.stats + 2 * sizeof(double));
+  w.spart = up(w.dv + (size_t)n * 4);
   w.table = up(w.spart + (size_t)((S + 255) / 256) * 2 * sizeof(double));
   // unit rows: at most 256 units x PpoTable<32, 16>::kStride floats
   w.partial = up(w.table + (size_t)swarm::kPpoMaxHidden * swarm::PpoTable<32, 16>::kStride * 4);
@@ -1790,7 +1789,6 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
   float* values = reinterpret_cast<float*>(base + ws.values);
   float* adv = reinterpret_cast<float*>(base + ws.adv);
   float* dv = reinterpret_cast<float*>(base + ws.dv);
-  double* stats = reinterpret_cast<double*>(base + ws.stats);
   float* partial = reinterpret_cast<float*>(base + ws.partial);
   float* table = reinterpret_cast<float*>(base + ws.table);
   double* spart = reinterpret_cast<double*>(base + ws.spart);
@@ -1810,9 +1808,12 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
                        s, w1, b1, d_in, hidden, wa, k, wc, 128 * NN, table);                  \
     hipLaunchKernelGGL((swarm::k_ppo_values<DD, KK>), dim3(vblocks), dim3(256), 0, s, x, n,   \
                        d_in, table, hidden, bc, values);                                      \
-    hipLaunchKernelGGL(swarm::k_ppo_gae, dim3((unsigned)gae_blocks), dim3(256), 0, s, rewards, \
-                       values, T, S, gamma, lambda, adv, dv, spart);                          \
-    hipLaunchKernelGGL(swarm::k_ppo_stats, dim3(1), dim3(256), 0, s, spart, gae_blocks, stats); \
+    if (T <= 32)                                                                              \
+      hipLaunchKernelGGL(swarm::k_ppo_gae<32>, dim3((unsigned)gae_blocks), dim3(256), 0, s,   \
+                         rewards, values, T, S, gamma, lambda, adv, dv, spart);               \
+    else                                                                                      \
+      hipLaunchKernelGGL(swarm::k_ppo_gae<0>, dim3((unsigned)gae_blocks), dim3(256), 0, s,    \
+                         rewards, values, T, S, gamma, lambda, adv, dv, spart);               \
     const void* fn = reinterpret_cast<const void*>(&swarm::k_ppo_grads<NN, DD, KK>);          \
     const int lds = swarm::ppo_grads_lds_floats<NN, KK>() * (int)sizeof(float);               \
     if (lds > 65536)                                                                          \
@@ -1820,8 +1821,8 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
     hipLaunchKernelGGL((swarm::k_ppo_grads<NN, DD, KK>), dim3((unsigned)blocks),             \
                        dim3(64 * NN),                                                         \
                        (size_t)lds, s, x, n, d_in, w1, b1, hidden, wa, ba, k, wc, bc,         \
-                       actions, old_logp, adv, dv, stats, table, clip_eps, entropy_coef,      \
-                       partial);                                                              \
+                       actions, old_logp, adv, dv, spart, gae_blocks, table, clip_eps,        \
+                       entropy_coef, partial);                                                \
   } while (0)
 #define SWARM_PPO_H(NN)                          \
   do {                                           \

@@ -11,8 +11,8 @@
 //   k_ppo_values  V = critic(relu(W1 x + b1)) of every sample
 //   k_ppo_gae     per agent column: the generalized advantages and returns
 //                 (generalized_advantage_estimate.py:42-72), the sum and sum
-//                 of squares of the advantages (fp64 block partials summed
-//                 in a fixed order by k_ppo_stats, for their
+//                 of squares of the advantages (fp64 block partials, summed
+//                 in a fixed order by each grads workgroup, for their
 //                 normalisation), and dL/dV of the critic term -- which, as
 //                 in the reference, differentiates the returns too
 //                 (R = A + V is built from the predicted values; only the
@@ -121,6 +121,10 @@ __global__ __launch_bounds__(256) void k_ppo_values(const float* __restrict__ x,
 // adv: raw advantages; dv: dL/dV = 0.5 huber'(V - R) minus the returns'
 // dependence on later values, dR_t/dV_u = gamma (1 - lambda) (gamma
 // lambda)^(u-1-t) for u > t; part[2 block + 0..1] = the block's sum A, sum A^2.
+// TM > 0: the column's T <= TM rewards and values are loaded into registers
+// up front (one memory latency instead of a dependent chain of T); the
+// arithmetic is the same in either form.
+template <int TM>
 __global__ __launch_bounds__(256) void k_ppo_gae(const float* __restrict__ rewards,
                                                  const float* __restrict__ values, int T, int S,
                                                  float gamma, float lambda,
@@ -129,13 +133,43 @@ __global__ __launch_bounds__(256) void k_ppo_gae(const float* __restrict__ rewar
   __shared__ double red[2][4];
   const int col = blockIdx.x * blockDim.x + threadIdx.x;
   double s1 = 0.0, s2 = 0.0;
-  if (col < S) {
+  const float gl = gamma * lambda, g1 = gamma * (1.0f - lambda);
+  if (col < S && TM > 0) {
+    float vr[TM > 0 ? TM : 1], rr[TM > 0 ? TM : 1];
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      vr[t] = t < T ? values[(size_t)t * S + col] : 0.0f;
+      rr[t] = t < T ? rewards[(size_t)t * S + col] : 0.0f;
+    }
+    float gae = 0.0f;
+#pragma unroll
+    for (int t = TM - 1; t >= 0; --t) {
+      if (t < T) {
+        const float v = vr[t];
+        const float delta = t != T - 1 ? rr[t] + gamma * vr[t < TM - 1 ? t + 1 : t] - v : rr[t] - v;
+        gae = delta + gl * gae;
+        adv[(size_t)t * S + col] = gae;
+        rr[t] = 0.5f * fminf(fmaxf(v - (gae + v), -1.0f), 1.0f);  // direct dL/dV
+        s1 += (double)gae;
+        s2 += (double)gae * (double)gae;
+      }
+    }
+    float carry = 0.0f;
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      if (t < T) {
+        const float g = rr[t];
+        dv[(size_t)t * S + col] = g - g1 * carry;
+        carry = gl * carry + g;
+      }
+    }
+  } else if (col < S) {
     float gae = 0.0f;
     for (int t = T - 1; t >= 0; --t) {
       const size_t i = (size_t)t * S + col;
       const float v = values[i];
       const float delta = t != T - 1 ? rewards[i] + gamma * values[i + S] - v : rewards[i] - v;
-      gae = delta + gamma * lambda * gae;
+      gae = delta + gl * gae;
       adv[i] = gae;
       // critic term 0.5 huber(V, R), R = A + V: d/dV (direct) = 0.5 clip(V - R, -1, 1)
       dv[i] = 0.5f * fminf(fmaxf(v - (gae + v), -1.0f), 1.0f);
@@ -143,7 +177,6 @@ __global__ __launch_bounds__(256) void k_ppo_gae(const float* __restrict__ rewar
       s2 += (double)gae * (double)gae;
     }
     // through the returns: dL/dV_u -= gamma (1 - lambda) sum_{t<u} g_t (gamma lambda)^(u-1-t)
-    const float gl = gamma * lambda, g1 = gamma * (1.0f - lambda);
     float carry = 0.0f;
     for (int t = 0; t < T; ++t) {
       const size_t i = (size_t)t * S + col;
@@ -173,29 +206,35 @@ __global__ __launch_bounds__(256) void k_ppo_gae(const float* __restrict__ rewar
   }
 }
 
-// stats[0..1] = the sums of the GAE blocks' partials, in a fixed order.
-__global__ __launch_bounds__(256) void k_ppo_stats(const double* __restrict__ part,
-                                                   int n_part, double* __restrict__ stats) {
-  __shared__ double red[2][256];
+// The sums of the GAE blocks' partials, in a fixed order (thread-strided
+// sums, xor-shuffle tree, waves in order): every workgroup of the grads
+// kernel computes the same two numbers.  Needs blockDim = 64 * nw, nw <= 4.
+__device__ inline void ppo_advantage_sums(const double* __restrict__ part, int n_part,
+                                          double* out) {
+  __shared__ double red[2][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   double a = 0.0, b = 0.0;
-  for (int i = threadIdx.x; i < n_part; i += 256) {
+  for (int i = threadIdx.x; i < n_part; i += blockDim.x) {
     a += part[2 * i];
     b += part[2 * i + 1];
   }
-  red[0][threadIdx.x] = a;
-  red[1][threadIdx.x] = b;
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  if (lane == 0) {
+    red[0][w] = a;
+    red[1][w] = b;
+  }
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + o];
-      red[1][threadIdx.x] += red[1][threadIdx.x + o];
-    }
-    __syncthreads();
+  a = 0.0;
+  b = 0.0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+    a += red[0][i];
+    b += red[1][i];
   }
-  if (threadIdx.x == 0) {
-    stats[0] = red[0][0];
-    stats[1] = red[1][0];
-  }
+  out[0] = a;
+  out[1] = b;
 }
 
 // Value of lane l of a wave (v_readlane: wave-uniform result).
@@ -239,7 +278,7 @@ __global__ __launch_bounds__(64 * NW) void k_ppo_grads(
     const float* __restrict__ ba, int k, const float* __restrict__ wc,
     const float* __restrict__ bc, const int64_t* __restrict__ actions,
     const float* __restrict__ old_logp, const float* __restrict__ adv,
-    const float* __restrict__ dvalue, const double* __restrict__ stats,
+    const float* __restrict__ dvalue, const double* __restrict__ gae_part, int n_part,
     const float* __restrict__ table, float clip_eps, float c_ent, float* __restrict__ partial) {
   constexpr int KP = K + 1, kTab = PpoTable<D, K>::kStride, kRow = PpoHeads<K>::kRow;
   extern __shared__ float ppo_lds[];
@@ -266,6 +305,8 @@ __global__ __launch_bounds__(64 * NW) void k_ppo_grads(
 #pragma unroll
   for (int q = 0; q < KP; ++q) bo[q] = q < k ? ba[q] : (q == K ? bc[0] : 0.0f);
   // normalised advantages (A - mean) / (std + eps): population std, fp32 eps
+  double stats[2];
+  ppo_advantage_sums(gae_part, n_part, stats);
   const double mean = stats[0] / (double)n;
   const double var = fmax(stats[1] / (double)n - mean * mean, 0.0);
   const float a_mean = (float)mean;
