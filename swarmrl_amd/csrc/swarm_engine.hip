@@ -1806,8 +1806,12 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
     hipLaunchKernelGGL((swarm::k_ppo_pack<DD, KK>),                                           \
                        dim3((unsigned)((128 * NN * Tb::kStride + 255) / 256)), dim3(256), 0, \
                        s, w1, b1, d_in, hidden, wa, k, wc, 128 * NN, table);                  \
-    hipLaunchKernelGGL((swarm::k_ppo_values<DD, KK>), dim3(vblocks), dim3(256), 0, s, x, n,   \
-                       d_in, table, hidden, bc, values);                                      \
+    if (n < (1 << 20))                                                                        \
+      hipLaunchKernelGGL((swarm::k_ppo_values_split<DD, KK>), dim3((unsigned)tiles),          \
+                         dim3(256), 0, s, x, n, d_in, table, hidden, bc, values);             \
+    else                                                                                      \
+      hipLaunchKernelGGL((swarm::k_ppo_values<DD, KK>), dim3(vblocks), dim3(256), 0, s, x, n, \
+                         d_in, table, hidden, bc, values);                                    \
     if (T <= 32)                                                                              \
       hipLaunchKernelGGL(swarm::k_ppo_gae<32>, dim3((unsigned)gae_blocks), dim3(256), 0, s,   \
                          rewards, values, T, S, gamma, lambda, adv, dv, spart);               \

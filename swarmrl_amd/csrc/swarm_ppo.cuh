@@ -117,6 +117,45 @@ __global__ __launch_bounds__(256) void k_ppo_values(const float* __restrict__ x,
   if (s + 1 < n) values[s + 1] = v.y;
 }
 
+// V at small sample counts, where the per-thread chain over all units is
+// the latency: a workgroup of 4 waves takes 64 samples (lane = sample) and
+// wave w sums units [w H/4, (w + 1) H/4) (wave-uniform rows); the four
+// partials are added in a fixed order.
+template <int D, int K>
+__global__ __launch_bounds__(256) void k_ppo_values_split(const float* __restrict__ x, int n,
+                                                          int d,
+                                                          const float* __restrict__ table,
+                                                          int hidden,
+                                                          const float* __restrict__ bc,
+                                                          float* __restrict__ values) {
+  using Tb = PpoTable<D, K>;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const long s = (long)blockIdx.x * 64 + lane;
+  const float* xp = x + (size_t)min(s, (long)n - 1) * d;
+  float xs[D];
+#pragma unroll
+  for (int c = 0; c < D; ++c) {
+    const float v = xp[min(c, d - 1)];
+    xs[c] = c < d ? v : 0.0f;
+  }
+  const int per = (hidden + 3) / 4, j0 = w * per, j1 = min(hidden, j0 + per);
+  float v = 0.0f;
+#pragma unroll 4
+  for (int j = j0; j < j1; ++j) {
+    const float* row = table + (size_t)j * Tb::kStride;
+    float h = row[Tb::kB1];
+#pragma unroll
+    for (int c = 0; c < D; ++c) h = fmaf(row[Tb::kW1 + c], xs[c], h);
+    v = fmaf(row[K], fmaxf(h, 0.0f), v);
+  }
+  red[w][lane] = v;
+  __syncthreads();
+  if (w == 0 && s < n) values[s] = bc[0] + ((red[0][lane] + red[1][lane]) + red[2][lane]) +
+                                   red[3][lane];
+}
+
 // One thread per agent column of the T x S sample grid (sample t * S + col).
 // adv: raw advantages; dv: dL/dV = 0.5 huber'(V - R) minus the returns'
 // dependence on later values, dR_t/dV_u = gamma (1 - lambda) (gamma

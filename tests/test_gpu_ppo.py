@@ -88,6 +88,7 @@ def _check(got, want):
     (5, 517, 32, 6, 256),      # widest: 32 features, 256 units, 16-action variant
     (3, 64, 2, 4, 64),
     (40, 150, 2, 4, 128),      # T > 32: the GAE kernel's uncached loop
+    (20, 53000, 4, 4, 128),    # >= 2^20 samples: the packed two-sample values kernel
 ])
 def test_fused_epoch_grad_matches_autograd(T, S, d, k, hidden):
     from swarmrl_amd.losses.proximal_policy_loss import ProximalPolicyLoss
