@@ -25,10 +25,10 @@
 //                 sums in a fixed order: deterministic), torch layouts
 //
 // The loss is a sum over samples, so its gradient is the sum of the
-// per-sample gradients; the caller's optimizer takes the step.
-// Workgroup: HB threads (HB = hidden rounded up to 64/128/256), thread j owns
-// hidden unit j (its W1 row, W2 column and their gradient accumulators live
-// in registers); tiles of samples stream through LDS.
+// per-sample gradients; the caller's optimizer takes the step.  Before them,
+// k_ppo_pack lays the parameters out as per-unit rows (the wave-uniform
+// scalar-load operands of the sample-major loops).  All fp32 arithmetic with
+// explicit fmaf; cross-sample sums in a fixed order (run-to-run identical).
 #pragma once
 
 #include <hip/hip_runtime.h>
