@@ -7,7 +7,9 @@ Plus the critic gradient of the reference's loss -- returns R = A + V stay
 differentiable (proximal_policy_loss.py:101-124, only the normalised
 advantages are stop_gradient-ed) -- checked against a float64 finite
 difference of the loss, and the closed form the device kernel k_ppo_gae
-uses (swarm_ppo.cuh) against both.
+uses (swarm_ppo.cuh) against both.  Also ExpectedReturns against
+CI/unit_tests/value_functions/test_expected_returns.py and the
+PolicyGradientLoss (policy_gradient_loss.py:47-106) against its formula.
 """
 
 import numpy as np
@@ -120,3 +122,61 @@ def test_critic_gradient_flows_through_returns():
     _, ret = GAE(gamma, lam)(r, v)
     (0.5 * F.huber_loss(v, ret, reduction="sum", delta=1.0)).backward()
     np.testing.assert_allclose(v.grad.numpy(), closed, rtol=1e-4, atol=1e-5)
+
+
+def test_expected_returns_reference_kats():
+    """CI/unit_tests/value_functions/test_expected_returns.py:16-53."""
+    from swarmrl_amd.value_functions.expected_returns import ExpectedReturns
+
+    got = ExpectedReturns(gamma=1.0, standardize=False)(
+        torch.tensor([[1.0, 4], [2, 5], [3, 6]]))
+    np.testing.assert_array_equal(got.numpy(), [[6, 15], [5, 11], [3, 6]])
+    rewards = torch.tensor([[1.0, 4], [2, 5], [3, 6], [4, 7], [5, 8], [6, 9], [7, 10]])
+    got = ExpectedReturns(gamma=0.79, standardize=True)(rewards).numpy()
+    np.testing.assert_array_almost_equal(got.mean(0), [0.0, 0.0], decimal=6)
+    np.testing.assert_array_almost_equal(got.std(0), [1.0, 1.0], decimal=6)
+
+
+def test_policy_gradient_loss_matches_hand_computation():
+    """PolicyGradientLoss._calculate_loss (policy_gradient_loss.py:47-106) on
+    a small random network against the formula evaluated in float64 numpy:
+    -sum(log(p_a + 1e-8) (R - V)) + sum(huber(V, R)), R the standardised
+    discounted returns (gamma 0.99); the critic gradient flows through V only."""
+    from swarmrl_amd.losses.policy_gradient_loss import PolicyGradientLoss
+    from swarmrl_amd.networks.torch_network import ActorCriticMLP
+
+    torch.manual_seed(0)
+    net = ActorCriticMLP(3, 4, 16)
+    T, P = 5, 7
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(T, P, 3, generator=g)
+    actions = torch.randint(0, 4, (T, P), generator=g)
+    rewards = torch.randn(T, P, generator=g)
+
+    class Wrap:
+        def __call__(self, features, obs_ndim=1):
+            return net(features)
+
+    loss = PolicyGradientLoss()._calculate_loss(Wrap(), x, actions, rewards)
+    with torch.no_grad():
+        logits, v = net(x)
+    logits, v = logits.double().numpy(), v.double().numpy()[..., 0]
+    p = np.exp(logits - logits.max(-1, keepdims=True))
+    p /= p.sum(-1, keepdims=True)
+    pa = np.take_along_axis(p, actions.numpy()[..., None], -1)[..., 0]
+    r = rewards.double().numpy()
+    ret = np.zeros_like(r)
+    acc = np.zeros(P)
+    for t in reversed(range(T)):
+        acc = r[t] + 0.99 * acc
+        ret[t] = acc
+    ret = (ret - ret.mean(0)) / (ret.std(0) + np.finfo(np.float32).eps)
+    d = v - ret
+    hub = np.where(np.abs(d) <= 1.0, 0.5 * d * d, np.abs(d) - 0.5)
+    want = -(np.log(pa + 1e-8) * (ret - v)).sum() + hub.sum()
+    np.testing.assert_allclose(float(loss.detach()), want, rtol=1e-5)
+    # critic gradient through V only: d/dV = clip(V - R, -1, 1) (returns fixed)
+    net.zero_grad()
+    vv = torch.tensor(v, requires_grad=True)
+    F.huber_loss(vv, torch.tensor(ret), reduction="sum", delta=1.0).backward()
+    np.testing.assert_allclose(vv.grad.numpy(), np.clip(d, -1, 1), rtol=1e-12)
