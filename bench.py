@@ -287,8 +287,9 @@ def measure(args, E, rank, world, device):
         agent.reset_trajectory()
         episode_graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(episode_graph, pool=slice_graph.pool()):
-            for _ in range(T):
-                one_slice()
+            # one episode as the trainers run it (episodic_trainer.py:35 ->
+            # engine.integrate(episode_length, force_fn))
+            eng.integrate(T, ff)
     else:
         agent.reset_trajectory()
 

@@ -439,3 +439,32 @@ def test_add_walls_2d_engine(tmp_path):
     assert np.all(poss[:, :2] < 60)
     assert np.all(poss[:, :2] > 40)
     assert runner.wall_violations() == 0
+
+
+def test_early_build_fork_equals_serial():
+    """The bench workload (vision cones, actor-critic sampling, GradientSensing
+    reward) over 4 slices of one integrate call: the next slice's build forked
+    right after the run (ahead of the reward, SwarmEngine._early_prebuild)
+    gives the same positions, actions and rewards as the serial slice."""
+    import argparse
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    dev = torch.device("cuda", 0)
+    out = []
+    for overlap in (True, False):
+        ns = argparse.Namespace(colloids=1024, envs_per_gpu=1)
+        eng, ff, agent = bench.build_workload(ns, 7, dev)
+        eng.overlap_build = overlap
+        eng.integrate(4, ff)
+        st = eng.get_raw_state()
+        tr = agent.trajectory
+        out.append((st, torch.stack([torch.as_tensor(a) for a in tr.actions]).cpu(),
+                    torch.stack([torch.as_tensor(r) for r in tr.rewards]).cpu()))
+    (s0, a0, r0), (s1, a1, r1) = out
+    for k in ("q", "img", "ang"):
+        assert np.array_equal(s0[k], s1[k])
+    assert torch.equal(a0, a1) and torch.equal(r0, r1)

@@ -35,8 +35,7 @@ if graph:
     agent.reset_trajectory()
     episode_graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(episode_graph):
-        for _ in range(T):
-            eng.integrate(1, ff)
+        eng.integrate(T, ff)
     traj = agent.trajectory  # the graph's output tensors, rewritten by every replay
 else:
     agent.reset_trajectory()
