@@ -899,7 +899,7 @@ class SwarmEngine(Engine):
 
             if self.step_idx == self.params.steps_per_slice * self.slice_idx:
                 self.slice_idx += 1
-                if device_path and self.overlap_build and self._prebuild_pending is None:
+                if device_path and self.overlap_build:
                     self._prebuild(min(
                         self.params.steps_per_write_interval * self.write_idx - self.step_idx,
                         self.params.steps_per_slice * self.slice_idx - self.step_idx))
@@ -912,43 +912,9 @@ class SwarmEngine(Engine):
             steps_to_next = min(steps_to_next_write, steps_to_next_slice)
 
             self._run(steps_to_next)
-            if device_path and self.overlap_build:
-                self._early_prebuild(steps_to_next, old_slice_idx + n_slices)
             if force_model is not None:
                 force_model.calc_reward(self.swarm_view() if device_path else self.colloids)
             self.step_idx += steps_to_next
-        self._join_prebuild()
-
-    def _early_prebuild(self, steps_run: int, end_slice: int):
-        """
-        Latency-bound engines: fork the next slice's build right after the
-        run, ahead of the reward kernels, so the side branch (build) runs
-        beside reward + observables + policy instead of beside observables +
-        policy only (the reward is off the slice's critical path).  The build
-        is a function of the positions alone, which nothing changes until the
-        next run; _run joins it.  Only when the next loop iteration starts a
-        slice of this integrate call (a kill switch ending the loop early
-        leaves a valid build, joined by _join_prebuild).
-        """
-        if self.n_envs * self.n_particles > 32768:
-            return  # throughput-bound: the build is launched in _run (see _prebuild)
-        sps, spw = self.params.steps_per_slice, self.params.steps_per_write_interval
-        step = self.step_idx + steps_run
-        if step != sps * self.slice_idx or step >= sps * end_slice:
-            return
-        write_idx = self.write_idx + (1 if step == spw * self.write_idx else 0)
-        self._prebuild(min(spw * write_idx - step, sps * (self.slice_idx + 1) - step))
-
-    def _join_prebuild(self):
-        """Order a pending (unconsumed) prebuild before later main-stream work."""
-        if self._prebuild_pending is None:
-            return
-        side, fork, _ = self._prebuild_pending
-        if fork is not None:  # deferred build never launched: nothing to join
-            self._prebuild_pending = None
-            return
-        torch.cuda.current_stream().wait_stream(side)
-        self._prebuild_pending = None
 
     def finalize(self):
         """Write the last trajectory chunk (espresso.py:1310-1318)."""

@@ -441,11 +441,11 @@ def test_add_walls_2d_engine(tmp_path):
     assert runner.wall_violations() == 0
 
 
-def test_early_build_fork_equals_serial():
+def test_bench_workload_overlap_equals_serial():
     """The bench workload (vision cones, actor-critic sampling, GradientSensing
-    reward) over 4 slices of one integrate call: the next slice's build forked
-    right after the run (ahead of the reward, SwarmEngine._early_prebuild)
-    gives the same positions, actions and rewards as the serial slice."""
+    reward) over 4 slices of one integrate call: the build on a side stream
+    beside the observables and policy gives the same positions, actions and
+    rewards as the serial single-stream slice."""
     import argparse
     import os
     import sys
