@@ -228,12 +228,49 @@ __global__ __launch_bounds__(1024) void k_vision_grid(DevState st, swarm_vision_
   if (e == 0)
     for (int a = tid; a < n_agents; a += T) vs.agent_row[agents[a]] = a;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
+  int32_t* so = start + (size_t)e * (ncell + 1);
+  constexpr int kPer = 8;  // colloids per thread kept in registers (N <= 8 T)
+  if (N <= kPer * T) {
+    // every colloid's record fields are loaded once, up front, so their
+    // latency overlaps the count and the scan
+    uint4 r0[kPer], r1[kPer];
+    int cell[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int i = tid + k * T;
+      if (i < N) {
+        const size_t g = base + i;
+        const uint32_t qx = st.q[g], qy = st.q[M + g];
+        const int tj = types[i];
+        int ti = -1;
+        for (int tt = 0; tt < vp.n_types; ++tt)
+          if (vp.detected_types[tt] == tj) ti = tt;
+        r0[k] = make_uint4(qx, qy, (uint32_t)st.img[g], (uint32_t)st.img[M + g]);
+        r1[k] = make_uint4(__float_as_uint(radii[i]), (uint32_t)i, (uint32_t)ti, 0u);
+        cell[k] = cell_index(qx, qy, lx, ly);
+        atomicAdd(&cnt[cell[k]], 1);
+      }
+    }
+    __syncthreads();
+    block_exclusive_scan(cnt, ncell, wave_sums);
+    __syncthreads();
+    for (int c = tid; c <= ncell; c += T) so[c] = cnt[c];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      if (tid + k * T < N) {
+        const size_t pos = base + atomicAdd(&cnt[cell[k]], 1);
+        vs.rec[2 * pos] = r0[k];
+        vs.rec[2 * pos + 1] = r1[k];
+      }
+    }
+    return;
+  }
   for (int i = tid; i < N; i += T)
     atomicAdd(&cnt[cell_index(st.q[base + i], st.q[M + base + i], lx, ly)], 1);
   __syncthreads();
   block_exclusive_scan(cnt, ncell, wave_sums);
   __syncthreads();
-  int32_t* so = start + (size_t)e * (ncell + 1);
   for (int c = tid; c <= ncell; c += T) so[c] = cnt[c];
   __syncthreads();
   for (int i = tid; i < N; i += T) {
