@@ -108,7 +108,8 @@ def test_agent_uses_fused_path_under_graph_capture(tmp_path):
 
 
 @pytest.mark.parametrize("n,d_in,hidden,k", [(4096, 3, 128, 4), (1000, 9, 64, 6),
-                                             (40_000, 3, 128, 4), (100_000, 16, 256, 16)])
+                                             (40_000, 3, 128, 4), (100_000, 16, 256, 16),
+                                             (100_001, 3, 128, 4)])
 def test_fused_mlp_policy_matches_torch_and_sampler(n, d_in, hidden, k):
     """swarm_policy_mlp_sample: logits within fp32 tolerance of the torch
     module (rtol 1e-5, atol 1e-5: summation order differs from the GEMM), and
