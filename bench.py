@@ -47,6 +47,8 @@ def parse_args():
     ap.add_argument("--cpu-all-core-slices", type=int, default=10,
                     help="slices per env of the all-cores CPU baseline (0: skip it)")
     ap.add_argument("--bd-reps", type=int, default=20)
+    ap.add_argument("--stub", action="store_true",
+                    help="CPU plumbing test: no GPU, gloo, synthetic trajectories")
     return ap.parse_args()
 
 
@@ -293,6 +295,8 @@ def measure(args, E, rank, world, device):
     else:
         agent.reset_trajectory()
 
+    gstats = []
+
     def run(n_steps, timed):
         k = 0
         while k < n_steps:
@@ -300,7 +304,10 @@ def measure(args, E, rank, world, device):
                 episode_graph.replay()
                 k += T
                 if timed and world > 1:
-                    gather_trajectory(agent.trajectory)
+                    st = {}
+                    gather_trajectory(agent.trajectory, stats=st if len(gstats) < 4 else None)
+                    if st:
+                        gstats.append(st)
             elif slice_graph is not None:
                 slice_graph.replay()
                 k += 1
@@ -322,10 +329,7 @@ def measure(args, E, rank, world, device):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    timing = _finish_timing(args, E, world, device, elapsed, gstats, None, None)
 
     kernel_ms, kernel = time_run_kernel(eng, args.bd_reps)
     N = args.colloids
@@ -333,10 +337,8 @@ def measure(args, E, rank, world, device):
     bytes_per_launch = BYTES_PER_PARTICLE_SUBSTEP * N * sub * E
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic("k_cluster_run", E, N)
-    out = {
-        "E": E,
-        "value": N * E * world * args.steps / elapsed,
-        "ms_per_step": elapsed / args.steps * 1e3,
+    out = dict(timing)
+    out.update({
         "hip_graph": episode_graph is not None,
         "roofline": {
             "bound": "hbm",
@@ -351,7 +353,7 @@ def measure(args, E, rank, world, device):
             "algorithmic_bytes": f"{BYTES_PER_PARTICLE_SUBSTEP} B per colloid-sub-step "
                                  f"(SURVEY 8d) x {N} colloids x {sub} sub-steps x {E} env(s)",
         },
-    }
+    })
     if traffic_src:
         out["roofline"]["traffic_source"] = traffic_src
     del eng, ff, agent, slice_graph, episode_graph
@@ -359,24 +361,133 @@ def measure(args, E, rank, world, device):
     return out
 
 
-def main():
-    args = parse_args()
+def launch_ranks(args) -> int:
+    """`--gpus N` (N > 1) without a launcher: start N rank processes (one per
+    GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run
+    would) before anything touches the GPU, wait for all, return the worst
+    exit code.  Rank 0 prints the JSON line.  The reference's fan-out this
+    replaces is training_routines/ensemble_submit.py:76-85."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
+def stub_measure(args, E, rank, world, device):
+    """--stub: the launch / rendezvous / gather / max-over-ranks plumbing
+    without a GPU (CPU tests): a synthetic trajectory of the bench's shapes
+    (E envs x colloids agents, episode_length slices) is all-gathered once
+    per episode, the 'rollout' is a host sleep."""
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    from swarmrl_amd.rollout import gather_trajectory
+    from swarmrl_amd.utils.colloid_utils import TrajectoryInformation
+
+    T, A = args.episode_length, args.colloids
+    traj = TrajectoryInformation(particle_type=0)
+    for t in range(T):
+        traj.features.append(torch.full((E, A, 3), float(rank), device=device))
+        traj.actions.append(torch.full((E, A), rank, dtype=torch.int64, device=device))
+        traj.log_probs.append(torch.zeros((E, A), device=device))
+        traj.rewards.append(torch.zeros((E, A), device=device))
+    gstats = []
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(0, args.steps, T):
+        time.sleep(1e-4 * min(T, args.steps - k))
+        st = {}
+        out = gather_trajectory(traj, stats=st)
+        if st:
+            gstats.append(st)
+        assert out["actions"].shape[1] == world * E
+        assert all(int(out["actions"][0, r * E, 0]) == r for r in range(world))
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    return _finish_timing(args, E, world, device, elapsed, gstats, None, None, stub=True)
+
+
+def _finish_timing(args, E, world, device, elapsed, gstats, kernel_ms, kernel, stub=False):
+    """Per-rank values, max-over-ranks time, gather statistics."""
+    import torch
+    import torch.distributed as dist
+
+    from swarmrl_amd.rollout import gather_ms
+
+    N = args.colloids
+    mine = N * E * args.steps / elapsed
+    per_rank = [mine]
+    if world > 1:
+        t = torch.tensor([elapsed, mine], dtype=torch.float64, device=device)
+        allv = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allv, t)
+        elapsed = max(float(v[0]) for v in allv)
+        per_rank = [float(v[1]) for v in allv]
+    out = {
+        "E": E,
+        "value": N * E * world * args.steps / elapsed,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "per_rank": per_rank,
+    }
+    if gstats:
+        out["gather"] = {
+            "collective": "all_gather_into_tensor (one packed buffer per episode)",
+            "bytes_per_rank": gstats[-1].get("bytes"),
+            "ms_mean": sum(gather_ms(g) for g in gstats) / len(gstats),
+            "per_run": len(gstats),
+        }
+    return out
+
+
+def main():
+    args = parse_args()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    import torch
+    import torch.distributed as dist
 
-    E = args.envs_per_gpu
-    head = measure(args, E, rank, world, device)
-    batched = None
-    if args.batched_envs > 0 and args.batched_envs != E:
-        batched = measure(args, args.batched_envs, rank, world, device)
+    if args.stub:
+        if world > 1:
+            dist.init_process_group("gloo", init_method="env://")
+        device = torch.device("cpu")
+        head = stub_measure(args, args.envs_per_gpu, rank, world, device)
+        head["roofline"] = None
+        head["hip_graph"] = False
+        batched = None
+    else:
+        if world > 1:
+            dist.init_process_group("nccl", init_method="env://")
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+        E = args.envs_per_gpu
+        head = measure(args, E, rank, world, device)
+        batched = None
+        if args.batched_envs > 0 and args.batched_envs != E:
+            batched = measure(args, args.batched_envs, rank, world, device)
+    if world > 1 and dist.get_world_size() != args.gpus:
+        print("bench.py: process group size differs from --gpus", file=sys.stderr)
+        sys.exit(2)
     N = args.colloids
     line = {
         "metric": METRIC,
@@ -394,26 +505,36 @@ def main():
         "config": {
             "workload": "4096-colloid WCA+vision-cone rollout",
             "colloids_per_env": N,
-            "envs_per_gpu": E,
+            "envs_per_gpu": head["E"],
             "substeps_per_slice": 100,
             "episode_length": args.episode_length,
             "policy": "MLP 3-128-(4+1), Gumbel sampling",
             "task": "GradientSensing (find centre)",
             "parallelism": f"episode-parallel, {world} process(es), one env per GPU, "
-                           f"RCCL all-gather per episode",
+                           f"one packed all-gather of the trajectory per episode",
             "hip_graph": head["hip_graph"],
         },
+        "world": world,
+        "per_rank_value": head["per_rank"],
         "roofline": head["roofline"],
     }
+    if "gather" in head:
+        line["gather"] = head["gather"]
+    for k in ("roofline_valu", "c5"):
+        if k in head:
+            line[k] = head[k]
     if batched is not None:
         line["batched"] = {
             "envs_per_gpu": batched["E"],
             "value": batched["value"],
             "unit": "agent-steps/s",
             "ms_per_step": batched["ms_per_step"],
+            "per_rank_value": batched["per_rank"],
             "roofline": batched["roofline"],
         }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if "gather" in batched:
+            line["batched"]["gather"] = batched["gather"]
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.stub:
         line["cpu_baseline"] = cpu_baseline(args)
         if args.cpu_all_core_slices > 0:
             line["cpu_baseline_all_cores"] = cpu_baseline_all_cores(args)

@@ -20,7 +20,6 @@ from swarmrl_amd import (  # noqa: F401
     observables,
     sampling_strategies,
     tasks,
-    trainers,
     units,
     utils,
     value_functions,

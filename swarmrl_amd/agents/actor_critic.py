@@ -41,9 +41,6 @@ class ActorCriticAgent(Agent):
         self.intrinsic_reward = intrinsic_reward
         self.trajectory = TrajectoryInformation(particle_type=self.particle_type)
         self._tables = None
-        # optional device ring buffers (swarmrl_amd.rollout.EpisodeRecorder):
-        # graph-capturable recording of the batched path
-        self.recorder = None
 
     def __name__(self) -> str:
         return "ActorCriticAgent"
@@ -132,8 +129,6 @@ class ActorCriticAgent(Agent):
             if f_act is None:
                 f_act, t_act = ftab[idx], ttab[idx]
             chosen = DeviceActions(f_act, t_act, new_dir, mask)
-            if self.recorder is not None:
-                self.recorder.record_action(state_description, idx, logp)
             if self.train:
                 self.trajectory.features.append(state_description)
                 self.trajectory.actions.append(idx)
@@ -155,8 +150,6 @@ class ActorCriticAgent(Agent):
             rewards = rewards + self.intrinsic_reward.compute_reward(episode_data=self.trajectory)
         if not (isinstance(external_reward, (int, float)) and external_reward == 0):
             rewards = rewards + external_reward
-        if self.recorder is not None and is_view(colloids):
-            self.recorder.record_reward(rewards)
         if self.train:
             self.trajectory.rewards.append(rewards)
         self.kill_switch = self.task.kill_switch

@@ -22,6 +22,7 @@ class RNDReward(IntrinsicReward):
         self.iterations = 0
         self.metric_results = None
         in_dim = int(np.prod(rnd_config.input_shape))
+        self.in_dim = in_dim
         dev = rnd_config.device or (torch.device("cuda", torch.cuda.current_device())
                                     if torch.cuda.is_available() else torch.device("cpu"))
         self.device = torch.device(dev)
@@ -33,20 +34,27 @@ class RNDReward(IntrinsicReward):
                                           lr=rnd_config.learning_rate)
 
     @staticmethod
-    def _reshape_data(x) -> torch.Tensor:
-        """Flatten time and ensemble axes: (T, N, *obs) -> (T * N, prod(obs))."""
+    def _stack(x) -> torch.Tensor:
         if isinstance(x, (list, tuple)):
             x = torch.stack([torch.as_tensor(np.asarray(v)) if not isinstance(v, torch.Tensor)
                              else v for v in x])
-        x = torch.as_tensor(x)
+        return torch.as_tensor(x)
+
+    @staticmethod
+    def _reshape_data(x) -> torch.Tensor:
+        """Flatten time and ensemble axes: (T, N, *obs) -> (T * N, prod(obs))
+        (random_network_distillation.py:58-77)."""
+        x = RNDReward._stack(x)
         return x.reshape(x.shape[0] * x.shape[1], -1).to(torch.float32)
 
     def _features(self, episode_data, last_only: bool):
+        """Every leading axis (time, and on the device path env and agent)
+        is a sample axis; the observation is the trailing prod(input_shape)."""
         feats = episode_data.features
         if last_only:
             feats = feats[-1:]
-        x = self._reshape_data(feats)
-        return x.to(self.device)
+        x = self._stack(feats)
+        return x.reshape(-1, self.in_dim).to(torch.float32).to(self.device)
 
     @torch.no_grad()
     def compute_distance(self, points: torch.Tensor) -> torch.Tensor:
@@ -73,9 +81,16 @@ class RNDReward(IntrinsicReward):
         self.iterations += 1
 
     def compute_reward(self, episode_data):
-        """Mean clipped RND distance of the latest observations (scalar tensor)."""
+        """Mean clipped RND distance of the latest observations
+        (random_network_distillation.py:126-143): a scalar tensor, or on the
+        device path (features [E, A, *obs]) one mean per env, [E, 1], which
+        broadcasts over the env's agents."""
+        last = episode_data.features[-1]
         points = self._features(episode_data, last_only=True)
         r = self.compute_distance(points)
+        per_env = isinstance(last, torch.Tensor) and last.dim() == len(self.input_shape) + 2
+        if per_env:
+            r = self.metric_results.reshape(last.shape[0], -1).mean(dim=1, keepdim=True)
         if self.clip_rewards is not None:
             r = torch.clamp(r, *self.clip_rewards)
         return r

@@ -1,4 +1,3 @@
-from swarmrl_amd.utils import utils
 from swarmrl_amd.utils.colloid_utils import TrajectoryInformation
 
-__all__ = ["utils", "TrajectoryInformation"]
+__all__ = ["TrajectoryInformation"]

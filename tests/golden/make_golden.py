@@ -67,6 +67,13 @@ def vision():
     box = [L, L, L]
     pos = np.zeros((n, 3))
     pos[:, :2] = rng.random((n, 2)) * L
+    # mixed image counters (the reference compares UNWRAPPED positions with
+    # no minimum image, subdivided_vision_cones.py:116-121): half of the
+    # colloids move to a neighbouring image, so folded-box neighbours in
+    # different images are invisible and colloids across a box edge in
+    # adjacent images are seen
+    moved = rng.random(n) < 0.5
+    pos[moved, :2] += rng.integers(-1, 2, (int(moved.sum()), 2)) * L
     a = rng.random(n) * 2 * np.pi
     dirs = np.stack([np.cos(a), np.sin(a), np.zeros(n)], 1)
     types = rng.integers(0, 3, n).astype(np.int32)
