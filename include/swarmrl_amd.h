@@ -238,6 +238,10 @@ int swarm_engine_profile(swarm_engine_t *e, int32_t enable, double *run_ms,
 /* Diagnostics: 32 shader-clock stamps of the last cluster build's phases
  * (env 0), filled only by builds compiled with -DSWARM_PHASE_TIMING. */
 int swarm_engine_debug_phases(swarm_engine_t *e, uint64_t *out32);
+/* Diagnostics (SWARM_PHASE_TIMING builds fill it; zeros otherwise): per run
+ * wave w of the last cluster window, out[4w..4w+3] = realtime stamps (100 MHz)
+ * at the wave's entry and end, its pair passes and pair count. */
+int swarm_engine_debug_wave_stamps(swarm_engine_t *e, uint64_t *out, int32_t n_words);
 
 /* Total number of BD sub-steps integrated so far (the noise counter). */
 int64_t swarm_engine_step_count(const swarm_engine_t *e);

@@ -744,6 +744,7 @@ struct swarm_engine {
   // next_table_ready: the last window did that (the table's first step and
   // length are checked on the device, this flag only skips k_noise).
   bool wide_run = false;
+  int run_wpb = 4;  // run waves per block (= per CU) of k_cluster_run_wide
   // k_build_env: the whole build in one LDS-resident workgroup per env
   bool env_build = false;
   int noise_blocks = 0;
@@ -896,17 +897,18 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
     HIP_TRY(hipEventRecord(ev0, e->stream));
   }
   if (e->wide_run) {
-    // dynamic LDS beyond half a CU's keeps one block (4 run waves) per CU
-    const dim3 grid((unsigned)(e->noise_blocks + (waves + 3) / 4));
+    // dynamic LDS beyond half a CU's keeps one block (run_wpb run waves) per CU
+    const int R = e->run_wpb;
+    const dim3 grid((unsigned)(e->noise_blocks + (waves + R - 1) / R));
     const size_t lds = 96 * 1024;
     if (multi)
       hipLaunchKernelGGL(swarm::k_cluster_run_wide<true>, grid, dim3(1024), lds, e->stream,
                          e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise,
-                         e->noise_blocks);
+                         e->noise_blocks, R);
     else
       hipLaunchKernelGGL(swarm::k_cluster_run_wide<false>, grid, dim3(1024), lds, e->stream,
                          e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise,
-                         e->noise_blocks);
+                         e->noise_blocks, R);
     e->next_table_ready = e->noise_blocks > 0;
   } else {
     const dim3 run_grid((unsigned)((waves + 3) / 4)), run_block(256);
@@ -1156,7 +1158,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->sc.gnpairs, (size_t)n_envs);
   if (e->big_build) rc = rc ? rc : dev_alloc(e, &e->sc.gclus, 3 * M);
   rc = rc ? rc : dev_alloc(e, &e->sc.wave_npairs, (size_t)n_envs * (S / 64));
-  rc = rc ? rc : dev_alloc(e, &e->sc.phase, 32);
+  rc = rc ? rc : dev_alloc(e, &e->sc.phase, 32 + 4 * (size_t)n_envs * (S / 64));
   rc = rc ? rc : dev_alloc(e, &e->sc.disp, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.env_waves, (size_t)n_envs);
   rc = rc ? rc : dev_alloc(e, &e->sc.fallback, (size_t)n_envs);
@@ -1200,6 +1202,15 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     if (ow && ow[0] == '0') e->wide_run = false, e->noise_blocks = 0;
     const char* on = std::getenv("SWARMRL_AMD_WIDE_NOISE");
     if (on && on[0] == '0') e->noise_blocks = 0;
+    // run waves per CU: a wave alone on its CU does not share the CU's
+    // texture path with other waves' scattered noise-table gathers; four per
+    // CU once the run's waves (~1 per 46 particles) would not fit one per CU
+    {
+      const long est = (long)M / 46 + 1;
+      e->run_wpb = est + e->noise_blocks <= 224 ? 1 : (est / 2 + e->noise_blocks <= 224 ? 2 : 4);
+      const char* orw = std::getenv("SWARMRL_AMD_RUN_WAVES_PER_CU");
+      if (orw && (orw[0] == '1' || orw[0] == '2' || orw[0] == '4')) e->run_wpb = orw[0] - '0';
+    }
 
   }
   set_lds_attributes();
@@ -1424,6 +1435,16 @@ int swarm_engine_debug_phases(swarm_engine_t* e, uint64_t* out32) {
 #ifdef SWARM_PHASE_TIMING
   HIP_TRY(hipMemcpyFromSymbol(out32 + 24, HIP_SYMBOL(swarm::g_global_phase), 3 * sizeof(uint64_t)));
 #endif
+  return SWARM_OK;
+}
+
+int swarm_engine_debug_wave_stamps(swarm_engine_t* e, uint64_t* out, int32_t n_words) {
+  if (!e || !out) return fail(SWARM_EINVAL, "null argument");
+  const size_t cap = 4 * (size_t)e->n_envs * (e->sc.S / 64);
+  if (n_words < 0 || (size_t)n_words > cap) return fail(SWARM_EINVAL, "n_words out of range");
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipMemcpy(out, e->sc.phase + 32, (size_t)n_words * sizeof(uint64_t),
+                    hipMemcpyDeviceToHost));
   return SWARM_OK;
 }
 

@@ -1453,6 +1453,9 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
   const int w = gw - e * sc.wmax;
   if (e >= n_envs) return;
   if (sc.fallback[e] != 0 || w >= sc.env_waves[e]) return;
+#ifdef SWARM_PHASE_TIMING
+  const uint64_t t_wave0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int slot = w * 64 + lane;
@@ -1526,7 +1529,11 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     if (stamp) t0s = t1s = __builtin_amdgcn_s_memtime();
 #endif
     float gt[3] = {gn[0], gn[1], gn[2]};
+#ifdef SWARM_ABL_NOTABLE  // timing ablation only (tools/_variants): no table loads
+    if (false) {
+#else
     if (kTable && !kLast) {  // the next sub-step's normals, one sub-step ahead
+#endif
       const float* nx = tcol + (size_t)(s + 1) * 3 * ts;
       gn[0] = nx[0];
       gn[1] = nx[ts];
@@ -1567,7 +1574,12 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     if (pc.noisy) dth = dth + pc.sig_r * gt[2];
     const uint32_t an_next = p.an + (uint32_t)f2i32(dth * kAngInvScale);
     float dnext[2];
+#ifdef SWARM_ABL_NOSINCOS  // timing ablation only: the director stays fixed
+    dnext[0] = dir[0];
+    dnext[1] = dir[1];
+#else
     if (!kLast) sincos_turn(an_next, &dnext[0], &dnext[1]);
+#endif
     __builtin_amdgcn_sched_barrier(0);
     __asm__ volatile("" ::: "memory");  // keep the read-back after the director
     if (kPass > 0) {
@@ -1613,7 +1625,11 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     for (int s = 0; s < n_steps - 1; ++s) substep(s, std::false_type{}, pass_t);
     substep(n_steps - 1, std::true_type{}, pass_t);  // velocities of the last sub-step
   };
+#ifdef SWARM_ABL_NOPAIR  // timing ablation only: no pair section
+  if (true)
+#else
   if (npass == 0)
+#endif
     run_steps(std::integral_constant<int, 0>{});
   else if (npass == 1)
     run_steps(std::integral_constant<int, 1>{});
@@ -1626,6 +1642,13 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     sc.phase[18] = t_bd;
     sc.phase[19] = (uint64_t)n_steps;
     sc.phase[20] = (uint64_t)npass;
+  }
+  if (lane == 0) {  // per-wave realtime stamps (100 MHz): entry, end, passes, pairs
+    uint64_t* ws = sc.phase + 32 + 4 * (size_t)gw;
+    ws[0] = t_wave0;
+    ws[1] = __builtin_amdgcn_s_memrealtime();
+    ws[2] = (uint64_t)npass;
+    ws[3] = (uint64_t)np;
   }
 #endif
   if (active) {
@@ -1698,13 +1721,15 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
 // block per CU.  Blocks [0, nnb) fill the NEXT window's noise table
 // (kMaxWindow sub-steps from this window's end) on CUs the run leaves idle,
 // so no noise kernel sits between the policy and the run; the other blocks
-// run with waves 0-3 only, one wave per SIMD.
+// run with waves [0, run_wpb) only: one run wave per CU at E = 1 (its
+// scattered noise-table gathers then have the CU's texture path to themselves),
+// up to one per SIMD for more envs.
 template <bool kMulti>
 __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __restrict__ d,
                                                            DevState st, Scratch sc, int n_envs,
                                                            int n_steps, uint64_t* __restrict__ ctl,
                                                            float* __restrict__ tables,
-                                                           int n_noise_blocks) {
+                                                           int n_noise_blocks, int run_wpb) {
   __shared__ PairTables pt;
   __shared__ uint2 lpos[4][64];
   __shared__ unsigned long long lacc[4][2][64];
@@ -1728,8 +1753,8 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
     return;
   }
   const int lane = tid & 63, wv = tid >> 6;
-  if (wv >= 4) return;
-  const int gw = (b - n_noise_blocks) * 4 + wv;
+  if (wv >= run_wpb) return;
+  const int gw = (b - n_noise_blocks) * run_wpb + wv;
   const bool table_ok = ctl[kCtlTStep + par] == step0 && (uint64_t)n_steps <= ctl[kCtlTLen + par];
   run_wave_dispatch<kMulti>(d, st, sc, n_envs, n_steps, step0,
                             table_ok ? tables + par * noise_table_words(M) : nullptr, gw, lane,
