@@ -47,6 +47,10 @@ def parse_args():
     ap.add_argument("--cpu-all-core-slices", type=int, default=10,
                     help="slices per env of the all-cores CPU baseline (0: skip it)")
     ap.add_argument("--bd-reps", type=int, default=20)
+    ap.add_argument("--c5-colloids", type=int, default=16384,
+                    help="BASELINE config 5 line ('c5': chemotaxis + RND, one env; 0: off)")
+    ap.add_argument("--write-interval", type=float, default=1e4,
+                    help="trajectory write interval in seconds (reference default 1.0)")
     ap.add_argument("--stub", action="store_true",
                     help="CPU plumbing test: no GPU, gloo, synthetic trajectories")
     return ap.parse_args()
@@ -73,7 +77,7 @@ def build_workload(args, env_seed, device):
         time_step=ureg.Quantity(1e-3, "second"),
         time_slice=ureg.Quantity(0.1, "second"),
         # trajectory output (a "next" row) stays outside the timed slices
-        write_interval=ureg.Quantity(1e4, "second"),
+        write_interval=ureg.Quantity(getattr(args, "write_interval", 1e4), "second"),
     )
     eng = SwarmEngine(params, n_dims=2, seed=env_seed, n_envs=E,
                       out_folder=f"/tmp/swarm_bench_{os.getpid()}")
@@ -92,6 +96,59 @@ def build_workload(args, env_seed, device):
         "DoNothing": Action(),
     }
     agent = ActorCriticAgent(0, net, task, observable, actions, train=True)
+    ff = ForceFunction({"0": agent})
+    agent.reset_agent(eng.colloids)
+    return eng, ff, agent
+
+
+def build_c5_workload(args, env_seed, device):
+    """BASELINE config 5: 16384 colloids, concentration-field chemotaxis +
+    intrinsic reward: ConcentrationField observable (scale
+    10000) + GradientSensing task (scale 10), f(d) = 1 - d, source at the box
+    centre, and an RND intrinsic reward (3 x Dense(32) target/predictor) on
+    the device; MLP 1-128-(4+1)."""
+    import torch
+
+    from swarmrl_amd.actions import Action
+    from swarmrl_amd.agents import ActorCriticAgent
+    from swarmrl_amd.engine import MDParams, SwarmEngine
+    from swarmrl_amd.force_functions import ForceFunction
+    from swarmrl_amd.intrinsic_reward import RNDConfig, RNDReward
+    from swarmrl_amd.networks import ActorCriticMLP, TorchModel
+    from swarmrl_amd.observables import ConcentrationField
+    from swarmrl_amd.tasks.searching import GradientSensing
+    from swarmrl_amd.units import UnitRegistry
+
+    N, E = args.colloids, args.envs_per_gpu
+    L = 2.0 * math.sqrt(N * 1.0**2 / 0.1)
+    ureg = UnitRegistry()
+    params = MDParams(
+        ureg=ureg,
+        box_length=ureg.Quantity([L, L, L], "micrometer"),
+        time_step=ureg.Quantity(1e-3, "second"),
+        time_slice=ureg.Quantity(0.1, "second"),
+        write_interval=ureg.Quantity(getattr(args, "write_interval", 1e4), "second"),
+    )
+    eng = SwarmEngine(params, n_dims=2, seed=env_seed, n_envs=E,
+                      out_folder=f"/tmp/swarm_bench_c5_{os.getpid()}")
+    eng.add_colloids(N, ureg.Quantity(1.0, "micrometer"),
+                     ureg.Quantity(np.array([L / 2, L / 2, 0.0]), "micrometer"),
+                     ureg.Quantity(L / 2, "micrometer"))
+    box = np.array([L, L, L])
+    src = np.array([L / 2, L / 2, 0.0])
+    obs = ConcentrationField(src, lambda d: 1 - d, box, scale_factor=10000)
+    task = GradientSensing(source=src, decay_function=lambda d: 1 - d, box_length=box,
+                           reward_scale_factor=10)
+    torch.manual_seed(env_seed)
+    rnd = RNDReward(RNDConfig(input_shape=(1,), device=device))
+    net = TorchModel(ActorCriticMLP(1, 4, 128), input_shape=(1,), device=device)
+    actions = {
+        "RotateClockwise": Action(torque=np.array([0.0, 0.0, 10.0])),
+        "Translate": Action(force=10.0),
+        "RotateCounterClockwise": Action(torque=np.array([0.0, 0.0, -10.0])),
+        "DoNothing": Action(),
+    }
+    agent = ActorCriticAgent(0, net, task, obs, actions, train=True, intrinsic_reward=rnd)
     ff = ForceFunction({"0": agent})
     agent.reset_agent(eng.colloids)
     return eng, ff, agent
@@ -133,16 +190,17 @@ def pmc_traffic(kernel_prefix, E, N):
     """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3
     PMC summary (profiles/, separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE
     x2 per MI355X_MICROARCH.md), when it was collected on this workload."""
-    path = os.path.join(ROOT, "profiles", "r1_traffic.json")
-    try:
-        with open(path) as f:
-            rows = json.load(f)
-    except (OSError, ValueError):
-        return None, None
-    for r in rows:
-        if kernel_prefix in r.get("kernel", "") and r.get("envs") == E and \
-                r.get("colloids") == N:
-            return float(r["bytes_per_launch"]), f"profiles/{r['source']}"
+    for tag in ("r2", "r1"):  # the newest round's summary first
+        path = os.path.join(ROOT, "profiles", f"{tag}_traffic.json")
+        try:
+            with open(path) as f:
+                rows = json.load(f)
+        except (OSError, ValueError):
+            continue
+        for r in rows:
+            if kernel_prefix in r.get("kernel", "") and r.get("envs") == E and \
+                    r.get("colloids") == N:
+                return float(r["bytes_per_launch"]), f"profiles/{r['source']}"
     return None, None
 
 
@@ -254,7 +312,7 @@ def cpu_baseline_all_cores(args):
     }
 
 
-def measure(args, E, rank, world, device):
+def measure(args, E, rank, world, device, builder=None, colloids=None):
     """Build, capture and time one workload of E envs per GPU; returns the
     timing and roofline numbers (all ranks)."""
     import torch
@@ -264,7 +322,10 @@ def measure(args, E, rank, world, device):
 
     args_e = argparse.Namespace(**vars(args))
     args_e.envs_per_gpu = E
-    eng, ff, agent = build_workload(args_e, 42 + rank * E, device)
+    if colloids is not None:
+        args_e.colloids = colloids
+    args = args_e
+    eng, ff, agent = (builder or build_workload)(args_e, 42 + rank * E, device)
     eng.integrate(1, ff)  # setup, overlap removal, first slice (eager)
 
     def one_slice():
@@ -485,6 +546,19 @@ def main():
         batched = None
         if args.batched_envs > 0 and args.batched_envs != E:
             batched = measure(args, args.batched_envs, rank, world, device)
+        if args.c5_colloids > 0:
+            c5 = measure(args, 1, rank, world, device, builder=build_c5_workload,
+                         colloids=args.c5_colloids)
+            head["c5"] = {
+                "workload": f"BASELINE config 5: {args.c5_colloids} colloids, ConcentrationField "
+                            f"observable + GradientSensing reward + RND intrinsic reward, "
+                            f"one env per GPU",
+                "value": c5["value"],
+                "unit": "agent-steps/s",
+                "ms_per_step": c5["ms_per_step"],
+                "per_rank_value": c5["per_rank"],
+                "roofline": c5["roofline"],
+            }
     if world > 1 and dist.get_world_size() != args.gpus:
         print("bench.py: process group size differs from --gpus", file=sys.stderr)
         sys.exit(2)

@@ -95,6 +95,58 @@ __device__ __forceinline__ Sampled sample_logits(Logit L, int k, int a,
   return {idx, logf(p + 1e-8f)};
 }
 
+// sample_logits over logits held in registers (lg[K], K the padded width):
+// every loop is unrolled over compile-time indices guarded by q < k, so no
+// logit is read through a run-time index (which spilled lg to scratch for
+// K = 16).  Same draws and operation sequence as sample_logits.
+template <int K>
+__device__ __forceinline__ Sampled sample_logits_reg(const float (&lg)[K], int k, int a,
+                                                     unsigned long long ctr, uint32_t key0,
+                                                     uint32_t key1, float explore_p) {
+  float best = -__builtin_inff(), m = -__builtin_inff();
+  int idx = 0;
+#pragma unroll
+  for (int j0 = 0; j0 < K; j0 += 4) {
+    if (j0 < k) {
+      u32x4 c = {(uint32_t)a, (uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)(j0 >> 2)};
+      const u32x4 r = philox4x32_10(c, key0, key1);
+      const uint32_t rw[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = j0 + q;
+        if (j < k) {
+          const float lj = lg[j];
+          const float g = lj - logf(-logf(uniform24(rw[q])));
+          if (g > best) {  // first maximum, as argmax
+            best = g;
+            idx = j;
+          }
+          m = fmaxf(m, lj);
+        }
+      }
+    }
+  }
+  if (explore_p > 0.0f) {
+    u32x4 c = {(uint32_t)a, (uint32_t)ctr, (uint32_t)(ctr >> 32), 0x80000000u};
+    const u32x4 r = philox4x32_10(c, key0, key1);
+    float tbc = fminf(fmaxf(uniform24(r.x) - explore_p, 0.0f), 1.0f);
+    tbc = fminf(fmaxf(tbc * 1e6f, 0.0f), 1.0f);
+    const float keep = fminf(fmaxf(tbc * -10.0f + 1.0f, 0.0f), 1.0f);
+    const int rnd = min((int)(uniform24(r.y) * (float)k), k - 1);
+    idx = (int)((float)idx * tbc + (float)rnd * keep);
+  }
+  float s = 0.0f, li = 0.0f;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    if (j < k) {
+      s += expf(lg[j] - m);
+      li = j == idx ? lg[j] : li;
+    }
+  }
+  const float p = expf(li - m) / s;
+  return {idx, logf(p + 1e-8f)};
+}
+
 // The block's threads have all read their group counters: advance them.
 // Groups of 64 agents never straddle a block (agents per block % 64 == 0).
 __device__ __forceinline__ void advance_group_counter(unsigned long long* state, int a, int n,
@@ -195,25 +247,15 @@ __global__ __launch_bounds__(256) void k_policy_mlp_sample(
 #pragma unroll
   for (int q = 0; q < K; ++q) lg[q] = acc[q] + sb2[q];
   if (valid && sub == 0) {
-    const Sampled s = sample_logits(
-        [&](int j) {
-          float v = lg[0];
-#pragma unroll
-          for (int q = 1; q < K; ++q) v = j == q ? lg[q] : v;
-          return v;
-        },
-        k, a, ctr, key0, key1, explore_p);
+    const Sampled s = sample_logits_reg<K>(lg, k, a, ctr, key0, key1, explore_p);
     out_idx[a] = s.idx;
     out_logp[a] = s.logp;
     out_f[a] = ftab[s.idx];
     out_t[a] = ttab[s.idx];
     if (out_logits) {
-      for (int q = 0; q < k; ++q) {
-        float v = lg[0];
 #pragma unroll
-        for (int p = 1; p < K; ++p) v = q == p ? lg[p] : v;
-        out_logits[(size_t)a * k + q] = v;
-      }
+      for (int q = 0; q < K; ++q)
+        if (q < k) out_logits[(size_t)a * k + q] = lg[q];
     }
   }
   advance_group_counter(state, a, n, sub == 0, ctr);
