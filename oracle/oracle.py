@@ -98,6 +98,8 @@ def lib():
         L.or_signed_angle.argtypes = [_P, _P]
         L.or_normals3.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_uint64, ctypes.c_uint32, _P]
+        L.or_step_normals.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_uint64, _P]
         L.or_bd_run.restype = ctypes.c_int
         L.or_bd_run.argtypes = [ctypes.POINTER(Params), ctypes.c_int, _P, _P, _P, _P, _P, _P,
                                 _P, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, _P, _P,
@@ -369,6 +371,14 @@ def philox(ctr, key):
     o = (ctypes.c_uint32 * 4)()
     lib().or_philox4x32_10(c, k, o)
     return list(o)
+
+
+def step_normals(seed, env, pid, t):
+    """Sub-step t's three translation/rotation normals (swarm_oracle.c
+    or_step_normals: four-word Philox groups of four sub-steps)."""
+    out = np.zeros(3, np.float32)
+    lib().or_step_normals(int(seed), int(env), int(pid), int(t), _ptr(out))
+    return out
 
 
 def normals3(seed, env, pid, step, tag):

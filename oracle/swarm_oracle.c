@@ -228,6 +228,41 @@ void or_normals3(uint64_t seed, uint32_t env, uint32_t id, uint64_t step,
   out[2] = rad1 * c1;
 }
 
+/* Translation/rotation normals of sub-step t (the tag-0 stream; the
+ * engine's swarm_device.cuh StepNoise): sub-steps 4g..4g+3 take the twelve
+ * normals of three Philox blocks with counter (id, g lo, g hi, 0x10 + b),
+ * block b giving two full Box-Muller pairs (words 0/1, then 2/3: cosine
+ * leg, sine leg); sub-step t takes normals 3j..3j+2 of its group, j = t & 3. */
+static void group_block(uint64_t seed, uint32_t env, uint32_t id, uint64_t g,
+                        uint32_t b, float n[4]) {
+  uint32_t ctr[4] = {id, (uint32_t)g, (uint32_t)(g >> 32), 0x10u + b};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32) ^ env};
+  uint32_t r[4];
+  or_philox4x32_10(ctr, key, r);
+  float rad0 = bm_radius(r[0]);
+  float rad1 = bm_radius(r[2]);
+  float s0, c0, s1, c1;
+  or_sincos_turn(r[1], &s0, &c0);
+  or_sincos_turn(r[3], &s1, &c1);
+  n[0] = rad0 * c0;
+  n[1] = rad0 * s0;
+  n[2] = rad1 * c1;
+  n[3] = rad1 * s1;
+}
+
+void or_step_normals(uint64_t seed, uint32_t env, uint32_t id, uint64_t t,
+                     float out[3]) {
+  float n[12];
+  uint64_t g = t >> 2;
+  int j = (int)(t & 3u);
+  /* the blocks holding normals 3j .. 3j+2 */
+  int b_lo = (3 * j) / 4, b_hi = (3 * j + 2) / 4;
+  for (int b = b_lo; b <= b_hi; ++b) group_block(seed, env, id, g, (uint32_t)b, n + 4 * b);
+  out[0] = n[3 * j];
+  out[1] = n[3 * j + 1];
+  out[2] = n[3 * j + 2];
+}
+
 /* ------------------------------------------------------------------ */
 /* Derived fp32 constants (same derivation as swarm_engine.hip).       */
 /* ------------------------------------------------------------------ */
@@ -598,7 +633,7 @@ int or_bd_run_walls(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
       float dth = torque_z[i] * d.rot_dt[sp];
       if (noisy) {
         float g[3];
-        or_normals3(p->seed, env, (uint32_t)i, step, 0u, g);
+        or_step_normals(p->seed, env, (uint32_t)i, step, g);
         dx = dx + d.sig_t[sp] * g[0];
         dy = dy + d.sig_t[sp] * g[1];
         dth = dth + d.sig_r[sp] * g[2];
@@ -816,7 +851,7 @@ int or_bd_run3(const swarm_params_t *p, int n, uint32_t *q, int32_t *img, float 
       }
       if (noisy) {
         float g[3], h[3];
-        or_normals3(p->seed, env, (uint32_t)i, step, 0u, g);
+        or_step_normals(p->seed, env, (uint32_t)i, step, g);
         or_normals3(p->seed, env, (uint32_t)i, step, 2u, h);
         for (int a = 0; a < 3; ++a) {
           dq[a] = dq[a] + d.sig_t[sp] * g[a];

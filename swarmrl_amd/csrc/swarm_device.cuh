@@ -184,6 +184,98 @@ __device__ __forceinline__ void normals3(uint32_t k0, uint32_t k1, uint32_t id,
   g[2] = rad1 * c1;
 }
 
+// Translation/rotation normals of the Brownian step (tag 0 stream), all
+// four Philox words used: sub-steps t = 4 g .. 4 g + 3 ("group" g) take the
+// twelve normals n[0..11] of three Philox blocks with counter (id, g lo,
+// g hi, kGroupTag + b), b = 0, 1, 2; block b gives n[4b..4b+3] as two full
+// Box-Muller pairs (words x/y, then z/w: cosine leg, sine leg).  Sub-step t
+// takes n[3j..3j+2], j = t & 3.  Per sub-step 0.75 Philox blocks and 1.5
+// Box-Muller pairs (three normals per block before: one block, two pairs).
+constexpr uint32_t kGroupTag = 0x10u;
+
+// the four normals of block b of group g
+__device__ __forceinline__ void group_block(uint32_t k0, uint32_t k1, uint32_t id, uint64_t g,
+                                            uint32_t b, float n[4]) {
+  u32x4 c;
+  c.x = id;
+  c.y = (uint32_t)g;
+  c.z = (uint32_t)(g >> 32);
+  c.w = kGroupTag + b;
+  const u32x4 r = philox4x32_10(c, k0, k1);
+  const float rad0 = bm_radius(r.x);
+  const float rad1 = bm_radius(r.z);
+  float s0, c0, s1, c1;
+  sincos_turn(r.y, &s0, &c0);
+  sincos_turn(r.w, &s1, &c1);
+  n[0] = rad0 * c0;
+  n[1] = rad0 * s0;
+  n[2] = rad1 * c1;
+  n[3] = rad1 * s1;
+}
+
+// The normals of consecutive sub-steps: next(t) returns sub-step t's three,
+// generating a block only when the group reaches it and carrying the rest
+// (at most three floats).  fresh: t does not follow the previous call (the
+// first sub-step of a window), so the blocks it shares are drawn again.
+struct StepNoise {
+  float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f;
+  __device__ __forceinline__ void next(uint32_t k0, uint32_t k1, uint32_t id, uint64_t t,
+                                       bool fresh, float g[3]) {
+    const uint32_t j = (uint32_t)t & 3u;
+    const uint64_t grp = t >> 2;
+    float n[4];
+    if (j == 0u) {
+      group_block(k0, k1, id, grp, 0u, n);
+      g[0] = n[0];
+      g[1] = n[1];
+      g[2] = n[2];
+      c0 = n[3];
+    } else if (j == 1u) {
+      if (fresh) {
+        group_block(k0, k1, id, grp, 0u, n);
+        c0 = n[3];
+      }
+      group_block(k0, k1, id, grp, 1u, n);
+      g[0] = c0;
+      g[1] = n[0];
+      g[2] = n[1];
+      c0 = n[2];
+      c1 = n[3];
+    } else if (j == 2u) {
+      if (fresh) {
+        group_block(k0, k1, id, grp, 1u, n);
+        c0 = n[2];
+        c1 = n[3];
+      }
+      group_block(k0, k1, id, grp, 2u, n);
+      g[0] = c0;
+      g[1] = c1;
+      g[2] = n[0];
+      c0 = n[1];
+      c1 = n[2];
+      c2 = n[3];
+    } else {
+      if (fresh) {
+        group_block(k0, k1, id, grp, 2u, n);
+        c0 = n[1];
+        c1 = n[2];
+        c2 = n[3];
+      }
+      g[0] = c0;
+      g[1] = c1;
+      g[2] = c2;
+    }
+  }
+};
+
+// Sub-step t's three normals from scratch (paths that are not a run of
+// consecutive sub-steps of one particle in one thread).
+__device__ __forceinline__ void step_normals(uint32_t k0, uint32_t k1, uint32_t id, uint64_t t,
+                                             float g[3]) {
+  StepNoise sn;
+  sn.next(k0, k1, id, t, true, g);
+}
+
 // --------------------------------------------------- fixed-point helpers
 __device__ __forceinline__ int32_t f2i32(float v) {
   v = fminf(fmaxf(v, -2147483520.0f), 2147483520.0f);

@@ -816,8 +816,10 @@ void set_lds_attributes() {
                        reinterpret_cast<const void*>(&swarm::k_check),
                        reinterpret_cast<const void*>(&k_grid_build),
                        reinterpret_cast<const void*>(&k_vision_grid),
-                       reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<false>),
-                       reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<true>)};
+                       reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<false, false>),
+                       reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<true, false>),
+                       reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<false, true>),
+                       reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<true, true>)};
   for (const void* f : fns)
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
   (void)hipGetLastError();
@@ -844,8 +846,9 @@ int launch_global(swarm_engine* e, int n_steps, int sd_mode, float g, float md) 
 // step counter.
 int launch_noise(swarm_engine* e, hipStream_t stream, int n) {
   const long M = (long)e->n_envs * e->n;
-  hipLaunchKernelGGL(swarm::k_noise, dim3((unsigned)((M + 255) / 256), (unsigned)n), dim3(256), 0,
-                     stream, e->d_derived, e->st, e->d_step, e->d_noise);
+  hipLaunchKernelGGL(swarm::k_noise, dim3((unsigned)((M + 255) / 256),
+                                         (unsigned)swarm::noise_groups(n)),
+                     dim3(256), 0, stream, e->d_derived, e->st, e->d_step, e->d_noise, n);
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
 }
@@ -890,6 +893,7 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
   }
   const long waves = (long)e->n_envs * e->sc.wmax;
   const bool multi = e->params.n_species > 1;
+  const bool walls = e->derived.n_walls != 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   if (e->profile) {
     HIP_TRY(hipEventCreate(&ev0));
@@ -901,31 +905,48 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
     const int R = e->run_wpb;
     const dim3 grid((unsigned)(e->noise_blocks + (waves + R - 1) / R));
     const size_t lds = 96 * 1024;
-    if (multi)
-      hipLaunchKernelGGL(swarm::k_cluster_run_wide<true>, grid, dim3(1024), lds, e->stream,
-                         e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise,
-                         e->noise_blocks, R);
-    else
-      hipLaunchKernelGGL(swarm::k_cluster_run_wide<false>, grid, dim3(1024), lds, e->stream,
-                         e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise,
-                         e->noise_blocks, R);
+#define SWARM_WIDE(MULTI, WALLS)                                                             \
+  hipLaunchKernelGGL((swarm::k_cluster_run_wide<MULTI, WALLS>), grid, dim3(1024), lds, e->stream, \
+                     e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise,      \
+                     e->noise_blocks, R)
+    if (walls) {
+      if (multi)
+        SWARM_WIDE(true, true);
+      else
+        SWARM_WIDE(false, true);
+    } else {
+      if (multi)
+        SWARM_WIDE(true, false);
+      else
+        SWARM_WIDE(false, false);
+    }
+#undef SWARM_WIDE
     e->next_table_ready = e->noise_blocks > 0;
   } else {
     const dim3 run_grid((unsigned)((waves + 3) / 4)), run_block(256);
-#define SWARM_RUN(MULTI, TABLE)                                                              \
-  hipLaunchKernelGGL((swarm::k_cluster_run<MULTI, TABLE>), run_grid, run_block, 0, e->stream, \
-                     e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise)
+#define SWARM_RUN(MULTI, TABLE, WALLS)                                                     \
+  hipLaunchKernelGGL((swarm::k_cluster_run<MULTI, TABLE, WALLS>), run_grid, run_block, 0,   \
+                     e->stream, e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step,  \
+                     e->d_noise)
+#define SWARM_RUN_W(MULTI, TABLE)      \
+  do {                                 \
+    if (walls)                         \
+      SWARM_RUN(MULTI, TABLE, true);   \
+    else                               \
+      SWARM_RUN(MULTI, TABLE, false);  \
+  } while (0)
     if (e->noise_table) {
       if (multi)
-        SWARM_RUN(true, true);
+        SWARM_RUN_W(true, true);
       else
-        SWARM_RUN(false, true);
+        SWARM_RUN_W(false, true);
     } else {
       if (multi)
-        SWARM_RUN(true, false);
+        SWARM_RUN_W(true, false);
       else
-        SWARM_RUN(false, false);
+        SWARM_RUN_W(false, false);
     }
+#undef SWARM_RUN_W
 #undef SWARM_RUN
     e->next_table_ready = false;
   }

@@ -40,6 +40,9 @@
 namespace swarm {
 
 constexpr int kMaxSpecies = SWARM_MAX_SPECIES;
+#ifndef SWARM_RUN_MINB
+#define SWARM_RUN_MINB 5  // k_cluster_run: 5 blocks (waves) per CU (SIMD): <= 96 VGPRs
+#endif
 constexpr int kMaxWindow = 128;   // sub-steps per cluster window
 constexpr int kPairsPerWave = 256;  // neighbour pairs of one 64-lane wave (4 passes)
 // Clusters wider than a wave ("big" clusters) run in k_check's workgroup, one
@@ -352,7 +355,8 @@ __device__ __forceinline__ void bd_step(const PConst& c, PState& p, int64_t ax, 
                                         float fs, float tz, float fex, float fey, uint32_t k0,
                                         uint32_t k1, uint32_t id, uint64_t step, bool last,
                                         float* vx, float* vy, float* w,
-                                        const float* gt = nullptr, const float* dir = nullptr) {
+                                        const float* gt = nullptr, const float* dir = nullptr,
+                                        StepNoise* noise = nullptr, bool fresh = true) {
   float sn, cs;
   if (dir) {  // director of this sub-step, computed ahead by the caller
     sn = dir[0];
@@ -375,8 +379,10 @@ __device__ __forceinline__ void bd_step(const PConst& c, PState& p, int64_t ax, 
       g[0] = gt[0];
       g[1] = gt[1];
       g[2] = gt[2];
+    } else if (noise) {  // consecutive sub-steps of one particle: carried normals
+      noise->next(k0, k1, id, step, fresh, g);
     } else {
-      normals3(k0, k1, id, step, 0u, g);
+      step_normals(k0, k1, id, step, g);
     }
     dx = dx + c.sig_t * g[0];
     dy = dy + c.sig_t * g[1];
@@ -1408,34 +1414,48 @@ __device__ __forceinline__ void wave_lds_sync() {
 // match its table draws the normals itself.
 __host__ __device__ inline size_t noise_table_words(size_t M) { return (size_t)kMaxWindow * 3 * M; }
 
-__device__ __forceinline__ void noise_entry(const Derived* __restrict__ d, const DevState& st,
-                                            uint64_t step_start, float* __restrict__ table,
-                                            long gi, int s) {
+// Group k of a table starting at step_start: sub-steps t = 4 (g0 + k) + j
+// (g0 = step_start / 4) of particle gi, those within [start, start + len).
+// One thread draws the group's three Philox blocks (StepNoise).
+__device__ __forceinline__ void noise_group(const Derived* __restrict__ d, const DevState& st,
+                                            uint64_t step_start, int len,
+                                            float* __restrict__ table, long gi, int k) {
   const long M = st.m;
   const int e = (int)(gi / st.n);
   const int i = (int)(gi - (long)e * st.n);
-  float g[3];
-  normals3(d->key0, d->key1 ^ (uint32_t)e, (uint32_t)i, step_start + (uint64_t)s, 0u, g);
-  float* o = table + (size_t)s * 3 * M + gi;
-  o[0] = g[0];
-  o[M] = g[1];
-  o[2 * M] = g[2];
+  const uint64_t t0 = (step_start & ~3ull) + 4ull * (uint64_t)k;
+  StepNoise sn;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float g[3];
+    sn.next(d->key0, d->key1 ^ (uint32_t)e, (uint32_t)i, t0 + (uint64_t)j, j == 0, g);
+    const long s = (long)(t0 + (uint64_t)j) - (long)step_start;
+    if (s >= 0 && s < len) {
+      float* o = table + (size_t)s * 3 * M + gi;
+      o[0] = g[0];
+      o[M] = g[1];
+      o[2 * M] = g[2];
+    }
+  }
 }
 
-// This window's table (grid.y = sub-steps) from the current step counter.
+__host__ __device__ inline int noise_groups(int len) { return len / 4 + 2; }  // any alignment
+
+// This window's table of len sub-steps (grid.y = noise_groups(len)) from the
+// current step counter.
 __global__ __launch_bounds__(256) void k_noise(const Derived* __restrict__ d, DevState st,
                                                uint64_t* __restrict__ ctl,
-                                               float* __restrict__ tables) {
+                                               float* __restrict__ tables, int len) {
   const long M = st.m;
   const int par = window_parity(ctl);
   const uint64_t step0 = ctl[kCtlStep];
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
     ctl[kCtlTStep + par] = step0;
-    ctl[kCtlTLen + par] = gridDim.y;
+    ctl[kCtlTLen + par] = (uint64_t)len;
   }
   const long gi = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (gi >= M) return;
-  noise_entry(d, st, step0, tables + par * noise_table_words(M), gi, blockIdx.y);
+  noise_group(d, st, step0, len, tables + par * noise_table_words(M), gi, blockIdx.y);
 }
 
 // One wave of the cluster run: all n_steps sub-steps of the particles in
@@ -1488,16 +1508,17 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
   const int np = sc.wave_npairs[(size_t)e * sc.wmax + w];
   const int npass = (np + 63) >> 6;
   const uint32_t* pw = sc.pairs + ((size_t)e * sc.wmax + w) * kPairsPerWave;
-  uint32_t pr[kPairsPerWave / 64];
-#pragma unroll
-  for (int q = 0; q < kPairsPerWave / 64; ++q)
-    pr[q] = q * 64 + lane < np ? pw[q * 64 + lane] : 0xffffffffu;
+  // the first pass's pair stays in a register; a wave with more passes
+  // (rare: a cluster denser than 2 pairs per particle) reloads the others
+  // from L2 each sub-step, so they do not hold registers for the run
+  const uint32_t pr0 = lane < np ? pw[lane] : 0xffffffffu;
   lacc_x[lane] = 0ull;
   lacc_y[lane] = 0ull;
   const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
   const float sx0 = d->sx[0], sx1 = d->sx[1];
   const float eps24 = d->eps24;
-  const PConst pc = load_pconst(d, si);
+  // one species: its constants are wave-uniform (scalar registers)
+  const PConst pc = load_pconst(d, kMulti ? si : 0);
   const float cut2_0 = d->cut2[0], sig6_0 = d->sig6[0];
   const uint32_t q0x = p.qx, q0y = p.qy;
   float dmax2 = 0.0f;
@@ -1505,6 +1526,7 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
   const long ts = (long)M;
   const float* tcol = table + gi;
   float gn[3] = {0.0f, 0.0f, 0.0f};
+  StepNoise noise;  // !kTable: the window's normals drawn here, group by group
   if (kTable) {  // idle lanes read particle 0's (never stored)
     gn[0] = tcol[0];
     gn[1] = tcol[ts];
@@ -1539,15 +1561,15 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
       gn[1] = nx[ts];
       gn[2] = nx[2 * ts];
     }
-    if (!kTable && pc.noisy) normals3(k0, k1, (uint32_t)i, step0 + (uint64_t)s, 0u, gt);
+    if (!kTable && pc.noisy) noise.next(k0, k1, (uint32_t)i, step0 + (uint64_t)s, s == 0, gt);
     int64_t ax = 0, ay = 0;
     if (kPass > 0) {
       lpos_w[lane] = make_uint2(p.qx, p.qy);
       wave_lds_sync();
-#pragma unroll
-      for (int q = 0; q < (kPass == 1 ? 1 : kPairsPerWave / 64); ++q) {
-        if (kPass == 1 || q < npass) {  // wave-uniform; an empty slot names the lane twice
-          const uint32_t e_ = pr[q];
+      for (int q = 0; q < (kPass == 1 ? 1 : npass); ++q) {
+        {  // wave-uniform; an empty slot names the lane twice
+          const uint32_t e_ = q == 0 ? pr0
+                                     : (q * 64 + lane < np ? pw[q * 64 + lane] : 0xffffffffu);
           const int a = e_ == 0xffffffffu ? lane : (int)(e_ & 63u);
           const int b = e_ == 0xffffffffu ? lane : (int)((e_ >> 6) & 63u);
           const uint2 pa = lpos_w[a], pb = lpos_w[b];
@@ -1667,7 +1689,7 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
 
 // Uniform dispatch to the compile-time variants: normals from a table
 // (table != null) or drawn here; walls or none.
-template <bool kMulti>
+template <bool kMulti, bool kWalls>
 __device__ __forceinline__ void run_wave_dispatch(const Derived* __restrict__ d, const DevState& st,
                                                   const Scratch& sc, int n_envs, int n_steps,
                                                   uint64_t step0, const float* __restrict__ table,
@@ -1675,27 +1697,18 @@ __device__ __forceinline__ void run_wave_dispatch(const Derived* __restrict__ d,
                                                   unsigned long long* lacc_x,
                                                   unsigned long long* lacc_y,
                                                   const PairTables& pt) {
-  const bool walls = d->n_walls != 0;
-  if (table) {
-    if (walls)
-      run_wave<kMulti, true, true>(d, st, sc, n_envs, n_steps, step0, table, gw, lane, lpos_w,
+  if (table)
+    run_wave<kMulti, true, kWalls>(d, st, sc, n_envs, n_steps, step0, table, gw, lane, lpos_w,
                                    lacc_x, lacc_y, pt);
-    else
-      run_wave<kMulti, true, false>(d, st, sc, n_envs, n_steps, step0, table, gw, lane, lpos_w,
+  else
+    run_wave<kMulti, false, kWalls>(d, st, sc, n_envs, n_steps, step0, nullptr, gw, lane, lpos_w,
                                     lacc_x, lacc_y, pt);
-  } else {
-    if (walls)
-      run_wave<kMulti, false, true>(d, st, sc, n_envs, n_steps, step0, nullptr, gw, lane, lpos_w,
-                                    lacc_x, lacc_y, pt);
-    else
-      run_wave<kMulti, false, false>(d, st, sc, n_envs, n_steps, step0, nullptr, gw, lane,
-                                     lpos_w, lacc_x, lacc_y, pt);
-  }
 }
 
-// Throughput launch: 256-thread blocks, 4 waves each.
-template <bool kMulti, bool kTable>
-__global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__ d, DevState st,
+// Throughput launch: 256-thread blocks, 4 waves each.  kWalls (host-chosen)
+// keeps the wall-force variant's registers out of the wall-free kernel.
+template <bool kMulti, bool kTable, bool kWalls>
+__global__ __launch_bounds__(256, SWARM_RUN_MINB) void k_cluster_run(const Derived* __restrict__ d, DevState st,
                                                      Scratch sc, int n_envs, int n_steps,
                                                      const uint64_t* __restrict__ ctl,
                                                      const float* __restrict__ tables) {
@@ -1711,9 +1724,9 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
   const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   // a table that does not cover this window (the device check; the host
   // normally guarantees it) -> the normals are drawn in the kernel
-  run_wave_dispatch<kMulti>(d, st, sc, n_envs, n_steps, step0,
-                            table_ok ? tables + par * noise_table_words(st.m) : nullptr, gw, lane,
-                            lpos[wv], lacc[wv][0], lacc[wv][1], pt);
+  run_wave_dispatch<kMulti, kWalls>(d, st, sc, n_envs, n_steps, step0,
+                                    table_ok ? tables + par * noise_table_words(st.m) : nullptr,
+                                    gw, lane, lpos[wv], lacc[wv][0], lacc[wv][1], pt);
 }
 
 // Latency-bound launch (few envs x particles: the run's waves fill few
@@ -1724,7 +1737,7 @@ __global__ __launch_bounds__(256) void k_cluster_run(const Derived* __restrict__
 // run with waves [0, run_wpb) only: one run wave per CU at E = 1 (its
 // scattered noise-table gathers then have the CU's texture path to themselves),
 // up to one per SIMD for more envs.
-template <bool kMulti>
+template <bool kMulti, bool kWalls>
 __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __restrict__ d,
                                                            DevState st, Scratch sc, int n_envs,
                                                            int n_steps, uint64_t* __restrict__ ctl,
@@ -1745,10 +1758,10 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
       ctl[kCtlTLen + (par ^ 1)] = (uint64_t)kMaxWindow;
     }
     float* t = tables + (par ^ 1) * noise_table_words(M);
-    const long total = (long)kMaxWindow * (long)M;
+    const long total = (long)noise_groups(kMaxWindow) * (long)M;
     for (long k = (long)b * blockDim.x + tid; k < total; k += (long)n_noise_blocks * blockDim.x) {
-      const int s = (int)(k / (long)M);
-      noise_entry(d, st, start, t, k - (long)s * (long)M, s);
+      const int grp = (int)(k / (long)M);
+      noise_group(d, st, start, kMaxWindow, t, k - (long)grp * (long)M, grp);
     }
     return;
   }
@@ -1756,9 +1769,9 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
   if (wv >= run_wpb) return;
   const int gw = (b - n_noise_blocks) * run_wpb + wv;
   const bool table_ok = ctl[kCtlTStep + par] == step0 && (uint64_t)n_steps <= ctl[kCtlTLen + par];
-  run_wave_dispatch<kMulti>(d, st, sc, n_envs, n_steps, step0,
-                            table_ok ? tables + par * noise_table_words(M) : nullptr, gw, lane,
-                            lpos[wv], lacc[wv][0], lacc[wv][1], pt);
+  run_wave_dispatch<kMulti, kWalls>(d, st, sc, n_envs, n_steps, step0,
+                                    table_ok ? tables + par * noise_table_words(M) : nullptr, gw,
+                                    lane, lpos[wv], lacc[wv][0], lacc[wv][1], pt);
 }
 
 // The env's big clusters (wider than a wave) for the window, by k_check's
@@ -1806,6 +1819,7 @@ __device__ void run_big_clusters(const Derived* __restrict__ d, const DevState& 
   const float sx0 = d->sx[0], sx1 = d->sx[1];
   const float eps24 = d->eps24;
   float dmax2 = 0.0f, vx = 0.0f, vy = 0.0f, om = 0.0f;
+  StepNoise noise;
   if (mem) {
     ax[tid] = 0ull;
     ay[tid] = 0ull;
@@ -1840,7 +1854,7 @@ __device__ void run_big_clusters(const Derived* __restrict__ d, const DevState& 
                        st.wall_viol);
       }
       bd_step(pc, p, fxs, fys, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
-              s == n_steps - 1, &vx, &vy, &om);
+              s == n_steps - 1, &vx, &vy, &om, nullptr, nullptr, &noise, s == 0);
       const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
       const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
       dmax2 = fmaxf(dmax2, ddx * ddx + ddy * ddy);

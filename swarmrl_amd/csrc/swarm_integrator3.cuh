@@ -185,7 +185,7 @@ __device__ void block_global_run3(const Derived* __restrict__ d, const DevState&
         const uint64_t step = step0 + (uint64_t)s;
         if (noisy) {
           float gt[3], gr[3];
-          normals3(k0, k1, (uint32_t)i, step, 0u, gt);
+          step_normals(k0, k1, (uint32_t)i, step, gt);
           normals3(k0, k1, (uint32_t)i, step, 2u, gr);
 #pragma unroll
           for (int a = 0; a < 3; ++a) {

@@ -166,10 +166,25 @@ class _Particle:
         return f"Particle(id={self.id}, type={self.type})"
 
 
+# Engine handles whose owner was collected while a HIP graph capture was in
+# progress: freeing device memory then would invalidate the capture (the
+# garbage collector may run a finalizer at any allocation), so they are
+# destroyed at the next engine creation instead.
+_DEFERRED_DESTROY = []
+
+
+def _destroy_deferred():
+    while _DEFERRED_DESTROY:
+        lib, ptr = _DEFERRED_DESTROY.pop()
+        lib.swarm_engine_destroy(ptr)
+
+
 class _NativeEngine:
     """Owner of one C-ABI engine handle."""
 
     def __init__(self, params: _capi.SwarmParams, n_envs: int, species: np.ndarray):
+        if not torch.cuda.is_current_stream_capturing():
+            _destroy_deferred()
         self._lib = _capi.lib()
         self.ptr = ctypes.c_void_p()
         sp = np.ascontiguousarray(species, dtype=np.int32)
@@ -189,7 +204,10 @@ class _NativeEngine:
     def __del__(self):
         try:
             if self.ptr:
-                self._lib.swarm_engine_destroy(self.ptr)
+                if torch.cuda.is_current_stream_capturing():
+                    _DEFERRED_DESTROY.append((self._lib, self.ptr))
+                else:
+                    self._lib.swarm_engine_destroy(self.ptr)
                 self.ptr = ctypes.c_void_p()
         except Exception:  # pragma: no cover - interpreter shutdown
             pass

@@ -23,7 +23,7 @@ def _run(x, a):
         g.build()
     lib = ctypes.CDLL(str(lib_path))
     n = len(x)
-    out = np.zeros(9 * n, np.float32)
+    out = np.zeros(9 * n + 30 * min(n, 4096), np.float32)
     rc = lib.devmath_selftest(x.ctypes.data_as(ctypes.c_void_p), a.ctypes.data_as(ctypes.c_void_p),
                               ctypes.c_int(n), out.ctypes.data_as(ctypes.c_void_p))
     assert rc == 0
@@ -44,7 +44,8 @@ def test_device_math_bit_exact(oracle_mod):
     o_sqrt, o_log, o_acos = out[:n], out[n:2 * n], out[2 * n:3 * n]
     o_sin, o_cos = out[3 * n:4 * n], out[4 * n:5 * n]
     g = out[5 * n:8 * n].reshape(n, 3)
-    o_sqrtp = out[8 * n:]
+    o_sqrtp = out[8 * n:9 * n]
+    steps = out[9 * n:].reshape(-1, 30)
     assert np.array_equal(o_sqrt, np.sqrt(x))  # numpy sqrt is IEEE correctly rounded
     xp = (np.float32(1.1920929e-07) + x * np.float32(40.0)).astype(np.float32)
     bm = xp < np.float32(41.0)  # the radius range sqrt_pos serves (x < 1 part)
@@ -58,3 +59,11 @@ def test_device_math_bit_exact(oracle_mod):
         assert o_sin[i] == np.float32(s) and o_cos[i] == np.float32(c), i
         assert np.array_equal(g[i], oracle_mod.normals3(42, 0, int(i), 7, 0)), i
     assert math.isfinite(float(o_log[0]))
+    # grouped step normals (StepNoise): sub-steps carried across a group and
+    # started at every alignment equal the oracle's from-scratch restatement
+    for i in list(range(0, 64 * 8, 9)) + list(range(4000, 4096, 7)):
+        t0 = 1000 + i // 64
+        for s_ in range(9):
+            ref = oracle_mod.step_normals(42, 5, i % 64, t0 + s_)
+            assert np.array_equal(steps[i, 3 * s_:3 * s_ + 3], ref), (i, s_)
+        assert np.array_equal(steps[i, 27:30], oracle_mod.step_normals(42, 5, i % 64, t0 + 8))

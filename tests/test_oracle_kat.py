@@ -31,6 +31,28 @@ def test_normals_are_standard(oracle_mod):
     assert abs(np.mean(g**4) - 3.0) < 0.15
 
 
+def test_step_normals_are_standard_and_independent(oracle_mod):
+    # the grouped four-word stream: every position j of a group standard
+    # normal, no correlation between the three components of a sub-step or
+    # between consecutive sub-steps (the sine and cosine legs of one pair
+    # land in different positions of the group)
+    g = np.array([oracle_mod.step_normals(42, 0, i, t) for i in range(48) for t in range(240)])
+    g = g.reshape(48, 240, 3)
+    for j in range(4):
+        x = g[:, j::4, :].reshape(-1)
+        assert abs(x.mean()) < 0.03 and abs(x.std() - 1.0) < 0.03
+    flat = g.reshape(-1, 3)
+    c = np.corrcoef(flat.T)
+    assert np.all(np.abs(c - np.eye(3)) < 0.03)
+    seq = g.reshape(48, -1)  # the stream in draw order
+    for lag in (1, 2, 3, 4):
+        r = np.mean(seq[:, :-lag] * seq[:, lag:])
+        assert abs(r) < 0.03, lag
+    # a group's sub-steps use disjoint normals: 12 distinct values per group
+    grp = g[0, 8:12, :].reshape(-1)
+    assert len(set(grp.tolist())) == 12
+
+
 def test_elementary_functions_accuracy(oracle_mod):
     rng = np.random.default_rng(0)
     for x in rng.random(2000) * 0.999 + 1e-6:
