@@ -27,6 +27,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "agent-steps/sec, 4096-colloid WCA+vision-cone rollout @1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# MI355X_MICROARCH.md: a wave issues a VALU instruction over 2 cycles; 1024
+# SIMDs at 2.4 GHz -> 1.2288e12 VALU wave-instructions/s (= the 157.3 TF f32
+# vector peak / (64 lanes x 2 flop))
+VALU_PEAK_WAVE_INSTS = 1024 * 2.4e9 / 2
 BYTES_PER_PARTICLE_SUBSTEP = 40
 
 
@@ -187,11 +191,14 @@ def time_run_kernel(eng, reps):
 
 
 def pmc_traffic(kernel_prefix, E, N):
-    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3
-    PMC summary (profiles/, separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE
-    x2 per MI355X_MICROARCH.md), when it was collected on this workload."""
-    for tag in ("r2", "r1"):  # the newest round's summary first
-        path = os.path.join(ROOT, "profiles", f"{tag}_traffic.json")
+    """Per-launch HBM bytes and VALU wave-instructions of the dominant kernel
+    from the newest committed rocprofv3 PMC summary (profiles/<tag>_traffic.json:
+    separate FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU passes, FETCH_SIZE x2 per
+    MI355X_MICROARCH.md), when it was collected on this workload."""
+    import glob
+
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")), reverse=True)
+    for path in paths:  # the newest round's summary first (r2b > r2a > r1)
         try:
             with open(path) as f:
                 rows = json.load(f)
@@ -200,8 +207,9 @@ def pmc_traffic(kernel_prefix, E, N):
         for r in rows:
             if kernel_prefix in r.get("kernel", "") and r.get("envs") == E and \
                     r.get("colloids") == N:
-                return float(r["bytes_per_launch"]), f"profiles/{r['source']}"
-    return None, None
+                return (float(r["bytes_per_launch"]), r.get("valu_insts_per_launch"),
+                        f"profiles/{r['source']}")
+    return None, None, None
 
 
 def _cpu_env(N, slices, seed, barrier=None):
@@ -397,7 +405,7 @@ def measure(args, E, rank, world, device, builder=None, colloids=None):
     sub = eng.params.steps_per_slice
     bytes_per_launch = BYTES_PER_PARTICLE_SUBSTEP * N * sub * E
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic("k_cluster_run", E, N)
+    traffic, valu, traffic_src = pmc_traffic("k_cluster_run", E, N)
     out = dict(timing)
     out.update({
         "hip_graph": episode_graph is not None,
@@ -417,6 +425,18 @@ def measure(args, E, rank, world, device, builder=None, colloids=None):
     })
     if traffic_src:
         out["roofline"]["traffic_source"] = traffic_src
+    if valu:
+        # the bound that binds (SURVEY 8d asks for HBM; the fused kernel keeps
+        # its state in registers, so VALU issue is what it runs into)
+        out["roofline"]["valu"] = {
+            "achieved": valu / (kernel_ms * 1e-3),
+            "peak": VALU_PEAK_WAVE_INSTS,
+            "unit": "VALU wave-instructions/s",
+            "frac": valu / (kernel_ms * 1e-3) / VALU_PEAK_WAVE_INSTS,
+            "insts_per_launch": valu,
+            "lane_insts_per_colloid_substep": valu * 64 / (N * sub * E),
+            "source": traffic_src,
+        }
     del eng, ff, agent, slice_graph, episode_graph
     torch.cuda.synchronize()
     return out
@@ -594,7 +614,7 @@ def main():
     }
     if "gather" in head:
         line["gather"] = head["gather"]
-    for k in ("roofline_valu", "c5"):
+    for k in ("c5",):
         if k in head:
             line[k] = head[k]
     if batched is not None:

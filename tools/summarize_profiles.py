@@ -19,6 +19,7 @@ import sys
 
 tag = sys.argv[1]
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+N_C5 = int(sys.argv[3]) if len(sys.argv) > 3 else 16384  # bench.py --c5-colloids
 
 
 def envs_of_grid(g, wide):
@@ -46,6 +47,7 @@ for line in open(f"{src}/trace_bench.log"):
             f.write(line)
 
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
+first = {}
 for sub in ("fetch", "write", "valu"):
     path = f"{src}/{sub}/run_counter_collection.csv"
     if not os.path.exists(path):
@@ -55,6 +57,7 @@ for sub in ("fetch", "write", "valu"):
         name = re.sub(r"^void ", "", name).split("(")[0][:80]
         key = (name, int(r["Grid_Size"]))
         acc[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        first.setdefault(key, int(r["Dispatch_Id"]))
 names = ["FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "SQ_WAVES"]
 with open(f"{dst}/{tag}_pmc_summary.csv", "w", newline="") as f:
     w = csv.writer(f)
@@ -63,18 +66,30 @@ with open(f"{dst}/{tag}_pmc_summary.csv", "w", newline="") as f:
         n = max(len(v) for v in cs.values())
         w.writerow([k, g, n] + [f"{sum(cs[c]) / len(cs[c]):.1f}" if cs.get(c) else "" for c in names])
 
+# bench.py measures E = 1 (4096 colloids), then the batched envs, then the
+# config-5 env (16384 colloids): the latency-bound (wide) launches in order of
+# their first dispatch are the E = 1 line and the C5 line.
+wide_keys = sorted((key for key in acc if "k_cluster_run_wide" in key[0]), key=lambda kk: first[kk])
 traffic = []
 for (k, g), cs in acc.items():
     if "k_cluster_run" not in k or not cs.get("FETCH_SIZE") or not cs.get("WRITE_SIZE"):
         continue
-    E = envs_of_grid(g, "wide" in k)
+    n_env = N
+    if "wide" in k:
+        E = 1
+        if wide_keys.index((k, g)) > 0:
+            n_env = N_C5
+    else:
+        E = envs_of_grid(g, False)
     fetch_kb = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"])
     write_kb = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"])
     traffic.append({
-        "kernel": k, "envs": E, "colloids": N,
+        "kernel": k, "envs": E, "colloids": n_env,
         "fetch_size_kb": fetch_kb, "write_size_kb": write_kb,
         # FETCH_SIZE/WRITE_SIZE are in KB; FETCH_SIZE reads half the bytes on gfx950
         "bytes_per_launch": (2 * fetch_kb + write_kb) * 1024.0,
+        "valu_insts_per_launch": (sum(cs["SQ_INSTS_VALU"]) / len(cs["SQ_INSTS_VALU"])
+                                  if cs.get("SQ_INSTS_VALU") else None),
         "source": f"{tag}_pmc_summary.csv",
     })
 with open(f"{dst}/{tag}_traffic.json", "w") as f:
