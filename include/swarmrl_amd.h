@@ -59,7 +59,15 @@ typedef struct swarm_params {
   double wca_epsilon; /* WCA epsilon (espresso.py:814-819) */
   uint64_t seed;    /* thermostat seed (espresso.py:1183) */
   int32_t n_species;
-  int32_t reserved0;
+  /* ESPResSo's integrator.run(k, reuse_forces=True) (espresso.py:1304-1306):
+   * the Brownian propagator takes each step's forces from the force
+   * calculation that ended the previous step, and a run with reuse_forces
+   * does not recompute them first -- so sub-step 0 of every run uses the
+   * swim force, torque and director of the previous run's last force
+   * calculation (the actions set since then act from sub-step 1).
+   * 1: that semantics (SwarmEngine's default, as the reference);
+   * 0: every sub-step uses the current actions. */
+  int32_t reuse_forces;
   double radius[SWARM_MAX_SPECIES];
   double gamma_t[SWARM_MAX_SPECIES];  /* 6 pi eta r  (espresso.py:108-113) */
   double gamma_r[SWARM_MAX_SPECIES];  /* 8 pi eta r^3 */

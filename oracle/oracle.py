@@ -39,7 +39,7 @@ class Params(ctypes.Structure):
         ("wca_epsilon", ctypes.c_double),
         ("seed", ctypes.c_uint64),
         ("n_species", ctypes.c_int32),
-        ("reserved0", ctypes.c_int32),
+        ("reuse_forces", ctypes.c_int32),
         ("radius", ctypes.c_double * MAX_SPECIES),
         ("gamma_t", ctypes.c_double * MAX_SPECIES),
         ("gamma_r", ctypes.c_double * MAX_SPECIES),
@@ -118,13 +118,13 @@ def lib():
                                         ctypes.c_double, _P, ctypes.c_int]
         L.or_cell_grid.argtypes = [ctypes.POINTER(Params), ctypes.c_int, ctypes.c_double, _P, _P]
         L.or_bd_run_walls.restype = ctypes.c_int
-        L.or_bd_run_walls.argtypes = L.or_bd_run.argtypes + [_P, ctypes.c_int, _P]
+        L.or_bd_run_walls.argtypes = L.or_bd_run.argtypes + [_P, ctypes.c_int, _P, _P, _P, _P]
         L.or_sd_run_walls.restype = ctypes.c_int
         L.or_sd_run_walls.argtypes = L.or_sd_run.argtypes + [_P, ctypes.c_int]
         L.or_bd_run3.restype = ctypes.c_int
         L.or_bd_run3.argtypes = [ctypes.POINTER(Params), ctypes.c_int, _P, _P, _P, _P, _P, _P,
                                  _P, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, _P, _P,
-                                 _P, ctypes.c_int, _P]
+                                 _P, ctypes.c_int, _P, _P, _P, _P]
         L.or_sd_run3.restype = ctypes.c_int
         L.or_sd_run3.argtypes = [ctypes.POINTER(Params), ctypes.c_int, _P, _P, _P, _P, _P, _P,
                                  _P, ctypes.c_int, ctypes.c_double, ctypes.c_double, _P,
@@ -222,10 +222,13 @@ def _copy_state(state):
 
 # ------------------------------------------------------------- dynamics
 def bd_run(params, state, species, f_swim, torque_z, n_steps, step0=0, env=0, f_ext=None,
-           use_cells=True, walls=None, violations=None):
+           use_cells=True, walls=None, violations=None, prev=None):
     """n_steps BD sub-steps of one env; returns (new_state, vel [3,N], omega [N]).
     walls: list of wall dicts (make_walls); violations: 1-element uint64
-    array that receives the added count of wall contacts."""
+    array that receives the added count of wall contacts.  prev: None, or
+    reuse_forces (espresso.py:1304-1306) -- {"f": f_swim, "t": torque_z,
+    "ang": orientation} of the previous run's last force calculation, used by
+    sub-step 0 (see ReuseForces)."""
     st = _copy_state(state)
     n = st["ang"].shape[0]
     sp = np.ascontiguousarray(species, dtype=np.uint8)
@@ -236,19 +239,26 @@ def bd_run(params, state, species, f_swim, torque_z, n_steps, step0=0, env=0, f_
     om = np.zeros(n, np.float32)
     wa, nw = make_walls(walls or [])
     viol = np.zeros(1, np.uint64) if violations is None else violations
+    f0 = t0 = a0 = None
+    if prev is not None:
+        f0 = np.ascontiguousarray(prev["f"], dtype=np.float32)
+        t0 = np.ascontiguousarray(prev["t"], dtype=np.float32)
+        a0 = np.ascontiguousarray(prev["ang"], dtype=np.uint32)
     rc = lib().or_bd_run_walls(ctypes.byref(params), n, _ptr(st["q"]), _ptr(st["img"]),
                                _ptr(st["ang"]), _ptr(sp), _ptr(fs), _ptr(tz), _ptr(fe),
                                int(step0), int(n_steps), int(env), _ptr(vel), _ptr(om),
-                               1 if use_cells else 0, ctypes.cast(wa, _P), nw, _ptr(viol))
+                               1 if use_cells else 0, ctypes.cast(wa, _P), nw, _ptr(viol),
+                               _ptr(f0), _ptr(t0), _ptr(a0))
     if rc != 0:
         raise ValueError(f"or_bd_run failed ({rc})")
     return st, vel, om
 
 
 def bd_run3(params, state, species, f_swim, torque, n_steps, step0=0, env=0, f_ext=None,
-            walls=None, violations=None):
+            walls=None, violations=None, prev=None):
     """3-D: n_steps BD sub-steps of one env (state with 'dir' [3,N]); torque
-    [3,N] lab frame.  Returns (new_state, vel [3,N], omega [3,N])."""
+    [3,N] lab frame.  Returns (new_state, vel [3,N], omega [3,N]).  prev:
+    reuse_forces, {"f", "t" [3,N], "dir" [3,N]} (see bd_run)."""
     st = _copy_state(state)
     n = st["q"].shape[1]
     sp = np.ascontiguousarray(species, dtype=np.uint8)
@@ -259,10 +269,15 @@ def bd_run3(params, state, species, f_swim, torque, n_steps, step0=0, env=0, f_e
     om = np.zeros((3, n), np.float32)
     wa, nw = make_walls(walls or [])
     viol = np.zeros(1, np.uint64) if violations is None else violations
+    f0 = t0 = d0 = None
+    if prev is not None:
+        f0 = np.ascontiguousarray(prev["f"], dtype=np.float32)
+        t0 = np.ascontiguousarray(prev["t"], dtype=np.float32).reshape(3, n)
+        d0 = np.ascontiguousarray(prev["dir"], dtype=np.float32).reshape(3, n)
     rc = lib().or_bd_run3(ctypes.byref(params), n, _ptr(st["q"]), _ptr(st["img"]),
                           _ptr(st["dir"]), _ptr(sp), _ptr(fs), _ptr(tq), _ptr(fe), int(step0),
                           int(n_steps), int(env), _ptr(vel), _ptr(om), ctypes.cast(wa, _P), nw,
-                          _ptr(viol))
+                          _ptr(viol), _ptr(f0), _ptr(t0), _ptr(d0))
     if rc != 0:
         raise ValueError(f"or_bd_run3 failed ({rc})")
     return st, vel, om
@@ -282,6 +297,32 @@ def sd_run3(params, state, species, n_steps, gamma=0.1, max_disp=0.1, f_swim=Non
                              _ptr(st["dir"]), _ptr(sp), _ptr(fs), _ptr(tq), _ptr(fe),
                              int(n_steps), float(gamma), float(max_disp), ctypes.cast(wa, _P), nw)
     return st, steps
+
+
+class ReuseForces:
+    """Oracle-side bookkeeping of reuse_forces for a sequence of runs of one
+    env (the engine's f_prev / tz_prev / ang_prev): starts from zero actions
+    (nothing swims before the first manage_forces, espresso.py:1228-1235) and
+    the initial orientation; run() integrates and remembers what the next
+    run's sub-step 0 reuses."""
+
+    def __init__(self, state, dims=2):
+        n = state["q"].shape[1]
+        self.dims = dims
+        if dims == 3:
+            self.prev = {"f": np.zeros(n, np.float32), "t": np.zeros((3, n), np.float32),
+                         "dir": np.asarray(state["dir"], np.float32).copy()}
+        else:
+            self.prev = {"f": np.zeros(n, np.float32), "t": np.zeros(n, np.float32),
+                         "ang": np.asarray(state["ang"], np.uint32).copy()}
+
+    def run(self, params, state, species, f_swim, torque, n_steps, **kw):
+        fn = bd_run3 if self.dims == 3 else bd_run
+        st, vel, om = fn(params, state, species, f_swim, torque, n_steps, prev=self.prev, **kw)
+        key = "dir" if self.dims == 3 else "ang"
+        self.prev = {"f": np.asarray(f_swim, np.float32).copy(),
+                     "t": np.asarray(torque, np.float32).copy(), key: st[key].copy()}
+        return st, vel, om
 
 
 def rotate_director(v, phi):

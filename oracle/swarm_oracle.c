@@ -593,13 +593,18 @@ static void cl_free(celllist_t *cl) {
  * vel/omega (NULL allowed) receive the BD velocity of the last sub-step.
  * step0: global step index of the first sub-step (noise counter).
  * use_cells: 0 = O(n^2) pair search, 1 = cell list (same result).
+ * f_swim0 / torque0 / ang0 (NULL: the current ones): what sub-step 0 uses --
+ * ESPResSo's run(k, reuse_forces=True) (espresso.py:1304-1306) propagates
+ * with the forces of the previous run's last force calculation, i.e. that
+ * run's swim force and torque along the orientation it ended with.
  */
 int or_bd_run_walls(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
                     uint32_t *ang, const uint8_t *species, const float *f_swim,
                     const float *torque_z, const float *f_ext, uint64_t step0,
                     int n_steps, uint32_t env, float *vel, float *omega,
                     int use_cells, const swarm_wall_t *walls, int n_walls,
-                    uint64_t *violations) {
+                    uint64_t *violations, const float *f_swim0, const float *torque0,
+                    const uint32_t *ang0) {
   if (p->n_dims != 2)
     return SWARM_EINVAL;
   derived_t d;
@@ -619,18 +624,21 @@ int or_bd_run_walls(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
       if (d.n_walls)
         wall_forces(&d, sp, (float)q[i] * d.sx[0], (float)q[n + i] * d.sx[1], 0.0f, 2,
                     &acc[i], &acc[n + i], NULL, &viol);
-      or_sincos_turn(ang[i], &sn, &cs);
+      const int first = s == 0;
+      const float fs = first && f_swim0 ? f_swim0[i] : f_swim[i];
+      const float tz = first && torque0 ? torque0[i] : torque_z[i];
+      or_sincos_turn(first && ang0 ? ang0[i] : ang[i], &sn, &cs);
       float fx = (float)acc[i] * 5.9604644775390625e-08f;
       float fy = (float)acc[n + i] * 5.9604644775390625e-08f;
       if (f_ext) {
         fx = fx + f_ext[i];
         fy = fy + f_ext[n + i];
       }
-      fx = fx + f_swim[i] * cs;
-      fy = fy + f_swim[i] * sn;
+      fx = fx + fs * cs;
+      fy = fy + fs * sn;
       float dx = fx * d.mob_dt[sp];
       float dy = fy * d.mob_dt[sp];
-      float dth = torque_z[i] * d.rot_dt[sp];
+      float dth = tz * d.rot_dt[sp];
       if (noisy) {
         float g[3];
         or_step_normals(p->seed, env, (uint32_t)i, step, g);
@@ -643,7 +651,7 @@ int or_bd_run_walls(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
       ang[i] = ang[i] + (uint32_t)f2i32(dth * ANG_INV_SCALE);
       if (s == n_steps - 1) {
         float vx = fx * d.inv_gt[sp], vy = fy * d.inv_gt[sp];
-        float w = torque_z[i] * d.inv_gr[sp];
+        float w = tz * d.inv_gr[sp];
         if (noisy) {
           float g[3];
           or_normals3(p->seed, env, (uint32_t)i, step, 1u, g);
@@ -675,7 +683,7 @@ int or_bd_run(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
               int n_steps, uint32_t env, float *vel, float *omega,
               int use_cells) {
   return or_bd_run_walls(p, n, q, img, ang, species, f_swim, torque_z, f_ext, step0,
-                         n_steps, env, vel, omega, use_cells, NULL, 0, NULL);
+                         n_steps, env, vel, omega, use_cells, NULL, 0, NULL, NULL, NULL, NULL);
 }
 
 /*
@@ -817,12 +825,15 @@ void or_rotate_director(float v[3], float px, float py, float pz) {
  * dir [3][n] fp32 unit directors; torque [3][n] lab frame; f_ext [3][n] or
  * NULL; vel/omega [3][n] (NULL allowed): BD velocity and angular velocity of
  * the last sub-step.  Noise tags: 0 translation, 2 rotation, 1 velocity,
- * 3 angular velocity.
+ * 3 angular velocity.  f_swim0 / torque0 [3][n] / dir0 [3][n] (NULL: the
+ * current ones): sub-step 0's swim force, torque and swim direction
+ * (reuse_forces, see or_bd_run_walls).
  */
 int or_bd_run3(const swarm_params_t *p, int n, uint32_t *q, int32_t *img, float *dir,
                const uint8_t *species, const float *f_swim, const float *torque,
                const float *f_ext, uint64_t step0, int n_steps, uint32_t env, float *vel,
-               float *omega, const swarm_wall_t *walls, int n_walls, uint64_t *violations) {
+               float *omega, const swarm_wall_t *walls, int n_walls, uint64_t *violations,
+               const float *f_swim0, const float *torque0, const float *dir0) {
   if (p->n_dims != 3)
     return SWARM_EINVAL;
   derived_t d;
@@ -841,13 +852,17 @@ int or_bd_run3(const swarm_params_t *p, int n, uint32_t *q, int32_t *img, float 
                     (float)q[2 * n + i] * d.sx[2], 3, &acc[i], &acc[n + i], &acc[2 * n + i],
                     &viol);
       float f[3], dq[3], ph[3], v[3] = {dir[i], dir[n + i], dir[2 * n + i]};
+      const int first = s == 0;
+      const float fs = first && f_swim0 ? f_swim0[i] : f_swim[i];
+      const float *tq = first && torque0 ? torque0 : torque;
       for (int a = 0; a < 3; ++a) {
+        const float va = first && dir0 ? dir0[a * n + i] : v[a];
         f[a] = (float)acc[a * n + i] * 5.9604644775390625e-08f;
         if (f_ext)
           f[a] = f[a] + f_ext[a * n + i];
-        f[a] = f[a] + f_swim[i] * v[a];
+        f[a] = f[a] + fs * va;
         dq[a] = f[a] * d.mob_dt[sp];
-        ph[a] = torque[a * n + i] * d.rot_dt[sp];
+        ph[a] = tq[a * n + i] * d.rot_dt[sp];
       }
       if (noisy) {
         float g[3], h[3];
@@ -868,7 +883,7 @@ int or_bd_run3(const swarm_params_t *p, int n, uint32_t *q, int32_t *img, float 
         float vv[3], ww[3];
         for (int a = 0; a < 3; ++a) {
           vv[a] = f[a] * d.inv_gt[sp];
-          ww[a] = torque[a * n + i] * d.inv_gr[sp];
+          ww[a] = tq[a * n + i] * d.inv_gr[sp];
         }
         if (noisy) {
           float g[3], h[3];

@@ -42,7 +42,7 @@ class SwarmParams(ctypes.Structure):
         ("wca_epsilon", ctypes.c_double),
         ("seed", ctypes.c_uint64),
         ("n_species", ctypes.c_int32),
-        ("reserved0", ctypes.c_int32),
+        ("reuse_forces", ctypes.c_int32),
         ("radius", ctypes.c_double * SWARM_MAX_SPECIES),
         ("gamma_t", ctypes.c_double * SWARM_MAX_SPECIES),
         ("gamma_r", ctypes.c_double * SWARM_MAX_SPECIES),

@@ -976,7 +976,7 @@ struct swarm_engine {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
   float* own_f_swim = nullptr;
   float* own_torque_z = nullptr;
-  void* allocs[64] = {};
+  void* allocs[96] = {};
   int n_allocs = 0;
 };
 
@@ -1386,6 +1386,11 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->st.torque_xy, 2 * M);
   rc = rc ? rc : dev_alloc(e, &e->st.omega_xy, 2 * M);
   rc = rc ? rc : dev_alloc(e, &e->st.wall_viol, 1);
+  rc = rc ? rc : dev_alloc(e, &e->st.f_prev, M);
+  rc = rc ? rc : dev_alloc(e, &e->st.tz_prev, M);
+  rc = rc ? rc : dev_alloc(e, &e->st.ang_prev, M);
+  rc = rc ? rc : dev_alloc(e, &e->st.dir3_prev, three_d ? 3 * M : 1);
+  rc = rc ? rc : dev_alloc(e, &e->st.txy_prev, three_d ? 2 * M : 1);
   rc = rc ? rc : dev_alloc(e, &e->sc.sidx, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.bq, 2 * M);
   rc = rc ? rc : dev_alloc(e, &e->sc.bimg, 2 * M);
@@ -1464,6 +1469,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   e->st.n = n_particles;
   e->st.m = (int32_t)M;
   e->st.dims = params->n_dims;
+  e->st.reuse = params->reuse_forces ? 1 : 0;
   std::vector<uint8_t> sp(n_particles);
   for (int i = 0; i < n_particles; ++i) sp[i] = (uint8_t)species[i];
   if (hipMemcpy(e->st.species, sp.data(), sp.size(), hipMemcpyHostToDevice) != hipSuccess ||
@@ -1504,6 +1510,9 @@ int swarm_engine_upload_raw(swarm_engine_t* e, const uint32_t* q, const int32_t*
   HIP_TRY(hipMemcpyAsync(e->st.q, q, 3 * M * sizeof(uint32_t), hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(e->st.img, img, 3 * M * sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(e->st.ang, ang, M * sizeof(uint32_t), hipMemcpyHostToDevice, e->stream));
+  // a fresh state: the last force calculation saw these orientations
+  HIP_TRY(hipMemcpyAsync(e->st.ang_prev, ang, M * sizeof(uint32_t), hipMemcpyHostToDevice,
+                         e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   return SWARM_OK;
 }
@@ -1626,7 +1635,12 @@ int swarm_engine_set_directors(swarm_engine_t* e, const double* dir, const uint8
       if (!(nm > 0.0)) return fail(SWARM_EINVAL, "new_direction must be non-zero");
       for (int a = 0; a < 3; ++a) d3[a * M + g] = (float)(v[a] / nm);
     }
-    return swarm_engine_upload_directors(e, d3.data());
+    // the director only: with reuse_forces the next run's sub-step 0 still
+    // swims along the director of the last force calculation (dir3_prev)
+    HIP_TRY(hipMemcpyAsync(e->st.dir3, d3.data(), 3 * M * sizeof(float), hipMemcpyHostToDevice,
+                           e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return SWARM_OK;
   }
   std::vector<uint32_t> ang(M);
   HIP_TRY(hipMemcpyAsync(ang.data(), e->st.ang, M * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
@@ -1953,6 +1967,8 @@ int swarm_engine_upload_directors(swarm_engine_t* e, const float* dir3) {
   if (!e || !dir3) return fail(SWARM_EINVAL, "null argument");
   const size_t M = (size_t)e->st.m;
   HIP_TRY(hipMemcpyAsync(e->st.dir3, dir3, 3 * M * sizeof(float), hipMemcpyHostToDevice,
+                         e->stream));
+  HIP_TRY(hipMemcpyAsync(e->st.dir3_prev, dir3, 3 * M * sizeof(float), hipMemcpyHostToDevice,
                          e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   return SWARM_OK;

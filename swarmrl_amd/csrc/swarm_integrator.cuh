@@ -103,7 +103,41 @@ struct DevState {
   float* torque_xy;  // [2][M] (z: torque_z)
   float* omega_xy;   // [2][M] (z: omega)
   unsigned long long* wall_viol;  // [1] wall contacts with dist <= 0
+  // reuse_forces (swarm_params_t): what the last force calculation of the
+  // previous run used -- sub-step 0 of a run takes its swim force, torque
+  // and director from here (espresso.py:1304-1306); saved at every window end
+  int32_t reuse;
+  float* f_prev;       // [M]
+  float* tz_prev;      // [M]
+  uint32_t* ang_prev;  // [M]    2-D orientation
+  float* dir3_prev;    // [3][M] 3-D director
+  float* txy_prev;     // [2][M] 3-D torque x, y
 };
+
+// End of a window (every path): the actions and orientations that the next
+// run's sub-step 0 reuses.  Called by the thread that wrote particle gi's
+// final state.
+__device__ __forceinline__ void save_forces(const DevState& st, size_t gi) {
+  const size_t M = (size_t)st.m;
+  st.f_prev[gi] = st.f_swim[gi];
+  st.tz_prev[gi] = st.torque_z[gi];
+  if (st.dims == 3) {
+    st.dir3_prev[gi] = st.dir3[gi];
+    st.dir3_prev[M + gi] = st.dir3[M + gi];
+    st.dir3_prev[2 * M + gi] = st.dir3[2 * M + gi];
+    st.txy_prev[gi] = st.torque_xy[gi];
+    st.txy_prev[M + gi] = st.torque_xy[M + gi];
+  } else {
+    st.ang_prev[gi] = st.ang[gi];
+  }
+}
+
+__device__ __forceinline__ void save_forces_env(const DevState& st, int e) {
+  if (!st.reuse) return;
+  __syncthreads();
+  const size_t base = (size_t)e * st.n;
+  for (int i = threadIdx.x; i < st.n; i += blockDim.x) save_forces(st, base + i);
+}
 
 // Device control block (uint64 words): step counter, window counter, and
 // the two noise tables' first step / length (by window parity, see k_noise).
@@ -349,21 +383,18 @@ __device__ __forceinline__ void stage_pair_tables(const Derived* __restrict__ d,
 }
 
 // One Brownian-dynamics sub-step of one particle from its summed WCA force.
+// an_swim: the orientation the swim force points along (p.an, or with
+// reuse_forces at sub-step 0 the previous run's last one).
 // kTable: the step's three normals come precomputed in gt (k_noise).
 template <bool kTable = false>
 __device__ __forceinline__ void bd_step(const PConst& c, PState& p, int64_t ax, int64_t ay,
                                         float fs, float tz, float fex, float fey, uint32_t k0,
                                         uint32_t k1, uint32_t id, uint64_t step, bool last,
-                                        float* vx, float* vy, float* w,
-                                        const float* gt = nullptr, const float* dir = nullptr,
-                                        StepNoise* noise = nullptr, bool fresh = true) {
+                                        float* vx, float* vy, float* w, uint32_t an_swim,
+                                        const float* gt = nullptr, StepNoise* noise = nullptr,
+                                        bool fresh = true) {
   float sn, cs;
-  if (dir) {  // director of this sub-step, computed ahead by the caller
-    sn = dir[0];
-    cs = dir[1];
-  } else {
-    sincos_turn(p.an, &sn, &cs);
-  }
+  sincos_turn(an_swim, &sn, &cs);
   float fx = i64_to_f32(ax) * 5.9604644775390625e-08f;
   float fy = i64_to_f32(ay) * 5.9604644775390625e-08f;
   fx = fx + fex;
@@ -535,7 +566,9 @@ __device__ void block_global_run(const Derived* __restrict__ d, const DevState& 
         wall_forces<2>(d, si, (float)p.qx * sx0, (float)p.qy * sx1, 0.0f, ax, ay, az,
                        st.wall_viol);
       }
-      const float fs = st.f_swim[gi], tz = st.torque_z[gi];
+      const bool first = st.reuse && s == 0 && !sd_mode;  // reuse_forces: previous run's
+      const float fs = first ? st.f_prev[gi] : st.f_swim[gi];
+      const float tz = first ? st.tz_prev[gi] : st.torque_z[gi];
       const float fex = st.f_ext[gi], fey = st.f_ext[M + gi];
       const PConst pc = load_pconst(d, si);
       if (sd_mode) {
@@ -544,7 +577,7 @@ __device__ void block_global_run(const Derived* __restrict__ d, const DevState& 
         float vx, vy, w;
         const bool last = s == n_steps - 1;
         bd_step(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s, last,
-                &vx, &vy, &w);
+                &vx, &vy, &w, first ? st.ang_prev[gi] : p.an);
         if (last) {
           st.vel[gi] = vx;
           st.vel[M + gi] = vy;
@@ -654,7 +687,9 @@ __device__ __forceinline__ void block_global_run_lds(const Derived* __restrict__
       const int i = pki & 0xffffff, sik = pki >> 24;
       const size_t gi = base + i;
       PState pp = {lqx[i], lqy[i], lan[i], lix[i], liy[i]};
-      const float fs = st.f_swim[gi], tz = st.torque_z[gi];
+      const bool first = st.reuse && s == 0 && !sd_mode;  // reuse_forces: previous run's
+      const float fs = first ? st.f_prev[gi] : st.f_swim[gi];
+      const float tz = first ? st.tz_prev[gi] : st.torque_z[gi];
       const float fex = st.f_ext[gi], fey = st.f_ext[M + gi];
       int64_t ax = 0, ay = 0;
       const int c0 = cell_index(pp.qx, pp.qy, lx, ly);
@@ -692,7 +727,7 @@ __device__ __forceinline__ void block_global_run_lds(const Derived* __restrict__
         float vx, vy, w;
         const bool last = s == n_steps - 1;
         bd_step(pc, pp, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
-                last, &vx, &vy, &w);
+                last, &vx, &vy, &w, first ? st.ang_prev[gi] : pp.an);
         if (last) {
           st.vel[gi] = vx;
           st.vel[M + gi] = vy;
@@ -766,6 +801,7 @@ __global__ __launch_bounds__(1024) void k_global(const Derived* __restrict__ d, 
   else
     block_global_run(d, st, sc, blockIdx.x, n_steps, step0, lx, ly, sd_mode != 0, g, md, cnt,
                      wave_sums, &pt);
+  save_forces_env(st, blockIdx.x);
   if (!sd_mode) advance_counter(step_ctr, arrive, step0, n_steps);
 }
 
@@ -1483,7 +1519,10 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
   const bool active = i >= 0;
   PState p = {0u, 0u, 0u, 0, 0};
   int si = 0;
+  // fs, tz: this sub-step's swim force and torque -- for sub-step 0 with
+  // reuse_forces the previous run's (the current ones are loaded after it)
   float fs = 0.0f, tz = 0.0f, fex = 0.0f, fey = 0.0f;
+  uint32_t an0 = 0u;  // orientation of sub-step 0's swim force
   const size_t gi = base + (active ? i : 0);
   if (active) {
     p.qx = st.q[gi];
@@ -1492,8 +1531,9 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     p.iy = st.img[M + gi];
     p.an = st.ang[gi];
     si = st.species[i];
-    fs = st.f_swim[gi];
-    tz = st.torque_z[gi];
+    fs = st.reuse ? st.f_prev[gi] : st.f_swim[gi];
+    tz = st.reuse ? st.tz_prev[gi] : st.torque_z[gi];
+    an0 = st.reuse ? st.ang_prev[gi] : p.an;
     fex = st.f_ext[gi];
     fey = st.f_ext[M + gi];
     // window-start snapshot for k_check's exact test and re-run (taken here,
@@ -1543,7 +1583,7 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
   // the pass count (0, 1 or up to 4) and the last sub-step (velocities) are
   // compile-time variants, and idle lanes compute along (never stored).
   float dir[2];
-  sincos_turn(p.an, &dir[0], &dir[1]);
+  sincos_turn(an0, &dir[0], &dir[1]);
   auto substep = [&](const int s, auto last_t, auto pass_t) __attribute__((always_inline)) {
     constexpr bool kLast = decltype(last_t)::value;
     constexpr int kPass = decltype(pass_t)::value;  // 0, 1, or 4: up to npass
@@ -1644,8 +1684,19 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
 #endif
   };
   auto run_steps = [&](auto pass_t) __attribute__((always_inline)) {
-    for (int s = 0; s < n_steps - 1; ++s) substep(s, std::false_type{}, pass_t);
-    substep(n_steps - 1, std::true_type{}, pass_t);  // velocities of the last sub-step
+    int s = 0;
+    if (n_steps > 1) {
+      // sub-step 0 peeled: with reuse_forces it swims with the previous run's
+      // actions, and the current ones are loaded once after it (no register
+      // holds them across the loop)
+      substep(0, std::false_type{}, pass_t);
+      if (st.reuse && active) {
+        fs = st.f_swim[gi];
+        tz = st.torque_z[gi];
+      }
+      for (s = 1; s < n_steps - 1; ++s) substep(s, std::false_type{}, pass_t);
+    }
+    substep(s, std::true_type{}, pass_t);  // velocities of the last sub-step
   };
 #ifdef SWARM_ABL_NOPAIR  // timing ablation only: no pair section
   if (true)
@@ -1798,6 +1849,9 @@ __device__ void run_big_clusters(const Derived* __restrict__ d, const DevState& 
   PState p = {st.q[gi], st.q[M + gi], st.ang[gi], st.img[gi], st.img[M + gi]};
   const int si = st.species[i];
   const float fs = st.f_swim[gi], tz = st.torque_z[gi];
+  // reuse_forces: sub-step 0 takes the previous run's actions and director
+  const float fs0 = st.reuse ? st.f_prev[gi] : fs, tz0 = st.reuse ? st.tz_prev[gi] : tz;
+  const uint32_t an0 = st.reuse ? st.ang_prev[gi] : p.an;
   const float fex = st.f_ext[gi], fey = st.f_ext[M + gi];
   const PConst pc = load_pconst(d, si);
   if (mem) {
@@ -1853,8 +1907,9 @@ __device__ void run_big_clusters(const Derived* __restrict__ d, const DevState& 
         wall_forces<2>(d, si, (float)p.qx * sx0, (float)p.qy * sx1, 0.0f, fxs, fys, az,
                        st.wall_viol);
       }
-      bd_step(pc, p, fxs, fys, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
-              s == n_steps - 1, &vx, &vy, &om, nullptr, nullptr, &noise, s == 0);
+      bd_step(pc, p, fxs, fys, s == 0 ? fs0 : fs, s == 0 ? tz0 : tz, fex, fey, k0, k1,
+              (uint32_t)i, step0 + (uint64_t)s, s == n_steps - 1, &vx, &vy, &om,
+              s == 0 ? an0 : p.an, nullptr, &noise, s == 0);
       const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
       const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
       dmax2 = fmaxf(dmax2, ddx * ddx + ddy * ddy);
@@ -1973,6 +2028,7 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
       block_global_run(d, st, sc, e, n_steps, step0, lx, ly, false, 0.0f, 0.0f, cnt, wave_sums,
                        &pt);
   }
+  save_forces_env(st, e);
   advance_counter(step_ctr, arrive, step0, n_steps);
 }
 

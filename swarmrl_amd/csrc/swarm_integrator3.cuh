@@ -130,6 +130,8 @@ __device__ void block_global_run3(const Derived* __restrict__ d, const DevState&
         im[a] = st.img[a * M + gi];
       }
       float v[3] = {st.dir3[gi], st.dir3[M + gi], st.dir3[2 * M + gi]};
+      // reuse_forces: sub-step 0 takes the previous run's actions and director
+      const bool first = st.reuse && s == 0 && !sd_mode;
       const int si = st.species[i];
       int64_t acc[3] = {0, 0, 0};
       const int c0 = cell_index3(q[0], q[1], q[2], lx, ly, lz);
@@ -158,14 +160,18 @@ __device__ void block_global_run3(const Derived* __restrict__ d, const DevState&
       if (d->n_walls)
         wall_forces<3>(d, si, (float)q[0] * sx[0], (float)q[1] * sx[1], (float)q[2] * sx[2],
                        acc[0], acc[1], acc[2], st.wall_viol);
-      const float fs = st.f_swim[gi];
-      const float tq[3] = {st.torque_xy[gi], st.torque_xy[M + gi], st.torque_z[gi]};
+      const float fs = first ? st.f_prev[gi] : st.f_swim[gi];
+      const float tq[3] = {first ? st.txy_prev[gi] : st.torque_xy[gi],
+                           first ? st.txy_prev[M + gi] : st.torque_xy[M + gi],
+                           first ? st.tz_prev[gi] : st.torque_z[gi]};
+      const float vs[3] = {first ? st.dir3_prev[gi] : v[0], first ? st.dir3_prev[M + gi] : v[1],
+                           first ? st.dir3_prev[2 * M + gi] : v[2]};
       float f[3], dq[3], ph[3];
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
         f[a] = i64_to_f32(acc[a]) * 5.9604644775390625e-08f;
         f[a] = f[a] + st.f_ext[a * M + gi];
-        f[a] = f[a] + fs * v[a];
+        f[a] = f[a] + fs * vs[a];
       }
       if (sd_mode) {
 #pragma unroll
@@ -249,6 +255,7 @@ __global__ __launch_bounds__(1024) void k_global3(const Derived* __restrict__ d,
   const uint64_t step0 = sd_mode ? 0ull : *step_ctr;
   block_global_run3(d, st, sc, blockIdx.x, n_steps, step0, lx, ly, lz, sd_mode != 0, g, md, cnt,
                     wave_sums, &pt);
+  save_forces_env(st, blockIdx.x);
   if (!sd_mode) advance_counter(step_ctr, arrive, step0, n_steps);
 }
 

@@ -233,8 +233,14 @@ class SwarmEngine(Engine):
         system=None,
         h5_group_tag: str = None,
         n_envs: int = 1,
+        reuse_forces: bool = True,
     ):
         self.params: MDParams = md_params
+        # integrator.run(k, reuse_forces=True) (espresso.py:1304-1306): the
+        # first sub-step of every run uses the forces of the previous run's
+        # last force calculation (swim force, torque, director), as ESPResSo's
+        # Brownian propagator does; False: the current actions throughout
+        self.reuse_forces = bool(reuse_forces)
         self.out_folder = pathlib.Path(out_folder).resolve()
         self.seed = seed
         self.rng = np.random.default_rng(self.seed)
@@ -641,6 +647,7 @@ class SwarmEngine(Engine):
         p.wca_epsilon = float(self.params.WCA_epsilon.m_as("sim_energy"))
         p.seed = int(self.seed) & 0xFFFFFFFFFFFFFFFF
         p.n_species = len(self._species_keys)
+        p.reuse_forces = 1 if self.reuse_forces else 0
         for s, (r, gt, gr, m, rin) in enumerate(self._species_keys):
             p.radius[s], p.gamma_t[s], p.gamma_r[s] = r, gt, gr
             p.mass[s], p.rinertia[s] = m, rin

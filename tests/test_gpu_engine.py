@@ -138,8 +138,15 @@ def test_kt0_drift_and_velocity_kat(tmp_path):
     gt, _ = eng.get_friction_coefficients(1)
     for v in new["Velocities"]:
         np.testing.assert_array_almost_equal(v, force * direc / gt)
-    np.testing.assert_allclose(old["Unwrapped_Positions"] + eng.system.time * force * direc / gt,
-                               new["Unwrapped_Positions"], rtol=2e-6)
+    # reuse_forces (espresso.py:1304-1306): the first sub-step of the 10
+    # slices still swims with the rotation slice's zero force, so the drift
+    # lasts t - dt.  (The reference's x0 + t v at rtol 2e-6 admits that lag,
+    # dt v = 3e-4 um, only where |x| > 150 um; this port's seed places a
+    # colloid at x = 77 um.)
+    dt = eng.params.time_step.m_as("second")
+    np.testing.assert_allclose(
+        old["Unwrapped_Positions"] + (eng.system.time - dt) * force * direc / gt,
+        new["Unwrapped_Positions"], rtol=2e-6)
     eng.finalize()
 
 

@@ -215,6 +215,35 @@ def test_bd_kt0_velocity_and_drift_kat(oracle_mod):
     np.testing.assert_allclose(x0 + 1.0 * v_expect, x1, rtol=2e-6)
 
 
+def test_bd_kt0_reuse_forces_closed_form(oracle_mod):
+    """reuse_forces (espresso.py:1304-1306): sub-step 0 swims with the
+    previous run's force along the previous orientation, with the previous
+    torque: x = x0 + dt v_old d_old + (n - 1) dt v_new d, and the orientation
+    turns by dt tau_old / gamma_r + (n - 1) dt tau_new / gamma_r."""
+    gt, gr = refsem.friction(1e-3, 1.0)
+    box = [1000.0, 1000.0, 1000.0]
+    p = oracle_mod.make_params(box, 0.01, 0.0, 0.0, 1, [(1.0, gt, gr, 1.0, 1.0)])
+    st = oracle_mod.state_from_positions([[500.0, 500.0, 0]], [[1.0, 0, 0]], box)
+    old = {"f": [2.0], "t": [0.0], "ang": oracle_mod.angle_fixed(0.0, 1.0)[None]}  # swam along +y
+    n = 10
+    st1, vel, om = oracle_mod.bd_run(p, st, [0], [7.0], [0.0], n, prev=old)
+    dx = oracle_mod.unwrapped(st1, box) - oracle_mod.unwrapped(st, box)
+    np.testing.assert_allclose(dx[0, :2], [(n - 1) * 0.01 * 7.0 / gt, 0.01 * 2.0 / gt],
+                               rtol=1e-5, atol=2e-6)
+    assert vel[0, 0] == pytest.approx(7.0 / gt, rel=1e-6)  # last sub-step: current force
+    # torque lag
+    st2, _, _ = oracle_mod.bd_run(p, st, [0], [0.0], [3.0], n,
+                                  prev={"f": [0.0], "t": [1.0], "ang": st["ang"]})
+    dth = ((int(st2["ang"][0]) - int(st["ang"][0])) % 2**32) * 2 * np.pi / 2**32
+    assert dth == pytest.approx(0.01 * (1.0 + (n - 1) * 3.0) / gr, rel=1e-5)
+    # prev equal to the current actions: the same bits as no reuse
+    a, _, _ = oracle_mod.bd_run(p, st, [0], [7.0], [3.0], n)
+    b, _, _ = oracle_mod.bd_run(p, st, [0], [7.0], [3.0], n,
+                                prev={"f": [7.0], "t": [3.0], "ang": st["ang"]})
+    for k in ("q", "img", "ang"):
+        assert np.array_equal(a[k], b[k])
+
+
 def test_bd_kt0_torque_kat(oracle_mod):
     """test_espresso_2d.py:168-179 analogue: omega_z = tau / gamma_rot."""
     gt, gr = refsem.friction(8.9e-4, 1.0)
