@@ -47,9 +47,11 @@ def parse_args():
     ap.add_argument("--episode-length", type=int, default=20)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-slices", type=int, default=100)
-    ap.add_argument("--cpu-all-core-slices", type=int, default=10,
-                    help="slices per env of the all-cores CPU baseline (0: skip it)")
+    ap.add_argument("--cpu-sample-slices", type=int, default=200)
+    ap.add_argument("--cpu-all-core-slices", type=int, default=200,
+                    help="slices of the all-cores (OpenMP) CPU baseline (0: skip it)")
+    ap.add_argument("--cpu-all-pairs-slices", type=int, default=10,
+                    help="slices of the all-pairs-vision CPU context row (0: skip it)")
     ap.add_argument("--bd-reps", type=int, default=20)
     ap.add_argument("--c5-colloids", type=int, default=16384,
                     help="BASELINE config 5 line ('c5': chemotaxis + RND, one env; 0: off)")
@@ -212,15 +214,19 @@ def pmc_traffic(kernel_prefix, E, N):
     return None, None, None
 
 
-def _cpu_env(N, slices, seed, barrier=None):
-    """One env of the CPU baseline: the CPU oracle (C restatement) + the
-    torch-CPU policy on one thread.  Returns (agent-steps, t_start, t_end)
-    of the timed loop (after setup; `barrier` lines up concurrent workers)."""
+def _cpu_env(N, slices, seed, threads=1, cells=True):
+    """One env of the CPU comparator: the C restatement of the
+    path -- cell-list WCA + Brownian dynamics, the vision cone over a cell
+    list (cells=False: the reference's all-pairs loop), the field reward --
+    plus the torch-CPU policy, on `threads` threads (OpenMP over particles /
+    agents in the C code, torch intra-op threads for the MLP).  Returns
+    (agent-steps, seconds) of the timed loop (after setup)."""
     import torch
 
     from oracle import oracle
 
-    torch.set_num_threads(1)
+    torch.set_num_threads(threads)
+    oracle.set_threads(threads)
     L = 2.0 * math.sqrt(N / 0.1)
     box = [L, L, L]
     rng = np.random.default_rng(seed)
@@ -242,12 +248,10 @@ def _cpu_env(N, slices, seed, barrier=None):
     ftab = np.array([0.0, 10.0, 0.0, 0.0], np.float32)
     ttab = np.array([10.0, 0.0, -10.0, 0.0], np.float32)
     src = np.array([L / 2, L / 2, 0.0])
-    if barrier is not None:
-        barrier.wait()
-    t0 = time.time()
+    ones, zeros = np.ones(N, np.float32), np.zeros(N, np.int32)
+    t0 = time.perf_counter()
     for s in range(slices):
-        obs = oracle.vision_cone(p, st, agents, np.ones(N, np.float32), np.zeros(N, np.int32),
-                                 10.0, np.pi / 2, 3, [0])
+        obs = oracle.vision_cone(p, st, agents, ones, zeros, 10.0, np.pi / 2, 3, [0], cells=cells)
         with torch.no_grad():
             logits = net(torch.as_tensor(obs.reshape(N, 3)))[:, :4]
             u = torch.rand(logits.shape)
@@ -256,67 +260,99 @@ def _cpu_env(N, slices, seed, barrier=None):
         st, _, _ = oracle.bd_run(p, st, sp, ftab[idx], ttab[idx], 100, step0=100 * s)
         dc, dp = oracle.field_distance(p, st, agents, src, np.array(box), hist)
         np.clip(10 * ((1 - dc) - (1 - dp)), 0, None)
-    return N * slices, t0, time.time()
+    dt = time.perf_counter() - t0
+    oracle.set_threads(1)
+    return N * slices, dt
 
 
-_POOL_BARRIER = None
-
-
-def _pool_init(barrier):
-    global _POOL_BARRIER
-    _POOL_BARRIER = barrier
-
-
-def _pool_env(job):
-    N, slices, seed = job
-    return _cpu_env(N, slices, seed, _POOL_BARRIER)
+def _cpu_host():
+    """CPU model and the cores this process may run on."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    return model, avail
 
 
 def cpu_baseline(args):
-    """The CPU oracle + torch-CPU policy on one 4096-colloid env, one
-    thread, for a bounded number of slices."""
+    """The CPU comparator on one 4096-colloid env, one thread, for a bounded
+    number of slices (the reference CI runs single-threaded,
+    .github/workflows/espresso.yml:41)."""
     import torch
 
     torch_threads = torch.get_num_threads()
     try:
-        steps, t0, t1 = _cpu_env(args.colloids, args.cpu_sample_slices, 42)
+        steps, dt = _cpu_env(args.colloids, args.cpu_sample_slices, 42, threads=1, cells=True)
     finally:
         torch.set_num_threads(torch_threads)
-    dt = t1 - t0
+    model, avail = _cpu_host()
     return {
         "value": steps / dt,
         "unit": "agent-steps/s",
         "cores": 1,
         "kind": "port",
+        "cpu_model": model,
+        "nproc": avail,
         "sample": f"{args.cpu_sample_slices} slices x {args.colloids} colloids (1 env, 100 "
-                  f"sub-steps each, O(N^2) vision cone as in the reference) on 1 host core, "
-                  f"{dt:.1f} s",
+                  f"sub-steps each; cell-list WCA and vision cone, C restatement + torch-CPU "
+                  f"policy) on 1 host core, {dt:.1f} s",
+    }
+
+
+def cpu_baseline_all_pairs(args):
+    """Context row: the same with the reference's all-pairs vision cone
+    (subdivided_vision_cones.py:178-205 is O(N^2)), a short sample."""
+    import torch
+
+    torch_threads = torch.get_num_threads()
+    try:
+        steps, dt = _cpu_env(args.colloids, args.cpu_all_pairs_slices, 42, threads=1, cells=False)
+    finally:
+        torch.set_num_threads(torch_threads)
+    return {
+        "value": steps / dt,
+        "unit": "agent-steps/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{args.cpu_all_pairs_slices} slices x {args.colloids} colloids with the "
+                  f"reference's all-pairs vision cone, 1 core, {dt:.1f} s (context, not the "
+                  f"comparator)",
     }
 
 
 def cpu_baseline_all_cores(args):
-    """The same CPU baseline with one env per host core (independent envs,
-    the reference's episode parallelism), all running at once: worker
-    processes (spawned, not forked from this GPU process) line up on a
-    barrier; value = all their agent-steps / (last end - first start)."""
-    import multiprocessing as mp
+    """The CPU comparator with OpenMP over the particles / agents of one env
+    on all the cores this process may use (up to the 16-core share of a
+    one-GPU box), torch intra-op threads for the policy."""
+    import torch
 
-    cores = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
-    cores = max(1, min(cores, 16, os.cpu_count() or 1))
-    ctx = mp.get_context("spawn")
-    barrier = ctx.Barrier(cores)
-    jobs = [(args.colloids, args.cpu_all_core_slices, 42 + i) for i in range(cores)]
-    with ctx.Pool(cores, initializer=_pool_init, initargs=(barrier,)) as pool:
-        res = pool.map(_pool_env, jobs, chunksize=1)
-    steps = sum(r[0] for r in res)
-    dt = max(r[2] for r in res) - min(r[1] for r in res)
+    model, avail = _cpu_host()
+    cores = int(os.environ.get("OMP_NUM_THREADS") or avail)
+    cores = max(1, min(cores, 16, avail))
+    torch_threads = torch.get_num_threads()
+    try:
+        steps, dt = _cpu_env(args.colloids, args.cpu_all_core_slices, 42, threads=cores,
+                             cells=True)
+    finally:
+        torch.set_num_threads(torch_threads)
     return {
         "value": steps / dt,
         "unit": "agent-steps/s",
         "cores": cores,
         "kind": "port",
-        "sample": f"{cores} envs x {args.cpu_all_core_slices} slices x {args.colloids} colloids, "
-                  f"one env per core in concurrent processes, {dt:.1f} s",
+        "cpu_model": model,
+        "nproc": avail,
+        "sample": f"{args.cpu_all_core_slices} slices x {args.colloids} colloids (1 env), "
+                  f"OpenMP over particles and agents on {cores} threads, {dt:.1f} s",
     }
 
 
@@ -632,6 +668,8 @@ def main():
         line["cpu_baseline"] = cpu_baseline(args)
         if args.cpu_all_core_slices > 0:
             line["cpu_baseline_all_cores"] = cpu_baseline_all_cores(args)
+        if args.cpu_all_pairs_slices > 0:
+            line["cpu_baseline_all_pairs_vision"] = cpu_baseline_all_pairs(args)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

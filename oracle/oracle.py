@@ -111,6 +111,11 @@ def lib():
         L.or_vision_cone.argtypes = [ctypes.POINTER(Params), ctypes.c_int, _P, _P, _P, _P,
                                      ctypes.c_int, _P, _P, ctypes.c_float, ctypes.c_int, _P,
                                      ctypes.c_int, _P, _P]
+        L.or_vision_cone_cells.restype = ctypes.c_int
+        L.or_vision_cone_cells.argtypes = L.or_vision_cone.argtypes
+        L.or_set_threads.argtypes = [ctypes.c_int]
+        L.or_get_threads.restype = ctypes.c_int
+        L.or_set_threads(1)  # the scalar restatement unless a caller asks for threads
         L.or_field_distance.argtypes = [ctypes.POINTER(Params), ctypes.c_int, _P, _P, _P,
                                         ctypes.c_int, _P, _P, _P, _P, _P, _P, ctypes.c_int]
         L.or_neighbor_pairs.restype = ctypes.c_int
@@ -354,8 +359,16 @@ def vision_rims(half_angle, n_cones):
     return (-a + ((k * a) * np.float32(2)) / np.float32(n_cones)).astype(np.float32)
 
 
+def set_threads(n):
+    """OpenMP threads of the oracle's per-particle / per-agent loops (the
+    results do not depend on it)."""
+    lib().or_set_threads(int(n))
+
+
 def vision_cone(params, state, agents, radii, types, vision_range, half_angle, n_cones,
-                detected_types):
+                detected_types, cells=False):
+    """cells=False: the reference's all-pairs loop; True: over a cell list
+    (same bits; needs 2 vision_range < box)."""
     n = state["ang"].shape[0]
     ag = np.ascontiguousarray(agents, dtype=np.int32)
     rad = np.ascontiguousarray(radii, dtype=np.float32)
@@ -364,10 +377,12 @@ def vision_cone(params, state, agents, radii, types, vision_range, half_angle, n
     rims = vision_rims(half_angle, n_cones)
     out = np.zeros((len(ag), n_cones, len(det)), np.float32)
     st = _copy_state(state)
-    lib().or_vision_cone(ctypes.byref(params), n, _ptr(st["q"]), _ptr(st["img"]),
-                         _ptr(st["ang"]), _ptr(ag), len(ag), _ptr(rad), _ptr(ty),
-                         float(vision_range), int(n_cones), _ptr(rims), len(det), _ptr(det),
-                         _ptr(out))
+    fn = lib().or_vision_cone_cells if cells else lib().or_vision_cone
+    rc = fn(ctypes.byref(params), n, _ptr(st["q"]), _ptr(st["img"]), _ptr(st["ang"]), _ptr(ag),
+            len(ag), _ptr(rad), _ptr(ty), float(vision_range), int(n_cones), _ptr(rims), len(det),
+            _ptr(det), _ptr(out))
+    if cells and rc:
+        raise ValueError("or_vision_cone_cells needs a periodic box wider than 2 vision_range")
     return out
 
 

@@ -47,6 +47,29 @@
 
 #include "../include/swarmrl_amd.h"
 
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* Threads of the per-particle / per-agent loops (OpenMP; 1 = the scalar
+ * restatement).  Every parallel loop writes only its own particle's or
+ * agent's outputs and sums in int64, so results do not depend on it. */
+void or_set_threads(int n) {
+#ifdef _OPENMP
+  omp_set_num_threads(n > 0 ? n : 1);
+#else
+  (void)n;
+#endif
+}
+
+int or_get_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
+
 /* ------------------------------------------------------------------ */
 /* Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11 "Parallel random   */
 /* numbers: as easy as 1, 2, 3").                                      */
@@ -536,6 +559,7 @@ static void wca_forces(const swarm_params_t *p, const derived_t *d, int n,
   }
   cl_build(cl, p, q, img, n);
   int ncx = 1 << cl->lx, ncy = 1 << cl->ly;
+#pragma omp parallel for schedule(static)
   for (int i = 0; i < n; ++i) {
     int c = cl->cell[i];
     int cx = c % ncx, cy = c / ncx;
@@ -618,12 +642,16 @@ int or_bd_run_walls(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
   for (int s = 0; s < n_steps; ++s) {
     uint64_t step = step0 + (uint64_t)s;
     wca_forces(p, &d, n, q, img, species, acc, have_cl ? &cl : NULL);
+#pragma omp parallel for schedule(static) reduction(+ : viol)
     for (int i = 0; i < n; ++i) {
       int sp = species[i];
       float sn, cs;
-      if (d.n_walls)
+      if (d.n_walls) {
+        uint64_t vi = 0;
         wall_forces(&d, sp, (float)q[i] * d.sx[0], (float)q[n + i] * d.sx[1], 0.0f, 2,
-                    &acc[i], &acc[n + i], NULL, &viol);
+                    &acc[i], &acc[n + i], NULL, &vi);
+        viol += vi;
+      }
       const int first = s == 0;
       const float fs = first && f_swim0 ? f_swim0[i] : f_swim[i];
       const float tz = first && torque0 ? torque0[i] : torque_z[i];
@@ -960,6 +988,63 @@ int or_sd_run3(const swarm_params_t *p, int n, uint32_t *q, int32_t *img, float 
  * radii[n]: radius of the seen colloid by list position; types[n]: type of
  * every colloid; det[n_types]: detected types; rims[n_cones + 1].
  */
+/* What colloid j adds to agent i's cone bins (subdivided_vision_cones.py:
+ * 116-153, 199-205); director (mx, my) of i. */
+static void vision_pair(const derived_t *d, int n, const uint32_t *q, const int32_t *img,
+                        int i, int j, float mx, float my, const float *radii,
+                        const int *types, float vision_range, int n_cones, const float *rims,
+                        int n_types, const int *det, int64_t *acc) {
+  if (j == i)
+    return;
+  int ti = -1;
+  for (int t = 0; t < n_types; ++t)
+    if (det[t] == types[j])
+      ti = t;
+  if (ti < 0)
+    return;
+  /* unwrapped difference, no minimum image (subdivided_vision_cones.py:116) */
+  float dd[2];
+  int far = 0;
+  for (int a = 0; a < 2; ++a) {
+    int64_t dq = ((int64_t)(img[a * n + j] - img[a * n + i]) * (int64_t)4294967296LL) +
+                 ((int64_t)q[a * n + j] - (int64_t)q[a * n + i]);
+    if (dq < -2147483647LL || dq > 2147483647LL)
+      far = 1; /* more than half a box away: never within vision_range */
+    dd[a] = (float)dq * d->sx[a];
+  }
+  if (far)
+    return;
+  float dist2 = dd[0] * dd[0] + dd[1] * dd[1];
+  float dist = sqrtf(dist2);
+  if (!(dist < vision_range) || dist == 0.0f)
+    return;
+  float amp = (2.0f * radii[j]) / dist;
+  amp = fminf(1.0f, amp);
+  float ux = dd[0] / dist, uy = dd[1] / dist;
+  float dot = ux * mx + uy * my;
+  dot = fminf(fmaxf(dot, -1.0f), 1.0f);
+  float an = or_acosf(dot);
+  float orth = ux * (-my) + uy * mx;
+  if (orth < 0.0f)
+    an = -an;
+  for (int k = 0; k < n_cones; ++k)
+    if (rims[k] < an && an < rims[k + 1])
+      acc[k * n_types + ti] += (int64_t)llrintf(amp * 4294967296.0f);
+}
+
+static void vision_director(const uint32_t *ang, int i, float *mx, float *my) {
+  float sn, cs;
+  or_sincos_turn(ang[i], &sn, &cs);
+  float nm = sqrtf(cs * cs + sn * sn);
+  *mx = cs / nm;
+  *my = sn / nm;
+}
+
+static void vision_store(const int64_t *acc, int ai, int nb, float *out) {
+  for (int k = 0; k < nb; ++k)
+    out[(size_t)ai * (size_t)nb + (size_t)k] = (float)acc[k] * 2.3283064365386963e-10f;
+}
+
 void or_vision_cone(const swarm_params_t *p, int n, const uint32_t *q,
                     const int32_t *img, const uint32_t *ang, const int *agents,
                     int n_agents, const float *radii, const int *types,
@@ -967,56 +1052,67 @@ void or_vision_cone(const swarm_params_t *p, int n, const uint32_t *q,
                     int n_types, const int *det, float *out) {
   derived_t d;
   derive(p, &d);
-  int64_t acc[SWARM_MAX_CONES * SWARM_MAX_DETECTED_TYPES];
+#pragma omp parallel for schedule(dynamic, 16)
   for (int ai = 0; ai < n_agents; ++ai) {
+    int64_t acc[SWARM_MAX_CONES * SWARM_MAX_DETECTED_TYPES];
     int i = agents[ai];
     memset(acc, 0, sizeof(acc));
-    float sn, cs;
-    or_sincos_turn(ang[i], &sn, &cs);
-    float nm = sqrtf(cs * cs + sn * sn);
-    float mx = cs / nm, my = sn / nm;
-    for (int j = 0; j < n; ++j) {
-      if (j == i)
-        continue;
-      int ti = -1;
-      for (int t = 0; t < n_types; ++t)
-        if (det[t] == types[j])
-          ti = t;
-      if (ti < 0)
-        continue;
-      /* unwrapped difference, no minimum image (subdivided_vision_cones.py:116) */
-      float dd[2];
-      int far = 0;
-      for (int a = 0; a < 2; ++a) {
-        int64_t dq = ((int64_t)(img[a * n + j] - img[a * n + i]) * (int64_t)4294967296LL) +
-                     ((int64_t)q[a * n + j] - (int64_t)q[a * n + i]);
-        if (dq < -2147483647LL || dq > 2147483647LL)
-          far = 1; /* more than half a box away: never within vision_range */
-        dd[a] = (float)dq * d.sx[a];
-      }
-      if (far)
-        continue;
-      float dist2 = dd[0] * dd[0] + dd[1] * dd[1];
-      float dist = sqrtf(dist2);
-      if (!(dist < vision_range) || dist == 0.0f)
-        continue;
-      float amp = (2.0f * radii[j]) / dist;
-      amp = fminf(1.0f, amp);
-      float ux = dd[0] / dist, uy = dd[1] / dist;
-      float dot = ux * mx + uy * my;
-      dot = fminf(fmaxf(dot, -1.0f), 1.0f);
-      float an = or_acosf(dot);
-      float orth = ux * (-my) + uy * mx;
-      if (orth < 0.0f)
-        an = -an;
-      for (int k = 0; k < n_cones; ++k)
-        if (rims[k] < an && an < rims[k + 1])
-          acc[k * n_types + ti] += (int64_t)llrintf(amp * 4294967296.0f);
-    }
-    for (int k = 0; k < n_cones * n_types; ++k)
-      out[(size_t)ai * (size_t)(n_cones * n_types) + (size_t)k] =
-          (float)acc[k] * 2.3283064365386963e-10f;
+    float mx, my;
+    vision_director(ang, i, &mx, &my);
+    for (int j = 0; j < n; ++j)
+      vision_pair(&d, n, q, img, i, j, mx, my, radii, types, vision_range, n_cones, rims,
+                  n_types, det, acc);
+    vision_store(acc, ai, n_cones * n_types, out);
   }
+}
+
+/*
+ * The same vision cones over a cell list (the CPU comparator of SURVEY
+ * 8(d)): cells of side >= vision_range over the folded positions, the 3 x 3
+ * cells around each agent (periodic).  A colloid within vision_range of the
+ * agent by its unwrapped difference is within vision_range by the minimum
+ * image too (vision_range < L / 2), so it lies in those cells; the bins are
+ * int64 sums, so the result has the bits of or_vision_cone.  Returns
+ * SWARM_EINVAL when 2 vision_range >= the box (use or_vision_cone).
+ */
+int or_vision_cone_cells(const swarm_params_t *p, int n, const uint32_t *q,
+                         const int32_t *img, const uint32_t *ang, const int *agents,
+                         int n_agents, const float *radii, const int *types,
+                         float vision_range, int n_cones, const float *rims,
+                         int n_types, const int *det, float *out) {
+  if (!p->periodic || !(2.0 * vision_range < p->box[0]) || !(2.0 * vision_range < p->box[1]))
+    return SWARM_EINVAL;
+  derived_t d;
+  derive(p, &d);
+  celllist_t cl;
+  or_cell_grid(p, n, vision_range, &cl.lx, &cl.ly);
+  cl.ncell = 1 << (cl.lx + cl.ly);
+  cl.start = (int *)malloc(sizeof(int) * (size_t)(cl.ncell + 1));
+  cl.list = (int *)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+  cl.cell = (int *)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+  cl_build(&cl, p, q, img, n);
+  const int ncx = 1 << cl.lx, ncy = 1 << cl.ly;
+  const int lox = ncx >= 3 ? -1 : 0, hix = ncx >= 3 ? 1 : ncx - 1;
+  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int ai = 0; ai < n_agents; ++ai) {
+    int64_t acc[SWARM_MAX_CONES * SWARM_MAX_DETECTED_TYPES];
+    int i = agents[ai];
+    memset(acc, 0, sizeof(acc));
+    float mx, my;
+    vision_director(ang, i, &mx, &my);
+    const int c = cl.cell[i], cx = c % ncx, cy = c / ncx;
+    for (int oy = loy; oy <= hiy; ++oy)
+      for (int ox = lox; ox <= hix; ++ox) {
+        const int cc = ((cy + oy + ncy) % ncy) * ncx + (cx + ox + ncx) % ncx;
+        for (int k = cl.start[cc]; k < cl.start[cc + 1]; ++k)
+          vision_pair(&d, n, q, img, i, cl.list[k], mx, my, radii, types, vision_range,
+                      n_cones, rims, n_types, det, acc);
+      }
+    vision_store(acc, ai, n_cones * n_types, out);
+  }
+  cl_free(&cl);
+  return SWARM_OK;
 }
 
 /* unwrapped position along axis a, fp64 */
@@ -1036,6 +1132,7 @@ void or_field_distance(const swarm_params_t *p, int n, const uint32_t *q,
   double src[3];
   for (int a = 0; a < 3; ++a)
     src[a] = source[a] / box_scale[a];
+#pragma omp parallel for schedule(static)
   for (int ai = 0; ai < n_agents; ++ai) {
     int i = agents[ai];
     float cur[3], prev[3];

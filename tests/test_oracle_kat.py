@@ -379,3 +379,54 @@ def test_refsem_pair_field_nonzero_size_quirk():
     # sensing type 0 from agent 0: d = [0 (self), 0 (coincident)] -> pad with col 0
     f = refsem.pair_field(pos, types, [0], 0, np.ones(3), lambda x: x + 10)
     assert f[0] == 10.0
+
+
+def test_cell_list_vision_cone_equals_all_pairs(oracle_mod):
+    """The CPU comparator's cell-list vision cone (bench.py cpu_baseline)
+    gives the bits of the reference's all-pairs loop, with mixed image
+    counters (unwrapped differences, no minimum image), several types and
+    one to eight OpenMP threads."""
+    rng = np.random.default_rng(5)
+    box = [60.0, 60.0, 60.0]
+    n = 700
+    pos = np.zeros((n, 3))
+    pos[:, :2] = rng.random((n, 2)) * 60.0 + rng.integers(-2, 3, (n, 2)) * 60.0
+    a = rng.random(n) * 2 * np.pi
+    dirs = np.stack([np.cos(a), np.sin(a), np.zeros(n)], 1)
+    p = oracle_mod.make_params(box, 1e-3, 1.0, 1.0, 1, [(1.0, 4.66, 6.21, 1.0, 1.0)])
+    st = oracle_mod.state_from_positions(pos, dirs, box)
+    assert np.count_nonzero(st["img"][:2]) > n
+    agents = np.arange(0, n, 3)
+    radii = rng.random(n).astype(np.float32) + 0.5
+    types = rng.integers(0, 3, n)
+    ref = oracle_mod.vision_cone(p, st, agents, radii, types, 9.0, np.pi / 2, 5, [0, 2])
+    assert np.count_nonzero(ref) > 50
+    for threads in (1, 8):
+        oracle_mod.set_threads(threads)
+        got = oracle_mod.vision_cone(p, st, agents, radii, types, 9.0, np.pi / 2, 5, [0, 2],
+                                     cells=True)
+        assert np.array_equal(got, ref)
+    oracle_mod.set_threads(1)
+
+
+def test_oracle_threads_do_not_change_dynamics(oracle_mod):
+    """OpenMP threads in the BD loop (bench.py's all-cores CPU leg) leave the
+    trajectory bit-identical."""
+    rng = np.random.default_rng(6)
+    box = [80.0, 80.0, 80.0]
+    n = 600
+    pos = np.zeros((n, 3))
+    pos[:, :2] = rng.random((n, 2)) * 80.0
+    a = rng.random(n) * 2 * np.pi
+    dirs = np.stack([np.cos(a), np.sin(a), np.zeros(n)], 1)
+    p = oracle_mod.make_params(box, 1e-3, 1.0239, 1.0239, 3, [(1.0, 4.66, 6.21, 1.0, 1.0)])
+    st = oracle_mod.state_from_positions(pos, dirs, box)
+    f = rng.random(n) * 10
+    t = rng.normal(size=n)
+    outs = []
+    for threads in (1, 6):
+        oracle_mod.set_threads(threads)
+        outs.append(oracle_mod.bd_run(p, st, np.zeros(n), f, t, 40)[0])
+    oracle_mod.set_threads(1)
+    for k in ("q", "img", "ang"):
+        assert np.array_equal(outs[0][k], outs[1][k])
