@@ -251,6 +251,29 @@ int swarm_engine_debug_phases(swarm_engine_t *e, uint64_t *out32);
  * at the wave's entry and end, its pair passes and pair count. */
 int swarm_engine_debug_wave_stamps(swarm_engine_t *e, uint64_t *out, int32_t n_words);
 
+/* Trajectory recording (espresso.py:1110-1159: _update_traj_holder at every
+ * write interval, chunks written to HDF5) without a host synchronisation, so
+ * it can sit inside a captured HIP graph.  swarm_engine_traj_ring allocates
+ * a ring of `capacity` entries for env `env` in host-pinned, device-mapped,
+ * coherent memory and returns its host address: bytes [0, 8) hold the count
+ * of entries recorded so far (uint64), entry k % capacity starts at byte
+ * 64 + (k % capacity) * entry_bytes.  swarm_engine_traj_record launches, on
+ * the engine stream, the copy of the env's state into the next slot (the
+ * slot index is a device counter, so graph replays fill successive slots)
+ * and then publishes the new count.  The caller drains entries
+ * [drained, count) with swarm_traj_entry_to_host, and must do so before
+ * `capacity` newer ones overwrite them.  Entry layout: uint64 step counter,
+ * uint32 q[D][N], int32 img[D][N], then uint32 ang[N] (2-D) or float
+ * dir[3][N] (3-D), then float vel[D][N]. */
+int swarm_engine_traj_ring(swarm_engine_t *e, int32_t capacity, int32_t env,
+                           void **host_ring, int64_t *entry_bytes);
+int swarm_engine_traj_record(swarm_engine_t *e);
+/* One ring entry -> fp64 [N][3] arrays exactly as swarm_engine_download_state
+ * converts the live state (unwrapped positions, directors, velocities) and
+ * its step counter; any output may be NULL.  Host only (no device access). */
+int swarm_traj_entry_to_host(const swarm_engine_t *e, const void *entry, double *pos,
+                             double *director, double *velocity, uint64_t *step);
+
 /* Total number of BD sub-steps integrated so far (the noise counter). */
 int64_t swarm_engine_step_count(const swarm_engine_t *e);
 

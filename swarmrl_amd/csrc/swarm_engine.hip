@@ -925,6 +925,52 @@ __global__ __launch_bounds__(256) void k_pairs(DevState st, const Derived* __res
   }
 }
 
+// ---------------------------------------------------- trajectory ring
+// One trajectory entry of env `env` (espresso.py:1110-1130: the state at a
+// write point) into slot count % cap of a host-pinned, device-mapped ring:
+// the step counter, then q[D][N], img[D][N], ang[N] (2-D) or dir3[3][N]
+// (3-D), vel[D][N].  The slot comes from a device counter, so captured
+// graphs record into successive slots on every replay; k_traj_bump
+// publishes the count after the entry is complete (stream order).
+__global__ __launch_bounds__(256) void k_traj_write(DevState st, int env,
+                                                    unsigned char* __restrict__ ring, int cap,
+                                                    size_t entry_bytes,
+                                                    const uint64_t* __restrict__ count,
+                                                    const uint64_t* __restrict__ ctl) {
+  const int N = st.n, D = st.dims;
+  const size_t M = (size_t)st.m;
+  const uint64_t slot = *count % (uint64_t)cap;
+  unsigned char* ent = ring + 64 + slot * entry_bytes;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) *reinterpret_cast<uint64_t*>(ent) = ctl[0];
+  if (i >= N) return;
+  const size_t gi = (size_t)env * N + i;
+  uint32_t* w = reinterpret_cast<uint32_t*>(ent + 8);
+  for (int a = 0; a < D; ++a) w[(size_t)a * N + i] = st.q[a * M + gi];
+  w += (size_t)D * N;
+  for (int a = 0; a < D; ++a) w[(size_t)a * N + i] = (uint32_t)st.img[a * M + gi];
+  w += (size_t)D * N;
+  if (D == 3) {
+    float* f = reinterpret_cast<float*>(w);
+    for (int a = 0; a < 3; ++a) f[(size_t)a * N + i] = st.dir3[a * M + gi];
+    w += (size_t)3 * N;
+  } else {
+    w[i] = st.ang[gi];
+    w += N;
+  }
+  float* v = reinterpret_cast<float*>(w);
+  for (int a = 0; a < D; ++a) v[(size_t)a * N + i] = st.vel[a * M + gi];
+}
+
+__global__ void k_traj_bump(uint64_t* __restrict__ count, unsigned char* __restrict__ ring) {
+  if (threadIdx.x == 0) {
+    const uint64_t c = *count + 1;
+    *count = c;
+    __threadfence_system();
+    *reinterpret_cast<volatile uint64_t*>(ring) = c;
+  }
+}
+
 }  // namespace
 
 // =================================================================== C ABI
@@ -940,6 +986,12 @@ struct swarm_engine {
   double* d_box = nullptr;
   uint64_t* d_step = nullptr;
   uint32_t* d_arrive = nullptr;
+  // trajectory ring (swarm_engine_traj_ring): host-pinned, device-mapped
+  unsigned char* traj_host = nullptr;
+  unsigned char* traj_dev = nullptr;
+  uint64_t* d_traj_count = nullptr;
+  int traj_cap = 0, traj_env = 0;
+  size_t traj_entry = 0;
   // observable grid scratch
   int32_t* d_start = nullptr;
   size_t start_cap = 0;
@@ -1493,6 +1545,8 @@ void swarm_engine_destroy(swarm_engine_t* e) {
   for (int k = 0; k < e->n_allocs; ++k) (void)hipFree(e->allocs[k]);
   if (e->d_start) (void)hipFree(e->d_start);
   if (e->d_pairs) (void)hipFree(e->d_pairs);
+  if (e->traj_host) (void)hipHostFree(e->traj_host);
+  if (e->d_traj_count) (void)hipFree(e->d_traj_count);
   delete e;
 }
 
@@ -1737,6 +1791,88 @@ int swarm_engine_window_stats(swarm_engine_t* e, int32_t* fallback, int32_t* wav
     HIP_TRY(hipMemcpyAsync(waves, e->sc.env_waves, E * sizeof(int32_t), hipMemcpyDeviceToHost,
                            e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
+  return SWARM_OK;
+}
+
+// ---------------------------------------------------- trajectory ring
+static size_t traj_entry_bytes(int n, int dims) {
+  const size_t b = 8 + 4 * (size_t)n * (size_t)(3 * dims + (dims == 3 ? 3 : 1));
+  return (b + 255) & ~(size_t)255;
+}
+
+int swarm_engine_traj_ring(swarm_engine_t* e, int32_t capacity, int32_t env, void** host_ring,
+                           int64_t* entry_bytes) {
+  if (!e || !host_ring || !entry_bytes) return fail(SWARM_EINVAL, "null argument");
+  if (capacity < 1 || env < 0 || env >= e->n_envs)
+    return fail(SWARM_EINVAL, "trajectory ring: capacity >= 1 and 0 <= env < n_envs");
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (e->traj_host) {
+    HIP_TRY(hipHostFree(e->traj_host));
+    e->traj_host = e->traj_dev = nullptr;
+  }
+  if (!e->d_traj_count) HIP_TRY(hipMalloc(&e->d_traj_count, sizeof(uint64_t)));
+  HIP_TRY(hipMemset(e->d_traj_count, 0, sizeof(uint64_t)));
+  const size_t eb = traj_entry_bytes(e->n, e->params.n_dims);
+  const size_t bytes = 64 + eb * (size_t)capacity;
+  void* h = nullptr;
+  HIP_TRY(hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(h, 0, bytes);
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+    (void)hipHostFree(h);
+    return fail(SWARM_EDEVICE, "hipHostGetDevicePointer failed");
+  }
+  e->traj_host = reinterpret_cast<unsigned char*>(h);
+  e->traj_dev = reinterpret_cast<unsigned char*>(d);
+  e->traj_cap = capacity;
+  e->traj_env = env;
+  e->traj_entry = eb;
+  *host_ring = h;
+  *entry_bytes = (int64_t)eb;
+  return SWARM_OK;
+}
+
+int swarm_engine_traj_record(swarm_engine_t* e) {
+  if (!e) return fail(SWARM_EINVAL, "null engine");
+  if (!e->traj_dev) return fail(SWARM_ESTATE, "no trajectory ring (swarm_engine_traj_ring)");
+  hipLaunchKernelGGL(k_traj_write, dim3((unsigned)((e->n + 255) / 256)), dim3(256), 0, e->stream,
+                     e->st, e->traj_env, e->traj_dev, e->traj_cap, e->traj_entry,
+                     e->d_traj_count, e->d_step);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_traj_bump, dim3(1), dim3(64), 0, e->stream, e->d_traj_count, e->traj_dev);
+  HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+
+int swarm_traj_entry_to_host(const swarm_engine_t* e, const void* entry, double* pos,
+                             double* director, double* velocity, uint64_t* step) {
+  if (!e || !entry) return fail(SWARM_EINVAL, "null argument");
+  const int N = e->n, D = e->params.n_dims;
+  const unsigned char* b = reinterpret_cast<const unsigned char*>(entry);
+  if (step) std::memcpy(step, b, 8);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(b + 8);
+  const int32_t* img = reinterpret_cast<const int32_t*>(q + (size_t)D * N);
+  const uint32_t* ang = reinterpret_cast<const uint32_t*>(img + (size_t)D * N);
+  const float* d3 = reinterpret_cast<const float*>(ang);
+  const float* vel = reinterpret_cast<const float*>(ang + (D == 3 ? (size_t)3 * N : (size_t)N));
+  for (size_t g = 0; g < (size_t)N; ++g) {  // as swarm_engine_download_state
+    if (pos)
+      for (int a = 0; a < 3; ++a)
+        pos[3 * g + a] = a < D ? ((double)img[a * N + g] + (double)q[a * N + g] / kTwo32) *
+                                     e->params.box[a]
+                               : 0.0;
+    if (director && D == 3) {
+      for (int a = 0; a < 3; ++a) director[3 * g + a] = d3[a * N + g];
+    } else if (director) {
+      float so, co;
+      host_sincos_turn(ang[g], &so, &co);
+      director[3 * g + 0] = co;
+      director[3 * g + 1] = so;
+      director[3 * g + 2] = 0.0;
+    }
+    if (velocity)
+      for (int a = 0; a < 3; ++a) velocity[3 * g + a] = a < D ? vel[a * N + g] : 0.0;
+  }
   return SWARM_OK;
 }
 

@@ -284,6 +284,9 @@ class SwarmEngine(Engine):
         self._side_stream = None
         self._prebuild_pending = None
         self.traj_holder = None
+        self._ring = None  # device trajectory ring (_init_traj_ring)
+        self._steps_run = 0  # BD sub-steps launched (= the device step counter)
+        self._time_offset = 0.0
         self.write_idx = 0
         self.slice_idx = 0
         self.step_idx = 0
@@ -707,19 +710,100 @@ class SwarmEngine(Engine):
         )
         self.write_idx = 0
         self.h5_time_steps_written = 0
+        self._init_traj_ring()
+
+    def _init_traj_ring(self):
+        """Device trajectory recording (swarm_engine_traj_ring): each write
+        point copies env 0's state into a host-pinned ring from the engine
+        stream, with no host synchronisation, so writes can sit inside a
+        captured episode graph; the host drains the ring into traj_holder
+        (eagerly after each write when not capturing, as the reference's
+        _update_traj_holder; otherwise at flush_trajectory / finalize)."""
+        self._ring = None
+        if self._native is None or len(self.colloids) == 0 or \
+                os.environ.get("SWARMRL_AMD_DEVICE_TRAJ", "1") == "0":
+            return
+        host = ctypes.c_void_p()
+        eb = ctypes.c_int64()
+        entry_bytes = 8 + 4 * self.n_particles * (3 * self.n_dims + (3 if self.n_dims == 3 else 1))
+        cap = max(16, min(2 * int(self.write_chunk_size), (256 << 20) // max(entry_bytes, 1)))
+        self._native.bind_stream()
+        self._native.call("swarm_engine_traj_ring", int(cap), 0, ctypes.byref(host),
+                          ctypes.byref(eb))
+        if not host.value:  # a backend without the ring: host-path writes
+            return
+        self._ring = {"ptr": host.value, "cap": cap, "entry": eb.value, "drained": 0,
+                      "count": np.ctypeslib.as_array((ctypes.c_uint64 * 1).from_address(host.value))}
+        self._time_offset = self.system.time - self._steps_run * self._time_step
 
     def _update_traj_holder(self):
         """espresso.py:1110-1130 (env 0)."""
         if len(self.colloids) == 0:
             logger.warning("No colloids in the system. Not writing to hdf5")
             return
+        if self._ring is not None:
+            # Times = step * dt + offset: a replayed graph records at the
+            # device step counter, which the host does not see
+            self._time_offset = self.system.time - self._steps_run * self._time_step
+            self._native.bind_stream()
+            self._native.call("swarm_engine_traj_record")
+            if not torch.cuda.is_current_stream_capturing():
+                self.drain_trajectory(block=True)
+            return
         h = self._host()
-        self.traj_holder["Times"].append(np.array([self.system.time])[:, np.newaxis])
+        self._append_traj(self.system.time, h["pos"][0].copy(), h["vel"][0].copy(),
+                          h["dir"][0].copy())
+
+    def _append_traj(self, time, pos, vel, dirs):
+        self.traj_holder["Times"].append(np.array([time])[:, np.newaxis])
         self.traj_holder["Ids"].append(np.arange(self.n_particles)[:, np.newaxis])
         self.traj_holder["Types"].append(np.asarray(self._types_list)[:, np.newaxis])
-        self.traj_holder["Unwrapped_Positions"].append(h["pos"][0].copy())
-        self.traj_holder["Velocities"].append(h["vel"][0].copy())
-        self.traj_holder["Directors"].append(h["dir"][0].copy())
+        self.traj_holder["Unwrapped_Positions"].append(pos)
+        self.traj_holder["Velocities"].append(vel)
+        self.traj_holder["Directors"].append(dirs)
+
+    def drain_trajectory(self, block: bool = True) -> int:
+        """Move the ring entries recorded so far into traj_holder, writing a
+        chunk whenever write_chunk_size entries are held (espresso.py:
+        1278-1285).  block=False reads what the device has published without
+        waiting (entries of work still queued stay for a later call).
+        Returns the number of entries drained."""
+        ring = self._ring
+        if ring is None or self.traj_holder is None:
+            return 0
+        if block:
+            torch.cuda.current_stream().synchronize()
+        count = int(ring["count"][0])
+        start = ring["drained"]
+        if count - start > ring["cap"]:
+            raise RuntimeError(
+                f"trajectory ring overflow: {count - start} entries since the last drain, "
+                f"capacity {ring['cap']} (drain more often)")
+        N = self.n_particles
+        step = np.zeros(1, np.uint64)
+        for k in range(start, count):
+            addr = ring["ptr"] + 64 + (k % ring["cap"]) * ring["entry"]
+            pos = np.zeros((N, 3))
+            dirs = np.zeros((N, 3))
+            vel = np.zeros((N, 3))
+            self._native.call("swarm_traj_entry_to_host", ctypes.c_void_p(addr), pos.ctypes.data,
+                              dirs.ctypes.data, vel.ctypes.data, step.ctypes.data)
+            self._append_traj(self._time_offset + int(step[0]) * self._time_step, pos, vel, dirs)
+            if len(self.traj_holder["Times"]) >= self.write_chunk_size:
+                self._write_traj_chunk_to_file()
+                for val in self.traj_holder.values():
+                    val.clear()
+        if int(ring["count"][0]) - start > ring["cap"]:  # overwritten while being read
+            raise RuntimeError("trajectory ring overflow while draining (drain more often)")
+        ring["drained"] = count
+        return count - start
+
+    def flush_trajectory(self):
+        """Drain the device ring and write everything held to the file."""
+        self.drain_trajectory(block=True)
+        self._write_traj_chunk_to_file()
+        for val in self.traj_holder.values():
+            val.clear()
 
     def _write_traj_chunk_to_file(self):
         """espresso.py:1132-1159."""
@@ -894,6 +978,7 @@ class SwarmEngine(Engine):
         self._native.bind_stream()
         self._native.call("swarm_engine_integrate", int(n_steps))
         self.system.time += n_steps * self._time_step
+        self._steps_run += n_steps
         self._host_cache = None
 
     def integrate(self, n_slices, force_model=None):
@@ -913,7 +998,7 @@ class SwarmEngine(Engine):
             if self.step_idx == self.params.steps_per_write_interval * self.write_idx:
                 self._update_traj_holder()
                 self.write_idx += 1
-                if len(self.traj_holder["Times"]) >= self.write_chunk_size:
+                if len(self.traj_holder["Times"]) >= self.write_chunk_size:  # host path
                     self._write_traj_chunk_to_file()
                     for val in self.traj_holder.values():
                         val.clear()
@@ -945,6 +1030,7 @@ class SwarmEngine(Engine):
         """Write the last trajectory chunk (espresso.py:1310-1318)."""
         if self.traj_holder is None:
             return
+        self.drain_trajectory(block=True)
         self._write_traj_chunk_to_file()
         for val in self.traj_holder.values():
             val.clear()
