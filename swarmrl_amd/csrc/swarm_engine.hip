@@ -911,8 +911,12 @@ __global__ __launch_bounds__(256) void k_pairs(DevState st, const Derived* __res
         const int j = oo[jj];
         if (j <= i) continue;
         const size_t gj = (size_t)env * N + j;
-        const float rx = (float)(int32_t)(st.q[gj] - qxi) * d->sx[0];
-        const float ry = (float)(int32_t)(st.q[M + gj] - qyi) * d->sx[1];
+        // minimum image in a periodic box, else the unwrapped difference
+        // (the grid search wraps either way: a pair within cutoff < L / 2 is
+        // within it by the minimum image too)
+        const bool per = d->periodic != 0;
+        const float rx = swarm::pair_disp(st.q[gj], st.img[gj], qxi, st.img[gi], d->sx[0], per);
+        const float ry = swarm::pair_disp(st.q[M + gj], st.img[M + gj], qyi, st.img[M + gi], d->sx[1], per);
         if (rx * rx + ry * ry < cut2) {
           const int slot = atomicAdd(count, 1);
           if (slot < max_pairs) {
@@ -1340,8 +1344,6 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   *out = nullptr;
   if (params->n_dims != 2 && params->n_dims != 3)
     return fail(SWARM_EINVAL, "n_dims must be 2 or 3");
-  if (!params->periodic)
-    return fail(SWARM_EINVAL, "non-periodic boxes are not implemented on the GPU in this build");
   if (n_envs < 1 || n_particles < 1) return fail(SWARM_EINVAL, "n_envs and n_particles must be >= 1");
   if (params->n_species < 1 || params->n_species > kMaxSpecies)
     return fail(SWARM_EINVAL, "n_species out of range");
@@ -1383,7 +1385,9 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   // build grid; otherwise every window runs on the global path
   e->big_build = build_is_big(n_particles);
   e->sc.pair_cap = build_pair_cap(n_particles, e->big_build);
-  e->cluster_path = !three_d && e->sc.pair_cap >= n_particles && n_particles < 65536 &&
+  // non-periodic boxes (no minimum image, edge cells) run on the global path
+  e->cluster_path = !three_d && params->periodic && e->sc.pair_cap >= n_particles &&
+                    n_particles < 65536 &&
                     swarm::build_lds_words_big(n_particles) * 4 <= kMaxLds &&
                     (size_t)(16 + (1 << (e->lxb + e->lyb)) + 1) * 4 <= kMaxLds &&
                     (1 << e->lxb) >= 3 && (1 << e->lyb) >= 3;

@@ -200,6 +200,23 @@ __device__ __forceinline__ int cell_index(uint32_t qx, uint32_t qy, int lx, int 
   return (cy << lx) | cx;
 }
 
+// Non-periodic boxes (MDParams.periodic = False, espresso.py:270; global
+// path only): the cell of a particle outside the box is the edge cell on its
+// side, and pair displacements are plain differences of the unwrapped
+// positions (no minimum image) -- the oracle's cell_of / pair_disp.
+__device__ __forceinline__ int cell_coord(uint32_t q, int32_t im, int l, bool periodic) {
+  const int v = l == 0 ? 0 : (int)(q >> (32 - l));
+  if (periodic) return v;
+  return im < 0 ? 0 : (im > 0 ? (1 << l) - 1 : v);
+}
+
+__device__ __forceinline__ float pair_disp(uint32_t qj, int32_t ij, uint32_t qi, int32_t ii,
+                                           float sx, bool periodic) {
+  if (periodic) return (float)(int32_t)(qj - qi) * sx;
+  const int64_t dq = (int64_t)(ij - ii) * 4294967296LL + ((int64_t)qj - (int64_t)qi);
+  return (float)dq * sx;
+}
+
 // Exclusive scan of data[0..n) in LDS by the whole block; data[n] = total.
 __device__ inline void block_exclusive_scan(int32_t* data, int n, int32_t* wave_sums) {
   const int T = blockDim.x;
@@ -516,17 +533,21 @@ __device__ void block_global_run(const Derived* __restrict__ d, const DevState& 
   const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
   const float sx0 = d->sx[0], sx1 = d->sx[1];
   const float eps24 = d->eps24;
+  const bool per = d->periodic != 0;
+  auto cell_of = [&](size_t gi) {
+    return (cell_coord(st.q[M + gi], st.img[M + gi], ly, per) << lx) |
+           cell_coord(st.q[gi], st.img[gi], lx, per);
+  };
   for (int s = 0; s < n_steps; ++s) {
     for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
     __syncthreads();
-    for (int i = tid; i < N; i += T)
-      atomicAdd(&cnt[cell_index(st.q[base + i], st.q[M + base + i], lx, ly)], 1);
+    for (int i = tid; i < N; i += T) atomicAdd(&cnt[cell_of(base + i)], 1);
     __syncthreads();
     block_exclusive_scan(cnt, ncell, wave_sums);
     __syncthreads();
     for (int i = tid; i < N; i += T) {
       const uint32_t qx = st.q[base + i], qy = st.q[M + base + i];
-      const int pos = atomicAdd(&cnt[cell_index(qx, qy, lx, ly)], 1);
+      const int pos = atomicAdd(&cnt[cell_of(base + i)], 1);
       sc.sqx[base + pos] = qx;
       sc.sqy[base + pos] = qy;
       sc.sidx[base + pos] = i;
@@ -543,19 +564,25 @@ __device__ void block_global_run(const Derived* __restrict__ d, const DevState& 
       p.an = st.ang[gi];
       const int si = st.species[i];
       int64_t ax = 0, ay = 0;
-      const int c0 = cell_index(p.qx, p.qy, lx, ly);
+      const int c0 = cell_of(gi);
       const int cx = c0 & (ncx - 1), cy = c0 >> lx;
       for (int oy = loy; oy <= hiy; ++oy) {
+        if (!per && (cy + oy < 0 || cy + oy >= ncy)) continue;
         const int y = (cy + oy + ncy) & (ncy - 1);
         for (int ox = lox; ox <= hix; ++ox) {
+          if (!per && (cx + ox < 0 || cx + ox >= ncx)) continue;
           const int x = (cx + ox + ncx) & (ncx - 1);
           const int cc = (y << lx) | x;
           const int jb = cc ? cnt[cc - 1] : 0, je = cnt[cc];
           for (int jj = jb; jj < je; ++jj) {
             const int j = sc.sidx[base + jj];
             if (j == i) continue;
-            const float rx = (float)(int32_t)(sc.sqx[base + jj] - p.qx) * sx0;
-            const float ry = (float)(int32_t)(sc.sqy[base + jj] - p.qy) * sx1;
+            const float rx = per ? (float)(int32_t)(sc.sqx[base + jj] - p.qx) * sx0
+                                 : pair_disp(sc.sqx[base + jj], st.img[base + j], p.qx, p.ix, sx0,
+                                             false);
+            const float ry = per ? (float)(int32_t)(sc.sqy[base + jj] - p.qy) * sx1
+                                 : pair_disp(sc.sqy[base + jj], st.img[M + base + j], p.qy, p.iy,
+                                             sx1, false);
             const int pk = si * kMaxSpecies + st.species[j];
             pair_force(pt->cut2[pk], pt->sig6[pk], eps24, rx, ry, ax, ay);
           }
@@ -795,7 +822,8 @@ __global__ __launch_bounds__(1024) void k_global(const Derived* __restrict__ d, 
   int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
   int32_t* cnt = wave_sums + 16;
   const uint64_t step0 = sd_mode ? 0ull : *step_ctr;
-  if (global_lds_extra_words(st.n, st.dims, 1 << (lx + ly)) && blockDim.x == 1024)
+  // the LDS variant assumes a periodic box (minimum image, folded cells)
+  if (global_lds_extra_words(st.n, st.dims, 1 << (lx + ly)) && blockDim.x == 1024 && d->periodic)
     block_global_run_lds(d, st, blockIdx.x, n_steps, step0, lx, ly, sd_mode != 0, g, md, cnt,
                          wave_sums, cnt + (1 << (lx + ly)) + 1, &pt);
   else

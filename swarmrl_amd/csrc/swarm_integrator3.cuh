@@ -100,19 +100,23 @@ __device__ void block_global_run3(const Derived* __restrict__ d, const DevState&
   const float sx[3] = {d->sx[0], d->sx[1], d->sx[2]};
   const float eps24 = d->eps24;
   const bool noisy = d->noisy != 0;
+  const bool per = d->periodic != 0;  // non-periodic: edge cells, unwrapped differences
+  auto cell_of3 = [&](size_t gi) {
+    return (((cell_coord(st.q[2 * M + gi], st.img[2 * M + gi], lz, per) << ly) |
+             cell_coord(st.q[M + gi], st.img[M + gi], ly, per))
+            << lx) |
+           cell_coord(st.q[gi], st.img[gi], lx, per);
+  };
   for (int s = 0; s < n_steps; ++s) {
     for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
     __syncthreads();
-    for (int i = tid; i < N; i += T)
-      atomicAdd(&cnt[cell_index3(st.q[base + i], st.q[M + base + i], st.q[2 * M + base + i], lx,
-                                 ly, lz)],
-                1);
+    for (int i = tid; i < N; i += T) atomicAdd(&cnt[cell_of3(base + i)], 1);
     __syncthreads();
     block_exclusive_scan(cnt, ncell, wave_sums);
     __syncthreads();
     for (int i = tid; i < N; i += T) {
       const uint32_t qx = st.q[base + i], qy = st.q[M + base + i], qz = st.q[2 * M + base + i];
-      const int pos = atomicAdd(&cnt[cell_index3(qx, qy, qz, lx, ly, lz)], 1);
+      const int pos = atomicAdd(&cnt[cell_of3(base + i)], 1);
       sc.sqx[base + pos] = qx;
       sc.sqy[base + pos] = qy;
       sc.sqz[base + pos] = qz;
@@ -134,22 +138,33 @@ __device__ void block_global_run3(const Derived* __restrict__ d, const DevState&
       const bool first = st.reuse && s == 0 && !sd_mode;
       const int si = st.species[i];
       int64_t acc[3] = {0, 0, 0};
-      const int c0 = cell_index3(q[0], q[1], q[2], lx, ly, lz);
+      const int c0 = cell_of3(gi);
       const int cc[3] = {c0 & (nc[0] - 1), (c0 >> lx) & (nc[1] - 1), c0 >> (lx + ly)};
       for (int oz = lo[2]; oz <= hi[2]; ++oz) {
+        if (!per && (cc[2] + oz < 0 || cc[2] + oz >= nc[2])) continue;
         const int z = (cc[2] + oz + nc[2]) & (nc[2] - 1);
         for (int oy = lo[1]; oy <= hi[1]; ++oy) {
+          if (!per && (cc[1] + oy < 0 || cc[1] + oy >= nc[1])) continue;
           const int y = (cc[1] + oy + nc[1]) & (nc[1] - 1);
           for (int ox = lo[0]; ox <= hi[0]; ++ox) {
+            if (!per && (cc[0] + ox < 0 || cc[0] + ox >= nc[0])) continue;
             const int x = (cc[0] + ox + nc[0]) & (nc[0] - 1);
             const int cell = (((z << ly) | y) << lx) | x;
             const int jb = cell ? cnt[cell - 1] : 0, je = cnt[cell];
             for (int jj = jb; jj < je; ++jj) {
               const int j = sc.sidx[base + jj];
               if (j == i) continue;
-              const float rx = (float)(int32_t)(sc.sqx[base + jj] - q[0]) * sx[0];
-              const float ry = (float)(int32_t)(sc.sqy[base + jj] - q[1]) * sx[1];
-              const float rz = (float)(int32_t)(sc.sqz[base + jj] - q[2]) * sx[2];
+              const size_t gj = base + j;
+              float rx, ry, rz;
+              if (per) {
+                rx = (float)(int32_t)(sc.sqx[base + jj] - q[0]) * sx[0];
+                ry = (float)(int32_t)(sc.sqy[base + jj] - q[1]) * sx[1];
+                rz = (float)(int32_t)(sc.sqz[base + jj] - q[2]) * sx[2];
+              } else {
+                rx = pair_disp(sc.sqx[base + jj], st.img[gj], q[0], im[0], sx[0], false);
+                ry = pair_disp(sc.sqy[base + jj], st.img[M + gj], q[1], im[1], sx[1], false);
+                rz = pair_disp(sc.sqz[base + jj], st.img[2 * M + gj], q[2], im[2], sx[2], false);
+              }
               const int pk = si * kMaxSpecies + st.species[j];
               pair_force3(pt->cut2[pk], pt->sig6[pk], eps24, rx, ry, rz, acc[0], acc[1],
                           acc[2]);

@@ -637,8 +637,6 @@ class SwarmEngine(Engine):
             raise ValueError("integrator_type must be one of ['brownian', 'langevin']")
         if self.params.thermostat_type == "langevin":
             raise NotImplementedError("the Langevin integrator is not implemented in this build")
-        if not self.params.periodic:
-            raise NotImplementedError("non-periodic boxes are not implemented on the GPU yet")
 
         p = _capi.SwarmParams()
         p.n_dims = self.n_dims

@@ -16,10 +16,10 @@ def species_list(kT_scale=1.0):
     return [(1.0, 4.6595, 6.2126, 1.0358e-6, 4.143e-7), (0.7, 3.2617, 2.1309, 3.55e-7, 7.0e-8)]
 
 
-def capi_params(box, dt, kT, eps, seed, species, n_dims=2, reuse=False):
+def capi_params(box, dt, kT, eps, seed, species, n_dims=2, reuse=False, periodic=True):
     p = _capi.SwarmParams()
     p.n_dims = n_dims
-    p.periodic = 1
+    p.periodic = 1 if periodic else 0
     p.reuse_forces = 1 if reuse else 0
     for a in range(3):
         p.box[a] = float(box[a])
@@ -35,14 +35,15 @@ def capi_params(box, dt, kT, eps, seed, species, n_dims=2, reuse=False):
 
 class Harness:
     def __init__(self, box, dt, kT, eps, seed, species, sp_of, n_envs=1, n_dims=2,
-                 reuse=False):
+                 reuse=False, periodic=True):
         self.box = box
         self.n = len(sp_of)
         self.E = n_envs
         self.dims = n_dims
         self.sp = np.asarray(sp_of, dtype=np.int32)
-        self.cp = capi_params(box, dt, kT, eps, seed, species, n_dims, reuse)
-        self.op = oracle.make_params(box, dt, kT, eps, seed, species, n_dims=n_dims)
+        self.cp = capi_params(box, dt, kT, eps, seed, species, n_dims, reuse, periodic)
+        self.op = oracle.make_params(box, dt, kT, eps, seed, species, periodic=periodic,
+                                     n_dims=n_dims)
         self.native = _NativeEngine(self.cp, n_envs, self.sp)
 
     def upload(self, states):

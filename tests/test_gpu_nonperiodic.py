@@ -1,0 +1,145 @@
+"""
+Non-periodic boxes (MDParams.periodic = False -> system.periodicity =
+[False] * 3, espresso.py:270): no minimum image -- pair forces act along the
+plain difference of the unwrapped positions -- and particles may leave the
+box (they stay in the edge cells of the pair search).  These engines run on
+the global path; bit-exact against the oracle's restatement (cell list with
+edge cells in 2-D, all pairs in 3-D), including particles that start outside
+the box and pairs that straddle its faces.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    from swarmrl_amd import _capi
+
+    _capi.require_gpu()
+    torch.cuda.set_device(0)
+
+
+def _eq(a, b, keys=("q", "img", "ang")):
+    for k in keys:
+        assert np.array_equal(a[k], b[k]), k
+
+
+def _straddling(rng, n, L):
+    """Colloids spread over [-0.1 L, 1.1 L) (some outside the box), plus
+    pairs just across the x = 0 and y = L faces: close in the unwrapped
+    positions, far apart in the minimum image sense no more."""
+    pos = np.zeros((n, 3))
+    pos[:, :2] = -0.1 * L + rng.random((n, 2)) * 1.2 * L
+    k = 0
+    for y in np.linspace(0.2 * L, 0.8 * L, 6):
+        pos[k, :2] = (-0.8, y)
+        pos[k + 1, :2] = (0.8, y + 0.3)
+        k += 2
+    for x in np.linspace(0.2 * L, 0.8 * L, 6):
+        pos[k, :2] = (x, L - 0.9)
+        pos[k + 1, :2] = (x + 0.2, L + 0.8)
+        k += 2
+    a = 2 * np.pi * rng.random(n)
+    return pos, np.stack([np.cos(a), np.sin(a), np.zeros(n)], 1)
+
+
+@pytest.mark.parametrize("kT", [0.0, 1.0239])
+def test_nonperiodic_2d_bit_exact(kT):
+    from gpu_harness import Harness, species_list
+
+    rng = np.random.default_rng(41)
+    L = 50.0
+    box = [L, L, L]
+    n = 400
+    sp = rng.integers(0, 2, n)
+    pos, dirs = _straddling(rng, n, L)
+    st = oracle.state_from_positions(pos, dirs, box)
+    assert np.count_nonzero(st["img"][:2]) > 20
+    h = Harness(box, 1e-3, kT, 1.0239, 8, species_list(), sp, periodic=False)
+    h.upload([st])
+    h.sd(200)
+    st = oracle.sd_run(h.op, st, sp, 200)[0]
+    _eq(h.download()[0], st)
+    step = 0
+    for nsteps in (60, 40):
+        f = rng.normal(size=n).astype(np.float32) * 20
+        t = rng.normal(size=n).astype(np.float32) * 5
+        h.set_actions(f, t)
+        h.integrate(nsteps)
+        st, vel, _ = oracle.bd_run(h.op, st, sp, f, t, nsteps, step0=step)
+        step += nsteps
+        _eq(h.download()[0], st)
+        assert np.array_equal(h.velocities(), vel)
+    # the semantics is observable: the periodic restatement differs
+    pp = oracle.make_params(box, 1e-3, kT, 1.0239, 8, species_list(), periodic=True)
+    alt = oracle.sd_run(pp, oracle.state_from_positions(pos, dirs, box), sp, 200)[0]
+    assert not np.array_equal(alt["q"], oracle.sd_run(h.op, oracle.state_from_positions(
+        pos, dirs, box), sp, 200)[0]["q"])
+
+
+def test_nonperiodic_3d_bit_exact():
+    from gpu_harness import Harness, species_list
+
+    rng = np.random.default_rng(42)
+    L = 20.0
+    box = [L, L, L]
+    n = 150
+    sp = rng.integers(0, 2, n)
+    pos = -0.1 * L + rng.random((n, 3)) * 1.2 * L
+    pos[0] = (-0.7, 5.0, 5.0)
+    pos[1] = (0.7, 5.2, 5.1)
+    d = rng.normal(size=(n, 3))
+    st = oracle.state3_from_positions(pos, d, box)
+    h = Harness(box, 1e-3, 1.0239, 1.0239, 4, species_list(), sp, n_dims=3, periodic=False)
+    h.upload([st])
+    h.sd(100)
+    st, _ = oracle.sd_run3(h.op, st, sp, 100)
+    _eq(h.download()[0], st, ("q", "img", "dir"))
+    f = rng.normal(size=n).astype(np.float32) * 10
+    tq = rng.normal(size=(3, n)).astype(np.float32) * 3
+    h.set_torque_xy(tq[:2])
+    h.set_actions(f, tq[2])
+    h.integrate(50)
+    ref, vel, _ = oracle.bd_run3(h.op, st, sp, f, tq, 50)
+    _eq(h.download()[0], ref, ("q", "img", "dir"))
+    assert np.array_equal(h.velocities(), vel)
+
+
+def test_nonperiodic_engine_and_neighbor_pairs(tmp_path):
+    """Through the product API: MDParams(periodic=False) builds, integrates,
+    and neighbour pairs follow the unwrapped distance (no minimum image)."""
+    import ctypes
+
+    from swarmrl_amd.agents import dummy_models
+    from swarmrl_amd.engine import MDParams, SwarmEngine
+    from swarmrl_amd.force_functions import ForceFunction
+    from swarmrl_amd.units import UnitRegistry
+
+    ureg = UnitRegistry()
+    p = MDParams(ureg=ureg, box_length=ureg.Quantity([60.0] * 3, "micrometer"),
+                 time_step=ureg.Quantity(1e-3, "second"),
+                 time_slice=ureg.Quantity(0.05, "second"),
+                 write_interval=ureg.Quantity(0.05, "second"), periodic=False)
+    eng = SwarmEngine(p, n_dims=2, seed=3, out_folder=tmp_path)
+    eng.add_colloids(100, ureg.Quantity(1.0, "micrometer"),
+                     ureg.Quantity(np.array([30.0, 30.0, 0.0]), "micrometer"),
+                     ureg.Quantity(28.0, "micrometer"))
+    eng.integrate(3, ForceFunction({"0": dummy_models.ConstForce(3.0)}))
+    raw = eng.get_raw_state()
+    st = {"q": raw["q"][:, :100], "img": raw["img"][:, :100], "ang": raw["ang"][:100]}
+    op = oracle.make_params(eng._box, 1e-3, 1.0, 1.0, 1, [(1.0, 1.0, 1.0, 1.0, 1.0)],
+                            periodic=False)
+    ref = {tuple(x) for x in oracle.neighbor_pairs(op, st, 5.0)}
+    pairs = np.zeros((4096, 2), np.int32)
+    npairs = ctypes.c_int32()
+    eng._native.call("swarm_engine_neighbor_pairs", 0, ctypes.c_double(5.0), pairs.ctypes.data,
+                     4096, ctypes.byref(npairs))
+    got = {tuple(x) for x in pairs[:npairs.value]}
+    assert got == ref and len(ref) > 0
+    eng.finalize()
