@@ -1002,18 +1002,14 @@ static void vision_pair(const derived_t *d, int n, const uint32_t *q, const int3
       ti = t;
   if (ti < 0)
     return;
-  /* unwrapped difference, no minimum image (subdivided_vision_cones.py:116) */
+  /* unwrapped difference, no minimum image and no range limit
+   * (subdivided_vision_cones.py:116-121) */
   float dd[2];
-  int far = 0;
   for (int a = 0; a < 2; ++a) {
     int64_t dq = ((int64_t)(img[a * n + j] - img[a * n + i]) * (int64_t)4294967296LL) +
                  ((int64_t)q[a * n + j] - (int64_t)q[a * n + i]);
-    if (dq < -2147483647LL || dq > 2147483647LL)
-      far = 1; /* more than half a box away: never within vision_range */
     dd[a] = (float)dq * d->sx[a];
   }
-  if (far)
-    return;
   float dist2 = dd[0] * dd[0] + dd[1] * dd[1];
   float dist = sqrtf(dist2);
   if (!(dist < vision_range) || dist == 0.0f)

@@ -318,19 +318,28 @@ struct VisionLane {
 };
 
 // The in-range test of one candidate record (shared by both phases).
+// kAny: vision_range may reach half the box or more (the all-records scan):
+// every unwrapped separation is converted from int64.
+template <bool kAny = false>
 __device__ __forceinline__ bool vision_offsets(const VisionLane& L, const uint4& c0, float* dx,
                                                float* dy) {
   const int64_t dqx = ((int64_t)((int32_t)c0.z - L.ixi) * (int64_t)4294967296LL) +
                       ((int64_t)c0.x - (int64_t)L.qxi);
   const int64_t dqy = ((int64_t)((int32_t)c0.w - L.iyi) * (int64_t)4294967296LL) +
                       ((int64_t)c0.y - (int64_t)L.qyi);
-  // unwrapped separations beyond half a box are never within range
-  // (vision_range < L/2): skip them and convert the rest from int32, whose
-  // conversion is a single exact-rounding instruction.
-  if (dqx < -2147483647LL || dqx > 2147483647LL || dqy < -2147483647LL || dqy > 2147483647LL)
-    return false;
-  *dx = (float)(int32_t)dqx * L.sx0;
-  *dy = (float)(int32_t)dqy * L.sx1;
+  if (kAny) {
+    *dx = (float)dqx * L.sx0;
+    *dy = (float)dqy * L.sx1;
+  } else {
+    // unwrapped separations beyond half a box are never within range
+    // (vision_range < L/2): skip them and convert the rest from int32, whose
+    // conversion is a single exact-rounding instruction.
+    if (dqx < -2147483647LL || dqx > 2147483647LL || dqy < -2147483647LL ||
+        dqy > 2147483647LL)
+      return false;
+    *dx = (float)(int32_t)dqx * L.sx0;
+    *dy = (float)(int32_t)dqy * L.sx1;
+  }
   const float dist2 = *dx * *dx + *dy * *dy;
   // conservative pre-test on dist^2 (the exact test is on the fp32 sqrt)
   return dist2 < L.R * L.R * 1.0001f && dist2 != 0.0f;
@@ -347,11 +356,11 @@ __device__ __forceinline__ bool vision_near(const VisionLane& L, const uint4& c0
   return dist2 < L.R * L.R * 1.0001f && dist2 != 0.0f;
 }
 
-template <int NB>
+template <int NB, bool kAny = false>
 __device__ __forceinline__ void vision_hit(const VisionLane& L, const swarm_vision_params_t& vp,
                                            const uint4& c0, const uint4& c1, int64_t* acc) {
   float dx, dy;
-  if (!vision_offsets(L, c0, &dx, &dy)) return;
+  if (!vision_offsets<kAny>(L, c0, &dx, &dy)) return;
   const int ti = vision_rec_type(c1.y);
   if (ti < 0 || vision_rec_id(c1.y) == L.i) return;
   const float dist = swarm::sqrt_rn(dx * dx + dy * dy);
@@ -373,7 +382,7 @@ __device__ __forceinline__ void vision_hit(const VisionLane& L, const swarm_visi
 }
 
 // Cone arithmetic over a lane's listed hits, records fetched four at a time.
-template <int NB>
+template <int NB, bool kAny = false>
 __device__ __forceinline__ void vision_drain(const VisionLane& L, const swarm_vision_params_t& vp,
                                              const uint4* __restrict__ rec, size_t base,
                                              const uint32_t (*hits)[256], int nh, int64_t* acc) {
@@ -389,11 +398,14 @@ __device__ __forceinline__ void vision_drain(const VisionLane& L, const swarm_vi
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      if (k0 + u < nh) vision_hit<NB>(L, vp, c0[u], c1[u], acc);
+      if (k0 + u < nh) vision_hit<NB, kAny>(L, vp, c0[u], c1[u], acc);
   }
 }
 
-template <int NB, int G>
+// kAll: vision_range >= half the box (the reference has no range limit,
+// subdivided_vision_cones.py:116-121): every record of the env is a
+// candidate, tested on its unwrapped (int64) separation.
+template <int NB, int G, bool kAll = false>
 __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __restrict__ d,
                                                 swarm_vision_params_t vp, int lx, int ly,
                                                 const int32_t* __restrict__ start, VisionSorted vs,
@@ -445,7 +457,9 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
   for (int r = 0; r < 9; ++r) {
     const int oy = r / 3 - 1, ox = r % 3 - 1;
     int jb = 0, je = 0;
-    if (oy >= loy && oy <= hiy && ox >= lox && ox <= hix) {
+    if (kAll) {  // one range: all records
+      je = r == 0 ? N : 0;
+    } else if (oy >= loy && oy <= hiy && ox >= lox && ox <= hix) {
       const int y = (cy + oy + ncy) & (ncy - 1);
       const int x = (cx + ox + ncx) & (ncx - 1);
       const int cc = (y << lx) | x;
@@ -470,15 +484,17 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      if (f0 + u * G < total && vision_near(L, c0[u]))
+      float ddx, ddy;
+      if (f0 + u * G < total &&
+          (kAll ? vision_offsets<true>(L, c0[u], &ddx, &ddy) : vision_near(L, c0[u])))
         hits[nh++][threadIdx.x] = jj[u];
     }
     if (__any(nh > kVisionHits - 4)) {  // no room for four more: drain every lane's
-      vision_drain<NB>(L, vp, vs.rec, base, hits, nh, acc);
+      vision_drain<NB, kAll>(L, vp, vs.rec, base, hits, nh, acc);
       nh = 0;
     }
   }
-  vision_drain<NB>(L, vp, vs.rec, base, hits, nh, acc);
+  vision_drain<NB, kAll>(L, vp, vs.rec, base, hits, nh, acc);
 #pragma unroll
   for (int off = G / 2; off > 0; off >>= 1) {
 #pragma unroll
@@ -1918,8 +1934,8 @@ int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const 
     return fail(SWARM_ECAPACITY, "n_cones * n_types exceeds this build's limit (32)");
   if (n_agents <= 0) return SWARM_OK;
   if (e->n >= (1 << 24)) return fail(SWARM_ECAPACITY, "vision records hold particle ids < 2^24");
-  if (!(2.0 * vp->vision_range < std::min(e->params.box[0], e->params.box[1])))
-    return fail(SWARM_EINVAL, "vision_range must be below half the box length");
+  // a range of half the box or more: every record is a candidate (k_vision<.., kAll>)
+  const bool all = !(2.0 * vp->vision_range < std::min(e->params.box[0], e->params.box[1]));
   int lx, ly;
   cell_grid(e->params, e->n, (double)vp->vision_range, &lx, &ly);
   int rc = ensure_grid_scratch(e, lx, ly);
@@ -1940,6 +1956,24 @@ int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const 
   // bytes) and its VALU count, yet run 77 vs 63 us (rocprof): a workgroup
   // holds its LDS until its slowest wave ends, and the average residency
   // halves ("Vision cone").
+  if (all) {
+    const dim3 agrid((unsigned)((total * 16 + 255) / 256)), ablock(256);
+#define SWARM_VALL(NBV)                                                                         \
+  hipLaunchKernelGGL((k_vision<NBV, 16, true>), agrid, ablock, 0, e->stream, e->st, e->d_derived, \
+                     *vp, lx, ly, e->d_start, e->vs, n_agents, out, e->n_envs)
+    if (nb <= 4) {
+      SWARM_VALL(4);
+    } else if (nb <= 8) {
+      SWARM_VALL(8);
+    } else if (nb <= 16) {
+      SWARM_VALL(16);
+    } else {
+      SWARM_VALL(32);
+    }
+#undef SWARM_VALL
+    HIP_TRY(hipGetLastError());
+    return SWARM_OK;
+  }
   bool tiled = false;
   if (const char* ot = std::getenv("SWARMRL_AMD_VISION_TILE"))
     tiled = ot[0] == '1' && lx >= 3 && ly >= 3;

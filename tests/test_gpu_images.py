@@ -199,3 +199,40 @@ def test_engine_made_images_vision_and_field_bit_exact(tmp_path):
     assert np.array_equal(d_cur[0].cpu().numpy(), rc)
     assert np.array_equal(d_prev[0].cpu().numpy(), rp)
     del view
+
+
+@pytest.mark.parametrize("R", [20.0, 35.0, 130.0])
+def test_vision_range_beyond_half_box_bit_exact(R):
+    """The reference has no range limit and no minimum image
+    (subdivided_vision_cones.py:116-121): a vision range of half the box or
+    more scans every record of the env on its unwrapped separation (the
+    all-records variant of k_vision), bit-exact against the oracle, with
+    colloids several images away."""
+    from gpu_harness import Harness, species_list
+    from swarmrl_amd.engine import ops
+
+    rng = np.random.default_rng(22)
+    L = 40.0
+    box = [L, L, L]
+    n, E = 700, 2
+    types = rng.integers(0, 2, n)
+    h = Harness(box, 1e-3, 0.0, 1.0, 0, species_list(), np.zeros(n, int), n_envs=E)
+    states = []
+    for _ in range(E):
+        pos = np.zeros((n, 3))
+        pos[:, :2] = rng.random((n, 2)) * L + rng.integers(-3, 4, (n, 2)) * L
+        a = 2 * np.pi * rng.random(n)
+        dirs = np.stack([np.cos(a), np.sin(a), np.zeros(n)], 1)
+        states.append(oracle.state_from_positions(pos, dirs, box))
+    h.upload(states)
+    agents = np.arange(0, n, 2, dtype=np.int32)
+    radii = (0.5 + rng.random(n)).astype(np.float32)
+    dev = torch.device("cuda", 0)
+    vp = ops.vision_params(R, np.pi / 3, 4, [0, 1])
+    out = ops.vision_cone(h.native, E, torch.as_tensor(agents, device=dev),
+                          torch.as_tensor(radii, device=dev),
+                          torch.as_tensor(types.astype(np.int32), device=dev), vp).cpu().numpy()
+    for e in range(E):
+        ref = oracle.vision_cone(h.op, states[e], agents, radii, types, R, np.pi / 3, 4, [0, 1])
+        assert np.array_equal(out[e], ref)
+        assert np.count_nonzero(ref) > 100
