@@ -281,6 +281,8 @@ class SwarmEngine(Engine):
         # device path: prepare each window's build on a side stream while
         # the force model computes the slice's actions (see _prebuild)
         self.overlap_build = os.environ.get("SWARMRL_AMD_OVERLAP_BUILD", "1") != "0"
+        # fork the next slice's build right after the run (before the reward)
+        self.early_fork = os.environ.get("SWARMRL_AMD_EARLY_FORK", "1") != "0"
         self._side_stream = None
         self._prebuild_pending = None
         self.traj_holder = None
@@ -1007,7 +1009,7 @@ class SwarmEngine(Engine):
 
             if self.step_idx == self.params.steps_per_slice * self.slice_idx:
                 self.slice_idx += 1
-                if device_path and self.overlap_build:
+                if device_path and self.overlap_build and self._prebuild_pending is None:
                     self._prebuild(min(
                         self.params.steps_per_write_interval * self.write_idx - self.step_idx,
                         self.params.steps_per_slice * self.slice_idx - self.step_idx))
@@ -1020,6 +1022,14 @@ class SwarmEngine(Engine):
             steps_to_next = min(steps_to_next_write, steps_to_next_slice)
 
             self._run(steps_to_next)
+            nxt = self.step_idx + steps_to_next
+            if (device_path and self.overlap_build and self.early_fork
+                    and nxt == self.params.steps_per_slice * self.slice_idx
+                    and nxt < self.params.steps_per_slice * (old_slice_idx + n_slices)):
+                # the next slice's cluster build depends on the positions
+                # only: fork it now, so it overlaps this chunk's reward as
+                # well as the next slice's observables and policy
+                self._prebuild(self.params.steps_per_slice)
             if force_model is not None:
                 force_model.calc_reward(self.swarm_view() if device_path else self.colloids)
             self.step_idx += steps_to_next
