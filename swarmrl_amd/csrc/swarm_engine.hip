@@ -1105,7 +1105,9 @@ void set_lds_attributes() {
   const void* fns[] = {reinterpret_cast<const void*>(&swarm::k_global),
                        reinterpret_cast<const void*>(&swarm::k_cluster_build<false>),
                        reinterpret_cast<const void*>(&swarm::k_cluster_build<true>),
-                       reinterpret_cast<const void*>(&swarm::k_build_sort),
+                       reinterpret_cast<const void*>(&swarm::k_cluster_build_packed),
+                       reinterpret_cast<const void*>(&swarm::k_build_sort<4>),
+                       reinterpret_cast<const void*>(&swarm::k_build_sort<16>),
                        reinterpret_cast<const void*>(&swarm::k_build_env),
                        reinterpret_cast<const void*>(&swarm::k_check),
                        reinterpret_cast<const void*>(&k_grid_build),
@@ -1157,13 +1159,21 @@ int launch_build(swarm_engine* e, hipStream_t stream) {
     HIP_TRY(hipGetLastError());
     return SWARM_OK;
   }
-  hipLaunchKernelGGL(swarm::k_build_sort, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4, stream,
-                     e->st, e->sc, e->lxb, e->lyb);
+  if (e->n > 4096)
+    hipLaunchKernelGGL(swarm::k_build_sort<16>, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4,
+                       stream, e->st, e->sc, e->lxb, e->lyb);
+  else
+    hipLaunchKernelGGL(swarm::k_build_sort<4>, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4,
+                       stream, e->st, e->sc, e->lxb, e->lyb);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(swarm::k_build_pairs, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
                      dim3(256), 0, stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb);
   HIP_TRY(hipGetLastError());
-  if (e->big_build)
+  if (e->big_build && swarm::build_lds_words_packed(e->n) * 4 <= kMaxLds &&
+      !(std::getenv("SWARMRL_AMD_PACKED_BUILD") && std::getenv("SWARMRL_AMD_PACKED_BUILD")[0] == '0'))
+    hipLaunchKernelGGL(swarm::k_cluster_build_packed, dim3(e->n_envs), dim3(1024),
+                       swarm::build_lds_words_packed(e->n) * 4, stream, e->st, e->sc);
+  else if (e->big_build)
     hipLaunchKernelGGL(swarm::k_cluster_build<true>, dim3(e->n_envs), dim3(1024),
                        swarm::build_lds_words_big(e->n) * 4, stream, e->st, e->sc);
   else

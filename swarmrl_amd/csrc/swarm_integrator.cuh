@@ -218,7 +218,14 @@ __device__ __forceinline__ float pair_disp(uint32_t qj, int32_t ij, uint32_t qi,
 }
 
 // Exclusive scan of data[0..n) in LDS by the whole block; data[n] = total.
-__device__ inline void block_exclusive_scan(int32_t* data, int n, int32_t* wave_sums) {
+// Each wave scans a contiguous chunk 64 entries at a time (lane k reads
+// entry base + k: no LDS bank conflicts, unlike one contiguous run per
+// thread), carrying its running total; a second pass adds the exclusive
+// prefix of the waves' totals.
+// Up to 4 entries per thread the one-run-per-thread scan is shorter (its
+// few strided reads conflict little): measured 2.6 vs 1.8 us at 4096 cells,
+// 7.0 vs 11.5 us at 16384.
+__device__ inline void block_exclusive_scan_runs(int32_t* data, int n, int32_t* wave_sums) {
   const int T = blockDim.x;
   const int tid = threadIdx.x;
   const int per = (n + T - 1) / T;
@@ -252,6 +259,48 @@ __device__ inline void block_exclusive_scan(int32_t* data, int n, int32_t* wave_
     run += c;
   }
   if (tid == T - 1) data[n] = run;
+}
+
+__device__ inline void block_exclusive_scan(int32_t* data, int n, int32_t* wave_sums) {
+  const int T = blockDim.x;
+  if (n <= 4 * T) {
+    block_exclusive_scan_runs(data, n, wave_sums);
+    return;
+  }
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int nw = (T + 63) >> 6;
+  const int chunk = (((n + nw - 1) / nw) + 63) & ~63;
+  const int lo = min(wave * chunk, n), hi = min(lo + chunk, n);
+  int32_t carry = 0;
+  for (int b = lo; b < hi; b += 64) {
+    const int k = b + lane;
+    const int32_t x = k < hi ? data[k] : 0;
+    int32_t v = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int32_t o = __shfl_up(v, off, 64);
+      if (lane >= off) v += o;
+    }
+    if (k < hi) data[k] = carry + v - x;
+    carry += __shfl(v, 63, 64);
+  }
+  if (lane == 0) wave_sums[wave] = carry;
+  __syncthreads();
+  if (wave == 0) {
+    int32_t w = lane < nw ? wave_sums[lane] : 0;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int32_t o = __shfl_up(w, off, 64);
+      if (lane >= off) w += o;
+    }
+    if (lane < nw) wave_sums[lane] = w;  // inclusive prefix of the wave totals
+  }
+  __syncthreads();
+  const int32_t add = wave > 0 ? wave_sums[wave - 1] : 0;
+  if (add != 0)
+    for (int k = lo + lane; k < hi; k += 64) data[k] += add;
+  if (tid == T - 1) data[n] = wave_sums[nw - 1];
 }
 
 // WCA force on i from j (r = x_j - x_i), accumulated in 2^-24 fixed point.
@@ -876,9 +925,9 @@ __host__ __device__ inline size_t build_lds_words(int n, int pair_cap) {
 
 // Build step 1, one workgroup per env: counting sort into cells of side
 // >= rc_max + skin (global arrays for the chip-wide pair search).
+template <int CH>  // particles per thread kept in registers across the scan (4, or 16 above 4096)
 __global__ __launch_bounds__(1024) void k_build_sort(DevState st, Scratch sc, int lx, int ly) {
   extern __shared__ __align__(16) unsigned char smem[];
-  constexpr int CH = 4;  // particles per thread kept in registers across the scan
   const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly);
@@ -1106,32 +1155,66 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
     }
   }
   __syncthreads();
-  for (int k = tid; k < npairs; k += T) {
-    const uint32_t pr = plist[k];
-    uf_union(parent, (int)(pr & 0xffffu), (int)(pr >> 16));
+  // (kBig: the arrays below live in global memory, so every loop issues
+  // its loads / atomics kU at a time before using them -- one memory
+  // latency per kU iterations, not one per iteration)
+  constexpr int kU = kBig ? 8 : 1;
+  for (int k0 = tid; k0 < npairs; k0 += kU * T) {
+    uint32_t pr[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) pr[u] = k0 + u * T < npairs ? plist[k0 + u * T] : 0u;
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (k0 + u * T < npairs) uf_union(parent, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
   }
   __syncthreads();
   SWARM_STAMP(7);
   for (int i = tid; i < N; i += T) parent[i] = uf_find(parent, i);
   __syncthreads();
-  for (int i = tid; i < N; i += T) lslot[i] = atomicAdd(&csz[parent[i]], 1);
+  for (int i0 = tid; i0 < N; i0 += kU * T) {
+    int32_t r[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) r[u] = i0 + u * T < N ? atomicAdd(&csz[parent[i0 + u * T]], 1) : 0;
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (i0 + u * T < N) lslot[i0 + u * T] = r[u];
+  }
   if (sc.one_pass)
-    for (int k = tid; k < npairs; k += T) atomicAdd(&cbase[parent[plist[k] & 0xffffu]], 1);
+    for (int k0 = tid; k0 < npairs; k0 += kU * T) {
+      uint32_t pr[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) pr[u] = k0 + u * T < npairs ? plist[k0 + u * T] : 0u;
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (k0 + u * T < npairs) atomicAdd(&cbase[parent[pr[u] & 0xffffu]], 1);
+    }
   __syncthreads();
   // Lanes reserved per cluster (its packing class w): its size s, or with
   // one-pass packing max(s, min(pairs, 64, 2 s)), so that the clusters of a
   // wave have at most 64 pairs (one pair pass per sub-step) unless a cluster
   // is denser than 2 pairs per particle.  Results do not depend on it.
-  for (int i = tid; i < N; i += T) {
-    if (parent[i] != i) continue;
-    const int s = csz[i];
-    if (s > 64) {  // wider than a wave: a big cluster, run by k_check's workgroup
-      atomicAdd(&misc[4], s);
-      cbase[i] = kBigMark;
-    } else {
-      const int w = sc.one_pass ? max(s, min(min(cbase[i], 64), 2 * s)) : s;
-      csz[i] = w;
-      cbase[i] = atomicAdd(&classcnt[w], 1);
+  for (int i0 = tid; i0 < N; i0 += kU * T) {
+    int32_t sz[kU], pc[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * T;
+      const bool root = i < N && parent[i] == i;
+      sz[u] = root ? csz[i] : 0;
+      pc[u] = root ? cbase[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * T;
+      if (i >= N || parent[i] != i) continue;
+      const int s = sz[u];
+      if (s > 64) {  // wider than a wave: a big cluster, run by k_check's workgroup
+        atomicAdd(&misc[4], s);
+        cbase[i] = kBigMark;
+      } else {
+        const int w = sc.one_pass ? max(s, min(min(pc[u], 64), 2 * s)) : s;
+        csz[i] = w;
+        cbase[i] = atomicAdd(&classcnt[w], 1);
+      }
     }
   }
   __syncthreads();
@@ -1182,10 +1265,21 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   }
   __syncthreads();
   const int nfree = misc[3];
-  for (int i = tid; i < N; i += T) {
-    if (parent[i] != i) continue;
-    const int s = csz[i];
-    const int r = cbase[i];
+  for (int i0 = tid; i0 < N; i0 += kU * T) {
+   int32_t sz[kU], rk[kU];
+#pragma unroll
+   for (int u = 0; u < kU; ++u) {
+     const int i = i0 + u * T;
+     const bool root = i < N && parent[i] == i;
+     sz[u] = root ? csz[i] : 0;
+     rk[u] = root ? cbase[i] : 0;
+   }
+#pragma unroll
+   for (int u = 0; u < kU; ++u) {
+    const int i = i0 + u * T;
+    if (i >= N || parent[i] != i) continue;
+    const int s = sz[u];
+    const int r = rk[u];
     if (r == kBigMark) continue;
     if (s == 1 && r < nfree) {
       // the class v whose free-lane range holds r (largest v >= 2 with
@@ -1215,30 +1309,55 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
       const int per = 64 / s;
       cbase[i] = (wavebase[s] + r / per) * 64 + (r % per) * s;
     }
+   }
   }
   __syncthreads();
-  for (int i = tid; i < N; i += T) {
-    const int root = parent[i];
-    int slot;
-    if (cbase[root] == kBigMark) {  // big-cluster member m: slot -1 - m
-      const int m = atomicAdd(&misc[5], 1);
-      sc.big_list[(size_t)e * kBigMax + m] = i;
-      slot = -1 - m;
-    } else {
-      slot = cbase[root] + lslot[i];
-      sc.perm[(size_t)e * S + slot] = i;
+  for (int i0 = tid; i0 < N; i0 += kU * T) {
+    int32_t cb[kU], ls[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * T;
+      cb[u] = i < N ? cbase[parent[i]] : 0;
+      ls[u] = i < N ? lslot[i] : 0;
     }
-    lslot[i] = slot;
-    sc.slot_of[base + i] = slot;
-    sc.root[base + i] = root;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * T;
+      if (i >= N) continue;
+      const int root = parent[i];
+      int slot;
+      if (cb[u] == kBigMark) {  // big-cluster member m: slot -1 - m
+        const int m = atomicAdd(&misc[5], 1);
+        sc.big_list[(size_t)e * kBigMax + m] = i;
+        slot = -1 - m;
+      } else {
+        slot = cb[u] + ls[u];
+        sc.perm[(size_t)e * S + slot] = i;
+      }
+      lslot[i] = slot;
+      sc.slot_of[base + i] = slot;
+      sc.root[base + i] = root;
+    }
   }
   __syncthreads();
   SWARM_STAMP(9);
   // per-wave pair lists (both particles of a pair share a cluster, so a wave)
-  for (int k = tid; k < npairs; k += T) {
-    const uint32_t pr = plist[k];
+  for (int k0 = tid; k0 < npairs; k0 += kU * T) {
+   uint32_t prs[kU];
+#pragma unroll
+   for (int u = 0; u < kU; ++u) prs[u] = k0 + u * T < npairs ? plist[k0 + u * T] : 0u;
+   int32_t sis[kU], sjs[kU];
+#pragma unroll
+   for (int u = 0; u < kU; ++u) {
+     sis[u] = lslot[prs[u] & 0xffffu];
+     sjs[u] = lslot[prs[u] >> 16];
+   }
+#pragma unroll
+   for (int u = 0; u < kU; ++u) {
+    if (k0 + u * T >= npairs) continue;
+    const uint32_t pr = prs[u];
     const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
-    const int si = lslot[i], sj = lslot[j];
+    const int si = sis[u], sj = sjs[u];
     const uint32_t spp = (uint32_t)(st.species[i] * kMaxSpecies + st.species[j]);
     if (si < 0) {  // a big cluster's pair (both members of it)
       const int idx = atomicAdd(&misc[6], 1);
@@ -1256,6 +1375,7 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
           (uint32_t)(si & 63) | ((uint32_t)(sj & 63) << 6) | (spp << 12);
     else
       misc[2] = 1;  // a wave with more than kPairsPerWave pairs
+   }
   }
   __syncthreads();
   SWARM_STAMP(10);
@@ -1267,6 +1387,239 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
     sc.big_n[e] = misc[5];
     sc.big_np[e] = min(misc[6], kBigPairs);
   }
+}
+
+// LDS words of the packed large-N build: two words per particle (N < 65536).
+__host__ __device__ inline size_t build_lds_words_packed(int n) {
+  const int wmax = slots_per_env(n, true) / 64;
+  return 16 + 16 + 3 * 68 + (size_t)((wmax + 3) & ~3) + 2 * (size_t)n;
+}
+
+// The large-N build (same result as cluster_build_env<true, false>) with
+// its per-particle and per-cluster arrays packed into two LDS words per
+// particle instead of global memory (whose returning atomics and dependent
+// loads cost ~3x LDS per element from one CU):
+//   A[i]: union-find parent; then root | rank << 16 (rank = i's lane within
+//         its cluster); then i's wave slot;
+//   B[r]: for a root r, size | pairs << 16 (atomic counters, no carry:
+//         size < 2^16); then class rank | w << 24; then the cluster's first
+//         slot (or kBigMark).
+// The pair list stays in global memory (read kU at a time).
+__device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, int e,
+                                         unsigned char* smem, int found) {
+  const int T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t base = (size_t)e * N;
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);  // 16
+  int32_t* misc = wave_sums + 16;                          // 16: 0 flag, 1 waves
+  int32_t* classcnt = misc + 16;                           // 68
+  int32_t* wavebase = classcnt + 68;                       // 68
+  int32_t* freebase = wavebase + 68;                       // 68
+  const int wmax = sc.wmax;
+  int32_t* wave_np = freebase + 68;                        // wmax (padded)
+  int32_t* A = wave_np + ((wmax + 3) & ~3);                // N
+  int32_t* B = A + N;                                      // N
+  const uint32_t* plist = sc.gplist + (size_t)e * sc.pair_cap;
+  const int S = sc.S;
+  constexpr int kU = 8;
+  SWARM_STAMP(6);
+  const int npairs = min(found, sc.pair_cap);
+  for (int k = tid; k < 68; k += T) classcnt[k] = 0;
+  for (int k = tid; k < wmax; k += T) wave_np[k] = 0;
+  if (tid < 16) misc[tid] = tid == 0 && found > sc.pair_cap ? 1 : 0;  // overflow -> global path
+  for (int i = tid; i < N; i += T) {
+    A[i] = i;
+    B[i] = 0;
+  }
+  __syncthreads();
+  for (int k0 = tid; k0 < npairs; k0 += kU * T) {
+    uint32_t pr[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) pr[u] = k0 + u * T < npairs ? plist[k0 + u * T] : 0u;
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (k0 + u * T < npairs) uf_union(A, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
+  }
+  __syncthreads();
+  SWARM_STAMP(7);
+  for (int i = tid; i < N; i += T) A[i] = uf_find(A, i);
+  __syncthreads();
+  for (int i = tid; i < N; i += T) {
+    const int root = A[i];
+    const uint32_t r = (uint32_t)atomicAdd(&B[root], 1) & 0xffffu;
+    A[i] = root | (int32_t)(r << 16);
+  }
+  if (sc.one_pass)
+    for (int k0 = tid; k0 < npairs; k0 += kU * T) {
+      uint32_t pr[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) pr[u] = k0 + u * T < npairs ? plist[k0 + u * T] : 0u;
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (k0 + u * T < npairs) {
+          // the root of the pair's first particle: A holds root | rank << 16
+          // of particles whose rank is already stored, root otherwise
+          const int a = (int)(pr[u] & 0xffffu);
+          atomicAdd(&B[A[a] & 0xffff], 1 << 16);
+        }
+    }
+  __syncthreads();
+  // lanes reserved per cluster (cluster_build_env): class w, class rank
+  for (int i = tid; i < N; i += T) {
+    if ((A[i] & 0xffff) != i) continue;  // roots only
+    const uint32_t b = (uint32_t)B[i];
+    const int s = (int)(b & 0xffffu), pairs = (int)(b >> 16);
+    if (s > 64) {  // wider than a wave: a big cluster, run by k_check's workgroup
+      atomicAdd(&misc[4], s);
+      B[i] = kBigMark;
+    } else {
+      const int w = sc.one_pass ? max(s, min(min(pairs, 64), 2 * s)) : s;
+      B[i] = atomicAdd(&classcnt[w], 1) | (w << 24);
+    }
+  }
+  __syncthreads();
+  SWARM_STAMP(8);
+  if (tid == 0 && misc[4] > min(kBigMax, (int)blockDim.x)) misc[0] = 1;  // -> global path
+  __syncthreads();
+  if (misc[0]) {
+    if (tid == 0) {
+      sc.fallback[e] = 1;
+      sc.env_waves[e] = 0;
+      sc.big_n[e] = 0;
+      sc.big_np[e] = 0;
+    }
+    return;
+  }
+  if (tid < 64) {  // waves per class (cluster_build_env)
+    const int w = tid + 1;
+    const int per = 64 / w;
+    const int cnt = classcnt[w];
+    int32_t nw = (cnt + per - 1) / per;
+    int32_t fl = 0;
+    if (w >= 2 && nw > 0) fl = (nw - 1) * (64 - per * w) + (64 - (cnt - (nw - 1) * per) * w);
+    int32_t f = fl;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int32_t o = __shfl_up(f, off, 64);
+      if (tid >= off) f += o;
+    }
+    freebase[w] = f - fl;
+    const int32_t F = sc.fill_singletons ? __shfl(f, 63, 64) : 0;
+    if (w == 1) nw = (max(cnt - F, 0) + 63) / 64;
+    int32_t v = nw;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int32_t o = __shfl_up(v, off, 64);
+      if (tid >= off) v += o;
+    }
+    wavebase[w] = v - nw;
+    if (tid == 63) {
+      misc[1] = v;
+      misc[3] = F;
+      freebase[65] = F;
+    }
+  }
+  __syncthreads();
+  const int nfree = misc[3];
+  for (int i = tid; i < N; i += T) {
+    if ((A[i] & 0xffff) != i) continue;
+    const int32_t b = B[i];
+    if (b == kBigMark) continue;
+    const int s = (b >> 24) & 0x7f;
+    const int r = b & 0xffffff;
+    int cb;
+    if (s == 1 && r < nfree) {
+      int lo = 2, hi = 64;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (freebase[mid] <= r) lo = mid; else hi = mid - 1;
+      }
+      const int v = lo, per = 64 / v;
+      const int nw = (classcnt[v] + per - 1) / per;
+      const int ffull = 64 - per * v;
+      const int t = r - freebase[v];
+      int j, lane;
+      if (t < (nw - 1) * ffull) {
+        j = t / ffull;
+        lane = per * v + t % ffull;
+      } else {
+        j = nw - 1;
+        lane = (classcnt[v] - (nw - 1) * per) * v + (t - (nw - 1) * ffull);
+      }
+      cb = (wavebase[v] + j) * 64 + lane;
+    } else if (s == 1) {
+      const int r2 = r - nfree;
+      cb = (wavebase[1] + r2 / 64) * 64 + r2 % 64;
+    } else {
+      const int per = 64 / s;
+      cb = (wavebase[s] + r / per) * 64 + (r % per) * s;
+    }
+    B[i] = cb;
+  }
+  __syncthreads();
+  for (int i = tid; i < N; i += T) {
+    const int32_t a = A[i];
+    const int root = a & 0xffff;
+    const int rank = (int)((uint32_t)a >> 16);
+    const int32_t cb = B[root];
+    int slot;
+    if (cb == kBigMark) {  // big-cluster member m: slot -1 - m
+      const int m = atomicAdd(&misc[5], 1);
+      sc.big_list[(size_t)e * kBigMax + m] = i;
+      slot = -1 - m;
+    } else {
+      slot = cb + rank;
+      sc.perm[(size_t)e * S + slot] = i;
+    }
+    sc.slot_of[base + i] = slot;
+    sc.root[base + i] = root;
+    A[i] = slot;  // only this thread reads A[i] in this loop
+  }
+  __syncthreads();
+  SWARM_STAMP(9);
+  for (int k0 = tid; k0 < npairs; k0 += kU * T) {
+    uint32_t prs[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) prs[u] = k0 + u * T < npairs ? plist[k0 + u * T] : 0u;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (k0 + u * T >= npairs) continue;
+      const uint32_t pr = prs[u];
+      const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
+      const int si = A[i], sj = A[j];
+      const uint32_t spp = (uint32_t)(st.species[i] * kMaxSpecies + st.species[j]);
+      if (si < 0) {  // a big cluster's pair (both members of it)
+        const int idx = atomicAdd(&misc[6], 1);
+        if (idx < kBigPairs)
+          sc.big_pairs[(size_t)e * kBigPairs + idx] =
+              (uint32_t)(-1 - si) | ((uint32_t)(-1 - sj) << 10) | (spp << 20);
+        else
+          misc[2] = 1;  // -> global path
+        continue;
+      }
+      const int wv = si >> 6;
+      const int idx = atomicAdd(&wave_np[wv], 1);
+      if (idx < kPairsPerWave)
+        sc.pairs[((size_t)e * wmax + wv) * kPairsPerWave + idx] =
+            (uint32_t)(si & 63) | ((uint32_t)(sj & 63) << 6) | (spp << 12);
+      else
+        misc[2] = 1;  // a wave with more than kPairsPerWave pairs
+    }
+  }
+  __syncthreads();
+  SWARM_STAMP(10);
+  for (int w = tid; w < misc[1]; w += T)
+    sc.wave_npairs[(size_t)e * wmax + w] = min(wave_np[w], kPairsPerWave);
+  if (tid == 0) {
+    sc.env_waves[e] = misc[2] ? 0 : misc[1];
+    sc.fallback[e] = misc[2] ? 1 : 0;
+    sc.big_n[e] = misc[5];
+    sc.big_np[e] = min(misc[6], kBigPairs);
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_cluster_build_packed(DevState st, Scratch sc) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  cluster_build_env_packed(st, sc, blockIdx.x, smem, sc.gnpairs[blockIdx.x]);
 }
 
 template <bool kBig>

@@ -14,7 +14,7 @@ sys.path.insert(0, "tests")
 from gpu_harness import Harness, species_list  # noqa: E402
 
 torch.cuda.set_device(0)
-n = 4096
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 L = 2 * np.sqrt(n / 0.1)
 rng = np.random.default_rng(1)
 h = Harness([L, L, L], 1e-3, 1.0239, 1.0239, 42, species_list()[:1], np.zeros(n, int))
