@@ -394,6 +394,20 @@ int swarm_ppo_epoch_grad(const float *x, int32_t T, int32_t S, int32_t d_in,
                          float gamma, float lambda, float clip_eps, float entropy_coef,
                          void *workspace, int64_t workspace_bytes, float *grad, void *stream);
 
+/* Random Network Distillation distance (the intrinsic reward of
+ * swarmrl/intrinsic_reward/random_network_distillation.py:126-143 with the
+ * networks of rnd_configs.py:17-38): for every observation a < n of x
+ * [n][d_in] (device fp32), target and predictor networks Dense(width) ->
+ * ReLU -> Dense(width) -> ReLU -> Dense(width), and
+ *   out[a] = (sum_k |t_k - p_k|^order)^(1/order)      (ZnNL OrderNDifference).
+ * target / predictor: host arrays of the six device parameter pointers
+ * w1 [width][d_in], b1, w2 [width][width], b2, w3 [width][width], b3 (torch
+ * Linear layouts, read in place).  width = 32, d_in <= 16.  Asynchronous on
+ * `stream`. */
+int swarm_rnd_distance(const float *x, int32_t n, int32_t d_in, int32_t width,
+                       const float *const *target, const float *const *predictor,
+                       int32_t order, float *out, void *stream);
+
 /* Neighbour reductions for the classical agents (all pointers device):
  * get_colloids_in_vision of bechinger_models.py:156-171 (range + cone) and
  * lymburn_model.py:113-125 (range only, half_angle < 0), fused with the

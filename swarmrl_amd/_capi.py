@@ -151,6 +151,10 @@ _SIGNATURES = {
          ctypes.c_float, _P, ctypes.c_int64, _P, _P],
     ),
     "swarm_engine_step_count": (ctypes.c_int64, [_P]),
+    "swarm_rnd_distance": (
+        ctypes.c_int,
+        [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_int32, _P, _P],
+    ),
     "swarm_engine_traj_ring": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _P, _P]),
     "swarm_engine_traj_record": (ctypes.c_int, [_P]),
     "swarm_traj_entry_to_host": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),

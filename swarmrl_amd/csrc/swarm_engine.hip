@@ -34,6 +34,7 @@
 #include "swarm_integrator3.cuh"
 #include "swarm_policy.cuh"
 #include "swarm_ppo.cuh"
+#include "swarm_rnd.cuh"
 
 namespace {
 
@@ -1903,6 +1904,32 @@ int swarm_traj_entry_to_host(const swarm_engine_t* e, const void* entry, double*
     if (velocity)
       for (int a = 0; a < 3; ++a) velocity[3 * g + a] = a < D ? vel[a * N + g] : 0.0;
   }
+  return SWARM_OK;
+}
+
+int swarm_rnd_distance(const float* x, int32_t n, int32_t d_in, int32_t width,
+                       const float* const* target, const float* const* predictor, int32_t order,
+                       float* out, void* stream) {
+  if (!x || !target || !predictor || !out) return fail(SWARM_EINVAL, "null argument");
+  if (width != swarm::kRndWidth) return fail(SWARM_ECAPACITY, "RND width must be 32");
+  if (d_in < 1 || d_in > swarm::kRndMaxIn) return fail(SWARM_ECAPACITY, "1 <= d_in <= 16");
+  if (order < 1) return fail(SWARM_EINVAL, "distance order must be >= 1");
+  swarm::RndPtrs tp, pp;
+  for (int k = 0; k < 6; ++k) {
+    if (!target[k] || !predictor[k]) return fail(SWARM_EINVAL, "null parameter");
+    tp.w[k] = target[k];
+    pp.w[k] = predictor[k];
+  }
+  if (n <= 0) return SWARM_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  if (d_in <= 4)
+    hipLaunchKernelGGL(swarm::k_rnd_distance<4>, dim3(blocks), dim3(256), 0, s, x, n, d_in, tp,
+                       pp, order, out);
+  else
+    hipLaunchKernelGGL(swarm::k_rnd_distance<16>, dim3(blocks), dim3(256), 0, s, x, n, d_in, tp,
+                       pp, order, out);
+  HIP_TRY(hipGetLastError());
   return SWARM_OK;
 }
 

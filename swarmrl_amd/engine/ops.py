@@ -430,3 +430,28 @@ def neighbor_reduce(pos: torch.Tensor, directors: torch.Tensor, velocities, type
         agent_idx.to(torch.int32).contiguous().data_ptr(), A, ctypes.c_uint32(mask),
         float(vision_range), float(half_angle), out.data_ptr(), ctypes.c_void_p(stream)))
     return out
+
+
+def rnd_distance(points: torch.Tensor, target: torch.nn.Module, predictor: torch.nn.Module,
+                 order: int) -> torch.Tensor:
+    """The RND metric of every observation in one launch (swarm_rnd_distance):
+    points [n, d] fp32 device; target / predictor: the stock RNDArchitecture
+    (three Linear layers of width 32), weights read in place.  Returns [n]."""
+    points = points.contiguous()
+    n, d = points.shape
+    out = torch.empty(n, dtype=torch.float32, device=points.device)
+
+    def ptrs(net):
+        lin = [m for m in net.modules() if isinstance(m, torch.nn.Linear)]
+        arr = (ctypes.c_void_p * 6)()
+        for k, m in enumerate(lin):
+            arr[2 * k] = m.weight.data_ptr()
+            arr[2 * k + 1] = m.bias.data_ptr()
+        return arr
+
+    stream = torch.cuda.current_stream(points.device).cuda_stream
+    tp, pp = ptrs(target), ptrs(predictor)
+    _capi.check(_capi.lib().swarm_rnd_distance(
+        points.data_ptr(), n, d, 32, ctypes.cast(tp, ctypes.c_void_p),
+        ctypes.cast(pp, ctypes.c_void_p), int(order), out.data_ptr(), ctypes.c_void_p(stream)))
+    return out

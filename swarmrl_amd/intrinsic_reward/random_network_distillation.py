@@ -56,11 +56,30 @@ class RNDReward(IntrinsicReward):
         x = self._stack(feats)
         return x.reshape(-1, self.in_dim).to(torch.float32).to(self.device)
 
+    def _fused_ok(self, points: torch.Tensor) -> bool:
+        """The one-launch HIP metric applies to the stock architecture
+        (three Linear(32) layers, fp32 parameters) on the GPU."""
+        if not (points.is_cuda and points.dtype == torch.float32 and 1 <= self.in_dim <= 16):
+            return False
+        for net in (self.target_network, self.predictor_network):
+            lin = [m for m in net.modules() if isinstance(m, torch.nn.Linear)]
+            if len(lin) != 3 or any(m.out_features != 32 or m.bias is None or
+                                    m.weight.dtype != torch.float32 or not m.weight.is_cuda
+                                    for m in lin):
+                return False
+        return True
+
     @torch.no_grad()
     def compute_distance(self, points: torch.Tensor) -> torch.Tensor:
-        self.metric_results = order_n_difference(self.target_network(points),
-                                                 self.predictor_network(points),
-                                                 self.distance_order)
+        if self._fused_ok(points):
+            from swarmrl_amd.engine import ops
+
+            self.metric_results = ops.rnd_distance(points, self.target_network,
+                                                   self.predictor_network, self.distance_order)
+        else:
+            self.metric_results = order_n_difference(self.target_network(points),
+                                                     self.predictor_network(points),
+                                                     self.distance_order)
         return torch.mean(self.metric_results)
 
     def update(self, episode_data):
