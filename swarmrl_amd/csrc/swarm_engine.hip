@@ -1469,11 +1469,13 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->st.torque_xy, 2 * M);
   rc = rc ? rc : dev_alloc(e, &e->st.omega_xy, 2 * M);
   rc = rc ? rc : dev_alloc(e, &e->st.wall_viol, 1);
-  rc = rc ? rc : dev_alloc(e, &e->st.f_prev, M);
-  rc = rc ? rc : dev_alloc(e, &e->st.tz_prev, M);
-  rc = rc ? rc : dev_alloc(e, &e->st.ang_prev, M);
-  rc = rc ? rc : dev_alloc(e, &e->st.dir3_prev, three_d ? 3 * M : 1);
-  rc = rc ? rc : dev_alloc(e, &e->st.txy_prev, three_d ? 2 * M : 1);
+  rc = rc ? rc : dev_alloc(e, &e->st.f_prev, 2 * M);  // two slots (window parity)
+  rc = rc ? rc : dev_alloc(e, &e->st.tz_prev, 2 * M);
+  rc = rc ? rc : dev_alloc(e, &e->st.ang_prev, 2 * M);
+  rc = rc ? rc : dev_alloc(e, &e->st.dir3_prev, three_d ? 6 * M : 1);
+  rc = rc ? rc : dev_alloc(e, &e->st.txy_prev, three_d ? 4 * M : 1);
+  rc = rc ? rc : dev_alloc(e, &e->sc.nmov, (size_t)n_envs);
+  rc = rc ? rc : dev_alloc(e, &e->sc.movers, (size_t)n_envs * swarm::kMaxMovers);
   rc = rc ? rc : dev_alloc(e, &e->sc.sidx, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.bq, 2 * M);
   rc = rc ? rc : dev_alloc(e, &e->sc.bimg, 2 * M);
@@ -1595,9 +1597,11 @@ int swarm_engine_upload_raw(swarm_engine_t* e, const uint32_t* q, const int32_t*
   HIP_TRY(hipMemcpyAsync(e->st.q, q, 3 * M * sizeof(uint32_t), hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(e->st.img, img, 3 * M * sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipMemcpyAsync(e->st.ang, ang, M * sizeof(uint32_t), hipMemcpyHostToDevice, e->stream));
-  // a fresh state: the last force calculation saw these orientations
-  HIP_TRY(hipMemcpyAsync(e->st.ang_prev, ang, M * sizeof(uint32_t), hipMemcpyHostToDevice,
-                         e->stream));
+  // a fresh state: the last force calculation saw these orientations (both
+  // reuse_forces slots: the device window counter's parity is not known here)
+  for (int k = 0; k < 2; ++k)
+    HIP_TRY(hipMemcpyAsync(e->st.ang_prev + k * M, ang, M * sizeof(uint32_t),
+                           hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   return SWARM_OK;
 }
@@ -2179,8 +2183,9 @@ int swarm_engine_upload_directors(swarm_engine_t* e, const float* dir3) {
   const size_t M = (size_t)e->st.m;
   HIP_TRY(hipMemcpyAsync(e->st.dir3, dir3, 3 * M * sizeof(float), hipMemcpyHostToDevice,
                          e->stream));
-  HIP_TRY(hipMemcpyAsync(e->st.dir3_prev, dir3, 3 * M * sizeof(float), hipMemcpyHostToDevice,
-                         e->stream));
+  for (int k = 0; k < 2; ++k)
+    HIP_TRY(hipMemcpyAsync(e->st.dir3_prev + k * 3 * M, dir3, 3 * M * sizeof(float),
+                           hipMemcpyHostToDevice, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   return SWARM_OK;
 }

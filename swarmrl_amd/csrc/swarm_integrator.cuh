@@ -50,6 +50,7 @@ constexpr int kPairsPerWave = 256;  // neighbour pairs of one 64-lane wave (4 pa
 constexpr int kBigMax = 1024;
 constexpr int kBigPairs = 4096;
 constexpr int kBigMark = -0x40000000;  // cbase of a big cluster's root
+constexpr int kMaxMovers = 1024;       // listed movers per env (more: exact re-run)
 
 // Wave slots per env: every cluster packs into one wave, worst case 2 N
 // slots plus per-size-class rounding.  One-pass packing (latency-bound
@@ -105,38 +106,62 @@ struct DevState {
   unsigned long long* wall_viol;  // [1] wall contacts with dist <= 0
   // reuse_forces (swarm_params_t): what the last force calculation of the
   // previous run used -- sub-step 0 of a run takes its swim force, torque
-  // and director from here (espresso.py:1304-1306); saved at every window end
+  // and director from here (espresso.py:1304-1306).  Two slots, by the
+  // device window counter's parity: window w reads slot w & 1 and writes
+  // slot (w + 1) & 1 (the run kernel for its particles, the check only after
+  // an exact re-run), so a re-run still finds the old values.
   int32_t reuse;
-  float* f_prev;       // [M]
-  float* tz_prev;      // [M]
-  uint32_t* ang_prev;  // [M]    2-D orientation
-  float* dir3_prev;    // [3][M] 3-D director
-  float* txy_prev;     // [2][M] 3-D torque x, y
+  float* f_prev;       // [2][M]
+  float* tz_prev;      // [2][M]
+  uint32_t* ang_prev;  // [2][M]    2-D orientation
+  float* dir3_prev;    // [2][3][M] 3-D director
+  float* txy_prev;     // [2][2][M] 3-D torque x, y
 };
 
-// End of a window (every path): the actions and orientations that the next
-// run's sub-step 0 reuses.  Called by the thread that wrote particle gi's
-// final state.
-__device__ __forceinline__ void save_forces(const DevState& st, size_t gi) {
+// The reuse_forces slot p of the engine (see DevState).
+struct PrevSlot {
+  float* f;
+  float* tz;
+  uint32_t* ang;
+  float* dir3;
+  float* txy;
+};
+
+__device__ __forceinline__ PrevSlot prev_slot(const DevState& st, int p) {
   const size_t M = (size_t)st.m;
-  st.f_prev[gi] = st.f_swim[gi];
-  st.tz_prev[gi] = st.torque_z[gi];
+  PrevSlot s;
+  s.f = st.f_prev + p * M;
+  s.tz = st.tz_prev + p * M;
+  s.ang = st.ang_prev + p * M;
+  s.dir3 = st.dir3_prev + (st.dims == 3 ? p * 3 * M : 0);
+  s.txy = st.txy_prev + (st.dims == 3 ? p * 2 * M : 0);
+  return s;
+}
+
+// End of a window: the actions and orientation particle gi's next run
+// reuses at sub-step 0, into slot wp.  Called by the thread that wrote gi's
+// final state.
+__device__ __forceinline__ void save_forces(const DevState& st, size_t gi, int wp) {
+  const size_t M = (size_t)st.m;
+  const PrevSlot w = prev_slot(st, wp);
+  w.f[gi] = st.f_swim[gi];
+  w.tz[gi] = st.torque_z[gi];
   if (st.dims == 3) {
-    st.dir3_prev[gi] = st.dir3[gi];
-    st.dir3_prev[M + gi] = st.dir3[M + gi];
-    st.dir3_prev[2 * M + gi] = st.dir3[2 * M + gi];
-    st.txy_prev[gi] = st.torque_xy[gi];
-    st.txy_prev[M + gi] = st.torque_xy[M + gi];
+    w.dir3[gi] = st.dir3[gi];
+    w.dir3[M + gi] = st.dir3[M + gi];
+    w.dir3[2 * M + gi] = st.dir3[2 * M + gi];
+    w.txy[gi] = st.torque_xy[gi];
+    w.txy[M + gi] = st.torque_xy[M + gi];
   } else {
-    st.ang_prev[gi] = st.ang[gi];
+    w.ang[gi] = st.ang[gi];
   }
 }
 
-__device__ __forceinline__ void save_forces_env(const DevState& st, int e) {
+__device__ __forceinline__ void save_forces_env(const DevState& st, int e, int wp) {
   if (!st.reuse) return;
   __syncthreads();
   const size_t base = (size_t)e * st.n;
-  for (int i = threadIdx.x; i < st.n; i += blockDim.x) save_forces(st, base + i);
+  for (int i = threadIdx.x; i < st.n; i += blockDim.x) save_forces(st, base + i, wp);
 }
 
 // Device control block (uint64 words): step counter, window counter, and
@@ -167,6 +192,10 @@ struct Scratch {
   uint32_t* big_pairs;  // [E][kBigPairs] member a | member b << 10 | species pair << 20
   int32_t* big_n;     // [E] members
   int32_t* big_np;    // [E] pairs
+  // colloids that moved >= skin / 2 in the window (appended by the run
+  // kernel and the big-cluster run, consumed and reset by k_check)
+  int32_t* nmov;      // [E]
+  int32_t* movers;    // [E][kMaxMovers]
   // cluster build (k_build_sort -> k_build_pairs -> k_cluster_build)
   uint32_t* bsq;      // [2][M] cell-sorted positions (x, y)
   int32_t* bsid;      // [M] particle | species << 24 of a sorted entry
@@ -572,7 +601,8 @@ __device__ __forceinline__ bool sd_step(const PConst& c, PState& p, int64_t ax, 
 __device__ void block_global_run(const Derived* __restrict__ d, const DevState& st,
                                  const Scratch& sc, int e, int n_steps, uint64_t step0, int lx,
                                  int ly, bool sd_mode, float g, float md, int32_t* cnt,
-                                 int32_t* wave_sums, const PairTables* pt) {
+                                 int32_t* wave_sums, const PairTables* pt, int rp) {
+  const PrevSlot prv = prev_slot(st, rp);  // reuse_forces: sub-step 0 reads slot rp
   const int T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly);
@@ -643,8 +673,8 @@ __device__ void block_global_run(const Derived* __restrict__ d, const DevState& 
                        st.wall_viol);
       }
       const bool first = st.reuse && s == 0 && !sd_mode;  // reuse_forces: previous run's
-      const float fs = first ? st.f_prev[gi] : st.f_swim[gi];
-      const float tz = first ? st.tz_prev[gi] : st.torque_z[gi];
+      const float fs = first ? prv.f[gi] : st.f_swim[gi];
+      const float tz = first ? prv.tz[gi] : st.torque_z[gi];
       const float fex = st.f_ext[gi], fey = st.f_ext[M + gi];
       const PConst pc = load_pconst(d, si);
       if (sd_mode) {
@@ -653,7 +683,7 @@ __device__ void block_global_run(const Derived* __restrict__ d, const DevState& 
         float vx, vy, w;
         const bool last = s == n_steps - 1;
         bd_step(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s, last,
-                &vx, &vy, &w, first ? st.ang_prev[gi] : p.an);
+                &vx, &vy, &w, first ? prv.ang[gi] : p.an);
         if (last) {
           st.vel[gi] = vx;
           st.vel[M + gi] = vy;
@@ -700,7 +730,8 @@ __host__ __device__ inline size_t global_lds_extra_words(int n, int dims, int nc
 __device__ __forceinline__ void block_global_run_lds(const Derived* __restrict__ d, const DevState& st, int e,
                                      int n_steps, uint64_t step0, int lx, int ly, bool sd_mode,
                                      float g, float md, int32_t* cnt, int32_t* wave_sums,
-                                     int32_t* lsq, const PairTables* pt) {
+                                     int32_t* lsq, const PairTables* pt, int rp) {
+  const PrevSlot prv = prev_slot(st, rp);  // reuse_forces: sub-step 0 reads slot rp
   const int T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly);
@@ -764,8 +795,8 @@ __device__ __forceinline__ void block_global_run_lds(const Derived* __restrict__
       const size_t gi = base + i;
       PState pp = {lqx[i], lqy[i], lan[i], lix[i], liy[i]};
       const bool first = st.reuse && s == 0 && !sd_mode;  // reuse_forces: previous run's
-      const float fs = first ? st.f_prev[gi] : st.f_swim[gi];
-      const float tz = first ? st.tz_prev[gi] : st.torque_z[gi];
+      const float fs = first ? prv.f[gi] : st.f_swim[gi];
+      const float tz = first ? prv.tz[gi] : st.torque_z[gi];
       const float fex = st.f_ext[gi], fey = st.f_ext[M + gi];
       int64_t ax = 0, ay = 0;
       const int c0 = cell_index(pp.qx, pp.qy, lx, ly);
@@ -803,7 +834,7 @@ __device__ __forceinline__ void block_global_run_lds(const Derived* __restrict__
         float vx, vy, w;
         const bool last = s == n_steps - 1;
         bd_step(pc, pp, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
-                last, &vx, &vy, &w, first ? st.ang_prev[gi] : pp.an);
+                last, &vx, &vy, &w, first ? prv.ang[gi] : pp.an);
         if (last) {
           st.vel[gi] = vx;
           st.vel[M + gi] = vy;
@@ -871,14 +902,18 @@ __global__ __launch_bounds__(1024) void k_global(const Derived* __restrict__ d, 
   int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
   int32_t* cnt = wave_sums + 16;
   const uint64_t step0 = sd_mode ? 0ull : *step_ctr;
+  // reuse_forces slots: a BD window reads w & 1 and writes the next window's
+  // (w + 1) & 1; steepest descent does not advance the window counter, so it
+  // writes the slot the next window reads
+  const int par = window_parity(step_ctr);
   // the LDS variant assumes a periodic box (minimum image, folded cells)
   if (global_lds_extra_words(st.n, st.dims, 1 << (lx + ly)) && blockDim.x == 1024 && d->periodic)
     block_global_run_lds(d, st, blockIdx.x, n_steps, step0, lx, ly, sd_mode != 0, g, md, cnt,
-                         wave_sums, cnt + (1 << (lx + ly)) + 1, &pt);
+                         wave_sums, cnt + (1 << (lx + ly)) + 1, &pt, par);
   else
     block_global_run(d, st, sc, blockIdx.x, n_steps, step0, lx, ly, sd_mode != 0, g, md, cnt,
-                     wave_sums, &pt);
-  save_forces_env(st, blockIdx.x);
+                     wave_sums, &pt, par);
+  save_forces_env(st, blockIdx.x, sd_mode ? par : par ^ 1);
   if (!sd_mode) advance_counter(step_ctr, arrive, step0, n_steps);
 }
 
@@ -1885,7 +1920,7 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
                                          uint64_t step0, const float* __restrict__ table,
                                          int gw, int lane, uint2* lpos_w,
                                          unsigned long long* lacc_x, unsigned long long* lacc_y,
-                                         const PairTables& pt) {
+                                         const PairTables& pt, int par) {
   const int e = gw / sc.wmax;
   const int w = gw - e * sc.wmax;
   if (e >= n_envs) return;
@@ -1912,9 +1947,10 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     p.iy = st.img[M + gi];
     p.an = st.ang[gi];
     si = st.species[i];
-    fs = st.reuse ? st.f_prev[gi] : st.f_swim[gi];
-    tz = st.reuse ? st.tz_prev[gi] : st.torque_z[gi];
-    an0 = st.reuse ? st.ang_prev[gi] : p.an;
+    const PrevSlot prv = prev_slot(st, par);  // reuse_forces: this window's slot
+    fs = st.reuse ? prv.f[gi] : st.f_swim[gi];
+    tz = st.reuse ? prv.tz[gi] : st.torque_z[gi];
+    an0 = st.reuse ? prv.ang[gi] : p.an;
     fex = st.f_ext[gi];
     fey = st.f_ext[M + gi];
     // window-start snapshot for k_check's exact test and re-run (taken here,
@@ -2115,7 +2151,18 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     st.vel[M + gi] = vy;
     st.vel[2 * M + gi] = 0.0f;
     st.omega[gi] = om;
-    sc.disp[gi] = sqrt_rn(dmax2);
+    const float disp = sqrt_rn(dmax2);
+    sc.disp[gi] = disp;
+    if (!(disp < 0.5f * d->skin)) {  // a mover (k_check's exact test)
+      const int k = atomicAdd(&sc.nmov[e], 1);
+      if (k < kMaxMovers) sc.movers[(size_t)e * kMaxMovers + k] = i;
+    }
+    if (st.reuse) {  // the next window's sub-step 0 (the other slot)
+      const PrevSlot w = prev_slot(st, par ^ 1);
+      w.f[gi] = fs;
+      w.tz[gi] = tz;
+      w.ang[gi] = p.an;
+    }
   }
 }
 
@@ -2128,13 +2175,13 @@ __device__ __forceinline__ void run_wave_dispatch(const Derived* __restrict__ d,
                                                   int gw, int lane, uint2* lpos_w,
                                                   unsigned long long* lacc_x,
                                                   unsigned long long* lacc_y,
-                                                  const PairTables& pt) {
+                                                  const PairTables& pt, int par) {
   if (table)
     run_wave<kMulti, true, kWalls>(d, st, sc, n_envs, n_steps, step0, table, gw, lane, lpos_w,
-                                   lacc_x, lacc_y, pt);
+                                   lacc_x, lacc_y, pt, par);
   else
     run_wave<kMulti, false, kWalls>(d, st, sc, n_envs, n_steps, step0, nullptr, gw, lane, lpos_w,
-                                    lacc_x, lacc_y, pt);
+                                    lacc_x, lacc_y, pt, par);
 }
 
 // Throughput launch: 256-thread blocks, 4 waves each.  kWalls (host-chosen)
@@ -2158,7 +2205,7 @@ __global__ __launch_bounds__(256, SWARM_RUN_MINB) void k_cluster_run(const Deriv
   // normally guarantees it) -> the normals are drawn in the kernel
   run_wave_dispatch<kMulti, kWalls>(d, st, sc, n_envs, n_steps, step0,
                                     table_ok ? tables + par * noise_table_words(st.m) : nullptr,
-                                    gw, lane, lpos[wv], lacc[wv][0], lacc[wv][1], pt);
+                                    gw, lane, lpos[wv], lacc[wv][0], lacc[wv][1], pt, par);
 }
 
 // Latency-bound launch (few envs x particles: the run's waves fill few
@@ -2203,7 +2250,7 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
   const bool table_ok = ctl[kCtlTStep + par] == step0 && (uint64_t)n_steps <= ctl[kCtlTLen + par];
   run_wave_dispatch<kMulti, kWalls>(d, st, sc, n_envs, n_steps, step0,
                                     table_ok ? tables + par * noise_table_words(M) : nullptr, gw,
-                                    lane, lpos[wv], lacc[wv][0], lacc[wv][1], pt);
+                                    lane, lpos[wv], lacc[wv][0], lacc[wv][1], pt, par);
 }
 
 // The env's big clusters (wider than a wave) for the window, by k_check's
@@ -2217,7 +2264,7 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
 // lds: 6 * kBigMax + 2 words (uint2 positions, two u64 force sums).
 __device__ void run_big_clusters(const Derived* __restrict__ d, const DevState& st,
                                  const Scratch& sc, int e, int n_steps, uint64_t step0,
-                                 int32_t* lds, const PairTables* pt) {
+                                 int32_t* lds, const PairTables* pt, int par) {
   const int T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int nm = sc.big_n[e], np = sc.big_np[e];
@@ -2231,8 +2278,9 @@ __device__ void run_big_clusters(const Derived* __restrict__ d, const DevState& 
   const int si = st.species[i];
   const float fs = st.f_swim[gi], tz = st.torque_z[gi];
   // reuse_forces: sub-step 0 takes the previous run's actions and director
-  const float fs0 = st.reuse ? st.f_prev[gi] : fs, tz0 = st.reuse ? st.tz_prev[gi] : tz;
-  const uint32_t an0 = st.reuse ? st.ang_prev[gi] : p.an;
+  const PrevSlot prv = prev_slot(st, par);
+  const float fs0 = st.reuse ? prv.f[gi] : fs, tz0 = st.reuse ? prv.tz[gi] : tz;
+  const uint32_t an0 = st.reuse ? prv.ang[gi] : p.an;
   const float fex = st.f_ext[gi], fey = st.f_ext[M + gi];
   const PConst pc = load_pconst(d, si);
   if (mem) {
@@ -2306,7 +2354,18 @@ __device__ void run_big_clusters(const Derived* __restrict__ d, const DevState& 
     st.vel[M + gi] = vy;
     st.vel[2 * M + gi] = 0.0f;
     st.omega[gi] = om;
-    sc.disp[gi] = sqrt_rn(dmax2);
+    const float disp = sqrt_rn(dmax2);
+    sc.disp[gi] = disp;
+    if (!(disp < 0.5f * d->skin)) {  // a mover
+      const int k = atomicAdd(&sc.nmov[e], 1);
+      if (k < kMaxMovers) sc.movers[(size_t)e * kMaxMovers + k] = i;
+    }
+    if (st.reuse) {
+      const PrevSlot w = prev_slot(st, par ^ 1);
+      w.f[gi] = fs;
+      w.tz[gi] = tz;
+      w.ang[gi] = p.an;
+    }
   }
   __threadfence();
   __syncthreads();
@@ -2318,7 +2377,6 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
                                                 uint64_t* __restrict__ step_ctr,
                                                 uint32_t* __restrict__ arrive, int lx, int ly) {
   extern __shared__ __align__(16) unsigned char smem[];
-  constexpr int kMaxMovers = 1024;
   int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);  // 16
   int32_t* misc = wave_sums + 16;                          // 16
   int32_t* movers = misc + 16;                             // kMaxMovers
@@ -2328,21 +2386,24 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
   const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const uint64_t step0 = step_ctr[kCtlStep];
+  const int par = window_parity(step_ctr);  // reuse_forces slot of this window
   if (tid < 16) misc[tid] = 0;
   __syncthreads();
   const bool flagged_build = sc.fallback[e] != 0;
   if (!flagged_build && sc.big_n[e] > 0)
-    run_big_clusters(d, st, sc, e, n_steps, step0, cnt, &pt);
+    run_big_clusters(d, st, sc, e, n_steps, step0, cnt, &pt, par);
   if (!flagged_build) {
-    const float half = 0.5f * d->skin;
-    for (int i = tid; i < N; i += T) {
-      if (!(sc.disp[base + i] < half)) {
-        const int k = atomicAdd(&misc[0], 1);
-        if (k < kMaxMovers) movers[k] = i;
-      }
-    }
+    // the movers (displacement >= skin / 2) were listed by the run kernel
+    // and the big-cluster run: no scan over all colloids here
+    // (agent-scope loads: the big-cluster run of this workgroup appended
+    // entries a moment ago)
+    if (tid == 0) misc[0] = __hip_atomic_load(&sc.nmov[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     const int nm = misc[0];
+    for (int k = tid; k < min(nm, kMaxMovers); k += T)
+      movers[k] = __hip_atomic_load(&sc.movers[(size_t)e * kMaxMovers + k], __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
     if (nm > kMaxMovers) {
       if (tid == 0) misc[1] = 1;
     } else if (nm > 0) {
@@ -2404,12 +2465,14 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
     __syncthreads();
     if (global_lds_extra_words(N, st.dims, 1 << (lx + ly)))
       block_global_run_lds(d, st, e, n_steps, step0, lx, ly, false, 0.0f, 0.0f, cnt, wave_sums,
-                           cnt + (1 << (lx + ly)) + 1, &pt);
+                           cnt + (1 << (lx + ly)) + 1, &pt, par);
     else
       block_global_run(d, st, sc, e, n_steps, step0, lx, ly, false, 0.0f, 0.0f, cnt, wave_sums,
-                       &pt);
+                       &pt, par);
+    save_forces_env(st, e, par ^ 1);  // the re-run replaced the run kernel's final state
   }
-  save_forces_env(st, e);
+  __syncthreads();  // every read of nmov above is done
+  if (tid == 0) sc.nmov[e] = 0;
   advance_counter(step_ctr, arrive, step0, n_steps);
 }
 

@@ -85,7 +85,8 @@ __device__ __forceinline__ void rotate_director(float v[3], float px, float py, 
 __device__ void block_global_run3(const Derived* __restrict__ d, const DevState& st,
                                   const Scratch& sc, int e, int n_steps, uint64_t step0, int lx,
                                   int ly, int lz, bool sd_mode, float g, float md, int32_t* cnt,
-                                  int32_t* wave_sums, const PairTables* pt) {
+                                  int32_t* wave_sums, const PairTables* pt, int rp) {
+  const PrevSlot prv = prev_slot(st, rp);  // reuse_forces: sub-step 0 reads slot rp
   const int T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly + lz);
@@ -175,12 +176,12 @@ __device__ void block_global_run3(const Derived* __restrict__ d, const DevState&
       if (d->n_walls)
         wall_forces<3>(d, si, (float)q[0] * sx[0], (float)q[1] * sx[1], (float)q[2] * sx[2],
                        acc[0], acc[1], acc[2], st.wall_viol);
-      const float fs = first ? st.f_prev[gi] : st.f_swim[gi];
-      const float tq[3] = {first ? st.txy_prev[gi] : st.torque_xy[gi],
-                           first ? st.txy_prev[M + gi] : st.torque_xy[M + gi],
-                           first ? st.tz_prev[gi] : st.torque_z[gi]};
-      const float vs[3] = {first ? st.dir3_prev[gi] : v[0], first ? st.dir3_prev[M + gi] : v[1],
-                           first ? st.dir3_prev[2 * M + gi] : v[2]};
+      const float fs = first ? prv.f[gi] : st.f_swim[gi];
+      const float tq[3] = {first ? prv.txy[gi] : st.torque_xy[gi],
+                           first ? prv.txy[M + gi] : st.torque_xy[M + gi],
+                           first ? prv.tz[gi] : st.torque_z[gi]};
+      const float vs[3] = {first ? prv.dir3[gi] : v[0], first ? prv.dir3[M + gi] : v[1],
+                           first ? prv.dir3[2 * M + gi] : v[2]};
       float f[3], dq[3], ph[3];
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
@@ -268,9 +269,10 @@ __global__ __launch_bounds__(1024) void k_global3(const Derived* __restrict__ d,
   int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
   int32_t* cnt = wave_sums + 16;
   const uint64_t step0 = sd_mode ? 0ull : *step_ctr;
+  const int par = window_parity(step_ctr);  // reuse_forces slots (k_global)
   block_global_run3(d, st, sc, blockIdx.x, n_steps, step0, lx, ly, lz, sd_mode != 0, g, md, cnt,
-                    wave_sums, &pt);
-  save_forces_env(st, blockIdx.x);
+                    wave_sums, &pt, par);
+  save_forces_env(st, blockIdx.x, sd_mode ? par : par ^ 1);
   if (!sd_mode) advance_counter(step_ctr, arrive, step0, n_steps);
 }
 
