@@ -1021,7 +1021,7 @@ struct swarm_engine {
   int32_t* d_pairs = nullptr;
   size_t pairs_cap = 0;
   int lxg = 0, lyg = 0, lzg = 0;  // global-path grid: cell side >= rc_max (lzg: 3-D)
-  int lxb = 0, lyb = 0;  // cluster-build grid: cell side >= rc_max + skin
+  int lxb = 0, lyb = 0, lzb = 0;  // cluster-build grid: cell side >= rc_max + skin
   bool cluster_path = false;
   bool big_build = false;  // k_cluster_build<true>: cluster arrays in global memory
   VisionSorted vs{};
@@ -1097,6 +1097,11 @@ size_t check_lds_bytes(int lx, int ly, int n, int dims) {
   return (16 + 16 + 1024 + std::max(rerun, big)) * 4;
 }
 
+// k_check3: wave sums, misc, movers, then the 3-D global path's cell counts
+size_t check3_lds_bytes(const swarm_engine* e) {
+  return (16 + 16 + (size_t)swarm::kMaxMovers + (size_t)(1 << (e->lxg + e->lyg + e->lzg)) + 1) * 4;
+}
+
 // ROCm admits dynamic LDS up to the device limit at launch; this attribute
 // is only a hint, a refusal is not an error (a launch that really exceeds the
 // limit fails at hipGetLastError after the launch).
@@ -1152,7 +1157,7 @@ int launch_noise(swarm_engine* e, hipStream_t stream, int n) {
 
 // Cluster build of the next window.
 int launch_build(swarm_engine* e, hipStream_t stream) {
-  const int ncb = 1 << (e->lxb + e->lyb);
+  const int ncb = 1 << (e->lxb + e->lyb + e->lzb);
   if (e->env_build) {
     hipLaunchKernelGGL(swarm::k_build_env, dim3(e->n_envs), dim3(1024),
                        build_lds_bytes(e->n, e->sc.pair_cap), stream, e->d_derived, e->st, e->sc,
@@ -1160,15 +1165,26 @@ int launch_build(swarm_engine* e, hipStream_t stream) {
     HIP_TRY(hipGetLastError());
     return SWARM_OK;
   }
-  if (e->n > 4096)
+  if (e->params.n_dims == 3) {
+    if (e->n > 4096)
+      hipLaunchKernelGGL(swarm::k_build_sort3<16>, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4,
+                         stream, e->st, e->sc, e->lxb, e->lyb, e->lzb);
+    else
+      hipLaunchKernelGGL(swarm::k_build_sort3<4>, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4,
+                         stream, e->st, e->sc, e->lxb, e->lyb, e->lzb);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(swarm::k_build_pairs3, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
+                       dim3(256), 0, stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb, e->lzb);
+  } else if (e->n > 4096)
     hipLaunchKernelGGL(swarm::k_build_sort<16>, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4,
                        stream, e->st, e->sc, e->lxb, e->lyb);
   else
     hipLaunchKernelGGL(swarm::k_build_sort<4>, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4,
                        stream, e->st, e->sc, e->lxb, e->lyb);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(swarm::k_build_pairs, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
-                     dim3(256), 0, stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb);
+  if (e->params.n_dims != 3)
+    hipLaunchKernelGGL(swarm::k_build_pairs, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
+                       dim3(256), 0, stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb);
   HIP_TRY(hipGetLastError());
   if (e->big_build && swarm::build_lds_words_packed(e->n) * 4 <= kMaxLds &&
       !(std::getenv("SWARMRL_AMD_PACKED_BUILD") && std::getenv("SWARMRL_AMD_PACKED_BUILD")[0] == '0'))
@@ -1199,6 +1215,32 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
   const long waves = (long)e->n_envs * e->sc.wmax;
   const bool multi = e->params.n_species > 1;
   const bool walls = e->derived.n_walls != 0;
+  if (e->params.n_dims == 3) {
+    // one wave per block (so per CU) while the waves fit the chip, else four
+    const int tpb = waves <= 256 ? 64 : 256;
+    const dim3 grid((unsigned)((waves * 64 + tpb - 1) / tpb));
+#define SWARM_RUN3(MULTI, WALLS)                                                              \
+  hipLaunchKernelGGL((swarm::k_cluster_run3<MULTI, WALLS>), grid, dim3(tpb), 0, e->stream,     \
+                     e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step)
+    if (walls) {
+      if (multi)
+        SWARM_RUN3(true, true);
+      else
+        SWARM_RUN3(false, true);
+    } else {
+      if (multi)
+        SWARM_RUN3(true, false);
+      else
+        SWARM_RUN3(false, false);
+    }
+#undef SWARM_RUN3
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(swarm::k_check3, dim3(e->n_envs), dim3(1024), check3_lds_bytes(e), e->stream,
+                       e->d_derived, e->st, e->sc, n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg,
+                       e->lzg);
+    HIP_TRY(hipGetLastError());
+    return SWARM_OK;
+  }
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   if (e->profile) {
     HIP_TRY(hipEventCreate(&ev0));
@@ -1400,7 +1442,11 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     cell_grid3(*params, n_particles, e->derived.rc_max, &e->lxg, &e->lyg, &e->lzg);
   else
     cell_grid(*params, n_particles, e->derived.rc_max, &e->lxg, &e->lyg);
-  cell_grid(*params, n_particles, e->derived.rc_max + skin_um(), &e->lxb, &e->lyb);
+  if (three_d)
+    cell_grid3(*params, n_particles, e->derived.rc_max + skin_um(), &e->lxb, &e->lyb, &e->lzb);
+  else
+    cell_grid(*params, n_particles, e->derived.rc_max + skin_um(), &e->lxb, &e->lyb);
+  const int lcb = e->lxb + e->lyb + e->lzb;  // build cells 2^lcb
   // static LDS of the kernels: pair tables (k_global, k_check, k_cluster_run)
   // and the link table of k_cluster_build
   constexpr size_t kStaticLds = sizeof(swarm::PairTables);
@@ -1412,12 +1458,18 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   // build grid; otherwise every window runs on the global path
   e->big_build = build_is_big(n_particles);
   e->sc.pair_cap = build_pair_cap(n_particles, e->big_build);
-  // non-periodic boxes (no minimum image, edge cells) run on the global path
-  e->cluster_path = !three_d && params->periodic && e->sc.pair_cap >= n_particles &&
+  // non-periodic boxes (no minimum image, edge cells) run on the global path;
+  // SWARMRL_AMD_CLUSTER_PATH=0 forces it (A/B and parity of the two paths)
+  e->cluster_path = params->periodic && e->sc.pair_cap >= n_particles &&
                     n_particles < 65536 &&
                     swarm::build_lds_words_big(n_particles) * 4 <= kMaxLds &&
-                    (size_t)(16 + (1 << (e->lxb + e->lyb)) + 1) * 4 <= kMaxLds &&
-                    (1 << e->lxb) >= 3 && (1 << e->lyb) >= 3;
+                    (size_t)(16 + (1 << lcb) + 1) * 4 <= kMaxLds &&
+                    (1 << e->lxb) >= 3 && (1 << e->lyb) >= 3 && (!three_d || (1 << e->lzb) >= 3) &&
+                    (!three_d || check3_lds_bytes(e) <= kMaxLds);
+  {
+    const char* oc = std::getenv("SWARMRL_AMD_CLUSTER_PATH");
+    if (oc && oc[0] == '0') e->cluster_path = false;
+  }
   const size_t M = (size_t)n_envs * n_particles;
   int rc = SWARM_OK;
   rc = rc ? rc : dev_alloc(e, &e->st.q, 3 * M);
@@ -1477,16 +1529,17 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->sc.nmov, (size_t)n_envs);
   rc = rc ? rc : dev_alloc(e, &e->sc.movers, (size_t)n_envs * swarm::kMaxMovers);
   rc = rc ? rc : dev_alloc(e, &e->sc.sidx, M);
-  rc = rc ? rc : dev_alloc(e, &e->sc.bq, 2 * M);
-  rc = rc ? rc : dev_alloc(e, &e->sc.bimg, 2 * M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.bq, (three_d ? 3 : 2) * M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.bimg, (three_d ? 3 : 2) * M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.bdir3, three_d ? 3 * M : 1);
   rc = rc ? rc : dev_alloc(e, &e->sc.bang, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.root, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.slot_of, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.perm, (size_t)n_envs * S);
   rc = rc ? rc : dev_alloc(e, &e->sc.pairs, (size_t)n_envs * (S / 64) * swarm::kPairsPerWave);
-  rc = rc ? rc : dev_alloc(e, &e->sc.bsq, 2 * M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.bsq, (three_d ? 3 : 2) * M);
   rc = rc ? rc : dev_alloc(e, &e->sc.bsid, M);
-  rc = rc ? rc : dev_alloc(e, &e->sc.bcstart, (size_t)n_envs * ((1 << (e->lxb + e->lyb)) + 1));
+  rc = rc ? rc : dev_alloc(e, &e->sc.bcstart, (size_t)n_envs * ((1 << lcb) + 1));
   rc = rc ? rc : dev_alloc(e, &e->sc.gplist, (size_t)n_envs * std::max(e->sc.pair_cap, 1));
   rc = rc ? rc : dev_alloc(e, &e->sc.gnpairs, (size_t)n_envs);
   if (e->big_build) rc = rc ? rc : dev_alloc(e, &e->sc.gclus, 3 * M);
@@ -1509,7 +1562,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     bool want = latency_bound;
     if (ov && ov[0] == '0') want = false;
     if (ov && ov[0] == '1') want = true;
-    e->noise_table = want && e->derived.noisy && e->cluster_path;
+    e->noise_table = want && e->derived.noisy && e->cluster_path && !three_d;  // 3-D: drawn in the run
     if (e->noise_table)
       rc = rc ? rc : dev_alloc(e, &e->d_noise, 2 * swarm::noise_table_words(M));
     // the one-launch build (one CU per env) for throughput-bound engines
@@ -1519,12 +1572,12 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     {
       const int wm = S / 64;
       const size_t below = 16 + 16 + 3 * 68 + (size_t)((wm + 3) & ~3) + 4 * (size_t)n_particles;
-      e->env_build = e->cluster_path && !e->big_build && !latency_bound &&
+      e->env_build = e->cluster_path && !e->big_build && !latency_bound && !three_d &&
                      swarm::build_env_sort_words(n_particles, 1 << (e->lxb + e->lyb)) <= below;
       const char* ob = std::getenv("SWARMRL_AMD_ENV_BUILD");
       if (ob && ob[0] == '0') e->env_build = false;
       if (ob && ob[0] == '1')
-        e->env_build = e->cluster_path && !e->big_build &&
+        e->env_build = e->cluster_path && !e->big_build && !three_d &&
                        swarm::build_env_sort_words(n_particles, 1 << (e->lxb + e->lyb)) <= below;
     }
     // one block per CU for latency-bound runs; beside a run of up to 8192

@@ -177,8 +177,8 @@ struct Scratch {
   uint32_t* sqy;      // [M]
   uint32_t* sqz;      // [M] (3-D global path)
   int32_t* sidx;      // [M] particle index of a sorted entry
-  uint32_t* bq;       // [2][M] window-start snapshot
-  int32_t* bimg;      // [2][M]
+  uint32_t* bq;       // [dims][M] window-start snapshot
+  int32_t* bimg;      // [dims][M]
   uint32_t* bang;     // [M]
   int32_t* root;      // [M] cluster id (root particle)
   int32_t* slot_of;   // [M] wave slot of a particle
@@ -186,6 +186,7 @@ struct Scratch {
   uint32_t* pairs;    // [E][wmax][kPairsPerWave]: lane a | lane b << 6 | species pair << 12
   int32_t* wave_npairs;  // [E][wmax]
   float* disp;        // [M] max displacement over the window
+  float* bdir3;       // [3][M] window-start directors (3-D cluster path)
   int32_t* env_waves; // [E]
   int32_t* fallback;  // [E]
   int32_t* big_list;  // [E][kBigMax] particles of the env's big clusters (member order)
@@ -197,7 +198,7 @@ struct Scratch {
   int32_t* nmov;      // [E]
   int32_t* movers;    // [E][kMaxMovers]
   // cluster build (k_build_sort -> k_build_pairs -> k_cluster_build)
-  uint32_t* bsq;      // [2][M] cell-sorted positions (x, y)
+  uint32_t* bsq;      // [dims][M] cell-sorted positions (x, y[, z])
   int32_t* bsid;      // [M] particle | species << 24 of a sorted entry
   int32_t* bcstart;   // [E][ncb + 1] first sorted entry of every cell, [ncb] = N
   uint32_t* gplist;   // [E][pair_cap] neighbour pairs i | j << 16, i < j
@@ -1254,7 +1255,9 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   }
   __syncthreads();
   SWARM_STAMP(8);
-  if (tid == 0 && misc[4] > min(kBigMax, (int)blockDim.x)) misc[0] = 1;  // -> global path
+  // -> global path (3-D: any big cluster; its run is 2-D only)
+  if (tid == 0 && (misc[4] > min(kBigMax, (int)blockDim.x) || (st.dims == 3 && misc[4] > 0)))
+    misc[0] = 1;
   __syncthreads();
   if (misc[0]) {
     if (tid == 0) {
@@ -1513,7 +1516,9 @@ __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, 
   }
   __syncthreads();
   SWARM_STAMP(8);
-  if (tid == 0 && misc[4] > min(kBigMax, (int)blockDim.x)) misc[0] = 1;  // -> global path
+  // -> global path (3-D: any big cluster; its run is 2-D only)
+  if (tid == 0 && (misc[4] > min(kBigMax, (int)blockDim.x) || (st.dims == 3 && misc[4] > 0)))
+    misc[0] = 1;
   __syncthreads();
   if (misc[0]) {
     if (tid == 0) {
@@ -2158,9 +2163,10 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
       if (k < kMaxMovers) sc.movers[(size_t)e * kMaxMovers + k] = i;
     }
     if (st.reuse) {  // the next window's sub-step 0 (the other slot)
+      // (fs, tz hold this run's actions unless the window was one sub-step)
       const PrevSlot w = prev_slot(st, par ^ 1);
-      w.f[gi] = fs;
-      w.tz[gi] = tz;
+      w.f[gi] = n_steps > 1 ? fs : st.f_swim[gi];
+      w.tz[gi] = n_steps > 1 ? tz : st.torque_z[gi];
       w.ang[gi] = p.an;
     }
   }

@@ -276,4 +276,558 @@ __global__ __launch_bounds__(1024) void k_global3(const Derived* __restrict__ d,
   if (!sd_mode) advance_counter(step_ctr, arrive, step0, n_steps);
 }
 
+
+// ------------------------------------------------- 3-D cluster window
+// Build step 1 (3-D), one workgroup per env: counting sort into cells of
+// side >= rc_max + skin.  Same output layout as k_build_sort with a third
+// position row: bsq[0..2][M], bsid, bcstart[E][ncb + 1].
+template <int CH>
+__global__ __launch_bounds__(1024) void k_build_sort3(DevState st, Scratch sc, int lx, int ly,
+                                                      int lz) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int ncell = 1 << (lx + ly + lz);
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
+  int32_t* cnt = wave_sums + 16;
+  uint32_t cq[CH][3];
+  int32_t cid[CH];
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int i = tid + k * T;
+    const bool ok = i < N;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) cq[k][a] = ok ? st.q[a * M + base + i] : 0u;
+    cid[k] = ok ? (i | ((int32_t)st.species[i] << 24)) : -1;
+  }
+  for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
+  if (tid == 0) sc.gnpairs[e] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < CH; ++k)
+    if (cid[k] >= 0) atomicAdd(&cnt[cell_index3(cq[k][0], cq[k][1], cq[k][2], lx, ly, lz)], 1);
+  for (int i = tid + CH * T; i < N; i += T)
+    atomicAdd(&cnt[cell_index3(st.q[base + i], st.q[M + base + i], st.q[2 * M + base + i], lx, ly,
+                               lz)],
+              1);
+  __syncthreads();
+  block_exclusive_scan(cnt, ncell, wave_sums);
+  __syncthreads();
+  int32_t* cs = sc.bcstart + (size_t)e * (ncell + 1);
+  for (int c = tid; c <= ncell; c += T) cs[c] = cnt[c];
+  __syncthreads();  // cnt is read above and incremented below
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    if (cid[k] < 0) continue;
+    const size_t pos =
+        base + atomicAdd(&cnt[cell_index3(cq[k][0], cq[k][1], cq[k][2], lx, ly, lz)], 1);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) sc.bsq[a * M + pos] = cq[k][a];
+    sc.bsid[pos] = cid[k];
+  }
+  for (int i = tid + CH * T; i < N; i += T) {
+    const uint32_t qx = st.q[base + i], qy = st.q[M + base + i], qz = st.q[2 * M + base + i];
+    const size_t pos = base + atomicAdd(&cnt[cell_index3(qx, qy, qz, lx, ly, lz)], 1);
+    sc.bsq[pos] = qx;
+    sc.bsq[M + pos] = qy;
+    sc.bsq[2 * M + pos] = qz;
+    sc.bsid[pos] = i | ((int32_t)st.species[i] << 24);
+  }
+  for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
+}
+
+// Build step 2 (3-D), chip-wide (grid.y = env, one thread per sorted
+// entry): every pair within r_i + r_j + skin once (i < j), into the same
+// pair list k_cluster_build consumes.  The 27-cell stencil is nine rows
+// (y, z offsets), each a contiguous x range of the sorted order plus a wrap
+// range at the grid edge: 18 range bounds, loaded together.
+__global__ __launch_bounds__(256) void k_build_pairs3(const Derived* __restrict__ d, DevState st,
+                                                      Scratch sc, int lx, int ly, int lz) {
+  constexpr int kKeep = 8;
+  constexpr int kR = 18;
+  __shared__ float nb2[kMaxSpecies * kMaxSpecies];
+  for (int k = threadIdx.x; k < kMaxSpecies * kMaxSpecies; k += blockDim.x) nb2[k] = d->nb2[k];
+  const int e = blockIdx.y, N = st.n;
+  const int ps = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = ps < N;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int ncell = 1 << (lx + ly + lz);
+  const int32_t* cs = sc.bcstart + (size_t)e * (ncell + 1);
+  const int ncx = 1 << lx, ncy = 1 << ly, ncz = 1 << lz;
+  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+  const int loz = ncz >= 3 ? -1 : 0, hiz = ncz >= 3 ? 1 : ncz - 1;
+  const float sx0 = d->sx[0], sx1 = d->sx[1], sx2 = d->sx[2];
+  int pk = 0, i = 0;
+  uint32_t qx = 0, qy = 0, qz = 0;
+  if (valid) {
+    pk = sc.bsid[base + ps];
+    i = pk & 0xffffff;
+    qx = sc.bsq[base + ps];
+    qy = sc.bsq[M + base + ps];
+    qz = sc.bsq[2 * M + base + ps];
+  }
+  const int c0 = cell_index3(qx, qy, qz, lx, ly, lz);
+  const int cx = c0 & (ncx - 1), cy = (c0 >> lx) & (ncy - 1), cz = c0 >> (lx + ly);
+  const int xa = ncx >= 3 ? max(cx - 1, 0) : 0;
+  const int xb = ncx >= 3 ? min(cx + 1, ncx - 1) : ncx - 1;
+  const int xw = ncx >= 3 ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
+  int rb[kR], re[kR];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    const int row = r >> 1, part = r & 1;
+    const int oy = loy + row % 3, oz = loz + row / 3;
+    const bool use = valid && oy <= hiy && oz <= hiz && (part == 0 || xw >= 0);
+    const int rowc = ((((cz + oz + ncz) & (ncz - 1)) << ly) | ((cy + oy + ncy) & (ncy - 1))) << lx;
+    const int c_lo = rowc | (part == 0 ? xa : xw), c_hi = rowc | (part == 0 ? xb : xw);
+    rb[r] = use ? cs[c_lo] : 0;
+    re[r] = use ? cs[c_hi + 1] : 0;
+  }
+  __syncthreads();  // nb2
+  const float* nb2_row = nb2 + (pk >> 24) * kMaxSpecies;
+  int found = 0;
+  uint32_t keep[kKeep];
+#pragma unroll
+  for (int v = 0; v < kKeep; ++v) keep[v] = 0u;
+  auto near = [&](int jj, int packed) {
+    const float rx = (float)(int32_t)(sc.bsq[base + jj] - qx) * sx0;
+    const float ry = (float)(int32_t)(sc.bsq[M + base + jj] - qy) * sx1;
+    const float rz = (float)(int32_t)(sc.bsq[2 * M + base + jj] - qz) * sx2;
+    float r2 = rx * rx + ry * ry;
+    r2 = r2 + rz * rz;
+    return i < (packed & 0xffffff) && r2 < nb2_row[packed >> 24];
+  };
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    for (int jj0 = rb[r]; jj0 < re[r]; jj0 += 4) {
+      int pk4[4];
+      uint32_t x4[4], y4[4], z4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int jj = jj0 + u;
+        const bool ok = jj < re[r];
+        pk4[u] = ok ? sc.bsid[base + jj] : -1;
+        x4[u] = ok ? sc.bsq[base + jj] : 0u;
+        y4[u] = ok ? sc.bsq[M + base + jj] : 0u;
+        z4[u] = ok ? sc.bsq[2 * M + base + jj] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (pk4[u] < 0) continue;
+        const int j = pk4[u] & 0xffffff;
+        const float rx = (float)(int32_t)(x4[u] - qx) * sx0;
+        const float ry = (float)(int32_t)(y4[u] - qy) * sx1;
+        const float rz = (float)(int32_t)(z4[u] - qz) * sx2;
+        float r2 = rx * rx + ry * ry;
+        r2 = r2 + rz * rz;
+        if (i < j && r2 < nb2_row[pk4[u] >> 24]) {
+#pragma unroll
+          for (int v = 0; v < kKeep; ++v) keep[v] = found == v ? (uint32_t)j : keep[v];
+          ++found;
+        }
+      }
+    }
+  }
+  const int lane = threadIdx.x & 63;
+  int v = found;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(v, off, 64);
+    if (lane >= off) v += o;
+  }
+  int wbase = 0;
+  if (lane == 63) wbase = atomicAdd(&sc.gnpairs[e], v);
+  wbase = __shfl(wbase, 63, 64);
+  const int my_off = wbase + v - found;
+  uint32_t* out = sc.gplist + (size_t)e * sc.pair_cap;
+  if (!__any(found > kKeep)) {
+#pragma unroll
+    for (int u = 0; u < kKeep; ++u) {
+      const int k = my_off + u;
+      if (u < found && k < sc.pair_cap) out[k] = (uint32_t)i | (keep[u] << 16);
+    }
+    return;
+  }
+  // a lane found more than kKeep pairs: rescan and write in order
+  int w = 0;
+  for (int r = 0; r < kR; ++r) {
+    for (int jj = rb[r]; jj < re[r]; ++jj) {
+      const int packed = sc.bsid[base + jj];
+      if (near(jj, packed)) {
+        const int k = my_off + w;
+        if (k < sc.pair_cap) out[k] = (uint32_t)i | ((uint32_t)(packed & 0xffffff) << 16);
+        ++w;
+      }
+    }
+  }
+}
+
+// Branch-free pair_force3 for the run kernel's pair passes (pair_fix_sel
+// with a third component): the force on the first particle in 2^-24 fixed
+// point, zero out of range or for an empty slot (r2 = 0).
+__device__ __forceinline__ void pair_fix_sel3(float cut2, float sig6, float eps24, float rx,
+                                              float ry, float rz, int64_t& fx, int64_t& fy,
+                                              int64_t& fz) {
+  float r2 = rx * rx + ry * ry;
+  r2 = r2 + rz * rz;
+  const bool in = r2 < cut2 && r2 > 0.0f;
+  const float ir2 = 1.0f / (in ? r2 : 1.0f);
+  float ir6 = ir2 * ir2;
+  ir6 = ir6 * ir2;
+  const float s6 = sig6 * ir6;
+  float t = 2.0f * s6;
+  t = t - 1.0f;
+  float fr = eps24 * s6;
+  fr = fr * t;
+  fr = fr * ir2;
+  const float vx = (in ? -fr * rx : 0.0f) * 16777216.0f;
+  const float vy = (in ? -fr * ry : 0.0f) * 16777216.0f;
+  const float vz = (in ? -fr * rz : 0.0f) * 16777216.0f;
+  if (__builtin_expect(__all(fabsf(vx) < 2147483520.0f && fabsf(vy) < 2147483520.0f &&
+                             fabsf(vz) < 2147483520.0f),
+                       1)) {
+    fx = (int64_t)__float2int_rn(vx);
+    fy = (int64_t)__float2int_rn(vy);
+    fz = (int64_t)__float2int_rn(vz);
+  } else {
+    constexpr float kLim = 4.611686018427387904e18f;
+    fx = __float2ll_rn(fminf(fmaxf(vx, -kLim), kLim));
+    fy = __float2ll_rn(fminf(fmaxf(vy, -kLim), kLim));
+    fz = __float2ll_rn(fminf(fmaxf(vz, -kLim), kLim));
+  }
+}
+
+// One wave of the 3-D cluster run: all n_steps sub-steps of the particles
+// in its 64 slots (lane = particle), the wave's neighbour pairs one per lane
+// and pass, positions exchanged through the wave's LDS row, force sums as
+// int64 LDS atomics (order-free, so the bits of block_global_run3).  The
+// update is block_global_run3's sequence: translation from F = WCA + walls +
+// f_ext + f_swim * director, then the Rodrigues turn of the director; the
+// turn does not depend on the forces, so it is computed while the force sums
+// are in flight.  Normals are drawn here (translation: StepNoise, the
+// step_normals numbers; rotation: normals3 tag 2).
+template <bool kMulti, bool kWalls>
+__device__ __forceinline__ void run_wave3(const Derived* __restrict__ d, const DevState& st,
+                                          const Scratch& sc, int n_envs, int n_steps,
+                                          uint64_t step0, int gw, int lane, uint4* lpos_w,
+                                          unsigned long long* lacc_x, unsigned long long* lacc_y,
+                                          unsigned long long* lacc_z, const PairTables& pt,
+                                          int par) {
+  const int e = gw / sc.wmax;
+  const int w = gw - e * sc.wmax;
+  if (e >= n_envs) return;
+  if (sc.fallback[e] != 0 || w >= sc.env_waves[e]) return;
+  const int N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int slot = w * 64 + lane;
+  const int i = sc.perm[(size_t)e * sc.S + slot];
+  const bool active = i >= 0;
+  const size_t gi = base + (active ? i : 0);
+  const int si = kMulti ? st.species[active ? i : 0] : 0;
+  uint32_t q[3];
+  int32_t im[3];
+  float v[3], vs0[3], fex[3], tq[3];
+  float fs;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    q[a] = st.q[a * M + gi];
+    im[a] = st.img[a * M + gi];
+    v[a] = st.dir3[a * M + gi];
+    fex[a] = st.f_ext[a * M + gi];
+  }
+  {
+    // sub-step 0's swim force, torque and swim direction: with
+    // reuse_forces the previous run's (the current ones load after it)
+    const PrevSlot prv = prev_slot(st, par);
+    fs = st.reuse ? prv.f[gi] : st.f_swim[gi];
+    tq[0] = st.reuse ? prv.txy[gi] : st.torque_xy[gi];
+    tq[1] = st.reuse ? prv.txy[M + gi] : st.torque_xy[M + gi];
+    tq[2] = st.reuse ? prv.tz[gi] : st.torque_z[gi];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) vs0[a] = st.reuse ? prv.dir3[a * M + gi] : v[a];
+  }
+  if (active) {  // window-start snapshot (k_check3's exact test and re-run)
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      sc.bq[a * M + gi] = q[a];
+      sc.bimg[a * M + gi] = im[a];
+      sc.bdir3[a * M + gi] = v[a];
+    }
+  }
+  const int np = sc.wave_npairs[(size_t)e * sc.wmax + w];
+  const int npass = (np + 63) >> 6;
+  const uint32_t* pw = sc.pairs + ((size_t)e * sc.wmax + w) * kPairsPerWave;
+  const uint32_t pr0 = lane < np ? pw[lane] : 0xffffffffu;
+  lacc_x[lane] = 0ull;
+  lacc_y[lane] = 0ull;
+  lacc_z[lane] = 0ull;
+  const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
+  const float sx[3] = {d->sx[0], d->sx[1], d->sx[2]};
+  const float isx[3] = {d->inv_sx[0], d->inv_sx[1], d->inv_sx[2]};
+  const float eps24 = d->eps24;
+  const bool noisy = d->noisy != 0;
+  const float mob_dt = d->mob_dt[si], sig_t = d->sig_t[si], rot_dt = d->rot_dt[si],
+              sig_r = d->sig_r[si];
+  const float cut2_0 = d->cut2[0], sig6_0 = d->sig6[0];
+  const uint32_t q0[3] = {q[0], q[1], q[2]};
+  float dmax2 = 0.0f;
+  StepNoise noise;
+  auto substep = [&](const int s, auto first_t, auto last_t, auto pass_t)
+                     __attribute__((always_inline)) {
+    constexpr bool kFirst = decltype(first_t)::value;
+    constexpr bool kLast = decltype(last_t)::value;
+    constexpr int kPass = decltype(pass_t)::value;  // 0, 1, or 4: up to npass
+    const uint64_t step = step0 + (uint64_t)s;
+    float gt[3] = {0.0f, 0.0f, 0.0f}, gr[3] = {0.0f, 0.0f, 0.0f};
+    if (noisy) {
+      noise.next(k0, k1, (uint32_t)i, step, kFirst, gt);
+      normals3(k0, k1, (uint32_t)i, step, 2u, gr);
+    }
+    if (kPass > 0) {
+      lpos_w[lane] = make_uint4(q[0], q[1], q[2], 0u);
+      wave_lds_sync();
+      for (int p = 0; p < (kPass == 1 ? 1 : npass); ++p) {
+        const uint32_t e_ =
+            p == 0 ? pr0 : (p * 64 + lane < np ? pw[p * 64 + lane] : 0xffffffffu);
+        const int a = e_ == 0xffffffffu ? lane : (int)(e_ & 63u);
+        const int b = e_ == 0xffffffffu ? lane : (int)((e_ >> 6) & 63u);
+        const uint4 pa = lpos_w[a], pb = lpos_w[b];
+        const float rx = (float)(int32_t)(pb.x - pa.x) * sx[0];
+        const float ry = (float)(int32_t)(pb.y - pa.y) * sx[1];
+        const float rz = (float)(int32_t)(pb.z - pa.z) * sx[2];
+        int64_t fx, fy, fz;  // on a; b receives exactly the negation
+        if (kMulti) {
+          const int sp = (int)((e_ >> 12) & 255u);
+          pair_fix_sel3(pt.cut2[sp], pt.sig6[sp], eps24, rx, ry, rz, fx, fy, fz);
+        } else {
+          pair_fix_sel3(cut2_0, sig6_0, eps24, rx, ry, rz, fx, fy, fz);
+        }
+        atomicAdd(&lacc_x[a], (unsigned long long)fx);
+        atomicAdd(&lacc_y[a], (unsigned long long)fy);
+        atomicAdd(&lacc_z[a], (unsigned long long)fz);
+        atomicAdd(&lacc_x[b], (unsigned long long)(-fx));
+        atomicAdd(&lacc_y[b], (unsigned long long)(-fy));
+        atomicAdd(&lacc_z[b], (unsigned long long)(-fz));
+      }
+    }
+    // the director's turn (independent of the forces) while the sums land
+    __builtin_amdgcn_sched_barrier(0);
+    float ph[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      ph[a] = tq[a] * rot_dt;
+      if (noisy) ph[a] = ph[a] + sig_r * gr[a];
+    }
+    float vn[3] = {v[0], v[1], v[2]};
+    rotate_director(vn, ph[0], ph[1], ph[2]);
+    __builtin_amdgcn_sched_barrier(0);
+    __asm__ volatile("" ::: "memory");
+    int64_t acc[3] = {0, 0, 0};
+    if (kPass > 0) {
+      wave_lds_sync();
+      acc[0] = (int64_t)lacc_x[lane];
+      acc[1] = (int64_t)lacc_y[lane];
+      acc[2] = (int64_t)lacc_z[lane];
+      lacc_x[lane] = 0ull;
+      lacc_y[lane] = 0ull;
+      lacc_z[lane] = 0ull;
+    }
+    if (kWalls && active)
+      wall_forces<3>(d, si, (float)q[0] * sx[0], (float)q[1] * sx[1], (float)q[2] * sx[2], acc[0],
+                     acc[1], acc[2], st.wall_viol);
+    float f[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      f[a] = i64_to_f32(acc[a]) * 5.9604644775390625e-08f;
+      f[a] = f[a] + fex[a];
+      f[a] = f[a] + fs * (kFirst ? vs0[a] : v[a]);
+      float dq = f[a] * mob_dt;
+      if (noisy) dq = dq + sig_t * gt[a];
+      advance(q[a], im[a], f2i32(dq * isx[a]));
+    }
+    if (kLast && active) {  // velocities of the last sub-step
+      const float inv_gt = d->inv_gt[si], inv_gr = d->inv_gr[si];
+      float vv[3], ww[3];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        vv[a] = f[a] * inv_gt;
+        ww[a] = tq[a] * inv_gr;
+      }
+      if (noisy) {
+        float gv[3], gw[3];
+        normals3(k0, k1, (uint32_t)i, step, 1u, gv);
+        normals3(k0, k1, (uint32_t)i, step, 3u, gw);
+        const float sig_v = d->sig_v[si], sig_w = d->sig_w[si];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          vv[a] = vv[a] + sig_v * gv[a];
+          ww[a] = ww[a] + sig_w * gw[a];
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < 3; ++a) st.vel[a * M + gi] = vv[a];
+      st.omega_xy[gi] = ww[0];
+      st.omega_xy[M + gi] = ww[1];
+      st.omega[gi] = ww[2];
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) v[a] = vn[a];
+    float dd[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) dd[a] = (float)(int32_t)(q[a] - q0[a]) * sx[a];
+    float d2 = dd[0] * dd[0] + dd[1] * dd[1];
+    d2 = d2 + dd[2] * dd[2];
+    dmax2 = fmaxf(dmax2, d2);
+  };
+  auto run_steps = [&](auto pass_t) __attribute__((always_inline)) {
+    if (n_steps == 1) {
+      substep(0, std::true_type{}, std::true_type{}, pass_t);
+      return;
+    }
+    substep(0, std::true_type{}, std::false_type{}, pass_t);
+    if (st.reuse) {  // this run's actions from sub-step 1 on
+      fs = st.f_swim[gi];
+      tq[0] = st.torque_xy[gi];
+      tq[1] = st.torque_xy[M + gi];
+      tq[2] = st.torque_z[gi];
+    }
+    int s = 1;
+    for (; s < n_steps - 1; ++s) substep(s, std::false_type{}, std::false_type{}, pass_t);
+    substep(s, std::false_type{}, std::true_type{}, pass_t);
+  };
+  if (npass == 0)
+    run_steps(std::integral_constant<int, 0>{});
+  else if (npass == 1)
+    run_steps(std::integral_constant<int, 1>{});
+  else
+    run_steps(std::integral_constant<int, 4>{});
+  if (active) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      st.q[a * M + gi] = q[a];
+      st.img[a * M + gi] = im[a];
+      st.dir3[a * M + gi] = v[a];
+    }
+    const float disp = sqrt_rn(dmax2);
+    sc.disp[gi] = disp;
+    if (!(disp < 0.5f * d->skin)) {  // a mover (k_check3's exact test)
+      const int k = atomicAdd(&sc.nmov[e], 1);
+      if (k < kMaxMovers) sc.movers[(size_t)e * kMaxMovers + k] = i;
+    }
+    if (st.reuse) {  // the next window's sub-step 0 (the other slot)
+      // (fs, tq hold this run's actions unless the window was one sub-step)
+      const PrevSlot wsl = prev_slot(st, par ^ 1);
+      const bool one = n_steps == 1;
+      wsl.f[gi] = one ? st.f_swim[gi] : fs;
+      wsl.tz[gi] = one ? st.torque_z[gi] : tq[2];
+      wsl.txy[gi] = one ? st.torque_xy[gi] : tq[0];
+      wsl.txy[M + gi] = one ? st.torque_xy[M + gi] : tq[1];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) wsl.dir3[a * M + gi] = v[a];
+    }
+  }
+}
+
+// 3-D cluster run: 64 or 256 threads per block (one wave per CU for
+// latency-bound windows, four otherwise), one wave per 64 slots.
+template <bool kMulti, bool kWalls>
+__global__ __launch_bounds__(256) void k_cluster_run3(const Derived* __restrict__ d, DevState st,
+                                                      Scratch sc, int n_envs, int n_steps,
+                                                      const uint64_t* __restrict__ ctl) {
+  __shared__ PairTables pt;
+  __shared__ uint4 lpos[4][64];
+  __shared__ unsigned long long lacc[4][3][64];
+  stage_pair_tables(d, &pt);
+  const int par = window_parity(ctl);
+  const uint64_t step0 = ctl[kCtlStep];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  run_wave3<kMulti, kWalls>(d, st, sc, n_envs, n_steps, step0, gw, lane, lpos[wv], lacc[wv][0],
+                            lacc[wv][1], lacc[wv][2], pt, par);
+}
+
+// 3-D check, one workgroup per env: k_check's exact validity test of the
+// window (every mover against every colloid at the window-start positions,
+// d0 < rc + D_i + D_j only for listed neighbour pairs) in three dimensions;
+// a failed window (or one the build flagged: overflow, or any cluster wider
+// than a wave) is re-run from the snapshot on the 3-D global path.
+// LDS: 16 + 16 + kMaxMovers words, then the global path's cell counts.
+__global__ __launch_bounds__(1024) void k_check3(const Derived* __restrict__ d, DevState st,
+                                                 Scratch sc, int n_steps,
+                                                 uint64_t* __restrict__ step_ctr,
+                                                 uint32_t* __restrict__ arrive, int lx, int ly,
+                                                 int lz) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);  // 16
+  int32_t* misc = wave_sums + 16;                          // 16
+  int32_t* movers = misc + 16;                             // kMaxMovers
+  int32_t* cnt = movers + kMaxMovers;                      // global-path cell counts
+  __shared__ PairTables pt;
+  stage_pair_tables(d, &pt);
+  const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const uint64_t step0 = step_ctr[kCtlStep];
+  const int par = window_parity(step_ctr);
+  if (tid < 16) misc[tid] = 0;
+  __syncthreads();
+  const bool flagged_build = sc.fallback[e] != 0;
+  if (!flagged_build) {
+    const int nm = sc.nmov[e];
+    for (int k = tid; k < min(nm, kMaxMovers); k += T) movers[k] = sc.movers[(size_t)e * kMaxMovers + k];
+    __syncthreads();
+    if (nm > kMaxMovers) {
+      if (tid == 0) misc[1] = 1;
+    } else if (nm > 0) {
+      const float rc = d->rc_max_f;
+      const float sx0 = d->sx[0], sx1 = d->sx[1], sx2 = d->sx[2];
+      const long total = (long)nm * N;
+      for (long t = tid; t < total; t += T) {
+        const int m = movers[t / N];
+        const int j = (int)(t % N);
+        if (j == m) continue;
+        const float rx = (float)(int32_t)(sc.bq[base + j] - sc.bq[base + m]) * sx0;
+        const float ry = (float)(int32_t)(sc.bq[M + base + j] - sc.bq[M + base + m]) * sx1;
+        const float rz = (float)(int32_t)(sc.bq[2 * M + base + j] - sc.bq[2 * M + base + m]) * sx2;
+        const float lim = rc + sc.disp[base + m] + sc.disp[base + j] + 1e-3f;
+        float r2 = rx * rx + ry * ry;
+        r2 = r2 + rz * rz;
+        if (r2 < lim * lim) {
+          bool listed = false;
+          if (sc.root[base + j] == sc.root[base + m]) {  // same wave: its pairs
+            const int sm = sc.slot_of[base + m], sj = sc.slot_of[base + j];
+            const int wv = sm >> 6;
+            const uint32_t lm = (uint32_t)(sm & 63), lj = (uint32_t)(sj & 63);
+            const uint32_t* pw = sc.pairs + ((size_t)e * sc.wmax + wv) * kPairsPerWave;
+            const int np = sc.wave_npairs[(size_t)e * sc.wmax + wv];
+            for (int k = 0; k < np; ++k) {
+              const uint32_t a = pw[k] & 63u, b = (pw[k] >> 6) & 63u;
+              listed |= (a == lm && b == lj) || (a == lj && b == lm);
+            }
+          }
+          if (!listed) misc[1] = 1;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (flagged_build || misc[1] != 0) {
+    for (int i = tid; i < N && !flagged_build; i += T) {
+      const size_t gi = base + i;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        st.q[a * M + gi] = sc.bq[a * M + gi];
+        st.img[a * M + gi] = sc.bimg[a * M + gi];
+        st.dir3[a * M + gi] = sc.bdir3[a * M + gi];
+      }
+    }
+    if (tid == 0) sc.fallback[e] = 2;  // diagnostics: env re-run on the global path
+    __syncthreads();
+    block_global_run3(d, st, sc, e, n_steps, step0, lx, ly, lz, false, 0.0f, 0.0f, cnt, wave_sums,
+                      &pt, par);
+    save_forces_env(st, e, par ^ 1);  // the re-run replaced the run kernel's final state
+  }
+  __syncthreads();  // every read of nmov above is done
+  if (tid == 0) sc.nmov[e] = 0;
+  advance_counter(step_ctr, arrive, step0, n_steps);
+}
+
 }  // namespace swarm

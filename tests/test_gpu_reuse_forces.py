@@ -64,7 +64,7 @@ def test_reuse_cluster_path_4096_bit_exact(wide, E, monkeypatch):
     track = [oracle.ReuseForces(s) for s in states]
     check = sorted({0, E - 1})
     step = 0
-    for nsteps in (100, 37, 100):
+    for nsteps in (100, 37, 1, 100):  # 1: the saved actions of a one-sub-step window
         f = rng.choice([0.0, 10.0], E * n).astype(np.float32)
         t = rng.choice([-10.0, 0.0, 10.0], E * n).astype(np.float32)
         h.set_actions(f, t)
