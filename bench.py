@@ -59,6 +59,9 @@ def parse_args():
                     help="trajectory write interval in seconds (the reference default, "
                          "espresso.py:64-77); recorded on the device inside the captured "
                          "episode and drained without blocking between episodes")
+    ap.add_argument("--dims3", type=int, default=1,
+                    help="3-D at scale line ('dims3': BD+WCA slices of --colloids colloids in a "
+                         "periodic 3-D box on the cluster path vs the 3-D global path; 0: off)")
     ap.add_argument("--stub", action="store_true",
                     help="CPU plumbing test: no GPU, gloo, synthetic trajectories")
     return ap.parse_args()
@@ -159,6 +162,83 @@ def build_c5_workload(args, env_seed, device):
     ff = ForceFunction({"0": agent})
     agent.reset_agent(eng.colloids)
     return eng, ff, agent
+
+
+def measure_dims3(args, E, reps, global_reps=0):
+    """3-D at scale: n_dims=3 is the reference engine's default
+    (EspressoMD(n_dims=3), espresso.py:143-152).  E envs of --colloids
+    colloids at volume fraction 0.04 (placed in the centred sphere, overlaps
+    removed), random swim forces and lab-frame torques, timed over `reps`
+    slices of 100 BD+WCA sub-steps (engine only: the reference's vision
+    cones are 2-D).  At this density the rc + skin graph percolates, so the
+    engine takes the neighbour-list window (one chip-wide launch per
+    sub-step); also timed: the cluster window forced (its clusters exceed a
+    wave, so every window re-runs) and the 3-D global path (one workgroup
+    per env per window, the round-1 3-D path), global_reps slices each."""
+    import torch
+
+    from swarmrl_amd.engine import MDParams, SwarmEngine
+    from swarmrl_amd.units import UnitRegistry
+
+    N = args.colloids
+    L = (N * (4.0 / 3.0) * math.pi / 0.04) ** (1.0 / 3.0)
+    ureg = UnitRegistry()
+    params = MDParams(ureg=ureg, box_length=ureg.Quantity([L, L, L], "micrometer"),
+                      time_step=ureg.Quantity(1e-3, "second"),
+                      time_slice=ureg.Quantity(0.1, "second"),
+                      write_interval=ureg.Quantity(1e4, "second"))
+    rng = np.random.default_rng(7)
+    f = rng.choice([0.0, 10.0], E * N).astype(np.float32)
+    tq = rng.normal(scale=5.0, size=(3, E * N)).astype(np.float32)
+
+    def make(mode):
+        os.environ["SWARMRL_AMD_CLUSTER_PATH"] = "0" if mode == "global" else "1"
+        os.environ["SWARMRL_AMD_NLIST"] = "1" if mode == "nlist" else "0"
+        try:
+            eng = SwarmEngine(params, n_dims=3, seed=11, n_envs=E,
+                              out_folder=f"/tmp/swarm_bench_3d_{os.getpid()}")
+            eng.add_colloids(N, ureg.Quantity(1.0, "micrometer"),
+                             ureg.Quantity(np.array([L / 2, L / 2, L / 2]), "micrometer"),
+                             ureg.Quantity(L / 2, "micrometer"))
+            eng.integrate(1)  # set-up, overlap removal, one slice
+        finally:
+            del os.environ["SWARMRL_AMD_CLUSTER_PATH"]
+            del os.environ["SWARMRL_AMD_NLIST"]
+        nat = eng._native
+        nat.bind_stream()
+        nat.call("swarm_engine_set_actions", f.ctypes.data, tq[2].copy().ctypes.data, 0)
+        nat.call("swarm_engine_set_torque_xy", np.ascontiguousarray(tq[:2]).ctypes.data, 0)
+        return eng
+
+    def time_slices(eng, n):
+        for _ in range(3):
+            eng._run(100)
+        torch.cuda.synchronize()
+        t0 = torch.cuda.Event(enable_timing=True)
+        t1 = torch.cuda.Event(enable_timing=True)
+        t0.record()
+        for _ in range(n):
+            eng._run(100)
+        t1.record()
+        t1.synchronize()
+        return t0.elapsed_time(t1) / n
+
+    eng = make("nlist")
+    ms = time_slices(eng, reps)
+    fb = np.zeros(E, np.int32)
+    waves = np.zeros(E, np.int32)
+    eng._native.call("swarm_engine_window_stats", fb.ctypes.data, waves.ctypes.data)
+    out = {"envs": E, "colloids_per_env": N, "path": "neighbour-list window", "ms_per_slice": ms,
+           "value": E * N / (ms * 1e-3), "unit": "colloid-slices/s (100 sub-steps each)",
+           "last_window_reruns": int((fb == 2).sum()), "last_window_flagged": int((fb == 1).sum())}
+    del eng
+    if global_reps > 0:
+        for mode in ("cluster", "global"):
+            g = make(mode)
+            out[f"{mode}_path_ms_per_slice"] = time_slices(g, global_reps)
+            del g
+        out["speedup_vs_global_path"] = out["global_path_ms_per_slice"] / ms
+    return out
 
 
 def time_run_kernel(eng, reps):
@@ -624,6 +704,14 @@ def main():
                 "per_rank_value": c5["per_rank"],
                 "roofline": c5["roofline"],
             }
+        if args.dims3 and world == 1:
+            head["dims3"] = {
+                "workload": f"3-D at scale: {args.colloids} colloids per env, periodic box at "
+                            f"volume fraction 0.04, BD+WCA slices of 100 sub-steps (engine only)",
+                "E1": measure_dims3(args, 1, 50, global_reps=3),
+                f"E{args.batched_envs}": measure_dims3(args, max(args.batched_envs, 1), 20,
+                                                       global_reps=2),
+            }
     if world > 1 and dist.get_world_size() != args.gpus:
         print("bench.py: process group size differs from --gpus", file=sys.stderr)
         sys.exit(2)
@@ -660,7 +748,7 @@ def main():
     }
     if "gather" in head:
         line["gather"] = head["gather"]
-    for k in ("c5",):
+    for k in ("c5", "dims3"):
         if k in head:
             line[k] = head[k]
     if batched is not None:

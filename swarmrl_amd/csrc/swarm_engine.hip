@@ -1023,6 +1023,9 @@ struct swarm_engine {
   int lxg = 0, lyg = 0, lzg = 0;  // global-path grid: cell side >= rc_max (lzg: 3-D)
   int lxb = 0, lyb = 0, lzb = 0;  // cluster-build grid: cell side >= rc_max + skin
   bool cluster_path = false;
+  // 3-D boxes whose rc + skin graph percolates: chip-wide sub-steps over a
+  // per-window Verlet list instead of per-wave clusters (swarm_integrator3.cuh)
+  bool nlist_path = false;
   bool big_build = false;  // k_cluster_build<true>: cluster arrays in global memory
   VisionSorted vs{};
   // latency-bound windows read their normals from a table (k_noise)
@@ -1173,6 +1176,12 @@ int launch_build(swarm_engine* e, hipStream_t stream) {
       hipLaunchKernelGGL(swarm::k_build_sort3<4>, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4,
                          stream, e->st, e->sc, e->lxb, e->lyb, e->lzb);
     HIP_TRY(hipGetLastError());
+    if (e->nlist_path) {  // Verlet lists, no clusters
+      hipLaunchKernelGGL(swarm::k_build_nlist3, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
+                         dim3(256), 0, stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb, e->lzb);
+      HIP_TRY(hipGetLastError());
+      return SWARM_OK;
+    }
     hipLaunchKernelGGL(swarm::k_build_pairs3, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
                        dim3(256), 0, stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb, e->lzb);
   } else if (e->n > 4096)
@@ -1215,6 +1224,33 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
   const long waves = (long)e->n_envs * e->sc.wmax;
   const bool multi = e->params.n_species > 1;
   const bool walls = e->derived.n_walls != 0;
+  if (e->params.n_dims == 3 && e->nlist_path) {
+    const long M = (long)e->n_envs * e->n;
+    const dim3 grid((unsigned)((M + 255) / 256));
+    for (int s = 0; s < n_steps; ++s) {
+#define SWARM_NL(MULTI, WALLS)                                                                \
+  hipLaunchKernelGGL((swarm::k_nl_step3<MULTI, WALLS>), grid, dim3(256), 0, e->stream,         \
+                     e->d_derived, e->st, e->sc, n_steps, s, e->d_step)
+      if (walls) {
+        if (multi)
+          SWARM_NL(true, true);
+        else
+          SWARM_NL(false, true);
+      } else {
+        if (multi)
+          SWARM_NL(true, false);
+        else
+          SWARM_NL(false, false);
+      }
+#undef SWARM_NL
+      HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(swarm::k_check3, dim3(e->n_envs), dim3(1024), check3_lds_bytes(e), e->stream,
+                       e->d_derived, e->st, e->sc, n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg,
+                       e->lzg, 1);
+    HIP_TRY(hipGetLastError());
+    return SWARM_OK;
+  }
   if (e->params.n_dims == 3) {
     // one wave per block (so per CU) while the waves fit the chip, else four
     const int tpb = waves <= 256 ? 64 : 256;
@@ -1237,7 +1273,7 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(swarm::k_check3, dim3(e->n_envs), dim3(1024), check3_lds_bytes(e), e->stream,
                        e->d_derived, e->st, e->sc, n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg,
-                       e->lzg);
+                       e->lzg, 0);
     HIP_TRY(hipGetLastError());
     return SWARM_OK;
   }
@@ -1470,6 +1506,21 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     const char* oc = std::getenv("SWARMRL_AMD_CLUSTER_PATH");
     if (oc && oc[0] == '0') e->cluster_path = false;
   }
+  if (three_d && e->cluster_path) {
+    // mean number of colloids within 2 r_max + skin of one: above ~2 the
+    // links percolate into clusters wider than a wave (which re-run on the
+    // global path), so the window runs on the neighbour-list path instead.
+    // SWARMRL_AMD_NLIST=0|1 overrides.
+    double rmax = 0.0;
+    for (int s = 0; s < params->n_species; ++s) rmax = std::max(rmax, params->radius[s]);
+    const double link = 2.0 * rmax + skin_um();
+    const double vol = params->box[0] * params->box[1] * params->box[2];
+    const double deg = (double)n_particles / vol * (2.0 / 3.0) * kTwoPi * link * link * link;
+    e->nlist_path = deg > 2.0;
+    const char* on = std::getenv("SWARMRL_AMD_NLIST");
+    if (on && on[0] == '0') e->nlist_path = false;
+    if (on && on[0] == '1') e->nlist_path = true;
+  }
   const size_t M = (size_t)n_envs * n_particles;
   int rc = SWARM_OK;
   rc = rc ? rc : dev_alloc(e, &e->st.q, 3 * M);
@@ -1538,6 +1589,9 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->sc.perm, (size_t)n_envs * S);
   rc = rc ? rc : dev_alloc(e, &e->sc.pairs, (size_t)n_envs * (S / 64) * swarm::kPairsPerWave);
   rc = rc ? rc : dev_alloc(e, &e->sc.bsq, (three_d ? 3 : 2) * M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.nl, e->nlist_path ? (size_t)swarm::kNlMax * M : 1);
+  rc = rc ? rc : dev_alloc(e, &e->sc.nn, e->nlist_path ? M : 1);
+  rc = rc ? rc : dev_alloc(e, &e->sc.qalt, e->nlist_path ? 3 * M : 1);
   rc = rc ? rc : dev_alloc(e, &e->sc.bsid, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.bcstart, (size_t)n_envs * ((1 << lcb) + 1));
   rc = rc ? rc : dev_alloc(e, &e->sc.gplist, (size_t)n_envs * std::max(e->sc.pair_cap, 1));

@@ -197,6 +197,10 @@ struct Scratch {
   // kernel and the big-cluster run, consumed and reset by k_check)
   int32_t* nmov;      // [E]
   int32_t* movers;    // [E][kMaxMovers]
+  // neighbour-list path (dense 3-D boxes, swarm_integrator3.cuh)
+  int32_t* nl;        // [kNlMax][M] neighbours j | species << 24 of particle gi
+  int32_t* nn;        // [M] neighbour count
+  uint32_t* qalt;     // [3][M] second position buffer (sub-steps alternate)
   // cluster build (k_build_sort -> k_build_pairs -> k_cluster_build)
   uint32_t* bsq;      // [dims][M] cell-sorted positions (x, y[, z])
   int32_t* bsid;      // [M] particle | species << 24 of a sorted entry

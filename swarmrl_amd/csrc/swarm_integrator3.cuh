@@ -301,7 +301,10 @@ __global__ __launch_bounds__(1024) void k_build_sort3(DevState st, Scratch sc, i
     cid[k] = ok ? (i | ((int32_t)st.species[i] << 24)) : -1;
   }
   for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
-  if (tid == 0) sc.gnpairs[e] = 0;
+  if (tid == 0) {
+    sc.gnpairs[e] = 0;
+    sc.fallback[e] = 0;  // the neighbour-list build sets it on overflow
+  }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < CH; ++k)
@@ -755,7 +758,7 @@ __global__ __launch_bounds__(1024) void k_check3(const Derived* __restrict__ d, 
                                                  Scratch sc, int n_steps,
                                                  uint64_t* __restrict__ step_ctr,
                                                  uint32_t* __restrict__ arrive, int lx, int ly,
-                                                 int lz) {
+                                                 int lz, int nlist) {
   extern __shared__ __align__(16) unsigned char smem[];
   int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);  // 16
   int32_t* misc = wave_sums + 16;                          // 16
@@ -770,6 +773,14 @@ __global__ __launch_bounds__(1024) void k_check3(const Derived* __restrict__ d, 
   if (tid < 16) misc[tid] = 0;
   __syncthreads();
   const bool flagged_build = sc.fallback[e] != 0;
+  if (!flagged_build && nlist && (n_steps & 1)) {
+    // neighbour-list path, odd window: the last sub-step wrote the second
+    // position buffer (the exact test below reads only the snapshot)
+    for (int k = tid; k < 3 * N; k += T) {
+      const size_t o = (size_t)(k / N) * M + base + (k % N);
+      st.q[o] = sc.qalt[o];
+    }
+  }
   if (!flagged_build) {
     const int nm = sc.nmov[e];
     for (int k = tid; k < min(nm, kMaxMovers); k += T) movers[k] = sc.movers[(size_t)e * kMaxMovers + k];
@@ -792,7 +803,11 @@ __global__ __launch_bounds__(1024) void k_check3(const Derived* __restrict__ d, 
         r2 = r2 + rz * rz;
         if (r2 < lim * lim) {
           bool listed = false;
-          if (sc.root[base + j] == sc.root[base + m]) {  // same wave: its pairs
+          if (nlist) {  // j among m's listed neighbours
+            const int nn = sc.nn[base + m];
+            for (int k = 0; k < nn; ++k)
+              listed |= (sc.nl[(size_t)k * M + base + m] & 0xffffff) == j;
+          } else if (sc.root[base + j] == sc.root[base + m]) {  // same wave: its pairs
             const int sm = sc.slot_of[base + m], sj = sc.slot_of[base + j];
             const int wv = sm >> 6;
             const uint32_t lm = (uint32_t)(sm & 63), lj = (uint32_t)(sj & 63);
@@ -828,6 +843,253 @@ __global__ __launch_bounds__(1024) void k_check3(const Derived* __restrict__ d, 
   __syncthreads();  // every read of nmov above is done
   if (tid == 0) sc.nmov[e] = 0;
   advance_counter(step_ctr, arrive, step0, n_steps);
+}
+
+
+// ------------------------------------------- 3-D neighbour-list window
+// Dense boxes (the rc + skin graph percolates: most colloids in clusters
+// wider than a wave) cannot be cut into per-wave clusters.  There the window
+// keeps the same build grid, exact check and re-run, but the sub-steps run
+// chip-wide: a Verlet list (every j within r_i + r_j + skin) per colloid,
+// then one launch per sub-step with one thread per colloid, reading the
+// positions of sub-step s from one buffer and writing the other (st.q and
+// sc.qalt alternate; k_check3 copies back after an odd window).  Forces,
+// noise and update are block_global_run3's, so the bits are the same.
+constexpr int kNlMax = 48;  // neighbours per colloid (more: the env re-runs)
+
+// Build step 2 (neighbour-list path), grid (ceil(N / 256), E), one thread
+// per sorted entry: its neighbours into nl[k][gi] (neighbour-major, so the
+// sub-step's reads coalesce).
+__global__ __launch_bounds__(256) void k_build_nlist3(const Derived* __restrict__ d, DevState st,
+                                                      Scratch sc, int lx, int ly, int lz) {
+  constexpr int kR = 18;
+  __shared__ float nb2[kMaxSpecies * kMaxSpecies];
+  for (int k = threadIdx.x; k < kMaxSpecies * kMaxSpecies; k += blockDim.x) nb2[k] = d->nb2[k];
+  __syncthreads();
+  const int e = blockIdx.y, N = st.n;
+  const int ps = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ps >= N) return;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int ncell = 1 << (lx + ly + lz);
+  const int32_t* cs = sc.bcstart + (size_t)e * (ncell + 1);
+  const int ncx = 1 << lx, ncy = 1 << ly, ncz = 1 << lz;
+  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+  const int loz = ncz >= 3 ? -1 : 0, hiz = ncz >= 3 ? 1 : ncz - 1;
+  const float sx0 = d->sx[0], sx1 = d->sx[1], sx2 = d->sx[2];
+  const int pk = sc.bsid[base + ps];
+  const int i = pk & 0xffffff;
+  const uint32_t qx = sc.bsq[base + ps], qy = sc.bsq[M + base + ps], qz = sc.bsq[2 * M + base + ps];
+  const int c0 = cell_index3(qx, qy, qz, lx, ly, lz);
+  const int cx = c0 & (ncx - 1), cy = (c0 >> lx) & (ncy - 1), cz = c0 >> (lx + ly);
+  const int xa = ncx >= 3 ? max(cx - 1, 0) : 0;
+  const int xb = ncx >= 3 ? min(cx + 1, ncx - 1) : ncx - 1;
+  const int xw = ncx >= 3 ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
+  int rb[kR], re[kR];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    const int row = r >> 1, part = r & 1;
+    const int oy = loy + row % 3, oz = loz + row / 3;
+    const bool use = oy <= hiy && oz <= hiz && (part == 0 || xw >= 0);
+    const int rowc = ((((cz + oz + ncz) & (ncz - 1)) << ly) | ((cy + oy + ncy) & (ncy - 1))) << lx;
+    const int c_lo = rowc | (part == 0 ? xa : xw), c_hi = rowc | (part == 0 ? xb : xw);
+    rb[r] = use ? cs[c_lo] : 0;
+    re[r] = use ? cs[c_hi + 1] : 0;
+  }
+  const float* nb2_row = nb2 + (pk >> 24) * kMaxSpecies;
+  int cnt = 0;
+  int32_t* out = sc.nl + base + i;
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    for (int jj0 = rb[r]; jj0 < re[r]; jj0 += 4) {
+      int pk4[4];
+      uint32_t x4[4], y4[4], z4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int jj = jj0 + u;
+        const bool ok = jj < re[r];
+        pk4[u] = ok ? sc.bsid[base + jj] : -1;
+        x4[u] = ok ? sc.bsq[base + jj] : 0u;
+        y4[u] = ok ? sc.bsq[M + base + jj] : 0u;
+        z4[u] = ok ? sc.bsq[2 * M + base + jj] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (pk4[u] < 0 || (pk4[u] & 0xffffff) == i) continue;
+        const float rx = (float)(int32_t)(x4[u] - qx) * sx0;
+        const float ry = (float)(int32_t)(y4[u] - qy) * sx1;
+        const float rz = (float)(int32_t)(z4[u] - qz) * sx2;
+        float r2 = rx * rx + ry * ry;
+        r2 = r2 + rz * rz;
+        if (r2 < nb2_row[pk4[u] >> 24]) {
+          if (cnt < kNlMax) out[(size_t)cnt * M] = pk4[u];
+          ++cnt;
+        }
+      }
+    }
+  }
+  sc.nn[base + i] = min(cnt, kNlMax);
+  if (cnt > kNlMax) sc.fallback[e] = 1;  // -> the env re-runs on the global path
+}
+
+// Sub-step s of the neighbour-list window, one thread per colloid of every
+// env: block_global_run3's force sum (over the listed neighbours: pairs
+// beyond them cannot be in range while k_check3's test holds) and update.
+// Reads positions from (s odd ? qalt : q), writes the other buffer; image
+// counters and directors are the colloid's own and update in place.
+// sc.disp holds the squared maximum displacement until the last sub-step.
+template <bool kMulti, bool kWalls>
+__global__ __launch_bounds__(256) void k_nl_step3(const Derived* __restrict__ d, DevState st,
+                                                  Scratch sc, int n_steps, int s,
+                                                  const uint64_t* __restrict__ ctl) {
+  __shared__ PairTables pt;
+  if (kMulti) stage_pair_tables(d, &pt);
+  const size_t M = (size_t)st.m;
+  const size_t gi = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi >= M) return;
+  const int N = st.n;
+  const int e = (int)(gi / N), i = (int)(gi - (size_t)e * N);
+  if (sc.fallback[e] != 0) return;
+  const size_t base = (size_t)e * N;
+  const bool first = s == 0, last = s == n_steps - 1;
+  const uint32_t* R = (s & 1) ? sc.qalt : st.q;
+  uint32_t* W = (s & 1) ? st.q : sc.qalt;
+  const int par = window_parity(ctl);
+  const uint64_t step = ctl[kCtlStep] + (uint64_t)s;
+  const int si = kMulti ? st.species[i] : 0;
+  const float sx[3] = {d->sx[0], d->sx[1], d->sx[2]};
+  uint32_t q[3], q0[3];
+  int32_t im[3];
+  float v[3];
+  // issue every own load first: one memory latency
+  const int nn = sc.nn[gi];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    q[a] = R[a * M + gi];
+    im[a] = st.img[a * M + gi];
+    v[a] = st.dir3[a * M + gi];
+  }
+  float dmax2 = 0.0f;
+  if (first) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      q0[a] = q[a];
+      sc.bq[a * M + gi] = q[a];
+      sc.bimg[a * M + gi] = im[a];
+      sc.bdir3[a * M + gi] = v[a];
+    }
+  } else {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) q0[a] = sc.bq[a * M + gi];
+    dmax2 = sc.disp[gi];
+  }
+  const bool reuse0 = st.reuse && first;  // sub-step 0 reuses the previous run's actions
+  const PrevSlot prv = prev_slot(st, par);
+  const float fs = reuse0 ? prv.f[gi] : st.f_swim[gi];
+  const float tq[3] = {reuse0 ? prv.txy[gi] : st.torque_xy[gi],
+                       reuse0 ? prv.txy[M + gi] : st.torque_xy[M + gi],
+                       reuse0 ? prv.tz[gi] : st.torque_z[gi]};
+  float vs[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) vs[a] = reuse0 ? prv.dir3[a * M + gi] : v[a];
+  const float eps24 = d->eps24;
+  int64_t acc[3] = {0, 0, 0};
+  const int32_t* nlp = sc.nl + gi;
+  for (int k0 = 0; k0 < nn; k0 += 4) {
+    int32_t pk[4];
+    uint32_t qj[4][3];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pk[u] = k0 + u < nn ? nlp[(size_t)(k0 + u) * M] : -1;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t gj = base + (pk[u] < 0 ? i : (pk[u] & 0xffffff));
+#pragma unroll
+      for (int a = 0; a < 3; ++a) qj[u][a] = R[a * M + gj];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (pk[u] < 0) continue;
+      const float rx = (float)(int32_t)(qj[u][0] - q[0]) * sx[0];
+      const float ry = (float)(int32_t)(qj[u][1] - q[1]) * sx[1];
+      const float rz = (float)(int32_t)(qj[u][2] - q[2]) * sx[2];
+      if (kMulti) {
+        const int sp = si * kMaxSpecies + (pk[u] >> 24);
+        pair_force3(pt.cut2[sp], pt.sig6[sp], eps24, rx, ry, rz, acc[0], acc[1], acc[2]);
+      } else {
+        pair_force3(d->cut2[0], d->sig6[0], eps24, rx, ry, rz, acc[0], acc[1], acc[2]);
+      }
+    }
+  }
+  if (kWalls)
+    wall_forces<3>(d, si, (float)q[0] * sx[0], (float)q[1] * sx[1], (float)q[2] * sx[2], acc[0],
+                   acc[1], acc[2], st.wall_viol);
+  const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
+  const bool noisy = d->noisy != 0;
+  float f[3], ph[3];
+  float gt[3], gr[3];
+  if (noisy) {
+    step_normals(k0, k1, (uint32_t)i, step, gt);
+    normals3(k0, k1, (uint32_t)i, step, 2u, gr);
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    f[a] = i64_to_f32(acc[a]) * 5.9604644775390625e-08f;
+    f[a] = f[a] + st.f_ext[a * M + gi];
+    f[a] = f[a] + fs * vs[a];
+    float dq = f[a] * d->mob_dt[si];
+    ph[a] = tq[a] * d->rot_dt[si];
+    if (noisy) {
+      dq = dq + d->sig_t[si] * gt[a];
+      ph[a] = ph[a] + d->sig_r[si] * gr[a];
+    }
+    advance(q[a], im[a], f2i32(dq * d->inv_sx[a]));
+  }
+  rotate_director(v, ph[0], ph[1], ph[2]);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    W[a * M + gi] = q[a];
+    st.img[a * M + gi] = im[a];
+    st.dir3[a * M + gi] = v[a];
+  }
+  float dd[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) dd[a] = (float)(int32_t)(q[a] - q0[a]) * sx[a];
+  float d2 = dd[0] * dd[0] + dd[1] * dd[1];
+  d2 = d2 + dd[2] * dd[2];
+  dmax2 = fmaxf(dmax2, d2);
+  if (!last) {
+    sc.disp[gi] = dmax2;
+    return;
+  }
+  {  // velocities of the last sub-step (block_global_run3's sequence)
+    float vv[3], ww[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      vv[a] = f[a] * d->inv_gt[si];
+      ww[a] = tq[a] * d->inv_gr[si];
+    }
+    if (noisy) {
+      float gv[3], gw[3];
+      normals3(k0, k1, (uint32_t)i, step, 1u, gv);
+      normals3(k0, k1, (uint32_t)i, step, 3u, gw);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        vv[a] = vv[a] + d->sig_v[si] * gv[a];
+        ww[a] = ww[a] + d->sig_w[si] * gw[a];
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) st.vel[a * M + gi] = vv[a];
+    st.omega_xy[gi] = ww[0];
+    st.omega_xy[M + gi] = ww[1];
+    st.omega[gi] = ww[2];
+  }
+  const float disp = sqrt_rn(dmax2);
+  sc.disp[gi] = disp;
+  if (!(disp < 0.5f * d->skin)) {  // a mover (k_check3's exact test)
+    const int k = atomicAdd(&sc.nmov[e], 1);
+    if (k < kMaxMovers) sc.movers[(size_t)e * kMaxMovers + k] = i;
+  }
+  if (st.reuse) save_forces(st, gi, par ^ 1);  // this run's actions, the final director
 }
 
 }  // namespace swarm

@@ -1,7 +1,12 @@
 """
-3-D at scale: the cluster-window path in three dimensions
-(k_build_sort3 -> k_build_pairs3 -> k_cluster_build -> k_cluster_run3 ->
-k_check3, swarm_integrator3.cuh) against the CPU oracle, bit for bit.
+3-D at scale: the two windowed 3-D paths against the CPU oracle, bit for
+bit (swarm_integrator3.cuh):
+  cluster  k_build_sort3 -> k_build_pairs3 -> k_cluster_build ->
+           k_cluster_run3 -> k_check3 (dilute boxes)
+  nlist    k_build_sort3 -> k_build_nlist3 -> one k_nl_step3 per sub-step ->
+           k_check3 (boxes whose rc + skin graph percolates)
+SWARMRL_AMD_NLIST=0|1 picks the path (by default the engine picks it from
+the density).
 
 The reference engine's default dimension is 3 (EspressoMD(n_dims=3),
 espresso.py:143-152; free rotation about all axes, espresso.py:415-426);
@@ -44,6 +49,12 @@ def _lattice3(rng, n, a=4.6, jitter=0.3):
     return pos, d, k * a
 
 
+@pytest.fixture(params=["cluster", "nlist"])
+def path3(request, monkeypatch):
+    monkeypatch.setenv("SWARMRL_AMD_NLIST", "1" if request.param == "nlist" else "0")
+    return request.param
+
+
 def _stats(h):
     fb = np.zeros(h.E, np.int32)
     w = np.zeros(h.E, np.int32)
@@ -52,7 +63,7 @@ def _stats(h):
 
 
 @pytest.mark.parametrize("E,n_species", [(1, 1), (3, 2)])
-def test_cluster3_4096_bit_exact(E, n_species):
+def test_cluster3_4096_bit_exact(E, n_species, path3):
     """4096 colloids at volume fraction ~0.04: every window passes the check (no re-run), three slices with new
     actions, positions / images / directors / velocities bit-exact."""
     from gpu_harness import Harness, species_list
@@ -76,7 +87,8 @@ def test_cluster3_4096_bit_exact(E, n_species):
         h.set_torque_xy(tq[:2])
         h.integrate(nsteps)
         fb, waves = _stats(h)
-        assert (fb == 0).all() and (waves > 0).all()  # cluster path, check passed
+        assert (fb == 0).all()  # check passed, no re-run
+        assert (waves > 0).all() == (path3 == "cluster")
         got = h.download()
         vel = h.velocities()
         om = h.omegas3()
@@ -90,7 +102,7 @@ def test_cluster3_4096_bit_exact(E, n_species):
 
 
 def test_cluster3_matches_global_path(monkeypatch):
-    """The same engine run on both 3-D paths (SWARMRL_AMD_CLUSTER_PATH=0
+    """The same engine run on the three 3-D paths (SWARMRL_AMD_CLUSTER_PATH=0
     forces the global one) gives the same bits."""
     from gpu_harness import Harness, species_list
 
@@ -102,8 +114,9 @@ def test_cluster3_matches_global_path(monkeypatch):
     f = rng.choice([0.0, 20.0], n).astype(np.float32)
     tq = rng.normal(scale=5.0, size=(3, n)).astype(np.float32)
     out = {}
-    for path in ("1", "0"):
-        monkeypatch.setenv("SWARMRL_AMD_CLUSTER_PATH", path)
+    for path in ("1", "0", "nl"):
+        monkeypatch.setenv("SWARMRL_AMD_CLUSTER_PATH", "0" if path == "0" else "1")
+        monkeypatch.setenv("SWARMRL_AMD_NLIST", "1" if path == "nl" else "0")
         h = Harness(box, 1e-3, 1.0239, 1.0239, 5, species_list()[:1], np.zeros(n, int),
                     n_dims=3)
         h.upload([st])
@@ -111,12 +124,14 @@ def test_cluster3_matches_global_path(monkeypatch):
         h.set_torque_xy(tq[:2])
         h.integrate(150)
         out[path] = (h.download()[0], h.velocities(), h.omegas3(), _stats(h))
-    _eq3(out["1"][0], out["0"][0])
-    assert np.array_equal(out["1"][1], out["0"][1]) and np.array_equal(out["1"][2], out["0"][2])
+    for p in ("1", "nl"):
+        _eq3(out[p][0], out["0"][0])
+        assert np.array_equal(out[p][1], out["0"][1]) and np.array_equal(out[p][2], out["0"][2])
+        assert out[p][3][0][0] == 0  # windowed path, check passed
     assert out["1"][3][1][0] > 0 and out["0"][3][1][0] == 0  # waves: cluster vs global
 
 
-def test_cluster3_reuse_one_substep_window():
+def test_cluster3_reuse_one_substep_window(path3):
     """reuse_forces on the 3-D cluster path, including a window of one
     sub-step (its saved actions are this run's, not the reused ones)."""
     from gpu_harness import Harness, species_list
@@ -142,10 +157,10 @@ def test_cluster3_reuse_one_substep_window():
         _eq3(h.download()[0], st)
         assert np.array_equal(h.velocities(), v) and np.array_equal(h.omegas3(), w)
         fb, waves = _stats(h)
-        assert fb[0] == 0 and waves[0] > 0
+        assert fb[0] == 0 and (waves[0] > 0) == (path3 == "cluster")
 
 
-def test_cluster3_rerun_and_big_cluster_bit_exact():
+def test_cluster3_rerun_and_big_cluster_bit_exact(path3):
     """A dense block of touching colloids (one cluster wider than a wave: the
     build flags the env) and fast swimmers (movers that fail the check) both
     re-run on the 3-D global path from the window-start snapshot."""
@@ -178,7 +193,7 @@ def test_cluster3_rerun_and_big_cluster_bit_exact():
     assert 2 in seen  # re-run on the global path
 
 
-def test_cluster3_walls_bit_exact():
+def test_cluster3_walls_bit_exact(path3):
     """Plane walls (espresso.py:667-711) on the 3-D cluster path."""
     from gpu_harness import Harness, species_list
 
@@ -202,4 +217,4 @@ def test_cluster3_walls_bit_exact():
     _eq3(h.download()[0], ref)
     assert np.array_equal(h.velocities(), v)
     fb, waves = _stats(h)
-    assert waves[0] > 0
+    assert (waves[0] > 0) == (path3 == "cluster")
