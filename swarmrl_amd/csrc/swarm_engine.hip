@@ -1226,10 +1226,13 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
   const bool walls = e->derived.n_walls != 0;
   if (e->params.n_dims == 3 && e->nlist_path) {
     const long M = (long)e->n_envs * e->n;
-    const dim3 grid((unsigned)((M + 255) / 256));
+    // latency-bound windows: one wave per workgroup (spread over more CUs);
+    // a multiple of 8 workgroups (k_nl_step3's XCD-aware order)
+    const int tpb = M <= 32768 ? 64 : 256;
+    const dim3 grid((unsigned)(((M + tpb - 1) / tpb + 7) & ~7L));
     for (int s = 0; s < n_steps; ++s) {
 #define SWARM_NL(MULTI, WALLS)                                                                \
-  hipLaunchKernelGGL((swarm::k_nl_step3<MULTI, WALLS>), grid, dim3(256), 0, e->stream,         \
+  hipLaunchKernelGGL((swarm::k_nl_step3<MULTI, WALLS>), grid, dim3(tpb), 0, e->stream,         \
                      e->d_derived, e->st, e->sc, n_steps, s, e->d_step)
       if (walls) {
         if (multi)

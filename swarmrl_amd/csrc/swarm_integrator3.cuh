@@ -944,7 +944,12 @@ __global__ __launch_bounds__(256) void k_nl_step3(const Derived* __restrict__ d,
   __shared__ PairTables pt;
   if (kMulti) stage_pair_tables(d, &pt);
   const size_t M = (size_t)st.m;
-  const size_t gi = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // XCD-aware order: workgroup b runs on XCD b % 8, so consecutive logical
+  // blocks (one env's colloids, whose positions the neighbour reads share)
+  // go to the same XCD and its L2 (grid: a multiple of 8 blocks)
+  const unsigned per_xcd = gridDim.x >> 3;
+  const unsigned lb = (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3);
+  const size_t gi = (size_t)lb * blockDim.x + threadIdx.x;
   if (gi >= M) return;
   const int N = st.n;
   const int e = (int)(gi / N), i = (int)(gi - (size_t)e * N);
@@ -994,19 +999,25 @@ __global__ __launch_bounds__(256) void k_nl_step3(const Derived* __restrict__ d,
   const float eps24 = d->eps24;
   int64_t acc[3] = {0, 0, 0};
   const int32_t* nlp = sc.nl + gi;
-  for (int k0 = 0; k0 < nn; k0 += 4) {
-    int32_t pk[4];
-    uint32_t qj[4][3];
+#ifdef SWARM_ABL_NL_NOPAIR  // timing ablation only (tools/_variants)
+  for (int k0 = 0; k0 < 0; k0 += 4) {
+#else
+  for (int k0 = 0; k0 < nn; k0 += 8) {
+#endif
+    // eight neighbours per round: their indices, then their positions, in
+    // flight together (two memory latencies per round)
+    int32_t pk[8];
+    uint32_t qj[8][3];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) pk[u] = k0 + u < nn ? nlp[(size_t)(k0 + u) * M] : -1;
+    for (int u = 0; u < 8; ++u) pk[u] = k0 + u < nn ? nlp[(size_t)(k0 + u) * M] : -1;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 8; ++u) {
       const size_t gj = base + (pk[u] < 0 ? i : (pk[u] & 0xffffff));
 #pragma unroll
       for (int a = 0; a < 3; ++a) qj[u][a] = R[a * M + gj];
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 8; ++u) {
       if (pk[u] < 0) continue;
       const float rx = (float)(int32_t)(qj[u][0] - q[0]) * sx[0];
       const float ry = (float)(int32_t)(qj[u][1] - q[1]) * sx[1];
@@ -1025,11 +1036,13 @@ __global__ __launch_bounds__(256) void k_nl_step3(const Derived* __restrict__ d,
   const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
   const bool noisy = d->noisy != 0;
   float f[3], ph[3];
-  float gt[3], gr[3];
+  float gt[3] = {0.0f, 0.0f, 0.0f}, gr[3] = {0.0f, 0.0f, 0.0f};
+#ifndef SWARM_ABL_NL_NONOISE  // timing ablation only (tools/_variants)
   if (noisy) {
     step_normals(k0, k1, (uint32_t)i, step, gt);
     normals3(k0, k1, (uint32_t)i, step, 2u, gr);
   }
+#endif
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     f[a] = i64_to_f32(acc[a]) * 5.9604644775390625e-08f;
@@ -1043,7 +1056,9 @@ __global__ __launch_bounds__(256) void k_nl_step3(const Derived* __restrict__ d,
     }
     advance(q[a], im[a], f2i32(dq * d->inv_sx[a]));
   }
+#ifndef SWARM_ABL_NL_NOROT  // timing ablation only (tools/_variants)
   rotate_director(v, ph[0], ph[1], ph[2]);
+#endif
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     W[a * M + gi] = q[a];
