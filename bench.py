@@ -17,6 +17,7 @@ import argparse
 import json
 import math
 import os
+import re
 import sys
 import time
 
@@ -169,7 +170,7 @@ def measure_dims3(args, E, reps, global_reps=0):
     (EspressoMD(n_dims=3), espresso.py:143-152).  E envs of --colloids
     colloids at volume fraction 0.04 (placed in the centred sphere, overlaps
     removed), random swim forces and lab-frame torques, timed over `reps`
-    slices of 100 BD+WCA sub-steps (engine only: the reference's vision
+    HIP-graph replays of a slice of 100 BD+WCA sub-steps (engine only: the reference's vision
     cones are 2-D).  At this density the rc + skin graph percolates, so the
     engine takes the neighbour-list window (one chip-wide launch per
     sub-step); also timed: the cluster window forced (its clusters exceed a
@@ -211,14 +212,25 @@ def measure_dims3(args, E, reps, global_reps=0):
         return eng
 
     def time_slices(eng, n):
+        # one slice captured in a HIP graph (as the rollout captures its
+        # episodes), replayed n times
         for _ in range(3):
             eng._run(100)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            eng._run(100)
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            eng._run(100)
+        graph.replay()
         torch.cuda.synchronize()
         t0 = torch.cuda.Event(enable_timing=True)
         t1 = torch.cuda.Event(enable_timing=True)
         t0.record()
         for _ in range(n):
-            eng._run(100)
+            graph.replay()
         t1.record()
         t1.synchronize()
         return t0.elapsed_time(t1) / n
@@ -273,7 +285,7 @@ def time_run_kernel(eng, reps):
     return ms.value / cnt.value, name
 
 
-def pmc_traffic(kernel_prefix, E, N):
+def pmc_traffic(kernel_re, E, N):
     """Per-launch HBM bytes and VALU wave-instructions of the dominant kernel
     from the newest committed rocprofv3 PMC summary (profiles/<tag>_traffic.json:
     separate FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU passes, FETCH_SIZE x2 per
@@ -288,7 +300,7 @@ def pmc_traffic(kernel_prefix, E, N):
         except (OSError, ValueError):
             continue
         for r in rows:
-            if kernel_prefix in r.get("kernel", "") and r.get("envs") == E and \
+            if re.search(kernel_re, r.get("kernel", "")) and r.get("envs") == E and \
                     r.get("colloids") == N:
                 return (float(r["bytes_per_launch"]), r.get("valu_insts_per_launch"),
                         f"profiles/{r['source']}")
@@ -527,7 +539,8 @@ def measure(args, E, rank, world, device, builder=None, colloids=None):
     sub = eng.params.steps_per_slice
     bytes_per_launch = BYTES_PER_PARTICLE_SUBSTEP * N * sub * E
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-    traffic, valu, traffic_src = pmc_traffic("k_cluster_run", E, N)
+    # the 2-D run kernels (not k_cluster_run3 of the dims3 line)
+    traffic, valu, traffic_src = pmc_traffic(r"k_cluster_run(_wide)?<", E, N)
     out = dict(timing)
     out.update({
         "hip_graph": episode_graph is not None,
