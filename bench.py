@@ -165,7 +165,7 @@ def build_c5_workload(args, env_seed, device):
     return eng, ff, agent
 
 
-def measure_dims3(args, E, reps, global_reps=0):
+def measure_dims3(args, E, reps, global_reps=0, dims=3, fraction=0.04):
     """3-D at scale: n_dims=3 is the reference engine's default
     (EspressoMD(n_dims=3), espresso.py:143-152).  E envs of --colloids
     colloids at volume fraction 0.04 (placed in the centred sphere, overlaps
@@ -182,7 +182,10 @@ def measure_dims3(args, E, reps, global_reps=0):
     from swarmrl_amd.units import UnitRegistry
 
     N = args.colloids
-    L = (N * (4.0 / 3.0) * math.pi / 0.04) ** (1.0 / 3.0)
+    if dims == 3:
+        L = (N * (4.0 / 3.0) * math.pi / fraction) ** (1.0 / 3.0)
+    else:  # dense 2-D (dims=2): area fraction in the box, placed in the centred disc
+        L = math.sqrt(N * math.pi / fraction)
     ureg = UnitRegistry()
     params = MDParams(ureg=ureg, box_length=ureg.Quantity([L, L, L], "micrometer"),
                       time_step=ureg.Quantity(1e-3, "second"),
@@ -196,10 +199,11 @@ def measure_dims3(args, E, reps, global_reps=0):
         os.environ["SWARMRL_AMD_CLUSTER_PATH"] = "0" if mode == "global" else "1"
         os.environ["SWARMRL_AMD_NLIST"] = "1" if mode == "nlist" else "0"
         try:
-            eng = SwarmEngine(params, n_dims=3, seed=11, n_envs=E,
+            eng = SwarmEngine(params, n_dims=dims, seed=11, n_envs=E,
                               out_folder=f"/tmp/swarm_bench_3d_{os.getpid()}")
             eng.add_colloids(N, ureg.Quantity(1.0, "micrometer"),
-                             ureg.Quantity(np.array([L / 2, L / 2, L / 2]), "micrometer"),
+                             ureg.Quantity(np.array([L / 2, L / 2, L / 2 if dims == 3 else 0.0]),
+                                           "micrometer"),
                              ureg.Quantity(L / 2, "micrometer"))
             eng.integrate(1)  # set-up, overlap removal, one slice
         finally:
@@ -208,7 +212,8 @@ def measure_dims3(args, E, reps, global_reps=0):
         nat = eng._native
         nat.bind_stream()
         nat.call("swarm_engine_set_actions", f.ctypes.data, tq[2].copy().ctypes.data, 0)
-        nat.call("swarm_engine_set_torque_xy", np.ascontiguousarray(tq[:2]).ctypes.data, 0)
+        if dims == 3:
+            nat.call("swarm_engine_set_torque_xy", np.ascontiguousarray(tq[:2]).ctypes.data, 0)
         return eng
 
     def time_slices(eng, n):
@@ -725,6 +730,14 @@ def main():
                 f"E{args.batched_envs}": measure_dims3(args, max(args.batched_envs, 1), 20,
                                                        global_reps=2),
             }
+            head["dense2d"] = {
+                "workload": f"dense 2-D: {args.colloids} colloids per env at area fraction 0.3 "
+                            f"(placed in the centred disc), BD+WCA slices of 100 sub-steps "
+                            f"(engine only); the rc + skin graph percolates",
+                "E1": measure_dims3(args, 1, 50, global_reps=3, dims=2, fraction=0.3),
+                f"E{args.batched_envs}": measure_dims3(args, max(args.batched_envs, 1), 20,
+                                                       global_reps=2, dims=2, fraction=0.3),
+            }
     if world > 1 and dist.get_world_size() != args.gpus:
         print("bench.py: process group size differs from --gpus", file=sys.stderr)
         sys.exit(2)
@@ -761,7 +774,7 @@ def main():
     }
     if "gather" in head:
         line["gather"] = head["gather"]
-    for k in ("c5", "dims3"):
+    for k in ("c5", "dims3", "dense2d"):
         if k in head:
             line[k] = head[k]
     if batched is not None:

@@ -1191,6 +1191,12 @@ int launch_build(swarm_engine* e, hipStream_t stream) {
     hipLaunchKernelGGL(swarm::k_build_sort<4>, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4,
                        stream, e->st, e->sc, e->lxb, e->lyb);
   HIP_TRY(hipGetLastError());
+  if (e->params.n_dims != 3 && e->nlist_path) {  // Verlet lists, no clusters
+    hipLaunchKernelGGL(swarm::k_build_nlist2, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
+                       dim3(256), 0, stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb);
+    HIP_TRY(hipGetLastError());
+    return SWARM_OK;
+  }
   if (e->params.n_dims != 3)
     hipLaunchKernelGGL(swarm::k_build_pairs, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
                        dim3(256), 0, stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb);
@@ -1224,6 +1230,34 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
   const long waves = (long)e->n_envs * e->sc.wmax;
   const bool multi = e->params.n_species > 1;
   const bool walls = e->derived.n_walls != 0;
+  if (e->params.n_dims == 2 && e->nlist_path) {
+    const long M = (long)e->n_envs * e->n;
+    const int tpb = M <= 32768 ? 64 : 256;
+    const dim3 grid((unsigned)(((M + tpb - 1) / tpb + 7) & ~7L));
+    for (int s = 0; s < n_steps; ++s) {
+#define SWARM_NL2(MULTI, WALLS)                                                               \
+  hipLaunchKernelGGL((swarm::k_nl_step2<MULTI, WALLS>), grid, dim3(tpb), 0, e->stream,         \
+                     e->d_derived, e->st, e->sc, n_steps, s, e->d_step)
+      if (walls) {
+        if (multi)
+          SWARM_NL2(true, true);
+        else
+          SWARM_NL2(false, true);
+      } else {
+        if (multi)
+          SWARM_NL2(true, false);
+        else
+          SWARM_NL2(false, false);
+      }
+#undef SWARM_NL2
+      HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(swarm::k_check, dim3(e->n_envs), dim3(1024),
+                       check_lds_bytes(e->lxg, e->lyg, e->n, e->params.n_dims), e->stream,
+                       e->d_derived, e->st, e->sc, n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg, 1);
+    HIP_TRY(hipGetLastError());
+    return SWARM_OK;
+  }
   if (e->params.n_dims == 3 && e->nlist_path) {
     const long M = (long)e->n_envs * e->n;
     // latency-bound windows: one wave per workgroup (spread over more CUs);
@@ -1343,7 +1377,7 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
   }
   hipLaunchKernelGGL(swarm::k_check, dim3(e->n_envs), dim3(1024),
                      check_lds_bytes(e->lxg, e->lyg, e->n, e->params.n_dims), e->stream, e->d_derived, e->st, e->sc,
-                     n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg);
+                     n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg, 0);
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
 }
@@ -1509,17 +1543,21 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     const char* oc = std::getenv("SWARMRL_AMD_CLUSTER_PATH");
     if (oc && oc[0] == '0') e->cluster_path = false;
   }
-  if (three_d && e->cluster_path) {
-    // mean number of colloids within 2 r_max + skin of one: above ~2 the
-    // links percolate into clusters wider than a wave (which re-run on the
-    // global path), so the window runs on the neighbour-list path instead.
-    // SWARMRL_AMD_NLIST=0|1 overrides.
+  if (e->cluster_path) {
+    // mean number of colloids within 2 r_max + skin of one (deg): above ~2
+    // in 3-D, ~3 in 2-D the links percolate into clusters wider than a wave
+    // (3-D: re-run on the global path; 2-D: k_check's one-workgroup big
+    // cluster run, then the global path), so the window runs on the
+    // neighbour-list path instead.  SWARMRL_AMD_NLIST=0|1 overrides.
     double rmax = 0.0;
     for (int s = 0; s < params->n_species; ++s) rmax = std::max(rmax, params->radius[s]);
     const double link = 2.0 * rmax + skin_um();
-    const double vol = params->box[0] * params->box[1] * params->box[2];
-    const double deg = (double)n_particles / vol * (2.0 / 3.0) * kTwoPi * link * link * link;
-    e->nlist_path = deg > 2.0;
+    const double deg =
+        three_d ? (double)n_particles / (params->box[0] * params->box[1] * params->box[2]) *
+                      (2.0 / 3.0) * kTwoPi * link * link * link
+                : (double)n_particles / (params->box[0] * params->box[1]) * 0.5 * kTwoPi * link *
+                      link;
+    e->nlist_path = deg > (three_d ? 2.0 : 3.0);
     const char* on = std::getenv("SWARMRL_AMD_NLIST");
     if (on && on[0] == '0') e->nlist_path = false;
     if (on && on[0] == '1') e->nlist_path = true;
@@ -1594,7 +1632,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->sc.bsq, (three_d ? 3 : 2) * M);
   rc = rc ? rc : dev_alloc(e, &e->sc.nl, e->nlist_path ? (size_t)swarm::kNlMax * M : 1);
   rc = rc ? rc : dev_alloc(e, &e->sc.nn, e->nlist_path ? M : 1);
-  rc = rc ? rc : dev_alloc(e, &e->sc.qalt, e->nlist_path ? 3 * M : 1);
+  rc = rc ? rc : dev_alloc(e, &e->sc.qalt, e->nlist_path ? (three_d ? 3 : 2) * M : 1);
   rc = rc ? rc : dev_alloc(e, &e->sc.bsid, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.bcstart, (size_t)n_envs * ((1 << lcb) + 1));
   rc = rc ? rc : dev_alloc(e, &e->sc.gplist, (size_t)n_envs * std::max(e->sc.pair_cap, 1));
@@ -1619,7 +1657,8 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     bool want = latency_bound;
     if (ov && ov[0] == '0') want = false;
     if (ov && ov[0] == '1') want = true;
-    e->noise_table = want && e->derived.noisy && e->cluster_path && !three_d;  // 3-D: drawn in the run
+    // 3-D and neighbour-list windows draw their normals in the kernels
+    e->noise_table = want && e->derived.noisy && e->cluster_path && !three_d && !e->nlist_path;
     if (e->noise_table)
       rc = rc ? rc : dev_alloc(e, &e->d_noise, 2 * swarm::noise_table_words(M));
     // the one-launch build (one CU per env) for throughput-bound engines
@@ -1630,11 +1669,12 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
       const int wm = S / 64;
       const size_t below = 16 + 16 + 3 * 68 + (size_t)((wm + 3) & ~3) + 4 * (size_t)n_particles;
       e->env_build = e->cluster_path && !e->big_build && !latency_bound && !three_d &&
+                     !e->nlist_path &&
                      swarm::build_env_sort_words(n_particles, 1 << (e->lxb + e->lyb)) <= below;
       const char* ob = std::getenv("SWARMRL_AMD_ENV_BUILD");
       if (ob && ob[0] == '0') e->env_build = false;
       if (ob && ob[0] == '1')
-        e->env_build = e->cluster_path && !e->big_build && !three_d &&
+        e->env_build = e->cluster_path && !e->big_build && !three_d && !e->nlist_path &&
                        swarm::build_env_sort_words(n_particles, 1 << (e->lxb + e->lyb)) <= below;
     }
     // one block per CU for latency-bound runs; beside a run of up to 8192

@@ -197,10 +197,10 @@ struct Scratch {
   // kernel and the big-cluster run, consumed and reset by k_check)
   int32_t* nmov;      // [E]
   int32_t* movers;    // [E][kMaxMovers]
-  // neighbour-list path (dense 3-D boxes, swarm_integrator3.cuh)
+  // neighbour-list path (boxes whose rc + skin graph percolates)
   int32_t* nl;        // [kNlMax][M] neighbours j | species << 24 of particle gi
   int32_t* nn;        // [M] neighbour count
-  uint32_t* qalt;     // [3][M] second position buffer (sub-steps alternate)
+  uint32_t* qalt;     // [dims][M] second position buffer (sub-steps alternate)
   // cluster build (k_build_sort -> k_build_pairs -> k_cluster_build)
   uint32_t* bsq;      // [dims][M] cell-sorted positions (x, y[, z])
   int32_t* bsid;      // [M] particle | species << 24 of a sorted entry
@@ -986,7 +986,10 @@ __global__ __launch_bounds__(1024) void k_build_sort(DevState st, Scratch sc, in
     cid[k] = ok ? (i | ((int32_t)st.species[i] << 24)) : -1;
   }
   for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
-  if (tid == 0) sc.gnpairs[e] = 0;
+  if (tid == 0) {
+    sc.gnpairs[e] = 0;
+    sc.fallback[e] = 0;  // the neighbour-list build sets it on overflow
+  }
   __syncthreads();
   SWARM_STAMP(1);
 #pragma unroll
@@ -2381,11 +2384,204 @@ __device__ void run_big_clusters(const Derived* __restrict__ d, const DevState& 
   __syncthreads();
 }
 
+// ------------------------------------------- neighbour-list window (2-D)
+// Dense boxes: the rc + skin graph percolates, so clusters exceed a wave
+// (and k_check's big-cluster workgroup).  The window keeps the build grid,
+// the exact check and the exact re-run, but its sub-steps run chip-wide: a
+// Verlet list per colloid (every j within r_i + r_j + skin), then one launch
+// per sub-step with one thread per colloid, positions read from one buffer
+// and written to the other (st.q, sc.qalt alternate; k_check copies back
+// after an odd window).  Forces, noise and update are block_global_run's
+// (pair_force, bd_step with the step's normals drawn fresh), so the bits are
+// the same.  The 3-D twin is k_build_nlist3 / k_nl_step3.
+constexpr int kNlMax = 48;  // neighbours per colloid (more: the env re-runs)
+
+// Build step 2 (neighbour-list path), grid (ceil(N / 256), E), one thread
+// per cell-sorted entry of k_build_sort: its neighbours into nl[k][gi]
+// (neighbour-major, so the sub-step's reads coalesce).
+__global__ __launch_bounds__(256) void k_build_nlist2(const Derived* __restrict__ d, DevState st,
+                                                      Scratch sc, int lx, int ly) {
+  __shared__ float nb2[kMaxSpecies * kMaxSpecies];
+  for (int k = threadIdx.x; k < kMaxSpecies * kMaxSpecies; k += blockDim.x) nb2[k] = d->nb2[k];
+  __syncthreads();
+  const int e = blockIdx.y, N = st.n;
+  const int ps = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ps >= N) return;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int ncell = 1 << (lx + ly);
+  const int32_t* cs = sc.bcstart + (size_t)e * (ncell + 1);
+  const int ncx = 1 << lx, ncy = 1 << ly;
+  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const int pk = sc.bsid[base + ps];
+  const int i = pk & 0xffffff;
+  const uint32_t qx = sc.bsq[base + ps], qy = sc.bsq[M + base + ps];
+  const int c0 = cell_index(qx, qy, lx, ly);
+  const int cx = c0 & (ncx - 1), cy = c0 >> lx;
+  const int xa = ncx >= 3 ? max(cx - 1, 0) : 0;
+  const int xb = ncx >= 3 ? min(cx + 1, ncx - 1) : ncx - 1;
+  const int xw = ncx >= 3 ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
+  int rb[6], re[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const int oy = loy + (r >> 1), part = r & 1;
+    const bool use = oy <= hiy && (part == 0 || xw >= 0);
+    const int row = ((cy + oy + ncy) & (ncy - 1)) << lx;
+    const int c_lo = row | (part == 0 ? xa : xw), c_hi = row | (part == 0 ? xb : xw);
+    rb[r] = use ? cs[c_lo] : 0;
+    re[r] = use ? cs[c_hi + 1] : 0;
+  }
+  const float* nb2_row = nb2 + (pk >> 24) * kMaxSpecies;
+  int cnt = 0;
+  int32_t* out = sc.nl + base + i;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    for (int jj0 = rb[r]; jj0 < re[r]; jj0 += 4) {
+      int pk4[4];
+      uint32_t x4[4], y4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int jj = jj0 + u;
+        const bool ok = jj < re[r];
+        pk4[u] = ok ? sc.bsid[base + jj] : -1;
+        x4[u] = ok ? sc.bsq[base + jj] : 0u;
+        y4[u] = ok ? sc.bsq[M + base + jj] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (pk4[u] < 0 || (pk4[u] & 0xffffff) == i) continue;
+        const float rx = (float)(int32_t)(x4[u] - qx) * sx0;
+        const float ry = (float)(int32_t)(y4[u] - qy) * sx1;
+        if (rx * rx + ry * ry < nb2_row[pk4[u] >> 24]) {
+          if (cnt < kNlMax) out[(size_t)cnt * M] = pk4[u];
+          ++cnt;
+        }
+      }
+    }
+  }
+  sc.nn[base + i] = min(cnt, kNlMax);
+  if (cnt > kNlMax) sc.fallback[e] = 1;  // -> the env re-runs on the global path
+}
+
+// Sub-step s of the 2-D neighbour-list window, one thread per colloid of
+// every env (XCD-aware workgroup order: one env's colloids share an L2).
+// sc.disp holds the squared maximum displacement until the last sub-step.
+template <bool kMulti, bool kWalls>
+__global__ __launch_bounds__(256) void k_nl_step2(const Derived* __restrict__ d, DevState st,
+                                                  Scratch sc, int n_steps, int s,
+                                                  const uint64_t* __restrict__ ctl) {
+  __shared__ PairTables pt;
+  if (kMulti) stage_pair_tables(d, &pt);
+  const size_t M = (size_t)st.m;
+  const unsigned per_xcd = gridDim.x >> 3;  // grid: a multiple of 8 workgroups
+  const unsigned lb = (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3);
+  const size_t gi = (size_t)lb * blockDim.x + threadIdx.x;
+  if (gi >= M) return;
+  const int N = st.n;
+  const int e = (int)(gi / N), i = (int)(gi - (size_t)e * N);
+  if (sc.fallback[e] != 0) return;
+  const size_t base = (size_t)e * N;
+  const bool first = s == 0, last = s == n_steps - 1;
+  const uint32_t* R = (s & 1) ? sc.qalt : st.q;
+  uint32_t* W = (s & 1) ? st.q : sc.qalt;
+  const int par = window_parity(ctl);
+  const uint64_t step = ctl[kCtlStep] + (uint64_t)s;
+  const int si = kMulti ? st.species[i] : 0;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const int nn = sc.nn[gi];
+  PState p;
+  p.qx = R[gi];
+  p.qy = R[M + gi];
+  p.ix = st.img[gi];
+  p.iy = st.img[M + gi];
+  p.an = st.ang[gi];
+  uint32_t q0x, q0y;
+  float dmax2 = 0.0f;
+  if (first) {
+    q0x = p.qx;
+    q0y = p.qy;
+    sc.bq[gi] = p.qx;
+    sc.bq[M + gi] = p.qy;
+    sc.bimg[gi] = p.ix;
+    sc.bimg[M + gi] = p.iy;
+    sc.bang[gi] = p.an;
+  } else {
+    q0x = sc.bq[gi];
+    q0y = sc.bq[M + gi];
+    dmax2 = sc.disp[gi];
+  }
+  const float eps24 = d->eps24;
+  int64_t ax = 0, ay = 0;
+  const int32_t* nlp = sc.nl + gi;
+  for (int k0 = 0; k0 < nn; k0 += 8) {
+    // eight neighbours per round: indices, then positions, in flight together
+    int32_t pk[8];
+    uint32_t xj[8], yj[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) pk[u] = k0 + u < nn ? nlp[(size_t)(k0 + u) * M] : -1;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const size_t gj = base + (pk[u] < 0 ? i : (pk[u] & 0xffffff));
+      xj[u] = R[gj];
+      yj[u] = R[M + gj];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (pk[u] < 0) continue;
+      const float rx = (float)(int32_t)(xj[u] - p.qx) * sx0;
+      const float ry = (float)(int32_t)(yj[u] - p.qy) * sx1;
+      if (kMulti) {
+        const int sp = si * kMaxSpecies + (pk[u] >> 24);
+        pair_force(pt.cut2[sp], pt.sig6[sp], eps24, rx, ry, ax, ay);
+      } else {
+        pair_force(d->cut2[0], d->sig6[0], eps24, rx, ry, ax, ay);
+      }
+    }
+  }
+  if (kWalls) {
+    int64_t az = 0;
+    wall_forces<2>(d, si, (float)p.qx * sx0, (float)p.qy * sx1, 0.0f, ax, ay, az, st.wall_viol);
+  }
+  const bool reuse0 = st.reuse && first;  // sub-step 0 reuses the previous run's actions
+  const PrevSlot prv = prev_slot(st, par);
+  const float fs = reuse0 ? prv.f[gi] : st.f_swim[gi];
+  const float tz = reuse0 ? prv.tz[gi] : st.torque_z[gi];
+  const uint32_t an_swim = reuse0 ? prv.ang[gi] : p.an;
+  const PConst pc = load_pconst(d, si);
+  float vx = 0.0f, vy = 0.0f, om = 0.0f;
+  bd_step(pc, p, ax, ay, fs, tz, st.f_ext[gi], st.f_ext[M + gi], d->key0, d->key1 ^ (uint32_t)e,
+          (uint32_t)i, step, last, &vx, &vy, &om, an_swim);
+  W[gi] = p.qx;
+  W[M + gi] = p.qy;
+  st.img[gi] = p.ix;
+  st.img[M + gi] = p.iy;
+  st.ang[gi] = p.an;
+  const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
+  const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
+  dmax2 = fmaxf(dmax2, ddx * ddx + ddy * ddy);
+  if (!last) {
+    sc.disp[gi] = dmax2;
+    return;
+  }
+  st.vel[gi] = vx;
+  st.vel[M + gi] = vy;
+  st.vel[2 * M + gi] = 0.0f;
+  st.omega[gi] = om;
+  const float disp = sqrt_rn(dmax2);
+  sc.disp[gi] = disp;
+  if (!(disp < 0.5f * d->skin)) {  // a mover (k_check's exact test)
+    const int k = atomicAdd(&sc.nmov[e], 1);
+    if (k < kMaxMovers) sc.movers[(size_t)e * kMaxMovers + k] = i;
+  }
+  if (st.reuse) save_forces(st, gi, par ^ 1);  // this run's actions, the final angle
+}
+
 // ---------------------------------------------------------------- check
 __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, DevState st,
                                                 Scratch sc, int n_steps,
                                                 uint64_t* __restrict__ step_ctr,
-                                                uint32_t* __restrict__ arrive, int lx, int ly) {
+                                                uint32_t* __restrict__ arrive, int lx, int ly,
+                                                int nlist) {
   extern __shared__ __align__(16) unsigned char smem[];
   int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);  // 16
   int32_t* misc = wave_sums + 16;                          // 16
@@ -2400,7 +2596,15 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
   if (tid < 16) misc[tid] = 0;
   __syncthreads();
   const bool flagged_build = sc.fallback[e] != 0;
-  if (!flagged_build && sc.big_n[e] > 0)
+  if (!flagged_build && nlist && (n_steps & 1)) {
+    // neighbour-list window, odd length: the last sub-step wrote the second
+    // position buffer (the exact test below reads only the snapshot)
+    for (int k = tid; k < 2 * N; k += T) {
+      const size_t o = (size_t)(k / N) * M + base + (k % N);
+      st.q[o] = sc.qalt[o];
+    }
+  }
+  if (!flagged_build && !nlist && sc.big_n[e] > 0)
     run_big_clusters(d, st, sc, e, n_steps, step0, cnt, &pt, par);
   if (!flagged_build) {
     // the movers (displacement >= skin / 2) were listed by the run kernel
@@ -2422,7 +2626,8 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
       // force being computed.  Same-cluster pairs count too: a cluster links
       // particles through chains, so two of its members need not be listed
       // neighbours of each other.
-      const float rc = d->rc_max_f;
+      const bool multi = d->n_species > 1;  // else every pair's cutoff is cut2[0]
+      const float rc0 = sqrtf(pt.cut2[0]);
       const float sx0 = d->sx[0], sx1 = d->sx[1];
       const long total = (long)nm * N;
       for (long t = tid; t < total; t += T) {
@@ -2431,11 +2636,18 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
         if (j == m) continue;
         const float rx = (float)(int32_t)(sc.bq[base + j] - sc.bq[base + m]) * sx0;
         const float ry = (float)(int32_t)(sc.bq[M + base + j] - sc.bq[M + base + m]) * sx1;
+        // the pair's own WCA cutoff r_m + r_j (not the largest one: a dense
+        // mixture would fail the test for pairs that cannot interact)
+        const float rc = multi ? sqrtf(pt.cut2[st.species[m] * kMaxSpecies + st.species[j]]) : rc0;
         const float lim = rc + sc.disp[base + m] + sc.disp[base + j] + 1e-3f;
         if (rx * rx + ry * ry < lim * lim) {
           bool listed = false;
           const int sm = sc.slot_of[base + m], sj = sc.slot_of[base + j];
-          if (sc.root[base + j] == sc.root[base + m] && sm < 0) {  // same big cluster
+          if (nlist) {  // j among m's listed neighbours
+            const int nn = sc.nn[base + m];
+            for (int k = 0; k < nn; ++k)
+              listed |= (sc.nl[(size_t)k * M + base + m] & 0xffffff) == j;
+          } else if (sc.root[base + j] == sc.root[base + m] && sm < 0) {  // same big cluster
             const uint32_t bm = (uint32_t)(-1 - sm), bj = (uint32_t)(-1 - sj);
             const uint32_t* bp = sc.big_pairs + (size_t)e * kBigPairs;
             const int np = sc.big_np[e];

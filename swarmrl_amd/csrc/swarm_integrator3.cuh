@@ -788,7 +788,8 @@ __global__ __launch_bounds__(1024) void k_check3(const Derived* __restrict__ d, 
     if (nm > kMaxMovers) {
       if (tid == 0) misc[1] = 1;
     } else if (nm > 0) {
-      const float rc = d->rc_max_f;
+      const bool multi = d->n_species > 1;  // else every pair's cutoff is cut2[0]
+      const float rc0 = sqrtf(pt.cut2[0]);
       const float sx0 = d->sx[0], sx1 = d->sx[1], sx2 = d->sx[2];
       const long total = (long)nm * N;
       for (long t = tid; t < total; t += T) {
@@ -798,6 +799,9 @@ __global__ __launch_bounds__(1024) void k_check3(const Derived* __restrict__ d, 
         const float rx = (float)(int32_t)(sc.bq[base + j] - sc.bq[base + m]) * sx0;
         const float ry = (float)(int32_t)(sc.bq[M + base + j] - sc.bq[M + base + m]) * sx1;
         const float rz = (float)(int32_t)(sc.bq[2 * M + base + j] - sc.bq[2 * M + base + m]) * sx2;
+        // the pair's own WCA cutoff r_m + r_j (not the largest one: a dense
+        // mixture would fail the test for pairs that cannot interact)
+        const float rc = multi ? sqrtf(pt.cut2[st.species[m] * kMaxSpecies + st.species[j]]) : rc0;
         const float lim = rc + sc.disp[base + m] + sc.disp[base + j] + 1e-3f;
         float r2 = rx * rx + ry * ry;
         r2 = r2 + rz * rz;
@@ -855,7 +859,6 @@ __global__ __launch_bounds__(1024) void k_check3(const Derived* __restrict__ d, 
 // positions of sub-step s from one buffer and writing the other (st.q and
 // sc.qalt alternate; k_check3 copies back after an odd window).  Forces,
 // noise and update are block_global_run3's, so the bits are the same.
-constexpr int kNlMax = 48;  // neighbours per colloid (more: the env re-runs)
 
 // Build step 2 (neighbour-list path), grid (ceil(N / 256), E), one thread
 // per sorted entry: its neighbours into nl[k][gi] (neighbour-major, so the
