@@ -1026,6 +1026,9 @@ struct swarm_engine {
   // 3-D boxes whose rc + skin graph percolates: chip-wide sub-steps over a
   // per-window Verlet list instead of per-wave clusters (swarm_integrator3.cuh)
   bool nlist_path = false;
+  // neighbour-list window as one persistent launch (<= 256 one-wave
+  // workgroups, grid barriers between sub-steps); opt-in
+  bool nl_persist = false;
   bool big_build = false;  // k_cluster_build<true>: cluster arrays in global memory
   VisionSorted vs{};
   // latency-bound windows read their normals from a table (k_noise)
@@ -1230,6 +1233,45 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
   const long waves = (long)e->n_envs * e->sc.wmax;
   const bool multi = e->params.n_species > 1;
   const bool walls = e->derived.n_walls != 0;
+  if (e->nlist_path && e->nl_persist) {
+    const long M = (long)e->n_envs * e->n;
+    const dim3 grid((unsigned)((M + 63) / 64));  // <= 256: every workgroup resident
+#define SWARM_NLR(KER, MULTI, WALLS)                                                          \
+  hipLaunchKernelGGL((swarm::KER<MULTI, WALLS>), grid, dim3(64), 0, e->stream, e->d_derived,    \
+                     e->st, e->sc, n_steps, e->d_step)
+#define SWARM_NLR_ALL(KER)          \
+  do {                              \
+    if (walls) {                    \
+      if (multi)                    \
+        SWARM_NLR(KER, true, true); \
+      else                          \
+        SWARM_NLR(KER, false, true); \
+    } else {                        \
+      if (multi)                    \
+        SWARM_NLR(KER, true, false); \
+      else                          \
+        SWARM_NLR(KER, false, false); \
+    }                               \
+  } while (0)
+    if (e->params.n_dims == 3)
+      SWARM_NLR_ALL(k_nl_run3);
+    else
+      SWARM_NLR_ALL(k_nl_run2);
+#undef SWARM_NLR_ALL
+#undef SWARM_NLR
+    HIP_TRY(hipGetLastError());
+    if (e->params.n_dims == 3)
+      hipLaunchKernelGGL(swarm::k_check3, dim3(e->n_envs), dim3(1024), check3_lds_bytes(e),
+                         e->stream, e->d_derived, e->st, e->sc, n_steps, e->d_step, e->d_arrive,
+                         e->lxg, e->lyg, e->lzg, 1);
+    else
+      hipLaunchKernelGGL(swarm::k_check, dim3(e->n_envs), dim3(1024),
+                         check_lds_bytes(e->lxg, e->lyg, e->n, e->params.n_dims), e->stream,
+                         e->d_derived, e->st, e->sc, n_steps, e->d_step, e->d_arrive, e->lxg,
+                         e->lyg, 1);
+    HIP_TRY(hipGetLastError());
+    return SWARM_OK;
+  }
   if (e->params.n_dims == 2 && e->nlist_path) {
     const long M = (long)e->n_envs * e->n;
     const int tpb = M <= 32768 ? 64 : 256;
@@ -1561,6 +1603,12 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     const char* on = std::getenv("SWARMRL_AMD_NLIST");
     if (on && on[0] == '0') e->nlist_path = false;
     if (on && on[0] == '1') e->nlist_path = true;
+    // persistent window: opt-in (SWARMRL_AMD_NL_PERSIST=1, at most 256
+    // one-wave workgroups); measured slower than a launch per sub-step
+    // (its agent-scope fences cost more than the launch boundary: DESIGN.md)
+    const long Mp = (long)n_envs * n_particles;
+    const char* op = std::getenv("SWARMRL_AMD_NL_PERSIST");
+    e->nl_persist = e->nlist_path && (Mp + 63) / 64 <= 256 && op && op[0] == '1';
   }
   const size_t M = (size_t)n_envs * n_particles;
   int rc = SWARM_OK;
@@ -1633,6 +1681,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->sc.nl, e->nlist_path ? (size_t)swarm::kNlMax * M : 1);
   rc = rc ? rc : dev_alloc(e, &e->sc.nn, e->nlist_path ? M : 1);
   rc = rc ? rc : dev_alloc(e, &e->sc.qalt, e->nlist_path ? (three_d ? 3 : 2) * M : 1);
+  rc = rc ? rc : dev_alloc(e, &e->sc.nl_bar, 1);
   rc = rc ? rc : dev_alloc(e, &e->sc.bsid, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.bcstart, (size_t)n_envs * ((1 << lcb) + 1));
   rc = rc ? rc : dev_alloc(e, &e->sc.gplist, (size_t)n_envs * std::max(e->sc.pair_cap, 1));
