@@ -1263,12 +1263,12 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
     if (e->params.n_dims == 3)
       hipLaunchKernelGGL(swarm::k_check3, dim3(e->n_envs), dim3(1024), check3_lds_bytes(e),
                          e->stream, e->d_derived, e->st, e->sc, n_steps, e->d_step, e->d_arrive,
-                         e->lxg, e->lyg, e->lzg, 1);
+                         e->lxg, e->lyg, e->lzg, 2);
     else
       hipLaunchKernelGGL(swarm::k_check, dim3(e->n_envs), dim3(1024),
                          check_lds_bytes(e->lxg, e->lyg, e->n, e->params.n_dims), e->stream,
                          e->d_derived, e->st, e->sc, n_steps, e->d_step, e->d_arrive, e->lxg,
-                         e->lyg, 1);
+                         e->lyg, 2);
     HIP_TRY(hipGetLastError());
     return SWARM_OK;
   }
@@ -1682,6 +1682,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->sc.nn, e->nlist_path ? M : 1);
   rc = rc ? rc : dev_alloc(e, &e->sc.qalt, e->nlist_path ? (three_d ? 3 : 2) * M : 1);
   rc = rc ? rc : dev_alloc(e, &e->sc.nl_bar, 1);
+  rc = rc ? rc : dev_alloc(e, &e->sc.qa, e->nlist_path ? 2 * M : 1);
   rc = rc ? rc : dev_alloc(e, &e->sc.bsid, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.bcstart, (size_t)n_envs * ((1 << lcb) + 1));
   rc = rc ? rc : dev_alloc(e, &e->sc.gplist, (size_t)n_envs * std::max(e->sc.pair_cap, 1));

@@ -202,6 +202,8 @@ struct Scratch {
   int32_t* nn;        // [M] neighbour count
   uint32_t* qalt;     // [dims][M] second position buffer (sub-steps alternate)
   uint32_t* nl_bar;   // [1] grid-barrier counter of the persistent window (reset by the build)
+  uint4* qa;          // [2][M] AoS position ping-pong of the per-launch window:
+                      // (x, y, z, 0) in 3-D, uint2 (x, y) in 2-D
   // cluster build (k_build_sort -> k_build_pairs -> k_cluster_build)
   uint32_t* bsq;      // [dims][M] cell-sorted positions (x, y[, z])
   int32_t* bsid;      // [M] particle | species << 24 of a sorted entry
@@ -2462,11 +2464,15 @@ __global__ __launch_bounds__(256) void k_build_nlist2(const Derived* __restrict_
     }
   }
   sc.nn[base + i] = min(cnt, kNlMax);
+  reinterpret_cast<uint2*>(sc.qa)[base + i] = make_uint2(qx, qy);  // sub-step 0's read buffer
   if (cnt > kNlMax) sc.fallback[e] = 1;  // -> the env re-runs on the global path
 }
 
 // Sub-step s of the 2-D neighbour-list window, one thread per colloid of
 // every env (XCD-aware workgroup order: one env's colloids share an L2).
+// Positions ping-pong between two AoS uint2 buffers in sc.qa (sub-step s
+// reads buffer s & 1, the build filled buffer 0); the last sub-step writes
+// st.q.
 // sc.disp holds the squared maximum displacement until the last sub-step.
 template <bool kMulti, bool kWalls>
 __global__ __launch_bounds__(256) void k_nl_step2(const Derived* __restrict__ d, DevState st,
@@ -2484,16 +2490,17 @@ __global__ __launch_bounds__(256) void k_nl_step2(const Derived* __restrict__ d,
   if (sc.fallback[e] != 0) return;
   const size_t base = (size_t)e * N;
   const bool first = s == 0, last = s == n_steps - 1;
-  const uint32_t* R = (s & 1) ? sc.qalt : st.q;
-  uint32_t* W = (s & 1) ? st.q : sc.qalt;
+  const uint2* R = reinterpret_cast<const uint2*>(sc.qa) + (s & 1) * M;
+  uint2* W = reinterpret_cast<uint2*>(sc.qa) + ((s & 1) ^ 1) * M;
   const int par = window_parity(ctl);
   const uint64_t step = ctl[kCtlStep] + (uint64_t)s;
   const int si = kMulti ? st.species[i] : 0;
   const float sx0 = d->sx[0], sx1 = d->sx[1];
   const int nn = sc.nn[gi];
   PState p;
-  p.qx = R[gi];
-  p.qy = R[M + gi];
+  const uint2 qo = R[gi];
+  p.qx = qo.x;
+  p.qy = qo.y;
   p.ix = st.img[gi];
   p.iy = st.img[M + gi];
   p.an = st.ang[gi];
@@ -2523,9 +2530,9 @@ __global__ __launch_bounds__(256) void k_nl_step2(const Derived* __restrict__ d,
     for (int u = 0; u < 8; ++u) pk[u] = k0 + u < nn ? nlp[(size_t)(k0 + u) * M] : -1;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const size_t gj = base + (pk[u] < 0 ? i : (pk[u] & 0xffffff));
-      xj[u] = R[gj];
-      yj[u] = R[M + gj];
+      const uint2 qj = R[base + (pk[u] < 0 ? i : (pk[u] & 0xffffff))];
+      xj[u] = qj.x;
+      yj[u] = qj.y;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -2553,8 +2560,12 @@ __global__ __launch_bounds__(256) void k_nl_step2(const Derived* __restrict__ d,
   float vx = 0.0f, vy = 0.0f, om = 0.0f;
   bd_step(pc, p, ax, ay, fs, tz, st.f_ext[gi], st.f_ext[M + gi], d->key0, d->key1 ^ (uint32_t)e,
           (uint32_t)i, step, last, &vx, &vy, &om, an_swim);
-  W[gi] = p.qx;
-  W[M + gi] = p.qy;
+  if (last) {  // nobody reads st.q during the window
+    st.q[gi] = p.qx;
+    st.q[M + gi] = p.qy;
+  } else {
+    W[gi] = make_uint2(p.qx, p.qy);
+  }
   st.img[gi] = p.ix;
   st.img[M + gi] = p.iy;
   st.ang[gi] = p.an;
@@ -2744,9 +2755,9 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
   // (partial state: restore the snapshot and re-run)
   const int fbv = sc.fallback[e];
   const bool flagged_build = fbv == 1, timed_out = fbv == 3;
-  if (!flagged_build && !timed_out && nlist && (n_steps & 1)) {
-    // neighbour-list window, odd length: the last sub-step wrote the second
-    // position buffer (the exact test below reads only the snapshot)
+  if (!flagged_build && !timed_out && nlist == 2 && (n_steps & 1)) {
+    // persistent neighbour-list window (nlist 2), odd length: the last
+    // sub-step wrote the second position buffer (the test reads the snapshot)
     for (int k = tid; k < 2 * N; k += T) {
       const size_t o = (size_t)(k / N) * M + base + (k % N);
       st.q[o] = sc.qalt[o];

@@ -777,9 +777,9 @@ __global__ __launch_bounds__(1024) void k_check3(const Derived* __restrict__ d, 
   // (partial state: restore the snapshot and re-run)
   const int fbv = sc.fallback[e];
   const bool flagged_build = fbv == 1, timed_out = fbv == 3;
-  if (!flagged_build && !timed_out && nlist && (n_steps & 1)) {
-    // neighbour-list path, odd window: the last sub-step wrote the second
-    // position buffer (the exact test below reads only the snapshot)
+  if (!flagged_build && !timed_out && nlist == 2 && (n_steps & 1)) {
+    // persistent neighbour-list window (nlist 2), odd length: the last
+    // sub-step wrote the second position buffer (the test reads the snapshot)
     for (int k = tid; k < 3 * N; k += T) {
       const size_t o = (size_t)(k / N) * M + base + (k % N);
       st.q[o] = sc.qalt[o];
@@ -936,14 +936,17 @@ __global__ __launch_bounds__(256) void k_build_nlist3(const Derived* __restrict_
     }
   }
   sc.nn[base + i] = min(cnt, kNlMax);
+  sc.qa[base + i] = make_uint4(qx, qy, qz, 0u);  // sub-step 0's read buffer
   if (cnt > kNlMax) sc.fallback[e] = 1;  // -> the env re-runs on the global path
 }
 
 // Sub-step s of the neighbour-list window, one thread per colloid of every
 // env: block_global_run3's force sum (over the listed neighbours: pairs
 // beyond them cannot be in range while k_check3's test holds) and update.
-// Reads positions from (s odd ? qalt : q), writes the other buffer; image
-// counters and directors are the colloid's own and update in place.
+// Positions ping-pong between two AoS buffers (one 16-B load per
+// neighbour): sub-step s reads qa[s & 1] (the build filled qa[0]) and writes
+// the other; the last sub-step writes st.q.  Image counters and directors
+// are the colloid's own and update in place.
 // sc.disp holds the squared maximum displacement until the last sub-step.
 template <bool kMulti, bool kWalls>
 __global__ __launch_bounds__(256) void k_nl_step3(const Derived* __restrict__ d, DevState st,
@@ -964,8 +967,8 @@ __global__ __launch_bounds__(256) void k_nl_step3(const Derived* __restrict__ d,
   if (sc.fallback[e] != 0) return;
   const size_t base = (size_t)e * N;
   const bool first = s == 0, last = s == n_steps - 1;
-  const uint32_t* R = (s & 1) ? sc.qalt : st.q;
-  uint32_t* W = (s & 1) ? st.q : sc.qalt;
+  const uint4* R = sc.qa + (s & 1) * M;
+  uint4* W = sc.qa + ((s & 1) ^ 1) * M;
   const int par = window_parity(ctl);
   const uint64_t step = ctl[kCtlStep] + (uint64_t)s;
   const int si = kMulti ? st.species[i] : 0;
@@ -975,9 +978,12 @@ __global__ __launch_bounds__(256) void k_nl_step3(const Derived* __restrict__ d,
   float v[3];
   // issue every own load first: one memory latency
   const int nn = sc.nn[gi];
+  const uint4 qo = R[gi];
+  q[0] = qo.x;
+  q[1] = qo.y;
+  q[2] = qo.z;
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
-    q[a] = R[a * M + gi];
     im[a] = st.img[a * M + gi];
     v[a] = st.dir3[a * M + gi];
   }
@@ -1015,21 +1021,17 @@ __global__ __launch_bounds__(256) void k_nl_step3(const Derived* __restrict__ d,
     // eight neighbours per round: their indices, then their positions, in
     // flight together (two memory latencies per round)
     int32_t pk[8];
-    uint32_t qj[8][3];
+    uint4 qj[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) pk[u] = k0 + u < nn ? nlp[(size_t)(k0 + u) * M] : -1;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const size_t gj = base + (pk[u] < 0 ? i : (pk[u] & 0xffffff));
-#pragma unroll
-      for (int a = 0; a < 3; ++a) qj[u][a] = R[a * M + gj];
-    }
+    for (int u = 0; u < 8; ++u) qj[u] = R[base + (pk[u] < 0 ? i : (pk[u] & 0xffffff))];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       if (pk[u] < 0) continue;
-      const float rx = (float)(int32_t)(qj[u][0] - q[0]) * sx[0];
-      const float ry = (float)(int32_t)(qj[u][1] - q[1]) * sx[1];
-      const float rz = (float)(int32_t)(qj[u][2] - q[2]) * sx[2];
+      const float rx = (float)(int32_t)(qj[u].x - q[0]) * sx[0];
+      const float ry = (float)(int32_t)(qj[u].y - q[1]) * sx[1];
+      const float rz = (float)(int32_t)(qj[u].z - q[2]) * sx[2];
       if (kMulti) {
         const int sp = si * kMaxSpecies + (pk[u] >> 24);
         pair_force3(pt.cut2[sp], pt.sig6[sp], eps24, rx, ry, rz, acc[0], acc[1], acc[2]);
@@ -1067,9 +1069,14 @@ __global__ __launch_bounds__(256) void k_nl_step3(const Derived* __restrict__ d,
 #ifndef SWARM_ABL_NL_NOROT  // timing ablation only (tools/_variants)
   rotate_director(v, ph[0], ph[1], ph[2]);
 #endif
+  if (last) {  // nobody reads st.q during the window
+#pragma unroll
+    for (int a = 0; a < 3; ++a) st.q[a * M + gi] = q[a];
+  } else {
+    W[gi] = make_uint4(q[0], q[1], q[2], 0u);
+  }
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
-    W[a * M + gi] = q[a];
     st.img[a * M + gi] = im[a];
     st.dir3[a * M + gi] = v[a];
   }
