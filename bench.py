@@ -467,7 +467,12 @@ def measure(args, E, rank, world, device, builder=None, colloids=None):
     if colloids is not None:
         args_e.colloids = colloids
     args = args_e
-    eng, ff, agent = (builder or build_workload)(args_e, 42 + rank * E, device)
+    from swarmrl_amd.rollout import shard_envs
+
+    # this rank's contiguous block of the world * E envs (rollout.shard_envs):
+    # env g is placed with default_rng(42 + g) (swarm_engine.add_colloids)
+    envs = shard_envs(world * E, rank, world)
+    eng, ff, agent = (builder or build_workload)(args_e, 42 + envs[0], device)
     eng.integrate(1, ff)  # setup, overlap removal, first slice (eager)
 
     def one_slice():

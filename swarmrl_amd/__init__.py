@@ -20,6 +20,7 @@ from swarmrl_amd import (  # noqa: F401
     observables,
     sampling_strategies,
     tasks,
+    trainers,
     units,
     utils,
     value_functions,

@@ -201,7 +201,6 @@ struct Scratch {
   int32_t* nl;        // [kNlMax][M] neighbours j | species << 24 of particle gi
   int32_t* nn;        // [M] neighbour count
   uint32_t* qalt;     // [dims][M] second position buffer (sub-steps alternate)
-  uint32_t* nl_bar;   // [1] grid-barrier counter of the persistent window (reset by the build)
   uint4* qa;          // [2][M] AoS position ping-pong of the per-launch window:
                       // (x, y, z, 0) in 3-D, uint2 (x, y) in 2-D
   // cluster build (k_build_sort -> k_build_pairs -> k_cluster_build)
@@ -2409,7 +2408,6 @@ __global__ __launch_bounds__(256) void k_build_nlist2(const Derived* __restrict_
   __syncthreads();
   const int e = blockIdx.y, N = st.n;
   const int ps = blockIdx.x * blockDim.x + threadIdx.x;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *sc.nl_bar = 0;
   if (ps >= N) return;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly);
@@ -2589,148 +2587,6 @@ __global__ __launch_bounds__(256) void k_nl_step2(const Derived* __restrict__ d,
   if (st.reuse) save_forces(st, gi, par ^ 1);  // this run's actions, the final angle
 }
 
-// Grid-wide barrier of a persistent launch whose workgroups are all resident
-// (the host launches at most 256 workgroups of one wave): arrive with a
-// release, poll the agent-scope counter (vector loads), then acquire, which
-// invalidates this CU's L1 so the next reads see the other workgroups'
-// stores.  Bounded: after ~2^22 polls it returns false and the caller
-// abandons the window (k_check restores the snapshot and re-runs it).
-__device__ __forceinline__ bool grid_barrier(uint32_t* bar, uint32_t target) {
-  __shared__ int ok;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    atomicAdd(bar, 1u);
-    int good = 1;
-    uint32_t it = 0;
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++it > (1u << 22)) {
-        good = 0;
-        break;
-      }
-    }
-    ok = good;
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  return ok != 0;
-}
-
-// The whole 2-D neighbour-list window in ONE persistent launch (latency-
-// bound windows: E N <= 16384, one 64-thread workgroup per 64 colloids, all
-// resident): each thread keeps its colloid's state, actions and first eight
-// neighbours in registers across the sub-steps, publishes its position to
-// the sub-step's write buffer, and a grid barrier separates the sub-steps
-// (instead of a launch each).  Same bits as k_nl_step2 (StepNoise carries
-// the normals of consecutive sub-steps: the step_normals numbers).
-template <bool kMulti, bool kWalls>
-__global__ __launch_bounds__(64) void k_nl_run2(const Derived* __restrict__ d, DevState st,
-                                                Scratch sc, int n_steps,
-                                                const uint64_t* __restrict__ ctl) {
-  __shared__ PairTables pt;
-  if (kMulti) stage_pair_tables(d, &pt);
-  const size_t M = (size_t)st.m;
-  const size_t gi = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int N = st.n;
-  const bool inb = gi < M;
-  const int e = inb ? (int)(gi / N) : 0;
-  const int i = inb ? (int)(gi - (size_t)e * N) : 0;
-  const bool act = inb && sc.fallback[e] == 0;
-  const size_t g = act ? gi : 0;  // idle lanes compute on colloid 0 (never stored)
-  const size_t base = (size_t)e * N;
-  const int par = window_parity(ctl);
-  const uint64_t step0 = ctl[kCtlStep];
-  const int si = kMulti ? st.species[i] : 0;
-  const float sx0 = d->sx[0], sx1 = d->sx[1], eps24 = d->eps24;
-  const PConst pc = load_pconst(d, si);
-  const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
-  PState p = {st.q[g], st.q[M + g], st.ang[g], st.img[g], st.img[M + g]};
-  const float fex = st.f_ext[g], fey = st.f_ext[M + g];
-  const float fs = st.f_swim[g], tz = st.torque_z[g];
-  const PrevSlot prv = prev_slot(st, par);  // reuse_forces: sub-step 0's actions
-  const float fs0 = st.reuse ? prv.f[g] : fs, tz0 = st.reuse ? prv.tz[g] : tz;
-  const uint32_t an0 = st.reuse ? prv.ang[g] : p.an;
-  const int nn = act ? sc.nn[g] : 0;
-  int32_t nlr[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) nlr[u] = u < nn ? sc.nl[(size_t)u * M + g] : -1;
-  if (act) {
-    sc.bq[g] = p.qx;
-    sc.bq[M + g] = p.qy;
-    sc.bimg[g] = p.ix;
-    sc.bimg[M + g] = p.iy;
-    sc.bang[g] = p.an;
-  }
-  const uint32_t q0x = p.qx, q0y = p.qy;
-  float dmax2 = 0.0f, vx = 0.0f, vy = 0.0f, om = 0.0f;
-  StepNoise noise;
-  for (int s = 0; s < n_steps; ++s) {
-    const uint32_t* R = (s & 1) ? sc.qalt : st.q;
-    uint32_t* W = (s & 1) ? st.q : sc.qalt;
-    int64_t ax = 0, ay = 0;
-    for (int kb = 0; kb < nn; kb += 8) {
-      int32_t pk[8];
-      uint32_t xj[8], yj[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        pk[u] = kb == 0 ? nlr[u] : (kb + u < nn ? sc.nl[(size_t)(kb + u) * M + g] : -1);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const size_t gj = base + (pk[u] < 0 ? i : (pk[u] & 0xffffff));
-        xj[u] = R[gj];
-        yj[u] = R[M + gj];
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (pk[u] < 0) continue;
-        const float rx = (float)(int32_t)(xj[u] - p.qx) * sx0;
-        const float ry = (float)(int32_t)(yj[u] - p.qy) * sx1;
-        if (kMulti) {
-          const int sp = si * kMaxSpecies + (pk[u] >> 24);
-          pair_force(pt.cut2[sp], pt.sig6[sp], eps24, rx, ry, ax, ay);
-        } else {
-          pair_force(d->cut2[0], d->sig6[0], eps24, rx, ry, ax, ay);
-        }
-      }
-    }
-    if (kWalls && act) {
-      int64_t az = 0;
-      wall_forces<2>(d, si, (float)p.qx * sx0, (float)p.qy * sx1, 0.0f, ax, ay, az, st.wall_viol);
-    }
-    const bool first = s == 0;
-    bd_step(pc, p, ax, ay, first ? fs0 : fs, first ? tz0 : tz, fex, fey, k0, k1, (uint32_t)i,
-            step0 + (uint64_t)s, s == n_steps - 1, &vx, &vy, &om, first ? an0 : p.an, nullptr,
-            &noise, first);
-    if (act) {
-      W[g] = p.qx;
-      W[M + g] = p.qy;
-    }
-    const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
-    const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
-    dmax2 = fmaxf(dmax2, ddx * ddx + ddy * ddy);
-    if (s < n_steps - 1 && !grid_barrier(sc.nl_bar, gridDim.x * (uint32_t)(s + 1))) {
-      if (act) sc.fallback[e] = 3;  // abandoned: k_check restores and re-runs
-      return;
-    }
-  }
-  if (!act) return;
-  st.img[g] = p.ix;
-  st.img[M + g] = p.iy;
-  st.ang[g] = p.an;
-  st.vel[g] = vx;
-  st.vel[M + g] = vy;
-  st.vel[2 * M + g] = 0.0f;
-  st.omega[g] = om;
-  const float disp = sqrt_rn(dmax2);
-  sc.disp[g] = disp;
-  if (!(disp < 0.5f * d->skin)) {  // a mover (k_check's exact test)
-    const int k = atomicAdd(&sc.nmov[e], 1);
-    if (k < kMaxMovers) sc.movers[(size_t)e * kMaxMovers + k] = i;
-  }
-  if (st.reuse) save_forces(st, g, par ^ 1);
-}
-
 // ---------------------------------------------------------------- check
 __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, DevState st,
                                                 Scratch sc, int n_steps,
@@ -2750,22 +2606,11 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
   const int par = window_parity(step_ctr);  // reuse_forces slot of this window
   if (tid < 16) misc[tid] = 0;
   __syncthreads();
-  // 1: flagged by the build (the env did not run: its state is the window
-  // start); 3: a persistent neighbour-list run timed out at a grid barrier
-  // (partial state: restore the snapshot and re-run)
-  const int fbv = sc.fallback[e];
-  const bool flagged_build = fbv == 1, timed_out = fbv == 3;
-  if (!flagged_build && !timed_out && nlist == 2 && (n_steps & 1)) {
-    // persistent neighbour-list window (nlist 2), odd length: the last
-    // sub-step wrote the second position buffer (the test reads the snapshot)
-    for (int k = tid; k < 2 * N; k += T) {
-      const size_t o = (size_t)(k / N) * M + base + (k % N);
-      st.q[o] = sc.qalt[o];
-    }
-  }
-  if (!flagged_build && !timed_out && !nlist && sc.big_n[e] > 0)
+  // flagged by the build: the env did not run (its state is the window start)
+  const bool flagged_build = sc.fallback[e] == 1;
+  if (!flagged_build && !nlist && sc.big_n[e] > 0)
     run_big_clusters(d, st, sc, e, n_steps, step0, cnt, &pt, par);
-  if (!flagged_build && !timed_out) {
+  if (!flagged_build) {
     // the movers (displacement >= skin / 2) were listed by the run kernel
     // and the big-cluster run: no scan over all colloids here
     // (agent-scope loads: the big-cluster run of this workgroup appended
@@ -2830,7 +2675,7 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
     }
     __syncthreads();
   }
-  const bool rerun = flagged_build || timed_out || misc[1] != 0;
+  const bool rerun = flagged_build || misc[1] != 0;
   if (rerun) {
     // a flagged env was skipped by k_cluster_run: its state is the window
     // start already; otherwise restore the snapshot k_cluster_run took

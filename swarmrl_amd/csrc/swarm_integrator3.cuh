@@ -772,20 +772,9 @@ __global__ __launch_bounds__(1024) void k_check3(const Derived* __restrict__ d, 
   const int par = window_parity(step_ctr);
   if (tid < 16) misc[tid] = 0;
   __syncthreads();
-  // 1: flagged by the build (the env did not run: its state is the window
-  // start); 3: a persistent neighbour-list run timed out at a grid barrier
-  // (partial state: restore the snapshot and re-run)
-  const int fbv = sc.fallback[e];
-  const bool flagged_build = fbv == 1, timed_out = fbv == 3;
-  if (!flagged_build && !timed_out && nlist == 2 && (n_steps & 1)) {
-    // persistent neighbour-list window (nlist 2), odd length: the last
-    // sub-step wrote the second position buffer (the test reads the snapshot)
-    for (int k = tid; k < 3 * N; k += T) {
-      const size_t o = (size_t)(k / N) * M + base + (k % N);
-      st.q[o] = sc.qalt[o];
-    }
-  }
-  if (!flagged_build && !timed_out) {
+  // flagged by the build: the env did not run (its state is the window start)
+  const bool flagged_build = sc.fallback[e] == 1;
+  if (!flagged_build) {
     const int nm = sc.nmov[e];
     for (int k = tid; k < min(nm, kMaxMovers); k += T) movers[k] = sc.movers[(size_t)e * kMaxMovers + k];
     __syncthreads();
@@ -832,7 +821,7 @@ __global__ __launch_bounds__(1024) void k_check3(const Derived* __restrict__ d, 
     }
     __syncthreads();
   }
-  if (flagged_build || timed_out || misc[1] != 0) {
+  if (flagged_build || misc[1] != 0) {
     for (int i = tid; i < N && !flagged_build; i += T) {
       const size_t gi = base + i;
 #pragma unroll
@@ -875,7 +864,6 @@ __global__ __launch_bounds__(256) void k_build_nlist3(const Derived* __restrict_
   __syncthreads();
   const int e = blockIdx.y, N = st.n;
   const int ps = blockIdx.x * blockDim.x + threadIdx.x;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *sc.nl_bar = 0;
   if (ps >= N) return;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly + lz);
@@ -1122,177 +1110,5 @@ __global__ __launch_bounds__(256) void k_nl_step3(const Derived* __restrict__ d,
   if (st.reuse) save_forces(st, gi, par ^ 1);  // this run's actions, the final director
 }
 
-
-// The whole 3-D neighbour-list window in ONE persistent launch (k_nl_run2's
-// scheme in 3-D: state, actions and the first eight neighbours in
-// registers, a grid barrier between sub-steps; same bits as k_nl_step3).
-template <bool kMulti, bool kWalls>
-__global__ __launch_bounds__(64) void k_nl_run3(const Derived* __restrict__ d, DevState st,
-                                                Scratch sc, int n_steps,
-                                                const uint64_t* __restrict__ ctl) {
-  __shared__ PairTables pt;
-  if (kMulti) stage_pair_tables(d, &pt);
-  const size_t M = (size_t)st.m;
-  const size_t gi = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int N = st.n;
-  const bool inb = gi < M;
-  const int e = inb ? (int)(gi / N) : 0;
-  const int i = inb ? (int)(gi - (size_t)e * N) : 0;
-  const bool act = inb && sc.fallback[e] == 0;
-  const size_t g = act ? gi : 0;  // idle lanes compute on colloid 0 (never stored)
-  const size_t base = (size_t)e * N;
-  const int par = window_parity(ctl);
-  const uint64_t step0 = ctl[kCtlStep];
-  const int si = kMulti ? st.species[i] : 0;
-  const float sx[3] = {d->sx[0], d->sx[1], d->sx[2]};
-  const float isx[3] = {d->inv_sx[0], d->inv_sx[1], d->inv_sx[2]};
-  const float eps24 = d->eps24;
-  const bool noisy = d->noisy != 0;
-  const float mob_dt = d->mob_dt[si], sig_t = d->sig_t[si], rot_dt = d->rot_dt[si],
-              sig_r = d->sig_r[si];
-  const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
-  uint32_t q[3], q0[3];
-  int32_t im[3];
-  float v[3], fex[3], vs0[3], tq0[3];
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    q[a] = st.q[a * M + g];
-    im[a] = st.img[a * M + g];
-    v[a] = st.dir3[a * M + g];
-    fex[a] = st.f_ext[a * M + g];
-    q0[a] = q[a];
-  }
-  const float fs = st.f_swim[g];
-  const float tq[3] = {st.torque_xy[g], st.torque_xy[M + g], st.torque_z[g]};
-  const PrevSlot prv = prev_slot(st, par);  // reuse_forces: sub-step 0's actions
-  const float fs0 = st.reuse ? prv.f[g] : fs;
-  tq0[0] = st.reuse ? prv.txy[g] : tq[0];
-  tq0[1] = st.reuse ? prv.txy[M + g] : tq[1];
-  tq0[2] = st.reuse ? prv.tz[g] : tq[2];
-#pragma unroll
-  for (int a = 0; a < 3; ++a) vs0[a] = st.reuse ? prv.dir3[a * M + g] : v[a];
-  const int nn = act ? sc.nn[g] : 0;
-  int32_t nlr[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) nlr[u] = u < nn ? sc.nl[(size_t)u * M + g] : -1;
-  if (act) {
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      sc.bq[a * M + g] = q[a];
-      sc.bimg[a * M + g] = im[a];
-      sc.bdir3[a * M + g] = v[a];
-    }
-  }
-  float dmax2 = 0.0f, f[3] = {0.0f, 0.0f, 0.0f};
-  StepNoise noise;
-  for (int s = 0; s < n_steps; ++s) {
-    const uint32_t* R = (s & 1) ? sc.qalt : st.q;
-    uint32_t* W = (s & 1) ? st.q : sc.qalt;
-    const bool first = s == 0;
-    const uint64_t step = step0 + (uint64_t)s;
-    int64_t acc[3] = {0, 0, 0};
-    for (int kb = 0; kb < nn; kb += 8) {
-      int32_t pk[8];
-      uint32_t qj[8][3];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        pk[u] = kb == 0 ? nlr[u] : (kb + u < nn ? sc.nl[(size_t)(kb + u) * M + g] : -1);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const size_t gj = base + (pk[u] < 0 ? i : (pk[u] & 0xffffff));
-#pragma unroll
-        for (int a = 0; a < 3; ++a) qj[u][a] = R[a * M + gj];
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (pk[u] < 0) continue;
-        const float rx = (float)(int32_t)(qj[u][0] - q[0]) * sx[0];
-        const float ry = (float)(int32_t)(qj[u][1] - q[1]) * sx[1];
-        const float rz = (float)(int32_t)(qj[u][2] - q[2]) * sx[2];
-        if (kMulti) {
-          const int sp = si * kMaxSpecies + (pk[u] >> 24);
-          pair_force3(pt.cut2[sp], pt.sig6[sp], eps24, rx, ry, rz, acc[0], acc[1], acc[2]);
-        } else {
-          pair_force3(d->cut2[0], d->sig6[0], eps24, rx, ry, rz, acc[0], acc[1], acc[2]);
-        }
-      }
-    }
-    if (kWalls && act)
-      wall_forces<3>(d, si, (float)q[0] * sx[0], (float)q[1] * sx[1], (float)q[2] * sx[2], acc[0],
-                     acc[1], acc[2], st.wall_viol);
-    float gt[3] = {0.0f, 0.0f, 0.0f}, gr[3] = {0.0f, 0.0f, 0.0f};
-    if (noisy) {
-      noise.next(k0, k1, (uint32_t)i, step, first, gt);
-      normals3(k0, k1, (uint32_t)i, step, 2u, gr);
-    }
-    float ph[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      f[a] = i64_to_f32(acc[a]) * 5.9604644775390625e-08f;
-      f[a] = f[a] + fex[a];
-      f[a] = f[a] + (first ? fs0 : fs) * (first ? vs0[a] : v[a]);
-      float dq = f[a] * mob_dt;
-      ph[a] = (first ? tq0[a] : tq[a]) * rot_dt;
-      if (noisy) {
-        dq = dq + sig_t * gt[a];
-        ph[a] = ph[a] + sig_r * gr[a];
-      }
-      advance(q[a], im[a], f2i32(dq * isx[a]));
-    }
-    rotate_director(v, ph[0], ph[1], ph[2]);
-    if (act) {
-#pragma unroll
-      for (int a = 0; a < 3; ++a) W[a * M + g] = q[a];
-    }
-    float dd[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) dd[a] = (float)(int32_t)(q[a] - q0[a]) * sx[a];
-    float d2 = dd[0] * dd[0] + dd[1] * dd[1];
-    d2 = d2 + dd[2] * dd[2];
-    dmax2 = fmaxf(dmax2, d2);
-    if (s < n_steps - 1 && !grid_barrier(sc.nl_bar, gridDim.x * (uint32_t)(s + 1))) {
-      if (act) sc.fallback[e] = 3;  // abandoned: k_check3 restores and re-runs
-      return;
-    }
-  }
-  if (!act) return;
-  {  // velocities of the last sub-step (block_global_run3's sequence)
-    const int sl = n_steps - 1;
-    const float* tql = sl == 0 ? tq0 : tq;
-    float vv[3], ww[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      vv[a] = f[a] * d->inv_gt[si];
-      ww[a] = tql[a] * d->inv_gr[si];
-    }
-    if (noisy) {
-      float gv[3], gw[3];
-      normals3(k0, k1, (uint32_t)i, step0 + (uint64_t)sl, 1u, gv);
-      normals3(k0, k1, (uint32_t)i, step0 + (uint64_t)sl, 3u, gw);
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        vv[a] = vv[a] + d->sig_v[si] * gv[a];
-        ww[a] = ww[a] + d->sig_w[si] * gw[a];
-      }
-    }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) st.vel[a * M + g] = vv[a];
-    st.omega_xy[g] = ww[0];
-    st.omega_xy[M + g] = ww[1];
-    st.omega[g] = ww[2];
-  }
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    st.img[a * M + g] = im[a];
-    st.dir3[a * M + g] = v[a];
-  }
-  const float disp = sqrt_rn(dmax2);
-  sc.disp[g] = disp;
-  if (!(disp < 0.5f * d->skin)) {  // a mover (k_check3's exact test)
-    const int k = atomicAdd(&sc.nmov[e], 1);
-    if (k < kMaxMovers) sc.movers[(size_t)e * kMaxMovers + k] = i;
-  }
-  if (st.reuse) save_forces(st, g, par ^ 1);  // this run's actions, the final director
-}
 
 }  // namespace swarm

@@ -775,26 +775,32 @@ class SwarmEngine(Engine):
             torch.cuda.current_stream().synchronize()
         count = int(ring["count"][0])
         start = ring["drained"]
-        if count - start > ring["cap"]:
+        cap = ring["cap"]
+        # Entry k lives in slot k % cap and is overwritten by entry k + cap,
+        # whose write starts as soon as the published count reaches k + cap
+        # (before the count moves past it).  With the stream drained nothing
+        # is in flight, so cap entries are readable; without waiting, entry k
+        # is readable only while the count stays below k + cap.
+        if count - start > (cap if block else cap - 1):
             raise RuntimeError(
                 f"trajectory ring overflow: {count - start} entries since the last drain, "
-                f"capacity {ring['cap']} (drain more often)")
+                f"capacity {cap} (drain more often)")
         N = self.n_particles
         step = np.zeros(1, np.uint64)
         for k in range(start, count):
-            addr = ring["ptr"] + 64 + (k % ring["cap"]) * ring["entry"]
+            addr = ring["ptr"] + 64 + (k % cap) * ring["entry"]
             pos = np.zeros((N, 3))
             dirs = np.zeros((N, 3))
             vel = np.zeros((N, 3))
             self._native.call("swarm_traj_entry_to_host", ctypes.c_void_p(addr), pos.ctypes.data,
                               dirs.ctypes.data, vel.ctypes.data, step.ctypes.data)
+            if not block and int(ring["count"][0]) >= k + cap:  # overwritten while being read
+                raise RuntimeError("trajectory ring overflow while draining (drain more often)")
             self._append_traj(self._time_offset + int(step[0]) * self._time_step, pos, vel, dirs)
             if len(self.traj_holder["Times"]) >= self.write_chunk_size:
                 self._write_traj_chunk_to_file()
                 for val in self.traj_holder.values():
                     val.clear()
-        if int(ring["count"][0]) - start > ring["cap"]:  # overwritten while being read
-            raise RuntimeError("trajectory ring overflow while draining (drain more often)")
         ring["drained"] = count
         return count - start
 

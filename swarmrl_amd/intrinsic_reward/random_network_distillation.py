@@ -56,18 +56,38 @@ class RNDReward(IntrinsicReward):
         x = self._stack(feats)
         return x.reshape(-1, self.in_dim).to(torch.float32).to(self.device)
 
+    @staticmethod
+    def fused_architecture_ok(net: torch.nn.Module, in_dim: int) -> bool:
+        """k_rnd_distance hard-codes the stock network: an RNDArchitecture
+        whose Sequential is exactly Linear(in_dim, 32) -> ReLU -> Linear(32, 32)
+        -> ReLU -> Linear(32, 32) with contiguous fp32 parameters (read in place
+        as [out][in] rows).  Anything else -- another activation, an extra
+        layer, a transposed or non-contiguous parameter -- takes the torch
+        path."""
+        if type(net) is not RNDArchitecture or not isinstance(net.net, torch.nn.Sequential):
+            return False
+        layers = list(net.net)
+        kinds = [torch.nn.Linear, torch.nn.ReLU, torch.nn.Linear, torch.nn.ReLU, torch.nn.Linear]
+        if len(layers) != len(kinds) or any(type(m) is not k for m, k in zip(layers, kinds)):
+            return False
+        for m, fan_in in zip(layers[0::2], (in_dim, 32, 32)):
+            if m.in_features != fan_in or m.out_features != 32 or m.bias is None:
+                return False
+            if tuple(m.weight.shape) != (32, fan_in) or tuple(m.bias.shape) != (32,):
+                return False
+            for t in (m.weight, m.bias):
+                if t.dtype != torch.float32 or not t.is_contiguous():
+                    return False
+        return True
+
     def _fused_ok(self, points: torch.Tensor) -> bool:
-        """The one-launch HIP metric applies to the stock architecture
-        (three Linear(32) layers, fp32 parameters) on the GPU."""
+        """The one-launch HIP metric applies to the stock architecture on the
+        GPU (fused_architecture_ok), for inputs of 1..16 features."""
         if not (points.is_cuda and points.dtype == torch.float32 and 1 <= self.in_dim <= 16):
             return False
-        for net in (self.target_network, self.predictor_network):
-            lin = [m for m in net.modules() if isinstance(m, torch.nn.Linear)]
-            if len(lin) != 3 or any(m.out_features != 32 or m.bias is None or
-                                    m.weight.dtype != torch.float32 or not m.weight.is_cuda
-                                    for m in lin):
-                return False
-        return True
+        return all(self.fused_architecture_ok(net, self.in_dim) and
+                   all(p.is_cuda for p in net.parameters())
+                   for net in (self.target_network, self.predictor_network))
 
     @torch.no_grad()
     def compute_distance(self, points: torch.Tensor) -> torch.Tensor:

@@ -27,8 +27,18 @@ _NAMES = ("features", "actions", "log_probs", "rewards")
 
 
 def shard_envs(total_envs: int, rank: int, world: int):
-    """Env ids owned by a rank: e with e mod world == rank."""
-    return [e for e in range(total_envs) if e % world == rank]
+    """Env ids owned by a rank: one contiguous block, rank r of G owning
+    envs [r E, (r + 1) E) with E = total / G (the first total mod G ranks one
+    more).  Contiguous blocks, not SURVEY 8(e)'s e mod G: the all-gather
+    below concatenates the ranks' [T, E, ...] buffers rank-major, so the
+    gathered env axis is then the global env id.  bench.py creates each
+    rank's engine with seed 42 + its first env id, so env g is placed with
+    default_rng(42 + g) whatever the world size."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"rank {rank} outside a world of {world}")
+    per, extra = divmod(total_envs, world)
+    lo = rank * per + min(rank, extra)
+    return list(range(lo, lo + per + (1 if rank < extra else 0)))
 
 
 def _stacked(trajectory) -> Dict[str, torch.Tensor]:

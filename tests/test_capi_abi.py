@@ -43,3 +43,39 @@ def test_params_struct_layout_matches_oracle():
     assert ctypes.sizeof(_capi.SwarmParams) == ctypes.sizeof(oracle.Params)
     for (n1, t1), (n2, t2) in zip(_capi.SwarmParams._fields_, oracle.Params._fields_):
         assert n1 == n2 and ctypes.sizeof(t1) == ctypes.sizeof(t2)
+
+
+def _header_struct_fields(name):
+    """Member names of `typedef struct ... } name;` in include/swarmrl_amd.h."""
+    text = (ROOT / "include" / "swarmrl_amd.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    body = re.search(r"typedef struct[^{]*\{([^}]*)\}\s*" + name + r"\s*;", text).group(1)
+    return re.findall(r"\b([A-Za-z_0-9]+)\s*(?:\[[^\]]*\])?\s*;", body)
+
+
+def test_params_struct_matches_header():
+    from swarmrl_amd import _capi
+
+    assert [n for n, _ in _capi.SwarmParams._fields_] == _header_struct_fields("swarm_params_t")
+
+
+def test_integration_sketch_matches_binding():
+    """INTEGRATION.md's maintainer sketch (the reference-side ctypes stub)
+    declares swarm_params_t exactly as the binding does, and creates the
+    engine with reuse_forces = 1 -- the reference's
+    integrator.run(k, reuse_forces=True) (espresso.py:1304-1306)."""
+    from swarmrl_amd import _capi
+
+    text = (ROOT / "INTEGRATION.md").read_text()
+    block = next(b for b in re.findall(r"```python\n(.*?)```", text, flags=re.S)
+                 if "class SwarmParams" in b)
+    cls = re.search(r"class SwarmParams\(ctypes\.Structure\):.*?\n\n", block, flags=re.S).group(0)
+    ns = {"ctypes": ctypes}
+    exec(cls, ns)  # the sketch's struct definition only (no library calls)
+    sketch = ns["SwarmParams"]
+    assert [n for n, _ in sketch._fields_] == [n for n, _ in _capi.SwarmParams._fields_]
+    for (n, t1), (_, t2) in zip(sketch._fields_, _capi.SwarmParams._fields_):
+        assert ctypes.sizeof(t1) == ctypes.sizeof(t2), n
+    assert ctypes.sizeof(sketch) == ctypes.sizeof(_capi.SwarmParams)
+    create = re.search(r"p = SwarmParams\((.*?)\)\n", block, flags=re.S).group(1)
+    assert re.search(r"\breuse_forces\s*=\s*1\b", create)

@@ -32,7 +32,7 @@ def _worker(rank, world, port, q):
                 ok &= bool(torch.all(out["actions"][t, r * E:(r + 1) * E] == v))
                 ok &= bool(torch.all(out["rewards"][t, r * E:(r + 1) * E] == v + 0.5))
         envs = shard_envs(64, rank, world)
-        ok &= len(envs) == 32 and all(e % world == rank for e in envs)
+        ok &= envs == list(range(32 * rank, 32 * rank + 32))
         q.put((rank, ok))
     finally:
         dist.destroy_process_group()
@@ -49,6 +49,21 @@ def test_gather_trajectory_two_ranks_gloo():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def test_shard_envs_contiguous_blocks_cover_every_env():
+    """Rank r owns a contiguous block; the blocks tile the env ids in rank
+    order, which is the env order of the rank-major all-gather."""
+    from swarmrl_amd.rollout import shard_envs
+
+    for total in (1, 7, 8, 64, 65):
+        for world in (1, 2, 3, 8):
+            blocks = [shard_envs(total, r, world) for r in range(world)]
+            assert sum(blocks, []) == list(range(total))
+            assert max(map(len, blocks)) - min(map(len, blocks)) <= 1
+    assert shard_envs(64, 3, 8) == list(range(24, 32))
+    with pytest.raises(ValueError):
+        shard_envs(8, 2, 2)
 
 
 def test_gather_single_process_is_identity():

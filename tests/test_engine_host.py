@@ -241,3 +241,53 @@ def test_walls_registration_and_errors(fake_backend, tmp_path):
     eng2.integrate(1, ForceFunction({"1": dummy_models.ConstForce(1.0)}))
     names = [c[0] for c in fake_backend.instances[-1].calls]
     assert "swarm_engine_set_walls" in names
+
+
+class _RingNative(FakeNative):
+    """FakeNative whose device keeps recording while the host drains: every
+    entry read advances the published count by `advance` (a replay still
+    queued on the stream)."""
+
+    advance = 0
+
+    def call(self, name, *args):
+        super().call(name, *args)
+        if name == "swarm_traj_entry_to_host":
+            self.ring["count"][0] += self.advance
+            step = np.ctypeslib.as_array(ctypes.cast(args[4], ctypes.POINTER(ctypes.c_uint64)), (1,))
+            step[0] = 0
+
+
+def _ring_engine(monkeypatch, tmp_path, cap, count, advance):
+    monkeypatch.setattr(swarm_engine, "_NativeEngine", _RingNative)
+    eng = _engine(tmp_path, 2, 2)
+    eng._setup_interactions()
+    eng._init_h5_output()
+    _RingNative.advance = advance
+    eng._native.ring = eng._ring = {"ptr": 0, "cap": cap, "entry": 64, "drained": 0,
+                                    "count": np.array([count], np.uint64)}
+    eng._time_offset = 0.0
+    return eng
+
+
+@pytest.mark.parametrize("count,advance,block,ok", [
+    (8, 0, True, True),     # stream drained: all cap entries readable
+    (8, 0, False, False),   # cap entries with work in flight: entry 0 may be being overwritten
+    (7, 0, False, True),
+    (7, 1, False, False),   # the device publishes entry 8 while entry 0..6 are read
+    (4, 1, False, True),    # count reaches 8 only after entry 3 (< 0 + cap) has been read
+])
+def test_trajectory_ring_overflow_is_detected(fake_backend, monkeypatch, tmp_path, count, advance,
+                                              block, ok):
+    """drain_trajectory(block=False) between graph replays: entry k of a ring
+    of capacity cap is overwritten by entry k + cap, whose write starts as
+    soon as the published count reaches k + cap -- so k is readable only
+    while count < k + cap (the checks used count - start > cap)."""
+    monkeypatch.setattr(swarm_engine.torch.cuda, "current_stream",
+                        lambda: type("S", (), {"synchronize": lambda self: None})())
+    eng = _ring_engine(monkeypatch, tmp_path, 8, count, advance)
+    if ok:
+        assert eng.drain_trajectory(block=block) == count
+    else:
+        with pytest.raises(RuntimeError, match="overflow"):
+            eng.drain_trajectory(block=block)

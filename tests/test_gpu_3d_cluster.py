@@ -3,8 +3,8 @@
 bit (swarm_integrator3.cuh):
   cluster  k_build_sort3 -> k_build_pairs3 -> k_cluster_build ->
            k_cluster_run3 -> k_check3 (dilute boxes)
-  nlist    k_build_sort3 -> k_build_nlist3 -> one persistent k_nl_run3 (or
-           one k_nl_step3 per sub-step) -> k_check3 (boxes whose rc + skin
+  nlist    k_build_sort3 -> k_build_nlist3 -> one k_nl_step3 per sub-step
+           -> k_check3 (boxes whose rc + skin
            graph percolates)
 SWARMRL_AMD_NLIST=0|1 picks the path (by default the engine picks it from
 the density).
@@ -50,12 +50,11 @@ def _lattice3(rng, n, a=4.6, jitter=0.3):
     return pos, d, k * a
 
 
-@pytest.fixture(params=["cluster", "nlist", "nlist-launches"])
+@pytest.fixture(params=["cluster", "nlist"])
 def path3(request, monkeypatch):
-    """nlist: the persistent window (k_nl_run3, opt-in, E N <= 16384);
-    nlist-launches: one k_nl_step3 launch per sub-step (the default)."""
+    """cluster: the cluster window; nlist: one k_nl_step3 launch per
+    sub-step over per-colloid Verlet lists."""
     monkeypatch.setenv("SWARMRL_AMD_NLIST", "0" if request.param == "cluster" else "1")
-    monkeypatch.setenv("SWARMRL_AMD_NL_PERSIST", "0" if request.param == "nlist-launches" else "1")
     return request.param
 
 

@@ -243,14 +243,15 @@ def test_observables_device_vs_list(tmp_path):
 
 
 def test_ppo_training_device_path(tmp_path):
-    """A continuous training loop + ActorCriticAgent (vision cones, gradient sensing,
-    PPO) entirely on the device path."""
+    """ContinuousTrainer (swarmrl_amd.trainers, the reference's
+    continuous_trainer.py:22-89) + ActorCriticAgent (vision cones, gradient
+    sensing, PPO) entirely on the device path."""
     from swarmrl_amd.actions import Action
     from swarmrl_amd.agents import ActorCriticAgent
     from swarmrl_amd.networks import ActorCriticMLP, TorchModel
     from swarmrl_amd.observables import SubdividedVisionCones
     from swarmrl_amd.tasks.searching import GradientSensing
-    from trainer_driver import continuous_training
+    from swarmrl_amd.trainers import ContinuousTrainer
     from swarmrl_amd.units import UnitRegistry
 
     ureg = UnitRegistry()
@@ -267,7 +268,8 @@ def test_ppo_training_device_path(tmp_path):
                                 np.array([L, L, L]), 10, particle_type=1),
         SubdividedVisionCones(10.0, np.pi / 2, 3, [1.0] * n, particle_type=1), actions)
     agent.loss.n_epochs = 3
-    rewards = continuous_training(eng, [agent], n_episodes=3, episode_length=4)
+    rewards = ContinuousTrainer([agent]).perform_rl_training(eng, n_episodes=3, episode_length=4,
+                                                              load_bar=False)
     assert rewards.shape == (4,) and np.all(np.isfinite(rewards))
     after = list(net.model.parameters())
     assert any(not torch.equal(a, b) for a, b in zip(after, before))

@@ -1,6 +1,6 @@
 """
 The 2-D neighbour-list window (k_build_sort -> k_build_nlist2 -> one
-k_nl_step2 per sub-step, or one persistent k_nl_run2 -> k_check,
+k_nl_step2 per sub-step -> k_check,
 swarm_integrator.cuh) against the CPU
 oracle, bit for bit.  It serves dense boxes, where the rc + skin graph
 percolates and per-wave clusters do not exist (a 4096-colloid square lattice
@@ -51,13 +51,9 @@ def _stats(h):
     return fb, w
 
 
-@pytest.mark.parametrize("persist", ["1", "0"])
 @pytest.mark.parametrize("E,n_species", [(1, 1), (3, 2)])
-def test_nlist2d_4096_dense_bit_exact(E, n_species, persist, monkeypatch):
-    """persist 1: the whole window in one launch with grid barriers
-    (k_nl_run2, opt-in, E N <= 16384); 0: one k_nl_step2 launch per
-    sub-step (the default)."""
-    monkeypatch.setenv("SWARMRL_AMD_NL_PERSIST", persist)
+def test_nlist2d_4096_dense_bit_exact(E, n_species):
+    """One k_nl_step2 launch per sub-step, bit-exact against the oracle."""
     from gpu_harness import Harness, species_list
 
     rng = np.random.default_rng(51)

@@ -377,22 +377,17 @@ def test_c5_16384_large_build_bit_exact():
 
 
 @pytest.mark.parametrize("E,n,box_len,env", [
-    (1, 2000, 90.0, {}),                                   # record-streaming kernel, 16 lanes
-    (20, 4096, 200.0, {"SWARMRL_AMD_VISION_TILE": "1"}),   # LDS tiles, records staged
-    (20, 4096, 200.0, {"SWARMRL_AMD_VISION_TILE": "1", "SWARMRL_AMD_VISION_TILE_G": "16"}),
-    (20, 4096, 200.0, {"SWARMRL_AMD_VISION_TILE": "1", "SWARMRL_AMD_VISION_TILE_G": "1"}),
-    (20, 4096, 200.0, {}),                                 # record-streaming kernel, 16 lanes
-    (64, 4096, 160.0, {"SWARMRL_AMD_VISION_TILE": "1"}),   # dense: tiles read global records
-    (64, 4096, 160.0, {"SWARMRL_AMD_VISION_G": "1"}),
-    (64, 4096, 160.0, {}),                                 # record-streaming kernel, 4 lanes
+    (1, 2000, 90.0, {}),                                   # 16 lanes per agent
+    (20, 4096, 200.0, {"SWARMRL_AMD_VISION_G": "4"}),
+    (20, 4096, 200.0, {}),                                 # 16 lanes per agent
+    (64, 4096, 160.0, {"SWARMRL_AMD_VISION_G": "16"}),
+    (64, 4096, 160.0, {}),                                 # 4 lanes per agent
 ])
 def test_vision_cone_parity_lane_variants_and_dense(E, n, box_len, env, monkeypatch):
-    """Both vision kernels: LDS tiles (k_vision_tile: records staged, or read
-    from global memory for a tile denser than its LDS capacity; 16/4/1 lanes
-    per agent) and the record-streaming k_vision (grids under 8 x 8 cells, or
-    by override; 16/4/1 lanes), with dense neighbourhoods (more in-range hits
-    per lane than its LDS hit list holds, so the list is drained mid-scan),
-    bit-exact against the oracle on the first and last env."""
+    """k_vision with 16 / 4 lanes per agent (by size, or by override), with
+    dense neighbourhoods (more in-range hits per lane than its LDS hit list
+    holds, so the list is drained mid-scan), bit-exact against the oracle on
+    the first and last env."""
     from gpu_harness import Harness, random_state, species_list
     from swarmrl_amd.engine import ops
 
