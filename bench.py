@@ -28,11 +28,36 @@ sys.path.insert(0, ROOT)
 
 METRIC = "agent-steps/sec, 4096-colloid WCA+vision-cone rollout @1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# MI355X_MICROARCH.md: a wave issues a VALU instruction over 2 cycles; 1024
-# SIMDs at 2.4 GHz -> 1.2288e12 VALU wave-instructions/s (= the 157.3 TF f32
-# vector peak / (64 lanes x 2 flop))
-VALU_PEAK_WAVE_INSTS = 1024 * 2.4e9 / 2
+# VALU issue roofline (MI355X_MICROARCH.md:489, 'vector-instruction ISSUE
+# cost'): one wave's stream issues v_fma/v_add-class instructions at 4 cycles
+# and transcendentals (v_exp/log/rcp/rsq/sqrt/sin/cos) at 8 on its SIMD;
+# 1024 SIMDs at 2.4 GHz.  (The 2-cycle rate of line 473 needs two waves
+# issuing on a SIMD; it is the 157.3 TF f32 vector peak.)
+SIMD_CLOCKS_PER_S = 1024 * 2.4e9
+VALU_CYCLES, TRANS_CYCLES = 4, 8
+VALU_PEAK_WAVE_INSTS = SIMD_CLOCKS_PER_S / VALU_CYCLES
+F32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: F32 row (= vector peak)
 BYTES_PER_PARTICLE_SUBSTEP = 40
+PPO_MAC_PER_SAMPLE = 2944        # DESIGN.md section 6 "PPO update" (3-128-(4+1) MLP)
+# the lines one bench.py run can measure (--only): see main()
+LINES = ("head", "batched", "c2", "c4", "c5", "c3train", "dims3", "dense2d")
+
+
+def source_sha() -> str:
+    """Hash of the HIP sources and the C-ABI header the library is built from:
+    profiles/<tag>_traffic.json rows carry it, so a kernel change is not
+    reported with stale counter numbers."""
+    import glob
+    import hashlib
+
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "swarmrl_amd", "csrc", "*")) +
+                   glob.glob(os.path.join(ROOT, "include", "*.h")))
+    for path in files:
+        h.update(os.path.basename(path).encode())
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:12]
 
 
 def parse_args():
@@ -63,6 +88,16 @@ def parse_args():
     ap.add_argument("--dims3", type=int, default=1,
                     help="3-D at scale line ('dims3': BD+WCA slices of --colloids colloids in a "
                          "periodic 3-D box on the cluster path vs the 3-D global path; 0: off)")
+    ap.add_argument("--only", default="all",
+                    help="comma-separated lines to measure (" + ", ".join(LINES) + "; default all): "
+                         "config-pure runs for profiles/profile_round.sh")
+    ap.add_argument("--c2-colloids", type=int, default=1024,
+                    help="BASELINE config 2 line ('c2': vision cone + random MLP, one env)")
+    ap.add_argument("--c4-envs", type=int, default=8,
+                    help="BASELINE config 4 per-rank shard ('c4': envs per GPU of 64 x 1024)")
+    ap.add_argument("--c4-colloids", type=int, default=1024)
+    ap.add_argument("--train-episodes", type=int, default=4,
+                    help="timed episodes of the 'c3train' line (rollout + PPO update)")
     ap.add_argument("--stub", action="store_true",
                     help="CPU plumbing test: no GPU, gloo, synthetic trajectories")
     return ap.parse_args()
@@ -112,7 +147,15 @@ def build_workload(args, env_seed, device):
     return eng, ff, agent
 
 
-def build_c5_workload(args, env_seed, device):
+def build_c3_workload(args, env_seed, device):
+    """BASELINE config 3: the find-centre task of the reference's PPO test
+    (test_rl_trainers.py:105-118): ConcentrationField
+    observable (scale 10000) + GradientSensing reward (scale 10), f(d) = 1 - d,
+    source at the box centre, MLP 1-128-(4+1), PPO defaults."""
+    return build_c5_workload(args, env_seed, device, rnd=False)
+
+
+def build_c5_workload(args, env_seed, device, rnd=True):
     """BASELINE config 5: 16384 colloids, concentration-field chemotaxis +
     intrinsic reward: ConcentrationField observable (scale
     10000) + GradientSensing task (scale 10), f(d) = 1 - d, source at the box
@@ -151,7 +194,7 @@ def build_c5_workload(args, env_seed, device):
     task = GradientSensing(source=src, decay_function=lambda d: 1 - d, box_length=box,
                            reward_scale_factor=10)
     torch.manual_seed(env_seed)
-    rnd = RNDReward(RNDConfig(input_shape=(1,), device=device))
+    intrinsic = RNDReward(RNDConfig(input_shape=(1,), device=device)) if rnd else None
     net = TorchModel(ActorCriticMLP(1, 4, 128), input_shape=(1,), device=device)
     actions = {
         "RotateClockwise": Action(torque=np.array([0.0, 0.0, 10.0])),
@@ -159,7 +202,7 @@ def build_c5_workload(args, env_seed, device):
         "RotateCounterClockwise": Action(torque=np.array([0.0, 0.0, -10.0])),
         "DoNothing": Action(),
     }
-    agent = ActorCriticAgent(0, net, task, obs, actions, train=True, intrinsic_reward=rnd)
+    agent = ActorCriticAgent(0, net, task, obs, actions, train=True, intrinsic_reward=intrinsic)
     ff = ForceFunction({"0": agent})
     agent.reset_agent(eng.colloids)
     return eng, ff, agent
@@ -290,26 +333,134 @@ def time_run_kernel(eng, reps):
     return ms.value / cnt.value, name
 
 
-def pmc_traffic(kernel_re, E, N):
-    """Per-launch HBM bytes and VALU wave-instructions of the dominant kernel
-    from the newest committed rocprofv3 PMC summary (profiles/<tag>_traffic.json:
-    separate FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU passes, FETCH_SIZE x2 per
-    MI355X_MICROARCH.md), when it was collected on this workload."""
+def time_ppo_grads(agent, traj, line, reps):
+    """Roofline of the PPO update's dominant kernel, k_ppo_grads (the caller
+    side of the rollout): `reps` eager epochs of the
+    episode `traj` with HIP events around every k_ppo_grads launch
+    (swarm_ppo_profile), useful work = PPO_MAC_PER_SAMPLE multiply-adds per
+    sample per epoch against the f32 vector peak."""
+    import ctypes
+
+    import torch
+
+    from swarmrl_amd import _capi
+
+    lib = _capi.lib()
+    ms, cnt = ctypes.c_double(), ctypes.c_int32()
+    loss = agent.loss
+    epochs = loss.n_epochs
+    prev = os.environ.get("SWARMRL_AMD_PPO_GRAPH")
+    os.environ["SWARMRL_AMD_PPO_GRAPH"] = "0"  # eager epochs: events around each launch
+    try:
+        torch.cuda.synchronize()
+        lib.swarm_ppo_profile(1, ctypes.byref(ms), ctypes.byref(cnt))
+        loss.n_epochs = max(1, reps)
+        loss.compute_loss(network=agent.network, episode_data=traj)
+        lib.swarm_ppo_profile(0, ctypes.byref(ms), ctypes.byref(cnt))
+    finally:
+        loss.n_epochs = epochs
+        if prev is None:
+            del os.environ["SWARMRL_AMD_PPO_GRAPH"]
+        else:
+            os.environ["SWARMRL_AMD_PPO_GRAPH"] = prev
+    if cnt.value == 0:
+        return None  # not the fused path (another network or sampling strategy)
+    kernel_ms = ms.value / cnt.value
+    samples = len(traj.actions) * int(traj.actions[0].numel())
+    tflops = 2.0 * PPO_MAC_PER_SAMPLE * samples / (kernel_ms * 1e-3) / 1e12
+    out = {"bound": "valu", "kernel": "k_ppo_grads (one PPO epoch's gradient)",
+           "achieved": tflops, "peak": F32_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
+           "frac": tflops / F32_VECTOR_PEAK_TFLOPS, "kernel_ms": kernel_ms,
+           "samples_per_launch": samples,
+           "algorithmic_flops": f"2 x {PPO_MAC_PER_SAMPLE} per sample (DESIGN.md 6) x {samples}"}
+    row = profile_row(line, r"k_ppo_grads")
+    if row:
+        out["profile"] = {"source": row["source"], "src_sha": row.get("src_sha"),
+                          "stale": bool(row.get("stale")),
+                          "rocprof_mean_ms": row.get("mean_duration_us", 0.0) * 1e-3 or None,
+                          "traffic": row.get("bytes_per_launch")}
+    return out
+
+
+def _round_key(path):
+    """profiles/r<round><letter>_<line>_traffic.json -> sortable (round, letter)."""
+    m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+    return (int(m.group(1)), m.group(2)) if m else (-1, "")
+
+
+def profile_row(line, kernel_re):
+    """The counter row of `line`'s dominant kernel from the newest committed
+    config-pure profile (profiles/r*_traffic.json, tools/summarize_profiles.py):
+    per-launch HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md
+    gfx950 correction), VALU and transcendental wave-instructions, and the
+    rocprofv3 mean duration.  A row of other sources than the ones built here
+    is returned flagged stale."""
     import glob
 
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")), reverse=True)
-    for path in paths:  # the newest round's summary first (r2b > r2a > r1)
+    sha = source_sha()
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")), key=_round_key,
+                   reverse=True)
+    fallback = None
+    for path in paths:
         try:
             with open(path) as f:
                 rows = json.load(f)
         except (OSError, ValueError):
             continue
         for r in rows:
-            if re.search(kernel_re, r.get("kernel", "")) and r.get("envs") == E and \
-                    r.get("colloids") == N:
-                return (float(r["bytes_per_launch"]), r.get("valu_insts_per_launch"),
-                        f"profiles/{r['source']}")
-    return None, None, None
+            if r.get("line") != line or not re.search(kernel_re, r.get("kernel", "")):
+                continue
+            r = dict(r, source=f"profiles/{os.path.basename(path)}")
+            if r.get("src_sha") == sha:
+                return r
+            if fallback is None:
+                fallback = dict(r, stale=True)
+    return fallback
+
+
+def make_roofline(line, kernel_re, kernel, kernel_ms, units, bytes_per_unit, unit_desc):
+    """HBM roofline of one line's dominant kernel: algorithmic bytes per
+    launch (SURVEY 8(d)'s per-unit figure x the units of one launch) over the
+    live HIP-event launch duration, the counter traffic of the same kernel
+    from its config-pure profile, and the VALU issue roofline from the
+    profile's instruction counts."""
+    bytes_per_launch = bytes_per_unit * units
+    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    row = profile_row(line, kernel_re)
+    out = {
+        "bound": "hbm",
+        "kernel": kernel,
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "traffic": row["bytes_per_launch"] if row else None,
+        "kernel_ms": kernel_ms,
+        "bytes_per_launch": bytes_per_launch,
+        "algorithmic_bytes": f"{bytes_per_unit} B per {unit_desc} (SURVEY 8d) x {units}",
+    }
+    if row:
+        out["profile"] = {"source": row["source"], "src_sha": row.get("src_sha"),
+                          "stale": bool(row.get("stale")),
+                          "rocprof_mean_ms": row.get("mean_duration_us", 0.0) * 1e-3 or None,
+                          "launches": row.get("dispatches")}
+        valu, trans = row.get("valu_insts_per_launch"), row.get("valu_trans_per_launch")
+        if valu:
+            # issue cycles the launch needs on its SIMDs over the cycles the
+            # chip offers in the measured duration
+            cycles = VALU_CYCLES * (valu - (trans or 0.0)) + TRANS_CYCLES * (trans or 0.0)
+            out["valu"] = {
+                "achieved": valu / (kernel_ms * 1e-3),
+                "peak": VALU_PEAK_WAVE_INSTS,
+                "unit": "VALU wave-instructions/s",
+                "frac": cycles / (SIMD_CLOCKS_PER_S * kernel_ms * 1e-3),
+                "issue_model": f"{VALU_CYCLES} cycles per VALU, {TRANS_CYCLES} per transcendental "
+                               f"wave-instruction (MI355X_MICROARCH.md:489)"
+                               + ("" if trans is not None else "; transcendentals not counted"),
+                "insts_per_launch": valu,
+                "trans_per_launch": trans,
+            }
+    return out
 
 
 def _cpu_env(N, slices, seed, threads=1, cells=True):
@@ -454,9 +605,12 @@ def cpu_baseline_all_cores(args):
     }
 
 
-def measure(args, E, rank, world, device, builder=None, colloids=None):
+def measure(args, E, rank, world, device, builder=None, colloids=None, line="head",
+            train=False):
     """Build, capture and time one workload of E envs per GPU; returns the
-    timing and roofline numbers (all ranks)."""
+    timing and roofline numbers (all ranks).  train: each episode is also
+    followed by the agent's PPO update (ProximalPolicyLoss.compute_loss,
+    proximal_policy_loss.py:140-170) inside the timed region."""
     import torch
     import torch.distributed as dist
 
@@ -505,12 +659,16 @@ def measure(args, E, rank, world, device, builder=None, colloids=None):
 
     gstats = []
 
+    traj = agent.trajectory  # the episode graph's output tensors
+
     def run(n_steps, timed):
         k = 0
         while k < n_steps:
             if episode_graph is not None and n_steps - k >= T:
                 episode_graph.replay()
                 k += T
+                if train:  # the update of the episode the graph recorded
+                    agent.loss.compute_loss(network=agent.network, episode_data=traj)
                 # trajectory entries the device has published so far (the
                 # ring is filled by the replayed graph; no host wait)
                 eng.drain_trajectory(block=False)
@@ -547,44 +705,23 @@ def measure(args, E, rank, world, device, builder=None, colloids=None):
     kernel_ms, kernel = time_run_kernel(eng, args.bd_reps)
     N = args.colloids
     sub = eng.params.steps_per_slice
-    bytes_per_launch = BYTES_PER_PARTICLE_SUBSTEP * N * sub * E
-    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-    # the 2-D run kernels (not k_cluster_run3 of the dims3 line)
-    traffic, valu, traffic_src = pmc_traffic(r"k_cluster_run(_wide)?<", E, N)
     out = dict(timing)
     out.update({
         "hip_graph": episode_graph is not None,
         "trajectory": {"write_interval_s": args.write_interval, "entries_recorded": traj_written,
                        "recorder": "device ring (swarm_engine_traj_record) inside the graph"
                        if eng._ring is not None else "host"},
-        "roofline": {
-            "bound": "hbm",
-            "kernel": kernel,
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "kernel_ms": kernel_ms,
-            "bytes_per_launch": bytes_per_launch,
-            "algorithmic_bytes": f"{BYTES_PER_PARTICLE_SUBSTEP} B per colloid-sub-step "
-                                 f"(SURVEY 8d) x {N} colloids x {sub} sub-steps x {E} env(s)",
-        },
+        # the 2-D run kernels (not k_cluster_run3 of the dims3 line)
+        "roofline": make_roofline(line, r"k_cluster_run(_wide)?<", kernel, kernel_ms,
+                                  N * sub * E, BYTES_PER_PARTICLE_SUBSTEP,
+                                  f"colloid-sub-step; {N} colloids x {sub} sub-steps x {E} env(s)"),
+        "src_sha": source_sha(),
     })
-    if traffic_src:
-        out["roofline"]["traffic_source"] = traffic_src
+    valu = out["roofline"].get("valu")
     if valu:
-        # the bound that binds (SURVEY 8d asks for HBM; the fused kernel keeps
-        # its state in registers, so VALU issue is what it runs into)
-        out["roofline"]["valu"] = {
-            "achieved": valu / (kernel_ms * 1e-3),
-            "peak": VALU_PEAK_WAVE_INSTS,
-            "unit": "VALU wave-instructions/s",
-            "frac": valu / (kernel_ms * 1e-3) / VALU_PEAK_WAVE_INSTS,
-            "insts_per_launch": valu,
-            "lane_insts_per_colloid_substep": valu * 64 / (N * sub * E),
-            "source": traffic_src,
-        }
+        valu["lane_insts_per_colloid_substep"] = valu["insts_per_launch"] * 64 / (N * sub * E)
+    if train:
+        out["roofline_update"] = time_ppo_grads(agent, traj, line, args.bd_reps)
     del eng, ff, agent, slice_graph, episode_graph
     torch.cuda.synchronize()
     return out
@@ -682,8 +819,80 @@ def _finish_timing(args, E, world, device, elapsed, gstats, kernel_ms, kernel, s
     return out
 
 
+def _sub_line(res, workload, extra=None):
+    """A sub-line of the JSON record from a measure() result."""
+    out = {"workload": workload, "value": res["value"], "unit": "agent-steps/s",
+           "envs_per_gpu": res["E"], "ms_per_step": res["ms_per_step"],
+           "per_rank_value": res["per_rank"], "roofline": res["roofline"]}
+    for k in ("gather", "roofline_update"):
+        if res.get(k) is not None:
+            out[k] = res[k]
+    out.update(extra or {})
+    return out
+
+
+def run_lines(args, lines, rank, world, device):
+    """Measure the selected lines; returns {line: record}."""
+    res = {}
+    if "head" in lines:
+        res["head"] = measure(args, args.envs_per_gpu, rank, world, device, line="head")
+    if "batched" in lines and args.batched_envs > 0:
+        r = measure(args, args.batched_envs, rank, world, device, line="batched")
+        res["batched"] = _sub_line(r, f"{args.batched_envs} envs x {args.colloids} colloids per "
+                                      f"GPU batched per launch, the headline's slice")
+    if "c2" in lines and args.c2_colloids > 0:
+        r = measure(args, 1, rank, world, device, colloids=args.c2_colloids, line="c2")
+        res["c2"] = _sub_line(r, f"BASELINE config 2: {args.c2_colloids} colloids, WCA + "
+                                 f"vision-cone observable, random-init MLP policy, one env per GPU")
+    if "c4" in lines and args.c4_envs > 0:
+        r = measure(args, args.c4_envs, rank, world, device, colloids=args.c4_colloids, line="c4")
+        res["c4"] = _sub_line(r, f"BASELINE config 4 per-rank shard: {args.c4_envs} envs x "
+                                 f"{args.c4_colloids} colloids per GPU (64 x {args.c4_colloids} "
+                                 f"over 8 GPUs), vision cone + MLP, trajectory all-gather per "
+                                 f"episode when world > 1")
+    if "c5" in lines and args.c5_colloids > 0:
+        r = measure(args, 1, rank, world, device, builder=build_c5_workload,
+                    colloids=args.c5_colloids, line="c5")
+        res["c5"] = _sub_line(r, f"BASELINE config 5: {args.c5_colloids} colloids, "
+                                 f"ConcentrationField observable + GradientSensing reward + RND "
+                                 f"intrinsic reward, one env per GPU")
+    if "c3train" in lines and args.train_episodes > 0:
+        targs = argparse.Namespace(**vars(args))
+        T = args.episode_length
+        targs.steps = args.train_episodes * T
+        targs.warmup = max(args.warmup, 2 * T)  # eager first update, then the PPO graph capture
+        r = measure(targs, 1, rank, world, device, builder=build_c3_workload, colloids=4096,
+                    line="c3train", train=True)
+        res["c3train"] = _sub_line(r, "BASELINE config 3: 4096 colloids, find-centre task "
+                                      "(ConcentrationField + GradientSensing), actor-critic PPO "
+                                      "training: each 20-slice episode's rollout and its PPO "
+                                      "update (20 epochs, fused gradient kernels + Adam) timed "
+                                      "together", {"episodes": args.train_episodes})
+    if world == 1:
+        for key, dims, frac, desc in (
+                ("dims3", 3, 0.04, "3-D at scale: {N} colloids per env, periodic box at volume "
+                                   "fraction 0.04, BD+WCA slices of 100 sub-steps (engine only)"),
+                ("dense2d", 2, 0.3, "dense 2-D: {N} colloids per env at area fraction 0.3 "
+                                    "(placed in the centred disc), BD+WCA slices of 100 "
+                                    "sub-steps (engine only); the rc + skin graph percolates")):
+            if key in lines and args.dims3:
+                res[key] = {
+                    "workload": desc.format(N=args.colloids),
+                    "E1": measure_dims3(args, 1, 50, global_reps=3, dims=dims, fraction=frac),
+                    f"E{args.batched_envs}": measure_dims3(args, max(args.batched_envs, 1), 20,
+                                                           global_reps=2, dims=dims,
+                                                           fraction=frac),
+                }
+    return res
+
+
 def main():
     args = parse_args()
+    lines = LINES if args.only == "all" else tuple(x.strip() for x in args.only.split(","))
+    bad = [x for x in lines if x not in LINES]
+    if bad:
+        print(f"bench.py: unknown line(s) {bad}; choose from {LINES}", file=sys.stderr)
+        sys.exit(2)
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
         sys.exit(launch_ranks(args))
@@ -703,50 +912,26 @@ def main():
         head = stub_measure(args, args.envs_per_gpu, rank, world, device)
         head["roofline"] = None
         head["hip_graph"] = False
-        batched = None
+        res = {"head": head}
     else:
         if world > 1:
             dist.init_process_group("nccl", init_method="env://")
         torch.cuda.set_device(local_rank)
         device = torch.device("cuda", local_rank)
-        E = args.envs_per_gpu
-        head = measure(args, E, rank, world, device)
-        batched = None
-        if args.batched_envs > 0 and args.batched_envs != E:
-            batched = measure(args, args.batched_envs, rank, world, device)
-        if args.c5_colloids > 0:
-            c5 = measure(args, 1, rank, world, device, builder=build_c5_workload,
-                         colloids=args.c5_colloids)
-            head["c5"] = {
-                "workload": f"BASELINE config 5: {args.c5_colloids} colloids, ConcentrationField "
-                            f"observable + GradientSensing reward + RND intrinsic reward, "
-                            f"one env per GPU",
-                "value": c5["value"],
-                "unit": "agent-steps/s",
-                "ms_per_step": c5["ms_per_step"],
-                "per_rank_value": c5["per_rank"],
-                "roofline": c5["roofline"],
-            }
-        if args.dims3 and world == 1:
-            head["dims3"] = {
-                "workload": f"3-D at scale: {args.colloids} colloids per env, periodic box at "
-                            f"volume fraction 0.04, BD+WCA slices of 100 sub-steps (engine only)",
-                "E1": measure_dims3(args, 1, 50, global_reps=3),
-                f"E{args.batched_envs}": measure_dims3(args, max(args.batched_envs, 1), 20,
-                                                       global_reps=2),
-            }
-            head["dense2d"] = {
-                "workload": f"dense 2-D: {args.colloids} colloids per env at area fraction 0.3 "
-                            f"(placed in the centred disc), BD+WCA slices of 100 sub-steps "
-                            f"(engine only); the rc + skin graph percolates",
-                "E1": measure_dims3(args, 1, 50, global_reps=3, dims=2, fraction=0.3),
-                f"E{args.batched_envs}": measure_dims3(args, max(args.batched_envs, 1), 20,
-                                                       global_reps=2, dims=2, fraction=0.3),
-            }
+        res = run_lines(args, lines, rank, world, device)
     if world > 1 and dist.get_world_size() != args.gpus:
         print("bench.py: process group size differs from --gpus", file=sys.stderr)
         sys.exit(2)
     N = args.colloids
+    head = res.get("head")
+    if head is None:  # a config-pure run of other lines: the first one heads the record
+        name = next((k for k in lines if "value" in res.get(k, {})), None)
+        rec = res.pop(name) if name else {"value": None, "ms_per_step": None, "roofline": None}
+        head = dict(rec, E=rec.get("envs_per_gpu"), per_rank=rec.get("per_rank_value"))
+        workload = f"{name}: {rec.get('workload')}"
+    else:
+        res.pop("head")
+        workload = "4096-colloid WCA+vision-cone rollout"
     line = {
         "metric": METRIC,
         "value": head["value"],
@@ -761,38 +946,28 @@ def main():
         "dtype": "f32 (uint32 fixed-point positions)",
         "data": "synthetic: seeded disc placement (area fraction 0.1), random-init actor-critic",
         "config": {
-            "workload": "4096-colloid WCA+vision-cone rollout",
+            "workload": workload,
             "colloids_per_env": N,
-            "envs_per_gpu": head["E"],
+            "envs_per_gpu": head.get("E"),
             "substeps_per_slice": 100,
             "episode_length": args.episode_length,
             "policy": "MLP 3-128-(4+1), Gumbel sampling",
             "task": "GradientSensing (find centre)",
             "parallelism": f"episode-parallel, {world} process(es), one env per GPU, "
                            f"one packed all-gather of the trajectory per episode",
-            "hip_graph": head["hip_graph"],
+            "hip_graph": head.get("hip_graph"),
             "trajectory": head.get("trajectory"),
         },
         "world": world,
-        "per_rank_value": head["per_rank"],
+        "per_rank_value": head.get("per_rank"),
         "roofline": head["roofline"],
+        "src_sha": source_sha(),
     }
     if "gather" in head:
         line["gather"] = head["gather"]
-    for k in ("c5", "dims3", "dense2d"):
-        if k in head:
-            line[k] = head[k]
-    if batched is not None:
-        line["batched"] = {
-            "envs_per_gpu": batched["E"],
-            "value": batched["value"],
-            "unit": "agent-steps/s",
-            "ms_per_step": batched["ms_per_step"],
-            "per_rank_value": batched["per_rank"],
-            "roofline": batched["roofline"],
-        }
-        if "gather" in batched:
-            line["batched"]["gather"] = batched["gather"]
+    for k in LINES:
+        if k in res:
+            line[k] = res[k]
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.stub:
         line["cpu_baseline"] = cpu_baseline(args)
         if args.cpu_all_core_slices > 0:

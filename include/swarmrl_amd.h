@@ -364,6 +364,13 @@ int swarm_policy_mlp_sample(const float *obs, int32_t n, int32_t d_in, const flo
                             int64_t *out_idx, float *out_logp, float *out_f, float *out_t,
                             float *out_logits, void *stream);
 
+/* Kernel timing for measurement (bench.py's roofline of the PPO update):
+ * the summed duration (ms) and count of the k_ppo_grads launches this
+ * thread made through swarm_ppo_epoch_grad since the previous call (HIP
+ * events on the caller's stream; waits for them), then enables (1) or
+ * disables (0) recording.  Not for use under graph capture. */
+int swarm_ppo_profile(int32_t enable, double *grads_ms, int32_t *launches);
+
 /* The gradient of one PPO epoch -- ProximalPolicyLoss._calculate_loss
  * differentiated by jax.value_and_grad (swarmrl/losses/
  * proximal_policy_loss.py:62-138, :160-168) with its GAE value function

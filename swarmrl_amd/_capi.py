@@ -150,6 +150,7 @@ _SIGNATURES = {
          _P, _P, ctypes.c_int32, _P, _P, ctypes.c_float, ctypes.c_float, ctypes.c_float,
          ctypes.c_float, _P, ctypes.c_int64, _P, _P],
     ),
+    "swarm_ppo_profile": (ctypes.c_int, [ctypes.c_int32, _P, _P]),
     "swarm_engine_step_count": (ctypes.c_int64, [_P]),
     "swarm_rnd_distance": (
         ctypes.c_int,

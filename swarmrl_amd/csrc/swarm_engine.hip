@@ -2246,6 +2246,33 @@ int64_t swarm_ppo_workspace_bytes(int32_t T, int32_t S, int32_t d_in, int32_t hi
   return (int64_t)ppo_workspace((long)T * S, S, d_in, hidden, k).total;
 }
 
+// swarm_ppo_profile: HIP events around every k_ppo_grads launch of this
+// thread (bench.py's roofline of the update); not under graph capture.
+namespace {
+struct PpoProfile {
+  bool on = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+};
+thread_local PpoProfile g_ppo_prof;
+}  // namespace
+
+int swarm_ppo_profile(int32_t enable, double* grads_ms, int32_t* launches) {
+  double total = 0.0;
+  for (auto& pr : g_ppo_prof.ev) {
+    float ms = 0.0f;
+    HIP_TRY(hipEventSynchronize(pr.second));
+    HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+    total += ms;
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  if (grads_ms) *grads_ms = total;
+  if (launches) *launches = (int32_t)g_ppo_prof.ev.size();
+  g_ppo_prof.ev.clear();
+  g_ppo_prof.on = enable != 0;
+  return SWARM_OK;
+}
+
 int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
                          const int64_t* actions, const float* old_logp, const float* rewards,
                          const float* w1, const float* b1, int32_t hidden, const float* wa,
@@ -2302,11 +2329,19 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
     const int lds = swarm::ppo_grads_lds_floats<NN, KK>() * (int)sizeof(float);               \
     if (lds > 65536)                                                                          \
       (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);         \
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;                                                 \
+    if (g_ppo_prof.on && hipEventCreate(&ev0) == hipSuccess &&                                \
+        hipEventCreate(&ev1) == hipSuccess)                                                   \
+      (void)hipEventRecord(ev0, s);                                                           \
     hipLaunchKernelGGL((swarm::k_ppo_grads<NN, DD, KK>), dim3((unsigned)blocks),             \
                        dim3(64 * NN),                                                         \
                        (size_t)lds, s, x, n, d_in, w1, b1, hidden, wa, ba, k, wc, bc,         \
                        actions, old_logp, adv, dv, spart, gae_blocks, table, clip_eps,        \
                        entropy_coef, partial);                                                \
+    if (ev1) {                                                                                \
+      (void)hipEventRecord(ev1, s);                                                           \
+      g_ppo_prof.ev.emplace_back(ev0, ev1);                                                   \
+    }                                                                                         \
   } while (0)
 #define SWARM_PPO_H(NN)                          \
   do {                                           \
