@@ -301,6 +301,36 @@ def measure_dims3(args, E, reps, global_reps=0, dims=3, fraction=0.04):
     return out
 
 
+def graph_kernel_ms(eng):
+    """Mean duration (ms) of the run-kernel launches of the last episode-graph
+    replay: the engine's HIP events were recorded into the graph at capture
+    (swarm_engine_profile 1 ... 2), so each replay re-records them."""
+    import ctypes
+
+    ms, cnt = ctypes.c_double(), ctypes.c_int32()
+    try:
+        eng._native.call("swarm_engine_profile", 0, ctypes.byref(ms), ctypes.byref(cnt))
+    except RuntimeError as err:  # the runtime cannot time graph-recorded events
+        print(f"bench.py: graph-captured run-kernel events unreadable ({err}); "
+              f"eager timing only", file=sys.stderr)
+        return None
+    return ms.value / cnt.value if cnt.value else None
+
+
+def graph_ppo_ms():
+    """Mean duration (ms) of k_ppo_grads in the last replay of the PPO epochs
+    graph (swarm_ppo_profile events recorded at its capture)."""
+    import ctypes
+
+    from swarmrl_amd import _capi
+
+    ms, cnt = ctypes.c_double(), ctypes.c_int32()
+    rc = _capi.lib().swarm_ppo_profile(0, ctypes.byref(ms), ctypes.byref(cnt))
+    if rc != 0 or cnt.value == 0:
+        return None
+    return ms.value / cnt.value
+
+
 def time_run_kernel(eng, reps):
     """Average duration (ms) of k_cluster_run, the dominant kernel: HIP events
     recorded by the engine around each launch on the stream it runs on
@@ -333,7 +363,7 @@ def time_run_kernel(eng, reps):
     return ms.value / cnt.value, name
 
 
-def time_ppo_grads(agent, traj, line, reps):
+def time_ppo_grads(agent, traj, line, reps, graph_ms=None):
     """Roofline of the PPO update's dominant kernel, k_ppo_grads (the caller
     side of the rollout): `reps` eager epochs of the
     episode `traj` with HIP events around every k_ppo_grads launch
@@ -365,19 +395,24 @@ def time_ppo_grads(agent, traj, line, reps):
             os.environ["SWARMRL_AMD_PPO_GRAPH"] = prev
     if cnt.value == 0:
         return None  # not the fused path (another network or sampling strategy)
-    kernel_ms = ms.value / cnt.value
+    eager_ms = ms.value / cnt.value
+    kernel_ms = graph_ms or eager_ms
     samples = len(traj.actions) * int(traj.actions[0].numel())
     tflops = 2.0 * PPO_MAC_PER_SAMPLE * samples / (kernel_ms * 1e-3) / 1e12
     out = {"bound": "valu", "kernel": "k_ppo_grads (one PPO epoch's gradient)",
            "achieved": tflops, "peak": F32_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
            "frac": tflops / F32_VECTOR_PEAK_TFLOPS, "kernel_ms": kernel_ms,
+           "kernel_ms_eager": eager_ms,
+           "kernel_timing": "HIP events captured into the PPO epochs graph, last replay" if graph_ms
+                            else "HIP events around eager epochs",
            "samples_per_launch": samples,
            "algorithmic_flops": f"2 x {PPO_MAC_PER_SAMPLE} per sample (DESIGN.md 6) x {samples}"}
     row = profile_row(line, r"k_ppo_grads")
     if row:
         out["profile"] = {"source": row["source"], "src_sha": row.get("src_sha"),
                           "stale": bool(row.get("stale")),
-                          "rocprof_mean_ms": row.get("mean_duration_us", 0.0) * 1e-3 or None,
+                          "rocprof_mean_ms": (row.get("mean_duration_graph_us") or
+                                              row.get("mean_duration_us") or 0.0) * 1e-3 or None,
                           "traffic": row.get("bytes_per_launch")}
     return out
 
@@ -442,7 +477,8 @@ def make_roofline(line, kernel_re, kernel, kernel_ms, units, bytes_per_unit, uni
     if row:
         out["profile"] = {"source": row["source"], "src_sha": row.get("src_sha"),
                           "stale": bool(row.get("stale")),
-                          "rocprof_mean_ms": row.get("mean_duration_us", 0.0) * 1e-3 or None,
+                          "rocprof_mean_ms": (row.get("mean_duration_graph_us") or
+                                              row.get("mean_duration_us") or 0.0) * 1e-3 or None,
                           "launches": row.get("dispatches")}
         valu, trans = row.get("valu_insts_per_launch"), row.get("valu_trans_per_launch")
         if valu:
@@ -650,16 +686,30 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
             one_slice()
         agent.reset_trajectory()
         episode_graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(episode_graph, pool=slice_graph.pool()):
-            # one episode as the trainers run it (episodic_trainer.py:35 ->
-            # engine.integrate(episode_length, force_fn))
-            eng.integrate(T, ff)
+        # HIP events around every run-kernel launch of the episode become graph
+        # nodes: after the timed replays they time the last replay's launches
+        # (the kernel as it runs in the workload; read by graph_kernel_ms)
+        eng._native.call("swarm_engine_profile", 1, None, None)
+        try:
+            with torch.cuda.graph(episode_graph, pool=slice_graph.pool()):
+                # one episode as the trainers run it (episodic_trainer.py:35 ->
+                # engine.integrate(episode_length, force_fn))
+                eng.integrate(T, ff)
+        finally:
+            eng._native.call("swarm_engine_profile", 2, None, None)
     else:
         agent.reset_trajectory()
 
     gstats = []
 
     traj = agent.trajectory  # the episode graph's output tensors
+    if train and episode_graph is not None:
+        from swarmrl_amd import _capi
+
+        # events around the k_ppo_grads launches of the PPO graph's capture
+        # (the epochs replay as one graph from the second episode on)
+        lib = _capi.lib()
+        agent.loss.capture_hook = lambda on: lib.swarm_ppo_profile(1 if on else 2, None, None)
 
     def run(n_steps, timed):
         k = 0
@@ -702,7 +752,10 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
 
     eng.drain_trajectory(block=True)
     traj_written = eng.h5_time_steps_written + len(eng.traj_holder["Times"])
-    kernel_ms, kernel = time_run_kernel(eng, args.bd_reps)
+    graph_ms = graph_kernel_ms(eng) if episode_graph is not None else None
+    update_graph_ms = graph_ppo_ms() if train and episode_graph is not None else None
+    eager_ms, kernel = time_run_kernel(eng, args.bd_reps)
+    kernel_ms = graph_ms or eager_ms
     N = args.colloids
     sub = eng.params.steps_per_slice
     out = dict(timing)
@@ -717,11 +770,16 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
                                   f"colloid-sub-step; {N} colloids x {sub} sub-steps x {E} env(s)"),
         "src_sha": source_sha(),
     })
+    out["roofline"]["kernel_timing"] = (
+        "HIP events around each launch, captured into the episode graph: mean over the last "
+        f"replay's launches; eager launches {eager_ms * 1e3:.1f} us" if graph_ms else
+        "HIP events around each of the eager launches")
+    out["roofline"]["kernel_ms_eager"] = eager_ms
     valu = out["roofline"].get("valu")
     if valu:
         valu["lane_insts_per_colloid_substep"] = valu["insts_per_launch"] * 64 / (N * sub * E)
     if train:
-        out["roofline_update"] = time_ppo_grads(agent, traj, line, args.bd_reps)
+        out["roofline_update"] = time_ppo_grads(agent, traj, line, args.bd_reps, update_graph_ms)
     del eng, ff, agent, slice_graph, episode_graph
     torch.cuda.synchronize()
     return out

@@ -239,7 +239,11 @@ int swarm_engine_window_stats(swarm_engine_t *e, int32_t *fallback,
 /* Kernel timing for measurement (bench.py roofline): returns the summed
  * duration (ms) and count of the k_cluster_run launches recorded since the
  * previous call (HIP events on the engine stream; waits for them), then
- * enables (1) or disables (0) recording.  Not for use under graph capture. */
+ * enables (1) or disables (0) recording.  Recording may be on while a graph
+ * is captured: the event records become graph nodes, so after replays the
+ * pairs time the LAST replay's launches.  enable = 2 pauses recording and
+ * keeps the recorded pairs unread (end of a capture; read them later with
+ * 0 or 1). */
 int swarm_engine_profile(swarm_engine_t *e, int32_t enable, double *run_ms,
                          int32_t *launches);
 
@@ -368,7 +372,9 @@ int swarm_policy_mlp_sample(const float *obs, int32_t n, int32_t d_in, const flo
  * the summed duration (ms) and count of the k_ppo_grads launches this
  * thread made through swarm_ppo_epoch_grad since the previous call (HIP
  * events on the caller's stream; waits for them), then enables (1) or
- * disables (0) recording.  Not for use under graph capture. */
+ * disables (0) recording; 2 pauses and keeps the pairs unread.  As for
+ * swarm_engine_profile, pairs recorded under graph capture time the last
+ * replay. */
 int swarm_ppo_profile(int32_t enable, double *grads_ms, int32_t *launches);
 
 /* The gradient of one PPO epoch -- ProximalPolicyLoss._calculate_loss

@@ -949,9 +949,9 @@ int launch_global(swarm_engine* e, int n_steps, int sd_mode, float g, float md) 
 // step counter.
 int launch_noise(swarm_engine* e, hipStream_t stream, int n) {
   const long M = (long)e->n_envs * e->n;
-  hipLaunchKernelGGL(swarm::k_noise, dim3((unsigned)((M + 255) / 256),
-                                         (unsigned)swarm::noise_groups(n)),
-                     dim3(256), 0, stream, e->d_derived, e->st, e->d_step, e->d_noise, n);
+  const long items = M * (long)swarm::noise_groups(n);
+  hipLaunchKernelGGL(swarm::k_noise, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, stream,
+                     e->d_derived, e->st, e->d_step, e->d_noise, n);
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
 }
@@ -1705,22 +1705,39 @@ int swarm_engine_integrate(swarm_engine_t* e, int32_t n_steps) {
   return run_bd(e, n_steps);
 }
 
-int swarm_engine_profile(swarm_engine_t* e, int32_t enable, double* run_ms, int32_t* launches) {
-  if (!e) return fail(SWARM_EINVAL, "null engine");
+namespace {
+// Sum the event pairs (all recorded launches have run), destroy them.
+int read_event_pairs(std::vector<std::pair<hipEvent_t, hipEvent_t>>& ev, double* total_ms,
+                     int32_t* count) {
   double total = 0.0;
-  for (auto& pr : e->prof_events) {
+  int rc = SWARM_OK;
+  for (auto& pr : ev) {
     float ms = 0.0f;
-    HIP_TRY(hipEventSynchronize(pr.second));
-    HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+    if (rc == SWARM_OK) {
+      hipError_t err = hipEventSynchronize(pr.second);
+      if (err == hipSuccess) err = hipEventElapsedTime(&ms, pr.first, pr.second);
+      if (err != hipSuccess) rc = fail(SWARM_EDEVICE, hipGetErrorString(err));
+    }
     total += ms;
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
   }
-  if (run_ms) *run_ms = total;
-  if (launches) *launches = (int32_t)e->prof_events.size();
-  e->prof_events.clear();
+  if (total_ms) *total_ms = total;
+  if (count) *count = (int32_t)ev.size();
+  ev.clear();
+  return rc;
+}
+}  // namespace
+
+int swarm_engine_profile(swarm_engine_t* e, int32_t enable, double* run_ms, int32_t* launches) {
+  if (!e) return fail(SWARM_EINVAL, "null engine");
+  if (enable == 2) {  // pause: keep the recorded pairs (e.g. captured into a graph) unread
+    e->profile = false;
+    return SWARM_OK;
+  }
+  const int rc = read_event_pairs(e->prof_events, run_ms, launches);
   e->profile = enable != 0;
-  return SWARM_OK;
+  return rc;
 }
 
 int swarm_engine_debug_phases(swarm_engine_t* e, uint64_t* out32) {
@@ -2257,20 +2274,13 @@ thread_local PpoProfile g_ppo_prof;
 }  // namespace
 
 int swarm_ppo_profile(int32_t enable, double* grads_ms, int32_t* launches) {
-  double total = 0.0;
-  for (auto& pr : g_ppo_prof.ev) {
-    float ms = 0.0f;
-    HIP_TRY(hipEventSynchronize(pr.second));
-    HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
-    total += ms;
-    (void)hipEventDestroy(pr.first);
-    (void)hipEventDestroy(pr.second);
+  if (enable == 2) {  // pause: keep the recorded pairs unread
+    g_ppo_prof.on = false;
+    return SWARM_OK;
   }
-  if (grads_ms) *grads_ms = total;
-  if (launches) *launches = (int32_t)g_ppo_prof.ev.size();
-  g_ppo_prof.ev.clear();
+  const int rc = read_event_pairs(g_ppo_prof.ev, grads_ms, launches);
   g_ppo_prof.on = enable != 0;
-  return SWARM_OK;
+  return rc;
 }
 
 int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,

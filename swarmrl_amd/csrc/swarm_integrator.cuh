@@ -1867,18 +1867,31 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // Noise table for latency-bound windows (few waves per SIMD): the normals of
-// every (sub-step, particle) computed ahead of the run,
-// table[(s * 3 + c) * M + e * N + i].  Indexed by particle, not wave slot,
-// so it does not wait for the cluster build.  Step-major on purpose: the
-// 3 x 4 B x M of one sub-step are read by every wave in the same few
-// microseconds, so 32 particles share a 128-B line and the lines stay hot in
-// L2 (each XCD's L2 fetches its own copy: rocprof FETCH ~ 8 x the table).
-// Particle-major layouts (one line per lane) measured 8-20 % slower.
+// every (sub-step, particle) computed ahead of the run.  Indexed by particle,
+// not wave slot, so it does not wait for the cluster build.
+// Particle-major (SWARM_NOISE_PMAJOR, the default): particle gi's sub-steps
+// are one contiguous run of 12-B records, table[(gi * kMaxWindow + s) * 3 +
+// c], so a lane reads its sub-step's three normals with one 12-B load and a
+// 128-B line (~10 sub-steps of one particle) is fetched by the one XCD that
+// runs the particle.  The step-major layout, table[(s * 3 + c) * M + gi],
+// shares each line among 32 particles spread over every XCD, so each XCD's
+// L2 fetched its own copy (rocprof FETCH ~ 7-8 x the table).
 // Two tables, by window parity: the wide run kernel fills the next window's
 // on otherwise idle CUs while it reads this one's.  The control block
 // records each table's first step and length; a run whose window does not
 // match its table draws the normals itself.
+#ifndef SWARM_NOISE_PMAJOR
+#define SWARM_NOISE_PMAJOR 1
+#endif
+constexpr bool kNoisePMajor = SWARM_NOISE_PMAJOR != 0;
 __host__ __device__ inline size_t noise_table_words(size_t M) { return (size_t)kMaxWindow * 3 * M; }
+// word of normal c of sub-step s of particle gi; the step and component strides
+__host__ __device__ inline size_t noise_index(size_t M, size_t gi, int s, int c) {
+  return kNoisePMajor ? (gi * kMaxWindow + (size_t)s) * 3 + (size_t)c
+                      : ((size_t)s * 3 + (size_t)c) * M + gi;
+}
+__host__ __device__ inline size_t noise_step_stride(size_t M) { return kNoisePMajor ? 3 : 3 * M; }
+__host__ __device__ inline size_t noise_comp_stride(size_t M) { return kNoisePMajor ? 1 : M; }
 
 // Group k of a table starting at step_start: sub-steps t = 4 (g0 + k) + j
 // (g0 = step_start / 4) of particle gi, those within [start, start + len).
@@ -1890,6 +1903,7 @@ __device__ __forceinline__ void noise_group(const Derived* __restrict__ d, const
   const int e = (int)(gi / st.n);
   const int i = (int)(gi - (long)e * st.n);
   const uint64_t t0 = (step_start & ~3ull) + 4ull * (uint64_t)k;
+  const size_t cs = noise_comp_stride((size_t)M);
   StepNoise sn;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -1897,11 +1911,25 @@ __device__ __forceinline__ void noise_group(const Derived* __restrict__ d, const
     sn.next(d->key0, d->key1 ^ (uint32_t)e, (uint32_t)i, t0 + (uint64_t)j, j == 0, g);
     const long s = (long)(t0 + (uint64_t)j) - (long)step_start;
     if (s >= 0 && s < len) {
-      float* o = table + (size_t)s * 3 * M + gi;
+      float* o = table + noise_index((size_t)M, (size_t)gi, (int)s, 0);
       o[0] = g[0];
-      o[M] = g[1];
-      o[2 * M] = g[2];
+      o[cs] = g[1];
+      o[2 * cs] = g[2];
     }
+  }
+}
+
+// Work item k of a table fill over M particles x G groups: particle-major
+// tables give consecutive items the consecutive groups of one particle (the
+// stores of a wave then cover contiguous records), step-major ones the same
+// group of consecutive particles.
+__device__ __forceinline__ void noise_item(long k, long M, int G, long* gi, int* grp) {
+  if (kNoisePMajor) {
+    *gi = k / G;
+    *grp = (int)(k - *gi * G);
+  } else {
+    *grp = (int)(k / M);
+    *gi = k - (long)*grp * M;
   }
 }
 
@@ -1915,13 +1943,17 @@ __global__ __launch_bounds__(256) void k_noise(const Derived* __restrict__ d, De
   const long M = st.m;
   const int par = window_parity(ctl);
   const uint64_t step0 = ctl[kCtlStep];
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     ctl[kCtlTStep + par] = step0;
     ctl[kCtlTLen + par] = (uint64_t)len;
   }
-  const long gi = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gi >= M) return;
-  noise_group(d, st, step0, len, tables + par * noise_table_words(M), gi, blockIdx.y);
+  const int G = noise_groups(len);
+  const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= M * G) return;
+  long gi;
+  int grp;
+  noise_item(k, M, G, &gi, &grp);
+  noise_group(d, st, step0, len, tables + par * noise_table_words(M), gi, grp);
 }
 
 // One wave of the cluster run: all n_steps sub-steps of the particles in
@@ -1994,8 +2026,8 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
   const uint32_t q0x = p.qx, q0y = p.qy;
   float dmax2 = 0.0f;
   float vx = 0.0f, vy = 0.0f, om = 0.0f;
-  const long ts = (long)M;
-  const float* tcol = table + gi;
+  const size_t tstep = noise_step_stride(M), ts = noise_comp_stride(M);
+  const float* tcol = kTable ? table + noise_index(M, gi, 0, 0) : nullptr;
   float gn[3] = {0.0f, 0.0f, 0.0f};
   StepNoise noise;  // !kTable: the window's normals drawn here, group by group
   if (kTable) {  // idle lanes read particle 0's (never stored)
@@ -2027,7 +2059,7 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
 #else
     if (kTable && !kLast) {  // the next sub-step's normals, one sub-step ahead
 #endif
-      const float* nx = tcol + (size_t)(s + 1) * 3 * ts;
+      const float* nx = tcol + (size_t)(s + 1) * tstep;
       gn[0] = nx[0];
       gn[1] = nx[ts];
       gn[2] = nx[2 * ts];
@@ -2252,10 +2284,13 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
       ctl[kCtlTLen + (par ^ 1)] = (uint64_t)kMaxWindow;
     }
     float* t = tables + (par ^ 1) * noise_table_words(M);
-    const long total = (long)noise_groups(kMaxWindow) * (long)M;
+    const int G = noise_groups(kMaxWindow);
+    const long total = (long)G * (long)M;
     for (long k = (long)b * blockDim.x + tid; k < total; k += (long)n_noise_blocks * blockDim.x) {
-      const int grp = (int)(k / (long)M);
-      noise_group(d, st, start, kMaxWindow, t, k - (long)grp * (long)M, grp);
+      long gi;
+      int grp;
+      noise_item(k, (long)M, G, &gi, &grp);
+      noise_group(d, st, start, kMaxWindow, t, gi, grp);
     }
     return;
   }

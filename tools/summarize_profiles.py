@@ -31,6 +31,7 @@ src = f"gpurun_out/prof_{tag}"
 dst = "profiles"
 DOMINANT = {"head": r"k_cluster_run", "batched": r"k_cluster_run", "c2": r"k_cluster_run",
             "c4": r"k_cluster_run", "c5": r"k_cluster_run", "c3train": r"k_cluster_run|k_ppo_grads"}
+EAGER_TAIL = 21  # bench.py --bd-reps 20 (+ the one window that precedes them)
 COUNTERS = ["FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "SQ_INSTS_VALU_TRANS_F32", "SQ_WAVES"]
 
 
@@ -51,7 +52,9 @@ for line in bench.LINES:
             with open(f"{dst}/{tag}_{line}_bench.json", "w") as f:
                 f.write(ln)
     dur = collections.defaultdict(list)
-    for r in csv.DictReader(open(f"{d}/trace/run_kernel_trace.csv")):
+    rows = sorted(csv.DictReader(open(f"{d}/trace/run_kernel_trace.csv")),
+                  key=lambda r: int(r["Start_Timestamp"]))
+    for r in rows:
         dur[short(r["Kernel_Name"])].append(
             (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3)  # ns -> us
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -71,6 +74,12 @@ for line in bench.LINES:
             traffic.append({
                 "line": line, "kernel": k, "dispatches": len(dur.get(k, [])),
                 "mean_duration_us": us,
+                # the launches of the captured graphs (the workload as timed):
+                # all but the EAGER_TAIL eager launches bench.py makes last
+                # (time_run_kernel: 1 + bd_reps windows; time_ppo_grads:
+                # bd_reps epochs)
+                "mean_duration_graph_us": (sum(dur[k][:-EAGER_TAIL]) / len(dur[k][:-EAGER_TAIL])
+                                           if len(dur.get(k, [])) > EAGER_TAIL else None),
                 "fetch_size_kb": mean["FETCH_SIZE"], "write_size_kb": mean["WRITE_SIZE"],
                 "bytes_per_launch": (2 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0,
                 "valu_insts_per_launch": mean["SQ_INSTS_VALU"],
