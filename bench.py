@@ -301,54 +301,29 @@ def measure_dims3(args, E, reps, global_reps=0, dims=3, fraction=0.04):
     return out
 
 
-def graph_kernel_ms(eng):
-    """Mean duration (ms) of the run-kernel launches of the last episode-graph
-    replay: the engine's HIP events were recorded into the graph at capture
-    (swarm_engine_profile 1 ... 2), so each replay re-records them."""
-    import ctypes
-
-    ms, cnt = ctypes.c_double(), ctypes.c_int32()
-    try:
-        eng._native.call("swarm_engine_profile", 0, ctypes.byref(ms), ctypes.byref(cnt))
-    except RuntimeError as err:  # the runtime cannot time graph-recorded events
-        print(f"bench.py: graph-captured run-kernel events unreadable ({err}); "
-              f"eager timing only", file=sys.stderr)
-        return None
-    return ms.value / cnt.value if cnt.value else None
-
-
-def graph_ppo_ms():
-    """Mean duration (ms) of k_ppo_grads in the last replay of the PPO epochs
-    graph (swarm_ppo_profile events recorded at its capture)."""
-    import ctypes
-
-    from swarmrl_amd import _capi
-
-    ms, cnt = ctypes.c_double(), ctypes.c_int32()
-    rc = _capi.lib().swarm_ppo_profile(0, ctypes.byref(ms), ctypes.byref(cnt))
-    if rc != 0 or cnt.value == 0:
-        return None
-    return ms.value / cnt.value
-
-
 def time_run_kernel(eng, reps):
-    """Average duration (ms) of k_cluster_run, the dominant kernel: HIP events
-    recorded by the engine around each launch on the stream it runs on
-    (swarm_engine_profile), over `reps` eager 100-sub-step windows."""
+    """Duration (ms) of the dominant kernel, the 2-D run kernel of the
+    latency- (k_cluster_run_wide) or throughput-bound (k_cluster_run) cluster
+    window: `reps` back-to-back launches on one freshly built window between
+    two HIP events on the engine's stream (swarm_engine_time_run), after the
+    timed region -- so the per-launch figure carries no per-launch event or
+    dispatch overhead, and profiles/ rows of the same launches (the last
+    `reps` dispatches of a config-pure rocprofv3 run) time the same work."""
     import ctypes
 
     import torch
 
     nat = eng._native
-    ms = ctypes.c_double()
-    cnt = ctypes.c_int32()
-    eng._run(eng.params.steps_per_slice)
+    wide = eng.n_envs * eng.n_particles <= 32768  # latency-bound engines (DESIGN.md section 6)
+    name = ("k_cluster_run_wide (100 fused BD+WCA sub-steps; the next window's noise table "
+            "filled beside them)" if wide else "k_cluster_run (100 fused BD+WCA sub-steps)")
     torch.cuda.synchronize()
-    nat.call("swarm_engine_profile", 1, ctypes.byref(ms), ctypes.byref(cnt))
-    for _ in range(reps):
-        eng._run(eng.params.steps_per_slice)
-    nat.call("swarm_engine_profile", 0, ctypes.byref(ms), ctypes.byref(cnt))
-    if cnt.value == 0:  # global path only (no cluster windows): whole windows
+    ms = ctypes.c_double()
+    try:
+        nat.call("swarm_engine_time_run", int(eng.params.steps_per_slice), int(reps),
+                 ctypes.byref(ms))
+    except (RuntimeError, ValueError):
+        # no 2-D cluster windows (global path): whole windows, HIP events
         start = torch.cuda.Event(enable_timing=True)
         stop = torch.cuda.Event(enable_timing=True)
         start.record()
@@ -356,19 +331,18 @@ def time_run_kernel(eng, reps):
             eng._run(eng.params.steps_per_slice)
         stop.record()
         stop.synchronize()
-        return start.elapsed_time(stop) / reps, "k_global (100 sub-steps)"
-    wide = eng.n_envs * eng.n_particles <= 32768  # latency-bound engines
-    name = ("k_cluster_run_wide (100 fused BD+WCA sub-steps; the next window's noise table "
-            "filled beside them)" if wide else "k_cluster_run (100 fused BD+WCA sub-steps)")
-    return ms.value / cnt.value, name
+        return start.elapsed_time(stop) / reps, "k_global (100 sub-steps)", "whole windows"
+    torch.cuda.synchronize()
+    return ms.value, name, (f"HIP events around {reps} back-to-back launches on one window "
+                            f"(swarm_engine_time_run), after the timed region")
 
 
-def time_ppo_grads(agent, traj, line, reps, graph_ms=None):
+def time_ppo_grads(agent, traj, line, reps):
     """Roofline of the PPO update's dominant kernel, k_ppo_grads (the caller
-    side of the rollout): `reps` eager epochs of the
-    episode `traj` with HIP events around every k_ppo_grads launch
-    (swarm_ppo_profile), useful work = PPO_MAC_PER_SAMPLE multiply-adds per
-    sample per epoch against the f32 vector peak."""
+    side of the rollout): one eager epoch of the episode
+    `traj` whose gradient kernel is launched `reps` times back to back between
+    two HIP events (swarm_ppo_profile), useful work = PPO_MAC_PER_SAMPLE
+    multiply-adds per sample per launch against the f32 vector peak."""
     import ctypes
 
     import torch
@@ -380,11 +354,11 @@ def time_ppo_grads(agent, traj, line, reps, graph_ms=None):
     loss = agent.loss
     epochs = loss.n_epochs
     prev = os.environ.get("SWARMRL_AMD_PPO_GRAPH")
-    os.environ["SWARMRL_AMD_PPO_GRAPH"] = "0"  # eager epochs: events around each launch
+    os.environ["SWARMRL_AMD_PPO_GRAPH"] = "0"  # one eager epoch, events around its launches
     try:
         torch.cuda.synchronize()
-        lib.swarm_ppo_profile(1, ctypes.byref(ms), ctypes.byref(cnt))
-        loss.n_epochs = max(1, reps)
+        lib.swarm_ppo_profile(max(1, reps), ctypes.byref(ms), ctypes.byref(cnt))
+        loss.n_epochs = 1
         loss.compute_loss(network=agent.network, episode_data=traj)
         lib.swarm_ppo_profile(0, ctypes.byref(ms), ctypes.byref(cnt))
     finally:
@@ -395,24 +369,22 @@ def time_ppo_grads(agent, traj, line, reps, graph_ms=None):
             os.environ["SWARMRL_AMD_PPO_GRAPH"] = prev
     if cnt.value == 0:
         return None  # not the fused path (another network or sampling strategy)
-    eager_ms = ms.value / cnt.value
-    kernel_ms = graph_ms or eager_ms
+    kernel_ms = ms.value / cnt.value
     samples = len(traj.actions) * int(traj.actions[0].numel())
     tflops = 2.0 * PPO_MAC_PER_SAMPLE * samples / (kernel_ms * 1e-3) / 1e12
     out = {"bound": "valu", "kernel": "k_ppo_grads (one PPO epoch's gradient)",
            "achieved": tflops, "peak": F32_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
            "frac": tflops / F32_VECTOR_PEAK_TFLOPS, "kernel_ms": kernel_ms,
-           "kernel_ms_eager": eager_ms,
-           "kernel_timing": "HIP events captured into the PPO epochs graph, last replay" if graph_ms
-                            else "HIP events around eager epochs",
+           "kernel_timing": f"HIP events around {max(1, reps)} back-to-back launches of one "
+                            f"epoch's gradient kernel, after the timed region",
            "samples_per_launch": samples,
            "algorithmic_flops": f"2 x {PPO_MAC_PER_SAMPLE} per sample (DESIGN.md 6) x {samples}"}
     row = profile_row(line, r"k_ppo_grads")
     if row:
         out["profile"] = {"source": row["source"], "src_sha": row.get("src_sha"),
                           "stale": bool(row.get("stale")),
-                          "rocprof_mean_ms": (row.get("mean_duration_graph_us") or
-                                              row.get("mean_duration_us") or 0.0) * 1e-3 or None,
+                          "rocprof_timed_mean_ms": (row.get("mean_duration_timed_us") or 0.0) * 1e-3
+                          or None,
                           "traffic": row.get("bytes_per_launch")}
     return out
 
@@ -477,8 +449,10 @@ def make_roofline(line, kernel_re, kernel, kernel_ms, units, bytes_per_unit, uni
     if row:
         out["profile"] = {"source": row["source"], "src_sha": row.get("src_sha"),
                           "stale": bool(row.get("stale")),
-                          "rocprof_mean_ms": (row.get("mean_duration_graph_us") or
-                                              row.get("mean_duration_us") or 0.0) * 1e-3 or None,
+                          "rocprof_timed_mean_ms": (row.get("mean_duration_timed_us") or 0.0) * 1e-3
+                          or None,
+                          "rocprof_graph_mean_ms": (row.get("mean_duration_graph_us") or 0.0) * 1e-3
+                          or None,
                           "launches": row.get("dispatches")}
         valu, trans = row.get("valu_insts_per_launch"), row.get("valu_trans_per_launch")
         if valu:
@@ -686,30 +660,16 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
             one_slice()
         agent.reset_trajectory()
         episode_graph = torch.cuda.CUDAGraph()
-        # HIP events around every run-kernel launch of the episode become graph
-        # nodes: after the timed replays they time the last replay's launches
-        # (the kernel as it runs in the workload; read by graph_kernel_ms)
-        eng._native.call("swarm_engine_profile", 1, None, None)
-        try:
-            with torch.cuda.graph(episode_graph, pool=slice_graph.pool()):
-                # one episode as the trainers run it (episodic_trainer.py:35 ->
-                # engine.integrate(episode_length, force_fn))
-                eng.integrate(T, ff)
-        finally:
-            eng._native.call("swarm_engine_profile", 2, None, None)
+        with torch.cuda.graph(episode_graph, pool=slice_graph.pool()):
+            # one episode as the trainers run it (episodic_trainer.py:35 ->
+            # engine.integrate(episode_length, force_fn))
+            eng.integrate(T, ff)
     else:
         agent.reset_trajectory()
 
     gstats = []
 
     traj = agent.trajectory  # the episode graph's output tensors
-    if train and episode_graph is not None:
-        from swarmrl_amd import _capi
-
-        # events around the k_ppo_grads launches of the PPO graph's capture
-        # (the epochs replay as one graph from the second episode on)
-        lib = _capi.lib()
-        agent.loss.capture_hook = lambda on: lib.swarm_ppo_profile(1 if on else 2, None, None)
 
     def run(n_steps, timed):
         k = 0
@@ -752,10 +712,7 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
 
     eng.drain_trajectory(block=True)
     traj_written = eng.h5_time_steps_written + len(eng.traj_holder["Times"])
-    graph_ms = graph_kernel_ms(eng) if episode_graph is not None else None
-    update_graph_ms = graph_ppo_ms() if train and episode_graph is not None else None
-    eager_ms, kernel = time_run_kernel(eng, args.bd_reps)
-    kernel_ms = graph_ms or eager_ms
+    kernel_ms, kernel, timing = time_run_kernel(eng, args.bd_reps)
     N = args.colloids
     sub = eng.params.steps_per_slice
     out = dict(timing)
@@ -770,16 +727,12 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
                                   f"colloid-sub-step; {N} colloids x {sub} sub-steps x {E} env(s)"),
         "src_sha": source_sha(),
     })
-    out["roofline"]["kernel_timing"] = (
-        "HIP events around each launch, captured into the episode graph: mean over the last "
-        f"replay's launches; eager launches {eager_ms * 1e3:.1f} us" if graph_ms else
-        "HIP events around each of the eager launches")
-    out["roofline"]["kernel_ms_eager"] = eager_ms
+    out["roofline"]["kernel_timing"] = timing
     valu = out["roofline"].get("valu")
     if valu:
         valu["lane_insts_per_colloid_substep"] = valu["insts_per_launch"] * 64 / (N * sub * E)
     if train:
-        out["roofline_update"] = time_ppo_grads(agent, traj, line, args.bd_reps, update_graph_ms)
+        out["roofline_update"] = time_ppo_grads(agent, traj, line, args.bd_reps)
     del eng, ff, agent, slice_graph, episode_graph
     torch.cuda.synchronize()
     return out

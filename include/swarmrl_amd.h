@@ -239,13 +239,20 @@ int swarm_engine_window_stats(swarm_engine_t *e, int32_t *fallback,
 /* Kernel timing for measurement (bench.py roofline): returns the summed
  * duration (ms) and count of the k_cluster_run launches recorded since the
  * previous call (HIP events on the engine stream; waits for them), then
- * enables (1) or disables (0) recording.  Recording may be on while a graph
- * is captured: the event records become graph nodes, so after replays the
- * pairs time the LAST replay's launches.  enable = 2 pauses recording and
- * keeps the recorded pairs unread (end of a capture; read them later with
- * 0 or 1). */
+ * enables (1) or disables (0) recording.  Not for use under graph capture. */
 int swarm_engine_profile(swarm_engine_t *e, int32_t enable, double *run_ms,
                          int32_t *launches);
+
+/* Kernel timing for measurement (bench.py roofline): builds the next 2-D
+ * cluster window from the current positions, then launches its run kernel
+ * `reps` times back to back between two HIP events on the engine stream and
+ * returns the mean duration (ms) per launch; the exact check follows
+ * (untimed).  The repeats integrate the same window again and again on one
+ * decomposition, so the state afterwards is for measurement only (re-upload
+ * it to continue a simulation).  SWARM_ESTATE unless the engine runs 2-D
+ * cluster windows. */
+int swarm_engine_time_run(swarm_engine_t *e, int32_t n_steps, int32_t reps,
+                          double *run_ms);
 
 /* Diagnostics: 32 shader-clock stamps of the last cluster build's phases
  * (env 0), filled only by builds compiled with -DSWARM_PHASE_TIMING. */
@@ -371,10 +378,10 @@ int swarm_policy_mlp_sample(const float *obs, int32_t n, int32_t d_in, const flo
 /* Kernel timing for measurement (bench.py's roofline of the PPO update):
  * the summed duration (ms) and count of the k_ppo_grads launches this
  * thread made through swarm_ppo_epoch_grad since the previous call (HIP
- * events on the caller's stream; waits for them), then enables (1) or
- * disables (0) recording; 2 pauses and keeps the pairs unread.  As for
- * swarm_engine_profile, pairs recorded under graph capture time the last
- * replay. */
+ * events on the caller's stream around each epoch's launches; waits for
+ * them), then enables recording with `enable` back-to-back launches of the
+ * (deterministic) gradient kernel per epoch, or disables it (0).  Not for
+ * use under graph capture. */
 int swarm_ppo_profile(int32_t enable, double *grads_ms, int32_t *launches);
 
 /* The gradient of one PPO epoch -- ProximalPolicyLoss._calculate_loss

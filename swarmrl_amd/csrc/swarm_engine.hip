@@ -406,18 +406,29 @@ __device__ __forceinline__ void vision_drain(const VisionLane& L, const swarm_vi
 // kAll: vision_range >= half the box (the reference has no range limit,
 // subdivided_vision_cones.py:116-121): every record of the env is a
 // candidate, tested on its unwrapped (int64) separation.
+// xcd_bpe > 0: blocks placed on XCDs by env (swarm::xcd_env_block, xcd_bpe
+// blocks per env), so the records an env's agents read stay in one L2.
 template <int NB, int G, bool kAll = false>
 __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __restrict__ d,
                                                 swarm_vision_params_t vp, int lx, int ly,
                                                 const int32_t* __restrict__ start, VisionSorted vs,
                                                 int n_agents, float* __restrict__ out,
-                                                int n_envs) {
+                                                int n_envs, int xcd_bpe) {
   __shared__ uint32_t hits[kVisionHits][256];
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int grp = t / G, sub = t & (G - 1);
   const int N = st.n;
-  if (grp >= n_envs * N) return;  // whole groups only (G divides 64)
-  const int e = grp / N, ps = grp - e * N;
+  const int sub = threadIdx.x & (G - 1);
+  int e, ps;
+  if (xcd_bpe > 0) {
+    int lb;
+    if (!swarm::xcd_env_block((int)blockIdx.x, xcd_bpe, n_envs, &e, &lb)) return;
+    ps = (lb * (int)blockDim.x + (int)threadIdx.x) / G;
+    if (ps >= N) return;  // whole groups only (G divides 64)
+  } else {
+    const int grp = (blockIdx.x * blockDim.x + threadIdx.x) / G;
+    if (grp >= n_envs * N) return;
+    e = grp / N;
+    ps = grp - e * N;
+  }
   const size_t base = (size_t)e * N;
   const uint4 own0 = vs.rec[2 * (base + ps)];
   const uint4 own1 = vs.rec[2 * (base + ps) + 1];
@@ -443,43 +454,47 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
   for (int k = 0; k < NB; ++k) acc[k] = 0;
   const int ncell = 1 << (lx + ly);
   const int ncx = 1 << lx, ncy = 1 << ly;
-  const int lox = ncx >= 3 ? -1 : 0, hix = ncx >= 3 ? 1 : ncx - 1;
   const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
   const int cc0 = cell_index(L.qxi, L.qyi, lx, ly);
   const int cx = cc0 & (ncx - 1), cy = cc0 >> lx;
   const int32_t* so = start + (size_t)e * (ncell + 1);
   int nh = 0;
-  // the 3x3 candidate cells as one flat index range [0, total): all 18
-  // bounds loaded together, then candidates four at a time per lane (their
-  // record loads in flight together), a lane taking f = sub, sub + G, ...
-  int jbs[9], pre[10];
+  // the 3x3 candidate cells as one flat index range [0, total): a stencil
+  // row (cells x-1..x+1) is one contiguous sorted range, plus one wrap cell
+  // at the grid edge -- six ranges, their 12 bounds loaded together; then
+  // candidates four at a time per lane (their record loads in flight
+  // together), a lane taking f = sub, sub + G, ...; record index j = f +
+  // off[r] of the range r holding f
+  const int xa = ncx >= 3 ? max(cx - 1, 0) : 0;
+  const int xb = ncx >= 3 ? min(cx + 1, ncx - 1) : ncx - 1;
+  const int xw = ncx >= 3 ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
+  int off[6], pre[7];
   pre[0] = 0;
 #pragma unroll
-  for (int r = 0; r < 9; ++r) {
-    const int oy = r / 3 - 1, ox = r % 3 - 1;
+  for (int r = 0; r < 6; ++r) {
+    const int oy = loy + (r >> 1), part = r & 1;
     int jb = 0, je = 0;
     if (kAll) {  // one range: all records
       je = r == 0 ? N : 0;
-    } else if (oy >= loy && oy <= hiy && ox >= lox && ox <= hix) {
-      const int y = (cy + oy + ncy) & (ncy - 1);
-      const int x = (cx + ox + ncx) & (ncx - 1);
-      const int cc = (y << lx) | x;
-      jb = so[cc];
-      je = so[cc + 1];
+    } else if (oy <= hiy && (part == 0 || xw >= 0)) {
+      const int row = ((cy + oy + ncy) & (ncy - 1)) << lx;
+      jb = so[row | (part == 0 ? xa : xw)];
+      je = so[(row | (part == 0 ? xb : xw)) + 1];
     }
-    jbs[r] = jb;
+    off[r] = jb - pre[r];
     pre[r + 1] = pre[r] + (je - jb);
   }
-  const int total = pre[9];
+  const int total = pre[6];
   for (int f0 = sub; f0 < total; f0 += 4 * G) {
     uint4 c0[4];
     int jj[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int f = f0 + u * G;
-      int j = jbs[0] + f;
+      int o = off[0];
 #pragma unroll
-      for (int r = 1; r < 9; ++r) j = f >= pre[r] ? jbs[r] + (f - pre[r]) : j;
+      for (int r = 1; r < 6; ++r) o = f >= pre[r] ? off[r] : o;
+      const int j = f + o;
       jj[u] = j;
       if (f < total) c0[u] = vs.rec[2 * (base + j)];
     }
@@ -843,6 +858,9 @@ struct swarm_engine {
   int run_wpb = 4;  // run waves per block (= per CU) of k_cluster_run_wide
   // k_build_env: the whole build in one LDS-resident workgroup per env
   bool env_build = false;
+  // XCD-aware env placement of the throughput run kernel and the vision
+  // cone (SWARMRL_AMD_XCD_MAP=0 turns it off)
+  bool xcd_map = true;
   int noise_blocks = 0;
   bool next_table_ready = false;
   // swarm_engine_profile: HIP events around every k_cluster_run launch
@@ -1013,6 +1031,82 @@ int launch_build(swarm_engine* e, hipStream_t stream) {
   return SWARM_OK;
 }
 
+// The 2-D cluster window's run kernel (k_cluster_run_wide for latency-bound
+// engines, else k_cluster_run) over the current decomposition.
+int launch_run(swarm_engine* e, int n_steps) {
+  const long waves = (long)e->n_envs * e->sc.wmax;
+  const bool multi = e->params.n_species > 1;
+  const bool walls = e->derived.n_walls != 0;
+  if (e->wide_run) {
+    // dynamic LDS beyond half a CU's keeps one block (run_wpb run waves) per CU
+    const int R = e->run_wpb;
+    const dim3 grid((unsigned)(e->noise_blocks + (waves + R - 1) / R));
+    const size_t lds = 96 * 1024;
+#define SWARM_WIDE(MULTI, WALLS)                                                             \
+  hipLaunchKernelGGL((swarm::k_cluster_run_wide<MULTI, WALLS>), grid, dim3(1024), lds, e->stream, \
+                     e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise,      \
+                     e->noise_blocks, R)
+    if (walls) {
+      if (multi)
+        SWARM_WIDE(true, true);
+      else
+        SWARM_WIDE(false, true);
+    } else {
+      if (multi)
+        SWARM_WIDE(true, false);
+      else
+        SWARM_WIDE(false, false);
+    }
+#undef SWARM_WIDE
+    e->next_table_ready = e->noise_blocks > 0;
+  } else {
+    // XCD-aware env placement (swarm::xcd_env_block) once the envs fill the
+    // eight XCDs evenly (or nearly: 64 and more)
+    const int E = e->n_envs;
+    const int bpe = (e->sc.wmax + 3) / 4;
+    const bool xcd = e->xcd_map && E >= 8 && (E % 8 == 0 || E >= 64);
+    const dim3 run_grid((unsigned)(xcd ? 8 * ((E + 7) / 8) * bpe : (waves + 3) / 4)),
+        run_block(256);
+#define SWARM_RUN(MULTI, TABLE, WALLS)                                                     \
+  hipLaunchKernelGGL((swarm::k_cluster_run<MULTI, TABLE, WALLS>), run_grid, run_block, 0,   \
+                     e->stream, e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step,  \
+                     e->d_noise, xcd ? bpe : 0)
+#define SWARM_RUN_W(MULTI, TABLE)      \
+  do {                                 \
+    if (walls)                         \
+      SWARM_RUN(MULTI, TABLE, true);   \
+    else                               \
+      SWARM_RUN(MULTI, TABLE, false);  \
+  } while (0)
+    if (e->noise_table) {
+      if (multi)
+        SWARM_RUN_W(true, true);
+      else
+        SWARM_RUN_W(false, true);
+    } else {
+      if (multi)
+        SWARM_RUN_W(true, false);
+      else
+        SWARM_RUN_W(false, false);
+    }
+#undef SWARM_RUN_W
+#undef SWARM_RUN
+    e->next_table_ready = false;
+  }
+  HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+
+// The 2-D cluster window's exact check (and re-run on failure).
+int launch_check(swarm_engine* e, int n_steps) {
+  hipLaunchKernelGGL(swarm::k_check, dim3(e->n_envs), dim3(1024),
+                     check_lds_bytes(e->lxg, e->lyg, e->n, e->params.n_dims), e->stream,
+                     e->d_derived, e->st, e->sc, n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg,
+                     0);
+  HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+
 // One integration window: cluster build -> cluster run -> check/fallback.
 // use_prebuilt: the build ran already; noise_ready: the noise table holds
 // this many sub-steps from the current counter.
@@ -1118,66 +1212,13 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
     HIP_TRY(hipEventCreate(&ev1));
     HIP_TRY(hipEventRecord(ev0, e->stream));
   }
-  if (e->wide_run) {
-    // dynamic LDS beyond half a CU's keeps one block (run_wpb run waves) per CU
-    const int R = e->run_wpb;
-    const dim3 grid((unsigned)(e->noise_blocks + (waves + R - 1) / R));
-    const size_t lds = 96 * 1024;
-#define SWARM_WIDE(MULTI, WALLS)                                                             \
-  hipLaunchKernelGGL((swarm::k_cluster_run_wide<MULTI, WALLS>), grid, dim3(1024), lds, e->stream, \
-                     e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise,      \
-                     e->noise_blocks, R)
-    if (walls) {
-      if (multi)
-        SWARM_WIDE(true, true);
-      else
-        SWARM_WIDE(false, true);
-    } else {
-      if (multi)
-        SWARM_WIDE(true, false);
-      else
-        SWARM_WIDE(false, false);
-    }
-#undef SWARM_WIDE
-    e->next_table_ready = e->noise_blocks > 0;
-  } else {
-    const dim3 run_grid((unsigned)((waves + 3) / 4)), run_block(256);
-#define SWARM_RUN(MULTI, TABLE, WALLS)                                                     \
-  hipLaunchKernelGGL((swarm::k_cluster_run<MULTI, TABLE, WALLS>), run_grid, run_block, 0,   \
-                     e->stream, e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step,  \
-                     e->d_noise)
-#define SWARM_RUN_W(MULTI, TABLE)      \
-  do {                                 \
-    if (walls)                         \
-      SWARM_RUN(MULTI, TABLE, true);   \
-    else                               \
-      SWARM_RUN(MULTI, TABLE, false);  \
-  } while (0)
-    if (e->noise_table) {
-      if (multi)
-        SWARM_RUN_W(true, true);
-      else
-        SWARM_RUN_W(false, true);
-    } else {
-      if (multi)
-        SWARM_RUN_W(true, false);
-      else
-        SWARM_RUN_W(false, false);
-    }
-#undef SWARM_RUN_W
-#undef SWARM_RUN
-    e->next_table_ready = false;
-  }
-  HIP_TRY(hipGetLastError());
+  int rc = launch_run(e, n_steps);
+  if (rc) return rc;
   if (e->profile) {
     HIP_TRY(hipEventRecord(ev1, e->stream));
     e->prof_events.emplace_back(ev0, ev1);
   }
-  hipLaunchKernelGGL(swarm::k_check, dim3(e->n_envs), dim3(1024),
-                     check_lds_bytes(e->lxg, e->lyg, e->n, e->params.n_dims), e->stream, e->d_derived, e->st, e->sc,
-                     n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg, 0);
-  HIP_TRY(hipGetLastError());
-  return SWARM_OK;
+  return launch_check(e, n_steps);
 }
 
 int run_bd(swarm_engine* e, int n_steps) {
@@ -1470,6 +1511,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
       e->env_build = e->cluster_path && !e->big_build && !latency_bound && !three_d &&
                      !e->nlist_path &&
                      swarm::build_env_sort_words(n_particles, 1 << (e->lxb + e->lyb)) <= below;
+      if (const char* ox = std::getenv("SWARMRL_AMD_XCD_MAP")) e->xcd_map = ox[0] != '0';
       const char* ob = std::getenv("SWARMRL_AMD_ENV_BUILD");
       if (ob && ob[0] == '0') e->env_build = false;
       if (ob && ob[0] == '1')
@@ -1731,13 +1773,42 @@ int read_event_pairs(std::vector<std::pair<hipEvent_t, hipEvent_t>>& ev, double*
 
 int swarm_engine_profile(swarm_engine_t* e, int32_t enable, double* run_ms, int32_t* launches) {
   if (!e) return fail(SWARM_EINVAL, "null engine");
-  if (enable == 2) {  // pause: keep the recorded pairs (e.g. captured into a graph) unread
-    e->profile = false;
-    return SWARM_OK;
-  }
   const int rc = read_event_pairs(e->prof_events, run_ms, launches);
   e->profile = enable != 0;
   return rc;
+}
+
+int swarm_engine_time_run(swarm_engine_t* e, int32_t n_steps, int32_t reps, double* run_ms) {
+  if (!e || !run_ms) return fail(SWARM_EINVAL, "null argument");
+  if (n_steps < 1 || n_steps > swarm::kMaxWindow || reps < 1)
+    return fail(SWARM_EINVAL, "1 <= n_steps <= 128 and reps >= 1");
+  if (!e->cluster_path || e->nlist_path || e->params.n_dims != 2)
+    return fail(SWARM_ESTATE, "swarm_engine_time_run times the 2-D cluster window only");
+  if (e->prebuilt) {  // a pending side-stream build would race with this one
+    HIP_TRY(hipDeviceSynchronize());
+    e->prebuilt = false;
+  }
+  int rc = launch_build(e, e->stream);
+  if (!rc && e->noise_table && !e->next_table_ready) rc = launch_noise(e, e->stream, n_steps);
+  if (rc) return rc;
+  hipEvent_t ev0, ev1;
+  HIP_TRY(hipEventCreate(&ev0));
+  HIP_TRY(hipEventCreate(&ev1));
+  HIP_TRY(hipEventRecord(ev0, e->stream));
+  for (int r = 0; r < reps && !rc; ++r) rc = launch_run(e, n_steps);
+  HIP_TRY(hipEventRecord(ev1, e->stream));
+  // the exact check restores a consistent state (the repeated windows ran on
+  // one decomposition and their movers overflow the list: exact re-run)
+  if (!rc) rc = launch_check(e, n_steps);
+  float ms = 0.0f;
+  hipError_t err = hipEventSynchronize(ev1);
+  if (err == hipSuccess) err = hipEventElapsedTime(&ms, ev0, ev1);
+  (void)hipEventDestroy(ev0);
+  (void)hipEventDestroy(ev1);
+  if (rc) return rc;
+  if (err != hipSuccess) return fail(SWARM_EDEVICE, hipGetErrorString(err));
+  *run_ms = (double)ms / reps;
+  return SWARM_OK;
 }
 
 int swarm_engine_debug_phases(swarm_engine_t* e, uint64_t* out32) {
@@ -1961,7 +2032,7 @@ int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const 
     const dim3 agrid((unsigned)((total * 16 + 255) / 256)), ablock(256);
 #define SWARM_VALL(NBV)                                                                         \
   hipLaunchKernelGGL((k_vision<NBV, 16, true>), agrid, ablock, 0, e->stream, e->st, e->d_derived, \
-                     *vp, lx, ly, e->d_start, e->vs, n_agents, out, e->n_envs)
+                     *vp, lx, ly, e->d_start, e->vs, n_agents, out, e->n_envs, 0)
     if (nb <= 4) {
       SWARM_VALL(4);
     } else if (nb <= 8) {
@@ -1983,10 +2054,15 @@ int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const 
     const int v = std::atoi(og);
     if (v == 4 || v == 16) G = v;
   }
-  const dim3 grid((unsigned)((total * G + 255) / 256)), block(256);
+  // XCD-aware env placement once the envs fill the eight XCDs (as k_cluster_run)
+  const int E = e->n_envs;
+  const int bpe = (int)(((long)e->n * G + 255) / 256);
+  const bool xcd = e->xcd_map && E >= 8 && (E % 8 == 0 || E >= 64);
+  const dim3 grid((unsigned)(xcd ? 8L * ((E + 7) / 8) * bpe : (total * G + 255) / 256)),
+      block(256);
 #define SWARM_VISION(NBV, GV)                                                              \
   hipLaunchKernelGGL((k_vision<NBV, GV>), grid, block, 0, e->stream, e->st, e->d_derived, *vp, \
-                     lx, ly, e->d_start, e->vs, n_agents, out, e->n_envs)
+                     lx, ly, e->d_start, e->vs, n_agents, out, e->n_envs, xcd ? bpe : 0)
 #define SWARM_VISION_G(NBV) \
   if (G == 4)               \
     SWARM_VISION(NBV, 4);   \
@@ -2268,18 +2344,18 @@ int64_t swarm_ppo_workspace_bytes(int32_t T, int32_t S, int32_t d_in, int32_t hi
 namespace {
 struct PpoProfile {
   bool on = false;
+  int reps = 1;  // back-to-back k_ppo_grads launches per epoch while timing
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
 };
 thread_local PpoProfile g_ppo_prof;
 }  // namespace
 
 int swarm_ppo_profile(int32_t enable, double* grads_ms, int32_t* launches) {
-  if (enable == 2) {  // pause: keep the recorded pairs unread
-    g_ppo_prof.on = false;
-    return SWARM_OK;
-  }
-  const int rc = read_event_pairs(g_ppo_prof.ev, grads_ms, launches);
-  g_ppo_prof.on = enable != 0;
+  int32_t pairs = 0;
+  const int rc = read_event_pairs(g_ppo_prof.ev, grads_ms, &pairs);
+  if (launches) *launches = pairs * g_ppo_prof.reps;
+  g_ppo_prof.reps = enable > 0 ? enable : 1;
+  g_ppo_prof.on = enable > 0;
   return rc;
 }
 
@@ -2343,11 +2419,12 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
     if (g_ppo_prof.on && hipEventCreate(&ev0) == hipSuccess &&                                \
         hipEventCreate(&ev1) == hipSuccess)                                                   \
       (void)hipEventRecord(ev0, s);                                                           \
-    hipLaunchKernelGGL((swarm::k_ppo_grads<NN, DD, KK>), dim3((unsigned)blocks),             \
-                       dim3(64 * NN),                                                         \
-                       (size_t)lds, s, x, n, d_in, w1, b1, hidden, wa, ba, k, wc, bc,         \
-                       actions, old_logp, adv, dv, spart, gae_blocks, table, clip_eps,        \
-                       entropy_coef, partial);                                                \
+    for (int rep = 0; rep < (ev1 ? g_ppo_prof.reps : 1); ++rep) /* same partial rows */      \
+      hipLaunchKernelGGL((swarm::k_ppo_grads<NN, DD, KK>), dim3((unsigned)blocks),           \
+                         dim3(64 * NN),                                                       \
+                         (size_t)lds, s, x, n, d_in, w1, b1, hidden, wa, ba, k, wc, bc,       \
+                         actions, old_logp, adv, dv, spart, gae_blocks, table, clip_eps,      \
+                         entropy_coef, partial);                                              \
     if (ev1) {                                                                                \
       (void)hipEventRecord(ev1, s);                                                           \
       g_ppo_prof.ev.emplace_back(ev0, ev1);                                                   \

@@ -2231,13 +2231,32 @@ __device__ __forceinline__ void run_wave_dispatch(const Derived* __restrict__ d,
                                     lacc_x, lacc_y, pt, par);
 }
 
+// XCD-aware placement of per-env work (envs_per_xcd_map: blocks of one env):
+// workgroup b is dispatched to XCD b mod 8 (MI355X_MICROARCH.md: for speed
+// only, nothing depends on it), so the env's blocks are the b with
+// b mod 8 == e mod 8.  All waves of an env then share one XCD's L2: the
+// particle-indexed state lines an env's scattered lanes load and store are
+// fetched and written back by one L2 instead of partial copies in eight.
+// Returns false for a block beyond the last env.
+__device__ __forceinline__ bool xcd_env_block(int b, int blocks_per_env, int n_envs, int* e,
+                                              int* lb) {
+  const int x = b & 7, k = b >> 3;
+  *e = x + 8 * (k / blocks_per_env);
+  *lb = k - (k / blocks_per_env) * blocks_per_env;
+  return *e < n_envs;
+}
+
 // Throughput launch: 256-thread blocks, 4 waves each.  kWalls (host-chosen)
 // keeps the wall-force variant's registers out of the wall-free kernel.
+// xcd_bpe > 0: blocks placed by xcd_env_block with xcd_bpe blocks per env
+// (ceil(wmax / 4)); else block b runs waves 4 b .. 4 b + 3 of the env-major
+// wave list.
 template <bool kMulti, bool kTable, bool kWalls>
 __global__ __launch_bounds__(256, SWARM_RUN_MINB) void k_cluster_run(const Derived* __restrict__ d, DevState st,
                                                      Scratch sc, int n_envs, int n_steps,
                                                      const uint64_t* __restrict__ ctl,
-                                                     const float* __restrict__ tables) {
+                                                     const float* __restrict__ tables,
+                                                     int xcd_bpe) {
   __shared__ PairTables pt;
   __shared__ uint2 lpos[4][64];                  // positions of the block's 4 waves
   __shared__ unsigned long long lacc[4][2][64];  // int64 force sums (x, y)
@@ -2247,7 +2266,14 @@ __global__ __launch_bounds__(256, SWARM_RUN_MINB) void k_cluster_run(const Deriv
   const bool table_ok = kTable && ctl[kCtlTStep + par] == step0 &&
                         (uint64_t)n_steps <= ctl[kCtlTLen + par];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (xcd_bpe > 0) {
+    int e, lb;
+    if (!xcd_env_block((int)blockIdx.x, xcd_bpe, n_envs, &e, &lb)) return;
+    const int w = lb * 4 + wv;
+    if (w >= sc.wmax) return;
+    gw = e * sc.wmax + w;
+  }
   // a table that does not cover this window (the device check; the host
   // normally guarantees it) -> the normals are drawn in the kernel
   run_wave_dispatch<kMulti, kWalls>(d, st, sc, n_envs, n_steps, step0,

@@ -139,17 +139,10 @@ class ProximalPolicyLoss(Loss):
             ops.ppo_epoch_grad(*args, out=grad)  # sizes the workspace outside the capture
             torch.cuda.synchronize(features.device)
             graph = torch.cuda.CUDAGraph()
-            hook = getattr(self, "capture_hook", None)  # measurement (bench.py): around the capture
-            if hook:
-                hook(True)
-            try:
-                with torch.cuda.graph(graph):
-                    for _ in range(self.n_epochs):
-                        ops.ppo_epoch_grad(*args, out=grad)
-                        opt.step()
-            finally:
-                if hook:
-                    hook(False)
+            with torch.cuda.graph(graph):
+                for _ in range(self.n_epochs):
+                    ops.ppo_epoch_grad(*args, out=grad)
+                    opt.step()
             cache = self._ppo_graph = {"sig": sig, "graph": graph, "inputs": (x, act, olp, rew),
                                        "grad": grad}
         x, act, olp, rew = cache["inputs"]

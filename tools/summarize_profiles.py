@@ -31,7 +31,7 @@ src = f"gpurun_out/prof_{tag}"
 dst = "profiles"
 DOMINANT = {"head": r"k_cluster_run", "batched": r"k_cluster_run", "c2": r"k_cluster_run",
             "c4": r"k_cluster_run", "c5": r"k_cluster_run", "c3train": r"k_cluster_run|k_ppo_grads"}
-EAGER_TAIL = 21  # bench.py --bd-reps 20 (+ the one window that precedes them)
+TIMED_TAIL = 20  # bench.py --bd-reps
 COUNTERS = ["FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "SQ_INSTS_VALU_TRANS_F32", "SQ_WAVES"]
 
 
@@ -74,12 +74,14 @@ for line in bench.LINES:
             traffic.append({
                 "line": line, "kernel": k, "dispatches": len(dur.get(k, [])),
                 "mean_duration_us": us,
-                # the launches of the captured graphs (the workload as timed):
-                # all but the EAGER_TAIL eager launches bench.py makes last
-                # (time_run_kernel: 1 + bd_reps windows; time_ppo_grads:
-                # bd_reps epochs)
-                "mean_duration_graph_us": (sum(dur[k][:-EAGER_TAIL]) / len(dur[k][:-EAGER_TAIL])
-                                           if len(dur.get(k, [])) > EAGER_TAIL else None),
+                # the launches bench.py's HIP events time: its last TIMED_TAIL
+                # dispatches of the kernel, back to back (time_run_kernel /
+                # time_ppo_grads, --bd-reps)
+                "mean_duration_timed_us": (sum(dur[k][-TIMED_TAIL:]) / TIMED_TAIL
+                                           if len(dur.get(k, [])) >= TIMED_TAIL else None),
+                # the captured graphs' launches (the workload itself)
+                "mean_duration_graph_us": (sum(dur[k][:-TIMED_TAIL]) / len(dur[k][:-TIMED_TAIL])
+                                           if len(dur.get(k, [])) > TIMED_TAIL else None),
                 "fetch_size_kb": mean["FETCH_SIZE"], "write_size_kb": mean["WRITE_SIZE"],
                 "bytes_per_launch": (2 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0,
                 "valu_insts_per_launch": mean["SQ_INSTS_VALU"],
