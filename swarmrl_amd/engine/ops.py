@@ -98,14 +98,15 @@ def field_distance(native, n_envs: int, agent_idx: torch.Tensor, source, box_sca
 
 # ------------------------------------------------------------ list path
 class _PointsEngine:
-    """A scratch single-env engine that holds an arbitrary point set."""
+    """A scratch single-env engine that holds an arbitrary point set (2-D, or
+    3-D for points off the z = 0 plane)."""
 
-    def __init__(self, n: int, box: float):
+    def __init__(self, n: int, box: float, dims: int = 2):
         from swarmrl_amd.engine.swarm_engine import _NativeEngine
 
         _capi.require_gpu()
         p = _capi.SwarmParams()
-        p.n_dims = 2
+        p.n_dims = int(dims)
         p.periodic = 1
         for a in range(3):
             p.box[a] = box
@@ -135,15 +136,23 @@ def virtual_box(extent: float) -> float:
     return float(2.0 ** max(4, math.ceil(math.log2(max(extent, 1.0) * 4.0 + 1.0))))
 
 
-def points_engine(n: int, box: float) -> _PointsEngine:
-    key = (n, box, torch.cuda.current_device())
+def points_engine(n: int, box: float, dims: int = 2) -> _PointsEngine:
+    key = (n, box, int(dims), torch.cuda.current_device())
     eng = _points_cache.get(key)
     if eng is None:
         if len(_points_cache) > 32:
             _points_cache.clear()
-        eng = _PointsEngine(n, box)
+        eng = _PointsEngine(n, box, dims)
         _points_cache[key] = eng
     return eng
+
+
+def points_dims(*arrays) -> int:
+    """3 when any point of the (k, 3) arrays lies off the z = 0 plane (the
+    reference's observables take norms of 3-vectors, concentration_field.py:
+    100-101), else 2."""
+    return 3 if any(np.any(np.asarray(a, dtype=np.float64).reshape(-1, 3)[:, 2] != 0)
+                    for a in arrays) else 2
 
 
 def list_vision_cone(positions: np.ndarray, directors: np.ndarray, types: np.ndarray,
@@ -176,26 +185,26 @@ def list_field_distance(cur_scaled: np.ndarray, prev_scaled: np.ndarray,
     if A == 0:
         return np.zeros(0, np.float32), np.zeros(0, np.float32)
     src = np.asarray(source_scaled, dtype=np.float64).reshape(3)
+    dims = points_dims(cur_scaled, prev_scaled)
     extent = max(
-        float(np.max(np.abs(cur_scaled[:, :2]))), float(np.max(np.abs(prev_scaled[:, :2]))), 1.0
-    )
+        float(np.max(np.abs(cur_scaled[:, :dims]))), float(np.max(np.abs(prev_scaled[:, :dims]))),
+        1.0)
     L = virtual_box(extent)
-    eng = points_engine(A, L)
+    eng = points_engine(A, L, dims)
     dirs = np.zeros((A, 3))
     dirs[:, 0] = 1.0
     pos = cur_scaled.copy()
-    pos[:, 2] = 0.0
+    if dims == 2:
+        pos[:, 2] = 0.0
     eng.upload(pos, dirs)
     dev = torch.device("cuda", torch.cuda.current_device())
     hq = np.zeros((3, A), dtype=np.uint32)
     hi = np.zeros((3, A), dtype=np.int32)
-    for a in range(2):
+    for a in range(dims):
         hq[a], hi[a] = to_fixed_host(prev_scaled[:, a], L)
     hq_t = torch.as_tensor(hq.view(np.int32), device=dev)
     hi_t = torch.as_tensor(hi, device=dev)
     agent_t = torch.arange(A, dtype=torch.int32, device=dev)
-    if np.any(cur_scaled[:, 2] != 0) or np.any(prev_scaled[:, 2] != 0):
-        raise NotImplementedError("positions off the z = 0 plane are not supported (2-D build)")
     # the kernel scales engine coordinates by box[a] / box_scale[a]; the
     # engine already holds scaled coordinates, so box_scale = 1.
     d_cur, d_prev = field_distance(eng.native, 1, agent_t, src, np.ones(3), hq_t, hi_t,
@@ -227,7 +236,7 @@ def snapshot_history(engine, p_type: int):
     hi = np.zeros((3, E, A), dtype=np.int32)
     if engine._native is None:
         pos = np.stack([np.stack(v) for v in engine._pos])  # [E, N, 3]
-        for a in range(2):
+        for a in range(int(engine.n_dims)):
             q, im = to_fixed_host(pos[:, idx, a], float(engine._box[a]))
             hq[a], hi[a] = q, im
     else:

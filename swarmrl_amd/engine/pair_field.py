@@ -68,10 +68,9 @@ def list_pair_field(colloids, agent_indices, sensing_type: int, box_scale, decay
     from swarmrl_amd.engine import ops
 
     pos = np.stack([np.asarray(c.pos, dtype=np.float64) for c in colloids])
-    if np.any(pos[:, 2] != 0):
-        raise NotImplementedError("positions off the z = 0 plane are not supported (2-D build)")
+    dims = ops.points_dims(pos)  # 3-D norms when any colloid is off z = 0
     n = len(pos)
-    eng = ops.points_engine(n, ops.virtual_box(float(np.max(np.abs(pos[:, :2]))) + 1.0))
+    eng = ops.points_engine(n, ops.virtual_box(float(np.max(np.abs(pos[:, :dims]))) + 1.0), dims)
     dirs = np.zeros((n, 3))
     dirs[:, 0] = 1.0
     eng.upload(pos, dirs)
