@@ -223,6 +223,17 @@ int swarm_engine_integrate(swarm_engine_t *e, int32_t n_steps);
  * global path.  n_steps_hint is unused (kept for the noise variant below). */
 int swarm_engine_prebuild(swarm_engine_t *e, void *stream, int32_t n_steps_hint);
 
+/* Defer the next window's cluster decomposition instead (latency-bound 2-D
+ * engines with the three-launch build): its three stages -- counting sort,
+ * pair search, cluster build -- then ride along as extra workgroups in the
+ * slice's next engine-bound launches, swarm_vision_cone (stages 1 and 2)
+ * and swarm_engine_policy_mlp_sample (stage 3), on the engine stream with
+ * no second stream, fork or join (espresso.py:1253-1306: the positions do
+ * not change between manage_forces and integrator.run).  Stages no launch
+ * carried run at the next swarm_engine_integrate.  *deferred = 0 when the
+ * engine cannot defer (use swarm_engine_prebuild). */
+int swarm_engine_defer_build(swarm_engine_t *e, int32_t *deferred);
+
 /* Same contract for the noise table of latency-bound engines: the normals
  * of the next min(n_steps_hint, 128) sub-steps, computed on `stream` (it
  * depends on the step counter only, so it may run beside the build).  No-op
@@ -374,6 +385,18 @@ int swarm_policy_mlp_sample(const float *obs, int32_t n, int32_t d_in, const flo
                             float explore_p, const float *f_table, const float *t_table,
                             int64_t *out_idx, float *out_logp, float *out_f, float *out_t,
                             float *out_logits, void *stream);
+
+/* swarm_policy_mlp_sample, also carrying the last stage of engine e's
+ * deferred build (swarm_engine_defer_build) as extra workgroups of the same
+ * launch when it is pending; same arguments and results otherwise. */
+int swarm_engine_policy_mlp_sample(swarm_engine_t *e, const float *obs, int32_t n,
+                                   int32_t d_in, const float *w1, const float *b1,
+                                   int32_t hidden, const float *w2, const float *b2,
+                                   int32_t k, uint64_t seed, uint64_t *state,
+                                   int32_t n_state, float explore_p, const float *f_table,
+                                   const float *t_table, int64_t *out_idx, float *out_logp,
+                                   float *out_f, float *out_t, float *out_logits,
+                                   void *stream);
 
 /* Kernel timing for measurement (bench.py's roofline of the PPO update):
  * the summed duration (ms) and count of the k_ppo_grads launches this

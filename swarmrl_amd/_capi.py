@@ -141,6 +141,12 @@ _SIGNATURES = {
         [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_int32, _P, _P, ctypes.c_int32,
          ctypes.c_uint64, _P, ctypes.c_int32, ctypes.c_float, _P, _P, _P, _P, _P, _P, _P, _P],
     ),
+    "swarm_engine_policy_mlp_sample": (
+        ctypes.c_int,
+        [_P, _P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_int32, _P, _P, ctypes.c_int32,
+         ctypes.c_uint64, _P, ctypes.c_int32, ctypes.c_float, _P, _P, _P, _P, _P, _P, _P, _P],
+    ),
+    "swarm_engine_defer_build": (ctypes.c_int, [_P, _P]),
     "swarm_ppo_workspace_bytes": (
         ctypes.c_int64,
         [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32],

@@ -45,6 +45,16 @@ class ActorCriticAgent(Agent):
     def __name__(self) -> str:
         return "ActorCriticAgent"
 
+    def absorbs_build(self) -> bool:
+        """True when this agent's device calc_action launches the engine-bound
+        kernels a deferred cluster build rides along in (the vision cone, then
+        the one-kernel policy): SwarmEngine then defers the build instead of
+        forking it onto a second stream."""
+        from swarmrl_amd.observables.subdivided_vision_cones import SubdividedVisionCones
+
+        return (isinstance(self.observable, SubdividedVisionCones)
+                and getattr(self.network, "accepts_engine", False))
+
     def supports_device(self) -> bool:
         ok = getattr(self.observable, "supports_device", False) and getattr(
             self.task, "supports_device", False
@@ -107,7 +117,11 @@ class ActorCriticAgent(Agent):
             _, ftab, ttab, has_dir = self._action_tables(colloids.device)
             fused = getattr(self.network, "fused_sampling_ok", None)
             if fused is not None and fused(flat):
-                idx, logp, f_act, t_act = self.network.compute_action_fused(flat, ftab, ttab)
+                if getattr(self.network, "accepts_engine", False):
+                    idx, logp, f_act, t_act = self.network.compute_action_fused(
+                        flat, ftab, ttab, engine=colloids.engine._native)
+                else:
+                    idx, logp, f_act, t_act = self.network.compute_action_fused(flat, ftab, ttab)
                 f_act, t_act = f_act.reshape(E, A), t_act.reshape(E, A)
             else:
                 idx, logp = self.network.compute_action(observables=flat)

@@ -220,15 +220,32 @@ __device__ __forceinline__ int vision_rec_type(uint32_t w) { return (int)(w >> 2
 // Vision grid: counting sort of every env into cells of side >= vision range,
 // writing cell-sorted records so a candidate cell is one contiguous run; the
 // env-0 workgroup also inverts the agent list (agent_row).
-__global__ __launch_bounds__(1024) void k_vision_grid(DevState st, swarm_vision_params_t vp,
-                                                      int lx, int ly,
-                                                      const float* __restrict__ radii,
-                                                      const int32_t* __restrict__ types,
-                                                      const int32_t* __restrict__ agents,
-                                                      int n_agents,
-                                                      int32_t* __restrict__ start, VisionSorted vs) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
+// The vision-cone launch arguments (one struct, so fused launches carry it).
+struct VisionArgs {
+  swarm_vision_params_t vp;
+  int lx, ly;
+  const float* radii;
+  const int32_t* types;
+  const int32_t* agents;
+  int n_agents;
+  int32_t* start;
+  VisionSorted vs;
+  float* out;
+  int n_envs;
+};
+
+// Body for the workgroup of env e (k_vision_grid, or k_vgrid_sort).
+__device__ __forceinline__ void vision_grid_body(const DevState& st, const VisionArgs& va, int e,
+                                                 unsigned char* smem) {
+  const swarm_vision_params_t& vp = va.vp;
+  const int lx = va.lx, ly = va.ly;
+  const float* __restrict__ radii = va.radii;
+  const int32_t* __restrict__ types = va.types;
+  const int32_t* __restrict__ agents = va.agents;
+  const int n_agents = va.n_agents;
+  int32_t* __restrict__ start = va.start;
+  const VisionSorted& vs = va.vs;
+  const int T = blockDim.x, tid = threadIdx.x, N = st.n;
   const int ncell = 1 << (lx + ly);
   int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
   int32_t* cnt = wave_sums + 16;
@@ -295,6 +312,11 @@ __global__ __launch_bounds__(1024) void k_vision_grid(DevState st, swarm_vision_
     vs.rec[2 * pos] = make_uint4(qx, qy, (uint32_t)st.img[g], (uint32_t)st.img[M + g]);
     vs.rec[2 * pos + 1] = make_uint4(__float_as_uint(radii[i]), vision_id_word(i, ti), st.ang[g], 0u);
   }
+}
+
+__global__ __launch_bounds__(1024) void k_vision_grid(DevState st, VisionArgs va) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  vision_grid_body(st, va, blockIdx.x, smem);
 }
 
 // ---------------------------------------------------------- vision cone
@@ -408,23 +430,28 @@ __device__ __forceinline__ void vision_drain(const VisionLane& L, const swarm_vi
 // candidate, tested on its unwrapped (int64) separation.
 // xcd_bpe > 0: blocks placed on XCDs by env (swarm::xcd_env_block, xcd_bpe
 // blocks per env), so the records an env's agents read stay in one L2.
+// Body for block vb (k_vision, or a workgroup of k_vision_pairs); hits: the
+// block's [kVisionHits][256] LDS hit lists (blockDim 256).
 template <int NB, int G, bool kAll = false>
-__global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __restrict__ d,
-                                                swarm_vision_params_t vp, int lx, int ly,
-                                                const int32_t* __restrict__ start, VisionSorted vs,
-                                                int n_agents, float* __restrict__ out,
-                                                int n_envs, int xcd_bpe) {
-  __shared__ uint32_t hits[kVisionHits][256];
+__device__ __forceinline__ void vision_body(const DevState& st, const Derived* __restrict__ d,
+                                            const VisionArgs& va, int vb, int xcd_bpe,
+                                            uint32_t (*hits)[256]) {
+  const swarm_vision_params_t& vp = va.vp;
+  const int lx = va.lx, ly = va.ly;
+  const int32_t* __restrict__ start = va.start;
+  const VisionSorted& vs = va.vs;
+  const int n_agents = va.n_agents, n_envs = va.n_envs;
+  float* __restrict__ out = va.out;
   const int N = st.n;
   const int sub = threadIdx.x & (G - 1);
   int e, ps;
   if (xcd_bpe > 0) {
     int lb;
-    if (!swarm::xcd_env_block((int)blockIdx.x, xcd_bpe, n_envs, &e, &lb)) return;
+    if (!swarm::xcd_env_block(vb, xcd_bpe, n_envs, &e, &lb)) return;
     ps = (lb * (int)blockDim.x + (int)threadIdx.x) / G;
     if (ps >= N) return;  // whole groups only (G divides 64)
   } else {
-    const int grp = (blockIdx.x * blockDim.x + threadIdx.x) / G;
+    const int grp = (vb * (int)blockDim.x + (int)threadIdx.x) / G;
     if (grp >= n_envs * N) return;
     e = grp / N;
     ps = grp - e * N;
@@ -525,6 +552,63 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
 #pragma unroll
   for (int k = 0; k < NB; ++k)
     if (k < nb) o[k] = (float)acc[k] * 2.3283064365386963e-10f;
+}
+
+template <int NB, int G, bool kAll = false>
+__global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __restrict__ d,
+                                                VisionArgs va, int xcd_bpe) {
+  __shared__ uint32_t hits[kVisionHits][256];
+  vision_body<NB, G, kAll>(st, d, va, blockIdx.x, xcd_bpe, hits);
+}
+
+// ------------------------------------------- build stages riding along
+// Latency-bound engines (swarm_engine_defer_build): the next window's
+// cluster decomposition does not fork onto a second stream; its three
+// stages ride along in the slice's observable and policy launches instead,
+// as extra workgroups of the same kernels (no graph fork/join edges, no
+// launch of their own):
+//   k_vgrid_sort     the vision grid's env workgroups + k_build_sort's
+//   k_vision_pairs   the vision cone's blocks + k_build_pairs's
+//   k_policy_cbuild  the policy's blocks (1024 threads) + k_cluster_build's
+// Each stage needs the previous one complete, which the launch order on
+// the engine stream guarantees.
+template <int CH>
+__global__ __launch_bounds__(1024) void k_vgrid_sort(DevState st, VisionArgs va, Scratch sc,
+                                                     int lxb, int lyb) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int b = blockIdx.x;
+  if (b < va.n_envs)
+    vision_grid_body(st, va, b, smem);
+  else
+    swarm::build_sort_body<CH>(st, sc, lxb, lyb, b - va.n_envs, smem);
+}
+
+template <int NB, int G>
+__global__ __launch_bounds__(256) void k_vision_pairs(DevState st, const Derived* __restrict__ d,
+                                                      VisionArgs va, int n_vblocks, Scratch sc,
+                                                      int lxb, int lyb, int pair_bx) {
+  __shared__ uint32_t hits[kVisionHits][256];
+  __shared__ float nb2[swarm::kMaxSpecies * swarm::kMaxSpecies];
+  const int b = blockIdx.x;
+  if (b < n_vblocks) {
+    vision_body<NB, G, false>(st, d, va, b, 0, hits);
+  } else {
+    const int pb = b - n_vblocks;
+    swarm::build_pairs_body(d, st, sc, lxb, lyb, pb % pair_bx, pb / pair_bx, nb2);
+  }
+}
+
+template <int G, int D, int K>
+__global__ __launch_bounds__(1024) void k_policy_cbuild(swarm::MlpArgs m, int n_pblocks,
+                                                        DevState st, Scratch sc) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int b = blockIdx.x;
+  if (b < n_pblocks) {
+    swarm::policy_body<G, D, K>(m, b, reinterpret_cast<float*>(smem));
+  } else {
+    const int e = b - n_pblocks;
+    swarm::cluster_build_env<false, true>(st, sc, e, smem, sc.gnpairs[e]);
+  }
 }
 
 // ------------------------------------------- neighbour reductions (fp64)
@@ -847,6 +931,10 @@ struct swarm_engine {
   // swarm_engine_prebuild: the next window's build (and noise table) were
   // launched ahead on another stream from the current positions
   bool prebuilt = false;
+  // swarm_engine_defer_build: the next stage of the deferred three-launch
+  // build (1 sort, 2 pairs, 3 cluster build; 0 none) that rides along in the
+  // next observable / policy launch; flushed before a window runs
+  int ride_stage = 0;
   // swarm_engine_prebuild_noise: the next window's noise table for this many
   // sub-steps was launched ahead (on a stream of the caller's)
   int prebuilt_noise_steps = 0;
@@ -940,7 +1028,10 @@ void set_lds_attributes() {
                        reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<false, false>),
                        reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<true, false>),
                        reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<false, true>),
-                       reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<true, true>)};
+                       reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<true, true>),
+                       reinterpret_cast<const void*>(&k_vgrid_sort<4>),
+                       reinterpret_cast<const void*>(&k_vgrid_sort<16>),
+                       reinterpret_cast<const void*>(&k_policy_cbuild<4, 4, 4>)};
   for (const void* f : fns)
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
   (void)hipGetLastError();
@@ -1028,6 +1119,34 @@ int launch_build(swarm_engine* e, hipStream_t stream) {
     hipLaunchKernelGGL(swarm::k_cluster_build<false>, dim3(e->n_envs), dim3(1024),
                        build_lds_bytes(e->n, e->sc.pair_cap), stream, e->st, e->sc);
   HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+
+// Launch the deferred build's pending stages on the engine stream (no
+// consumer carried them along); the window then uses the build.
+int flush_ride_along(swarm_engine* e) {
+  const int stage = e->ride_stage;
+  if (stage == 0) return SWARM_OK;
+  e->ride_stage = 0;
+  const int ncb = 1 << (e->lxb + e->lyb);
+  if (stage <= 1) {
+    if (e->n > 4096)
+      hipLaunchKernelGGL(swarm::k_build_sort<16>, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4,
+                         e->stream, e->st, e->sc, e->lxb, e->lyb);
+    else
+      hipLaunchKernelGGL(swarm::k_build_sort<4>, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4,
+                         e->stream, e->st, e->sc, e->lxb, e->lyb);
+    HIP_TRY(hipGetLastError());
+  }
+  if (stage <= 2) {
+    hipLaunchKernelGGL(swarm::k_build_pairs, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
+                       dim3(256), 0, e->stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb);
+    HIP_TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(swarm::k_cluster_build<false>, dim3(e->n_envs), dim3(1024),
+                     build_lds_bytes(e->n, e->sc.pair_cap), e->stream, e->st, e->sc);
+  HIP_TRY(hipGetLastError());
+  e->prebuilt = true;
   return SWARM_OK;
 }
 
@@ -1222,6 +1341,10 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
 }
 
 int run_bd(swarm_engine* e, int n_steps) {
+  if (e->ride_stage > 0) {  // a deferred build no launch carried along
+    const int rc = flush_ride_along(e);
+    if (rc) return rc;
+  }
   bool pre = e->prebuilt;
   int noise_ready = e->prebuilt_noise_steps;
   e->prebuilt = false;
@@ -1582,7 +1705,7 @@ int swarm_engine_set_stream(swarm_engine_t* e, void* stream) {
 
 int swarm_engine_upload_raw(swarm_engine_t* e, const uint32_t* q, const int32_t* img,
                             const uint32_t* ang) {
-  if (e) e->prebuilt = false, e->prebuilt_noise_steps = 0;
+  if (e) e->prebuilt = false, e->prebuilt_noise_steps = 0, e->ride_stage = 0;
   if (!e || !q || !img || !ang) return fail(SWARM_EINVAL, "null argument");
   const size_t M = (size_t)e->st.m;
   HIP_TRY(hipMemcpyAsync(e->st.q, q, 3 * M * sizeof(uint32_t), hipMemcpyHostToDevice, e->stream));
@@ -1735,6 +1858,7 @@ int swarm_engine_set_directors(swarm_engine_t* e, const double* dir, const uint8
 int swarm_engine_remove_overlap(swarm_engine_t* e, int32_t n_steps, double gamma, double max_disp) {
   if (!e) return fail(SWARM_EINVAL, "null engine");
   e->prebuilt = false;
+  e->ride_stage = 0;
   e->prebuilt_noise_steps = 0;
   if (n_steps <= 0) return SWARM_OK;
   return launch_global(e, n_steps, 1, (float)gamma, (float)max_disp);
@@ -1788,6 +1912,7 @@ int swarm_engine_time_run(swarm_engine_t* e, int32_t n_steps, int32_t reps, doub
     HIP_TRY(hipDeviceSynchronize());
     e->prebuilt = false;
   }
+  e->ride_stage = 0;  // a deferred build is superseded by the one below
   int rc = launch_build(e, e->stream);
   if (!rc && e->noise_table && !e->next_table_ready) rc = launch_noise(e, e->stream, n_steps);
   if (rc) return rc;
@@ -2018,21 +2143,54 @@ int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const 
   cell_grid(e->params, e->n, (double)vp->vision_range, &lx, &ly);
   int rc = ensure_grid_scratch(e, lx, ly);
   if (rc) return rc;
-  {
-    const int ncell = 1 << (lx + ly);
-    const size_t lds = 16 * 4 + (size_t)(ncell + 1) * 4;
-    if (lds > kMaxLds) return fail(SWARM_ECAPACITY, "observable cell grid too large");
-    hipLaunchKernelGGL(k_vision_grid, dim3(e->n_envs), dim3(1024), lds, e->stream, e->st, *vp,
-                       lx, ly, radii, types, agent_idx, n_agents, e->d_start, e->vs);
-    HIP_TRY(hipGetLastError());
-  }
+  const VisionArgs va{*vp, lx, ly, radii, types, agent_idx, n_agents, e->d_start, e->vs, out,
+                      e->n_envs};
   const long total = (long)e->n * e->n_envs;  // one group per sorted particle
   const int nb = vp->n_cones * vp->n_types;
+  // lanes per agent: enough threads to give every SIMD a few waves, few
+  // enough that the lanes of a wave stay busy (measured, tools/vision_time.py:
+  // 64 x 4096 agents 107 -> 93 us with G = 4 instead of 1)
+  int G = total >= (1L << 15) ? 4 : 16;
+  if (const char* og = std::getenv("SWARMRL_AMD_VISION_G")) {
+    const int v = std::atoi(og);
+    if (v == 4 || v == 16) G = v;
+  }
+  // a deferred build rides along in the grid and cone launches (stages 1, 2)
+  // when their fused variants apply; else its pending stages launch first
+  const bool ride = e->ride_stage == 1 && !all && nb <= 4 && G == 16;
+  if (e->ride_stage > 0 && !ride) {
+    rc = flush_ride_along(e);
+    if (rc) return rc;
+  }
+  const int ncell = 1 << (lx + ly);
+  const size_t glds = 16 * 4 + (size_t)(ncell + 1) * 4;
+  if (glds > kMaxLds) return fail(SWARM_ECAPACITY, "observable cell grid too large");
+  if (ride) {
+    const size_t slds = (16 + (size_t)(1 << (e->lxb + e->lyb)) + 1) * 4;
+    const dim3 grid((unsigned)(2 * e->n_envs));
+    if (e->n > 4096)
+      hipLaunchKernelGGL(k_vgrid_sort<16>, grid, dim3(1024), std::max(glds, slds), e->stream,
+                         e->st, va, e->sc, e->lxb, e->lyb);
+    else
+      hipLaunchKernelGGL(k_vgrid_sort<4>, grid, dim3(1024), std::max(glds, slds), e->stream,
+                         e->st, va, e->sc, e->lxb, e->lyb);
+    HIP_TRY(hipGetLastError());
+    const int nvb = (int)((total * 16 + 255) / 256);
+    const int pbx = (e->n + 255) / 256;
+    hipLaunchKernelGGL((k_vision_pairs<4, 16>), dim3((unsigned)(nvb + pbx * e->n_envs)),
+                       dim3(256), 0, e->stream, e->st, e->d_derived, va, nvb, e->sc, e->lxb,
+                       e->lyb, pbx);
+    HIP_TRY(hipGetLastError());
+    e->ride_stage = 3;
+    return SWARM_OK;
+  }
+  hipLaunchKernelGGL(k_vision_grid, dim3(e->n_envs), dim3(1024), glds, e->stream, e->st, va);
+  HIP_TRY(hipGetLastError());
   if (all) {
     const dim3 agrid((unsigned)((total * 16 + 255) / 256)), ablock(256);
-#define SWARM_VALL(NBV)                                                                         \
+#define SWARM_VALL(NBV)                                                                          \
   hipLaunchKernelGGL((k_vision<NBV, 16, true>), agrid, ablock, 0, e->stream, e->st, e->d_derived, \
-                     *vp, lx, ly, e->d_start, e->vs, n_agents, out, e->n_envs, 0)
+                     va, 0)
     if (nb <= 4) {
       SWARM_VALL(4);
     } else if (nb <= 8) {
@@ -2046,23 +2204,15 @@ int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const 
     HIP_TRY(hipGetLastError());
     return SWARM_OK;
   }
-  // lanes per agent: enough threads to give every SIMD a few waves, few
-  // enough that the lanes of a wave stay busy (measured, tools/vision_time.py:
-  // 64 x 4096 agents 107 -> 93 us with G = 4 instead of 1)
-  int G = total >= (1L << 15) ? 4 : 16;
-  if (const char* og = std::getenv("SWARMRL_AMD_VISION_G")) {
-    const int v = std::atoi(og);
-    if (v == 4 || v == 16) G = v;
-  }
   // XCD-aware env placement once the envs fill the eight XCDs (as k_cluster_run)
   const int E = e->n_envs;
   const int bpe = (int)(((long)e->n * G + 255) / 256);
   const bool xcd = e->xcd_map && E >= 8 && (E % 8 == 0 || E >= 64);
   const dim3 grid((unsigned)(xcd ? 8L * ((E + 7) / 8) * bpe : (total * G + 255) / 256)),
       block(256);
-#define SWARM_VISION(NBV, GV)                                                              \
-  hipLaunchKernelGGL((k_vision<NBV, GV>), grid, block, 0, e->stream, e->st, e->d_derived, *vp, \
-                     lx, ly, e->d_start, e->vs, n_agents, out, e->n_envs, xcd ? bpe : 0)
+#define SWARM_VISION(NBV, GV)                                                                  \
+  hipLaunchKernelGGL((k_vision<NBV, GV>), grid, block, 0, e->stream, e->st, e->d_derived, va, \
+                     xcd ? bpe : 0)
 #define SWARM_VISION_G(NBV) \
   if (G == 4)               \
     SWARM_VISION(NBV, 4);   \
@@ -2262,12 +2412,15 @@ int swarm_sample_actions(const float* logits, int32_t n, int32_t k, uint64_t see
   return SWARM_OK;
 }
 
-int swarm_policy_mlp_sample(const float* obs, int32_t n, int32_t d_in, const float* w1,
-                            const float* b1, int32_t hidden, const float* w2, const float* b2,
-                            int32_t k, uint64_t seed, uint64_t* state, int32_t n_state,
-                            float explore_p, const float* f_table, const float* t_table,
-                            int64_t* out_idx, float* out_logp, float* out_f, float* out_t,
-                            float* out_logits, void* stream) {
+namespace {
+// The rollout policy launch (swarm_policy_mlp_sample); ride: the engine whose
+// deferred build's last stage (the cluster build) rides along as extra
+// workgroups of the same launch (k_policy_cbuild), or null.
+int policy_launch(const float* obs, int32_t n, int32_t d_in, const float* w1, const float* b1,
+                  int32_t hidden, const float* w2, const float* b2, int32_t k, uint64_t seed,
+                  uint64_t* state, int32_t n_state, float explore_p, const float* f_table,
+                  const float* t_table, int64_t* out_idx, float* out_logp, float* out_f,
+                  float* out_t, float* out_logits, void* stream, swarm_engine* ride) {
   if (!obs || !w1 || !b1 || !w2 || !b2 || !state || !f_table || !t_table || !out_idx ||
       !out_logp || !out_f || !out_t)
     return fail(SWARM_EINVAL, "null argument");
@@ -2286,11 +2439,29 @@ int swarm_policy_mlp_sample(const float* obs, int32_t n, int32_t d_in, const flo
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   auto* st = reinterpret_cast<unsigned long long*>(state);
+  const swarm::MlpArgs m{obs,   n,          d_in,    w1,      b1,       hidden, w2,
+                         b2,    k,          k0,      k1,      st,       explore_p, f_table,
+                         t_table, out_idx,  out_logp, out_f,  out_t,    out_logits};
+  if (ride && ride->ride_stage == 3 && G == 4 && small_in && small_k) {
+    // policy blocks of 1024 threads (256 agents: whole counter groups) and
+    // one cluster-build workgroup per env
+    const int pblocks = (int)(((long)n * G + 1023) / 1024);
+    const size_t plds = (size_t)(hidden * swarm::MlpRow<4, 4>::kStride + 4) * sizeof(float);
+    const size_t lds = std::max(plds, build_lds_bytes(ride->n, ride->sc.pair_cap));
+    hipLaunchKernelGGL((k_policy_cbuild<4, 4, 4>), dim3((unsigned)(pblocks + ride->n_envs)),
+                       dim3(1024), lds, s, m, pblocks, ride->st, ride->sc);
+    HIP_TRY(hipGetLastError());
+    ride->ride_stage = 0;
+    ride->prebuilt = true;
+    return SWARM_OK;
+  }
+  if (ride && ride->ride_stage > 0) {
+    const int rc = flush_ride_along(ride);
+    if (rc) return rc;
+  }
 #define SWARM_MLP(GG, DD, KK)                                                                   \
   hipLaunchKernelGGL((swarm::k_policy_mlp_sample<GG, DD, KK>), dim3(blocks), dim3(256),        \
-                     (size_t)(hidden * swarm::MlpRow<DD, KK>::kStride + KK) * sizeof(float), s, \
-                     obs, n, d_in, w1, b1, hidden, w2, b2, k, k0, k1, st, explore_p, f_table,  \
-                     t_table, out_idx, out_logp, out_f, out_t, out_logits)
+                     (size_t)(hidden * swarm::MlpRow<DD, KK>::kStride + KK) * sizeof(float), s, m)
 #define SWARM_MLP_G(GG)                 \
   do {                                  \
     if (small_in && small_k)            \
@@ -2311,6 +2482,46 @@ int swarm_policy_mlp_sample(const float* obs, int32_t n, int32_t d_in, const flo
 #undef SWARM_MLP_G
 #undef SWARM_MLP
   HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+}  // namespace
+
+int swarm_policy_mlp_sample(const float* obs, int32_t n, int32_t d_in, const float* w1,
+                            const float* b1, int32_t hidden, const float* w2, const float* b2,
+                            int32_t k, uint64_t seed, uint64_t* state, int32_t n_state,
+                            float explore_p, const float* f_table, const float* t_table,
+                            int64_t* out_idx, float* out_logp, float* out_f, float* out_t,
+                            float* out_logits, void* stream) {
+  return policy_launch(obs, n, d_in, w1, b1, hidden, w2, b2, k, seed, state, n_state, explore_p,
+                       f_table, t_table, out_idx, out_logp, out_f, out_t, out_logits, stream,
+                       nullptr);
+}
+
+int swarm_engine_policy_mlp_sample(swarm_engine_t* e, const float* obs, int32_t n, int32_t d_in,
+                                   const float* w1, const float* b1, int32_t hidden,
+                                   const float* w2, const float* b2, int32_t k, uint64_t seed,
+                                   uint64_t* state, int32_t n_state, float explore_p,
+                                   const float* f_table, const float* t_table, int64_t* out_idx,
+                                   float* out_logp, float* out_f, float* out_t, float* out_logits,
+                                   void* stream) {
+  if (!e) return fail(SWARM_EINVAL, "null engine");
+  return policy_launch(obs, n, d_in, w1, b1, hidden, w2, b2, k, seed, state, n_state, explore_p,
+                       f_table, t_table, out_idx, out_logp, out_f, out_t, out_logits, stream, e);
+}
+
+int swarm_engine_defer_build(swarm_engine_t* e, int32_t* deferred) {
+  if (!e || !deferred) return fail(SWARM_EINVAL, "null argument");
+  *deferred = 0;
+  // the three-launch 2-D cluster build of a latency-bound engine only (the
+  // stages the fused observable / policy launches know how to carry)
+  const bool ok = e->cluster_path && !e->nlist_path && !e->env_build && !e->big_build &&
+                  e->params.n_dims == 2 && e->wide_run &&
+                  !(std::getenv("SWARMRL_AMD_RIDE_ALONG") &&
+                    std::getenv("SWARMRL_AMD_RIDE_ALONG")[0] == '0');
+  if (!ok) return SWARM_OK;
+  e->prebuilt = false;
+  e->ride_stage = 1;
+  *deferred = 1;
   return SWARM_OK;
 }
 

@@ -967,10 +967,12 @@ __host__ __device__ inline size_t build_lds_words(int n, int pair_cap) {
 
 // Build step 1, one workgroup per env: counting sort into cells of side
 // >= rc_max + skin (global arrays for the chip-wide pair search).
+// The body runs in the workgroup of env e (k_build_sort, or a workgroup of a
+// fused launch that carries the build along: k_vgrid_sort).
 template <int CH>  // particles per thread kept in registers across the scan (4, or 16 above 4096)
-__global__ __launch_bounds__(1024) void k_build_sort(DevState st, Scratch sc, int lx, int ly) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
+__device__ __forceinline__ void build_sort_body(const DevState& st, const Scratch& sc, int lx,
+                                                int ly, int e, unsigned char* smem) {
+  const int T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly);
   int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
@@ -1029,6 +1031,12 @@ __global__ __launch_bounds__(1024) void k_build_sort(DevState st, Scratch sc, in
   SWARM_STAMP(5);
 }
 
+template <int CH>
+__global__ __launch_bounds__(1024) void k_build_sort(DevState st, Scratch sc, int lx, int ly) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  build_sort_body<CH>(st, sc, lx, ly, blockIdx.x, smem);
+}
+
 // Build step 2, chip-wide (grid.y = env, one thread per sorted entry): every
 // pair within r_i + r_j + skin once (i < j).  A stencil row (cells x-1..x+1)
 // is one contiguous sorted range, plus a wrap range at the grid edge.  The
@@ -1036,13 +1044,15 @@ __global__ __launch_bounds__(1024) void k_build_sort(DevState st, Scratch sc, in
 // memory latencies per thread, not one per candidate); up to kKeep pairs per
 // thread stay in registers, one atomic per wave reserves the output, and a
 // wave with a denser thread rescans to write.
-__global__ __launch_bounds__(256) void k_build_pairs(const Derived* __restrict__ d, DevState st,
-                                                     Scratch sc, int lx, int ly) {
+// Body for block bx of env e (k_build_pairs: grid (ceil(N / blockDim), E);
+// fused launches pass their own block index); nb2: a block-shared table.
+__device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, const DevState& st,
+                                                 const Scratch& sc, int lx, int ly, int bx, int e,
+                                                 float* nb2) {
   constexpr int kKeep = 8;
-  __shared__ float nb2[kMaxSpecies * kMaxSpecies];
   for (int k = threadIdx.x; k < kMaxSpecies * kMaxSpecies; k += blockDim.x) nb2[k] = d->nb2[k];
-  const int e = blockIdx.y, N = st.n;
-  const int ps = blockIdx.x * blockDim.x + threadIdx.x;
+  const int N = st.n;
+  const int ps = bx * blockDim.x + threadIdx.x;
   const bool valid = ps < N;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly);
@@ -1143,6 +1153,12 @@ __global__ __launch_bounds__(256) void k_build_pairs(const Derived* __restrict__
       }
     }
   }
+}
+
+__global__ __launch_bounds__(256) void k_build_pairs(const Derived* __restrict__ d, DevState st,
+                                                     Scratch sc, int lx, int ly) {
+  __shared__ float nb2[kMaxSpecies * kMaxSpecies];
+  build_pairs_body(d, st, sc, lx, ly, blockIdx.x, blockIdx.y, nb2);
 }
 
 // LDS words of the large-N variant: the union-find forest only.

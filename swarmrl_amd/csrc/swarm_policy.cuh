@@ -184,15 +184,48 @@ struct MlpRow {
 // One agent per G lanes; lane `sub` of an agent takes hidden units
 // j = sub, sub + G, ...; the partial logits are summed with xor-shuffles.
 // D, K: padded widths of the observable and of the action set.
+// The policy's launch arguments (one struct, so fused launches can carry it).
+struct MlpArgs {
+  const float* obs;
+  int n, d_in;
+  const float* w1;
+  const float* b1;
+  int hidden;
+  const float* w2;
+  const float* b2;
+  int k;
+  uint32_t key0, key1;
+  unsigned long long* state;
+  float explore_p;
+  const float* ftab;
+  const float* ttab;
+  int64_t* out_idx;
+  float* out_logp;
+  float* out_f;
+  float* out_t;
+  float* out_logits;
+};
+
+// Body for block vb of the policy (k_policy_mlp_sample, or a workgroup of a
+// fused launch: k_policy_cbuild); sw: the block's dynamic LDS.
 template <int G, int D, int K>
-__global__ __launch_bounds__(256) void k_policy_mlp_sample(
-    const float* __restrict__ obs, int n, int d_in, const float* __restrict__ w1,
-    const float* __restrict__ b1, int hidden, const float* __restrict__ w2,
-    const float* __restrict__ b2, int k, uint32_t key0, uint32_t key1,
-    unsigned long long* __restrict__ state, float explore_p, const float* __restrict__ ftab,
-    const float* __restrict__ ttab, int64_t* __restrict__ out_idx, float* __restrict__ out_logp,
-    float* __restrict__ out_f, float* __restrict__ out_t, float* __restrict__ out_logits) {
-  extern __shared__ __align__(16) float sw[];
+__device__ __forceinline__ void policy_body(const MlpArgs& m, int vb, float* sw) {
+  const float* __restrict__ obs = m.obs;
+  const int n = m.n, d_in = m.d_in, hidden = m.hidden, k = m.k;
+  const float* __restrict__ w1 = m.w1;
+  const float* __restrict__ b1 = m.b1;
+  const float* __restrict__ w2 = m.w2;
+  const float* __restrict__ b2 = m.b2;
+  const uint32_t key0 = m.key0, key1 = m.key1;
+  unsigned long long* __restrict__ state = m.state;
+  const float explore_p = m.explore_p;
+  const float* __restrict__ ftab = m.ftab;
+  const float* __restrict__ ttab = m.ttab;
+  int64_t* __restrict__ out_idx = m.out_idx;
+  float* __restrict__ out_logp = m.out_logp;
+  float* __restrict__ out_f = m.out_f;
+  float* __restrict__ out_t = m.out_t;
+  float* __restrict__ out_logits = m.out_logits;
   constexpr int R = MlpRow<D, K>::kStride;
   for (int t = threadIdx.x; t < hidden * R; t += blockDim.x) {
     const int j = t / R, c = t - j * R;
@@ -209,7 +242,7 @@ __global__ __launch_bounds__(256) void k_policy_mlp_sample(
   }
   float* sb2 = sw + hidden * R;
   if (threadIdx.x < K) sb2[threadIdx.x] = (int)threadIdx.x < k ? b2[threadIdx.x] : 0.0f;
-  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int gt = vb * blockDim.x + threadIdx.x;
   const int a = gt / G, sub = gt & (G - 1);
   const bool valid = a < n;
   const unsigned long long ctr = valid ? state[a >> 6] : 0ull;
@@ -259,6 +292,12 @@ __global__ __launch_bounds__(256) void k_policy_mlp_sample(
     }
   }
   advance_group_counter(state, a, n, sub == 0, ctr);
+}
+
+template <int G, int D, int K>
+__global__ __launch_bounds__(256) void k_policy_mlp_sample(MlpArgs m) {
+  extern __shared__ __align__(16) float sw[];
+  policy_body<G, D, K>(m, blockIdx.x, sw);
 }
 
 }  // namespace swarm

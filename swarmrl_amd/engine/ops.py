@@ -332,12 +332,15 @@ def sample_actions(logits: torch.Tensor, seed: int, state: torch.Tensor, explore
 
 def policy_mlp_sample(obs: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor,
                       b2: torch.Tensor, seed: int, state: torch.Tensor, explore_p: float,
-                      f_table: torch.Tensor, t_table: torch.Tensor, want_logits: bool = False):
+                      f_table: torch.Tensor, t_table: torch.Tensor, want_logits: bool = False,
+                      engine=None):
     """
     The rollout policy in one kernel (swarm_policy_mlp_sample): actor logits
     W2 relu(W1 obs + b1) + b2 from the torch Linear weights in place, then the
     sampling of sample_actions (same counters and bits).  obs [n, d_in] fp32
-    device.  Returns (idx, log_prob, f_swim, torque_z[, logits]).
+    device.  Returns (idx, log_prob, f_swim, torque_z[, logits]).  engine: a
+    native engine whose deferred build's last stage rides along in the same
+    launch (swarm_engine_policy_mlp_sample); same results.
     """
     obs = obs.contiguous()
     n, d_in = obs.shape
@@ -349,12 +352,15 @@ def policy_mlp_sample(obs: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2:
     t = torch.empty(n, dtype=torch.float32, device=dev)
     logits = torch.empty(n, k, dtype=torch.float32, device=dev) if want_logits else None
     stream = torch.cuda.current_stream(dev).cuda_stream
-    _capi.check(_capi.lib().swarm_policy_mlp_sample(
-        obs.data_ptr(), n, d_in, w1.data_ptr(), b1.data_ptr(), hidden, w2.data_ptr(),
-        b2.data_ptr(), k, ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), state.data_ptr(),
-        int(state.numel()), ctypes.c_float(explore_p), f_table.data_ptr(), t_table.data_ptr(),
-        idx.data_ptr(), logp.data_ptr(), f.data_ptr(), t.data_ptr(),
-        logits.data_ptr() if want_logits else None, ctypes.c_void_p(stream)))
+    args = (obs.data_ptr(), n, d_in, w1.data_ptr(), b1.data_ptr(), hidden, w2.data_ptr(),
+            b2.data_ptr(), k, ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), state.data_ptr(),
+            int(state.numel()), ctypes.c_float(explore_p), f_table.data_ptr(), t_table.data_ptr(),
+            idx.data_ptr(), logp.data_ptr(), f.data_ptr(), t.data_ptr(),
+            logits.data_ptr() if want_logits else None, ctypes.c_void_p(stream))
+    if engine is not None:
+        _capi.check(_capi.lib().swarm_engine_policy_mlp_sample(engine.ptr, *args))
+    else:
+        _capi.check(_capi.lib().swarm_policy_mlp_sample(*args))
     if want_logits:
         return idx, logp, f, t, logits
     return idx, logp, f, t

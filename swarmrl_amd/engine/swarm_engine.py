@@ -283,6 +283,11 @@ class SwarmEngine(Engine):
         self.overlap_build = os.environ.get("SWARMRL_AMD_OVERLAP_BUILD", "1") != "0"
         # fork the next slice's build right after the run (before the reward)
         self.early_fork = os.environ.get("SWARMRL_AMD_EARLY_FORK", "1") != "0"
+        # latency-bound engines: the next window's build rides along in the
+        # vision-cone and policy launches instead of a forked side stream
+        # (swarm_engine_defer_build; the engine declines when it cannot)
+        self.ride_along_build = os.environ.get("SWARMRL_AMD_RIDE_ALONG", "1") != "0"
+        self._ride_along = False
         self._side_stream = None
         self._prebuild_pending = None
         self.traj_holder = None
@@ -951,6 +956,16 @@ class SwarmEngine(Engine):
         policy kernels of manage_forces; _run joins it.  Positions cannot
         change in between (espresso.py:1253-1306), see swarm_engine_prebuild.
         """
+        if self._ride_along:
+            # the force model's vision-cone and policy launches carry the
+            # three build stages along (swarm_engine_defer_build): no side
+            # stream, fork or join in the slice
+            self._native.bind_stream()
+            deferred = ctypes.c_int32()
+            self._native.call("swarm_engine_defer_build", ctypes.byref(deferred))
+            if deferred.value:
+                self._prebuild_pending = ("ride",)
+                return
         main = torch.cuda.current_stream()
         if self._side_stream is None:
             self._side_stream = torch.cuda.Stream(device=main.device)
@@ -969,6 +984,11 @@ class SwarmEngine(Engine):
         self._prebuild_pending = (side, None, 0)
 
     def _run(self, n_steps: int):
+        if self._prebuild_pending is not None and self._prebuild_pending[0] == "ride":
+            # stages no launch carried along run in swarm_engine_integrate
+            self._prebuild_pending = None
+            self._native.bind_stream()
+            self._native.call("swarm_engine_prebuild_noise", None, int(n_steps))
         if self._prebuild_pending is not None:
             # The noise table (latency-bound engines) runs on the main stream
             # after the policy kernels, ahead of the join: the build usually
@@ -998,6 +1018,9 @@ class SwarmEngine(Engine):
             self.integration_initialised = True
 
         device_path = force_model is not None and self._device_capable(force_model)
+        # ride-along builds (SWARMRL_AMD_RIDE_ALONG=0: fork onto a side stream)
+        self._ride_along = bool(device_path and self.ride_along_build and
+                                getattr(force_model, "absorbs_build", lambda: False)())
         old_slice_idx = self.slice_idx
 
         while self.step_idx < self.params.steps_per_slice * (old_slice_idx + n_slices):

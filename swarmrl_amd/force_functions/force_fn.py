@@ -35,6 +35,11 @@ class ForceFunction:
     def kill_switch(self, value):
         self._kill_switch = value
 
+    def absorbs_build(self) -> bool:
+        """True when an agent's device calc_action carries a deferred cluster
+        build along in its launches (ActorCriticAgent.absorbs_build)."""
+        return any(getattr(a, "absorbs_build", lambda: False)() for a in self.agents.values())
+
     def supports_device(self) -> bool:
         """True when every agent can act on a SwarmView (the GPU fast path)."""
         if len(self.agents) == 0:

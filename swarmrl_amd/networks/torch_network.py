@@ -130,10 +130,16 @@ class TorchModel:
                 and type(self.exploration_policy) is RandomExploration)
 
     @torch.no_grad()
+    # compute_action_fused takes the engine whose deferred build may ride
+    # along in the policy launch (SwarmEngine._prebuild, ride-along mode)
+    accepts_engine = True
+
     def compute_action_fused(self, observables: torch.Tensor, f_table: torch.Tensor,
-                             t_table: torch.Tensor):
+                             t_table: torch.Tensor, engine=None):
         """compute_action + action-table lookup in one sampling kernel:
-        returns (indices, log_probs, f_swim, torque_z) device tensors."""
+        returns (indices, log_probs, f_swim, torque_z) device tensors.
+        engine: the native engine of the slice (its deferred build's last
+        stage rides along in the one-kernel policy launch)."""
         from swarmrl_amd.engine import ops
 
         obs = observables.to(torch.float32)
@@ -143,7 +149,7 @@ class TorchModel:
         layers = self._mlp_layers(obs.shape[1], int(f_table.numel()))
         if layers is not None:  # stock MLP: network + sampling in one kernel
             return ops.policy_mlp_sample(obs, *layers, self._fused_seed, self._fused_state, p,
-                                         f_table, t_table)
+                                         f_table, t_table, engine=engine)
         if hasattr(self.model, "logits"):
             logits = self.model.logits(obs)
         else:

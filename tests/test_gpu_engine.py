@@ -449,6 +449,60 @@ def test_add_walls_2d_engine(tmp_path):
     assert runner.wall_violations() == 0
 
 
+@pytest.mark.parametrize("E,N", [(1, 1024), (8, 1024), (1, 4096)])
+def test_bench_workload_build_modes_bit_identical(E, N):
+    """The bench workload (vision cones, actor-critic sampling, GradientSensing
+    reward) over 4 slices of one integrate call, the next window's cluster
+    build (a) riding along in the vision-cone and policy launches
+    (swarm_engine_defer_build, the default for latency-bound engines),
+    (b) forked onto a side stream beside the observables and policy, (c) in
+    the serial single-stream slice: the same positions, observables, actions
+    and rewards, bit for bit.  Also (d) the ride-along episode captured in a
+    HIP graph and replayed."""
+    import argparse
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    dev = torch.device("cuda", 0)
+    out = []
+    for mode in ("ride", "fork", "serial", "graph"):
+        ns = argparse.Namespace(colloids=N, envs_per_gpu=E)
+        eng, ff, agent = bench.build_workload(ns, 7, dev)
+        eng.overlap_build = mode != "serial"
+        eng.ride_along_build = mode in ("ride", "graph")
+        if mode == "graph":
+            eng.integrate(1, ff)  # set-up, overlap removal (eager), first slice
+            st0 = eng.get_raw_state()
+            agent.reset_trajectory()
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                eng.integrate(3, ff)
+            # capture does not run the work: restart from the first slice's state
+            eng.set_raw_state(st0["q"], st0["img"], st0["ang"])
+            g.replay()
+            torch.cuda.synchronize()
+        else:
+            eng.integrate(1, ff)
+            agent.reset_trajectory()
+            eng.integrate(3, ff)
+        assert eng._ride_along == (mode in ("ride", "graph"))
+        st = eng.get_raw_state()
+        tr = agent.trajectory
+        out.append((mode, st, torch.stack([torch.as_tensor(a) for a in tr.actions]).cpu(),
+                    torch.stack([torch.as_tensor(r) for r in tr.rewards]).cpu(),
+                    torch.stack([torch.as_tensor(f) for f in tr.features]).cpu()))
+    ref = out[0]
+    for mode, st, a, r, f in out[1:]:
+        for k in ("q", "img", "ang"):
+            assert np.array_equal(ref[1][k], st[k]), (mode, k)
+        assert torch.equal(ref[2], a) and torch.equal(ref[3], r) and torch.equal(ref[4], f), mode
+
+
 def test_bench_workload_overlap_equals_serial():
     """The bench workload (vision cones, actor-critic sampling, GradientSensing
     reward) over 4 slices of one integrate call: the build on a side stream
