@@ -129,11 +129,11 @@ class TorchModel:
                 and type(self.sampling_strategy) is GumbelDistribution
                 and type(self.exploration_policy) is RandomExploration)
 
-    @torch.no_grad()
     # compute_action_fused takes the engine whose deferred build may ride
     # along in the policy launch (SwarmEngine._prebuild, ride-along mode)
     accepts_engine = True
 
+    @torch.no_grad()
     def compute_action_fused(self, observables: torch.Tensor, f_table: torch.Tensor,
                              t_table: torch.Tensor, engine=None):
         """compute_action + action-table lookup in one sampling kernel:
