@@ -1216,6 +1216,7 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
     }
   }
   __syncthreads();
+  SWARM_STAMP(11);
   // (kBig: the arrays below live in global memory, so every loop issues
   // its loads / atomics kU at a time before using them -- one memory
   // latency per kU iterations, not one per iteration)

@@ -30,6 +30,13 @@ for rep in range(5):
         ns = int(out[19])
         print(f"run (wave 0, npass {int(out[20])}): cycles/sub-step pairs {int(out[16]) // ns} "
               f"read-back {int(out[17]) // ns} bd {int(out[18]) // ns}")
-    k = int(np.max(np.nonzero(out[:16])[0])) + 1
-    d = np.diff(out[:k].astype(np.int64))
-    print("phase cycles:", " ".join(f"{x:6d}" for x in d), " total", int(out[k - 1]) - int(out[0]))
+    t = out.astype(np.int64)
+    # k_build_sort: 0 load, 1 count, 2 scan, 3 starts, 4 scatter, 5 end;
+    # k_cluster_build: 6 start, 11 init + pair copy, 7 union-find, 8 roots /
+    # sizes / classes, 9 packing, 10 per-wave pair lists (s_memtime is per
+    # XCD: compare stamps of one kernel only)
+    sort = [("load", 0, 1), ("count", 1, 2), ("scan", 2, 3), ("starts", 3, 4), ("scatter", 4, 5)]
+    build = [("init+copy", 6, 11), ("union", 11, 7), ("roots/classes", 7, 8), ("packing", 8, 9),
+             ("wave pairs", 9, 10)]
+    for name, rows in (("sort", sort), ("cluster build", build)):
+        print(f"{name} cycles: " + "  ".join(f"{n} {int(t[b] - t[a])}" for n, a, b in rows))
