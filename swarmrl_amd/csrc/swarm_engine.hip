@@ -1493,9 +1493,12 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   // build grid; otherwise every window runs on the global path
   e->big_build = build_is_big(n_particles);
   e->sc.pair_cap = build_pair_cap(n_particles, e->big_build);
-  // non-periodic boxes (no minimum image, edge cells) run on the global path;
-  // SWARMRL_AMD_CLUSTER_PATH=0 forces it (A/B and parity of the two paths)
-  e->cluster_path = params->periodic && e->sc.pair_cap >= n_particles &&
+  // non-periodic boxes run windowed in 2-D (edge cells and unwrapped
+  // distances in the build and the exact check; a listed pair's folded
+  // difference is its unwrapped one), on the global path in 3-D;
+  // SWARMRL_AMD_CLUSTER_PATH=0 forces the global path (A/B and parity)
+  e->sc.periodic = params->periodic ? 1 : 0;
+  e->cluster_path = (params->periodic || !three_d) && e->sc.pair_cap >= n_particles &&
                     n_particles < 65536 &&
                     swarm::build_lds_words_big(n_particles) * 4 <= kMaxLds &&
                     (size_t)(16 + (1 << lcb) + 1) * 4 <= kMaxLds &&
@@ -1523,6 +1526,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     const char* on = std::getenv("SWARMRL_AMD_NLIST");
     if (on && on[0] == '0') e->nlist_path = false;
     if (on && on[0] == '1') e->nlist_path = true;
+    if (!params->periodic) e->nlist_path = false;  // the Verlet-list window is periodic-only
   }
   const size_t M = (size_t)n_envs * n_particles;
   int rc = SWARM_OK;
@@ -1632,13 +1636,14 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
       const int wm = S / 64;
       const size_t below = 16 + 16 + 3 * 68 + (size_t)((wm + 3) & ~3) + 4 * (size_t)n_particles;
       e->env_build = e->cluster_path && !e->big_build && !latency_bound && !three_d &&
-                     !e->nlist_path &&
+                     !e->nlist_path && params->periodic &&
                      swarm::build_env_sort_words(n_particles, 1 << (e->lxb + e->lyb)) <= below;
       if (const char* ox = std::getenv("SWARMRL_AMD_XCD_MAP")) e->xcd_map = ox[0] != '0';
       const char* ob = std::getenv("SWARMRL_AMD_ENV_BUILD");
       if (ob && ob[0] == '0') e->env_build = false;
       if (ob && ob[0] == '1')
         e->env_build = e->cluster_path && !e->big_build && !three_d && !e->nlist_path &&
+                       params->periodic &&
                        swarm::build_env_sort_words(n_particles, 1 << (e->lxb + e->lyb)) <= below;
     }
     // one block per CU for latency-bound runs; beside a run of up to 8192

@@ -213,6 +213,7 @@ struct Scratch {
   int32_t pair_cap;   // pairs per env
   int32_t one_pass;   // 1: pack clusters so that a wave has <= 64 pairs
   int32_t fill_singletons;  // 1: singletons take the tail lanes of the other classes
+  int32_t periodic;   // 0: non-periodic box (edge cells, unwrapped pair distances; 2-D build)
   int32_t S;          // slots per env
   int32_t wmax;       // S / 64
   uint64_t* phase;    // [32] build phase stamps (SWARM_PHASE_TIMING builds only)
@@ -977,6 +978,15 @@ __device__ __forceinline__ void build_sort_body(const DevState& st, const Scratc
   const int ncell = 1 << (lx + ly);
   int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
   int32_t* cnt = wave_sums + 16;
+  // cell of particle i at (qx, qy): folded positions in a periodic box; in a
+  // non-periodic one a particle outside the box takes the edge cell on its
+  // side (cell_coord, as the global path and the oracle)
+  const bool per = sc.periodic != 0;
+  auto cell_of = [&](int i, uint32_t qx, uint32_t qy) {
+    if (per) return cell_index(qx, qy, lx, ly);
+    return (cell_coord(qy, st.img[M + base + i], ly, false) << lx) |
+           cell_coord(qx, st.img[base + i], lx, false);
+  };
   SWARM_STAMP(0);
   // all loads of the cached particles first (one memory latency, not CH)
   uint32_t cqx[CH], cqy[CH];
@@ -998,9 +1008,9 @@ __device__ __forceinline__ void build_sort_body(const DevState& st, const Scratc
   SWARM_STAMP(1);
 #pragma unroll
   for (int k = 0; k < CH; ++k)
-    if (cid[k] >= 0) atomicAdd(&cnt[cell_index(cqx[k], cqy[k], lx, ly)], 1);
+    if (cid[k] >= 0) atomicAdd(&cnt[cell_of(tid + k * T, cqx[k], cqy[k])], 1);
   for (int i = tid + CH * T; i < N; i += T)
-    atomicAdd(&cnt[cell_index(st.q[base + i], st.q[M + base + i], lx, ly)], 1);
+    atomicAdd(&cnt[cell_of(i, st.q[base + i], st.q[M + base + i])], 1);
   __syncthreads();
   SWARM_STAMP(2);
   block_exclusive_scan(cnt, ncell, wave_sums);
@@ -1013,14 +1023,14 @@ __device__ __forceinline__ void build_sort_body(const DevState& st, const Scratc
 #pragma unroll
   for (int k = 0; k < CH; ++k) {
     if (cid[k] < 0) continue;
-    const size_t pos = base + atomicAdd(&cnt[cell_index(cqx[k], cqy[k], lx, ly)], 1);
+    const size_t pos = base + atomicAdd(&cnt[cell_of(tid + k * T, cqx[k], cqy[k])], 1);
     sc.bsq[pos] = cqx[k];
     sc.bsq[M + pos] = cqy[k];
     sc.bsid[pos] = cid[k];
   }
   for (int i = tid + CH * T; i < N; i += T) {
     const uint32_t qx = st.q[base + i], qy = st.q[M + base + i];
-    const size_t pos = base + atomicAdd(&cnt[cell_index(qx, qy, lx, ly)], 1);
+    const size_t pos = base + atomicAdd(&cnt[cell_of(i, qx, qy)], 1);
     sc.bsq[pos] = qx;
     sc.bsq[M + pos] = qy;
     sc.bsid[pos] = i | ((int32_t)st.species[i] << 24);
@@ -1060,24 +1070,35 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
   const int ncx = 1 << lx, ncy = 1 << ly;
   const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
   const float sx0 = d->sx[0], sx1 = d->sx[1];
+  // non-periodic box (d->periodic == 0): edge cells, no wrap of the stencil,
+  // unwrapped pair distances (pair_disp) -- a pair near across the box edge
+  // only in the folded sense must not be listed
+  const bool per = d->periodic != 0;
   int pk = 0, i = 0;
   uint32_t qx = 0, qy = 0;
+  int32_t ix = 0, iy = 0;
   if (valid) {
     pk = sc.bsid[base + ps];
     i = pk & 0xffffff;
     qx = sc.bsq[base + ps];
     qy = sc.bsq[M + base + ps];
+    if (!per) {
+      ix = st.img[base + i];
+      iy = st.img[M + base + i];
+    }
   }
-  const int c0 = cell_index(qx, qy, lx, ly);
+  const int c0 = per ? cell_index(qx, qy, lx, ly)
+                     : (cell_coord(qy, iy, ly, false) << lx) | cell_coord(qx, ix, lx, false);
   const int cx = c0 & (ncx - 1), cy = c0 >> lx;
   const int xa = ncx >= 3 ? max(cx - 1, 0) : 0;
   const int xb = ncx >= 3 ? min(cx + 1, ncx - 1) : ncx - 1;
-  const int xw = ncx >= 3 ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
+  const int xw = ncx >= 3 && per ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
   int rb[6], re[6];
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     const int oy = loy + (r >> 1), part = r & 1;
-    const bool use = valid && oy <= hiy && (part == 0 || xw >= 0);
+    const bool use = valid && oy <= hiy && (part == 0 || xw >= 0) &&
+                     (per || (cy + oy >= 0 && cy + oy < ncy));
     const int row = ((cy + oy + ncy) & (ncy - 1)) << lx;
     const int c_lo = row | (part == 0 ? xa : xw), c_hi = row | (part == 0 ? xb : xw);
     rb[r] = use ? cs[c_lo] : 0;
@@ -1106,8 +1127,10 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
       for (int u = 0; u < 4; ++u) {
         if (pk4[u] < 0) continue;
         const int j = pk4[u] & 0xffffff;
-        const float rx = (float)(int32_t)(x4[u] - qx) * sx0;
-        const float ry = (float)(int32_t)(y4[u] - qy) * sx1;
+        const float rx = per ? (float)(int32_t)(x4[u] - qx) * sx0
+                             : pair_disp(x4[u], st.img[base + j], qx, ix, sx0, false);
+        const float ry = per ? (float)(int32_t)(y4[u] - qy) * sx1
+                             : pair_disp(y4[u], st.img[M + base + j], qy, iy, sx1, false);
         if (i < j && rx * rx + ry * ry < nb2_row[pk4[u] >> 24]) {
 #pragma unroll
           for (int v = 0; v < kKeep; ++v) keep[v] = found == v ? (uint32_t)j : keep[v];
@@ -1144,8 +1167,11 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
     for (int jj = rb[r]; jj < re[r]; ++jj) {
       const int packed = sc.bsid[base + jj];
       const int j = packed & 0xffffff;
-      const float rx = (float)(int32_t)(sc.bsq[base + jj] - qx) * sx0;
-      const float ry = (float)(int32_t)(sc.bsq[M + base + jj] - qy) * sx1;
+      const float rx = per ? (float)(int32_t)(sc.bsq[base + jj] - qx) * sx0
+                           : pair_disp(sc.bsq[base + jj], st.img[base + j], qx, ix, sx0, false);
+      const float ry = per ? (float)(int32_t)(sc.bsq[M + base + jj] - qy) * sx1
+                           : pair_disp(sc.bsq[M + base + jj], st.img[M + base + j], qy, iy, sx1,
+                                       false);
       if (i < j && rx * rx + ry * ry < nb2_row[packed >> 24]) {
         const int k = my_off + w;
         if (k < sc.pair_cap) out[k] = (uint32_t)i | ((uint32_t)j << 16);
@@ -2711,13 +2737,20 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
       const bool multi = d->n_species > 1;  // else every pair's cutoff is cut2[0]
       const float rc0 = sqrtf(pt.cut2[0]);
       const float sx0 = d->sx[0], sx1 = d->sx[1];
+      const bool per = d->periodic != 0;
       const long total = (long)nm * N;
       for (long t = tid; t < total; t += T) {
         const int m = movers[t / N];
         const int j = (int)(t % N);
         if (j == m) continue;
-        const float rx = (float)(int32_t)(sc.bq[base + j] - sc.bq[base + m]) * sx0;
-        const float ry = (float)(int32_t)(sc.bq[M + base + j] - sc.bq[M + base + m]) * sx1;
+        // (non-periodic box: the unwrapped separation; the folded one would
+        // only make the test stricter)
+        const float rx = per ? (float)(int32_t)(sc.bq[base + j] - sc.bq[base + m]) * sx0
+                             : pair_disp(sc.bq[base + j], sc.bimg[base + j], sc.bq[base + m],
+                                         sc.bimg[base + m], sx0, false);
+        const float ry = per ? (float)(int32_t)(sc.bq[M + base + j] - sc.bq[M + base + m]) * sx1
+                             : pair_disp(sc.bq[M + base + j], sc.bimg[M + base + j],
+                                         sc.bq[M + base + m], sc.bimg[M + base + m], sx1, false);
         // the pair's own WCA cutoff r_m + r_j (not the largest one: a dense
         // mixture would fail the test for pairs that cannot interact)
         const float rc = multi ? sqrtf(pt.cut2[st.species[m] * kMaxSpecies + st.species[j]]) : rc0;
@@ -2767,7 +2800,7 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
     }
     if (tid == 0) sc.fallback[e] = 2;  // diagnostics: env re-run on the global path
     __syncthreads();
-    if (global_lds_extra_words(N, st.dims, 1 << (lx + ly)))
+    if (global_lds_extra_words(N, st.dims, 1 << (lx + ly)) && d->periodic)  // LDS variant: periodic
       block_global_run_lds(d, st, e, n_steps, step0, lx, ly, false, 0.0f, 0.0f, cnt, wave_sums,
                            cnt + (1 << (lx + ly)) + 1, &pt, par);
     else

@@ -3,7 +3,7 @@ Non-periodic boxes (MDParams.periodic = False -> system.periodicity =
 [False] * 3, espresso.py:270): no minimum image -- pair forces act along the
 plain difference of the unwrapped positions -- and particles may leave the
 box (they stay in the edge cells of the pair search).  These engines run on
-the global path; bit-exact against the oracle's restatement (cell list with
+bit-exact against the oracle's restatement (cell list with
 edge cells in 2-D, all pairs in 3-D), including particles that start outside
 the box and pairs that straddle its faces.
 """
@@ -49,8 +49,11 @@ def _straddling(rng, n, L):
     return pos, np.stack([np.cos(a), np.sin(a), np.zeros(n)], 1)
 
 
+@pytest.mark.parametrize("path", ["cluster", "global"])
 @pytest.mark.parametrize("kT", [0.0, 1.0239])
-def test_nonperiodic_2d_bit_exact(kT):
+def test_nonperiodic_2d_bit_exact(kT, path, monkeypatch):
+    if path == "global":
+        monkeypatch.setenv("SWARMRL_AMD_CLUSTER_PATH", "0")
     from gpu_harness import Harness, species_list
 
     rng = np.random.default_rng(41)
@@ -81,6 +84,42 @@ def test_nonperiodic_2d_bit_exact(kT):
     alt = oracle.sd_run(pp, oracle.state_from_positions(pos, dirs, box), sp, 200)[0]
     assert not np.array_equal(alt["q"], oracle.sd_run(h.op, oracle.state_from_positions(
         pos, dirs, box), sp, 200)[0]["q"])
+
+
+def test_nonperiodic_2d_cluster_windows_4096():
+    """4096 colloids at area fraction 0.1 in a non-periodic box, some outside
+    it and pairs close across the x = 0 and y = L faces (close unwrapped, far
+    in the folded cells): the windows run on the cluster path (no re-run in
+    the last window) and match the oracle bit for bit; the folded-neighbour
+    pairs across a face never interact."""
+    from gpu_harness import Harness, species_list
+
+    rng = np.random.default_rng(43)
+    n = 4096
+    L = 2 * np.sqrt(n * np.pi * 0.25 / 0.1)
+    box = [L, L, L]
+    pos, dirs = _straddling(rng, n, L)
+    sp = np.zeros(n, int)
+    st = oracle.state_from_positions(pos, dirs, box)
+    h = Harness(box, 1e-3, 1.0239, 1.0239, 12, species_list()[:1], sp, periodic=False)
+    h.upload([st])
+    h.sd(300)
+    st = oracle.sd_run(h.op, st, sp, 300)[0]
+    _eq(h.download()[0], st)
+    step = 0
+    for nsteps in (100, 100, 37):
+        f = rng.choice([0.0, 10.0], n).astype(np.float32)
+        t = rng.choice([-10.0, 0.0, 10.0], n).astype(np.float32)
+        h.set_actions(f, t)
+        h.integrate(nsteps)
+        st, vel, _ = oracle.bd_run(h.op, st, sp, f, t, nsteps, step0=step)
+        step += nsteps
+        _eq(h.download()[0], st)
+        assert np.array_equal(h.velocities(), vel)
+    fb = np.zeros(1, np.int32)
+    w = np.zeros(1, np.int32)
+    h.native.call("swarm_engine_window_stats", fb.ctypes.data, w.ctypes.data)
+    assert w[0] > 0 and fb[0] == 0, (fb, w)  # a cluster window, not re-run
 
 
 def test_nonperiodic_3d_bit_exact():
