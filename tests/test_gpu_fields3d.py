@@ -30,7 +30,7 @@ def _colloids(pos, ids=None):
     from swarmrl_amd.components import Colloid
 
     ids = range(len(pos)) if ids is None else ids
-    return [Colloid(np.asarray(p, dtype=float), np.array([0.0, 0.0, 1.0]), int(i), 0)
+    return [Colloid(np.asarray(p, dtype=float), np.array([0.0, 0.0, 1.0]), int(i), type=0)
             for p, i in zip(pos, ids)]
 
 
@@ -105,7 +105,8 @@ def test_particle_sensing_3d_matches_restatement():
     types = rng.integers(0, 2, 40)
     from swarmrl_amd.components import Colloid
 
-    cols = [Colloid(p, np.array([1.0, 0, 0]), i, int(t)) for i, (p, t) in enumerate(zip(pos, types))]
+    cols = [Colloid(p, np.array([1.0, 0, 0]), i, type=int(t))
+            for i, (p, t) in enumerate(zip(pos, types))]
     box = np.array([10.0, 10.0, 10.0])
     obs = ParticleSensing(decay_fn=lambda x: -1 * x, box_length=box, particle_type=0,
                           sensing_type=1)
