@@ -1575,6 +1575,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->sc.sqx, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.sqy, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.sqz, M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.simg, params->periodic ? 1 : 3 * M);
   rc = rc ? rc : dev_alloc(e, &e->st.dir3, 3 * M);
   rc = rc ? rc : dev_alloc(e, &e->st.torque_xy, 2 * M);
   rc = rc ? rc : dev_alloc(e, &e->st.omega_xy, 2 * M);

@@ -176,6 +176,7 @@ struct Scratch {
   uint32_t* sqx;      // [M] positions sorted by cell
   uint32_t* sqy;      // [M]
   uint32_t* sqz;      // [M] (3-D global path)
+  int32_t* simg;      // [3][M] image counters sorted with sqx/sqy/sqz (non-periodic global path)
   int32_t* sidx;      // [M] particle index of a sorted entry
   uint32_t* bq;       // [dims][M] window-start snapshot
   int32_t* bimg;      // [dims][M]
@@ -638,6 +639,10 @@ __device__ void block_global_run(const Derived* __restrict__ d, const DevState& 
       sc.sqx[base + pos] = qx;
       sc.sqy[base + pos] = qy;
       sc.sidx[base + pos] = i;
+      if (!per) {  // the images too: the update below rewrites st.img in place
+        sc.simg[base + pos] = st.img[base + i];
+        sc.simg[M + base + pos] = st.img[M + base + i];
+      }
     }
     __syncthreads();  // cell c now spans [c ? cnt[c-1] : 0, cnt[c])
     int any = 0;
@@ -665,10 +670,10 @@ __device__ void block_global_run(const Derived* __restrict__ d, const DevState& 
             const int j = sc.sidx[base + jj];
             if (j == i) continue;
             const float rx = per ? (float)(int32_t)(sc.sqx[base + jj] - p.qx) * sx0
-                                 : pair_disp(sc.sqx[base + jj], st.img[base + j], p.qx, p.ix, sx0,
-                                             false);
+                                 : pair_disp(sc.sqx[base + jj], sc.simg[base + jj], p.qx, p.ix,
+                                             sx0, false);
             const float ry = per ? (float)(int32_t)(sc.sqy[base + jj] - p.qy) * sx1
-                                 : pair_disp(sc.sqy[base + jj], st.img[M + base + j], p.qy, p.iy,
+                                 : pair_disp(sc.sqy[base + jj], sc.simg[M + base + jj], p.qy, p.iy,
                                              sx1, false);
             const int pk = si * kMaxSpecies + st.species[j];
             pair_force(pt->cut2[pk], pt->sig6[pk], eps24, rx, ry, ax, ay);

@@ -122,6 +122,8 @@ __device__ void block_global_run3(const Derived* __restrict__ d, const DevState&
       sc.sqy[base + pos] = qy;
       sc.sqz[base + pos] = qz;
       sc.sidx[base + pos] = i;
+      if (!per)  // the images too: the update below rewrites st.img in place
+        for (int a = 0; a < 3; ++a) sc.simg[(size_t)a * M + base + pos] = st.img[a * M + base + i];
     }
     __syncthreads();  // cell c now spans [c ? cnt[c-1] : 0, cnt[c])
     int any = 0;
@@ -155,16 +157,17 @@ __device__ void block_global_run3(const Derived* __restrict__ d, const DevState&
             for (int jj = jb; jj < je; ++jj) {
               const int j = sc.sidx[base + jj];
               if (j == i) continue;
-              const size_t gj = base + j;
               float rx, ry, rz;
               if (per) {
                 rx = (float)(int32_t)(sc.sqx[base + jj] - q[0]) * sx[0];
                 ry = (float)(int32_t)(sc.sqy[base + jj] - q[1]) * sx[1];
                 rz = (float)(int32_t)(sc.sqz[base + jj] - q[2]) * sx[2];
               } else {
-                rx = pair_disp(sc.sqx[base + jj], st.img[gj], q[0], im[0], sx[0], false);
-                ry = pair_disp(sc.sqy[base + jj], st.img[M + gj], q[1], im[1], sx[1], false);
-                rz = pair_disp(sc.sqz[base + jj], st.img[2 * M + gj], q[2], im[2], sx[2], false);
+                rx = pair_disp(sc.sqx[base + jj], sc.simg[base + jj], q[0], im[0], sx[0], false);
+                ry = pair_disp(sc.sqy[base + jj], sc.simg[M + base + jj], q[1], im[1], sx[1],
+                               false);
+                rz = pair_disp(sc.sqz[base + jj], sc.simg[2 * M + base + jj], q[2], im[2], sx[2],
+                               false);
               }
               const int pk = si * kMaxSpecies + st.species[j];
               pair_force3(pt->cut2[pk], pt->sig6[pk], eps24, rx, ry, rz, acc[0], acc[1],

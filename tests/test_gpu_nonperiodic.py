@@ -122,13 +122,15 @@ def test_nonperiodic_2d_cluster_windows_4096():
     assert w[0] > 0 and fb[0] == 0, (fb, w)  # a cluster window, not re-run
 
 
-def test_nonperiodic_3d_bit_exact():
+@pytest.mark.parametrize("n,L", [(150, 20.0), (2500, 60.0)])
+def test_nonperiodic_3d_bit_exact(n, L):
+    """(2500: more colloids than workgroup threads, so each thread updates
+    several and the pair search must read the step's sorted image copies,
+    not the image counters being updated.)"""
     from gpu_harness import Harness, species_list
 
     rng = np.random.default_rng(42)
-    L = 20.0
     box = [L, L, L]
-    n = 150
     sp = rng.integers(0, 2, n)
     pos = -0.1 * L + rng.random((n, 3)) * 1.2 * L
     pos[0] = (-0.7, 5.0, 5.0)
