@@ -1115,32 +1115,46 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
   uint32_t keep[kKeep];
 #pragma unroll
   for (int v = 0; v < kKeep; ++v) keep[v] = 0u;
+  // the six ranges as one flat candidate index f in [0, total), record
+  // jj = f + off[r] of the range r holding f: kFly candidates in flight per
+  // iteration whatever the split over the ranges (about 11 candidates at
+  // area fraction 0.1: two rounds of loads, not one per range)
+  constexpr int kFly = 8;
+  int off[6], pre[7];
+  pre[0] = 0;
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
-    for (int jj0 = rb[r]; jj0 < re[r]; jj0 += 4) {
-      int pk4[4];
-      uint32_t x4[4], y4[4];
+    off[r] = rb[r] - pre[r];
+    pre[r + 1] = pre[r] + (re[r] - rb[r]);
+  }
+  const int total = pre[6];
+  for (int f0 = 0; f0 < total; f0 += kFly) {
+    int pk4[kFly];
+    uint32_t x4[kFly], y4[kFly];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int jj = jj0 + u;
-        const bool ok = jj < re[r];
-        pk4[u] = ok ? sc.bsid[base + jj] : -1;
-        x4[u] = ok ? sc.bsq[base + jj] : 0u;
-        y4[u] = ok ? sc.bsq[M + base + jj] : 0u;
-      }
+    for (int u = 0; u < kFly; ++u) {
+      const int f = f0 + u;
+      int o = off[0];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (pk4[u] < 0) continue;
-        const int j = pk4[u] & 0xffffff;
-        const float rx = per ? (float)(int32_t)(x4[u] - qx) * sx0
-                             : pair_disp(x4[u], st.img[base + j], qx, ix, sx0, false);
-        const float ry = per ? (float)(int32_t)(y4[u] - qy) * sx1
-                             : pair_disp(y4[u], st.img[M + base + j], qy, iy, sx1, false);
-        if (i < j && rx * rx + ry * ry < nb2_row[pk4[u] >> 24]) {
+      for (int r = 1; r < 6; ++r) o = f >= pre[r] ? off[r] : o;
+      const int jj = f + o;
+      const bool ok = f < total;
+      pk4[u] = ok ? sc.bsid[base + jj] : -1;
+      x4[u] = ok ? sc.bsq[base + jj] : 0u;
+      y4[u] = ok ? sc.bsq[M + base + jj] : 0u;
+    }
 #pragma unroll
-          for (int v = 0; v < kKeep; ++v) keep[v] = found == v ? (uint32_t)j : keep[v];
-          ++found;
-        }
+    for (int u = 0; u < kFly; ++u) {
+      if (pk4[u] < 0) continue;
+      const int j = pk4[u] & 0xffffff;
+      const float rx = per ? (float)(int32_t)(x4[u] - qx) * sx0
+                           : pair_disp(x4[u], st.img[base + j], qx, ix, sx0, false);
+      const float ry = per ? (float)(int32_t)(y4[u] - qy) * sx1
+                           : pair_disp(y4[u], st.img[M + base + j], qy, iy, sx1, false);
+      if (i < j && rx * rx + ry * ry < nb2_row[pk4[u] >> 24]) {
+#pragma unroll
+        for (int v = 0; v < kKeep; ++v) keep[v] = found == v ? (uint32_t)j : keep[v];
+        ++found;
       }
     }
   }

@@ -8,6 +8,7 @@ done
 for r in 0 1; do
   SWARMRL_AMD_RIDE_ALONG=$r timeout -k 10 300 python bench.py --only head,c2,c4 --no-cpu-baseline > gpurun_out/r3d_bench_ride$r.log 2>&1
 done
+SWARMRL_AMD_LIB=$PWD/tools/_variants/lib_PT.so timeout -k 10 120 python tools/build_phases.py 4096 > gpurun_out/r3d_phases.log 2>&1
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for x in 0 1; do
   for c in FETCH_SIZE WRITE_SIZE; do
@@ -16,4 +17,5 @@ for x in 0 1; do
   done
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r3d_trace -o run -- python3 bench.py --only head --no-cpu-baseline > gpurun_out/r3d_trace.log 2>&1
+SWARMRL_AMD_LIB=$PWD/tools/_variants/lib_pairs6.so timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r3d_trace_pairs6 -o run -- python3 bench.py --only head --no-cpu-baseline > gpurun_out/r3d_trace_pairs6.log 2>&1
 timeout -k 10 400 python bench.py --only batched,c5,c3train --no-cpu-baseline > gpurun_out/r3d_bench.log 2>&1
