@@ -712,7 +712,7 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
 
     eng.drain_trajectory(block=True)
     traj_written = eng.h5_time_steps_written + len(eng.traj_holder["Times"])
-    kernel_ms, kernel, timing = time_run_kernel(eng, args.bd_reps)
+    kernel_ms, kernel, timing_note = time_run_kernel(eng, args.bd_reps)
     N = args.colloids
     sub = eng.params.steps_per_slice
     out = dict(timing)
@@ -727,7 +727,7 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
                                   f"colloid-sub-step; {N} colloids x {sub} sub-steps x {E} env(s)"),
         "src_sha": source_sha(),
     })
-    out["roofline"]["kernel_timing"] = timing
+    out["roofline"]["kernel_timing"] = timing_note
     valu = out["roofline"].get("valu")
     if valu:
         valu["lane_insts_per_colloid_substep"] = valu["insts_per_launch"] * 64 / (N * sub * E)
