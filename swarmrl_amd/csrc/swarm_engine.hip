@@ -1217,11 +1217,17 @@ int launch_run(swarm_engine* e, int n_steps) {
 }
 
 // The 2-D cluster window's exact check (and re-run on failure).
+// The window's cell-sorted snapshot is in global memory unless the build
+// was k_build_env (LDS-resident): k_check then takes each mover's
+// candidates from its cells (-1: every colloid).
+int check_cell_lx(const swarm_engine* e) { return e->env_build ? -1 : e->lxb; }
+int check_cell_ly(const swarm_engine* e) { return e->env_build ? -1 : e->lyb; }
+
 int launch_check(swarm_engine* e, int n_steps) {
   hipLaunchKernelGGL(swarm::k_check, dim3(e->n_envs), dim3(1024),
                      check_lds_bytes(e->lxg, e->lyg, e->n, e->params.n_dims), e->stream,
                      e->d_derived, e->st, e->sc, n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg,
-                     0);
+                     0, check_cell_lx(e), check_cell_ly(e));
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
 }
@@ -1265,7 +1271,8 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
     }
     hipLaunchKernelGGL(swarm::k_check, dim3(e->n_envs), dim3(1024),
                        check_lds_bytes(e->lxg, e->lyg, e->n, e->params.n_dims), e->stream,
-                       e->d_derived, e->st, e->sc, n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg, 1);
+                       e->d_derived, e->st, e->sc, n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg, 1,
+                       check_cell_lx(e), check_cell_ly(e));
     HIP_TRY(hipGetLastError());
     return SWARM_OK;
   }

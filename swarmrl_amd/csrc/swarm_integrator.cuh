@@ -1266,13 +1266,29 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   // its loads / atomics kU at a time before using them -- one memory
   // latency per kU iterations, not one per iteration)
   constexpr int kU = kBig ? 8 : 1;
-  for (int k0 = tid; k0 < npairs; k0 += kU * T) {
+  // The pair sweeps visit the LDS pair list in a spread order: neighbouring
+  // pairs of the cell-sorted list usually share a cluster, so lanes of one
+  // wave taking consecutive pairs contend on the same root / wave counter
+  // (LDS atomics to one address serialise, union-find CAS retries).  Sweep
+  // index k maps to pair (k mod 64) R + k / 64, R = ceil(npairs / 64): the
+  // lanes of a wave take pairs R apart (phase stamps: the union phase was
+  // 16 k cycles of k_cluster_build's 46 k at E = 1).  kBig keeps the
+  // identity (its list is in global memory, read kU at a time).
+  const int spread_r = (npairs + 63) >> 6;
+  const int nsweep = kBig ? npairs : 64 * spread_r;
+  auto sweep_pair = [&](int k) { return kBig ? k : (k & 63) * spread_r + (k >> 6); };
+  for (int k0 = tid; k0 < nsweep; k0 += kU * T) {
     uint32_t pr[kU];
+    bool ok[kU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) pr[u] = k0 + u * T < npairs ? plist[k0 + u * T] : 0u;
+    for (int u = 0; u < kU; ++u) {
+      const int pk = sweep_pair(k0 + u * T);
+      ok[u] = k0 + u * T < nsweep && pk < npairs;
+      pr[u] = ok[u] ? plist[pk] : 0u;
+    }
 #pragma unroll
     for (int u = 0; u < kU; ++u)
-      if (k0 + u * T < npairs) uf_union(parent, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
+      if (ok[u]) uf_union(parent, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
   }
   __syncthreads();
   SWARM_STAMP(7);
@@ -1287,13 +1303,18 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
       if (i0 + u * T < N) lslot[i0 + u * T] = r[u];
   }
   if (sc.one_pass)
-    for (int k0 = tid; k0 < npairs; k0 += kU * T) {
+    for (int k0 = tid; k0 < nsweep; k0 += kU * T) {
       uint32_t pr[kU];
+      bool ok[kU];
 #pragma unroll
-      for (int u = 0; u < kU; ++u) pr[u] = k0 + u * T < npairs ? plist[k0 + u * T] : 0u;
+      for (int u = 0; u < kU; ++u) {
+        const int pk = sweep_pair(k0 + u * T);
+        ok[u] = k0 + u * T < nsweep && pk < npairs;
+        pr[u] = ok[u] ? plist[pk] : 0u;
+      }
 #pragma unroll
       for (int u = 0; u < kU; ++u)
-        if (k0 + u * T < npairs) atomicAdd(&cbase[parent[pr[u] & 0xffffu]], 1);
+        if (ok[u]) atomicAdd(&cbase[parent[pr[u] & 0xffffu]], 1);
     }
   __syncthreads();
   // Lanes reserved per cluster (its packing class w): its size s, or with
@@ -1451,10 +1472,15 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   __syncthreads();
   SWARM_STAMP(9);
   // per-wave pair lists (both particles of a pair share a cluster, so a wave)
-  for (int k0 = tid; k0 < npairs; k0 += kU * T) {
+  for (int k0 = tid; k0 < nsweep; k0 += kU * T) {
    uint32_t prs[kU];
+   bool okp[kU];
 #pragma unroll
-   for (int u = 0; u < kU; ++u) prs[u] = k0 + u * T < npairs ? plist[k0 + u * T] : 0u;
+   for (int u = 0; u < kU; ++u) {
+     const int pk = sweep_pair(k0 + u * T);
+     okp[u] = k0 + u * T < nsweep && pk < npairs;
+     prs[u] = okp[u] ? plist[pk] : 0u;
+   }
    int32_t sis[kU], sjs[kU];
 #pragma unroll
    for (int u = 0; u < kU; ++u) {
@@ -1463,7 +1489,7 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
    }
 #pragma unroll
    for (int u = 0; u < kU; ++u) {
-    if (k0 + u * T >= npairs) continue;
+    if (!okp[u]) continue;
     const uint32_t pr = prs[u];
     const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
     const int si = sis[u], sj = sjs[u];
@@ -2711,11 +2737,14 @@ __global__ __launch_bounds__(256) void k_nl_step2(const Derived* __restrict__ d,
 }
 
 // ---------------------------------------------------------------- check
+// cell_lx, cell_ly: the window's build grid when its counting sort left the
+// cell-sorted snapshot in global memory (sc.bsq / bsid / bcstart: the
+// three-launch build, not k_build_env); -1: scan every colloid per mover.
 __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, DevState st,
                                                 Scratch sc, int n_steps,
                                                 uint64_t* __restrict__ step_ctr,
                                                 uint32_t* __restrict__ arrive, int lx, int ly,
-                                                int nlist) {
+                                                int nlist, int cell_lx, int cell_ly) {
   extern __shared__ __align__(16) unsigned char smem[];
   int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);  // 16
   int32_t* misc = wave_sums + 16;                          // 16
@@ -2757,11 +2786,7 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
       const float rc0 = sqrtf(pt.cut2[0]);
       const float sx0 = d->sx[0], sx1 = d->sx[1];
       const bool per = d->periodic != 0;
-      const long total = (long)nm * N;
-      for (long t = tid; t < total; t += T) {
-        const int m = movers[t / N];
-        const int j = (int)(t % N);
-        if (j == m) continue;
+      auto test_pair = [&](int m, int j) {
         // (non-periodic box: the unwrapped separation; the folded one would
         // only make the test stricter)
         const float rx = per ? (float)(int32_t)(sc.bq[base + j] - sc.bq[base + m]) * sx0
@@ -2800,6 +2825,83 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
             }
           }
           if (!listed) misc[1] = 1;
+        }
+      };
+      // Candidates of a mover from the window's cell-sorted snapshot: every
+      // j with d0 < rc + D_m + D_j lies within lim_max = rc_max + 2 D_max of
+      // m (D_max: the largest displacement; non-movers moved less than
+      // skin / 2), so within kc = ceil(lim_max / cell side) cells.  One wave
+      // per mover, its lanes over the (2 kc + 1) rows' ranges.  Grids too
+      // coarse for that (kc > 2, or fewer than 2 kc + 1 cells a side) scan
+      // every colloid.
+      int kc = 99;
+      const int ncx = cell_lx >= 1 ? 1 << cell_lx : 0, ncy = cell_ly >= 1 ? 1 << cell_ly : 0;
+      if (cell_lx >= 1 && cell_ly >= 1) {
+        if (tid == 0) misc[7] = __float_as_int(0.5f * d->skin);
+        __syncthreads();
+        for (int k = tid; k < nm; k += T)
+          atomicMax(&misc[7], __float_as_int(sc.disp[base + movers[k]]));  // >= 0: int order
+        __syncthreads();
+        const float dmax = __int_as_float(misc[7]);
+        const float lim_max = d->rc_max_f + 2.0f * dmax + 1e-3f;
+        const float side = fminf(sx0 * (float)(1u << (32 - cell_lx)),
+                                 sx1 * (float)(1u << (32 - cell_ly)));
+        kc = (int)ceilf(lim_max / side);
+        if (kc > 2 || ncx < 2 * kc + 1 || ncy < 2 * kc + 1) kc = 99;
+      }
+      if (kc <= 2) {
+        const int32_t* cs = sc.bcstart + (size_t)e * ((size_t)ncx * ncy + 1);
+        const int lane = tid & 63, nwv = T >> 6;
+        for (int k = tid >> 6; k < nm; k += nwv) {  // wave-uniform mover
+          const int m = movers[k];
+          const uint32_t qx = sc.bq[base + m], qy = sc.bq[M + base + m];
+          const int cx = per ? (int)(qx >> (32 - cell_lx))
+                             : cell_coord(qx, sc.bimg[base + m], cell_lx, false);
+          const int cy = per ? (int)(qy >> (32 - cell_ly))
+                             : cell_coord(qy, sc.bimg[M + base + m], cell_ly, false);
+          // up to two ranges per row (a periodic row wraps once)
+          int rb[10], rl[10], nr = 0;
+          for (int oy = -kc; oy <= kc; ++oy) {
+            int y = cy + oy;
+            if (!per && (y < 0 || y >= ncy)) continue;
+            y = (y + ncy) & (ncy - 1);
+            const int row = y << cell_lx;
+            int x0 = cx - kc, x1 = cx + kc;
+            if (!per) {
+              x0 = max(x0, 0);
+              x1 = min(x1, ncx - 1);
+            }
+            if (x0 < 0) {  // periodic wrap on the left
+              rb[nr] = cs[row | (ncx + x0)];
+              rl[nr] = cs[(row | (ncx - 1)) + 1] - rb[nr];
+              ++nr;
+              x0 = 0;
+            }
+            if (x1 > ncx - 1) {  // periodic wrap on the right
+              rb[nr] = cs[row];
+              rl[nr] = cs[(row | (x1 - ncx)) + 1] - rb[nr];
+              ++nr;
+              x1 = ncx - 1;
+            }
+            rb[nr] = cs[row | x0];
+            rl[nr] = cs[(row | x1) + 1] - rb[nr];
+            ++nr;
+          }
+          int total = 0;
+          for (int r = 0; r < nr; ++r) total += rl[r];
+          for (int f = lane; f < total; f += 64) {
+            int jj = f, r = 0;
+            while (jj >= rl[r]) jj -= rl[r++];
+            const int j = sc.bsid[base + rb[r] + jj] & 0xffffff;
+            if (j != m) test_pair(m, j);
+          }
+        }
+      } else {
+        const long total = (long)nm * N;
+        for (long t = tid; t < total; t += T) {
+          const int m = movers[t / N];
+          const int j = (int)(t % N);
+          if (j != m) test_pair(m, j);
         }
       }
     }

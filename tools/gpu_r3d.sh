@@ -1,6 +1,6 @@
 set -euo pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/r3d_gpu_tests.log 2>&1
+true
 for x in 0 1; do
   SWARMRL_AMD_XCD_MAP=$x timeout -k 10 120 python tools/run_kernel_time.py 64 > gpurun_out/r3d_run_xcd$x.log 2>&1
   SWARMRL_AMD_XCD_MAP=$x timeout -k 10 120 python tools/vision_time.py 64 > gpurun_out/r3d_vis_xcd$x.log 2>&1
