@@ -255,6 +255,20 @@ __device__ __forceinline__ float pair_disp(uint32_t qj, int32_t ij, uint32_t qi,
   return (float)dq * sx;
 }
 
+// Inclusive prefix sum over a wave's 64 lanes on the DPP network: row
+// shifts 1, 2, 4, 8 scan each 16-lane row, the gfx9 row broadcasts 15 and 31
+// carry rows into the next ones.  VALU only (no ds_bpermute round trip per
+// step, as __shfl_up's).  Every lane of the wave must be active.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
 // Exclusive scan of data[0..n) in LDS by the whole block; data[n] = total.
 // Each wave scans a contiguous chunk 64 entries at a time (lane k reads
 // entry base + k: no LDS bank conflicts, unlike one contiguous run per
@@ -268,29 +282,41 @@ __device__ inline void block_exclusive_scan_runs(int32_t* data, int n, int32_t* 
   const int tid = threadIdx.x;
   const int per = (n + T - 1) / T;
   const int lo = min(tid * per, n), hi = min(lo + per, n);
+  // four entries per thread, 16-byte aligned: one ds_read_b128 / write_b128
+  const bool quad = per == 4 && (n & 3) == 0 && (reinterpret_cast<uintptr_t>(data) & 15) == 0;
+  int4 x4 = make_int4(0, 0, 0, 0);
   int32_t local = 0;
-  for (int k = lo; k < hi; ++k) local += data[k];
+  if (quad) {
+    if (lo < n) x4 = reinterpret_cast<const int4*>(data)[tid];
+    local = x4.x + x4.y + x4.z + x4.w;
+  } else {
+    for (int k = lo; k < hi; ++k) local += data[k];
+  }
   const int lane = tid & 63, wave = tid >> 6;
   int32_t v = local;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int32_t o = __shfl_up(v, off, 64);
-    if (lane >= off) v += o;
-  }
+  v = wave_incl_scan(v);
   if (lane == 63) wave_sums[wave] = v;
   __syncthreads();
   if (wave == 0) {
     const int nw = (T + 63) >> 6;
     int32_t w = lane < nw ? wave_sums[lane] : 0;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int32_t o = __shfl_up(w, off, 64);
-      if (lane >= off) w += o;
-    }
+    w = wave_incl_scan(w);
     if (lane < nw) wave_sums[lane] = w;
   }
   __syncthreads();
   int32_t run = v - local + (wave > 0 ? wave_sums[wave - 1] : 0);
+  if (quad) {
+    if (lo < n) {
+      int4 y;
+      y.x = run;
+      y.y = run + x4.x;
+      y.z = y.y + x4.y;
+      y.w = y.z + x4.z;
+      reinterpret_cast<int4*>(data)[tid] = y;
+    }
+    if (tid == T - 1) data[n] = run + local;
+    return;
+  }
   for (int k = lo; k < hi; ++k) {
     const int32_t c = data[k];
     data[k] = run;
@@ -315,23 +341,15 @@ __device__ inline void block_exclusive_scan(int32_t* data, int n, int32_t* wave_
     const int k = b + lane;
     const int32_t x = k < hi ? data[k] : 0;
     int32_t v = x;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int32_t o = __shfl_up(v, off, 64);
-      if (lane >= off) v += o;
-    }
+    v = wave_incl_scan(v);
     if (k < hi) data[k] = carry + v - x;
-    carry += __shfl(v, 63, 64);
+    carry += __builtin_amdgcn_readlane(v, 63);
   }
   if (lane == 0) wave_sums[wave] = carry;
   __syncthreads();
   if (wave == 0) {
     int32_t w = lane < nw ? wave_sums[lane] : 0;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int32_t o = __shfl_up(w, off, 64);
-      if (lane >= off) w += o;
-    }
+    w = wave_incl_scan(w);
     if (lane < nw) wave_sums[lane] = w;  // inclusive prefix of the wave totals
   }
   __syncthreads();
@@ -1161,14 +1179,10 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
   // wave prefix sum, one atomic per wave
   const int lane = threadIdx.x & 63;
   int v = found;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int o = __shfl_up(v, off, 64);
-    if (lane >= off) v += o;
-  }
+  v = wave_incl_scan(v);
   int wbase = 0;
   if (lane == 63) wbase = atomicAdd(&sc.gnpairs[e], v);
-  wbase = __shfl(wbase, 63, 64);
+  wbase = __builtin_amdgcn_readlane(wbase, 63);
   const int my_off = wbase + v - found;
   uint32_t* out = sc.gplist + (size_t)e * sc.pair_cap;
   if (!__any(found > kKeep)) {
@@ -1372,20 +1386,12 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
     int32_t fl = 0;
     if (w >= 2 && nw > 0) fl = (nw - 1) * (64 - per * w) + (64 - (cnt - (nw - 1) * per) * w);
     int32_t f = fl;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int32_t o = __shfl_up(f, off, 64);
-      if (tid >= off) f += o;
-    }
+    f = wave_incl_scan(f);
     freebase[w] = f - fl;
-    const int32_t F = sc.fill_singletons ? __shfl(f, 63, 64) : 0;
+    const int32_t F = sc.fill_singletons ? __builtin_amdgcn_readlane(f, 63) : 0;
     if (w == 1) nw = (max(cnt - F, 0) + 63) / 64;
     int32_t v = nw;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int32_t o = __shfl_up(v, off, 64);
-      if (tid >= off) v += o;
-    }
+    v = wave_incl_scan(v);
     wavebase[w] = v - nw;
     if (tid == 63) {
       misc[1] = v;
@@ -1634,20 +1640,12 @@ __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, 
     int32_t fl = 0;
     if (w >= 2 && nw > 0) fl = (nw - 1) * (64 - per * w) + (64 - (cnt - (nw - 1) * per) * w);
     int32_t f = fl;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int32_t o = __shfl_up(f, off, 64);
-      if (tid >= off) f += o;
-    }
+    f = wave_incl_scan(f);
     freebase[w] = f - fl;
-    const int32_t F = sc.fill_singletons ? __shfl(f, 63, 64) : 0;
+    const int32_t F = sc.fill_singletons ? __builtin_amdgcn_readlane(f, 63) : 0;
     if (w == 1) nw = (max(cnt - F, 0) + 63) / 64;
     int32_t v = nw;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int32_t o = __shfl_up(v, off, 64);
-      if (tid >= off) v += o;
-    }
+    v = wave_incl_scan(v);
     wavebase[w] = v - nw;
     if (tid == 63) {
       misc[1] = v;
@@ -1904,14 +1902,10 @@ __global__ __launch_bounds__(1024) void k_build_env(const Derived* __restrict__ 
     }
     // wave prefix sum, one LDS atomic per wave
     int v = found;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int o = __shfl_up(v, off, 64);
-      if (lane >= off) v += o;
-    }
+    v = wave_incl_scan(v);
     int wbase = 0;
     if (lane == 63) wbase = atomicAdd(&npair, v);
-    wbase = __shfl(wbase, 63, 64);
+    wbase = __builtin_amdgcn_readlane(wbase, 63);
     const int my_off = wbase + v - found;
     if (!__any(found > kKeep)) {
 #pragma unroll

@@ -435,14 +435,10 @@ __global__ __launch_bounds__(256) void k_build_pairs3(const Derived* __restrict_
   }
   const int lane = threadIdx.x & 63;
   int v = found;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int o = __shfl_up(v, off, 64);
-    if (lane >= off) v += o;
-  }
+  v = wave_incl_scan(v);
   int wbase = 0;
   if (lane == 63) wbase = atomicAdd(&sc.gnpairs[e], v);
-  wbase = __shfl(wbase, 63, 64);
+  wbase = __builtin_amdgcn_readlane(wbase, 63);
   const int my_off = wbase + v - found;
   uint32_t* out = sc.gplist + (size_t)e * sc.pair_cap;
   if (!__any(found > kKeep)) {
