@@ -1505,6 +1505,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   // difference is its unwrapped one), on the global path in 3-D;
   // SWARMRL_AMD_CLUSTER_PATH=0 forces the global path (A/B and parity)
   e->sc.periodic = params->periodic ? 1 : 0;
+  e->sc.multi_species = params->n_species > 1 ? 1 : 0;
   e->cluster_path = (params->periodic || !three_d) && e->sc.pair_cap >= n_particles &&
                     n_particles < 65536 &&
                     swarm::build_lds_words_big(n_particles) * 4 <= kMaxLds &&

@@ -215,6 +215,7 @@ struct Scratch {
   int32_t one_pass;   // 1: pack clusters so that a wave has <= 64 pairs
   int32_t fill_singletons;  // 1: singletons take the tail lanes of the other classes
   int32_t periodic;   // 0: non-periodic box (edge cells, unwrapped pair distances; 2-D build)
+  int32_t multi_species;  // 0: one species (species pair bits 0, no species loads in the build)
   int32_t S;          // slots per env
   int32_t wmax;       // S / 64
   uint64_t* phase;    // [32] build phase stamps (SWARM_PHASE_TIMING builds only)
@@ -253,6 +254,17 @@ __device__ __forceinline__ float pair_disp(uint32_t qj, int32_t ij, uint32_t qi,
   if (periodic) return (float)(int32_t)(qj - qi) * sx;
   const int64_t dq = (int64_t)(ij - ii) * 4294967296LL + ((int64_t)qj - (int64_t)qi);
   return (float)dq * sx;
+}
+
+// floor(n / d) for 0 <= n < 2^20 and 1 <= d < 2^20: a float reciprocal
+// estimate (within one of the quotient) and one correction, instead of the
+// compiler's ~40-instruction integer division (the cluster build's packing
+// divides per cluster: 64 / s, r / per).
+__device__ __forceinline__ int udiv_small(int n, int d) {
+  int q = (int)((float)n * __builtin_amdgcn_rcpf((float)d));
+  const int r = n - q * d;
+  q += (r >= d ? 1 : 0) - (r < 0 ? 1 : 0);
+  return q;
 }
 
 // Inclusive prefix sum over a wave's 64 lanes on the DPP network: row
@@ -1276,10 +1288,15 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   }
   __syncthreads();
   SWARM_STAMP(11);
-  // (kBig: the arrays below live in global memory, so every loop issues
-  // its loads / atomics kU at a time before using them -- one memory
-  // latency per kU iterations, not one per iteration)
-  constexpr int kU = kBig ? 8 : 1;
+  // kBig: the arrays below live in global memory, so every loop issues its
+  // loads / atomics kU at a time before using them -- one memory latency per
+  // kU iterations, not one per iteration.  (In LDS, kU = 4 measured no
+  // better than 1 at E = 1: the union phase 1 k cycles shorter, the
+  // others longer.)
+#ifndef SWARM_BUILD_KU
+#define SWARM_BUILD_KU 1
+#endif
+  constexpr int kU = kBig ? 8 : SWARM_BUILD_KU;
   // The pair sweeps visit the LDS pair list in a spread order: neighbouring
   // pairs of the cell-sorted list usually share a cluster, so lanes of one
   // wave taking consecutive pairs contend on the same root / wave counter
@@ -1380,9 +1397,9 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   // waves: the run kernel's cost is per wave).
   if (tid < 64) {
     const int w = tid + 1;
-    const int per = 64 / w;
+    const int per = udiv_small(64, w);
     const int cnt = classcnt[w];
-    int32_t nw = (cnt + per - 1) / per;
+    int32_t nw = udiv_small(cnt + per - 1, per);
     int32_t fl = 0;
     if (w >= 2 && nw > 0) fl = (nw - 1) * (64 - per * w) + (64 - (cnt - (nw - 1) * per) * w);
     int32_t f = fl;
@@ -1425,14 +1442,14 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
         const int mid = (lo + hi + 1) >> 1;
         if (freebase[mid] <= r) lo = mid; else hi = mid - 1;
       }
-      const int v = lo, per = 64 / v;
-      const int nw = (classcnt[v] + per - 1) / per;
+      const int v = lo, per = udiv_small(64, v);
+      const int nw = udiv_small(classcnt[v] + per - 1, per);
       const int ffull = 64 - per * v;
       const int t = r - freebase[v];
       int j, lane;
       if (t < (nw - 1) * ffull) {
-        j = t / ffull;
-        lane = per * v + t % ffull;
+        j = udiv_small(t, ffull);
+        lane = per * v + (t - j * ffull);
       } else {
         j = nw - 1;
         lane = (classcnt[v] - (nw - 1) * per) * v + (t - (nw - 1) * ffull);
@@ -1442,8 +1459,8 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
       const int r2 = r - nfree;
       cbase[i] = (wavebase[1] + r2 / 64) * 64 + r2 % 64;
     } else {
-      const int per = 64 / s;
-      cbase[i] = (wavebase[s] + r / per) * 64 + (r % per) * s;
+      const int per = udiv_small(64, s), rq = udiv_small(r, per);
+      cbase[i] = (wavebase[s] + rq) * 64 + (r - rq * per) * s;
     }
    }
   }
@@ -1499,7 +1516,8 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
     const uint32_t pr = prs[u];
     const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
     const int si = sis[u], sj = sjs[u];
-    const uint32_t spp = (uint32_t)(st.species[i] * kMaxSpecies + st.species[j]);
+    const uint32_t spp =
+        sc.multi_species ? (uint32_t)(st.species[i] * kMaxSpecies + st.species[j]) : 0u;
     if (si < 0) {  // a big cluster's pair (both members of it)
       const int idx = atomicAdd(&misc[6], 1);
       if (idx < kBigPairs)
@@ -1634,9 +1652,9 @@ __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, 
   }
   if (tid < 64) {  // waves per class (cluster_build_env)
     const int w = tid + 1;
-    const int per = 64 / w;
+    const int per = udiv_small(64, w);
     const int cnt = classcnt[w];
-    int32_t nw = (cnt + per - 1) / per;
+    int32_t nw = udiv_small(cnt + per - 1, per);
     int32_t fl = 0;
     if (w >= 2 && nw > 0) fl = (nw - 1) * (64 - per * w) + (64 - (cnt - (nw - 1) * per) * w);
     int32_t f = fl;
@@ -1668,14 +1686,14 @@ __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, 
         const int mid = (lo + hi + 1) >> 1;
         if (freebase[mid] <= r) lo = mid; else hi = mid - 1;
       }
-      const int v = lo, per = 64 / v;
-      const int nw = (classcnt[v] + per - 1) / per;
+      const int v = lo, per = udiv_small(64, v);
+      const int nw = udiv_small(classcnt[v] + per - 1, per);
       const int ffull = 64 - per * v;
       const int t = r - freebase[v];
       int j, lane;
       if (t < (nw - 1) * ffull) {
-        j = t / ffull;
-        lane = per * v + t % ffull;
+        j = udiv_small(t, ffull);
+        lane = per * v + (t - j * ffull);
       } else {
         j = nw - 1;
         lane = (classcnt[v] - (nw - 1) * per) * v + (t - (nw - 1) * ffull);
@@ -1685,8 +1703,8 @@ __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, 
       const int r2 = r - nfree;
       cb = (wavebase[1] + r2 / 64) * 64 + r2 % 64;
     } else {
-      const int per = 64 / s;
-      cb = (wavebase[s] + r / per) * 64 + (r % per) * s;
+      const int per = udiv_small(64, s), rq = udiv_small(r, per);
+      cb = (wavebase[s] + rq) * 64 + (r - rq * per) * s;
     }
     B[i] = cb;
   }
@@ -1721,7 +1739,8 @@ __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, 
       const uint32_t pr = prs[u];
       const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
       const int si = A[i], sj = A[j];
-      const uint32_t spp = (uint32_t)(st.species[i] * kMaxSpecies + st.species[j]);
+      const uint32_t spp =
+        sc.multi_species ? (uint32_t)(st.species[i] * kMaxSpecies + st.species[j]) : 0u;
       if (si < 0) {  // a big cluster's pair (both members of it)
         const int idx = atomicAdd(&misc[6], 1);
         if (idx < kBigPairs)
