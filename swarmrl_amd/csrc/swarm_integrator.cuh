@@ -1032,7 +1032,7 @@ __device__ __forceinline__ void build_sort_body(const DevState& st, const Scratc
     const bool ok = i < N;
     cqx[k] = ok ? st.q[base + i] : 0u;
     cqy[k] = ok ? st.q[M + base + i] : 0u;
-    cid[k] = ok ? (i | ((int32_t)st.species[i] << 24)) : -1;
+    cid[k] = ok ? (i | (sc.multi_species ? (int32_t)st.species[i] << 24 : 0)) : -1;
   }
   for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
   if (tid == 0) {
@@ -1068,7 +1068,7 @@ __device__ __forceinline__ void build_sort_body(const DevState& st, const Scratc
     const size_t pos = base + atomicAdd(&cnt[cell_of(i, qx, qy)], 1);
     sc.bsq[pos] = qx;
     sc.bsq[M + pos] = qy;
-    sc.bsid[pos] = i | ((int32_t)st.species[i] << 24);
+    sc.bsid[pos] = i | (sc.multi_species ? (int32_t)st.species[i] << 24 : 0);
   }
   // idle wave slots of the next run (k_cluster_build writes the used ones);
   // last, so the stores drain in the shadow of the scatter
@@ -2764,28 +2764,44 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
   int32_t* movers = misc + 16;                             // kMaxMovers
   int32_t* cnt = movers + kMaxMovers;                      // global-path cell counts
   __shared__ PairTables pt;
-  stage_pair_tables(d, &pt);
   const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
+  // every load the test starts from is issued here together -- the window
+  // counters, the build's flags, the mover count and list (written by the
+  // run kernel) and the pair tables: one memory latency, not a chain
   const uint64_t step0 = step_ctr[kCtlStep];
   const int par = window_parity(step_ctr);  // reuse_forces slot of this window
+  const int fb = sc.fallback[e];
+  const int bign = nlist ? 0 : sc.big_n[e];
+  const int nm_run = sc.nmov[e];
+  const int mv_run = tid < kMaxMovers ? sc.movers[(size_t)e * kMaxMovers + tid] : 0;
+  for (int k = tid; k < kMaxSpecies * kMaxSpecies; k += T) {
+    pt.cut2[k] = d->cut2[k];
+    pt.sig6[k] = d->sig6[k];
+  }
   if (tid < 16) misc[tid] = 0;
   __syncthreads();
   // flagged by the build: the env did not run (its state is the window start)
-  const bool flagged_build = sc.fallback[e] == 1;
-  if (!flagged_build && !nlist && sc.big_n[e] > 0)
+  const bool flagged_build = fb == 1;
+  if (!flagged_build && bign > 0)
     run_big_clusters(d, st, sc, e, n_steps, step0, cnt, &pt, par);
   if (!flagged_build) {
     // the movers (displacement >= skin / 2) were listed by the run kernel
     // and the big-cluster run: no scan over all colloids here
-    // (agent-scope loads: the big-cluster run of this workgroup appended
-    // entries a moment ago)
-    if (tid == 0) misc[0] = __hip_atomic_load(&sc.nmov[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const int nm = misc[0];
-    for (int k = tid; k < min(nm, kMaxMovers); k += T)
-      movers[k] = __hip_atomic_load(&sc.movers[(size_t)e * kMaxMovers + k], __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
+    int nm = nm_run;
+    if (bign > 0) {
+      // the big-cluster run of this workgroup appended entries a moment
+      // ago: agent-scope loads
+      if (tid == 0) misc[0] = __hip_atomic_load(&sc.nmov[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      nm = misc[0];
+      for (int k = tid; k < min(nm, kMaxMovers); k += T)
+        movers[k] = __hip_atomic_load(&sc.movers[(size_t)e * kMaxMovers + k], __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      for (int k = tid; k < min(nm, kMaxMovers); k += T)
+        movers[k] = k < kMaxMovers && k == tid ? mv_run : sc.movers[(size_t)e * kMaxMovers + k];
+    }
     __syncthreads();
     if (nm > kMaxMovers) {
       if (tid == 0) misc[1] = 1;
