@@ -980,10 +980,30 @@ __device__ __forceinline__ int uf_find(int32_t* parent_g, int x) {
   }
 }
 
+// The roots of a and b, both walks in lockstep (path halving): each step's
+// two LDS reads are in flight together, so a union costs the longer walk's
+// round trips, not the sum of both.
+__device__ __forceinline__ void uf_find2(int32_t* parent_g, int& a, int& b) {
+  volatile lds_i32* parent = (volatile lds_i32*)(parent_g);
+  int pa = parent[a], pb = parent[b];
+  while (pa != a || pb != b) {
+    const int ga = parent[pa], gb = parent[pb];
+    if (pa != a) {
+      if (ga != pa) parent[a] = ga;
+      a = ga;
+    }
+    if (pb != b) {
+      if (gb != pb) parent[b] = gb;
+      b = gb;
+    }
+    pa = parent[a];
+    pb = parent[b];
+  }
+}
+
 __device__ __forceinline__ void uf_union(int32_t* parent, int a, int b) {
   while (true) {
-    a = uf_find(parent, a);
-    b = uf_find(parent, b);
+    uf_find2(parent, a, b);
     if (a == b) return;
     if (a < b) {
       const int t = a;
@@ -1308,17 +1328,20 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   const int spread_r = (npairs + 63) >> 6;
   const int nsweep = kBig ? npairs : 64 * spread_r;
   auto sweep_pair = [&](int k) { return kBig ? k : (k & 63) * spread_r + (k >> 6); };
-  for (int k0 = tid; k0 < nsweep; k0 += kU * T) {
-    uint32_t pr[kU];
-    bool ok[kU];
+  // (the union sweep reads its pairs four at a time even in LDS: the
+  // unions are serial per thread, the list reads need not be)
+  constexpr int kUU = kU > 4 ? kU : 4;
+  for (int k0 = tid; k0 < nsweep; k0 += kUU * T) {
+    uint32_t pr[kUU];
+    bool ok[kUU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < kUU; ++u) {
       const int pk = sweep_pair(k0 + u * T);
       ok[u] = k0 + u * T < nsweep && pk < npairs;
       pr[u] = ok[u] ? plist[pk] : 0u;
     }
 #pragma unroll
-    for (int u = 0; u < kU; ++u)
+    for (int u = 0; u < kUU; ++u)
       if (ok[u]) uf_union(parent, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
   }
   __syncthreads();
