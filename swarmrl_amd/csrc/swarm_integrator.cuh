@@ -1346,7 +1346,14 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   }
   __syncthreads();
   SWARM_STAMP(7);
-  for (int i = tid; i < N; i += T) parent[i] = uf_find(parent, i);
+  // every particle points at its root (two walks in lockstep per thread)
+  for (int i = tid; i < N; i += 2 * T) {
+    const bool two = i + T < N;
+    int a = i, b = two ? i + T : i;
+    uf_find2(parent, a, b);
+    parent[i] = a;
+    if (two) parent[i + T] = b;
+  }
   __syncthreads();
   for (int i0 = tid; i0 < N; i0 += kU * T) {
     int32_t r[kU];
