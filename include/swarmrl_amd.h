@@ -311,6 +311,18 @@ int swarm_vision_cone(swarm_engine_t *e, const swarm_vision_params_t *vp,
                       const int32_t *agent_idx, int32_t n_agents,
                       const float *radii, const int32_t *types, float *out);
 
+/* swarm_vision_cone with the caller's promise that agent_idx, radii and
+ * types stay allocated and unchanged while the engine lives (the
+ * SubdividedVisionCones observable keeps them).  The engine remembers the
+ * arguments: when the next build is deferred (swarm_engine_defer_build),
+ * the slice's reward launch (swarm_field_transform / swarm_field_distance)
+ * also builds the vision grid of the positions it sees, and the next call
+ * with the same arguments -- the next slice's observable, nothing having
+ * moved the colloids in between -- runs the cone without a grid launch. */
+int swarm_vision_cone_persistent(swarm_engine_t *e, const swarm_vision_params_t *vp,
+                                 const int32_t *agent_idx, int32_t n_agents,
+                                 const float *radii, const int32_t *types, float *out);
+
 /* Distances to a source for the concentration-field observable and the
  * gradient-sensing task (concentration_field.py:84-108,
  * gradient_sensing.py:92-126): for agent a of env e,

@@ -172,6 +172,10 @@ _SIGNATURES = {
         ctypes.c_int,
         [_P, ctypes.POINTER(SwarmVisionParams), _P, ctypes.c_int32, _P, _P, _P],
     ),
+    "swarm_vision_cone_persistent": (
+        ctypes.c_int,
+        [_P, ctypes.POINTER(SwarmVisionParams), _P, ctypes.c_int32, _P, _P, _P],
+    ),
     "swarm_field_distance": (
         ctypes.c_int,
         [_P, _P, ctypes.c_int32, _P, _P, _P, _P, _P, _P, ctypes.c_int32, ctypes.c_int32],

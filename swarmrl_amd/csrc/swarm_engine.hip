@@ -254,7 +254,8 @@ __device__ __forceinline__ void vision_grid_body(const DevState& st, const Visio
     for (int i = tid; i < N; i += T) vs.agent_row[i] = -1;
   __syncthreads();
   if (e == 0)
-    for (int a = tid; a < n_agents; a += T) vs.agent_row[agents[a]] = a;
+    for (int a = tid; a < n_agents; a += T)
+      if ((unsigned)agents[a] < (unsigned)N) vs.agent_row[agents[a]] = a;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   int32_t* so = start + (size_t)e * (ncell + 1);
   constexpr int kPer = 8;  // colloids per thread kept in registers (N <= 8 T)
@@ -738,32 +739,41 @@ __global__ __launch_bounds__(256) void k_pair_dist(DevState st, const double* __
 }
 
 // ------------------------------------------------------- field distance
-__global__ __launch_bounds__(256) void k_field(DevState st, const double* __restrict__ box,
-                                               const int32_t* __restrict__ agents, int n_agents,
-                                               double s0, double s1, double s2,
-                                               double b0, double b1, double b2,
-                                               uint32_t* __restrict__ hq, int32_t* __restrict__ himg,
-                                               float* __restrict__ d_cur, float* __restrict__ d_prev,
-                                               int update, int init_only, int n_envs,
-                                               int mode, float fa, float fb, float fscale,
-                                               float* __restrict__ out) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int A = n_agents * n_envs;
+struct FieldArgs {
+  const double* box;
+  const int32_t* agents;
+  int n_agents;
+  double s0, s1, s2;  // source
+  double b0, b1, b2;  // box scale
+  uint32_t* hq;
+  int32_t* himg;
+  float* d_cur;
+  float* d_prev;
+  int update, init_only, n_envs;
+  int mode;  // 0: distances; 1: scale (f(d_cur) - f(d_prev)), f(d) = fa + fb d; 2: same, clipped at 0
+  float fa, fb, fscale;
+  float* out;
+};
+
+// Agent slot t (env-major) of k_field, or of a workgroup of k_field_vgrid_sort.
+__device__ __forceinline__ void field_body(const DevState& st, const FieldArgs& f, int t) {
+  const int A = f.n_agents * f.n_envs;
   if (t >= A) return;
-  const int e = t / n_agents, ai = t - e * n_agents;
+  const int e = t / f.n_agents, ai = t - e * f.n_agents;
   const int N = st.n;
   const size_t M = (size_t)st.m;
-  const size_t gi = (size_t)e * N + agents[ai];
+  const size_t gi = (size_t)e * N + f.agents[ai];
   const double inv32 = 1.0 / 4294967296.0;
-  if (!init_only) {
-    const double src[3] = {s0 / b0, s1 / b1, s2 / b2};
-    const double bs[3] = {b0, b1, b2};
+  if (!f.init_only) {
+    const double src[3] = {f.s0 / f.b0, f.s1 / f.b1, f.s2 / f.b2};
+    const double bs[3] = {f.b0, f.b1, f.b2};
     float cur[3], prev[3];
     for (int a = 0; a < 3; ++a) {
       double pc, hp;
       if (a < st.dims) {
-        pc = ((double)st.img[a * M + gi] + (double)st.q[a * M + gi] * inv32) * box[a] / bs[a];
-        hp = ((double)himg[(size_t)a * A + t] + (double)hq[(size_t)a * A + t] * inv32) * box[a] / bs[a];
+        pc = ((double)st.img[a * M + gi] + (double)st.q[a * M + gi] * inv32) * f.box[a] / bs[a];
+        hp = ((double)f.himg[(size_t)a * A + t] + (double)f.hq[(size_t)a * A + t] * inv32) *
+             f.box[a] / bs[a];
       } else {
         pc = 0.0 / bs[a];
         hp = 0.0 / bs[a];
@@ -773,26 +783,49 @@ __global__ __launch_bounds__(256) void k_field(DevState st, const double* __rest
     }
     const float dc = swarm::sqrt_rn(cur[0] * cur[0] + cur[1] * cur[1] + cur[2] * cur[2]);
     const float dp = swarm::sqrt_rn(prev[0] * prev[0] + prev[1] * prev[1] + prev[2] * prev[2]);
-    if (mode == 0) {
-      d_cur[t] = dc;
-      d_prev[t] = dp;
+    if (f.mode == 0) {
+      f.d_cur[t] = dc;
+      f.d_prev[t] = dp;
     } else {
       // affine decay f(d) = fa + fb * d; value = scale * (f(d_cur) - f(d_prev))
       // (concentration_field.py:102-104); mode 2 clips at 0
       // (gradient_sensing.py:117-118; NaN propagates as in torch.clamp)
-      const float fc = fa + fb * dc;
-      const float fp = fa + fb * dp;
-      float v = fscale * (fc - fp);
-      if (mode == 2) v = v < 0.0f ? 0.0f : v;
-      out[t] = v;
+      const float fc = f.fa + f.fb * dc;
+      const float fp = f.fa + f.fb * dp;
+      float v = f.fscale * (fc - fp);
+      if (f.mode == 2) v = v < 0.0f ? 0.0f : v;
+      f.out[t] = v;
     }
   }
-  if (update || init_only) {
+  if (f.update || f.init_only) {
     for (int a = 0; a < 3; ++a) {
-      hq[(size_t)a * A + t] = a < st.dims ? st.q[a * M + gi] : 0u;
-      himg[(size_t)a * A + t] = a < st.dims ? st.img[a * M + gi] : 0;
+      f.hq[(size_t)a * A + t] = a < st.dims ? st.q[a * M + gi] : 0u;
+      f.himg[(size_t)a * A + t] = a < st.dims ? st.img[a * M + gi] : 0;
     }
   }
+}
+
+__global__ __launch_bounds__(256) void k_field(DevState st, FieldArgs f) {
+  field_body(st, f, blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// The reward launch of a slice whose observable is a persistent vision
+// cone (swarm_vision_cone_persistent) and whose next build is deferred:
+// the field's agents, the NEXT observable's vision grid (from the positions
+// the reward sees, which the observable will see too) and build stage 1,
+// so the observable launch only runs the cone (beside stage 2).
+template <int CH>
+__global__ __launch_bounds__(1024) void k_field_vgrid_sort(FieldArgs f, int n_fblocks, DevState st,
+                                                           VisionArgs va, Scratch sc, int lxb,
+                                                           int lyb) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int b = blockIdx.x;
+  if (b < n_fblocks)
+    field_body(st, f, b * blockDim.x + threadIdx.x);
+  else if (b < n_fblocks + va.n_envs)
+    vision_grid_body(st, va, b - n_fblocks, smem);
+  else
+    swarm::build_sort_body<CH>(st, sc, lxb, lyb, b - n_fblocks - va.n_envs, smem);
 }
 
 // --------------------------------------------------------- pair listing
@@ -935,6 +968,15 @@ struct swarm_engine {
   // build (1 sort, 2 pairs, 3 cluster build; 0 none) that rides along in the
   // next observable / policy launch; flushed before a window runs
   int ride_stage = 0;
+  // speculative vision grid (swarm_vision_cone_persistent): the last
+  // persistent call's arguments; vgrid_ready: the reward launch built the
+  // grid of the current positions for them (honoured while the deferred
+  // build is at stage 2, i.e. nothing moved the colloids since).
+  // SWARMRL_AMD_SPEC_VGRID=0 turns it off.
+  bool spec_on = true;
+  bool spec_ok = false;
+  VisionArgs spec_va{};
+  bool vgrid_ready = false;
   // swarm_engine_prebuild_noise: the next window's noise table for this many
   // sub-steps was launched ahead (on a stream of the caller's)
   int prebuilt_noise_steps = 0;
@@ -1031,6 +1073,8 @@ void set_lds_attributes() {
                        reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<true, true>),
                        reinterpret_cast<const void*>(&k_vgrid_sort<4>),
                        reinterpret_cast<const void*>(&k_vgrid_sort<16>),
+                       reinterpret_cast<const void*>(&k_field_vgrid_sort<4>),
+                       reinterpret_cast<const void*>(&k_field_vgrid_sort<16>),
                        reinterpret_cast<const void*>(&k_policy_cbuild<4, 4, 4>)};
   for (const void* f : fns)
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
@@ -1126,6 +1170,7 @@ int launch_build(swarm_engine* e, hipStream_t stream) {
 // consumer carried them along); the window then uses the build.
 int flush_ride_along(swarm_engine* e) {
   const int stage = e->ride_stage;
+  e->vgrid_ready = false;
   if (stage == 0) return SWARM_OK;
   e->ride_stage = 0;
   const int ncb = 1 << (e->lxb + e->lyb);
@@ -1661,6 +1706,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     e->noise_blocks = e->wide_run && M <= 8192 ? 64 : 0;
     const char* ow = std::getenv("SWARMRL_AMD_WIDE_RUN");
     if (ow && ow[0] == '0') e->wide_run = false, e->noise_blocks = 0;
+    if (const char* osv = std::getenv("SWARMRL_AMD_SPEC_VGRID")) e->spec_on = osv[0] != '0';
     const char* on = std::getenv("SWARMRL_AMD_WIDE_NOISE");
     if (on && on[0] == '0') e->noise_blocks = 0;
     // run waves per CU: a wave alone on its CU does not share the CU's
@@ -2142,8 +2188,16 @@ int swarm_engine_device_views(swarm_engine_t* e, swarm_device_views_t* v) {
   return SWARM_OK;
 }
 
-int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const int32_t* agent_idx,
-                      int32_t n_agents, const float* radii, const int32_t* types, float* out) {
+namespace {
+bool same_grid_args(const VisionArgs& a, const VisionArgs& b) {
+  return std::memcmp(&a.vp, &b.vp, sizeof(a.vp)) == 0 && a.lx == b.lx && a.ly == b.ly &&
+         a.radii == b.radii && a.types == b.types && a.agents == b.agents &&
+         a.n_agents == b.n_agents && a.n_envs == b.n_envs;
+}
+
+int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const int32_t* agent_idx,
+                     int32_t n_agents, const float* radii, const int32_t* types, float* out,
+                     bool persistent) {
   if (!e || !vp || !agent_idx || !radii || !types || !out) return fail(SWARM_EINVAL, "null argument");
   if (e->params.n_dims != 2) return fail(SWARM_EINVAL, "the vision-cone kernel is 2-D only");
   if (vp->n_cones < 1 || vp->n_cones > SWARM_MAX_CONES || vp->n_types < 1 ||
@@ -2169,17 +2223,24 @@ int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const 
     const int v = std::atoi(og);
     if (v == 4 || v == 16) G = v;
   }
-  // a deferred build rides along in the grid and cone launches (stages 1, 2)
-  // when their fused variants apply; else its pending stages launch first
-  const bool ride = e->ride_stage == 1 && !all && nb <= 4 && G == 16;
-  if (e->ride_stage > 0 && !ride) {
-    rc = flush_ride_along(e);
-    if (rc) return rc;
-  }
   const int ncell = 1 << (lx + ly);
   const size_t glds = 16 * 4 + (size_t)(ncell + 1) * 4;
   if (glds > kMaxLds) return fail(SWARM_ECAPACITY, "observable cell grid too large");
-  if (ride) {
+  // the grid of the current positions for these arguments, built by the
+  // reward launch (launch_field) while nothing moved the colloids since
+  const bool have_grid = !all && e->vgrid_ready && e->ride_stage == 2 &&
+                         same_grid_args(e->spec_va, va);
+  e->vgrid_ready = false;
+  e->spec_ok = persistent && !all;
+  if (e->spec_ok) e->spec_va = va;
+  // a deferred build rides along in the grid and cone launches (stages 1, 2)
+  // when their fused variants apply; else its pending stages launch first
+  const bool ride_ok = !all && nb <= 4 && G == 16;
+  if (e->ride_stage > 0 && !(ride_ok && e->ride_stage <= 2)) {
+    rc = flush_ride_along(e);
+    if (rc) return rc;
+  }
+  if (e->ride_stage == 1) {  // grid | sort, then cone | pairs
     const size_t slds = (16 + (size_t)(1 << (e->lxb + e->lyb)) + 1) * 4;
     const dim3 grid((unsigned)(2 * e->n_envs));
     if (e->n > 4096)
@@ -2189,6 +2250,12 @@ int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const 
       hipLaunchKernelGGL(k_vgrid_sort<4>, grid, dim3(1024), std::max(glds, slds), e->stream,
                          e->st, va, e->sc, e->lxb, e->lyb);
     HIP_TRY(hipGetLastError());
+    e->ride_stage = 2;
+  } else if (!have_grid) {
+    hipLaunchKernelGGL(k_vision_grid, dim3(e->n_envs), dim3(1024), glds, e->stream, e->st, va);
+    HIP_TRY(hipGetLastError());
+  }
+  if (e->ride_stage == 2) {  // cone | pairs
     const int nvb = (int)((total * 16 + 255) / 256);
     const int pbx = (e->n + 255) / 256;
     hipLaunchKernelGGL((k_vision_pairs<4, 16>), dim3((unsigned)(nvb + pbx * e->n_envs)),
@@ -2198,8 +2265,6 @@ int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const 
     e->ride_stage = 3;
     return SWARM_OK;
   }
-  hipLaunchKernelGGL(k_vision_grid, dim3(e->n_envs), dim3(1024), glds, e->stream, e->st, va);
-  HIP_TRY(hipGetLastError());
   if (all) {
     const dim3 agrid((unsigned)((total * 16 + 255) / 256)), ablock(256);
 #define SWARM_VALL(NBV)                                                                          \
@@ -2246,6 +2311,47 @@ int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const 
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
 }
+}  // namespace
+
+int swarm_vision_cone(swarm_engine_t* e, const swarm_vision_params_t* vp, const int32_t* agent_idx,
+                      int32_t n_agents, const float* radii, const int32_t* types, float* out) {
+  return vision_cone_impl(e, vp, agent_idx, n_agents, radii, types, out, false);
+}
+
+int swarm_vision_cone_persistent(swarm_engine_t* e, const swarm_vision_params_t* vp,
+                                 const int32_t* agent_idx, int32_t n_agents, const float* radii,
+                                 const int32_t* types, float* out) {
+  return vision_cone_impl(e, vp, agent_idx, n_agents, radii, types, out, true);
+}
+
+namespace {
+// k_field, or with a pending deferred build and a persistent vision cone the
+// fused k_field_vgrid_sort (stage 1 and the next observable's grid ride
+// along in the reward launch).
+int launch_field(swarm_engine* e, const FieldArgs& f) {
+  const int total = f.n_agents * e->n_envs;
+  if (e->spec_on && e->spec_ok && e->ride_stage == 1) {
+    const VisionArgs& va = e->spec_va;
+    const size_t glds = (16 + (size_t)(1 << (va.lx + va.ly)) + 1) * 4;
+    const size_t slds = (16 + (size_t)(1 << (e->lxb + e->lyb)) + 1) * 4;
+    const int nfb = (total + 1023) / 1024;
+    const dim3 grid((unsigned)(nfb + 2 * e->n_envs));
+    if (e->n > 4096)
+      hipLaunchKernelGGL(k_field_vgrid_sort<16>, grid, dim3(1024), std::max(glds, slds),
+                         e->stream, f, nfb, e->st, va, e->sc, e->lxb, e->lyb);
+    else
+      hipLaunchKernelGGL(k_field_vgrid_sort<4>, grid, dim3(1024), std::max(glds, slds),
+                         e->stream, f, nfb, e->st, va, e->sc, e->lxb, e->lyb);
+    HIP_TRY(hipGetLastError());
+    e->ride_stage = 2;
+    e->vgrid_ready = true;
+    return SWARM_OK;
+  }
+  hipLaunchKernelGGL(k_field, dim3((total + 255) / 256), dim3(256), 0, e->stream, e->st, f);
+  HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+}  // namespace
 
 int swarm_field_distance(swarm_engine_t* e, const int32_t* agent_idx, int32_t n_agents,
                          const double source[3], const double box_scale[3], uint32_t* hist_q,
@@ -2254,16 +2360,13 @@ int swarm_field_distance(swarm_engine_t* e, const int32_t* agent_idx, int32_t n_
   if (!e || !agent_idx || !hist_q || !hist_img) return fail(SWARM_EINVAL, "null argument");
   if (!init_only && (!d_cur || !d_prev || !source || !box_scale)) return fail(SWARM_EINVAL, "null argument");
   if (n_agents <= 0) return SWARM_OK;
-  const int total = n_agents * e->n_envs;
   const double s[3] = {source ? source[0] : 0.0, source ? source[1] : 0.0, source ? source[2] : 0.0};
   const double b[3] = {box_scale ? box_scale[0] : 1.0, box_scale ? box_scale[1] : 1.0,
                        box_scale ? box_scale[2] : 1.0};
-  hipLaunchKernelGGL(k_field, dim3((total + 255) / 256), dim3(256), 0, e->stream, e->st, e->d_box,
-                     agent_idx, n_agents, s[0], s[1], s[2], b[0], b[1], b[2], hist_q, hist_img,
-                     d_cur, d_prev, update_history, init_only, e->n_envs, 0, 0.0f, 0.0f, 0.0f,
-                     nullptr);
-  HIP_TRY(hipGetLastError());
-  return SWARM_OK;
+  const FieldArgs f{e->d_box, agent_idx, n_agents, s[0], s[1], s[2], b[0], b[1], b[2], hist_q,
+                    hist_img, d_cur, d_prev, update_history, init_only, e->n_envs, 0, 0.0f, 0.0f,
+                    0.0f, nullptr};
+  return launch_field(e, f);
 }
 
 int swarm_field_transform(swarm_engine_t* e, const int32_t* agent_idx, int32_t n_agents,
@@ -2273,13 +2376,10 @@ int swarm_field_transform(swarm_engine_t* e, const int32_t* agent_idx, int32_t n
   if (!e || !agent_idx || !hist_q || !hist_img || !source || !box_scale || !out)
     return fail(SWARM_EINVAL, "null argument");
   if (n_agents <= 0) return SWARM_OK;
-  const int total = n_agents * e->n_envs;
-  hipLaunchKernelGGL(k_field, dim3((total + 255) / 256), dim3(256), 0, e->stream, e->st, e->d_box,
-                     agent_idx, n_agents, source[0], source[1], source[2], box_scale[0],
-                     box_scale[1], box_scale[2], hist_q, hist_img, nullptr, nullptr, 1, 0,
-                     e->n_envs, clip_at_zero ? 2 : 1, decay_a, decay_b, scale, out);
-  HIP_TRY(hipGetLastError());
-  return SWARM_OK;
+  const FieldArgs f{e->d_box, agent_idx, n_agents, source[0], source[1], source[2],
+                    box_scale[0], box_scale[1], box_scale[2], hist_q, hist_img, nullptr, nullptr,
+                    1, 0, e->n_envs, clip_at_zero ? 2 : 1, decay_a, decay_b, scale, out};
+  return launch_field(e, f);
 }
 
 int swarm_pair_distances(swarm_engine_t* e, const int32_t* agent_idx, int32_t n_agents,
@@ -2535,6 +2635,7 @@ int swarm_engine_defer_build(swarm_engine_t* e, int32_t* deferred) {
   if (!ok) return SWARM_OK;
   e->prebuilt = false;
   e->ride_stage = 1;
+  e->vgrid_ready = false;
   *deferred = 1;
   return SWARM_OK;
 }

@@ -60,8 +60,12 @@ def vision_params(vision_range, half_angle, n_cones, detected_types) -> _capi.Sw
 
 
 def vision_cone(native, n_envs: int, agent_idx: torch.Tensor, radii: torch.Tensor,
-                types: torch.Tensor, vp: _capi.SwarmVisionParams) -> torch.Tensor:
-    """[E, A, n_cones, n_types] fp32 device tensor (k_vision)."""
+                types: torch.Tensor, vp: _capi.SwarmVisionParams,
+                persistent: bool = False) -> torch.Tensor:
+    """[E, A, n_cones, n_types] fp32 device tensor (k_vision).  persistent:
+    the caller keeps agent_idx, radii and types alive and unchanged for the
+    engine's lifetime (swarm_vision_cone_persistent: the next slice's grid
+    may then be built by the reward launch)."""
     A = int(agent_idx.numel())
     out = torch.empty((n_envs, A, vp.n_cones, vp.n_types), dtype=torch.float32,
                       device=agent_idx.device)
@@ -69,8 +73,8 @@ def vision_cone(native, n_envs: int, agent_idx: torch.Tensor, radii: torch.Tenso
         return out
     native.bind_stream()
     native.call(
-        "swarm_vision_cone", ctypes.byref(vp), agent_idx.data_ptr(), A, radii.data_ptr(),
-        types.data_ptr(), out.data_ptr(),
+        "swarm_vision_cone_persistent" if persistent else "swarm_vision_cone", ctypes.byref(vp),
+        agent_idx.data_ptr(), A, radii.data_ptr(), types.data_ptr(), out.data_ptr(),
     )
     return out
 

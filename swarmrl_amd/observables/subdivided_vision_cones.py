@@ -90,10 +90,12 @@ class SubdividedVisionCones(Observable):
                 self._radii_device = torch.as_tensor(
                     np.asarray(self.radii, dtype=np.float32), device=view.device
                 )
+            # agents (cached by the view), radii (cached here) and types (the
+            # engine's) outlive the engine's use of them: persistent call
             agents = view.indices_of_type(self.particle_type)
             return ops.vision_cone(
                 view.engine._native, view.n_envs, agents, self._radii_device, view.types,
-                self._params(),
+                self._params(), persistent=True,
             )
         reference_ids = self.get_colloid_indices(colloids)
         if len(reference_ids) == 0:
