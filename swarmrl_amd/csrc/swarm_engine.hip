@@ -232,7 +232,15 @@ struct VisionArgs {
   VisionSorted vs;
   float* out;
   int n_envs;
+  int staged;  // 1: the records are scattered into LDS, then written in order
 };
+
+// LDS of the vision grid's workgroup: wave sums, cell counts and, staged,
+// the env's 2 x uint4 records (host and device agree through va.staged).
+inline size_t vision_grid_lds_bytes(int lx, int ly, int n, bool staged) {
+  const size_t counts = (16 + ((size_t)1 << (lx + ly)) + 1) * 4;
+  return staged ? ((counts + 15) & ~(size_t)15) + 32 * (size_t)n : counts;
+}
 
 // Body for the workgroup of env e (k_vision_grid, or k_vgrid_sort).
 __device__ __forceinline__ void vision_grid_body(const DevState& st, const VisionArgs& va, int e,
@@ -285,6 +293,24 @@ __device__ __forceinline__ void vision_grid_body(const DevState& st, const Visio
     __syncthreads();
     for (int c = tid; c <= ncell; c += T) so[c] = cnt[c];
     __syncthreads();
+    if (va.staged) {
+      // scatter into LDS (16-byte aligned after the counts), then write the
+      // records in order: coalesced stores instead of 2 N scattered ones
+      uint4* lrec = reinterpret_cast<uint4*>(
+          smem + (((16 + (size_t)ncell + 1) * 4 + 15) & ~(size_t)15));
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        if (tid + k * T < N) {
+          const int pos = atomicAdd(&cnt[cell[k]], 1);
+          lrec[2 * pos] = r0[k];
+          lrec[2 * pos + 1] = r1[k];
+        }
+      }
+      __syncthreads();
+      uint4* grec = vs.rec + 2 * base;
+      for (int p = tid; p < 2 * N; p += T) grec[p] = lrec[p];
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       if (tid + k * T < N) {
@@ -1046,6 +1072,10 @@ size_t check_lds_bytes(int lx, int ly, int n, int dims) {
   return (16 + 16 + 1024 + std::max(rerun, big)) * 4;
 }
 
+// k_build_sort (and the fused launches carrying it): wave sums, cell counts
+// and, staged, the sorted x | y | id rows.
+size_t sort_lds_bytes(const swarm_engine* e);
+
 // k_check3: wave sums, misc, movers, then the 3-D global path's cell counts
 size_t check3_lds_bytes(const swarm_engine* e) {
   return (16 + 16 + (size_t)swarm::kMaxMovers + (size_t)(1 << (e->lxg + e->lyg + e->lzg)) + 1) * 4;
@@ -1111,7 +1141,6 @@ int launch_noise(swarm_engine* e, hipStream_t stream, int n) {
 
 // Cluster build of the next window.
 int launch_build(swarm_engine* e, hipStream_t stream) {
-  const int ncb = 1 << (e->lxb + e->lyb + e->lzb);
   if (e->env_build) {
     hipLaunchKernelGGL(swarm::k_build_env, dim3(e->n_envs), dim3(1024),
                        build_lds_bytes(e->n, e->sc.pair_cap), stream, e->d_derived, e->st, e->sc,
@@ -1121,10 +1150,10 @@ int launch_build(swarm_engine* e, hipStream_t stream) {
   }
   if (e->params.n_dims == 3) {
     if (e->n > 4096)
-      hipLaunchKernelGGL(swarm::k_build_sort3<16>, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4,
+      hipLaunchKernelGGL(swarm::k_build_sort3<16>, dim3(e->n_envs), dim3(1024), sort_lds_bytes(e),
                          stream, e->st, e->sc, e->lxb, e->lyb, e->lzb);
     else
-      hipLaunchKernelGGL(swarm::k_build_sort3<4>, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4,
+      hipLaunchKernelGGL(swarm::k_build_sort3<4>, dim3(e->n_envs), dim3(1024), sort_lds_bytes(e),
                          stream, e->st, e->sc, e->lxb, e->lyb, e->lzb);
     HIP_TRY(hipGetLastError());
     if (e->nlist_path) {  // Verlet lists, no clusters
@@ -1136,10 +1165,10 @@ int launch_build(swarm_engine* e, hipStream_t stream) {
     hipLaunchKernelGGL(swarm::k_build_pairs3, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
                        dim3(256), 0, stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb, e->lzb);
   } else if (e->n > 4096)
-    hipLaunchKernelGGL(swarm::k_build_sort<16>, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4,
+    hipLaunchKernelGGL(swarm::k_build_sort<16>, dim3(e->n_envs), dim3(1024), sort_lds_bytes(e),
                        stream, e->st, e->sc, e->lxb, e->lyb);
   else
-    hipLaunchKernelGGL(swarm::k_build_sort<4>, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4,
+    hipLaunchKernelGGL(swarm::k_build_sort<4>, dim3(e->n_envs), dim3(1024), sort_lds_bytes(e),
                        stream, e->st, e->sc, e->lxb, e->lyb);
   HIP_TRY(hipGetLastError());
   if (e->params.n_dims != 3 && e->nlist_path) {  // Verlet lists, no clusters
@@ -1173,13 +1202,12 @@ int flush_ride_along(swarm_engine* e) {
   e->vgrid_ready = false;
   if (stage == 0) return SWARM_OK;
   e->ride_stage = 0;
-  const int ncb = 1 << (e->lxb + e->lyb);
   if (stage <= 1) {
     if (e->n > 4096)
-      hipLaunchKernelGGL(swarm::k_build_sort<16>, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4,
+      hipLaunchKernelGGL(swarm::k_build_sort<16>, dim3(e->n_envs), dim3(1024), sort_lds_bytes(e),
                          e->stream, e->st, e->sc, e->lxb, e->lyb);
     else
-      hipLaunchKernelGGL(swarm::k_build_sort<4>, dim3(e->n_envs), dim3(1024), (16 + ncb + 1) * 4,
+      hipLaunchKernelGGL(swarm::k_build_sort<4>, dim3(e->n_envs), dim3(1024), sort_lds_bytes(e),
                          e->stream, e->st, e->sc, e->lxb, e->lyb);
     HIP_TRY(hipGetLastError());
   }
@@ -1265,6 +1293,11 @@ int launch_run(swarm_engine* e, int n_steps) {
 // The window's cell-sorted snapshot is in global memory unless the build
 // was k_build_env (LDS-resident): k_check then takes each mover's
 // candidates from its cells (-1: every colloid).
+size_t sort_lds_bytes(const swarm_engine* e) {
+  const size_t ncb = (size_t)1 << (e->lxb + e->lyb + e->lzb);
+  return (16 + ncb + 1 + (e->sc.sort_staged ? 3 * (size_t)e->n : 0)) * 4;
+}
+
 int check_cell_lx(const swarm_engine* e) { return e->env_build ? -1 : e->lxb; }
 int check_cell_ly(const swarm_engine* e) { return e->env_build ? -1 : e->lyb; }
 
@@ -1551,6 +1584,13 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   // SWARMRL_AMD_CLUSTER_PATH=0 forces the global path (A/B and parity)
   e->sc.periodic = params->periodic ? 1 : 0;
   e->sc.multi_species = params->n_species > 1 ? 1 : 0;
+  // the 2-D build sort stages its scatter in LDS when the sorted rows fit
+  // beside the cell counts (SWARMRL_AMD_SORT_STAGED=0 turns it off)
+  e->sc.sort_staged =
+      params->n_dims == 2 && n_particles <= 4096 &&
+      (16 + ((size_t)1 << (e->lxb + e->lyb)) + 1 + 3 * (size_t)n_particles) * 4 <= kMaxLds;
+  if (const char* oss = std::getenv("SWARMRL_AMD_SORT_STAGED"))
+    if (oss[0] == '0') e->sc.sort_staged = 0;
   e->cluster_path = (params->periodic || !three_d) && e->sc.pair_cap >= n_particles &&
                     n_particles < 65536 &&
                     swarm::build_lds_words_big(n_particles) * 4 <= kMaxLds &&
@@ -2211,8 +2251,12 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
   cell_grid(e->params, e->n, (double)vp->vision_range, &lx, &ly);
   int rc = ensure_grid_scratch(e, lx, ly);
   if (rc) return rc;
-  const VisionArgs va{*vp, lx, ly, radii, types, agent_idx, n_agents, e->d_start, e->vs, out,
-                      e->n_envs};
+  // records staged in LDS when the env's fit (N <= 8 x 1024: the register path)
+  const bool staged = e->n <= 8 * 1024 && vision_grid_lds_bytes(lx, ly, e->n, true) <= kMaxLds &&
+                      !(std::getenv("SWARMRL_AMD_VGRID_STAGED") &&
+                        std::getenv("SWARMRL_AMD_VGRID_STAGED")[0] == '0');
+  const VisionArgs va{*vp,          lx,        ly,    radii, types, agent_idx, n_agents,
+                      e->d_start,   e->vs,     out,   e->n_envs, staged ? 1 : 0};
   const long total = (long)e->n * e->n_envs;  // one group per sorted particle
   const int nb = vp->n_cones * vp->n_types;
   // lanes per agent: enough threads to give every SIMD a few waves, few
@@ -2223,8 +2267,7 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
     const int v = std::atoi(og);
     if (v == 4 || v == 16) G = v;
   }
-  const int ncell = 1 << (lx + ly);
-  const size_t glds = 16 * 4 + (size_t)(ncell + 1) * 4;
+  const size_t glds = vision_grid_lds_bytes(lx, ly, e->n, staged);
   if (glds > kMaxLds) return fail(SWARM_ECAPACITY, "observable cell grid too large");
   // the grid of the current positions for these arguments, built by the
   // reward launch (launch_field) while nothing moved the colloids since
@@ -2241,7 +2284,7 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
     if (rc) return rc;
   }
   if (e->ride_stage == 1) {  // grid | sort, then cone | pairs
-    const size_t slds = (16 + (size_t)(1 << (e->lxb + e->lyb)) + 1) * 4;
+    const size_t slds = sort_lds_bytes(e);
     const dim3 grid((unsigned)(2 * e->n_envs));
     if (e->n > 4096)
       hipLaunchKernelGGL(k_vgrid_sort<16>, grid, dim3(1024), std::max(glds, slds), e->stream,
@@ -2332,8 +2375,8 @@ int launch_field(swarm_engine* e, const FieldArgs& f) {
   const int total = f.n_agents * e->n_envs;
   if (e->spec_on && e->spec_ok && e->ride_stage == 1) {
     const VisionArgs& va = e->spec_va;
-    const size_t glds = (16 + (size_t)(1 << (va.lx + va.ly)) + 1) * 4;
-    const size_t slds = (16 + (size_t)(1 << (e->lxb + e->lyb)) + 1) * 4;
+    const size_t glds = vision_grid_lds_bytes(va.lx, va.ly, e->n, va.staged != 0);
+    const size_t slds = sort_lds_bytes(e);
     const int nfb = (total + 1023) / 1024;
     const dim3 grid((unsigned)(nfb + 2 * e->n_envs));
     if (e->n > 4096)
