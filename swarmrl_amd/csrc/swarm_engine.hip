@@ -452,6 +452,57 @@ __device__ __forceinline__ void vision_drain(const VisionLane& L, const swarm_vi
   }
 }
 
+// The same over the G lanes' lists of a group together: the group's hits,
+// concatenated in lane order, are dealt round-robin to its lanes, so a lane
+// evaluates ceil(total / G) of them instead of its own list's length (the
+// wave runs as long as its longest: ~6 hits of Poisson(2) lists against ~4
+// of the balanced ones at E = 64).  Integer bin sums: the same result.
+// Whole groups are active together (they share one agent).
+template <int NB, int G, bool kAny = false>
+__device__ __forceinline__ void vision_drain_group(const VisionLane& L,
+                                                   const swarm_vision_params_t& vp,
+                                                   const uint4* __restrict__ rec, size_t base,
+                                                   const uint32_t (*hits)[256], int nh,
+                                                   int64_t* acc) {
+  // the other lanes' list entries are read below: keep the compiler from
+  // moving those LDS reads above this lane's writes (one wave's LDS
+  // operations complete in order)
+  __asm__ volatile("" ::: "memory");
+  const int sub = threadIdx.x & (G - 1);
+  const int lane0 = (threadIdx.x & 63) - sub;  // the group's first lane in the wave
+  const int tid0 = threadIdx.x - sub;
+  int cnt[G];
+  int total = 0;
+#pragma unroll
+  for (int l = 0; l < G; ++l) {
+    cnt[l] = __shfl(nh, lane0 + l, 64);
+    total += cnt[l];
+  }
+  for (int h0 = sub; __any(h0 < total); h0 += 4 * G) {
+    uint4 c0[4], c1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int h = h0 + u * G;
+      if (h < total) {
+        int owner = 0, k = h, pre = 0;
+#pragma unroll
+        for (int l = 0; l < G; ++l) {
+          const bool in = h >= pre && h < pre + cnt[l];
+          owner = in ? l : owner;
+          k = in ? h - pre : k;
+          pre += cnt[l];
+        }
+        const size_t jj = base + hits[k][tid0 + owner];
+        c0[u] = rec[2 * jj];
+        c1[u] = rec[2 * jj + 1];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (h0 + u * G < total) vision_hit<NB, kAny>(L, vp, c0[u], c1[u], acc);
+  }
+}
+
 // kAll: vision_range >= half the box (the reference has no range limit,
 // subdivided_vision_cones.py:116-121): every record of the env is a
 // candidate, tested on its unwrapped (int64) separation.
@@ -489,7 +540,8 @@ __device__ __forceinline__ void vision_body(const DevState& st, const Derived* _
   VisionLane L;
   L.i = vision_rec_id(own1.y);
   const int row = vs.agent_row[L.i];
-  if (row < 0) return;
+  // (the candidate ranges below load beside agent_row: both wait on the own
+  // record only; a non-agent group leaves after them)
   L.qxi = own0.x;
   L.qyi = own0.y;
   L.ixi = (int32_t)own0.z;
@@ -538,12 +590,20 @@ __device__ __forceinline__ void vision_body(const DevState& st, const Derived* _
     off[r] = jb - pre[r];
     pre[r + 1] = pre[r] + (je - jb);
   }
+  if (row < 0) return;
   const int total = pre[6];
-  for (int f0 = sub; f0 < total; f0 += 4 * G) {
-    uint4 c0[4];
-    int jj[4];
+  // kVF candidates per lane in flight per round
+#ifndef SWARM_VISION_FLY
+#define SWARM_VISION_FLY 4
+#endif
+  constexpr int kVF = SWARM_VISION_FLY;
+  // (group-uniform trip count: a drain below always finds whole groups)
+  for (int f00 = 0; f00 < total; f00 += kVF * G) {
+    const int f0 = f00 + sub;
+    uint4 c0[kVF];
+    int jj[kVF];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kVF; ++u) {
       const int f = f0 + u * G;
       int o = off[0];
 #pragma unroll
@@ -553,18 +613,24 @@ __device__ __forceinline__ void vision_body(const DevState& st, const Derived* _
       if (f < total) c0[u] = vs.rec[2 * (base + j)];
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kVF; ++u) {
       float ddx, ddy;
       if (f0 + u * G < total &&
           (kAll ? vision_offsets<true>(L, c0[u], &ddx, &ddy) : vision_near(L, c0[u])))
         hits[nh++][threadIdx.x] = jj[u];
     }
-    if (__any(nh > kVisionHits - 4)) {  // no room for four more: drain every lane's
-      vision_drain<NB, kAll>(L, vp, vs.rec, base, hits, nh, acc);
+    if (__any(nh > kVisionHits - kVF)) {  // no room for kVF more: drain every lane's
+      if (G <= 8)
+        vision_drain_group<NB, G, kAll>(L, vp, vs.rec, base, hits, nh, acc);
+      else
+        vision_drain<NB, kAll>(L, vp, vs.rec, base, hits, nh, acc);
       nh = 0;
     }
   }
-  vision_drain<NB, kAll>(L, vp, vs.rec, base, hits, nh, acc);
+  if (G <= 8)
+    vision_drain_group<NB, G, kAll>(L, vp, vs.rec, base, hits, nh, acc);
+  else
+    vision_drain<NB, kAll>(L, vp, vs.rec, base, hits, nh, acc);
 #pragma unroll
   for (int off = G / 2; off > 0; off >>= 1) {
 #pragma unroll
@@ -2262,10 +2328,13 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
   // lanes per agent: enough threads to give every SIMD a few waves, few
   // enough that the lanes of a wave stay busy (measured, tools/vision_time.py:
   // 64 x 4096 agents 107 -> 93 us with G = 4 instead of 1)
-  int G = total >= (1L << 15) ? 4 : 16;
+#ifndef SWARM_VISION_G_WIDE
+#define SWARM_VISION_G_WIDE 4
+#endif
+  int G = total >= (1L << 15) ? SWARM_VISION_G_WIDE : 16;
   if (const char* og = std::getenv("SWARMRL_AMD_VISION_G")) {
     const int v = std::atoi(og);
-    if (v == 4 || v == 16) G = v;
+    if (v == SWARM_VISION_G_WIDE || v == 16) G = v;
   }
   const size_t glds = vision_grid_lds_bytes(lx, ly, e->n, staged);
   if (glds > kMaxLds) return fail(SWARM_ECAPACITY, "observable cell grid too large");
@@ -2335,10 +2404,10 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
 #define SWARM_VISION(NBV, GV)                                                                  \
   hipLaunchKernelGGL((k_vision<NBV, GV>), grid, block, 0, e->stream, e->st, e->d_derived, va, \
                      xcd ? bpe : 0)
-#define SWARM_VISION_G(NBV) \
-  if (G == 4)               \
-    SWARM_VISION(NBV, 4);   \
-  else                      \
+#define SWARM_VISION_G(NBV)                      \
+  if (G == SWARM_VISION_G_WIDE)                  \
+    SWARM_VISION(NBV, SWARM_VISION_G_WIDE);      \
+  else                                           \
     SWARM_VISION(NBV, 16)
   if (nb <= 4) {
     SWARM_VISION_G(4);

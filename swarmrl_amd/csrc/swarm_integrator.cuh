@@ -1206,7 +1206,10 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
   // jj = f + off[r] of the range r holding f: kFly candidates in flight per
   // iteration whatever the split over the ranges (about 11 candidates at
   // area fraction 0.1: two rounds of loads, not one per range)
-  constexpr int kFly = 8;
+#ifndef SWARM_PAIRS_FLY
+#define SWARM_PAIRS_FLY 8
+#endif
+  constexpr int kFly = SWARM_PAIRS_FLY;
   int off[6], pre[7];
   pre[0] = 0;
 #pragma unroll
