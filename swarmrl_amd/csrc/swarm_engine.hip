@@ -1361,7 +1361,7 @@ int launch_run(swarm_engine* e, int n_steps) {
 // candidates from its cells (-1: every colloid).
 size_t sort_lds_bytes(const swarm_engine* e) {
   const size_t ncb = (size_t)1 << (e->lxb + e->lyb + e->lzb);
-  return (16 + ncb + 1 + (e->sc.sort_staged ? 3 * (size_t)e->n : 0)) * 4;
+  return (16 + ncb + 1 + 3 * (size_t)e->sc.sort_stage_k) * 4;
 }
 
 int check_cell_lx(const swarm_engine* e) { return e->env_build ? -1 : e->lxb; }
@@ -1650,13 +1650,20 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   // SWARMRL_AMD_CLUSTER_PATH=0 forces the global path (A/B and parity)
   e->sc.periodic = params->periodic ? 1 : 0;
   e->sc.multi_species = params->n_species > 1 ? 1 : 0;
-  // the 2-D build sort stages its scatter in LDS when the sorted rows fit
-  // beside the cell counts (SWARMRL_AMD_SORT_STAGED=0 turns it off)
-  e->sc.sort_staged =
-      params->n_dims == 2 && n_particles <= 4096 &&
-      (16 + ((size_t)1 << (e->lxb + e->lyb)) + 1 + 3 * (size_t)n_particles) * 4 <= kMaxLds;
-  if (const char* oss = std::getenv("SWARMRL_AMD_SORT_STAGED"))
-    if (oss[0] == '0') e->sc.sort_staged = 0;
+  // the 2-D build sort stages its scatter in LDS: the sorted rows of up to
+  // K entries per pass beside the cell counts (K a multiple of 4, at least
+  // N / 4; SWARMRL_AMD_SORT_STAGED=0 turns it off)
+  {
+    const size_t counts = (16 + ((size_t)1 << (e->lxb + e->lyb)) + 1) * 4;
+    const size_t room = counts + 4096 < kMaxLds ? kMaxLds - counts - 4096 : 0;
+    const size_t k = std::min((size_t)n_particles, room / 12) & ~(size_t)3;
+    e->sc.sort_stage_k = params->n_dims == 2 && n_particles <= 16 * 1024 &&
+                                 4 * k >= (size_t)n_particles
+                             ? (int32_t)k
+                             : 0;
+    if (const char* oss = std::getenv("SWARMRL_AMD_SORT_STAGED"))
+      if (oss[0] == '0') e->sc.sort_stage_k = 0;
+  }
   e->cluster_path = (params->periodic || !three_d) && e->sc.pair_cap >= n_particles &&
                     n_particles < 65536 &&
                     swarm::build_lds_words_big(n_particles) * 4 <= kMaxLds &&

@@ -216,7 +216,8 @@ struct Scratch {
   int32_t fill_singletons;  // 1: singletons take the tail lanes of the other classes
   int32_t periodic;   // 0: non-periodic box (edge cells, unwrapped pair distances; 2-D build)
   int32_t multi_species;  // 0: one species (species pair bits 0, no species loads in the build)
-  int32_t sort_staged;    // 1: the build sort scatters into LDS and writes its output coalesced
+  int32_t sort_stage_k;   // > 0: the build sort scatters into LDS, this many sorted entries per
+                          // pass, and writes its output coalesced (0: scattered stores)
   int32_t S;          // slots per env
   int32_t wmax;       // S / 64
   uint64_t* phase;    // [32] build phase stamps (SWARM_PHASE_TIMING builds only)
@@ -1076,37 +1077,51 @@ __device__ __forceinline__ void build_sort_body(const DevState& st, const Scratc
   for (int c = tid; c <= ncell; c += T) cs[c] = cnt[c];
   __syncthreads();  // cnt is read above and incremented below
   SWARM_STAMP(4);
-  if (sc.sort_staged && N <= CH * T) {
-    // scatter into LDS (x | y | id rows of N words after the counts), then
-    // write the sorted arrays in order: coalesced 16-byte stores instead of
-    // 3 N scattered 4-byte ones, which one CU issues slowly
-    uint32_t* lx_ = reinterpret_cast<uint32_t*>(cnt + ncell + 1);
-    uint32_t* ly_ = lx_ + N;
-    int32_t* lid = reinterpret_cast<int32_t*>(ly_ + N);
+  if (sc.sort_stage_k > 0 && N <= CH * T) {
+    // claim every cached particle's sorted position, then per pass of K
+    // sorted entries scatter the ones that fall in it into LDS (x | y | id
+    // rows after the counts) and write the pass out in order: coalesced
+    // 16-byte stores instead of 3 N scattered 4-byte ones, which one CU
+    // issues at about one lane per cycle (43 k of the 63 k cycles of a
+    // 16384-colloid sort)
+    const int K = sc.sort_stage_k;
+    int spos[CH];
 #pragma unroll
-    for (int k = 0; k < CH; ++k) {
-      if (cid[k] < 0) continue;
-      const int pos = atomicAdd(&cnt[cell_of(tid + k * T, cqx[k], cqy[k])], 1);
-      lx_[pos] = cqx[k];
-      ly_[pos] = cqy[k];
-      lid[pos] = cid[k];
-    }
-    __syncthreads();
-    if ((N & 3) == 0 && (M & 3) == 0) {
-      uint4* gx = reinterpret_cast<uint4*>(sc.bsq + base);
-      uint4* gy = reinterpret_cast<uint4*>(sc.bsq + M + base);
-      int4* gi = reinterpret_cast<int4*>(sc.bsid + base);
-      for (int p = tid; p < (N >> 2); p += T) {
-        gx[p] = reinterpret_cast<const uint4*>(lx_)[p];
-        gy[p] = reinterpret_cast<const uint4*>(ly_)[p];
-        gi[p] = reinterpret_cast<const int4*>(lid)[p];
+    for (int k = 0; k < CH; ++k)
+      spos[k] = cid[k] >= 0 ? atomicAdd(&cnt[cell_of(tid + k * T, cqx[k], cqy[k])], 1) : -1;
+    uint32_t* lx_ = reinterpret_cast<uint32_t*>(cnt + ncell + 1);
+    uint32_t* ly_ = lx_ + K;
+    int32_t* lid = reinterpret_cast<int32_t*>(ly_ + K);
+    const bool vec = (N & 3) == 0 && (M & 3) == 0 && (K & 3) == 0;
+    for (int p0 = 0; p0 < N; p0 += K) {
+      const int kn = min(K, N - p0);
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {
+        const int r = spos[k] - p0;
+        if (r >= 0 && r < kn) {
+          lx_[r] = cqx[k];
+          ly_[r] = cqy[k];
+          lid[r] = cid[k];
+        }
       }
-    } else {
-      for (int p = tid; p < N; p += T) {
-        sc.bsq[base + p] = lx_[p];
-        sc.bsq[M + base + p] = ly_[p];
-        sc.bsid[base + p] = lid[p];
+      __syncthreads();
+      if (vec) {
+        uint4* gx = reinterpret_cast<uint4*>(sc.bsq + base + p0);
+        uint4* gy = reinterpret_cast<uint4*>(sc.bsq + M + base + p0);
+        int4* gi = reinterpret_cast<int4*>(sc.bsid + base + p0);
+        for (int v = tid; v < (kn >> 2); v += T) {
+          gx[v] = reinterpret_cast<const uint4*>(lx_)[v];
+          gy[v] = reinterpret_cast<const uint4*>(ly_)[v];
+          gi[v] = reinterpret_cast<const int4*>(lid)[v];
+        }
+      } else {
+        for (int v = tid; v < kn; v += T) {
+          sc.bsq[base + p0 + v] = lx_[v];
+          sc.bsq[M + base + p0 + v] = ly_[v];
+          sc.bsid[base + p0 + v] = lid[v];
+        }
       }
+      __syncthreads();  // the rows are refilled by the next pass
     }
     for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
     SWARM_STAMP(5);
