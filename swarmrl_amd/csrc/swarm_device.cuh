@@ -295,12 +295,60 @@ __device__ __forceinline__ int64_t f2fix24(float v) {
 // correctly rounded value in four branch-free instructions; larger values
 // (never in practice) take the generic conversion behind a wave-uniform
 // branch.
-__device__ __forceinline__ float i64_to_f32(int64_t a) {
+__device__ __forceinline__ float i64_to_f32_wide(int64_t a) {
   const double d = fma((double)(int32_t)(a >> 32), 4294967296.0, (double)(uint32_t)a);
   float r = (float)d;
   const bool big = a >= (int64_t)9007199254740992LL || a <= -(int64_t)9007199254740992LL;
   if (__builtin_expect(__any(big), 0)) r = big ? (float)a : r;
   return r;
+}
+
+// every active lane's predicate (one v_cmp into an SGPR pair and a scalar
+// compare with exec; __all goes through a VGPR select and a second compare)
+__device__ __forceinline__ bool wave_all(bool p) {
+  return __builtin_amdgcn_ballot_w64(p) == __builtin_amdgcn_read_exec();
+}
+
+__device__ __forceinline__ bool fits_i32(int64_t a) {
+  return (int32_t)(a >> 32) == ((int32_t)a >> 31);
+}
+
+// int64 -> fp32 round-to-nearest; when every lane's value fits in int32
+// (force sums below 128 in 2^-24 fixed point: the common case) one
+// v_cvt_f32_i32 -- the same correctly rounded value -- instead of the fp64
+// path.
+__device__ __forceinline__ float i64_to_f32(int64_t a) {
+  if (__builtin_expect(wave_all(fits_i32(a)), 1)) return (float)(int32_t)a;
+  return i64_to_f32_wide(a);
+}
+
+// both components behind one wave-uniform test
+__device__ __forceinline__ void i64x2_to_f32(int64_t ax, int64_t ay, float* fx, float* fy) {
+  if (__builtin_expect(wave_all(fits_i32(ax) && fits_i32(ay)), 1)) {
+    *fx = (float)(int32_t)ax;
+    *fy = (float)(int32_t)ay;
+  } else {
+    *fx = i64_to_f32_wide(ax);
+    *fy = i64_to_f32_wide(ay);
+  }
+}
+
+// 1 / x correctly rounded, for x in [2^-96, 2^96] (every in-range squared
+// pair distance: the fixed-point grid step is >= 2^-48).  It is the
+// compiler's IEEE division sequence for 1.0f / x (v_rcp_f32, a Newton step,
+// then two residual corrections) without the v_div_scale / v_div_fmas /
+// v_div_fixup range handling, which is the identity on this range (no
+// scaling: the exponents of 1 and x differ by < 96, neither is denormal).
+// Bit-identical to 1.0f / x over the whole range: tests/test_gpu_rcp.py
+// checks every float in it on the GPU.
+__device__ __forceinline__ float rcp_rn(float x) {
+  float y = __builtin_amdgcn_rcpf(x);
+  const float e = __builtin_fmaf(-x, y, 1.0f);
+  y = __builtin_fmaf(e, y, y);
+  float r = __builtin_fmaf(-x, y, 1.0f);
+  const float q = __builtin_fmaf(r, y, y);
+  r = __builtin_fmaf(-x, q, 1.0f);
+  return __builtin_fmaf(r, y, q);
 }
 
 // q + dq with the box crossing carried into the image counter: the high

@@ -1604,10 +1604,16 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     return fail(SWARM_EINVAL, "n_species out of range");
   for (int a = 0; a < params->n_dims; ++a)
     if (!(params->box[a] > 0.0)) return fail(SWARM_EINVAL, "box lengths must be positive");
+  // the run kernels' 1/r^2 (rcp_rn) is exact for r^2 in [2^-96, 2^96]: a
+  // fixed-point grid step of at least 2^-48 and radii below 2^40
+  for (int a = 0; a < params->n_dims; ++a)
+    if (!(params->box[a] >= 0x1p-16)) return fail(SWARM_EINVAL, "box lengths must be >= 2^-16");
   if (!(params->time_step > 0.0)) return fail(SWARM_EINVAL, "time_step must be positive");
-  for (int s = 0; s < params->n_species; ++s)
+  for (int s = 0; s < params->n_species; ++s) {
     if (!(params->gamma_t[s] > 0.0) || !(params->gamma_r[s] > 0.0) || !(params->radius[s] >= 0.0))
       return fail(SWARM_EINVAL, "friction coefficients must be positive");
+    if (!(params->radius[s] < 0x1p40)) return fail(SWARM_EINVAL, "radius must be < 2^40");
+  }
   if (n_particles > (1 << 20))
     return fail(SWARM_ECAPACITY, "more than 2^20 particles per env are not supported");
   for (int i = 0; i < n_particles; ++i)

@@ -401,7 +401,7 @@ __device__ __forceinline__ void pair_fix_sel(float cut2, float sig6, float eps24
                                              float ry, int64_t& fx, int64_t& fy) {
   const float r2 = rx * rx + ry * ry;
   const bool in = r2 < cut2 && r2 > 0.0f;
-  const float ir2 = 1.0f / (in ? r2 : 1.0f);
+  const float ir2 = rcp_rn(in ? r2 : 1.0f);  // = 1.0f / r2 (in range: r2 >= 2^-96)
   float ir6 = ir2 * ir2;
   ir6 = ir6 * ir2;
   const float s6 = sig6 * ir6;
@@ -412,7 +412,7 @@ __device__ __forceinline__ void pair_fix_sel(float cut2, float sig6, float eps24
   fr = fr * ir2;
   const float vx = (in ? -fr * rx : 0.0f) * 16777216.0f;
   const float vy = (in ? -fr * ry : 0.0f) * 16777216.0f;
-  if (__builtin_expect(__all(fabsf(vx) < 2147483520.0f && fabsf(vy) < 2147483520.0f), 1)) {
+  if (__builtin_expect(wave_all(fabsf(vx) < 2147483520.0f && fabsf(vy) < 2147483520.0f), 1)) {
     fx = (int64_t)__float2int_rn(vx);
     fy = (int64_t)__float2int_rn(vy);
   } else {
@@ -582,8 +582,10 @@ __device__ __forceinline__ void bd_translate(const PConst& c, PState& p, int64_t
                                              uint32_t k0, uint32_t k1, uint32_t id, uint64_t step,
                                              bool last, float* vx, float* vy, float* w,
                                              const float* g, float sn, float cs) {
-  float fx = i64_to_f32(ax) * 5.9604644775390625e-08f;
-  float fy = i64_to_f32(ay) * 5.9604644775390625e-08f;
+  float fx, fy;
+  i64x2_to_f32(ax, ay, &fx, &fy);
+  fx = fx * 5.9604644775390625e-08f;
+  fy = fy * 5.9604644775390625e-08f;
   fx = fx + fex;
   fy = fy + fey;
   fx = fx + fs * cs;

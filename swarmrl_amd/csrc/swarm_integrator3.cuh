@@ -472,7 +472,7 @@ __device__ __forceinline__ void pair_fix_sel3(float cut2, float sig6, float eps2
   float r2 = rx * rx + ry * ry;
   r2 = r2 + rz * rz;
   const bool in = r2 < cut2 && r2 > 0.0f;
-  const float ir2 = 1.0f / (in ? r2 : 1.0f);
+  const float ir2 = rcp_rn(in ? r2 : 1.0f);  // = 1.0f / r2 (in range: r2 >= 2^-96)
   float ir6 = ir2 * ir2;
   ir6 = ir6 * ir2;
   const float s6 = sig6 * ir6;
@@ -484,7 +484,7 @@ __device__ __forceinline__ void pair_fix_sel3(float cut2, float sig6, float eps2
   const float vx = (in ? -fr * rx : 0.0f) * 16777216.0f;
   const float vy = (in ? -fr * ry : 0.0f) * 16777216.0f;
   const float vz = (in ? -fr * rz : 0.0f) * 16777216.0f;
-  if (__builtin_expect(__all(fabsf(vx) < 2147483520.0f && fabsf(vy) < 2147483520.0f &&
+  if (__builtin_expect(wave_all(fabsf(vx) < 2147483520.0f && fabsf(vy) < 2147483520.0f &&
                              fabsf(vz) < 2147483520.0f),
                        1)) {
     fx = (int64_t)__float2int_rn(vx);

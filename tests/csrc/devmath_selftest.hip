@@ -55,3 +55,59 @@ extern "C" int devmath_selftest(const float* x, const uint32_t* a, int n, float*
   (void)hipFree(dout);
   return 0;
 }
+
+// rcp_rn (the run kernels' 1/r^2) against the compiler's IEEE division
+// 1.0f / x for every float bit pattern in [lo, hi): mismatch count and the
+// first mismatching pattern (0 if none).
+__global__ void k_rcp_check(uint32_t lo, uint32_t hi, unsigned long long* bad, uint32_t* first) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  unsigned long long nb = 0;
+  for (uint32_t b = lo + blockIdx.x * blockDim.x + threadIdx.x; b < hi && b >= lo; b += stride) {
+    const float x = __uint_as_float(b);
+    if (__float_as_uint(swarm::rcp_rn(x)) != __float_as_uint(1.0f / x)) {
+      ++nb;
+      atomicCAS(first, 0u, b);
+    }
+  }
+  if (nb) atomicAdd(bad, nb);
+}
+
+// i64 -> fp32 conversions (fast int32 path and the wide path) on given values
+__global__ void k_i64(const int64_t* v, int n, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float a, b;
+  swarm::i64x2_to_f32(v[i], v[(i + 1) % n], &a, &b);
+  out[3 * i] = a;
+  out[3 * i + 1] = b;
+  out[3 * i + 2] = swarm::i64_to_f32(v[i]);
+}
+
+extern "C" int devmath_rcp_check(uint32_t lo, uint32_t hi, unsigned long long* bad,
+                                 uint32_t* first) {
+  unsigned long long* d;
+  if (hipMalloc(&d, 16)) return 1;
+  (void)hipMemset(d, 0, 16);
+  hipLaunchKernelGGL(k_rcp_check, dim3(4096), dim3(256), 0, 0, lo, hi, d,
+                     reinterpret_cast<uint32_t*>(d + 1));
+  if (hipDeviceSynchronize() != hipSuccess) return 2;
+  unsigned long long h[2];
+  (void)hipMemcpy(h, d, 16, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  *bad = h[0];
+  *first = (uint32_t)h[1];
+  return 0;
+}
+
+extern "C" int devmath_i64_to_f32(const int64_t* v, int n, float* out) {
+  int64_t* dv;
+  float* dout;
+  if (hipMalloc(&dv, n * 8) || hipMalloc(&dout, n * 12)) return 1;
+  (void)hipMemcpy(dv, v, n * 8, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(k_i64, dim3((n + 255) / 256), dim3(256), 0, 0, dv, n, dout);
+  if (hipDeviceSynchronize() != hipSuccess) return 2;
+  (void)hipMemcpy(out, dout, n * 12, hipMemcpyDeviceToHost);
+  (void)hipFree(dv);
+  (void)hipFree(dout);
+  return 0;
+}

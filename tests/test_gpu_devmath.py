@@ -67,3 +67,49 @@ def test_device_math_bit_exact(oracle_mod):
             ref = oracle_mod.step_normals(42, 5, i % 64, t0 + s_)
             assert np.array_equal(steps[i, 3 * s_:3 * s_ + 3], ref), (i, s_)
         assert np.array_equal(steps[i, 27:30], oracle_mod.step_normals(42, 5, i % 64, t0 + 8))
+
+
+def _lib():
+    import torch  # noqa: F401  (HIP runtime first)
+
+    lib_path = ROOT / "tests" / "csrc" / "libdevmath.so"
+    if not lib_path.exists():
+        import __graft_entry__ as g
+
+        g.build()
+    return ctypes.CDLL(str(lib_path))
+
+
+def test_rcp_rn_exhaustive():
+    """rcp_rn (the run kernels' 1/r^2, swarm_device.cuh) equals the IEEE
+    division 1.0f / x for EVERY float in [2^-96, 2^96] -- the range the
+    engine admits for in-range squared pair distances (box >= 2^-16, radii
+    < 2^40; swarm_engine_create rejects the rest)."""
+    lib = _lib()
+    bad = ctypes.c_ulonglong(0)
+    first = ctypes.c_uint32(0)
+    lo, hi = 31 << 23, 223 << 23  # 2^-96 .. 2^96
+    rc = lib.devmath_rcp_check(ctypes.c_uint32(lo), ctypes.c_uint32(hi), ctypes.byref(bad),
+                               ctypes.byref(first))
+    assert rc == 0
+    assert bad.value == 0, (bad.value, hex(first.value))
+
+
+def test_i64_to_f32_paths():
+    """The int32 fast path and the fp64 wide path of the force-sum
+    conversion both round to nearest (numpy's int64 -> float32 cast)."""
+    lib = _lib()
+    rng = np.random.default_rng(3)
+    n = 1 << 16
+    small = rng.integers(-2**31, 2**31, n // 2, dtype=np.int64)
+    wide = rng.integers(-2**62, 2**62, n // 2, dtype=np.int64) >> rng.integers(0, 40, n // 2)
+    for v in (small, np.concatenate([small, wide])):
+        v = np.ascontiguousarray(v)
+        out = np.zeros(3 * len(v), np.float32)
+        rc = lib.devmath_i64_to_f32(v.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(len(v)),
+                                    out.ctypes.data_as(ctypes.c_void_p))
+        assert rc == 0
+        ref = v.astype(np.float32)
+        assert np.array_equal(out[0::3], ref)
+        assert np.array_equal(out[1::3], np.roll(ref, -1))
+        assert np.array_equal(out[2::3], ref)
