@@ -309,6 +309,13 @@ __device__ __forceinline__ bool wave_all(bool p) {
   return __builtin_amdgcn_ballot_w64(p) == __builtin_amdgcn_read_exec();
 }
 
+// both predicates on every active lane: two compares straight into SGPR
+// masks and one scalar AND
+__device__ __forceinline__ bool wave_all2(bool p, bool q) {
+  return (__builtin_amdgcn_ballot_w64(p) & __builtin_amdgcn_ballot_w64(q)) ==
+         __builtin_amdgcn_read_exec();
+}
+
 __device__ __forceinline__ bool fits_i32(int64_t a) {
   return (int32_t)(a >> 32) == ((int32_t)a >> 31);
 }
@@ -324,7 +331,7 @@ __device__ __forceinline__ float i64_to_f32(int64_t a) {
 
 // both components behind one wave-uniform test
 __device__ __forceinline__ void i64x2_to_f32(int64_t ax, int64_t ay, float* fx, float* fy) {
-  if (__builtin_expect(wave_all(fits_i32(ax) && fits_i32(ay)), 1)) {
+  if (__builtin_expect(wave_all2(fits_i32(ax), fits_i32(ay)), 1)) {
     *fx = (float)(int32_t)ax;
     *fy = (float)(int32_t)ay;
   } else {

@@ -412,7 +412,7 @@ __device__ __forceinline__ void pair_fix_sel(float cut2, float sig6, float eps24
   fr = fr * ir2;
   const float vx = (in ? -fr * rx : 0.0f) * 16777216.0f;
   const float vy = (in ? -fr * ry : 0.0f) * 16777216.0f;
-  if (__builtin_expect(wave_all(fabsf(vx) < 2147483520.0f && fabsf(vy) < 2147483520.0f), 1)) {
+  if (__builtin_expect(wave_all2(fabsf(vx) < 2147483520.0f, fabsf(vy) < 2147483520.0f), 1)) {
     fx = (int64_t)__float2int_rn(vx);
     fy = (int64_t)__float2int_rn(vy);
   } else {
@@ -2275,8 +2275,9 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
           }
           atomicAdd(&lacc_x[a], (unsigned long long)fx);
           atomicAdd(&lacc_y[a], (unsigned long long)fy);
-          atomicAdd(&lacc_x[b], (unsigned long long)(-fx));
-          atomicAdd(&lacc_y[b], (unsigned long long)(-fy));
+          // b: the exact negation, as an LDS subtract (no negated copy)
+          atomicSub(&lacc_x[b], (unsigned long long)fx);
+          atomicSub(&lacc_y[b], (unsigned long long)fy);
         }
       }
     }

@@ -606,9 +606,9 @@ __device__ __forceinline__ void run_wave3(const Derived* __restrict__ d, const D
         atomicAdd(&lacc_x[a], (unsigned long long)fx);
         atomicAdd(&lacc_y[a], (unsigned long long)fy);
         atomicAdd(&lacc_z[a], (unsigned long long)fz);
-        atomicAdd(&lacc_x[b], (unsigned long long)(-fx));
-        atomicAdd(&lacc_y[b], (unsigned long long)(-fy));
-        atomicAdd(&lacc_z[b], (unsigned long long)(-fz));
+        atomicSub(&lacc_x[b], (unsigned long long)fx);
+        atomicSub(&lacc_y[b], (unsigned long long)fy);
+        atomicSub(&lacc_z[b], (unsigned long long)fz);
       }
     }
     // the director's turn (independent of the forces) while the sums land
