@@ -2275,7 +2275,8 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
           }
           atomicAdd(&lacc_x[a], (unsigned long long)fx);
           atomicAdd(&lacc_y[a], (unsigned long long)fy);
-          // b: the exact negation, as an LDS subtract (no negated copy)
+          // b: the exact negation (written as a subtract; the compiler still
+          // emits ds_add_u64 of the negated value)
           atomicSub(&lacc_x[b], (unsigned long long)fx);
           atomicSub(&lacc_y[b], (unsigned long long)fy);
         }
