@@ -414,12 +414,17 @@ def test_vision_cone_parity_lane_variants_and_dense(E, n, box_len, env, monkeypa
         assert np.count_nonzero(ref) > len(agents)
 
 
-def test_big_clusters_run_in_check_bit_exact():
+@pytest.mark.parametrize("wide", ["1", "0"])
+def test_big_clusters_run_in_check_bit_exact(wide, monkeypatch):
     """Clusters wider than a wave (three 10 x 10 patches at 2.5 um spacing:
     100 colloids each, within r_c + skin of their neighbours) run in k_check's
-    workgroup instead of sending the env to the global path: bit-exact
-    against the oracle over several windows, without a global-path re-run."""
+    workgroup instead of sending the env to the global path, after either run
+    kernel (wide = "1": k_cluster_run_wide, "0": the throughput
+    k_cluster_run): bit-exact against the oracle over several windows,
+    without a global-path re-run."""
     from gpu_harness import Harness, species_list
+
+    monkeypatch.setenv("SWARMRL_AMD_WIDE_RUN", wide)
 
     rng = np.random.default_rng(21)
     box = [200.0, 200.0, 200.0]
