@@ -2349,14 +2349,19 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
         fs = st.f_swim[gi];
         tz = st.torque_z[gi];
       }
-      // two sub-steps per iteration: the next normals load into alternating
-      // registers (no copies) and the scheduler sees across the boundary
-      // (E=1 run 53.9 -> 53.4 us, E=64 250 -> 247 us)
-      for (s = 1; s + 1 < n_steps - 1; s += 2) {
-        substep(s, std::false_type{}, pass_t);
-        substep(s + 1, std::false_type{}, pass_t);
+      if constexpr (kTable) {
+        // two sub-steps per iteration: the next normals load into alternating
+        // registers (no copies) and the scheduler sees across the boundary
+        // (E=1 run 53.9 -> 53.4 us).  Not in the in-kernel-noise variant: at
+        // its 96-VGPR bound the unrolled loop spills 80 B/lane, not 24.
+        for (s = 1; s + 1 < n_steps - 1; s += 2) {
+          substep(s, std::false_type{}, pass_t);
+          substep(s + 1, std::false_type{}, pass_t);
+        }
+        if (s < n_steps - 1) substep(s++, std::false_type{}, pass_t);
+      } else {
+        for (s = 1; s < n_steps - 1; ++s) substep(s, std::false_type{}, pass_t);
       }
-      if (s < n_steps - 1) substep(s++, std::false_type{}, pass_t);
     }
     substep(s, std::true_type{}, pass_t);  // velocities of the last sub-step
   };
