@@ -16,5 +16,5 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
   rc=$?; [ $rc -eq 0 ] || { tail "$out/bench_default.err"; exit $rc; }
   python3 -c "import json;d=json.load(open('$out/bench_default.json'));print('head',d['value']/1e6,{k:v['value']/1e6 for k,v in d.items() if isinstance(v,dict) and 'value' in v and v.get('unit')=='agent-steps/s'})"
 fi
-[ -n "${LINES:-}" ] && bash profiles/profile_round.sh r3c
+[ -n "${LINES:-}" ] && bash profiles/profile_round.sh "${TAG:-r3c}"
 exit 0
