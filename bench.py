@@ -624,7 +624,8 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
     import torch
     import torch.distributed as dist
 
-    from swarmrl_amd.rollout import gather_trajectory
+    from swarmrl_amd.rollout import (broadcast_agent, gather_episode, gather_trajectory,
+                                     replicated_update)
 
     args_e = argparse.Namespace(**vars(args))
     args_e.envs_per_gpu = E
@@ -637,6 +638,8 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
     # env g is placed with default_rng(42 + g) (swarm_engine.add_colloids)
     envs = shard_envs(world * E, rank, world)
     eng, ff, agent = (builder or build_workload)(args_e, 42 + envs[0], device)
+    if train and world > 1:
+        broadcast_agent(agent)  # rank 0's replica everywhere (EpisodeParallelTrainer)
     eng.integrate(1, ff)  # setup, overlap removal, first slice (eager)
 
     def one_slice():
@@ -668,8 +671,30 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
         agent.reset_trajectory()
 
     gstats = []
+    n_updates = [0]
 
-    traj = agent.trajectory  # the episode graph's output tensors
+    def episode_end(timed):
+        """After an episode: the update (train) and the trajectory gather.
+        At world > 1 every rank all-gathers the episode's trajectory (one
+        packed collective) and, when training, runs the identical update on
+        the gathered [T, world E, ...] episode (rollout.replicated_update,
+        SURVEY 8(e)); at world 1 the update runs on the local episode."""
+        traj = agent.trajectory  # in graph mode: the episode graph's output tensors
+        st = {} if (timed and world > 1 and len(gstats) < 4) else None
+        if train:
+            n_updates[0] += 1
+            if world > 1:
+                episode = gather_episode(traj, stats=st)
+                replicated_update(agent, episode, seed=1000 + n_updates[0])
+            else:
+                agent.loss.compute_loss(network=agent.network, episode_data=traj)
+        elif timed and world > 1:
+            gather_trajectory(traj, stats=st)
+        if st:
+            gstats.append(st)
+        # trajectory entries the device has published so far (the ring is
+        # filled by the replayed graph; no host wait)
+        eng.drain_trajectory(block=False)
 
     def run(n_steps, timed):
         k = 0
@@ -677,26 +702,22 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
             if episode_graph is not None and n_steps - k >= T:
                 episode_graph.replay()
                 k += T
-                if train:  # the update of the episode the graph recorded
-                    agent.loss.compute_loss(network=agent.network, episode_data=traj)
-                # trajectory entries the device has published so far (the
-                # ring is filled by the replayed graph; no host wait)
-                eng.drain_trajectory(block=False)
-                if timed and world > 1:
-                    st = {}
-                    gather_trajectory(agent.trajectory, stats=st if len(gstats) < 4 else None)
-                    if st:
-                        gstats.append(st)
+                episode_end(timed)
             elif slice_graph is not None:
                 slice_graph.replay()
                 k += 1
             else:
                 one_slice()
                 k += 1
-                if timed and world > 1 and len(agent.trajectory.actions) >= T:
-                    gather_trajectory(agent.trajectory)
+                if len(agent.trajectory.actions) >= T:
+                    episode_end(timed)
                     agent.reset_trajectory()
 
+    if episode_graph is not None:
+        # the first launch of a captured graph uploads it: one untimed
+        # episode replay (and its update) before the W warmup steps, so the
+        # timed region never holds a graph's first launch
+        run(T, False)
     run(args.warmup, False)
     torch.cuda.synchronize()
     if world > 1:
@@ -732,7 +753,9 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
     if valu:
         valu["lane_insts_per_colloid_substep"] = valu["insts_per_launch"] * 64 / (N * sub * E)
     if train:
-        out["roofline_update"] = time_ppo_grads(agent, traj, line, args.bd_reps)
+        traj = agent.trajectory  # the episode graph's tensors (eager: the last episode's)
+        if len(traj.actions) > 0:
+            out["roofline_update"] = time_ppo_grads(agent, traj, line, args.bd_reps)
     del eng, ff, agent, slice_graph, episode_graph
     torch.cuda.synchronize()
     return out

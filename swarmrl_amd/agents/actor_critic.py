@@ -64,12 +64,23 @@ class ActorCriticAgent(Agent):
         return bool(ok) and hasattr(self.network, "compute_action")
 
     # ----------------------------------------------------------- training
-    def update_agent(self) -> tuple:
-        rewards = self.trajectory.rewards
-        killed = self.trajectory.killed
-        self.loss.compute_loss(network=self.network, episode_data=self.trajectory)
-        if self.intrinsic_reward:
-            self.intrinsic_reward.update(self.trajectory)
+    def update_agent(self, episode_data=None, update_fn=None) -> tuple:
+        """Train on the episode and start a new trajectory (actor_critic.py:
+        80-109).  episode_data: the episode to learn from, by default this
+        agent's own trajectory -- the episode-parallel trainer passes the
+        trajectory all-gathered over the ranks (rollout.gather_episode), and
+        update_fn(agent, episode) replaces the loss + intrinsic-reward step
+        (rollout.replicated_update).  Returns the rewards and the kill switch
+        of that episode."""
+        episode = self.trajectory if episode_data is None else episode_data
+        rewards = episode.rewards
+        killed = episode.killed
+        if update_fn is not None:
+            update_fn(self, episode)
+        else:
+            self.loss.compute_loss(network=self.network, episode_data=episode)
+            if self.intrinsic_reward:
+                self.intrinsic_reward.update(episode)
         self.reset_trajectory()
         return rewards, killed
 

@@ -1361,7 +1361,7 @@ int launch_run(swarm_engine* e, int n_steps) {
 // candidates from its cells (-1: every colloid).
 size_t sort_lds_bytes(const swarm_engine* e) {
   const size_t ncb = (size_t)1 << (e->lxb + e->lyb + e->lzb);
-  return (16 + ncb + 1 + 3 * (size_t)e->sc.sort_stage_k) * 4;
+  return (16 + ((ncb + 4) & ~(size_t)3) + 3 * (size_t)e->sc.sort_stage_k) * 4;
 }
 
 int check_cell_lx(const swarm_engine* e) { return e->env_build ? -1 : e->lxb; }
@@ -1515,6 +1515,9 @@ int run_bd(swarm_engine* e, int n_steps) {
 int ensure_grid_scratch(swarm_engine* e, int lx, int ly) {
   const size_t need = (size_t)e->n_envs * ((size_t)(1 << (lx + ly)) + 1);
   if (need > e->start_cap) {
+    // the speculative vision grid's saved arguments point into the old buffer
+    e->vgrid_ready = false;
+    e->spec_ok = false;
     if (e->d_start) HIP_TRY(hipFree(e->d_start));
     HIP_TRY(hipMalloc(&e->d_start, need * sizeof(int32_t)));
     e->start_cap = need;
@@ -1525,6 +1528,8 @@ int ensure_grid_scratch(swarm_engine* e, int lx, int ly) {
 int build_grid(swarm_engine* e, int lx, int ly) {
   int rc = ensure_grid_scratch(e, lx, ly);
   if (rc) return rc;
+  // this grid overwrites the cell starts a speculative vision grid left
+  e->vgrid_ready = false;
   const int ncell = 1 << (lx + ly);
   const size_t lds = 16 * 4 + (size_t)(ncell + 1) * 4;
   if (lds > kMaxLds) return fail(SWARM_ECAPACITY, "observable cell grid too large");
@@ -2681,7 +2686,9 @@ int policy_launch(const float* obs, int32_t n, int32_t d_in, const float* w1, co
   const swarm::MlpArgs m{obs,   n,          d_in,    w1,      b1,       hidden, w2,
                          b2,    k,          k0,      k1,      st,       explore_p, f_table,
                          t_table, out_idx,  out_logp, out_f,  out_t,    out_logits};
-  if (ride && ride->ride_stage == 3 && G == 4 && small_in && small_k) {
+  // the build stage may only ride along on the engine's stream: stages 1-2
+  // and the run that consumes the build are ordered on it
+  if (ride && s == ride->stream && ride->ride_stage == 3 && G == 4 && small_in && small_k) {
     // policy blocks of 1024 threads (256 agents: whole counter groups) and
     // one cluster-build workgroup per env
     const int pblocks = (int)(((long)n * G + 1023) / 1024);

@@ -1091,7 +1091,9 @@ __device__ __forceinline__ void build_sort_body(const DevState& st, const Scratc
 #pragma unroll
     for (int k = 0; k < CH; ++k)
       spos[k] = cid[k] >= 0 ? atomicAdd(&cnt[cell_of(tid + k * T, cqx[k], cqy[k])], 1) : -1;
-    uint32_t* lx_ = reinterpret_cast<uint32_t*>(cnt + ncell + 1);
+    // rows start 16-byte aligned (read as uint4 below): the counts round up
+    // to a multiple of four words (sort_lds_bytes)
+    uint32_t* lx_ = reinterpret_cast<uint32_t*>(cnt + ((ncell + 4) & ~3));
     uint32_t* ly_ = lx_ + K;
     int32_t* lid = reinterpret_cast<int32_t*>(ly_ + K);
     const bool vec = (N & 3) == 0 && (M & 3) == 0 && (K & 3) == 0;

@@ -800,8 +800,12 @@ class SwarmEngine(Engine):
             self._native.call("swarm_traj_entry_to_host", ctypes.c_void_p(addr), pos.ctypes.data,
                               dirs.ctypes.data, vel.ctypes.data, step.ctypes.data)
             if not block and int(ring["count"][0]) >= k + cap:  # overwritten while being read
+                # entries start..k-1 are in traj_holder already: a caller that
+                # catches this and drains again must not append them twice
+                ring["drained"] = k
                 raise RuntimeError("trajectory ring overflow while draining (drain more often)")
             self._append_traj(self._time_offset + int(step[0]) * self._time_step, pos, vel, dirs)
+            ring["drained"] = k + 1
             if len(self.traj_holder["Times"]) >= self.write_chunk_size:
                 self._write_traj_chunk_to_file()
                 for val in self.traj_holder.values():

@@ -1,29 +1,39 @@
 """
 Episode-parallel rollout plumbing: the exchange of trajectory buffers
-between ranks at the end of an episode.
+between ranks at the end of an episode, and the replicated update built on it.
 
 The reference runs independent trainings as separate Dask worker processes
 and never exchanges trajectories (swarmrl/training_routines/
 ensemble_submit.py:76-138).  Here every rank (one process per GPU) runs its
 own envs with no communication during the rollout; at the end of an episode
-the per-rank trajectory buffers are concatenated on every rank so each rank
-can run the identical PPO update.
+the per-rank trajectory buffers are concatenated on every rank, and every
+rank runs the identical update on the gathered episode:
+the replicas start from rank 0's parameters (``broadcast_agent``) and each
+update is a deterministic function of the gathered data, so they stay
+bit-identical with no gradient all-reduce or parameter broadcast per episode
+(``replicated_update``; tests/test_distributed.py checks the parameters of
+two gloo ranks after two updates).
 
-The four buffers (features, actions, log-probs, rewards) are packed into ONE
-flat byte buffer and exchanged with ONE all_gather_into_tensor (RCCL over
-xGMI for backend "nccl", gloo on CPU): a ring all-gather is bound per xGMI
-link, so one large collective per episode beats four small ones.
+The four buffers (features, actions, log-probs, rewards) plus the kill flag
+are packed into ONE flat byte buffer and exchanged with ONE
+all_gather_into_tensor (RCCL over xGMI for backend "nccl", gloo on CPU): a
+ring all-gather is bound per xGMI link, so one large collective per episode
+beats five small ones.
 """
 
 from __future__ import annotations
 
 import time
-from typing import Dict, Optional
+from typing import Dict, Optional, Sequence
 
 import torch
 import torch.distributed as dist
 
+from swarmrl_amd.utils.colloid_utils import TrajectoryInformation
+
 _NAMES = ("features", "actions", "log_probs", "rewards")
+# per-rank env counts established by _env_counts, keyed by (group, local shapes)
+_COUNTS: Dict[tuple, list] = {}
 
 
 def shard_envs(total_envs: int, rank: int, world: int):
@@ -31,9 +41,10 @@ def shard_envs(total_envs: int, rank: int, world: int):
     envs [r E, (r + 1) E) with E = total / G (the first total mod G ranks one
     more).  Contiguous blocks, not SURVEY 8(e)'s e mod G: the all-gather
     below concatenates the ranks' [T, E, ...] buffers rank-major, so the
-    gathered env axis is then the global env id.  bench.py creates each
-    rank's engine with seed 42 + its first env id, so env g is placed with
-    default_rng(42 + g) whatever the world size."""
+    gathered env axis is then the global env id (gather_trajectory pads
+    uneven blocks).  bench.py creates each rank's engine with seed 42 + its
+    first env id, so env g is placed with default_rng(42 + g) whatever the
+    world size."""
     if world < 1 or not 0 <= rank < world:
         raise ValueError(f"rank {rank} outside a world of {world}")
     per, extra = divmod(total_envs, world)
@@ -41,21 +52,66 @@ def shard_envs(total_envs: int, rank: int, world: int):
     return list(range(lo, lo + per + (1 if rank < extra else 0)))
 
 
+def _is_distributed(group=None) -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+
+
+def _as_tensor(x, device) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        return x.to(device)
+    return torch.as_tensor(x, device=device)
+
+
 def _stacked(trajectory) -> Dict[str, torch.Tensor]:
-    return {
-        "features": torch.stack(list(trajectory.features)),
-        "actions": torch.stack(list(trajectory.actions)),
-        "log_probs": torch.stack(list(trajectory.log_probs)),
-        "rewards": torch.stack(list(trajectory.rewards)),
-    }
+    dev = None
+    for x in trajectory.features:
+        if isinstance(x, torch.Tensor):
+            dev = x.device
+            break
+    dev = dev or torch.device("cpu")
+    return {k: torch.stack([_as_tensor(x, dev) for x in getattr(trajectory, k)])
+            for k in _NAMES}
 
 
-def gather_trajectory(trajectory, group=None, stats: Optional[dict] = None
-                      ) -> Dict[str, torch.Tensor]:
+def _killed_flag(killed, device) -> torch.Tensor:
+    """The kill switch as one uint8 on `device` (no host sync for a tensor)."""
+    if isinstance(killed, torch.Tensor):
+        return killed.reshape(-1).any().to(device=device, dtype=torch.uint8).reshape(1)
+    return torch.tensor([1 if killed else 0], dtype=torch.uint8, device=device)
+
+
+def _env_counts(bufs, group, env_counts: Optional[Sequence[int]]) -> list:
+    """Env count of every rank.  Given by the caller (shard_envs), or
+    exchanged once per (group, local buffer shapes) with a small all-gather
+    and cached: the shapes of an engine's trajectory do not change between
+    episodes, so the per-episode collective stays the single packed one."""
+    world = dist.get_world_size(group)
+    if env_counts is not None:
+        if len(env_counts) != world:
+            raise ValueError(f"env_counts has {len(env_counts)} entries for a world of {world}")
+        return [int(c) for c in env_counts]
+    key = (id(group),) + tuple(tuple(b.shape) for b in bufs.values())
+    if key not in _COUNTS:
+        dev = bufs["actions"].device
+        mine = torch.tensor([bufs["actions"].shape[1]], dtype=torch.int64, device=dev)
+        allc = torch.zeros(world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(allc, mine, group=group)
+        _COUNTS[key] = [int(c) for c in allc.cpu()]
+    return _COUNTS[key]
+
+
+def gather_trajectory(trajectory, group=None, stats: Optional[dict] = None,
+                      env_counts: Optional[Sequence[int]] = None) -> Dict[str, torch.Tensor]:
     """
     Stack an agent's device trajectory (lists of [E, A, ...] tensors, one entry
     per slice) into [T, E, ...] tensors and all-gather them along the env axis
-    -> [T, world * E, ...] on every rank (rank-major env order).
+    -> [T, sum(E), ...] on every rank (rank-major env order), plus "killed":
+    whether any rank's task raised the kill switch (a bool on the host when
+    not distributed, else a uint8 device tensor).
+
+    Ranks may hold different env counts (shard_envs of a total that the
+    world does not divide): each rank's block is padded to the largest count
+    for the collective and the padding dropped after it.
 
     stats (optional dict): receives "bytes" (this rank's packed buffer) and
     the collective's duration: "ms" on the host (CPU tensors) or "events"
@@ -63,13 +119,28 @@ def gather_trajectory(trajectory, group=None, stats: Optional[dict] = None
     gather_ms after synchronising).
     """
     bufs = _stacked(trajectory)
-    if not (dist.is_available() and dist.is_initialized()):
+    if not _is_distributed(group):
+        bufs["killed"] = trajectory.killed
         return bufs
     world = dist.get_world_size(group)
-    parts = [bufs[k].contiguous().reshape(-1).view(torch.uint8) for k in _NAMES]
+    counts = _env_counts(bufs, group, env_counts)
+    if counts[dist.get_rank(group)] != bufs["actions"].shape[1]:
+        raise ValueError("env_counts does not match this rank's trajectory")
+    emax = max(counts)
+    dev = bufs["actions"].device
+    padded = {}
+    for k in _NAMES:
+        b = bufs[k]
+        if b.shape[1] < emax:
+            pad = torch.zeros((b.shape[0], emax - b.shape[1]) + tuple(b.shape[2:]), dtype=b.dtype,
+                              device=dev)
+            b = torch.cat([b, pad], 1)
+        padded[k] = b
+    parts = [padded[k].contiguous().reshape(-1).view(torch.uint8) for k in _NAMES]
+    parts.append(_killed_flag(trajectory.killed, dev))
     sizes = [p.numel() for p in parts]
     packed = torch.cat(parts)
-    out = torch.empty(world * packed.numel(), dtype=torch.uint8, device=packed.device)
+    out = torch.empty(world * packed.numel(), dtype=torch.uint8, device=dev)
     if stats is None:
         dist.all_gather_into_tensor(out, packed, group=group)
     elif packed.is_cuda:
@@ -91,13 +162,33 @@ def gather_trajectory(trajectory, group=None, stats: Optional[dict] = None
     result = {}
     off = 0
     for name, sz in zip(_NAMES, sizes):
-        src = bufs[name]
+        src = padded[name]
         chunk = per_rank[:, off:off + sz].contiguous().view(src.dtype)
-        chunk = chunk.view(world, *src.shape)  # [world, T, E, ...]
-        result[name] = chunk.transpose(0, 1).reshape(src.shape[0], world * src.shape[1],
-                                                     *src.shape[2:])
+        chunk = chunk.view(world, *src.shape)  # [world, T, Emax, ...]
+        if all(c == emax for c in counts):
+            result[name] = chunk.transpose(0, 1).reshape(src.shape[0], world * emax,
+                                                         *src.shape[2:])
+        else:
+            result[name] = torch.cat([chunk[r, :, :counts[r]] for r in range(world)], 1)
         off += sz
+    result["killed"] = per_rank[:, off].amax()
     return result
+
+
+def gather_episode(trajectory, group=None, stats: Optional[dict] = None,
+                   env_counts: Optional[Sequence[int]] = None) -> TrajectoryInformation:
+    """The episode of every rank as one TrajectoryInformation: per slice one
+    [sum(E), A, ...] tensor (views into the gathered buffers), the kill
+    switch raised when any rank raised it."""
+    g = gather_trajectory(trajectory, group=group, stats=stats, env_counts=env_counts)
+    return TrajectoryInformation(
+        particle_type=trajectory.particle_type,
+        features=list(g["features"].unbind(0)),
+        actions=list(g["actions"].unbind(0)),
+        log_probs=list(g["log_probs"].unbind(0)),
+        rewards=list(g["rewards"].unbind(0)),
+        killed=g["killed"],
+    )
 
 
 def gather_ms(stats: dict) -> float:
@@ -106,3 +197,76 @@ def gather_ms(stats: dict) -> float:
         ev0, ev1 = stats["events"]
         return float(ev0.elapsed_time(ev1))
     return float(stats.get("ms", 0.0))
+
+
+# ------------------------------------------------------- replicated update
+def _agent_tensors(agent):
+    """Every tensor that determines an agent's future updates: the network's
+    parameters and buffers, its optimizer's state, and those of an intrinsic
+    reward (RND target / predictor and its optimizer), in a fixed order."""
+    out = []
+
+    def add_module(m):
+        out.extend(t for t in m.state_dict().values() if isinstance(t, torch.Tensor))
+
+    def add_optimizer(opt):
+        if opt is None:
+            return
+        for group in opt.param_groups:
+            for p in group["params"]:
+                for k in sorted(opt.state.get(p, {})):
+                    v = opt.state[p][k]
+                    if isinstance(v, torch.Tensor):
+                        out.append(v)
+
+    net = getattr(agent, "network", None)
+    if net is not None and getattr(net, "model", None) is not None:
+        add_module(net.model)
+        add_optimizer(getattr(net, "optimizer", None))
+    ir = getattr(agent, "intrinsic_reward", None)
+    if ir is not None:
+        for name in ("target_network", "predictor_network"):
+            if getattr(ir, name, None) is not None:
+                add_module(getattr(ir, name))
+        add_optimizer(getattr(ir, "optimizer", None))
+    return out
+
+
+@torch.no_grad()
+def broadcast_agent(agent, src: int = 0, group=None) -> None:
+    """Make every rank's replica of `agent` equal to rank `src`'s (group
+    rank): parameters, buffers and optimizer state, broadcast in place.  Run
+    once before the first episode (EpisodeParallelTrainer)."""
+    if not _is_distributed(group):
+        return
+    root = src if group is None else dist.get_global_rank(group, src)
+    for t in _agent_tensors(agent):
+        dist.broadcast(t, root, group=group)
+
+
+@torch.no_grad()
+def replica_digest(agent) -> torch.Tensor:
+    """The bytes of every tensor of _agent_tensors as one uint8 vector on the
+    host (tests: replicas are identical iff their digests are)."""
+    parts = [t.detach().reshape(-1).contiguous().cpu().view(torch.uint8)
+             for t in _agent_tensors(agent)]
+    return torch.cat(parts) if parts else torch.zeros(0, dtype=torch.uint8)
+
+
+def replicated_update(agent, episode: TrajectoryInformation, seed: int):
+    """One learning agent's update on a gathered episode, run identically
+    on every rank: the loss (ProximalPolicyLoss.compute_loss, deterministic:
+    the fused HIP gradient sums in a fixed order, tests/test_gpu_ppo.py) and
+    an intrinsic reward's predictor update, whose minibatch permutation
+    (random_network_distillation.py:105-120) draws from torch's generators,
+    here re-seeded with `seed` (the same on every rank) inside a forked RNG
+    state so the rollout's own streams are untouched."""
+    devices = []
+    for t in episode.features[:1]:
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            devices = [t.device.index]
+    agent.loss.compute_loss(network=agent.network, episode_data=episode)
+    if getattr(agent, "intrinsic_reward", None):
+        with torch.random.fork_rng(devices=devices):
+            torch.manual_seed(seed)
+            agent.intrinsic_reward.update(episode)

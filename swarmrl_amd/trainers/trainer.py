@@ -69,10 +69,15 @@ class Trainer:
         for agent in self.agents.values():
             if not isinstance(agent, ActorCriticAgent):
                 continue  # classical / scripted agents do not learn
-            rewards, killed = agent.update_agent()
+            rewards, killed = self._update_agent(agent)
             total += mean_reward(rewards)
             stop = stop or _is_killed(killed)
         return ForceFunction(agents=self.agents), np.array(total), stop
+
+    def _update_agent(self, agent):
+        """One learning agent's update after an episode (the episode-parallel
+        trainers gather the episode over the ranks first)."""
+        return agent.update_agent()
 
     def export_models(self, directory: str = "Models"):
         """Save every agent's network into `directory` (trainer.py:103-118)."""

@@ -33,8 +33,9 @@ def test_launcher_yields_n_ranks_gloo():
     assert line["n_gpus"] == 3 and line["world"] == 3
     assert len(line["per_rank_value"]) == 3
     assert line["value"] > 0
-    # 20-slice episodes of 128 agents: features 12 B + action 8 + logp 4 + reward 4
-    assert line["gather"]["bytes_per_rank"] == 20 * 128 * 28
+    # 20-slice episodes of 128 agents: features 12 B + action 8 + logp 4 + reward 4,
+    # plus the one-byte kill flag
+    assert line["gather"]["bytes_per_rank"] == 20 * 128 * 28 + 1
     assert line["gather"]["per_run"] == 2
 
 
