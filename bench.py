@@ -301,14 +301,18 @@ def measure_dims3(args, E, reps, global_reps=0, dims=3, fraction=0.04):
     return out
 
 
-def time_run_kernel(eng, reps):
-    """Duration (ms) of the dominant kernel, the 2-D run kernel of the
+def time_run_kernel(eng, ff, agent, episode_length, replays=3):
+    """Duration (ms) of the dominant kernel -- the 2-D run kernel of the
     latency- (k_cluster_run_wide) or throughput-bound (k_cluster_run) cluster
-    window: `reps` back-to-back launches on one freshly built window between
-    two HIP events on the engine's stream (swarm_engine_time_run), after the
-    timed region -- so the per-launch figure carries no per-launch event or
-    dispatch overhead, and profiles/ rows of the same launches (the last
-    `reps` dispatches of a config-pure rocprofv3 run) time the same work."""
+    window -- as it runs in the workload: after the timed region
+    one more episode of the workload is captured with engine recording on,
+    which puts HIP event-record nodes around each window's run node
+    (swarm_engine_profile -> hipEventRecordExternal), and that graph is
+    replayed `replays` times; every replay's run nodes are read back
+    (swarm_engine_profile_graph).  Returns (mean ms, kernel name, note,
+    number of run launches timed): the rocprofv3 trace of the same command
+    holds those launches as the kernel's last dispatches
+    (tools/summarize_profiles.py reads the count from the bench line)."""
     import ctypes
 
     import torch
@@ -319,22 +323,38 @@ def time_run_kernel(eng, reps):
             "filled beside them)" if wide else "k_cluster_run (100 fused BD+WCA sub-steps)")
     torch.cuda.synchronize()
     ms = ctypes.c_double()
+    cnt = ctypes.c_int32()
+    saved = agent.trajectory
+    agent.reset_trajectory()
+    nat.call("swarm_engine_profile", 1, ctypes.byref(ms), ctypes.byref(cnt))
     try:
-        nat.call("swarm_engine_time_run", int(eng.params.steps_per_slice), int(reps),
-                 ctypes.byref(ms))
-    except (RuntimeError, ValueError):
-        # no 2-D cluster windows (global path): whole windows, HIP events
-        start = torch.cuda.Event(enable_timing=True)
-        stop = torch.cuda.Event(enable_timing=True)
-        start.record()
-        for _ in range(reps):
-            eng._run(eng.params.steps_per_slice)
-        stop.record()
-        stop.synchronize()
-        return start.elapsed_time(stop) / reps, "k_global (100 sub-steps)", "whole windows"
-    torch.cuda.synchronize()
-    return ms.value, name, (f"HIP events around {reps} back-to-back launches on one window "
-                            f"(swarm_engine_time_run), after the timed region")
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            eng.integrate(episode_length, ff)
+    finally:
+        nat.call("swarm_engine_profile", 0, ctypes.byref(ms), ctypes.byref(cnt))
+    samples = []
+    buf = (ctypes.c_float * 4096)()
+    try:
+        for _ in range(replays):
+            graph.replay()
+            nat.call("swarm_engine_profile_graph", 0, buf, 4096, ctypes.byref(cnt))
+            samples.extend(buf[k] for k in range(min(cnt.value, 4096)))
+        eng.drain_trajectory(block=True)
+    finally:
+        del graph
+        torch.cuda.synchronize()
+        nat.call("swarm_engine_profile_graph", 1, None, 0, ctypes.byref(cnt))
+        agent.trajectory = saved
+    if not samples:  # no 2-D cluster windows (global path): nothing was recorded
+        return None, name, "no run-kernel launches recorded", 0
+    samples.sort()
+    mean = sum(samples) / len(samples)
+    note = (f"HIP event-record nodes around the run node of each window of an episode graph "
+            f"captured after the timed region, {replays} replays x {len(samples) // replays} "
+            f"windows = {len(samples)} launches; median {samples[len(samples) // 2]:.5f} ms, "
+            f"min {samples[0]:.5f}, max {samples[-1]:.5f}")
+    return mean, name, note, len(samples)
 
 
 def time_ppo_grads(agent, traj, line, reps):
@@ -432,7 +452,7 @@ def make_roofline(line, kernel_re, kernel, kernel_ms, units, bytes_per_unit, uni
     from its config-pure profile, and the VALU issue roofline from the
     profile's instruction counts."""
     bytes_per_launch = bytes_per_unit * units
-    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9 if kernel_ms else None
     row = profile_row(line, kernel_re)
     out = {
         "bound": "hbm",
@@ -440,7 +460,7 @@ def make_roofline(line, kernel_re, kernel, kernel_ms, units, bytes_per_unit, uni
         "achieved": achieved,
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
-        "frac": achieved / HBM_PEAK_GBS,
+        "frac": achieved / HBM_PEAK_GBS if achieved else None,
         "traffic": row["bytes_per_launch"] if row else None,
         "kernel_ms": kernel_ms,
         "bytes_per_launch": bytes_per_launch,
@@ -455,7 +475,7 @@ def make_roofline(line, kernel_re, kernel, kernel_ms, units, bytes_per_unit, uni
                           or None,
                           "launches": row.get("dispatches")}
         valu, trans = row.get("valu_insts_per_launch"), row.get("valu_trans_per_launch")
-        if valu:
+        if valu and kernel_ms:
             # issue cycles the launch needs on its SIMDs over the cycles the
             # chip offers in the measured duration
             cycles = VALU_CYCLES * (valu - (trans or 0.0)) + TRANS_CYCLES * (trans or 0.0)
@@ -615,6 +635,35 @@ def cpu_baseline_all_cores(args):
     }
 
 
+def capture_episode(eng, ff, agent, T):
+    """Two eager warm-up slices on a side stream, then the graphs the bench
+    replays: one per slice (for step counts that are not a multiple of T) and
+    one per episode, whose T slices write T distinct trajectory tensors, so
+    replaying it records a whole episode with no copies (agent.trajectory
+    holds references to those tensors).  Returns (slice graph, episode graph,
+    the trajectory of the eager slices so far)."""
+    import torch
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            eng.integrate(1, ff)
+    torch.cuda.current_stream().wait_stream(side)
+    warm = agent.trajectory
+    agent.reset_trajectory()
+    slice_graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(slice_graph):
+        eng.integrate(1, ff)
+    agent.reset_trajectory()
+    episode_graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(episode_graph, pool=slice_graph.pool()):
+        # one episode as the trainers run it (episodic_trainer.py:35 ->
+        # engine.integrate(episode_length, force_fn))
+        eng.integrate(T, ff)
+    return slice_graph, episode_graph, warm
+
+
 def measure(args, E, rank, world, device, builder=None, colloids=None, line="head",
             train=False):
     """Build, capture and time one workload of E envs per GPU; returns the
@@ -648,25 +697,7 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
     T = args.episode_length
     slice_graph = episode_graph = None
     if not args.no_graph:
-        # One graph per slice (for step counts that are not a multiple of T)
-        # and one per episode: the episode graph's T slices write T distinct
-        # trajectory tensors, so replaying it records a whole episode with no
-        # copies (agent.trajectory holds references to those tensors).
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(2):
-                one_slice()
-        torch.cuda.current_stream().wait_stream(side)
-        slice_graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(slice_graph):
-            one_slice()
-        agent.reset_trajectory()
-        episode_graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(episode_graph, pool=slice_graph.pool()):
-            # one episode as the trainers run it (episodic_trainer.py:35 ->
-            # engine.integrate(episode_length, force_fn))
-            eng.integrate(T, ff)
+        slice_graph, episode_graph, _ = capture_episode(eng, ff, agent, T)
     else:
         agent.reset_trajectory()
 
@@ -733,7 +764,7 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
 
     eng.drain_trajectory(block=True)
     traj_written = eng.h5_time_steps_written + len(eng.traj_holder["Times"])
-    kernel_ms, kernel, timing_note = time_run_kernel(eng, args.bd_reps)
+    kernel_ms, kernel, timing_note, timed_launches = time_run_kernel(eng, ff, agent, T)
     N = args.colloids
     sub = eng.params.steps_per_slice
     out = dict(timing)
@@ -749,6 +780,7 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
         "src_sha": source_sha(),
     })
     out["roofline"]["kernel_timing"] = timing_note
+    out["roofline"]["kernel_timing_launches"] = timed_launches
     valu = out["roofline"].get("valu")
     if valu:
         valu["lane_insts_per_colloid_substep"] = valu["insts_per_launch"] * 64 / (N * sub * E)

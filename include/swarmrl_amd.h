@@ -248,11 +248,23 @@ int swarm_engine_window_stats(swarm_engine_t *e, int32_t *fallback,
                               int32_t *waves);
 
 /* Kernel timing for measurement (bench.py roofline): returns the summed
- * duration (ms) and count of the k_cluster_run launches recorded since the
- * previous call (HIP events on the engine stream; waits for them), then
- * enables (1) or disables (0) recording.  Not for use under graph capture. */
+ * duration (ms) and count of the eager k_cluster_run launches recorded since
+ * the previous call (HIP events on the engine stream; waits for them), then
+ * enables (1) or disables (0) recording.  While recording, a window captured
+ * into a HIP graph gets event-record nodes (hipEventRecordExternal) around
+ * its run-kernel node instead: see swarm_engine_profile_graph. */
 int swarm_engine_profile(swarm_engine_t *e, int32_t enable, double *run_ms,
                          int32_t *launches);
+
+/* Run-kernel durations inside captured graphs (bench.py roofline: the kernel
+ * timed as it runs in the replayed episode): after a replay of a
+ * graph captured with recording enabled has been launched, waits for the
+ * device and writes the duration (ms) of every captured run node, in capture
+ * order, to ms_out[0..cap) and their count to *launches (each value is the
+ * latest replay's).  release = 1 then destroys the events (only once no graph
+ * holding them replays again). */
+int swarm_engine_profile_graph(swarm_engine_t *e, int32_t release, float *ms_out,
+                               int32_t cap, int32_t *launches);
 
 /* Kernel timing for measurement (bench.py roofline): builds the next 2-D
  * cluster window from the current positions, then launches its run kernel

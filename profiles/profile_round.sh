@@ -8,7 +8,8 @@
 #      WRITE_SIZE do not fit one pass; PMC passes carry no other trace domains)
 # then tools/summarize_profiles.py <tag> writes profiles/<tag>_*.
 # Usage: bash profiles/profile_round.sh <tag> [bench args...]
-#        (LINES="head batched" to profile a subset)
+#        (LINES="head batched" to profile a subset, PASSES="trace" to skip the
+#        counter passes)
 set -euo pipefail
 tag=$1; shift
 lines=${LINES:-"head batched c2 c4 c5 c3train"}
@@ -22,10 +23,15 @@ for line in $lines; do
       python3 bench.py --only "$line" --no-cpu-baseline "${BENCH_ARGS[@]}" > "$out/${sub}_bench.log" 2>&1
   }
   BENCH_ARGS=("$@")
-  run trace --kernel-trace --stats
-  run fetch --pmc FETCH_SIZE
-  run write --pmc WRITE_SIZE
-  run valu --pmc SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_WAVES
+  passes=${PASSES:-"trace fetch write valu"}
+  for p in $passes; do
+    case $p in
+      trace) run trace --kernel-trace --stats ;;
+      fetch) run fetch --pmc FETCH_SIZE ;;
+      write) run write --pmc WRITE_SIZE ;;
+      valu) run valu --pmc SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_WAVES ;;
+    esac
+  done
   echo "profiled $line"
 done
 echo "profiles written to gpurun_out/prof_${tag}"

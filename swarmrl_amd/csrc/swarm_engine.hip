@@ -1085,9 +1085,12 @@ struct swarm_engine {
   bool xcd_map = true;
   int noise_blocks = 0;
   bool next_table_ready = false;
-  // swarm_engine_profile: HIP events around every k_cluster_run launch
+  // swarm_engine_profile: HIP events around every k_cluster_run launch;
+  // launches captured into a graph get event-record nodes whose events are
+  // kept (graph_events) for swarm_engine_profile_graph after each replay
   bool profile = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> graph_events;
   float* own_f_swim = nullptr;
   float* own_torque_z = nullptr;
   void* allocs[96] = {};
@@ -1477,16 +1480,24 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
     return SWARM_OK;
   }
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool in_graph = false;
   if (e->profile) {
+    // under stream capture: event-record nodes around the run node, so each
+    // replay of the graph times the kernel as it runs in the workload
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIP_TRY(hipStreamIsCapturing(e->stream, &cs));
+    in_graph = cs == hipStreamCaptureStatusActive;
     HIP_TRY(hipEventCreate(&ev0));
     HIP_TRY(hipEventCreate(&ev1));
-    HIP_TRY(hipEventRecord(ev0, e->stream));
+    HIP_TRY(hipEventRecordWithFlags(ev0, e->stream,
+                                    in_graph ? hipEventRecordExternal : hipEventRecordDefault));
   }
   int rc = launch_run(e, n_steps);
   if (rc) return rc;
   if (e->profile) {
-    HIP_TRY(hipEventRecord(ev1, e->stream));
-    e->prof_events.emplace_back(ev0, ev1);
+    HIP_TRY(hipEventRecordWithFlags(ev1, e->stream,
+                                    in_graph ? hipEventRecordExternal : hipEventRecordDefault));
+    (in_graph ? e->graph_events : e->prof_events).emplace_back(ev0, ev1);
   }
   return launch_check(e, n_steps);
 }
@@ -1869,10 +1880,11 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
 void swarm_engine_destroy(swarm_engine_t* e) {
   if (!e) return;
   (void)hipDeviceSynchronize();
-  for (auto& pr : e->prof_events) {
-    (void)hipEventDestroy(pr.first);
-    (void)hipEventDestroy(pr.second);
-  }
+  for (auto* v : {&e->prof_events, &e->graph_events})
+    for (auto& pr : *v) {
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
+    }
   for (int k = 0; k < e->n_allocs; ++k) (void)hipFree(e->allocs[k]);
   if (e->d_start) (void)hipFree(e->d_start);
   if (e->d_pairs) (void)hipFree(e->d_pairs);
@@ -2083,6 +2095,32 @@ int swarm_engine_profile(swarm_engine_t* e, int32_t enable, double* run_ms, int3
   if (!e) return fail(SWARM_EINVAL, "null engine");
   const int rc = read_event_pairs(e->prof_events, run_ms, launches);
   e->profile = enable != 0;
+  return rc;
+}
+
+int swarm_engine_profile_graph(swarm_engine_t* e, int32_t release, float* ms_out, int32_t cap,
+                               int32_t* launches) {
+  if (!e) return fail(SWARM_EINVAL, "null engine");
+  if (cap < 0 || (cap > 0 && !ms_out)) return fail(SWARM_EINVAL, "ms_out needs cap entries");
+  // the replay ran on a stream the engine does not know: wait for the device
+  HIP_TRY(hipDeviceSynchronize());
+  int rc = SWARM_OK;
+  int k = 0;
+  for (auto& pr : e->graph_events) {
+    float ms = 0.0f;
+    const hipError_t err = hipEventElapsedTime(&ms, pr.first, pr.second);
+    if (err != hipSuccess && rc == SWARM_OK) rc = fail(SWARM_EDEVICE, hipGetErrorString(err));
+    if (k < cap) ms_out[k] = ms;
+    ++k;
+  }
+  if (launches) *launches = k;
+  if (release) {
+    for (auto& pr : e->graph_events) {
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
+    }
+    e->graph_events.clear();
+  }
   return rc;
 }
 

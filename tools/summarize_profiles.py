@@ -47,10 +47,19 @@ for line in bench.LINES:
     if not os.path.isdir(d):
         continue
     shutil.copy(f"{d}/trace/run_kernel_stats.csv", f"{dst}/{tag}_{line}_kernel_stats.csv")
+    timed_n = {}  # kernel regex -> launches bench.py timed at the end of the run
     for ln in open(f"{d}/trace_bench.log"):
         if ln.startswith("{"):
             with open(f"{dst}/{tag}_{line}_bench.json", "w") as f:
                 f.write(ln)
+            rec = json.loads(ln)
+            roof = rec.get("roofline") or {}
+            if roof.get("kernel_timing_launches"):
+                # the run kernel: event-timed inside an episode graph replayed
+                # after the timed region (bench.time_run_kernel)
+                timed_n[r"k_cluster_run"] = int(roof["kernel_timing_launches"])
+            if (rec.get("roofline_update") or {}).get("kernel"):
+                timed_n[r"k_ppo_grads"] = TIMED_TAIL  # swarm_ppo_profile's back-to-back reps
     dur = collections.defaultdict(list)
     rows = sorted(csv.DictReader(open(f"{d}/trace/run_kernel_trace.csv")),
                   key=lambda r: int(r["Start_Timestamp"]))
@@ -71,17 +80,20 @@ for line in bench.LINES:
         summary.append([line, k, len(dur.get(k, [])), f"{us:.2f}" if us else ""] +
                        [f"{mean[c]:.1f}" if mean[c] is not None else "" for c in COUNTERS])
         if re.search(DOMINANT.get(line, "$^"), k) and mean["FETCH_SIZE"] and mean["WRITE_SIZE"]:
+            n = next((v for rx, v in timed_n.items() if re.search(rx, k)), TIMED_TAIL)
+            ks = dur.get(k, [])
             traffic.append({
-                "line": line, "kernel": k, "dispatches": len(dur.get(k, [])),
+                "line": line, "kernel": k, "dispatches": len(ks),
                 "mean_duration_us": us,
-                # the launches bench.py's HIP events time: its last TIMED_TAIL
-                # dispatches of the kernel, back to back (time_run_kernel /
-                # time_ppo_grads, --bd-reps)
-                "mean_duration_timed_us": (sum(dur[k][-TIMED_TAIL:]) / TIMED_TAIL
-                                           if len(dur.get(k, [])) >= TIMED_TAIL else None),
-                # the captured graphs' launches (the workload itself)
-                "mean_duration_graph_us": (sum(dur[k][:-TIMED_TAIL]) / len(dur[k][:-TIMED_TAIL])
-                                           if len(dur.get(k, [])) > TIMED_TAIL else None),
+                # the launches bench.py's HIP events time: the kernel's last n
+                # dispatches (the run kernel: the windows of the episode graph
+                # replayed after the timed region; k_ppo_grads: --bd-reps
+                # back-to-back launches)
+                "timed_launches": n,
+                "mean_duration_timed_us": sum(ks[-n:]) / n if len(ks) >= n else None,
+                # every earlier launch (the workload itself: warmup and the
+                # timed region, mostly graph replays)
+                "mean_duration_graph_us": (sum(ks[:-n]) / len(ks[:-n]) if len(ks) > n else None),
                 "fetch_size_kb": mean["FETCH_SIZE"], "write_size_kb": mean["WRITE_SIZE"],
                 "bytes_per_launch": (2 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0,
                 "valu_insts_per_launch": mean["SQ_INSTS_VALU"],
