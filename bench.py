@@ -326,20 +326,36 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
     cnt = ctypes.c_int32()
     saved = agent.trajectory
     agent.reset_trajectory()
+    samples = []
+    how = (f"HIP event-record nodes around the run node of each window of an episode graph "
+           f"captured after the timed region, {replays} replays")
     nat.call("swarm_engine_profile", 1, ctypes.byref(ms), ctypes.byref(cnt))
+    graph = None
     try:
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             eng.integrate(episode_length, ff)
+    except RuntimeError as err:  # no event nodes in this HIP: eager episodes instead
+        graph = None
+        how = (f"HIP events around each run launch of {replays} eager episodes after the "
+               f"timed region (graph event nodes refused: {err})")
     finally:
         nat.call("swarm_engine_profile", 0, ctypes.byref(ms), ctypes.byref(cnt))
-    samples = []
     buf = (ctypes.c_float * 4096)()
     try:
-        for _ in range(replays):
-            graph.replay()
-            nat.call("swarm_engine_profile_graph", 0, buf, 4096, ctypes.byref(cnt))
-            samples.extend(buf[k] for k in range(min(cnt.value, 4096)))
+        if graph is not None:
+            for _ in range(replays):
+                graph.replay()
+                nat.call("swarm_engine_profile_graph", 0, buf, 4096, ctypes.byref(cnt))
+                samples.extend(buf[k] for k in range(min(cnt.value, 4096)))
+        else:
+            torch.cuda.synchronize()
+            agent.reset_trajectory()
+            nat.call("swarm_engine_profile", 1, ctypes.byref(ms), ctypes.byref(cnt))
+            for _ in range(replays):
+                eng.integrate(episode_length, ff)
+            nat.call("swarm_engine_profile", 0, ctypes.byref(ms), ctypes.byref(cnt))
+            samples = [ms.value / max(cnt.value, 1)] * cnt.value
         eng.drain_trajectory(block=True)
     finally:
         del graph
@@ -350,9 +366,7 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
         return None, name, "no run-kernel launches recorded", 0
     samples.sort()
     mean = sum(samples) / len(samples)
-    note = (f"HIP event-record nodes around the run node of each window of an episode graph "
-            f"captured after the timed region, {replays} replays x {len(samples) // replays} "
-            f"windows = {len(samples)} launches; median {samples[len(samples) // 2]:.5f} ms, "
+    note = (f"{how}: {len(samples)} launches; median {samples[len(samples) // 2]:.5f} ms, "
             f"min {samples[0]:.5f}, max {samples[-1]:.5f}")
     return mean, name, note, len(samples)
 

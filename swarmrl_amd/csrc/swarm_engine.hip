@@ -1379,6 +1379,27 @@ int launch_check(swarm_engine* e, int n_steps) {
   return SWARM_OK;
 }
 
+// Record `ev` on `s`; under capture as an event-record node appended to the
+// captured graph (this HIP refuses hipEventRecordWithFlags(.., External)
+// while capturing, so the node is added by hand and made the stream's
+// capture dependency).
+int record_event(hipStream_t s, hipEvent_t ev, bool in_graph) {
+  if (!in_graph) {
+    HIP_TRY(hipEventRecord(ev, s));
+    return SWARM_OK;
+  }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  hipGraph_t g = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t nd = 0;
+  HIP_TRY(hipStreamGetCaptureInfo_v2(s, &cs, &id, &g, &deps, &nd));
+  hipGraphNode_t node = nullptr;
+  HIP_TRY(hipGraphAddEventRecordNode(&node, g, deps, nd, ev));
+  HIP_TRY(hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies));
+  return SWARM_OK;
+}
+
 // One integration window: cluster build -> cluster run -> check/fallback.
 // use_prebuilt: the build ran already; noise_ready: the noise table holds
 // this many sub-steps from the current counter.
@@ -1489,14 +1510,14 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
     in_graph = cs == hipStreamCaptureStatusActive;
     HIP_TRY(hipEventCreate(&ev0));
     HIP_TRY(hipEventCreate(&ev1));
-    HIP_TRY(hipEventRecordWithFlags(ev0, e->stream,
-                                    in_graph ? hipEventRecordExternal : hipEventRecordDefault));
+    const int rc0 = record_event(e->stream, ev0, in_graph);
+    if (rc0) return rc0;
   }
   int rc = launch_run(e, n_steps);
   if (rc) return rc;
   if (e->profile) {
-    HIP_TRY(hipEventRecordWithFlags(ev1, e->stream,
-                                    in_graph ? hipEventRecordExternal : hipEventRecordDefault));
+    rc = record_event(e->stream, ev1, in_graph);
+    if (rc) return rc;
     (in_graph ? e->graph_events : e->prof_events).emplace_back(ev0, ev1);
   }
   return launch_check(e, n_steps);

@@ -102,3 +102,40 @@ def test_c3_training_4096_matches_oracle(tmp_path):
             step += 1
     for k in ("q", "img", "ang"):
         assert np.array_equal(got[k], st[k]), k
+
+
+def test_replicated_update_on_graph_episode_matches_local_update():
+    """The episode-parallel update path on the GPU (rollout.gather_episode +
+    replicated_update, as bench.py's c3train runs it at world > 1), here in
+    one process: the gathered episode of a replayed episode graph equals the
+    local trajectory, and the replicated update (fused PPO gradient, the PPO
+    graph from the second update on) leaves bit for bit the parameters and
+    Adam state of a twin agent updated with compute_loss on the local data."""
+    sys.path.insert(0, ROOT)
+    import copy
+
+    import bench
+    from swarmrl_amd import rollout
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    ns = argparse.Namespace(colloids=1024, envs_per_gpu=2, write_interval=1.0)
+    eng, ff, agent = bench.build_c3_workload(ns, 42, dev)
+    agent.loss.n_epochs = 3
+    twin = copy.deepcopy(agent.network)
+    eng.integrate(1, ff)
+    _, graph, _ = bench.capture_episode(eng, ff, agent, 5)
+    for ep in range(3):
+        graph.replay()
+        episode = rollout.gather_episode(agent.trajectory)
+        for k in ("features", "actions", "log_probs", "rewards"):
+            assert all(torch.equal(a, b) for a, b in zip(getattr(episode, k),
+                                                          getattr(agent.trajectory, k))), k
+        rollout.replicated_update(agent, episode, seed=ep)
+        agent.loss.compute_loss(network=twin, episode_data=agent.trajectory)
+        torch.cuda.synchronize()
+    a = rollout.replica_digest(agent)
+    tw = copy.copy(agent)
+    tw.network = twin
+    tw.intrinsic_reward = None
+    assert torch.equal(a, rollout.replica_digest(tw))
