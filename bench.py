@@ -342,12 +342,15 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
     finally:
         nat.call("swarm_engine_profile", 0, ctypes.byref(ms), ctypes.byref(cnt))
     buf = (ctypes.c_float * 4096)()
+    cal = (ctypes.c_float * 4096)()
+    cal_samples = []
     try:
         if graph is not None:
             for _ in range(replays):
                 graph.replay()
-                nat.call("swarm_engine_profile_graph", 0, buf, 4096, ctypes.byref(cnt))
+                nat.call("swarm_engine_profile_graph", 0, buf, cal, 4096, ctypes.byref(cnt))
                 samples.extend(buf[k] for k in range(min(cnt.value, 4096)))
+                cal_samples.extend(cal[k] for k in range(min(cnt.value, 4096)))
         else:
             torch.cuda.synchronize()
             agent.reset_trajectory()
@@ -360,14 +363,20 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
     finally:
         del graph
         torch.cuda.synchronize()
-        nat.call("swarm_engine_profile_graph", 1, None, 0, ctypes.byref(cnt))
+        nat.call("swarm_engine_profile_graph", 1, None, None, 0, ctypes.byref(cnt))
         agent.trajectory = saved
     if not samples:  # no 2-D cluster windows (global path): nothing was recorded
         return None, name, "no run-kernel launches recorded", 0
     samples.sort()
-    mean = sum(samples) / len(samples)
-    note = (f"{how}: {len(samples)} launches; median {samples[len(samples) // 2]:.5f} ms, "
-            f"min {samples[0]:.5f}, max {samples[-1]:.5f}")
+    raw = sum(samples) / len(samples)
+    # an empty pair of event nodes right after each run node measures what
+    # the pair adds by itself (marker packets, the dispatch gap they open):
+    # subtracted, the figure is the kernel's own duration in the workload
+    over = sum(cal_samples) / len(cal_samples) if cal_samples else 0.0
+    mean = raw - over
+    note = (f"{how}: {len(samples)} launches; event pair around the run node: mean {raw:.5f} "
+            f"ms, median {samples[len(samples) // 2]:.5f}, min {samples[0]:.5f}, max "
+            f"{samples[-1]:.5f}; minus an empty event-node pair ({over:.5f} ms)")
     return mean, name, note, len(samples)
 
 

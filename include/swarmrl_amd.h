@@ -259,12 +259,15 @@ int swarm_engine_profile(swarm_engine_t *e, int32_t enable, double *run_ms,
 /* Run-kernel durations inside captured graphs (bench.py roofline: the kernel
  * timed as it runs in the replayed episode): after a replay of a
  * graph captured with recording enabled has been launched, waits for the
- * device and writes the duration (ms) of every captured run node, in capture
- * order, to ms_out[0..cap) and their count to *launches (each value is the
- * latest replay's).  release = 1 then destroys the events (only once no graph
- * holding them replays again). */
+ * device and writes the time (ms) between the event nodes around every
+ * captured run node, in capture order, to ms_out[0..cap), and (cal_out, may
+ * be NULL) the time between the two event nodes of an empty pair recorded
+ * right after each run node -- what a pair of event nodes adds by itself --
+ * and their count to *launches (each value is the latest replay's).
+ * release = 1 then destroys the events (only once no graph holding them
+ * replays again). */
 int swarm_engine_profile_graph(swarm_engine_t *e, int32_t release, float *ms_out,
-                               int32_t cap, int32_t *launches);
+                               float *cal_out, int32_t cap, int32_t *launches);
 
 /* Kernel timing for measurement (bench.py roofline): builds the next 2-D
  * cluster window from the current positions, then launches its run kernel
@@ -474,6 +477,24 @@ int swarm_ppo_epoch_grad(const float *x, int32_t T, int32_t S, int32_t d_in,
 int swarm_rnd_distance(const float *x, int32_t n, int32_t d_in, int32_t width,
                        const float *const *target, const float *const *predictor,
                        int32_t order, float *out, void *stream);
+
+/* The per-env RND intrinsic reward added to the task reward (the device
+ * path of random_network_distillation.py:126-143 followed by the
+ * `task + intrinsic` of actor_critic.py calc_reward): x [n_envs * per_env]
+ * [d_in] observations (env-major), the metric of every observation into
+ * metric[n_envs * per_env] (as swarm_rnd_distance), r_e = mean of env e's
+ * metrics (fp64 sum in a fixed order), clipped to [clip_lo, clip_hi] when
+ * clip != 0, into env_reward[n_envs], and
+ *   rewards[e][a] = base[e][a] + r_e   (base NULL: r_e).
+ * workspace: device memory of swarm_rnd_env_workspace_bytes(n_envs, per_env)
+ * bytes.  Two launches, asynchronous on `stream`; no host synchronisation. */
+int swarm_rnd_env_reward(const float *x, int32_t n_envs, int32_t per_env, int32_t d_in,
+                         int32_t width, const float *const *target,
+                         const float *const *predictor, int32_t order, int32_t clip,
+                         float clip_lo, float clip_hi, const float *base, float *metric,
+                         float *env_reward, float *rewards, void *workspace,
+                         int64_t workspace_bytes, void *stream);
+int64_t swarm_rnd_env_workspace_bytes(int32_t n_envs, int32_t per_env);
 
 /* Neighbour reductions for the classical agents (all pointers device):
  * get_colloids_in_vision of bechinger_models.py:156-171 (range + cone) and

@@ -123,7 +123,8 @@ _SIGNATURES = {
     "swarm_engine_prebuild": (ctypes.c_int, [_P, _P, ctypes.c_int32]),
     "swarm_engine_prebuild_noise": (ctypes.c_int, [_P, _P, ctypes.c_int32]),
     "swarm_engine_profile": (ctypes.c_int, [_P, ctypes.c_int32, _P, _P]),
-    "swarm_engine_profile_graph": (ctypes.c_int, [_P, ctypes.c_int32, _P, ctypes.c_int32, _P]),
+    "swarm_engine_profile_graph": (ctypes.c_int, [_P, ctypes.c_int32, _P, _P, ctypes.c_int32,
+                                                  _P]),
     "swarm_engine_time_run": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _P]),
     "swarm_engine_debug_phases": (ctypes.c_int, [_P, _P]),
     "swarm_engine_debug_wave_stamps": (ctypes.c_int, [_P, _P, ctypes.c_int32]),
@@ -164,6 +165,13 @@ _SIGNATURES = {
         ctypes.c_int,
         [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_int32, _P, _P],
     ),
+    "swarm_rnd_env_reward": (
+        ctypes.c_int,
+        [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P,
+         ctypes.c_int32, ctypes.c_int32, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P,
+         ctypes.c_int64, _P],
+    ),
+    "swarm_rnd_env_workspace_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
     "swarm_engine_traj_ring": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _P, _P]),
     "swarm_engine_traj_record": (ctypes.c_int, [_P]),
     "swarm_traj_entry_to_host": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),

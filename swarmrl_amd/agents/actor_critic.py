@@ -172,7 +172,12 @@ class ActorCriticAgent(Agent):
     def calc_reward(self, colloids, external_reward: float = 0.0):
         rewards = self.task(colloids)
         if self.intrinsic_reward:
-            rewards = rewards + self.intrinsic_reward.compute_reward(episode_data=self.trajectory)
+            add = getattr(self.intrinsic_reward, "add_to_reward", None)
+            if add is not None:  # task + intrinsic fused on the device (RNDReward)
+                rewards = add(rewards, self.trajectory)
+            else:
+                rewards = rewards + self.intrinsic_reward.compute_reward(
+                    episode_data=self.trajectory)
         if not (isinstance(external_reward, (int, float)) and external_reward == 0):
             rewards = rewards + external_reward
         if self.train:

@@ -682,12 +682,13 @@ __global__ __launch_bounds__(256) void k_vision_pairs(DevState st, const Derived
                                                       int lxb, int lyb, int pair_bx) {
   __shared__ uint32_t hits[kVisionHits][256];
   __shared__ float nb2[swarm::kMaxSpecies * swarm::kMaxSpecies];
+  __shared__ int32_t uf[2 * 256];
   const int b = blockIdx.x;
   if (b < n_vblocks) {
     vision_body<NB, G, false>(st, d, va, b, 0, hits);
   } else {
     const int pb = b - n_vblocks;
-    swarm::build_pairs_body(d, st, sc, lxb, lyb, pb % pair_bx, pb / pair_bx, nb2);
+    swarm::build_pairs_body(d, st, sc, lxb, lyb, pb % pair_bx, pb / pair_bx, nb2, uf);
   }
 }
 
@@ -700,7 +701,7 @@ __global__ __launch_bounds__(1024) void k_policy_cbuild(swarm::MlpArgs m, int n_
     swarm::policy_body<G, D, K>(m, b, reinterpret_cast<float*>(smem));
   } else {
     const int e = b - n_pblocks;
-    swarm::cluster_build_env<false, true>(st, sc, e, smem, sc.gnpairs[e]);
+    swarm::cluster_build_env<false, true, true>(st, sc, e, smem, sc.gnpairs[e]);
   }
 }
 
@@ -1091,6 +1092,9 @@ struct swarm_engine {
   bool profile = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> graph_events;
+  // per captured run node, an empty event pair recorded right after it: the
+  // cost of an event-record node pair itself (swarm_engine_profile_graph)
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> graph_cal;
   float* own_f_swim = nullptr;
   float* own_torque_z = nullptr;
   void* allocs[96] = {};
@@ -1157,9 +1161,12 @@ void set_lds_attributes() {
   static bool done = false;
   if (done) return;
   const void* fns[] = {reinterpret_cast<const void*>(&swarm::k_global),
-                       reinterpret_cast<const void*>(&swarm::k_cluster_build<false>),
-                       reinterpret_cast<const void*>(&swarm::k_cluster_build<true>),
-                       reinterpret_cast<const void*>(&swarm::k_cluster_build_packed),
+                       reinterpret_cast<const void*>(&swarm::k_cluster_build<false, false>),
+                       reinterpret_cast<const void*>(&swarm::k_cluster_build<false, true>),
+                       reinterpret_cast<const void*>(&swarm::k_cluster_build<true, false>),
+                       reinterpret_cast<const void*>(&swarm::k_cluster_build<true, true>),
+                       reinterpret_cast<const void*>(&swarm::k_cluster_build_packed<false>),
+                       reinterpret_cast<const void*>(&swarm::k_cluster_build_packed<true>),
                        reinterpret_cast<const void*>(&swarm::k_build_sort<4>),
                        reinterpret_cast<const void*>(&swarm::k_build_sort<16>),
                        reinterpret_cast<const void*>(&swarm::k_build_env),
@@ -1250,16 +1257,31 @@ int launch_build(swarm_engine* e, hipStream_t stream) {
     hipLaunchKernelGGL(swarm::k_build_pairs, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
                        dim3(256), 0, stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb);
   HIP_TRY(hipGetLastError());
+  // 2-D: the pair search left block-local union-find roots and a cross list
+  // (build_pairs_body); 3-D (k_build_pairs3): the whole pair list is unioned
+  const bool local = e->params.n_dims == 2;
   if (e->big_build && swarm::build_lds_words_packed(e->n) * 4 <= kMaxLds &&
-      !(std::getenv("SWARMRL_AMD_PACKED_BUILD") && std::getenv("SWARMRL_AMD_PACKED_BUILD")[0] == '0'))
-    hipLaunchKernelGGL(swarm::k_cluster_build_packed, dim3(e->n_envs), dim3(1024),
-                       swarm::build_lds_words_packed(e->n) * 4, stream, e->st, e->sc);
-  else if (e->big_build)
-    hipLaunchKernelGGL(swarm::k_cluster_build<true>, dim3(e->n_envs), dim3(1024),
-                       swarm::build_lds_words_big(e->n) * 4, stream, e->st, e->sc);
-  else
-    hipLaunchKernelGGL(swarm::k_cluster_build<false>, dim3(e->n_envs), dim3(1024),
+      !(std::getenv("SWARMRL_AMD_PACKED_BUILD") && std::getenv("SWARMRL_AMD_PACKED_BUILD")[0] == '0')) {
+    if (local)
+      hipLaunchKernelGGL(swarm::k_cluster_build_packed<true>, dim3(e->n_envs), dim3(1024),
+                         swarm::build_lds_words_packed(e->n) * 4, stream, e->st, e->sc);
+    else
+      hipLaunchKernelGGL(swarm::k_cluster_build_packed<false>, dim3(e->n_envs), dim3(1024),
+                         swarm::build_lds_words_packed(e->n) * 4, stream, e->st, e->sc);
+  } else if (e->big_build) {
+    if (local)
+      hipLaunchKernelGGL((swarm::k_cluster_build<true, true>), dim3(e->n_envs), dim3(1024),
+                         swarm::build_lds_words_big(e->n) * 4, stream, e->st, e->sc);
+    else
+      hipLaunchKernelGGL((swarm::k_cluster_build<true, false>), dim3(e->n_envs), dim3(1024),
+                         swarm::build_lds_words_big(e->n) * 4, stream, e->st, e->sc);
+  } else if (local) {
+    hipLaunchKernelGGL((swarm::k_cluster_build<false, true>), dim3(e->n_envs), dim3(1024),
                        build_lds_bytes(e->n, e->sc.pair_cap), stream, e->st, e->sc);
+  } else {
+    hipLaunchKernelGGL((swarm::k_cluster_build<false, false>), dim3(e->n_envs), dim3(1024),
+                       build_lds_bytes(e->n, e->sc.pair_cap), stream, e->st, e->sc);
+  }
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
 }
@@ -1285,7 +1307,7 @@ int flush_ride_along(swarm_engine* e) {
                        dim3(256), 0, e->stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb);
     HIP_TRY(hipGetLastError());
   }
-  hipLaunchKernelGGL(swarm::k_cluster_build<false>, dim3(e->n_envs), dim3(1024),
+  hipLaunchKernelGGL((swarm::k_cluster_build<false, true>), dim3(e->n_envs), dim3(1024),
                      build_lds_bytes(e->n, e->sc.pair_cap), e->stream, e->st, e->sc);
   HIP_TRY(hipGetLastError());
   e->prebuilt = true;
@@ -1519,6 +1541,15 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
     rc = record_event(e->stream, ev1, in_graph);
     if (rc) return rc;
     (in_graph ? e->graph_events : e->prof_events).emplace_back(ev0, ev1);
+    if (in_graph) {
+      hipEvent_t c0 = nullptr, c1 = nullptr;
+      HIP_TRY(hipEventCreate(&c0));
+      HIP_TRY(hipEventCreate(&c1));
+      rc = record_event(e->stream, c0, true);
+      if (!rc) rc = record_event(e->stream, c1, true);
+      if (rc) return rc;
+      e->graph_cal.emplace_back(c0, c1);
+    }
   }
   return launch_check(e, n_steps);
 }
@@ -1813,6 +1844,9 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->sc.bsid, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.bcstart, (size_t)n_envs * ((1 << lcb) + 1));
   rc = rc ? rc : dev_alloc(e, &e->sc.gplist, (size_t)n_envs * std::max(e->sc.pair_cap, 1));
+  rc = rc ? rc : dev_alloc(e, &e->sc.xpairs, (size_t)n_envs * std::max(e->sc.pair_cap, 1));
+  rc = rc ? rc : dev_alloc(e, &e->sc.lroot, M);
+  rc = rc ? rc : dev_alloc(e, &e->sc.gnx, (size_t)n_envs);
   rc = rc ? rc : dev_alloc(e, &e->sc.gnpairs, (size_t)n_envs);
   if (e->big_build) rc = rc ? rc : dev_alloc(e, &e->sc.gclus, 3 * M);
   rc = rc ? rc : dev_alloc(e, &e->sc.wave_npairs, (size_t)n_envs * (S / 64));
@@ -1901,7 +1935,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
 void swarm_engine_destroy(swarm_engine_t* e) {
   if (!e) return;
   (void)hipDeviceSynchronize();
-  for (auto* v : {&e->prof_events, &e->graph_events})
+  for (auto* v : {&e->prof_events, &e->graph_events, &e->graph_cal})
     for (auto& pr : *v) {
       (void)hipEventDestroy(pr.first);
       (void)hipEventDestroy(pr.second);
@@ -2119,28 +2153,35 @@ int swarm_engine_profile(swarm_engine_t* e, int32_t enable, double* run_ms, int3
   return rc;
 }
 
-int swarm_engine_profile_graph(swarm_engine_t* e, int32_t release, float* ms_out, int32_t cap,
-                               int32_t* launches) {
+int swarm_engine_profile_graph(swarm_engine_t* e, int32_t release, float* ms_out, float* cal_out,
+                               int32_t cap, int32_t* launches) {
   if (!e) return fail(SWARM_EINVAL, "null engine");
   if (cap < 0 || (cap > 0 && !ms_out)) return fail(SWARM_EINVAL, "ms_out needs cap entries");
   // the replay ran on a stream the engine does not know: wait for the device
   HIP_TRY(hipDeviceSynchronize());
   int rc = SWARM_OK;
-  int k = 0;
-  for (auto& pr : e->graph_events) {
-    float ms = 0.0f;
-    const hipError_t err = hipEventElapsedTime(&ms, pr.first, pr.second);
-    if (err != hipSuccess && rc == SWARM_OK) rc = fail(SWARM_EDEVICE, hipGetErrorString(err));
-    if (k < cap) ms_out[k] = ms;
-    ++k;
-  }
+  auto read = [&](std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, float* out) {
+    int k = 0;
+    for (auto& pr : v) {
+      float ms = 0.0f;
+      const hipError_t err = hipEventElapsedTime(&ms, pr.first, pr.second);
+      if (err != hipSuccess && rc == SWARM_OK) rc = fail(SWARM_EDEVICE, hipGetErrorString(err));
+      if (out && k < cap) out[k] = ms;
+      ++k;
+    }
+    return k;
+  };
+  const int k = read(e->graph_events, ms_out);
+  read(e->graph_cal, cal_out);
   if (launches) *launches = k;
   if (release) {
-    for (auto& pr : e->graph_events) {
-      (void)hipEventDestroy(pr.first);
-      (void)hipEventDestroy(pr.second);
+    for (auto* v : {&e->graph_events, &e->graph_cal}) {
+      for (auto& pr : *v) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+      }
+      v->clear();
     }
-    e->graph_events.clear();
   }
   return rc;
 }
@@ -2340,6 +2381,48 @@ int swarm_rnd_distance(const float* x, int32_t n, int32_t d_in, int32_t width,
                        pp, order, out);
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
+}
+
+int swarm_rnd_env_reward(const float* x, int32_t n_envs, int32_t per_env, int32_t d_in,
+                         int32_t width, const float* const* target, const float* const* predictor,
+                         int32_t order, int32_t clip, float clip_lo, float clip_hi,
+                         const float* base, float* metric, float* env_reward, float* rewards,
+                         void* workspace, int64_t workspace_bytes, void* stream) {
+  if (!x || !target || !predictor || !metric || !env_reward || !rewards || !workspace)
+    return fail(SWARM_EINVAL, "null argument");
+  if (width != swarm::kRndWidth) return fail(SWARM_ECAPACITY, "RND width must be 32");
+  if (d_in < 1 || d_in > swarm::kRndMaxIn) return fail(SWARM_ECAPACITY, "1 <= d_in <= 16");
+  if (order < 1) return fail(SWARM_EINVAL, "distance order must be >= 1");
+  if (n_envs < 0 || per_env < 0) return fail(SWARM_EINVAL, "n_envs, per_env >= 0");
+  if (n_envs == 0 || per_env == 0) return SWARM_OK;
+  const int kb = (per_env + 255) / 256;
+  if (workspace_bytes < (int64_t)n_envs * kb * (int64_t)sizeof(double))
+    return fail(SWARM_ECAPACITY, "workspace below swarm_rnd_env_workspace_bytes");
+  swarm::RndPtrs tp, pp;
+  for (int k = 0; k < 6; ++k) {
+    if (!target[k] || !predictor[k]) return fail(SWARM_EINVAL, "null parameter");
+    tp.w[k] = target[k];
+    pp.w[k] = predictor[k];
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  double* partial = static_cast<double*>(workspace);
+  const dim3 grid((unsigned)kb, (unsigned)n_envs);
+  if (d_in <= 4)
+    hipLaunchKernelGGL(swarm::k_rnd_env_partial<4>, grid, dim3(256), 0, s, x, per_env, d_in, tp,
+                       pp, order, metric, partial);
+  else
+    hipLaunchKernelGGL(swarm::k_rnd_env_partial<16>, grid, dim3(256), 0, s, x, per_env, d_in, tp,
+                       pp, order, metric, partial);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(swarm::k_rnd_env_finish, dim3((unsigned)n_envs), dim3(1024), 0, s, partial,
+                     kb, per_env, clip ? 1 : 0, clip_lo, clip_hi, base, env_reward, rewards);
+  HIP_TRY(hipGetLastError());
+  return SWARM_OK;
+}
+
+int64_t swarm_rnd_env_workspace_bytes(int32_t n_envs, int32_t per_env) {
+  if (n_envs < 0 || per_env < 0) return -1;
+  return (int64_t)n_envs * ((per_env + 255) / 256) * (int64_t)sizeof(double);
 }
 
 int64_t swarm_engine_step_count(const swarm_engine_t* e) {

@@ -210,6 +210,13 @@ struct Scratch {
   int32_t* bcstart;   // [E][ncb + 1] first sorted entry of every cell, [ncb] = N
   uint32_t* gplist;   // [E][pair_cap] neighbour pairs i | j << 16, i < j
   int32_t* gnpairs;   // [E] pairs found (may exceed pair_cap: overflow)
+  // 2-D pair search (build_pairs_body): every block unions the pairs whose
+  // both ends lie in its range of sorted entries (a compact band of cells)
+  // in LDS and writes each particle's block-local root; the pairs between
+  // blocks go to a cross list, the only pairs the cluster build still unions
+  int32_t* lroot;     // [M] block-local union-find root (a particle of the env)
+  uint32_t* xpairs;   // [E][pair_cap] cross-block pairs i | j << 16
+  int32_t* gnx;       // [E] cross-block pairs found
   int32_t* gclus;     // [3][M] cluster sizes / bases / slots (large-N build only)
   int32_t pair_cap;   // pairs per env
   int32_t one_pass;   // 1: pack clusters so that a wave has <= 64 pairs
@@ -1018,6 +1025,23 @@ __device__ __forceinline__ void uf_union(int32_t* parent, int a, int b) {
   }
 }
 
+// A class counter increment aggregated over the wave: one LDS atomic per
+// wave for its lanes with pred set; returns the lane's rank (the counter's
+// old value + the lanes below it).  The packing's singleton and pair classes
+// otherwise take hundreds (E = 1) to thousands (C5) of same-address atomics,
+// which the LDS executes one after another.
+__device__ __forceinline__ int wave_class_add(int32_t* ctr, bool pred) {
+  const uint64_t m = __ballot(pred);
+  if (m == 0) return 0;
+  const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  const int leader = __builtin_ctzll(m);
+  int base = 0;
+  if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(ctr, __builtin_popcountll(m));
+  base = __shfl(base, leader);
+  return base + below;
+}
+
 // LDS words of k_cluster_build: 168 fixed + per-wave pair counters +
 // parent[N] + 3 N (cluster sizes, bases, slots) + the env's pair list.
 __host__ __device__ inline size_t build_lds_words(int n, int pair_cap) {
@@ -1061,6 +1085,7 @@ __device__ __forceinline__ void build_sort_body(const DevState& st, const Scratc
   for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
   if (tid == 0) {
     sc.gnpairs[e] = 0;
+    sc.gnx[e] = 0;
     sc.fallback[e] = 0;  // the neighbour-list build sets it on overflow
   }
   __syncthreads();
@@ -1169,11 +1194,13 @@ __global__ __launch_bounds__(1024) void k_build_sort(DevState st, Scratch sc, in
 // fused launches pass their own block index); nb2: a block-shared table.
 __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, const DevState& st,
                                                  const Scratch& sc, int lx, int ly, int bx, int e,
-                                                 float* nb2) {
+                                                 float* nb2, int32_t* uf) {
   constexpr int kKeep = 8;
   for (int k = threadIdx.x; k < kMaxSpecies * kMaxSpecies; k += blockDim.x) nb2[k] = d->nb2[k];
   const int N = st.n;
-  const int ps = bx * blockDim.x + threadIdx.x;
+  const int T = blockDim.x, t = threadIdx.x;
+  const int lo = bx * T;  // this block's sorted entries [lo, lo + T)
+  const int ps = lo + t;
   const bool valid = ps < N;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly);
@@ -1238,7 +1265,7 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
   }
   const int total = pre[6];
   for (int f0 = 0; f0 < total; f0 += kFly) {
-    int pk4[kFly];
+    int pk4[kFly], jj4[kFly];
     uint32_t x4[kFly], y4[kFly];
 #pragma unroll
     for (int u = 0; u < kFly; ++u) {
@@ -1248,6 +1275,7 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
       for (int r = 1; r < 6; ++r) o = f >= pre[r] ? off[r] : o;
       const int jj = f + o;
       const bool ok = f < total;
+      jj4[u] = jj;
       pk4[u] = ok ? sc.bsid[base + jj] : -1;
       x4[u] = ok ? sc.bsq[base + jj] : 0u;
       y4[u] = ok ? sc.bsq[M + base + jj] : 0u;
@@ -1261,26 +1289,68 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
       const float ry = per ? (float)(int32_t)(y4[u] - qy) * sx1
                            : pair_disp(y4[u], st.img[M + base + j], qy, iy, sx1, false);
       if (i < j && rx * rx + ry * ry < nb2_row[pk4[u] >> 24]) {
+        // j, and for a partner inside this block's sorted range its block
+        // slot + 1 (a pair the block unions itself)
+        const int ls = jj4[u] - lo;
+        const uint32_t kv = (uint32_t)j | (ls >= 0 && ls < T ? (uint32_t)(ls + 1) << 16 : 0u);
 #pragma unroll
-        for (int v = 0; v < kKeep; ++v) keep[v] = found == v ? (uint32_t)j : keep[v];
+        for (int v = 0; v < kKeep; ++v) keep[v] = found == v ? kv : keep[v];
         ++found;
       }
     }
   }
-  // wave prefix sum, one atomic per wave
+  // Block-local union-find of the pairs whose both ends are in this block
+  // (LDS only; done before any global store is issued, so the block
+  // barriers below wait for LDS operations and not for store write-backs).
   const int lane = threadIdx.x & 63;
-  int v = found;
+  const bool dense = __any(found > kKeep);  // a lane kept only kKeep: the wave rescans
+  int32_t* lpar = uf;       // [T] block-local union-find over the block's entries
+  int32_t* lid = uf + T;    // [T] particle of a block slot
+  lpar[t] = t;
+  lid[t] = valid ? i : -1;
+  __syncthreads();
+  if (!dense) {
+#pragma unroll
+    for (int u = 0; u < kKeep; ++u)
+      if (u < found && (keep[u] >> 16) != 0u) uf_union(lpar, t, (int)(keep[u] >> 16) - 1);
+  }
+  __syncthreads();
+  if (valid) sc.lroot[base + i] = lid[uf_find(lpar, t)];
+  // wave prefix sums, one atomic per wave: every pair to the pair list, the
+  // pairs whose partner lies outside the block (all of a dense wave's) also
+  // to the cross list
+  int nx = 0;
+  if (!dense) {
+#pragma unroll
+    for (int u = 0; u < kKeep; ++u) nx += u < found && (keep[u] >> 16) == 0u ? 1 : 0;
+  } else {
+    nx = found;
+  }
+  int v = found, vx = nx;
   v = wave_incl_scan(v);
-  int wbase = 0;
-  if (lane == 63) wbase = atomicAdd(&sc.gnpairs[e], v);
+  vx = wave_incl_scan(vx);
+  int wbase = 0, xbase = 0;
+  if (lane == 63) {
+    wbase = atomicAdd(&sc.gnpairs[e], v);
+    xbase = atomicAdd(&sc.gnx[e], vx);
+  }
   wbase = __builtin_amdgcn_readlane(wbase, 63);
+  xbase = __builtin_amdgcn_readlane(xbase, 63);
   const int my_off = wbase + v - found;
+  const int my_xoff = xbase + vx - nx;
   uint32_t* out = sc.gplist + (size_t)e * sc.pair_cap;
-  if (!__any(found > kKeep)) {
+  uint32_t* xout = sc.xpairs + (size_t)e * sc.pair_cap;
+  if (!dense) {
+    int w = 0;
 #pragma unroll
     for (int u = 0; u < kKeep; ++u) {
       const int k = my_off + u;
-      if (u < found && k < sc.pair_cap) out[k] = (uint32_t)i | (keep[u] << 16);
+      const uint32_t j = keep[u] & 0xffffu;
+      if (u < found && k < sc.pair_cap) out[k] = (uint32_t)i | (j << 16);
+      if (u < found && (keep[u] >> 16) == 0u) {
+        if (my_xoff + w < sc.pair_cap) xout[my_xoff + w] = (uint32_t)i | (j << 16);
+        ++w;
+      }
     }
     return;
   }
@@ -1299,6 +1369,7 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
       if (i < j && rx * rx + ry * ry < nb2_row[packed >> 24]) {
         const int k = my_off + w;
         if (k < sc.pair_cap) out[k] = (uint32_t)i | ((uint32_t)j << 16);
+        if (my_xoff + w < sc.pair_cap) xout[my_xoff + w] = (uint32_t)i | ((uint32_t)j << 16);
         ++w;
       }
     }
@@ -1308,7 +1379,8 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
 __global__ __launch_bounds__(256) void k_build_pairs(const Derived* __restrict__ d, DevState st,
                                                      Scratch sc, int lx, int ly) {
   __shared__ float nb2[kMaxSpecies * kMaxSpecies];
-  build_pairs_body(d, st, sc, lx, ly, blockIdx.x, blockIdx.y, nb2);
+  __shared__ int32_t uf[2 * 256];
+  build_pairs_body(d, st, sc, lx, ly, blockIdx.x, blockIdx.y, nb2, uf);
 }
 
 // LDS words of the large-N variant: the union-find forest only.
@@ -1324,7 +1396,7 @@ __host__ __device__ inline size_t build_lds_words_big(int n) {
 // too large for them in LDS); the forest is always in LDS.
 // kCopy: the pair list (found pairs) is copied from sc.gplist into LDS;
 // otherwise (!kBig) it is in LDS already (k_build_env).
-template <bool kBig, bool kCopy>
+template <bool kBig, bool kCopy, bool kLocal = false>
 __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scratch& sc, int e,
                                                   unsigned char* smem, int found) {
   const int T = blockDim.x, tid = threadIdx.x, N = st.n;
@@ -1346,11 +1418,16 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   const int S = sc.S;
   SWARM_STAMP(6);
   const int npairs = min(found, sc.pair_cap);
+  // kLocal: the pair search's blocks unioned their own pairs already
+  // (sc.lroot: a forest of depth one), only the cross-block pairs remain
+  const int nx = kLocal ? sc.gnx[e] : 0;
+  const uint32_t* xl = sc.xpairs + (size_t)e * sc.pair_cap;
   for (int k = tid; k < 68; k += T) classcnt[k] = 0;
   for (int k = tid; k < wmax; k += T) wave_np[k] = 0;
-  if (tid < 16) misc[tid] = tid == 0 && found > sc.pair_cap ? 1 : 0;  // overflow -> global path
+  // overflow of the pair or cross list -> global path
+  if (tid < 16) misc[tid] = tid == 0 && (found > sc.pair_cap || nx > sc.pair_cap) ? 1 : 0;
   for (int i = tid; i < N; i += T) {
-    parent[i] = i;
+    parent[i] = kLocal ? sc.lroot[base + i] : i;
     csz[i] = 0;
     cbase[i] = 0;  // pair count of a cluster (one-pass packing), then its base
   }
@@ -1390,18 +1467,30 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   // (the union sweep reads its pairs four at a time even in LDS: the
   // unions are serial per thread, the list reads need not be)
   constexpr int kUU = kU > 4 ? kU : 4;
-  for (int k0 = tid; k0 < nsweep; k0 += kUU * T) {
-    uint32_t pr[kUU];
-    bool ok[kUU];
+  if (kLocal) {  // the cross-block pairs only (global memory, few)
+    const int nxc = min(nx, sc.pair_cap);
+    for (int k0 = tid; k0 < nxc; k0 += kUU * T) {
+      uint32_t pr[kUU];
 #pragma unroll
-    for (int u = 0; u < kUU; ++u) {
-      const int pk = sweep_pair(k0 + u * T);
-      ok[u] = k0 + u * T < nsweep && pk < npairs;
-      pr[u] = ok[u] ? plist[pk] : 0u;
+      for (int u = 0; u < kUU; ++u) pr[u] = k0 + u * T < nxc ? xl[k0 + u * T] : 0u;
+#pragma unroll
+      for (int u = 0; u < kUU; ++u)
+        if (k0 + u * T < nxc) uf_union(parent, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
     }
+  } else {
+    for (int k0 = tid; k0 < nsweep; k0 += kUU * T) {
+      uint32_t pr[kUU];
+      bool ok[kUU];
 #pragma unroll
-    for (int u = 0; u < kUU; ++u)
-      if (ok[u]) uf_union(parent, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
+      for (int u = 0; u < kUU; ++u) {
+        const int pk = sweep_pair(k0 + u * T);
+        ok[u] = k0 + u * T < nsweep && pk < npairs;
+        pr[u] = ok[u] ? plist[pk] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kUU; ++u)
+        if (ok[u]) uf_union(parent, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
+    }
   }
   __syncthreads();
   SWARM_STAMP(7);
@@ -1453,15 +1542,19 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int i = i0 + u * T;
-      if (i >= N || parent[i] != i) continue;
+      const bool root = i < N && parent[i] == i;
       const int s = sz[u];
+      const int w = sc.one_pass ? max(s, min(min(pc[u], 64), 2 * s)) : s;
+      // the two most frequent classes by one atomic per wave
+      const int r1 = wave_class_add(&classcnt[1], root && s <= 64 && w == 1);
+      const int r2 = wave_class_add(&classcnt[2], root && s <= 64 && w == 2);
+      if (!root) continue;
       if (s > 64) {  // wider than a wave: a big cluster, run by k_check's workgroup
         atomicAdd(&misc[4], s);
         cbase[i] = kBigMark;
       } else {
-        const int w = sc.one_pass ? max(s, min(min(pc[u], 64), 2 * s)) : s;
         csz[i] = w;
-        cbase[i] = atomicAdd(&classcnt[w], 1);
+        cbase[i] = w == 1 ? r1 : (w == 2 ? r2 : atomicAdd(&classcnt[w], 1));
       }
     }
   }
@@ -1653,6 +1746,7 @@ __host__ __device__ inline size_t build_lds_words_packed(int n) {
 //         size < 2^16); then class rank | w << 24; then the cluster's first
 //         slot (or kBigMark).
 // The pair list stays in global memory (read kU at a time).
+template <bool kLocal>
 __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, int e,
                                          unsigned char* smem, int found) {
   const int T = blockDim.x, tid = threadIdx.x, N = st.n;
@@ -1671,21 +1765,27 @@ __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, 
   constexpr int kU = 8;
   SWARM_STAMP(6);
   const int npairs = min(found, sc.pair_cap);
+  // kLocal: start from the pair search's block-local forest, union the
+  // cross-block pairs only (cluster_build_env)
+  const int nx = kLocal ? sc.gnx[e] : 0;
+  const int nun = kLocal ? min(nx, sc.pair_cap) : npairs;
+  const uint32_t* ulist = kLocal ? sc.xpairs + (size_t)e * sc.pair_cap : plist;
   for (int k = tid; k < 68; k += T) classcnt[k] = 0;
   for (int k = tid; k < wmax; k += T) wave_np[k] = 0;
-  if (tid < 16) misc[tid] = tid == 0 && found > sc.pair_cap ? 1 : 0;  // overflow -> global path
+  // overflow of the pair or cross list -> global path
+  if (tid < 16) misc[tid] = tid == 0 && (found > sc.pair_cap || nx > sc.pair_cap) ? 1 : 0;
   for (int i = tid; i < N; i += T) {
-    A[i] = i;
+    A[i] = kLocal ? sc.lroot[base + i] : i;
     B[i] = 0;
   }
   __syncthreads();
-  for (int k0 = tid; k0 < npairs; k0 += kU * T) {
+  for (int k0 = tid; k0 < nun; k0 += kU * T) {
     uint32_t pr[kU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) pr[u] = k0 + u * T < npairs ? plist[k0 + u * T] : 0u;
+    for (int u = 0; u < kU; ++u) pr[u] = k0 + u * T < nun ? ulist[k0 + u * T] : 0u;
 #pragma unroll
     for (int u = 0; u < kU; ++u)
-      if (k0 + u * T < npairs) uf_union(A, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
+      if (k0 + u * T < nun) uf_union(A, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
   }
   __syncthreads();
   SWARM_STAMP(7);
@@ -1713,15 +1813,19 @@ __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, 
   __syncthreads();
   // lanes reserved per cluster (cluster_build_env): class w, class rank
   for (int i = tid; i < N; i += T) {
-    if ((A[i] & 0xffff) != i) continue;  // roots only
-    const uint32_t b = (uint32_t)B[i];
+    const bool root = (A[i] & 0xffff) == i;  // roots only
+    const uint32_t b = root ? (uint32_t)B[i] : 0u;
     const int s = (int)(b & 0xffffu), pairs = (int)(b >> 16);
+    const int w = sc.one_pass ? max(s, min(min(pairs, 64), 2 * s)) : s;
+    // the two most frequent classes by one atomic per wave
+    const int r1 = wave_class_add(&classcnt[1], root && s <= 64 && w == 1);
+    const int r2 = wave_class_add(&classcnt[2], root && s <= 64 && w == 2);
+    if (!root) continue;
     if (s > 64) {  // wider than a wave: a big cluster, run by k_check's workgroup
       atomicAdd(&misc[4], s);
       B[i] = kBigMark;
     } else {
-      const int w = sc.one_pass ? max(s, min(min(pairs, 64), 2 * s)) : s;
-      B[i] = atomicAdd(&classcnt[w], 1) | (w << 24);
+      B[i] = (w == 1 ? r1 : (w == 2 ? r2 : atomicAdd(&classcnt[w], 1))) | (w << 24);
     }
   }
   __syncthreads();
@@ -1860,15 +1964,17 @@ __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, 
   }
 }
 
+template <bool kLocal>
 __global__ __launch_bounds__(1024) void k_cluster_build_packed(DevState st, Scratch sc) {
   extern __shared__ __align__(16) unsigned char smem[];
-  cluster_build_env_packed(st, sc, blockIdx.x, smem, sc.gnpairs[blockIdx.x]);
+  cluster_build_env_packed<kLocal>(st, sc, blockIdx.x, smem, sc.gnpairs[blockIdx.x]);
 }
 
-template <bool kBig>
+// kLocal: after the 2-D pair search (block-local forests + cross list)
+template <bool kBig, bool kLocal>
 __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc) {
   extern __shared__ __align__(16) unsigned char smem[];
-  cluster_build_env<kBig, !kBig>(st, sc, blockIdx.x, smem, sc.gnpairs[blockIdx.x]);
+  cluster_build_env<kBig, !kBig, kLocal>(st, sc, blockIdx.x, smem, sc.gnpairs[blockIdx.x]);
 }
 
 // Words of k_build_env's sort/search region (wave sums, cell ends, sorted

@@ -306,6 +306,7 @@ __global__ __launch_bounds__(1024) void k_build_sort3(DevState st, Scratch sc, i
   for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
   if (tid == 0) {
     sc.gnpairs[e] = 0;
+    sc.gnx[e] = 0;
     sc.fallback[e] = 0;  // the neighbour-list build sets it on overflow
   }
   __syncthreads();

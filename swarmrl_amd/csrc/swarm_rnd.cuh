@@ -101,17 +101,11 @@ __device__ __forceinline__ void rnd_forward(const RndNet<D>& net, const float* x
   rnd_square(net.w3t, net.b3, hb, out);
 }
 
+// The metric of observation a (both networks from the block's LDS copies).
 template <int D>
-__global__ __launch_bounds__(256) void k_rnd_distance(const float* __restrict__ x, int n,
-                                                      int d_in, RndPtrs tp, RndPtrs pp,
-                                                      int order, float* __restrict__ out) {
-  __shared__ RndNet<D> tnet, pnet;
-  __shared__ float hb[kRndWidth][256];  // the thread's hidden activations (column tid)
-  rnd_stage<D>(&tnet, tp.w, d_in);
-  rnd_stage<D>(&pnet, pp.w, d_in);
-  __syncthreads();
-  const int a = blockIdx.x * blockDim.x + threadIdx.x;
-  if (a >= n) return;  // no barrier below
+__device__ __forceinline__ float rnd_metric(const RndNet<D>& tnet, const RndNet<D>& pnet,
+                                            const float* __restrict__ x, int a, int d_in,
+                                            int order, float (*hb)[256]) {
   constexpr int W = kRndWidth;
   float xi[D];
 #pragma unroll
@@ -125,7 +119,82 @@ __global__ __launch_bounds__(256) void k_rnd_distance(const float* __restrict__ 
     const float dlt = fabsf(t[j] - p[j]);
     acc += order == 2 ? dlt * dlt : powf(dlt, (float)order);
   }
-  out[a] = order == 2 ? sqrtf(acc) : powf(acc, 1.0f / (float)order);
+  return order == 2 ? sqrtf(acc) : powf(acc, 1.0f / (float)order);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_rnd_distance(const float* __restrict__ x, int n,
+                                                      int d_in, RndPtrs tp, RndPtrs pp,
+                                                      int order, float* __restrict__ out) {
+  __shared__ RndNet<D> tnet, pnet;
+  __shared__ float hb[kRndWidth][256];  // the thread's hidden activations (column tid)
+  rnd_stage<D>(&tnet, tp.w, d_in);
+  rnd_stage<D>(&pnet, pp.w, d_in);
+  __syncthreads();
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= n) return;  // no barrier below
+  out[a] = rnd_metric<D>(tnet, pnet, x, a, d_in, order, hb);
+}
+
+// The per-env intrinsic reward (random_network_distillation.py:126-143 on
+// the device path: the mean metric of the env's latest observations,
+// clipped) added to the task reward, in two launches instead of the metric
+// kernel + torch's mean, clamp and add (five launches and a copy on C5's
+// critical path).  Pass 1 (grid E x kb, 256 threads): the metric of every
+// observation of env e = blockIdx.y and the block's fp64 partial sum.
+template <int D>
+__global__ __launch_bounds__(256) void k_rnd_env_partial(const float* __restrict__ x, int per_env,
+                                                         int d_in, RndPtrs tp, RndPtrs pp,
+                                                         int order, float* __restrict__ metric,
+                                                         double* __restrict__ partial) {
+  __shared__ RndNet<D> tnet, pnet;
+  __shared__ float hb[kRndWidth][256];
+  __shared__ double wsum[4];
+  rnd_stage<D>(&tnet, tp.w, d_in);
+  rnd_stage<D>(&pnet, pp.w, d_in);
+  __syncthreads();
+  const int e = blockIdx.y, k = blockIdx.x * blockDim.x + threadIdx.x;
+  double v = 0.0;
+  if (k < per_env) {
+    const int a = e * per_env + k;
+    const float m = rnd_metric<D>(tnet, pnet, x, a, d_in, order, hb);
+    metric[a] = m;
+    v = (double)m;
+  }
+  // fixed-order block sum: xor butterfly in the wave, then the four waves
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    partial[(size_t)e * gridDim.x + blockIdx.x] = ((wsum[0] + wsum[1]) + wsum[2]) + wsum[3];
+}
+
+// Pass 2 (one 1024-thread block per env): the env's partials summed in block
+// order (deterministic), mean -> fp32 -> clip, then
+// rewards[e][a] = base[e][a] + r_e (base null: rewards[e][a] = r_e).
+__global__ __launch_bounds__(1024) void k_rnd_env_finish(const double* __restrict__ partial,
+                                                         int kb, int per_env, int clip,
+                                                         float lo, float hi,
+                                                         const float* __restrict__ base,
+                                                         float* __restrict__ env_reward,
+                                                         float* __restrict__ rewards) {
+  __shared__ float r_e;
+  const int e = blockIdx.x;
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int k = 0; k < kb; ++k) s += partial[(size_t)e * kb + k];
+    float r = (float)(s / (double)per_env);
+    if (clip) r = fminf(fmaxf(r, lo), hi);
+    r_e = r;
+    env_reward[e] = r;
+  }
+  __syncthreads();
+  const float r = r_e;
+  for (int a = threadIdx.x; a < per_env; a += blockDim.x) {
+    const size_t g = (size_t)e * per_env + a;
+    rewards[g] = base ? base[g] + r : r;
+  }
 }
 
 }  // namespace swarm

@@ -474,3 +474,49 @@ def rnd_distance(points: torch.Tensor, target: torch.nn.Module, predictor: torch
         points.data_ptr(), n, d, 32, ctypes.cast(tp, ctypes.c_void_p),
         ctypes.cast(pp, ctypes.c_void_p), int(order), out.data_ptr(), ctypes.c_void_p(stream)))
     return out
+
+
+_RND_WS = {}
+
+
+def rnd_env_reward(points: torch.Tensor, n_envs: int, target: torch.nn.Module,
+                   predictor: torch.nn.Module, order: int, clip, base: torch.Tensor = None):
+    """The per-env RND reward added to the task reward in two launches
+    (swarm_rnd_env_reward): points [n_envs * per_env, d] fp32 device (env-
+    major); returns (metric [n], env_reward [n_envs, 1], rewards [n_envs,
+    per_env] = base + env_reward, or env_reward broadcast when base is None).
+    clip: (lo, hi) or None."""
+    points = points.contiguous()
+    n, d = points.shape
+    per_env = n // n_envs
+    dev = points.device
+    metric = torch.empty(n, dtype=torch.float32, device=dev)
+    env_r = torch.empty(n_envs, 1, dtype=torch.float32, device=dev)
+    rewards = torch.empty(n_envs, per_env, dtype=torch.float32, device=dev)
+    if base is not None:
+        base = base.to(torch.float32).reshape(n_envs, per_env).contiguous()
+    lib = _capi.lib()
+    nbytes = int(lib.swarm_rnd_env_workspace_bytes(n_envs, per_env))
+    key = (dev, nbytes)
+    ws = _RND_WS.get(key)
+    if ws is None:  # one workspace per size (kept: captured graphs read it)
+        ws = _RND_WS[key] = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=dev)
+
+    def ptrs(net):
+        lin = [m for m in net.modules() if isinstance(m, torch.nn.Linear)]
+        arr = (ctypes.c_void_p * 6)()
+        for k, m in enumerate(lin):
+            arr[2 * k] = m.weight.data_ptr()
+            arr[2 * k + 1] = m.bias.data_ptr()
+        return arr
+
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    tp, pp = ptrs(target), ptrs(predictor)
+    lo, hi = (float(clip[0]), float(clip[1])) if clip is not None else (0.0, 0.0)
+    _capi.check(lib.swarm_rnd_env_reward(
+        points.data_ptr(), n_envs, per_env, d, 32, ctypes.cast(tp, ctypes.c_void_p),
+        ctypes.cast(pp, ctypes.c_void_p), int(order), 1 if clip is not None else 0, lo, hi,
+        base.data_ptr() if base is not None else None, metric.data_ptr(), env_r.data_ptr(),
+        rewards.data_ptr(), ws.data_ptr(), ctypes.c_int64(ws.numel()), ctypes.c_void_p(stream)))
+    return metric, env_r, rewards
+

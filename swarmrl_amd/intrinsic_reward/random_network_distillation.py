@@ -49,12 +49,19 @@ class RNDReward(IntrinsicReward):
 
     def _features(self, episode_data, last_only: bool):
         """Every leading axis (time, and on the device path env and agent)
-        is a sample axis; the observation is the trailing prod(input_shape)."""
+        is a sample axis; the observation is the trailing prod(input_shape).
+        The latest observations of a device trajectory are read in place (no
+        stacking copy)."""
         feats = episode_data.features
-        if last_only:
-            feats = feats[-1:]
-        x = self._stack(feats)
+        if last_only and isinstance(feats[-1], torch.Tensor):
+            x = feats[-1]
+        else:
+            x = self._stack(feats[-1:] if last_only else feats)
         return x.reshape(-1, self.in_dim).to(torch.float32).to(self.device)
+
+    def _per_env(self, last) -> bool:
+        """Device-path observations [E, A, *obs]: one reward per env."""
+        return isinstance(last, torch.Tensor) and last.dim() == len(self.input_shape) + 2
 
     @staticmethod
     def fused_architecture_ok(net: torch.nn.Module, in_dim: int) -> bool:
@@ -126,10 +133,34 @@ class RNDReward(IntrinsicReward):
         broadcasts over the env's agents."""
         last = episode_data.features[-1]
         points = self._features(episode_data, last_only=True)
+        if self._per_env(last) and self._fused_ok(points):
+            from swarmrl_amd.engine import ops
+
+            self.metric_results, r, _ = ops.rnd_env_reward(
+                points, int(last.shape[0]), self.target_network, self.predictor_network,
+                self.distance_order, self.clip_rewards)
+            return r
         r = self.compute_distance(points)
-        per_env = isinstance(last, torch.Tensor) and last.dim() == len(self.input_shape) + 2
-        if per_env:
+        if self._per_env(last):
             r = self.metric_results.reshape(last.shape[0], -1).mean(dim=1, keepdim=True)
         if self.clip_rewards is not None:
             r = torch.clamp(r, *self.clip_rewards)
         return r
+
+    def add_to_reward(self, rewards, episode_data):
+        """rewards + compute_reward(episode_data) (the agent's task +
+        intrinsic sum); on the device path with the stock networks the metric,
+        the per-env mean, the clip and the sum are two launches
+        (swarm_rnd_env_reward) instead of five and a copy."""
+        last = episode_data.features[-1]
+        if (isinstance(rewards, torch.Tensor) and rewards.is_cuda and self._per_env(last)
+                and rewards.numel() == last.shape[0] * last.shape[1]):
+            points = self._features(episode_data, last_only=True)
+            if self._fused_ok(points):
+                from swarmrl_amd.engine import ops
+
+                self.metric_results, _, out = ops.rnd_env_reward(
+                    points, int(last.shape[0]), self.target_network, self.predictor_network,
+                    self.distance_order, self.clip_rewards, base=rewards)
+                return out.reshape(rewards.shape)
+        return rewards + self.compute_reward(episode_data)

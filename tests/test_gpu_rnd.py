@@ -57,11 +57,44 @@ def test_rnd_reward_device_path_uses_the_fused_metric(monkeypatch):
     calls = []
     from swarmrl_amd.engine import ops
 
-    orig = ops.rnd_distance
-    monkeypatch.setattr(ops, "rnd_distance", lambda *a: calls.append(1) or orig(*a))
+    orig = ops.rnd_env_reward
+    monkeypatch.setattr(ops, "rnd_env_reward", lambda *a, **k: calls.append(1) or orig(*a, **k))
     fused = rnd.compute_reward(traj)
     assert calls, "the fused metric was not used"
     monkeypatch.setattr(RNDReward, "_fused_ok", lambda self, p: False)
     ref = rnd.compute_reward(traj)
     assert fused.shape == (4, 1)
     torch.testing.assert_close(fused, ref, rtol=2e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("E,A,clip", [(1, 16384, (-5.0, 5.0)), (3, 1000, None), (2, 77, (0.0, 0.1))])
+def test_rnd_env_reward_added_to_task_reward(E, A, clip):
+    """The agent's task + intrinsic sum on the device path (RNDReward.
+    add_to_reward -> swarm_rnd_env_reward: metric, per-env fp64 mean, clip
+    and the sum in two launches) against the torch composition of the same
+    steps: torch metric, per-env mean, clamp, broadcast add (rtol 2e-5);
+    ragged env sizes (not a multiple of the 256-observation blocks)."""
+    from swarmrl_amd.intrinsic_reward import RNDConfig, RNDReward
+    from swarmrl_amd.intrinsic_reward.rnd_configs import order_n_difference
+    from swarmrl_amd.utils.colloid_utils import TrajectoryInformation
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(E * 100 + A)
+    rnd = RNDReward(RNDConfig(input_shape=(1,), device=dev, clip_rewards=clip))
+    traj = TrajectoryInformation(particle_type=0)
+    traj.features.append(torch.randn(E, A, 1, device=dev) * 2)
+    base = torch.rand(E, A, device=dev)
+    got = rnd.add_to_reward(base, traj)
+    assert got.shape == (E, A)
+    x = traj.features[-1].reshape(-1, 1)
+    with torch.no_grad():
+        m = order_n_difference(rnd.target_network(x), rnd.predictor_network(x), 2)
+    torch.testing.assert_close(rnd.metric_results, m, rtol=2e-5, atol=2e-6)
+    r = m.double().reshape(E, A).mean(dim=1, keepdim=True).float()
+    if clip is not None:
+        r = torch.clamp(r, *clip)
+    torch.testing.assert_close(got, base + r, rtol=2e-5, atol=2e-6)
+    # run-to-run: the fixed-order reduction gives the same bits
+    again = rnd.add_to_reward(base, traj)
+    assert torch.equal(got, again)
+
