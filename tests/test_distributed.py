@@ -2,10 +2,19 @@
 
 import os
 
+import socket
+
 import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+
+def _free_port() -> int:
+    """A port nothing listens on (the OS picks it), for one test's rendezvous."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
 
 
 def _worker(rank, world, port, q):
@@ -41,7 +50,7 @@ def _worker(rank, world, port, q):
 def test_gather_trajectory_two_ranks_gloo():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + (os.getpid() % 1000)
+    port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
@@ -183,7 +192,7 @@ def test_episode_parallel_trainer_keeps_replicas_identical_gloo():
     the rank-local update (no gather) would diverge."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 30600 + (os.getpid() % 1000)
+    port = _free_port()
     procs = [ctx.Process(target=_replica_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
@@ -235,7 +244,7 @@ def test_gather_uneven_env_blocks_gloo():
     kill switch of any rank."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 31700 + (os.getpid() % 1000)
+    port = _free_port()
     procs = [ctx.Process(target=_uneven_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
