@@ -1324,7 +1324,9 @@ int launch_run(swarm_engine* e, int n_steps) {
     // dynamic LDS beyond half a CU's keeps one block (run_wpb run waves) per CU
     const int R = e->run_wpb;
     const dim3 grid((unsigned)(e->noise_blocks + (waves + R - 1) / R));
-    const size_t lds = 96 * 1024;
+    // at least 96 KB (one block per CU), and the precomputed rotation of
+    // one or two run waves (swarm::precompute_swim)
+    const size_t lds = std::max<size_t>(96 * 1024, R <= 2 ? swarm::wide_dir_lds_bytes(R) : 0);
 #define SWARM_WIDE(MULTI, WALLS)                                                             \
   hipLaunchKernelGGL((swarm::k_cluster_run_wide<MULTI, WALLS>), grid, dim3(1024), lds, e->stream, \
                      e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise,      \

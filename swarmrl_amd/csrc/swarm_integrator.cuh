@@ -621,6 +621,46 @@ __device__ __forceinline__ void bd_translate(const PConst& c, PState& p, int64_t
   }
 }
 
+// bd_translate with the swim force vector given (swx, swy = fs * cos,
+// fs * sin of the orientation, precompute_swim): the same operation
+// sequence, so the same bits.
+__device__ __forceinline__ void bd_translate_sw(const PConst& c, PState& p, int64_t ax, int64_t ay,
+                                                float swx, float swy, float tz, float fex,
+                                                float fey, uint32_t k0, uint32_t k1, uint32_t id,
+                                                uint64_t step, bool last, float* vx, float* vy,
+                                                float* w, const float* g) {
+  float fx, fy;
+  i64x2_to_f32(ax, ay, &fx, &fy);
+  fx = fx * 5.9604644775390625e-08f;
+  fy = fy * 5.9604644775390625e-08f;
+  fx = fx + fex;
+  fy = fy + fey;
+  fx = fx + swx;
+  fy = fy + swy;
+  float dx = fx * c.mob_dt;
+  float dy = fy * c.mob_dt;
+  if (c.noisy) {
+    dx = dx + c.sig_t * g[0];
+    dy = dy + c.sig_t * g[1];
+  }
+  advance(p.qx, p.ix, f2i32(dx * c.inv_sx0));
+  advance(p.qy, p.iy, f2i32(dy * c.inv_sx1));
+  if (last) {
+    float v0 = fx * c.inv_gt, v1 = fy * c.inv_gt;
+    float om = tz * c.inv_gr;
+    if (c.noisy) {
+      float gv[3];
+      normals3(k0, k1, id, step, 1u, gv);
+      v0 = v0 + c.sig_v * gv[0];
+      v1 = v1 + c.sig_v * gv[1];
+      om = om + c.sig_w * gv[2];
+    }
+    *vx = v0;
+    *vy = v1;
+    *w = om;
+  }
+}
+
 // One steepest-descent step of one particle (espresso.py:1163-1168).
 __device__ __forceinline__ bool sd_step(const PConst& c, PState& p, int64_t ax, int64_t ay,
                                         float fs, float tz, float fex, float fey, float g,
@@ -2256,13 +2296,20 @@ __global__ __launch_bounds__(256) void k_noise(const Derived* __restrict__ d, De
 // its 64 slots.  kTable: the normals come from this window's noise table
 // (prefetched one sub-step ahead), else they are drawn here.
 // kMulti = false: one species, so the pair constants are wave-uniform scalars.
-template <bool kMulti, bool kTable, bool kWalls>
+// kDir (latency-bound launches, k_cluster_run_wide): the swim vector of
+// every sub-step, fs * (cos, sin) of the orientation, and the final angle
+// were computed ahead by the block's idle waves (precompute_swim) into LDS
+// (dtab[s * 64 + lane], angfin[lane]): the rotation is position-independent,
+// so the run wave's dependency chain loses the angle update and sin/cos.
+template <bool kMulti, bool kTable, bool kWalls, bool kDir = false>
 __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const DevState& st,
                                          const Scratch& sc, int n_envs, int n_steps,
                                          uint64_t step0, const float* __restrict__ table,
                                          int gw, int lane, uint2* lpos_w,
                                          unsigned long long* lacc_x, unsigned long long* lacc_y,
-                                         const PairTables& pt, int par) {
+                                         const PairTables& pt, int par,
+                                         const float2* __restrict__ dtab = nullptr,
+                                         const uint32_t* __restrict__ angfin = nullptr) {
   const int e = gw / sc.wmax;
   const int w = gw - e * sc.wmax;
   if (e >= n_envs) return;
@@ -2342,7 +2389,11 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
   // the pass count (0, 1 or up to 4) and the last sub-step (velocities) are
   // compile-time variants, and idle lanes compute along (never stored).
   float dir[2];
-  sincos_turn(an0, &dir[0], &dir[1]);
+  float2 swn = make_float2(0.0f, 0.0f);  // kDir: the next sub-step's swim vector
+  if (kDir)
+    swn = dtab[lane];
+  else
+    sincos_turn(an0, &dir[0], &dir[1]);
   auto substep = [&](const int s, auto last_t, auto pass_t) __attribute__((always_inline)) {
     constexpr bool kLast = decltype(last_t)::value;
     constexpr int kPass = decltype(pass_t)::value;  // 0, 1, or 4: up to npass
@@ -2350,6 +2401,8 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     if (stamp) t0s = t1s = __builtin_amdgcn_s_memtime();
 #endif
     float gt[3] = {gn[0], gn[1], gn[2]};
+    const float2 sw = swn;
+    if (kDir && !kLast) swn = dtab[(s + 1) * 64 + lane];
 #ifdef SWARM_ABL_NOTABLE  // timing ablation only (tools/_variants): no table loads
     if (false) {
 #else
@@ -2393,16 +2446,16 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     // rotation (bd_step's sequence) and the next director, between the
     // force-sum atomics and their read-back
     __builtin_amdgcn_sched_barrier(0);
-    float dth = tz * pc.rot_dt;
-    if (pc.noisy) dth = dth + pc.sig_r * gt[2];
-    const uint32_t an_next = p.an + (uint32_t)f2i32(dth * kAngInvScale);
-    float dnext[2];
-#ifdef SWARM_ABL_NOSINCOS  // timing ablation only: the director stays fixed
-    dnext[0] = dir[0];
-    dnext[1] = dir[1];
-#else
-    if (!kLast) sincos_turn(an_next, &dnext[0], &dnext[1]);
+    uint32_t an_next = p.an;
+    float dnext[2] = {dir[0], dir[1]};
+    if (!kDir) {
+      float dth = tz * pc.rot_dt;
+      if (pc.noisy) dth = dth + pc.sig_r * gt[2];
+      an_next = p.an + (uint32_t)f2i32(dth * kAngInvScale);
+#ifndef SWARM_ABL_NOSINCOS  // timing ablation only: the director stays fixed
+      if (!kLast) sincos_turn(an_next, &dnext[0], &dnext[1]);
 #endif
+    }
     __builtin_amdgcn_sched_barrier(0);
     __asm__ volatile("" ::: "memory");  // keep the read-back after the director
     if (kPass > 0) {
@@ -2430,15 +2483,19 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
       wall_forces<2>(d, si, (float)p.qx * sx0, (float)p.qy * sx1, 0.0f, ax, ay, az,
                      st.wall_viol);
     }
-    bd_translate(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s, kLast,
-                 &vx, &vy, &om, gt, dir[0], dir[1]);
+    if (kDir)
+      bd_translate_sw(pc, p, ax, ay, sw.x, sw.y, tz, fex, fey, k0, k1, (uint32_t)i,
+                      step0 + (uint64_t)s, kLast, &vx, &vy, &om, gt);
+    else
+      bd_translate(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
+                   kLast, &vx, &vy, &om, gt, dir[0], dir[1]);
     const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
     const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
     // non-negative floats order like their bit patterns: one v_max_u32
     // (fmaxf adds a canonicalising max)
     dmax2 = __uint_as_float(max(__float_as_uint(dmax2), __float_as_uint(ddx * ddx + ddy * ddy)));
     p.an = an_next;
-    if (!kLast) {
+    if (!kDir && !kLast) {
       dir[0] = dnext[0];
       dir[1] = dnext[1];
     }
@@ -2499,6 +2556,7 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     ws[3] = (uint64_t)np;
   }
 #endif
+  if (kDir) p.an = angfin[lane];  // the rotation was integrated ahead
   if (active) {
     st.q[gi] = p.qx;
     st.q[M + gi] = p.qy;
@@ -2601,12 +2659,90 @@ __global__ __launch_bounds__(256, SWARM_RUN_MINB) void k_cluster_run(const Deriv
 // run with waves [0, run_wpb) only: one run wave per CU at E = 1 (its
 // scattered noise-table gathers then have the CU's texture path to themselves),
 // up to one per SIMD for more envs.
+// The rotation of the block's R run waves (first global wave gw0),
+// integrated ahead by the whole block (1024 threads: 16 / R chunks of the
+// window's sub-steps x 64 R particles) while the run waves would otherwise
+// compute it serially, sub-step by sub-step: per particle the angle
+// increments of bd_step's sequence (dth = tz rot_dt + sig_r g2, rounded to
+// turn units; with reuse_forces sub-step 0 turns with the previous run's
+// torque), an exclusive prefix over the chunks (integer adds: exact in any
+// order), then the swim vector of every sub-step, fs * sincos(orientation)
+// -- sub-step 0 swims along the orientation (and with the force) of the last
+// force calculation -- into dtab[(r * kMaxWindow + s) * 64 + lane] and the
+// final angle into angfin[r * 64 + lane].  Same values as run_wave computes
+// inline.  Block-uniform: every thread of the block calls it.
+template <bool kMulti, int R>
+__device__ __forceinline__ void precompute_swim(const Derived* __restrict__ d, const DevState& st,
+                                                const Scratch& sc, int n_envs, int gw0,
+                                                int n_steps, const float* __restrict__ table,
+                                                int par, float2* dtab, uint32_t* angfin,
+                                                uint32_t* partial) {
+  constexpr int P = 64 * R, C = 1024 / P;             // particles, chunks
+  constexpr int kChunk = (kMaxWindow + C - 1) / C;    // sub-steps per chunk at most
+  const int tid = threadIdx.x, pidx = tid % P, c = tid / P;
+  const int rw = pidx >> 6, l = pidx & 63;
+  const int gw = gw0 + rw;
+  const int e = gw / sc.wmax, w = gw - e * sc.wmax;
+  const int N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int i = e < n_envs ? sc.perm[(size_t)e * sc.S + w * 64 + l] : -1;
+  const size_t gi = i >= 0 ? base + i : 0;
+  const PConst pc = load_pconst(d, kMulti ? (i >= 0 ? (int)st.species[i] : 0) : 0);
+  const PrevSlot prv = prev_slot(st, par);
+  const float tz1 = st.torque_z[gi], fs1 = st.f_swim[gi];
+  const float tz0 = st.reuse ? prv.tz[gi] : tz1, fs0 = st.reuse ? prv.f[gi] : fs1;
+  const uint32_t an_start = st.ang[gi];
+  const uint32_t an0 = st.reuse ? prv.ang[gi] : an_start;
+  const int K = (n_steps + C - 1) / C;
+  const int s0 = c * K;
+  const float* tcol = table + noise_index(M, gi, 0, 0);
+  const size_t tstep = noise_step_stride(M), ts = noise_comp_stride(M);
+  float g2[kChunk];
+#pragma unroll
+  for (int k = 0; k < kChunk; ++k)
+    g2[k] = k < K && s0 + k < n_steps ? tcol[(s0 + k) * tstep + 2 * ts] : 0.0f;
+  uint32_t inc[kChunk];
+  uint32_t sum = 0u;
+#pragma unroll
+  for (int k = 0; k < kChunk; ++k) {
+    const int s = s0 + k;
+    float dth = (s == 0 ? tz0 : tz1) * pc.rot_dt;
+    if (pc.noisy) dth = dth + pc.sig_r * g2[k];
+    inc[k] = k < K && s < n_steps ? (uint32_t)f2i32(dth * kAngInvScale) : 0u;
+    sum += inc[k];
+  }
+  partial[c * P + pidx] = sum;
+  __syncthreads();
+  uint32_t an = an_start;
+  for (int k = 0; k < c; ++k) an += partial[k * P + pidx];
+  float2* dt = dtab + (size_t)rw * kMaxWindow * 64;
+#pragma unroll
+  for (int k = 0; k < kChunk; ++k) {
+    const int s = s0 + k;
+    if (k < K && s < n_steps) {
+      float sn, cs;
+      sincos_turn(s == 0 ? an0 : an, &sn, &cs);
+      const float fs = s == 0 ? fs0 : fs1;
+      dt[s * 64 + l] = make_float2(fs * cs, fs * sn);
+      an += inc[k];
+      if (s == n_steps - 1) angfin[rw * 64 + l] = an;
+    }
+  }
+  __syncthreads();
+}
+
+// Dynamic LDS of k_cluster_run_wide's precomputed rotation (R run waves).
+__host__ __device__ constexpr size_t wide_dir_lds_bytes(int R) {
+  return (size_t)R * kMaxWindow * 64 * sizeof(float2) + (size_t)R * 64 * 4 + 1024 * 4;
+}
+
 template <bool kMulti, bool kWalls>
 __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __restrict__ d,
                                                            DevState st, Scratch sc, int n_envs,
                                                            int n_steps, uint64_t* __restrict__ ctl,
                                                            float* __restrict__ tables,
                                                            int n_noise_blocks, int run_wpb) {
+  extern __shared__ __align__(16) unsigned char wide_lds[];
   __shared__ PairTables pt;
   __shared__ uint2 lpos[4][64];
   __shared__ unsigned long long lacc[4][2][64];
@@ -2633,12 +2769,32 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
     return;
   }
   const int lane = tid & 63, wv = tid >> 6;
-  if (wv >= run_wpb) return;
-  const int gw = (b - n_noise_blocks) * run_wpb + wv;
+  const int gw0 = (b - n_noise_blocks) * run_wpb;
   const bool table_ok = ctl[kCtlTStep + par] == step0 && (uint64_t)n_steps <= ctl[kCtlTLen + par];
-  run_wave_dispatch<kMulti, kWalls>(d, st, sc, n_envs, n_steps, step0,
-                                    table_ok ? tables + par * noise_table_words(M) : nullptr, gw,
-                                    lane, lpos[wv], lacc[wv][0], lacc[wv][1], pt, par);
+  const float* table = table_ok ? tables + par * noise_table_words(M) : nullptr;
+  // one or two run waves per block (a latency-bound launch; the host sized
+  // the dynamic LDS, wide_dir_lds_bytes) and this window's normals in the
+  // table: the other waves integrate the run waves' rotation ahead
+  if ((run_wpb == 1 || run_wpb == 2) && table_ok && blockDim.x == 1024 && tables != nullptr) {
+    float2* dtab = reinterpret_cast<float2*>(wide_lds);  // [R][kMaxWindow][64]
+    uint32_t* angfin = reinterpret_cast<uint32_t*>(dtab + (size_t)run_wpb * kMaxWindow * 64);
+    uint32_t* partial = angfin + run_wpb * 64;           // [1024]
+    if (run_wpb == 1)
+      precompute_swim<kMulti, 1>(d, st, sc, n_envs, gw0, n_steps, table, par, dtab, angfin,
+                                 partial);
+    else
+      precompute_swim<kMulti, 2>(d, st, sc, n_envs, gw0, n_steps, table, par, dtab, angfin,
+                                 partial);
+    if (wv >= run_wpb) return;
+    run_wave<kMulti, true, kWalls, true>(d, st, sc, n_envs, n_steps, step0, table, gw0 + wv,
+                                         lane, lpos[wv], lacc[wv][0], lacc[wv][1], pt, par,
+                                         dtab + (size_t)wv * kMaxWindow * 64, angfin + wv * 64);
+    return;
+  }
+  if (wv >= run_wpb) return;
+  const int gw = gw0 + wv;
+  run_wave_dispatch<kMulti, kWalls>(d, st, sc, n_envs, n_steps, step0, table, gw, lane, lpos[wv],
+                                    lacc[wv][0], lacc[wv][1], pt, par);
 }
 
 // The env's big clusters (wider than a wave) for the window, by k_check's
