@@ -1720,10 +1720,11 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   // build grid; otherwise every window runs on the global path
   e->big_build = build_is_big(n_particles);
   e->sc.pair_cap = build_pair_cap(n_particles, e->big_build);
-  // non-periodic boxes run windowed in 2-D (edge cells and unwrapped
-  // distances in the build and the exact check; a listed pair's folded
-  // difference is its unwrapped one), on the global path in 3-D;
-  // SWARMRL_AMD_CLUSTER_PATH=0 forces the global path (A/B and parity)
+  // non-periodic boxes run windowed in 2-D and 3-D (edge cells and
+  // unwrapped distances in the build and the exact check; a listed pair's
+  // folded difference is its unwrapped one), the neighbour-list window is
+  // periodic-only; SWARMRL_AMD_CLUSTER_PATH=0 forces the global path (A/B
+  // and parity)
   e->sc.periodic = params->periodic ? 1 : 0;
   e->sc.multi_species = params->n_species > 1 ? 1 : 0;
   // the 2-D build sort stages its scatter in LDS: the sorted rows of up to
@@ -1740,7 +1741,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     if (const char* oss = std::getenv("SWARMRL_AMD_SORT_STAGED"))
       if (oss[0] == '0') e->sc.sort_stage_k = 0;
   }
-  e->cluster_path = (params->periodic || !three_d) && e->sc.pair_cap >= n_particles &&
+  e->cluster_path = e->sc.pair_cap >= n_particles &&
                     n_particles < 65536 &&
                     swarm::build_lds_words_big(n_particles) * 4 <= kMaxLds &&
                     (size_t)(16 + (1 << lcb) + 1) * 4 <= kMaxLds &&

@@ -293,6 +293,17 @@ __global__ __launch_bounds__(1024) void k_build_sort3(DevState st, Scratch sc, i
   const int ncell = 1 << (lx + ly + lz);
   int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
   int32_t* cnt = wave_sums + 16;
+  // cell of particle i: folded positions in a periodic box; in a
+  // non-periodic one a particle outside the box takes the edge cell on its
+  // side (cell_coord, as the 2-D build sort and the global path)
+  const bool per = sc.periodic != 0;
+  auto cell_of = [&](int i, uint32_t qx, uint32_t qy, uint32_t qz) {
+    if (per) return cell_index3(qx, qy, qz, lx, ly, lz);
+    return (((cell_coord(qz, st.img[2 * M + base + i], lz, false) << ly) |
+             cell_coord(qy, st.img[M + base + i], ly, false))
+            << lx) |
+           cell_coord(qx, st.img[base + i], lx, false);
+  };
   uint32_t cq[CH][3];
   int32_t cid[CH];
 #pragma unroll
@@ -312,11 +323,9 @@ __global__ __launch_bounds__(1024) void k_build_sort3(DevState st, Scratch sc, i
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < CH; ++k)
-    if (cid[k] >= 0) atomicAdd(&cnt[cell_index3(cq[k][0], cq[k][1], cq[k][2], lx, ly, lz)], 1);
+    if (cid[k] >= 0) atomicAdd(&cnt[cell_of(tid + k * T, cq[k][0], cq[k][1], cq[k][2])], 1);
   for (int i = tid + CH * T; i < N; i += T)
-    atomicAdd(&cnt[cell_index3(st.q[base + i], st.q[M + base + i], st.q[2 * M + base + i], lx, ly,
-                               lz)],
-              1);
+    atomicAdd(&cnt[cell_of(i, st.q[base + i], st.q[M + base + i], st.q[2 * M + base + i])], 1);
   __syncthreads();
   block_exclusive_scan(cnt, ncell, wave_sums);
   __syncthreads();
@@ -326,15 +335,14 @@ __global__ __launch_bounds__(1024) void k_build_sort3(DevState st, Scratch sc, i
 #pragma unroll
   for (int k = 0; k < CH; ++k) {
     if (cid[k] < 0) continue;
-    const size_t pos =
-        base + atomicAdd(&cnt[cell_index3(cq[k][0], cq[k][1], cq[k][2], lx, ly, lz)], 1);
+    const size_t pos = base + atomicAdd(&cnt[cell_of(tid + k * T, cq[k][0], cq[k][1], cq[k][2])], 1);
 #pragma unroll
     for (int a = 0; a < 3; ++a) sc.bsq[a * M + pos] = cq[k][a];
     sc.bsid[pos] = cid[k];
   }
   for (int i = tid + CH * T; i < N; i += T) {
     const uint32_t qx = st.q[base + i], qy = st.q[M + base + i], qz = st.q[2 * M + base + i];
-    const size_t pos = base + atomicAdd(&cnt[cell_index3(qx, qy, qz, lx, ly, lz)], 1);
+    const size_t pos = base + atomicAdd(&cnt[cell_of(i, qx, qy, qz)], 1);
     sc.bsq[pos] = qx;
     sc.bsq[M + pos] = qy;
     sc.bsq[2 * M + pos] = qz;
@@ -364,26 +372,40 @@ __global__ __launch_bounds__(256) void k_build_pairs3(const Derived* __restrict_
   const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
   const int loz = ncz >= 3 ? -1 : 0, hiz = ncz >= 3 ? 1 : ncz - 1;
   const float sx0 = d->sx[0], sx1 = d->sx[1], sx2 = d->sx[2];
+  // non-periodic box (d->periodic == 0): edge cells, no wrap of the stencil,
+  // unwrapped pair distances (pair_disp) -- a pair near across the box edge
+  // only in the folded sense must not be listed
+  const bool per = d->periodic != 0;
   int pk = 0, i = 0;
   uint32_t qx = 0, qy = 0, qz = 0;
+  int32_t ix = 0, iy = 0, iz = 0;
   if (valid) {
     pk = sc.bsid[base + ps];
     i = pk & 0xffffff;
     qx = sc.bsq[base + ps];
     qy = sc.bsq[M + base + ps];
     qz = sc.bsq[2 * M + base + ps];
+    if (!per) {
+      ix = st.img[base + i];
+      iy = st.img[M + base + i];
+      iz = st.img[2 * M + base + i];
+    }
   }
-  const int c0 = cell_index3(qx, qy, qz, lx, ly, lz);
+  const int c0 = per ? cell_index3(qx, qy, qz, lx, ly, lz)
+                     : (((cell_coord(qz, iz, lz, false) << ly) | cell_coord(qy, iy, ly, false))
+                        << lx) |
+                           cell_coord(qx, ix, lx, false);
   const int cx = c0 & (ncx - 1), cy = (c0 >> lx) & (ncy - 1), cz = c0 >> (lx + ly);
   const int xa = ncx >= 3 ? max(cx - 1, 0) : 0;
   const int xb = ncx >= 3 ? min(cx + 1, ncx - 1) : ncx - 1;
-  const int xw = ncx >= 3 ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
+  const int xw = ncx >= 3 && per ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
   int rb[kR], re[kR];
 #pragma unroll
   for (int r = 0; r < kR; ++r) {
     const int row = r >> 1, part = r & 1;
     const int oy = loy + row % 3, oz = loz + row / 3;
-    const bool use = valid && oy <= hiy && oz <= hiz && (part == 0 || xw >= 0);
+    const bool use = valid && oy <= hiy && oz <= hiz && (part == 0 || xw >= 0) &&
+                     (per || (cy + oy >= 0 && cy + oy < ncy && cz + oz >= 0 && cz + oz < ncz));
     const int rowc = ((((cz + oz + ncz) & (ncz - 1)) << ly) | ((cy + oy + ncy) & (ncy - 1))) << lx;
     const int c_lo = rowc | (part == 0 ? xa : xw), c_hi = rowc | (part == 0 ? xb : xw);
     rb[r] = use ? cs[c_lo] : 0;
@@ -395,10 +417,23 @@ __global__ __launch_bounds__(256) void k_build_pairs3(const Derived* __restrict_
   uint32_t keep[kKeep];
 #pragma unroll
   for (int v = 0; v < kKeep; ++v) keep[v] = 0u;
+  // separation of sorted entry jj (particle j) from this particle: minimum
+  // image, or the unwrapped difference in a non-periodic box
+  auto sep = [&](uint32_t xj, uint32_t yj, uint32_t zj, int j, float* rx, float* ry, float* rz) {
+    if (per) {
+      *rx = (float)(int32_t)(xj - qx) * sx0;
+      *ry = (float)(int32_t)(yj - qy) * sx1;
+      *rz = (float)(int32_t)(zj - qz) * sx2;
+    } else {
+      *rx = pair_disp(xj, st.img[base + j], qx, ix, sx0, false);
+      *ry = pair_disp(yj, st.img[M + base + j], qy, iy, sx1, false);
+      *rz = pair_disp(zj, st.img[2 * M + base + j], qz, iz, sx2, false);
+    }
+  };
   auto near = [&](int jj, int packed) {
-    const float rx = (float)(int32_t)(sc.bsq[base + jj] - qx) * sx0;
-    const float ry = (float)(int32_t)(sc.bsq[M + base + jj] - qy) * sx1;
-    const float rz = (float)(int32_t)(sc.bsq[2 * M + base + jj] - qz) * sx2;
+    float rx, ry, rz;
+    sep(sc.bsq[base + jj], sc.bsq[M + base + jj], sc.bsq[2 * M + base + jj], packed & 0xffffff,
+        &rx, &ry, &rz);
     float r2 = rx * rx + ry * ry;
     r2 = r2 + rz * rz;
     return i < (packed & 0xffffff) && r2 < nb2_row[packed >> 24];
@@ -421,9 +456,8 @@ __global__ __launch_bounds__(256) void k_build_pairs3(const Derived* __restrict_
       for (int u = 0; u < 4; ++u) {
         if (pk4[u] < 0) continue;
         const int j = pk4[u] & 0xffffff;
-        const float rx = (float)(int32_t)(x4[u] - qx) * sx0;
-        const float ry = (float)(int32_t)(y4[u] - qy) * sx1;
-        const float rz = (float)(int32_t)(z4[u] - qz) * sx2;
+        float rx, ry, rz;
+        sep(x4[u], y4[u], z4[u], j, &rx, &ry, &rz);
         float r2 = rx * rx + ry * ry;
         r2 = r2 + rz * rz;
         if (i < j && r2 < nb2_row[pk4[u] >> 24]) {
@@ -784,14 +818,20 @@ __global__ __launch_bounds__(1024) void k_check3(const Derived* __restrict__ d, 
       const bool multi = d->n_species > 1;  // else every pair's cutoff is cut2[0]
       const float rc0 = sqrtf(pt.cut2[0]);
       const float sx0 = d->sx[0], sx1 = d->sx[1], sx2 = d->sx[2];
+      const bool per = d->periodic != 0;
       const long total = (long)nm * N;
       for (long t = tid; t < total; t += T) {
         const int m = movers[t / N];
         const int j = (int)(t % N);
         if (j == m) continue;
-        const float rx = (float)(int32_t)(sc.bq[base + j] - sc.bq[base + m]) * sx0;
-        const float ry = (float)(int32_t)(sc.bq[M + base + j] - sc.bq[M + base + m]) * sx1;
-        const float rz = (float)(int32_t)(sc.bq[2 * M + base + j] - sc.bq[2 * M + base + m]) * sx2;
+        // window-start separation: minimum image, or (non-periodic box) the
+        // unwrapped difference -- the folded one would only be stricter
+        const float rx = pair_disp(sc.bq[base + j], sc.bimg[base + j], sc.bq[base + m],
+                                   sc.bimg[base + m], sx0, per);
+        const float ry = pair_disp(sc.bq[M + base + j], sc.bimg[M + base + j], sc.bq[M + base + m],
+                                   sc.bimg[M + base + m], sx1, per);
+        const float rz = pair_disp(sc.bq[2 * M + base + j], sc.bimg[2 * M + base + j],
+                                   sc.bq[2 * M + base + m], sc.bimg[2 * M + base + m], sx2, per);
         // the pair's own WCA cutoff r_m + r_j (not the largest one: a dense
         // mixture would fail the test for pairs that cannot interact)
         const float rc = multi ? sqrtf(pt.cut2[st.species[m] * kMaxSpecies + st.species[j]]) : rc0;

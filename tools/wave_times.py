@@ -16,13 +16,16 @@ import bench  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("envs", nargs="?", type=int, default=1)
 ap.add_argument("slices", nargs="?", type=int, default=30)
+ap.add_argument("--c5", action="store_true", help="the C5 workload (16384 colloids, field + RND)")
 a = ap.parse_args()
-ns = bench.argparse.Namespace(colloids=4096, envs_per_gpu=a.envs)
+n = 16384 if a.c5 else 4096
+ns = bench.argparse.Namespace(colloids=n, envs_per_gpu=a.envs)
 torch.cuda.set_device(0)
-eng, ff, agent = bench.build_workload(ns, 42, torch.device("cuda", 0))
+eng, ff, agent = (bench.build_c5_workload if a.c5 else bench.build_workload)(
+    ns, 42, torch.device("cuda", 0))
 eng.integrate(1, ff)
 nat = eng._native
-wmax_words = 4 * a.envs * ((4 * 4096 + 4224) // 64)
+wmax_words = 4 * a.envs * ((4 * n + 4224) // 64)
 for rep in range(4):
     eng.integrate(a.slices // 4, ff)
     torch.cuda.synchronize()
