@@ -1050,6 +1050,7 @@ struct swarm_engine {
   // per-window Verlet list instead of per-wave clusters (swarm_integrator3.cuh)
   bool nlist_path = false;
   bool big_build = false;  // k_cluster_build<true>: cluster arrays in global memory
+  bool chip_sort = false;  // 2-D envs above 4096 colloids: the three-launch chip-wide sort
   VisionSorted vs{};
   // latency-bound windows read their normals from a table (k_noise)
   bool noise_table = false;
@@ -1105,6 +1106,8 @@ namespace {
 
 template <typename T>
 int dev_alloc(swarm_engine* e, T** p, size_t count) {
+  if (e->n_allocs >= (int)(sizeof(e->allocs) / sizeof(e->allocs[0])))
+    return fail(SWARM_ECAPACITY, "engine allocation table full");
   void* v = nullptr;
   HIP_TRY(hipMalloc(&v, std::max<size_t>(count, 1) * sizeof(T)));
   HIP_TRY(hipMemsetAsync(v, 0, std::max<size_t>(count, 1) * sizeof(T), e->stream));
@@ -1168,6 +1171,7 @@ void set_lds_attributes() {
                        reinterpret_cast<const void*>(&swarm::k_cluster_build_packed<false>),
                        reinterpret_cast<const void*>(&swarm::k_cluster_build_packed<true>),
                        reinterpret_cast<const void*>(&swarm::k_build_sort<4>),
+                       reinterpret_cast<const void*>(&swarm::k_sort_scan),
                        reinterpret_cast<const void*>(&swarm::k_build_sort<16>),
                        reinterpret_cast<const void*>(&swarm::k_build_env),
                        reinterpret_cast<const void*>(&swarm::k_check),
@@ -1240,12 +1244,24 @@ int launch_build(swarm_engine* e, hipStream_t stream) {
     }
     hipLaunchKernelGGL(swarm::k_build_pairs3, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
                        dim3(256), 0, stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb, e->lzb);
-  } else if (e->n > 4096)
+  } else if (e->chip_sort) {
+    const dim3 pgrid((unsigned)((e->n + 255) / 256), (unsigned)e->n_envs);
+    hipLaunchKernelGGL(swarm::k_sort_count, pgrid, dim3(256), 0, stream, e->st, e->sc, e->lxb,
+                       e->lyb);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(swarm::k_sort_scan, dim3(e->n_envs), dim3(1024),
+                       (size_t)(16 + (1 << (e->lxb + e->lyb)) + 1) * 4, stream, e->sc, e->lxb,
+                       e->lyb);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(swarm::k_sort_scatter, pgrid, dim3(256), 0, stream, e->st, e->sc, e->lxb,
+                       e->lyb);
+  } else if (e->n > 4096) {
     hipLaunchKernelGGL(swarm::k_build_sort<16>, dim3(e->n_envs), dim3(1024), sort_lds_bytes(e),
                        stream, e->st, e->sc, e->lxb, e->lyb);
-  else
+  } else {
     hipLaunchKernelGGL(swarm::k_build_sort<4>, dim3(e->n_envs), dim3(1024), sort_lds_bytes(e),
                        stream, e->st, e->sc, e->lxb, e->lyb);
+  }
   HIP_TRY(hipGetLastError());
   if (e->params.n_dims != 3 && e->nlist_path) {  // Verlet lists, no clusters
     hipLaunchKernelGGL(swarm::k_build_nlist2, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
@@ -1850,6 +1866,15 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->sc.xpairs, (size_t)n_envs * std::max(e->sc.pair_cap, 1));
   rc = rc ? rc : dev_alloc(e, &e->sc.lroot, M);
   rc = rc ? rc : dev_alloc(e, &e->sc.gnx, (size_t)n_envs);
+  // chip-wide build sort of large 2-D envs (k_sort_count/scan/scatter):
+  // per-cell counters (zero between builds) and each particle's cell / rank
+  e->chip_sort = params->n_dims == 2 && n_particles > 4096 &&
+                 !(std::getenv("SWARMRL_AMD_CHIP_SORT") && std::getenv("SWARMRL_AMD_CHIP_SORT")[0] == '0');
+  if (e->chip_sort) {
+    rc = rc ? rc : dev_alloc(e, &e->sc.gcnt, (size_t)n_envs << (e->lxb + e->lyb));
+    rc = rc ? rc : dev_alloc(e, &e->sc.gcell, M);
+    rc = rc ? rc : dev_alloc(e, &e->sc.grank, M);
+  }
   rc = rc ? rc : dev_alloc(e, &e->sc.gnpairs, (size_t)n_envs);
   if (e->big_build) rc = rc ? rc : dev_alloc(e, &e->sc.gclus, 3 * M);
   rc = rc ? rc : dev_alloc(e, &e->sc.wave_npairs, (size_t)n_envs * (S / 64));

@@ -214,6 +214,9 @@ struct Scratch {
   // both ends lie in its range of sorted entries (a compact band of cells)
   // in LDS and writes each particle's block-local root; the pairs between
   // blocks go to a cross list, the only pairs the cluster build still unions
+  int32_t* gcnt;      // [E][ncb] per-cell counters of the chip-wide sort (zero between builds)
+  int32_t* gcell;     // [M] cell of a particle (chip-wide sort)
+  int32_t* grank;     // [M] its rank within the cell
   int32_t* lroot;     // [M] block-local union-find root (a particle of the env)
   uint32_t* xpairs;   // [E][pair_cap] cross-block pairs i | j << 16
   int32_t* gnx;       // [E] cross-block pairs found
@@ -1215,6 +1218,66 @@ __device__ __forceinline__ void build_sort_body(const DevState& st, const Scratc
   // last, so the stores drain in the shadow of the scatter
   for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
   SWARM_STAMP(5);
+}
+
+// Chip-wide 2-D build sort of large envs (N > 4096 outside the ride-along
+// launches): the one-workgroup counting sort keeps 16 particles per thread
+// going through every phase on one CU (21 us at 16384 colloids).  Here
+// k_sort_count ranks every particle in its cell with a global atomic (one
+// thread per particle), k_sort_scan (one workgroup per env) turns the
+// counts into the cell starts and clears them for the next build, and
+// k_sort_scatter writes every particle to its sorted entry.  Same output as
+// k_build_sort (bsq, bsid, bcstart, the reset counters and slots); the
+// entries of one cell come in atomic order, which nothing depends on (the
+// decomposition never changes the integrated bits).
+__device__ __forceinline__ int build_cell_of(const DevState& st, const Scratch& sc, size_t M,
+                                             size_t gi, uint32_t qx, uint32_t qy, int lx, int ly) {
+  if (sc.periodic) return cell_index(qx, qy, lx, ly);
+  return (cell_coord(qy, st.img[M + gi], ly, false) << lx) | cell_coord(qx, st.img[gi], lx, false);
+}
+
+__global__ __launch_bounds__(256) void k_sort_count(DevState st, Scratch sc, int lx, int ly) {
+  const int e = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x, N = st.n;
+  if (i >= N) return;
+  const size_t M = (size_t)st.m, gi = (size_t)e * N + i;
+  const int c = build_cell_of(st, sc, M, gi, st.q[gi], st.q[M + gi], lx, ly);
+  sc.gcell[gi] = c;
+  sc.grank[gi] = atomicAdd(&sc.gcnt[((size_t)e << (lx + ly)) + c], 1);
+}
+
+__global__ __launch_bounds__(1024) void k_sort_scan(Scratch sc, int lx, int ly) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
+  int32_t* cnt = wave_sums + 16;
+  const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x;
+  const int ncell = 1 << (lx + ly);
+  int32_t* g = sc.gcnt + ((size_t)e << (lx + ly));
+  for (int c = tid; c < ncell; c += T) {
+    cnt[c] = g[c];
+    g[c] = 0;  // the next build's counters
+  }
+  if (tid == 0) {
+    sc.gnpairs[e] = 0;
+    sc.gnx[e] = 0;
+    sc.fallback[e] = 0;  // the neighbour-list build sets it on overflow
+  }
+  for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
+  __syncthreads();
+  block_exclusive_scan(cnt, ncell, wave_sums);
+  __syncthreads();
+  int32_t* cs = sc.bcstart + (size_t)e * (ncell + 1);
+  for (int c = tid; c <= ncell; c += T) cs[c] = cnt[c];
+}
+
+__global__ __launch_bounds__(256) void k_sort_scatter(DevState st, Scratch sc, int lx, int ly) {
+  const int e = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x, N = st.n;
+  if (i >= N) return;
+  const size_t M = (size_t)st.m, base = (size_t)e * N, gi = base + i;
+  const int ncell = 1 << (lx + ly);
+  const size_t pos = base + sc.bcstart[(size_t)e * (ncell + 1) + sc.gcell[gi]] + sc.grank[gi];
+  sc.bsq[pos] = st.q[gi];
+  sc.bsq[M + pos] = st.q[M + gi];
+  sc.bsid[pos] = i | (sc.multi_species ? (int32_t)st.species[i] << 24 : 0);
 }
 
 template <int CH>
