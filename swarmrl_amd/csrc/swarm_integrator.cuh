@@ -217,7 +217,7 @@ struct Scratch {
   int32_t* gcnt;      // [E][ncb] per-cell counters of the chip-wide sort (zero between builds)
   int32_t* gcell;     // [M] cell of a particle (chip-wide sort)
   int32_t* grank;     // [M] its rank within the cell
-  int32_t* lroot;     // [M] block-local union-find root (a particle of the env)
+  int32_t* lroot;     // [M] block-local union-find root (a particle of the env) | pairs << 16
   uint32_t* xpairs;   // [E][pair_cap] cross-block pairs i | j << 16
   int32_t* gnx;       // [E] cross-block pairs found
   int32_t* gclus;     // [3][M] cluster sizes / bases / slots (large-N build only)
@@ -1418,7 +1418,10 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
       if (u < found && (keep[u] >> 16) != 0u) uf_union(lpar, t, (int)(keep[u] >> 16) - 1);
   }
   __syncthreads();
-  if (valid) sc.lroot[base + i] = lid[uf_find(lpar, t)];
+  // the local root, and in the upper half the pairs this particle found
+  // (as the lower id: each pair once) -- the cluster build's pair count per
+  // cluster without another pass over the pair list
+  if (valid) sc.lroot[base + i] = lid[uf_find(lpar, t)] | (min(found, 0xffff) << 16);
   // wave prefix sums, one atomic per wave: every pair to the pair list, the
   // pairs whose partner lies outside the block (all of a dense wave's) also
   // to the cross list
@@ -1530,7 +1533,7 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   // overflow of the pair or cross list -> global path
   if (tid < 16) misc[tid] = tid == 0 && (found > sc.pair_cap || nx > sc.pair_cap) ? 1 : 0;
   for (int i = tid; i < N; i += T) {
-    parent[i] = kLocal ? sc.lroot[base + i] : i;
+    parent[i] = kLocal ? (sc.lroot[base + i] & 0xffff) : i;
     csz[i] = 0;
     cbase[i] = 0;  // pair count of a cluster (one-pass packing), then its base
   }
@@ -1613,8 +1616,16 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
 #pragma unroll
     for (int u = 0; u < kU; ++u)
       if (i0 + u * T < N) lslot[i0 + u * T] = r[u];
+    if (kLocal && sc.one_pass) {  // the cluster's pairs: the members' counts of the pair search
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int i = i0 + u * T;
+        const int np_i = i < N ? (int)((uint32_t)sc.lroot[base + i] >> 16) : 0;
+        if (np_i > 0) atomicAdd(&cbase[parent[i]], np_i);
+      }
+    }
   }
-  if (sc.one_pass)
+  if (!kLocal && sc.one_pass)
     for (int k0 = tid; k0 < nsweep; k0 += kU * T) {
       uint32_t pr[kU];
       bool ok[kU];
@@ -1878,7 +1889,7 @@ __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, 
   // overflow of the pair or cross list -> global path
   if (tid < 16) misc[tid] = tid == 0 && (found > sc.pair_cap || nx > sc.pair_cap) ? 1 : 0;
   for (int i = tid; i < N; i += T) {
-    A[i] = kLocal ? sc.lroot[base + i] : i;
+    A[i] = kLocal ? (sc.lroot[base + i] & 0xffff) : i;
     B[i] = 0;
   }
   __syncthreads();
@@ -1896,10 +1907,12 @@ __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, 
   __syncthreads();
   for (int i = tid; i < N; i += T) {
     const int root = A[i];
-    const uint32_t r = (uint32_t)atomicAdd(&B[root], 1) & 0xffffu;
+    // size, and (kLocal) the member's pair count of the pair search
+    const int np_i = kLocal && sc.one_pass ? (int)((uint32_t)sc.lroot[base + i] >> 16) : 0;
+    const uint32_t r = (uint32_t)atomicAdd(&B[root], 1 + (np_i << 16)) & 0xffffu;
     A[i] = root | (int32_t)(r << 16);
   }
-  if (sc.one_pass)
+  if (!kLocal && sc.one_pass)
     for (int k0 = tid; k0 < npairs; k0 += kU * T) {
       uint32_t pr[kU];
 #pragma unroll
