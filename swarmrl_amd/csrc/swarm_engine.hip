@@ -701,7 +701,10 @@ __global__ __launch_bounds__(1024) void k_policy_cbuild(swarm::MlpArgs m, int n_
     swarm::policy_body<G, D, K>(m, b, reinterpret_cast<float*>(smem));
   } else {
     const int e = b - n_pblocks;
-    swarm::cluster_build_env<false, true, true>(st, sc, e, smem, sc.gnpairs[e]);
+    if (sc.local_uf)
+      swarm::cluster_build_env<false, true, true>(st, sc, e, smem, sc.gnpairs[e]);
+    else
+      swarm::cluster_build_env<false, true, false>(st, sc, e, smem, sc.gnpairs[e]);
   }
 }
 
@@ -1051,6 +1054,9 @@ struct swarm_engine {
   bool nlist_path = false;
   bool big_build = false;  // k_cluster_build<true>: cluster arrays in global memory
   bool chip_sort = false;  // 2-D envs above 4096 colloids: the three-launch chip-wide sort
+  // k_cluster_run_wide's idle waves integrate the rotation ahead
+  // (swarm::precompute_swim; SWARMRL_AMD_ROT_AHEAD=0 turns it off)
+  bool rot_ahead = true;
   VisionSorted vs{};
   // latency-bound windows read their normals from a table (k_noise)
   bool noise_table = false;
@@ -1275,7 +1281,7 @@ int launch_build(swarm_engine* e, hipStream_t stream) {
   HIP_TRY(hipGetLastError());
   // 2-D: the pair search left block-local union-find roots and a cross list
   // (build_pairs_body); 3-D (k_build_pairs3): the whole pair list is unioned
-  const bool local = e->params.n_dims == 2;
+  const bool local = e->params.n_dims == 2 && e->sc.local_uf;
   if (e->big_build && swarm::build_lds_words_packed(e->n) * 4 <= kMaxLds &&
       !(std::getenv("SWARMRL_AMD_PACKED_BUILD") && std::getenv("SWARMRL_AMD_PACKED_BUILD")[0] == '0')) {
     if (local)
@@ -1323,8 +1329,12 @@ int flush_ride_along(swarm_engine* e) {
                        dim3(256), 0, e->stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb);
     HIP_TRY(hipGetLastError());
   }
-  hipLaunchKernelGGL((swarm::k_cluster_build<false, true>), dim3(e->n_envs), dim3(1024),
-                     build_lds_bytes(e->n, e->sc.pair_cap), e->stream, e->st, e->sc);
+  if (e->sc.local_uf)
+    hipLaunchKernelGGL((swarm::k_cluster_build<false, true>), dim3(e->n_envs), dim3(1024),
+                       build_lds_bytes(e->n, e->sc.pair_cap), e->stream, e->st, e->sc);
+  else
+    hipLaunchKernelGGL((swarm::k_cluster_build<false, false>), dim3(e->n_envs), dim3(1024),
+                       build_lds_bytes(e->n, e->sc.pair_cap), e->stream, e->st, e->sc);
   HIP_TRY(hipGetLastError());
   e->prebuilt = true;
   return SWARM_OK;
@@ -1346,7 +1356,7 @@ int launch_run(swarm_engine* e, int n_steps) {
 #define SWARM_WIDE(MULTI, WALLS)                                                             \
   hipLaunchKernelGGL((swarm::k_cluster_run_wide<MULTI, WALLS>), grid, dim3(1024), lds, e->stream, \
                      e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise,      \
-                     e->noise_blocks, R)
+                     e->noise_blocks, R, e->rot_ahead ? 1 : 0)
     if (walls) {
       if (multi)
         SWARM_WIDE(true, true);
@@ -1742,6 +1752,13 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   // periodic-only; SWARMRL_AMD_CLUSTER_PATH=0 forces the global path (A/B
   // and parity)
   e->sc.periodic = params->periodic ? 1 : 0;
+  // block-local union-find in the 2-D pair search (SWARMRL_AMD_LOCAL_UF=0|1;
+  // default: for envs above 4096 colloids, whose one-workgroup union phase
+  // is long; at 4096 the pair search's block barriers cost more than the
+  // union saves, measured)
+  e->sc.local_uf = n_particles > 4096 ? 1 : 0;
+  if (const char* olu = std::getenv("SWARMRL_AMD_LOCAL_UF")) e->sc.local_uf = olu[0] != '0';
+  if (const char* ora = std::getenv("SWARMRL_AMD_ROT_AHEAD")) e->rot_ahead = ora[0] != '0';
   e->sc.multi_species = params->n_species > 1 ? 1 : 0;
   // the 2-D build sort stages its scatter in LDS: the sorted rows of up to
   // K entries per pass beside the cell counts (K a multiple of 4, at least

@@ -220,6 +220,7 @@ struct Scratch {
   int32_t* lroot;     // [M] block-local union-find root (a particle of the env) | pairs << 16
   uint32_t* xpairs;   // [E][pair_cap] cross-block pairs i | j << 16
   int32_t* gnx;       // [E] cross-block pairs found
+  int32_t local_uf;   // 1: the 2-D pair search unions its blocks' pairs (lroot, xpairs)
   int32_t* gclus;     // [3][M] cluster sizes / bases / slots (large-N build only)
   int32_t pair_cap;   // pairs per env
   int32_t one_pass;   // 1: pack clusters so that a wave has <= 64 pairs
@@ -1402,11 +1403,47 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
       }
     }
   }
+  const int lane = threadIdx.x & 63;
+  const bool dense = __any(found > kKeep);  // a lane kept only kKeep: the wave rescans
+  if (!sc.local_uf) {  // block-uniform: the pair list only (every pair unioned by the build)
+    int v = found;
+    v = wave_incl_scan(v);
+    int wbase = 0;
+    if (lane == 63) wbase = atomicAdd(&sc.gnpairs[e], v);
+    wbase = __builtin_amdgcn_readlane(wbase, 63);
+    const int my_off = wbase + v - found;
+    uint32_t* out = sc.gplist + (size_t)e * sc.pair_cap;
+    if (!dense) {
+#pragma unroll
+      for (int u = 0; u < kKeep; ++u) {
+        const int k = my_off + u;
+        if (u < found && k < sc.pair_cap) out[k] = (uint32_t)i | ((keep[u] & 0xffffu) << 16);
+      }
+      return;
+    }
+    int w = 0;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      for (int jj = rb[r]; jj < re[r]; ++jj) {
+        const int packed = sc.bsid[base + jj];
+        const int j = packed & 0xffffff;
+        const float rx = per ? (float)(int32_t)(sc.bsq[base + jj] - qx) * sx0
+                             : pair_disp(sc.bsq[base + jj], st.img[base + j], qx, ix, sx0, false);
+        const float ry = per ? (float)(int32_t)(sc.bsq[M + base + jj] - qy) * sx1
+                             : pair_disp(sc.bsq[M + base + jj], st.img[M + base + j], qy, iy,
+                                         sx1, false);
+        if (i < j && rx * rx + ry * ry < nb2_row[packed >> 24]) {
+          const int k = my_off + w;
+          if (k < sc.pair_cap) out[k] = (uint32_t)i | ((uint32_t)j << 16);
+          ++w;
+        }
+      }
+    }
+    return;
+  }
   // Block-local union-find of the pairs whose both ends are in this block
   // (LDS only; done before any global store is issued, so the block
   // barriers below wait for LDS operations and not for store write-backs).
-  const int lane = threadIdx.x & 63;
-  const bool dense = __any(found > kKeep);  // a lane kept only kKeep: the wave rescans
   int32_t* lpar = uf;       // [T] block-local union-find over the block's entries
   int32_t* lid = uf + T;    // [T] particle of a block slot
   lpar[t] = t;
@@ -1533,7 +1570,13 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   // overflow of the pair or cross list -> global path
   if (tid < 16) misc[tid] = tid == 0 && (found > sc.pair_cap || nx > sc.pair_cap) ? 1 : 0;
   for (int i = tid; i < N; i += T) {
-    parent[i] = kLocal ? (sc.lroot[base + i] & 0xffff) : i;
+    if (kLocal) {
+      const uint32_t l = (uint32_t)sc.lroot[base + i];
+      parent[i] = (int32_t)(l & 0xffffu);
+      lslot[i] = (int32_t)(l >> 16);  // the member's pair count, until its rank replaces it
+    } else {
+      parent[i] = i;
+    }
     csz[i] = 0;
     cbase[i] = 0;  // pair count of a cluster (one-pass packing), then its base
   }
@@ -1610,7 +1653,9 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   }
   __syncthreads();
   for (int i0 = tid; i0 < N; i0 += kU * T) {
-    int32_t r[kU];
+    int32_t r[kU], np_u[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) np_u[u] = kLocal && i0 + u * T < N ? lslot[i0 + u * T] : 0;
 #pragma unroll
     for (int u = 0; u < kU; ++u) r[u] = i0 + u * T < N ? atomicAdd(&csz[parent[i0 + u * T]], 1) : 0;
 #pragma unroll
@@ -1618,11 +1663,8 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
       if (i0 + u * T < N) lslot[i0 + u * T] = r[u];
     if (kLocal && sc.one_pass) {  // the cluster's pairs: the members' counts of the pair search
 #pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int i = i0 + u * T;
-        const int np_i = i < N ? (int)((uint32_t)sc.lroot[base + i] >> 16) : 0;
-        if (np_i > 0) atomicAdd(&cbase[parent[i]], np_i);
-      }
+      for (int u = 0; u < kU; ++u)
+        if (np_u[u] > 0) atomicAdd(&cbase[parent[i0 + u * T]], np_u[u]);
     }
   }
   if (!kLocal && sc.one_pass)
@@ -1888,7 +1930,22 @@ __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, 
   for (int k = tid; k < wmax; k += T) wave_np[k] = 0;
   // overflow of the pair or cross list -> global path
   if (tid < 16) misc[tid] = tid == 0 && (found > sc.pair_cap || nx > sc.pair_cap) ? 1 : 0;
-  for (int i = tid; i < N; i += T) {
+  // kLocal: the members' pair counts of the pair search, kept in registers
+  // from here to the size pass (same particles per thread; N <= kPer T)
+  constexpr int kPer = 20;
+  int32_t np_k[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int i = tid + k * T;
+    np_k[k] = 0;
+    if (i < N) {
+      const uint32_t l = kLocal ? (uint32_t)sc.lroot[base + i] : (uint32_t)i;
+      A[i] = (int32_t)(l & 0xffffu);
+      np_k[k] = (int32_t)(l >> 16);
+      B[i] = 0;
+    }
+  }
+  for (int i = tid + kPer * T; i < N; i += T) {  // beyond kPer T: no pair counts kept
     A[i] = kLocal ? (sc.lroot[base + i] & 0xffff) : i;
     B[i] = 0;
   }
@@ -1905,9 +1962,19 @@ __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, 
   SWARM_STAMP(7);
   for (int i = tid; i < N; i += T) A[i] = uf_find(A, i);
   __syncthreads();
-  for (int i = tid; i < N; i += T) {
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int i = tid + k * T;
+    if (i < N) {
+      const int root = A[i];
+      // size, and (kLocal) the member's pair count of the pair search
+      const int np_i = kLocal && sc.one_pass ? np_k[k] : 0;
+      const uint32_t r = (uint32_t)atomicAdd(&B[root], 1 + (np_i << 16)) & 0xffffu;
+      A[i] = root | (int32_t)(r << 16);
+    }
+  }
+  for (int i = tid + kPer * T; i < N; i += T) {
     const int root = A[i];
-    // size, and (kLocal) the member's pair count of the pair search
     const int np_i = kLocal && sc.one_pass ? (int)((uint32_t)sc.lroot[base + i] >> 16) : 0;
     const uint32_t r = (uint32_t)atomicAdd(&B[root], 1 + (np_i << 16)) & 0xffffu;
     A[i] = root | (int32_t)(r << 16);
@@ -2377,7 +2444,7 @@ __global__ __launch_bounds__(256) void k_noise(const Derived* __restrict__ d, De
 // were computed ahead by the block's idle waves (precompute_swim) into LDS
 // (dtab[s * 64 + lane], angfin[lane]): the rotation is position-independent,
 // so the run wave's dependency chain loses the angle update and sin/cos.
-template <bool kMulti, bool kTable, bool kWalls, bool kDir = false>
+template <bool kMulti, bool kTable, bool kWalls, bool kDir = false, bool kTwoPass = false>
 __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const DevState& st,
                                          const Scratch& sc, int n_envs, int n_steps,
                                          uint64_t step0, const float* __restrict__ table,
@@ -2434,6 +2501,11 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
   // (rare: a cluster denser than 2 pairs per particle) reloads the others
   // from L2 each sub-step, so they do not hold registers for the run
   const uint32_t pr0 = lane < np ? pw[lane] : 0xffffffffu;
+  // two passes (a cluster with more than 64 pairs: 65-128 in the wave): the
+  // second pass's pair in a register too, and both passes unrolled so their
+  // LDS reads and force arithmetic interleave (C5: such a wave set the
+  // launch's duration in a third of the windows, 1.7x a one-pass wave)
+  const uint32_t pr1 = npass == 2 && 64 + lane < np ? pw[64 + lane] : 0xffffffffu;
   lacc_x[lane] = 0ull;
   lacc_y[lane] = 0ull;
   const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
@@ -2494,10 +2566,12 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     if (kPass > 0) {
       lpos_w[lane] = make_uint2(p.qx, p.qy);
       wave_lds_sync();
-      for (int q = 0; q < (kPass == 1 ? 1 : npass); ++q) {
+      for (int q = 0; q < (kPass == 1 ? 1 : (kPass == 2 ? 2 : npass)); ++q) {
         {  // wave-uniform; an empty slot names the lane twice
           const uint32_t e_ = q == 0 ? pr0
-                                     : (q * 64 + lane < np ? pw[q * 64 + lane] : 0xffffffffu);
+                                     : (kPass == 2 ? pr1
+                                                   : (q * 64 + lane < np ? pw[q * 64 + lane]
+                                                                         : 0xffffffffu));
           const int a = e_ == 0xffffffffu ? lane : (int)(e_ & 63u);
           const int b = e_ == 0xffffffffu ? lane : (int)((e_ >> 6) & 63u);
           const uint2 pa = lpos_w[a], pb = lpos_w[b];
@@ -2614,6 +2688,8 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     run_steps(std::integral_constant<int, 0>{});
   else if (npass == 1)
     run_steps(std::integral_constant<int, 1>{});
+  else if (kTwoPass && npass == 2)  // (the throughput kernel: not worth its registers)
+    run_steps(std::integral_constant<int, 2>{});
   else
     run_steps(std::integral_constant<int, 4>{});
 #ifdef SWARM_PHASE_TIMING
@@ -2817,7 +2893,8 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
                                                            DevState st, Scratch sc, int n_envs,
                                                            int n_steps, uint64_t* __restrict__ ctl,
                                                            float* __restrict__ tables,
-                                                           int n_noise_blocks, int run_wpb) {
+                                                           int n_noise_blocks, int run_wpb,
+                                                           int rot_ahead) {
   extern __shared__ __align__(16) unsigned char wide_lds[];
   __shared__ PairTables pt;
   __shared__ uint2 lpos[4][64];
@@ -2851,7 +2928,8 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
   // one or two run waves per block (a latency-bound launch; the host sized
   // the dynamic LDS, wide_dir_lds_bytes) and this window's normals in the
   // table: the other waves integrate the run waves' rotation ahead
-  if ((run_wpb == 1 || run_wpb == 2) && table_ok && blockDim.x == 1024 && tables != nullptr) {
+  if (rot_ahead && (run_wpb == 1 || run_wpb == 2) && table_ok && blockDim.x == 1024 &&
+      tables != nullptr) {
     float2* dtab = reinterpret_cast<float2*>(wide_lds);  // [R][kMaxWindow][64]
     uint32_t* angfin = reinterpret_cast<uint32_t*>(dtab + (size_t)run_wpb * kMaxWindow * 64);
     uint32_t* partial = angfin + run_wpb * 64;           // [1024]
@@ -2862,7 +2940,7 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
       precompute_swim<kMulti, 2>(d, st, sc, n_envs, gw0, n_steps, table, par, dtab, angfin,
                                  partial);
     if (wv >= run_wpb) return;
-    run_wave<kMulti, true, kWalls, true>(d, st, sc, n_envs, n_steps, step0, table, gw0 + wv,
+    run_wave<kMulti, true, kWalls, true, true>(d, st, sc, n_envs, n_steps, step0, table, gw0 + wv,
                                          lane, lpos[wv], lacc[wv][0], lacc[wv][1], pt, par,
                                          dtab + (size_t)wv * kMaxWindow * 64, angfin + wv * 64);
     return;

@@ -218,9 +218,9 @@ def test_nonperiodic_3d_cluster_windows_4096():
     h.set_torque_xy(tq[:2])
     h.set_actions(f, tq[2])
     ref = st
-    for _ in range(3):
+    for k in range(3):
         h.integrate(100)
-        ref, vel, _ = oracle.bd_run3(h.op, ref, sp, f, tq, 100)
+        ref, vel, _ = oracle.bd_run3(h.op, ref, sp, f, tq, 100, step0=100 * k)
         _eq(h.download()[0], ref, ("q", "img", "dir"))
     assert np.array_equal(h.velocities(), vel)
     fb = np.zeros(1, np.int32)
