@@ -343,14 +343,20 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
         nat.call("swarm_engine_profile", 0, ctypes.byref(ms), ctypes.byref(cnt))
     buf = (ctypes.c_float * 4096)()
     cal = (ctypes.c_float * 4096)()
-    cal_samples = []
+    dev = (ctypes.c_float * 4096)()
+    cal_samples, dev_samples = [], []
     try:
         if graph is not None:
             for _ in range(replays):
+                nat.call("swarm_engine_profile_stamps", 1,
+                         ctypes.c_void_p(torch.cuda.current_stream().cuda_stream), None, 0,
+                         ctypes.byref(cnt))
                 graph.replay()
                 nat.call("swarm_engine_profile_graph", 0, buf, cal, 4096, ctypes.byref(cnt))
                 samples.extend(buf[k] for k in range(min(cnt.value, 4096)))
                 cal_samples.extend(cal[k] for k in range(min(cnt.value, 4096)))
+                nat.call("swarm_engine_profile_stamps", 0, None, dev, 4096, ctypes.byref(cnt))
+                dev_samples.extend(dev[k] for k in range(min(cnt.value, 4096)))
         else:
             torch.cuda.synchronize()
             agent.reset_trajectory()
@@ -369,14 +375,22 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
         return None, name, "no run-kernel launches recorded", 0
     samples.sort()
     raw = sum(samples) / len(samples)
-    # an empty pair of event nodes right after each run node measures what
-    # the pair adds by itself (marker packets, the dispatch gap they open):
-    # subtracted, the figure is the kernel's own duration in the workload
+    # the event-record nodes add their own marker latency around the kernel
+    # (an empty pair of them right after each run node: `over`); the run
+    # kernel's own stamps (earliest block start, latest wave end, device
+    # wall clock) time the launch as it ran in the replayed workload
     over = sum(cal_samples) / len(cal_samples) if cal_samples else 0.0
-    mean = raw - over
-    note = (f"{how}: {len(samples)} launches; event pair around the run node: mean {raw:.5f} "
-            f"ms, median {samples[len(samples) // 2]:.5f}, min {samples[0]:.5f}, max "
-            f"{samples[-1]:.5f}; minus an empty event-node pair ({over:.5f} ms)")
+    dev_ok = [x for x in dev_samples if x > 0.0]
+    if dev_ok and len(dev_ok) == len(samples):
+        mean = sum(dev_ok) / len(dev_ok)
+        how_ms = (f"the kernel's own start / end stamps (device wall clock): mean {mean:.5f} ms, "
+                  f"min {min(dev_ok):.5f}, max {max(dev_ok):.5f}; ")
+    else:
+        mean = raw
+        how_ms = ""
+    note = (f"{how}: {len(samples)} launches; {how_ms}HIP event pair around the run node: mean "
+            f"{raw:.5f} ms, median {samples[len(samples) // 2]:.5f}, min {samples[0]:.5f}, max "
+            f"{samples[-1]:.5f}; an empty event-node pair alone: {over:.5f} ms")
     return mean, name, note, len(samples)
 
 

@@ -269,6 +269,17 @@ int swarm_engine_profile(swarm_engine_t *e, int32_t enable, double *run_ms,
 int swarm_engine_profile_graph(swarm_engine_t *e, int32_t release, float *ms_out,
                                float *cal_out, int32_t cap, int32_t *launches);
 
+/* The same captured run nodes timed by the kernel itself: each records the
+ * earliest start of its blocks and the latest end of its waves on the
+ * device's constant-rate wall clock.  reset = 1: clears the stamps on
+ * `stream` (before a replay); reset = 0: waits for the device and writes the
+ * durations (ms, end - start) of the captured run nodes, in capture order,
+ * to ms_out[0..cap) (each the latest replay's).  *launches = the number of
+ * stamped nodes (at most 512; swarm_engine_profile_graph's release resets
+ * the count). */
+int swarm_engine_profile_stamps(swarm_engine_t *e, int32_t reset, void *stream, float *ms_out,
+                                int32_t cap, int32_t *launches);
+
 /* Kernel timing for measurement (bench.py roofline): builds the next 2-D
  * cluster window from the current positions, then launches its run kernel
  * `reps` times back to back between two HIP events on the engine stream and

@@ -1102,6 +1102,10 @@ struct swarm_engine {
   // per captured run node, an empty event pair recorded right after it: the
   // cost of an event-record node pair itself (swarm_engine_profile_graph)
   std::vector<std::pair<hipEvent_t, hipEvent_t>> graph_cal;
+  // and each captured run node's own start / end stamps (swarm::stamp_start,
+  // stamp_end): d_tstamp[2 k], [2 k + 1] for the k-th captured run node
+  unsigned long long* d_tstamp = nullptr;
+  int stamp_next = 0;
   float* own_f_swim = nullptr;
   float* own_torque_z = nullptr;
   void* allocs[96] = {};
@@ -1342,7 +1346,9 @@ int flush_ride_along(swarm_engine* e) {
 
 // The 2-D cluster window's run kernel (k_cluster_run_wide for latency-bound
 // engines, else k_cluster_run) over the current decomposition.
-int launch_run(swarm_engine* e, int n_steps) {
+constexpr int kMaxStamps = 512;  // captured run nodes with launch stamps
+
+int launch_run(swarm_engine* e, int n_steps, unsigned long long* tstamp = nullptr) {
   const long waves = (long)e->n_envs * e->sc.wmax;
   const bool multi = e->params.n_species > 1;
   const bool walls = e->derived.n_walls != 0;
@@ -1356,7 +1362,7 @@ int launch_run(swarm_engine* e, int n_steps) {
 #define SWARM_WIDE(MULTI, WALLS)                                                             \
   hipLaunchKernelGGL((swarm::k_cluster_run_wide<MULTI, WALLS>), grid, dim3(1024), lds, e->stream, \
                      e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise,      \
-                     e->noise_blocks, R, e->rot_ahead ? 1 : 0)
+                     e->noise_blocks, R, e->rot_ahead ? 1 : 0, tstamp)
     if (walls) {
       if (multi)
         SWARM_WIDE(true, true);
@@ -1381,7 +1387,7 @@ int launch_run(swarm_engine* e, int n_steps) {
 #define SWARM_RUN(MULTI, TABLE, WALLS)                                                     \
   hipLaunchKernelGGL((swarm::k_cluster_run<MULTI, TABLE, WALLS>), run_grid, run_block, 0,   \
                      e->stream, e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step,  \
-                     e->d_noise, xcd ? bpe : 0)
+                     e->d_noise, xcd ? bpe : 0, tstamp)
 #define SWARM_RUN_W(MULTI, TABLE)      \
   do {                                 \
     if (walls)                         \
@@ -1563,7 +1569,12 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
     const int rc0 = record_event(e->stream, ev0, in_graph);
     if (rc0) return rc0;
   }
-  int rc = launch_run(e, n_steps);
+  unsigned long long* tstamp = nullptr;
+  if (e->profile && in_graph) {
+    if (!e->d_tstamp) HIP_TRY(hipMalloc(&e->d_tstamp, 2 * kMaxStamps * sizeof(unsigned long long)));
+    if (e->stamp_next < kMaxStamps) tstamp = e->d_tstamp + 2 * e->stamp_next++;
+  }
+  int rc = launch_run(e, n_steps, tstamp);
   if (rc) return rc;
   if (e->profile) {
     rc = record_event(e->stream, ev1, in_graph);
@@ -1980,6 +1991,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
 void swarm_engine_destroy(swarm_engine_t* e) {
   if (!e) return;
   (void)hipDeviceSynchronize();
+  if (e->d_tstamp) (void)hipFree(e->d_tstamp);
   for (auto* v : {&e->prof_events, &e->graph_events, &e->graph_cal})
     for (auto& pr : *v) {
       (void)hipEventDestroy(pr.first);
@@ -2227,8 +2239,45 @@ int swarm_engine_profile_graph(swarm_engine_t* e, int32_t release, float* ms_out
       }
       v->clear();
     }
+    e->stamp_next = 0;
   }
   return rc;
+}
+
+namespace {
+__global__ void k_stamp_reset(unsigned long long* t, int n) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) {
+    t[2 * k] = ~0ull;
+    t[2 * k + 1] = 0ull;
+  }
+}
+}  // namespace
+
+int swarm_engine_profile_stamps(swarm_engine_t* e, int32_t reset, void* stream, float* ms_out,
+                                int32_t cap, int32_t* launches) {
+  if (!e) return fail(SWARM_EINVAL, "null engine");
+  const int n = e->stamp_next;
+  if (launches) *launches = n;
+  if (!e->d_tstamp || n == 0) return SWARM_OK;
+  if (reset) {
+    hipLaunchKernelGGL(k_stamp_reset, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), e->d_tstamp, n);
+    HIP_TRY(hipGetLastError());
+    return SWARM_OK;
+  }
+  if (cap < 0 || (cap > 0 && !ms_out)) return fail(SWARM_EINVAL, "ms_out needs cap entries");
+  HIP_TRY(hipDeviceSynchronize());
+  std::vector<unsigned long long> t(2 * (size_t)n);
+  HIP_TRY(hipMemcpy(t.data(), e->d_tstamp, t.size() * sizeof(unsigned long long),
+                    hipMemcpyDeviceToHost));
+  int dev = 0, khz = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+  if (khz <= 0) return fail(SWARM_EDEVICE, "no wall clock rate");
+  for (int k = 0; k < n && k < cap; ++k)
+    ms_out[k] = t[2 * k + 1] > t[2 * k] ? (float)((double)(t[2 * k + 1] - t[2 * k]) / khz) : 0.0f;
+  return SWARM_OK;
 }
 
 int swarm_engine_time_run(swarm_engine_t* e, int32_t n_steps, int32_t reps, double* run_ms) {

@@ -2753,6 +2753,17 @@ __device__ __forceinline__ void run_wave_dispatch(const Derived* __restrict__ d,
                                     lacc_x, lacc_y, pt, par);
 }
 
+// Launch-duration stamps for measurement (bench.py, swarm_engine_profile
+// under graph capture): tstamp[0] = the earliest block start, tstamp[1] = the
+// latest wave end, realtime clock (100 MHz); null otherwise (one uniform
+// branch per block / wave).
+__device__ __forceinline__ void stamp_start(unsigned long long* tstamp) {
+  if (tstamp && threadIdx.x == 0) atomicMin(&tstamp[0], (unsigned long long)wall_clock64());
+}
+__device__ __forceinline__ void stamp_end(unsigned long long* tstamp) {
+  if (tstamp && (threadIdx.x & 63) == 0) atomicMax(&tstamp[1], (unsigned long long)wall_clock64());
+}
+
 // XCD-aware placement of per-env work (envs_per_xcd_map: blocks of one env):
 // workgroup b is dispatched to XCD b mod 8 (MI355X_MICROARCH.md: for speed
 // only, nothing depends on it), so the env's blocks are the b with
@@ -2778,10 +2789,12 @@ __global__ __launch_bounds__(256, SWARM_RUN_MINB) void k_cluster_run(const Deriv
                                                      Scratch sc, int n_envs, int n_steps,
                                                      const uint64_t* __restrict__ ctl,
                                                      const float* __restrict__ tables,
-                                                     int xcd_bpe) {
+                                                     int xcd_bpe,
+                                                     unsigned long long* __restrict__ tstamp) {
   __shared__ PairTables pt;
   __shared__ uint2 lpos[4][64];                  // positions of the block's 4 waves
   __shared__ unsigned long long lacc[4][2][64];  // int64 force sums (x, y)
+  stamp_start(tstamp);
   stage_pair_tables(d, &pt);
   const int par = window_parity(ctl);
   const uint64_t step0 = ctl[kCtlStep];
@@ -2801,6 +2814,7 @@ __global__ __launch_bounds__(256, SWARM_RUN_MINB) void k_cluster_run(const Deriv
   run_wave_dispatch<kMulti, kWalls>(d, st, sc, n_envs, n_steps, step0,
                                     table_ok ? tables + par * noise_table_words(st.m) : nullptr,
                                     gw, lane, lpos[wv], lacc[wv][0], lacc[wv][1], pt, par);
+  stamp_end(tstamp);
 }
 
 // Latency-bound launch (few envs x particles: the run's waves fill few
@@ -2894,11 +2908,13 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
                                                            int n_steps, uint64_t* __restrict__ ctl,
                                                            float* __restrict__ tables,
                                                            int n_noise_blocks, int run_wpb,
-                                                           int rot_ahead) {
+                                                           int rot_ahead,
+                                                           unsigned long long* __restrict__ tstamp) {
   extern __shared__ __align__(16) unsigned char wide_lds[];
   __shared__ PairTables pt;
   __shared__ uint2 lpos[4][64];
   __shared__ unsigned long long lacc[4][2][64];
+  stamp_start(tstamp);
   stage_pair_tables(d, &pt);
   const int par = window_parity(ctl);
   const uint64_t step0 = ctl[kCtlStep];
@@ -2919,6 +2935,7 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
       noise_item(k, (long)M, G, &gi, &grp);
       noise_group(d, st, start, kMaxWindow, t, gi, grp);
     }
+    stamp_end(tstamp);
     return;
   }
   const int lane = tid & 63, wv = tid >> 6;
@@ -2943,12 +2960,14 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
     run_wave<kMulti, true, kWalls, true, true>(d, st, sc, n_envs, n_steps, step0, table, gw0 + wv,
                                          lane, lpos[wv], lacc[wv][0], lacc[wv][1], pt, par,
                                          dtab + (size_t)wv * kMaxWindow * 64, angfin + wv * 64);
+    stamp_end(tstamp);
     return;
   }
   if (wv >= run_wpb) return;
   const int gw = gw0 + wv;
   run_wave_dispatch<kMulti, kWalls>(d, st, sc, n_envs, n_steps, step0, table, gw, lane, lpos[wv],
                                     lacc[wv][0], lacc[wv][1], pt, par);
+  stamp_end(tstamp);
 }
 
 // The env's big clusters (wider than a wave) for the window, by k_check's
