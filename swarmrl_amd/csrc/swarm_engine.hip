@@ -1570,10 +1570,8 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
     if (rc0) return rc0;
   }
   unsigned long long* tstamp = nullptr;
-  if (e->profile && in_graph) {
-    if (!e->d_tstamp) HIP_TRY(hipMalloc(&e->d_tstamp, 2 * kMaxStamps * sizeof(unsigned long long)));
-    if (e->stamp_next < kMaxStamps) tstamp = e->d_tstamp + 2 * e->stamp_next++;
-  }
+  if (e->profile && in_graph && e->d_tstamp && e->stamp_next < kMaxStamps)
+    tstamp = e->d_tstamp + 2 * e->stamp_next++;
   int rc = launch_run(e, n_steps, tstamp);
   if (rc) return rc;
   if (e->profile) {
@@ -2207,6 +2205,9 @@ int swarm_engine_profile(swarm_engine_t* e, int32_t enable, double* run_ms, int3
   if (!e) return fail(SWARM_EINVAL, "null engine");
   const int rc = read_event_pairs(e->prof_events, run_ms, launches);
   e->profile = enable != 0;
+  // the launch stamps of captured run nodes (allocated here: never under capture)
+  if (e->profile && !e->d_tstamp)
+    HIP_TRY(hipMalloc(&e->d_tstamp, 2 * kMaxStamps * sizeof(unsigned long long)));
   return rc;
 }
 
