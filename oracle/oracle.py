@@ -25,7 +25,13 @@ TWO32 = 4294967296.0
 
 
 def build() -> pathlib.Path:
-    subprocess.run(["make", "-s", "-C", str(_DIR)], check=True)
+    # one make at a time (parallel test workers would otherwise rewrite the
+    # library while another loads it)
+    import fcntl
+
+    with open(_DIR / ".build.lock", "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", str(_DIR)], check=True)
     return _LIB_PATH
 
 
