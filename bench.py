@@ -345,6 +345,9 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
     cal = (ctypes.c_float * 4096)()
     dev = (ctypes.c_float * 4096)()
     cal_samples, dev_samples = [], []
+    n_roles = ctypes.c_int32(0)
+    rbuf = (ctypes.c_double * (2 * 8 * 512))()
+    role_samples = {}
     try:
         if graph is not None:
             for _ in range(replays):
@@ -357,6 +360,12 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
                 cal_samples.extend(cal[k] for k in range(min(cnt.value, 4096)))
                 nat.call("swarm_engine_profile_stamps", 0, None, dev, 4096, ctypes.byref(cnt))
                 dev_samples.extend(dev[k] for k in range(min(cnt.value, 4096)))
+                nat.call("swarm_engine_profile_roles", rbuf, len(rbuf), ctypes.byref(n_roles))
+                for k in range(min(cnt.value, 512)):
+                    for q in range(n_roles.value):
+                        b, e = rbuf[2 * (k * n_roles.value + q)], rbuf[2 * (k * n_roles.value + q) + 1]
+                        if b == b and e == e:  # not NaN
+                            role_samples.setdefault(q, []).append((b, e))
         else:
             torch.cuda.synchronize()
             agent.reset_trajectory()
@@ -372,7 +381,7 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
         nat.call("swarm_engine_profile_graph", 1, None, None, 0, ctypes.byref(cnt))
         agent.trajectory = saved
     if not samples:  # no 2-D cluster windows (global path): nothing was recorded
-        return None, name, "no run-kernel launches recorded", 0
+        return None, name, "no run-kernel launches recorded", 0, {}
     samples.sort()
     raw = sum(samples) / len(samples)
     # the event-record nodes add their own marker latency around the kernel
@@ -391,7 +400,17 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
     note = (f"{how}: {len(samples)} launches; {how_ms}HIP event pair around the run node: mean "
             f"{raw:.5f} ms, median {samples[len(samples) // 2]:.5f}, min {samples[0]:.5f}, max "
             f"{samples[-1]:.5f}; an empty event-node pair alone: {over:.5f} ms")
-    return mean, name, note, len(samples)
+    # the workgroup roles of the launches between run nodes (role stamps):
+    # mean start / end after the previous run node's end, and mean duration
+    names = ("k_check", "build sort", "vision grid", "field (reward)", "pair search",
+             "vision cone", "cluster build", "policy MLP")
+    timeline = {}
+    for q, v in sorted(role_samples.items()):
+        timeline[names[q] if q < len(names) else f"role{q}"] = {
+            "start_us": round(sum(b for b, _ in v) / len(v), 2),
+            "end_us": round(sum(e for _, e in v) / len(v), 2),
+            "dur_us": round(sum(e - b for b, e in v) / len(v), 2), "n": len(v)}
+    return mean, name, note, len(samples), timeline
 
 
 def time_ppo_grads(agent, traj, line, reps):
@@ -801,7 +820,7 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
 
     eng.drain_trajectory(block=True)
     traj_written = eng.h5_time_steps_written + len(eng.traj_holder["Times"])
-    kernel_ms, kernel, timing_note, timed_launches = time_run_kernel(eng, ff, agent, T)
+    kernel_ms, kernel, timing_note, timed_launches, timeline = time_run_kernel(eng, ff, agent, T)
     N = args.colloids
     sub = eng.params.steps_per_slice
     out = dict(timing)
@@ -818,6 +837,10 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
     })
     out["roofline"]["kernel_timing"] = timing_note
     out["roofline"]["kernel_timing_launches"] = timed_launches
+    if timeline:
+        # after each run node: its check, then the next window's build and
+        # observable workgroups (device wall-clock role stamps, same replays)
+        out["slice_timeline_us"] = timeline
     valu = out["roofline"].get("valu")
     if valu:
         valu["lane_insts_per_colloid_substep"] = valu["insts_per_launch"] * 64 / (N * sub * E)
@@ -927,7 +950,7 @@ def _sub_line(res, workload, extra=None):
     out = {"workload": workload, "value": res["value"], "unit": "agent-steps/s",
            "envs_per_gpu": res["E"], "ms_per_step": res["ms_per_step"],
            "per_rank_value": res["per_rank"], "roofline": res["roofline"]}
-    for k in ("gather", "roofline_update"):
+    for k in ("gather", "roofline_update", "slice_timeline_us"):
         if res.get(k) is not None:
             out[k] = res[k]
     out.update(extra or {})
@@ -1068,6 +1091,8 @@ def main():
     }
     if "gather" in head:
         line["gather"] = head["gather"]
+    if head.get("slice_timeline_us"):
+        line["slice_timeline_us"] = head["slice_timeline_us"]
     for k in LINES:
         if k in res:
             line[k] = res[k]

@@ -280,6 +280,17 @@ int swarm_engine_profile_graph(swarm_engine_t *e, int32_t release, float *ms_out
 int swarm_engine_profile_stamps(swarm_engine_t *e, int32_t reset, void *stream, float *ms_out,
                                 int32_t cap, int32_t *launches);
 
+/* The workgroup roles of the launches between the captured run nodes,
+ * stamped the same way while profiling (stamp slot k: the k_check after the
+ * k-th run node and the next window's build / observable / policy launches
+ * up to the next run).  Writes, for slot k and role q (k_check, build sort,
+ * vision grid, field, pair search, vision cone, cluster build, policy MLP;
+ * *n_roles = 8), us_out[2 (k n_roles + q) + 0 / 1] = the role's earliest
+ * start / latest end in microseconds after the k-th run node's end (NaN
+ * where the role did not run), for entries below cap.  Waits for the
+ * device; reset with swarm_engine_profile_stamps. */
+int swarm_engine_profile_roles(swarm_engine_t *e, double *us_out, int32_t cap, int32_t *n_roles);
+
 /* Kernel timing for measurement (bench.py roofline): builds the next 2-D
  * cluster window from the current positions, then launches its run kernel
  * `reps` times back to back between two HIP events on the engine stream and

@@ -127,6 +127,7 @@ _SIGNATURES = {
                                                   _P]),
     "swarm_engine_profile_stamps": (ctypes.c_int, [_P, ctypes.c_int32, _P, _P, ctypes.c_int32,
                                                    _P]),
+    "swarm_engine_profile_roles": (ctypes.c_int, [_P, _P, ctypes.c_int32, _P]),
     "swarm_engine_time_run": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _P]),
     "swarm_engine_debug_phases": (ctypes.c_int, [_P, _P]),
     "swarm_engine_debug_wave_stamps": (ctypes.c_int, [_P, _P, ctypes.c_int32]),

@@ -664,48 +664,62 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
 //   k_vision_pairs   the vision cone's blocks + k_build_pairs's
 //   k_policy_cbuild  the policy's blocks (1024 threads) + k_cluster_build's
 // Each stage needs the previous one complete, which the launch order on
-// the engine stream guarantees.
+// the engine stream guarantees.  The build's workgroups take the first block
+// indices of each launch: the build chain (sort -> pairs -> cluster build)
+// is the longer one, so its workgroups are dealt out first.
 template <int CH>
 __global__ __launch_bounds__(1024) void k_vgrid_sort(DevState st, VisionArgs va, Scratch sc,
                                                      int lxb, int lyb) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int b = blockIdx.x;
+  const int role = b < va.n_envs ? swarm::kRoleSort : swarm::kRoleVgrid;
+  swarm::role_begin(sc, role);
   if (b < va.n_envs)
-    vision_grid_body(st, va, b, smem);
+    swarm::build_sort_body<CH>(st, sc, lxb, lyb, b, smem);
   else
-    swarm::build_sort_body<CH>(st, sc, lxb, lyb, b - va.n_envs, smem);
+    vision_grid_body(st, va, b - va.n_envs, smem);
+  swarm::role_end(sc, role);
 }
 
-template <int NB, int G>
+// The pair blocks come first: theirs is the longer chain (the cluster build
+// waits on it), so they are dealt out before the cone blocks.  kStaged: the
+// pair blocks stage their env's sorted records in (dynamic) LDS.
+template <int NB, int G, bool kStaged>
 __global__ __launch_bounds__(256) void k_vision_pairs(DevState st, const Derived* __restrict__ d,
-                                                      VisionArgs va, int n_vblocks, Scratch sc,
+                                                      VisionArgs va, int n_pblocks, Scratch sc,
                                                       int lxb, int lyb, int pair_bx) {
   __shared__ uint32_t hits[kVisionHits][256];
   __shared__ float nb2[swarm::kMaxSpecies * swarm::kMaxSpecies];
   __shared__ int32_t uf[2 * 256];
+  extern __shared__ __align__(16) uint32_t pstage[];
   const int b = blockIdx.x;
-  if (b < n_vblocks) {
-    vision_body<NB, G, false>(st, d, va, b, 0, hits);
+  const int role = b < n_pblocks ? swarm::kRolePairs : swarm::kRoleCone;
+  swarm::role_begin(sc, role);
+  if (b < n_pblocks) {
+    swarm::build_pairs_body<kStaged>(d, st, sc, lxb, lyb, b % pair_bx, b / pair_bx, nb2, uf,
+                                     pstage);
   } else {
-    const int pb = b - n_vblocks;
-    swarm::build_pairs_body(d, st, sc, lxb, lyb, pb % pair_bx, pb / pair_bx, nb2, uf);
+    vision_body<NB, G, false>(st, d, va, b - n_pblocks, 0, hits);
   }
+  swarm::role_end(sc, role);
 }
 
 template <int G, int D, int K>
-__global__ __launch_bounds__(1024) void k_policy_cbuild(swarm::MlpArgs m, int n_pblocks,
+__global__ __launch_bounds__(1024) void k_policy_cbuild(swarm::MlpArgs m, int n_envs,
                                                         DevState st, Scratch sc) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int b = blockIdx.x;
-  if (b < n_pblocks) {
-    swarm::policy_body<G, D, K>(m, b, reinterpret_cast<float*>(smem));
-  } else {
-    const int e = b - n_pblocks;
+  const int role = b < n_envs ? swarm::kRoleCbuild : swarm::kRoleMlp;
+  swarm::role_begin(sc, role);
+  if (b < n_envs) {
     if (sc.local_uf)
-      swarm::cluster_build_env<false, true, true>(st, sc, e, smem, sc.gnpairs[e]);
+      swarm::cluster_build_env<false, true, true>(st, sc, b, smem, sc.gnpairs[b]);
     else
-      swarm::cluster_build_env<false, true, false>(st, sc, e, smem, sc.gnpairs[e]);
+      swarm::cluster_build_env<false, true, false>(st, sc, b, smem, sc.gnpairs[b]);
+  } else {
+    swarm::policy_body<G, D, K>(m, b - n_envs, reinterpret_cast<float*>(smem));
   }
+  swarm::role_end(sc, role);
 }
 
 // ------------------------------------------- neighbour reductions (fp64)
@@ -916,12 +930,17 @@ __global__ __launch_bounds__(1024) void k_field_vgrid_sort(FieldArgs f, int n_fb
                                                            int lyb) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int b = blockIdx.x;
-  if (b < n_fblocks)
-    field_body(st, f, b * blockDim.x + threadIdx.x);
-  else if (b < n_fblocks + va.n_envs)
-    vision_grid_body(st, va, b - n_fblocks, smem);
+  const int role = b < va.n_envs       ? swarm::kRoleSort
+                   : b < 2 * va.n_envs ? swarm::kRoleVgrid
+                                       : swarm::kRoleField;
+  swarm::role_begin(sc, role);
+  if (b < va.n_envs)
+    swarm::build_sort_body<CH>(st, sc, lxb, lyb, b, smem);
+  else if (b < 2 * va.n_envs)
+    vision_grid_body(st, va, b - va.n_envs, smem);
   else
-    swarm::build_sort_body<CH>(st, sc, lxb, lyb, b - n_fblocks - va.n_envs, smem);
+    field_body(st, f, (b - 2 * va.n_envs) * blockDim.x + threadIdx.x);
+  swarm::role_end(sc, role);
 }
 
 // --------------------------------------------------------- pair listing
@@ -1054,9 +1073,11 @@ struct swarm_engine {
   bool nlist_path = false;
   bool big_build = false;  // k_cluster_build<true>: cluster arrays in global memory
   bool chip_sort = false;  // 2-D envs above 4096 colloids: the three-launch chip-wide sort
+  bool pairs_staged = false;  // the ride-along pair search stages its env in LDS
   // k_cluster_run_wide's idle waves integrate the rotation ahead
-  // (swarm::precompute_swim; SWARMRL_AMD_ROT_AHEAD=0 turns it off)
-  bool rot_ahead = true;
+  // (swarm::precompute_swim; SWARMRL_AMD_ROT_AHEAD=1 turns it on: measured
+  // slower, 4096 colloids 42.2 M vs 41.9 M agent-steps/s, C4 78.0 M vs 67.5 M)
+  bool rot_ahead = false;
   VisionSorted vs{};
   // latency-bound windows read their normals from a table (k_noise)
   bool noise_table = false;
@@ -1106,6 +1127,10 @@ struct swarm_engine {
   // stamp_end): d_tstamp[2 k], [2 k + 1] for the k-th captured run node
   unsigned long long* d_tstamp = nullptr;
   int stamp_next = 0;
+  // [kMaxStamps][kRoles][2]: the workgroup roles of the launches that follow
+  // the k-th captured run node (its k_check, then the next window's build and
+  // observable launches), swarm::role_begin / role_end
+  unsigned long long* d_rstamp = nullptr;
   float* own_f_swim = nullptr;
   float* own_torque_z = nullptr;
   void* allocs[96] = {};
@@ -1572,6 +1597,11 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
   unsigned long long* tstamp = nullptr;
   if (e->profile && in_graph && e->d_tstamp && e->stamp_next < kMaxStamps)
     tstamp = e->d_tstamp + 2 * e->stamp_next++;
+  // the check and the launches up to the next run record their roles in
+  // this run's slot (profiling under capture only)
+  e->sc.rstamp = tstamp && e->d_rstamp
+                     ? e->d_rstamp + (size_t)(e->stamp_next - 1) * 2 * swarm::kRoles
+                     : nullptr;
   int rc = launch_run(e, n_steps, tstamp);
   if (rc) return rc;
   if (e->profile) {
@@ -1768,6 +1798,14 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   e->sc.local_uf = n_particles > 4096 ? 1 : 0;
   if (const char* olu = std::getenv("SWARMRL_AMD_LOCAL_UF")) e->sc.local_uf = olu[0] != '0';
   if (const char* ora = std::getenv("SWARMRL_AMD_ROT_AHEAD")) e->rot_ahead = ora[0] != '0';
+  // 2-D LDS builds without the local union-find: the pair-search blocks
+  // write their own regions of the list (no returning global atomic on the
+  // search's chain); SWARMRL_AMD_PAIR_REGIONS=0 turns it off
+  e->sc.pair_region = 0;
+  if (params->n_dims == 2 && !e->big_build && !e->sc.local_uf && n_particles <= 4096 &&
+      !(std::getenv("SWARMRL_AMD_PAIR_REGIONS") && std::getenv("SWARMRL_AMD_PAIR_REGIONS")[0] == '0'))
+    e->sc.pair_region = e->sc.pair_cap / ((n_particles + 255) / 256);
+  e->sc.rstamp = nullptr;
   e->sc.multi_species = params->n_species > 1 ? 1 : 0;
   // the 2-D build sort stages its scatter in LDS: the sorted rows of up to
   // K entries per pass beside the cell counts (K a multiple of 4, at least
@@ -1901,7 +1939,24 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     rc = rc ? rc : dev_alloc(e, &e->sc.gcell, M);
     rc = rc ? rc : dev_alloc(e, &e->sc.grank, M);
   }
+  // the ride-along pair search (k_vision_pairs) stages its env's sorted
+  // records in LDS when few envs leave it latency-bound and they fit
+  // (SWARMRL_AMD_PAIRS_STAGED=0|1 overrides)
+  {
+    const size_t pb = swarm::pairs_stage_words(n_particles, e->lxb, e->lyb) * sizeof(uint32_t);
+    const char* ov = std::getenv("SWARMRL_AMD_PAIRS_STAGED");
+    // off by default: the staged records' LDS keeps the cone's blocks from
+    // sharing a CU with a pair block (4096 colloids: 42.0 M vs 44.0 M)
+    bool want = false;
+    if (ov && ov[0] == '0') want = false;
+    if (ov && ov[0] == '1') want = true;
+    e->pairs_staged = want && params->n_dims == 2 && pb <= 96 * 1024;
+    if (e->pairs_staged)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vision_pairs<4, 16, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)pb);
+  }
   rc = rc ? rc : dev_alloc(e, &e->sc.gnpairs, (size_t)n_envs);
+  rc = rc ? rc : dev_alloc(e, &e->sc.gbcnt, (size_t)n_envs * ((n_particles + 255) / 256));
   if (e->big_build) rc = rc ? rc : dev_alloc(e, &e->sc.gclus, 3 * M);
   rc = rc ? rc : dev_alloc(e, &e->sc.wave_npairs, (size_t)n_envs * (S / 64));
   rc = rc ? rc : dev_alloc(e, &e->sc.phase, 32 + 4 * (size_t)n_envs * (S / 64));
@@ -2208,6 +2263,10 @@ int swarm_engine_profile(swarm_engine_t* e, int32_t enable, double* run_ms, int3
   // the launch stamps of captured run nodes (allocated here: never under capture)
   if (e->profile && !e->d_tstamp)
     HIP_TRY(hipMalloc(&e->d_tstamp, 2 * kMaxStamps * sizeof(unsigned long long)));
+  if (e->profile && !e->d_rstamp)
+    HIP_TRY(hipMalloc(&e->d_rstamp,
+                      2 * (size_t)kMaxStamps * swarm::kRoles * sizeof(unsigned long long)));
+  if (!e->profile) e->sc.rstamp = nullptr;
   return rc;
 }
 
@@ -2264,6 +2323,11 @@ int swarm_engine_profile_stamps(swarm_engine_t* e, int32_t reset, void* stream, 
   if (reset) {
     hipLaunchKernelGGL(k_stamp_reset, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), e->d_tstamp, n);
+    if (e->d_rstamp) {
+      const int nr = n * swarm::kRoles;
+      hipLaunchKernelGGL(k_stamp_reset, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0,
+                         reinterpret_cast<hipStream_t>(stream), e->d_rstamp, nr);
+    }
     HIP_TRY(hipGetLastError());
     return SWARM_OK;
   }
@@ -2278,6 +2342,40 @@ int swarm_engine_profile_stamps(swarm_engine_t* e, int32_t reset, void* stream, 
   if (khz <= 0) return fail(SWARM_EDEVICE, "no wall clock rate");
   for (int k = 0; k < n && k < cap; ++k)
     ms_out[k] = t[2 * k + 1] > t[2 * k] ? (float)((double)(t[2 * k + 1] - t[2 * k]) / khz) : 0.0f;
+  return SWARM_OK;
+}
+
+int swarm_engine_profile_roles(swarm_engine_t* e, double* us_out, int32_t cap,
+                               int32_t* n_roles) {
+  if (!e) return fail(SWARM_EINVAL, "null engine");
+  if (n_roles) *n_roles = swarm::kRoles;
+  const int n = e->stamp_next;
+  if (cap < 0 || (cap > 0 && !us_out)) return fail(SWARM_EINVAL, "us_out needs cap entries");
+  const size_t per = 2 * (size_t)swarm::kRoles;
+  for (int32_t k = 0; k < cap; ++k) us_out[k] = std::nan("");
+  if (!e->d_tstamp || !e->d_rstamp || n == 0) return SWARM_OK;
+  HIP_TRY(hipDeviceSynchronize());
+  std::vector<unsigned long long> t(2 * (size_t)n), r(per * n);
+  HIP_TRY(hipMemcpy(t.data(), e->d_tstamp, t.size() * sizeof(unsigned long long),
+                    hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(r.data(), e->d_rstamp, r.size() * sizeof(unsigned long long),
+                    hipMemcpyDeviceToHost));
+  int dev = 0, khz = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+  if (khz <= 0) return fail(SWARM_EDEVICE, "no wall clock rate");
+  const double us_per_tick = 1000.0 / khz;
+  for (int k = 0; k < n; ++k) {
+    const unsigned long long ref = t[2 * k + 1];  // end of the k-th run node
+    if (ref == 0) continue;
+    for (int q = 0; q < swarm::kRoles; ++q) {
+      const unsigned long long b = r[per * k + 2 * q], en = r[per * k + 2 * q + 1];
+      const size_t o = per * k + 2 * q;
+      if (b == ~0ull || en == 0 || o + 1 >= (size_t)cap) continue;
+      us_out[o] = ((double)b - (double)ref) * us_per_tick;
+      us_out[o + 1] = ((double)en - (double)ref) * us_per_tick;
+    }
+  }
   return SWARM_OK;
 }
 
@@ -2622,12 +2720,19 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
     hipLaunchKernelGGL(k_vision_grid, dim3(e->n_envs), dim3(1024), glds, e->stream, e->st, va);
     HIP_TRY(hipGetLastError());
   }
-  if (e->ride_stage == 2) {  // cone | pairs
+  if (e->ride_stage == 2) {  // pairs | cone
     const int nvb = (int)((total * 16 + 255) / 256);
     const int pbx = (e->n + 255) / 256;
-    hipLaunchKernelGGL((k_vision_pairs<4, 16>), dim3((unsigned)(nvb + pbx * e->n_envs)),
-                       dim3(256), 0, e->stream, e->st, e->d_derived, va, nvb, e->sc, e->lxb,
-                       e->lyb, pbx);
+    const int npb = pbx * e->n_envs;
+    const dim3 grid((unsigned)(nvb + npb));
+    if (e->pairs_staged) {
+      const size_t plds = swarm::pairs_stage_words(e->n, e->lxb, e->lyb) * sizeof(uint32_t);
+      hipLaunchKernelGGL((k_vision_pairs<4, 16, true>), grid, dim3(256), plds, e->stream, e->st,
+                         e->d_derived, va, npb, e->sc, e->lxb, e->lyb, pbx);
+    } else {
+      hipLaunchKernelGGL((k_vision_pairs<4, 16, false>), grid, dim3(256), 0, e->stream, e->st,
+                         e->d_derived, va, npb, e->sc, e->lxb, e->lyb, pbx);
+    }
     HIP_TRY(hipGetLastError());
     e->ride_stage = 3;
     return SWARM_OK;
@@ -2932,7 +3037,7 @@ int policy_launch(const float* obs, int32_t n, int32_t d_in, const float* w1, co
     const size_t plds = (size_t)(hidden * swarm::MlpRow<4, 4>::kStride + 4) * sizeof(float);
     const size_t lds = std::max(plds, build_lds_bytes(ride->n, ride->sc.pair_cap));
     hipLaunchKernelGGL((k_policy_cbuild<4, 4, 4>), dim3((unsigned)(pblocks + ride->n_envs)),
-                       dim3(1024), lds, s, m, pblocks, ride->st, ride->sc);
+                       dim3(1024), lds, s, m, ride->n_envs, ride->st, ride->sc);
     HIP_TRY(hipGetLastError());
     ride->ride_stage = 0;
     ride->prebuilt = true;
@@ -3083,31 +3188,36 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
   const int gae_blocks = (S + 255) / 256;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int NW = hidden <= 128 ? 1 : 2;  // waves of 128 units
-  const long tiles = ((long)n + 63) / 64;
-  // every block writes its partial row; the reduce reads exactly the rows written
-  const int blocks = (int)std::min<long>(tiles, swarm::kPpoBlocks);
+  const long tiles = ((long)n + 63) / 64;  // k_ppo_values_split: 64 samples a block
+  // k_ppo_grads: tiles of 128 samples; every block writes its partial row and
+  // the reduce reads exactly the rows written
+  // hidden <= 128: blocks of 4 tile waves (NT), else 2 unit waves (NW)
+  const int NT = NW == 1 ? 4 : 1;
+  const int blocks =
+      (int)std::min<long>((((long)n + 127) / 128 + NT - 1) / NT, swarm::kPpoBlocks);
   const unsigned vblocks = (unsigned)(((n + 1) / 2 + 255) / 256);
-  // pack the unit rows, V of every sample, GAE + dL/dV, then the gradients
+  // V of every sample, GAE + dL/dV (+ the table), then the gradients
 #define SWARM_PPO(NN, DD, KK)                                                                 \
   do {                                                                                        \
     using Tb = swarm::PpoTable<DD, KK>;                                                       \
-    hipLaunchKernelGGL((swarm::k_ppo_pack<DD, KK>),                                           \
-                       dim3((unsigned)((128 * NN * Tb::kStride + 255) / 256)), dim3(256), 0, \
-                       s, w1, b1, d_in, hidden, wa, k, wc, 128 * NN, table);                  \
+    const swarm::PpoPack pk{w1, b1, wa, wc, d_in, hidden, k, 128 * NN, table};                \
+    const int pack_blocks = (128 * NN * Tb::kStride + 255) / 256;                             \
+    const dim3 ggrid((unsigned)(gae_blocks + pack_blocks));                                   \
     if (n < (1 << 20))                                                                        \
-      hipLaunchKernelGGL((swarm::k_ppo_values_split<DD, KK>), dim3((unsigned)tiles),          \
-                         dim3(256), 0, s, x, n, d_in, table, hidden, bc, values);             \
+      hipLaunchKernelGGL((swarm::k_ppo_values_split<DD>), dim3((unsigned)tiles), dim3(256),   \
+                         0, s, x, n, d_in, w1, b1, hidden, wc, bc, values);                   \
     else                                                                                      \
-      hipLaunchKernelGGL((swarm::k_ppo_values<DD, KK>), dim3(vblocks), dim3(256), 0, s, x, n, \
-                         d_in, table, hidden, bc, values);                                    \
+      hipLaunchKernelGGL((swarm::k_ppo_values<DD>), dim3(vblocks), dim3(256), 0, s, x, n,     \
+                         d_in, w1, b1, hidden, wc, bc, values);                               \
     if (T <= 32)                                                                              \
-      hipLaunchKernelGGL(swarm::k_ppo_gae<32>, dim3((unsigned)gae_blocks), dim3(256), 0, s,   \
-                         rewards, values, T, S, gamma, lambda, adv, dv, spart);               \
+      hipLaunchKernelGGL((swarm::k_ppo_gae<32, DD, KK>), ggrid, dim3(256), 0, s, rewards,     \
+                         values, T, S, gamma, lambda, adv, dv, spart, gae_blocks, pk);        \
     else                                                                                      \
-      hipLaunchKernelGGL(swarm::k_ppo_gae<0>, dim3((unsigned)gae_blocks), dim3(256), 0, s,    \
-                         rewards, values, T, S, gamma, lambda, adv, dv, spart);               \
-    const void* fn = reinterpret_cast<const void*>(&swarm::k_ppo_grads<NN, DD, KK>);          \
-    const int lds = swarm::ppo_grads_lds_floats<NN, KK>() * (int)sizeof(float);               \
+      hipLaunchKernelGGL((swarm::k_ppo_gae<0, DD, KK>), ggrid, dim3(256), 0, s, rewards,      \
+                         values, T, S, gamma, lambda, adv, dv, spart, gae_blocks, pk);        \
+    constexpr int TT = NN == 1 ? 4 : 1;                                                       \
+    const void* fn = reinterpret_cast<const void*>(&swarm::k_ppo_grads<NN, TT, DD, KK>);      \
+    const int lds = swarm::ppo_grads_lds_floats<NN, TT, DD, KK>() * (int)sizeof(float);       \
     if (lds > 65536)                                                                          \
       (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);         \
     hipEvent_t ev0 = nullptr, ev1 = nullptr;                                                 \
@@ -3115,8 +3225,8 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
         hipEventCreate(&ev1) == hipSuccess)                                                   \
       (void)hipEventRecord(ev0, s);                                                           \
     for (int rep = 0; rep < (ev1 ? g_ppo_prof.reps : 1); ++rep) /* same partial rows */      \
-      hipLaunchKernelGGL((swarm::k_ppo_grads<NN, DD, KK>), dim3((unsigned)blocks),           \
-                         dim3(64 * NN),                                                       \
+      hipLaunchKernelGGL((swarm::k_ppo_grads<NN, TT, DD, KK>), dim3((unsigned)blocks),       \
+                         dim3(64 * NN * TT),                                                  \
                          (size_t)lds, s, x, n, d_in, w1, b1, hidden, wa, ba, k, wc, bc,       \
                          actions, old_logp, adv, dv, spart, gae_blocks, table, clip_eps,      \
                          entropy_coef, partial);                                              \

@@ -221,6 +221,11 @@ struct Scratch {
   uint32_t* xpairs;   // [E][pair_cap] cross-block pairs i | j << 16
   int32_t* gnx;       // [E] cross-block pairs found
   int32_t local_uf;   // 1: the 2-D pair search unions its blocks' pairs (lroot, xpairs)
+  // > 0 (2-D, no local union-find, LDS cluster build): pair-search block b of
+  // env e writes its pairs to gplist[e][b * pair_region ...] and their count
+  // to gbcnt[e][b] -- no returning global atomic; the build gathers them
+  int32_t pair_region;
+  int32_t* gbcnt;     // [E][ceil(N / 256)] pairs found per pair-search block
   int32_t* gclus;     // [3][M] cluster sizes / bases / slots (large-N build only)
   int32_t pair_cap;   // pairs per env
   int32_t one_pass;   // 1: pack clusters so that a wave has <= 64 pairs
@@ -232,7 +237,31 @@ struct Scratch {
   int32_t S;          // slots per env
   int32_t wmax;       // S / 64
   uint64_t* phase;    // [32] build phase stamps (SWARM_PHASE_TIMING builds only)
+  // profiling only (else null): [kRoles][2] earliest start / latest end
+  // (device wall clock) of each workgroup role of the launches of one window
+  unsigned long long* rstamp;
 };
+
+// Workgroup roles of the window's launches (role_begin / role_end, rstamp)
+enum RoleId {
+  kRoleCheck = 0,
+  kRoleSort,
+  kRoleVgrid,
+  kRoleField,
+  kRolePairs,
+  kRoleCone,
+  kRoleCbuild,
+  kRoleMlp,
+  kRoles
+};
+
+__device__ __forceinline__ void role_begin(const Scratch& sc, int r) {
+  if (sc.rstamp && threadIdx.x == 0) atomicMin(&sc.rstamp[2 * r], (unsigned long long)wall_clock64());
+}
+__device__ __forceinline__ void role_end(const Scratch& sc, int r) {
+  if (sc.rstamp && (threadIdx.x & 63) == 0)
+    atomicMax(&sc.rstamp[2 * r + 1], (unsigned long long)wall_clock64());
+}
 
 #ifdef SWARM_PHASE_TIMING
 #define SWARM_STAMP(k)                                                    \
@@ -1296,9 +1325,20 @@ __global__ __launch_bounds__(1024) void k_build_sort(DevState st, Scratch sc, in
 // wave with a denser thread rescans to write.
 // Body for block bx of env e (k_build_pairs: grid (ceil(N / blockDim), E);
 // fused launches pass their own block index); nb2: a block-shared table.
+// kStaged (latency-bound launches, few envs): the env's sorted records and
+// cell starts are first copied into LDS (`stage`, pairs_stage_words(N, lx,
+// ly) words) by coalesced loads in flight together, so the dependent chain
+// own record -> cell bounds -> candidates reads LDS instead of three rounds
+// of memory latency.
+__host__ __device__ inline size_t pairs_stage_words(int n, int lx, int ly) {
+  return 3 * (size_t)n + ((size_t)1 << (lx + ly)) + 1;
+}
+
+template <bool kStaged = false>
 __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, const DevState& st,
                                                  const Scratch& sc, int lx, int ly, int bx, int e,
-                                                 float* nb2, int32_t* uf) {
+                                                 float* nb2, int32_t* uf,
+                                                 uint32_t* stage = nullptr) {
   constexpr int kKeep = 8;
   for (int k = threadIdx.x; k < kMaxSpecies * kMaxSpecies; k += blockDim.x) nb2[k] = d->nb2[k];
   const int N = st.n;
@@ -1308,7 +1348,26 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
   const bool valid = ps < N;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly);
-  const int32_t* cs = sc.bcstart + (size_t)e * (ncell + 1);
+  const int32_t* gcs = sc.bcstart + (size_t)e * (ncell + 1);
+  if constexpr (kStaged) {
+#pragma unroll 4
+    for (int k = t; k < N; k += T) {
+      const uint32_t x = sc.bsq[base + k], y = sc.bsq[M + base + k];
+      const int32_t id = sc.bsid[base + k];
+      stage[k] = x;
+      stage[N + k] = y;
+      stage[2 * N + k] = (uint32_t)id;
+    }
+    for (int k = t; k <= ncell; k += T) stage[3 * N + k] = (uint32_t)gcs[k];
+    __syncthreads();
+  }
+  // the sorted records (x, y, id) and cell starts, from LDS or memory
+  auto QX = [&](int j) -> uint32_t { return kStaged ? stage[j] : sc.bsq[base + j]; };
+  auto QY = [&](int j) -> uint32_t { return kStaged ? stage[N + j] : sc.bsq[M + base + j]; };
+  auto SID = [&](int j) -> int32_t {
+    return kStaged ? (int32_t)stage[2 * N + j] : sc.bsid[base + j];
+  };
+  auto CS = [&](int c) -> int32_t { return kStaged ? (int32_t)stage[3 * N + c] : gcs[c]; };
   const int ncx = 1 << lx, ncy = 1 << ly;
   const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
   const float sx0 = d->sx[0], sx1 = d->sx[1];
@@ -1320,10 +1379,10 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
   uint32_t qx = 0, qy = 0;
   int32_t ix = 0, iy = 0;
   if (valid) {
-    pk = sc.bsid[base + ps];
+    pk = SID(ps);
     i = pk & 0xffffff;
-    qx = sc.bsq[base + ps];
-    qy = sc.bsq[M + base + ps];
+    qx = QX(ps);
+    qy = QY(ps);
     if (!per) {
       ix = st.img[base + i];
       iy = st.img[M + base + i];
@@ -1343,8 +1402,8 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
                      (per || (cy + oy >= 0 && cy + oy < ncy));
     const int row = ((cy + oy + ncy) & (ncy - 1)) << lx;
     const int c_lo = row | (part == 0 ? xa : xw), c_hi = row | (part == 0 ? xb : xw);
-    rb[r] = use ? cs[c_lo] : 0;
-    re[r] = use ? cs[c_hi + 1] : 0;
+    rb[r] = use ? CS(c_lo) : 0;
+    re[r] = use ? CS(c_hi + 1) : 0;
   }
   __syncthreads();  // nb2
   const float* nb2_row = nb2 + (pk >> 24) * kMaxSpecies;
@@ -1355,9 +1414,9 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
   // the six ranges as one flat candidate index f in [0, total), record
   // jj = f + off[r] of the range r holding f: kFly candidates in flight per
   // iteration whatever the split over the ranges (about 11 candidates at
-  // area fraction 0.1: two rounds of loads, not one per range)
+  // area fraction 0.1: one round of loads, not one per range)
 #ifndef SWARM_PAIRS_FLY
-#define SWARM_PAIRS_FLY 8
+#define SWARM_PAIRS_FLY 16
 #endif
   constexpr int kFly = SWARM_PAIRS_FLY;
   int off[6], pre[7];
@@ -1380,9 +1439,9 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
       const int jj = f + o;
       const bool ok = f < total;
       jj4[u] = jj;
-      pk4[u] = ok ? sc.bsid[base + jj] : -1;
-      x4[u] = ok ? sc.bsq[base + jj] : 0u;
-      y4[u] = ok ? sc.bsq[M + base + jj] : 0u;
+      pk4[u] = ok ? SID(jj) : -1;
+      x4[u] = ok ? QX(jj) : 0u;
+      y4[u] = ok ? QY(jj) : 0u;
     }
 #pragma unroll
     for (int u = 0; u < kFly; ++u) {
@@ -1409,15 +1468,33 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
     int v = found;
     v = wave_incl_scan(v);
     int wbase = 0;
-    if (lane == 63) wbase = atomicAdd(&sc.gnpairs[e], v);
-    wbase = __builtin_amdgcn_readlane(wbase, 63);
-    const int my_off = wbase + v - found;
     uint32_t* out = sc.gplist + (size_t)e * sc.pair_cap;
+    int cap = sc.pair_cap;
+    if (sc.pair_region > 0) {
+      // this block's own region of the list and its count (no returning
+      // global atomic): the waves' totals scanned in LDS (uf is free here)
+      const int wv = threadIdx.x >> 6, nw = (T + 63) >> 6;
+      if (lane == 63) uf[wv] = v;
+      __syncthreads();
+      int tot = 0;
+      for (int q = 0; q < nw; ++q) {
+        const int c = uf[q];
+        wbase += q < wv ? c : 0;
+        tot += c;
+      }
+      if (threadIdx.x == 0) sc.gbcnt[(size_t)e * ((N + T - 1) / T) + bx] = tot;
+      out += (size_t)bx * sc.pair_region;
+      cap = sc.pair_region;  // a fuller block: the build sees count > region
+    } else {
+      if (lane == 63) wbase = atomicAdd(&sc.gnpairs[e], v);
+      wbase = __builtin_amdgcn_readlane(wbase, 63);
+    }
+    const int my_off = wbase + v - found;
     if (!dense) {
 #pragma unroll
       for (int u = 0; u < kKeep; ++u) {
         const int k = my_off + u;
-        if (u < found && k < sc.pair_cap) out[k] = (uint32_t)i | ((keep[u] & 0xffffu) << 16);
+        if (u < found && k < cap) out[k] = (uint32_t)i | ((keep[u] & 0xffffu) << 16);
       }
       return;
     }
@@ -1425,16 +1502,15 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
       for (int jj = rb[r]; jj < re[r]; ++jj) {
-        const int packed = sc.bsid[base + jj];
+        const int packed = SID(jj);
         const int j = packed & 0xffffff;
-        const float rx = per ? (float)(int32_t)(sc.bsq[base + jj] - qx) * sx0
-                             : pair_disp(sc.bsq[base + jj], st.img[base + j], qx, ix, sx0, false);
-        const float ry = per ? (float)(int32_t)(sc.bsq[M + base + jj] - qy) * sx1
-                             : pair_disp(sc.bsq[M + base + jj], st.img[M + base + j], qy, iy,
-                                         sx1, false);
+        const float rx = per ? (float)(int32_t)(QX(jj) - qx) * sx0
+                             : pair_disp(QX(jj), st.img[base + j], qx, ix, sx0, false);
+        const float ry = per ? (float)(int32_t)(QY(jj) - qy) * sx1
+                             : pair_disp(QY(jj), st.img[M + base + j], qy, iy, sx1, false);
         if (i < j && rx * rx + ry * ry < nb2_row[packed >> 24]) {
           const int k = my_off + w;
-          if (k < sc.pair_cap) out[k] = (uint32_t)i | ((uint32_t)j << 16);
+          if (k < cap) out[k] = (uint32_t)i | ((uint32_t)j << 16);
           ++w;
         }
       }
@@ -1502,13 +1578,12 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     for (int jj = rb[r]; jj < re[r]; ++jj) {
-      const int packed = sc.bsid[base + jj];
+      const int packed = SID(jj);
       const int j = packed & 0xffffff;
-      const float rx = per ? (float)(int32_t)(sc.bsq[base + jj] - qx) * sx0
-                           : pair_disp(sc.bsq[base + jj], st.img[base + j], qx, ix, sx0, false);
-      const float ry = per ? (float)(int32_t)(sc.bsq[M + base + jj] - qy) * sx1
-                           : pair_disp(sc.bsq[M + base + jj], st.img[M + base + j], qy, iy, sx1,
-                                       false);
+      const float rx = per ? (float)(int32_t)(QX(jj) - qx) * sx0
+                           : pair_disp(QX(jj), st.img[base + j], qx, ix, sx0, false);
+      const float ry = per ? (float)(int32_t)(QY(jj) - qy) * sx1
+                           : pair_disp(QY(jj), st.img[M + base + j], qy, iy, sx1, false);
       if (i < j && rx * rx + ry * ry < nb2_row[packed >> 24]) {
         const int k = my_off + w;
         if (k < sc.pair_cap) out[k] = (uint32_t)i | ((uint32_t)j << 16);
@@ -1560,6 +1635,24 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
                          : reinterpret_cast<uint32_t*>(parent + 4 * N);  // pair_cap
   const int S = sc.S;
   SWARM_STAMP(6);
+  // region lists (sc.pair_region): the blocks' counts, their prefix sums in
+  // freebase (free until the packing), the total as `found`
+  const bool regions = !kBig && kCopy && sc.pair_region > 0;
+  const int nreg = (N + 255) / 256;
+  if (regions) {
+    if (tid < 64) {
+      const int c = tid < nreg ? sc.gbcnt[(size_t)e * nreg + tid] : 0;
+      const int v = wave_incl_scan(c);
+      freebase[tid] = v - c;
+      const bool over = __any(c > sc.pair_region);
+      if (tid == 63) {
+        freebase[64] = v;
+        misc[7] = over ? 1 : 0;
+      }
+    }
+    __syncthreads();
+    found = misc[7] ? sc.pair_cap + 1 : freebase[64];
+  }
   const int npairs = min(found, sc.pair_cap);
   // kLocal: the pair search's blocks unioned their own pairs already
   // (sc.lroot: a forest of depth one), only the cross-block pairs remain
@@ -1567,8 +1660,9 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   const uint32_t* xl = sc.xpairs + (size_t)e * sc.pair_cap;
   for (int k = tid; k < 68; k += T) classcnt[k] = 0;
   for (int k = tid; k < wmax; k += T) wave_np[k] = 0;
-  // overflow of the pair or cross list -> global path
-  if (tid < 16) misc[tid] = tid == 0 && (found > sc.pair_cap || nx > sc.pair_cap) ? 1 : 0;
+  // overflow of the pair or cross list -> global path (misc[7]: read above)
+  if (tid < 16 && tid != 7)
+    misc[tid] = tid == 0 && (found > sc.pair_cap || nx > sc.pair_cap) ? 1 : 0;
   for (int i = tid; i < N; i += T) {
     if (kLocal) {
       const uint32_t l = (uint32_t)sc.lroot[base + i];
@@ -1580,7 +1674,22 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
     csz[i] = 0;
     cbase[i] = 0;  // pair count of a cluster (one-pass packing), then its base
   }
-  if (!kBig && kCopy) {  // pair list into LDS, four loads in flight per thread
+  if (regions) {  // each wave gathers whole regions, four loads in flight per lane
+    const uint32_t* gp = sc.gplist + (size_t)e * sc.pair_cap;
+    const int lane = tid & 63, nw = T >> 6;
+    for (int b = tid >> 6; b < nreg; b += nw) {
+      const int c = freebase[b + 1] - freebase[b], o = freebase[b];
+      const uint32_t* src = gp + (size_t)b * sc.pair_region;
+      for (int k0 = lane; k0 < c; k0 += 4 * 64) {
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = k0 + u * 64 < c ? src[k0 + u * 64] : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (k0 + u * 64 < c && o + k0 + u * 64 < npairs) plist[o + k0 + u * 64] = v[u];
+      }
+    }
+  } else if (!kBig && kCopy) {  // pair list into LDS, four loads in flight per thread
     const uint32_t* gp = sc.gplist + (size_t)e * sc.pair_cap;
     for (int k0 = tid; k0 < npairs; k0 += 4 * T) {
       uint32_t v[4];
@@ -3306,6 +3415,7 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
   __shared__ PairTables pt;
   const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
+  role_begin(sc, kRoleCheck);
   // every load the test starts from is issued here together -- the window
   // counters, the build's flags, the mover count and list (written by the
   // run kernel) and the pair tables: one memory latency, not a chain
@@ -3501,6 +3611,7 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
   __syncthreads();  // every read of nmov above is done
   if (tid == 0) sc.nmov[e] = 0;
   advance_counter(step_ctr, arrive, step0, n_steps);
+  role_end(sc, kRoleCheck);
 }
 
 }  // namespace swarm

@@ -25,10 +25,11 @@
 //                 sums in a fixed order: deterministic), torch layouts
 //
 // The loss is a sum over samples, so its gradient is the sum of the
-// per-sample gradients; the caller's optimizer takes the step.  Before them,
-// k_ppo_pack lays the parameters out as per-unit rows (the wave-uniform
-// scalar-load operands of the sample-major loops).  All fp32 arithmetic with
-// explicit fmaf; cross-sample sums in a fixed order (run-to-run identical).
+// per-sample gradients; the caller's optimizer takes the step.  Each unit's
+// parameters are read as wave-uniform scalar loads by the sample-major loops
+// (for the gradient kernel from a per-unit table laid out beside the GAE).
+// All fp32 arithmetic with explicit fmaf; cross-sample sums in a fixed order
+// (run-to-run identical).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -39,15 +40,16 @@ namespace swarm {
 constexpr int kPpoMaxIn = 32;
 constexpr int kPpoMaxK = 16;
 constexpr int kPpoMaxHidden = 256;
-constexpr int kPpoBlocks = 2048;  // grad blocks (one or two waves each)
+constexpr int kPpoBlocks = 2048;  // grad blocks (four tile waves or two unit waves each)
 
 // Gradient layout (floats): W1 [H][D] | b1 [H] | Wa [K][H] | ba [K] | Wc [H] | bc
 __host__ __device__ inline int ppo_grad_size(int d, int h, int k) {
   return h * d + h + k * h + k + h + 1;
 }
 
-// Per-unit parameter rows, the wave-uniform operands of the sample-major
-// loops (one scalar-load row per unit): [Wa[:, u], Wc[u], 0 ... | W1[u, :], b1[u], 0 ...]
+// Per-unit parameter rows, the wave-uniform operands of the gradient
+// kernel's sample-major loop (one scalar-load row per unit):
+// [Wa[:, u], Wc[u], 0 ... | W1[u, :], b1[u], 0 ...]
 template <int D, int K>
 struct PpoTable {
   static constexpr int kHeads = (K + 1 + 7) / 8 * 8;
@@ -56,15 +58,15 @@ struct PpoTable {
   static constexpr int kStride = kHeads + (D + 1 + 7) / 8 * 8;
 };
 
-// rows = hidden rounded up to the grads block (zero rows past hidden)
+// Entry t of the table (rows = hidden rounded up to the grads block, zero
+// rows past hidden); written by extra workgroups of the GAE launch.
 template <int D, int K>
-__global__ __launch_bounds__(256) void k_ppo_pack(const float* __restrict__ w1,
-                                                  const float* __restrict__ b1, int d,
-                                                  int hidden, const float* __restrict__ wa,
-                                                  int k, const float* __restrict__ wc, int rows,
-                                                  float* __restrict__ table) {
+__device__ __forceinline__ void ppo_pack_entry(const float* __restrict__ w1,
+                                               const float* __restrict__ b1, int d, int hidden,
+                                               const float* __restrict__ wa, int k,
+                                               const float* __restrict__ wc, int rows, int t,
+                                               float* __restrict__ table) {
   using Tb = PpoTable<D, K>;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= rows * Tb::kStride) return;
   const int u = t / Tb::kStride, col = t - u * Tb::kStride;
   float v = 0.0f;
@@ -84,14 +86,15 @@ __global__ __launch_bounds__(256) void k_ppo_pack(const float* __restrict__ w1,
 typedef float ppo_f2 __attribute__((ext_vector_type(2)));
 
 // V of every sample: one thread per two adjacent samples (packed fp32 FMAs,
-// v_pk_fma_f32), their features in registers, the unit rows wave-uniform
-// scalar loads.
-template <int D, int K>
+// v_pk_fma_f32), their features in registers, each unit's parameters
+// wave-uniform scalar loads.
+template <int D>
 __global__ __launch_bounds__(256) void k_ppo_values(const float* __restrict__ x, int n, int d,
-                                                    const float* __restrict__ table, int hidden,
+                                                    const float* __restrict__ w1,
+                                                    const float* __restrict__ b1, int hidden,
+                                                    const float* __restrict__ wc,
                                                     const float* __restrict__ bc,
                                                     float* __restrict__ values) {
-  using Tb = PpoTable<D, K>;
   const long s = 2 * ((long)blockIdx.x * blockDim.x + threadIdx.x);
   if (s >= n) return;
   const long s1 = min(s + 1, (long)n - 1);  // an odd n pairs the last sample with itself
@@ -106,12 +109,12 @@ __global__ __launch_bounds__(256) void k_ppo_values(const float* __restrict__ x,
   ppo_f2 v = bc[0];
 #pragma unroll 4
   for (int j = 0; j < hidden; ++j) {
-    const float* row = table + (size_t)j * Tb::kStride;
-    ppo_f2 h = row[Tb::kB1];
+    ppo_f2 h = b1[j];
 #pragma unroll
-    for (int c = 0; c < D; ++c) h = __builtin_elementwise_fma((ppo_f2)row[Tb::kW1 + c], xs[c], h);
+    for (int c = 0; c < D; ++c)  // clamped load: a feature c >= d is zero
+      h = __builtin_elementwise_fma((ppo_f2)w1[(size_t)j * d + min(c, d - 1)], xs[c], h);
     h = __builtin_elementwise_max(h, (ppo_f2)0.0f);
-    v = __builtin_elementwise_fma((ppo_f2)row[K], h, v);
+    v = __builtin_elementwise_fma((ppo_f2)wc[j], h, v);
   }
   values[s] = v.x;
   if (s + 1 < n) values[s + 1] = v.y;
@@ -121,14 +124,14 @@ __global__ __launch_bounds__(256) void k_ppo_values(const float* __restrict__ x,
 // the latency: a workgroup of 4 waves takes 64 samples (lane = sample) and
 // wave w sums units [w H/4, (w + 1) H/4) (wave-uniform rows); the four
 // partials are added in a fixed order.
-template <int D, int K>
+template <int D>
 __global__ __launch_bounds__(256) void k_ppo_values_split(const float* __restrict__ x, int n,
-                                                          int d,
-                                                          const float* __restrict__ table,
+                                                          int d, const float* __restrict__ w1,
+                                                          const float* __restrict__ b1,
                                                           int hidden,
+                                                          const float* __restrict__ wc,
                                                           const float* __restrict__ bc,
                                                           float* __restrict__ values) {
-  using Tb = PpoTable<D, K>;
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -144,11 +147,11 @@ __global__ __launch_bounds__(256) void k_ppo_values_split(const float* __restric
   float v = 0.0f;
 #pragma unroll 4
   for (int j = j0; j < j1; ++j) {
-    const float* row = table + (size_t)j * Tb::kStride;
-    float h = row[Tb::kB1];
+    float h = b1[j];
 #pragma unroll
-    for (int c = 0; c < D; ++c) h = fmaf(row[Tb::kW1 + c], xs[c], h);
-    v = fmaf(row[K], fmaxf(h, 0.0f), v);
+    for (int c = 0; c < D; ++c)  // clamped load: a feature c >= d is zero
+      h = fmaf(w1[(size_t)j * d + min(c, d - 1)], xs[c], h);
+    v = fmaf(wc[j], fmaxf(h, 0.0f), v);
   }
   red[w][lane] = v;
   __syncthreads();
@@ -163,13 +166,27 @@ __global__ __launch_bounds__(256) void k_ppo_values_split(const float* __restric
 // TM > 0: the column's T <= TM rewards and values are loaded into registers
 // up front (one memory latency instead of a dependent chain of T); the
 // arithmetic is the same in either form.
-template <int TM>
+// Workgroups past n_gae (blockIdx.x >= n_gae) lay out the gradient
+// kernel's parameter table instead (PpoPack: no launch of their own).
+struct PpoPack {
+  const float *w1, *b1, *wa, *wc;
+  int d, hidden, k, rows;
+  float* table;
+};
+
+template <int TM, int D, int K>
 __global__ __launch_bounds__(256) void k_ppo_gae(const float* __restrict__ rewards,
                                                  const float* __restrict__ values, int T, int S,
                                                  float gamma, float lambda,
                                                  float* __restrict__ adv, float* __restrict__ dv,
-                                                 double* __restrict__ part) {
+                                                 double* __restrict__ part, int n_gae,
+                                                 PpoPack pk) {
   __shared__ double red[2][4];
+  if ((int)blockIdx.x >= n_gae) {
+    ppo_pack_entry<D, K>(pk.w1, pk.b1, pk.d, pk.hidden, pk.wa, pk.k, pk.wc, pk.rows,
+                         ((int)blockIdx.x - n_gae) * blockDim.x + threadIdx.x, pk.table);
+    return;
+  }
   const int col = blockIdx.x * blockDim.x + threadIdx.x;
   double s1 = 0.0, s2 = 0.0;
   const float gl = gamma * lambda, g1 = gamma * (1.0f - lambda);
@@ -276,42 +293,69 @@ __device__ inline void ppo_advantage_sums(const double* __restrict__ part, int n
   out[1] = b;
 }
 
-// Value of lane l of a wave (v_readlane: wave-uniform result).
-__device__ __forceinline__ float lane_value(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-
-template <int K>
-struct PpoHeads {
-  static constexpr int kP = K + 1;                  // logits + value
-  static constexpr int kRow = (K + 1 + 3) / 4 * 4;  // a sample's dL/d(heads) row in LDS
+// A sample's row in LDS: dL/d(logits) [K] | dL/dV | features [D], padded to
+// whole float4s (read back by every lane at one address: a broadcast).
+template <int D, int K>
+struct PpoRow {
+  static constexpr int kRow = (K + 1 + D + 3) / 4 * 4;
 };
 
-template <int NW, int K>
+// Floats a lane hands over in the final combine of a block's tile waves.
+template <int D, int K>
+__host__ __device__ constexpr int ppo_combine_floats() {
+  return 2 * (D + 1 + K + 1) + K + 1;
+}
+
+template <int NW, int NT, int D, int K>
 __host__ __device__ constexpr int ppo_grads_lds_floats() {
-  // per-wave H half-block transpose [64][65] | head partials of waves 1..
-  // [K+1][64] | dL/d(logits, value) [64][kRow]
-  return NW * 64 * 65 + (NW - 1) * (K + 1) * 64 + 64 * PpoHeads<K>::kRow;
+  // per tile wave: sample rows [128][kRow] | logit partials of unit waves 1..
+  // [NW - 1][K][128]; after the tiles, the combine buffer [kC][64] aliases them
+  return NT * 128 * PpoRow<D, K>::kRow + (NW - 1) * K * 128 >
+                 (NT > 1 ? 64 * ppo_combine_floats<D, K>() : 0)
+             ? NT * 128 * PpoRow<D, K>::kRow + (NW - 1) * K * 128
+             : 64 * ppo_combine_floats<D, K>();
+}
+
+// The LDS hand-over between the phases of one tile: the whole block when
+// units are split over NW > 1 waves, else the one wave that owns the tile
+// (LDS operations of a wave complete in order; the fences keep the compiler
+// from moving memory operations across).
+template <int NW>
+__device__ __forceinline__ void ppo_group_sync() {
+  if constexpr (NW > 1) {
+    __syncthreads();
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
 }
 
 __device__ __forceinline__ ppo_f2 ppo_splat(float v) { return ppo_f2{v, v}; }
 
-// Per-block parameter gradients; NW waves, each owning 128 hidden units --
-// thread (w, lane) holds units u0 = 128 w + lane and u1 = u0 + 64 as the two
-// halves of packed fp32 registers, so every broadcast operand feeds a
-// v_pk_fma_f32 for two units.  Dynamic LDS ppo_grads_lds_floats<NW, K>()
-// floats; partial: [gridDim.x][ppo_grad_size].  Tiles of 64 samples:
-//   A  h of both units for the tile's 64 samples into registers, each
-//      sample's features broadcast from its lane by v_readlane
-//   B  lane = sample: the heads' partial sums over the wave's 128 units, H
-//      transposed through LDS one 64-unit half at a time, the unit's head
-//      weights one scalar-load row of the packed table; wave 0 adds the other
-//      waves' partials (fixed order) and forms dL/dz, dL/dV of its lane's
-//      sample
-//   C  gradient accumulation over the 64 samples, dL/dz of each broadcast by
-//      v_readlane
-template <int NW, int D, int K>
-__global__ __launch_bounds__(64 * NW) void k_ppo_grads(
+// Per-block parameter gradients.  NW waves each own 128 hidden units of a
+// tile (hidden > 128), or (NW = 1) NT waves each take their own tiles and
+// add their sums in a fixed order at the end.  Dynamic LDS
+// ppo_grads_lds_floats<NW, NT, D, K>() floats; partial: [gridDim.x][ppo_grad_size].  Tiles of 128 samples, three phases, no
+// cross-lane broadcasts (v_readlane) and no transposes:
+//   F  lane = the sample pair (s, s + 64) as the two halves of packed fp32
+//      registers: the logits over the wave's units, each unit's hidden
+//      activation recomputed from its wave-uniform table row (scalar loads)
+//      -- D + 1 + K v_pk_fma_f32 per unit and pair.  The value head is not
+//      needed: dL/dV comes from k_ppo_gae.
+//   P  wave 0, lane = sample: the other waves' logit partials added in a
+//      fixed order, dL/dz of the clipped surrogate and the entropy term, the
+//      output-bias sums; each sample's row [dL/dz, dL/dV, x] to LDS
+//   B  lane = the unit pair (u, u + 64), the 128 samples in order: each row
+//      read by every lane at one address (LDS broadcast, float4), h
+//      recomputed, then dWo += g h, dh = Wo g (masked by h > 0), db1 += dh,
+//      dW1 += dh x -- packed FMAs over the two units.
+// Every sum runs in a fixed order (run-to-run identical).  The tensor shapes
+// (1-128-(4+1) stock) make matrix cores a poor fit: the heads' 5 columns
+// would fill 5 of every 16 rows of a v_mfma_f32_16x16x4_f32, whose f32 rate
+// is the packed-VALU rate on gfx950 (MI355X_MICROARCH.md, "Peak FP32").
+template <int NW, int NT, int D, int K>
+__global__ __launch_bounds__(64 * NW * NT) void k_ppo_grads(
     const float* __restrict__ x, int n, int d, const float* __restrict__ w1,
     const float* __restrict__ b1, int hidden, const float* __restrict__ wa,
     const float* __restrict__ ba, int k, const float* __restrict__ wc,
@@ -319,13 +363,16 @@ __global__ __launch_bounds__(64 * NW) void k_ppo_grads(
     const float* __restrict__ old_logp, const float* __restrict__ adv,
     const float* __restrict__ dvalue, const double* __restrict__ gae_part, int n_part,
     const float* __restrict__ table, float clip_eps, float c_ent, float* __restrict__ partial) {
-  constexpr int KP = K + 1, kTab = PpoTable<D, K>::kStride, kRow = PpoHeads<K>::kRow;
+  using Tb = PpoTable<D, K>;
+  constexpr int KP = K + 1, kTab = Tb::kStride, kRow = PpoRow<D, K>::kRow;
   extern __shared__ float ppo_lds[];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  static_assert(NW == 1 || NT == 1, "tile waves or unit waves, not both");
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int w = NW > 1 ? wid : 0;  // unit wave
+  const int t = NW > 1 ? 0 : wid;  // tile wave
   const int wu = __builtin_amdgcn_readfirstlane(w);
-  float* sh = ppo_lds + w * 64 * 65;   // this wave's H half-block, [sample][unit]
-  float* red = ppo_lds + NW * 64 * 65; // [NW - 1][KP][64]
-  float* sz = red + (NW - 1) * KP * 64;
+  float* srow = ppo_lds + t * 128 * kRow;     // [128][kRow]
+  float* red = ppo_lds + NT * 128 * kRow;     // [NW - 1][K][128]
   const int u0 = 128 * w + lane, u1 = u0 + 64;
   const bool in0 = u0 < hidden, in1 = u1 < hidden;
   ppo_f2 w1p[D], wop[KP];
@@ -340,9 +387,9 @@ __global__ __launch_bounds__(64 * NW) void k_ppo_grads(
     const bool live = q < k || q == K;
     wop[q] = ppo_f2{live && in0 ? col[u0] : 0.0f, live && in1 ? col[u1] : 0.0f};
   }
-  float bo[KP];
+  float bo[K];
 #pragma unroll
-  for (int q = 0; q < KP; ++q) bo[q] = q < k ? ba[q] : (q == K ? bc[0] : 0.0f);
+  for (int q = 0; q < K; ++q) bo[q] = q < k ? ba[q] : 0.0f;
   // normalised advantages (A - mean) / (std + eps): population std, fp32 eps
   double stats[2];
   ppo_advantage_sums(gae_part, n_part, stats);
@@ -359,129 +406,135 @@ __global__ __launch_bounds__(64 * NW) void k_ppo_grads(
     gwop[q] = ppo_splat(0.0f);
     gbias[q] = 0.0f;
   }
-  const float* rows = table + (size_t)wu * 128 * kTab;
-  const long tiles = ((long)n + 63) / 64;
-  for (long tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-    const long si = tile * 64 + lane;
-    const bool valid = si < n;
-    float xr[D];
+  // this wave's unit rows (zero rows past hidden up to 128 NW), whole quads
+  const float* urows = table + (size_t)wu * 128 * kTab;
+  const int nunits = (min(128, hidden - 128 * wu) + 3) & ~3;
+  const long tiles = ((long)n + 127) / 128;
+  for (long tile = (long)blockIdx.x * NT + t; tile < tiles; tile += (long)gridDim.x * NT) {
+    const long sa = tile * 128 + lane, sb = sa + 64;
+    ppo_f2 xs[D];
     {
       // clamped loads and a select, no branches (a feature c >= d meets a
       // zero weight; a sample past n has dL/dz = 0 below, so adds nothing)
-      const float* xs = x + (size_t)min(si, (long)n - 1) * d;
+      const float* xa = x + (size_t)min(sa, (long)n - 1) * d;
+      const float* xb = x + (size_t)min(sb, (long)n - 1) * d;
 #pragma unroll
       for (int c = 0; c < D; ++c) {
-        const float v = xs[min(c, d - 1)];
-        xr[c] = c < d ? v : 0.0f;
+        const float va = xa[min(c, d - 1)], vb = xb[min(c, d - 1)];
+        xs[c] = c < d ? ppo_f2{va, vb} : ppo_splat(0.0f);
       }
     }
-    // A: hidden activations of both units for the 64 samples
-    ppo_f2 hs[64];
+    // F: logits of the sample pair over this wave's units
+    ppo_f2 z[K];
 #pragma unroll
-    for (int s = 0; s < 64; ++s) {
-      ppo_f2 h = b1p;
-#pragma unroll
-      for (int c = 0; c < D; ++c)
-        h = __builtin_elementwise_fma(w1p[c], ppo_splat(lane_value(xr[c], s)), h);
-      hs[s] = __builtin_elementwise_max(h, ppo_splat(0.0f));
-    }
-    // B: heads, lane = sample, the wave's units one 64-unit half at a time
-    float acc[KP];
-#pragma unroll
-    for (int q = 0; q < KP; ++q) acc[q] = 0.0f;
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      if (half) __syncthreads();  // the first half's readers are done
-#pragma unroll
-      for (int s = 0; s < 64; ++s) sh[s * 65 + lane] = half ? hs[s].y : hs[s].x;
-      __syncthreads();
-      const float* row = rows + (size_t)half * 64 * kTab;
+    for (int q = 0; q < K; ++q) z[q] = ppo_splat(0.0f);
 #pragma unroll 4
-      for (int u = 0; u < 64; ++u) {
-        const float h = sh[lane * 65 + u];
+    for (int u = 0; u < nunits; ++u) {
+      const float* r = urows + (size_t)u * kTab;
+      ppo_f2 h = ppo_splat(r[Tb::kB1]);
 #pragma unroll
-        for (int q = 0; q < KP; ++q) acc[q] = fmaf(row[u * kTab + q], h, acc[q]);
-      }
+      for (int c = 0; c < D; ++c) h = __builtin_elementwise_fma(ppo_splat(r[Tb::kW1 + c]), xs[c], h);
+      h = __builtin_elementwise_max(h, ppo_splat(0.0f));
+#pragma unroll
+      for (int q = 0; q < K; ++q) z[q] = __builtin_elementwise_fma(ppo_splat(r[q]), h, z[q]);
     }
     if (NW > 1 && w > 0) {
 #pragma unroll
-      for (int q = 0; q < KP; ++q) red[((w - 1) * KP + q) * 64 + lane] = acc[q];
+      for (int q = 0; q < K; ++q) {
+        red[((w - 1) * K + q) * 128 + lane] = z[q].x;
+        red[((w - 1) * K + q) * 128 + 64 + lane] = z[q].y;
+      }
     }
     if (NW > 1) __syncthreads();
-    float g[KP];
-#pragma unroll
-    for (int q = 0; q < KP; ++q) g[q] = 0.0f;
+    // P: dL/dz and dL/dV of each sample, its row to LDS
     if (w == 0) {
 #pragma unroll
-      for (int ww = 1; ww < NW; ++ww) {
-#pragma unroll
-        for (int q = 0; q < KP; ++q) acc[q] += red[((ww - 1) * KP + q) * 64 + lane];
-      }
-      if (valid) {
-        float p[K];
-        float m = acc[0] + bo[0];
-#pragma unroll
-        for (int q = 1; q < K; ++q)
-          if (q < k) m = fmaxf(m, acc[q] + bo[q]);
-        float sum = 0.0f;
+      for (int half = 0; half < 2; ++half) {
+        const long si = half ? sb : sa;
+        const int slot = half * 64 + lane;
+        float acc[K];
 #pragma unroll
         for (int q = 0; q < K; ++q) {
-          p[q] = q < k ? expf(acc[q] + bo[q] - m) : 0.0f;
-          sum += p[q];
+          acc[q] = half ? z[q].y : z[q].x;
+#pragma unroll
+          for (int ww = 1; ww < NW; ++ww) acc[q] += red[((ww - 1) * K + q) * 128 + slot];
         }
-        const int a = (int)actions[si];
-        float pa = 0.0f;
+        float g[KP];
 #pragma unroll
-        for (int q = 0; q < K; ++q) {
-          p[q] = p[q] / sum;
-          pa = q == a ? p[q] : pa;
+        for (int q = 0; q < KP; ++q) g[q] = 0.0f;
+        if (si < n) {
+          float p[K];
+          float m = acc[0] + bo[0];
+#pragma unroll
+          for (int q = 1; q < K; ++q)
+            if (q < k) m = fmaxf(m, acc[q] + bo[q]);
+          float sum = 0.0f;
+#pragma unroll
+          for (int q = 0; q < K; ++q) {
+            p[q] = q < k ? expf(acc[q] + bo[q] - m) : 0.0f;
+            sum += p[q];
+          }
+          const int a = (int)actions[si];
+          float pa = 0.0f;
+#pragma unroll
+          for (int q = 0; q < K; ++q) {
+            p[q] = p[q] / sum;
+            pa = q == a ? p[q] : pa;
+          }
+          // -min(r A, clip(r, 1 - eps, 1 + eps) A): a tie splits the gradient
+          // evenly between the two arguments, clip passes it on its closed range
+          const float A = (adv[si] - a_mean) / a_den;
+          const float r = expf(logf(pa + 1e-8f) - old_logp[si]);
+          const float lo = 1.0f - clip_eps, hi = 1.0f + clip_eps;
+          const float rc = fminf(fmaxf(r, lo), hi);
+          const float t1 = r * A, t2 = rc * A;
+          const float w1st = t1 < t2 ? 1.0f : (t1 > t2 ? 0.0f : 0.5f);
+          const float in = (r >= lo && r <= hi) ? 1.0f : 0.0f;
+          const float d_r = -A * (w1st + (1.0f - w1st) * in);
+          const float d_pa = d_r * r / (pa + 1e-8f);
+          // entropy term: + c_ent sum_q (p_q + eps) log(p_q + eps)
+          float dp[K], pdp = 0.0f;
+#pragma unroll
+          for (int q = 0; q < K; ++q) {
+            dp[q] = q < k ? c_ent * (logf(p[q] + 1e-8f) + 1.0f) + (q == a ? d_pa : 0.0f) : 0.0f;
+            pdp = fmaf(p[q], dp[q], pdp);
+          }
+#pragma unroll
+          for (int q = 0; q < K; ++q) g[q] = p[q] * (dp[q] - pdp);
+          g[K] = dvalue[si];
         }
-        // -min(r A, clip(r, 1 - eps, 1 + eps) A): a tie splits the gradient
-        // evenly between the two arguments, clip passes it on its closed range
-        const float A = (adv[si] - a_mean) / a_den;
-        const float r = expf(logf(pa + 1e-8f) - old_logp[si]);
-        const float lo = 1.0f - clip_eps, hi = 1.0f + clip_eps;
-        const float rc = fminf(fmaxf(r, lo), hi);
-        const float t1 = r * A, t2 = rc * A;
-        const float w1st = t1 < t2 ? 1.0f : (t1 > t2 ? 0.0f : 0.5f);
-        const float in = (r >= lo && r <= hi) ? 1.0f : 0.0f;
-        const float d_r = -A * (w1st + (1.0f - w1st) * in);
-        const float d_pa = d_r * r / (pa + 1e-8f);
-        // entropy term: + c_ent sum_q (p_q + eps) log(p_q + eps)
-        float dp[K], pdp = 0.0f;
+        float* row = srow + slot * kRow;
 #pragma unroll
-        for (int q = 0; q < K; ++q) {
-          dp[q] = q < k ? c_ent * (logf(p[q] + 1e-8f) + 1.0f) + (q == a ? d_pa : 0.0f) : 0.0f;
-          pdp = fmaf(p[q], dp[q], pdp);
+        for (int q = 0; q < KP; ++q) {
+          gbias[q] += g[q];
+          row[q] = g[q];
         }
 #pragma unroll
-        for (int q = 0; q < K; ++q) g[q] = p[q] * (dp[q] - pdp);
-        g[K] = dvalue[si];
-      }
-#pragma unroll
-      for (int q = 0; q < KP; ++q) gbias[q] += g[q];
-      if (NW > 1) {
-#pragma unroll
-        for (int q = 0; q < KP; ++q) sz[lane * kRow + q] = g[q];
+        for (int c = 0; c < D; ++c) row[KP + c] = half ? xs[c].y : xs[c].x;
       }
     }
-    if (NW > 1) {
-      __syncthreads();
+    ppo_group_sync<NW>();
+    // B: both units' gradients over the 128 samples
+#pragma unroll 2
+    for (int s = 0; s < 128; ++s) {
+      float rv[kRow];
+      const float4* r4 = reinterpret_cast<const float4*>(srow + s * kRow);
 #pragma unroll
-      for (int q = 0; q < KP; ++q) g[q] = sz[lane * kRow + q];
-    }
-    // broadcast the features again in C rather than keep phase A's 64 x D
-    // uniform copies alive (they would spill the SGPR file)
+      for (int i = 0; i < kRow / 4; ++i) {
+        const float4 v = r4[i];
+        rv[4 * i] = v.x;
+        rv[4 * i + 1] = v.y;
+        rv[4 * i + 2] = v.z;
+        rv[4 * i + 3] = v.w;
+      }
+      ppo_f2 h = b1p;
 #pragma unroll
-    for (int c = 0; c < D; ++c) asm volatile("" : "+v"(xr[c]));
-    // C: both units' gradients over the 64 samples, dL/dz of each broadcast
-#pragma unroll
-    for (int s = 0; s < 64; ++s) {
-      const ppo_f2 h = hs[s];
+      for (int c = 0; c < D; ++c) h = __builtin_elementwise_fma(w1p[c], ppo_splat(rv[KP + c]), h);
+      h = __builtin_elementwise_max(h, ppo_splat(0.0f));
       ppo_f2 dh = ppo_splat(0.0f);
 #pragma unroll
       for (int q = 0; q < KP; ++q) {
-        const ppo_f2 gs = ppo_splat(lane_value(g[q], s));
+        const ppo_f2 gs = ppo_splat(rv[q]);
         gwop[q] = __builtin_elementwise_fma(gs, h, gwop[q]);
         dh = __builtin_elementwise_fma(wop[q], gs, dh);
       }
@@ -490,12 +543,47 @@ __global__ __launch_bounds__(64 * NW) void k_ppo_grads(
       gb1p += dh;
 #pragma unroll
       for (int c = 0; c < D; ++c)
-        gw1p[c] = __builtin_elementwise_fma(dh, ppo_splat(lane_value(xr[c], s)), gw1p[c]);
+        gw1p[c] = __builtin_elementwise_fma(dh, ppo_splat(rv[KP + c]), gw1p[c]);
     }
-    if (NW > 1) __syncthreads();  // sz and red are rewritten next tile
+    ppo_group_sync<NW>();  // the rows (and red) are rewritten next tile
+  }
+  if constexpr (NT > 1) {
+    // tile waves 1.. hand their sums to wave 0 in order: ((s0 + s1) + s2) + ...
+    float* cb = ppo_lds + lane;  // [ppo_combine_floats][64]
+    auto xfer = [&](bool put) {
+      int i = 0;
+      auto two = [&](ppo_f2& v) {
+        if (put) {
+          cb[64 * i] = v.x;
+          cb[64 * (i + 1)] = v.y;
+        } else {
+          v += ppo_f2{cb[64 * i], cb[64 * (i + 1)]};
+        }
+        i += 2;
+      };
+#pragma unroll
+      for (int c = 0; c < D; ++c) two(gw1p[c]);
+      two(gb1p);
+#pragma unroll
+      for (int q = 0; q < KP; ++q) two(gwop[q]);
+#pragma unroll
+      for (int q = 0; q < KP; ++q) {
+        if (put)
+          cb[64 * i] = gbias[q];
+        else
+          gbias[q] += cb[64 * i];
+        ++i;
+      }
+    };
+    for (int src = 1; src < NT; ++src) {
+      __syncthreads();  // the tiles' rows, or the previous round's buffer, are done with
+      if (t == src) xfer(true);
+      __syncthreads();
+      if (t == 0) xfer(false);
+    }
   }
   // output-bias gradients: wave 0's per-lane sums, reduced across the wave
-  if (w == 0) {
+  if (wid == 0) {
 #pragma unroll
     for (int q = 0; q < KP; ++q) {
       float v = gbias[q];
@@ -509,7 +597,7 @@ __global__ __launch_bounds__(64 * NW) void k_ppo_grads(
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     const int u = half ? u1 : u0;
-    if (u < hidden) {
+    if (t == 0 && u < hidden) {
 #pragma unroll
       for (int c = 0; c < D; ++c)
         if (c < d) out[u * d + c] = half ? gw1p[c].y : gw1p[c].x;
