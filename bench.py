@@ -327,8 +327,8 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
     saved = agent.trajectory
     agent.reset_trajectory()
     samples = []
-    how = (f"HIP event-record nodes around the run node of each window of an episode graph "
-           f"captured after the timed region, {replays} replays")
+    how = (f"an episode graph of the workload captured after the timed region with engine "
+           f"profiling on, {replays} replays")
     nat.call("swarm_engine_profile", 1, ctypes.byref(ms), ctypes.byref(cnt))
     graph = None
     try:
@@ -380,26 +380,28 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
         torch.cuda.synchronize()
         nat.call("swarm_engine_profile_graph", 1, None, None, 0, ctypes.byref(cnt))
         agent.trajectory = saved
-    if not samples:  # no 2-D cluster windows (global path): nothing was recorded
-        return None, name, "no run-kernel launches recorded", 0, {}
-    samples.sort()
-    raw = sum(samples) / len(samples)
-    # the event-record nodes add their own marker latency around the kernel
-    # (an empty pair of them right after each run node: `over`); the run
-    # kernel's own stamps (earliest block start, latest wave end, device
-    # wall clock) time the launch as it ran in the replayed workload
-    over = sum(cal_samples) / len(cal_samples) if cal_samples else 0.0
+    # the run kernel's own launch stamps (earliest block start, latest wave
+    # end, device wall clock) time each run node as it ran in the replayed
+    # workload; HIP events only where there are no stamps (eager episodes, or
+    # event-record nodes asked for with SWARMRL_AMD_PROFILE_EVENT_NODES=1)
     dev_ok = [x for x in dev_samples if x > 0.0]
-    if dev_ok and len(dev_ok) == len(samples):
+    if not dev_ok and not samples:  # no 2-D cluster windows (global path)
+        return None, name, "no run-kernel launches recorded", 0, {}
+    if dev_ok:
         mean = sum(dev_ok) / len(dev_ok)
-        how_ms = (f"the kernel's own start / end stamps (device wall clock): mean {mean:.5f} ms, "
-                  f"min {min(dev_ok):.5f}, max {max(dev_ok):.5f}; ")
+        n_timed = len(dev_ok)
+        note = (f"{how}: {n_timed} run nodes timed by their own start / end stamps (device "
+                f"wall clock): mean {mean:.5f} ms, min {min(dev_ok):.5f}, max {max(dev_ok):.5f}")
     else:
-        mean = raw
-        how_ms = ""
-    note = (f"{how}: {len(samples)} launches; {how_ms}HIP event pair around the run node: mean "
-            f"{raw:.5f} ms, median {samples[len(samples) // 2]:.5f}, min {samples[0]:.5f}, max "
-            f"{samples[-1]:.5f}; an empty event-node pair alone: {over:.5f} ms")
+        samples.sort()
+        mean = sum(samples) / len(samples)
+        n_timed = len(samples)
+        note = (f"{how}: HIP events around {n_timed} run launches: mean {mean:.5f} ms, median "
+                f"{samples[len(samples) // 2]:.5f}, min {samples[0]:.5f}, max {samples[-1]:.5f}")
+    if samples and cal_samples:
+        over = sum(cal_samples) / len(cal_samples)
+        note += (f"; event-record nodes around the run node: mean {sum(samples) / len(samples):.5f}"
+                 f" ms, an empty pair of them alone {over:.5f} ms")
     # the workgroup roles of the launches between run nodes (role stamps):
     # mean start / end after the previous run node's end, and mean duration
     names = ("k_check", "build sort", "vision grid", "field (reward)", "pair search",
@@ -410,7 +412,7 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
             "start_us": round(sum(b for b, _ in v) / len(v), 2),
             "end_us": round(sum(e for _, e in v) / len(v), 2),
             "dur_us": round(sum(e - b for b, e in v) / len(v), 2), "n": len(v)}
-    return mean, name, note, len(samples), timeline
+    return mean, name, note, n_timed, timeline
 
 
 def time_ppo_grads(agent, traj, line, reps):

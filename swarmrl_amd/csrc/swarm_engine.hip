@@ -432,10 +432,10 @@ __device__ __forceinline__ void vision_hit(const VisionLane& L, const swarm_visi
 }
 
 // Cone arithmetic over a lane's listed hits, records fetched four at a time.
-template <int NB, bool kAny = false>
+template <int NB, bool kAny = false, int BS = 256>
 __device__ __forceinline__ void vision_drain(const VisionLane& L, const swarm_vision_params_t& vp,
                                              const uint4* __restrict__ rec, size_t base,
-                                             const uint32_t (*hits)[256], int nh, int64_t* acc) {
+                                             const uint32_t (*hits)[BS], int nh, int64_t* acc) {
   for (int k0 = 0; __any(k0 < nh); k0 += 4) {  // over the active lanes' longest list
     uint4 c0[4], c1[4];
 #pragma unroll
@@ -458,11 +458,11 @@ __device__ __forceinline__ void vision_drain(const VisionLane& L, const swarm_vi
 // wave runs as long as its longest: ~6 hits of Poisson(2) lists against ~4
 // of the balanced ones at E = 64).  Integer bin sums: the same result.
 // Whole groups are active together (they share one agent).
-template <int NB, int G, bool kAny = false>
+template <int NB, int G, bool kAny = false, int BS = 256>
 __device__ __forceinline__ void vision_drain_group(const VisionLane& L,
                                                    const swarm_vision_params_t& vp,
                                                    const uint4* __restrict__ rec, size_t base,
-                                                   const uint32_t (*hits)[256], int nh,
+                                                   const uint32_t (*hits)[BS], int nh,
                                                    int64_t* acc) {
   // the other lanes' list entries are read below: keep the compiler from
   // moving those LDS reads above this lane's writes (one wave's LDS
@@ -508,12 +508,13 @@ __device__ __forceinline__ void vision_drain_group(const VisionLane& L,
 // candidate, tested on its unwrapped (int64) separation.
 // xcd_bpe > 0: blocks placed on XCDs by env (swarm::xcd_env_block, xcd_bpe
 // blocks per env), so the records an env's agents read stay in one L2.
-// Body for block vb (k_vision, or a workgroup of k_vision_pairs); hits: the
-// block's [kVisionHits][256] LDS hit lists (blockDim 256).
-template <int NB, int G, bool kAll = false>
+// Body for block vb (k_vision, or a workgroup of k_vision_pairs /
+// k_vision_cbuild); hits: the block's [kVisionHits][BS] LDS hit lists
+// (blockDim BS).
+template <int NB, int G, bool kAll = false, int BS = 256>
 __device__ __forceinline__ void vision_body(const DevState& st, const Derived* __restrict__ d,
                                             const VisionArgs& va, int vb, int xcd_bpe,
-                                            uint32_t (*hits)[256]) {
+                                            uint32_t (*hits)[BS]) {
   const swarm_vision_params_t& vp = va.vp;
   const int lx = va.lx, ly = va.ly;
   const int32_t* __restrict__ start = va.start;
@@ -667,15 +668,16 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
 // the engine stream guarantees.  The build's workgroups take the first block
 // indices of each launch: the build chain (sort -> pairs -> cluster build)
 // is the longer one, so its workgroups are dealt out first.
-template <int CH>
+template <int CH, bool kPairs>
 __global__ __launch_bounds__(1024) void k_vgrid_sort(DevState st, VisionArgs va, Scratch sc,
-                                                     int lxb, int lyb) {
+                                                     int lxb, int lyb,
+                                                     const Derived* __restrict__ d) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int b = blockIdx.x;
   const int role = b < va.n_envs ? swarm::kRoleSort : swarm::kRoleVgrid;
   swarm::role_begin(sc, role);
   if (b < va.n_envs)
-    swarm::build_sort_body<CH>(st, sc, lxb, lyb, b, smem);
+    swarm::build_sort_body<CH, kPairs>(st, sc, lxb, lyb, b, smem, d);
   else
     vision_grid_body(st, va, b - va.n_envs, smem);
   swarm::role_end(sc, role);
@@ -701,6 +703,25 @@ __global__ __launch_bounds__(256) void k_vision_pairs(DevState st, const Derived
   } else {
     vision_body<NB, G, false>(st, d, va, b - n_pblocks, 0, hits);
   }
+  swarm::role_end(sc, role);
+}
+
+// sort_pairs engines: the pair list came with the sort (L1), so the cluster
+// build rides in the vision cone's launch -- 1024-thread blocks: the build's
+// workgroup(s) first, then the cone's (their hit lists in the same dynamic
+// LDS), and the policy runs alone after it.
+template <int NB, int G>
+__global__ __launch_bounds__(1024) void k_vision_cbuild(DevState st, const Derived* __restrict__ d,
+                                                        VisionArgs va, Scratch sc) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int role = b < va.n_envs ? swarm::kRoleCbuild : swarm::kRoleCone;
+  swarm::role_begin(sc, role);
+  if (b < va.n_envs)
+    swarm::cluster_build_env<false, true, false>(st, sc, b, smem, sc.gnpairs[b]);
+  else
+    vision_body<NB, G, false, 1024>(st, d, va, b - va.n_envs, 0,
+                                    reinterpret_cast<uint32_t(*)[1024]>(smem));
   swarm::role_end(sc, role);
 }
 
@@ -924,10 +945,11 @@ __global__ __launch_bounds__(256) void k_field(DevState st, FieldArgs f) {
 // the field's agents, the NEXT observable's vision grid (from the positions
 // the reward sees, which the observable will see too) and build stage 1,
 // so the observable launch only runs the cone (beside stage 2).
-template <int CH>
+template <int CH, bool kPairs>
 __global__ __launch_bounds__(1024) void k_field_vgrid_sort(FieldArgs f, int n_fblocks, DevState st,
                                                            VisionArgs va, Scratch sc, int lxb,
-                                                           int lyb) {
+                                                           int lyb,
+                                                           const Derived* __restrict__ d) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int b = blockIdx.x;
   const int role = b < va.n_envs       ? swarm::kRoleSort
@@ -935,7 +957,7 @@ __global__ __launch_bounds__(1024) void k_field_vgrid_sort(FieldArgs f, int n_fb
                                        : swarm::kRoleField;
   swarm::role_begin(sc, role);
   if (b < va.n_envs)
-    swarm::build_sort_body<CH>(st, sc, lxb, lyb, b, smem);
+    swarm::build_sort_body<CH, kPairs>(st, sc, lxb, lyb, b, smem, d);
   else if (b < 2 * va.n_envs)
     vision_grid_body(st, va, b - va.n_envs, smem);
   else
@@ -1074,6 +1096,10 @@ struct swarm_engine {
   bool big_build = false;  // k_cluster_build<true>: cluster arrays in global memory
   bool chip_sort = false;  // 2-D envs above 4096 colloids: the three-launch chip-wide sort
   bool pairs_staged = false;  // the ride-along pair search stages its env in LDS
+  // ride-along build of small periodic 2-D envs: the pair search runs in the
+  // sort's workgroup from its LDS rows (stage 1), and the cluster build rides
+  // in the vision cone's launch (k_vision_cbuild)
+  bool sort_pairs = false;
   // k_cluster_run_wide's idle waves integrate the rotation ahead
   // (swarm::precompute_swim; SWARMRL_AMD_ROT_AHEAD=1 turns it on: measured
   // slower, 4096 colloids 42.2 M vs 41.9 M agent-steps/s, C4 78.0 M vs 67.5 M)
@@ -1124,13 +1150,14 @@ struct swarm_engine {
   // cost of an event-record node pair itself (swarm_engine_profile_graph)
   std::vector<std::pair<hipEvent_t, hipEvent_t>> graph_cal;
   // and each captured run node's own start / end stamps (swarm::stamp_start,
-  // stamp_end): d_tstamp[2 k], [2 k + 1] for the k-th captured run node
+  // stamp_end): d_tstamp[k][kStampSub][2] for the k-th captured run node
   unsigned long long* d_tstamp = nullptr;
   int stamp_next = 0;
   // [kMaxStamps][kRoles][2]: the workgroup roles of the launches that follow
   // the k-th captured run node (its k_check, then the next window's build and
   // observable launches), swarm::role_begin / role_end
   unsigned long long* d_rstamp = nullptr;
+  bool graph_event_nodes = false;  // SWARMRL_AMD_PROFILE_EVENT_NODES=1
   float* own_f_swim = nullptr;
   float* own_torque_z = nullptr;
   void* allocs[96] = {};
@@ -1216,10 +1243,13 @@ void set_lds_attributes() {
                        reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<true, false>),
                        reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<false, true>),
                        reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<true, true>),
-                       reinterpret_cast<const void*>(&k_vgrid_sort<4>),
-                       reinterpret_cast<const void*>(&k_vgrid_sort<16>),
-                       reinterpret_cast<const void*>(&k_field_vgrid_sort<4>),
-                       reinterpret_cast<const void*>(&k_field_vgrid_sort<16>),
+                       reinterpret_cast<const void*>(&k_vgrid_sort<4, false>),
+                       reinterpret_cast<const void*>(&k_vgrid_sort<16, false>),
+                       reinterpret_cast<const void*>(&k_vgrid_sort<4, true>),
+                       reinterpret_cast<const void*>(&k_field_vgrid_sort<4, false>),
+                       reinterpret_cast<const void*>(&k_field_vgrid_sort<16, false>),
+                       reinterpret_cast<const void*>(&k_field_vgrid_sort<4, true>),
+                       reinterpret_cast<const void*>(&k_vision_cbuild<4, 16>),
                        reinterpret_cast<const void*>(&k_policy_cbuild<4, 4, 4>)};
   for (const void* f : fns)
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
@@ -1582,13 +1612,18 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
     return SWARM_OK;
   }
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool in_graph = false;
+  bool in_graph = false, events = false;
   if (e->profile) {
-    // under stream capture: event-record nodes around the run node, so each
-    // replay of the graph times the kernel as it runs in the workload
+    // eager: HIP events around the run launch; under stream capture the run
+    // node stamps itself (launch stamps below), and event-record nodes around
+    // it only with SWARMRL_AMD_PROFILE_EVENT_NODES=1 (they put ~15 us gaps
+    // into the replayed graph)
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     HIP_TRY(hipStreamIsCapturing(e->stream, &cs));
     in_graph = cs == hipStreamCaptureStatusActive;
+    events = !in_graph || e->graph_event_nodes;
+  }
+  if (events) {
     HIP_TRY(hipEventCreate(&ev0));
     HIP_TRY(hipEventCreate(&ev1));
     const int rc0 = record_event(e->stream, ev0, in_graph);
@@ -1596,15 +1631,16 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
   }
   unsigned long long* tstamp = nullptr;
   if (e->profile && in_graph && e->d_tstamp && e->stamp_next < kMaxStamps)
-    tstamp = e->d_tstamp + 2 * e->stamp_next++;
+    tstamp = e->d_tstamp + (size_t)2 * swarm::kStampSub * e->stamp_next++;
   // the check and the launches up to the next run record their roles in
   // this run's slot (profiling under capture only)
   e->sc.rstamp = tstamp && e->d_rstamp
-                     ? e->d_rstamp + (size_t)(e->stamp_next - 1) * 2 * swarm::kRoles
+                     ? e->d_rstamp + (size_t)(e->stamp_next - 1) * 2 * swarm::kRoles *
+                                         swarm::kStampSub
                      : nullptr;
   int rc = launch_run(e, n_steps, tstamp);
   if (rc) return rc;
-  if (e->profile) {
+  if (events) {
     rc = record_event(e->stream, ev1, in_graph);
     if (rc) return rc;
     (in_graph ? e->graph_events : e->prof_events).emplace_back(ev0, ev1);
@@ -1806,6 +1842,8 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
       !(std::getenv("SWARMRL_AMD_PAIR_REGIONS") && std::getenv("SWARMRL_AMD_PAIR_REGIONS")[0] == '0'))
     e->sc.pair_region = e->sc.pair_cap / ((n_particles + 255) / 256);
   e->sc.rstamp = nullptr;
+  e->graph_event_nodes = std::getenv("SWARMRL_AMD_PROFILE_EVENT_NODES") &&
+                         std::getenv("SWARMRL_AMD_PROFILE_EVENT_NODES")[0] == '1';
   e->sc.multi_species = params->n_species > 1 ? 1 : 0;
   // the 2-D build sort stages its scatter in LDS: the sorted rows of up to
   // K entries per pass beside the cell counts (K a multiple of 4, at least
@@ -1821,6 +1859,16 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     if (const char* oss = std::getenv("SWARMRL_AMD_SORT_STAGED"))
       if (oss[0] == '0') e->sc.sort_stage_k = 0;
   }
+  // the pair search in the sort's workgroup (SWARMRL_AMD_SORT_PAIRS=1: on):
+  // periodic 2-D envs whose sort stages all its rows in one LDS pass.  Off
+  // by default: measured (role stamps, 4096 colloids) its one workgroup
+  // takes 31 us for the pairs the 16-block search finds in 12 us, so moving
+  // the cluster build beside the cone does not pay (35.1 M vs 43.2 M)
+  e->sort_pairs = params->n_dims == 2 && params->periodic && n_particles <= 4096 &&
+                  e->sc.sort_stage_k >= n_particles && !e->sc.local_uf && !e->big_build &&
+                  std::getenv("SWARMRL_AMD_SORT_PAIRS") &&
+                  std::getenv("SWARMRL_AMD_SORT_PAIRS")[0] == '1';
+  if (e->sort_pairs) e->sc.pair_region = 0;  // its list is contiguous (gnpairs)
   e->cluster_path = e->sc.pair_cap >= n_particles &&
                     n_particles < 65536 &&
                     swarm::build_lds_words_big(n_particles) * 4 <= kMaxLds &&
@@ -2045,6 +2093,7 @@ void swarm_engine_destroy(swarm_engine_t* e) {
   if (!e) return;
   (void)hipDeviceSynchronize();
   if (e->d_tstamp) (void)hipFree(e->d_tstamp);
+  if (e->d_rstamp) (void)hipFree(e->d_rstamp);
   for (auto* v : {&e->prof_events, &e->graph_events, &e->graph_cal})
     for (auto& pr : *v) {
       (void)hipEventDestroy(pr.first);
@@ -2262,10 +2311,11 @@ int swarm_engine_profile(swarm_engine_t* e, int32_t enable, double* run_ms, int3
   e->profile = enable != 0;
   // the launch stamps of captured run nodes (allocated here: never under capture)
   if (e->profile && !e->d_tstamp)
-    HIP_TRY(hipMalloc(&e->d_tstamp, 2 * kMaxStamps * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&e->d_tstamp, 2 * (size_t)kMaxStamps * swarm::kStampSub *
+                                        sizeof(unsigned long long)));
   if (e->profile && !e->d_rstamp)
-    HIP_TRY(hipMalloc(&e->d_rstamp,
-                      2 * (size_t)kMaxStamps * swarm::kRoles * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&e->d_rstamp, 2 * (size_t)kMaxStamps * swarm::kRoles * swarm::kStampSub *
+                                        sizeof(unsigned long long)));
   if (!e->profile) e->sc.rstamp = nullptr;
   return rc;
 }
@@ -2305,6 +2355,32 @@ int swarm_engine_profile_graph(swarm_engine_t* e, int32_t release, float* ms_out
 }
 
 namespace {
+// The (min start, max end) of each of `n` stamp records of kStampSub pairs.
+void reduce_stamps(const std::vector<unsigned long long>& raw, int n,
+                   std::vector<unsigned long long>* out) {
+  out->assign(2 * (size_t)n, 0ull);
+  for (int k = 0; k < n; ++k) {
+    unsigned long long b = ~0ull, en = 0ull;
+    for (int j = 0; j < swarm::kStampSub; ++j) {
+      b = std::min(b, raw[2 * ((size_t)k * swarm::kStampSub + j)]);
+      en = std::max(en, raw[2 * ((size_t)k * swarm::kStampSub + j) + 1]);
+    }
+    (*out)[2 * (size_t)k] = b;
+    (*out)[2 * (size_t)k + 1] = en;
+  }
+}
+
+// The run nodes' (start, end) stamps, reduced over their pairs.
+int read_run_stamps(swarm_engine* e, std::vector<unsigned long long>* t) {
+  const int n = e->stamp_next;
+  HIP_TRY(hipDeviceSynchronize());
+  std::vector<unsigned long long> raw(2 * (size_t)n * swarm::kStampSub);
+  HIP_TRY(hipMemcpy(raw.data(), e->d_tstamp, raw.size() * sizeof(unsigned long long),
+                    hipMemcpyDeviceToHost));
+  reduce_stamps(raw, n, t);
+  return SWARM_OK;
+}
+
 __global__ void k_stamp_reset(unsigned long long* t, int n) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < n) {
@@ -2321,10 +2397,11 @@ int swarm_engine_profile_stamps(swarm_engine_t* e, int32_t reset, void* stream, 
   if (launches) *launches = n;
   if (!e->d_tstamp || n == 0) return SWARM_OK;
   if (reset) {
-    hipLaunchKernelGGL(k_stamp_reset, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), e->d_tstamp, n);
+    const int nt = n * swarm::kStampSub;
+    hipLaunchKernelGGL(k_stamp_reset, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), e->d_tstamp, nt);
     if (e->d_rstamp) {
-      const int nr = n * swarm::kRoles;
+      const int nr = n * swarm::kRoles * swarm::kStampSub;
       hipLaunchKernelGGL(k_stamp_reset, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0,
                          reinterpret_cast<hipStream_t>(stream), e->d_rstamp, nr);
     }
@@ -2332,10 +2409,9 @@ int swarm_engine_profile_stamps(swarm_engine_t* e, int32_t reset, void* stream, 
     return SWARM_OK;
   }
   if (cap < 0 || (cap > 0 && !ms_out)) return fail(SWARM_EINVAL, "ms_out needs cap entries");
-  HIP_TRY(hipDeviceSynchronize());
-  std::vector<unsigned long long> t(2 * (size_t)n);
-  HIP_TRY(hipMemcpy(t.data(), e->d_tstamp, t.size() * sizeof(unsigned long long),
-                    hipMemcpyDeviceToHost));
+  std::vector<unsigned long long> t;
+  int rc = read_run_stamps(e, &t);
+  if (rc) return rc;
   int dev = 0, khz = 0;
   HIP_TRY(hipGetDevice(&dev));
   HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
@@ -2354,12 +2430,13 @@ int swarm_engine_profile_roles(swarm_engine_t* e, double* us_out, int32_t cap,
   const size_t per = 2 * (size_t)swarm::kRoles;
   for (int32_t k = 0; k < cap; ++k) us_out[k] = std::nan("");
   if (!e->d_tstamp || !e->d_rstamp || n == 0) return SWARM_OK;
-  HIP_TRY(hipDeviceSynchronize());
-  std::vector<unsigned long long> t(2 * (size_t)n), r(per * n);
-  HIP_TRY(hipMemcpy(t.data(), e->d_tstamp, t.size() * sizeof(unsigned long long),
+  std::vector<unsigned long long> t, r;
+  int rc = read_run_stamps(e, &t);
+  if (rc) return rc;
+  std::vector<unsigned long long> raw(per * n * swarm::kStampSub);
+  HIP_TRY(hipMemcpy(raw.data(), e->d_rstamp, raw.size() * sizeof(unsigned long long),
                     hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(r.data(), e->d_rstamp, r.size() * sizeof(unsigned long long),
-                    hipMemcpyDeviceToHost));
+  reduce_stamps(raw, n * swarm::kRoles, &r);
   int dev = 0, khz = 0;
   HIP_TRY(hipGetDevice(&dev));
   HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
@@ -2693,7 +2770,8 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
   if (glds > kMaxLds) return fail(SWARM_ECAPACITY, "observable cell grid too large");
   // the grid of the current positions for these arguments, built by the
   // reward launch (launch_field) while nothing moved the colloids since
-  const bool have_grid = !all && e->vgrid_ready && e->ride_stage == 2 &&
+  const bool have_grid = !all && e->vgrid_ready &&
+                         (e->ride_stage == 2 || (e->ride_stage == 3 && e->sort_pairs)) &&
                          same_grid_args(e->spec_va, va);
   e->vgrid_ready = false;
   e->spec_ok = persistent && !all;
@@ -2701,24 +2779,40 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
   // a deferred build rides along in the grid and cone launches (stages 1, 2)
   // when their fused variants apply; else its pending stages launch first
   const bool ride_ok = !all && nb <= 4 && G == 16;
-  if (e->ride_stage > 0 && !(ride_ok && e->ride_stage <= 2)) {
+  const bool ride3 = ride_ok && e->sort_pairs && e->ride_stage == 3;  // cluster build | cone
+  if (e->ride_stage > 0 && !(ride_ok && e->ride_stage <= 2) && !ride3) {
     rc = flush_ride_along(e);
     if (rc) return rc;
   }
-  if (e->ride_stage == 1) {  // grid | sort, then cone | pairs
+  if (e->ride_stage == 1) {  // grid | sort (+ pairs), then cone | pairs (| cluster build)
     const size_t slds = sort_lds_bytes(e);
     const dim3 grid((unsigned)(2 * e->n_envs));
-    if (e->n > 4096)
-      hipLaunchKernelGGL(k_vgrid_sort<16>, grid, dim3(1024), std::max(glds, slds), e->stream,
-                         e->st, va, e->sc, e->lxb, e->lyb);
+    if (e->sort_pairs)
+      hipLaunchKernelGGL((k_vgrid_sort<4, true>), grid, dim3(1024), std::max(glds, slds),
+                         e->stream, e->st, va, e->sc, e->lxb, e->lyb, e->d_derived);
+    else if (e->n > 4096)
+      hipLaunchKernelGGL((k_vgrid_sort<16, false>), grid, dim3(1024), std::max(glds, slds),
+                         e->stream, e->st, va, e->sc, e->lxb, e->lyb, e->d_derived);
     else
-      hipLaunchKernelGGL(k_vgrid_sort<4>, grid, dim3(1024), std::max(glds, slds), e->stream,
-                         e->st, va, e->sc, e->lxb, e->lyb);
+      hipLaunchKernelGGL((k_vgrid_sort<4, false>), grid, dim3(1024), std::max(glds, slds),
+                         e->stream, e->st, va, e->sc, e->lxb, e->lyb, e->d_derived);
     HIP_TRY(hipGetLastError());
-    e->ride_stage = 2;
+    e->ride_stage = e->sort_pairs ? 3 : 2;
   } else if (!have_grid) {
     hipLaunchKernelGGL(k_vision_grid, dim3(e->n_envs), dim3(1024), glds, e->stream, e->st, va);
     HIP_TRY(hipGetLastError());
+  }
+  if (ride_ok && e->sort_pairs && e->ride_stage == 3) {
+    // cluster build | cone (1024-thread blocks; the policy runs alone)
+    const int ncb = (int)((total * 16 + 1023) / 1024);
+    const size_t lds = std::max(build_lds_bytes(e->n, e->sc.pair_cap),
+                                (size_t)kVisionHits * 1024 * sizeof(uint32_t));
+    hipLaunchKernelGGL((k_vision_cbuild<4, 16>), dim3((unsigned)(e->n_envs + ncb)), dim3(1024),
+                       lds, e->stream, e->st, e->d_derived, va, e->sc);
+    HIP_TRY(hipGetLastError());
+    e->ride_stage = 0;
+    e->prebuilt = true;
+    return SWARM_OK;
   }
   if (e->ride_stage == 2) {  // pairs | cone
     const int nvb = (int)((total * 16 + 255) / 256);
@@ -2808,14 +2902,18 @@ int launch_field(swarm_engine* e, const FieldArgs& f) {
     const size_t slds = sort_lds_bytes(e);
     const int nfb = (total + 1023) / 1024;
     const dim3 grid((unsigned)(nfb + 2 * e->n_envs));
-    if (e->n > 4096)
-      hipLaunchKernelGGL(k_field_vgrid_sort<16>, grid, dim3(1024), std::max(glds, slds),
-                         e->stream, f, nfb, e->st, va, e->sc, e->lxb, e->lyb);
+    if (e->sort_pairs)
+      hipLaunchKernelGGL((k_field_vgrid_sort<4, true>), grid, dim3(1024), std::max(glds, slds),
+                         e->stream, f, nfb, e->st, va, e->sc, e->lxb, e->lyb, e->d_derived);
+    else if (e->n > 4096)
+      hipLaunchKernelGGL((k_field_vgrid_sort<16, false>), grid, dim3(1024),
+                         std::max(glds, slds), e->stream, f, nfb, e->st, va, e->sc, e->lxb,
+                         e->lyb, e->d_derived);
     else
-      hipLaunchKernelGGL(k_field_vgrid_sort<4>, grid, dim3(1024), std::max(glds, slds),
-                         e->stream, f, nfb, e->st, va, e->sc, e->lxb, e->lyb);
+      hipLaunchKernelGGL((k_field_vgrid_sort<4, false>), grid, dim3(1024), std::max(glds, slds),
+                         e->stream, f, nfb, e->st, va, e->sc, e->lxb, e->lyb, e->d_derived);
     HIP_TRY(hipGetLastError());
-    e->ride_stage = 2;
+    e->ride_stage = e->sort_pairs ? 3 : 2;
     e->vgrid_ready = true;
     return SWARM_OK;
   }
@@ -3191,10 +3289,13 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
   const long tiles = ((long)n + 63) / 64;  // k_ppo_values_split: 64 samples a block
   // k_ppo_grads: tiles of 128 samples; every block writes its partial row and
   // the reduce reads exactly the rows written
-  // hidden <= 128: blocks of 4 tile waves (NT), else 2 unit waves (NW)
+  // hidden <= 128: blocks of 4 tile waves (NT), else 2 unit waves (NW);
+  // fewer tiles than 4 per grads block: the 4 waves share each tile (coop)
   const int NT = NW == 1 ? 4 : 1;
-  const int blocks =
-      (int)std::min<long>((((long)n + 127) / 128 + NT - 1) / NT, swarm::kPpoBlocks);
+  const long tiles128 = ((long)n + 127) / 128;
+  const bool coop = NW == 1 && tiles128 < 4L * swarm::kPpoBlocks;
+  const int blocks = (int)std::min<long>(coop ? tiles128 : (tiles128 + NT - 1) / NT,
+                                         swarm::kPpoBlocks);
   const unsigned vblocks = (unsigned)(((n + 1) / 2 + 255) / 256);
   // V of every sample, GAE + dL/dV (+ the table), then the gradients
 #define SWARM_PPO(NN, DD, KK)                                                                 \
@@ -3216,8 +3317,13 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
       hipLaunchKernelGGL((swarm::k_ppo_gae<0, DD, KK>), ggrid, dim3(256), 0, s, rewards,      \
                          values, T, S, gamma, lambda, adv, dv, spart, gae_blocks, pk);        \
     constexpr int TT = NN == 1 ? 4 : 1;                                                       \
-    const void* fn = reinterpret_cast<const void*>(&swarm::k_ppo_grads<NN, TT, DD, KK>);      \
-    const int lds = swarm::ppo_grads_lds_floats<NN, TT, DD, KK>() * (int)sizeof(float);       \
+    if (NN == 1 && coop) SWARM_PPO_GRADS(NN, TT, NN == 1, DD, KK);                            \
+    else SWARM_PPO_GRADS(NN, TT, false, DD, KK);                                              \
+  } while (0)
+#define SWARM_PPO_GRADS(NN, TT, CO, DD, KK)                                                   \
+  do {                                                                                        \
+    const void* fn = reinterpret_cast<const void*>(&swarm::k_ppo_grads<NN, TT, CO, DD, KK>);  \
+    const int lds = swarm::ppo_grads_lds_floats<NN, TT, CO, DD, KK>() * (int)sizeof(float);   \
     if (lds > 65536)                                                                          \
       (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);         \
     hipEvent_t ev0 = nullptr, ev1 = nullptr;                                                 \
@@ -3225,7 +3331,7 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
         hipEventCreate(&ev1) == hipSuccess)                                                   \
       (void)hipEventRecord(ev0, s);                                                           \
     for (int rep = 0; rep < (ev1 ? g_ppo_prof.reps : 1); ++rep) /* same partial rows */      \
-      hipLaunchKernelGGL((swarm::k_ppo_grads<NN, TT, DD, KK>), dim3((unsigned)blocks),       \
+      hipLaunchKernelGGL((swarm::k_ppo_grads<NN, TT, CO, DD, KK>), dim3((unsigned)blocks),   \
                          dim3(64 * NN * TT),                                                  \
                          (size_t)lds, s, x, n, d_in, w1, b1, hidden, wa, ba, k, wc, bc,       \
                          actions, old_logp, adv, dv, spart, gae_blocks, table, clip_eps,      \
@@ -3257,6 +3363,7 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
   else
     SWARM_PPO_H(2);
 #undef SWARM_PPO_H
+#undef SWARM_PPO_GRADS
 #undef SWARM_PPO
   const int size = swarm::ppo_grad_size(d_in, hidden, k);
   hipLaunchKernelGGL(swarm::k_ppo_reduce, dim3((unsigned)((size + 63) / 64)), dim3(1024), 0, s,

@@ -237,10 +237,17 @@ struct Scratch {
   int32_t S;          // slots per env
   int32_t wmax;       // S / 64
   uint64_t* phase;    // [32] build phase stamps (SWARM_PHASE_TIMING builds only)
-  // profiling only (else null): [kRoles][2] earliest start / latest end
-  // (device wall clock) of each workgroup role of the launches of one window
+  // profiling only (else null): [kRoles][kStampSub][2] earliest start /
+  // latest end (device wall clock) of each workgroup role of the launches of
+  // one window
   unsigned long long* rstamp;
 };
+
+// Launch stamps are spread over kStampSub (min, max) pairs by workgroup
+// (blockIdx.x mod kStampSub) so that the atomics of a launch's waves do not
+// queue on one address (which stretched the stamped launches); the reader
+// takes the min / max over the pairs.
+constexpr int kStampSub = 64;
 
 // Workgroup roles of the window's launches (role_begin / role_end, rstamp)
 enum RoleId {
@@ -256,11 +263,14 @@ enum RoleId {
 };
 
 __device__ __forceinline__ void role_begin(const Scratch& sc, int r) {
-  if (sc.rstamp && threadIdx.x == 0) atomicMin(&sc.rstamp[2 * r], (unsigned long long)wall_clock64());
+  if (sc.rstamp && threadIdx.x == 0)
+    atomicMin(&sc.rstamp[2 * (r * kStampSub + (blockIdx.x & (kStampSub - 1)))],
+              (unsigned long long)wall_clock64());
 }
 __device__ __forceinline__ void role_end(const Scratch& sc, int r) {
   if (sc.rstamp && (threadIdx.x & 63) == 0)
-    atomicMax(&sc.rstamp[2 * r + 1], (unsigned long long)wall_clock64());
+    atomicMax(&sc.rstamp[2 * (r * kStampSub + (blockIdx.x & (kStampSub - 1))) + 1],
+              (unsigned long long)wall_clock64());
 }
 
 #ifdef SWARM_PHASE_TIMING
@@ -1126,9 +1136,137 @@ __host__ __device__ inline size_t build_lds_words(int n, int pair_cap) {
 // >= rc_max + skin (global arrays for the chip-wide pair search).
 // The body runs in the workgroup of env e (k_build_sort, or a workgroup of a
 // fused launch that carries the build along: k_vgrid_sort).
-template <int CH>  // particles per thread kept in registers across the scan (4, or 16 above 4096)
+// The pair search of build_sort_body<CH, true>, from the sort's own LDS:
+// the sorted records (rx, ry, rid: N entries, one pass), the cell ends
+// (cend[c] = end of cell c after the claims) -- no memory latency between
+// the sort and the pair list, whose pairs (i < j, within r_i + r_j + skin,
+// as build_pairs_body) go to gplist[e] with their count in gnpairs[e].
+// Each thread takes its CH entries; an entry's six stencil ranges are one
+// flat candidate index (as build_pairs_body: lanes with different range
+// splits stay in step), up to kKeep pairs per entry in registers, one block
+// scan for the offsets, and an entry with more pairs rescans to write them.
+// Periodic 2-D boxes.
+template <int CH>
+__device__ __forceinline__ void sort_pairs_lds(const Derived* __restrict__ d, const Scratch& sc,
+                                               int lx, int ly, int e, int N,
+                                               const int32_t* cend, const uint32_t* rx,
+                                               const uint32_t* ry, const int32_t* rid,
+                                               int32_t* wave_sums) {
+  constexpr int kKeep = 4;
+  __shared__ float nb2[kMaxSpecies * kMaxSpecies];
+  const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int k = tid; k < kMaxSpecies * kMaxSpecies; k += T) nb2[k] = d->nb2[k];
+  __syncthreads();
+  const int ncx = 1 << lx, ncy = 1 << ly;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+  uint32_t keep[CH][kKeep];
+  int found[CH], off6[CH][6], pre6[CH][7];
+  int mine = 0;
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int ps = tid + k * T;
+    found[k] = 0;
+#pragma unroll
+    for (int u = 0; u < kKeep; ++u) keep[k][u] = 0u;
+    pre6[k][0] = 0;
+    if (ps >= N) {
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        off6[k][r] = 0;
+        pre6[k][r + 1] = 0;
+      }
+      continue;
+    }
+    const int pk = rid[ps], i = pk & 0xffffff;
+    const uint32_t qx = rx[ps], qy = ry[ps];
+    const int c0 = cell_index(qx, qy, lx, ly);
+    const int cx = c0 & (ncx - 1), cy = c0 >> lx;
+    const int xa = ncx >= 3 ? max(cx - 1, 0) : 0;
+    const int xb = ncx >= 3 ? min(cx + 1, ncx - 1) : ncx - 1;
+    const int xw = ncx >= 3 ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
+    // the six ranges (three rows, each a run of cells plus its wrap cell)
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const int oy = loy + (r >> 1), part = r & 1;
+      const bool use = oy <= hiy && (part == 0 || xw >= 0);
+      const int row = ((cy + oy + ncy) & (ncy - 1)) << lx;
+      const int c_lo = row | (part == 0 ? xa : xw), c_hi = row | (part == 0 ? xb : xw);
+      const int jb = use ? (c_lo ? cend[c_lo - 1] : 0) : 0;
+      const int je = use ? cend[c_hi] : 0;
+      off6[k][r] = jb - pre6[k][r];
+      pre6[k][r + 1] = pre6[k][r] + (je - jb);
+    }
+    const float* nb2_row = nb2 + (pk >> 24) * kMaxSpecies;
+    const int total = pre6[k][6];
+    for (int f = 0; f < total; ++f) {
+      int o = off6[k][0];
+#pragma unroll
+      for (int r = 1; r < 6; ++r) o = f >= pre6[k][r] ? off6[k][r] : o;
+      const int jj = f + o;
+      const int pj = rid[jj], j = pj & 0xffffff;
+      const float ddx = (float)(int32_t)(rx[jj] - qx) * sx0;
+      const float ddy = (float)(int32_t)(ry[jj] - qy) * sx1;
+      if (i < j && ddx * ddx + ddy * ddy < nb2_row[pj >> 24]) {
+        const uint32_t kv = (uint32_t)i | ((uint32_t)j << 16);
+#pragma unroll
+        for (int u = 0; u < kKeep; ++u) keep[k][u] = found[k] == u ? kv : keep[k][u];
+        ++found[k];
+      }
+    }
+    mine += found[k];
+  }
+  // block exclusive scan of the threads' counts (waves in order)
+  const int v = wave_incl_scan(mine);
+  if (lane == 63) wave_sums[wv] = v;
+  __syncthreads();
+  int before = 0, total_all = 0;
+  for (int q = 0; q < (T >> 6); ++q) {
+    const int c = wave_sums[q];
+    before += q < wv ? c : 0;
+    total_all += c;
+  }
+  int off = before + v - mine;
+  uint32_t* out = sc.gplist + (size_t)e * sc.pair_cap;
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int ps = tid + k * T;
+    if (found[k] <= kKeep) {
+#pragma unroll
+      for (int u = 0; u < kKeep; ++u)
+        if (u < found[k] && off + u < sc.pair_cap) out[off + u] = keep[k][u];
+    } else {  // a denser entry: its candidates again, every pair written
+      const int pk = rid[ps], i = pk & 0xffffff;
+      const uint32_t qx = rx[ps], qy = ry[ps];
+      const float* nb2_row = nb2 + (pk >> 24) * kMaxSpecies;
+      int w = 0;
+      for (int f = 0; f < pre6[k][6]; ++f) {
+        int o = off6[k][0];
+#pragma unroll
+        for (int r = 1; r < 6; ++r) o = f >= pre6[k][r] ? off6[k][r] : o;
+        const int jj = f + o;
+        const int pj = rid[jj], j = pj & 0xffffff;
+        const float ddx = (float)(int32_t)(rx[jj] - qx) * sx0;
+        const float ddy = (float)(int32_t)(ry[jj] - qy) * sx1;
+        if (i < j && ddx * ddx + ddy * ddy < nb2_row[pj >> 24]) {
+          if (off + w < sc.pair_cap) out[off + w] = (uint32_t)i | ((uint32_t)j << 16);
+          ++w;
+        }
+      }
+    }
+    off += found[k];
+  }
+  if (tid == 0) sc.gnpairs[e] = total_all;  // > pair_cap: the build takes the global path
+}
+
+// kPairs (ride-along launches, periodic 2-D, one staging pass): the pair
+// search follows from the sorted rows in LDS (sort_pairs_lds).
+// CH: particles per thread kept in registers across the scan (4, or 16
+// above 4096).
+template <int CH, bool kPairs = false>
 __device__ __forceinline__ void build_sort_body(const DevState& st, const Scratch& sc, int lx,
-                                                int ly, int e, unsigned char* smem) {
+                                                int ly, int e, unsigned char* smem,
+                                                const Derived* __restrict__ d = nullptr) {
   const int T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly);
@@ -1227,6 +1365,9 @@ __device__ __forceinline__ void build_sort_body(const DevState& st, const Scratc
     }
     for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
     SWARM_STAMP(5);
+    if constexpr (kPairs) {
+      if (K >= N) sort_pairs_lds<CH>(d, sc, lx, ly, e, N, cnt, lx_, ly_, lid, wave_sums);
+    }
     return;
   }
 #pragma unroll
@@ -1282,9 +1423,20 @@ __global__ __launch_bounds__(1024) void k_sort_scan(Scratch sc, int lx, int ly) 
   const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x;
   const int ncell = 1 << (lx + ly);
   int32_t* g = sc.gcnt + ((size_t)e << (lx + ly));
-  for (int c = tid; c < ncell; c += T) {
-    cnt[c] = g[c];
-    g[c] = 0;  // the next build's counters
+  // the counts into LDS, kB loads in flight per thread (one memory latency
+  // per kB cells, not per cell), then the next build's counters zeroed
+  constexpr int kB = 16;
+  for (int c0 = tid; c0 < ncell; c0 += kB * T) {
+    int32_t v[kB];
+#pragma unroll
+    for (int u = 0; u < kB; ++u) v[u] = c0 + u * T < ncell ? g[c0 + u * T] : 0;
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      if (c0 + u * T < ncell) {
+        cnt[c0 + u * T] = v[u];
+        g[c0 + u * T] = 0;
+      }
+    }
   }
   if (tid == 0) {
     sc.gnpairs[e] = 0;
@@ -2867,10 +3019,12 @@ __device__ __forceinline__ void run_wave_dispatch(const Derived* __restrict__ d,
 // latest wave end, realtime clock (100 MHz); null otherwise (one uniform
 // branch per block / wave).
 __device__ __forceinline__ void stamp_start(unsigned long long* tstamp) {
-  if (tstamp && threadIdx.x == 0) atomicMin(&tstamp[0], (unsigned long long)wall_clock64());
+  if (tstamp && threadIdx.x == 0)
+    atomicMin(&tstamp[2 * (blockIdx.x & (kStampSub - 1))], (unsigned long long)wall_clock64());
 }
 __device__ __forceinline__ void stamp_end(unsigned long long* tstamp) {
-  if (tstamp && (threadIdx.x & 63) == 0) atomicMax(&tstamp[1], (unsigned long long)wall_clock64());
+  if (tstamp && (threadIdx.x & 63) == 0)
+    atomicMax(&tstamp[2 * (blockIdx.x & (kStampSub - 1)) + 1], (unsigned long long)wall_clock64());
 }
 
 // XCD-aware placement of per-env work (envs_per_xcd_map: blocks of one env):

@@ -306,14 +306,16 @@ __host__ __device__ constexpr int ppo_combine_floats() {
   return 2 * (D + 1 + K + 1) + K + 1;
 }
 
-template <int NW, int NT, int D, int K>
+template <int NW, int NT, bool kCoop, int D, int K>
 __host__ __device__ constexpr int ppo_grads_lds_floats() {
-  // per tile wave: sample rows [128][kRow] | logit partials of unit waves 1..
-  // [NW - 1][K][128]; after the tiles, the combine buffer [kC][64] aliases them
-  return NT * 128 * PpoRow<D, K>::kRow + (NW - 1) * K * 128 >
-                 (NT > 1 ? 64 * ppo_combine_floats<D, K>() : 0)
-             ? NT * 128 * PpoRow<D, K>::kRow + (NW - 1) * K * 128
-             : 64 * ppo_combine_floats<D, K>();
+  // sample rows [128][kRow] per tile in flight (NT, or one shared by the
+  // kCoop waves) | logit partials of the other waves of a tile
+  // [max(NW, NT) - 1][K][128]; after the tiles, the combine buffer [kC][64]
+  // aliases them
+  constexpr int rows = (kCoop ? 1 : NT) * 128 * PpoRow<D, K>::kRow;
+  constexpr int part = ((kCoop ? NT : NW) - 1) * K * 128;
+  constexpr int comb = NT > 1 ? 64 * ppo_combine_floats<D, K>() : 0;
+  return rows + part > comb ? rows + part : comb;
 }
 
 // The LDS hand-over between the phases of one tile: the whole block when
@@ -335,8 +337,11 @@ __device__ __forceinline__ ppo_f2 ppo_splat(float v) { return ppo_f2{v, v}; }
 
 // Per-block parameter gradients.  NW waves each own 128 hidden units of a
 // tile (hidden > 128), or (NW = 1) NT waves each take their own tiles and
-// add their sums in a fixed order at the end.  Dynamic LDS
-// ppo_grads_lds_floats<NW, NT, D, K>() floats; partial: [gridDim.x][ppo_grad_size].  Tiles of 128 samples, three phases, no
+// add their sums in a fixed order at the end; kCoop (few samples: a wave per
+// tile would leave most SIMDs idle): the NT waves share each tile, phase F
+// split over their units and phase B over their samples.  Dynamic LDS
+// ppo_grads_lds_floats<NW, NT, kCoop, D, K>() floats; partial:
+// [gridDim.x][ppo_grad_size].  Tiles of 128 samples, three phases, no
 // cross-lane broadcasts (v_readlane) and no transposes:
 //   F  lane = the sample pair (s, s + 64) as the two halves of packed fp32
 //      registers: the logits over the wave's units, each unit's hidden
@@ -354,7 +359,7 @@ __device__ __forceinline__ ppo_f2 ppo_splat(float v) { return ppo_f2{v, v}; }
 // (1-128-(4+1) stock) make matrix cores a poor fit: the heads' 5 columns
 // would fill 5 of every 16 rows of a v_mfma_f32_16x16x4_f32, whose f32 rate
 // is the packed-VALU rate on gfx950 (MI355X_MICROARCH.md, "Peak FP32").
-template <int NW, int NT, int D, int K>
+template <int NW, int NT, bool kCoop, int D, int K>
 __global__ __launch_bounds__(64 * NW * NT) void k_ppo_grads(
     const float* __restrict__ x, int n, int d, const float* __restrict__ w1,
     const float* __restrict__ b1, int hidden, const float* __restrict__ wa,
@@ -367,12 +372,16 @@ __global__ __launch_bounds__(64 * NW * NT) void k_ppo_grads(
   constexpr int KP = K + 1, kTab = Tb::kStride, kRow = PpoRow<D, K>::kRow;
   extern __shared__ float ppo_lds[];
   static_assert(NW == 1 || NT == 1, "tile waves or unit waves, not both");
+  static_assert(!kCoop || (NW == 1 && 128 % NT == 0), "kCoop splits one 128-unit wave's work");
+  // the waves that share a tile (their logit partials meet in LDS)
+  constexpr int NX = kCoop ? NT : NW;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int w = NW > 1 ? wid : 0;  // unit wave
   const int t = NW > 1 ? 0 : wid;  // tile wave
+  const int wx = NX > 1 ? wid : 0;  // index among the waves of a tile
   const int wu = __builtin_amdgcn_readfirstlane(w);
-  float* srow = ppo_lds + t * 128 * kRow;     // [128][kRow]
-  float* red = ppo_lds + NT * 128 * kRow;     // [NW - 1][K][128]
+  float* srow = ppo_lds + (kCoop ? 0 : t) * 128 * kRow;  // [128][kRow]
+  float* red = ppo_lds + (kCoop ? 1 : NT) * 128 * kRow;  // [NX - 1][K][128]
   const int u0 = 128 * w + lane, u1 = u0 + 64;
   const bool in0 = u0 < hidden, in1 = u1 < hidden;
   ppo_f2 w1p[D], wop[KP];
@@ -406,11 +415,23 @@ __global__ __launch_bounds__(64 * NW * NT) void k_ppo_grads(
     gwop[q] = ppo_splat(0.0f);
     gbias[q] = 0.0f;
   }
-  // this wave's unit rows (zero rows past hidden up to 128 NW), whole quads
+  // this wave's unit rows (zero rows past hidden up to 128 NW), whole quads;
+  // kCoop: its share of them in phase F, and its share of the samples in B
   const float* urows = table + (size_t)wu * 128 * kTab;
-  const int nunits = (min(128, hidden - 128 * wu) + 3) & ~3;
+  int nunits = (min(128, hidden - 128 * wu) + 3) & ~3;
+  int s_lo = 0, s_hi = 128;
+  if constexpr (kCoop) {
+    const int tu = __builtin_amdgcn_readfirstlane(t);
+    const int per_u = 128 / NT;
+    urows += (size_t)tu * per_u * kTab;
+    nunits = max(0, min(per_u, nunits - tu * per_u));
+    s_lo = tu * (128 / NT);
+    s_hi = s_lo + 128 / NT;
+  }
   const long tiles = ((long)n + 127) / 128;
-  for (long tile = (long)blockIdx.x * NT + t; tile < tiles; tile += (long)gridDim.x * NT) {
+  const long t0 = kCoop ? (long)blockIdx.x : (long)blockIdx.x * NT + t;
+  const long tstep = kCoop ? (long)gridDim.x : (long)gridDim.x * NT;
+  for (long tile = t0; tile < tiles; tile += tstep) {
     const long sa = tile * 128 + lane, sb = sa + 64;
     ppo_f2 xs[D];
     {
@@ -438,16 +459,16 @@ __global__ __launch_bounds__(64 * NW * NT) void k_ppo_grads(
 #pragma unroll
       for (int q = 0; q < K; ++q) z[q] = __builtin_elementwise_fma(ppo_splat(r[q]), h, z[q]);
     }
-    if (NW > 1 && w > 0) {
+    if (NX > 1 && wx > 0) {
 #pragma unroll
       for (int q = 0; q < K; ++q) {
-        red[((w - 1) * K + q) * 128 + lane] = z[q].x;
-        red[((w - 1) * K + q) * 128 + 64 + lane] = z[q].y;
+        red[((wx - 1) * K + q) * 128 + lane] = z[q].x;
+        red[((wx - 1) * K + q) * 128 + 64 + lane] = z[q].y;
       }
     }
-    if (NW > 1) __syncthreads();
+    if (NX > 1) __syncthreads();
     // P: dL/dz and dL/dV of each sample, its row to LDS
-    if (w == 0) {
+    if (wx == 0) {
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
         const long si = half ? sb : sa;
@@ -457,7 +478,7 @@ __global__ __launch_bounds__(64 * NW * NT) void k_ppo_grads(
         for (int q = 0; q < K; ++q) {
           acc[q] = half ? z[q].y : z[q].x;
 #pragma unroll
-          for (int ww = 1; ww < NW; ++ww) acc[q] += red[((ww - 1) * K + q) * 128 + slot];
+          for (int ww = 1; ww < NX; ++ww) acc[q] += red[((ww - 1) * K + q) * 128 + slot];
         }
         float g[KP];
 #pragma unroll
@@ -513,10 +534,10 @@ __global__ __launch_bounds__(64 * NW * NT) void k_ppo_grads(
         for (int c = 0; c < D; ++c) row[KP + c] = half ? xs[c].y : xs[c].x;
       }
     }
-    ppo_group_sync<NW>();
-    // B: both units' gradients over the 128 samples
+    ppo_group_sync<NX>();
+    // B: both units' gradients over the tile's samples (kCoop: this wave's share)
 #pragma unroll 2
-    for (int s = 0; s < 128; ++s) {
+    for (int s = s_lo; s < s_hi; ++s) {
       float rv[kRow];
       const float4* r4 = reinterpret_cast<const float4*>(srow + s * kRow);
 #pragma unroll
@@ -545,7 +566,7 @@ __global__ __launch_bounds__(64 * NW * NT) void k_ppo_grads(
       for (int c = 0; c < D; ++c)
         gw1p[c] = __builtin_elementwise_fma(dh, ppo_splat(rv[KP + c]), gw1p[c]);
     }
-    ppo_group_sync<NW>();  // the rows (and red) are rewritten next tile
+    ppo_group_sync<NX>();  // the rows (and red) are rewritten next tile
   }
   if constexpr (NT > 1) {
     // tile waves 1.. hand their sums to wave 0 in order: ((s0 + s1) + s2) + ...
