@@ -261,9 +261,17 @@ __device__ __forceinline__ void vision_grid_body(const DevState& st, const Visio
   if (e == 0)
     for (int i = tid; i < N; i += T) vs.agent_row[i] = -1;
   __syncthreads();
-  if (e == 0)
-    for (int a = tid; a < n_agents; a += T)
-      if ((unsigned)agents[a] < (unsigned)N) vs.agent_row[agents[a]] = a;
+  if (e == 0) {  // agents' rows: their ids loaded together (one memory latency)
+    constexpr int kA = 8;
+    for (int a0 = tid; a0 < n_agents; a0 += kA * T) {
+      int ag[kA];
+#pragma unroll
+      for (int u = 0; u < kA; ++u) ag[u] = a0 + u * T < n_agents ? agents[a0 + u * T] : -1;
+#pragma unroll
+      for (int u = 0; u < kA; ++u)
+        if ((unsigned)ag[u] < (unsigned)N) vs.agent_row[ag[u]] = a0 + u * T;
+    }
+  }
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   int32_t* so = start + (size_t)e * (ncell + 1);
   constexpr int kPer = 8;  // colloids per thread kept in registers (N <= 8 T)
@@ -3257,6 +3265,24 @@ int swarm_ppo_profile(int32_t enable, double* grads_ms, int32_t* launches) {
   return rc;
 }
 
+namespace {
+// Workgroups of `fn` resident on the whole device at once (at least one).
+int ppo_resident_blocks(const void* fn, int threads, size_t lds) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 1;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  return std::max(1, per_cu * cus);
+}
+}  // namespace
+
 int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
                          const int64_t* actions, const float* old_logp, const float* rewards,
                          const float* w1, const float* b1, int32_t hidden, const float* wa,
@@ -3294,9 +3320,9 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
   const int NT = NW == 1 ? 4 : 1;
   const long tiles128 = ((long)n + 127) / 128;
   const bool coop = NW == 1 && tiles128 < 4L * swarm::kPpoBlocks;
-  const int blocks = (int)std::min<long>(coop ? tiles128 : (tiles128 + NT - 1) / NT,
-                                         swarm::kPpoBlocks);
-  const unsigned vblocks = (unsigned)(((n + 1) / 2 + 255) / 256);
+  int blocks = (int)std::min<long>(coop ? tiles128 : (tiles128 + NT - 1) / NT,
+                                   swarm::kPpoBlocks);
+  const unsigned vblocks = (unsigned)(((n + 3) / 4 + 255) / 256);  // k_ppo_values: 4 a thread
   // V of every sample, GAE + dL/dV (+ the table), then the gradients
 #define SWARM_PPO(NN, DD, KK)                                                                 \
   do {                                                                                        \
@@ -3326,6 +3352,9 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
     const int lds = swarm::ppo_grads_lds_floats<NN, TT, CO, DD, KK>() * (int)sizeof(float);   \
     if (lds > 65536)                                                                          \
       (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);         \
+    /* no more blocks than are resident at once: a second round of blocks */                  \
+    /* would leave most SIMDs idle for its tail */                                            \
+    if (!(CO)) blocks = std::min(blocks, ppo_resident_blocks(fn, 64 * NN * TT, lds));         \
     hipEvent_t ev0 = nullptr, ev1 = nullptr;                                                 \
     if (g_ppo_prof.on && hipEventCreate(&ev0) == hipSuccess &&                                \
         hipEventCreate(&ev1) == hipSuccess)                                                   \

@@ -227,18 +227,28 @@ __device__ __forceinline__ void policy_body(const MlpArgs& m, int vb, float* sw)
   float* __restrict__ out_t = m.out_t;
   float* __restrict__ out_logits = m.out_logits;
   constexpr int R = MlpRow<D, K>::kStride;
-  for (int t = threadIdx.x; t < hidden * R; t += blockDim.x) {
-    const int j = t / R, c = t - j * R;
-    float v = 0.0f;
-    if (c < D) {
-      v = c < d_in ? w1[(size_t)j * d_in + c] : 0.0f;
-    } else if (c == D) {
-      v = b1[j];
-    } else if (c >= D + 4) {
-      const int q = c - D - 4;
-      v = q < k ? w2[(size_t)q * hidden + j] : 0.0f;
+  // the weights into LDS rows, four entries per thread loaded together
+  for (int t0 = threadIdx.x; t0 < hidden * R; t0 += 4 * (int)blockDim.x) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + u * (int)blockDim.x;
+      const int j = t / R, c = t - j * R;
+      v[u] = 0.0f;
+      if (t < hidden * R) {
+        if (c < D) {
+          v[u] = c < d_in ? w1[(size_t)j * d_in + c] : 0.0f;
+        } else if (c == D) {
+          v[u] = b1[j];
+        } else if (c >= D + 4) {
+          const int q = c - D - 4;
+          v[u] = q < k ? w2[(size_t)q * hidden + j] : 0.0f;
+        }
+      }
     }
-    sw[t] = v;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (t0 + u * (int)blockDim.x < hidden * R) sw[t0 + u * (int)blockDim.x] = v[u];
   }
   float* sb2 = sw + hidden * R;
   if (threadIdx.x < K) sb2[threadIdx.x] = (int)threadIdx.x < k ? b2[threadIdx.x] : 0.0f;

@@ -85,9 +85,10 @@ __device__ __forceinline__ void ppo_pack_entry(const float* __restrict__ w1,
 
 typedef float ppo_f2 __attribute__((ext_vector_type(2)));
 
-// V of every sample: one thread per two adjacent samples (packed fp32 FMAs,
-// v_pk_fma_f32), their features in registers, each unit's parameters
-// wave-uniform scalar loads.
+// V of every sample: one thread per four samples -- two pairs of adjacent
+// samples in packed fp32 registers (v_pk_fma_f32), their features in
+// registers, each unit's parameters wave-uniform scalar loads (amortised
+// over the four).
 template <int D>
 __global__ __launch_bounds__(256) void k_ppo_values(const float* __restrict__ x, int n, int d,
                                                     const float* __restrict__ w1,
@@ -95,29 +96,41 @@ __global__ __launch_bounds__(256) void k_ppo_values(const float* __restrict__ x,
                                                     const float* __restrict__ wc,
                                                     const float* __restrict__ bc,
                                                     float* __restrict__ values) {
-  const long s = 2 * ((long)blockIdx.x * blockDim.x + threadIdx.x);
+  const long s = 4 * ((long)blockIdx.x * blockDim.x + threadIdx.x);
   if (s >= n) return;
-  const long s1 = min(s + 1, (long)n - 1);  // an odd n pairs the last sample with itself
-  ppo_f2 xs[D];
-  const float* xa = x + (size_t)s * d;
-  const float* xb = x + (size_t)s1 * d;
+  ppo_f2 xs[2][D];
 #pragma unroll
-  for (int c = 0; c < D; ++c) {
-    const float va = xa[min(c, d - 1)], vb = xb[min(c, d - 1)];
-    xs[c] = c < d ? ppo_f2{va, vb} : ppo_f2{0.0f, 0.0f};
+  for (int p = 0; p < 2; ++p) {
+    // past n: the last sample again (computed, not stored)
+    const float* xa = x + (size_t)min(s + 2 * p, (long)n - 1) * d;
+    const float* xb = x + (size_t)min(s + 2 * p + 1, (long)n - 1) * d;
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      const float va = xa[min(c, d - 1)], vb = xb[min(c, d - 1)];
+      xs[p][c] = c < d ? ppo_f2{va, vb} : ppo_f2{0.0f, 0.0f};
+    }
   }
-  ppo_f2 v = bc[0];
+  ppo_f2 v[2] = {(ppo_f2)bc[0], (ppo_f2)bc[0]};
 #pragma unroll 4
   for (int j = 0; j < hidden; ++j) {
-    ppo_f2 h = b1[j];
+    const float bj = b1[j], cj = wc[j];
+    float wj[D];
 #pragma unroll
-    for (int c = 0; c < D; ++c)  // clamped load: a feature c >= d is zero
-      h = __builtin_elementwise_fma((ppo_f2)w1[(size_t)j * d + min(c, d - 1)], xs[c], h);
-    h = __builtin_elementwise_max(h, (ppo_f2)0.0f);
-    v = __builtin_elementwise_fma((ppo_f2)wc[j], h, v);
+    for (int c = 0; c < D; ++c) wj[c] = w1[(size_t)j * d + min(c, d - 1)];  // c >= d: x is 0
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      ppo_f2 h = bj;
+#pragma unroll
+      for (int c = 0; c < D; ++c) h = __builtin_elementwise_fma((ppo_f2)wj[c], xs[p][c], h);
+      h = __builtin_elementwise_max(h, (ppo_f2)0.0f);
+      v[p] = __builtin_elementwise_fma((ppo_f2)cj, h, v[p]);
+    }
   }
-  values[s] = v.x;
-  if (s + 1 < n) values[s + 1] = v.y;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    if (s + 2 * p < n) values[s + 2 * p] = v[p].x;
+    if (s + 2 * p + 1 < n) values[s + 2 * p + 1] = v[p].y;
+  }
 }
 
 // V at small sample counts, where the per-thread chain over all units is
@@ -449,7 +462,7 @@ __global__ __launch_bounds__(64 * NW * NT) void k_ppo_grads(
     ppo_f2 z[K];
 #pragma unroll
     for (int q = 0; q < K; ++q) z[q] = ppo_splat(0.0f);
-#pragma unroll 4
+#pragma unroll 8
     for (int u = 0; u < nunits; ++u) {
       const float* r = urows + (size_t)u * kTab;
       ppo_f2 h = ppo_splat(r[Tb::kB1]);
@@ -535,19 +548,27 @@ __global__ __launch_bounds__(64 * NW * NT) void k_ppo_grads(
       }
     }
     ppo_group_sync<NX>();
-    // B: both units' gradients over the tile's samples (kCoop: this wave's share)
+    // B: both units' gradients over the tile's samples (kCoop: this wave's
+    // share); the next sample's row is read while this one's is used
+    float4 nxt[kRow / 4];
+#pragma unroll
+    for (int i = 0; i < kRow / 4; ++i)
+      nxt[i] = reinterpret_cast<const float4*>(srow + s_lo * kRow)[i];
 #pragma unroll 2
     for (int s = s_lo; s < s_hi; ++s) {
       float rv[kRow];
-      const float4* r4 = reinterpret_cast<const float4*>(srow + s * kRow);
 #pragma unroll
       for (int i = 0; i < kRow / 4; ++i) {
-        const float4 v = r4[i];
+        const float4 v = nxt[i];
         rv[4 * i] = v.x;
         rv[4 * i + 1] = v.y;
         rv[4 * i + 2] = v.z;
         rv[4 * i + 3] = v.w;
       }
+      const int sn = min(s + 1, s_hi - 1);
+#pragma unroll
+      for (int i = 0; i < kRow / 4; ++i)
+        nxt[i] = reinterpret_cast<const float4*>(srow + sn * kRow)[i];
       ppo_f2 h = b1p;
 #pragma unroll
       for (int c = 0; c < D; ++c) h = __builtin_elementwise_fma(w1p[c], ppo_splat(rv[KP + c]), h);
