@@ -30,6 +30,8 @@ for line in $lines; do
       fetch) run fetch --pmc FETCH_SIZE ;;
       write) run write --pmc WRITE_SIZE ;;
       valu) run valu --pmc SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_WAVES ;;
+      sq) run sq --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS \
+            SQ_INSTS_LDS SQ_ACTIVE_INST_VALU ;;
     esac
   done
   echo "profiled $line"

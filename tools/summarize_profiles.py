@@ -6,7 +6,10 @@ Summarize a profiles/profile_round.sh run (one config-pure bench.py --only
   profiles/<tag>_pmc_summary.csv          per line and kernel: dispatches, mean
                                           duration (kernel trace), FETCH_SIZE,
                                           WRITE_SIZE, SQ_INSTS_VALU,
-                                          SQ_INSTS_VALU_TRANS_F32, SQ_WAVES
+                                          SQ_INSTS_VALU_TRANS_F32, SQ_WAVES and
+                                          (sq pass) SQ_WAVE_CYCLES, SQ_BUSY_CYCLES,
+                                          SQ_WAIT_INST_ANY, SQ_WAIT_INST_LDS,
+                                          SQ_INSTS_LDS, SQ_ACTIVE_INST_VALU
   profiles/<tag>_traffic.json             per line, the dominant kernels' rows:
                                           bytes per launch (FETCH_SIZE x 2 +
                                           WRITE_SIZE, KB -> B; MI355X_MICROARCH.md
@@ -32,7 +35,9 @@ dst = "profiles"
 DOMINANT = {"head": r"k_cluster_run", "batched": r"k_cluster_run", "c2": r"k_cluster_run",
             "c4": r"k_cluster_run", "c5": r"k_cluster_run", "c3train": r"k_cluster_run|k_ppo_grads"}
 TIMED_TAIL = 20  # bench.py --bd-reps
-COUNTERS = ["FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "SQ_INSTS_VALU_TRANS_F32", "SQ_WAVES"]
+COUNTERS = ["FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "SQ_INSTS_VALU_TRANS_F32", "SQ_WAVES",
+            "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS",
+            "SQ_INSTS_LDS", "SQ_ACTIVE_INST_VALU"]
 
 
 def short(name):
@@ -67,7 +72,7 @@ for line in bench.LINES:
         dur[short(r["Kernel_Name"])].append(
             (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3)  # ns -> us
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
-    for sub in ("fetch", "write", "valu"):
+    for sub in ("fetch", "write", "valu", "sq"):
         path = f"{d}/{sub}/run_counter_collection.csv"
         if not os.path.exists(path):
             continue
@@ -99,6 +104,13 @@ for line in bench.LINES:
                 "valu_insts_per_launch": mean["SQ_INSTS_VALU"],
                 "valu_trans_per_launch": mean["SQ_INSTS_VALU_TRANS_F32"],
                 "waves_per_launch": mean["SQ_WAVES"],
+                # the sq pass (when run): wave-cycles and the cycles waves
+                # waited on any instruction / on LDS, per launch
+                "sq_wave_cycles": mean["SQ_WAVE_CYCLES"],
+                "sq_wait_inst_any": mean["SQ_WAIT_INST_ANY"],
+                "sq_wait_inst_lds": mean["SQ_WAIT_INST_LDS"],
+                "sq_insts_lds": mean["SQ_INSTS_LDS"],
+                "sq_active_inst_valu": mean["SQ_ACTIVE_INST_VALU"],
                 "src_sha": sha,
             })
 with open(f"{dst}/{tag}_pmc_summary.csv", "w", newline="") as f:
