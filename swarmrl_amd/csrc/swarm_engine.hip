@@ -676,12 +676,25 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
 // the engine stream guarantees.  The build's workgroups take the first block
 // indices of each launch: the build chain (sort -> pairs -> cluster build)
 // is the longer one, so its workgroups are dealt out first.
+// Block index of a fused launch whose first `nfirst` roles are the build's:
+// dealt out first (default), or last (-DSWARM_BUILD_LAST: the round-3 order,
+// kept for A/B measurement).
+__device__ __forceinline__ int fused_block(int nfirst) {
+#ifdef SWARM_BUILD_LAST
+  const int rest = (int)gridDim.x - nfirst;
+  return (int)blockIdx.x < rest ? (int)blockIdx.x + nfirst : (int)blockIdx.x - rest;
+#else
+  (void)nfirst;
+  return (int)blockIdx.x;
+#endif
+}
+
 template <int CH, bool kPairs>
 __global__ __launch_bounds__(1024) void k_vgrid_sort(DevState st, VisionArgs va, Scratch sc,
                                                      int lxb, int lyb,
                                                      const Derived* __restrict__ d) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const int b = blockIdx.x;
+  const int b = fused_block(va.n_envs);
   const int role = b < va.n_envs ? swarm::kRoleSort : swarm::kRoleVgrid;
   swarm::role_begin(sc, role);
   if (b < va.n_envs)
@@ -694,7 +707,7 @@ __global__ __launch_bounds__(1024) void k_vgrid_sort(DevState st, VisionArgs va,
 // The pair blocks come first: theirs is the longer chain (the cluster build
 // waits on it), so they are dealt out before the cone blocks.  kStaged: the
 // pair blocks stage their env's sorted records in (dynamic) LDS.
-template <int NB, int G, bool kStaged>
+template <int NB, int G, bool kStaged, bool kLocal>
 __global__ __launch_bounds__(256) void k_vision_pairs(DevState st, const Derived* __restrict__ d,
                                                       VisionArgs va, int n_pblocks, Scratch sc,
                                                       int lxb, int lyb, int pair_bx) {
@@ -702,12 +715,12 @@ __global__ __launch_bounds__(256) void k_vision_pairs(DevState st, const Derived
   __shared__ float nb2[swarm::kMaxSpecies * swarm::kMaxSpecies];
   __shared__ int32_t uf[2 * 256];
   extern __shared__ __align__(16) uint32_t pstage[];
-  const int b = blockIdx.x;
+  const int b = fused_block(n_pblocks);
   const int role = b < n_pblocks ? swarm::kRolePairs : swarm::kRoleCone;
   swarm::role_begin(sc, role);
   if (b < n_pblocks) {
-    swarm::build_pairs_body<kStaged>(d, st, sc, lxb, lyb, b % pair_bx, b / pair_bx, nb2, uf,
-                                     pstage);
+    swarm::build_pairs_body<kStaged, kLocal>(d, st, sc, lxb, lyb, b % pair_bx, b / pair_bx, nb2,
+                                             uf, pstage);
   } else {
     vision_body<NB, G, false>(st, d, va, b - n_pblocks, 0, hits);
   }
@@ -722,7 +735,7 @@ template <int NB, int G>
 __global__ __launch_bounds__(1024) void k_vision_cbuild(DevState st, const Derived* __restrict__ d,
                                                         VisionArgs va, Scratch sc) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const int b = blockIdx.x;
+  const int b = fused_block(va.n_envs);
   const int role = b < va.n_envs ? swarm::kRoleCbuild : swarm::kRoleCone;
   swarm::role_begin(sc, role);
   if (b < va.n_envs)
@@ -737,7 +750,7 @@ template <int G, int D, int K>
 __global__ __launch_bounds__(1024) void k_policy_cbuild(swarm::MlpArgs m, int n_envs,
                                                         DevState st, Scratch sc) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const int b = blockIdx.x;
+  const int b = fused_block(n_envs);
   const int role = b < n_envs ? swarm::kRoleCbuild : swarm::kRoleMlp;
   swarm::role_begin(sc, role);
   if (b < n_envs) {
@@ -959,7 +972,7 @@ __global__ __launch_bounds__(1024) void k_field_vgrid_sort(FieldArgs f, int n_fb
                                                            int lyb,
                                                            const Derived* __restrict__ d) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const int b = blockIdx.x;
+  const int b = fused_block(2 * va.n_envs);
   const int role = b < va.n_envs       ? swarm::kRoleSort
                    : b < 2 * va.n_envs ? swarm::kRoleVgrid
                                        : swarm::kRoleField;
@@ -1343,8 +1356,15 @@ int launch_build(swarm_engine* e, hipStream_t stream) {
     return SWARM_OK;
   }
   if (e->params.n_dims != 3)
-    hipLaunchKernelGGL(swarm::k_build_pairs, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
-                       dim3(256), 0, stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb);
+  {
+    const dim3 pg((unsigned)((e->n + 255) / 256), (unsigned)e->n_envs);
+    if (e->sc.local_uf)
+      hipLaunchKernelGGL(swarm::k_build_pairs<true>, pg, dim3(256), 0, stream, e->d_derived,
+                         e->st, e->sc, e->lxb, e->lyb);
+    else
+      hipLaunchKernelGGL(swarm::k_build_pairs<false>, pg, dim3(256), 0, stream, e->d_derived,
+                         e->st, e->sc, e->lxb, e->lyb);
+  }
   HIP_TRY(hipGetLastError());
   // 2-D: the pair search left block-local union-find roots and a cross list
   // (build_pairs_body); 3-D (k_build_pairs3): the whole pair list is unioned
@@ -1392,8 +1412,12 @@ int flush_ride_along(swarm_engine* e) {
     HIP_TRY(hipGetLastError());
   }
   if (stage <= 2) {
-    hipLaunchKernelGGL(swarm::k_build_pairs, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
-                       dim3(256), 0, e->stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb);
+    if (e->sc.local_uf)
+      hipLaunchKernelGGL(swarm::k_build_pairs<true>, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
+                         dim3(256), 0, e->stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb);
+    else
+      hipLaunchKernelGGL(swarm::k_build_pairs<false>, dim3((unsigned)((e->n + 255) / 256), e->n_envs),
+                         dim3(256), 0, e->stream, e->d_derived, e->st, e->sc, e->lxb, e->lyb);
     HIP_TRY(hipGetLastError());
   }
   if (e->sc.local_uf)
@@ -1842,12 +1866,14 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   e->sc.local_uf = n_particles > 4096 ? 1 : 0;
   if (const char* olu = std::getenv("SWARMRL_AMD_LOCAL_UF")) e->sc.local_uf = olu[0] != '0';
   if (const char* ora = std::getenv("SWARMRL_AMD_ROT_AHEAD")) e->rot_ahead = ora[0] != '0';
-  // 2-D LDS builds without the local union-find: the pair-search blocks
-  // write their own regions of the list (no returning global atomic on the
-  // search's chain); SWARMRL_AMD_PAIR_REGIONS=0 turns it off
+  // 2-D LDS builds without the local union-find: with
+  // SWARMRL_AMD_PAIR_REGIONS=1 the pair-search blocks write their own regions
+  // of the list (no returning global atomic on the search's chain).  Off by
+  // default: the build's gather of the regions costs more than the atomic
+  // (4096 colloids: cluster build 15.2 vs 15.8 us, 44.8 vs 44.1 M)
   e->sc.pair_region = 0;
   if (params->n_dims == 2 && !e->big_build && !e->sc.local_uf && n_particles <= 4096 &&
-      !(std::getenv("SWARMRL_AMD_PAIR_REGIONS") && std::getenv("SWARMRL_AMD_PAIR_REGIONS")[0] == '0'))
+      std::getenv("SWARMRL_AMD_PAIR_REGIONS") && std::getenv("SWARMRL_AMD_PAIR_REGIONS")[0] == '1')
     e->sc.pair_region = e->sc.pair_cap / ((n_particles + 255) / 256);
   e->sc.rstamp = nullptr;
   e->graph_event_nodes = std::getenv("SWARMRL_AMD_PROFILE_EVENT_NODES") &&
@@ -2008,8 +2034,9 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     if (ov && ov[0] == '1') want = true;
     e->pairs_staged = want && params->n_dims == 2 && pb <= 96 * 1024;
     if (e->pairs_staged)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_vision_pairs<4, 16, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)pb);
+      for (const void* f : {reinterpret_cast<const void*>(&k_vision_pairs<4, 16, true, false>),
+                            reinterpret_cast<const void*>(&k_vision_pairs<4, 16, true, true>)})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pb);
   }
   rc = rc ? rc : dev_alloc(e, &e->sc.gnpairs, (size_t)n_envs);
   rc = rc ? rc : dev_alloc(e, &e->sc.gbcnt, (size_t)n_envs * ((n_particles + 255) / 256));
@@ -2827,14 +2854,23 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
     const int pbx = (e->n + 255) / 256;
     const int npb = pbx * e->n_envs;
     const dim3 grid((unsigned)(nvb + npb));
+    const size_t plds =
+        e->pairs_staged ? swarm::pairs_stage_words(e->n, e->lxb, e->lyb) * sizeof(uint32_t) : 0;
+#define SWARM_VP(ST, LO)                                                                   \
+  hipLaunchKernelGGL((k_vision_pairs<4, 16, ST, LO>), grid, dim3(256), plds, e->stream, e->st, \
+                     e->d_derived, va, npb, e->sc, e->lxb, e->lyb, pbx)
     if (e->pairs_staged) {
-      const size_t plds = swarm::pairs_stage_words(e->n, e->lxb, e->lyb) * sizeof(uint32_t);
-      hipLaunchKernelGGL((k_vision_pairs<4, 16, true>), grid, dim3(256), plds, e->stream, e->st,
-                         e->d_derived, va, npb, e->sc, e->lxb, e->lyb, pbx);
+      if (e->sc.local_uf)
+        SWARM_VP(true, true);
+      else
+        SWARM_VP(true, false);
     } else {
-      hipLaunchKernelGGL((k_vision_pairs<4, 16, false>), grid, dim3(256), 0, e->stream, e->st,
-                         e->d_derived, va, npb, e->sc, e->lxb, e->lyb, pbx);
+      if (e->sc.local_uf)
+        SWARM_VP(false, true);
+      else
+        SWARM_VP(false, false);
     }
+#undef SWARM_VP
     HIP_TRY(hipGetLastError());
     e->ride_stage = 3;
     return SWARM_OK;

@@ -1486,7 +1486,9 @@ __host__ __device__ inline size_t pairs_stage_words(int n, int lx, int ly) {
   return 3 * (size_t)n + ((size_t)1 << (lx + ly)) + 1;
 }
 
-template <bool kStaged = false>
+// kLocal (= sc.local_uf, a compile-time variant so that the plain pair
+// search carries none of the local union-find's code or registers).
+template <bool kStaged = false, bool kLocal = false>
 __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, const DevState& st,
                                                  const Scratch& sc, int lx, int ly, int bx, int e,
                                                  float* nb2, int32_t* uf,
@@ -1566,9 +1568,10 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
   // the six ranges as one flat candidate index f in [0, total), record
   // jj = f + off[r] of the range r holding f: kFly candidates in flight per
   // iteration whatever the split over the ranges (about 11 candidates at
-  // area fraction 0.1: one round of loads, not one per range)
+  // area fraction 0.1: two rounds of loads, not one per range; 16 in
+  // flight measured slower, 4096 colloids)
 #ifndef SWARM_PAIRS_FLY
-#define SWARM_PAIRS_FLY 16
+#define SWARM_PAIRS_FLY 8
 #endif
   constexpr int kFly = SWARM_PAIRS_FLY;
   int off[6], pre[7];
@@ -1604,10 +1607,11 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
       const float ry = per ? (float)(int32_t)(y4[u] - qy) * sx1
                            : pair_disp(y4[u], st.img[M + base + j], qy, iy, sx1, false);
       if (i < j && rx * rx + ry * ry < nb2_row[pk4[u] >> 24]) {
-        // j, and for a partner inside this block's sorted range its block
-        // slot + 1 (a pair the block unions itself)
+        // j, and (kLocal) for a partner inside this block's sorted range its
+        // block slot + 1 (a pair the block unions itself)
         const int ls = jj4[u] - lo;
-        const uint32_t kv = (uint32_t)j | (ls >= 0 && ls < T ? (uint32_t)(ls + 1) << 16 : 0u);
+        const uint32_t kv =
+            (uint32_t)j | (kLocal && ls >= 0 && ls < T ? (uint32_t)(ls + 1) << 16 : 0u);
 #pragma unroll
         for (int v = 0; v < kKeep; ++v) keep[v] = found == v ? kv : keep[v];
         ++found;
@@ -1616,7 +1620,7 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
   }
   const int lane = threadIdx.x & 63;
   const bool dense = __any(found > kKeep);  // a lane kept only kKeep: the wave rescans
-  if (!sc.local_uf) {  // block-uniform: the pair list only (every pair unioned by the build)
+  if constexpr (!kLocal) {  // the pair list only (every pair unioned by the build)
     int v = found;
     v = wave_incl_scan(v);
     int wbase = 0;
@@ -1746,11 +1750,12 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
   }
 }
 
+template <bool kLocal>
 __global__ __launch_bounds__(256) void k_build_pairs(const Derived* __restrict__ d, DevState st,
                                                      Scratch sc, int lx, int ly) {
   __shared__ float nb2[kMaxSpecies * kMaxSpecies];
   __shared__ int32_t uf[2 * 256];
-  build_pairs_body(d, st, sc, lx, ly, blockIdx.x, blockIdx.y, nb2, uf);
+  build_pairs_body<false, kLocal>(d, st, sc, lx, ly, blockIdx.x, blockIdx.y, nb2, uf);
 }
 
 // LDS words of the large-N variant: the union-find forest only.
@@ -1962,16 +1967,16 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
       const bool root = i < N && parent[i] == i;
       const int s = sz[u];
       const int w = sc.one_pass ? max(s, min(min(pc[u], 64), 2 * s)) : s;
-      // the two most frequent classes by one atomic per wave
-      const int r1 = wave_class_add(&classcnt[1], root && s <= 64 && w == 1);
-      const int r2 = wave_class_add(&classcnt[2], root && s <= 64 && w == 2);
+      // one LDS atomic per root (measured, 4096 colloids: the wave-aggregated
+      // counters of the packed build cost this one-workgroup build ~0.9 us,
+      // cluster build 16.7 -> 15.8 us without them)
       if (!root) continue;
       if (s > 64) {  // wider than a wave: a big cluster, run by k_check's workgroup
         atomicAdd(&misc[4], s);
         cbase[i] = kBigMark;
       } else {
         csz[i] = w;
-        cbase[i] = w == 1 ? r1 : (w == 2 ? r2 : atomicAdd(&classcnt[w], 1));
+        cbase[i] = atomicAdd(&classcnt[w], 1);
       }
     }
   }
