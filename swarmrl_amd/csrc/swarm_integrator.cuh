@@ -1758,6 +1758,31 @@ __global__ __launch_bounds__(256) void k_build_pairs(const Derived* __restrict__
   build_pairs_body<false, kLocal>(d, st, sc, lx, ly, blockIdx.x, blockIdx.y, nb2, uf);
 }
 
+// The packing class v whose free-lane range holds singleton rank r < nfree:
+// the largest v >= 2 with freebase[v] <= r (its range is non-empty).
+// freebase[2..65] is non-decreasing and freebase[65] = nfree > r, so v - 1 =
+// #{u in [2, 65]: freebase[u] <= r}: counted in two rounds of eight
+// independent LDS reads (every 8th entry, then the eight from the last of
+// those <= r) -- two LDS latencies where a binary search waits for six.
+__device__ __forceinline__ int free_class(const int32_t* freebase, int r) {
+#ifdef SWARM_BUILD_BSEARCH
+  int lo = 2, hi = 64;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (freebase[mid] <= r) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+#else
+  int k8 = -1;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) k8 += freebase[2 + 8 * q] <= r ? 1 : 0;
+  int v = 1 + 8 * k8;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v += freebase[2 + 8 * k8 + q] <= r ? 1 : 0;
+  return v;
+#endif
+}
+
 // LDS words of the large-N variant: the union-find forest only.
 __host__ __device__ inline size_t build_lds_words_big(int n) {
   const int wmax = slots_per_env(n, true) / 64;  // either packing
@@ -1791,6 +1816,20 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   uint32_t* plist = kBig ? sc.gplist + (size_t)e * sc.pair_cap
                          : reinterpret_cast<uint32_t*>(parent + 4 * N);  // pair_cap
   const int S = sc.S;
+  // kFused (LDS forest): the root walks also count the cluster sizes;
+  // kCount: the union sweep counts each particle's pairs (as the lower index)
+  // in lslot, and the root walks add them to their cluster -- no separate
+  // sweep over the pair list for the one-pass pair counts
+#ifdef SWARM_BUILD_SPLIT_FIND
+  constexpr bool kFused = false;
+#else
+  constexpr bool kFused = !kBig;
+#endif
+#ifdef SWARM_BUILD_PAIR_SWEEP
+  constexpr bool kCount = false;
+#else
+  constexpr bool kCount = kFused && !kLocal;
+#endif
   SWARM_STAMP(6);
   // region lists (sc.pair_region): the blocks' counts, their prefix sums in
   // freebase (free until the packing), the total as `found`
@@ -1827,6 +1866,7 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
       lslot[i] = (int32_t)(l >> 16);  // the member's pair count, until its rank replaces it
     } else {
       parent[i] = i;
+      if (kCount) lslot[i] = 0;
     }
     csz[i] = 0;
     cbase[i] = 0;  // pair count of a cluster (one-pass packing), then its base
@@ -1904,20 +1944,40 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
       }
 #pragma unroll
       for (int u = 0; u < kUU; ++u)
-        if (ok[u]) uf_union(parent, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
+        if (ok[u]) {
+          if (kCount && sc.one_pass) atomicAdd(&lslot[pr[u] & 0xffffu], 1);
+          uf_union(parent, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
+        }
     }
   }
   __syncthreads();
   SWARM_STAMP(7);
-  // every particle points at its root (two walks in lockstep per thread)
+  // every particle points at its root (two walks in lockstep per thread);
+  // in LDS each walk's end counts its member at once (cluster sizes, the
+  // member's rank in lslot): the roots are final after the union sweep, and
+  // a walk that passes a member pointed at its root by another thread still
+  // ends at the same root -- one barrier and one pass over parent[] fewer
   for (int i = tid; i < N; i += 2 * T) {
     const bool two = i + T < N;
     int a = i, b = two ? i + T : i;
+    const int npa = kFused && (kLocal || kCount) ? lslot[i] : 0;
+    const int npb = kFused && (kLocal || kCount) && two ? lslot[i + T] : 0;
     uf_find2(parent, a, b);
     parent[i] = a;
     if (two) parent[i + T] = b;
+    if (kFused) {
+      const int ra = atomicAdd(&csz[a], 1);
+      const int rb = two ? atomicAdd(&csz[b], 1) : 0;
+      lslot[i] = ra;
+      if (two) lslot[i + T] = rb;
+      if ((kLocal || kCount) && sc.one_pass) {
+        if (npa > 0) atomicAdd(&cbase[a], npa);
+        if (npb > 0) atomicAdd(&cbase[b], npb);
+      }
+    }
   }
   __syncthreads();
+  if (!kFused)
   for (int i0 = tid; i0 < N; i0 += kU * T) {
     int32_t r[kU], np_u[kU];
 #pragma unroll
@@ -1933,7 +1993,7 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
         if (np_u[u] > 0) atomicAdd(&cbase[parent[i0 + u * T]], np_u[u]);
     }
   }
-  if (!kLocal && sc.one_pass)
+  if (!kLocal && !kCount && sc.one_pass)
     for (int k0 = tid; k0 < nsweep; k0 += kU * T) {
       uint32_t pr[kU];
       bool ok[kU];
@@ -1982,11 +2042,10 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   }
   __syncthreads();
   SWARM_STAMP(8);
-  // -> global path (3-D: any big cluster; its run is 2-D only)
-  if (tid == 0 && (misc[4] > min(kBigMax, (int)blockDim.x) || (st.dims == 3 && misc[4] > 0)))
-    misc[0] = 1;
-  __syncthreads();
-  if (misc[0]) {
+  // -> global path (3-D: any big cluster; its run is 2-D only).  misc[0]
+  // (list overflow) and misc[4] are final here, so every thread decides
+  // alike, with no barrier for a flag
+  if (misc[0] || misc[4] > min(kBigMax, (int)blockDim.x) || (st.dims == 3 && misc[4] > 0)) {
     if (tid == 0) {
       sc.fallback[e] = 1;
       sc.env_waves[e] = 0;
@@ -2021,74 +2080,61 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
     }
   }
   __syncthreads();
+  // Every particle's slot in one pass: its cluster's base (from the root's
+  // class and class rank, worked out by each member for itself -- no pass
+  // that stores the bases and no barrier before the members read them) plus
+  // its rank in the cluster.
   const int nfree = misc[3];
   for (int i0 = tid; i0 < N; i0 += kU * T) {
-   int32_t sz[kU], rk[kU];
-#pragma unroll
-   for (int u = 0; u < kU; ++u) {
-     const int i = i0 + u * T;
-     const bool root = i < N && parent[i] == i;
-     sz[u] = root ? csz[i] : 0;
-     rk[u] = root ? cbase[i] : 0;
-   }
-#pragma unroll
-   for (int u = 0; u < kU; ++u) {
-    const int i = i0 + u * T;
-    if (i >= N || parent[i] != i) continue;
-    const int s = sz[u];
-    const int r = rk[u];
-    if (r == kBigMark) continue;
-    if (s == 1 && r < nfree) {
-      // the class v whose free-lane range holds r (largest v >= 2 with
-      // freebase[v] <= r; its range is non-empty), then wave j and lane
-      int lo = 2, hi = 64;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (freebase[mid] <= r) lo = mid; else hi = mid - 1;
-      }
-      const int v = lo, per = udiv_small(64, v);
-      const int nw = udiv_small(classcnt[v] + per - 1, per);
-      const int ffull = 64 - per * v;
-      const int t = r - freebase[v];
-      int j, lane;
-      if (t < (nw - 1) * ffull) {
-        j = udiv_small(t, ffull);
-        lane = per * v + (t - j * ffull);
-      } else {
-        j = nw - 1;
-        lane = (classcnt[v] - (nw - 1) * per) * v + (t - (nw - 1) * ffull);
-      }
-      cbase[i] = (wavebase[v] + j) * 64 + lane;
-    } else if (s == 1) {
-      const int r2 = r - nfree;
-      cbase[i] = (wavebase[1] + r2 / 64) * 64 + r2 % 64;
-    } else {
-      const int per = udiv_small(64, s), rq = udiv_small(r, per);
-      cbase[i] = (wavebase[s] + rq) * 64 + (r - rq * per) * s;
-    }
-   }
-  }
-  __syncthreads();
-  for (int i0 = tid; i0 < N; i0 += kU * T) {
-    int32_t cb[kU], ls[kU];
+    int32_t rt[kU], ls[kU], sz[kU], rk[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int i = i0 + u * T;
-      cb[u] = i < N ? cbase[parent[i]] : 0;
+      rt[u] = i < N ? parent[i] : 0;
       ls[u] = i < N ? lslot[i] : 0;
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int i = i0 + u * T;
+      sz[u] = i < N ? csz[rt[u]] : 0;
+      rk[u] = i < N ? cbase[rt[u]] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * T;
       if (i >= N) continue;
-      const int root = parent[i];
+      const int root = rt[u], s = sz[u], r = rk[u];
       int slot;
-      if (cb[u] == kBigMark) {  // big-cluster member m: slot -1 - m
+      if (r == kBigMark) {  // big-cluster member m: slot -1 - m
         const int m = atomicAdd(&misc[5], 1);
         sc.big_list[(size_t)e * kBigMax + m] = i;
         slot = -1 - m;
       } else {
-        slot = cb[u] + ls[u];
+        int cb;
+        if (s == 1 && r < nfree) {
+          // the class v whose free-lane range holds r, then wave j and lane
+          const int v = free_class(freebase, r);
+          const int per = udiv_small(64, v);
+          const int nw = udiv_small(classcnt[v] + per - 1, per);
+          const int ffull = 64 - per * v;
+          const int t = r - freebase[v];
+          int j, lane;
+          if (t < (nw - 1) * ffull) {
+            j = udiv_small(t, ffull);
+            lane = per * v + (t - j * ffull);
+          } else {
+            j = nw - 1;
+            lane = (classcnt[v] - (nw - 1) * per) * v + (t - (nw - 1) * ffull);
+          }
+          cb = (wavebase[v] + j) * 64 + lane;
+        } else if (s == 1) {
+          const int r2 = r - nfree;
+          cb = (wavebase[1] + r2 / 64) * 64 + r2 % 64;
+        } else {
+          const int per = udiv_small(64, s), rq = udiv_small(r, per);
+          cb = (wavebase[s] + rq) * 64 + (r - rq * per) * s;
+        }
+        slot = cb + ls[u];
         sc.perm[(size_t)e * S + slot] = i;
       }
       lslot[i] = slot;
@@ -2323,12 +2369,7 @@ __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, 
     const int r = b & 0xffffff;
     int cb;
     if (s == 1 && r < nfree) {
-      int lo = 2, hi = 64;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (freebase[mid] <= r) lo = mid; else hi = mid - 1;
-      }
-      const int v = lo, per = udiv_small(64, v);
+      const int v = free_class(freebase, r), per = udiv_small(64, v);
       const int nw = udiv_small(classcnt[v] + per - 1, per);
       const int ffull = 64 - per * v;
       const int t = r - freebase[v];
