@@ -1108,6 +1108,19 @@ __device__ __forceinline__ void uf_union(int32_t* parent, int a, int b) {
   }
 }
 
+// The union of a listed pair: its larger index is hooked under the smaller
+// one at once while it is still a root -- one CAS, no walks.  parent[x] <= x
+// holds everywhere (uf_union hooks the larger root, path halving only
+// shortens), so a root may hang under any smaller node without closing a
+// cycle; the component's root stays its smallest index.
+__device__ __forceinline__ void uf_union_pair(int32_t* parent, int a, int b) {
+  const int lo = min(a, b), hi = max(a, b);
+#ifndef SWARM_BUILD_NO_HOOK
+  if (atomicCAS(&parent[hi], hi, lo) == hi) return;
+#endif
+  uf_union(parent, lo, hi);
+}
+
 // A class counter increment aggregated over the wave: one LDS atomic per
 // wave for its lanes with pred set; returns the lane's rank (the counter's
 // old value + the lanes below it).  The packing's singleton and pair classes
@@ -1946,7 +1959,7 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
       for (int u = 0; u < kUU; ++u)
         if (ok[u]) {
           if (kCount && sc.one_pass) atomicAdd(&lslot[pr[u] & 0xffffu], 1);
-          uf_union(parent, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
+          uf_union_pair(parent, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
         }
     }
   }
