@@ -305,11 +305,12 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
     """Duration (ms) of the dominant kernel -- the 2-D run kernel of the
     latency- (k_cluster_run_wide) or throughput-bound (k_cluster_run) cluster
     window -- as it runs in the workload: after the timed region
-    one more episode of the workload is captured with engine recording on,
-    which puts HIP event-record nodes around each window's run node
-    (swarm_engine_profile -> hipEventRecordExternal), and that graph is
-    replayed `replays` times; every replay's run nodes are read back
-    (swarm_engine_profile_graph).  Returns (mean ms, kernel name, note,
+    one more episode of the workload is captured with engine profiling on,
+    so every run node stamps its own earliest workgroup start and latest wave
+    end on the device wall clock (and the other launches of the slice their
+    workgroup roles), and that graph is replayed `replays` times; every
+    replay's stamps are read back (swarm_engine_profile_stamps / _roles).
+    Returns (mean ms, kernel name, note,
     number of run launches timed): the rocprofv3 trace of the same command
     holds those launches as the kernel's last dispatches
     (tools/summarize_profiles.py reads the count from the bench line)."""
@@ -382,8 +383,7 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
         agent.trajectory = saved
     # the run kernel's own launch stamps (earliest block start, latest wave
     # end, device wall clock) time each run node as it ran in the replayed
-    # workload; HIP events only where there are no stamps (eager episodes, or
-    # event-record nodes asked for with SWARMRL_AMD_PROFILE_EVENT_NODES=1)
+    # workload; HIP events only where there are no stamps (eager episodes)
     dev_ok = [x for x in dev_samples if x > 0.0]
     if not dev_ok and not samples:  # no 2-D cluster windows (global path)
         return None, name, "no run-kernel launches recorded", 0, {}

@@ -54,17 +54,12 @@ struct VisionSorted {
 constexpr int kMaxSpecies = SWARM_MAX_SPECIES;
 constexpr double kTwo32 = 4294967296.0;
 constexpr double kTwoPi = 6.283185307179586476925;
-// Verlet-style skin of the cluster decomposition (performance only: results
-// do not depend on it).  2 um keeps inter-cluster approaches below the cutoff
-// over a 100-step slice a ~5-sigma event at the reference's defaults.
 // Verlet skin of the cluster decomposition (um): pairs closer than
-// r_i + r_j + skin at the window start share a cluster.  Results do not
-// depend on it; SWARMRL_AMD_SKIN overrides it for tuning.
-double skin_um() {
-  const char* ov = std::getenv("SWARMRL_AMD_SKIN");
-  const double v = ov ? std::atof(ov) : 0.0;
-  return v > 0.0 ? v : 2.0;
-}
+// r_i + r_j + skin at the window start share a cluster.  Performance only:
+// results do not depend on it.  2 um keeps inter-cluster approaches below
+// the cutoff over a 100-step slice a ~5-sigma event at the reference's
+// defaults.
+double skin_um() { return 2.0; }
 
 thread_local std::string g_err;
 
@@ -602,10 +597,7 @@ __device__ __forceinline__ void vision_body(const DevState& st, const Derived* _
   if (row < 0) return;
   const int total = pre[6];
   // kVF candidates per lane in flight per round
-#ifndef SWARM_VISION_FLY
-#define SWARM_VISION_FLY 4
-#endif
-  constexpr int kVF = SWARM_VISION_FLY;
+  constexpr int kVF = 4;
   // (group-uniform trip count: a drain below always finds whole groups)
   for (int f00 = 0; f00 < total; f00 += kVF * G) {
     const int f0 = f00 + sub;
@@ -676,73 +668,44 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
 // the engine stream guarantees.  The build's workgroups take the first block
 // indices of each launch: the build chain (sort -> pairs -> cluster build)
 // is the longer one, so its workgroups are dealt out first.
-// Block index of a fused launch whose first `nfirst` roles are the build's:
-// dealt out first (default), or last (-DSWARM_BUILD_LAST: the round-3 order,
-// kept for A/B measurement).
+// Block index of a fused launch whose first `nfirst` roles are the build's
+// (dealt out first).
 __device__ __forceinline__ int fused_block(int nfirst) {
-#ifdef SWARM_BUILD_LAST
-  const int rest = (int)gridDim.x - nfirst;
-  return (int)blockIdx.x < rest ? (int)blockIdx.x + nfirst : (int)blockIdx.x - rest;
-#else
   (void)nfirst;
   return (int)blockIdx.x;
-#endif
 }
 
-template <int CH, bool kPairs>
+template <int CH>
 __global__ __launch_bounds__(1024) void k_vgrid_sort(DevState st, VisionArgs va, Scratch sc,
-                                                     int lxb, int lyb,
-                                                     const Derived* __restrict__ d) {
+                                                     int lxb, int lyb) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int b = fused_block(va.n_envs);
   const int role = b < va.n_envs ? swarm::kRoleSort : swarm::kRoleVgrid;
   swarm::role_begin(sc, role);
   if (b < va.n_envs)
-    swarm::build_sort_body<CH, kPairs>(st, sc, lxb, lyb, b, smem, d);
+    swarm::build_sort_body<CH>(st, sc, lxb, lyb, b, smem);
   else
     vision_grid_body(st, va, b - va.n_envs, smem);
   swarm::role_end(sc, role);
 }
 
 // The pair blocks come first: theirs is the longer chain (the cluster build
-// waits on it), so they are dealt out before the cone blocks.  kStaged: the
-// pair blocks stage their env's sorted records in (dynamic) LDS.
-template <int NB, int G, bool kStaged, bool kLocal>
+// waits on it), so they are dealt out before the cone blocks.
+template <int NB, int G, bool kLocal>
 __global__ __launch_bounds__(256) void k_vision_pairs(DevState st, const Derived* __restrict__ d,
                                                       VisionArgs va, int n_pblocks, Scratch sc,
                                                       int lxb, int lyb, int pair_bx) {
   __shared__ uint32_t hits[kVisionHits][256];
   __shared__ float nb2[swarm::kMaxSpecies * swarm::kMaxSpecies];
   __shared__ int32_t uf[2 * 256];
-  extern __shared__ __align__(16) uint32_t pstage[];
   const int b = fused_block(n_pblocks);
   const int role = b < n_pblocks ? swarm::kRolePairs : swarm::kRoleCone;
   swarm::role_begin(sc, role);
   if (b < n_pblocks) {
-    swarm::build_pairs_body<kStaged, kLocal>(d, st, sc, lxb, lyb, b % pair_bx, b / pair_bx, nb2,
-                                             uf, pstage);
+    swarm::build_pairs_body<kLocal>(d, st, sc, lxb, lyb, b % pair_bx, b / pair_bx, nb2, uf);
   } else {
     vision_body<NB, G, false>(st, d, va, b - n_pblocks, 0, hits);
   }
-  swarm::role_end(sc, role);
-}
-
-// sort_pairs engines: the pair list came with the sort (L1), so the cluster
-// build rides in the vision cone's launch -- 1024-thread blocks: the build's
-// workgroup(s) first, then the cone's (their hit lists in the same dynamic
-// LDS), and the policy runs alone after it.
-template <int NB, int G>
-__global__ __launch_bounds__(1024) void k_vision_cbuild(DevState st, const Derived* __restrict__ d,
-                                                        VisionArgs va, Scratch sc) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int b = fused_block(va.n_envs);
-  const int role = b < va.n_envs ? swarm::kRoleCbuild : swarm::kRoleCone;
-  swarm::role_begin(sc, role);
-  if (b < va.n_envs)
-    swarm::cluster_build_env<false, true, false>(st, sc, b, smem, sc.gnpairs[b]);
-  else
-    vision_body<NB, G, false, 1024>(st, d, va, b - va.n_envs, 0,
-                                    reinterpret_cast<uint32_t(*)[1024]>(smem));
   swarm::role_end(sc, role);
 }
 
@@ -966,11 +929,10 @@ __global__ __launch_bounds__(256) void k_field(DevState st, FieldArgs f) {
 // the field's agents, the NEXT observable's vision grid (from the positions
 // the reward sees, which the observable will see too) and build stage 1,
 // so the observable launch only runs the cone (beside stage 2).
-template <int CH, bool kPairs>
+template <int CH>
 __global__ __launch_bounds__(1024) void k_field_vgrid_sort(FieldArgs f, int n_fblocks, DevState st,
                                                            VisionArgs va, Scratch sc, int lxb,
-                                                           int lyb,
-                                                           const Derived* __restrict__ d) {
+                                                           int lyb) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int b = fused_block(2 * va.n_envs);
   const int role = b < va.n_envs       ? swarm::kRoleSort
@@ -978,7 +940,7 @@ __global__ __launch_bounds__(1024) void k_field_vgrid_sort(FieldArgs f, int n_fb
                                        : swarm::kRoleField;
   swarm::role_begin(sc, role);
   if (b < va.n_envs)
-    swarm::build_sort_body<CH, kPairs>(st, sc, lxb, lyb, b, smem, d);
+    swarm::build_sort_body<CH>(st, sc, lxb, lyb, b, smem);
   else if (b < 2 * va.n_envs)
     vision_grid_body(st, va, b - va.n_envs, smem);
   else
@@ -1116,15 +1078,6 @@ struct swarm_engine {
   bool nlist_path = false;
   bool big_build = false;  // k_cluster_build<true>: cluster arrays in global memory
   bool chip_sort = false;  // 2-D envs above 4096 colloids: the three-launch chip-wide sort
-  bool pairs_staged = false;  // the ride-along pair search stages its env in LDS
-  // ride-along build of small periodic 2-D envs: the pair search runs in the
-  // sort's workgroup from its LDS rows (stage 1), and the cluster build rides
-  // in the vision cone's launch (k_vision_cbuild)
-  bool sort_pairs = false;
-  // k_cluster_run_wide's idle waves integrate the rotation ahead
-  // (swarm::precompute_swim; SWARMRL_AMD_ROT_AHEAD=1 turns it on: measured
-  // slower, 4096 colloids 42.2 M vs 41.9 M agent-steps/s, C4 78.0 M vs 67.5 M)
-  bool rot_ahead = false;
   VisionSorted vs{};
   // latency-bound windows read their normals from a table (k_noise)
   bool noise_table = false;
@@ -1140,8 +1093,6 @@ struct swarm_engine {
   // persistent call's arguments; vgrid_ready: the reward launch built the
   // grid of the current positions for them (honoured while the deferred
   // build is at stage 2, i.e. nothing moved the colloids since).
-  // SWARMRL_AMD_SPEC_VGRID=0 turns it off.
-  bool spec_on = true;
   bool spec_ok = false;
   VisionArgs spec_va{};
   bool vgrid_ready = false;
@@ -1156,9 +1107,6 @@ struct swarm_engine {
   int run_wpb = 4;  // run waves per block (= per CU) of k_cluster_run_wide
   // k_build_env: the whole build in one LDS-resident workgroup per env
   bool env_build = false;
-  // XCD-aware env placement of the throughput run kernel and the vision
-  // cone (SWARMRL_AMD_XCD_MAP=0 turns it off)
-  bool xcd_map = true;
   int noise_blocks = 0;
   bool next_table_ready = false;
   // swarm_engine_profile: HIP events around every k_cluster_run launch;
@@ -1178,7 +1126,6 @@ struct swarm_engine {
   // the k-th captured run node (its k_check, then the next window's build and
   // observable launches), swarm::role_begin / role_end
   unsigned long long* d_rstamp = nullptr;
-  bool graph_event_nodes = false;  // SWARMRL_AMD_PROFILE_EVENT_NODES=1
   float* own_f_swim = nullptr;
   float* own_torque_z = nullptr;
   void* allocs[96] = {};
@@ -1264,13 +1211,10 @@ void set_lds_attributes() {
                        reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<true, false>),
                        reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<false, true>),
                        reinterpret_cast<const void*>(&swarm::k_cluster_run_wide<true, true>),
-                       reinterpret_cast<const void*>(&k_vgrid_sort<4, false>),
-                       reinterpret_cast<const void*>(&k_vgrid_sort<16, false>),
-                       reinterpret_cast<const void*>(&k_vgrid_sort<4, true>),
-                       reinterpret_cast<const void*>(&k_field_vgrid_sort<4, false>),
-                       reinterpret_cast<const void*>(&k_field_vgrid_sort<16, false>),
-                       reinterpret_cast<const void*>(&k_field_vgrid_sort<4, true>),
-                       reinterpret_cast<const void*>(&k_vision_cbuild<4, 16>),
+                       reinterpret_cast<const void*>(&k_vgrid_sort<4>),
+                       reinterpret_cast<const void*>(&k_vgrid_sort<16>),
+                       reinterpret_cast<const void*>(&k_field_vgrid_sort<4>),
+                       reinterpret_cast<const void*>(&k_field_vgrid_sort<16>),
                        reinterpret_cast<const void*>(&k_policy_cbuild<4, 4, 4>)};
   for (const void* f : fns)
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
@@ -1369,8 +1313,7 @@ int launch_build(swarm_engine* e, hipStream_t stream) {
   // 2-D: the pair search left block-local union-find roots and a cross list
   // (build_pairs_body); 3-D (k_build_pairs3): the whole pair list is unioned
   const bool local = e->params.n_dims == 2 && e->sc.local_uf;
-  if (e->big_build && swarm::build_lds_words_packed(e->n) * 4 <= kMaxLds &&
-      !(std::getenv("SWARMRL_AMD_PACKED_BUILD") && std::getenv("SWARMRL_AMD_PACKED_BUILD")[0] == '0')) {
+  if (e->big_build && swarm::build_lds_words_packed(e->n) * 4 <= kMaxLds) {
     if (local)
       hipLaunchKernelGGL(swarm::k_cluster_build_packed<true>, dim3(e->n_envs), dim3(1024),
                          swarm::build_lds_words_packed(e->n) * 4, stream, e->st, e->sc);
@@ -1443,13 +1386,11 @@ int launch_run(swarm_engine* e, int n_steps, unsigned long long* tstamp = nullpt
     // dynamic LDS beyond half a CU's keeps one block (run_wpb run waves) per CU
     const int R = e->run_wpb;
     const dim3 grid((unsigned)(e->noise_blocks + (waves + R - 1) / R));
-    // at least 96 KB (one block per CU), and the precomputed rotation of
-    // one or two run waves (swarm::precompute_swim)
-    const size_t lds = std::max<size_t>(96 * 1024, R <= 2 ? swarm::wide_dir_lds_bytes(R) : 0);
+    const size_t lds = 96 * 1024;  // one block per CU
 #define SWARM_WIDE(MULTI, WALLS)                                                             \
   hipLaunchKernelGGL((swarm::k_cluster_run_wide<MULTI, WALLS>), grid, dim3(1024), lds, e->stream, \
                      e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise,      \
-                     e->noise_blocks, R, e->rot_ahead ? 1 : 0, tstamp)
+                     e->noise_blocks, R, tstamp)
     if (walls) {
       if (multi)
         SWARM_WIDE(true, true);
@@ -1468,7 +1409,7 @@ int launch_run(swarm_engine* e, int n_steps, unsigned long long* tstamp = nullpt
     // eight XCDs evenly (or nearly: 64 and more)
     const int E = e->n_envs;
     const int bpe = (e->sc.wmax + 3) / 4;
-    const bool xcd = e->xcd_map && E >= 8 && (E % 8 == 0 || E >= 64);
+    const bool xcd = E >= 8 && (E % 8 == 0 || E >= 64);
     const dim3 run_grid((unsigned)(xcd ? 8 * ((E + 7) / 8) * bpe : (waves + 3) / 4)),
         run_block(256);
 #define SWARM_RUN(MULTI, TABLE, WALLS)                                                     \
@@ -1519,27 +1460,6 @@ int launch_check(swarm_engine* e, int n_steps) {
                      e->d_derived, e->st, e->sc, n_steps, e->d_step, e->d_arrive, e->lxg, e->lyg,
                      0, check_cell_lx(e), check_cell_ly(e));
   HIP_TRY(hipGetLastError());
-  return SWARM_OK;
-}
-
-// Record `ev` on `s`; under capture as an event-record node appended to the
-// captured graph (this HIP refuses hipEventRecordWithFlags(.., External)
-// while capturing, so the node is added by hand and made the stream's
-// capture dependency).
-int record_event(hipStream_t s, hipEvent_t ev, bool in_graph) {
-  if (!in_graph) {
-    HIP_TRY(hipEventRecord(ev, s));
-    return SWARM_OK;
-  }
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  unsigned long long id = 0;
-  hipGraph_t g = nullptr;
-  const hipGraphNode_t* deps = nullptr;
-  size_t nd = 0;
-  HIP_TRY(hipStreamGetCaptureInfo_v2(s, &cs, &id, &g, &deps, &nd));
-  hipGraphNode_t node = nullptr;
-  HIP_TRY(hipGraphAddEventRecordNode(&node, g, deps, nd, ev));
-  HIP_TRY(hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies));
   return SWARM_OK;
 }
 
@@ -1647,19 +1567,17 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
   bool in_graph = false, events = false;
   if (e->profile) {
     // eager: HIP events around the run launch; under stream capture the run
-    // node stamps itself (launch stamps below), and event-record nodes around
-    // it only with SWARMRL_AMD_PROFILE_EVENT_NODES=1 (they put ~15 us gaps
-    // into the replayed graph)
+    // node stamps itself (launch stamps below: event-record nodes put ~15 us
+    // gaps into the replayed graph)
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     HIP_TRY(hipStreamIsCapturing(e->stream, &cs));
     in_graph = cs == hipStreamCaptureStatusActive;
-    events = !in_graph || e->graph_event_nodes;
+    events = !in_graph;
   }
   if (events) {
     HIP_TRY(hipEventCreate(&ev0));
     HIP_TRY(hipEventCreate(&ev1));
-    const int rc0 = record_event(e->stream, ev0, in_graph);
-    if (rc0) return rc0;
+    HIP_TRY(hipEventRecord(ev0, e->stream));
   }
   unsigned long long* tstamp = nullptr;
   if (e->profile && in_graph && e->d_tstamp && e->stamp_next < kMaxStamps)
@@ -1673,18 +1591,8 @@ int launch_window(swarm_engine* e, int n_steps, bool use_prebuilt, int noise_rea
   int rc = launch_run(e, n_steps, tstamp);
   if (rc) return rc;
   if (events) {
-    rc = record_event(e->stream, ev1, in_graph);
-    if (rc) return rc;
-    (in_graph ? e->graph_events : e->prof_events).emplace_back(ev0, ev1);
-    if (in_graph) {
-      hipEvent_t c0 = nullptr, c1 = nullptr;
-      HIP_TRY(hipEventCreate(&c0));
-      HIP_TRY(hipEventCreate(&c1));
-      rc = record_event(e->stream, c0, true);
-      if (!rc) rc = record_event(e->stream, c1, true);
-      if (rc) return rc;
-      e->graph_cal.emplace_back(c0, c1);
-    }
+    HIP_TRY(hipEventRecord(ev1, e->stream));
+    e->prof_events.emplace_back(ev0, ev1);
   }
   return launch_check(e, n_steps);
 }
@@ -1865,23 +1773,11 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   // union saves, measured)
   e->sc.local_uf = n_particles > 4096 ? 1 : 0;
   if (const char* olu = std::getenv("SWARMRL_AMD_LOCAL_UF")) e->sc.local_uf = olu[0] != '0';
-  if (const char* ora = std::getenv("SWARMRL_AMD_ROT_AHEAD")) e->rot_ahead = ora[0] != '0';
-  // 2-D LDS builds without the local union-find: with
-  // SWARMRL_AMD_PAIR_REGIONS=1 the pair-search blocks write their own regions
-  // of the list (no returning global atomic on the search's chain).  Off by
-  // default: the build's gather of the regions costs more than the atomic
-  // (4096 colloids: cluster build 15.2 vs 15.8 us, 44.8 vs 44.1 M)
-  e->sc.pair_region = 0;
-  if (params->n_dims == 2 && !e->big_build && !e->sc.local_uf && n_particles <= 4096 &&
-      std::getenv("SWARMRL_AMD_PAIR_REGIONS") && std::getenv("SWARMRL_AMD_PAIR_REGIONS")[0] == '1')
-    e->sc.pair_region = e->sc.pair_cap / ((n_particles + 255) / 256);
   e->sc.rstamp = nullptr;
-  e->graph_event_nodes = std::getenv("SWARMRL_AMD_PROFILE_EVENT_NODES") &&
-                         std::getenv("SWARMRL_AMD_PROFILE_EVENT_NODES")[0] == '1';
   e->sc.multi_species = params->n_species > 1 ? 1 : 0;
   // the 2-D build sort stages its scatter in LDS: the sorted rows of up to
   // K entries per pass beside the cell counts (K a multiple of 4, at least
-  // N / 4; SWARMRL_AMD_SORT_STAGED=0 turns it off)
+  // N / 4)
   {
     const size_t counts = (16 + ((size_t)1 << (e->lxb + e->lyb)) + 1) * 4;
     const size_t room = counts + 4096 < kMaxLds ? kMaxLds - counts - 4096 : 0;
@@ -1890,19 +1786,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
                                  4 * k >= (size_t)n_particles
                              ? (int32_t)k
                              : 0;
-    if (const char* oss = std::getenv("SWARMRL_AMD_SORT_STAGED"))
-      if (oss[0] == '0') e->sc.sort_stage_k = 0;
   }
-  // the pair search in the sort's workgroup (SWARMRL_AMD_SORT_PAIRS=1: on):
-  // periodic 2-D envs whose sort stages all its rows in one LDS pass.  Off
-  // by default: measured (role stamps, 4096 colloids) its one workgroup
-  // takes 31 us for the pairs the 16-block search finds in 12 us, so moving
-  // the cluster build beside the cone does not pay (35.1 M vs 43.2 M)
-  e->sort_pairs = params->n_dims == 2 && params->periodic && n_particles <= 4096 &&
-                  e->sc.sort_stage_k >= n_particles && !e->sc.local_uf && !e->big_build &&
-                  std::getenv("SWARMRL_AMD_SORT_PAIRS") &&
-                  std::getenv("SWARMRL_AMD_SORT_PAIRS")[0] == '1';
-  if (e->sort_pairs) e->sc.pair_region = 0;  // its list is contiguous (gnpairs)
   e->cluster_path = e->sc.pair_cap >= n_particles &&
                     n_particles < 65536 &&
                     swarm::build_lds_words_big(n_particles) * 4 <= kMaxLds &&
@@ -1956,24 +1840,12 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   // One pair pass per wave and sub-step (k_cluster_build): the run kernel
   // lasts as long as its slowest waves, at any env count.  Latency-bound
   // launches (few envs x particles fill few SIMDs) also read their normals
-  // from a table (k_noise).  Overrides: SWARMRL_AMD_ONE_PASS /
-  // SWARMRL_AMD_NOISE_TABLE=0|1.
+  // from a table (k_noise; SWARMRL_AMD_NOISE_TABLE=0|1 overrides).
   const bool latency_bound = (long)n_envs * n_particles <= 32768;
-  {
-    const char* ov = std::getenv("SWARMRL_AMD_ONE_PASS");
-    bool want = true;
-    if (ov && ov[0] == '0') want = false;
-    if (ov && ov[0] == '1') want = true;
-    e->sc.one_pass = want ? 1 : 0;
-  }
+  e->sc.one_pass = 1;
   // fewer, fuller waves only pay when the waves compete for the SIMDs; a
   // latency-bound launch has SIMDs to spare and a shorter build is worth more
   e->sc.fill_singletons = latency_bound ? 0 : 1;
-  {
-    const char* ov = std::getenv("SWARMRL_AMD_FILL_SINGLETONS");
-    if (ov && ov[0] == '0') e->sc.fill_singletons = 0;
-    if (ov && ov[0] == '1') e->sc.fill_singletons = 1;
-  }
   const int S = swarm::slots_per_env(n_particles, e->sc.one_pass != 0);
   e->sc.S = S;
   e->sc.wmax = S / 64;
@@ -2014,32 +1886,13 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->sc.gnx, (size_t)n_envs);
   // chip-wide build sort of large 2-D envs (k_sort_count/scan/scatter):
   // per-cell counters (zero between builds) and each particle's cell / rank
-  e->chip_sort = params->n_dims == 2 && n_particles > 4096 &&
-                 !(std::getenv("SWARMRL_AMD_CHIP_SORT") && std::getenv("SWARMRL_AMD_CHIP_SORT")[0] == '0');
+  e->chip_sort = params->n_dims == 2 && n_particles > 4096;
   if (e->chip_sort) {
     rc = rc ? rc : dev_alloc(e, &e->sc.gcnt, (size_t)n_envs << (e->lxb + e->lyb));
     rc = rc ? rc : dev_alloc(e, &e->sc.gcell, M);
     rc = rc ? rc : dev_alloc(e, &e->sc.grank, M);
   }
-  // the ride-along pair search (k_vision_pairs) stages its env's sorted
-  // records in LDS when few envs leave it latency-bound and they fit
-  // (SWARMRL_AMD_PAIRS_STAGED=0|1 overrides)
-  {
-    const size_t pb = swarm::pairs_stage_words(n_particles, e->lxb, e->lyb) * sizeof(uint32_t);
-    const char* ov = std::getenv("SWARMRL_AMD_PAIRS_STAGED");
-    // off by default: the staged records' LDS keeps the cone's blocks from
-    // sharing a CU with a pair block (4096 colloids: 42.0 M vs 44.0 M)
-    bool want = false;
-    if (ov && ov[0] == '0') want = false;
-    if (ov && ov[0] == '1') want = true;
-    e->pairs_staged = want && params->n_dims == 2 && pb <= 96 * 1024;
-    if (e->pairs_staged)
-      for (const void* f : {reinterpret_cast<const void*>(&k_vision_pairs<4, 16, true, false>),
-                            reinterpret_cast<const void*>(&k_vision_pairs<4, 16, true, true>)})
-        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pb);
-  }
   rc = rc ? rc : dev_alloc(e, &e->sc.gnpairs, (size_t)n_envs);
-  rc = rc ? rc : dev_alloc(e, &e->sc.gbcnt, (size_t)n_envs * ((n_particles + 255) / 256));
   if (e->big_build) rc = rc ? rc : dev_alloc(e, &e->sc.gclus, 3 * M);
   rc = rc ? rc : dev_alloc(e, &e->sc.wave_npairs, (size_t)n_envs * (S / 64));
   rc = rc ? rc : dev_alloc(e, &e->sc.phase, 32 + 4 * (size_t)n_envs * (S / 64));
@@ -2053,8 +1906,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   rc = rc ? rc : dev_alloc(e, &e->vs.rec, 2 * M);
   rc = rc ? rc : dev_alloc(e, &e->vs.agent_row, (size_t)n_particles);
   // noise table for latency-bound windows: few envs fill few SIMDs, so the
-  // normals are better produced chip-wide ahead of the run.  Override with
-  // SWARMRL_AMD_NOISE_TABLE=0|1.
+  // normals are better produced chip-wide ahead of the run.
   {
     const char* ov = std::getenv("SWARMRL_AMD_NOISE_TABLE");
     bool want = latency_bound;
@@ -2074,7 +1926,6 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
       e->env_build = e->cluster_path && !e->big_build && !latency_bound && !three_d &&
                      !e->nlist_path && params->periodic &&
                      swarm::build_env_sort_words(n_particles, 1 << (e->lxb + e->lyb)) <= below;
-      if (const char* ox = std::getenv("SWARMRL_AMD_XCD_MAP")) e->xcd_map = ox[0] != '0';
       const char* ob = std::getenv("SWARMRL_AMD_ENV_BUILD");
       if (ob && ob[0] == '0') e->env_build = false;
       if (ob && ob[0] == '1')
@@ -2088,17 +1939,12 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     e->noise_blocks = e->wide_run && M <= 8192 ? 64 : 0;
     const char* ow = std::getenv("SWARMRL_AMD_WIDE_RUN");
     if (ow && ow[0] == '0') e->wide_run = false, e->noise_blocks = 0;
-    if (const char* osv = std::getenv("SWARMRL_AMD_SPEC_VGRID")) e->spec_on = osv[0] != '0';
-    const char* on = std::getenv("SWARMRL_AMD_WIDE_NOISE");
-    if (on && on[0] == '0') e->noise_blocks = 0;
     // run waves per CU: a wave alone on its CU does not share the CU's
     // texture path with other waves' scattered noise-table gathers; four per
     // CU once the run's waves (~1 per 46 particles) would not fit one per CU
     {
       const long est = (long)M / 46 + 1;
       e->run_wpb = est + e->noise_blocks <= 224 ? 1 : (est / 2 + e->noise_blocks <= 224 ? 2 : 4);
-      const char* orw = std::getenv("SWARMRL_AMD_RUN_WAVES_PER_CU");
-      if (orw && (orw[0] == '1' || orw[0] == '2' || orw[0] == '4')) e->run_wpb = orw[0] - '0';
     }
 
   }
@@ -2783,9 +2629,7 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
   int rc = ensure_grid_scratch(e, lx, ly);
   if (rc) return rc;
   // records staged in LDS when the env's fit (N <= 8 x 1024: the register path)
-  const bool staged = e->n <= 8 * 1024 && vision_grid_lds_bytes(lx, ly, e->n, true) <= kMaxLds &&
-                      !(std::getenv("SWARMRL_AMD_VGRID_STAGED") &&
-                        std::getenv("SWARMRL_AMD_VGRID_STAGED")[0] == '0');
+  const bool staged = e->n <= 8 * 1024 && vision_grid_lds_bytes(lx, ly, e->n, true) <= kMaxLds;
   const VisionArgs va{*vp,          lx,        ly,    radii, types, agent_idx, n_agents,
                       e->d_start,   e->vs,     out,   e->n_envs, staged ? 1 : 0};
   const long total = (long)e->n * e->n_envs;  // one group per sorted particle
@@ -2793,20 +2637,17 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
   // lanes per agent: enough threads to give every SIMD a few waves, few
   // enough that the lanes of a wave stay busy (measured, tools/vision_time.py:
   // 64 x 4096 agents 107 -> 93 us with G = 4 instead of 1)
-#ifndef SWARM_VISION_G_WIDE
-#define SWARM_VISION_G_WIDE 4
-#endif
-  int G = total >= (1L << 15) ? SWARM_VISION_G_WIDE : 16;
+  constexpr int kVisionGWide = 4;
+  int G = total >= (1L << 15) ? kVisionGWide : 16;
   if (const char* og = std::getenv("SWARMRL_AMD_VISION_G")) {
     const int v = std::atoi(og);
-    if (v == SWARM_VISION_G_WIDE || v == 16) G = v;
+    if (v == kVisionGWide || v == 16) G = v;
   }
   const size_t glds = vision_grid_lds_bytes(lx, ly, e->n, staged);
   if (glds > kMaxLds) return fail(SWARM_ECAPACITY, "observable cell grid too large");
   // the grid of the current positions for these arguments, built by the
   // reward launch (launch_field) while nothing moved the colloids since
-  const bool have_grid = !all && e->vgrid_ready &&
-                         (e->ride_stage == 2 || (e->ride_stage == 3 && e->sort_pairs)) &&
+  const bool have_grid = !all && e->vgrid_ready && e->ride_stage == 2 &&
                          same_grid_args(e->spec_va, va);
   e->vgrid_ready = false;
   e->spec_ok = persistent && !all;
@@ -2814,63 +2655,36 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
   // a deferred build rides along in the grid and cone launches (stages 1, 2)
   // when their fused variants apply; else its pending stages launch first
   const bool ride_ok = !all && nb <= 4 && G == 16;
-  const bool ride3 = ride_ok && e->sort_pairs && e->ride_stage == 3;  // cluster build | cone
-  if (e->ride_stage > 0 && !(ride_ok && e->ride_stage <= 2) && !ride3) {
+  if (e->ride_stage > 0 && !(ride_ok && e->ride_stage <= 2)) {
     rc = flush_ride_along(e);
     if (rc) return rc;
   }
-  if (e->ride_stage == 1) {  // grid | sort (+ pairs), then cone | pairs (| cluster build)
+  if (e->ride_stage == 1) {  // grid | sort, then cone | pairs
     const size_t slds = sort_lds_bytes(e);
     const dim3 grid((unsigned)(2 * e->n_envs));
-    if (e->sort_pairs)
-      hipLaunchKernelGGL((k_vgrid_sort<4, true>), grid, dim3(1024), std::max(glds, slds),
-                         e->stream, e->st, va, e->sc, e->lxb, e->lyb, e->d_derived);
-    else if (e->n > 4096)
-      hipLaunchKernelGGL((k_vgrid_sort<16, false>), grid, dim3(1024), std::max(glds, slds),
-                         e->stream, e->st, va, e->sc, e->lxb, e->lyb, e->d_derived);
+    if (e->n > 4096)
+      hipLaunchKernelGGL((k_vgrid_sort<16>), grid, dim3(1024), std::max(glds, slds), e->stream,
+                         e->st, va, e->sc, e->lxb, e->lyb);
     else
-      hipLaunchKernelGGL((k_vgrid_sort<4, false>), grid, dim3(1024), std::max(glds, slds),
-                         e->stream, e->st, va, e->sc, e->lxb, e->lyb, e->d_derived);
+      hipLaunchKernelGGL((k_vgrid_sort<4>), grid, dim3(1024), std::max(glds, slds), e->stream,
+                         e->st, va, e->sc, e->lxb, e->lyb);
     HIP_TRY(hipGetLastError());
-    e->ride_stage = e->sort_pairs ? 3 : 2;
+    e->ride_stage = 2;
   } else if (!have_grid) {
     hipLaunchKernelGGL(k_vision_grid, dim3(e->n_envs), dim3(1024), glds, e->stream, e->st, va);
     HIP_TRY(hipGetLastError());
-  }
-  if (ride_ok && e->sort_pairs && e->ride_stage == 3) {
-    // cluster build | cone (1024-thread blocks; the policy runs alone)
-    const int ncb = (int)((total * 16 + 1023) / 1024);
-    const size_t lds = std::max(build_lds_bytes(e->n, e->sc.pair_cap),
-                                (size_t)kVisionHits * 1024 * sizeof(uint32_t));
-    hipLaunchKernelGGL((k_vision_cbuild<4, 16>), dim3((unsigned)(e->n_envs + ncb)), dim3(1024),
-                       lds, e->stream, e->st, e->d_derived, va, e->sc);
-    HIP_TRY(hipGetLastError());
-    e->ride_stage = 0;
-    e->prebuilt = true;
-    return SWARM_OK;
   }
   if (e->ride_stage == 2) {  // pairs | cone
     const int nvb = (int)((total * 16 + 255) / 256);
     const int pbx = (e->n + 255) / 256;
     const int npb = pbx * e->n_envs;
     const dim3 grid((unsigned)(nvb + npb));
-    const size_t plds =
-        e->pairs_staged ? swarm::pairs_stage_words(e->n, e->lxb, e->lyb) * sizeof(uint32_t) : 0;
-#define SWARM_VP(ST, LO)                                                                   \
-  hipLaunchKernelGGL((k_vision_pairs<4, 16, ST, LO>), grid, dim3(256), plds, e->stream, e->st, \
-                     e->d_derived, va, npb, e->sc, e->lxb, e->lyb, pbx)
-    if (e->pairs_staged) {
-      if (e->sc.local_uf)
-        SWARM_VP(true, true);
-      else
-        SWARM_VP(true, false);
-    } else {
-      if (e->sc.local_uf)
-        SWARM_VP(false, true);
-      else
-        SWARM_VP(false, false);
-    }
-#undef SWARM_VP
+    if (e->sc.local_uf)
+      hipLaunchKernelGGL((k_vision_pairs<4, 16, true>), grid, dim3(256), 0, e->stream, e->st,
+                         e->d_derived, va, npb, e->sc, e->lxb, e->lyb, pbx);
+    else
+      hipLaunchKernelGGL((k_vision_pairs<4, 16, false>), grid, dim3(256), 0, e->stream, e->st,
+                         e->d_derived, va, npb, e->sc, e->lxb, e->lyb, pbx);
     HIP_TRY(hipGetLastError());
     e->ride_stage = 3;
     return SWARM_OK;
@@ -2896,15 +2710,15 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
   // XCD-aware env placement once the envs fill the eight XCDs (as k_cluster_run)
   const int E = e->n_envs;
   const int bpe = (int)(((long)e->n * G + 255) / 256);
-  const bool xcd = e->xcd_map && E >= 8 && (E % 8 == 0 || E >= 64);
+  const bool xcd = E >= 8 && (E % 8 == 0 || E >= 64);
   const dim3 grid((unsigned)(xcd ? 8L * ((E + 7) / 8) * bpe : (total * G + 255) / 256)),
       block(256);
 #define SWARM_VISION(NBV, GV)                                                                  \
   hipLaunchKernelGGL((k_vision<NBV, GV>), grid, block, 0, e->stream, e->st, e->d_derived, va, \
                      xcd ? bpe : 0)
 #define SWARM_VISION_G(NBV)                      \
-  if (G == SWARM_VISION_G_WIDE)                  \
-    SWARM_VISION(NBV, SWARM_VISION_G_WIDE);      \
+  if (G == kVisionGWide)                  \
+    SWARM_VISION(NBV, kVisionGWide);      \
   else                                           \
     SWARM_VISION(NBV, 16)
   if (nb <= 4) {
@@ -2940,24 +2754,20 @@ namespace {
 // along in the reward launch).
 int launch_field(swarm_engine* e, const FieldArgs& f) {
   const int total = f.n_agents * e->n_envs;
-  if (e->spec_on && e->spec_ok && e->ride_stage == 1) {
+  if (e->spec_ok && e->ride_stage == 1) {
     const VisionArgs& va = e->spec_va;
     const size_t glds = vision_grid_lds_bytes(va.lx, va.ly, e->n, va.staged != 0);
     const size_t slds = sort_lds_bytes(e);
     const int nfb = (total + 1023) / 1024;
     const dim3 grid((unsigned)(nfb + 2 * e->n_envs));
-    if (e->sort_pairs)
-      hipLaunchKernelGGL((k_field_vgrid_sort<4, true>), grid, dim3(1024), std::max(glds, slds),
-                         e->stream, f, nfb, e->st, va, e->sc, e->lxb, e->lyb, e->d_derived);
-    else if (e->n > 4096)
-      hipLaunchKernelGGL((k_field_vgrid_sort<16, false>), grid, dim3(1024),
-                         std::max(glds, slds), e->stream, f, nfb, e->st, va, e->sc, e->lxb,
-                         e->lyb, e->d_derived);
+    if (e->n > 4096)
+      hipLaunchKernelGGL((k_field_vgrid_sort<16>), grid, dim3(1024), std::max(glds, slds),
+                         e->stream, f, nfb, e->st, va, e->sc, e->lxb, e->lyb);
     else
-      hipLaunchKernelGGL((k_field_vgrid_sort<4, false>), grid, dim3(1024), std::max(glds, slds),
-                         e->stream, f, nfb, e->st, va, e->sc, e->lxb, e->lyb, e->d_derived);
+      hipLaunchKernelGGL((k_field_vgrid_sort<4>), grid, dim3(1024), std::max(glds, slds),
+                         e->stream, f, nfb, e->st, va, e->sc, e->lxb, e->lyb);
     HIP_TRY(hipGetLastError());
-    e->ride_stage = e->sort_pairs ? 3 : 2;
+    e->ride_stage = 2;
     e->vgrid_ready = true;
     return SWARM_OK;
   }
@@ -3245,9 +3055,7 @@ int swarm_engine_defer_build(swarm_engine_t* e, int32_t* deferred) {
   // the three-launch 2-D cluster build of a latency-bound engine only (the
   // stages the fused observable / policy launches know how to carry)
   const bool ok = e->cluster_path && !e->nlist_path && !e->env_build && !e->big_build &&
-                  e->params.n_dims == 2 && e->wide_run &&
-                  !(std::getenv("SWARMRL_AMD_RIDE_ALONG") &&
-                    std::getenv("SWARMRL_AMD_RIDE_ALONG")[0] == '0');
+                  e->params.n_dims == 2 && e->wide_run;
   if (!ok) return SWARM_OK;
   e->prebuilt = false;
   e->ride_stage = 1;
@@ -3302,15 +3110,14 @@ int swarm_ppo_profile(int32_t enable, double* grads_ms, int32_t* launches) {
 }
 
 namespace {
-// Workgroups of `fn` resident on the whole device at once (at least one).
+// Workgroups of `fn` resident at once on a whole MI355X (256 CUs).  The grid
+// size sets the fixed cross-block summation order of the gradient, so it is
+// a function of the kernel and n only -- never of the device it runs on or
+// its partition mode: replicas on any GPUs sum in the same order and stay
+// bit-identical.
+constexpr int kPpoOrderCUs = 256;
 int ppo_resident_blocks(const void* fn, int threads, size_t lds) {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 1;
-  }
+  const int cus = kPpoOrderCUs;
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds) != hipSuccess ||
       per_cu < 1)

@@ -40,9 +40,9 @@
 namespace swarm {
 
 constexpr int kMaxSpecies = SWARM_MAX_SPECIES;
-#ifndef SWARM_RUN_MINB
-#define SWARM_RUN_MINB 5  // k_cluster_run: 5 blocks (waves) per CU (SIMD): <= 96 VGPRs
-#endif
+// k_cluster_run: 5 blocks (waves) per CU (SIMD), so <= 96 VGPRs (the 24 B/lane
+// spill this costs measured cheaper than 4 waves per SIMD)
+constexpr int kRunMinBlocks = 5;
 constexpr int kMaxWindow = 128;   // sub-steps per cluster window
 constexpr int kPairsPerWave = 256;  // neighbour pairs of one 64-lane wave (4 passes)
 // Clusters wider than a wave ("big" clusters) run in k_check's workgroup, one
@@ -221,11 +221,6 @@ struct Scratch {
   uint32_t* xpairs;   // [E][pair_cap] cross-block pairs i | j << 16
   int32_t* gnx;       // [E] cross-block pairs found
   int32_t local_uf;   // 1: the 2-D pair search unions its blocks' pairs (lroot, xpairs)
-  // > 0 (2-D, no local union-find, LDS cluster build): pair-search block b of
-  // env e writes its pairs to gplist[e][b * pair_region ...] and their count
-  // to gbcnt[e][b] -- no returning global atomic; the build gathers them
-  int32_t pair_region;
-  int32_t* gbcnt;     // [E][ceil(N / 256)] pairs found per pair-search block
   int32_t* gclus;     // [3][M] cluster sizes / bases / slots (large-N build only)
   int32_t pair_cap;   // pairs per env
   int32_t one_pass;   // 1: pack clusters so that a wave has <= 64 pairs
@@ -664,46 +659,6 @@ __device__ __forceinline__ void bd_translate(const PConst& c, PState& p, int64_t
   }
 }
 
-// bd_translate with the swim force vector given (swx, swy = fs * cos,
-// fs * sin of the orientation, precompute_swim): the same operation
-// sequence, so the same bits.
-__device__ __forceinline__ void bd_translate_sw(const PConst& c, PState& p, int64_t ax, int64_t ay,
-                                                float swx, float swy, float tz, float fex,
-                                                float fey, uint32_t k0, uint32_t k1, uint32_t id,
-                                                uint64_t step, bool last, float* vx, float* vy,
-                                                float* w, const float* g) {
-  float fx, fy;
-  i64x2_to_f32(ax, ay, &fx, &fy);
-  fx = fx * 5.9604644775390625e-08f;
-  fy = fy * 5.9604644775390625e-08f;
-  fx = fx + fex;
-  fy = fy + fey;
-  fx = fx + swx;
-  fy = fy + swy;
-  float dx = fx * c.mob_dt;
-  float dy = fy * c.mob_dt;
-  if (c.noisy) {
-    dx = dx + c.sig_t * g[0];
-    dy = dy + c.sig_t * g[1];
-  }
-  advance(p.qx, p.ix, f2i32(dx * c.inv_sx0));
-  advance(p.qy, p.iy, f2i32(dy * c.inv_sx1));
-  if (last) {
-    float v0 = fx * c.inv_gt, v1 = fy * c.inv_gt;
-    float om = tz * c.inv_gr;
-    if (c.noisy) {
-      float gv[3];
-      normals3(k0, k1, id, step, 1u, gv);
-      v0 = v0 + c.sig_v * gv[0];
-      v1 = v1 + c.sig_v * gv[1];
-      om = om + c.sig_w * gv[2];
-    }
-    *vx = v0;
-    *vy = v1;
-    *w = om;
-  }
-}
-
 // One steepest-descent step of one particle (espresso.py:1163-1168).
 __device__ __forceinline__ bool sd_step(const PConst& c, PState& p, int64_t ax, int64_t ay,
                                         float fs, float tz, float fex, float fey, float g,
@@ -1115,9 +1070,7 @@ __device__ __forceinline__ void uf_union(int32_t* parent, int a, int b) {
 // cycle; the component's root stays its smallest index.
 __device__ __forceinline__ void uf_union_pair(int32_t* parent, int a, int b) {
   const int lo = min(a, b), hi = max(a, b);
-#ifndef SWARM_BUILD_NO_HOOK
   if (atomicCAS(&parent[hi], hi, lo) == hi) return;
-#endif
   uf_union(parent, lo, hi);
 }
 
@@ -1149,137 +1102,11 @@ __host__ __device__ inline size_t build_lds_words(int n, int pair_cap) {
 // >= rc_max + skin (global arrays for the chip-wide pair search).
 // The body runs in the workgroup of env e (k_build_sort, or a workgroup of a
 // fused launch that carries the build along: k_vgrid_sort).
-// The pair search of build_sort_body<CH, true>, from the sort's own LDS:
-// the sorted records (rx, ry, rid: N entries, one pass), the cell ends
-// (cend[c] = end of cell c after the claims) -- no memory latency between
-// the sort and the pair list, whose pairs (i < j, within r_i + r_j + skin,
-// as build_pairs_body) go to gplist[e] with their count in gnpairs[e].
-// Each thread takes its CH entries; an entry's six stencil ranges are one
-// flat candidate index (as build_pairs_body: lanes with different range
-// splits stay in step), up to kKeep pairs per entry in registers, one block
-// scan for the offsets, and an entry with more pairs rescans to write them.
-// Periodic 2-D boxes.
-template <int CH>
-__device__ __forceinline__ void sort_pairs_lds(const Derived* __restrict__ d, const Scratch& sc,
-                                               int lx, int ly, int e, int N,
-                                               const int32_t* cend, const uint32_t* rx,
-                                               const uint32_t* ry, const int32_t* rid,
-                                               int32_t* wave_sums) {
-  constexpr int kKeep = 4;
-  __shared__ float nb2[kMaxSpecies * kMaxSpecies];
-  const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int k = tid; k < kMaxSpecies * kMaxSpecies; k += T) nb2[k] = d->nb2[k];
-  __syncthreads();
-  const int ncx = 1 << lx, ncy = 1 << ly;
-  const float sx0 = d->sx[0], sx1 = d->sx[1];
-  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
-  uint32_t keep[CH][kKeep];
-  int found[CH], off6[CH][6], pre6[CH][7];
-  int mine = 0;
-#pragma unroll
-  for (int k = 0; k < CH; ++k) {
-    const int ps = tid + k * T;
-    found[k] = 0;
-#pragma unroll
-    for (int u = 0; u < kKeep; ++u) keep[k][u] = 0u;
-    pre6[k][0] = 0;
-    if (ps >= N) {
-#pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        off6[k][r] = 0;
-        pre6[k][r + 1] = 0;
-      }
-      continue;
-    }
-    const int pk = rid[ps], i = pk & 0xffffff;
-    const uint32_t qx = rx[ps], qy = ry[ps];
-    const int c0 = cell_index(qx, qy, lx, ly);
-    const int cx = c0 & (ncx - 1), cy = c0 >> lx;
-    const int xa = ncx >= 3 ? max(cx - 1, 0) : 0;
-    const int xb = ncx >= 3 ? min(cx + 1, ncx - 1) : ncx - 1;
-    const int xw = ncx >= 3 ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
-    // the six ranges (three rows, each a run of cells plus its wrap cell)
-#pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      const int oy = loy + (r >> 1), part = r & 1;
-      const bool use = oy <= hiy && (part == 0 || xw >= 0);
-      const int row = ((cy + oy + ncy) & (ncy - 1)) << lx;
-      const int c_lo = row | (part == 0 ? xa : xw), c_hi = row | (part == 0 ? xb : xw);
-      const int jb = use ? (c_lo ? cend[c_lo - 1] : 0) : 0;
-      const int je = use ? cend[c_hi] : 0;
-      off6[k][r] = jb - pre6[k][r];
-      pre6[k][r + 1] = pre6[k][r] + (je - jb);
-    }
-    const float* nb2_row = nb2 + (pk >> 24) * kMaxSpecies;
-    const int total = pre6[k][6];
-    for (int f = 0; f < total; ++f) {
-      int o = off6[k][0];
-#pragma unroll
-      for (int r = 1; r < 6; ++r) o = f >= pre6[k][r] ? off6[k][r] : o;
-      const int jj = f + o;
-      const int pj = rid[jj], j = pj & 0xffffff;
-      const float ddx = (float)(int32_t)(rx[jj] - qx) * sx0;
-      const float ddy = (float)(int32_t)(ry[jj] - qy) * sx1;
-      if (i < j && ddx * ddx + ddy * ddy < nb2_row[pj >> 24]) {
-        const uint32_t kv = (uint32_t)i | ((uint32_t)j << 16);
-#pragma unroll
-        for (int u = 0; u < kKeep; ++u) keep[k][u] = found[k] == u ? kv : keep[k][u];
-        ++found[k];
-      }
-    }
-    mine += found[k];
-  }
-  // block exclusive scan of the threads' counts (waves in order)
-  const int v = wave_incl_scan(mine);
-  if (lane == 63) wave_sums[wv] = v;
-  __syncthreads();
-  int before = 0, total_all = 0;
-  for (int q = 0; q < (T >> 6); ++q) {
-    const int c = wave_sums[q];
-    before += q < wv ? c : 0;
-    total_all += c;
-  }
-  int off = before + v - mine;
-  uint32_t* out = sc.gplist + (size_t)e * sc.pair_cap;
-#pragma unroll
-  for (int k = 0; k < CH; ++k) {
-    const int ps = tid + k * T;
-    if (found[k] <= kKeep) {
-#pragma unroll
-      for (int u = 0; u < kKeep; ++u)
-        if (u < found[k] && off + u < sc.pair_cap) out[off + u] = keep[k][u];
-    } else {  // a denser entry: its candidates again, every pair written
-      const int pk = rid[ps], i = pk & 0xffffff;
-      const uint32_t qx = rx[ps], qy = ry[ps];
-      const float* nb2_row = nb2 + (pk >> 24) * kMaxSpecies;
-      int w = 0;
-      for (int f = 0; f < pre6[k][6]; ++f) {
-        int o = off6[k][0];
-#pragma unroll
-        for (int r = 1; r < 6; ++r) o = f >= pre6[k][r] ? off6[k][r] : o;
-        const int jj = f + o;
-        const int pj = rid[jj], j = pj & 0xffffff;
-        const float ddx = (float)(int32_t)(rx[jj] - qx) * sx0;
-        const float ddy = (float)(int32_t)(ry[jj] - qy) * sx1;
-        if (i < j && ddx * ddx + ddy * ddy < nb2_row[pj >> 24]) {
-          if (off + w < sc.pair_cap) out[off + w] = (uint32_t)i | ((uint32_t)j << 16);
-          ++w;
-        }
-      }
-    }
-    off += found[k];
-  }
-  if (tid == 0) sc.gnpairs[e] = total_all;  // > pair_cap: the build takes the global path
-}
-
-// kPairs (ride-along launches, periodic 2-D, one staging pass): the pair
-// search follows from the sorted rows in LDS (sort_pairs_lds).
 // CH: particles per thread kept in registers across the scan (4, or 16
 // above 4096).
-template <int CH, bool kPairs = false>
+template <int CH>
 __device__ __forceinline__ void build_sort_body(const DevState& st, const Scratch& sc, int lx,
-                                                int ly, int e, unsigned char* smem,
-                                                const Derived* __restrict__ d = nullptr) {
+                                                int ly, int e, unsigned char* smem) {
   const int T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly);
@@ -1378,9 +1205,6 @@ __device__ __forceinline__ void build_sort_body(const DevState& st, const Scratc
     }
     for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
     SWARM_STAMP(5);
-    if constexpr (kPairs) {
-      if (K >= N) sort_pairs_lds<CH>(d, sc, lx, ly, e, N, cnt, lx_, ly_, lid, wave_sums);
-    }
     return;
   }
 #pragma unroll
@@ -1490,22 +1314,12 @@ __global__ __launch_bounds__(1024) void k_build_sort(DevState st, Scratch sc, in
 // wave with a denser thread rescans to write.
 // Body for block bx of env e (k_build_pairs: grid (ceil(N / blockDim), E);
 // fused launches pass their own block index); nb2: a block-shared table.
-// kStaged (latency-bound launches, few envs): the env's sorted records and
-// cell starts are first copied into LDS (`stage`, pairs_stage_words(N, lx,
-// ly) words) by coalesced loads in flight together, so the dependent chain
-// own record -> cell bounds -> candidates reads LDS instead of three rounds
-// of memory latency.
-__host__ __device__ inline size_t pairs_stage_words(int n, int lx, int ly) {
-  return 3 * (size_t)n + ((size_t)1 << (lx + ly)) + 1;
-}
-
 // kLocal (= sc.local_uf, a compile-time variant so that the plain pair
 // search carries none of the local union-find's code or registers).
-template <bool kStaged = false, bool kLocal = false>
+template <bool kLocal = false>
 __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, const DevState& st,
                                                  const Scratch& sc, int lx, int ly, int bx, int e,
-                                                 float* nb2, int32_t* uf,
-                                                 uint32_t* stage = nullptr) {
+                                                 float* nb2, int32_t* uf) {
   constexpr int kKeep = 8;
   for (int k = threadIdx.x; k < kMaxSpecies * kMaxSpecies; k += blockDim.x) nb2[k] = d->nb2[k];
   const int N = st.n;
@@ -1516,25 +1330,11 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly);
   const int32_t* gcs = sc.bcstart + (size_t)e * (ncell + 1);
-  if constexpr (kStaged) {
-#pragma unroll 4
-    for (int k = t; k < N; k += T) {
-      const uint32_t x = sc.bsq[base + k], y = sc.bsq[M + base + k];
-      const int32_t id = sc.bsid[base + k];
-      stage[k] = x;
-      stage[N + k] = y;
-      stage[2 * N + k] = (uint32_t)id;
-    }
-    for (int k = t; k <= ncell; k += T) stage[3 * N + k] = (uint32_t)gcs[k];
-    __syncthreads();
-  }
-  // the sorted records (x, y, id) and cell starts, from LDS or memory
-  auto QX = [&](int j) -> uint32_t { return kStaged ? stage[j] : sc.bsq[base + j]; };
-  auto QY = [&](int j) -> uint32_t { return kStaged ? stage[N + j] : sc.bsq[M + base + j]; };
-  auto SID = [&](int j) -> int32_t {
-    return kStaged ? (int32_t)stage[2 * N + j] : sc.bsid[base + j];
-  };
-  auto CS = [&](int c) -> int32_t { return kStaged ? (int32_t)stage[3 * N + c] : gcs[c]; };
+  // the sorted records (x, y, id) and cell starts
+  auto QX = [&](int j) -> uint32_t { return sc.bsq[base + j]; };
+  auto QY = [&](int j) -> uint32_t { return sc.bsq[M + base + j]; };
+  auto SID = [&](int j) -> int32_t { return sc.bsid[base + j]; };
+  auto CS = [&](int c) -> int32_t { return gcs[c]; };
   const int ncx = 1 << lx, ncy = 1 << ly;
   const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
   const float sx0 = d->sx[0], sx1 = d->sx[1];
@@ -1583,10 +1383,7 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
   // iteration whatever the split over the ranges (about 11 candidates at
   // area fraction 0.1: two rounds of loads, not one per range; 16 in
   // flight measured slower, 4096 colloids)
-#ifndef SWARM_PAIRS_FLY
-#define SWARM_PAIRS_FLY 8
-#endif
-  constexpr int kFly = SWARM_PAIRS_FLY;
+  constexpr int kFly = 8;
   int off[6], pre[7];
   pre[0] = 0;
 #pragma unroll
@@ -1638,26 +1435,9 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
     v = wave_incl_scan(v);
     int wbase = 0;
     uint32_t* out = sc.gplist + (size_t)e * sc.pair_cap;
-    int cap = sc.pair_cap;
-    if (sc.pair_region > 0) {
-      // this block's own region of the list and its count (no returning
-      // global atomic): the waves' totals scanned in LDS (uf is free here)
-      const int wv = threadIdx.x >> 6, nw = (T + 63) >> 6;
-      if (lane == 63) uf[wv] = v;
-      __syncthreads();
-      int tot = 0;
-      for (int q = 0; q < nw; ++q) {
-        const int c = uf[q];
-        wbase += q < wv ? c : 0;
-        tot += c;
-      }
-      if (threadIdx.x == 0) sc.gbcnt[(size_t)e * ((N + T - 1) / T) + bx] = tot;
-      out += (size_t)bx * sc.pair_region;
-      cap = sc.pair_region;  // a fuller block: the build sees count > region
-    } else {
-      if (lane == 63) wbase = atomicAdd(&sc.gnpairs[e], v);
-      wbase = __builtin_amdgcn_readlane(wbase, 63);
-    }
+    const int cap = sc.pair_cap;
+    if (lane == 63) wbase = atomicAdd(&sc.gnpairs[e], v);
+    wbase = __builtin_amdgcn_readlane(wbase, 63);
     const int my_off = wbase + v - found;
     if (!dense) {
 #pragma unroll
@@ -1768,7 +1548,7 @@ __global__ __launch_bounds__(256) void k_build_pairs(const Derived* __restrict__
                                                      Scratch sc, int lx, int ly) {
   __shared__ float nb2[kMaxSpecies * kMaxSpecies];
   __shared__ int32_t uf[2 * 256];
-  build_pairs_body<false, kLocal>(d, st, sc, lx, ly, blockIdx.x, blockIdx.y, nb2, uf);
+  build_pairs_body<kLocal>(d, st, sc, lx, ly, blockIdx.x, blockIdx.y, nb2, uf);
 }
 
 // The packing class v whose free-lane range holds singleton rank r < nfree:
@@ -1778,14 +1558,6 @@ __global__ __launch_bounds__(256) void k_build_pairs(const Derived* __restrict__
 // independent LDS reads (every 8th entry, then the eight from the last of
 // those <= r) -- two LDS latencies where a binary search waits for six.
 __device__ __forceinline__ int free_class(const int32_t* freebase, int r) {
-#ifdef SWARM_BUILD_BSEARCH
-  int lo = 2, hi = 64;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (freebase[mid] <= r) lo = mid; else hi = mid - 1;
-  }
-  return lo;
-#else
   int k8 = -1;
 #pragma unroll
   for (int q = 0; q < 8; ++q) k8 += freebase[2 + 8 * q] <= r ? 1 : 0;
@@ -1793,7 +1565,6 @@ __device__ __forceinline__ int free_class(const int32_t* freebase, int r) {
 #pragma unroll
   for (int q = 0; q < 8; ++q) v += freebase[2 + 8 * k8 + q] <= r ? 1 : 0;
   return v;
-#endif
 }
 
 // LDS words of the large-N variant: the union-find forest only.
@@ -1833,35 +1604,9 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   // kCount: the union sweep counts each particle's pairs (as the lower index)
   // in lslot, and the root walks add them to their cluster -- no separate
   // sweep over the pair list for the one-pass pair counts
-#ifdef SWARM_BUILD_SPLIT_FIND
-  constexpr bool kFused = false;
-#else
   constexpr bool kFused = !kBig;
-#endif
-#ifdef SWARM_BUILD_PAIR_SWEEP
-  constexpr bool kCount = false;
-#else
   constexpr bool kCount = kFused && !kLocal;
-#endif
   SWARM_STAMP(6);
-  // region lists (sc.pair_region): the blocks' counts, their prefix sums in
-  // freebase (free until the packing), the total as `found`
-  const bool regions = !kBig && kCopy && sc.pair_region > 0;
-  const int nreg = (N + 255) / 256;
-  if (regions) {
-    if (tid < 64) {
-      const int c = tid < nreg ? sc.gbcnt[(size_t)e * nreg + tid] : 0;
-      const int v = wave_incl_scan(c);
-      freebase[tid] = v - c;
-      const bool over = __any(c > sc.pair_region);
-      if (tid == 63) {
-        freebase[64] = v;
-        misc[7] = over ? 1 : 0;
-      }
-    }
-    __syncthreads();
-    found = misc[7] ? sc.pair_cap + 1 : freebase[64];
-  }
   const int npairs = min(found, sc.pair_cap);
   // kLocal: the pair search's blocks unioned their own pairs already
   // (sc.lroot: a forest of depth one), only the cross-block pairs remain
@@ -1869,9 +1614,8 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   const uint32_t* xl = sc.xpairs + (size_t)e * sc.pair_cap;
   for (int k = tid; k < 68; k += T) classcnt[k] = 0;
   for (int k = tid; k < wmax; k += T) wave_np[k] = 0;
-  // overflow of the pair or cross list -> global path (misc[7]: read above)
-  if (tid < 16 && tid != 7)
-    misc[tid] = tid == 0 && (found > sc.pair_cap || nx > sc.pair_cap) ? 1 : 0;
+  // overflow of the pair or cross list -> global path
+  if (tid < 16) misc[tid] = tid == 0 && (found > sc.pair_cap || nx > sc.pair_cap) ? 1 : 0;
   for (int i = tid; i < N; i += T) {
     if (kLocal) {
       const uint32_t l = (uint32_t)sc.lroot[base + i];
@@ -1884,22 +1628,7 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
     csz[i] = 0;
     cbase[i] = 0;  // pair count of a cluster (one-pass packing), then its base
   }
-  if (regions) {  // each wave gathers whole regions, four loads in flight per lane
-    const uint32_t* gp = sc.gplist + (size_t)e * sc.pair_cap;
-    const int lane = tid & 63, nw = T >> 6;
-    for (int b = tid >> 6; b < nreg; b += nw) {
-      const int c = freebase[b + 1] - freebase[b], o = freebase[b];
-      const uint32_t* src = gp + (size_t)b * sc.pair_region;
-      for (int k0 = lane; k0 < c; k0 += 4 * 64) {
-        uint32_t v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = k0 + u * 64 < c ? src[k0 + u * 64] : 0u;
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (k0 + u * 64 < c && o + k0 + u * 64 < npairs) plist[o + k0 + u * 64] = v[u];
-      }
-    }
-  } else if (!kBig && kCopy) {  // pair list into LDS, four loads in flight per thread
+  if (!kBig && kCopy) {  // pair list into LDS, four loads in flight per thread
     const uint32_t* gp = sc.gplist + (size_t)e * sc.pair_cap;
     for (int k0 = tid; k0 < npairs; k0 += 4 * T) {
       uint32_t v[4];
@@ -1917,10 +1646,7 @@ __device__ __forceinline__ void cluster_build_env(const DevState& st, const Scra
   // kU iterations, not one per iteration.  (In LDS, kU = 4 measured no
   // better than 1 at E = 1: the union phase 1 k cycles shorter, the
   // others longer.)
-#ifndef SWARM_BUILD_KU
-#define SWARM_BUILD_KU 1
-#endif
-  constexpr int kU = kBig ? 8 : SWARM_BUILD_KU;
+  constexpr int kU = kBig ? 8 : 1;
   // The pair sweeps visit the LDS pair list in a spread order: neighbouring
   // pairs of the cell-sorted list usually share a cluster, so lanes of one
   // wave taking consecutive pairs contend on the same root / wave counter
@@ -2668,7 +2394,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // Noise table for latency-bound windows (few waves per SIMD): the normals of
 // every (sub-step, particle) computed ahead of the run.  Indexed by particle,
 // not wave slot, so it does not wait for the cluster build.
-// Particle-major (SWARM_NOISE_PMAJOR, the default): particle gi's sub-steps
+// Particle-major: particle gi's sub-steps
 // are one contiguous run of 12-B records, table[(gi * kMaxWindow + s) * 3 +
 // c], so a lane reads its sub-step's three normals with one 12-B load and a
 // 128-B line (~10 sub-steps of one particle) is fetched by the one XCD that
@@ -2679,18 +2405,14 @@ __device__ __forceinline__ void wave_lds_sync() {
 // on otherwise idle CUs while it reads this one's.  The control block
 // records each table's first step and length; a run whose window does not
 // match its table draws the normals itself.
-#ifndef SWARM_NOISE_PMAJOR
-#define SWARM_NOISE_PMAJOR 1
-#endif
-constexpr bool kNoisePMajor = SWARM_NOISE_PMAJOR != 0;
 __host__ __device__ inline size_t noise_table_words(size_t M) { return (size_t)kMaxWindow * 3 * M; }
 // word of normal c of sub-step s of particle gi; the step and component strides
 __host__ __device__ inline size_t noise_index(size_t M, size_t gi, int s, int c) {
-  return kNoisePMajor ? (gi * kMaxWindow + (size_t)s) * 3 + (size_t)c
-                      : ((size_t)s * 3 + (size_t)c) * M + gi;
+  (void)M;
+  return (gi * kMaxWindow + (size_t)s) * 3 + (size_t)c;
 }
-__host__ __device__ inline size_t noise_step_stride(size_t M) { return kNoisePMajor ? 3 : 3 * M; }
-__host__ __device__ inline size_t noise_comp_stride(size_t M) { return kNoisePMajor ? 1 : M; }
+__host__ __device__ inline size_t noise_step_stride(size_t) { return 3; }
+__host__ __device__ inline size_t noise_comp_stride(size_t) { return 1; }
 
 // Group k of a table starting at step_start: sub-steps t = 4 (g0 + k) + j
 // (g0 = step_start / 4) of particle gi, those within [start, start + len).
@@ -2718,18 +2440,13 @@ __device__ __forceinline__ void noise_group(const Derived* __restrict__ d, const
   }
 }
 
-// Work item k of a table fill over M particles x G groups: particle-major
-// tables give consecutive items the consecutive groups of one particle (the
-// stores of a wave then cover contiguous records), step-major ones the same
-// group of consecutive particles.
+// Work item k of a table fill over M particles x G groups: consecutive
+// items are the consecutive groups of one particle (the stores of a wave
+// then cover contiguous records).
 __device__ __forceinline__ void noise_item(long k, long M, int G, long* gi, int* grp) {
-  if (kNoisePMajor) {
-    *gi = k / G;
-    *grp = (int)(k - *gi * G);
-  } else {
-    *grp = (int)(k / M);
-    *gi = k - (long)*grp * M;
-  }
+  (void)M;
+  *gi = k / G;
+  *grp = (int)(k - *gi * G);
 }
 
 __host__ __device__ inline int noise_groups(int len) { return len / 4 + 2; }  // any alignment
@@ -2759,20 +2476,15 @@ __global__ __launch_bounds__(256) void k_noise(const Derived* __restrict__ d, De
 // its 64 slots.  kTable: the normals come from this window's noise table
 // (prefetched one sub-step ahead), else they are drawn here.
 // kMulti = false: one species, so the pair constants are wave-uniform scalars.
-// kDir (latency-bound launches, k_cluster_run_wide): the swim vector of
-// every sub-step, fs * (cos, sin) of the orientation, and the final angle
-// were computed ahead by the block's idle waves (precompute_swim) into LDS
-// (dtab[s * 64 + lane], angfin[lane]): the rotation is position-independent,
-// so the run wave's dependency chain loses the angle update and sin/cos.
-template <bool kMulti, bool kTable, bool kWalls, bool kDir = false, bool kTwoPass = false>
+// kTwoPass: waves with 65-128 pairs get their own unrolled two-pass variant
+// (else the general up-to-four-pass loop).
+template <bool kMulti, bool kTable, bool kWalls, bool kTwoPass = false>
 __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const DevState& st,
                                          const Scratch& sc, int n_envs, int n_steps,
                                          uint64_t step0, const float* __restrict__ table,
                                          int gw, int lane, uint2* lpos_w,
                                          unsigned long long* lacc_x, unsigned long long* lacc_y,
-                                         const PairTables& pt, int par,
-                                         const float2* __restrict__ dtab = nullptr,
-                                         const uint32_t* __restrict__ angfin = nullptr) {
+                                         const PairTables& pt, int par) {
   const int e = gw / sc.wmax;
   const int w = gw - e * sc.wmax;
   if (e >= n_envs) return;
@@ -2857,25 +2569,15 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
   // the pass count (0, 1 or up to 4) and the last sub-step (velocities) are
   // compile-time variants, and idle lanes compute along (never stored).
   float dir[2];
-  float2 swn = make_float2(0.0f, 0.0f);  // kDir: the next sub-step's swim vector
-  if (kDir)
-    swn = dtab[lane];
-  else
-    sincos_turn(an0, &dir[0], &dir[1]);
+  sincos_turn(an0, &dir[0], &dir[1]);
   auto substep = [&](const int s, auto last_t, auto pass_t) __attribute__((always_inline)) {
     constexpr bool kLast = decltype(last_t)::value;
-    constexpr int kPass = decltype(pass_t)::value;  // 0, 1, or 4: up to npass
+    constexpr int kPass = decltype(pass_t)::value;  // 0, 1, 2 or 4: up to npass
 #ifdef SWARM_PHASE_TIMING
     if (stamp) t0s = t1s = __builtin_amdgcn_s_memtime();
 #endif
     float gt[3] = {gn[0], gn[1], gn[2]};
-    const float2 sw = swn;
-    if (kDir && !kLast) swn = dtab[(s + 1) * 64 + lane];
-#ifdef SWARM_ABL_NOTABLE  // timing ablation only (tools/_variants): no table loads
-    if (false) {
-#else
     if (kTable && !kLast) {  // the next sub-step's normals, one sub-step ahead
-#endif
       const float* nx = tcol + (size_t)(s + 1) * tstep;
       gn[0] = nx[0];
       gn[1] = nx[ts];
@@ -2916,16 +2618,11 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     // rotation (bd_step's sequence) and the next director, between the
     // force-sum atomics and their read-back
     __builtin_amdgcn_sched_barrier(0);
-    uint32_t an_next = p.an;
     float dnext[2] = {dir[0], dir[1]};
-    if (!kDir) {
-      float dth = tz * pc.rot_dt;
-      if (pc.noisy) dth = dth + pc.sig_r * gt[2];
-      an_next = p.an + (uint32_t)f2i32(dth * kAngInvScale);
-#ifndef SWARM_ABL_NOSINCOS  // timing ablation only: the director stays fixed
-      if (!kLast) sincos_turn(an_next, &dnext[0], &dnext[1]);
-#endif
-    }
+    float dth = tz * pc.rot_dt;
+    if (pc.noisy) dth = dth + pc.sig_r * gt[2];
+    const uint32_t an_next = p.an + (uint32_t)f2i32(dth * kAngInvScale);
+    if (!kLast) sincos_turn(an_next, &dnext[0], &dnext[1]);
     __builtin_amdgcn_sched_barrier(0);
     __asm__ volatile("" ::: "memory");  // keep the read-back after the director
     if (kPass > 0) {
@@ -2953,19 +2650,15 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
       wall_forces<2>(d, si, (float)p.qx * sx0, (float)p.qy * sx1, 0.0f, ax, ay, az,
                      st.wall_viol);
     }
-    if (kDir)
-      bd_translate_sw(pc, p, ax, ay, sw.x, sw.y, tz, fex, fey, k0, k1, (uint32_t)i,
-                      step0 + (uint64_t)s, kLast, &vx, &vy, &om, gt);
-    else
-      bd_translate(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
-                   kLast, &vx, &vy, &om, gt, dir[0], dir[1]);
+    bd_translate(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
+                 kLast, &vx, &vy, &om, gt, dir[0], dir[1]);
     const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
     const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
     // non-negative floats order like their bit patterns: one v_max_u32
     // (fmaxf adds a canonicalising max)
     dmax2 = __uint_as_float(max(__float_as_uint(dmax2), __float_as_uint(ddx * ddx + ddy * ddy)));
     p.an = an_next;
-    if (!kDir && !kLast) {
+    if (!kLast) {
       dir[0] = dnext[0];
       dir[1] = dnext[1];
     }
@@ -3000,15 +2693,11 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     }
     substep(s, std::true_type{}, pass_t);  // velocities of the last sub-step
   };
-#ifdef SWARM_ABL_NOPAIR  // timing ablation only: no pair section
-  if (true)
-#else
   if (npass == 0)
-#endif
     run_steps(std::integral_constant<int, 0>{});
   else if (npass == 1)
     run_steps(std::integral_constant<int, 1>{});
-  else if (kTwoPass && npass == 2)  // (the throughput kernel: not worth its registers)
+  else if (kTwoPass && npass == 2)
     run_steps(std::integral_constant<int, 2>{});
   else
     run_steps(std::integral_constant<int, 4>{});
@@ -3028,7 +2717,6 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     ws[3] = (uint64_t)np;
   }
 #endif
-  if (kDir) p.an = angfin[lane];  // the rotation was integrated ahead
   if (active) {
     st.q[gi] = p.qx;
     st.q[M + gi] = p.qy;
@@ -3107,7 +2795,7 @@ __device__ __forceinline__ bool xcd_env_block(int b, int blocks_per_env, int n_e
 // (ceil(wmax / 4)); else block b runs waves 4 b .. 4 b + 3 of the env-major
 // wave list.
 template <bool kMulti, bool kTable, bool kWalls>
-__global__ __launch_bounds__(256, SWARM_RUN_MINB) void k_cluster_run(const Derived* __restrict__ d, DevState st,
+__global__ __launch_bounds__(256, kRunMinBlocks) void k_cluster_run(const Derived* __restrict__ d, DevState st,
                                                      Scratch sc, int n_envs, int n_steps,
                                                      const uint64_t* __restrict__ ctl,
                                                      const float* __restrict__ tables,
@@ -3147,92 +2835,13 @@ __global__ __launch_bounds__(256, SWARM_RUN_MINB) void k_cluster_run(const Deriv
 // run with waves [0, run_wpb) only: one run wave per CU at E = 1 (its
 // scattered noise-table gathers then have the CU's texture path to themselves),
 // up to one per SIMD for more envs.
-// The rotation of the block's R run waves (first global wave gw0),
-// integrated ahead by the whole block (1024 threads: 16 / R chunks of the
-// window's sub-steps x 64 R particles) while the run waves would otherwise
-// compute it serially, sub-step by sub-step: per particle the angle
-// increments of bd_step's sequence (dth = tz rot_dt + sig_r g2, rounded to
-// turn units; with reuse_forces sub-step 0 turns with the previous run's
-// torque), an exclusive prefix over the chunks (integer adds: exact in any
-// order), then the swim vector of every sub-step, fs * sincos(orientation)
-// -- sub-step 0 swims along the orientation (and with the force) of the last
-// force calculation -- into dtab[(r * kMaxWindow + s) * 64 + lane] and the
-// final angle into angfin[r * 64 + lane].  Same values as run_wave computes
-// inline.  Block-uniform: every thread of the block calls it.
-template <bool kMulti, int R>
-__device__ __forceinline__ void precompute_swim(const Derived* __restrict__ d, const DevState& st,
-                                                const Scratch& sc, int n_envs, int gw0,
-                                                int n_steps, const float* __restrict__ table,
-                                                int par, float2* dtab, uint32_t* angfin,
-                                                uint32_t* partial) {
-  constexpr int P = 64 * R, C = 1024 / P;             // particles, chunks
-  constexpr int kChunk = (kMaxWindow + C - 1) / C;    // sub-steps per chunk at most
-  const int tid = threadIdx.x, pidx = tid % P, c = tid / P;
-  const int rw = pidx >> 6, l = pidx & 63;
-  const int gw = gw0 + rw;
-  const int e = gw / sc.wmax, w = gw - e * sc.wmax;
-  const int N = st.n;
-  const size_t M = (size_t)st.m, base = (size_t)e * N;
-  const int i = e < n_envs ? sc.perm[(size_t)e * sc.S + w * 64 + l] : -1;
-  const size_t gi = i >= 0 ? base + i : 0;
-  const PConst pc = load_pconst(d, kMulti ? (i >= 0 ? (int)st.species[i] : 0) : 0);
-  const PrevSlot prv = prev_slot(st, par);
-  const float tz1 = st.torque_z[gi], fs1 = st.f_swim[gi];
-  const float tz0 = st.reuse ? prv.tz[gi] : tz1, fs0 = st.reuse ? prv.f[gi] : fs1;
-  const uint32_t an_start = st.ang[gi];
-  const uint32_t an0 = st.reuse ? prv.ang[gi] : an_start;
-  const int K = (n_steps + C - 1) / C;
-  const int s0 = c * K;
-  const float* tcol = table + noise_index(M, gi, 0, 0);
-  const size_t tstep = noise_step_stride(M), ts = noise_comp_stride(M);
-  float g2[kChunk];
-#pragma unroll
-  for (int k = 0; k < kChunk; ++k)
-    g2[k] = k < K && s0 + k < n_steps ? tcol[(s0 + k) * tstep + 2 * ts] : 0.0f;
-  uint32_t inc[kChunk];
-  uint32_t sum = 0u;
-#pragma unroll
-  for (int k = 0; k < kChunk; ++k) {
-    const int s = s0 + k;
-    float dth = (s == 0 ? tz0 : tz1) * pc.rot_dt;
-    if (pc.noisy) dth = dth + pc.sig_r * g2[k];
-    inc[k] = k < K && s < n_steps ? (uint32_t)f2i32(dth * kAngInvScale) : 0u;
-    sum += inc[k];
-  }
-  partial[c * P + pidx] = sum;
-  __syncthreads();
-  uint32_t an = an_start;
-  for (int k = 0; k < c; ++k) an += partial[k * P + pidx];
-  float2* dt = dtab + (size_t)rw * kMaxWindow * 64;
-#pragma unroll
-  for (int k = 0; k < kChunk; ++k) {
-    const int s = s0 + k;
-    if (k < K && s < n_steps) {
-      float sn, cs;
-      sincos_turn(s == 0 ? an0 : an, &sn, &cs);
-      const float fs = s == 0 ? fs0 : fs1;
-      dt[s * 64 + l] = make_float2(fs * cs, fs * sn);
-      an += inc[k];
-      if (s == n_steps - 1) angfin[rw * 64 + l] = an;
-    }
-  }
-  __syncthreads();
-}
-
-// Dynamic LDS of k_cluster_run_wide's precomputed rotation (R run waves).
-__host__ __device__ constexpr size_t wide_dir_lds_bytes(int R) {
-  return (size_t)R * kMaxWindow * 64 * sizeof(float2) + (size_t)R * 64 * 4 + 1024 * 4;
-}
-
 template <bool kMulti, bool kWalls>
 __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __restrict__ d,
                                                            DevState st, Scratch sc, int n_envs,
                                                            int n_steps, uint64_t* __restrict__ ctl,
                                                            float* __restrict__ tables,
                                                            int n_noise_blocks, int run_wpb,
-                                                           int rot_ahead,
                                                            unsigned long long* __restrict__ tstamp) {
-  extern __shared__ __align__(16) unsigned char wide_lds[];
   __shared__ PairTables pt;
   __shared__ uint2 lpos[4][64];
   __shared__ unsigned long long lacc[4][2][64];
@@ -3264,27 +2873,6 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
   const int gw0 = (b - n_noise_blocks) * run_wpb;
   const bool table_ok = ctl[kCtlTStep + par] == step0 && (uint64_t)n_steps <= ctl[kCtlTLen + par];
   const float* table = table_ok ? tables + par * noise_table_words(M) : nullptr;
-  // one or two run waves per block (a latency-bound launch; the host sized
-  // the dynamic LDS, wide_dir_lds_bytes) and this window's normals in the
-  // table: the other waves integrate the run waves' rotation ahead
-  if (rot_ahead && (run_wpb == 1 || run_wpb == 2) && table_ok && blockDim.x == 1024 &&
-      tables != nullptr) {
-    float2* dtab = reinterpret_cast<float2*>(wide_lds);  // [R][kMaxWindow][64]
-    uint32_t* angfin = reinterpret_cast<uint32_t*>(dtab + (size_t)run_wpb * kMaxWindow * 64);
-    uint32_t* partial = angfin + run_wpb * 64;           // [1024]
-    if (run_wpb == 1)
-      precompute_swim<kMulti, 1>(d, st, sc, n_envs, gw0, n_steps, table, par, dtab, angfin,
-                                 partial);
-    else
-      precompute_swim<kMulti, 2>(d, st, sc, n_envs, gw0, n_steps, table, par, dtab, angfin,
-                                 partial);
-    if (wv >= run_wpb) return;
-    run_wave<kMulti, true, kWalls, true, true>(d, st, sc, n_envs, n_steps, step0, table, gw0 + wv,
-                                         lane, lpos[wv], lacc[wv][0], lacc[wv][1], pt, par,
-                                         dtab + (size_t)wv * kMaxWindow * 64, angfin + wv * 64);
-    stamp_end(tstamp);
-    return;
-  }
   if (wv >= run_wpb) return;
   const int gw = gw0 + wv;
   run_wave_dispatch<kMulti, kWalls>(d, st, sc, n_envs, n_steps, step0, table, gw, lane, lpos[wv],

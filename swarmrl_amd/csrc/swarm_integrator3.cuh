@@ -1041,11 +1041,7 @@ __global__ __launch_bounds__(256) void k_nl_step3(const Derived* __restrict__ d,
   const float eps24 = d->eps24;
   int64_t acc[3] = {0, 0, 0};
   const int32_t* nlp = sc.nl + gi;
-#ifdef SWARM_ABL_NL_NOPAIR  // timing ablation only (tools/_variants)
-  for (int k0 = 0; k0 < 0; k0 += 4) {
-#else
   for (int k0 = 0; k0 < nn; k0 += 8) {
-#endif
     // eight neighbours per round: their indices, then their positions, in
     // flight together (two memory latencies per round)
     int32_t pk[8];
@@ -1075,12 +1071,10 @@ __global__ __launch_bounds__(256) void k_nl_step3(const Derived* __restrict__ d,
   const bool noisy = d->noisy != 0;
   float f[3], ph[3];
   float gt[3] = {0.0f, 0.0f, 0.0f}, gr[3] = {0.0f, 0.0f, 0.0f};
-#ifndef SWARM_ABL_NL_NONOISE  // timing ablation only (tools/_variants)
   if (noisy) {
     step_normals(k0, k1, (uint32_t)i, step, gt);
     normals3(k0, k1, (uint32_t)i, step, 2u, gr);
   }
-#endif
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
     f[a] = i64_to_f32(acc[a]) * 5.9604644775390625e-08f;
@@ -1094,9 +1088,7 @@ __global__ __launch_bounds__(256) void k_nl_step3(const Derived* __restrict__ d,
     }
     advance(q[a], im[a], f2i32(dq * d->inv_sx[a]));
   }
-#ifndef SWARM_ABL_NL_NOROT  // timing ablation only (tools/_variants)
   rotate_director(v, ph[0], ph[1], ph[2]);
-#endif
   if (last) {  // nobody reads st.q during the window
 #pragma unroll
     for (int a = 0; a < 3; ++a) st.q[a * M + gi] = q[a];

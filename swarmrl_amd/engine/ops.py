@@ -476,16 +476,17 @@ def rnd_distance(points: torch.Tensor, target: torch.nn.Module, predictor: torch
     return out
 
 
-_RND_WS = {}
-
-
 def rnd_env_reward(points: torch.Tensor, n_envs: int, target: torch.nn.Module,
-                   predictor: torch.nn.Module, order: int, clip, base: torch.Tensor = None):
-    """The per-env RND reward added to the task reward in two launches
-    (swarm_rnd_env_reward): points [n_envs * per_env, d] fp32 device (env-
-    major); returns (metric [n], env_reward [n_envs, 1], rewards [n_envs,
-    per_env] = base + env_reward, or env_reward broadcast when base is None).
-    clip: (lo, hi) or None."""
+                   predictor: torch.nn.Module, order: int, clip, base: torch.Tensor = None,
+                   workspaces: dict = None):
+    """The per-env RND reward added to the task reward (swarm_rnd_env_reward):
+    points [n_envs * per_env, d] fp32 device (env-major); returns (metric [n],
+    env_reward [n_envs, 1], rewards [n_envs, per_env] = base + env_reward, or
+    env_reward broadcast when base is None).  clip: (lo, hi) or None.
+    workspaces: the caller's own cache of partial-sum workspaces (one per
+    device and size, kept alive for captured graphs that read them); without
+    one every call takes a fresh stream-ordered buffer, so no two callers
+    ever share one."""
     points = points.contiguous()
     n, d = points.shape
     per_env = n // n_envs
@@ -498,9 +499,11 @@ def rnd_env_reward(points: torch.Tensor, n_envs: int, target: torch.nn.Module,
     lib = _capi.lib()
     nbytes = int(lib.swarm_rnd_env_workspace_bytes(n_envs, per_env))
     key = (dev, nbytes)
-    ws = _RND_WS.get(key)
-    if ws is None:  # one workspace per size (kept: captured graphs read it)
-        ws = _RND_WS[key] = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=dev)
+    ws = workspaces.get(key) if workspaces is not None else None
+    if ws is None:
+        ws = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=dev)
+        if workspaces is not None:
+            workspaces[key] = ws
 
     def ptrs(net):
         lin = [m for m in net.modules() if isinstance(m, torch.nn.Linear)]

@@ -279,14 +279,15 @@ class SwarmEngine(Engine):
         self._view = None
         self._type_index_cache = {}
         # device path: prepare each window's build on a side stream while
-        # the force model computes the slice's actions (see _prebuild)
-        self.overlap_build = os.environ.get("SWARMRL_AMD_OVERLAP_BUILD", "1") != "0"
+        # the force model computes the slice's actions (see _prebuild); the
+        # tests turn these off to compare the schedules
+        self.overlap_build = True
         # fork the next slice's build right after the run (before the reward)
-        self.early_fork = os.environ.get("SWARMRL_AMD_EARLY_FORK", "1") != "0"
+        self.early_fork = True
         # latency-bound engines: the next window's build rides along in the
         # vision-cone and policy launches instead of a forked side stream
         # (swarm_engine_defer_build; the engine declines when it cannot)
-        self.ride_along_build = os.environ.get("SWARMRL_AMD_RIDE_ALONG", "1") != "0"
+        self.ride_along_build = True
         self._ride_along = False
         self._side_stream = None
         self._prebuild_pending = None
@@ -1022,7 +1023,7 @@ class SwarmEngine(Engine):
             self.integration_initialised = True
 
         device_path = force_model is not None and self._device_capable(force_model)
-        # ride-along builds (SWARMRL_AMD_RIDE_ALONG=0: fork onto a side stream)
+        # ride-along builds (ride_along_build = False: fork onto a side stream)
         self._ride_along = bool(device_path and self.ride_along_build and
                                 getattr(force_model, "absorbs_build", lambda: False)())
         old_slice_idx = self.slice_idx

@@ -30,8 +30,13 @@ class RNDReward(IntrinsicReward):
         self.predictor_network = RNDArchitecture(in_dim).to(self.device)
         for p in self.target_network.parameters():
             p.requires_grad_(False)
+        # capturable on the GPU: its step counters live on the device like the
+        # parameters (no host sync per step; broadcast_agent sends them over
+        # RCCL like every other tensor of the replica)
         self.optimizer = torch.optim.Adam(self.predictor_network.parameters(),
-                                          lr=rnd_config.learning_rate)
+                                          lr=rnd_config.learning_rate,
+                                          capturable=self.device.type == "cuda")
+        self._ws = {}  # swarm_rnd_env_reward partial-sum workspaces (ops.rnd_env_reward)
 
     @staticmethod
     def _stack(x) -> torch.Tensor:
@@ -138,7 +143,7 @@ class RNDReward(IntrinsicReward):
 
             self.metric_results, r, _ = ops.rnd_env_reward(
                 points, int(last.shape[0]), self.target_network, self.predictor_network,
-                self.distance_order, self.clip_rewards)
+                self.distance_order, self.clip_rewards, workspaces=self._ws)
             return r
         r = self.compute_distance(points)
         if self._per_env(last):
@@ -161,6 +166,6 @@ class RNDReward(IntrinsicReward):
 
                 self.metric_results, _, out = ops.rnd_env_reward(
                     points, int(last.shape[0]), self.target_network, self.predictor_network,
-                    self.distance_order, self.clip_rewards, base=rewards)
+                    self.distance_order, self.clip_rewards, base=rewards, workspaces=self._ws)
                 return out.reshape(rewards.shape)
         return rewards + self.compute_reward(episode_data)

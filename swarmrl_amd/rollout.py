@@ -32,8 +32,6 @@ import torch.distributed as dist
 from swarmrl_amd.utils.colloid_utils import TrajectoryInformation
 
 _NAMES = ("features", "actions", "log_probs", "rewards")
-# per-rank env counts established by _env_counts, keyed by (group, local shapes)
-_COUNTS: Dict[tuple, list] = {}
 
 
 def shard_envs(total_envs: int, rank: int, world: int):
@@ -81,23 +79,21 @@ def _killed_flag(killed, device) -> torch.Tensor:
 
 
 def _env_counts(bufs, group, env_counts: Optional[Sequence[int]]) -> list:
-    """Env count of every rank.  Given by the caller (shard_envs), or
-    exchanged once per (group, local buffer shapes) with a small all-gather
-    and cached: the shapes of an engine's trajectory do not change between
-    episodes, so the per-episode collective stays the single packed one."""
+    """Env count of every rank: given by the caller (shard_envs: the packed
+    all-gather is then the episode's only collective), or exchanged with a
+    small all-gather on every call -- every rank takes the same branch, so
+    the collectives always match (a per-rank cache could let one rank skip
+    the count exchange while another runs it)."""
     world = dist.get_world_size(group)
     if env_counts is not None:
         if len(env_counts) != world:
             raise ValueError(f"env_counts has {len(env_counts)} entries for a world of {world}")
         return [int(c) for c in env_counts]
-    key = (id(group),) + tuple(tuple(b.shape) for b in bufs.values())
-    if key not in _COUNTS:
-        dev = bufs["actions"].device
-        mine = torch.tensor([bufs["actions"].shape[1]], dtype=torch.int64, device=dev)
-        allc = torch.zeros(world, dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(allc, mine, group=group)
-        _COUNTS[key] = [int(c) for c in allc.cpu()]
-    return _COUNTS[key]
+    dev = bufs["actions"].device
+    mine = torch.tensor([bufs["actions"].shape[1]], dtype=torch.int64, device=dev)
+    allc = torch.zeros(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(allc, mine, group=group)
+    return [int(c) for c in allc.cpu()]
 
 
 def gather_trajectory(trajectory, group=None, stats: Optional[dict] = None,
@@ -240,8 +236,72 @@ def broadcast_agent(agent, src: int = 0, group=None) -> None:
     if not _is_distributed(group):
         return
     root = src if group is None else dist.get_global_rank(group, src)
+    dev = _collective_device(group)
     for t in _agent_tensors(agent):
-        dist.broadcast(t, root, group=group)
+        if t.device == dev or dev.type == "cpu":
+            dist.broadcast(t, root, group=group)
+        else:
+            # RCCL only moves device tensors: a host-side state tensor (e.g. a
+            # non-capturable optimizer's step counter) goes through a device
+            # copy
+            tmp = t.detach().to(dev)
+            dist.broadcast(tmp, root, group=group)
+            t.copy_(tmp.to(t.device))
+
+
+def _collective_device(group=None) -> torch.device:
+    """Where the group's collectives take their tensors: the current GPU for
+    an RCCL ("nccl") group, the host otherwise."""
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def any_rank(flag: bool, group=None) -> bool:
+    """True on every rank when `flag` is true on any rank (one small
+    all-reduce; the flag itself when not distributed)."""
+    if not _is_distributed(group):
+        return bool(flag)
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=_collective_device(group))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return bool(t.item())
+
+
+@torch.no_grad()
+def replica_checksum(agent, device=None) -> torch.Tensor:
+    """A cheap fingerprint of _agent_tensors on `device`: per tensor the sum
+    of its 32-bit words (int64, wrapping) and a position-weighted sum of
+    them -- equal replicas give equal checksums, and a drifted bit changes
+    them (replicas check each other with it, _ReplicatedUpdate)."""
+    sums = []
+    for t in _agent_tensors(agent):
+        x = t.detach().reshape(-1).contiguous()
+        if device is not None:
+            x = x.to(device)
+        b = x.view(torch.uint8)
+        pad = (-b.numel()) % 4
+        if pad:
+            b = torch.cat([b, torch.zeros(pad, dtype=torch.uint8, device=b.device)])
+        w = b.view(torch.int32).to(torch.int64)
+        pos = torch.arange(1, w.numel() + 1, dtype=torch.int64, device=w.device)
+        sums.append(torch.stack([w.sum(), (w * pos).sum()]))
+    if not sums:
+        return torch.zeros(0, dtype=torch.int64, device=device)
+    return torch.cat(sums)
+
+
+def replicas_match(agent, group=None) -> bool:
+    """Whether every rank's replica of `agent` has the same checksum (one
+    all-gather of a few int64 per tensor)."""
+    if not _is_distributed(group):
+        return True
+    dev = _collective_device(group)
+    mine = replica_checksum(agent, dev)
+    world = dist.get_world_size(group)
+    allc = torch.empty(world * mine.numel(), dtype=mine.dtype, device=dev)
+    dist.all_gather_into_tensor(allc, mine, group=group)
+    allc = allc.view(world, -1)
+    return bool((allc == allc[0:1]).all().item())
 
 
 @torch.no_grad()

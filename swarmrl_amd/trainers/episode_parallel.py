@@ -29,13 +29,31 @@ class _ReplicatedUpdate:
     group = None
     env_counts = None
     update_seed = 0
+    verify_every = 0
     _episodes = 0
 
-    def _setup_parallel(self, group, env_counts, update_seed):
+    def _setup_parallel(self, group, env_counts, update_seed, verify_every=0):
         self.group = group
         self.env_counts = env_counts
         self.update_seed = int(update_seed)
+        self.verify_every = int(verify_every)
         self._episodes = 0
+
+    def update_rl(self):
+        """The base update, then one agreement step: a task's kill switch on
+        any rank stops every rank (learning agents gather it with their
+        episode, the others would raise it on their own rank only, ADVICE
+        r4), and every `verify_every` episodes the replicas compare
+        checksums (rollout.replicas_match) -- a drift raises instead of
+        training on silently diverged models."""
+        ff, total, stop = super().update_rl()
+        stop = rollout.any_rank(stop, self.group)
+        if self.verify_every > 0 and self._episodes % self.verify_every == 0:
+            for agent in self.agents.values():
+                if getattr(agent, "train", False) and not rollout.replicas_match(agent, self.group):
+                    raise RuntimeError("episode-parallel replicas diverged "
+                                       f"(agent {agent.particle_type}, episode {self._episodes})")
+        return ff, total, stop
 
     def initialize_training(self):
         """Rank 0's replicas everywhere, then the first force function."""
@@ -68,16 +86,20 @@ class EpisodeParallelTrainer(_ReplicatedUpdate, ContinuousTrainer):
     group: the torch.distributed process group (default: the world);
     env_counts: the env count of every rank when they differ and are known
     (else exchanged once); update_seed: base seed of the per-episode RNG the
-    intrinsic reward's update draws from (the same on every rank)."""
+    intrinsic reward's update draws from (the same on every rank);
+    verify_every: compare the replicas' checksums every this many episodes
+    (0: never)."""
 
-    def __init__(self, agents, group=None, env_counts=None, update_seed: int = 0):
+    def __init__(self, agents, group=None, env_counts=None, update_seed: int = 0,
+                 verify_every: int = 0):
         super().__init__(agents)
-        self._setup_parallel(group, env_counts, update_seed)
+        self._setup_parallel(group, env_counts, update_seed, verify_every)
 
 
 class EpisodeParallelEpisodicTrainer(_ReplicatedUpdate, EpisodicTrainer):
     """EpisodicTrainer over ranks (get_engine builds this rank's engine)."""
 
-    def __init__(self, agents, group=None, env_counts=None, update_seed: int = 0):
+    def __init__(self, agents, group=None, env_counts=None, update_seed: int = 0,
+                 verify_every: int = 0):
         super().__init__(agents)
-        self._setup_parallel(group, env_counts, update_seed)
+        self._setup_parallel(group, env_counts, update_seed, verify_every)

@@ -79,3 +79,18 @@ def test_integration_sketch_matches_binding():
     assert ctypes.sizeof(sketch) == ctypes.sizeof(_capi.SwarmParams)
     create = re.search(r"p = SwarmParams\((.*?)\)\n", block, flags=re.S).group(1)
     assert re.search(r"\breuse_forces\s*=\s*1\b", create)
+
+
+def test_lib_env_selects_the_library(tmp_path):
+    """SWARMRL_AMD_LIB points the binding at another build of the same
+    library (read once, when swarmrl_amd._capi is imported)."""
+    import subprocess
+    import sys
+
+    code = ("import swarmrl_amd._capi as c, sys; "
+            "sys.stdout.write(str(c._LIB_PATH))")
+    alt = tmp_path / "libswarmrl_amd_alt.so"
+    env = dict(__import__("os").environ, SWARMRL_AMD_LIB=str(alt))
+    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=str(ROOT),
+                         capture_output=True, text=True, check=True).stdout
+    assert out == str(alt)

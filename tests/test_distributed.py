@@ -150,7 +150,7 @@ def _replica_body(rank, world, q):
     # the episode-parallel trainer: replicas seeded differently, synced
     # by initialize_training, then two updates on gathered episodes
     agent = _make_agent(seed=17 + rank)
-    trainer = EpisodeParallelTrainer([agent], update_seed=5)
+    trainer = EpisodeParallelTrainer([agent], update_seed=5, verify_every=1)
     trainer.initialize_training()
     init = rollout.replica_digest(agent).clone()
     rewards = []
@@ -182,6 +182,21 @@ def _replica_body(rank, world, q):
         Trainer([plain]).update_rl()
     dp = digests(plain)
     res["plain_diverges"] = not torch.equal(dp[0], dp[1])
+    res["plain_checksums_differ"] = not rollout.replicas_match(plain)
+    # initialize_training again after updates (the optimizers now
+    # hold state) broadcasts rank 0's replica, state included
+    trainer.initialize_training()
+    res["rebroadcast_match"] = rollout.replicas_match(agent)
+    # a kill switch raised on one rank only (a non-learning agent's task):
+    # update_rl stops every rank
+    frozen = _make_agent(seed=3)
+    frozen.train = False
+    frozen.task.kill_switch = rank == 1
+    kt = EpisodeParallelTrainer([frozen])
+    frozen.trajectory = _episode(rank, 0)
+    frozen.trajectory.killed = rank == 1
+    _, _, kstop = kt.update_rl()
+    res["kill_everywhere"] = bool(kstop)
     q.put((rank, res))
 
 
@@ -202,8 +217,9 @@ def test_episode_parallel_trainer_keeps_replicas_identical_gloo():
     for r in (0, 1):
         assert res[r]["identical"], res[r]
         assert res[r]["changed"] and res[r]["equals_single_process"], res[r]
-        assert res[r]["plain_diverges"], res[r]
+        assert res[r]["plain_diverges"] and res[r]["plain_checksums_differ"], res[r]
         assert not res[r]["stop0"] and not res[r]["stop1"]
+        assert res[r]["rebroadcast_match"] and res[r]["kill_everywhere"], res[r]
     assert res[0]["rewards"] == res[1]["rewards"]
 
 

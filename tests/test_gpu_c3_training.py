@@ -139,3 +139,54 @@ def test_replicated_update_on_graph_episode_matches_local_update():
     tw.network = twin
     tw.intrinsic_reward = None
     assert torch.equal(a, rollout.replica_digest(tw))
+
+
+def test_replicated_update_with_rnd_is_deterministic():
+    """a C5-shaped agent (ConcentrationField observable,
+    GradientSensing + RND intrinsic reward) and its deep copy each run
+    rollout.replicated_update on the same gathered episode for three
+    episodes -- the fused PPO gradient and Adam step, then the RND
+    predictor's update with its forked, re-seeded torch RNG (torch.randperm
+    on the device) and its capturable Adam -- and end bit-identical:
+    replica_digest covers the policy, the value head, both optimizers and the
+    RND target / predictor.  The replicas of an episode-parallel run on
+    different GPUs rely on exactly this (no gradient all-reduce; cross-device
+    identity itself is not measured here)."""
+    sys.path.insert(0, ROOT)
+    import copy
+
+    import bench
+    from swarmrl_amd import rollout
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    ns = argparse.Namespace(colloids=1024, envs_per_gpu=2, write_interval=1.0)
+    eng, ff, agent = bench.build_c5_workload(ns, 42, dev, rnd=True)
+    assert agent.intrinsic_reward is not None
+    agent.loss.n_epochs = 3
+    # the twin shares nothing a replicated update writes: its own network +
+    # optimizer, loss (and so PPO graph) and RND networks + optimizer
+    twin = copy.copy(agent)
+    twin.network = copy.deepcopy(agent.network)
+    twin.loss = copy.deepcopy(agent.loss)
+    twin.intrinsic_reward = copy.deepcopy(agent.intrinsic_reward)
+    eng.integrate(1, ff)
+    _, graph, _ = bench.capture_episode(eng, ff, agent, 5)
+    digests = []
+    for ep in range(3):
+        graph.replay()
+        episode = rollout.gather_episode(agent.trajectory)
+        rollout.replicated_update(agent, episode, seed=100 + ep)
+        rollout.replicated_update(twin, episode, seed=100 + ep)
+        torch.cuda.synchronize()
+        a, b = rollout.replica_digest(agent), rollout.replica_digest(twin)
+        assert torch.equal(a, b), ep
+        assert torch.equal(rollout.replica_checksum(agent), rollout.replica_checksum(twin))
+        digests.append(a)
+    # the updates did something: the replica changed from episode to episode
+    assert not torch.equal(digests[0], digests[-1])
+    # and a drifted bit is seen by the checksum the trainers compare
+    with torch.no_grad():
+        p = next(twin.intrinsic_reward.predictor_network.parameters())
+        p.view(-1)[0] = torch.nextafter(p.view(-1)[0], torch.tensor(1e9, device=p.device))
+    assert not torch.equal(rollout.replica_checksum(agent), rollout.replica_checksum(twin))

@@ -49,13 +49,11 @@ def _host(traj):
             for k in ("features", "actions", "rewards")}
 
 
-# build-mode switches read at engine creation: the default, the pair search
-# in the sort's workgroup with the cluster build beside the cone
-# (SWARMRL_AMD_SORT_PAIRS), and the pair search's block-local union-find
-# (SWARMRL_AMD_LOCAL_UF); every mode integrates the same bits
-@pytest.mark.parametrize("mode", [{}, {"SWARMRL_AMD_SORT_PAIRS": "1"},
-                                  {"SWARMRL_AMD_LOCAL_UF": "1"}],
-                         ids=["default", "sort_pairs", "local_uf"])
+# build-mode switches read at engine creation: the default and the pair
+# search's block-local union-find (SWARMRL_AMD_LOCAL_UF); every mode
+# integrates the same bits
+@pytest.mark.parametrize("mode", [{}, {"SWARMRL_AMD_LOCAL_UF": "1"}],
+                         ids=["default", "local_uf"])
 def test_headline_episode_graph_replays_match_oracle(tmp_path, monkeypatch, mode):
     for k, v in mode.items():
         monkeypatch.setenv(k, v)
