@@ -812,13 +812,27 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    import ctypes
+
+    wstats = (ctypes.c_uint64 * 4)()
+    eng._native.call("swarm_engine_build_stats", None, 1)  # (not under capture: counts windows)
     t0 = time.perf_counter()
     run(args.steps, True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    eng._native.call("swarm_engine_build_stats", wstats, 0)
     timing = _finish_timing(args, E, world, device, elapsed, gstats, None, None)
+    timing["windows"] = {
+        "checked": int(wstats[3]),
+        "pairs_from_candidate_lists": int(wstats[0]),
+        "pairs_after_waiting_for_the_sort": int(wstats[1]),
+        "exact_reruns": int(wstats[2]),
+        "note": "timed region, all envs of this rank: the slice's pair search filtered the "
+                "lists built during the previous run (hit) or waited for the fresh sort (miss); "
+                "re-runs: windows the exact check sent to the global path",
+    }
 
     eng.drain_trajectory(block=True)
     traj_written = eng.h5_time_steps_written + len(eng.traj_holder["Times"])
@@ -952,7 +966,7 @@ def _sub_line(res, workload, extra=None):
     out = {"workload": workload, "value": res["value"], "unit": "agent-steps/s",
            "envs_per_gpu": res["E"], "ms_per_step": res["ms_per_step"],
            "per_rank_value": res["per_rank"], "roofline": res["roofline"]}
-    for k in ("gather", "roofline_update", "slice_timeline_us"):
+    for k in ("gather", "roofline_update", "slice_timeline_us", "windows"):
         if res.get(k) is not None:
             out[k] = res[k]
     out.update(extra or {})
@@ -1095,6 +1109,8 @@ def main():
         line["gather"] = head["gather"]
     if head.get("slice_timeline_us"):
         line["slice_timeline_us"] = head["slice_timeline_us"]
+    if head.get("windows"):
+        line["windows"] = head["windows"]
     for k in LINES:
         if k in res:
             line[k] = res[k]

@@ -240,6 +240,15 @@ int swarm_engine_defer_build(swarm_engine_t *e, int32_t *deferred);
  * for engines without a noise table. */
 int swarm_engine_prebuild_noise(swarm_engine_t *e, void *stream, int32_t n_steps_hint);
 
+/* Counters of the cluster windows since the engine was created (or the
+ * last reset), summed over the envs: out4[0] windows whose pair search
+ * filtered the candidate lists prepared during the previous run, out4[1]
+ * windows whose pair search waited for the fresh build sort instead (the
+ * lists could not be used), out4[2] windows re-run exactly on the global
+ * path, out4[3] windows checked.  Measurement only (bench.py); reset != 0
+ * zeroes them after reading. */
+int swarm_engine_build_stats(swarm_engine_t *e, uint64_t *out4, int32_t reset);
+
 /* Diagnostics of the last integration window, per env (host arrays [E],
  * either may be NULL): fallback 0 = cluster path, 1 = flagged by the build
  * (cluster > 64 lanes or neighbour overflow), 2 = re-run on the global path;
@@ -359,6 +368,32 @@ int swarm_vision_cone(swarm_engine_t *e, const swarm_vision_params_t *vp,
 int swarm_vision_cone_persistent(swarm_engine_t *e, const swarm_vision_params_t *vp,
                                  const int32_t *agent_idx, int32_t n_agents,
                                  const float *radii, const int32_t *types, float *out);
+
+/* The observable and the rollout policy of an actor-critic agent in one
+ * launch: swarm_vision_cone_persistent's cones into `features` ([E][n_agents]
+ * [n_cones][n_types], n_cones * n_types <= 4) and, from them, the actor MLP +
+ * Gumbel sampling of swarm_policy_mlp_sample (features as its observation,
+ * d_in = n_cones * n_types, k <= 4 actions, hidden <= 256; weights read in
+ * place) into out_idx / out_logp / out_f / out_t[E * n_agents] (agent
+ * e * n_agents + a, the flattened observable's order; out_logits optional).
+ * Replaces SubdividedVisionCones.compute_observable + FlaxModel.compute_action
+ * + the sampling and action-table lookup of ActorCriticAgent.calc_action
+ * (subdivided_vision_cones.py:241-258, actor_critic.py:159-184,
+ * flax_network.py:153-195, gumbel_distribution.py:37-40).  agent_state:
+ * device call counters, one per agent (n_state >= E * n_agents; each call
+ * draws agent a's uniforms with counter agent_state[a] and advances it).
+ * Runs on the engine's stream; a deferred build rides along as in the two
+ * calls it replaces.  Sampling parity is statistical, as for
+ * swarm_policy_mlp_sample; the logits may differ from that kernel's in the
+ * last bits (the hidden units are summed in another split). */
+int swarm_engine_vision_policy(swarm_engine_t *e, const swarm_vision_params_t *vp,
+                               const int32_t *agent_idx, int32_t n_agents, const float *radii,
+                               const int32_t *types, float *features, const float *w1,
+                               const float *b1, int32_t hidden, const float *w2, const float *b2,
+                               int32_t k, uint64_t seed, uint64_t *agent_state, int32_t n_state,
+                               float explore_p, const float *f_table, const float *t_table,
+                               int64_t *out_idx, float *out_logp, float *out_f, float *out_t,
+                               float *out_logits);
 
 /* Distances to a source for the concentration-field observable and the
  * gradient-sensing task (concentration_field.py:84-108,

@@ -188,6 +188,13 @@ _SIGNATURES = {
         ctypes.c_int,
         [_P, ctypes.POINTER(SwarmVisionParams), _P, ctypes.c_int32, _P, _P, _P],
     ),
+    "swarm_engine_build_stats": (ctypes.c_int, [_P, _P, ctypes.c_int32]),
+    "swarm_engine_vision_policy": (
+        ctypes.c_int,
+        [_P, ctypes.POINTER(SwarmVisionParams), _P, ctypes.c_int32, _P, _P, _P, _P, _P,
+         ctypes.c_int32, _P, _P, ctypes.c_int32, ctypes.c_uint64, _P, ctypes.c_int32,
+         ctypes.c_float, _P, _P, _P, _P, _P, _P, _P],
+    ),
     "swarm_field_distance": (
         ctypes.c_int,
         [_P, _P, ctypes.c_int32, _P, _P, _P, _P, _P, _P, ctypes.c_int32, ctypes.c_int32],

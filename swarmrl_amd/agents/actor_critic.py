@@ -120,14 +120,26 @@ class ActorCriticAgent(Agent):
         return self._tables
 
     def calc_action(self, colloids):
-        state_description = self.observable.compute_observable(colloids)
+        joint = None
+        if is_view(colloids):
+            # the observable and the network's rollout policy in one launch
+            # when both allow it (SubdividedVisionCones + the stock MLP)
+            with_policy = getattr(self.observable, "compute_with_policy", None)
+            if with_policy is not None:
+                _, ftab, ttab, _ = self._action_tables(colloids.device)
+                joint = with_policy(colloids, self.network, ftab, ttab)
+        state_description = (joint[0] if joint is not None
+                             else self.observable.compute_observable(colloids))
         if is_view(colloids):
             E = colloids.n_envs
             A = int(state_description.shape[1])
             flat = state_description.reshape(E * A, -1)
             _, ftab, ttab, has_dir = self._action_tables(colloids.device)
             fused = getattr(self.network, "fused_sampling_ok", None)
-            if fused is not None and fused(flat):
+            if joint is not None:
+                idx, logp, f_act, t_act = joint[1:]
+                f_act, t_act = f_act.reshape(E, A), t_act.reshape(E, A)
+            elif fused is not None and fused(flat):
                 if getattr(self.network, "accepts_engine", False):
                     idx, logp, f_act, t_act = self.network.compute_action_fused(
                         flat, ftab, ttab, engine=colloids.engine._native)

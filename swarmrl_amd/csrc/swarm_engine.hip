@@ -506,6 +506,66 @@ __device__ __forceinline__ void vision_drain_group(const VisionLane& L,
   }
 }
 
+// What a vision group does with its agent's summed bins (every lane of the
+// group holds them): FeatureTail writes the observable row; PolicyTail
+// (swarm_vision_policy) also runs the actor MLP and the sampling on them.
+// pre() runs as soon as the agent's row is known (its loads overlap the
+// candidate scan), done() after the group's reduction.
+struct FeatureTail {
+  using Pre = int;
+  __device__ Pre pre(const VisionArgs&, int, int) const { return 0; }
+  template <int NB, int G>
+  __device__ void done(const VisionArgs& va, int e, int row, int sub, const int64_t (&acc)[NB],
+                       Pre) const {
+    if (sub != 0) return;
+    const int nb = va.vp.n_cones * va.vp.n_types;
+    float* o = va.out + ((size_t)e * va.n_agents + row) * nb;
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+      if (k < nb) o[k] = (float)acc[k] * 2.3283064365386963e-10f;
+  }
+};
+
+// The observable row, then the rollout policy of the same agent (flat agent
+// a = e * n_agents + row, as swarm_policy_mlp_sample sees the flattened
+// observable): the actor MLP over the group's G lanes, weights read in place
+// (mlp_group_logits_direct), and lane 0 samples with the agent's own call
+// counter state[a] (one group handles an agent per launch, so it reads and
+// advances it alone: no block barrier, no atomic).
+template <int D, int K>
+struct PolicyTail {
+  swarm::MlpArgs m;
+  using Pre = unsigned long long;
+  __device__ Pre pre(const VisionArgs& va, int e, int row) const {
+    return m.state[(size_t)e * va.n_agents + row];
+  }
+  template <int NB, int G>
+  __device__ void done(const VisionArgs& va, int e, int row, int sub, const int64_t (&acc)[NB],
+                       Pre ctr) const {
+    static_assert(NB <= D, "the fused policy takes the bins as its features");
+    const int nb = va.vp.n_cones * va.vp.n_types;
+    const int a = e * va.n_agents + row;
+    float x[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) x[k] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+      if (k < nb) x[k] = (float)acc[k] * 2.3283064365386963e-10f;
+    if (sub == 0) {
+      float* o = va.out + (size_t)a * nb;
+#pragma unroll
+      for (int k = 0; k < D; ++k)
+        if (k < nb) o[k] = x[k];
+    }
+    float lg[K];
+    swarm::mlp_group_logits_direct<G, D, K>(m, x, sub, lg);
+    if (sub == 0) {
+      swarm::policy_emit<K>(m, a, lg, ctr);
+      m.state[a] = ctr + 1ull;
+    }
+  }
+};
+
 // kAll: vision_range >= half the box (the reference has no range limit,
 // subdivided_vision_cones.py:116-121): every record of the env is a
 // candidate, tested on its unwrapped (int64) separation.
@@ -514,16 +574,15 @@ __device__ __forceinline__ void vision_drain_group(const VisionLane& L,
 // Body for block vb (k_vision, or a workgroup of k_vision_pairs /
 // k_vision_cbuild); hits: the block's [kVisionHits][BS] LDS hit lists
 // (blockDim BS).
-template <int NB, int G, bool kAll = false, int BS = 256>
+template <int NB, int G, bool kAll = false, int BS = 256, class Tail = FeatureTail>
 __device__ __forceinline__ void vision_body(const DevState& st, const Derived* __restrict__ d,
                                             const VisionArgs& va, int vb, int xcd_bpe,
-                                            uint32_t (*hits)[BS]) {
+                                            uint32_t (*hits)[BS], const Tail& tail = Tail{}) {
   const swarm_vision_params_t& vp = va.vp;
   const int lx = va.lx, ly = va.ly;
   const int32_t* __restrict__ start = va.start;
   const VisionSorted& vs = va.vs;
-  const int n_agents = va.n_agents, n_envs = va.n_envs;
-  float* __restrict__ out = va.out;
+  const int n_envs = va.n_envs;
   const int N = st.n;
   const int sub = threadIdx.x & (G - 1);
   int e, ps;
@@ -558,7 +617,6 @@ __device__ __forceinline__ void vision_body(const DevState& st, const Derived* _
   L.sx0 = d->sx[0];
   L.sx1 = d->sx[1];
   L.R = vp.vision_range;
-  const int nb = vp.n_cones * vp.n_types;
   int64_t acc[NB];
 #pragma unroll
   for (int k = 0; k < NB; ++k) acc[k] = 0;
@@ -595,6 +653,7 @@ __device__ __forceinline__ void vision_body(const DevState& st, const Derived* _
     pre[r + 1] = pre[r] + (je - jb);
   }
   if (row < 0) return;
+  const typename Tail::Pre tail_pre = tail.pre(va, e, row);
   const int total = pre[6];
   // kVF candidates per lane in flight per round
   constexpr int kVF = 4;
@@ -641,11 +700,7 @@ __device__ __forceinline__ void vision_body(const DevState& st, const Derived* _
       acc[b] += (int64_t)(((uint64_t)(uint32_t)hi << 32) | lo);
     }
   }
-  if (sub != 0) return;
-  float* o = out + ((size_t)e * n_agents + row) * nb;
-#pragma unroll
-  for (int k = 0; k < NB; ++k)
-    if (k < nb) o[k] = (float)acc[k] * 2.3283064365386963e-10f;
+  tail.template done<NB, G>(va, e, row, sub, acc, tail_pre);
 }
 
 template <int NB, int G, bool kAll = false>
@@ -653,6 +708,18 @@ __global__ __launch_bounds__(256) void k_vision(DevState st, const Derived* __re
                                                 VisionArgs va, int xcd_bpe) {
   __shared__ uint32_t hits[kVisionHits][256];
   vision_body<NB, G, kAll>(st, d, va, blockIdx.x, xcd_bpe, hits);
+}
+
+// The vision cone and the rollout policy of its agents in one launch
+// (swarm_engine_vision_policy): each agent's group computes its bins, writes
+// the observable row and runs the MLP + sampling on them (PolicyTail).
+template <int NB, int G, int D, int K>
+__global__ __launch_bounds__(256) void k_vision_policy(DevState st, const Derived* __restrict__ d,
+                                                       VisionArgs va, swarm::MlpArgs m,
+                                                       int xcd_bpe) {
+  __shared__ uint32_t hits[kVisionHits][256];
+  const PolicyTail<D, K> tail{m};
+  vision_body<NB, G, false, 256, PolicyTail<D, K>>(st, d, va, blockIdx.x, xcd_bpe, hits, tail);
 }
 
 // ------------------------------------------- build stages riding along
@@ -675,17 +742,42 @@ __device__ __forceinline__ int fused_block(int nfirst) {
   return (int)blockIdx.x;
 }
 
+// The l1_pairs pair-search role of the slice's first launch: n_fb blocks
+// per env of blockDim threads after the sort and grid workgroups
+// (swarm::pair_filter_body; ctl: the device control block, whose window
+// counter names this window's build sort).  smem: the launch's dynamic LDS,
+// at least l1_role_lds_bytes() (the fallback cell search's tables).
+constexpr size_t l1_role_lds_bytes() {
+  return (kMaxSpecies * kMaxSpecies + 2 * 1024) * sizeof(int32_t);
+}
+__device__ __forceinline__ void l1_pairs_role(const Derived* __restrict__ d, const DevState& st,
+                                              const Scratch& sc, int lxb, int lyb, int fb, int n_fb,
+                                              const uint64_t* ctl, unsigned char* smem) {
+  float* nb2 = reinterpret_cast<float*>(smem);
+  int32_t* uf = reinterpret_cast<int32_t*>(smem) + kMaxSpecies * kMaxSpecies;
+  swarm::role_begin(sc, swarm::kRolePairs);
+  swarm::pair_filter_body(d, st, sc, lxb, lyb, fb % n_fb, fb / n_fb, ctl[swarm::kCtlWin] + 1ull,
+                          nb2, uf);
+  swarm::role_end(sc, swarm::kRolePairs);
+}
+
 template <int CH>
 __global__ __launch_bounds__(1024) void k_vgrid_sort(DevState st, VisionArgs va, Scratch sc,
-                                                     int lxb, int lyb) {
+                                                     int lxb, int lyb, const Derived* __restrict__ d,
+                                                     int n_fb, const uint64_t* __restrict__ ctl) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int b = fused_block(va.n_envs);
-  const int role = b < va.n_envs ? swarm::kRoleSort : swarm::kRoleVgrid;
+  const int E = va.n_envs;
+  if (b >= 2 * E) {  // l1_pairs: the pair search beside the sort (n_fb > 0)
+    l1_pairs_role(d, st, sc, lxb, lyb, b - 2 * E, n_fb, ctl, smem);
+    return;
+  }
+  const int role = b < E ? swarm::kRoleSort : swarm::kRoleVgrid;
   swarm::role_begin(sc, role);
-  if (b < va.n_envs)
-    swarm::build_sort_body<CH>(st, sc, lxb, lyb, b, smem);
+  if (b < E)
+    swarm::build_sort_body<CH>(st, sc, lxb, lyb, b, smem, n_fb > 0 ? ctl[swarm::kCtlWin] + 1ull : 0ull);
   else
-    vision_grid_body(st, va, b - va.n_envs, smem);
+    vision_grid_body(st, va, b - E, smem);
   swarm::role_end(sc, role);
 }
 
@@ -705,6 +797,52 @@ __global__ __launch_bounds__(256) void k_vision_pairs(DevState st, const Derived
     swarm::build_pairs_body<kLocal>(d, st, sc, lxb, lyb, b % pair_bx, b / pair_bx, nb2, uf);
   } else {
     vision_body<NB, G, false>(st, d, va, b - n_pblocks, 0, hits);
+  }
+  swarm::role_end(sc, role);
+}
+
+// The same with the fused rollout policy on the cone side (PolicyTail): the
+// pair blocks first, then the cone + MLP + sampling blocks.
+template <int NB, int G, bool kLocal, int D, int K>
+__global__ __launch_bounds__(256) void k_vision_policy_pairs(DevState st,
+                                                             const Derived* __restrict__ d,
+                                                             VisionArgs va, swarm::MlpArgs m,
+                                                             int n_pblocks, Scratch sc, int lxb,
+                                                             int lyb, int pair_bx) {
+  __shared__ uint32_t hits[kVisionHits][256];
+  __shared__ float nb2[swarm::kMaxSpecies * swarm::kMaxSpecies];
+  __shared__ int32_t uf[2 * 256];
+  const int b = fused_block(n_pblocks);
+  const int role = b < n_pblocks ? swarm::kRolePairs : swarm::kRoleCone;
+  swarm::role_begin(sc, role);
+  if (b < n_pblocks) {
+    swarm::build_pairs_body<kLocal>(d, st, sc, lxb, lyb, b % pair_bx, b / pair_bx, nb2, uf);
+  } else {
+    const PolicyTail<D, K> tail{m};
+    vision_body<NB, G, false, 256, PolicyTail<D, K>>(st, d, va, b - n_pblocks, 0, hits, tail);
+  }
+  swarm::role_end(sc, role);
+}
+
+// l1_pairs slices: the pair list is ready when the cone runs, so the
+// cluster build rides beside the cone + MLP + sampling (1024-thread blocks:
+// the build's workgroup per env first, then the cone's, whose hit lists
+// share the build's dynamic LDS).
+template <int NB, int G, int D, int K>
+__global__ __launch_bounds__(1024) void k_vision_policy_cbuild(DevState st,
+                                                               const Derived* __restrict__ d,
+                                                               VisionArgs va, swarm::MlpArgs m,
+                                                               Scratch sc) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int b = fused_block(va.n_envs);
+  const int role = b < va.n_envs ? swarm::kRoleCbuild : swarm::kRoleCone;
+  swarm::role_begin(sc, role);
+  if (b < va.n_envs) {
+    swarm::cluster_build_env<false, true, false>(st, sc, b, smem, sc.gnpairs[b]);
+  } else {
+    auto* hits = reinterpret_cast<uint32_t(*)[1024]>(smem);
+    const PolicyTail<D, K> tail{m};
+    vision_body<NB, G, false, 1024, PolicyTail<D, K>>(st, d, va, b - va.n_envs, 0, hits, tail);
   }
   swarm::role_end(sc, role);
 }
@@ -929,22 +1067,28 @@ __global__ __launch_bounds__(256) void k_field(DevState st, FieldArgs f) {
 // the field's agents, the NEXT observable's vision grid (from the positions
 // the reward sees, which the observable will see too) and build stage 1,
 // so the observable launch only runs the cone (beside stage 2).
+// l1_pairs (n_fb > 0): the next window's pair search rides here too,
+// n_fb blocks per env after the grid workgroups (l1_pairs_role).
 template <int CH>
 __global__ __launch_bounds__(1024) void k_field_vgrid_sort(FieldArgs f, int n_fblocks, DevState st,
                                                            VisionArgs va, Scratch sc, int lxb,
-                                                           int lyb) {
+                                                           int lyb, const Derived* __restrict__ d,
+                                                           int n_fb, const uint64_t* __restrict__ ctl) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int b = fused_block(2 * va.n_envs);
-  const int role = b < va.n_envs       ? swarm::kRoleSort
-                   : b < 2 * va.n_envs ? swarm::kRoleVgrid
-                                       : swarm::kRoleField;
+  const int E = va.n_envs, npb = n_fb * E;
+  if (b >= 2 * E && b < 2 * E + npb) {
+    l1_pairs_role(d, st, sc, lxb, lyb, b - 2 * E, n_fb, ctl, smem);
+    return;
+  }
+  const int role = b < E ? swarm::kRoleSort : b < 2 * E ? swarm::kRoleVgrid : swarm::kRoleField;
   swarm::role_begin(sc, role);
-  if (b < va.n_envs)
-    swarm::build_sort_body<CH>(st, sc, lxb, lyb, b, smem);
-  else if (b < 2 * va.n_envs)
-    vision_grid_body(st, va, b - va.n_envs, smem);
+  if (b < E)
+    swarm::build_sort_body<CH>(st, sc, lxb, lyb, b, smem, n_fb > 0 ? ctl[swarm::kCtlWin] + 1ull : 0ull);
+  else if (b < 2 * E)
+    vision_grid_body(st, va, b - E, smem);
   else
-    field_body(st, f, (b - 2 * va.n_envs) * blockDim.x + threadIdx.x);
+    field_body(st, f, (b - 2 * E - npb) * blockDim.x + threadIdx.x);
   swarm::role_end(sc, role);
 }
 
@@ -1385,12 +1529,14 @@ int launch_run(swarm_engine* e, int n_steps, unsigned long long* tstamp = nullpt
   if (e->wide_run) {
     // dynamic LDS beyond half a CU's keeps one block (run_wpb run waves) per CU
     const int R = e->run_wpb;
-    const dim3 grid((unsigned)(e->noise_blocks + (waves + R - 1) / R));
+    // l1_pairs: the next window's candidate lists built beside the run
+    const int ncb = e->sc.l1_pairs ? e->n_envs * ((e->n + 1023) / 1024) : 0;
+    const dim3 grid((unsigned)(e->noise_blocks + ncb + (waves + R - 1) / R));
     const size_t lds = 96 * 1024;  // one block per CU
 #define SWARM_WIDE(MULTI, WALLS)                                                             \
   hipLaunchKernelGGL((swarm::k_cluster_run_wide<MULTI, WALLS>), grid, dim3(1024), lds, e->stream, \
                      e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise,      \
-                     e->noise_blocks, R, tstamp)
+                     e->noise_blocks, R, ncb, e->lxb, e->lyb, tstamp)
     if (walls) {
       if (multi)
         SWARM_WIDE(true, true);
@@ -1946,6 +2092,35 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
       const long est = (long)M / 46 + 1;
       e->run_wpb = est + e->noise_blocks <= 224 ? 1 : (est / 2 + e->noise_blocks <= 224 ? 2 : 4);
     }
+    // l1_pairs: the ride-along build's pair search moves into the slice's
+    // first launch as a filter of candidate lists prepared during the last
+    // run (periodic 2-D, the plain pair search, a build grid of at least 5
+    // cells a side for the 5 x 5 candidate stencil)
+    e->sc.l1_pairs = e->wide_run && e->cluster_path && !e->nlist_path && !e->env_build &&
+                             !e->big_build && !three_d && params->periodic && !e->sc.local_uf &&
+                             (1 << e->lxb) >= 5 && (1 << e->lyb) >= 5
+                         ? 1
+                         : 0;
+    if (e->sc.l1_pairs) {
+      // widening of the candidate radius: up to 1.5 um of motion per window
+      // (the bench's swimmers move ~0.3 um; > 1.5 um is a > 6 sigma event),
+      // at most half a cell side (the 5 x 5 stencil) and at least skin / 2
+      // (k_check sees every particle that moved more: the movers)
+      const double side = std::min(params->box[0] / (1 << e->lxb), params->box[1] / (1 << e->lyb));
+      const double cd = std::max(0.5 * skin_um(), std::min(1.5, 0.5 * side));
+      e->derived.cand_disp = (float)cd;
+      for (int a = 0; a < params->n_species; ++a)
+        for (int b = 0; b < params->n_species; ++b) {
+          const double r = params->radius[a] + params->radius[b] + skin_um() + 2.0 * cd;
+          e->derived.nbc2[a * kMaxSpecies + b] = (float)(r * r);
+        }
+      rc = rc ? rc : dev_alloc(e, &e->sc.cand, (size_t)swarm::kCandMax * M);
+      rc = rc ? rc : dev_alloc(e, &e->sc.ncand, M);
+    }
+    rc = rc ? rc : dev_alloc(e, &e->sc.cand_ok, (size_t)n_envs);
+    rc = rc ? rc : dev_alloc(e, &e->sc.cand_ovf, (size_t)n_envs);
+    rc = rc ? rc : dev_alloc(e, &e->sc.sort_done, (size_t)n_envs);
+    rc = rc ? rc : dev_alloc(e, &e->sc.stats, 4);
 
   }
   set_lds_attributes();
@@ -2413,6 +2588,21 @@ int swarm_engine_prebuild_noise(swarm_engine_t* e, void* stream, int32_t n_steps
   return SWARM_OK;
 }
 
+int swarm_engine_build_stats(swarm_engine_t* e, uint64_t* out4, int32_t reset) {
+  if (!e) return fail(SWARM_EINVAL, "null engine");
+  if (!e->sc.stats) {  // (not a cluster-window engine)
+    if (out4) std::memset(out4, 0, 4 * sizeof(uint64_t));
+    return SWARM_OK;
+  }
+  if (out4) {
+    HIP_TRY(hipMemcpyAsync(out4, e->sc.stats, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                           e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+  }
+  if (reset) HIP_TRY(hipMemsetAsync(e->sc.stats, 0, 4 * sizeof(uint64_t), e->stream));
+  return SWARM_OK;
+}
+
 int swarm_engine_window_stats(swarm_engine_t* e, int32_t* fallback, int32_t* waves) {
   if (!e) return fail(SWARM_EINVAL, "null engine");
   const size_t E = (size_t)e->n_envs;
@@ -2612,9 +2802,19 @@ bool same_grid_args(const VisionArgs& a, const VisionArgs& b) {
          a.n_agents == b.n_agents && a.n_envs == b.n_envs;
 }
 
+// LDS of a launch carrying the l1_pairs pair search (its fallback tables)
+// beside workgroups that need `other` bytes.
+size_t l1_launch_lds(const swarm_engine* e, size_t other) {
+  return e->sc.l1_pairs ? std::max(other, l1_role_lds_bytes()) : other;
+}
+int l1_blocks_per_env(const swarm_engine* e) { return e->sc.l1_pairs ? (e->n + 1023) / 1024 : 0; }
+
+// pol (swarm_engine_vision_policy): the rollout policy of the cone's agents
+// runs in the cone's launch (PolicyTail); the caller checked its limits
+// (n_cones * n_types <= 4 = d_in, k <= 4, hidden <= 256).
 int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const int32_t* agent_idx,
                      int32_t n_agents, const float* radii, const int32_t* types, float* out,
-                     bool persistent) {
+                     bool persistent, const swarm::MlpArgs* pol = nullptr) {
   if (!e || !vp || !agent_idx || !radii || !types || !out) return fail(SWARM_EINVAL, "null argument");
   if (e->params.n_dims != 2) return fail(SWARM_EINVAL, "the vision-cone kernel is 2-D only");
   if (vp->n_cones < 1 || vp->n_cones > SWARM_MAX_CONES || vp->n_types < 1 ||
@@ -2647,32 +2847,63 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
   if (glds > kMaxLds) return fail(SWARM_ECAPACITY, "observable cell grid too large");
   // the grid of the current positions for these arguments, built by the
   // reward launch (launch_field) while nothing moved the colloids since
-  const bool have_grid = !all && e->vgrid_ready && e->ride_stage == 2 &&
+  const bool l1 = e->sc.l1_pairs != 0;
+  const bool have_grid = !all && e->vgrid_ready && e->ride_stage == (l1 ? 3 : 2) &&
                          same_grid_args(e->spec_va, va);
   e->vgrid_ready = false;
   e->spec_ok = persistent && !all;
   if (e->spec_ok) e->spec_va = va;
-  // a deferred build rides along in the grid and cone launches (stages 1, 2)
+  // a deferred build rides along in the grid and cone launches (stages 1, 2;
+  // with l1_pairs the pair search rides in the grid's launch and the
+  // cluster build, stage 3, in the fused policy's or the policy's launch)
   // when their fused variants apply; else its pending stages launch first
   const bool ride_ok = !all && nb <= 4 && G == 16;
-  if (e->ride_stage > 0 && !(ride_ok && e->ride_stage <= 2)) {
+  if (e->ride_stage > 0 && !(ride_ok && (e->ride_stage <= 2 || (l1 && e->ride_stage == 3)))) {
     rc = flush_ride_along(e);
     if (rc) return rc;
   }
-  if (e->ride_stage == 1) {  // grid | sort, then cone | pairs
+  if (e->ride_stage == 1) {  // grid | sort (| pairs), then cone | pairs or cluster build
     const size_t slds = sort_lds_bytes(e);
-    const dim3 grid((unsigned)(2 * e->n_envs));
+    const int nfb = l1_blocks_per_env(e);
+    const dim3 grid((unsigned)((2 + nfb) * e->n_envs));
+    const size_t lds = l1_launch_lds(e, std::max(glds, slds));
     if (e->n > 4096)
-      hipLaunchKernelGGL((k_vgrid_sort<16>), grid, dim3(1024), std::max(glds, slds), e->stream,
-                         e->st, va, e->sc, e->lxb, e->lyb);
+      hipLaunchKernelGGL((k_vgrid_sort<16>), grid, dim3(1024), lds, e->stream, e->st, va, e->sc,
+                         e->lxb, e->lyb, e->d_derived, nfb, e->d_step);
     else
-      hipLaunchKernelGGL((k_vgrid_sort<4>), grid, dim3(1024), std::max(glds, slds), e->stream,
-                         e->st, va, e->sc, e->lxb, e->lyb);
+      hipLaunchKernelGGL((k_vgrid_sort<4>), grid, dim3(1024), lds, e->stream, e->st, va, e->sc,
+                         e->lxb, e->lyb, e->d_derived, nfb, e->d_step);
     HIP_TRY(hipGetLastError());
-    e->ride_stage = 2;
+    e->ride_stage = l1 ? 3 : 2;
   } else if (!have_grid) {
     hipLaunchKernelGGL(k_vision_grid, dim3(e->n_envs), dim3(1024), glds, e->stream, e->st, va);
     HIP_TRY(hipGetLastError());
+  }
+  if (pol && ride_ok && e->ride_stage == 3) {  // cluster build | cone + policy (l1_pairs)
+    const int ncb = (int)((total * 16 + 1023) / 1024);
+    const size_t lds = std::max(build_lds_bytes(e->n, e->sc.pair_cap),
+                                (size_t)kVisionHits * 1024 * sizeof(uint32_t));
+    hipLaunchKernelGGL((k_vision_policy_cbuild<4, 16, 4, 4>), dim3((unsigned)(e->n_envs + ncb)),
+                       dim3(1024), lds, e->stream, e->st, e->d_derived, va, *pol, e->sc);
+    HIP_TRY(hipGetLastError());
+    e->ride_stage = 0;
+    e->prebuilt = true;
+    return SWARM_OK;
+  }
+  if (pol && e->ride_stage == 2) {  // pairs | cone + policy
+    const int nvb = (int)((total * 16 + 255) / 256);
+    const int pbx = (e->n + 255) / 256;
+    const int npb = pbx * e->n_envs;
+    const dim3 grid((unsigned)(nvb + npb));
+    if (e->sc.local_uf)
+      hipLaunchKernelGGL((k_vision_policy_pairs<4, 16, true, 4, 4>), grid, dim3(256), 0,
+                         e->stream, e->st, e->d_derived, va, *pol, npb, e->sc, e->lxb, e->lyb, pbx);
+    else
+      hipLaunchKernelGGL((k_vision_policy_pairs<4, 16, false, 4, 4>), grid, dim3(256), 0,
+                         e->stream, e->st, e->d_derived, va, *pol, npb, e->sc, e->lxb, e->lyb, pbx);
+    HIP_TRY(hipGetLastError());
+    e->ride_stage = 3;
+    return SWARM_OK;
   }
   if (e->ride_stage == 2) {  // pairs | cone
     const int nvb = (int)((total * 16 + 255) / 256);
@@ -2690,6 +2921,7 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
     return SWARM_OK;
   }
   if (all) {
+    if (pol) return fail(SWARM_ECAPACITY, "the fused policy needs vision_range < half the box");
     const dim3 agrid((unsigned)((total * 16 + 255) / 256)), ablock(256);
 #define SWARM_VALL(NBV)                                                                          \
   hipLaunchKernelGGL((k_vision<NBV, 16, true>), agrid, ablock, 0, e->stream, e->st, e->d_derived, \
@@ -2713,6 +2945,16 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
   const bool xcd = E >= 8 && (E % 8 == 0 || E >= 64);
   const dim3 grid((unsigned)(xcd ? 8L * ((E + 7) / 8) * bpe : (total * G + 255) / 256)),
       block(256);
+  if (pol) {  // cone + policy, no build stage riding along
+    if (G == kVisionGWide)
+      hipLaunchKernelGGL((k_vision_policy<4, kVisionGWide, 4, 4>), grid, block, 0, e->stream,
+                         e->st, e->d_derived, va, *pol, xcd ? bpe : 0);
+    else
+      hipLaunchKernelGGL((k_vision_policy<4, 16, 4, 4>), grid, block, 0, e->stream, e->st,
+                         e->d_derived, va, *pol, xcd ? bpe : 0);
+    HIP_TRY(hipGetLastError());
+    return SWARM_OK;
+  }
 #define SWARM_VISION(NBV, GV)                                                                  \
   hipLaunchKernelGGL((k_vision<NBV, GV>), grid, block, 0, e->stream, e->st, e->d_derived, va, \
                      xcd ? bpe : 0)
@@ -2748,6 +2990,33 @@ int swarm_vision_cone_persistent(swarm_engine_t* e, const swarm_vision_params_t*
   return vision_cone_impl(e, vp, agent_idx, n_agents, radii, types, out, true);
 }
 
+int swarm_engine_vision_policy(swarm_engine_t* e, const swarm_vision_params_t* vp,
+                               const int32_t* agent_idx, int32_t n_agents, const float* radii,
+                               const int32_t* types, float* features, const float* w1,
+                               const float* b1, int32_t hidden, const float* w2, const float* b2,
+                               int32_t k, uint64_t seed, uint64_t* agent_state, int32_t n_state,
+                               float explore_p, const float* f_table, const float* t_table,
+                               int64_t* out_idx, float* out_logp, float* out_f, float* out_t,
+                               float* out_logits) {
+  if (!e || !vp || !w1 || !b1 || !w2 || !b2 || !agent_state || !f_table || !t_table || !out_idx ||
+      !out_logp || !out_f || !out_t)
+    return fail(SWARM_EINVAL, "null argument");
+  const int nb = vp->n_cones * vp->n_types;
+  if (nb < 1 || nb > 4) return fail(SWARM_ECAPACITY, "the fused policy takes <= 4 cone bins");
+  if (hidden < 1 || hidden > swarm::kMlpMaxHidden)
+    return fail(SWARM_ECAPACITY, "1 <= hidden <= 256");
+  if (k < 1 || k > 4) return fail(SWARM_ECAPACITY, "the fused policy takes 1 <= k <= 4 actions");
+  if (!(explore_p >= 0.0f && explore_p <= 1.0f))
+    return fail(SWARM_EINVAL, "exploration probability must be in [0, 1]");
+  if (n_agents <= 0) return SWARM_OK;
+  const long n = (long)e->n_envs * n_agents;
+  if (n_state < n) return fail(SWARM_EINVAL, "agent_state needs one counter per agent");
+  const swarm::MlpArgs m{features, (int)n, nb, w1, b1, hidden, w2, b2, k, (uint32_t)seed,
+                         (uint32_t)(seed >> 32), reinterpret_cast<unsigned long long*>(agent_state),
+                         explore_p, f_table, t_table, out_idx, out_logp, out_f, out_t, out_logits};
+  return vision_cone_impl(e, vp, agent_idx, n_agents, radii, types, features, true, &m);
+}
+
 namespace {
 // k_field, or with a pending deferred build and a persistent vision cone the
 // fused k_field_vgrid_sort (stage 1 and the next observable's grid ride
@@ -2759,15 +3028,17 @@ int launch_field(swarm_engine* e, const FieldArgs& f) {
     const size_t glds = vision_grid_lds_bytes(va.lx, va.ly, e->n, va.staged != 0);
     const size_t slds = sort_lds_bytes(e);
     const int nfb = (total + 1023) / 1024;
-    const dim3 grid((unsigned)(nfb + 2 * e->n_envs));
+    const int npf = l1_blocks_per_env(e);  // l1_pairs: the pair search rides here too
+    const dim3 grid((unsigned)(nfb + (2 + npf) * e->n_envs));
+    const size_t lds = l1_launch_lds(e, std::max(glds, slds));
     if (e->n > 4096)
-      hipLaunchKernelGGL((k_field_vgrid_sort<16>), grid, dim3(1024), std::max(glds, slds),
-                         e->stream, f, nfb, e->st, va, e->sc, e->lxb, e->lyb);
+      hipLaunchKernelGGL((k_field_vgrid_sort<16>), grid, dim3(1024), lds, e->stream, f, nfb,
+                         e->st, va, e->sc, e->lxb, e->lyb, e->d_derived, npf, e->d_step);
     else
-      hipLaunchKernelGGL((k_field_vgrid_sort<4>), grid, dim3(1024), std::max(glds, slds),
-                         e->stream, f, nfb, e->st, va, e->sc, e->lxb, e->lyb);
+      hipLaunchKernelGGL((k_field_vgrid_sort<4>), grid, dim3(1024), lds, e->stream, f, nfb,
+                         e->st, va, e->sc, e->lxb, e->lyb, e->d_derived, npf, e->d_step);
     HIP_TRY(hipGetLastError());
-    e->ride_stage = 2;
+    e->ride_stage = e->sc.l1_pairs ? 3 : 2;
     e->vgrid_ready = true;
     return SWARM_OK;
   }

@@ -51,6 +51,10 @@ constexpr int kBigMax = 1024;
 constexpr int kBigPairs = 4096;
 constexpr int kBigMark = -0x40000000;  // cbase of a big cluster's root
 constexpr int kMaxMovers = 1024;       // listed movers per env (more: exact re-run)
+// Candidate lists of the next window's pair search (latency-bound ride-along
+// builds, see cand_build_body): per particle up to kCandMax partners j > i
+// within r_i + r_j + skin + 2 cand_disp of the window-start positions.
+constexpr int kCandMax = 24;
 
 // Wave slots per env: every cluster packs into one wave, worst case 2 N
 // slots plus per-size-class rounding.  One-pass packing (latency-bound
@@ -71,6 +75,11 @@ struct Derived {
   float cut2[kMaxSpecies * kMaxSpecies];
   float sig6[kMaxSpecies * kMaxSpecies];
   float nb2[kMaxSpecies * kMaxSpecies];  // (r_i + r_j + skin)^2: cluster links
+  // (r_i + r_j + skin + 2 cand_disp)^2: candidate partners of the next
+  // window's pair search (cand_build_body), valid while no particle moves
+  // more than cand_disp in the window
+  float nbc2[kMaxSpecies * kMaxSpecies];
+  float cand_disp;
   float eps24;
   float skin;
   float rc_max_f;
@@ -231,6 +240,24 @@ struct Scratch {
                           // pass, and writes its output coalesced (0: scattered stores)
   int32_t S;          // slots per env
   int32_t wmax;       // S / 64
+  // The next window's pair search as a filter of candidate lists (l1_pairs:
+  // latency-bound periodic 2-D ride-along builds): the run kernel's extra
+  // workgroups list every particle's candidates from the window's sort
+  // (cand_build_body); k_check marks them usable for the next window
+  // (cand_ok) when no particle moved more than cand_disp and nothing
+  // overflowed or re-ran; the next slice's first launch then filters them at
+  // the new positions beside the fresh sort (pair_filter_body), which
+  // otherwise waits for that sort (sort_done) and searches its cells.
+  int32_t l1_pairs;
+  int32_t* cand;      // [kCandMax][M] partner j | species << 24 (j > i)
+  int32_t* ncand;     // [M] candidates of a particle
+  int32_t* cand_ok;   // [E] the lists hold every pair of the next window
+  int32_t* cand_ovf;  // [E] a list overflowed (set by the builder, reset by k_check)
+  uint64_t* sort_done;  // [E] window counter + 1 of the last finished build sort
+  // [4] window statistics summed over the envs (swarm_engine_build_stats):
+  // pair searches that filtered candidate lists, that waited for the fresh
+  // sort, exact re-runs, windows checked
+  unsigned long long* stats;
   uint64_t* phase;    // [32] build phase stamps (SWARM_PHASE_TIMING builds only)
   // profiling only (else null): [kRoles][kStampSub][2] earliest start /
   // latest end (device wall clock) of each workgroup role of the launches of
@@ -1103,10 +1130,23 @@ __host__ __device__ inline size_t build_lds_words(int n, int pair_cap) {
 // The body runs in the workgroup of env e (k_build_sort, or a workgroup of a
 // fused launch that carries the build along: k_vgrid_sort).
 // CH: particles per thread kept in registers across the scan (4, or 16
-// above 4096).
+// above 4096).  publish > 0 (l1_pairs launches, whose pair search runs
+// beside this sort): the pair counters were reset by the last k_check, and
+// the finished sort is announced in sort_done[e] = publish (release, agent
+// scope) for pair blocks that have to wait for it.
+__device__ __forceinline__ void publish_sort(const Scratch& sc, int e, uint64_t publish) {
+  // (usable candidate lists: no pair block waits for this sort)
+  if (publish == 0 || sc.cand_ok[e]) return;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&sc.sort_done[e], publish, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int CH>
 __device__ __forceinline__ void build_sort_body(const DevState& st, const Scratch& sc, int lx,
-                                                int ly, int e, unsigned char* smem) {
+                                                int ly, int e, unsigned char* smem,
+                                                uint64_t publish = 0) {
   const int T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int ncell = 1 << (lx + ly);
@@ -1135,8 +1175,10 @@ __device__ __forceinline__ void build_sort_body(const DevState& st, const Scratc
   }
   for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
   if (tid == 0) {
-    sc.gnpairs[e] = 0;
-    sc.gnx[e] = 0;
+    if (publish == 0) {  // (else k_check reset them: the pair search runs already)
+      sc.gnpairs[e] = 0;
+      sc.gnx[e] = 0;
+    }
     sc.fallback[e] = 0;  // the neighbour-list build sets it on overflow
   }
   __syncthreads();
@@ -1205,6 +1247,7 @@ __device__ __forceinline__ void build_sort_body(const DevState& st, const Scratc
     }
     for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
     SWARM_STAMP(5);
+    publish_sort(sc, e, publish);
     return;
   }
 #pragma unroll
@@ -1226,6 +1269,7 @@ __device__ __forceinline__ void build_sort_body(const DevState& st, const Scratc
   // last, so the stores drain in the shadow of the scatter
   for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
   SWARM_STAMP(5);
+  publish_sort(sc, e, publish);
 }
 
 // Chip-wide 2-D build sort of large envs (N > 4096 outside the ride-along
@@ -1549,6 +1593,196 @@ __global__ __launch_bounds__(256) void k_build_pairs(const Derived* __restrict__
   __shared__ float nb2[kMaxSpecies * kMaxSpecies];
   __shared__ int32_t uf[2 * 256];
   build_pairs_body<kLocal>(d, st, sc, lx, ly, blockIdx.x, blockIdx.y, nb2, uf);
+}
+
+// ----------------------------------------- candidate lists (l1_pairs)
+// The next window's pair search, prepared a window ahead.  A pair within
+// r_i + r_j + skin at the next window's start positions P' was within
+// r_i + r_j + skin + D_i + D_j at this window's start P (D: a particle's
+// displacement over the window), so while every D <= cand_disp the pairs of
+// P' are among the candidates listed here from P with the radius widened by
+// 2 cand_disp (nbc2).  k_check knows every particle that moved >= skin / 2
+// (the movers; cand_disp >= skin / 2) and marks the lists usable (cand_ok).
+// Built by the wide run kernel's extra workgroups during the run (from the
+// window's cell-sorted snapshot, which nothing rewrites before the next
+// window's build), so none of this is on the slice's critical path.
+
+// Sorted entry t of env e: its partners j > i among the (2 kc + 1)^2 cells
+// around its cell (kc = 2 covers the widened radius: cand_disp <= half a cell
+// side; the host requires >= 5 cells a side, so no cell is visited twice).
+__device__ __forceinline__ void cand_build_body(const Derived* __restrict__ d, const DevState& st,
+                                                const Scratch& sc, int lx, int ly, int e, int t) {
+  constexpr int kc = 2;
+  const int N = st.n;
+  if (t >= N) return;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int ncx = 1 << lx, ncy = 1 << ly;
+  const int32_t* cs = sc.bcstart + (size_t)e * ((size_t)ncx * ncy + 1);
+  const int pk = sc.bsid[base + t];
+  const int i = pk & 0xffffff;
+  const uint32_t qx = sc.bsq[base + t], qy = sc.bsq[M + base + t];
+  const int cx = (int)(qx >> (32 - lx)), cy = (int)(qy >> (32 - ly));
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const float* lim2 = d->nbc2 + (pk >> 24) * kMaxSpecies;
+  // the stencil rows as up to two contiguous sorted ranges each (a periodic
+  // row wraps at most once), flattened into one candidate index
+  int rb[2 * (2 * kc + 1)], rl[2 * (2 * kc + 1)], nr = 0;
+#pragma unroll
+  for (int oy = -kc; oy <= kc; ++oy) {
+    const int row = ((cy + oy + ncy) & (ncy - 1)) << lx;
+    int x0 = cx - kc, x1 = cx + kc;
+    if (x0 < 0) {
+      rb[nr] = cs[row | (ncx + x0)];
+      rl[nr] = cs[(row | (ncx - 1)) + 1] - rb[nr];
+      ++nr;
+      x0 = 0;
+    } else if (x1 > ncx - 1) {
+      rb[nr] = cs[row];
+      rl[nr] = cs[(row | (x1 - ncx)) + 1] - rb[nr];
+      ++nr;
+      x1 = ncx - 1;
+    }
+    rb[nr] = cs[row | x0];
+    rl[nr] = cs[(row | x1) + 1] - rb[nr];
+    ++nr;
+  }
+  const size_t gi = base + i;
+  int n = 0, r = 0, rem = nr > 0 ? rl[0] : 0, jj = nr > 0 ? rb[0] : 0;
+  while (true) {
+    // four candidates in flight per round
+    int pj[4];
+    uint32_t xj[4], yj[4];
+    int got = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      while (rem == 0 && r + 1 < nr) {
+        ++r;
+        rem = rl[r];
+        jj = rb[r];
+      }
+      pj[u] = -1;
+      if (rem > 0) {
+        pj[u] = sc.bsid[base + jj];
+        xj[u] = sc.bsq[base + jj];
+        yj[u] = sc.bsq[M + base + jj];
+        ++jj;
+        --rem;
+        ++got;
+      }
+    }
+    if (got == 0) break;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (pj[u] < 0) continue;
+      const int j = pj[u] & 0xffffff;
+      if (j <= i) continue;
+      const float rx = (float)(int32_t)(xj[u] - qx) * sx0;
+      const float ry = (float)(int32_t)(yj[u] - qy) * sx1;
+      if (rx * rx + ry * ry < lim2[pj[u] >> 24]) {
+        if (n < kCandMax) sc.cand[(size_t)n * M + gi] = (int32_t)((uint32_t)j | ((uint32_t)pj[u] & 0xff000000u));
+        ++n;
+      }
+    }
+  }
+  sc.ncand[gi] = min(n, kCandMax);
+  if (n > kCandMax) sc.cand_ovf[e] = 1;
+}
+
+// The pair search of the slice's first launch (l1_pairs): block bx of env e,
+// one thread per particle i (blockDim threads a block).  With usable lists
+// (cand_ok) every listed j is tested at the current positions -- the same
+// test and pair word as build_pairs_body, so the same pairs -- and kept in
+// registers, one atomic per wave reserves the output.  Otherwise the block
+// waits for this launch's build sort (sort_done == win1, published with a
+// release by its workgroup, which has the lowest block index of the launch
+// and so is dispatched before any waiting block) and searches its cells.
+__device__ __forceinline__ void pair_filter_body(const Derived* __restrict__ d, const DevState& st,
+                                                 const Scratch& sc, int lx, int ly, int bx, int e,
+                                                 uint64_t win1, float* nb2, int32_t* uf) {
+  const bool ok = sc.cand_ok[e] != 0;  // block-uniform
+  if (bx == 0 && threadIdx.x == 0) atomicAdd(&sc.stats[ok ? 0 : 1], 1ull);
+  if (!ok) {
+    if (threadIdx.x == 0)
+      while (__hip_atomic_load(&sc.sort_done[e], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != win1)
+        __builtin_amdgcn_s_sleep(8);
+    __syncthreads();
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    build_pairs_body<false>(d, st, sc, lx, ly, bx, e, nb2, uf);
+    return;
+  }
+  constexpr int kKeep = 8;
+  const int N = st.n, T = blockDim.x;
+  const int i = bx * T + (int)threadIdx.x;
+  const bool valid = i < N;
+  const size_t M = (size_t)st.m, base = (size_t)e * N, gi = base + (valid ? i : 0);
+  const int nc = valid ? sc.ncand[gi] : 0;
+  const uint32_t qx = st.q[gi], qy = st.q[M + gi];
+  // the first eight list entries load with the count (one memory latency,
+  // not two; entries past the count are never used)
+  int c0[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) c0[u] = sc.cand[(size_t)u * M + gi];
+  const bool multi = sc.multi_species != 0;
+  const int si = multi && valid ? (int)st.species[i] : 0;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const float* nb2_row = d->nb2 + si * kMaxSpecies;
+  int found = 0;
+  uint32_t keep[kKeep];
+#pragma unroll
+  for (int v = 0; v < kKeep; ++v) keep[v] = 0u;
+  auto test = [&](int c, uint32_t xj, uint32_t yj) {
+    const float rx = (float)(int32_t)(xj - qx) * sx0;
+    const float ry = (float)(int32_t)(yj - qy) * sx1;
+    return rx * rx + ry * ry < nb2_row[multi ? ((uint32_t)c >> 24) : 0];
+  };
+  for (int k0 = 0; k0 < nc; k0 += 8) {  // eight candidates in flight per round
+    int cj[8];
+    uint32_t xj[8], yj[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      cj[u] = k0 + u < nc ? (k0 == 0 ? c0[u] : sc.cand[(size_t)(k0 + u) * M + gi]) : -1;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const size_t gj = base + (cj[u] < 0 ? 0 : (cj[u] & 0xffffff));
+      xj[u] = st.q[gj];
+      yj[u] = st.q[M + gj];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (cj[u] >= 0 && test(cj[u], xj[u], yj[u])) {
+        const uint32_t kv = (uint32_t)(cj[u] & 0xffffff);
+#pragma unroll
+        for (int v = 0; v < kKeep; ++v) keep[v] = found == v ? kv : keep[v];
+        ++found;
+      }
+    }
+  }
+  const int lane = threadIdx.x & 63;
+  const bool dense = __any(found > kKeep);
+  int v = wave_incl_scan(found);
+  int wbase = 0;
+  if (lane == 63) wbase = atomicAdd(&sc.gnpairs[e], v);
+  wbase = __builtin_amdgcn_readlane(wbase, 63);
+  const int my_off = wbase + v - found;
+  uint32_t* out = sc.gplist + (size_t)e * sc.pair_cap;
+  const int cap = sc.pair_cap;
+  if (!dense) {
+#pragma unroll
+    for (int u = 0; u < kKeep; ++u) {
+      const int k = my_off + u;
+      if (u < found && k < cap) out[k] = (uint32_t)i | (keep[u] << 16);
+    }
+    return;
+  }
+  int w = 0;  // a lane kept only kKeep: the wave rescans its lists in order
+  for (int k = 0; k < nc; ++k) {
+    const int c = sc.cand[(size_t)k * M + gi];
+    const size_t gj = base + (c & 0xffffff);
+    if (test(c, st.q[gj], st.q[M + gj])) {
+      if (my_off + w < cap) out[my_off + w] = (uint32_t)i | ((uint32_t)(c & 0xffffff) << 16);
+      ++w;
+    }
+  }
 }
 
 // The packing class v whose free-lane range holds singleton rank r < nfree:
@@ -2841,6 +3075,7 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
                                                            int n_steps, uint64_t* __restrict__ ctl,
                                                            float* __restrict__ tables,
                                                            int n_noise_blocks, int run_wpb,
+                                                           int n_cand_blocks, int lxb, int lyb,
                                                            unsigned long long* __restrict__ tstamp) {
   __shared__ PairTables pt;
   __shared__ uint2 lpos[4][64];
@@ -2869,8 +3104,14 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
     stamp_end(tstamp);
     return;
   }
+  if (b < n_noise_blocks + n_cand_blocks) {  // the next window's candidate lists
+    const int cb = b - n_noise_blocks, bpe = n_cand_blocks / n_envs;
+    cand_build_body(d, st, sc, lxb, lyb, cb / bpe, (cb % bpe) * (int)blockDim.x + tid);
+    stamp_end(tstamp);
+    return;
+  }
   const int lane = tid & 63, wv = tid >> 6;
-  const int gw0 = (b - n_noise_blocks) * run_wpb;
+  const int gw0 = (b - n_noise_blocks - n_cand_blocks) * run_wpb;
   const bool table_ok = ctl[kCtlTStep + par] == step0 && (uint64_t)n_steps <= ctl[kCtlTLen + par];
   const float* table = table_ok ? tables + par * noise_table_words(M) : nullptr;
   if (wv >= run_wpb) return;
@@ -3226,6 +3467,7 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
   const int bign = nlist ? 0 : sc.big_n[e];
   const int nm_run = sc.nmov[e];
   const int mv_run = tid < kMaxMovers ? sc.movers[(size_t)e * kMaxMovers + tid] : 0;
+  const int ovf = sc.l1_pairs ? sc.cand_ovf[e] : 0;
   for (int k = tid; k < kMaxSpecies * kMaxSpecies; k += T) {
     pt.cut2[k] = d->cut2[k];
     pt.sig6[k] = d->sig6[k];
@@ -3236,10 +3478,12 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
   const bool flagged_build = fb == 1;
   if (!flagged_build && bign > 0)
     run_big_clusters(d, st, sc, e, n_steps, step0, cnt, &pt, par);
+  int nm = 0;  // movers of the window (listed in LDS below)
+  bool kc_dmax = false;  // misc[7] holds the movers' largest displacement
   if (!flagged_build) {
     // the movers (displacement >= skin / 2) were listed by the run kernel
     // and the big-cluster run: no scan over all colloids here
-    int nm = nm_run;
+    nm = nm_run;
     if (bign > 0) {
       // the big-cluster run of this workgroup appended entries a moment
       // ago: agent-scope loads
@@ -3323,6 +3567,7 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
           atomicMax(&misc[7], __float_as_int(sc.disp[base + movers[k]]));  // >= 0: int order
         __syncthreads();
         const float dmax = __int_as_float(misc[7]);
+        kc_dmax = true;
         const float lim_max = d->rc_max_f + 2.0f * dmax + 1e-3f;
         const float side = fminf(sx0 * (float)(1u << (32 - cell_lx)),
                                  sx1 * (float)(1u << (32 - cell_ly)));
@@ -3388,6 +3633,33 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
     __syncthreads();
   }
   const bool rerun = flagged_build || misc[1] != 0;
+  if (sc.l1_pairs) {
+    // the candidate lists the run's extra workgroups built from this
+    // window's start positions hold every pair of the next window's start
+    // when the window ran on its decomposition (no re-run), no list
+    // overflowed, and no particle moved more than cand_disp -- only movers
+    // (>= skin / 2 <= cand_disp) can have: their largest displacement is
+    // misc[7] when the cell test ran (kc_dmax), else it is taken here
+    bool far = false;
+    if (!rerun && nm > 0 && !kc_dmax) {
+      if (tid == 0) misc[8] = 0;
+      __syncthreads();
+      for (int k = tid; k < nm; k += T) far |= !(sc.disp[base + movers[k]] <= d->cand_disp);
+      if (far) misc[8] = 1;
+      __syncthreads();
+      far = misc[8] != 0;
+    } else if (!rerun && nm > 0) {
+      far = !(__int_as_float(misc[7]) <= d->cand_disp);
+    }
+    if (tid == 0) {
+      sc.cand_ok[e] = !rerun && !far && ovf == 0 ? 1 : 0;
+      sc.cand_ovf[e] = 0;
+    }
+  }
+  if (tid == 0) {
+    if (rerun) atomicAdd(&sc.stats[2], 1ull);
+    atomicAdd(&sc.stats[3], 1ull);
+  }
   if (rerun) {
     // a flagged env was skipped by k_cluster_run: its state is the window
     // start already; otherwise restore the snapshot k_cluster_run took
@@ -3410,7 +3682,13 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
     save_forces_env(st, e, par ^ 1);  // the re-run replaced the run kernel's final state
   }
   __syncthreads();  // every read of nmov above is done
-  if (tid == 0) sc.nmov[e] = 0;
+  if (tid == 0) {
+    sc.nmov[e] = 0;
+    // the next build's pair counters (an l1_pairs pair search starts before
+    // its sort, so the sort cannot reset them)
+    sc.gnpairs[e] = 0;
+    sc.gnx[e] = 0;
+  }
   advance_counter(step_ctr, arrive, step0, n_steps);
   role_end(sc, kRoleCheck);
 }

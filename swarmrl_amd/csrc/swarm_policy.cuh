@@ -206,28 +206,18 @@ struct MlpArgs {
   float* out_logits;
 };
 
-// Body for block vb of the policy (k_policy_mlp_sample, or a workgroup of a
-// fused launch: k_policy_cbuild); sw: the block's dynamic LDS.
-template <int G, int D, int K>
-__device__ __forceinline__ void policy_body(const MlpArgs& m, int vb, float* sw) {
-  const float* __restrict__ obs = m.obs;
-  const int n = m.n, d_in = m.d_in, hidden = m.hidden, k = m.k;
+// The actor's weights into the block's LDS rows (MlpRow<D, K>, hidden rows,
+// then the K padded output biases at sw + hidden * kStride), four entries
+// per thread loaded together.  Every thread of the block calls it; the
+// caller's __syncthreads publishes the rows.
+template <int D, int K>
+__device__ __forceinline__ void stage_mlp_rows(const MlpArgs& m, float* sw) {
   const float* __restrict__ w1 = m.w1;
   const float* __restrict__ b1 = m.b1;
   const float* __restrict__ w2 = m.w2;
   const float* __restrict__ b2 = m.b2;
-  const uint32_t key0 = m.key0, key1 = m.key1;
-  unsigned long long* __restrict__ state = m.state;
-  const float explore_p = m.explore_p;
-  const float* __restrict__ ftab = m.ftab;
-  const float* __restrict__ ttab = m.ttab;
-  int64_t* __restrict__ out_idx = m.out_idx;
-  float* __restrict__ out_logp = m.out_logp;
-  float* __restrict__ out_f = m.out_f;
-  float* __restrict__ out_t = m.out_t;
-  float* __restrict__ out_logits = m.out_logits;
+  const int d_in = m.d_in, hidden = m.hidden, k = m.k;
   constexpr int R = MlpRow<D, K>::kStride;
-  // the weights into LDS rows, four entries per thread loaded together
   for (int t0 = threadIdx.x; t0 < hidden * R; t0 += 4 * (int)blockDim.x) {
     float v[4];
 #pragma unroll
@@ -252,18 +242,20 @@ __device__ __forceinline__ void policy_body(const MlpArgs& m, int vb, float* sw)
   }
   float* sb2 = sw + hidden * R;
   if (threadIdx.x < K) sb2[threadIdx.x] = (int)threadIdx.x < k ? b2[threadIdx.x] : 0.0f;
-  const int gt = vb * blockDim.x + threadIdx.x;
-  const int a = gt / G, sub = gt & (G - 1);
-  const bool valid = a < n;
-  const unsigned long long ctr = valid ? state[a >> 6] : 0ull;
-  float x[D];
-#pragma unroll
-  for (int c = 0; c < D; ++c) x[c] = (valid && c < d_in) ? obs[(size_t)a * d_in + c] : 0.0f;
-  __syncthreads();
+}
+
+// The actor logits of one agent whose G consecutive lanes (lane `sub` of the
+// group, G dividing 64) all hold its padded features x: lane sub takes the
+// hidden units j = sub, sub + G, ... of the staged rows, and the partial
+// logits are summed with xor-shuffles (every lane ends with all K).
+template <int G, int D, int K>
+__device__ __forceinline__ void mlp_group_logits(const MlpArgs& m, const float* sw,
+                                                 const float (&x)[D], int sub, float (&lg)[K]) {
+  constexpr int R = MlpRow<D, K>::kStride;
   float acc[K];
 #pragma unroll
   for (int q = 0; q < K; ++q) acc[q] = 0.0f;
-  for (int j = sub; j < hidden; j += G) {
+  for (int j = sub; j < m.hidden; j += G) {
     const float4* r = reinterpret_cast<const float4*>(sw + j * R);
     float w[R];
 #pragma unroll
@@ -286,22 +278,94 @@ __device__ __forceinline__ void policy_body(const MlpArgs& m, int vb, float* sw)
 #pragma unroll
     for (int q = 0; q < K; ++q) acc[q] += __shfl_xor(acc[q], o, 64);
   }
-  float lg[K];
+  const float* sb2 = sw + m.hidden * R;
 #pragma unroll
   for (int q = 0; q < K; ++q) lg[q] = acc[q] + sb2[q];
-  if (valid && sub == 0) {
-    const Sampled s = sample_logits_reg<K>(lg, k, a, ctr, key0, key1, explore_p);
-    out_idx[a] = s.idx;
-    out_logp[a] = s.logp;
-    out_f[a] = ftab[s.idx];
-    out_t[a] = ttab[s.idx];
-    if (out_logits) {
+}
+
+// mlp_group_logits with the weights read straight from the torch module's
+// buffers instead of staged LDS rows (the fused observable + policy kernels,
+// whose blocks cannot wait on a barrier before their groups finish): a lane's
+// units come U at a time, every weight load of a round issued together (one
+// memory latency; the rows are shared by all groups, so L1 / L2 hits).  The
+// same operation sequence per unit and the same unit order as
+// mlp_group_logits.
+template <int G, int D, int K>
+__device__ __forceinline__ void mlp_group_logits_direct(const MlpArgs& m, const float (&x)[D],
+                                                        int sub, float (&lg)[K]) {
+  constexpr int U = 8;
+  const int hidden = m.hidden, d_in = m.d_in, k = m.k;
+  float acc[K];
 #pragma unroll
-      for (int q = 0; q < K; ++q)
-        if (q < k) out_logits[(size_t)a * k + q] = lg[q];
+  for (int q = 0; q < K; ++q) acc[q] = 0.0f;
+  for (int j0 = sub; j0 < hidden; j0 += U * G) {
+    float w[U][D], bb[U], wo[U][K];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + u * G;
+      const bool ok = j < hidden;
+#pragma unroll
+      for (int c = 0; c < D; ++c) w[u][c] = ok && c < d_in ? m.w1[(size_t)j * d_in + c] : 0.0f;
+      bb[u] = ok ? m.b1[j] : 0.0f;
+#pragma unroll
+      for (int q = 0; q < K; ++q) wo[u][q] = ok && q < k ? m.w2[(size_t)q * hidden + j] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float h = 0.0f;
+#pragma unroll
+      for (int c = 0; c < D; ++c) h = fmaf(w[u][c], x[c], h);
+      h = fmaxf(h + bb[u], 0.0f);  // bias + ReLU
+      if (j0 + u * G < hidden) {
+#pragma unroll
+        for (int q = 0; q < K; ++q) acc[q] = fmaf(h, wo[u][q], acc[q]);
+      }
     }
   }
-  advance_group_counter(state, a, n, sub == 0, ctr);
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) {
+#pragma unroll
+    for (int q = 0; q < K; ++q) acc[q] += __shfl_xor(acc[q], o, 64);
+  }
+#pragma unroll
+  for (int q = 0; q < K; ++q) lg[q] = acc[q] + (q < k ? m.b2[q] : 0.0f);
+}
+
+// Sampling and outputs of agent a from its logits (lane 0 of its group):
+// index, log-prob, action-table values and (optionally) the logits.
+template <int K>
+__device__ __forceinline__ void policy_emit(const MlpArgs& m, int a, const float (&lg)[K],
+                                            unsigned long long ctr) {
+  const Sampled s = sample_logits_reg<K>(lg, m.k, a, ctr, m.key0, m.key1, m.explore_p);
+  m.out_idx[a] = s.idx;
+  m.out_logp[a] = s.logp;
+  m.out_f[a] = m.ftab[s.idx];
+  m.out_t[a] = m.ttab[s.idx];
+  if (m.out_logits) {
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+      if (q < m.k) m.out_logits[(size_t)a * m.k + q] = lg[q];
+  }
+}
+
+// Body for block vb of the policy (k_policy_mlp_sample, or a workgroup of a
+// fused launch: k_policy_cbuild); sw: the block's dynamic LDS.
+template <int G, int D, int K>
+__device__ __forceinline__ void policy_body(const MlpArgs& m, int vb, float* sw) {
+  stage_mlp_rows<D, K>(m, sw);
+  const int n = m.n, d_in = m.d_in;
+  const int gt = vb * blockDim.x + threadIdx.x;
+  const int a = gt / G, sub = gt & (G - 1);
+  const bool valid = a < n;
+  const unsigned long long ctr = valid ? m.state[a >> 6] : 0ull;
+  float x[D];
+#pragma unroll
+  for (int c = 0; c < D; ++c) x[c] = (valid && c < d_in) ? m.obs[(size_t)a * d_in + c] : 0.0f;
+  __syncthreads();
+  float lg[K];
+  mlp_group_logits<G, D, K>(m, sw, x, sub, lg);
+  if (valid && sub == 0) policy_emit<K>(m, a, lg, ctr);
+  advance_group_counter(m.state, a, n, sub == 0, ctr);
 }
 
 template <int G, int D, int K>

@@ -79,6 +79,37 @@ def vision_cone(native, n_envs: int, agent_idx: torch.Tensor, radii: torch.Tenso
     return out
 
 
+def vision_policy(native, n_envs: int, agent_idx: torch.Tensor, radii: torch.Tensor,
+                  types: torch.Tensor, vp: _capi.SwarmVisionParams, w1, b1, w2, b2, seed: int,
+                  agent_state: torch.Tensor, explore_p: float, f_table: torch.Tensor,
+                  t_table: torch.Tensor):
+    """The persistent vision cone and the actor's rollout policy on it in one
+    launch (swarm_engine_vision_policy): returns (features [E, A, n_cones,
+    n_types], idx int64 [E * A], log_prob [E * A], f_swim [E * A], torque_z
+    [E * A]).  agent_state: int64 device counters, one per agent."""
+    A = int(agent_idx.numel())
+    dev = agent_idx.device
+    n = n_envs * A
+    feats = torch.empty((n_envs, A, vp.n_cones, vp.n_types), dtype=torch.float32, device=dev)
+    idx = torch.empty(n, dtype=torch.int64, device=dev)
+    logp = torch.empty(n, dtype=torch.float32, device=dev)
+    f = torch.empty(n, dtype=torch.float32, device=dev)
+    t = torch.empty(n, dtype=torch.float32, device=dev)
+    if A == 0:
+        return feats, idx, logp, f, t
+    hidden, k = int(w1.shape[0]), int(w2.shape[0])
+    native.bind_stream()
+    native.call(
+        "swarm_engine_vision_policy", ctypes.byref(vp), agent_idx.data_ptr(), A,
+        radii.data_ptr(), types.data_ptr(), feats.data_ptr(), w1.data_ptr(), b1.data_ptr(),
+        hidden, w2.data_ptr(), b2.data_ptr(), k, ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
+        agent_state.data_ptr(), int(agent_state.numel()), ctypes.c_float(explore_p),
+        f_table.data_ptr(), t_table.data_ptr(), idx.data_ptr(), logp.data_ptr(), f.data_ptr(),
+        t.data_ptr(), None,
+    )
+    return feats, idx, logp, f, t
+
+
 def field_distance(native, n_envs: int, agent_idx: torch.Tensor, source, box_scale,
                    hist_q: torch.Tensor, hist_img: torch.Tensor, update: bool,
                    init_only: bool = False):

@@ -90,6 +90,7 @@ class TorchModel:
         # torch's generator, call counter in device memory
         self._fused_seed = int(torch.randint(0, 2**62, (1,)).item())
         self._fused_state = None
+        self._agent_state = None  # per-agent call counters (swarm_engine_vision_policy)
 
     def reinitialize_network(self):
         for m in self.model.modules():
@@ -156,6 +157,29 @@ class TorchModel:
             logits, _ = self.model(obs)
         return ops.sample_actions(logits.float(), self._fused_seed, self._fused_state, p,
                                   f_table, t_table)
+
+    def fused_policy_args(self, n: int, d_in: int, k: int, device):
+        """What an observable needs to run this network's rollout policy in
+        its own launch (swarm_engine_vision_policy): (w1, b1, w2, b2, seed,
+        per-agent counters for n agents, exploration probability), or None
+        when the one-kernel policy does not apply (another network, sampling
+        strategy or exploration policy, or sizes beyond the fused kernel's:
+        d_in <= 4, k <= 4)."""
+        if not (type(self.sampling_strategy) is GumbelDistribution
+                and type(self.exploration_policy) is RandomExploration):
+            return None
+        if d_in > 4 or k > 4:
+            return None
+        layers = self._mlp_layers(d_in, k)
+        if layers is None:
+            return None
+        st = self._agent_state
+        if st is None or st.device != device or st.numel() < n:
+            grown = torch.zeros(max(n, 1), dtype=torch.int64, device=device)
+            if st is not None and st.device == device:
+                grown[: st.numel()] = st
+            self._agent_state = st = grown
+        return (*layers, self._fused_seed, st, float(self.exploration_policy.probability))
 
     def _mlp_layers(self, d_in: int, k: int):
         """The actor weights when the one-kernel policy applies (fp32 device

@@ -75,6 +75,33 @@ class SubdividedVisionCones(Observable):
         )
         return [out[k] for k in range(len(indices))]
 
+    def compute_with_policy(self, view, network, f_table, t_table):
+        """The observable of a SwarmView and the rollout policy of `network`
+        on it in one launch (ops.vision_policy): (features [E, A, n_cones,
+        n_types], idx, log_prob, f_swim, torque_z [E * A]), or None when the
+        network's policy cannot run there (TorchModel.fused_policy_args) or
+        the range reaches half the box (the all-records cone)."""
+        if not hasattr(network, "fused_policy_args"):
+            return None
+        if not 2.0 * float(self.vision_range) < float(np.min(view.engine._box[:2])):
+            return None
+        if self.detected_types is None:
+            self._detect_all_things_to_see(view.engine._types_host.tolist())
+        nb = int(self.n_cones) * len(self.detected_types)
+        agents = view.indices_of_type(self.particle_type)
+        args = network.fused_policy_args(view.n_envs * int(agents.numel()), nb,
+                                         int(f_table.numel()), view.device)
+        if args is None:
+            return None
+        if self._radii_device is None:
+            import torch
+
+            self._radii_device = torch.as_tensor(
+                np.asarray(self.radii, dtype=np.float32), device=view.device
+            )
+        return ops.vision_policy(view.engine._native, view.n_envs, agents, self._radii_device,
+                                 view.types, self._params(), *args, f_table, t_table)
+
     def compute_observable(self, colloids):
         """
         List input: list of (n_cones, n_types) arrays, one per agent (as the

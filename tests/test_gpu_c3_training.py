@@ -164,6 +164,11 @@ def test_replicated_update_with_rnd_is_deterministic():
     eng, ff, agent = bench.build_c5_workload(ns, 42, dev, rnd=True)
     assert agent.intrinsic_reward is not None
     agent.loss.n_epochs = 3
+    # the reference's RND recipe (100 epochs of batch 8) is 128 k predictor
+    # steps per update at this size; a few large batches exercise the same
+    # code paths (randperm, minibatches, capturable Adam)
+    agent.intrinsic_reward.n_epochs = 2
+    agent.intrinsic_reward.batch_size = 2048
     # the twin shares nothing a replicated update writes: its own network +
     # optimizer, loss (and so PPO graph) and RND networks + optimizer
     twin = copy.copy(agent)

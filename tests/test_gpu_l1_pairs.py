@@ -1,0 +1,126 @@
+"""
+The slice schedule of latency-bound engines with the pair search in the
+slice's first launch (l1_pairs, DESIGN.md section 6 "Pair search a window
+ahead") and the rollout policy fused into the vision-cone launch
+(swarm_engine_vision_policy), against the oracle on the headline's workload
+(bench.build_workload: 4096 colloids, SubdividedVisionCones, actor-critic MLP,
+GradientSensing).
+
+Two speeds of the Translate action: the bench's (every particle moves well
+under the candidate lists' 1.5 um per window, so the first launch filters the
+lists built during the last run) and ten times it (translating agents move
+~2 um per window: the lists are unusable, the pair blocks wait for the
+launch's fresh sort and search its cells).  Either way the decomposition may
+not change a bit of the result: features, rewards, the final state and the
+trajectory ring must equal the oracle's replay of the recorded actions
+(espresso.py:1251-1308, as tests/test_gpu_headline.py).
+"""
+
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _reward(p, st, agents, src, box, hist):
+    dc, dp = oracle.field_distance(p, st, agents, src, box, hist, update=True)
+    f32 = np.float32
+    v = (f32(10.0) * ((f32(1.0) - dc) - (f32(1.0) - dp))).astype(np.float32)
+    return np.where(v < 0, f32(0), v).astype(np.float32)
+
+
+def _host(traj):
+    return {k: [torch.as_tensor(x).detach().cpu().numpy().copy() for x in getattr(traj, k)]
+            for k in ("features", "actions", "rewards", "log_probs")}
+
+
+@pytest.mark.parametrize("force", [10.0, 100.0], ids=["lists", "fallback"])
+def test_l1_pairs_and_fused_policy_match_oracle(force):
+    sys.path.insert(0, ROOT)
+    import bench
+    from swarmrl_amd.actions import Action
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    N, T = 4096, 6
+    ns = argparse.Namespace(colloids=N, envs_per_gpu=1, write_interval=1.0)
+    eng, ff, agent = bench.build_workload(ns, 42, dev)
+    agent.actions["Translate"] = Action(force=force)
+    agent._tables = None
+    pos0 = np.stack(eng._pos[0])
+    dir0 = np.stack(eng._dir[0])
+    eng.integrate(1, ff)
+    _, episode_graph, warm = bench.capture_episode(eng, ff, agent, T)
+    slices = [_host(warm)]
+    episode_graph.replay()
+    torch.cuda.synchronize()
+    slices.append(_host(agent.trajectory))
+    eng.drain_trajectory(block=True)
+    got = eng.get_raw_state()
+    del episode_graph
+    stats = (ctypes.c_uint64 * 4)()
+    eng._native.call("swarm_engine_build_stats", stats, 0)
+    filtered, waited, reruns, windows = list(stats)
+
+    L = float(eng._box[0])
+    box = np.array([L, L, L])
+    src = np.array([L / 2, L / 2, 0.0])
+    p = oracle.make_params(eng._box, eng._time_step, eng._kT(),
+                           eng.params.WCA_epsilon.m_as("sim_energy"), 42, [eng._species_keys[0]])
+    agents = np.arange(N)
+    radii = np.ones(N, np.float32)
+    types = np.zeros(N, np.int32)
+    ftab = np.array([0.0, force, 0.0, 0.0], np.float32)
+    ttab = np.array([10.0, 0.0, -10.0, 0.0], np.float32)
+    sp = np.zeros(N, np.uint8)
+    st = oracle.state_from_positions(pos0, dir0, eng._box)
+    hist = oracle.history_from_state(st, agents)
+    st, _ = oracle.sd_run(p, st, sp, 1000)
+    prev = {"f": np.zeros(N, np.float32), "t": np.zeros(N, np.float32), "ang": st["ang"].copy()}
+    step = 0
+    moved = []
+    for block in slices:
+        for s in range(len(block["actions"])):
+            obs = oracle.vision_cone(p, st, agents, radii, types, 10.0, np.pi / 2, 3, [0],
+                                     cells=True)
+            assert np.array_equal(block["features"][s].reshape(obs.shape), obs), (step, "cone")
+            # the fused policy's log-probabilities are those of the network
+            # on these features (fp32 tolerance: another summation split)
+            with torch.no_grad():
+                x = torch.as_tensor(obs.reshape(N, 3), device=dev)
+                w1, b1, w2, b2 = agent.network.model.rollout_layers()
+                lg = torch.relu(x @ w1.T + b1) @ w2.T + b2
+                ref = torch.log(torch.softmax(lg, -1) + 1e-8)
+            idx = block["actions"][s].reshape(-1)
+            want = ref.gather(1, torch.as_tensor(idx, device=dev).view(-1, 1)).view(-1).cpu().numpy()
+            np.testing.assert_allclose(block["log_probs"][s].reshape(-1), want, rtol=0, atol=2e-5)
+            f, t = ftab[idx], ttab[idx]
+            q0 = st["q"].copy()
+            st, _, _ = oracle.bd_run(p, st, sp, f, t, 100, step0=100 * step, prev=prev)
+            d = (st["q"][:2].astype(np.int64) - q0[:2].astype(np.int64))
+            d = (d + 2**31) % 2**32 - 2**31
+            moved.append(float(np.max(np.hypot(d[0], d[1]) * L / 2.0**32)))
+            prev = {"f": f, "t": t, "ang": st["ang"].copy()}
+            rew = _reward(p, st, agents, src, box, hist)
+            assert np.array_equal(block["rewards"][s].reshape(-1), rew), (step, "reward")
+            step += 1
+    assert step == 3 + T
+    for k in ("q", "img", "ang"):
+        assert np.array_equal(got[k], st[k]), k
+    # the two parametrisations do exercise the two pair searches: every
+    # window after the first ride-along one filtered the lists, or none did
+    assert windows == step and filtered + waited > 0, list(stats)
+    if force == 10.0:
+        assert max(moved) < 1.5 and waited == 0 and filtered > 0, (moved, list(stats))
+    else:
+        assert max(moved) > 1.5 and waited > 0, (moved, list(stats))

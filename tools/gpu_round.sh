@@ -5,11 +5,14 @@
 # Outputs: gpurun_out/TAG/{gpu_tests.txt,bench.json,bench.err}
 tag=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 2
-out=gpurun_out/$tag
+out=$PWD/gpurun_out/$tag
 mkdir -p "$out"
+# WORKDIR: run the checks of another copy of the tree (e.g. a baseline
+# build unpacked under the repo); outputs still go to gpurun_out/TAG
+[ -n "$WORKDIR" ] && { cd "$WORKDIR" || exit 2; }
 sel=("$@")
 [ ${#sel[@]} -eq 0 ] && sel=(tests)
-timeout -k 10 900 python -u -m pytest "${sel[@]}" -m gpu -q --timeout 300 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest "${sel[@]}" -m gpu -v --timeout 150 --timeout-method thread \
   > "$out/gpu_tests.txt" 2>&1
 rc=$?
 echo "tests rc=$rc" >> "$out/gpu_tests.txt"
