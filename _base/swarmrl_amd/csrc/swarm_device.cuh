@@ -1,0 +1,369 @@
+// swarm_device.cuh -- device arithmetic shared by the engine kernels.
+//
+// Every function here fixes its fp32 operation sequence (the file is compiled
+// with -ffp-contract=off), so a kernel result is a deterministic function of
+// its inputs and is reproduced bit for bit by the CPU oracle (oracle/), which
+// restates the same number formats independently.  See DESIGN.md "Number
+// formats".
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace swarm {
+
+// ---------------------------------------------------------------- Philox
+// Philox4x32-10 (Salmon et al., SC'11).  Key = (seed lo, seed hi ^ env),
+// counter = (particle id, step lo, step hi, stream tag).
+struct u32x4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c.z;
+    u32x4 n;
+    n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+    n.y = (uint32_t)p1;
+    n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+    n.w = (uint32_t)p0;
+    c = n;
+  }
+  return c;
+}
+
+// ------------------------------------------------- elementary functions
+// Correctly rounded fp32 square root.  hipcc (ROCm 7.2) lowers sqrtf and
+// __fsqrt_rn to the bare v_sqrt_f32 (<= 1 ulp); the host's sqrtf is IEEE
+// exact.  Refine the hardware value by testing its two neighbours with an
+// exact-residual FMA (the sequence LLVM emits for correctly rounded sqrt).
+__device__ __forceinline__ float sqrt_rn(float x) {
+  if (!(x > 0.0f) || x == __builtin_inff()) return __builtin_sqrtf(x);
+  const bool tiny = x < 1.2621774483536189e-29f;  // 2^-96: keep clear of denormals
+  const float xs = tiny ? x * 4294967296.0f : x;
+  float s = __builtin_amdgcn_sqrtf(xs);
+  const uint32_t si = __float_as_uint(s);
+  const float s_dn = __uint_as_float(si - 1u);
+  const float s_up = __uint_as_float(si + 1u);
+  const float r_dn = __builtin_fmaf(-s_dn, s, xs);
+  const float r_up = __builtin_fmaf(-s_up, s, xs);
+  s = (r_dn <= 0.0f) ? s_dn : s;
+  s = (r_up > 0.0f) ? s_up : s;
+  return tiny ? s * 1.52587890625e-05f : s;  // * 2^-16
+}
+
+// Correctly rounded sqrt for a positive normal finite x (the Box-Muller
+// radius -2 ln u >= 1.19e-7): no special-case or denormal branch.
+__device__ __forceinline__ float sqrt_pos(float x) {
+  float s = __builtin_amdgcn_sqrtf(x);
+  const uint32_t si = __float_as_uint(s);
+  const float s_dn = __uint_as_float(si - 1u);
+  const float s_up = __uint_as_float(si + 1u);
+  const float r_dn = __builtin_fmaf(-s_dn, s, x);
+  const float r_up = __builtin_fmaf(-s_up, s, x);
+  s = (r_dn <= 0.0f) ? s_dn : s;
+  s = (r_up > 0.0f) ? s_up : s;
+  return s;
+}
+
+// Polynomials below are Horner chains of fused multiply-adds: one rounding
+// per step, reproduced by C fmaf() in the oracle.
+__device__ __forceinline__ float logf_fixed(float x) {
+  const uint32_t b = __float_as_uint(x);
+  int e = (int)((b >> 23) & 0xffu) - 126;
+  float m = __uint_as_float((b & 0x007fffffu) | 0x3f000000u);
+  if (m < 0.70710678118654752440f) {
+    e -= 1;
+    m = m + m;
+    m = m - 1.0f;
+  } else {
+    m = m - 1.0f;
+  }
+  const float z = m * m;
+  float y = 7.0376836292e-2f;
+  y = __builtin_fmaf(y, m, -1.1514610310e-1f);
+  y = __builtin_fmaf(y, m, 1.1676998740e-1f);
+  y = __builtin_fmaf(y, m, -1.2420140846e-1f);
+  y = __builtin_fmaf(y, m, 1.4249322787e-1f);
+  y = __builtin_fmaf(y, m, -1.6668057665e-1f);
+  y = __builtin_fmaf(y, m, 2.0000714765e-1f);
+  y = __builtin_fmaf(y, m, -2.4999993993e-1f);
+  y = __builtin_fmaf(y, m, 3.3333331174e-1f);
+  y = y * m;
+  y = y * z;
+  const float fe = (float)e;
+  y = __builtin_fmaf(-2.12194440e-4f, fe, y);
+  y = __builtin_fmaf(-0.5f, z, y);
+  float r = m + y;
+  r = __builtin_fmaf(0.693359375f, fe, r);
+  return r;
+}
+
+// sin/cos of a * 2 pi / 2^32
+__device__ __forceinline__ void sincos_turn(uint32_t a, float* s_out, float* c_out) {
+  const uint32_t b = a + 0x20000000u;
+  const uint32_t quad = b >> 30;
+  const int32_t rem = (int32_t)(b & 0x3FFFFFFFu) - 0x20000000;
+  const float x = (float)rem * 1.46291807926715968e-09f;
+  const float z = x * x;
+  float sp = -1.9515295891e-4f;
+  sp = __builtin_fmaf(sp, z, 8.3321608736e-3f);
+  sp = __builtin_fmaf(sp, z, -1.6666654611e-1f);
+  sp = sp * z;
+  const float s = __builtin_fmaf(sp, x, x);
+  float cp = 2.443315711809948e-5f;
+  cp = __builtin_fmaf(cp, z, -1.388731625493765e-3f);
+  cp = __builtin_fmaf(cp, z, 4.166664568298827e-2f);
+  cp = cp * z;
+  const float h = __builtin_fmaf(-0.5f, z, 1.0f);
+  const float c = __builtin_fmaf(cp, z, h);
+  // quadrant rotation: a swap and two sign flips on the float bits (exact)
+  const bool swap = (quad & 1u) != 0u;
+  const float so0 = swap ? c : s;
+  const float co0 = swap ? s : c;
+  const float so = __uint_as_float(__float_as_uint(so0) ^ ((quad >> 1) << 31));
+  const float co = __uint_as_float(__float_as_uint(co0) ^ (((quad ^ (quad >> 1)) & 1u) << 31));
+  *s_out = so;
+  *c_out = co;
+}
+
+__device__ __forceinline__ float asinf_small(float a) {
+  const float z = a * a;
+  float p = 4.2163199048e-2f;
+  p = __builtin_fmaf(p, z, 2.4181311049e-2f);
+  p = __builtin_fmaf(p, z, 4.5470025998e-2f);
+  p = __builtin_fmaf(p, z, 7.4953002686e-2f);
+  p = __builtin_fmaf(p, z, 1.6666752422e-1f);
+  p = p * z;
+  return __builtin_fmaf(p, a, a);
+}
+
+__device__ __forceinline__ float acosf_fixed(float x) {
+  if (x < -0.5f) {
+    float t = 1.0f + x;
+    t = 0.5f * t;
+    return 3.14159265358979323846f - 2.0f * asinf_small(sqrt_rn(t));
+  }
+  if (x > 0.5f) {
+    float t = 1.0f - x;
+    t = 0.5f * t;
+    return 2.0f * asinf_small(sqrt_rn(t));
+  }
+  return 1.57079632679489661923f - asinf_small(x);
+}
+
+// Three standard normals from one Philox block: a full Box-Muller pair from
+// words (x, y) and the cosine leg of a second pair from (z, w).
+__device__ __forceinline__ float bm_radius(uint32_t r) {
+  float u = (float)(r >> 9) + 0.5f;
+  u = u * 1.1920928955078125e-07f;  // 2^-23: u in (0, 1)
+  return sqrt_pos(-2.0f * logf_fixed(u));
+}
+
+__device__ __forceinline__ void normals3(uint32_t k0, uint32_t k1, uint32_t id,
+                                         uint64_t step, uint32_t tag, float g[3]) {
+  u32x4 c;
+  c.x = id;
+  c.y = (uint32_t)step;
+  c.z = (uint32_t)(step >> 32);
+  c.w = tag;
+  const u32x4 r = philox4x32_10(c, k0, k1);
+  const float rad0 = bm_radius(r.x);
+  const float rad1 = bm_radius(r.z);
+  float s0, c0, s1, c1;
+  sincos_turn(r.y, &s0, &c0);
+  sincos_turn(r.w, &s1, &c1);
+  g[0] = rad0 * c0;
+  g[1] = rad0 * s0;
+  g[2] = rad1 * c1;
+}
+
+// Translation/rotation normals of the Brownian step (tag 0 stream), all
+// four Philox words used: sub-steps t = 4 g .. 4 g + 3 ("group" g) take the
+// twelve normals n[0..11] of three Philox blocks with counter (id, g lo,
+// g hi, kGroupTag + b), b = 0, 1, 2; block b gives n[4b..4b+3] as two full
+// Box-Muller pairs (words x/y, then z/w: cosine leg, sine leg).  Sub-step t
+// takes n[3j..3j+2], j = t & 3.  Per sub-step 0.75 Philox blocks and 1.5
+// Box-Muller pairs (three normals per block before: one block, two pairs).
+constexpr uint32_t kGroupTag = 0x10u;
+
+// the four normals of block b of group g
+__device__ __forceinline__ void group_block(uint32_t k0, uint32_t k1, uint32_t id, uint64_t g,
+                                            uint32_t b, float n[4]) {
+  u32x4 c;
+  c.x = id;
+  c.y = (uint32_t)g;
+  c.z = (uint32_t)(g >> 32);
+  c.w = kGroupTag + b;
+  const u32x4 r = philox4x32_10(c, k0, k1);
+  const float rad0 = bm_radius(r.x);
+  const float rad1 = bm_radius(r.z);
+  float s0, c0, s1, c1;
+  sincos_turn(r.y, &s0, &c0);
+  sincos_turn(r.w, &s1, &c1);
+  n[0] = rad0 * c0;
+  n[1] = rad0 * s0;
+  n[2] = rad1 * c1;
+  n[3] = rad1 * s1;
+}
+
+// The normals of consecutive sub-steps: next(t) returns sub-step t's three,
+// generating a block only when the group reaches it and carrying the rest
+// (at most three floats).  fresh: t does not follow the previous call (the
+// first sub-step of a window), so the blocks it shares are drawn again.
+struct StepNoise {
+  float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f;
+  __device__ __forceinline__ void next(uint32_t k0, uint32_t k1, uint32_t id, uint64_t t,
+                                       bool fresh, float g[3]) {
+    const uint32_t j = (uint32_t)t & 3u;
+    const uint64_t grp = t >> 2;
+    float n[4];
+    if (j == 0u) {
+      group_block(k0, k1, id, grp, 0u, n);
+      g[0] = n[0];
+      g[1] = n[1];
+      g[2] = n[2];
+      c0 = n[3];
+    } else if (j == 1u) {
+      if (fresh) {
+        group_block(k0, k1, id, grp, 0u, n);
+        c0 = n[3];
+      }
+      group_block(k0, k1, id, grp, 1u, n);
+      g[0] = c0;
+      g[1] = n[0];
+      g[2] = n[1];
+      c0 = n[2];
+      c1 = n[3];
+    } else if (j == 2u) {
+      if (fresh) {
+        group_block(k0, k1, id, grp, 1u, n);
+        c0 = n[2];
+        c1 = n[3];
+      }
+      group_block(k0, k1, id, grp, 2u, n);
+      g[0] = c0;
+      g[1] = c1;
+      g[2] = n[0];
+      c0 = n[1];
+      c1 = n[2];
+      c2 = n[3];
+    } else {
+      if (fresh) {
+        group_block(k0, k1, id, grp, 2u, n);
+        c0 = n[1];
+        c1 = n[2];
+        c2 = n[3];
+      }
+      g[0] = c0;
+      g[1] = c1;
+      g[2] = c2;
+    }
+  }
+};
+
+// Sub-step t's three normals from scratch (paths that are not a run of
+// consecutive sub-steps of one particle in one thread).
+__device__ __forceinline__ void step_normals(uint32_t k0, uint32_t k1, uint32_t id, uint64_t t,
+                                             float g[3]) {
+  StepNoise sn;
+  sn.next(k0, k1, id, t, true, g);
+}
+
+// --------------------------------------------------- fixed-point helpers
+__device__ __forceinline__ int32_t f2i32(float v) {
+  v = fminf(fmaxf(v, -2147483520.0f), 2147483520.0f);
+  return __float2int_rn(v);
+}
+
+__device__ __forceinline__ int64_t f2fix24(float v) {
+  v = v * 16777216.0f;
+  // |v| < 2^31 (force below 128): one int32 conversion, same value
+  if (__builtin_expect(fabsf(v) < 2147483520.0f, 1)) return (int64_t)__float2int_rn(v);
+  v = fminf(fmaxf(v, -4.611686018427387904e18f), 4.611686018427387904e18f);
+  return __float2ll_rn(v);
+}
+
+// int64 -> fp32 round-to-nearest.  |a| < 2^53 (every realistic force sum):
+// hi * 2^32 + lo is exact in fp64, so one fp64 -> fp32 rounding gives the
+// correctly rounded value in four branch-free instructions; larger values
+// (never in practice) take the generic conversion behind a wave-uniform
+// branch.
+__device__ __forceinline__ float i64_to_f32_wide(int64_t a) {
+  const double d = fma((double)(int32_t)(a >> 32), 4294967296.0, (double)(uint32_t)a);
+  float r = (float)d;
+  const bool big = a >= (int64_t)9007199254740992LL || a <= -(int64_t)9007199254740992LL;
+  if (__builtin_expect(__any(big), 0)) r = big ? (float)a : r;
+  return r;
+}
+
+// every active lane's predicate (one v_cmp into an SGPR pair and a scalar
+// compare with exec; __all goes through a VGPR select and a second compare)
+__device__ __forceinline__ bool wave_all(bool p) {
+  return __builtin_amdgcn_ballot_w64(p) == __builtin_amdgcn_read_exec();
+}
+
+// both predicates on every active lane: two compares straight into SGPR
+// masks and one scalar AND
+__device__ __forceinline__ bool wave_all2(bool p, bool q) {
+  return (__builtin_amdgcn_ballot_w64(p) & __builtin_amdgcn_ballot_w64(q)) ==
+         __builtin_amdgcn_read_exec();
+}
+
+__device__ __forceinline__ bool fits_i32(int64_t a) {
+  return (int32_t)(a >> 32) == ((int32_t)a >> 31);
+}
+
+// int64 -> fp32 round-to-nearest; when every lane's value fits in int32
+// (force sums below 128 in 2^-24 fixed point: the common case) one
+// v_cvt_f32_i32 -- the same correctly rounded value -- instead of the fp64
+// path.
+__device__ __forceinline__ float i64_to_f32(int64_t a) {
+  if (__builtin_expect(wave_all(fits_i32(a)), 1)) return (float)(int32_t)a;
+  return i64_to_f32_wide(a);
+}
+
+// both components behind one wave-uniform test
+__device__ __forceinline__ void i64x2_to_f32(int64_t ax, int64_t ay, float* fx, float* fy) {
+  if (__builtin_expect(wave_all2(fits_i32(ax), fits_i32(ay)), 1)) {
+    *fx = (float)(int32_t)ax;
+    *fy = (float)(int32_t)ay;
+  } else {
+    *fx = i64_to_f32_wide(ax);
+    *fy = i64_to_f32_wide(ay);
+  }
+}
+
+// 1 / x correctly rounded, for x in [2^-96, 2^96] (every in-range squared
+// pair distance: the fixed-point grid step is >= 2^-48).  It is the
+// compiler's IEEE division sequence for 1.0f / x (v_rcp_f32, a Newton step,
+// then two residual corrections) without the v_div_scale / v_div_fmas /
+// v_div_fixup range handling, which is the identity on this range (no
+// scaling: the exponents of 1 and x differ by < 96, neither is denormal).
+// Bit-identical to 1.0f / x over the whole range: tests/test_gpu_rcp.py
+// checks every float in it on the GPU.
+__device__ __forceinline__ float rcp_rn(float x) {
+  float y = __builtin_amdgcn_rcpf(x);
+  const float e = __builtin_fmaf(-x, y, 1.0f);
+  y = __builtin_fmaf(e, y, y);
+  float r = __builtin_fmaf(-x, y, 1.0f);
+  const float q = __builtin_fmaf(r, y, y);
+  r = __builtin_fmaf(-x, q, 1.0f);
+  return __builtin_fmaf(r, y, q);
+}
+
+// q + dq with the box crossing carried into the image counter: the high
+// word of the 64-bit sum (q zero-extended, dq sign-extended) is -1, 0 or +1.
+__device__ __forceinline__ void advance(uint32_t& q, int32_t& img, int32_t dq) {
+  const int64_t sum = (int64_t)(uint64_t)q + (int64_t)dq;
+  img += (int32_t)(sum >> 32);
+  q = (uint32_t)sum;
+}
+
+}  // namespace swarm

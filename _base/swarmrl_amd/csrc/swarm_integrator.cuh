@@ -1,0 +1,3418 @@
+// swarm_integrator.cuh -- Brownian dynamics + WCA integrator kernels.
+//
+// One integration window (<= kMaxWindow sub-steps, normally one RL slice of
+// 100) is three launches:
+//
+//   k_cluster_build  one workgroup per env: cell list (side >= rc + skin),
+//                    neighbour lists, union-find connected components
+//                    ("clusters") of the rc+skin graph, and a packing of the
+//                    clusters into 64-lane wave slots that never straddle a
+//                    wave.  Depends on positions only, so it may run ahead
+//                    (swarm_engine_prebuild) while the slice's actions are
+//                    being computed.
+//   k_cluster_run    one wave per 64 slots, one lane per particle: all
+//                    sub-steps of the window with no block or grid barrier;
+//                    neighbour positions move lane-to-lane (ds_bpermute).
+//                    Snapshots the window-start state and tracks every
+//                    particle's maximum displacement D.
+//   k_check          one workgroup per env: exact validity test of the
+//                    decomposition (no pair that is not a listed neighbour
+//                    pair can have come within the WCA cutoff:
+//                    d0 >= rc + D_i + D_j for every such pair with a mover,
+//                    D >= skin / 2), and, if it failed (or the build flagged a
+//                    cluster > 64 / a neighbour-list overflow), re-runs the
+//                    env from the snapshot with the global per-sub-step
+//                    algorithm.  Advances the device noise counter.
+//
+// Both paths call the same pair_force() / bd_step() functions and sum pair
+// forces in int64 fixed point, so the result is independent of the
+// decomposition and bit-identical to the CPU oracle.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "../../include/swarmrl_amd.h"
+#include "swarm_device.cuh"
+
+namespace swarm {
+
+constexpr int kMaxSpecies = SWARM_MAX_SPECIES;
+// k_cluster_run: 5 blocks (waves) per CU (SIMD), so <= 96 VGPRs (the 24 B/lane
+// spill this costs measured cheaper than 4 waves per SIMD)
+constexpr int kRunMinBlocks = 5;
+constexpr int kMaxWindow = 128;   // sub-steps per cluster window
+constexpr int kPairsPerWave = 256;  // neighbour pairs of one 64-lane wave (4 passes)
+// Clusters wider than a wave ("big" clusters) run in k_check's workgroup, one
+// member per thread: up to kBigMax members and kBigPairs pairs per env.
+constexpr int kBigMax = 1024;
+constexpr int kBigPairs = 4096;
+constexpr int kBigMark = -0x40000000;  // cbase of a big cluster's root
+constexpr int kMaxMovers = 1024;       // listed movers per env (more: exact re-run)
+
+// Wave slots per env: every cluster packs into one wave, worst case 2 N
+// slots plus per-size-class rounding.  One-pass packing (latency-bound
+// launches, see k_cluster_build) reserves up to 2 s lanes for a cluster of
+// s particles: worst case 4 N.
+__host__ __device__ inline int slots_per_env(int n, bool one_pass = false) {
+  return (one_pass ? 4 : 2) * n + 64 * 66;
+}
+constexpr float kAngInvScale = 683565275.57643158f;  // 2^32 / (2 pi)
+
+// fp32 constants derived from swarm_params_t (same derivation as the oracle).
+struct Derived {
+  float sx[3], inv_sx[3];
+  float mob_dt[kMaxSpecies], sig_t[kMaxSpecies];
+  float rot_dt[kMaxSpecies], sig_r[kMaxSpecies];
+  float inv_gt[kMaxSpecies], inv_gr[kMaxSpecies];
+  float sig_v[kMaxSpecies], sig_w[kMaxSpecies];
+  float cut2[kMaxSpecies * kMaxSpecies];
+  float sig6[kMaxSpecies * kMaxSpecies];
+  float nb2[kMaxSpecies * kMaxSpecies];  // (r_i + r_j + skin)^2: cluster links
+  float eps24;
+  float skin;
+  float rc_max_f;
+  int32_t n_species;
+  uint32_t key0, key1;
+  int32_t noisy;
+  int32_t periodic;
+  double rc_max;
+  // walls (swarm_engine_set_walls): plane n0 n1 n2 off | slab o0 o1 a0 a1 b0 b1 la lb
+  int32_t n_walls;
+  int32_t wkind[SWARM_MAX_WALLS];
+  float wp[SWARM_MAX_WALLS][8];
+  float wcut2[kMaxSpecies], wsig6[kMaxSpecies];  // wall WCA per species (radius 0 wall)
+};
+
+struct DevState {
+  uint32_t* q;       // [3][M]
+  int32_t* img;      // [3][M]
+  uint32_t* ang;     // [M]
+  float* f_swim;     // [M]
+  float* torque_z;   // [M]
+  float* f_ext;      // [3][M]
+  float* vel;        // [3][M]
+  float* omega;      // [M]
+  uint8_t* species;  // [N]
+  int32_t n;         // particles per env
+  int32_t m;         // E * N
+  int32_t dims;      // 2 or 3
+  // 3-D only
+  float* dir3;       // [3][M] unit directors
+  float* torque_xy;  // [2][M] (z: torque_z)
+  float* omega_xy;   // [2][M] (z: omega)
+  unsigned long long* wall_viol;  // [1] wall contacts with dist <= 0
+  // reuse_forces (swarm_params_t): what the last force calculation of the
+  // previous run used -- sub-step 0 of a run takes its swim force, torque
+  // and director from here (espresso.py:1304-1306).  Two slots, by the
+  // device window counter's parity: window w reads slot w & 1 and writes
+  // slot (w + 1) & 1 (the run kernel for its particles, the check only after
+  // an exact re-run), so a re-run still finds the old values.
+  int32_t reuse;
+  float* f_prev;       // [2][M]
+  float* tz_prev;      // [2][M]
+  uint32_t* ang_prev;  // [2][M]    2-D orientation
+  float* dir3_prev;    // [2][3][M] 3-D director
+  float* txy_prev;     // [2][2][M] 3-D torque x, y
+};
+
+// The reuse_forces slot p of the engine (see DevState).
+struct PrevSlot {
+  float* f;
+  float* tz;
+  uint32_t* ang;
+  float* dir3;
+  float* txy;
+};
+
+__device__ __forceinline__ PrevSlot prev_slot(const DevState& st, int p) {
+  const size_t M = (size_t)st.m;
+  PrevSlot s;
+  s.f = st.f_prev + p * M;
+  s.tz = st.tz_prev + p * M;
+  s.ang = st.ang_prev + p * M;
+  s.dir3 = st.dir3_prev + (st.dims == 3 ? p * 3 * M : 0);
+  s.txy = st.txy_prev + (st.dims == 3 ? p * 2 * M : 0);
+  return s;
+}
+
+// End of a window: the actions and orientation particle gi's next run
+// reuses at sub-step 0, into slot wp.  Called by the thread that wrote gi's
+// final state.
+__device__ __forceinline__ void save_forces(const DevState& st, size_t gi, int wp) {
+  const size_t M = (size_t)st.m;
+  const PrevSlot w = prev_slot(st, wp);
+  w.f[gi] = st.f_swim[gi];
+  w.tz[gi] = st.torque_z[gi];
+  if (st.dims == 3) {
+    w.dir3[gi] = st.dir3[gi];
+    w.dir3[M + gi] = st.dir3[M + gi];
+    w.dir3[2 * M + gi] = st.dir3[2 * M + gi];
+    w.txy[gi] = st.torque_xy[gi];
+    w.txy[M + gi] = st.torque_xy[M + gi];
+  } else {
+    w.ang[gi] = st.ang[gi];
+  }
+}
+
+__device__ __forceinline__ void save_forces_env(const DevState& st, int e, int wp) {
+  if (!st.reuse) return;
+  __syncthreads();
+  const size_t base = (size_t)e * st.n;
+  for (int i = threadIdx.x; i < st.n; i += blockDim.x) save_forces(st, base + i, wp);
+}
+
+// Device control block (uint64 words): step counter, window counter, and
+// the two noise tables' first step / length (by window parity, see k_noise).
+constexpr int kCtlStep = 0, kCtlWin = 1, kCtlTStep = 2, kCtlTLen = 4, kCtlWords = 8;
+
+__device__ __forceinline__ int window_parity(const uint64_t* ctl) {
+  return (int)(ctl[kCtlWin] & 1ull);  // written by earlier launches only
+}
+
+struct Scratch {
+  uint32_t* sqx;      // [M] positions sorted by cell
+  uint32_t* sqy;      // [M]
+  uint32_t* sqz;      // [M] (3-D global path)
+  int32_t* simg;      // [3][M] image counters sorted with sqx/sqy/sqz (non-periodic global path)
+  int32_t* sidx;      // [M] particle index of a sorted entry
+  uint32_t* bq;       // [dims][M] window-start snapshot
+  int32_t* bimg;      // [dims][M]
+  uint32_t* bang;     // [M]
+  int32_t* root;      // [M] cluster id (root particle)
+  int32_t* slot_of;   // [M] wave slot of a particle
+  int32_t* perm;      // [E][S] particle of a slot (-1: idle lane)
+  uint32_t* pairs;    // [E][wmax][kPairsPerWave]: lane a | lane b << 6 | species pair << 12
+  int32_t* wave_npairs;  // [E][wmax]
+  float* disp;        // [M] max displacement over the window
+  float* bdir3;       // [3][M] window-start directors (3-D cluster path)
+  int32_t* env_waves; // [E]
+  int32_t* fallback;  // [E]
+  int32_t* big_list;  // [E][kBigMax] particles of the env's big clusters (member order)
+  uint32_t* big_pairs;  // [E][kBigPairs] member a | member b << 10 | species pair << 20
+  int32_t* big_n;     // [E] members
+  int32_t* big_np;    // [E] pairs
+  // colloids that moved >= skin / 2 in the window (appended by the run
+  // kernel and the big-cluster run, consumed and reset by k_check)
+  int32_t* nmov;      // [E]
+  int32_t* movers;    // [E][kMaxMovers]
+  // neighbour-list path (boxes whose rc + skin graph percolates)
+  int32_t* nl;        // [kNlMax][M] neighbours j | species << 24 of particle gi
+  int32_t* nn;        // [M] neighbour count
+  uint32_t* qalt;     // [dims][M] second position buffer (sub-steps alternate)
+  uint4* qa;          // [2][M] AoS position ping-pong of the per-launch window:
+                      // (x, y, z, 0) in 3-D, uint2 (x, y) in 2-D
+  // cluster build (k_build_sort -> k_build_pairs -> k_cluster_build)
+  uint32_t* bsq;      // [dims][M] cell-sorted positions (x, y[, z])
+  int32_t* bsid;      // [M] particle | species << 24 of a sorted entry
+  int32_t* bcstart;   // [E][ncb + 1] first sorted entry of every cell, [ncb] = N
+  uint32_t* gplist;   // [E][pair_cap] neighbour pairs i | j << 16, i < j
+  int32_t* gnpairs;   // [E] pairs found (may exceed pair_cap: overflow)
+  // 2-D pair search (build_pairs_body): every block unions the pairs whose
+  // both ends lie in its range of sorted entries (a compact band of cells)
+  // in LDS and writes each particle's block-local root; the pairs between
+  // blocks go to a cross list, the only pairs the cluster build still unions
+  int32_t* gcnt;      // [E][ncb] per-cell counters of the chip-wide sort (zero between builds)
+  int32_t* gcell;     // [M] cell of a particle (chip-wide sort)
+  int32_t* grank;     // [M] its rank within the cell
+  int32_t* lroot;     // [M] block-local union-find root (a particle of the env) | pairs << 16
+  uint32_t* xpairs;   // [E][pair_cap] cross-block pairs i | j << 16
+  int32_t* gnx;       // [E] cross-block pairs found
+  int32_t local_uf;   // 1: the 2-D pair search unions its blocks' pairs (lroot, xpairs)
+  int32_t* gclus;     // [3][M] cluster sizes / bases / slots (large-N build only)
+  int32_t pair_cap;   // pairs per env
+  int32_t one_pass;   // 1: pack clusters so that a wave has <= 64 pairs
+  int32_t fill_singletons;  // 1: singletons take the tail lanes of the other classes
+  int32_t periodic;   // 0: non-periodic box (edge cells, unwrapped pair distances; 2-D build)
+  int32_t multi_species;  // 0: one species (species pair bits 0, no species loads in the build)
+  int32_t sort_stage_k;   // > 0: the build sort scatters into LDS, this many sorted entries per
+                          // pass, and writes its output coalesced (0: scattered stores)
+  int32_t S;          // slots per env
+  int32_t wmax;       // S / 64
+  uint64_t* phase;    // [32] build phase stamps (SWARM_PHASE_TIMING builds only)
+  // profiling only (else null): [kRoles][kStampSub][2] earliest start /
+  // latest end (device wall clock) of each workgroup role of the launches of
+  // one window
+  unsigned long long* rstamp;
+};
+
+// Launch stamps are spread over kStampSub (min, max) pairs by workgroup
+// (blockIdx.x mod kStampSub) so that the atomics of a launch's waves do not
+// queue on one address (which stretched the stamped launches); the reader
+// takes the min / max over the pairs.
+constexpr int kStampSub = 64;
+
+// Workgroup roles of the window's launches (role_begin / role_end, rstamp)
+enum RoleId {
+  kRoleCheck = 0,
+  kRoleSort,
+  kRoleVgrid,
+  kRoleField,
+  kRolePairs,
+  kRoleCone,
+  kRoleCbuild,
+  kRoleMlp,
+  kRoles
+};
+
+__device__ __forceinline__ void role_begin(const Scratch& sc, int r) {
+  if (sc.rstamp && threadIdx.x == 0)
+    atomicMin(&sc.rstamp[2 * (r * kStampSub + (blockIdx.x & (kStampSub - 1)))],
+              (unsigned long long)wall_clock64());
+}
+__device__ __forceinline__ void role_end(const Scratch& sc, int r) {
+  if (sc.rstamp && (threadIdx.x & 63) == 0)
+    atomicMax(&sc.rstamp[2 * (r * kStampSub + (blockIdx.x & (kStampSub - 1))) + 1],
+              (unsigned long long)wall_clock64());
+}
+
+#ifdef SWARM_PHASE_TIMING
+#define SWARM_STAMP(k)                                                    \
+  do {                                                                    \
+    if (blockIdx.x == 0 && threadIdx.x == 0) sc.phase[k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define SWARM_STAMP(k) \
+  do {                 \
+  } while (0)
+#endif
+
+// ---------------------------------------------------------------- helpers
+__device__ __forceinline__ int cell_index(uint32_t qx, uint32_t qy, int lx, int ly) {
+  const int cx = lx == 0 ? 0 : (int)(qx >> (32 - lx));
+  const int cy = ly == 0 ? 0 : (int)(qy >> (32 - ly));
+  return (cy << lx) | cx;
+}
+
+// Non-periodic boxes (MDParams.periodic = False, espresso.py:270; global
+// path only): the cell of a particle outside the box is the edge cell on its
+// side, and pair displacements are plain differences of the unwrapped
+// positions (no minimum image) -- the oracle's cell_of / pair_disp.
+__device__ __forceinline__ int cell_coord(uint32_t q, int32_t im, int l, bool periodic) {
+  const int v = l == 0 ? 0 : (int)(q >> (32 - l));
+  if (periodic) return v;
+  return im < 0 ? 0 : (im > 0 ? (1 << l) - 1 : v);
+}
+
+__device__ __forceinline__ float pair_disp(uint32_t qj, int32_t ij, uint32_t qi, int32_t ii,
+                                           float sx, bool periodic) {
+  if (periodic) return (float)(int32_t)(qj - qi) * sx;
+  const int64_t dq = (int64_t)(ij - ii) * 4294967296LL + ((int64_t)qj - (int64_t)qi);
+  return (float)dq * sx;
+}
+
+// floor(n / d) for 0 <= n < 2^20 and 1 <= d < 2^20: a float reciprocal
+// estimate (within one of the quotient) and one correction, instead of the
+// compiler's ~40-instruction integer division (the cluster build's packing
+// divides per cluster: 64 / s, r / per).
+__device__ __forceinline__ int udiv_small(int n, int d) {
+  int q = (int)((float)n * __builtin_amdgcn_rcpf((float)d));
+  const int r = n - q * d;
+  q += (r >= d ? 1 : 0) - (r < 0 ? 1 : 0);
+  return q;
+}
+
+// Inclusive prefix sum over a wave's 64 lanes on the DPP network: row
+// shifts 1, 2, 4, 8 scan each 16-lane row, the gfx9 row broadcasts 15 and 31
+// carry rows into the next ones.  VALU only (no ds_bpermute round trip per
+// step, as __shfl_up's).  Every lane of the wave must be active.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
+// Exclusive scan of data[0..n) in LDS by the whole block; data[n] = total.
+// Each wave scans a contiguous chunk 64 entries at a time (lane k reads
+// entry base + k: no LDS bank conflicts, unlike one contiguous run per
+// thread), carrying its running total; a second pass adds the exclusive
+// prefix of the waves' totals.
+// Up to 4 entries per thread the one-run-per-thread scan is shorter (its
+// few strided reads conflict little): measured 2.6 vs 1.8 us at 4096 cells,
+// 7.0 vs 11.5 us at 16384.
+__device__ inline void block_exclusive_scan_runs(int32_t* data, int n, int32_t* wave_sums) {
+  const int T = blockDim.x;
+  const int tid = threadIdx.x;
+  const int per = (n + T - 1) / T;
+  const int lo = min(tid * per, n), hi = min(lo + per, n);
+  // four entries per thread, 16-byte aligned: one ds_read_b128 / write_b128
+  const bool quad = per == 4 && (n & 3) == 0 && (reinterpret_cast<uintptr_t>(data) & 15) == 0;
+  int4 x4 = make_int4(0, 0, 0, 0);
+  int32_t local = 0;
+  if (quad) {
+    if (lo < n) x4 = reinterpret_cast<const int4*>(data)[tid];
+    local = x4.x + x4.y + x4.z + x4.w;
+  } else {
+    for (int k = lo; k < hi; ++k) local += data[k];
+  }
+  const int lane = tid & 63, wave = tid >> 6;
+  int32_t v = local;
+  v = wave_incl_scan(v);
+  if (lane == 63) wave_sums[wave] = v;
+  __syncthreads();
+  if (wave == 0) {
+    const int nw = (T + 63) >> 6;
+    int32_t w = lane < nw ? wave_sums[lane] : 0;
+    w = wave_incl_scan(w);
+    if (lane < nw) wave_sums[lane] = w;
+  }
+  __syncthreads();
+  int32_t run = v - local + (wave > 0 ? wave_sums[wave - 1] : 0);
+  if (quad) {
+    if (lo < n) {
+      int4 y;
+      y.x = run;
+      y.y = run + x4.x;
+      y.z = y.y + x4.y;
+      y.w = y.z + x4.z;
+      reinterpret_cast<int4*>(data)[tid] = y;
+    }
+    if (tid == T - 1) data[n] = run + local;
+    return;
+  }
+  for (int k = lo; k < hi; ++k) {
+    const int32_t c = data[k];
+    data[k] = run;
+    run += c;
+  }
+  if (tid == T - 1) data[n] = run;
+}
+
+__device__ inline void block_exclusive_scan(int32_t* data, int n, int32_t* wave_sums) {
+  const int T = blockDim.x;
+  if (n <= 4 * T) {
+    block_exclusive_scan_runs(data, n, wave_sums);
+    return;
+  }
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int nw = (T + 63) >> 6;
+  const int chunk = (((n + nw - 1) / nw) + 63) & ~63;
+  const int lo = min(wave * chunk, n), hi = min(lo + chunk, n);
+  int32_t carry = 0;
+  for (int b = lo; b < hi; b += 64) {
+    const int k = b + lane;
+    const int32_t x = k < hi ? data[k] : 0;
+    int32_t v = x;
+    v = wave_incl_scan(v);
+    if (k < hi) data[k] = carry + v - x;
+    carry += __builtin_amdgcn_readlane(v, 63);
+  }
+  if (lane == 0) wave_sums[wave] = carry;
+  __syncthreads();
+  if (wave == 0) {
+    int32_t w = lane < nw ? wave_sums[lane] : 0;
+    w = wave_incl_scan(w);
+    if (lane < nw) wave_sums[lane] = w;  // inclusive prefix of the wave totals
+  }
+  __syncthreads();
+  const int32_t add = wave > 0 ? wave_sums[wave - 1] : 0;
+  if (add != 0)
+    for (int k = lo + lane; k < hi; k += 64) data[k] += add;
+  if (tid == T - 1) data[n] = wave_sums[nw - 1];
+}
+
+// WCA force on i from j (r = x_j - x_i), accumulated in 2^-24 fixed point.
+// cut2 = (r_i + r_j)^2, sig6 = sigma^6, eps24 = 24 epsilon (Derived tables).
+__device__ __forceinline__ void pair_force(float cut2, float sig6, float eps24, float rx,
+                                           float ry, int64_t& ax, int64_t& ay) {
+  const float r2 = rx * rx + ry * ry;
+  if (r2 < cut2 && r2 > 0.0f) {
+    const float ir2 = 1.0f / r2;
+    float ir6 = ir2 * ir2;
+    ir6 = ir6 * ir2;
+    const float s6 = sig6 * ir6;
+    float t = 2.0f * s6;
+    t = t - 1.0f;
+    float fr = eps24 * s6;
+    fr = fr * t;
+    fr = fr * ir2;
+    ax += f2fix24(-fr * rx);
+    ay += f2fix24(-fr * ry);
+  }
+}
+
+// Branch-free pair_force for the run kernel's pair passes: the force on the
+// first particle in 2^-24 fixed point, or zero out of range (r2 = 0 for an
+// empty slot that names one particle twice).  In-range values equal
+// pair_force's; the int32 conversion is taken when every lane fits.
+__device__ __forceinline__ void pair_fix_sel(float cut2, float sig6, float eps24, float rx,
+                                             float ry, int64_t& fx, int64_t& fy) {
+  const float r2 = rx * rx + ry * ry;
+  const bool in = r2 < cut2 && r2 > 0.0f;
+  const float ir2 = rcp_rn(in ? r2 : 1.0f);  // = 1.0f / r2 (in range: r2 >= 2^-96)
+  float ir6 = ir2 * ir2;
+  ir6 = ir6 * ir2;
+  const float s6 = sig6 * ir6;
+  float t = 2.0f * s6;
+  t = t - 1.0f;
+  float fr = eps24 * s6;
+  fr = fr * t;
+  fr = fr * ir2;
+  const float vx = (in ? -fr * rx : 0.0f) * 16777216.0f;
+  const float vy = (in ? -fr * ry : 0.0f) * 16777216.0f;
+  if (__builtin_expect(wave_all2(fabsf(vx) < 2147483520.0f, fabsf(vy) < 2147483520.0f), 1)) {
+    fx = (int64_t)__float2int_rn(vx);
+    fy = (int64_t)__float2int_rn(vy);
+  } else {
+    fx = __float2ll_rn(fminf(fmaxf(vx, -4.611686018427387904e18f), 4.611686018427387904e18f));
+    fy = __float2ll_rn(fminf(fmaxf(vy, -4.611686018427387904e18f), 4.611686018427387904e18f));
+  }
+}
+
+// WCA force of every wall on a particle of species si at the folded
+// position (x, y, z) in 2^-24 fixed point (same operation sequence as
+// oracle/swarm_oracle.c:wall_forces); contacts with dist <= 0 are counted.
+template <int D>
+__device__ __forceinline__ void wall_forces(const Derived* __restrict__ d, int si, float x, float y,
+                                            float z, int64_t& ax, int64_t& ay, int64_t& az,
+                                            unsigned long long* viol) {
+  const int nw = d->n_walls;
+  for (int k = 0; k < nw; ++k) {
+    const float* w = d->wp[k];
+    float vx, vy, vz, r2;
+    if (d->wkind[k] == 0) {
+      float dist = w[0] * x + w[1] * y;
+      dist = dist + w[2] * z;
+      dist = dist - w[3];
+      if (!(dist > 0.0f)) {
+        atomicAdd(viol, 1ull);
+        continue;
+      }
+      vx = w[0] * dist;
+      vy = w[1] * dist;
+      vz = w[2] * dist;
+      r2 = dist * dist;
+    } else {
+      const float px = x - w[0], py = y - w[1];
+      const float u = px * w[2] + py * w[3];
+      const float t = px * w[4] + py * w[5];
+      const float du = u - fminf(fmaxf(u, 0.0f), w[6]);
+      const float dt = t - fminf(fmaxf(t, 0.0f), w[7]);
+      if (du == 0.0f && dt == 0.0f) {
+        atomicAdd(viol, 1ull);
+        continue;
+      }
+      vx = du * w[2] + dt * w[4];
+      vy = du * w[3] + dt * w[5];
+      vz = 0.0f;
+      r2 = vx * vx + vy * vy;
+    }
+    if (r2 < d->wcut2[si]) {
+      const float ir2 = 1.0f / r2;
+      float ir6 = ir2 * ir2;
+      ir6 = ir6 * ir2;
+      const float s6 = d->wsig6[si] * ir6;
+      float t = 2.0f * s6;
+      t = t - 1.0f;
+      float fr = d->eps24 * s6;
+      fr = fr * t;
+      fr = fr * ir2;
+      ax += f2fix24(fr * vx);
+      ay += f2fix24(fr * vy);
+      if (D == 3) az += f2fix24(fr * vz);
+    }
+  }
+}
+
+struct PState {
+  uint32_t qx, qy, an;
+  int32_t ix, iy;
+};
+
+// Per-colloid constants, read once per launch (not per sub-step).
+struct PConst {
+  float mob_dt, sig_t, rot_dt, sig_r, inv_gt, inv_gr, sig_v, sig_w;
+  float inv_sx0, inv_sx1;
+  bool noisy;
+};
+
+__device__ __forceinline__ PConst load_pconst(const Derived* __restrict__ d, int si) {
+  PConst c;
+  c.mob_dt = d->mob_dt[si];
+  c.sig_t = d->sig_t[si];
+  c.rot_dt = d->rot_dt[si];
+  c.sig_r = d->sig_r[si];
+  c.inv_gt = d->inv_gt[si];
+  c.inv_gr = d->inv_gr[si];
+  c.sig_v = d->sig_v[si];
+  c.sig_w = d->sig_w[si];
+  c.inv_sx0 = d->inv_sx[0];
+  c.inv_sx1 = d->inv_sx[1];
+  c.noisy = d->noisy != 0;
+  return c;
+}
+
+// Pair tables staged in LDS by the whole block (call before any early exit).
+struct PairTables {
+  float cut2[kMaxSpecies * kMaxSpecies];
+  float sig6[kMaxSpecies * kMaxSpecies];
+};
+
+__device__ __forceinline__ void stage_pair_tables(const Derived* __restrict__ d, PairTables* t) {
+  for (int k = threadIdx.x; k < kMaxSpecies * kMaxSpecies; k += blockDim.x) {
+    t->cut2[k] = d->cut2[k];
+    t->sig6[k] = d->sig6[k];
+  }
+  __syncthreads();
+}
+
+// One Brownian-dynamics sub-step of one particle from its summed WCA force.
+// an_swim: the orientation the swim force points along (p.an, or with
+// reuse_forces at sub-step 0 the previous run's last one).
+// kTable: the step's three normals come precomputed in gt (k_noise).
+template <bool kTable = false>
+__device__ __forceinline__ void bd_step(const PConst& c, PState& p, int64_t ax, int64_t ay,
+                                        float fs, float tz, float fex, float fey, uint32_t k0,
+                                        uint32_t k1, uint32_t id, uint64_t step, bool last,
+                                        float* vx, float* vy, float* w, uint32_t an_swim,
+                                        const float* gt = nullptr, StepNoise* noise = nullptr,
+                                        bool fresh = true) {
+  float sn, cs;
+  sincos_turn(an_swim, &sn, &cs);
+  float fx = i64_to_f32(ax) * 5.9604644775390625e-08f;
+  float fy = i64_to_f32(ay) * 5.9604644775390625e-08f;
+  fx = fx + fex;
+  fy = fy + fey;
+  fx = fx + fs * cs;
+  fy = fy + fs * sn;
+  float dx = fx * c.mob_dt;
+  float dy = fy * c.mob_dt;
+  float dth = tz * c.rot_dt;
+  if (c.noisy) {
+    float g[3];
+    if (kTable) {
+      g[0] = gt[0];
+      g[1] = gt[1];
+      g[2] = gt[2];
+    } else if (noise) {  // consecutive sub-steps of one particle: carried normals
+      noise->next(k0, k1, id, step, fresh, g);
+    } else {
+      step_normals(k0, k1, id, step, g);
+    }
+    dx = dx + c.sig_t * g[0];
+    dy = dy + c.sig_t * g[1];
+    dth = dth + c.sig_r * g[2];
+  }
+  advance(p.qx, p.ix, f2i32(dx * c.inv_sx0));
+  advance(p.qy, p.iy, f2i32(dy * c.inv_sx1));
+  p.an = p.an + (uint32_t)f2i32(dth * kAngInvScale);
+  if (last) {
+    float v0 = fx * c.inv_gt, v1 = fy * c.inv_gt;
+    float om = tz * c.inv_gr;
+    if (c.noisy) {
+      float g[3];
+      normals3(k0, k1, id, step, 1u, g);
+      v0 = v0 + c.sig_v * g[0];
+      v1 = v1 + c.sig_v * g[1];
+      om = om + c.sig_w * g[2];
+    }
+    *vx = v0;
+    *vy = v1;
+    *w = om;
+  }
+}
+
+// bd_step without the rotation, for the cluster run (which updates the
+// angle, and the next sub-step's director, while the force sums are in
+// flight): same operation sequence for the translation and velocities.
+__device__ __forceinline__ void bd_translate(const PConst& c, PState& p, int64_t ax, int64_t ay,
+                                             float fs, float tz, float fex, float fey,
+                                             uint32_t k0, uint32_t k1, uint32_t id, uint64_t step,
+                                             bool last, float* vx, float* vy, float* w,
+                                             const float* g, float sn, float cs) {
+  float fx, fy;
+  i64x2_to_f32(ax, ay, &fx, &fy);
+  fx = fx * 5.9604644775390625e-08f;
+  fy = fy * 5.9604644775390625e-08f;
+  fx = fx + fex;
+  fy = fy + fey;
+  fx = fx + fs * cs;
+  fy = fy + fs * sn;
+  float dx = fx * c.mob_dt;
+  float dy = fy * c.mob_dt;
+  if (c.noisy) {
+    dx = dx + c.sig_t * g[0];
+    dy = dy + c.sig_t * g[1];
+  }
+  advance(p.qx, p.ix, f2i32(dx * c.inv_sx0));
+  advance(p.qy, p.iy, f2i32(dy * c.inv_sx1));
+  if (last) {
+    float v0 = fx * c.inv_gt, v1 = fy * c.inv_gt;
+    float om = tz * c.inv_gr;
+    if (c.noisy) {
+      float gv[3];
+      normals3(k0, k1, id, step, 1u, gv);
+      v0 = v0 + c.sig_v * gv[0];
+      v1 = v1 + c.sig_v * gv[1];
+      om = om + c.sig_w * gv[2];
+    }
+    *vx = v0;
+    *vy = v1;
+    *w = om;
+  }
+}
+
+// One steepest-descent step of one particle (espresso.py:1163-1168).
+__device__ __forceinline__ bool sd_step(const PConst& c, PState& p, int64_t ax, int64_t ay,
+                                        float fs, float tz, float fex, float fey, float g,
+                                        float md) {
+  float sn, cs;
+  sincos_turn(p.an, &sn, &cs);
+  float fx = i64_to_f32(ax) * 5.9604644775390625e-08f;
+  float fy = i64_to_f32(ay) * 5.9604644775390625e-08f;
+  fx = fx + fex;
+  fy = fy + fey;
+  fx = fx + fs * cs;
+  fy = fy + fs * sn;
+  const bool any = fx != 0.0f || fy != 0.0f || tz != 0.0f;
+  const float px = fminf(fmaxf(g * fx, -md), md);
+  const float py = fminf(fmaxf(g * fy, -md), md);
+  const float pa = fminf(fmaxf(g * tz, -md), md);
+  advance(p.qx, p.ix, f2i32(px * c.inv_sx0));
+  advance(p.qy, p.iy, f2i32(py * c.inv_sx1));
+  p.an = p.an + (uint32_t)f2i32(pa * kAngInvScale);
+  return any;
+}
+
+// ------------------------------------------------------- global path
+// All sub-steps of env e by one workgroup: per sub-step a counting sort into
+// cells of side >= rc_max (counts in LDS, sorted copy in global scratch), then
+// every particle sums its pair forces over the 3x3 cells and is advanced.
+// Spill-free: no per-thread particle arrays.
+__device__ void block_global_run(const Derived* __restrict__ d, const DevState& st,
+                                 const Scratch& sc, int e, int n_steps, uint64_t step0, int lx,
+                                 int ly, bool sd_mode, float g, float md, int32_t* cnt,
+                                 int32_t* wave_sums, const PairTables* pt, int rp) {
+  const PrevSlot prv = prev_slot(st, rp);  // reuse_forces: sub-step 0 reads slot rp
+  const int T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int ncell = 1 << (lx + ly);
+  const int ncx = 1 << lx, ncy = 1 << ly;
+  const int lox = ncx >= 3 ? -1 : 0, hix = ncx >= 3 ? 1 : ncx - 1;
+  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+  const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const float eps24 = d->eps24;
+  const bool per = d->periodic != 0;
+  auto cell_of = [&](size_t gi) {
+    return (cell_coord(st.q[M + gi], st.img[M + gi], ly, per) << lx) |
+           cell_coord(st.q[gi], st.img[gi], lx, per);
+  };
+  for (int s = 0; s < n_steps; ++s) {
+    for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
+    __syncthreads();
+    for (int i = tid; i < N; i += T) atomicAdd(&cnt[cell_of(base + i)], 1);
+    __syncthreads();
+    block_exclusive_scan(cnt, ncell, wave_sums);
+    __syncthreads();
+    for (int i = tid; i < N; i += T) {
+      const uint32_t qx = st.q[base + i], qy = st.q[M + base + i];
+      const int pos = atomicAdd(&cnt[cell_of(base + i)], 1);
+      sc.sqx[base + pos] = qx;
+      sc.sqy[base + pos] = qy;
+      sc.sidx[base + pos] = i;
+      if (!per) {  // the images too: the update below rewrites st.img in place
+        sc.simg[base + pos] = st.img[base + i];
+        sc.simg[M + base + pos] = st.img[M + base + i];
+      }
+    }
+    __syncthreads();  // cell c now spans [c ? cnt[c-1] : 0, cnt[c])
+    int any = 0;
+    for (int i = tid; i < N; i += T) {
+      const size_t gi = base + i;
+      PState p;
+      p.qx = st.q[gi];
+      p.qy = st.q[M + gi];
+      p.ix = st.img[gi];
+      p.iy = st.img[M + gi];
+      p.an = st.ang[gi];
+      const int si = st.species[i];
+      int64_t ax = 0, ay = 0;
+      const int c0 = cell_of(gi);
+      const int cx = c0 & (ncx - 1), cy = c0 >> lx;
+      for (int oy = loy; oy <= hiy; ++oy) {
+        if (!per && (cy + oy < 0 || cy + oy >= ncy)) continue;
+        const int y = (cy + oy + ncy) & (ncy - 1);
+        for (int ox = lox; ox <= hix; ++ox) {
+          if (!per && (cx + ox < 0 || cx + ox >= ncx)) continue;
+          const int x = (cx + ox + ncx) & (ncx - 1);
+          const int cc = (y << lx) | x;
+          const int jb = cc ? cnt[cc - 1] : 0, je = cnt[cc];
+          for (int jj = jb; jj < je; ++jj) {
+            const int j = sc.sidx[base + jj];
+            if (j == i) continue;
+            const float rx = per ? (float)(int32_t)(sc.sqx[base + jj] - p.qx) * sx0
+                                 : pair_disp(sc.sqx[base + jj], sc.simg[base + jj], p.qx, p.ix,
+                                             sx0, false);
+            const float ry = per ? (float)(int32_t)(sc.sqy[base + jj] - p.qy) * sx1
+                                 : pair_disp(sc.sqy[base + jj], sc.simg[M + base + jj], p.qy, p.iy,
+                                             sx1, false);
+            const int pk = si * kMaxSpecies + st.species[j];
+            pair_force(pt->cut2[pk], pt->sig6[pk], eps24, rx, ry, ax, ay);
+          }
+        }
+      }
+      if (d->n_walls) {
+        int64_t az = 0;
+        wall_forces<2>(d, si, (float)p.qx * sx0, (float)p.qy * sx1, 0.0f, ax, ay, az,
+                       st.wall_viol);
+      }
+      const bool first = st.reuse && s == 0 && !sd_mode;  // reuse_forces: previous run's
+      const float fs = first ? prv.f[gi] : st.f_swim[gi];
+      const float tz = first ? prv.tz[gi] : st.torque_z[gi];
+      const float fex = st.f_ext[gi], fey = st.f_ext[M + gi];
+      const PConst pc = load_pconst(d, si);
+      if (sd_mode) {
+        any |= sd_step(pc, p, ax, ay, fs, tz, fex, fey, g, md) ? 1 : 0;
+      } else {
+        float vx, vy, w;
+        const bool last = s == n_steps - 1;
+        bd_step(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s, last,
+                &vx, &vy, &w, first ? prv.ang[gi] : p.an);
+        if (last) {
+          st.vel[gi] = vx;
+          st.vel[M + gi] = vy;
+          st.vel[2 * M + gi] = 0.0f;
+          st.omega[gi] = w;
+        }
+      }
+      st.q[gi] = p.qx;
+      st.q[M + gi] = p.qy;
+      st.img[gi] = p.ix;
+      st.img[M + gi] = p.iy;
+      st.ang[gi] = p.an;
+    }
+    if (sd_mode) {
+      if (!__syncthreads_or(any)) break;
+    } else {
+      __syncthreads();
+    }
+  }
+}
+
+#ifdef SWARM_PHASE_TIMING
+__device__ unsigned long long g_global_phase[4];  // cycles: sort, forces+step, steps
+#endif
+
+// LDS words the register-resident global path needs after the cell counts
+// (sorted positions as uint2 + ids), 0 when it does not apply (3-D, or more
+// than kGlobalCH particles per thread of a 1024-thread block).
+constexpr int kGlobalCH = 4;
+__host__ __device__ inline size_t global_lds_extra_words(int n, int dims, int ncell) {
+  const size_t extra = 8 * (size_t)n + 2;
+  // k_check's layout (the larger): 16 + 16 + 1024 + ncell + 1 words first,
+  // and 4 KB of static LDS beside it
+  const bool fits = (16 + 16 + 1024 + (size_t)ncell + 1 + extra) * 4 + 4096 <= 160 * 1024;
+  return dims == 2 && n <= kGlobalCH * 1024 && fits ? extra : 0;
+}
+
+// The global path with the particle state and the per-sub-step cell sort in
+// LDS (up to kGlobalCH particles per thread): same pair_force / bd_step /
+// sd_step sequence and int64 force sums as block_global_run, so the same
+// bits, but no global round trip inside a sub-step (it is the exact re-run
+// of an env whose cluster window failed k_check, and the overlap removal).
+// lsq: 8 N + 2 LDS words after cnt[ncell + 1].
+__device__ __forceinline__ void block_global_run_lds(const Derived* __restrict__ d, const DevState& st, int e,
+                                     int n_steps, uint64_t step0, int lx, int ly, bool sd_mode,
+                                     float g, float md, int32_t* cnt, int32_t* wave_sums,
+                                     int32_t* lsq, const PairTables* pt, int rp) {
+  const PrevSlot prv = prev_slot(st, rp);  // reuse_forces: sub-step 0 reads slot rp
+  const int T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int ncell = 1 << (lx + ly);
+  const int ncx = 1 << lx, ncy = 1 << ly;
+  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+  const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const float eps24 = d->eps24;
+  uint2* sq = reinterpret_cast<uint2*>(lsq + ((reinterpret_cast<uintptr_t>(lsq) >> 2) & 1));
+  int32_t* sid = reinterpret_cast<int32_t*>(sq + N);
+  // particle state by particle index (the forces, velocities and species
+  // are re-read from global memory, L1-resident, where used)
+  uint32_t* lqx = reinterpret_cast<uint32_t*>(sid + N);
+  uint32_t* lqy = lqx + N;
+  int32_t* lix = reinterpret_cast<int32_t*>(lqy + N);
+  int32_t* liy = lix + N;
+  uint32_t* lan = reinterpret_cast<uint32_t*>(liy + N);
+  for (int i = tid; i < N; i += T) {
+    const size_t gi = base + i;
+    lqx[i] = st.q[gi];
+    lqy[i] = st.q[M + gi];
+    lix[i] = st.img[gi];
+    liy[i] = st.img[M + gi];
+    lan[i] = st.ang[gi];
+  }
+  __syncthreads();
+#ifdef SWARM_PHASE_TIMING
+  uint64_t t_sort = 0, t_force = 0, tA = 0;
+#endif
+  for (int s = 0; s < n_steps; ++s) {
+#ifdef SWARM_PHASE_TIMING
+    if (tid == 0) tA = __builtin_amdgcn_s_memtime();
+#endif
+    for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
+    __syncthreads();
+    for (int i = tid; i < N; i += T) atomicAdd(&cnt[cell_index(lqx[i], lqy[i], lx, ly)], 1);
+    __syncthreads();
+    block_exclusive_scan(cnt, ncell, wave_sums);
+    __syncthreads();
+    for (int i = tid; i < N; i += T) {
+      const uint32_t qx = lqx[i], qy = lqy[i];
+      const int pos = atomicAdd(&cnt[cell_index(qx, qy, lx, ly)], 1);
+      sq[pos] = make_uint2(qx, qy);
+      sid[pos] = i | ((int)st.species[i] << 24);
+    }
+    __syncthreads();  // cell c now spans [c ? cnt[c-1] : 0, cnt[c])
+#ifdef SWARM_PHASE_TIMING
+    if (tid == 0) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      t_sort += t - tA;
+      tA = t;
+    }
+#endif
+    int any = 0;
+    // sorted order: the lanes of a wave take neighbouring particles, so their
+    // candidate ranges (a stencil row = one contiguous sorted range, plus a
+    // wrap range at the grid edge) are alike and the loops stay converged
+    for (int ps = tid; ps < N; ps += T) {
+      const int pki = sid[ps];
+      const int i = pki & 0xffffff, sik = pki >> 24;
+      const size_t gi = base + i;
+      PState pp = {lqx[i], lqy[i], lan[i], lix[i], liy[i]};
+      const bool first = st.reuse && s == 0 && !sd_mode;  // reuse_forces: previous run's
+      const float fs = first ? prv.f[gi] : st.f_swim[gi];
+      const float tz = first ? prv.tz[gi] : st.torque_z[gi];
+      const float fex = st.f_ext[gi], fey = st.f_ext[M + gi];
+      int64_t ax = 0, ay = 0;
+      const int c0 = cell_index(pp.qx, pp.qy, lx, ly);
+      const int cx = c0 & (ncx - 1), cy = c0 >> lx;
+      const int xa = ncx >= 3 ? max(cx - 1, 0) : 0;
+      const int xb = ncx >= 3 ? min(cx + 1, ncx - 1) : ncx - 1;
+      const int xw = ncx >= 3 ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
+      for (int oy = loy; oy <= hiy; ++oy) {
+        const int row = ((cy + oy + ncy) & (ncy - 1)) << lx;
+#pragma unroll
+        for (int part = 0; part < 2; ++part) {
+          if (part == 1 && xw < 0) continue;
+          const int c_lo = row | (part == 0 ? xa : xw), c_hi = row | (part == 0 ? xb : xw);
+          const int jb = c_lo ? cnt[c_lo - 1] : 0, je = cnt[c_hi];
+          for (int jj = jb; jj < je; ++jj) {
+            const int pj = sid[jj];
+            if ((pj & 0xffffff) == i) continue;
+            const uint2 qj = sq[jj];
+            const float rx = (float)(int32_t)(qj.x - pp.qx) * sx0;
+            const float ry = (float)(int32_t)(qj.y - pp.qy) * sx1;
+            const int pk = sik * kMaxSpecies + (pj >> 24);
+            pair_force(pt->cut2[pk], pt->sig6[pk], eps24, rx, ry, ax, ay);
+          }
+        }
+      }
+      if (d->n_walls) {
+        int64_t az = 0;
+        wall_forces<2>(d, sik, (float)pp.qx * sx0, (float)pp.qy * sx1, 0.0f, ax, ay, az,
+                       st.wall_viol);
+      }
+      const PConst pc = load_pconst(d, sik);
+      if (sd_mode) {
+        any |= sd_step(pc, pp, ax, ay, fs, tz, fex, fey, g, md) ? 1 : 0;
+      } else {
+        float vx, vy, w;
+        const bool last = s == n_steps - 1;
+        bd_step(pc, pp, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
+                last, &vx, &vy, &w, first ? prv.ang[gi] : pp.an);
+        if (last) {
+          st.vel[gi] = vx;
+          st.vel[M + gi] = vy;
+          st.vel[2 * M + gi] = 0.0f;
+          st.omega[gi] = w;
+        }
+      }
+      lqx[i] = pp.qx;  // the sort of the next sub-step reads lqx/lqy after a barrier
+      lqy[i] = pp.qy;
+      lix[i] = pp.ix;
+      liy[i] = pp.iy;
+      lan[i] = pp.an;
+    }
+#ifdef SWARM_PHASE_TIMING
+    __syncthreads();
+    if (tid == 0) t_force += __builtin_amdgcn_s_memtime() - tA;
+#endif
+    if (sd_mode) {
+      if (!__syncthreads_or(any)) break;
+    } else {
+      __syncthreads();
+    }
+  }
+#ifdef SWARM_PHASE_TIMING
+  if (tid == 0) {
+    g_global_phase[0] = t_sort;
+    g_global_phase[1] = t_force;
+    g_global_phase[2] = (uint64_t)n_steps;
+  }
+#endif
+  __syncthreads();
+  for (int i = tid; i < N; i += T) {
+    const size_t gi = base + i;
+    st.q[gi] = lqx[i];
+    st.q[M + gi] = lqy[i];
+    st.img[gi] = lix[i];
+    st.img[M + gi] = liy[i];
+    st.ang[gi] = lan[i];
+  }
+}
+
+// Advance the device noise counter once every workgroup of the launch has
+// read it (the last arriving workgroup does it).
+__device__ __forceinline__ void advance_counter(uint64_t* step_ctr, uint32_t* arrive,
+                                                uint64_t step0, int n_steps) {
+  if (threadIdx.x == 0) {
+    const uint32_t ticket = atomicAdd(arrive, 1u);
+    if (ticket == gridDim.x - 1) {
+      step_ctr[kCtlStep] = step0 + (uint64_t)n_steps;
+      step_ctr[kCtlWin] += 1ull;  // window counter (noise table parity)
+      *arrive = 0u;
+    }
+  }
+}
+
+// Global-path launch: n_steps sub-steps (or SD steps) of every env.
+__global__ __launch_bounds__(1024) void k_global(const Derived* __restrict__ d, DevState st,
+                                                 Scratch sc, int n_steps,
+                                                 uint64_t* __restrict__ step_ctr,
+                                                 uint32_t* __restrict__ arrive, int lx, int ly,
+                                                 int sd_mode, float g, float md) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ PairTables pt;
+  stage_pair_tables(d, &pt);
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
+  int32_t* cnt = wave_sums + 16;
+  const uint64_t step0 = sd_mode ? 0ull : *step_ctr;
+  // reuse_forces slots: a BD window reads w & 1 and writes the next window's
+  // (w + 1) & 1; steepest descent does not advance the window counter, so it
+  // writes the slot the next window reads
+  const int par = window_parity(step_ctr);
+  // the LDS variant assumes a periodic box (minimum image, folded cells)
+  if (global_lds_extra_words(st.n, st.dims, 1 << (lx + ly)) && blockDim.x == 1024 && d->periodic)
+    block_global_run_lds(d, st, blockIdx.x, n_steps, step0, lx, ly, sd_mode != 0, g, md, cnt,
+                         wave_sums, cnt + (1 << (lx + ly)) + 1, &pt, par);
+  else
+    block_global_run(d, st, sc, blockIdx.x, n_steps, step0, lx, ly, sd_mode != 0, g, md, cnt,
+                     wave_sums, &pt, par);
+  save_forces_env(st, blockIdx.x, sd_mode ? par : par ^ 1);
+  if (!sd_mode) advance_counter(step_ctr, arrive, step0, n_steps);
+}
+
+// ------------------------------------------------------ cluster build
+// Concurrent union-find on LDS: find with path halving (a lane only ever
+// points a node at one of its ancestors), union hooks the larger root under
+// the smaller with CAS, so no cycle can form.
+// The forest always lives in LDS: typed LDS pointers give ds_* operations
+// (a generic volatile pointer compiles to flat accesses that wait on both
+// the vector-memory and the LDS counters).
+typedef __attribute__((address_space(3))) int32_t lds_i32;
+
+__device__ __forceinline__ int uf_find(int32_t* parent_g, int x) {
+  volatile lds_i32* parent = (volatile lds_i32*)(parent_g);
+  while (true) {
+    const int p = parent[x];
+    if (p == x) return x;
+    const int gp = parent[p];
+    if (gp != p) parent[x] = gp;
+    x = gp;
+  }
+}
+
+// The roots of a and b, both walks in lockstep (path halving): each step's
+// two LDS reads are in flight together, so a union costs the longer walk's
+// round trips, not the sum of both.
+__device__ __forceinline__ void uf_find2(int32_t* parent_g, int& a, int& b) {
+  volatile lds_i32* parent = (volatile lds_i32*)(parent_g);
+  int pa = parent[a], pb = parent[b];
+  while (pa != a || pb != b) {
+    const int ga = parent[pa], gb = parent[pb];
+    if (pa != a) {
+      if (ga != pa) parent[a] = ga;
+      a = ga;
+    }
+    if (pb != b) {
+      if (gb != pb) parent[b] = gb;
+      b = gb;
+    }
+    pa = parent[a];
+    pb = parent[b];
+  }
+}
+
+__device__ __forceinline__ void uf_union(int32_t* parent, int a, int b) {
+  while (true) {
+    uf_find2(parent, a, b);
+    if (a == b) return;
+    if (a < b) {
+      const int t = a;
+      a = b;
+      b = t;
+    }
+    if (atomicCAS(&parent[a], a, b) == a) return;
+  }
+}
+
+// The union of a listed pair: its larger index is hooked under the smaller
+// one at once while it is still a root -- one CAS, no walks.  parent[x] <= x
+// holds everywhere (uf_union hooks the larger root, path halving only
+// shortens), so a root may hang under any smaller node without closing a
+// cycle; the component's root stays its smallest index.
+__device__ __forceinline__ void uf_union_pair(int32_t* parent, int a, int b) {
+  const int lo = min(a, b), hi = max(a, b);
+  if (atomicCAS(&parent[hi], hi, lo) == hi) return;
+  uf_union(parent, lo, hi);
+}
+
+// A class counter increment aggregated over the wave: one LDS atomic per
+// wave for its lanes with pred set; returns the lane's rank (the counter's
+// old value + the lanes below it).  The packing's singleton and pair classes
+// otherwise take hundreds (E = 1) to thousands (C5) of same-address atomics,
+// which the LDS executes one after another.
+__device__ __forceinline__ int wave_class_add(int32_t* ctr, bool pred) {
+  const uint64_t m = __ballot(pred);
+  if (m == 0) return 0;
+  const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  const int leader = __builtin_ctzll(m);
+  int base = 0;
+  if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(ctr, __builtin_popcountll(m));
+  base = __shfl(base, leader);
+  return base + below;
+}
+
+// LDS words of k_cluster_build: 168 fixed + per-wave pair counters +
+// parent[N] + 3 N (cluster sizes, bases, slots) + the env's pair list.
+__host__ __device__ inline size_t build_lds_words(int n, int pair_cap) {
+  const int wmax = slots_per_env(n, true) / 64;  // either packing
+  return 16 + 16 + 3 * 68 + (size_t)((wmax + 3) & ~3) + 4 * (size_t)n + (size_t)pair_cap;
+}
+
+// Build step 1, one workgroup per env: counting sort into cells of side
+// >= rc_max + skin (global arrays for the chip-wide pair search).
+// The body runs in the workgroup of env e (k_build_sort, or a workgroup of a
+// fused launch that carries the build along: k_vgrid_sort).
+// CH: particles per thread kept in registers across the scan (4, or 16
+// above 4096).
+template <int CH>
+__device__ __forceinline__ void build_sort_body(const DevState& st, const Scratch& sc, int lx,
+                                                int ly, int e, unsigned char* smem) {
+  const int T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int ncell = 1 << (lx + ly);
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
+  int32_t* cnt = wave_sums + 16;
+  // cell of particle i at (qx, qy): folded positions in a periodic box; in a
+  // non-periodic one a particle outside the box takes the edge cell on its
+  // side (cell_coord, as the global path and the oracle)
+  const bool per = sc.periodic != 0;
+  auto cell_of = [&](int i, uint32_t qx, uint32_t qy) {
+    if (per) return cell_index(qx, qy, lx, ly);
+    return (cell_coord(qy, st.img[M + base + i], ly, false) << lx) |
+           cell_coord(qx, st.img[base + i], lx, false);
+  };
+  SWARM_STAMP(0);
+  // all loads of the cached particles first (one memory latency, not CH)
+  uint32_t cqx[CH], cqy[CH];
+  int32_t cid[CH];
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int i = tid + k * T;
+    const bool ok = i < N;
+    cqx[k] = ok ? st.q[base + i] : 0u;
+    cqy[k] = ok ? st.q[M + base + i] : 0u;
+    cid[k] = ok ? (i | (sc.multi_species ? (int32_t)st.species[i] << 24 : 0)) : -1;
+  }
+  for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
+  if (tid == 0) {
+    sc.gnpairs[e] = 0;
+    sc.gnx[e] = 0;
+    sc.fallback[e] = 0;  // the neighbour-list build sets it on overflow
+  }
+  __syncthreads();
+  SWARM_STAMP(1);
+#pragma unroll
+  for (int k = 0; k < CH; ++k)
+    if (cid[k] >= 0) atomicAdd(&cnt[cell_of(tid + k * T, cqx[k], cqy[k])], 1);
+  for (int i = tid + CH * T; i < N; i += T)
+    atomicAdd(&cnt[cell_of(i, st.q[base + i], st.q[M + base + i])], 1);
+  __syncthreads();
+  SWARM_STAMP(2);
+  block_exclusive_scan(cnt, ncell, wave_sums);
+  __syncthreads();
+  SWARM_STAMP(3);
+  int32_t* cs = sc.bcstart + (size_t)e * (ncell + 1);
+  for (int c = tid; c <= ncell; c += T) cs[c] = cnt[c];
+  __syncthreads();  // cnt is read above and incremented below
+  SWARM_STAMP(4);
+  if (sc.sort_stage_k > 0 && N <= CH * T) {
+    // claim every cached particle's sorted position, then per pass of K
+    // sorted entries scatter the ones that fall in it into LDS (x | y | id
+    // rows after the counts) and write the pass out in order: coalesced
+    // 16-byte stores instead of 3 N scattered 4-byte ones, which one CU
+    // issues at about one lane per cycle (43 k of the 63 k cycles of a
+    // 16384-colloid sort)
+    const int K = sc.sort_stage_k;
+    int spos[CH];
+#pragma unroll
+    for (int k = 0; k < CH; ++k)
+      spos[k] = cid[k] >= 0 ? atomicAdd(&cnt[cell_of(tid + k * T, cqx[k], cqy[k])], 1) : -1;
+    // rows start 16-byte aligned (read as uint4 below): the counts round up
+    // to a multiple of four words (sort_lds_bytes)
+    uint32_t* lx_ = reinterpret_cast<uint32_t*>(cnt + ((ncell + 4) & ~3));
+    uint32_t* ly_ = lx_ + K;
+    int32_t* lid = reinterpret_cast<int32_t*>(ly_ + K);
+    const bool vec = (N & 3) == 0 && (M & 3) == 0 && (K & 3) == 0;
+    for (int p0 = 0; p0 < N; p0 += K) {
+      const int kn = min(K, N - p0);
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {
+        const int r = spos[k] - p0;
+        if (r >= 0 && r < kn) {
+          lx_[r] = cqx[k];
+          ly_[r] = cqy[k];
+          lid[r] = cid[k];
+        }
+      }
+      __syncthreads();
+      if (vec) {
+        uint4* gx = reinterpret_cast<uint4*>(sc.bsq + base + p0);
+        uint4* gy = reinterpret_cast<uint4*>(sc.bsq + M + base + p0);
+        int4* gi = reinterpret_cast<int4*>(sc.bsid + base + p0);
+        for (int v = tid; v < (kn >> 2); v += T) {
+          gx[v] = reinterpret_cast<const uint4*>(lx_)[v];
+          gy[v] = reinterpret_cast<const uint4*>(ly_)[v];
+          gi[v] = reinterpret_cast<const int4*>(lid)[v];
+        }
+      } else {
+        for (int v = tid; v < kn; v += T) {
+          sc.bsq[base + p0 + v] = lx_[v];
+          sc.bsq[M + base + p0 + v] = ly_[v];
+          sc.bsid[base + p0 + v] = lid[v];
+        }
+      }
+      __syncthreads();  // the rows are refilled by the next pass
+    }
+    for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
+    SWARM_STAMP(5);
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    if (cid[k] < 0) continue;
+    const size_t pos = base + atomicAdd(&cnt[cell_of(tid + k * T, cqx[k], cqy[k])], 1);
+    sc.bsq[pos] = cqx[k];
+    sc.bsq[M + pos] = cqy[k];
+    sc.bsid[pos] = cid[k];
+  }
+  for (int i = tid + CH * T; i < N; i += T) {
+    const uint32_t qx = st.q[base + i], qy = st.q[M + base + i];
+    const size_t pos = base + atomicAdd(&cnt[cell_of(i, qx, qy)], 1);
+    sc.bsq[pos] = qx;
+    sc.bsq[M + pos] = qy;
+    sc.bsid[pos] = i | (sc.multi_species ? (int32_t)st.species[i] << 24 : 0);
+  }
+  // idle wave slots of the next run (k_cluster_build writes the used ones);
+  // last, so the stores drain in the shadow of the scatter
+  for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
+  SWARM_STAMP(5);
+}
+
+// Chip-wide 2-D build sort of large envs (N > 4096 outside the ride-along
+// launches): the one-workgroup counting sort keeps 16 particles per thread
+// going through every phase on one CU (21 us at 16384 colloids).  Here
+// k_sort_count ranks every particle in its cell with a global atomic (one
+// thread per particle), k_sort_scan (one workgroup per env) turns the
+// counts into the cell starts and clears them for the next build, and
+// k_sort_scatter writes every particle to its sorted entry.  Same output as
+// k_build_sort (bsq, bsid, bcstart, the reset counters and slots); the
+// entries of one cell come in atomic order, which nothing depends on (the
+// decomposition never changes the integrated bits).
+__device__ __forceinline__ int build_cell_of(const DevState& st, const Scratch& sc, size_t M,
+                                             size_t gi, uint32_t qx, uint32_t qy, int lx, int ly) {
+  if (sc.periodic) return cell_index(qx, qy, lx, ly);
+  return (cell_coord(qy, st.img[M + gi], ly, false) << lx) | cell_coord(qx, st.img[gi], lx, false);
+}
+
+__global__ __launch_bounds__(256) void k_sort_count(DevState st, Scratch sc, int lx, int ly) {
+  const int e = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x, N = st.n;
+  if (i >= N) return;
+  const size_t M = (size_t)st.m, gi = (size_t)e * N + i;
+  const int c = build_cell_of(st, sc, M, gi, st.q[gi], st.q[M + gi], lx, ly);
+  sc.gcell[gi] = c;
+  sc.grank[gi] = atomicAdd(&sc.gcnt[((size_t)e << (lx + ly)) + c], 1);
+}
+
+__global__ __launch_bounds__(1024) void k_sort_scan(Scratch sc, int lx, int ly) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);
+  int32_t* cnt = wave_sums + 16;
+  const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x;
+  const int ncell = 1 << (lx + ly);
+  int32_t* g = sc.gcnt + ((size_t)e << (lx + ly));
+  // the counts into LDS, kB loads in flight per thread (one memory latency
+  // per kB cells, not per cell), then the next build's counters zeroed
+  constexpr int kB = 16;
+  for (int c0 = tid; c0 < ncell; c0 += kB * T) {
+    int32_t v[kB];
+#pragma unroll
+    for (int u = 0; u < kB; ++u) v[u] = c0 + u * T < ncell ? g[c0 + u * T] : 0;
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      if (c0 + u * T < ncell) {
+        cnt[c0 + u * T] = v[u];
+        g[c0 + u * T] = 0;
+      }
+    }
+  }
+  if (tid == 0) {
+    sc.gnpairs[e] = 0;
+    sc.gnx[e] = 0;
+    sc.fallback[e] = 0;  // the neighbour-list build sets it on overflow
+  }
+  for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
+  __syncthreads();
+  block_exclusive_scan(cnt, ncell, wave_sums);
+  __syncthreads();
+  int32_t* cs = sc.bcstart + (size_t)e * (ncell + 1);
+  for (int c = tid; c <= ncell; c += T) cs[c] = cnt[c];
+}
+
+__global__ __launch_bounds__(256) void k_sort_scatter(DevState st, Scratch sc, int lx, int ly) {
+  const int e = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x, N = st.n;
+  if (i >= N) return;
+  const size_t M = (size_t)st.m, base = (size_t)e * N, gi = base + i;
+  const int ncell = 1 << (lx + ly);
+  const size_t pos = base + sc.bcstart[(size_t)e * (ncell + 1) + sc.gcell[gi]] + sc.grank[gi];
+  sc.bsq[pos] = st.q[gi];
+  sc.bsq[M + pos] = st.q[M + gi];
+  sc.bsid[pos] = i | (sc.multi_species ? (int32_t)st.species[i] << 24 : 0);
+}
+
+template <int CH>
+__global__ __launch_bounds__(1024) void k_build_sort(DevState st, Scratch sc, int lx, int ly) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  build_sort_body<CH>(st, sc, lx, ly, blockIdx.x, smem);
+}
+
+// Build step 2, chip-wide (grid.y = env, one thread per sorted entry): every
+// pair within r_i + r_j + skin once (i < j).  A stencil row (cells x-1..x+1)
+// is one contiguous sorted range, plus a wrap range at the grid edge.  The
+// six range bounds are loaded together and candidates four at a time (a few
+// memory latencies per thread, not one per candidate); up to kKeep pairs per
+// thread stay in registers, one atomic per wave reserves the output, and a
+// wave with a denser thread rescans to write.
+// Body for block bx of env e (k_build_pairs: grid (ceil(N / blockDim), E);
+// fused launches pass their own block index); nb2: a block-shared table.
+// kLocal (= sc.local_uf, a compile-time variant so that the plain pair
+// search carries none of the local union-find's code or registers).
+template <bool kLocal = false>
+__device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, const DevState& st,
+                                                 const Scratch& sc, int lx, int ly, int bx, int e,
+                                                 float* nb2, int32_t* uf) {
+  constexpr int kKeep = 8;
+  for (int k = threadIdx.x; k < kMaxSpecies * kMaxSpecies; k += blockDim.x) nb2[k] = d->nb2[k];
+  const int N = st.n;
+  const int T = blockDim.x, t = threadIdx.x;
+  const int lo = bx * T;  // this block's sorted entries [lo, lo + T)
+  const int ps = lo + t;
+  const bool valid = ps < N;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int ncell = 1 << (lx + ly);
+  const int32_t* gcs = sc.bcstart + (size_t)e * (ncell + 1);
+  // the sorted records (x, y, id) and cell starts
+  auto QX = [&](int j) -> uint32_t { return sc.bsq[base + j]; };
+  auto QY = [&](int j) -> uint32_t { return sc.bsq[M + base + j]; };
+  auto SID = [&](int j) -> int32_t { return sc.bsid[base + j]; };
+  auto CS = [&](int c) -> int32_t { return gcs[c]; };
+  const int ncx = 1 << lx, ncy = 1 << ly;
+  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  // non-periodic box (d->periodic == 0): edge cells, no wrap of the stencil,
+  // unwrapped pair distances (pair_disp) -- a pair near across the box edge
+  // only in the folded sense must not be listed
+  const bool per = d->periodic != 0;
+  int pk = 0, i = 0;
+  uint32_t qx = 0, qy = 0;
+  int32_t ix = 0, iy = 0;
+  if (valid) {
+    pk = SID(ps);
+    i = pk & 0xffffff;
+    qx = QX(ps);
+    qy = QY(ps);
+    if (!per) {
+      ix = st.img[base + i];
+      iy = st.img[M + base + i];
+    }
+  }
+  const int c0 = per ? cell_index(qx, qy, lx, ly)
+                     : (cell_coord(qy, iy, ly, false) << lx) | cell_coord(qx, ix, lx, false);
+  const int cx = c0 & (ncx - 1), cy = c0 >> lx;
+  const int xa = ncx >= 3 ? max(cx - 1, 0) : 0;
+  const int xb = ncx >= 3 ? min(cx + 1, ncx - 1) : ncx - 1;
+  const int xw = ncx >= 3 && per ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
+  int rb[6], re[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const int oy = loy + (r >> 1), part = r & 1;
+    const bool use = valid && oy <= hiy && (part == 0 || xw >= 0) &&
+                     (per || (cy + oy >= 0 && cy + oy < ncy));
+    const int row = ((cy + oy + ncy) & (ncy - 1)) << lx;
+    const int c_lo = row | (part == 0 ? xa : xw), c_hi = row | (part == 0 ? xb : xw);
+    rb[r] = use ? CS(c_lo) : 0;
+    re[r] = use ? CS(c_hi + 1) : 0;
+  }
+  __syncthreads();  // nb2
+  const float* nb2_row = nb2 + (pk >> 24) * kMaxSpecies;
+  int found = 0;
+  uint32_t keep[kKeep];
+#pragma unroll
+  for (int v = 0; v < kKeep; ++v) keep[v] = 0u;
+  // the six ranges as one flat candidate index f in [0, total), record
+  // jj = f + off[r] of the range r holding f: kFly candidates in flight per
+  // iteration whatever the split over the ranges (about 11 candidates at
+  // area fraction 0.1: two rounds of loads, not one per range; 16 in
+  // flight measured slower, 4096 colloids)
+  constexpr int kFly = 8;
+  int off[6], pre[7];
+  pre[0] = 0;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    off[r] = rb[r] - pre[r];
+    pre[r + 1] = pre[r] + (re[r] - rb[r]);
+  }
+  const int total = pre[6];
+  for (int f0 = 0; f0 < total; f0 += kFly) {
+    int pk4[kFly], jj4[kFly];
+    uint32_t x4[kFly], y4[kFly];
+#pragma unroll
+    for (int u = 0; u < kFly; ++u) {
+      const int f = f0 + u;
+      int o = off[0];
+#pragma unroll
+      for (int r = 1; r < 6; ++r) o = f >= pre[r] ? off[r] : o;
+      const int jj = f + o;
+      const bool ok = f < total;
+      jj4[u] = jj;
+      pk4[u] = ok ? SID(jj) : -1;
+      x4[u] = ok ? QX(jj) : 0u;
+      y4[u] = ok ? QY(jj) : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kFly; ++u) {
+      if (pk4[u] < 0) continue;
+      const int j = pk4[u] & 0xffffff;
+      const float rx = per ? (float)(int32_t)(x4[u] - qx) * sx0
+                           : pair_disp(x4[u], st.img[base + j], qx, ix, sx0, false);
+      const float ry = per ? (float)(int32_t)(y4[u] - qy) * sx1
+                           : pair_disp(y4[u], st.img[M + base + j], qy, iy, sx1, false);
+      if (i < j && rx * rx + ry * ry < nb2_row[pk4[u] >> 24]) {
+        // j, and (kLocal) for a partner inside this block's sorted range its
+        // block slot + 1 (a pair the block unions itself)
+        const int ls = jj4[u] - lo;
+        const uint32_t kv =
+            (uint32_t)j | (kLocal && ls >= 0 && ls < T ? (uint32_t)(ls + 1) << 16 : 0u);
+#pragma unroll
+        for (int v = 0; v < kKeep; ++v) keep[v] = found == v ? kv : keep[v];
+        ++found;
+      }
+    }
+  }
+  const int lane = threadIdx.x & 63;
+  const bool dense = __any(found > kKeep);  // a lane kept only kKeep: the wave rescans
+  if constexpr (!kLocal) {  // the pair list only (every pair unioned by the build)
+    int v = found;
+    v = wave_incl_scan(v);
+    int wbase = 0;
+    uint32_t* out = sc.gplist + (size_t)e * sc.pair_cap;
+    const int cap = sc.pair_cap;
+    if (lane == 63) wbase = atomicAdd(&sc.gnpairs[e], v);
+    wbase = __builtin_amdgcn_readlane(wbase, 63);
+    const int my_off = wbase + v - found;
+    if (!dense) {
+#pragma unroll
+      for (int u = 0; u < kKeep; ++u) {
+        const int k = my_off + u;
+        if (u < found && k < cap) out[k] = (uint32_t)i | ((keep[u] & 0xffffu) << 16);
+      }
+      return;
+    }
+    int w = 0;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      for (int jj = rb[r]; jj < re[r]; ++jj) {
+        const int packed = SID(jj);
+        const int j = packed & 0xffffff;
+        const float rx = per ? (float)(int32_t)(QX(jj) - qx) * sx0
+                             : pair_disp(QX(jj), st.img[base + j], qx, ix, sx0, false);
+        const float ry = per ? (float)(int32_t)(QY(jj) - qy) * sx1
+                             : pair_disp(QY(jj), st.img[M + base + j], qy, iy, sx1, false);
+        if (i < j && rx * rx + ry * ry < nb2_row[packed >> 24]) {
+          const int k = my_off + w;
+          if (k < cap) out[k] = (uint32_t)i | ((uint32_t)j << 16);
+          ++w;
+        }
+      }
+    }
+    return;
+  }
+  // Block-local union-find of the pairs whose both ends are in this block
+  // (LDS only; done before any global store is issued, so the block
+  // barriers below wait for LDS operations and not for store write-backs).
+  int32_t* lpar = uf;       // [T] block-local union-find over the block's entries
+  int32_t* lid = uf + T;    // [T] particle of a block slot
+  lpar[t] = t;
+  lid[t] = valid ? i : -1;
+  __syncthreads();
+  if (!dense) {
+#pragma unroll
+    for (int u = 0; u < kKeep; ++u)
+      if (u < found && (keep[u] >> 16) != 0u) uf_union(lpar, t, (int)(keep[u] >> 16) - 1);
+  }
+  __syncthreads();
+  // the local root, and in the upper half the pairs this particle found
+  // (as the lower id: each pair once) -- the cluster build's pair count per
+  // cluster without another pass over the pair list
+  if (valid) sc.lroot[base + i] = lid[uf_find(lpar, t)] | (min(found, 0xffff) << 16);
+  // wave prefix sums, one atomic per wave: every pair to the pair list, the
+  // pairs whose partner lies outside the block (all of a dense wave's) also
+  // to the cross list
+  int nx = 0;
+  if (!dense) {
+#pragma unroll
+    for (int u = 0; u < kKeep; ++u) nx += u < found && (keep[u] >> 16) == 0u ? 1 : 0;
+  } else {
+    nx = found;
+  }
+  int v = found, vx = nx;
+  v = wave_incl_scan(v);
+  vx = wave_incl_scan(vx);
+  int wbase = 0, xbase = 0;
+  if (lane == 63) {
+    wbase = atomicAdd(&sc.gnpairs[e], v);
+    xbase = atomicAdd(&sc.gnx[e], vx);
+  }
+  wbase = __builtin_amdgcn_readlane(wbase, 63);
+  xbase = __builtin_amdgcn_readlane(xbase, 63);
+  const int my_off = wbase + v - found;
+  const int my_xoff = xbase + vx - nx;
+  uint32_t* out = sc.gplist + (size_t)e * sc.pair_cap;
+  uint32_t* xout = sc.xpairs + (size_t)e * sc.pair_cap;
+  if (!dense) {
+    int w = 0;
+#pragma unroll
+    for (int u = 0; u < kKeep; ++u) {
+      const int k = my_off + u;
+      const uint32_t j = keep[u] & 0xffffu;
+      if (u < found && k < sc.pair_cap) out[k] = (uint32_t)i | (j << 16);
+      if (u < found && (keep[u] >> 16) == 0u) {
+        if (my_xoff + w < sc.pair_cap) xout[my_xoff + w] = (uint32_t)i | (j << 16);
+        ++w;
+      }
+    }
+    return;
+  }
+  // a lane found more than kKeep pairs: rescan and write in order
+  int w = 0;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    for (int jj = rb[r]; jj < re[r]; ++jj) {
+      const int packed = SID(jj);
+      const int j = packed & 0xffffff;
+      const float rx = per ? (float)(int32_t)(QX(jj) - qx) * sx0
+                           : pair_disp(QX(jj), st.img[base + j], qx, ix, sx0, false);
+      const float ry = per ? (float)(int32_t)(QY(jj) - qy) * sx1
+                           : pair_disp(QY(jj), st.img[M + base + j], qy, iy, sx1, false);
+      if (i < j && rx * rx + ry * ry < nb2_row[packed >> 24]) {
+        const int k = my_off + w;
+        if (k < sc.pair_cap) out[k] = (uint32_t)i | ((uint32_t)j << 16);
+        if (my_xoff + w < sc.pair_cap) xout[my_xoff + w] = (uint32_t)i | ((uint32_t)j << 16);
+        ++w;
+      }
+    }
+  }
+}
+
+template <bool kLocal>
+__global__ __launch_bounds__(256) void k_build_pairs(const Derived* __restrict__ d, DevState st,
+                                                     Scratch sc, int lx, int ly) {
+  __shared__ float nb2[kMaxSpecies * kMaxSpecies];
+  __shared__ int32_t uf[2 * 256];
+  build_pairs_body<kLocal>(d, st, sc, lx, ly, blockIdx.x, blockIdx.y, nb2, uf);
+}
+
+// The packing class v whose free-lane range holds singleton rank r < nfree:
+// the largest v >= 2 with freebase[v] <= r (its range is non-empty).
+// freebase[2..65] is non-decreasing and freebase[65] = nfree > r, so v - 1 =
+// #{u in [2, 65]: freebase[u] <= r}: counted in two rounds of eight
+// independent LDS reads (every 8th entry, then the eight from the last of
+// those <= r) -- two LDS latencies where a binary search waits for six.
+__device__ __forceinline__ int free_class(const int32_t* freebase, int r) {
+  int k8 = -1;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) k8 += freebase[2 + 8 * q] <= r ? 1 : 0;
+  int v = 1 + 8 * k8;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v += freebase[2 + 8 * k8 + q] <= r ? 1 : 0;
+  return v;
+}
+
+// LDS words of the large-N variant: the union-find forest only.
+__host__ __device__ inline size_t build_lds_words_big(int n) {
+  const int wmax = slots_per_env(n, true) / 64;  // either packing
+  return 16 + 16 + 3 * 68 + (size_t)((wmax + 3) & ~3) + (size_t)n;
+}
+
+// Build step 3, one workgroup per env: union-find over the pair list
+// (connected components = clusters), packing of the clusters into 64-lane
+// wave slots that never straddle a wave, per-wave pair lists.  kBig: the
+// cluster sizes, bases, slots and the pair list stay in global memory (N
+// too large for them in LDS); the forest is always in LDS.
+// kCopy: the pair list (found pairs) is copied from sc.gplist into LDS;
+// otherwise (!kBig) it is in LDS already (k_build_env).
+template <bool kBig, bool kCopy, bool kLocal = false>
+__device__ __forceinline__ void cluster_build_env(const DevState& st, const Scratch& sc, int e,
+                                                  unsigned char* smem, int found) {
+  const int T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t base = (size_t)e * N;
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);  // 16
+  int32_t* misc = wave_sums + 16;                          // 16: 0 flag, 1 waves
+  int32_t* classcnt = misc + 16;                           // 68
+  int32_t* wavebase = classcnt + 68;                       // 68
+  int32_t* freebase = wavebase + 68;                       // 68
+  const int wmax = sc.wmax;
+  int32_t* wave_np = freebase + 68;                        // wmax (padded)
+  int32_t* parent = wave_np + ((wmax + 3) & ~3);           // N
+  const size_t M = (size_t)st.m;
+  int32_t* csz = kBig ? sc.gclus + base : parent + N;              // N
+  int32_t* cbase = kBig ? sc.gclus + M + base : parent + 2 * N;    // N
+  int32_t* lslot = kBig ? sc.gclus + 2 * M + base : parent + 3 * N;  // N
+  uint32_t* plist = kBig ? sc.gplist + (size_t)e * sc.pair_cap
+                         : reinterpret_cast<uint32_t*>(parent + 4 * N);  // pair_cap
+  const int S = sc.S;
+  // kFused (LDS forest): the root walks also count the cluster sizes;
+  // kCount: the union sweep counts each particle's pairs (as the lower index)
+  // in lslot, and the root walks add them to their cluster -- no separate
+  // sweep over the pair list for the one-pass pair counts
+  constexpr bool kFused = !kBig;
+  constexpr bool kCount = kFused && !kLocal;
+  SWARM_STAMP(6);
+  const int npairs = min(found, sc.pair_cap);
+  // kLocal: the pair search's blocks unioned their own pairs already
+  // (sc.lroot: a forest of depth one), only the cross-block pairs remain
+  const int nx = kLocal ? sc.gnx[e] : 0;
+  const uint32_t* xl = sc.xpairs + (size_t)e * sc.pair_cap;
+  for (int k = tid; k < 68; k += T) classcnt[k] = 0;
+  for (int k = tid; k < wmax; k += T) wave_np[k] = 0;
+  // overflow of the pair or cross list -> global path
+  if (tid < 16) misc[tid] = tid == 0 && (found > sc.pair_cap || nx > sc.pair_cap) ? 1 : 0;
+  for (int i = tid; i < N; i += T) {
+    if (kLocal) {
+      const uint32_t l = (uint32_t)sc.lroot[base + i];
+      parent[i] = (int32_t)(l & 0xffffu);
+      lslot[i] = (int32_t)(l >> 16);  // the member's pair count, until its rank replaces it
+    } else {
+      parent[i] = i;
+      if (kCount) lslot[i] = 0;
+    }
+    csz[i] = 0;
+    cbase[i] = 0;  // pair count of a cluster (one-pass packing), then its base
+  }
+  if (!kBig && kCopy) {  // pair list into LDS, four loads in flight per thread
+    const uint32_t* gp = sc.gplist + (size_t)e * sc.pair_cap;
+    for (int k0 = tid; k0 < npairs; k0 += 4 * T) {
+      uint32_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = k0 + u * T < npairs ? gp[k0 + u * T] : 0u;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (k0 + u * T < npairs) plist[k0 + u * T] = v[u];
+    }
+  }
+  __syncthreads();
+  SWARM_STAMP(11);
+  // kBig: the arrays below live in global memory, so every loop issues its
+  // loads / atomics kU at a time before using them -- one memory latency per
+  // kU iterations, not one per iteration.  (In LDS, kU = 4 measured no
+  // better than 1 at E = 1: the union phase 1 k cycles shorter, the
+  // others longer.)
+  constexpr int kU = kBig ? 8 : 1;
+  // The pair sweeps visit the LDS pair list in a spread order: neighbouring
+  // pairs of the cell-sorted list usually share a cluster, so lanes of one
+  // wave taking consecutive pairs contend on the same root / wave counter
+  // (LDS atomics to one address serialise, union-find CAS retries).  Sweep
+  // index k maps to pair (k mod 64) R + k / 64, R = ceil(npairs / 64): the
+  // lanes of a wave take pairs R apart (phase stamps: the union phase was
+  // 16 k cycles of k_cluster_build's 46 k at E = 1).  kBig keeps the
+  // identity (its list is in global memory, read kU at a time).
+  const int spread_r = (npairs + 63) >> 6;
+  const int nsweep = kBig ? npairs : 64 * spread_r;
+  auto sweep_pair = [&](int k) { return kBig ? k : (k & 63) * spread_r + (k >> 6); };
+  // (the union sweep reads its pairs four at a time even in LDS: the
+  // unions are serial per thread, the list reads need not be)
+  constexpr int kUU = kU > 4 ? kU : 4;
+  if (kLocal) {  // the cross-block pairs only (global memory, few)
+    const int nxc = min(nx, sc.pair_cap);
+    for (int k0 = tid; k0 < nxc; k0 += kUU * T) {
+      uint32_t pr[kUU];
+#pragma unroll
+      for (int u = 0; u < kUU; ++u) pr[u] = k0 + u * T < nxc ? xl[k0 + u * T] : 0u;
+#pragma unroll
+      for (int u = 0; u < kUU; ++u)
+        if (k0 + u * T < nxc) uf_union(parent, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
+    }
+  } else {
+    for (int k0 = tid; k0 < nsweep; k0 += kUU * T) {
+      uint32_t pr[kUU];
+      bool ok[kUU];
+#pragma unroll
+      for (int u = 0; u < kUU; ++u) {
+        const int pk = sweep_pair(k0 + u * T);
+        ok[u] = k0 + u * T < nsweep && pk < npairs;
+        pr[u] = ok[u] ? plist[pk] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kUU; ++u)
+        if (ok[u]) {
+          if (kCount && sc.one_pass) atomicAdd(&lslot[pr[u] & 0xffffu], 1);
+          uf_union_pair(parent, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
+        }
+    }
+  }
+  __syncthreads();
+  SWARM_STAMP(7);
+  // every particle points at its root (two walks in lockstep per thread);
+  // in LDS each walk's end counts its member at once (cluster sizes, the
+  // member's rank in lslot): the roots are final after the union sweep, and
+  // a walk that passes a member pointed at its root by another thread still
+  // ends at the same root -- one barrier and one pass over parent[] fewer
+  for (int i = tid; i < N; i += 2 * T) {
+    const bool two = i + T < N;
+    int a = i, b = two ? i + T : i;
+    const int npa = kFused && (kLocal || kCount) ? lslot[i] : 0;
+    const int npb = kFused && (kLocal || kCount) && two ? lslot[i + T] : 0;
+    uf_find2(parent, a, b);
+    parent[i] = a;
+    if (two) parent[i + T] = b;
+    if (kFused) {
+      const int ra = atomicAdd(&csz[a], 1);
+      const int rb = two ? atomicAdd(&csz[b], 1) : 0;
+      lslot[i] = ra;
+      if (two) lslot[i + T] = rb;
+      if ((kLocal || kCount) && sc.one_pass) {
+        if (npa > 0) atomicAdd(&cbase[a], npa);
+        if (npb > 0) atomicAdd(&cbase[b], npb);
+      }
+    }
+  }
+  __syncthreads();
+  if (!kFused)
+  for (int i0 = tid; i0 < N; i0 += kU * T) {
+    int32_t r[kU], np_u[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) np_u[u] = kLocal && i0 + u * T < N ? lslot[i0 + u * T] : 0;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) r[u] = i0 + u * T < N ? atomicAdd(&csz[parent[i0 + u * T]], 1) : 0;
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (i0 + u * T < N) lslot[i0 + u * T] = r[u];
+    if (kLocal && sc.one_pass) {  // the cluster's pairs: the members' counts of the pair search
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (np_u[u] > 0) atomicAdd(&cbase[parent[i0 + u * T]], np_u[u]);
+    }
+  }
+  if (!kLocal && !kCount && sc.one_pass)
+    for (int k0 = tid; k0 < nsweep; k0 += kU * T) {
+      uint32_t pr[kU];
+      bool ok[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int pk = sweep_pair(k0 + u * T);
+        ok[u] = k0 + u * T < nsweep && pk < npairs;
+        pr[u] = ok[u] ? plist[pk] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (ok[u]) atomicAdd(&cbase[parent[pr[u] & 0xffffu]], 1);
+    }
+  __syncthreads();
+  // Lanes reserved per cluster (its packing class w): its size s, or with
+  // one-pass packing max(s, min(pairs, 64, 2 s)), so that the clusters of a
+  // wave have at most 64 pairs (one pair pass per sub-step) unless a cluster
+  // is denser than 2 pairs per particle.  Results do not depend on it.
+  for (int i0 = tid; i0 < N; i0 += kU * T) {
+    int32_t sz[kU], pc[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * T;
+      const bool root = i < N && parent[i] == i;
+      sz[u] = root ? csz[i] : 0;
+      pc[u] = root ? cbase[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * T;
+      const bool root = i < N && parent[i] == i;
+      const int s = sz[u];
+      const int w = sc.one_pass ? max(s, min(min(pc[u], 64), 2 * s)) : s;
+      // one LDS atomic per root (measured, 4096 colloids: the wave-aggregated
+      // counters of the packed build cost this one-workgroup build ~0.9 us,
+      // cluster build 16.7 -> 15.8 us without them)
+      if (!root) continue;
+      if (s > 64) {  // wider than a wave: a big cluster, run by k_check's workgroup
+        atomicAdd(&misc[4], s);
+        cbase[i] = kBigMark;
+      } else {
+        csz[i] = w;
+        cbase[i] = atomicAdd(&classcnt[w], 1);
+      }
+    }
+  }
+  __syncthreads();
+  SWARM_STAMP(8);
+  // -> global path (3-D: any big cluster; its run is 2-D only).  misc[0]
+  // (list overflow) and misc[4] are final here, so every thread decides
+  // alike, with no barrier for a flag
+  if (misc[0] || misc[4] > min(kBigMax, (int)blockDim.x) || (st.dims == 3 && misc[4] > 0)) {
+    if (tid == 0) {
+      sc.fallback[e] = 1;
+      sc.env_waves[e] = 0;
+      sc.big_n[e] = 0;
+      sc.big_np[e] = 0;
+    }
+    return;
+  }
+  // Waves per class.  The tail lanes a class leaves free in its waves
+  // (64 - per * w in a full wave, more in its last one) take the singletons
+  // first; only the rest of them get waves of their own (fewer, fuller
+  // waves: the run kernel's cost is per wave).
+  if (tid < 64) {
+    const int w = tid + 1;
+    const int per = udiv_small(64, w);
+    const int cnt = classcnt[w];
+    int32_t nw = udiv_small(cnt + per - 1, per);
+    int32_t fl = 0;
+    if (w >= 2 && nw > 0) fl = (nw - 1) * (64 - per * w) + (64 - (cnt - (nw - 1) * per) * w);
+    int32_t f = fl;
+    f = wave_incl_scan(f);
+    freebase[w] = f - fl;
+    const int32_t F = sc.fill_singletons ? __builtin_amdgcn_readlane(f, 63) : 0;
+    if (w == 1) nw = (max(cnt - F, 0) + 63) / 64;
+    int32_t v = nw;
+    v = wave_incl_scan(v);
+    wavebase[w] = v - nw;
+    if (tid == 63) {
+      misc[1] = v;
+      misc[3] = F;
+      freebase[65] = F;
+    }
+  }
+  __syncthreads();
+  // Every particle's slot in one pass: its cluster's base (from the root's
+  // class and class rank, worked out by each member for itself -- no pass
+  // that stores the bases and no barrier before the members read them) plus
+  // its rank in the cluster.
+  const int nfree = misc[3];
+  for (int i0 = tid; i0 < N; i0 += kU * T) {
+    int32_t rt[kU], ls[kU], sz[kU], rk[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * T;
+      rt[u] = i < N ? parent[i] : 0;
+      ls[u] = i < N ? lslot[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * T;
+      sz[u] = i < N ? csz[rt[u]] : 0;
+      rk[u] = i < N ? cbase[rt[u]] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * T;
+      if (i >= N) continue;
+      const int root = rt[u], s = sz[u], r = rk[u];
+      int slot;
+      if (r == kBigMark) {  // big-cluster member m: slot -1 - m
+        const int m = atomicAdd(&misc[5], 1);
+        sc.big_list[(size_t)e * kBigMax + m] = i;
+        slot = -1 - m;
+      } else {
+        int cb;
+        if (s == 1 && r < nfree) {
+          // the class v whose free-lane range holds r, then wave j and lane
+          const int v = free_class(freebase, r);
+          const int per = udiv_small(64, v);
+          const int nw = udiv_small(classcnt[v] + per - 1, per);
+          const int ffull = 64 - per * v;
+          const int t = r - freebase[v];
+          int j, lane;
+          if (t < (nw - 1) * ffull) {
+            j = udiv_small(t, ffull);
+            lane = per * v + (t - j * ffull);
+          } else {
+            j = nw - 1;
+            lane = (classcnt[v] - (nw - 1) * per) * v + (t - (nw - 1) * ffull);
+          }
+          cb = (wavebase[v] + j) * 64 + lane;
+        } else if (s == 1) {
+          const int r2 = r - nfree;
+          cb = (wavebase[1] + r2 / 64) * 64 + r2 % 64;
+        } else {
+          const int per = udiv_small(64, s), rq = udiv_small(r, per);
+          cb = (wavebase[s] + rq) * 64 + (r - rq * per) * s;
+        }
+        slot = cb + ls[u];
+        sc.perm[(size_t)e * S + slot] = i;
+      }
+      lslot[i] = slot;
+      sc.slot_of[base + i] = slot;
+      sc.root[base + i] = root;
+    }
+  }
+  __syncthreads();
+  SWARM_STAMP(9);
+  // per-wave pair lists (both particles of a pair share a cluster, so a wave)
+  for (int k0 = tid; k0 < nsweep; k0 += kU * T) {
+   uint32_t prs[kU];
+   bool okp[kU];
+#pragma unroll
+   for (int u = 0; u < kU; ++u) {
+     const int pk = sweep_pair(k0 + u * T);
+     okp[u] = k0 + u * T < nsweep && pk < npairs;
+     prs[u] = okp[u] ? plist[pk] : 0u;
+   }
+   int32_t sis[kU], sjs[kU];
+#pragma unroll
+   for (int u = 0; u < kU; ++u) {
+     sis[u] = lslot[prs[u] & 0xffffu];
+     sjs[u] = lslot[prs[u] >> 16];
+   }
+#pragma unroll
+   for (int u = 0; u < kU; ++u) {
+    if (!okp[u]) continue;
+    const uint32_t pr = prs[u];
+    const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
+    const int si = sis[u], sj = sjs[u];
+    const uint32_t spp =
+        sc.multi_species ? (uint32_t)(st.species[i] * kMaxSpecies + st.species[j]) : 0u;
+    if (si < 0) {  // a big cluster's pair (both members of it)
+      const int idx = atomicAdd(&misc[6], 1);
+      if (idx < kBigPairs)
+        sc.big_pairs[(size_t)e * kBigPairs + idx] =
+            (uint32_t)(-1 - si) | ((uint32_t)(-1 - sj) << 10) | (spp << 20);
+      else
+        misc[2] = 1;  // -> global path
+      continue;
+    }
+    const int wv = si >> 6;
+    const int idx = atomicAdd(&wave_np[wv], 1);
+    if (idx < kPairsPerWave)
+      sc.pairs[((size_t)e * wmax + wv) * kPairsPerWave + idx] =
+          (uint32_t)(si & 63) | ((uint32_t)(sj & 63) << 6) | (spp << 12);
+    else
+      misc[2] = 1;  // a wave with more than kPairsPerWave pairs
+   }
+  }
+  __syncthreads();
+  SWARM_STAMP(10);
+  for (int w = tid; w < misc[1]; w += T)
+    sc.wave_npairs[(size_t)e * wmax + w] = min(wave_np[w], kPairsPerWave);
+  if (tid == 0) {
+    sc.env_waves[e] = misc[2] ? 0 : misc[1];
+    sc.fallback[e] = misc[2] ? 1 : 0;
+    sc.big_n[e] = misc[5];
+    sc.big_np[e] = min(misc[6], kBigPairs);
+  }
+}
+
+// LDS words of the packed large-N build: two words per particle (N < 65536).
+__host__ __device__ inline size_t build_lds_words_packed(int n) {
+  const int wmax = slots_per_env(n, true) / 64;
+  return 16 + 16 + 3 * 68 + (size_t)((wmax + 3) & ~3) + 2 * (size_t)n;
+}
+
+// The large-N build (same result as cluster_build_env<true, false>) with
+// its per-particle and per-cluster arrays packed into two LDS words per
+// particle instead of global memory (whose returning atomics and dependent
+// loads cost ~3x LDS per element from one CU):
+//   A[i]: union-find parent; then root | rank << 16 (rank = i's lane within
+//         its cluster); then i's wave slot;
+//   B[r]: for a root r, size | pairs << 16 (atomic counters, no carry:
+//         size < 2^16); then class rank | w << 24; then the cluster's first
+//         slot (or kBigMark).
+// The pair list stays in global memory (read kU at a time).
+template <bool kLocal>
+__device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, int e,
+                                         unsigned char* smem, int found) {
+  const int T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t base = (size_t)e * N;
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);  // 16
+  int32_t* misc = wave_sums + 16;                          // 16: 0 flag, 1 waves
+  int32_t* classcnt = misc + 16;                           // 68
+  int32_t* wavebase = classcnt + 68;                       // 68
+  int32_t* freebase = wavebase + 68;                       // 68
+  const int wmax = sc.wmax;
+  int32_t* wave_np = freebase + 68;                        // wmax (padded)
+  int32_t* A = wave_np + ((wmax + 3) & ~3);                // N
+  int32_t* B = A + N;                                      // N
+  const uint32_t* plist = sc.gplist + (size_t)e * sc.pair_cap;
+  const int S = sc.S;
+  constexpr int kU = 8;
+  SWARM_STAMP(6);
+  const int npairs = min(found, sc.pair_cap);
+  // kLocal: start from the pair search's block-local forest, union the
+  // cross-block pairs only (cluster_build_env)
+  const int nx = kLocal ? sc.gnx[e] : 0;
+  const int nun = kLocal ? min(nx, sc.pair_cap) : npairs;
+  const uint32_t* ulist = kLocal ? sc.xpairs + (size_t)e * sc.pair_cap : plist;
+  for (int k = tid; k < 68; k += T) classcnt[k] = 0;
+  for (int k = tid; k < wmax; k += T) wave_np[k] = 0;
+  // overflow of the pair or cross list -> global path
+  if (tid < 16) misc[tid] = tid == 0 && (found > sc.pair_cap || nx > sc.pair_cap) ? 1 : 0;
+  // kLocal: the members' pair counts of the pair search, kept in registers
+  // from here to the size pass (same particles per thread; N <= kPer T)
+  constexpr int kPer = 20;
+  int32_t np_k[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int i = tid + k * T;
+    np_k[k] = 0;
+    if (i < N) {
+      const uint32_t l = kLocal ? (uint32_t)sc.lroot[base + i] : (uint32_t)i;
+      A[i] = (int32_t)(l & 0xffffu);
+      np_k[k] = (int32_t)(l >> 16);
+      B[i] = 0;
+    }
+  }
+  for (int i = tid + kPer * T; i < N; i += T) {  // beyond kPer T: no pair counts kept
+    A[i] = kLocal ? (sc.lroot[base + i] & 0xffff) : i;
+    B[i] = 0;
+  }
+  __syncthreads();
+  for (int k0 = tid; k0 < nun; k0 += kU * T) {
+    uint32_t pr[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) pr[u] = k0 + u * T < nun ? ulist[k0 + u * T] : 0u;
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (k0 + u * T < nun) uf_union(A, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
+  }
+  __syncthreads();
+  SWARM_STAMP(7);
+  for (int i = tid; i < N; i += T) A[i] = uf_find(A, i);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int i = tid + k * T;
+    if (i < N) {
+      const int root = A[i];
+      // size, and (kLocal) the member's pair count of the pair search
+      const int np_i = kLocal && sc.one_pass ? np_k[k] : 0;
+      const uint32_t r = (uint32_t)atomicAdd(&B[root], 1 + (np_i << 16)) & 0xffffu;
+      A[i] = root | (int32_t)(r << 16);
+    }
+  }
+  for (int i = tid + kPer * T; i < N; i += T) {
+    const int root = A[i];
+    const int np_i = kLocal && sc.one_pass ? (int)((uint32_t)sc.lroot[base + i] >> 16) : 0;
+    const uint32_t r = (uint32_t)atomicAdd(&B[root], 1 + (np_i << 16)) & 0xffffu;
+    A[i] = root | (int32_t)(r << 16);
+  }
+  if (!kLocal && sc.one_pass)
+    for (int k0 = tid; k0 < npairs; k0 += kU * T) {
+      uint32_t pr[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) pr[u] = k0 + u * T < npairs ? plist[k0 + u * T] : 0u;
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (k0 + u * T < npairs) {
+          // the root of the pair's first particle: A holds root | rank << 16
+          // of particles whose rank is already stored, root otherwise
+          const int a = (int)(pr[u] & 0xffffu);
+          atomicAdd(&B[A[a] & 0xffff], 1 << 16);
+        }
+    }
+  __syncthreads();
+  // lanes reserved per cluster (cluster_build_env): class w, class rank
+  for (int i = tid; i < N; i += T) {
+    const bool root = (A[i] & 0xffff) == i;  // roots only
+    const uint32_t b = root ? (uint32_t)B[i] : 0u;
+    const int s = (int)(b & 0xffffu), pairs = (int)(b >> 16);
+    const int w = sc.one_pass ? max(s, min(min(pairs, 64), 2 * s)) : s;
+    // the two most frequent classes by one atomic per wave
+    const int r1 = wave_class_add(&classcnt[1], root && s <= 64 && w == 1);
+    const int r2 = wave_class_add(&classcnt[2], root && s <= 64 && w == 2);
+    if (!root) continue;
+    if (s > 64) {  // wider than a wave: a big cluster, run by k_check's workgroup
+      atomicAdd(&misc[4], s);
+      B[i] = kBigMark;
+    } else {
+      B[i] = (w == 1 ? r1 : (w == 2 ? r2 : atomicAdd(&classcnt[w], 1))) | (w << 24);
+    }
+  }
+  __syncthreads();
+  SWARM_STAMP(8);
+  // -> global path (3-D: any big cluster; its run is 2-D only)
+  if (tid == 0 && (misc[4] > min(kBigMax, (int)blockDim.x) || (st.dims == 3 && misc[4] > 0)))
+    misc[0] = 1;
+  __syncthreads();
+  if (misc[0]) {
+    if (tid == 0) {
+      sc.fallback[e] = 1;
+      sc.env_waves[e] = 0;
+      sc.big_n[e] = 0;
+      sc.big_np[e] = 0;
+    }
+    return;
+  }
+  if (tid < 64) {  // waves per class (cluster_build_env)
+    const int w = tid + 1;
+    const int per = udiv_small(64, w);
+    const int cnt = classcnt[w];
+    int32_t nw = udiv_small(cnt + per - 1, per);
+    int32_t fl = 0;
+    if (w >= 2 && nw > 0) fl = (nw - 1) * (64 - per * w) + (64 - (cnt - (nw - 1) * per) * w);
+    int32_t f = fl;
+    f = wave_incl_scan(f);
+    freebase[w] = f - fl;
+    const int32_t F = sc.fill_singletons ? __builtin_amdgcn_readlane(f, 63) : 0;
+    if (w == 1) nw = (max(cnt - F, 0) + 63) / 64;
+    int32_t v = nw;
+    v = wave_incl_scan(v);
+    wavebase[w] = v - nw;
+    if (tid == 63) {
+      misc[1] = v;
+      misc[3] = F;
+      freebase[65] = F;
+    }
+  }
+  __syncthreads();
+  const int nfree = misc[3];
+  for (int i = tid; i < N; i += T) {
+    if ((A[i] & 0xffff) != i) continue;
+    const int32_t b = B[i];
+    if (b == kBigMark) continue;
+    const int s = (b >> 24) & 0x7f;
+    const int r = b & 0xffffff;
+    int cb;
+    if (s == 1 && r < nfree) {
+      const int v = free_class(freebase, r), per = udiv_small(64, v);
+      const int nw = udiv_small(classcnt[v] + per - 1, per);
+      const int ffull = 64 - per * v;
+      const int t = r - freebase[v];
+      int j, lane;
+      if (t < (nw - 1) * ffull) {
+        j = udiv_small(t, ffull);
+        lane = per * v + (t - j * ffull);
+      } else {
+        j = nw - 1;
+        lane = (classcnt[v] - (nw - 1) * per) * v + (t - (nw - 1) * ffull);
+      }
+      cb = (wavebase[v] + j) * 64 + lane;
+    } else if (s == 1) {
+      const int r2 = r - nfree;
+      cb = (wavebase[1] + r2 / 64) * 64 + r2 % 64;
+    } else {
+      const int per = udiv_small(64, s), rq = udiv_small(r, per);
+      cb = (wavebase[s] + rq) * 64 + (r - rq * per) * s;
+    }
+    B[i] = cb;
+  }
+  __syncthreads();
+  for (int i = tid; i < N; i += T) {
+    const int32_t a = A[i];
+    const int root = a & 0xffff;
+    const int rank = (int)((uint32_t)a >> 16);
+    const int32_t cb = B[root];
+    int slot;
+    if (cb == kBigMark) {  // big-cluster member m: slot -1 - m
+      const int m = atomicAdd(&misc[5], 1);
+      sc.big_list[(size_t)e * kBigMax + m] = i;
+      slot = -1 - m;
+    } else {
+      slot = cb + rank;
+      sc.perm[(size_t)e * S + slot] = i;
+    }
+    sc.slot_of[base + i] = slot;
+    sc.root[base + i] = root;
+    A[i] = slot;  // only this thread reads A[i] in this loop
+  }
+  __syncthreads();
+  SWARM_STAMP(9);
+  for (int k0 = tid; k0 < npairs; k0 += kU * T) {
+    uint32_t prs[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) prs[u] = k0 + u * T < npairs ? plist[k0 + u * T] : 0u;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (k0 + u * T >= npairs) continue;
+      const uint32_t pr = prs[u];
+      const int i = (int)(pr & 0xffffu), j = (int)(pr >> 16);
+      const int si = A[i], sj = A[j];
+      const uint32_t spp =
+        sc.multi_species ? (uint32_t)(st.species[i] * kMaxSpecies + st.species[j]) : 0u;
+      if (si < 0) {  // a big cluster's pair (both members of it)
+        const int idx = atomicAdd(&misc[6], 1);
+        if (idx < kBigPairs)
+          sc.big_pairs[(size_t)e * kBigPairs + idx] =
+              (uint32_t)(-1 - si) | ((uint32_t)(-1 - sj) << 10) | (spp << 20);
+        else
+          misc[2] = 1;  // -> global path
+        continue;
+      }
+      const int wv = si >> 6;
+      const int idx = atomicAdd(&wave_np[wv], 1);
+      if (idx < kPairsPerWave)
+        sc.pairs[((size_t)e * wmax + wv) * kPairsPerWave + idx] =
+            (uint32_t)(si & 63) | ((uint32_t)(sj & 63) << 6) | (spp << 12);
+      else
+        misc[2] = 1;  // a wave with more than kPairsPerWave pairs
+    }
+  }
+  __syncthreads();
+  SWARM_STAMP(10);
+  for (int w = tid; w < misc[1]; w += T)
+    sc.wave_npairs[(size_t)e * wmax + w] = min(wave_np[w], kPairsPerWave);
+  if (tid == 0) {
+    sc.env_waves[e] = misc[2] ? 0 : misc[1];
+    sc.fallback[e] = misc[2] ? 1 : 0;
+    sc.big_n[e] = misc[5];
+    sc.big_np[e] = min(misc[6], kBigPairs);
+  }
+}
+
+template <bool kLocal>
+__global__ __launch_bounds__(1024) void k_cluster_build_packed(DevState st, Scratch sc) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  cluster_build_env_packed<kLocal>(st, sc, blockIdx.x, smem, sc.gnpairs[blockIdx.x]);
+}
+
+// kLocal: after the 2-D pair search (block-local forests + cross list)
+template <bool kBig, bool kLocal>
+__global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  cluster_build_env<kBig, !kBig, kLocal>(st, sc, blockIdx.x, smem, sc.gnpairs[blockIdx.x]);
+}
+
+// Words of k_build_env's sort/search region (wave sums, cell ends, sorted
+// x, y, id), which must fit below the pair list of the build's LDS layout.
+__host__ __device__ inline size_t build_env_sort_words(int n, int ncell) {
+  return 16 + (size_t)((ncell + 2) & ~1) + 3 * (size_t)n;
+}
+
+// The whole build of one env in one workgroup, LDS-resident (no global
+// intermediates, one launch): counting sort of the positions into cells of
+// side >= rc_max + skin, the pair search over the sorted LDS copy (every pair
+// within r_i + r_j + skin once, straight into the LDS pair list), then
+// union-find and packing (cluster_build_env).  Same pair set as
+// k_build_sort -> k_build_pairs -> k_cluster_build, in one launch and without
+// their global round trips.
+__global__ __launch_bounds__(1024) void k_build_env(const Derived* __restrict__ d, DevState st,
+                                                    Scratch sc, int lx, int ly) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ float nb2[kMaxSpecies * kMaxSpecies];
+  __shared__ int32_t npair;
+  constexpr int CH = 4;   // particles per thread kept in registers across the scan
+  constexpr int kKeep = 8;
+  const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int ncell = 1 << (lx + ly);
+  const int ncx = 1 << lx, ncy = 1 << ly;
+  int32_t* ws = reinterpret_cast<int32_t*>(smem);
+  int32_t* cnt = ws + 16;  // counts, then exclusive starts, then cell ends
+  // sorted positions as (x, y) pairs (one 8-byte LDS read per candidate),
+  // then the ids; cnt padded to 8-byte alignment
+  uint2* lq = reinterpret_cast<uint2*>(cnt + ((ncell + 2) & ~1));
+  int32_t* lid = reinterpret_cast<int32_t*>(lq + N);
+  const int wmax = sc.wmax;
+  uint32_t* plist = reinterpret_cast<uint32_t*>(smem) +
+                    (16 + 16 + 3 * 68 + ((wmax + 3) & ~3) + 4 * (size_t)N);
+  SWARM_STAMP(0);
+  uint32_t cqx[CH], cqy[CH];
+  int32_t cid[CH];
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int i = tid + k * T;
+    const bool ok = i < N;
+    cqx[k] = ok ? st.q[base + i] : 0u;
+    cqy[k] = ok ? st.q[M + base + i] : 0u;
+    cid[k] = ok ? (i | ((int32_t)st.species[i] << 24)) : -1;
+  }
+  for (int k = tid; k < kMaxSpecies * kMaxSpecies; k += T) nb2[k] = d->nb2[k];
+  for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
+  if (tid == 0) npair = 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < CH; ++k)
+    if (cid[k] >= 0) atomicAdd(&cnt[cell_index(cqx[k], cqy[k], lx, ly)], 1);
+  for (int i = tid + CH * T; i < N; i += T)
+    atomicAdd(&cnt[cell_index(st.q[base + i], st.q[M + base + i], lx, ly)], 1);
+  __syncthreads();
+  block_exclusive_scan(cnt, ncell, ws);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    if (cid[k] < 0) continue;
+    const int pos = atomicAdd(&cnt[cell_index(cqx[k], cqy[k], lx, ly)], 1);
+    lq[pos] = make_uint2(cqx[k], cqy[k]);
+    lid[pos] = cid[k];
+  }
+  for (int i = tid + CH * T; i < N; i += T) {
+    const uint32_t qx = st.q[base + i], qy = st.q[M + base + i];
+    const int pos = atomicAdd(&cnt[cell_index(qx, qy, lx, ly)], 1);
+    lq[pos] = make_uint2(qx, qy);
+    lid[pos] = i | ((int32_t)st.species[i] << 24);
+  }
+  // idle wave slots of the next run (the packing writes the used ones)
+  for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
+  __syncthreads();  // cnt[c] = end of cell c = start of cell c + 1
+  SWARM_STAMP(1);
+  // pair search: a stencil row (cells x-1..x+1) is one contiguous sorted
+  // range, plus a wrap range at the grid edge
+  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const int lane = tid & 63;
+  for (int ps0 = 0; ps0 < N; ps0 += T) {  // uniform trip count: whole waves
+    const int ps = ps0 + tid;
+    const bool valid = ps < N;
+    int pk = 0, i = 0;
+    uint32_t qx = 0, qy = 0;
+    if (valid) {
+      pk = lid[ps];
+      i = pk & 0xffffff;
+      const uint2 q = lq[ps];
+      qx = q.x;
+      qy = q.y;
+    }
+    const int c0 = cell_index(qx, qy, lx, ly);
+    const int cx = c0 & (ncx - 1), cy = c0 >> lx;
+    const int xa = ncx >= 3 ? max(cx - 1, 0) : 0;
+    const int xb = ncx >= 3 ? min(cx + 1, ncx - 1) : ncx - 1;
+    const int xw = ncx >= 3 ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
+    int rb[6], re[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const int oy = loy + (r >> 1), part = r & 1;
+      const bool use = valid && oy <= hiy && (part == 0 || xw >= 0);
+      const int row = ((cy + oy + ncy) & (ncy - 1)) << lx;
+      const int c_lo = row | (part == 0 ? xa : xw), c_hi = row | (part == 0 ? xb : xw);
+      rb[r] = use ? (c_lo > 0 ? cnt[c_lo - 1] : 0) : 0;
+      re[r] = use ? cnt[c_hi] : 0;
+    }
+    const float* nb2_row = nb2 + (pk >> 24) * kMaxSpecies;
+    int found = 0;
+    uint32_t keep[kKeep];
+#pragma unroll
+    for (int v = 0; v < kKeep; ++v) keep[v] = 0u;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      for (int jj0 = rb[r]; jj0 < re[r]; jj0 += 4) {  // four candidates' loads in flight
+        int pk4[4];
+        uint32_t x4[4], y4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int jj = min(jj0 + u, N - 1);
+          pk4[u] = jj0 + u < re[r] ? lid[jj] : -1;
+          const uint2 q = lq[jj];
+          x4[u] = q.x;
+          y4[u] = q.y;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (pk4[u] < 0) continue;
+          const int j = pk4[u] & 0xffffff;
+          const float rx = (float)(int32_t)(x4[u] - qx) * sx0;
+          const float ry = (float)(int32_t)(y4[u] - qy) * sx1;
+          if (i < j && rx * rx + ry * ry < nb2_row[pk4[u] >> 24]) {
+#pragma unroll
+            for (int v = 0; v < kKeep; ++v) keep[v] = found == v ? (uint32_t)j : keep[v];
+            ++found;
+          }
+        }
+      }
+    }
+    // wave prefix sum, one LDS atomic per wave
+    int v = found;
+    v = wave_incl_scan(v);
+    int wbase = 0;
+    if (lane == 63) wbase = atomicAdd(&npair, v);
+    wbase = __builtin_amdgcn_readlane(wbase, 63);
+    const int my_off = wbase + v - found;
+    if (!__any(found > kKeep)) {
+#pragma unroll
+      for (int u = 0; u < kKeep; ++u) {
+        const int k = my_off + u;
+        if (u < found && k < sc.pair_cap) plist[k] = (uint32_t)i | (keep[u] << 16);
+      }
+    } else {  // a lane found more than kKeep pairs: rescan and write in order
+      int w = 0;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        for (int jj = rb[r]; jj < re[r]; ++jj) {
+          const int pkj = lid[jj];
+          const int j = pkj & 0xffffff;
+          const uint2 q = lq[jj];
+          const float rx = (float)(int32_t)(q.x - qx) * sx0;
+          const float ry = (float)(int32_t)(q.y - qy) * sx1;
+          if (i < j && rx * rx + ry * ry < nb2_row[pkj >> 24]) {
+            const int k = my_off + w;
+            if (k < sc.pair_cap) plist[k] = (uint32_t)i | ((uint32_t)j << 16);
+            ++w;
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  SWARM_STAMP(2);
+  const int found = npair;
+  __syncthreads();  // the sort region is reused by the union-find arrays
+  cluster_build_env<false, false>(st, sc, e, smem, found);
+}
+
+// -------------------------------------------------------- cluster run
+// Orders one wave's LDS accesses (DS operations of a wave execute in order;
+// this keeps the compiler from moving them across).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Noise table for latency-bound windows (few waves per SIMD): the normals of
+// every (sub-step, particle) computed ahead of the run.  Indexed by particle,
+// not wave slot, so it does not wait for the cluster build.
+// Particle-major: particle gi's sub-steps
+// are one contiguous run of 12-B records, table[(gi * kMaxWindow + s) * 3 +
+// c], so a lane reads its sub-step's three normals with one 12-B load and a
+// 128-B line (~10 sub-steps of one particle) is fetched by the one XCD that
+// runs the particle.  The step-major layout, table[(s * 3 + c) * M + gi],
+// shares each line among 32 particles spread over every XCD, so each XCD's
+// L2 fetched its own copy (rocprof FETCH ~ 7-8 x the table).
+// Two tables, by window parity: the wide run kernel fills the next window's
+// on otherwise idle CUs while it reads this one's.  The control block
+// records each table's first step and length; a run whose window does not
+// match its table draws the normals itself.
+__host__ __device__ inline size_t noise_table_words(size_t M) { return (size_t)kMaxWindow * 3 * M; }
+// word of normal c of sub-step s of particle gi; the step and component strides
+__host__ __device__ inline size_t noise_index(size_t M, size_t gi, int s, int c) {
+  (void)M;
+  return (gi * kMaxWindow + (size_t)s) * 3 + (size_t)c;
+}
+__host__ __device__ inline size_t noise_step_stride(size_t) { return 3; }
+__host__ __device__ inline size_t noise_comp_stride(size_t) { return 1; }
+
+// Group k of a table starting at step_start: sub-steps t = 4 (g0 + k) + j
+// (g0 = step_start / 4) of particle gi, those within [start, start + len).
+// One thread draws the group's three Philox blocks (StepNoise).
+__device__ __forceinline__ void noise_group(const Derived* __restrict__ d, const DevState& st,
+                                            uint64_t step_start, int len,
+                                            float* __restrict__ table, long gi, int k) {
+  const long M = st.m;
+  const int e = (int)(gi / st.n);
+  const int i = (int)(gi - (long)e * st.n);
+  const uint64_t t0 = (step_start & ~3ull) + 4ull * (uint64_t)k;
+  const size_t cs = noise_comp_stride((size_t)M);
+  StepNoise sn;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float g[3];
+    sn.next(d->key0, d->key1 ^ (uint32_t)e, (uint32_t)i, t0 + (uint64_t)j, j == 0, g);
+    const long s = (long)(t0 + (uint64_t)j) - (long)step_start;
+    if (s >= 0 && s < len) {
+      float* o = table + noise_index((size_t)M, (size_t)gi, (int)s, 0);
+      o[0] = g[0];
+      o[cs] = g[1];
+      o[2 * cs] = g[2];
+    }
+  }
+}
+
+// Work item k of a table fill over M particles x G groups: consecutive
+// items are the consecutive groups of one particle (the stores of a wave
+// then cover contiguous records).
+__device__ __forceinline__ void noise_item(long k, long M, int G, long* gi, int* grp) {
+  (void)M;
+  *gi = k / G;
+  *grp = (int)(k - *gi * G);
+}
+
+__host__ __device__ inline int noise_groups(int len) { return len / 4 + 2; }  // any alignment
+
+// This window's table of len sub-steps (grid.y = noise_groups(len)) from the
+// current step counter.
+__global__ __launch_bounds__(256) void k_noise(const Derived* __restrict__ d, DevState st,
+                                               uint64_t* __restrict__ ctl,
+                                               float* __restrict__ tables, int len) {
+  const long M = st.m;
+  const int par = window_parity(ctl);
+  const uint64_t step0 = ctl[kCtlStep];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    ctl[kCtlTStep + par] = step0;
+    ctl[kCtlTLen + par] = (uint64_t)len;
+  }
+  const int G = noise_groups(len);
+  const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= M * G) return;
+  long gi;
+  int grp;
+  noise_item(k, M, G, &gi, &grp);
+  noise_group(d, st, step0, len, tables + par * noise_table_words(M), gi, grp);
+}
+
+// One wave of the cluster run: all n_steps sub-steps of the particles in
+// its 64 slots.  kTable: the normals come from this window's noise table
+// (prefetched one sub-step ahead), else they are drawn here.
+// kMulti = false: one species, so the pair constants are wave-uniform scalars.
+// kTwoPass: waves with 65-128 pairs get their own unrolled two-pass variant
+// (else the general up-to-four-pass loop).
+template <bool kMulti, bool kTable, bool kWalls, bool kTwoPass = false>
+__device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const DevState& st,
+                                         const Scratch& sc, int n_envs, int n_steps,
+                                         uint64_t step0, const float* __restrict__ table,
+                                         int gw, int lane, uint2* lpos_w,
+                                         unsigned long long* lacc_x, unsigned long long* lacc_y,
+                                         const PairTables& pt, int par) {
+  const int e = gw / sc.wmax;
+  const int w = gw - e * sc.wmax;
+  if (e >= n_envs) return;
+  if (sc.fallback[e] != 0 || w >= sc.env_waves[e]) return;
+#ifdef SWARM_PHASE_TIMING
+  const uint64_t t_wave0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  const int N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int slot = w * 64 + lane;
+  const int i = sc.perm[(size_t)e * sc.S + slot];
+  const bool active = i >= 0;
+  PState p = {0u, 0u, 0u, 0, 0};
+  int si = 0;
+  // fs, tz: this sub-step's swim force and torque -- for sub-step 0 with
+  // reuse_forces the previous run's (the current ones are loaded after it)
+  float fs = 0.0f, tz = 0.0f, fex = 0.0f, fey = 0.0f;
+  uint32_t an0 = 0u;  // orientation of sub-step 0's swim force
+  const size_t gi = base + (active ? i : 0);
+  if (active) {
+    p.qx = st.q[gi];
+    p.qy = st.q[M + gi];
+    p.ix = st.img[gi];
+    p.iy = st.img[M + gi];
+    p.an = st.ang[gi];
+    si = st.species[i];
+    const PrevSlot prv = prev_slot(st, par);  // reuse_forces: this window's slot
+    fs = st.reuse ? prv.f[gi] : st.f_swim[gi];
+    tz = st.reuse ? prv.tz[gi] : st.torque_z[gi];
+    an0 = st.reuse ? prv.ang[gi] : p.an;
+    fex = st.f_ext[gi];
+    fey = st.f_ext[M + gi];
+    // window-start snapshot for k_check's exact test and re-run (taken here,
+    // not by the build, so a build may run ahead of the slice's actions)
+    sc.bq[gi] = p.qx;
+    sc.bq[M + gi] = p.qy;
+    sc.bimg[gi] = p.ix;
+    sc.bimg[M + gi] = p.iy;
+    sc.bang[gi] = p.an;
+  }
+  // this wave's neighbour pairs: one per lane and pass (wave-uniform count)
+  const int np = sc.wave_npairs[(size_t)e * sc.wmax + w];
+  const int npass = (np + 63) >> 6;
+  const uint32_t* pw = sc.pairs + ((size_t)e * sc.wmax + w) * kPairsPerWave;
+  // the first pass's pair stays in a register; a wave with more passes
+  // (rare: a cluster denser than 2 pairs per particle) reloads the others
+  // from L2 each sub-step, so they do not hold registers for the run
+  const uint32_t pr0 = lane < np ? pw[lane] : 0xffffffffu;
+  // two passes (a cluster with more than 64 pairs: 65-128 in the wave): the
+  // second pass's pair in a register too, and both passes unrolled so their
+  // LDS reads and force arithmetic interleave (C5: such a wave set the
+  // launch's duration in a third of the windows, 1.7x a one-pass wave)
+  const uint32_t pr1 = npass == 2 && 64 + lane < np ? pw[64 + lane] : 0xffffffffu;
+  lacc_x[lane] = 0ull;
+  lacc_y[lane] = 0ull;
+  const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const float eps24 = d->eps24;
+  // one species: its constants are wave-uniform (scalar registers)
+  const PConst pc = load_pconst(d, kMulti ? si : 0);
+  const float cut2_0 = d->cut2[0], sig6_0 = d->sig6[0];
+  const uint32_t q0x = p.qx, q0y = p.qy;
+  float dmax2 = 0.0f;
+  float vx = 0.0f, vy = 0.0f, om = 0.0f;
+  const size_t tstep = noise_step_stride(M), ts = noise_comp_stride(M);
+  const float* tcol = kTable ? table + noise_index(M, gi, 0, 0) : nullptr;
+  float gn[3] = {0.0f, 0.0f, 0.0f};
+  StepNoise noise;  // !kTable: the window's normals drawn here, group by group
+  if (kTable) {  // idle lanes read particle 0's (never stored)
+    gn[0] = tcol[0];
+    gn[1] = tcol[ts];
+    gn[2] = tcol[2 * ts];
+  }
+#ifdef SWARM_PHASE_TIMING
+  const bool stamp = e == 0 && w == sc.env_waves[e] - 1 && lane == 0;
+  uint64_t t_pairs = 0, t_read = 0, t_bd = 0, t0s = 0, t1s = 0;
+#endif
+  // The rotation and the director do not depend on the forces: each
+  // sub-step turns the angle and computes the next sub-step's director while
+  // its force sums are in flight in LDS (software-pipelined director).
+  // A lone wave pays for every taken branch, so the sub-step is branch-lean:
+  // the pass count (0, 1 or up to 4) and the last sub-step (velocities) are
+  // compile-time variants, and idle lanes compute along (never stored).
+  float dir[2];
+  sincos_turn(an0, &dir[0], &dir[1]);
+  auto substep = [&](const int s, auto last_t, auto pass_t) __attribute__((always_inline)) {
+    constexpr bool kLast = decltype(last_t)::value;
+    constexpr int kPass = decltype(pass_t)::value;  // 0, 1, 2 or 4: up to npass
+#ifdef SWARM_PHASE_TIMING
+    if (stamp) t0s = t1s = __builtin_amdgcn_s_memtime();
+#endif
+    float gt[3] = {gn[0], gn[1], gn[2]};
+    if (kTable && !kLast) {  // the next sub-step's normals, one sub-step ahead
+      const float* nx = tcol + (size_t)(s + 1) * tstep;
+      gn[0] = nx[0];
+      gn[1] = nx[ts];
+      gn[2] = nx[2 * ts];
+    }
+    if (!kTable && pc.noisy) noise.next(k0, k1, (uint32_t)i, step0 + (uint64_t)s, s == 0, gt);
+    int64_t ax = 0, ay = 0;
+    if (kPass > 0) {
+      lpos_w[lane] = make_uint2(p.qx, p.qy);
+      wave_lds_sync();
+      for (int q = 0; q < (kPass == 1 ? 1 : (kPass == 2 ? 2 : npass)); ++q) {
+        {  // wave-uniform; an empty slot names the lane twice
+          const uint32_t e_ = q == 0 ? pr0
+                                     : (kPass == 2 ? pr1
+                                                   : (q * 64 + lane < np ? pw[q * 64 + lane]
+                                                                         : 0xffffffffu));
+          const int a = e_ == 0xffffffffu ? lane : (int)(e_ & 63u);
+          const int b = e_ == 0xffffffffu ? lane : (int)((e_ >> 6) & 63u);
+          const uint2 pa = lpos_w[a], pb = lpos_w[b];
+          const float rx = (float)(int32_t)(pb.x - pa.x) * sx0;
+          const float ry = (float)(int32_t)(pb.y - pa.y) * sx1;
+          int64_t fx, fy;  // on a; b receives exactly the negation
+          if (kMulti) {
+            const int sp = (int)((e_ >> 12) & 255u);
+            pair_fix_sel(pt.cut2[sp], pt.sig6[sp], eps24, rx, ry, fx, fy);
+          } else {
+            pair_fix_sel(cut2_0, sig6_0, eps24, rx, ry, fx, fy);
+          }
+          atomicAdd(&lacc_x[a], (unsigned long long)fx);
+          atomicAdd(&lacc_y[a], (unsigned long long)fy);
+          // b: the exact negation (written as a subtract; the compiler still
+          // emits ds_add_u64 of the negated value)
+          atomicSub(&lacc_x[b], (unsigned long long)fx);
+          atomicSub(&lacc_y[b], (unsigned long long)fy);
+        }
+      }
+    }
+    // rotation (bd_step's sequence) and the next director, between the
+    // force-sum atomics and their read-back
+    __builtin_amdgcn_sched_barrier(0);
+    float dnext[2] = {dir[0], dir[1]};
+    float dth = tz * pc.rot_dt;
+    if (pc.noisy) dth = dth + pc.sig_r * gt[2];
+    const uint32_t an_next = p.an + (uint32_t)f2i32(dth * kAngInvScale);
+    if (!kLast) sincos_turn(an_next, &dnext[0], &dnext[1]);
+    __builtin_amdgcn_sched_barrier(0);
+    __asm__ volatile("" ::: "memory");  // keep the read-back after the director
+    if (kPass > 0) {
+      wave_lds_sync();
+#ifdef SWARM_PHASE_TIMING
+      if (stamp) {
+        t1s = __builtin_amdgcn_s_memtime();
+        t_pairs += t1s - t0s;
+      }
+#endif
+      ax = (int64_t)lacc_x[lane];
+      ay = (int64_t)lacc_y[lane];
+      lacc_x[lane] = 0ull;
+      lacc_y[lane] = 0ull;
+#ifdef SWARM_PHASE_TIMING
+      if (stamp) {
+        const uint64_t t2 = __builtin_amdgcn_s_memtime();
+        t_read += t2 - t1s;
+        t1s = t2;
+      }
+#endif
+    }
+    if (kWalls && active) {  // contacts of real particles only
+      int64_t az = 0;
+      wall_forces<2>(d, si, (float)p.qx * sx0, (float)p.qy * sx1, 0.0f, ax, ay, az,
+                     st.wall_viol);
+    }
+    bd_translate(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
+                 kLast, &vx, &vy, &om, gt, dir[0], dir[1]);
+    const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
+    const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
+    // non-negative floats order like their bit patterns: one v_max_u32
+    // (fmaxf adds a canonicalising max)
+    dmax2 = __uint_as_float(max(__float_as_uint(dmax2), __float_as_uint(ddx * ddx + ddy * ddy)));
+    p.an = an_next;
+    if (!kLast) {
+      dir[0] = dnext[0];
+      dir[1] = dnext[1];
+    }
+#ifdef SWARM_PHASE_TIMING
+    if (stamp) t_bd += __builtin_amdgcn_s_memtime() - t1s;
+#endif
+  };
+  auto run_steps = [&](auto pass_t) __attribute__((always_inline)) {
+    int s = 0;
+    if (n_steps > 1) {
+      // sub-step 0 peeled: with reuse_forces it swims with the previous run's
+      // actions, and the current ones are loaded once after it (no register
+      // holds them across the loop)
+      substep(0, std::false_type{}, pass_t);
+      if (st.reuse && active) {
+        fs = st.f_swim[gi];
+        tz = st.torque_z[gi];
+      }
+      if constexpr (kTable) {
+        // two sub-steps per iteration: the next normals load into alternating
+        // registers (no copies) and the scheduler sees across the boundary
+        // (E=1 run 53.9 -> 53.4 us).  Not in the in-kernel-noise variant: at
+        // its 96-VGPR bound the unrolled loop spills 80 B/lane, not 24.
+        for (s = 1; s + 1 < n_steps - 1; s += 2) {
+          substep(s, std::false_type{}, pass_t);
+          substep(s + 1, std::false_type{}, pass_t);
+        }
+        if (s < n_steps - 1) substep(s++, std::false_type{}, pass_t);
+      } else {
+        for (s = 1; s < n_steps - 1; ++s) substep(s, std::false_type{}, pass_t);
+      }
+    }
+    substep(s, std::true_type{}, pass_t);  // velocities of the last sub-step
+  };
+  if (npass == 0)
+    run_steps(std::integral_constant<int, 0>{});
+  else if (npass == 1)
+    run_steps(std::integral_constant<int, 1>{});
+  else if (kTwoPass && npass == 2)
+    run_steps(std::integral_constant<int, 2>{});
+  else
+    run_steps(std::integral_constant<int, 4>{});
+#ifdef SWARM_PHASE_TIMING
+  if (stamp) {
+    sc.phase[16] = t_pairs;
+    sc.phase[17] = t_read;
+    sc.phase[18] = t_bd;
+    sc.phase[19] = (uint64_t)n_steps;
+    sc.phase[20] = (uint64_t)npass;
+  }
+  if (lane == 0) {  // per-wave realtime stamps (100 MHz): entry, end, passes, pairs
+    uint64_t* ws = sc.phase + 32 + 4 * (size_t)gw;
+    ws[0] = t_wave0;
+    ws[1] = __builtin_amdgcn_s_memrealtime();
+    ws[2] = (uint64_t)npass;
+    ws[3] = (uint64_t)np;
+  }
+#endif
+  if (active) {
+    st.q[gi] = p.qx;
+    st.q[M + gi] = p.qy;
+    st.img[gi] = p.ix;
+    st.img[M + gi] = p.iy;
+    st.ang[gi] = p.an;
+    st.vel[gi] = vx;
+    st.vel[M + gi] = vy;
+    st.vel[2 * M + gi] = 0.0f;
+    st.omega[gi] = om;
+    const float disp = sqrt_rn(dmax2);
+    sc.disp[gi] = disp;
+    if (!(disp < 0.5f * d->skin)) {  // a mover (k_check's exact test)
+      const int k = atomicAdd(&sc.nmov[e], 1);
+      if (k < kMaxMovers) sc.movers[(size_t)e * kMaxMovers + k] = i;
+    }
+    if (st.reuse) {  // the next window's sub-step 0 (the other slot)
+      // (fs, tz hold this run's actions unless the window was one sub-step)
+      const PrevSlot w = prev_slot(st, par ^ 1);
+      w.f[gi] = n_steps > 1 ? fs : st.f_swim[gi];
+      w.tz[gi] = n_steps > 1 ? tz : st.torque_z[gi];
+      w.ang[gi] = p.an;
+    }
+  }
+}
+
+// Uniform dispatch to the compile-time variants: normals from a table
+// (table != null) or drawn here; walls or none.
+template <bool kMulti, bool kWalls>
+__device__ __forceinline__ void run_wave_dispatch(const Derived* __restrict__ d, const DevState& st,
+                                                  const Scratch& sc, int n_envs, int n_steps,
+                                                  uint64_t step0, const float* __restrict__ table,
+                                                  int gw, int lane, uint2* lpos_w,
+                                                  unsigned long long* lacc_x,
+                                                  unsigned long long* lacc_y,
+                                                  const PairTables& pt, int par) {
+  if (table)
+    run_wave<kMulti, true, kWalls>(d, st, sc, n_envs, n_steps, step0, table, gw, lane, lpos_w,
+                                   lacc_x, lacc_y, pt, par);
+  else
+    run_wave<kMulti, false, kWalls>(d, st, sc, n_envs, n_steps, step0, nullptr, gw, lane, lpos_w,
+                                    lacc_x, lacc_y, pt, par);
+}
+
+// Launch-duration stamps for measurement (bench.py, swarm_engine_profile
+// under graph capture): tstamp[0] = the earliest block start, tstamp[1] = the
+// latest wave end, realtime clock (100 MHz); null otherwise (one uniform
+// branch per block / wave).
+__device__ __forceinline__ void stamp_start(unsigned long long* tstamp) {
+  if (tstamp && threadIdx.x == 0)
+    atomicMin(&tstamp[2 * (blockIdx.x & (kStampSub - 1))], (unsigned long long)wall_clock64());
+}
+__device__ __forceinline__ void stamp_end(unsigned long long* tstamp) {
+  if (tstamp && (threadIdx.x & 63) == 0)
+    atomicMax(&tstamp[2 * (blockIdx.x & (kStampSub - 1)) + 1], (unsigned long long)wall_clock64());
+}
+
+// XCD-aware placement of per-env work (envs_per_xcd_map: blocks of one env):
+// workgroup b is dispatched to XCD b mod 8 (MI355X_MICROARCH.md: for speed
+// only, nothing depends on it), so the env's blocks are the b with
+// b mod 8 == e mod 8.  All waves of an env then share one XCD's L2: the
+// particle-indexed state lines an env's scattered lanes load and store are
+// fetched and written back by one L2 instead of partial copies in eight.
+// Returns false for a block beyond the last env.
+__device__ __forceinline__ bool xcd_env_block(int b, int blocks_per_env, int n_envs, int* e,
+                                              int* lb) {
+  const int x = b & 7, k = b >> 3;
+  *e = x + 8 * (k / blocks_per_env);
+  *lb = k - (k / blocks_per_env) * blocks_per_env;
+  return *e < n_envs;
+}
+
+// Throughput launch: 256-thread blocks, 4 waves each.  kWalls (host-chosen)
+// keeps the wall-force variant's registers out of the wall-free kernel.
+// xcd_bpe > 0: blocks placed by xcd_env_block with xcd_bpe blocks per env
+// (ceil(wmax / 4)); else block b runs waves 4 b .. 4 b + 3 of the env-major
+// wave list.
+template <bool kMulti, bool kTable, bool kWalls>
+__global__ __launch_bounds__(256, kRunMinBlocks) void k_cluster_run(const Derived* __restrict__ d, DevState st,
+                                                     Scratch sc, int n_envs, int n_steps,
+                                                     const uint64_t* __restrict__ ctl,
+                                                     const float* __restrict__ tables,
+                                                     int xcd_bpe,
+                                                     unsigned long long* __restrict__ tstamp) {
+  __shared__ PairTables pt;
+  __shared__ uint2 lpos[4][64];                  // positions of the block's 4 waves
+  __shared__ unsigned long long lacc[4][2][64];  // int64 force sums (x, y)
+  stamp_start(tstamp);
+  stage_pair_tables(d, &pt);
+  const int par = window_parity(ctl);
+  const uint64_t step0 = ctl[kCtlStep];
+  const bool table_ok = kTable && ctl[kCtlTStep + par] == step0 &&
+                        (uint64_t)n_steps <= ctl[kCtlTLen + par];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (xcd_bpe > 0) {
+    int e, lb;
+    if (!xcd_env_block((int)blockIdx.x, xcd_bpe, n_envs, &e, &lb)) return;
+    const int w = lb * 4 + wv;
+    if (w >= sc.wmax) return;
+    gw = e * sc.wmax + w;
+  }
+  // a table that does not cover this window (the device check; the host
+  // normally guarantees it) -> the normals are drawn in the kernel
+  run_wave_dispatch<kMulti, kWalls>(d, st, sc, n_envs, n_steps, step0,
+                                    table_ok ? tables + par * noise_table_words(st.m) : nullptr,
+                                    gw, lane, lpos[wv], lacc[wv][0], lacc[wv][1], pt, par);
+  stamp_end(tstamp);
+}
+
+// Latency-bound launch (few envs x particles: the run's waves fill few
+// SIMDs): 1024-thread blocks whose dynamic LDS (set by the host) keeps one
+// block per CU.  Blocks [0, nnb) fill the NEXT window's noise table
+// (kMaxWindow sub-steps from this window's end) on CUs the run leaves idle,
+// so no noise kernel sits between the policy and the run; the other blocks
+// run with waves [0, run_wpb) only: one run wave per CU at E = 1 (its
+// scattered noise-table gathers then have the CU's texture path to themselves),
+// up to one per SIMD for more envs.
+template <bool kMulti, bool kWalls>
+__global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __restrict__ d,
+                                                           DevState st, Scratch sc, int n_envs,
+                                                           int n_steps, uint64_t* __restrict__ ctl,
+                                                           float* __restrict__ tables,
+                                                           int n_noise_blocks, int run_wpb,
+                                                           unsigned long long* __restrict__ tstamp) {
+  __shared__ PairTables pt;
+  __shared__ uint2 lpos[4][64];
+  __shared__ unsigned long long lacc[4][2][64];
+  stamp_start(tstamp);
+  stage_pair_tables(d, &pt);
+  const int par = window_parity(ctl);
+  const uint64_t step0 = ctl[kCtlStep];
+  const size_t M = (size_t)st.m;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (b < n_noise_blocks) {
+    const uint64_t start = step0 + (uint64_t)n_steps;
+    if (b == 0 && tid == 0) {
+      ctl[kCtlTStep + (par ^ 1)] = start;
+      ctl[kCtlTLen + (par ^ 1)] = (uint64_t)kMaxWindow;
+    }
+    float* t = tables + (par ^ 1) * noise_table_words(M);
+    const int G = noise_groups(kMaxWindow);
+    const long total = (long)G * (long)M;
+    for (long k = (long)b * blockDim.x + tid; k < total; k += (long)n_noise_blocks * blockDim.x) {
+      long gi;
+      int grp;
+      noise_item(k, (long)M, G, &gi, &grp);
+      noise_group(d, st, start, kMaxWindow, t, gi, grp);
+    }
+    stamp_end(tstamp);
+    return;
+  }
+  const int lane = tid & 63, wv = tid >> 6;
+  const int gw0 = (b - n_noise_blocks) * run_wpb;
+  const bool table_ok = ctl[kCtlTStep + par] == step0 && (uint64_t)n_steps <= ctl[kCtlTLen + par];
+  const float* table = table_ok ? tables + par * noise_table_words(M) : nullptr;
+  if (wv >= run_wpb) return;
+  const int gw = gw0 + wv;
+  run_wave_dispatch<kMulti, kWalls>(d, st, sc, n_envs, n_steps, step0, table, gw, lane, lpos[wv],
+                                    lacc[wv][0], lacc[wv][1], pt, par);
+  stamp_end(tstamp);
+}
+
+// The env's big clusters (wider than a wave) for the window, by k_check's
+// workgroup: one member per thread, the clusters' pairs spread over the
+// threads; per sub-step the members publish their positions, every pair's
+// force goes to both members' int64 sums (LDS atomics, as in the run
+// kernel), then the members take the Brownian step (bd_step, normals drawn
+// here: the same numbers as the noise table).  Writes the window-start
+// snapshot, the final state, velocities and displacements like the run
+// kernel, so k_check's exact test covers the members too.
+// lds: 6 * kBigMax + 2 words (uint2 positions, two u64 force sums).
+__device__ void run_big_clusters(const Derived* __restrict__ d, const DevState& st,
+                                 const Scratch& sc, int e, int n_steps, uint64_t step0,
+                                 int32_t* lds, const PairTables* pt, int par) {
+  const int T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int nm = sc.big_n[e], np = sc.big_np[e];
+  uint2* lp = reinterpret_cast<uint2*>(lds + ((reinterpret_cast<uintptr_t>(lds) >> 2) & 1));
+  unsigned long long* ax = reinterpret_cast<unsigned long long*>(lp + kBigMax);
+  unsigned long long* ay = ax + kBigMax;
+  const bool mem = tid < nm;
+  const int i = mem ? sc.big_list[(size_t)e * kBigMax + tid] : 0;
+  const size_t gi = base + i;
+  PState p = {st.q[gi], st.q[M + gi], st.ang[gi], st.img[gi], st.img[M + gi]};
+  const int si = st.species[i];
+  const float fs = st.f_swim[gi], tz = st.torque_z[gi];
+  // reuse_forces: sub-step 0 takes the previous run's actions and director
+  const PrevSlot prv = prev_slot(st, par);
+  const float fs0 = st.reuse ? prv.f[gi] : fs, tz0 = st.reuse ? prv.tz[gi] : tz;
+  const uint32_t an0 = st.reuse ? prv.ang[gi] : p.an;
+  const float fex = st.f_ext[gi], fey = st.f_ext[M + gi];
+  const PConst pc = load_pconst(d, si);
+  if (mem) {
+    sc.bq[gi] = p.qx;
+    sc.bq[M + gi] = p.qy;
+    sc.bimg[gi] = p.ix;
+    sc.bimg[M + gi] = p.iy;
+    sc.bang[gi] = p.an;
+  }
+  const uint32_t q0x = p.qx, q0y = p.qy;
+  constexpr int kPer = kBigPairs / 1024;  // pairs per thread (blockDim 1024)
+  uint32_t pr[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int k = tid + u * T;
+    pr[u] = k < np ? sc.big_pairs[(size_t)e * kBigPairs + k] : 0u;  // 0: member 0 twice
+  }
+  const uint32_t k0 = d->key0, k1 = d->key1 ^ (uint32_t)e;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const float eps24 = d->eps24;
+  float dmax2 = 0.0f, vx = 0.0f, vy = 0.0f, om = 0.0f;
+  StepNoise noise;
+  if (mem) {
+    ax[tid] = 0ull;
+    ay[tid] = 0ull;
+  }
+  for (int s = 0; s < n_steps; ++s) {
+    if (mem) lp[tid] = make_uint2(p.qx, p.qy);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int a = (int)(pr[u] & 1023u), b = (int)((pr[u] >> 10) & 1023u);
+      const int sp = (int)(pr[u] >> 20);
+      const uint2 pa = lp[a], pb = lp[b];
+      const float rx = (float)(int32_t)(pb.x - pa.x) * sx0;
+      const float ry = (float)(int32_t)(pb.y - pa.y) * sx1;
+      int64_t fx, fy;  // zero for an empty slot (a == b: r = 0)
+      pair_fix_sel(pt->cut2[sp], pt->sig6[sp], eps24, rx, ry, fx, fy);
+      if (a != b) {
+        atomicAdd(&ax[a], (unsigned long long)fx);
+        atomicAdd(&ay[a], (unsigned long long)fy);
+        atomicAdd(&ax[b], (unsigned long long)(-fx));
+        atomicAdd(&ay[b], (unsigned long long)(-fy));
+      }
+    }
+    __syncthreads();
+    if (mem) {
+      int64_t fxs = (int64_t)ax[tid], fys = (int64_t)ay[tid];
+      ax[tid] = 0ull;
+      ay[tid] = 0ull;
+      if (d->n_walls) {
+        int64_t az = 0;
+        wall_forces<2>(d, si, (float)p.qx * sx0, (float)p.qy * sx1, 0.0f, fxs, fys, az,
+                       st.wall_viol);
+      }
+      bd_step(pc, p, fxs, fys, s == 0 ? fs0 : fs, s == 0 ? tz0 : tz, fex, fey, k0, k1,
+              (uint32_t)i, step0 + (uint64_t)s, s == n_steps - 1, &vx, &vy, &om,
+              s == 0 ? an0 : p.an, nullptr, &noise, s == 0);
+      const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
+      const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
+      dmax2 = fmaxf(dmax2, ddx * ddx + ddy * ddy);
+    }
+  }
+  if (mem) {
+    st.q[gi] = p.qx;
+    st.q[M + gi] = p.qy;
+    st.img[gi] = p.ix;
+    st.img[M + gi] = p.iy;
+    st.ang[gi] = p.an;
+    st.vel[gi] = vx;
+    st.vel[M + gi] = vy;
+    st.vel[2 * M + gi] = 0.0f;
+    st.omega[gi] = om;
+    const float disp = sqrt_rn(dmax2);
+    sc.disp[gi] = disp;
+    if (!(disp < 0.5f * d->skin)) {  // a mover
+      const int k = atomicAdd(&sc.nmov[e], 1);
+      if (k < kMaxMovers) sc.movers[(size_t)e * kMaxMovers + k] = i;
+    }
+    if (st.reuse) {
+      const PrevSlot w = prev_slot(st, par ^ 1);
+      w.f[gi] = fs;
+      w.tz[gi] = tz;
+      w.ang[gi] = p.an;
+    }
+  }
+  __threadfence();
+  __syncthreads();
+}
+
+// ------------------------------------------- neighbour-list window (2-D)
+// Dense boxes: the rc + skin graph percolates, so clusters exceed a wave
+// (and k_check's big-cluster workgroup).  The window keeps the build grid,
+// the exact check and the exact re-run, but its sub-steps run chip-wide: a
+// Verlet list per colloid (every j within r_i + r_j + skin), then one launch
+// per sub-step with one thread per colloid, positions read from one buffer
+// and written to the other (st.q, sc.qalt alternate; k_check copies back
+// after an odd window).  Forces, noise and update are block_global_run's
+// (pair_force, bd_step with the step's normals drawn fresh), so the bits are
+// the same.  The 3-D twin is k_build_nlist3 / k_nl_step3.
+constexpr int kNlMax = 48;  // neighbours per colloid (more: the env re-runs)
+
+// Build step 2 (neighbour-list path), grid (ceil(N / 256), E), one thread
+// per cell-sorted entry of k_build_sort: its neighbours into nl[k][gi]
+// (neighbour-major, so the sub-step's reads coalesce).
+__global__ __launch_bounds__(256) void k_build_nlist2(const Derived* __restrict__ d, DevState st,
+                                                      Scratch sc, int lx, int ly) {
+  __shared__ float nb2[kMaxSpecies * kMaxSpecies];
+  for (int k = threadIdx.x; k < kMaxSpecies * kMaxSpecies; k += blockDim.x) nb2[k] = d->nb2[k];
+  __syncthreads();
+  const int e = blockIdx.y, N = st.n;
+  const int ps = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ps >= N) return;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int ncell = 1 << (lx + ly);
+  const int32_t* cs = sc.bcstart + (size_t)e * (ncell + 1);
+  const int ncx = 1 << lx, ncy = 1 << ly;
+  const int loy = ncy >= 3 ? -1 : 0, hiy = ncy >= 3 ? 1 : ncy - 1;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const int pk = sc.bsid[base + ps];
+  const int i = pk & 0xffffff;
+  const uint32_t qx = sc.bsq[base + ps], qy = sc.bsq[M + base + ps];
+  const int c0 = cell_index(qx, qy, lx, ly);
+  const int cx = c0 & (ncx - 1), cy = c0 >> lx;
+  const int xa = ncx >= 3 ? max(cx - 1, 0) : 0;
+  const int xb = ncx >= 3 ? min(cx + 1, ncx - 1) : ncx - 1;
+  const int xw = ncx >= 3 ? (cx == 0 ? ncx - 1 : (cx == ncx - 1 ? 0 : -1)) : -1;
+  int rb[6], re[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const int oy = loy + (r >> 1), part = r & 1;
+    const bool use = oy <= hiy && (part == 0 || xw >= 0);
+    const int row = ((cy + oy + ncy) & (ncy - 1)) << lx;
+    const int c_lo = row | (part == 0 ? xa : xw), c_hi = row | (part == 0 ? xb : xw);
+    rb[r] = use ? cs[c_lo] : 0;
+    re[r] = use ? cs[c_hi + 1] : 0;
+  }
+  const float* nb2_row = nb2 + (pk >> 24) * kMaxSpecies;
+  int cnt = 0;
+  int32_t* out = sc.nl + base + i;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    for (int jj0 = rb[r]; jj0 < re[r]; jj0 += 4) {
+      int pk4[4];
+      uint32_t x4[4], y4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int jj = jj0 + u;
+        const bool ok = jj < re[r];
+        pk4[u] = ok ? sc.bsid[base + jj] : -1;
+        x4[u] = ok ? sc.bsq[base + jj] : 0u;
+        y4[u] = ok ? sc.bsq[M + base + jj] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (pk4[u] < 0 || (pk4[u] & 0xffffff) == i) continue;
+        const float rx = (float)(int32_t)(x4[u] - qx) * sx0;
+        const float ry = (float)(int32_t)(y4[u] - qy) * sx1;
+        if (rx * rx + ry * ry < nb2_row[pk4[u] >> 24]) {
+          if (cnt < kNlMax) out[(size_t)cnt * M] = pk4[u];
+          ++cnt;
+        }
+      }
+    }
+  }
+  sc.nn[base + i] = min(cnt, kNlMax);
+  reinterpret_cast<uint2*>(sc.qa)[base + i] = make_uint2(qx, qy);  // sub-step 0's read buffer
+  if (cnt > kNlMax) sc.fallback[e] = 1;  // -> the env re-runs on the global path
+}
+
+// Sub-step s of the 2-D neighbour-list window, one thread per colloid of
+// every env (XCD-aware workgroup order: one env's colloids share an L2).
+// Positions ping-pong between two AoS uint2 buffers in sc.qa (sub-step s
+// reads buffer s & 1, the build filled buffer 0); the last sub-step writes
+// st.q.
+// sc.disp holds the squared maximum displacement until the last sub-step.
+template <bool kMulti, bool kWalls>
+__global__ __launch_bounds__(256) void k_nl_step2(const Derived* __restrict__ d, DevState st,
+                                                  Scratch sc, int n_steps, int s,
+                                                  const uint64_t* __restrict__ ctl) {
+  __shared__ PairTables pt;
+  if (kMulti) stage_pair_tables(d, &pt);
+  const size_t M = (size_t)st.m;
+  const unsigned per_xcd = gridDim.x >> 3;  // grid: a multiple of 8 workgroups
+  const unsigned lb = (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3);
+  const size_t gi = (size_t)lb * blockDim.x + threadIdx.x;
+  if (gi >= M) return;
+  const int N = st.n;
+  const int e = (int)(gi / N), i = (int)(gi - (size_t)e * N);
+  if (sc.fallback[e] != 0) return;
+  const size_t base = (size_t)e * N;
+  const bool first = s == 0, last = s == n_steps - 1;
+  const uint2* R = reinterpret_cast<const uint2*>(sc.qa) + (s & 1) * M;
+  uint2* W = reinterpret_cast<uint2*>(sc.qa) + ((s & 1) ^ 1) * M;
+  const int par = window_parity(ctl);
+  const uint64_t step = ctl[kCtlStep] + (uint64_t)s;
+  const int si = kMulti ? st.species[i] : 0;
+  const float sx0 = d->sx[0], sx1 = d->sx[1];
+  const int nn = sc.nn[gi];
+  PState p;
+  const uint2 qo = R[gi];
+  p.qx = qo.x;
+  p.qy = qo.y;
+  p.ix = st.img[gi];
+  p.iy = st.img[M + gi];
+  p.an = st.ang[gi];
+  uint32_t q0x, q0y;
+  float dmax2 = 0.0f;
+  if (first) {
+    q0x = p.qx;
+    q0y = p.qy;
+    sc.bq[gi] = p.qx;
+    sc.bq[M + gi] = p.qy;
+    sc.bimg[gi] = p.ix;
+    sc.bimg[M + gi] = p.iy;
+    sc.bang[gi] = p.an;
+  } else {
+    q0x = sc.bq[gi];
+    q0y = sc.bq[M + gi];
+    dmax2 = sc.disp[gi];
+  }
+  const float eps24 = d->eps24;
+  int64_t ax = 0, ay = 0;
+  const int32_t* nlp = sc.nl + gi;
+  for (int k0 = 0; k0 < nn; k0 += 8) {
+    // eight neighbours per round: indices, then positions, in flight together
+    int32_t pk[8];
+    uint32_t xj[8], yj[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) pk[u] = k0 + u < nn ? nlp[(size_t)(k0 + u) * M] : -1;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint2 qj = R[base + (pk[u] < 0 ? i : (pk[u] & 0xffffff))];
+      xj[u] = qj.x;
+      yj[u] = qj.y;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (pk[u] < 0) continue;
+      const float rx = (float)(int32_t)(xj[u] - p.qx) * sx0;
+      const float ry = (float)(int32_t)(yj[u] - p.qy) * sx1;
+      if (kMulti) {
+        const int sp = si * kMaxSpecies + (pk[u] >> 24);
+        pair_force(pt.cut2[sp], pt.sig6[sp], eps24, rx, ry, ax, ay);
+      } else {
+        pair_force(d->cut2[0], d->sig6[0], eps24, rx, ry, ax, ay);
+      }
+    }
+  }
+  if (kWalls) {
+    int64_t az = 0;
+    wall_forces<2>(d, si, (float)p.qx * sx0, (float)p.qy * sx1, 0.0f, ax, ay, az, st.wall_viol);
+  }
+  const bool reuse0 = st.reuse && first;  // sub-step 0 reuses the previous run's actions
+  const PrevSlot prv = prev_slot(st, par);
+  const float fs = reuse0 ? prv.f[gi] : st.f_swim[gi];
+  const float tz = reuse0 ? prv.tz[gi] : st.torque_z[gi];
+  const uint32_t an_swim = reuse0 ? prv.ang[gi] : p.an;
+  const PConst pc = load_pconst(d, si);
+  float vx = 0.0f, vy = 0.0f, om = 0.0f;
+  bd_step(pc, p, ax, ay, fs, tz, st.f_ext[gi], st.f_ext[M + gi], d->key0, d->key1 ^ (uint32_t)e,
+          (uint32_t)i, step, last, &vx, &vy, &om, an_swim);
+  if (last) {  // nobody reads st.q during the window
+    st.q[gi] = p.qx;
+    st.q[M + gi] = p.qy;
+  } else {
+    W[gi] = make_uint2(p.qx, p.qy);
+  }
+  st.img[gi] = p.ix;
+  st.img[M + gi] = p.iy;
+  st.ang[gi] = p.an;
+  const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
+  const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
+  dmax2 = fmaxf(dmax2, ddx * ddx + ddy * ddy);
+  if (!last) {
+    sc.disp[gi] = dmax2;
+    return;
+  }
+  st.vel[gi] = vx;
+  st.vel[M + gi] = vy;
+  st.vel[2 * M + gi] = 0.0f;
+  st.omega[gi] = om;
+  const float disp = sqrt_rn(dmax2);
+  sc.disp[gi] = disp;
+  if (!(disp < 0.5f * d->skin)) {  // a mover (k_check's exact test)
+    const int k = atomicAdd(&sc.nmov[e], 1);
+    if (k < kMaxMovers) sc.movers[(size_t)e * kMaxMovers + k] = i;
+  }
+  if (st.reuse) save_forces(st, gi, par ^ 1);  // this run's actions, the final angle
+}
+
+// ---------------------------------------------------------------- check
+// cell_lx, cell_ly: the window's build grid when its counting sort left the
+// cell-sorted snapshot in global memory (sc.bsq / bsid / bcstart: the
+// three-launch build, not k_build_env); -1: scan every colloid per mover.
+__global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, DevState st,
+                                                Scratch sc, int n_steps,
+                                                uint64_t* __restrict__ step_ctr,
+                                                uint32_t* __restrict__ arrive, int lx, int ly,
+                                                int nlist, int cell_lx, int cell_ly) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  int32_t* wave_sums = reinterpret_cast<int32_t*>(smem);  // 16
+  int32_t* misc = wave_sums + 16;                          // 16
+  int32_t* movers = misc + 16;                             // kMaxMovers
+  int32_t* cnt = movers + kMaxMovers;                      // global-path cell counts
+  __shared__ PairTables pt;
+  const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  role_begin(sc, kRoleCheck);
+  // every load the test starts from is issued here together -- the window
+  // counters, the build's flags, the mover count and list (written by the
+  // run kernel) and the pair tables: one memory latency, not a chain
+  const uint64_t step0 = step_ctr[kCtlStep];
+  const int par = window_parity(step_ctr);  // reuse_forces slot of this window
+  const int fb = sc.fallback[e];
+  const int bign = nlist ? 0 : sc.big_n[e];
+  const int nm_run = sc.nmov[e];
+  const int mv_run = tid < kMaxMovers ? sc.movers[(size_t)e * kMaxMovers + tid] : 0;
+  for (int k = tid; k < kMaxSpecies * kMaxSpecies; k += T) {
+    pt.cut2[k] = d->cut2[k];
+    pt.sig6[k] = d->sig6[k];
+  }
+  if (tid < 16) misc[tid] = 0;
+  __syncthreads();
+  // flagged by the build: the env did not run (its state is the window start)
+  const bool flagged_build = fb == 1;
+  if (!flagged_build && bign > 0)
+    run_big_clusters(d, st, sc, e, n_steps, step0, cnt, &pt, par);
+  if (!flagged_build) {
+    // the movers (displacement >= skin / 2) were listed by the run kernel
+    // and the big-cluster run: no scan over all colloids here
+    int nm = nm_run;
+    if (bign > 0) {
+      // the big-cluster run of this workgroup appended entries a moment
+      // ago: agent-scope loads
+      if (tid == 0) misc[0] = __hip_atomic_load(&sc.nmov[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      nm = misc[0];
+      for (int k = tid; k < min(nm, kMaxMovers); k += T)
+        movers[k] = __hip_atomic_load(&sc.movers[(size_t)e * kMaxMovers + k], __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      for (int k = tid; k < min(nm, kMaxMovers); k += T)
+        movers[k] = k < kMaxMovers && k == tid ? mv_run : sc.movers[(size_t)e * kMaxMovers + k];
+    }
+    __syncthreads();
+    if (nm > kMaxMovers) {
+      if (tid == 0) misc[1] = 1;
+    } else if (nm > 0) {
+      // exact test of every (mover, non-neighbour) pair at the window-start
+      // positions: d0 < rc + D_i + D_j could have interacted without its
+      // force being computed.  Same-cluster pairs count too: a cluster links
+      // particles through chains, so two of its members need not be listed
+      // neighbours of each other.
+      const bool multi = d->n_species > 1;  // else every pair's cutoff is cut2[0]
+      const float rc0 = sqrtf(pt.cut2[0]);
+      const float sx0 = d->sx[0], sx1 = d->sx[1];
+      const bool per = d->periodic != 0;
+      auto test_pair = [&](int m, int j) {
+        // (non-periodic box: the unwrapped separation; the folded one would
+        // only make the test stricter)
+        const float rx = per ? (float)(int32_t)(sc.bq[base + j] - sc.bq[base + m]) * sx0
+                             : pair_disp(sc.bq[base + j], sc.bimg[base + j], sc.bq[base + m],
+                                         sc.bimg[base + m], sx0, false);
+        const float ry = per ? (float)(int32_t)(sc.bq[M + base + j] - sc.bq[M + base + m]) * sx1
+                             : pair_disp(sc.bq[M + base + j], sc.bimg[M + base + j],
+                                         sc.bq[M + base + m], sc.bimg[M + base + m], sx1, false);
+        // the pair's own WCA cutoff r_m + r_j (not the largest one: a dense
+        // mixture would fail the test for pairs that cannot interact)
+        const float rc = multi ? sqrtf(pt.cut2[st.species[m] * kMaxSpecies + st.species[j]]) : rc0;
+        const float lim = rc + sc.disp[base + m] + sc.disp[base + j] + 1e-3f;
+        if (rx * rx + ry * ry < lim * lim) {
+          bool listed = false;
+          const int sm = sc.slot_of[base + m], sj = sc.slot_of[base + j];
+          if (nlist) {  // j among m's listed neighbours
+            const int nn = sc.nn[base + m];
+            for (int k = 0; k < nn; ++k)
+              listed |= (sc.nl[(size_t)k * M + base + m] & 0xffffff) == j;
+          } else if (sc.root[base + j] == sc.root[base + m] && sm < 0) {  // same big cluster
+            const uint32_t bm = (uint32_t)(-1 - sm), bj = (uint32_t)(-1 - sj);
+            const uint32_t* bp = sc.big_pairs + (size_t)e * kBigPairs;
+            const int np = sc.big_np[e];
+            for (int k = 0; k < np; ++k) {
+              const uint32_t a = bp[k] & 1023u, b = (bp[k] >> 10) & 1023u;
+              listed |= (a == bm && b == bj) || (a == bj && b == bm);
+            }
+          } else if (sc.root[base + j] == sc.root[base + m]) {  // same wave: its pairs
+            const int wv = sm >> 6;
+            const uint32_t lm = (uint32_t)(sm & 63), lj = (uint32_t)(sj & 63);
+            const uint32_t* pw = sc.pairs + ((size_t)e * sc.wmax + wv) * kPairsPerWave;
+            const int np = sc.wave_npairs[(size_t)e * sc.wmax + wv];
+            for (int k = 0; k < np; ++k) {
+              const uint32_t a = pw[k] & 63u, b = (pw[k] >> 6) & 63u;
+              listed |= (a == lm && b == lj) || (a == lj && b == lm);
+            }
+          }
+          if (!listed) misc[1] = 1;
+        }
+      };
+      // Candidates of a mover from the window's cell-sorted snapshot: every
+      // j with d0 < rc + D_m + D_j lies within lim_max = rc_max + 2 D_max of
+      // m (D_max: the largest displacement; non-movers moved less than
+      // skin / 2), so within kc = ceil(lim_max / cell side) cells.  One wave
+      // per mover, its lanes over the (2 kc + 1) rows' ranges.  Grids too
+      // coarse for that (kc > 2, or fewer than 2 kc + 1 cells a side) scan
+      // every colloid.
+      int kc = 99;
+      const int ncx = cell_lx >= 1 ? 1 << cell_lx : 0, ncy = cell_ly >= 1 ? 1 << cell_ly : 0;
+      if (cell_lx >= 1 && cell_ly >= 1) {
+        if (tid == 0) misc[7] = __float_as_int(0.5f * d->skin);
+        __syncthreads();
+        for (int k = tid; k < nm; k += T)
+          atomicMax(&misc[7], __float_as_int(sc.disp[base + movers[k]]));  // >= 0: int order
+        __syncthreads();
+        const float dmax = __int_as_float(misc[7]);
+        const float lim_max = d->rc_max_f + 2.0f * dmax + 1e-3f;
+        const float side = fminf(sx0 * (float)(1u << (32 - cell_lx)),
+                                 sx1 * (float)(1u << (32 - cell_ly)));
+        kc = (int)ceilf(lim_max / side);
+        if (kc > 2 || ncx < 2 * kc + 1 || ncy < 2 * kc + 1) kc = 99;
+      }
+      if (kc <= 2) {
+        const int32_t* cs = sc.bcstart + (size_t)e * ((size_t)ncx * ncy + 1);
+        const int lane = tid & 63, nwv = T >> 6;
+        for (int k = tid >> 6; k < nm; k += nwv) {  // wave-uniform mover
+          const int m = movers[k];
+          const uint32_t qx = sc.bq[base + m], qy = sc.bq[M + base + m];
+          const int cx = per ? (int)(qx >> (32 - cell_lx))
+                             : cell_coord(qx, sc.bimg[base + m], cell_lx, false);
+          const int cy = per ? (int)(qy >> (32 - cell_ly))
+                             : cell_coord(qy, sc.bimg[M + base + m], cell_ly, false);
+          // up to two ranges per row (a periodic row wraps once)
+          int rb[10], rl[10], nr = 0;
+          for (int oy = -kc; oy <= kc; ++oy) {
+            int y = cy + oy;
+            if (!per && (y < 0 || y >= ncy)) continue;
+            y = (y + ncy) & (ncy - 1);
+            const int row = y << cell_lx;
+            int x0 = cx - kc, x1 = cx + kc;
+            if (!per) {
+              x0 = max(x0, 0);
+              x1 = min(x1, ncx - 1);
+            }
+            if (x0 < 0) {  // periodic wrap on the left
+              rb[nr] = cs[row | (ncx + x0)];
+              rl[nr] = cs[(row | (ncx - 1)) + 1] - rb[nr];
+              ++nr;
+              x0 = 0;
+            }
+            if (x1 > ncx - 1) {  // periodic wrap on the right
+              rb[nr] = cs[row];
+              rl[nr] = cs[(row | (x1 - ncx)) + 1] - rb[nr];
+              ++nr;
+              x1 = ncx - 1;
+            }
+            rb[nr] = cs[row | x0];
+            rl[nr] = cs[(row | x1) + 1] - rb[nr];
+            ++nr;
+          }
+          int total = 0;
+          for (int r = 0; r < nr; ++r) total += rl[r];
+          for (int f = lane; f < total; f += 64) {
+            int jj = f, r = 0;
+            while (jj >= rl[r]) jj -= rl[r++];
+            const int j = sc.bsid[base + rb[r] + jj] & 0xffffff;
+            if (j != m) test_pair(m, j);
+          }
+        }
+      } else {
+        const long total = (long)nm * N;
+        for (long t = tid; t < total; t += T) {
+          const int m = movers[t / N];
+          const int j = (int)(t % N);
+          if (j != m) test_pair(m, j);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const bool rerun = flagged_build || misc[1] != 0;
+  if (rerun) {
+    // a flagged env was skipped by k_cluster_run: its state is the window
+    // start already; otherwise restore the snapshot k_cluster_run took
+    for (int i = tid; i < N && !flagged_build; i += T) {
+      const size_t gi = base + i;
+      st.q[gi] = sc.bq[gi];
+      st.q[M + gi] = sc.bq[M + gi];
+      st.img[gi] = sc.bimg[gi];
+      st.img[M + gi] = sc.bimg[M + gi];
+      st.ang[gi] = sc.bang[gi];
+    }
+    if (tid == 0) sc.fallback[e] = 2;  // diagnostics: env re-run on the global path
+    __syncthreads();
+    if (global_lds_extra_words(N, st.dims, 1 << (lx + ly)) && d->periodic)  // LDS variant: periodic
+      block_global_run_lds(d, st, e, n_steps, step0, lx, ly, false, 0.0f, 0.0f, cnt, wave_sums,
+                           cnt + (1 << (lx + ly)) + 1, &pt, par);
+    else
+      block_global_run(d, st, sc, e, n_steps, step0, lx, ly, false, 0.0f, 0.0f, cnt, wave_sums,
+                       &pt, par);
+    save_forces_env(st, e, par ^ 1);  // the re-run replaced the run kernel's final state
+  }
+  __syncthreads();  // every read of nmov above is done
+  if (tid == 0) sc.nmov[e] = 0;
+  advance_counter(step_ctr, arrive, step0, n_steps);
+  role_end(sc, kRoleCheck);
+}
+
+}  // namespace swarm

@@ -1,0 +1,182 @@
+"""
+The fused PPO epoch gradient (swarm_ppo_epoch_grad, csrc/swarm_ppo.cuh)
+against torch autograd of ProximalPolicyLoss._calculate_loss (the restatement
+of swarmrl/losses/proximal_policy_loss.py:62-138 pinned by
+tests/test_ppo_loss_cpu.py) on the same fp32 parameters and samples.
+
+Tolerance: both sides are fp32 with different summation orders, and a
+sample whose ReLU pre-activation or ratio sits within rounding of a kink
+may take the other branch, so each parameter tensor's gradient is compared
+in norm: |g_fused - g_torch| <= 2e-4 |g_torch| (+1e-6), and elementwise
+within 2e-3 of the tensor's largest entry.
+"""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    from swarmrl_amd import _capi
+
+    _capi.require_gpu()
+    torch.cuda.set_device(0)
+
+
+def _episode(T, S, d, k, hidden, seed):
+    from swarmrl_amd.networks.torch_network import ActorCriticMLP
+
+    g = torch.Generator().manual_seed(seed)
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(seed)
+    net = ActorCriticMLP(d, n_actions=k, hidden=hidden).to(dev)
+    x = torch.randn(T, S, d, generator=g).to(dev)
+    actions = torch.randint(0, k, (T, S), generator=g).to(dev)
+    rewards = torch.randn(T, S, generator=g).to(dev)
+    with torch.no_grad():
+        logits, _ = net(x)
+        logp = torch.log(torch.softmax(logits, -1) + 1e-8).gather(-1, actions[..., None])[..., 0]
+    # old policy off by up to ~e^0.4: ratios on both sides of the clip range
+    old = (logp + 0.4 * torch.randn(T, S, generator=g).to(dev)).contiguous()
+    return net, x, actions, old, rewards
+
+
+class _Wrap:
+    def __init__(self, net):
+        self.net = net
+
+    def __call__(self, features, obs_ndim=1):
+        lead = features.shape[: features.ndim - obs_ndim]
+        return self.net(features.reshape(*lead, -1))
+
+
+def _torch_grads(loss, net, x, actions, old, rewards):
+    net.zero_grad(set_to_none=True)
+    loss._calculate_loss(_Wrap(net), x, actions, rewards, old).backward()
+    return [p.grad.detach().clone() for p in net.ppo_layers()]
+
+
+def _fused_grads(loss, net, x, actions, old, rewards):
+    from swarmrl_amd.engine import ops
+
+    layers = net.ppo_layers()
+    flat = ops.ppo_epoch_grad(x, actions, old, rewards, layers, loss.value_function.gamma,
+                              loss.value_function.lambda_, loss.epsilon,
+                              loss.entropy_coefficient)
+    out, off = [], 0
+    for t in layers:
+        out.append(flat[off:off + t.numel()].view_as(t))
+        off += t.numel()
+    assert off == flat.numel()
+    return out, flat
+
+
+def _check(got, want):
+    names = ["W1", "b1", "Wa", "ba", "Wc", "bc"]
+    for name, a, b in zip(names, got, want):
+        err = (a - b).norm().item()
+        assert err <= 2e-4 * b.norm().item() + 1e-6, (name, err, b.norm().item())
+        assert (a - b).abs().max().item() <= 2e-3 * b.abs().max().item() + 1e-6, name
+
+
+@pytest.mark.parametrize("T,S,d,k,hidden", [
+    (20, 1000, 1, 4, 128),     # concentration-field agents, stock network
+    (20, 4096, 4, 4, 128),
+    (7, 333, 10, 3, 100),      # ragged: hidden 100 in a 128-thread block, k < K
+    (5, 517, 32, 6, 256),      # widest: 32 features, 256 units, 16-action variant
+    (3, 64, 2, 4, 64),
+    (40, 150, 2, 4, 128),      # T > 32: the GAE kernel's uncached loop
+    (20, 53000, 4, 4, 128),    # >= 2^20 samples: the packed two-sample values kernel
+])
+def test_fused_epoch_grad_matches_autograd(T, S, d, k, hidden):
+    from swarmrl_amd.losses.proximal_policy_loss import ProximalPolicyLoss
+
+    loss = ProximalPolicyLoss()
+    net, x, actions, old, rewards = _episode(T, S, d, k, hidden, seed=T * 1000 + S)
+    want = _torch_grads(loss, net, x, actions, old, rewards)
+    got, _ = _fused_grads(loss, net, x, actions, old, rewards)
+    _check(got, want)
+
+
+def test_fused_epoch_grad_deterministic():
+    from swarmrl_amd.losses.proximal_policy_loss import ProximalPolicyLoss
+
+    loss = ProximalPolicyLoss()
+    net, x, actions, old, rewards = _episode(20, 20000, 1, 4, 128, seed=5)
+    _, a = _fused_grads(loss, net, x, actions, old, rewards)
+    _, b = _fused_grads(loss, net, x, actions, old, rewards)
+    assert torch.equal(a, b)
+
+
+def test_compute_loss_fused_equals_torch_path(monkeypatch):
+    """Two epochs of compute_loss with SGD: the fused path and the torch
+    path end on the same parameters."""
+    from swarmrl_amd.losses.proximal_policy_loss import ProximalPolicyLoss
+    from swarmrl_amd.networks.torch_network import ActorCriticMLP, TorchModel
+
+    dev = torch.device("cuda", 0)
+    T, E, A, d = 20, 2, 500, 1
+    g = torch.Generator().manual_seed(11)
+    feats = torch.randn(T, E, A, d, generator=g)
+    acts = torch.randint(0, 4, (T, E, A), generator=g)
+    rews = torch.randn(T, E, A, generator=g)
+    olp = -1.386 + 0.3 * torch.randn(T, E, A, generator=g)
+
+    class Episode:
+        features = [f.to(dev) for f in feats]
+        actions = [a.to(dev) for a in acts]
+        rewards = [r.to(dev) for r in rews]
+        log_probs = [lp.to(dev) for lp in olp]
+
+    steps = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("SWARMRL_AMD_FUSED_PPO", fused)
+        torch.manual_seed(0)
+        model = TorchModel(ActorCriticMLP(d, 4, 128), input_shape=(d,), device=dev,
+                           optimizer=lambda ps: torch.optim.SGD(ps, lr=1e-4))
+        before = [p.detach().clone() for p in model.model.ppo_layers()]
+        loss = ProximalPolicyLoss(n_epochs=2)
+        assert (loss._fused_layers(model, feats.reshape(T, E * A, d).to(dev),
+                                   acts.reshape(T, E * A)) is not None) == (fused == "1")
+        loss.compute_loss(model, Episode())
+        steps.append([p.detach() - b for p, b in zip(model.model.ppo_layers(), before)])
+    for a, b in zip(*steps):
+        # SGD: the parameter change is lr x the summed gradients of the two epochs
+        assert (a - b).norm().item() <= 1e-3 * b.norm().item() + 1e-7
+
+
+def test_graph_epochs_equal_eager(monkeypatch):
+    """Three episodes of compute_loss with the default (fused, capturable)
+    Adam: the captured-graph epochs (episode 1 eager, 2 captured + replayed,
+    3 replayed) end on bit-identical parameters to the eager loop."""
+    from swarmrl_amd.losses.proximal_policy_loss import ProximalPolicyLoss
+    from swarmrl_amd.networks.torch_network import ActorCriticMLP, TorchModel
+
+    dev = torch.device("cuda", 0)
+    T, E, A, d = 20, 1, 300, 4
+
+    def episode(seed):
+        g = torch.Generator().manual_seed(seed)
+
+        class Episode:
+            features = [f.to(dev) for f in torch.randn(T, E, A, d, generator=g)]
+            actions = [a.to(dev) for a in torch.randint(0, 4, (T, E, A), generator=g)]
+            rewards = [r.to(dev) for r in torch.randn(T, E, A, generator=g)]
+            log_probs = [lp.to(dev) for lp in -1.386 + 0.3 * torch.randn(T, E, A, generator=g)]
+        return Episode()
+
+    finals = []
+    for graph in ("1", "0"):
+        monkeypatch.setenv("SWARMRL_AMD_PPO_GRAPH", graph)
+        torch.manual_seed(0)
+        model = TorchModel(ActorCriticMLP(d, 4, 128), input_shape=(d,), device=dev)
+        loss = ProximalPolicyLoss(n_epochs=5)
+        for ep in range(3):
+            loss.compute_loss(model, episode(100 + ep))
+        assert (getattr(loss, "_ppo_graph", None) is not None) == (graph == "1")
+        assert model.epoch_count == 15
+        finals.append([p.detach().clone() for p in model.model.ppo_layers()])
+    for a, b in zip(*finals):
+        assert torch.equal(a, b)

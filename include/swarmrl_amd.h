@@ -544,7 +544,9 @@ int swarm_rnd_distance(const float *x, int32_t n, int32_t d_in, int32_t width,
  * clip != 0, into env_reward[n_envs], and
  *   rewards[e][a] = base[e][a] + r_e   (base NULL: r_e).
  * workspace: device memory of swarm_rnd_env_workspace_bytes(n_envs, per_env)
- * bytes.  Two launches, asynchronous on `stream`; no host synchronisation. */
+ * bytes, zeroed before its first use (the call leaves it ready for the
+ * next one; one workspace per concurrent caller).  One launch, asynchronous
+ * on `stream`; no host synchronisation. */
 int swarm_rnd_env_reward(const float *x, int32_t n_envs, int32_t per_env, int32_t d_in,
                          int32_t width, const float *const *target,
                          const float *const *predictor, int32_t order, int32_t clip,

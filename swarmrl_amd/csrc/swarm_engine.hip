@@ -2079,10 +2079,11 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
                        params->periodic &&
                        swarm::build_env_sort_words(n_particles, 1 << (e->lxb + e->lyb)) <= below;
     }
-    // one block per CU for latency-bound runs; beside a run of up to 8192
-    // particles, 64 CUs produce the next window's table in its shadow
+    // one block per CU for latency-bound runs; beside a run of up to 16384
+    // particles, 64 CUs produce the next window's table in its shadow (C5:
+    // no k_noise launch between the policy and the run)
     e->wide_run = e->noise_table;
-    e->noise_blocks = e->wide_run && M <= 8192 ? 64 : 0;
+    e->noise_blocks = e->wide_run && M <= 16384 ? 64 : 0;
     const char* ow = std::getenv("SWARMRL_AMD_WIDE_RUN");
     if (ow && ow[0] == '0') e->wide_run = false, e->noise_blocks = 0;
     // run waves per CU: a wave alone on its CU does not share the CU's
@@ -2090,7 +2091,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     // CU once the run's waves (~1 per 46 particles) would not fit one per CU
     {
       const long est = (long)M / 46 + 1;
-      e->run_wpb = est + e->noise_blocks <= 224 ? 1 : (est / 2 + e->noise_blocks <= 224 ? 2 : 4);
+      e->run_wpb = est + e->noise_blocks <= 224 ? 1 : (est / 2 + e->noise_blocks <= 256 ? 2 : 4);
     }
     // l1_pairs: the ride-along build's pair search moves into the slice's
     // first launch as a filter of candidate lists prepared during the last
@@ -2724,6 +2725,15 @@ int swarm_rnd_distance(const float* x, int32_t n, int32_t d_in, int32_t width,
   return SWARM_OK;
 }
 
+namespace {
+// swarm_rnd_env_reward's workspace: the blocks' fp64 partials, then one
+// ticket per env (zero between calls: the caller zeroes it once).
+size_t rnd_partials_bytes(int n_envs, int per_env) {
+  const int kb = (per_env + swarm::kRndObsPerBlock - 1) / swarm::kRndObsPerBlock;
+  return ((size_t)n_envs * kb * sizeof(double) + 255) & ~(size_t)255;
+}
+}  // namespace
+
 int swarm_rnd_env_reward(const float* x, int32_t n_envs, int32_t per_env, int32_t d_in,
                          int32_t width, const float* const* target, const float* const* predictor,
                          int32_t order, int32_t clip, float clip_lo, float clip_hi,
@@ -2736,8 +2746,9 @@ int swarm_rnd_env_reward(const float* x, int32_t n_envs, int32_t per_env, int32_
   if (order < 1) return fail(SWARM_EINVAL, "distance order must be >= 1");
   if (n_envs < 0 || per_env < 0) return fail(SWARM_EINVAL, "n_envs, per_env >= 0");
   if (n_envs == 0 || per_env == 0) return SWARM_OK;
-  const int kb = (per_env + 255) / 256;
-  if (workspace_bytes < (int64_t)n_envs * kb * (int64_t)sizeof(double))
+  const int kb = (per_env + swarm::kRndObsPerBlock - 1) / swarm::kRndObsPerBlock;
+  const size_t pb = rnd_partials_bytes(n_envs, per_env);
+  if (workspace_bytes < (int64_t)(pb + (size_t)n_envs * sizeof(uint32_t)))
     return fail(SWARM_ECAPACITY, "workspace below swarm_rnd_env_workspace_bytes");
   swarm::RndPtrs tp, pp;
   for (int k = 0; k < 6; ++k) {
@@ -2747,23 +2758,23 @@ int swarm_rnd_env_reward(const float* x, int32_t n_envs, int32_t per_env, int32_
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   double* partial = static_cast<double*>(workspace);
+  uint32_t* tickets = reinterpret_cast<uint32_t*>(static_cast<char*>(workspace) + pb);
   const dim3 grid((unsigned)kb, (unsigned)n_envs);
   if (d_in <= 4)
-    hipLaunchKernelGGL(swarm::k_rnd_env_partial<4>, grid, dim3(256), 0, s, x, per_env, d_in, tp,
-                       pp, order, metric, partial);
+    hipLaunchKernelGGL(swarm::k_rnd_env<4>, grid, dim3(256), 0, s, x, per_env, d_in, tp, pp,
+                       order, clip ? 1 : 0, clip_lo, clip_hi, base, metric, env_reward, rewards,
+                       partial, tickets);
   else
-    hipLaunchKernelGGL(swarm::k_rnd_env_partial<16>, grid, dim3(256), 0, s, x, per_env, d_in, tp,
-                       pp, order, metric, partial);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(swarm::k_rnd_env_finish, dim3((unsigned)n_envs), dim3(1024), 0, s, partial,
-                     kb, per_env, clip ? 1 : 0, clip_lo, clip_hi, base, env_reward, rewards);
+    hipLaunchKernelGGL(swarm::k_rnd_env<16>, grid, dim3(256), 0, s, x, per_env, d_in, tp, pp,
+                       order, clip ? 1 : 0, clip_lo, clip_hi, base, metric, env_reward, rewards,
+                       partial, tickets);
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
 }
 
 int64_t swarm_rnd_env_workspace_bytes(int32_t n_envs, int32_t per_env) {
   if (n_envs < 0 || per_env < 0) return -1;
-  return (int64_t)n_envs * ((per_env + 255) / 256) * (int64_t)sizeof(double);
+  return (int64_t)(rnd_partials_bytes(n_envs, per_env) + (size_t)n_envs * sizeof(uint32_t));
 }
 
 int64_t swarm_engine_step_count(const swarm_engine_t* e) {

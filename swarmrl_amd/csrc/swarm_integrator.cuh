@@ -2979,7 +2979,7 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
 
 // Uniform dispatch to the compile-time variants: normals from a table
 // (table != null) or drawn here; walls or none.
-template <bool kMulti, bool kWalls>
+template <bool kMulti, bool kWalls, bool kTwoPass = false>
 __device__ __forceinline__ void run_wave_dispatch(const Derived* __restrict__ d, const DevState& st,
                                                   const Scratch& sc, int n_envs, int n_steps,
                                                   uint64_t step0, const float* __restrict__ table,
@@ -2988,11 +2988,11 @@ __device__ __forceinline__ void run_wave_dispatch(const Derived* __restrict__ d,
                                                   unsigned long long* lacc_y,
                                                   const PairTables& pt, int par) {
   if (table)
-    run_wave<kMulti, true, kWalls>(d, st, sc, n_envs, n_steps, step0, table, gw, lane, lpos_w,
-                                   lacc_x, lacc_y, pt, par);
+    run_wave<kMulti, true, kWalls, kTwoPass>(d, st, sc, n_envs, n_steps, step0, table, gw, lane,
+                                             lpos_w, lacc_x, lacc_y, pt, par);
   else
-    run_wave<kMulti, false, kWalls>(d, st, sc, n_envs, n_steps, step0, nullptr, gw, lane, lpos_w,
-                                    lacc_x, lacc_y, pt, par);
+    run_wave<kMulti, false, kWalls, kTwoPass>(d, st, sc, n_envs, n_steps, step0, nullptr, gw, lane,
+                                              lpos_w, lacc_x, lacc_y, pt, par);
 }
 
 // Launch-duration stamps for measurement (bench.py, swarm_engine_profile
@@ -3116,8 +3116,11 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
   const float* table = table_ok ? tables + par * noise_table_words(M) : nullptr;
   if (wv >= run_wpb) return;
   const int gw = gw0 + wv;
-  run_wave_dispatch<kMulti, kWalls>(d, st, sc, n_envs, n_steps, step0, table, gw, lane, lpos[wv],
-                                    lacc[wv][0], lacc[wv][1], pt, par);
+  // latency-bound launches last as long as their slowest wave: one with
+  // 65-128 pairs (a cluster denser than two pairs per particle) runs its own
+  // unrolled two-pass sub-step instead of the general pass loop
+  run_wave_dispatch<kMulti, kWalls, true>(d, st, sc, n_envs, n_steps, step0, table, gw, lane,
+                                          lpos[wv], lacc[wv][0], lacc[wv][1], pt, par);
   stamp_end(tstamp);
 }
 

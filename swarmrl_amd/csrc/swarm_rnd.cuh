@@ -138,61 +138,176 @@ __global__ __launch_bounds__(256) void k_rnd_distance(const float* __restrict__ 
 
 // The per-env intrinsic reward (random_network_distillation.py:126-143 on
 // the device path: the mean metric of the env's latest observations,
-// clipped) added to the task reward, in two launches instead of the metric
+// clipped) added to the task reward, in ONE launch instead of the metric
 // kernel + torch's mean, clamp and add (five launches and a copy on C5's
-// critical path).  Pass 1 (grid E x kb, 256 threads): the metric of every
-// observation of env e = blockIdx.y and the block's fp64 partial sum.
+// critical path).  Grid E x kb blocks of 256 threads, eight lanes per
+// observation (32 a block): lane `sub` of a group computes outputs
+// 4 sub .. 4 sub + 3 of every layer (each output's sum over its inputs in
+// order, as rnd_forward), the group's hidden activations go through an LDS
+// row (one wave's group: wave-scope ordering only), and the group adds its
+// lanes' parts of the metric with xor-shuffles.  Each block writes its fp64
+// partial sum (fixed order); the last block of an env (a ticket) adds the
+// env's partials in a fixed tree, takes the mean, clips it and writes
+// rewards[e][a] = base[e][a] + r_e (base null: r_e).  Deterministic: the
+// same bits on every call and device.
+constexpr int kRndLanes = 8;                      // lanes per observation
+constexpr int kRndObsPerBlock = 256 / kRndLanes;  // 32
+constexpr int kRndOut = kRndWidth / kRndLanes;    // outputs per lane and layer
+
+// One network's weights in LDS, torch layouts (rows = outputs).
 template <int D>
-__global__ __launch_bounds__(256) void k_rnd_env_partial(const float* __restrict__ x, int per_env,
-                                                         int d_in, RndPtrs tp, RndPtrs pp,
-                                                         int order, float* __restrict__ metric,
-                                                         double* __restrict__ partial) {
-  __shared__ RndNet<D> tnet, pnet;
-  __shared__ float hb[kRndWidth][256];
-  __shared__ double wsum[4];
-  rnd_stage<D>(&tnet, tp.w, d_in);
-  rnd_stage<D>(&pnet, pp.w, d_in);
-  __syncthreads();
-  const int e = blockIdx.y, k = blockIdx.x * blockDim.x + threadIdx.x;
-  double v = 0.0;
-  if (k < per_env) {
-    const int a = e * per_env + k;
-    const float m = rnd_metric<D>(tnet, pnet, x, a, d_in, order, hb);
-    metric[a] = m;
-    v = (double)m;
+struct RndRows {
+  float w1[kRndWidth][D];
+  float b1[kRndWidth];
+  float4 w2[kRndWidth][kRndWidth / 4];
+  float b2[kRndWidth];
+  float4 w3[kRndWidth][kRndWidth / 4];
+  float b3[kRndWidth];
+};
+
+template <int D>
+__device__ __forceinline__ void rnd_stage_rows(RndRows<D>* net, const float* const* w, int d_in) {
+  constexpr int W = kRndWidth;
+  for (int k = threadIdx.x; k < W * D; k += blockDim.x) {
+    const int j = k / D, i = k - j * D;
+    net->w1[j][i] = i < d_in ? w[0][j * d_in + i] : 0.0f;
   }
-  // fixed-order block sum: xor butterfly in the wave, then the four waves
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
-  __syncthreads();
-  if (threadIdx.x == 0)
-    partial[(size_t)e * gridDim.x + blockIdx.x] = ((wsum[0] + wsum[1]) + wsum[2]) + wsum[3];
+  float* w2 = reinterpret_cast<float*>(net->w2);
+  float* w3 = reinterpret_cast<float*>(net->w3);
+  for (int k = threadIdx.x; k < W * W; k += blockDim.x) {
+    w2[k] = w[2][k];
+    w3[k] = w[4][k];
+  }
+  for (int k = threadIdx.x; k < W; k += blockDim.x) {
+    net->b1[k] = w[1][k];
+    net->b2[k] = w[3][k];
+    net->b3[k] = w[5][k];
+  }
 }
 
-// Pass 2 (one 1024-thread block per env): the env's partials summed in block
-// order (deterministic), mean -> fp32 -> clip, then
-// rewards[e][a] = base[e][a] + r_e (base null: rewards[e][a] = r_e).
-__global__ __launch_bounds__(1024) void k_rnd_env_finish(const double* __restrict__ partial,
-                                                         int kb, int per_env, int clip,
-                                                         float lo, float hi,
-                                                         const float* __restrict__ base,
-                                                         float* __restrict__ env_reward,
-                                                         float* __restrict__ rewards) {
-  __shared__ float r_e;
-  const int e = blockIdx.x;
-  if (threadIdx.x == 0) {
-    double s = 0.0;
-    for (int k = 0; k < kb; ++k) s += partial[(size_t)e * kb + k];
-    float r = (float)(s / (double)per_env);
-    if (clip) r = fminf(fmaxf(r, lo), hi);
-    r_e = r;
-    env_reward[e] = r;
+// A square layer: the lane's outputs j = 4 sub + r, a[r] = b[j] + sum_k
+// w[j][k] h[k] over the group's activations h (LDS row, float4 reads).
+__device__ __forceinline__ void rnd_square_lanes(const float4 (*w)[kRndWidth / 4], const float* b,
+                                                 const float4* h, int sub, float* a) {
+#pragma unroll
+  for (int r = 0; r < kRndOut; ++r) a[r] = b[kRndOut * sub + r];
+#pragma unroll
+  for (int q = 0; q < kRndWidth / 4; ++q) {
+    const float4 hv = h[q];
+#pragma unroll
+    for (int r = 0; r < kRndOut; ++r) {
+      const float4 wv = w[kRndOut * sub + r][q];
+      a[r] = __builtin_fmaf(wv.x, hv.x, a[r]);
+      a[r] = __builtin_fmaf(wv.y, hv.y, a[r]);
+      a[r] = __builtin_fmaf(wv.z, hv.z, a[r]);
+      a[r] = __builtin_fmaf(wv.w, hv.w, a[r]);
+    }
+  }
+}
+
+// The lane's four outputs of one network for the group's observation x;
+// row: the group's LDS activation row (kRndWidth floats, float4-aligned).
+template <int D>
+__device__ __forceinline__ void rnd_forward_lanes(const RndRows<D>& net, const float* x, int sub,
+                                                  float4* row, float* out) {
+  float a[kRndOut];
+#pragma unroll
+  for (int r = 0; r < kRndOut; ++r) {
+    const int j = kRndOut * sub + r;
+    float v = net.b1[j];
+#pragma unroll
+    for (int i = 0; i < D; ++i) v = __builtin_fmaf(net.w1[j][i], x[i], v);
+    a[r] = fmaxf(v, 0.0f);
+  }
+  auto publish = [&](const float* v) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // the group's previous reads of the row are done
+    row[sub] = make_float4(v[0], v[1], v[2], v[3]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  publish(a);
+  rnd_square_lanes(net.w2, net.b2, row, sub, a);
+#pragma unroll
+  for (int r = 0; r < kRndOut; ++r) a[r] = fmaxf(a[r], 0.0f);
+  publish(a);
+  rnd_square_lanes(net.w3, net.b3, row, sub, out);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_rnd_env(const float* __restrict__ x, int per_env,
+                                                 int d_in, RndPtrs tp, RndPtrs pp, int order,
+                                                 int clip, float lo, float hi,
+                                                 const float* __restrict__ base,
+                                                 float* __restrict__ metric,
+                                                 float* __restrict__ env_reward,
+                                                 float* __restrict__ rewards,
+                                                 double* __restrict__ partial,
+                                                 uint32_t* __restrict__ tickets) {
+  static_assert(kRndOut == 4, "float4 activation rows");
+  __shared__ RndRows<D> tnet, pnet;
+  __shared__ float4 rows[kRndObsPerBlock][kRndWidth / 4];
+  __shared__ double red[256];
+  __shared__ int last;
+  const int e = blockIdx.y, kb = gridDim.x, tid = threadIdx.x;
+  const int sub = tid & (kRndLanes - 1), grp = tid / kRndLanes;
+  const int k = blockIdx.x * kRndObsPerBlock + grp;
+  const bool valid = k < per_env;
+  const size_t a = (size_t)e * per_env + (valid ? k : 0);
+  float xi[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) xi[i] = i < d_in ? x[a * d_in + i] : 0.0f;
+  rnd_stage_rows<D>(&tnet, tp.w, d_in);
+  rnd_stage_rows<D>(&pnet, pp.w, d_in);
+  __syncthreads();
+  float t[kRndOut], p[kRndOut];
+  rnd_forward_lanes<D>(tnet, xi, sub, rows[grp], t);
+  rnd_forward_lanes<D>(pnet, xi, sub, rows[grp], p);
+  float acc = 0.0f;
+#pragma unroll
+  for (int r = 0; r < kRndOut; ++r) {
+    const float dlt = fabsf(t[r] - p[r]);
+    acc += order == 2 ? dlt * dlt : powf(dlt, (float)order);
+  }
+#pragma unroll
+  for (int o = 1; o < kRndLanes; o <<= 1) acc += __shfl_xor(acc, o, 64);
+  const float m = order == 2 ? sqrtf(acc) : powf(acc, 1.0f / (float)order);
+  if (valid && sub == 0) metric[a] = m;
+  // the block's sum of its (up to 32) metrics: fixed tree over the groups
+  red[tid] = valid && sub == 0 ? (double)m : 0.0;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (tid < w) red[tid] += red[tid + w];
+    __syncthreads();
+  }
+  double* pe = partial + (size_t)e * kb;
+  if (tid == 0) {
+    pe[blockIdx.x] = red[0];
+    __threadfence();  // the partial is visible before the ticket counts it
+    last = atomicAdd(&tickets[e], 1u) == (uint32_t)(kb - 1);
   }
   __syncthreads();
-  const float r = r_e;
-  for (int a = threadIdx.x; a < per_env; a += blockDim.x) {
-    const size_t g = (size_t)e * per_env + a;
+  if (!last) return;
+  // the env's last block: its partials in a fixed tree (kb <= 256 x 16 per thread)
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  double v = 0.0;
+  for (int b = tid; b < kb; b += 256)
+    v += __hip_atomic_load(&pe[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  red[tid] = v;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (tid < w) red[tid] += red[tid + w];
+    __syncthreads();
+  }
+  float r = (float)(red[0] / (double)per_env);
+  if (clip) r = fminf(fmaxf(r, lo), hi);
+  if (tid == 0) {
+    env_reward[e] = r;
+    tickets[e] = 0u;  // the next call's count (graph replays)
+  }
+  for (int q = tid; q < per_env; q += 256) {
+    const size_t g = (size_t)e * per_env + q;
     rewards[g] = base ? base[g] + r : r;
   }
 }

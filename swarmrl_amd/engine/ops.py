@@ -531,8 +531,8 @@ def rnd_env_reward(points: torch.Tensor, n_envs: int, target: torch.nn.Module,
     nbytes = int(lib.swarm_rnd_env_workspace_bytes(n_envs, per_env))
     key = (dev, nbytes)
     ws = workspaces.get(key) if workspaces is not None else None
-    if ws is None:
-        ws = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=dev)
+    if ws is None:  # zeroed once: the kernel leaves its tickets at zero after use
+        ws = torch.zeros(max(nbytes, 8), dtype=torch.uint8, device=dev)
         if workspaces is not None:
             workspaces[key] = ws
 
