@@ -347,7 +347,7 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
     dev = (ctypes.c_float * 4096)()
     cal_samples, dev_samples = [], []
     n_roles = ctypes.c_int32(0)
-    rbuf = (ctypes.c_double * (2 * 8 * 512))()
+    rbuf = (ctypes.c_double * (2 * 16 * 512))()
     role_samples = {}
     try:
         if graph is not None:
@@ -405,7 +405,8 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
     # the workgroup roles of the launches between run nodes (role stamps):
     # mean start / end after the previous run node's end, and mean duration
     names = ("k_check", "build sort", "vision grid", "field (reward)", "pair search",
-             "vision cone", "cluster build", "policy MLP")
+             "vision cone", "cluster build", "policy MLP", "pair search: lists tested",
+             "pair search: output reserved", "vision cone: bins summed")
     timeline = {}
     for q, v in sorted(role_samples.items()):
         timeline[names[q] if q < len(names) else f"role{q}"] = {

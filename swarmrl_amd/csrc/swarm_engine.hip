@@ -228,6 +228,7 @@ struct VisionArgs {
   float* out;
   int n_envs;
   int staged;  // 1: the records are scattered into LDS, then written in order
+  unsigned long long* rstamp;  // role stamps of the launch (profiling), or null
 };
 
 // LDS of the vision grid's workgroup: wave sums, cell counts and, staged,
@@ -700,6 +701,7 @@ __device__ __forceinline__ void vision_body(const DevState& st, const Derived* _
       acc[b] += (int64_t)(((uint64_t)(uint32_t)hi << 32) | lo);
     }
   }
+  swarm::role_mark(va.rstamp, swarm::kMarkConeReduced);
   tail.template done<NB, G>(va, e, row, sub, acc, tail_pre);
 }
 
@@ -2842,7 +2844,7 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
   // records staged in LDS when the env's fit (N <= 8 x 1024: the register path)
   const bool staged = e->n <= 8 * 1024 && vision_grid_lds_bytes(lx, ly, e->n, true) <= kMaxLds;
   const VisionArgs va{*vp,          lx,        ly,    radii, types, agent_idx, n_agents,
-                      e->d_start,   e->vs,     out,   e->n_envs, staged ? 1 : 0};
+                      e->d_start,   e->vs,     out,   e->n_envs, staged ? 1 : 0, e->sc.rstamp};
   const long total = (long)e->n * e->n_envs;  // one group per sorted particle
   const int nb = vp->n_cones * vp->n_types;
   // lanes per agent: enough threads to give every SIMD a few waves, few
@@ -2891,10 +2893,14 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
     HIP_TRY(hipGetLastError());
   }
   if (pol && ride_ok && e->ride_stage == 3) {  // cluster build | cone + policy (l1_pairs)
-    const int ncb = (int)((total * 16 + 1023) / 1024);
+#ifndef SWARM_EXP_CONE_G
+#define SWARM_EXP_CONE_G 16
+#endif
+    constexpr int GC = SWARM_EXP_CONE_G;
+    const int ncb = (int)((total * GC + 1023) / 1024);
     const size_t lds = std::max(build_lds_bytes(e->n, e->sc.pair_cap),
                                 (size_t)kVisionHits * 1024 * sizeof(uint32_t));
-    hipLaunchKernelGGL((k_vision_policy_cbuild<4, 16, 4, 4>), dim3((unsigned)(e->n_envs + ncb)),
+    hipLaunchKernelGGL((k_vision_policy_cbuild<4, GC, 4, 4>), dim3((unsigned)(e->n_envs + ncb)),
                        dim3(1024), lds, e->stream, e->st, e->d_derived, va, *pol, e->sc);
     HIP_TRY(hipGetLastError());
     e->ride_stage = 0;
@@ -3001,6 +3007,14 @@ int swarm_vision_cone_persistent(swarm_engine_t* e, const swarm_vision_params_t*
   return vision_cone_impl(e, vp, agent_idx, n_agents, radii, types, out, true);
 }
 
+namespace {
+int policy_launch(const float* obs, int32_t n, int32_t d_in, const float* w1, const float* b1,
+                  int32_t hidden, const float* w2, const float* b2, int32_t k, uint64_t seed,
+                  uint64_t* state, int32_t n_state, float explore_p, const float* f_table,
+                  const float* t_table, int64_t* out_idx, float* out_logp, float* out_f,
+                  float* out_t, float* out_logits, void* stream, swarm_engine* ride);
+}  // namespace
+
 int swarm_engine_vision_policy(swarm_engine_t* e, const swarm_vision_params_t* vp,
                                const int32_t* agent_idx, int32_t n_agents, const float* radii,
                                const int32_t* types, float* features, const float* w1,
@@ -3025,6 +3039,17 @@ int swarm_engine_vision_policy(swarm_engine_t* e, const swarm_vision_params_t* v
   const swarm::MlpArgs m{features, (int)n, nb, w1, b1, hidden, w2, b2, k, (uint32_t)seed,
                          (uint32_t)(seed >> 32), reinterpret_cast<unsigned long long*>(agent_state),
                          explore_p, f_table, t_table, out_idx, out_logp, out_f, out_t, out_logits};
+  if (!e->wide_run) {
+    // throughput-bound engines (many envs): the cone is VALU-bound and the
+    // MLP's four lanes per agent would lengthen every group; the two kernels
+    // of the calls this replaces, the policy drawing with the first
+    // ceil(n / 64) counters as its group counters
+    const int rc = vision_cone_impl(e, vp, agent_idx, n_agents, radii, types, features, true);
+    if (rc) return rc;
+    return policy_launch(features, (int32_t)n, nb, w1, b1, hidden, w2, b2, k, seed, agent_state,
+                         n_state, explore_p, f_table, t_table, out_idx, out_logp, out_f, out_t,
+                         out_logits, e->stream, e);
+  }
   return vision_cone_impl(e, vp, agent_idx, n_agents, radii, types, features, true, &m);
 }
 

@@ -281,6 +281,10 @@ enum RoleId {
   kRoleCone,
   kRoleCbuild,
   kRoleMlp,
+  // progress marks inside roles (first / last wave to reach the point)
+  kMarkFilterLoaded,    // pair filter: lists and positions in registers, tested
+  kMarkFilterReserved,  // pair filter: the wave's output range reserved (atomic returned)
+  kMarkConeReduced,     // vision cone: the group's bins summed (before the tail)
   kRoles
 };
 
@@ -294,6 +298,16 @@ __device__ __forceinline__ void role_end(const Scratch& sc, int r) {
     atomicMax(&sc.rstamp[2 * (r * kStampSub + (blockIdx.x & (kStampSub - 1))) + 1],
               (unsigned long long)wall_clock64());
 }
+// A wave reached progress mark r (first and last arrival are recorded).
+__device__ __forceinline__ void role_mark(unsigned long long* rstamp, int r) {
+  if (rstamp && (threadIdx.x & 63) == 0) {
+    const unsigned long long t = wall_clock64();
+    const size_t o = 2 * (r * kStampSub + (blockIdx.x & (kStampSub - 1)));
+    atomicMin(&rstamp[o], t);
+    atomicMax(&rstamp[o + 1], t);
+  }
+}
+__device__ __forceinline__ void role_mark(const Scratch& sc, int r) { role_mark(sc.rstamp, r); }
 
 #ifdef SWARM_PHASE_TIMING
 #define SWARM_STAMP(k)                                                    \
@@ -1758,11 +1772,13 @@ __device__ __forceinline__ void pair_filter_body(const Derived* __restrict__ d, 
     }
   }
   const int lane = threadIdx.x & 63;
+  role_mark(sc, kMarkFilterLoaded);
   const bool dense = __any(found > kKeep);
   int v = wave_incl_scan(found);
   int wbase = 0;
   if (lane == 63) wbase = atomicAdd(&sc.gnpairs[e], v);
   wbase = __builtin_amdgcn_readlane(wbase, 63);
+  role_mark(sc, kMarkFilterReserved);
   const int my_off = wbase + v - found;
   uint32_t* out = sc.gplist + (size_t)e * sc.pair_cap;
   const int cap = sc.pair_cap;

@@ -117,10 +117,12 @@ def test_l1_pairs_and_fused_policy_match_oracle(force):
     assert step == 3 + T
     for k in ("q", "img", "ang"):
         assert np.array_equal(got[k], st[k]), k
-    # the two parametrisations do exercise the two pair searches: every
-    # window after the first ride-along one filtered the lists, or none did
-    assert windows == step and filtered + waited > 0, list(stats)
+    # the two parametrisations do exercise the two pair searches: at the
+    # bench's speed every list is usable but (perhaps) the first window's,
+    # where the overlap removal's contacts push apart; ten times faster the
+    # translating agents outrun the lists
+    assert windows == step and filtered + waited == step, list(stats)
     if force == 10.0:
-        assert max(moved) < 1.5 and waited == 0 and filtered > 0, (moved, list(stats))
+        assert waited <= 1 and filtered >= step - 1, (moved, list(stats))
     else:
         assert max(moved) > 1.5 and waited > 0, (moved, list(stats))

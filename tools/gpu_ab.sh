@@ -4,7 +4,7 @@
 #   bash tools/gpu_ab.sh TAG prod NAME ...   (NAME -> tools/_variants/lib_NAME.so)
 set -uo pipefail
 tag=$1; shift
-out=gpurun_out/ab_$tag
+out=gpurun_out/$tag
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for v in "$@"; do

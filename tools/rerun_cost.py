@@ -10,7 +10,7 @@ import torch
 sys.path.insert(0, ".")
 sys.path.insert(0, "tools")
 sys.path.insert(0, "tests")
-from ablate_integrator import disc_states  # noqa: E402
+from bench_states import disc_states  # noqa: E402
 from gpu_harness import Harness, species_list  # noqa: E402
 
 torch.cuda.set_device(0)
