@@ -2683,9 +2683,16 @@ __device__ __forceinline__ void noise_group(const Derived* __restrict__ d, const
     const long s = (long)(t0 + (uint64_t)j) - (long)step_start;
     if (s >= 0 && s < len) {
       float* o = table + noise_index((size_t)M, (size_t)gi, (int)s, 0);
+#ifdef SWARM_EXP_NT_NOISE
+      // streaming stores: the table is read by the next window's run only
+      __builtin_nontemporal_store(g[0], o);
+      __builtin_nontemporal_store(g[1], o + cs);
+      __builtin_nontemporal_store(g[2], o + 2 * cs);
+#else
       o[0] = g[0];
       o[cs] = g[1];
       o[2 * cs] = g[2];
+#endif
     }
   }
 }
