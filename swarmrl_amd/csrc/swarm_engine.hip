@@ -1459,7 +1459,19 @@ int launch_build(swarm_engine* e, hipStream_t stream) {
   // 2-D: the pair search left block-local union-find roots and a cross list
   // (build_pairs_body); 3-D (k_build_pairs3): the whole pair list is unioned
   const bool local = e->params.n_dims == 2 && e->sc.local_uf;
-  if (e->big_build && swarm::build_lds_words_packed(e->n) * 4 <= kMaxLds) {
+  if (e->sc.bmisc) {  // multi-workgroup build: union, sizes, classes, slots + pair lists
+    const unsigned nbp = (unsigned)((e->n + 255) / 256);
+    hipLaunchKernelGGL(swarm::k_mwb_union, dim3((nbp + 3) / 4, e->n_envs), dim3(256), 0, stream,
+                       e->st, e->sc);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(swarm::k_mwb_size, dim3(nbp, e->n_envs), dim3(256), 0, stream, e->st, e->sc);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(swarm::k_mwb_class, dim3(nbp, e->n_envs), dim3(256), 0, stream, e->st,
+                       e->sc);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(swarm::k_mwb_slots, dim3(3 * nbp, e->n_envs), dim3(256), 0, stream, e->st,
+                       e->sc, (int)nbp);
+  } else if (e->big_build && swarm::build_lds_words_packed(e->n) * 4 <= kMaxLds) {
     if (local)
       hipLaunchKernelGGL(swarm::k_cluster_build_packed<true>, dim3(e->n_envs), dim3(1024),
                          swarm::build_lds_words_packed(e->n) * 4, stream, e->st, e->sc);
@@ -2042,6 +2054,13 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   }
   rc = rc ? rc : dev_alloc(e, &e->sc.gnpairs, (size_t)n_envs);
   if (e->big_build) rc = rc ? rc : dev_alloc(e, &e->sc.gclus, 3 * M);
+  // 2-D envs of the large-N build after the block-local pair search: the
+  // build spread over the chip (k_mwb_*) instead of one workgroup
+  e->sc.bmisc = nullptr;
+#ifndef SWARM_EXP_NO_MWB
+  if (e->big_build && params->n_dims == 2 && e->sc.local_uf)
+    rc = rc ? rc : dev_alloc(e, &e->sc.bmisc, (size_t)n_envs * swarm::kBmWords);
+#endif
   rc = rc ? rc : dev_alloc(e, &e->sc.wave_npairs, (size_t)n_envs * (S / 64));
   rc = rc ? rc : dev_alloc(e, &e->sc.phase, 32 + 4 * (size_t)n_envs * (S / 64));
   rc = rc ? rc : dev_alloc(e, &e->sc.disp, M);

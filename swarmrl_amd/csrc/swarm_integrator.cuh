@@ -50,6 +50,14 @@ constexpr int kPairsPerWave = 256;  // neighbour pairs of one 64-lane wave (4 pa
 constexpr int kBigMax = 1024;
 constexpr int kBigPairs = 4096;
 constexpr int kBigMark = -0x40000000;  // cbase of a big cluster's root
+// multi-workgroup build (k_mwb_*): sc.bmisc layout per env
+constexpr int kBmWords = 256;  // sc.bmisc words per env
+constexpr int kBmMisc = 0;     // [16]: 0 overflow, 1 waves, 2 pair overflow, 3 free lanes,
+                               // 4 big members, 6 big pairs, 8 / 9 tickets
+constexpr int kBmClass = 16;   // [68] cluster count per class
+constexpr int kBmWave = 84;    // [68] first wave of a class
+constexpr int kBmFree = 152;   // [68] first free tail lane of a class (singletons)
+constexpr uint32_t kMwbBig = 0x80000000u;  // B of a big cluster's root: kMwbBig | first member
 constexpr int kMaxMovers = 1024;       // listed movers per env (more: exact re-run)
 // Candidate lists of the next window's pair search (latency-bound ride-along
 // builds, see cand_build_body): per particle up to kCandMax partners j > i
@@ -231,6 +239,7 @@ struct Scratch {
   int32_t* gnx;       // [E] cross-block pairs found
   int32_t local_uf;   // 1: the 2-D pair search unions its blocks' pairs (lroot, xpairs)
   int32_t* gclus;     // [3][M] cluster sizes / bases / slots (large-N build only)
+  int32_t* bmisc;     // [E][kBmWords] multi-workgroup build counters (null: one-workgroup build)
   int32_t pair_cap;   // pairs per env
   int32_t one_pass;   // 1: pack clusters so that a wave has <= 64 pairs
   int32_t fill_singletons;  // 1: singletons take the tail lanes of the other classes
@@ -1541,7 +1550,18 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
   // the local root, and in the upper half the pairs this particle found
   // (as the lower id: each pair once) -- the cluster build's pair count per
   // cluster without another pass over the pair list
-  if (valid) sc.lroot[base + i] = lid[uf_find(lpar, t)] | (min(found, 0xffff) << 16);
+  if (valid) {
+    const int32_t lr = lid[uf_find(lpar, t)];
+    sc.lroot[base + i] = lr | (min(found, 0xffff) << 16);
+    if (sc.bmisc) {  // the multi-workgroup build's forest and zeroed cluster words
+      sc.gclus[base + i] = lr;
+      sc.gclus[M + base + i] = 0;
+    }
+  }
+  if (sc.bmisc && bx == 0) {  // its counters and the wave pair counts
+    for (int k = t; k < kBmWords; k += T) sc.bmisc[(size_t)e * kBmWords + k] = 0;
+    for (int k = t; k < sc.wmax; k += T) sc.wave_npairs[(size_t)e * sc.wmax + k] = 0;
+  }
   // wave prefix sums, one atomic per wave: every pair to the pair list, the
   // pairs whose partner lies outside the block (all of a dense wave's) also
   // to the cross list
@@ -2447,6 +2467,297 @@ template <bool kLocal>
 __global__ __launch_bounds__(1024) void k_cluster_build_packed(DevState st, Scratch sc) {
   extern __shared__ __align__(16) unsigned char smem[];
   cluster_build_env_packed<kLocal>(st, sc, blockIdx.x, smem, sc.gnpairs[blockIdx.x]);
+}
+
+// ------------------------------------- multi-workgroup build (large N, 2-D)
+// The cluster build of cluster_build_env_packed<true> spread over the chip
+// in four launches of 256-thread workgroups (one env per grid row), for envs
+// whose one-workgroup build is the slice's longest serial stage (C5, 16384
+// colloids: 47.5 us on one CU).  Same decomposition rules -- connected
+// components of the rc + skin graph, lanes per cluster by packing class,
+// singletons into the classes' tail lanes -- with the per-particle and
+// per-cluster words in global memory (sc.gclus) and the class counters in
+// sc.bmisc; the slot order differs from the one-workgroup build, which
+// results do not depend on (fixed-point sums).
+//   gclus[0 .. M):  P, the union-find forest; the pair search writes each
+//                   particle's block-local root (a forest of depth one)
+//   gclus[M .. 2M): B, per root: size | pairs << 16 (k_mwb_size), then
+//                   class rank | class << 24, or kMwbBig | first member
+//                   (k_mwb_class); zeroed by the pair search
+//   gclus[2M .. 3M): A, root | rank in the cluster << 16 (k_mwb_size)
+// Every launch boundary orders the phases; inside a launch the workgroups
+// meet only through agent-scope atomics, and the last workgroup of a launch
+// (a ticket) does the launch's serial remainder.
+
+__device__ __forceinline__ int32_t agent_load(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Root of x in the global forest while other workgroups link roots
+// (agent-scope loads: a link made on another XCD is seen).
+__device__ __forceinline__ int mwb_find(const int32_t* P, int x) {
+  int p = agent_load(P + x);
+  while (p != x) {
+    x = p;
+    p = agent_load(P + x);
+  }
+  return x;
+}
+
+// The last workgroup of a launch to finish (ticket): every earlier
+// workgroup's atomics are visible to it after the acquire fence.
+__device__ __forceinline__ bool mwb_last_block(int32_t* ticket, int nblocks, int32_t* flag_lds) {
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = atomicAdd(ticket, 1);
+    *flag_lds = t == nblocks - 1;
+    if (t == nblocks - 1) *ticket = 0;  // ready for the next build
+  }
+  __syncthreads();
+  const bool last = *flag_lds != 0;
+  if (last) __threadfence();
+  return last;
+}
+
+// k_mwb_union: the cross-block pairs of the pair search, unioned in the
+// global forest (the larger root is hooked under the smaller by CAS; a
+// failed CAS -- the root was hooked meanwhile -- walks again).
+__global__ __launch_bounds__(256) void k_mwb_union(DevState st, Scratch sc) {
+  const int e = blockIdx.y;
+  const size_t base = (size_t)e * st.n;
+  int32_t* P = sc.gclus + base;
+  const int nx = min(sc.gnx[e], sc.pair_cap);
+  const uint32_t* xl = sc.xpairs + (size_t)e * sc.pair_cap;
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nx; k += gridDim.x * blockDim.x) {
+    const uint32_t pr = xl[k];
+    int a = (int)(pr & 0xffffu), b = (int)(pr >> 16);
+    while (true) {
+      a = mwb_find(P, a);
+      b = mwb_find(P, b);
+      if (a == b) break;
+      if (a > b) {
+        const int t = a;
+        a = b;
+        b = t;
+      }
+      int expect = b;
+      if (__hip_atomic_compare_exchange_strong(P + b, &expect, a, __ATOMIC_RELAXED,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        break;
+    }
+  }
+}
+
+// k_mwb_size: every particle's root (the forest is final), its rank in the
+// cluster and the cluster's size and pair count (one atomic per particle on
+// its root's B word; the pair count is the pair search's per-particle count).
+__global__ __launch_bounds__(256) void k_mwb_size(DevState st, Scratch sc) {
+  const int e = blockIdx.y, N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const int32_t* P = sc.gclus + base;
+  int32_t* B = sc.gclus + M + base;
+  int r = i, p = P[i];
+  while (p != r) {
+    r = p;
+    p = P[r];
+  }
+  const int np_i = sc.one_pass ? (int)((uint32_t)sc.lroot[base + i] >> 16) : 0;
+  const uint32_t rank = (uint32_t)atomicAdd(&B[r], 1 + (np_i << 16)) & 0xffffu;
+  sc.gclus[2 * M + base + i] = r | (int32_t)(rank << 16);
+}
+
+// k_mwb_class: every root's packing class and rank in it (a wave-aggregated
+// atomic for the singleton and pair classes); a big cluster (wider than a
+// wave) reserves its members' range of the big list.  The last workgroup
+// lays the classes out in waves (cluster_build_env) or sends the env to the
+// global path (a list overflowed or too many big-cluster members).
+__global__ __launch_bounds__(256) void k_mwb_class(DevState st, Scratch sc) {
+  __shared__ int32_t last_flag;
+  const int e = blockIdx.y, N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  int32_t* bm = sc.bmisc + (size_t)e * kBmWords;
+  int32_t* B = sc.gclus + M + base;
+  const int32_t* A = sc.gclus + 2 * M + base;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool root = i < N && (A[i] & 0xffff) == i;
+  const uint32_t b = root ? (uint32_t)B[i] : 0u;
+  const int s = (int)(b & 0xffffu), pairs = (int)(b >> 16);
+  const int w = sc.one_pass ? max(s, min(min(pairs, 64), 2 * s)) : s;
+  const int r1 = wave_class_add(bm + kBmClass + 1, root && s <= 64 && w == 1);
+  const int r2 = wave_class_add(bm + kBmClass + 2, root && s <= 64 && w == 2);
+  if (root) {
+    if (s > 64)  // a big cluster, run by k_check's workgroup
+      B[i] = (int32_t)(kMwbBig | (uint32_t)atomicAdd(bm + kBmMisc + 4, s));
+    else
+      B[i] = (w == 1 ? r1 : (w == 2 ? r2 : atomicAdd(bm + kBmClass + w, 1))) | (w << 24);
+  }
+  if (!mwb_last_block(bm + kBmMisc + 8, gridDim.x, &last_flag)) return;
+  const int tid = threadIdx.x;
+  const bool over = agent_load(sc.gnpairs + e) > sc.pair_cap || agent_load(sc.gnx + e) > sc.pair_cap ||
+                    agent_load(bm + kBmMisc + 4) > min(kBigMax, 1024);
+  if (over) {
+    if (tid == 0) {
+      bm[kBmMisc + 0] = 1;
+      sc.fallback[e] = 1;
+      sc.env_waves[e] = 0;
+      sc.big_n[e] = 0;
+      sc.big_np[e] = 0;
+    }
+    return;
+  }
+  if (tid < 64) {  // waves per class (cluster_build_env)
+    const int w = tid + 1;
+    const int per = udiv_small(64, w);
+    const int cnt = agent_load(bm + kBmClass + w);
+    int32_t nw = udiv_small(cnt + per - 1, per);
+    int32_t fl = 0;
+    if (w >= 2 && nw > 0) fl = (nw - 1) * (64 - per * w) + (64 - (cnt - (nw - 1) * per) * w);
+    int32_t f = fl;
+    f = wave_incl_scan(f);
+    bm[kBmFree + w] = f - fl;
+    const int32_t F = sc.fill_singletons ? __builtin_amdgcn_readlane(f, 63) : 0;
+    if (w == 1) nw = (max(cnt - F, 0) + 63) / 64;
+    int32_t v = nw;
+    v = wave_incl_scan(v);
+    bm[kBmWave + w] = v - nw;
+    if (tid == 63) {
+      bm[kBmMisc + 1] = v;
+      bm[kBmMisc + 3] = F;
+      bm[kBmFree + 65] = F;
+    }
+  }
+}
+
+// A particle's wave slot from its root's class word and the class layout
+// (tables in LDS: counts, first waves, free-lane bases; misc[3] = free lanes).
+__device__ __forceinline__ int mwb_slot(int32_t a, int32_t broot, const int32_t* cls,
+                                        const int32_t* wbase, const int32_t* fbase, int nfree) {
+  const int rank = (int)((uint32_t)a >> 16);
+  if ((uint32_t)broot & kMwbBig) return -1 - (int)(((uint32_t)broot & ~kMwbBig) + rank);
+  const int s = (broot >> 24) & 0x7f;
+  const int r = broot & 0xffffff;
+  int cb;
+  if (s == 1 && r < nfree) {
+    const int v = free_class(fbase, r), per = udiv_small(64, v);
+    const int nw = udiv_small(cls[v] + per - 1, per);
+    const int ffull = 64 - per * v;
+    const int t = r - fbase[v];
+    int j, lane;
+    if (t < (nw - 1) * ffull) {
+      j = udiv_small(t, ffull);
+      lane = per * v + (t - j * ffull);
+    } else {
+      j = nw - 1;
+      lane = (cls[v] - (nw - 1) * per) * v + (t - (nw - 1) * ffull);
+    }
+    cb = (wbase[v] + j) * 64 + lane;
+  } else if (s == 1) {
+    const int r2 = r - nfree;
+    cb = (wbase[1] + r2 / 64) * 64 + r2 % 64;
+  } else {
+    const int per = udiv_small(64, s), rq = udiv_small(r, per);
+    cb = (wbase[s] + rq) * 64 + (r - rq * per) * s;
+  }
+  return cb + rank;
+}
+
+// k_mwb_slots: workgroups [0, nbp) place the particles (perm, slot_of, root,
+// big list); the others file the pairs into their waves' lists (both ends'
+// slots worked out again from A and B, so the two roles run side by side).
+// The last pair workgroup closes the build (wave pair counts, waves, flags).
+__global__ __launch_bounds__(256) void k_mwb_slots(DevState st, Scratch sc, int nbp) {
+  __shared__ int32_t tab[3 * 68];
+  __shared__ int32_t last_flag;
+  const int e = blockIdx.y, N = st.n, tid = threadIdx.x;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int32_t* bm = sc.bmisc + (size_t)e * kBmWords;
+  if (bm[kBmMisc + 0]) return;  // the env runs on the global path (k_mwb_class)
+  for (int k = tid; k < 3 * 68; k += blockDim.x) tab[k] = bm[kBmClass + k];
+  __syncthreads();
+  const int32_t *cls = tab, *wbase = tab + 68, *fbase = tab + 136;
+  const int nfree = bm[kBmMisc + 3];
+  const int32_t* B = sc.gclus + M + base;
+  const int32_t* A = sc.gclus + 2 * M + base;
+  if ((int)blockIdx.x < nbp) {
+    const int i = blockIdx.x * blockDim.x + tid;
+    if (i >= N) return;
+    const int32_t a = A[i];
+    const int root = a & 0xffff;
+    const int slot = mwb_slot(a, B[root], cls, wbase, fbase, nfree);
+    if (slot < 0)
+      sc.big_list[(size_t)e * kBigMax + (-1 - slot)] = i;
+    else
+      sc.perm[(size_t)e * sc.S + slot] = i;
+    sc.slot_of[base + i] = slot;
+    sc.root[base + i] = root;
+    return;
+  }
+  int32_t* bmw = sc.bmisc + (size_t)e * kBmWords;
+  const int npairs = min(sc.gnpairs[e], sc.pair_cap);
+  const uint32_t* plist = sc.gplist + (size_t)e * sc.pair_cap;
+  const int nbq = gridDim.x - nbp;
+  const int wmax = sc.wmax;
+  constexpr int kU = 4;
+  for (int k0 = (blockIdx.x - nbp) * blockDim.x + tid; k0 < npairs; k0 += kU * nbq * blockDim.x) {
+    uint32_t pr[kU];
+    int32_t ai[kU], aj[kU], bi[kU], bj[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int k = k0 + u * nbq * blockDim.x;
+      pr[u] = k < npairs ? plist[k] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      ai[u] = A[pr[u] & 0xffffu];
+      aj[u] = A[pr[u] >> 16];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      bi[u] = B[ai[u] & 0xffff];
+      bj[u] = B[aj[u] & 0xffff];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (k0 + u * nbq * blockDim.x >= npairs) continue;
+      const int i = (int)(pr[u] & 0xffffu), j = (int)(pr[u] >> 16);
+      const int si = mwb_slot(ai[u], bi[u], cls, wbase, fbase, nfree);
+      const int sj = mwb_slot(aj[u], bj[u], cls, wbase, fbase, nfree);
+      const uint32_t spp =
+          sc.multi_species ? (uint32_t)(st.species[i] * kMaxSpecies + st.species[j]) : 0u;
+      if (si < 0) {  // a big cluster's pair (both members of it)
+        const int idx = atomicAdd(bmw + kBmMisc + 6, 1);
+        if (idx < kBigPairs)
+          sc.big_pairs[(size_t)e * kBigPairs + idx] =
+              (uint32_t)(-1 - si) | ((uint32_t)(-1 - sj) << 10) | (spp << 20);
+        else
+          atomicOr(bmw + kBmMisc + 2, 1);  // -> global path
+        continue;
+      }
+      const int wv = si >> 6;
+      const int idx = atomicAdd(&sc.wave_npairs[(size_t)e * wmax + wv], 1);
+      if (idx < kPairsPerWave)
+        sc.pairs[((size_t)e * wmax + wv) * kPairsPerWave + idx] =
+            (uint32_t)(si & 63) | ((uint32_t)(sj & 63) << 6) | (spp << 12);
+      else
+        atomicOr(bmw + kBmMisc + 2, 1);  // a wave with more than kPairsPerWave pairs
+    }
+  }
+  if (!mwb_last_block(bmw + kBmMisc + 9, nbq, &last_flag)) return;
+  const int nw = bm[kBmMisc + 1];
+  for (int w = tid; w < nw; w += blockDim.x) {
+    int32_t* c = &sc.wave_npairs[(size_t)e * wmax + w];
+    *c = min(agent_load(c), kPairsPerWave);
+  }
+  if (tid == 0) {
+    const int ovf = agent_load(bmw + kBmMisc + 2);
+    sc.env_waves[e] = ovf ? 0 : nw;
+    sc.fallback[e] = ovf ? 1 : 0;
+    sc.big_n[e] = bm[kBmMisc + 4];
+    sc.big_np[e] = min(agent_load(bmw + kBmMisc + 6), kBigPairs);
+  }
 }
 
 // kLocal: after the 2-D pair search (block-local forests + cross list)

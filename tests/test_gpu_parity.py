@@ -462,6 +462,67 @@ def test_big_clusters_run_in_check_bit_exact(wide, monkeypatch):
         assert fb[0] == 0 and w[0] > 0, (fb, w)
 
 
+@pytest.mark.parametrize("E", [1, 2])
+def test_large_build_clusters_of_every_width_bit_exact(E):
+    """The multi-workgroup large-N build (k_mwb_*, 2-D envs above 4096
+    colloids): 8192 colloids of two species on a jittered lattice (no pairs)
+    with patches at 2.5 um spacing -- 10 x 10 (big clusters: run by k_check's
+    workgroup), 6 x 6 (110 pairs: a two-pass wave), 4 x 4 and 2 x 1 --
+    three windows bit-exact against the oracle on every env, no global-path
+    re-run.  E = 2: one grid row per env."""
+    from gpu_harness import Harness, species_list
+
+    rng = np.random.default_rng(88)
+    n, L, sp = 8192, 528.0, 5.5
+    box = [L, L, L]
+    patches = [(10, 30.0, 30.0), (10, 300.0, 100.0), (6, 150.0, 400.0), (6, 420.0, 420.0),
+               (4, 60.0, 250.0), (4, 250.0, 250.0), (2, 480.0, 40.0)]
+    pts = []
+    for k, cx, cy in patches:
+        for gx in range(k):
+            for gy in range(k if k > 2 else 1):
+                pts.append((cx + 2.5 * gx, cy + 2.5 * gy))
+    taken = np.array(pts)
+    g = int(L / sp)
+    cells = [(i, j) for i in range(g) for j in range(g)]
+    rng.shuffle(cells)
+    for i, j in cells:
+        if len(pts) >= n:
+            break
+        p = (sp * (i + 0.5) + rng.uniform(-0.4, 0.4), sp * (j + 0.5) + rng.uniform(-0.4, 0.4))
+        if np.min(np.hypot(taken[:, 0] - p[0], taken[:, 1] - p[1])) > 8.0:
+            pts.append(p)
+    assert len(pts) == n
+    pos = np.zeros((n, 3))
+    pos[:, :2] = pts
+    types = (rng.random(n) < 0.3).astype(int)
+    types[:len(taken)] = 0  # the patches: radius 1 (2.5 um apart, within r_c + skin)
+    states = []
+    for e in range(E):
+        a = 2 * np.pi * rng.random(n)
+        dirs = np.stack([np.cos(a), np.sin(a), np.zeros(n)], 1)
+        states.append(oracle.state_from_positions(pos, dirs, box))
+    h = Harness(box, 1e-3, 1.0239, 1.0239, 7, species_list(), types, n_envs=E)
+    h.upload(states)
+    step = 0
+    for nsteps in (100, 100, 40):
+        f = rng.choice([0.0, 5.0], E * n).astype(np.float32)
+        t = rng.choice([-5.0, 0.0, 5.0], E * n).astype(np.float32)
+        h.set_actions(f, t)
+        h.integrate(nsteps)
+        got = h.download()
+        for e in range(E):
+            sl = slice(e * n, (e + 1) * n)
+            states[e], _, _ = oracle.bd_run(h.op, states[e], types, f[sl], t[sl], nsteps,
+                                            step0=step, env=e)
+            _eq(got[e], states[e])
+        step += nsteps
+        fb = np.zeros(E, np.int32)
+        w = np.zeros(E, np.int32)
+        h.native.call("swarm_engine_window_stats", fb.ctypes.data, w.ctypes.data)
+        assert np.all(fb == 0) and np.all(w > 0), (fb, w)
+
+
 def test_c4_size_8_envs_x_1024_bit_exact():
     """SURVEY config C4 per GPU (8 envs x 1024 colloids, area fraction 0.1):
     the latency-bound wide run with its next-window noise, three windows,
