@@ -536,6 +536,7 @@ struct FeatureTail {
 template <int D, int K>
 struct PolicyTail {
   swarm::MlpArgs m;
+  const float* sw = nullptr;  // the weights staged in LDS (stage_mlp_rows), or read in place
   using Pre = unsigned long long;
   __device__ Pre pre(const VisionArgs& va, int e, int row) const {
     return m.state[(size_t)e * va.n_agents + row];
@@ -559,7 +560,10 @@ struct PolicyTail {
         if (k < nb) o[k] = x[k];
     }
     float lg[K];
-    swarm::mlp_group_logits_direct<G, D, K>(m, x, sub, lg);
+    if (sw)
+      swarm::mlp_group_logits<G, D, K>(m, sw, x, sub, lg);
+    else
+      swarm::mlp_group_logits_direct<G, D, K>(m, x, sub, lg);
     if (sub == 0) {
       swarm::policy_emit<K>(m, a, lg, ctr);
       m.state[a] = ctr + 1ull;
@@ -843,7 +847,12 @@ __global__ __launch_bounds__(1024) void k_vision_policy_cbuild(DevState st,
     swarm::cluster_build_env<false, true, false>(st, sc, b, smem, sc.gnpairs[b]);
   } else {
     auto* hits = reinterpret_cast<uint32_t(*)[1024]>(smem);
-    const PolicyTail<D, K> tail{m};
+    // the actor's rows into LDS behind the hit lists before any group starts
+    // (the groups' tails then read them at LDS latency, not L2's)
+    float* sw = reinterpret_cast<float*>(smem + (size_t)kVisionHits * 1024 * sizeof(uint32_t));
+    swarm::stage_mlp_rows<D, K>(m, sw);
+    __syncthreads();
+    const PolicyTail<D, K> tail{m, sw};
     vision_body<NB, G, false, 1024, PolicyTail<D, K>>(st, d, va, b - va.n_envs, 0, hits, tail);
   }
   swarm::role_end(sc, role);
@@ -1459,18 +1468,21 @@ int launch_build(swarm_engine* e, hipStream_t stream) {
   // 2-D: the pair search left block-local union-find roots and a cross list
   // (build_pairs_body); 3-D (k_build_pairs3): the whole pair list is unioned
   const bool local = e->params.n_dims == 2 && e->sc.local_uf;
-  if (e->sc.bmisc) {  // multi-workgroup build: union, sizes, classes, slots + pair lists
+  if (e->sc.bmisc) {  // multi-workgroup build: union, sizes, classes, slots, wave pair lists
     const unsigned nbp = (unsigned)((e->n + 255) / 256);
     hipLaunchKernelGGL(swarm::k_mwb_union, dim3((nbp + 3) / 4, e->n_envs), dim3(256), 0, stream,
                        e->st, e->sc);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(swarm::k_mwb_size, dim3(nbp, e->n_envs), dim3(256), 0, stream, e->st, e->sc);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(swarm::k_mwb_class, dim3(nbp, e->n_envs), dim3(256), 0, stream, e->st,
+    hipLaunchKernelGGL(swarm::k_mwb_class, dim3((unsigned)((e->n + 1023) / 1024), e->n_envs),
+                       dim3(1024), 0, stream, e->st, e->sc);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(swarm::k_mwb_slots, dim3(nbp, e->n_envs), dim3(256), 0, stream, e->st,
                        e->sc);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(swarm::k_mwb_slots, dim3(3 * nbp, e->n_envs), dim3(256), 0, stream, e->st,
-                       e->sc, (int)nbp);
+    hipLaunchKernelGGL(swarm::k_mwb_pairs, dim3((unsigned)((e->sc.wmax + 3) / 4), e->n_envs),
+                       dim3(256), 0, stream, e->st, e->sc);
   } else if (e->big_build && swarm::build_lds_words_packed(e->n) * 4 <= kMaxLds) {
     if (local)
       hipLaunchKernelGGL(swarm::k_cluster_build_packed<true>, dim3(e->n_envs), dim3(1024),
@@ -2053,14 +2065,16 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     rc = rc ? rc : dev_alloc(e, &e->sc.grank, M);
   }
   rc = rc ? rc : dev_alloc(e, &e->sc.gnpairs, (size_t)n_envs);
-  if (e->big_build) rc = rc ? rc : dev_alloc(e, &e->sc.gclus, 3 * M);
   // 2-D envs of the large-N build after the block-local pair search: the
-  // build spread over the chip (k_mwb_*) instead of one workgroup
+  // build spread over the chip (k_mwb_*) instead of one workgroup, with a
+  // fourth per-particle word (the offset of its pairs in the pair list)
   e->sc.bmisc = nullptr;
-#ifndef SWARM_EXP_NO_MWB
-  if (e->big_build && params->n_dims == 2 && e->sc.local_uf)
-    rc = rc ? rc : dev_alloc(e, &e->sc.bmisc, (size_t)n_envs * swarm::kBmWords);
+  bool mwb = e->big_build && params->n_dims == 2 && e->sc.local_uf;
+#ifdef SWARM_EXP_NO_MWB
+  mwb = false;
 #endif
+  if (e->big_build) rc = rc ? rc : dev_alloc(e, &e->sc.gclus, (mwb ? 4 : 3) * M);
+  if (mwb) rc = rc ? rc : dev_alloc(e, &e->sc.bmisc, (size_t)n_envs * swarm::kBmWords);
   rc = rc ? rc : dev_alloc(e, &e->sc.wave_npairs, (size_t)n_envs * (S / 64));
   rc = rc ? rc : dev_alloc(e, &e->sc.phase, 32 + 4 * (size_t)n_envs * (S / 64));
   rc = rc ? rc : dev_alloc(e, &e->sc.disp, M);
@@ -2912,13 +2926,13 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
     HIP_TRY(hipGetLastError());
   }
   if (pol && ride_ok && e->ride_stage == 3) {  // cluster build | cone + policy (l1_pairs)
-#ifndef SWARM_EXP_CONE_G
-#define SWARM_EXP_CONE_G 16
-#endif
-    constexpr int GC = SWARM_EXP_CONE_G;
+    // 16 lanes per agent (32 measured: the cone's bins summed ~2 us sooner,
+    // the MLP tail ~2 us longer, no change)
+    constexpr int GC = 16;
     const int ncb = (int)((total * GC + 1023) / 1024);
+    const size_t rows = ((size_t)pol->hidden * swarm::MlpRow<4, 4>::kStride + 4) * sizeof(float);
     const size_t lds = std::max(build_lds_bytes(e->n, e->sc.pair_cap),
-                                (size_t)kVisionHits * 1024 * sizeof(uint32_t));
+                                (size_t)kVisionHits * 1024 * sizeof(uint32_t) + rows);
     hipLaunchKernelGGL((k_vision_policy_cbuild<4, GC, 4, 4>), dim3((unsigned)(e->n_envs + ncb)),
                        dim3(1024), lds, e->stream, e->st, e->d_derived, va, *pol, e->sc);
     HIP_TRY(hipGetLastError());

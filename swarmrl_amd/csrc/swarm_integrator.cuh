@@ -1584,6 +1584,8 @@ __device__ __forceinline__ void build_pairs_body(const Derived* __restrict__ d, 
   xbase = __builtin_amdgcn_readlane(xbase, 63);
   const int my_off = wbase + v - found;
   const int my_xoff = xbase + vx - nx;
+  // the multi-workgroup build reads a particle's pairs from here
+  if (sc.bmisc && valid) sc.gclus[3 * M + base + i] = my_off;
   uint32_t* out = sc.gplist + (size_t)e * sc.pair_cap;
   uint32_t* xout = sc.xpairs + (size_t)e * sc.pair_cap;
   if (!dense) {
@@ -2504,10 +2506,12 @@ __device__ __forceinline__ int mwb_find(const int32_t* P, int x) {
   return x;
 }
 
-// The last workgroup of a launch to finish (ticket): every earlier
-// workgroup's atomics are visible to it after the acquire fence.
+// The last workgroup of a launch to finish (ticket).  No fences: what the
+// last workgroup reads are counters the others changed by atomics whose
+// results they waited for before their ticket (an agent-scope fence would
+// write back and invalidate the L2: ~0.4 us per workgroup, measured 24 us
+// for a 64-workgroup launch).
 __device__ __forceinline__ bool mwb_last_block(int32_t* ticket, int nblocks, int32_t* flag_lds) {
-  __threadfence();
   __syncthreads();
   if (threadIdx.x == 0) {
     const int t = atomicAdd(ticket, 1);
@@ -2515,9 +2519,7 @@ __device__ __forceinline__ bool mwb_last_block(int32_t* ticket, int nblocks, int
     if (t == nblocks - 1) *ticket = 0;  // ready for the next build
   }
   __syncthreads();
-  const bool last = *flag_lds != 0;
-  if (last) __threadfence();
-  return last;
+  return *flag_lds != 0;
 }
 
 // k_mwb_union: the cross-block pairs of the pair search, unioned in the
@@ -2569,35 +2571,45 @@ __global__ __launch_bounds__(256) void k_mwb_size(DevState st, Scratch sc) {
   sc.gclus[2 * M + base + i] = r | (int32_t)(rank << 16);
 }
 
-// k_mwb_class: every root's packing class and rank in it (a wave-aggregated
-// atomic for the singleton and pair classes); a big cluster (wider than a
-// wave) reserves its members' range of the big list.  The last workgroup
-// lays the classes out in waves (cluster_build_env) or sends the env to the
-// global path (a list overflowed or too many big-cluster members).
-__global__ __launch_bounds__(256) void k_mwb_class(DevState st, Scratch sc) {
+// k_mwb_class: every root's packing class and rank in it, counted per
+// workgroup in LDS (wave-aggregated for the singleton and pair classes) and
+// reserved with one global atomic per class and workgroup; a big cluster
+// (wider than a wave) reserves its members' range of the big list.  The
+// last workgroup lays the classes out in waves (cluster_build_env) and
+// publishes the env's waves and flags, or sends the env to the global path
+// (a list overflowed or too many big-cluster members).
+__global__ __launch_bounds__(1024) void k_mwb_class(DevState st, Scratch sc) {
+  __shared__ int32_t lcnt[68], lbase[68];
   __shared__ int32_t last_flag;
-  const int e = blockIdx.y, N = st.n;
+  const int e = blockIdx.y, N = st.n, tid = threadIdx.x;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   int32_t* bm = sc.bmisc + (size_t)e * kBmWords;
   int32_t* B = sc.gclus + M + base;
   const int32_t* A = sc.gclus + 2 * M + base;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid < 68) lcnt[tid] = 0;
+  __syncthreads();
+  const int i = blockIdx.x * blockDim.x + tid;
   const bool root = i < N && (A[i] & 0xffff) == i;
   const uint32_t b = root ? (uint32_t)B[i] : 0u;
   const int s = (int)(b & 0xffffu), pairs = (int)(b >> 16);
   const int w = sc.one_pass ? max(s, min(min(pairs, 64), 2 * s)) : s;
-  const int r1 = wave_class_add(bm + kBmClass + 1, root && s <= 64 && w == 1);
-  const int r2 = wave_class_add(bm + kBmClass + 2, root && s <= 64 && w == 2);
+  const int r1 = wave_class_add(lcnt + 1, root && s <= 64 && w == 1);
+  const int r2 = wave_class_add(lcnt + 2, root && s <= 64 && w == 2);
+  int lr = w == 1 ? r1 : r2;
+  if (root && s <= 64 && w > 2) lr = atomicAdd(&lcnt[w], 1);
+  __syncthreads();
+  if (tid < 68 && lcnt[tid] > 0) lbase[tid] = atomicAdd(bm + kBmClass + tid, lcnt[tid]);
+  __syncthreads();
   if (root) {
     if (s > 64)  // a big cluster, run by k_check's workgroup
       B[i] = (int32_t)(kMwbBig | (uint32_t)atomicAdd(bm + kBmMisc + 4, s));
     else
-      B[i] = (w == 1 ? r1 : (w == 2 ? r2 : atomicAdd(bm + kBmClass + w, 1))) | (w << 24);
+      B[i] = (lbase[w] + lr) | (w << 24);
   }
   if (!mwb_last_block(bm + kBmMisc + 8, gridDim.x, &last_flag)) return;
-  const int tid = threadIdx.x;
-  const bool over = agent_load(sc.gnpairs + e) > sc.pair_cap || agent_load(sc.gnx + e) > sc.pair_cap ||
-                    agent_load(bm + kBmMisc + 4) > min(kBigMax, 1024);
+  const int nbig = agent_load(bm + kBmMisc + 4);
+  const bool over = agent_load(sc.gnpairs + e) > sc.pair_cap ||
+                    agent_load(sc.gnx + e) > sc.pair_cap || nbig > min(kBigMax, 1024);
   if (over) {
     if (tid == 0) {
       bm[kBmMisc + 0] = 1;
@@ -2627,6 +2639,10 @@ __global__ __launch_bounds__(256) void k_mwb_class(DevState st, Scratch sc) {
       bm[kBmMisc + 1] = v;
       bm[kBmMisc + 3] = F;
       bm[kBmFree + 65] = F;
+      sc.env_waves[e] = v;
+      sc.fallback[e] = 0;  // set by k_mwb_pairs when a list overflows
+      sc.big_n[e] = nbig;
+      sc.big_np[e] = 0;
     }
   }
 }
@@ -2664,13 +2680,11 @@ __device__ __forceinline__ int mwb_slot(int32_t a, int32_t broot, const int32_t*
   return cb + rank;
 }
 
-// k_mwb_slots: workgroups [0, nbp) place the particles (perm, slot_of, root,
-// big list); the others file the pairs into their waves' lists (both ends'
-// slots worked out again from A and B, so the two roles run side by side).
-// The last pair workgroup closes the build (wave pair counts, waves, flags).
-__global__ __launch_bounds__(256) void k_mwb_slots(DevState st, Scratch sc, int nbp) {
+// k_mwb_slots: every particle's wave slot (perm, slot_of, root); a
+// big-cluster member lists its pairs (as the lower index) for k_check's
+// big-cluster run, its partner's member index worked out the same way.
+__global__ __launch_bounds__(256) void k_mwb_slots(DevState st, Scratch sc) {
   __shared__ int32_t tab[3 * 68];
-  __shared__ int32_t last_flag;
   const int e = blockIdx.y, N = st.n, tid = threadIdx.x;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   const int32_t* bm = sc.bmisc + (size_t)e * kBmWords;
@@ -2681,86 +2695,72 @@ __global__ __launch_bounds__(256) void k_mwb_slots(DevState st, Scratch sc, int 
   const int nfree = bm[kBmMisc + 3];
   const int32_t* B = sc.gclus + M + base;
   const int32_t* A = sc.gclus + 2 * M + base;
-  if ((int)blockIdx.x < nbp) {
-    const int i = blockIdx.x * blockDim.x + tid;
-    if (i >= N) return;
-    const int32_t a = A[i];
-    const int root = a & 0xffff;
-    const int slot = mwb_slot(a, B[root], cls, wbase, fbase, nfree);
-    if (slot < 0)
-      sc.big_list[(size_t)e * kBigMax + (-1 - slot)] = i;
-    else
-      sc.perm[(size_t)e * sc.S + slot] = i;
-    sc.slot_of[base + i] = slot;
-    sc.root[base + i] = root;
+  const int i = blockIdx.x * blockDim.x + tid;
+  if (i >= N) return;
+  const int32_t a = A[i];
+  const int root = a & 0xffff;
+  const int slot = mwb_slot(a, B[root], cls, wbase, fbase, nfree);
+  sc.slot_of[base + i] = slot;
+  sc.root[base + i] = root;
+  if (slot >= 0) {
+    sc.perm[(size_t)e * sc.S + slot] = i;
     return;
   }
-  int32_t* bmw = sc.bmisc + (size_t)e * kBmWords;
-  const int npairs = min(sc.gnpairs[e], sc.pair_cap);
+  sc.big_list[(size_t)e * kBigMax + (-1 - slot)] = i;
+  // the member's pairs (i the lower index): contiguous in the pair list
+  const int n_i = (int)((uint32_t)sc.lroot[base + i] >> 16);
+  const int off = sc.gclus[3 * M + base + i];
   const uint32_t* plist = sc.gplist + (size_t)e * sc.pair_cap;
-  const int nbq = gridDim.x - nbp;
-  const int wmax = sc.wmax;
-  constexpr int kU = 4;
-  for (int k0 = (blockIdx.x - nbp) * blockDim.x + tid; k0 < npairs; k0 += kU * nbq * blockDim.x) {
-    uint32_t pr[kU];
-    int32_t ai[kU], aj[kU], bi[kU], bj[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int k = k0 + u * nbq * blockDim.x;
-      pr[u] = k < npairs ? plist[k] : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      ai[u] = A[pr[u] & 0xffffu];
-      aj[u] = A[pr[u] >> 16];
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      bi[u] = B[ai[u] & 0xffff];
-      bj[u] = B[aj[u] & 0xffff];
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      if (k0 + u * nbq * blockDim.x >= npairs) continue;
-      const int i = (int)(pr[u] & 0xffffu), j = (int)(pr[u] >> 16);
-      const int si = mwb_slot(ai[u], bi[u], cls, wbase, fbase, nfree);
-      const int sj = mwb_slot(aj[u], bj[u], cls, wbase, fbase, nfree);
-      const uint32_t spp =
-          sc.multi_species ? (uint32_t)(st.species[i] * kMaxSpecies + st.species[j]) : 0u;
-      if (si < 0) {  // a big cluster's pair (both members of it)
-        const int idx = atomicAdd(bmw + kBmMisc + 6, 1);
-        if (idx < kBigPairs)
-          sc.big_pairs[(size_t)e * kBigPairs + idx] =
-              (uint32_t)(-1 - si) | ((uint32_t)(-1 - sj) << 10) | (spp << 20);
-        else
-          atomicOr(bmw + kBmMisc + 2, 1);  // -> global path
-        continue;
-      }
-      const int wv = si >> 6;
-      const int idx = atomicAdd(&sc.wave_npairs[(size_t)e * wmax + wv], 1);
-      if (idx < kPairsPerWave)
-        sc.pairs[((size_t)e * wmax + wv) * kPairsPerWave + idx] =
-            (uint32_t)(si & 63) | ((uint32_t)(sj & 63) << 6) | (spp << 12);
-      else
-        atomicOr(bmw + kBmMisc + 2, 1);  // a wave with more than kPairsPerWave pairs
-    }
-  }
-  if (!mwb_last_block(bmw + kBmMisc + 9, nbq, &last_flag)) return;
-  const int nw = bm[kBmMisc + 1];
-  for (int w = tid; w < nw; w += blockDim.x) {
-    int32_t* c = &sc.wave_npairs[(size_t)e * wmax + w];
-    *c = min(agent_load(c), kPairsPerWave);
-  }
-  if (tid == 0) {
-    const int ovf = agent_load(bmw + kBmMisc + 2);
-    sc.env_waves[e] = ovf ? 0 : nw;
-    sc.fallback[e] = ovf ? 1 : 0;
-    sc.big_n[e] = bm[kBmMisc + 4];
-    sc.big_np[e] = min(agent_load(bmw + kBmMisc + 6), kBigPairs);
+  for (int k = 0; k < n_i && off + k < sc.pair_cap; ++k) {
+    const int j = (int)(plist[off + k] >> 16);
+    const int32_t aj = A[j];
+    const int sj = mwb_slot(aj, B[aj & 0xffff], cls, wbase, fbase, nfree);
+    const uint32_t spp =
+        sc.multi_species ? (uint32_t)(st.species[i] * kMaxSpecies + st.species[j]) : 0u;
+    const int idx = atomicAdd(&sc.big_np[e], 1);
+    if (idx < kBigPairs)
+      sc.big_pairs[(size_t)e * kBigPairs + idx] =
+          (uint32_t)(-1 - slot) | ((uint32_t)(-1 - sj) << 10) | (spp << 20);
+    else
+      sc.fallback[e] = 1;  // -> global path
   }
 }
 
-// kLocal: after the 2-D pair search (block-local forests + cross list)
+// k_mwb_pairs: one wave per run wave: each lane's particle lists its pairs
+// (as the lower index, contiguous in the pair list from the pair search) at
+// its offset of the wave's exclusive scan -- the wave's pair list without
+// atomics; a wave with more than kPairsPerWave pairs sends the env to the
+// global path.
+__global__ __launch_bounds__(256) void k_mwb_pairs(DevState st, Scratch sc) {
+  const int e = blockIdx.y, N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int32_t* bm = sc.bmisc + (size_t)e * kBmWords;
+  if (bm[kBmMisc + 0]) return;
+  const int w = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6), lane = threadIdx.x & 63;
+  if (w >= bm[kBmMisc + 1]) return;
+  const int i = sc.perm[(size_t)e * sc.S + w * 64 + lane];
+  const int n_i = i >= 0 ? (int)((uint32_t)sc.lroot[base + i] >> 16) : 0;
+  const int off = i >= 0 ? sc.gclus[3 * M + base + i] : 0;
+  int v = n_i;
+  v = wave_incl_scan(v);
+  const int total = __builtin_amdgcn_readlane(v, 63);
+  const size_t wi = (size_t)e * sc.wmax + w;
+  if (lane == 0) sc.wave_npairs[wi] = min(total, kPairsPerWave);
+  if (total > kPairsPerWave) {
+    if (lane == 0) sc.fallback[e] = 1;  // a wave with more than kPairsPerWave pairs
+    return;
+  }
+  const uint32_t* plist = sc.gplist + (size_t)e * sc.pair_cap;
+  uint32_t* out = sc.pairs + wi * kPairsPerWave + (v - n_i);
+  for (int k = 0; k < n_i; ++k) {
+    const int j = (int)(plist[off + k] >> 16);
+    const int sj = sc.slot_of[base + j];
+    const uint32_t spp =
+        sc.multi_species ? (uint32_t)(st.species[i] * kMaxSpecies + st.species[j]) : 0u;
+    out[k] = (uint32_t)lane | ((uint32_t)(sj & 63) << 6) | (spp << 12);
+  }
+}
+
 template <bool kBig, bool kLocal>
 __global__ __launch_bounds__(1024) void k_cluster_build(DevState st, Scratch sc) {
   extern __shared__ __align__(16) unsigned char smem[];
@@ -2994,16 +2994,12 @@ __device__ __forceinline__ void noise_group(const Derived* __restrict__ d, const
     const long s = (long)(t0 + (uint64_t)j) - (long)step_start;
     if (s >= 0 && s < len) {
       float* o = table + noise_index((size_t)M, (size_t)gi, (int)s, 0);
-#ifdef SWARM_EXP_NT_NOISE
       // streaming stores: the table is read by the next window's run only
+      // (same-box A/B, E = 1: the launch ends ~1.1 us sooner, the next
+      // window's gathers cost ~0.6 us; head line 51.8 -> 52.5 M)
       __builtin_nontemporal_store(g[0], o);
       __builtin_nontemporal_store(g[1], o + cs);
       __builtin_nontemporal_store(g[2], o + 2 * cs);
-#else
-      o[0] = g[0];
-      o[cs] = g[1];
-      o[2 * cs] = g[2];
-#endif
     }
   }
 }
@@ -3472,7 +3468,7 @@ __device__ void run_big_clusters(const Derived* __restrict__ d, const DevState& 
                                  int32_t* lds, const PairTables* pt, int par) {
   const int T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
-  const int nm = sc.big_n[e], np = sc.big_np[e];
+  const int nm = sc.big_n[e], np = min(sc.big_np[e], kBigPairs);
   uint2* lp = reinterpret_cast<uint2*>(lds + ((reinterpret_cast<uintptr_t>(lds) >> 2) & 1));
   unsigned long long* ax = reinterpret_cast<unsigned long long*>(lp + kBigMax);
   unsigned long long* ay = ax + kBigMax;
@@ -3572,7 +3568,8 @@ __device__ void run_big_clusters(const Derived* __restrict__ d, const DevState& 
       w.ang[gi] = p.an;
     }
   }
-  __threadfence();
+  // the rest of k_check (this workgroup) reads the members' state, movers
+  // and displacements: the barrier's workgroup-scope fences suffice
   __syncthreads();
 }
 
@@ -3870,7 +3867,7 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
           } else if (sc.root[base + j] == sc.root[base + m] && sm < 0) {  // same big cluster
             const uint32_t bm = (uint32_t)(-1 - sm), bj = (uint32_t)(-1 - sj);
             const uint32_t* bp = sc.big_pairs + (size_t)e * kBigPairs;
-            const int np = sc.big_np[e];
+            const int np = min(sc.big_np[e], kBigPairs);
             for (int k = 0; k < np; ++k) {
               const uint32_t a = bp[k] & 1023u, b = (bp[k] >> 10) & 1023u;
               listed |= (a == bm && b == bj) || (a == bj && b == bm);

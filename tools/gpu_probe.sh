@@ -3,7 +3,8 @@
 # bench A/B of library variants (tools/gpu_ab.sh), then rocprofv3 kernel
 # traces of one bench line for the working tree and (optional) a baseline
 # copy of the tree.  Every step is time-limited; a crash ends the call.
-#   TESTS="tests/a.py ..." VARIANTS="prod X" LINES=head,c5 PROF_LINE=c5 BASE=_base \
+#   TESTS="tests/a.py ..." VARIANTS="prod X" LINES=head,c5 SCHED_LINE=c5 SCHEDS="default obs_side" \
+#     PROF_LINE=c5 BASE=_base \
 #     bash tools/gpu_probe.sh TAG
 tag=$1
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 2
@@ -17,6 +18,9 @@ if [ -n "$TESTS" ]; then
 fi
 if [ -n "$VARIANTS" ]; then
   bash tools/gpu_ab.sh "$tag" $VARIANTS > "$out/ab.txt" 2>&1 || exit $?
+fi
+if [ -n "$SCHED_LINE" ]; then  # schedule A/B: SCHED_LINE=c5 SCHEDS="default obs_side"
+  timeout -k 10 900 python3 tools/sched_ab.py "$SCHED_LINE" $SCHEDS > "$out/sched.txt" 2>&1 || exit $?
 fi
 prof() {  # prof <dir> <name>
   (cd "$1" && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
