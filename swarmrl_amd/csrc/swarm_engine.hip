@@ -1352,9 +1352,7 @@ void set_lds_attributes() {
                        reinterpret_cast<const void*>(&swarm::k_cluster_build<false, false>),
                        reinterpret_cast<const void*>(&swarm::k_cluster_build<false, true>),
                        reinterpret_cast<const void*>(&swarm::k_cluster_build<true, false>),
-                       reinterpret_cast<const void*>(&swarm::k_cluster_build<true, true>),
-                       reinterpret_cast<const void*>(&swarm::k_cluster_build_packed<false>),
-                       reinterpret_cast<const void*>(&swarm::k_cluster_build_packed<true>),
+                       reinterpret_cast<const void*>(&swarm::k_cluster_build_packed),
                        reinterpret_cast<const void*>(&swarm::k_build_sort<4>),
                        reinterpret_cast<const void*>(&swarm::k_sort_scan),
                        reinterpret_cast<const void*>(&swarm::k_build_sort<16>),
@@ -1483,20 +1481,12 @@ int launch_build(swarm_engine* e, hipStream_t stream) {
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(swarm::k_mwb_pairs, dim3((unsigned)((e->sc.wmax + 3) / 4), e->n_envs),
                        dim3(256), 0, stream, e->st, e->sc);
-  } else if (e->big_build && swarm::build_lds_words_packed(e->n) * 4 <= kMaxLds) {
-    if (local)
-      hipLaunchKernelGGL(swarm::k_cluster_build_packed<true>, dim3(e->n_envs), dim3(1024),
-                         swarm::build_lds_words_packed(e->n) * 4, stream, e->st, e->sc);
-    else
-      hipLaunchKernelGGL(swarm::k_cluster_build_packed<false>, dim3(e->n_envs), dim3(1024),
-                         swarm::build_lds_words_packed(e->n) * 4, stream, e->st, e->sc);
-  } else if (e->big_build) {
-    if (local)
-      hipLaunchKernelGGL((swarm::k_cluster_build<true, true>), dim3(e->n_envs), dim3(1024),
-                         swarm::build_lds_words_big(e->n) * 4, stream, e->st, e->sc);
-    else
-      hipLaunchKernelGGL((swarm::k_cluster_build<true, false>), dim3(e->n_envs), dim3(1024),
-                         swarm::build_lds_words_big(e->n) * 4, stream, e->st, e->sc);
+  } else if (e->big_build && !local && swarm::build_lds_words_packed(e->n) * 4 <= kMaxLds) {
+    hipLaunchKernelGGL(swarm::k_cluster_build_packed, dim3(e->n_envs), dim3(1024),
+                       swarm::build_lds_words_packed(e->n) * 4, stream, e->st, e->sc);
+  } else if (e->big_build) {  // (2-D envs with the local pair search took k_mwb_*)
+    hipLaunchKernelGGL((swarm::k_cluster_build<true, false>), dim3(e->n_envs), dim3(1024),
+                       swarm::build_lds_words_big(e->n) * 4, stream, e->st, e->sc);
   } else if (local) {
     hipLaunchKernelGGL((swarm::k_cluster_build<false, true>), dim3(e->n_envs), dim3(1024),
                        build_lds_bytes(e->n, e->sc.pair_cap), stream, e->st, e->sc);
@@ -2069,10 +2059,7 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
   // build spread over the chip (k_mwb_*) instead of one workgroup, with a
   // fourth per-particle word (the offset of its pairs in the pair list)
   e->sc.bmisc = nullptr;
-  bool mwb = e->big_build && params->n_dims == 2 && e->sc.local_uf;
-#ifdef SWARM_EXP_NO_MWB
-  mwb = false;
-#endif
+  const bool mwb = e->big_build && params->n_dims == 2 && e->sc.local_uf;
   if (e->big_build) rc = rc ? rc : dev_alloc(e, &e->sc.gclus, (mwb ? 4 : 3) * M);
   if (mwb) rc = rc ? rc : dev_alloc(e, &e->sc.bmisc, (size_t)n_envs * swarm::kBmWords);
   rc = rc ? rc : dev_alloc(e, &e->sc.wave_npairs, (size_t)n_envs * (S / 64));

@@ -2224,8 +2224,9 @@ __host__ __device__ inline size_t build_lds_words_packed(int n) {
 //   B[r]: for a root r, size | pairs << 16 (atomic counters, no carry:
 //         size < 2^16); then class rank | w << 24; then the cluster's first
 //         slot (or kBigMark).
-// The pair list stays in global memory (read kU at a time).
-template <bool kLocal>
+// The pair list stays in global memory (read kU at a time).  Used by the
+// large-N builds that union the whole pair list (3-D; 2-D envs with the
+// block-local pair search take the multi-workgroup build, k_mwb_*).
 __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, int e,
                                          unsigned char* smem, int found) {
   const int T = blockDim.x, tid = threadIdx.x, N = st.n;
@@ -2244,65 +2245,33 @@ __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, 
   constexpr int kU = 8;
   SWARM_STAMP(6);
   const int npairs = min(found, sc.pair_cap);
-  // kLocal: start from the pair search's block-local forest, union the
-  // cross-block pairs only (cluster_build_env)
-  const int nx = kLocal ? sc.gnx[e] : 0;
-  const int nun = kLocal ? min(nx, sc.pair_cap) : npairs;
-  const uint32_t* ulist = kLocal ? sc.xpairs + (size_t)e * sc.pair_cap : plist;
   for (int k = tid; k < 68; k += T) classcnt[k] = 0;
   for (int k = tid; k < wmax; k += T) wave_np[k] = 0;
-  // overflow of the pair or cross list -> global path
-  if (tid < 16) misc[tid] = tid == 0 && (found > sc.pair_cap || nx > sc.pair_cap) ? 1 : 0;
-  // kLocal: the members' pair counts of the pair search, kept in registers
-  // from here to the size pass (same particles per thread; N <= kPer T)
-  constexpr int kPer = 20;
-  int32_t np_k[kPer];
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int i = tid + k * T;
-    np_k[k] = 0;
-    if (i < N) {
-      const uint32_t l = kLocal ? (uint32_t)sc.lroot[base + i] : (uint32_t)i;
-      A[i] = (int32_t)(l & 0xffffu);
-      np_k[k] = (int32_t)(l >> 16);
-      B[i] = 0;
-    }
-  }
-  for (int i = tid + kPer * T; i < N; i += T) {  // beyond kPer T: no pair counts kept
-    A[i] = kLocal ? (sc.lroot[base + i] & 0xffff) : i;
+  // overflow of the pair list -> global path
+  if (tid < 16) misc[tid] = tid == 0 && found > sc.pair_cap ? 1 : 0;
+  for (int i = tid; i < N; i += T) {
+    A[i] = i;
     B[i] = 0;
   }
   __syncthreads();
-  for (int k0 = tid; k0 < nun; k0 += kU * T) {
+  for (int k0 = tid; k0 < npairs; k0 += kU * T) {
     uint32_t pr[kU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) pr[u] = k0 + u * T < nun ? ulist[k0 + u * T] : 0u;
+    for (int u = 0; u < kU; ++u) pr[u] = k0 + u * T < npairs ? plist[k0 + u * T] : 0u;
 #pragma unroll
     for (int u = 0; u < kU; ++u)
-      if (k0 + u * T < nun) uf_union(A, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
+      if (k0 + u * T < npairs) uf_union(A, (int)(pr[u] & 0xffffu), (int)(pr[u] >> 16));
   }
   __syncthreads();
   SWARM_STAMP(7);
   for (int i = tid; i < N; i += T) A[i] = uf_find(A, i);
   __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int i = tid + k * T;
-    if (i < N) {
-      const int root = A[i];
-      // size, and (kLocal) the member's pair count of the pair search
-      const int np_i = kLocal && sc.one_pass ? np_k[k] : 0;
-      const uint32_t r = (uint32_t)atomicAdd(&B[root], 1 + (np_i << 16)) & 0xffffu;
-      A[i] = root | (int32_t)(r << 16);
-    }
-  }
-  for (int i = tid + kPer * T; i < N; i += T) {
+  for (int i = tid; i < N; i += T) {  // size, the member's rank
     const int root = A[i];
-    const int np_i = kLocal && sc.one_pass ? (int)((uint32_t)sc.lroot[base + i] >> 16) : 0;
-    const uint32_t r = (uint32_t)atomicAdd(&B[root], 1 + (np_i << 16)) & 0xffffu;
+    const uint32_t r = (uint32_t)atomicAdd(&B[root], 1) & 0xffffu;
     A[i] = root | (int32_t)(r << 16);
   }
-  if (!kLocal && sc.one_pass)
+  if (sc.one_pass)
     for (int k0 = tid; k0 < npairs; k0 += kU * T) {
       uint32_t pr[kU];
 #pragma unroll
@@ -2465,10 +2434,9 @@ __device__ void cluster_build_env_packed(const DevState& st, const Scratch& sc, 
   }
 }
 
-template <bool kLocal>
 __global__ __launch_bounds__(1024) void k_cluster_build_packed(DevState st, Scratch sc) {
   extern __shared__ __align__(16) unsigned char smem[];
-  cluster_build_env_packed<kLocal>(st, sc, blockIdx.x, smem, sc.gnpairs[blockIdx.x]);
+  cluster_build_env_packed(st, sc, blockIdx.x, smem, sc.gnpairs[blockIdx.x]);
 }
 
 // ------------------------------------- multi-workgroup build (large N, 2-D)
@@ -3150,8 +3118,10 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     if (!kTable && pc.noisy) noise.next(k0, k1, (uint32_t)i, step0 + (uint64_t)s, s == 0, gt);
     int64_t ax = 0, ay = 0;
     if (kPass > 0) {
+#ifndef SWARM_EXP_BPERM
       lpos_w[lane] = make_uint2(p.qx, p.qy);
       wave_lds_sync();
+#endif
       for (int q = 0; q < (kPass == 1 ? 1 : (kPass == 2 ? 2 : npass)); ++q) {
         {  // wave-uniform; an empty slot names the lane twice
           const uint32_t e_ = q == 0 ? pr0
@@ -3160,7 +3130,14 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
                                                                          : 0xffffffffu));
           const int a = e_ == 0xffffffffu ? lane : (int)(e_ & 63u);
           const int b = e_ == 0xffffffffu ? lane : (int)((e_ >> 6) & 63u);
+#ifdef SWARM_EXP_BPERM
+          const uint2 pa = make_uint2((uint32_t)__builtin_amdgcn_ds_bpermute(a << 2, (int)p.qx),
+                                      (uint32_t)__builtin_amdgcn_ds_bpermute(a << 2, (int)p.qy));
+          const uint2 pb = make_uint2((uint32_t)__builtin_amdgcn_ds_bpermute(b << 2, (int)p.qx),
+                                      (uint32_t)__builtin_amdgcn_ds_bpermute(b << 2, (int)p.qy));
+#else
           const uint2 pa = lpos_w[a], pb = lpos_w[b];
+#endif
           const float rx = (float)(int32_t)(pb.x - pa.x) * sx0;
           const float ry = (float)(int32_t)(pb.y - pa.y) * sx1;
           int64_t fx, fy;  // on a; b receives exactly the negation

@@ -288,10 +288,6 @@ class SwarmEngine(Engine):
         # vision-cone and policy launches instead of a forked side stream
         # (swarm_engine_defer_build; the engine declines when it cannot)
         self.ride_along_build = True
-        # forked builds: the build on the engine stream right after the
-        # check and the reward / observables / policy on the side stream
-        # (False: the build on the side stream)
-        self.observables_on_side = False
         self._ride_along = False
         self._side_stream = None
         self._prebuild_pending = None
@@ -989,26 +985,10 @@ class SwarmEngine(Engine):
             self._prebuild_pending = (side, fork, int(n_steps))
             return
         side.wait_stream(main)
-        if self.observables_on_side:
-            # the side stream forked after the check carries the force
-            # model's kernels until _run joins it; the build stays in order
-            # behind the check on the engine stream
-            self._native.call("swarm_engine_prebuild", ctypes.c_void_p(main.cuda_stream),
-                              int(n_steps))
-            torch.cuda.set_stream(side)
-            self._prebuild_pending = ("obs_side", side, main)
-            return
         self._native.call("swarm_engine_prebuild", ctypes.c_void_p(side.cuda_stream), int(n_steps))
         self._prebuild_pending = (side, None, 0)
 
     def _run(self, n_steps: int):
-        if self._prebuild_pending is not None and self._prebuild_pending[0] == "obs_side":
-            _, side, main = self._prebuild_pending
-            torch.cuda.set_stream(main)
-            main.wait_stream(side)
-            self._prebuild_pending = None
-            self._native.bind_stream()
-            self._native.call("swarm_engine_prebuild_noise", None, int(n_steps))
         if self._prebuild_pending is not None and self._prebuild_pending[0] == "ride":
             # stages no launch carried along run in swarm_engine_integrate
             self._prebuild_pending = None
@@ -1047,15 +1027,7 @@ class SwarmEngine(Engine):
         self._ride_along = bool(device_path and self.ride_along_build and
                                 getattr(force_model, "absorbs_build", lambda: False)())
         old_slice_idx = self.slice_idx
-        try:
-            self._integrate_slices(n_slices, force_model, device_path, old_slice_idx)
-        finally:
-            if self._prebuild_pending is not None and self._prebuild_pending[0] == "obs_side":
-                # a loop left early: the caller's stream is current again
-                # (the pending side stream is joined by the next _run)
-                torch.cuda.set_stream(self._prebuild_pending[2])
 
-    def _integrate_slices(self, n_slices, force_model, device_path, old_slice_idx):
         while self.step_idx < self.params.steps_per_slice * (old_slice_idx + n_slices):
             if self.step_idx == self.params.steps_per_write_interval * self.write_idx:
                 self._update_traj_holder()

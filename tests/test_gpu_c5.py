@@ -122,26 +122,3 @@ def test_c5_16384_field_chemotaxis_and_rnd_on_device(tmp_path):
     eng.integrate(2, ff)  # the next episode runs on the updated networks
     assert len(agent.trajectory.rewards) == 2
 
-
-def test_c5_observables_on_side_stream_same_rollout(tmp_path):
-    """The forked-build schedule with the build on the engine stream and
-    the reward / observable / policy kernels on the side stream
-    (SwarmEngine.observables_on_side) integrates the same rollout bit for
-    bit as the default (build on the side stream): positions, features and
-    actions of four slices."""
-    runs = []
-    for side in (False, True):
-        eng, ff, agent, *_ = _c5(tmp_path / f"s{int(side)}")
-        eng.observables_on_side = side
-        eng.integrate(4, ff)
-        torch.cuda.synchronize()
-        assert torch.cuda.current_stream() == torch.cuda.default_stream()
-        raw = eng.get_raw_state()
-        tr = agent.trajectory
-        runs.append((raw["q"].copy(), raw["ang"].copy(),
-                     [f.cpu().numpy() for f in tr.features],
-                     [a.cpu().numpy() for a in tr.actions]))
-    (q0, a0, f0, x0), (q1, a1, f1, x1) = runs
-    assert np.array_equal(q0, q1) and np.array_equal(a0, a1)
-    assert all(np.array_equal(u, v) for u, v in zip(f0, f1)) and len(f0) == 4
-    assert all(np.array_equal(u, v) for u, v in zip(x0, x1))

@@ -3,7 +3,7 @@
 tool): runs bench.py's line with the engine attributes of each named
 schedule set on the workload's engine, prints value per schedule.
 usage: python tools/sched_ab.py LINE SCHED [SCHED ...]
-  SCHED: default | obs_side | no_early_fork | serial"""
+  SCHED: default | no_early_fork | serial"""
 import json
 import os
 import subprocess
@@ -11,7 +11,6 @@ import sys
 
 SCHEDS = {
     "default": {},
-    "obs_side": {"observables_on_side": True},
     "no_early_fork": {"early_fork": False},
     "serial": {"overlap_build": False},
 }
