@@ -2750,9 +2750,17 @@ int swarm_rnd_distance(const float* x, int32_t n, int32_t d_in, int32_t width,
 namespace {
 // swarm_rnd_env_reward's workspace: the blocks' fp64 partials, then one
 // ticket per env (zero between calls: the caller zeroes it once).
+// Workgroups per env: the 32-observation groups, at most kRndBlocks (each
+// stages both networks once and loops over its groups).
+#ifndef SWARM_EXP_RND_BLOCKS
+#define SWARM_EXP_RND_BLOCKS 1 << 30
+#endif
+constexpr int kRndBlocks = SWARM_EXP_RND_BLOCKS;
+int rnd_blocks(int per_env) {
+  return std::min((per_env + swarm::kRndObsPerBlock - 1) / swarm::kRndObsPerBlock, kRndBlocks);
+}
 size_t rnd_partials_bytes(int n_envs, int per_env) {
-  const int kb = (per_env + swarm::kRndObsPerBlock - 1) / swarm::kRndObsPerBlock;
-  return ((size_t)n_envs * kb * sizeof(double) + 255) & ~(size_t)255;
+  return ((size_t)n_envs * rnd_blocks(per_env) * sizeof(double) + 255) & ~(size_t)255;
 }
 }  // namespace
 
@@ -2768,7 +2776,7 @@ int swarm_rnd_env_reward(const float* x, int32_t n_envs, int32_t per_env, int32_
   if (order < 1) return fail(SWARM_EINVAL, "distance order must be >= 1");
   if (n_envs < 0 || per_env < 0) return fail(SWARM_EINVAL, "n_envs, per_env >= 0");
   if (n_envs == 0 || per_env == 0) return SWARM_OK;
-  const int kb = (per_env + swarm::kRndObsPerBlock - 1) / swarm::kRndObsPerBlock;
+  const int kb = rnd_blocks(per_env);
   const size_t pb = rnd_partials_bytes(n_envs, per_env);
   if (workspace_bytes < (int64_t)(pb + (size_t)n_envs * sizeof(uint32_t)))
     return fail(SWARM_ECAPACITY, "workspace below swarm_rnd_env_workspace_bytes");

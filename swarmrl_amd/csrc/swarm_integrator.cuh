@@ -3014,7 +3014,7 @@ template <bool kMulti, bool kTable, bool kWalls, bool kTwoPass = false>
 __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const DevState& st,
                                          const Scratch& sc, int n_envs, int n_steps,
                                          uint64_t step0, const float* __restrict__ table,
-                                         int gw, int lane, uint2* lpos_w,
+                                         int gw, int lane,
                                          unsigned long long* lacc_x, unsigned long long* lacc_y,
                                          const PairTables& pt, int par) {
   const int e = gw / sc.wmax;
@@ -3118,10 +3118,6 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     if (!kTable && pc.noisy) noise.next(k0, k1, (uint32_t)i, step0 + (uint64_t)s, s == 0, gt);
     int64_t ax = 0, ay = 0;
     if (kPass > 0) {
-#ifndef SWARM_EXP_BPERM
-      lpos_w[lane] = make_uint2(p.qx, p.qy);
-      wave_lds_sync();
-#endif
       for (int q = 0; q < (kPass == 1 ? 1 : (kPass == 2 ? 2 : npass)); ++q) {
         {  // wave-uniform; an empty slot names the lane twice
           const uint32_t e_ = q == 0 ? pr0
@@ -3130,14 +3126,13 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
                                                                          : 0xffffffffu));
           const int a = e_ == 0xffffffffu ? lane : (int)(e_ & 63u);
           const int b = e_ == 0xffffffffu ? lane : (int)((e_ >> 6) & 63u);
-#ifdef SWARM_EXP_BPERM
+          // both ends' positions straight from their lanes' registers
+          // (ds_bpermute: no LDS row written and waited for first; same-box
+          // A/B: E = 1 run 50.9 -> 50.3 us, E = 64 247.7 -> 244.5 us)
           const uint2 pa = make_uint2((uint32_t)__builtin_amdgcn_ds_bpermute(a << 2, (int)p.qx),
                                       (uint32_t)__builtin_amdgcn_ds_bpermute(a << 2, (int)p.qy));
           const uint2 pb = make_uint2((uint32_t)__builtin_amdgcn_ds_bpermute(b << 2, (int)p.qx),
                                       (uint32_t)__builtin_amdgcn_ds_bpermute(b << 2, (int)p.qy));
-#else
-          const uint2 pa = lpos_w[a], pb = lpos_w[b];
-#endif
           const float rx = (float)(int32_t)(pb.x - pa.x) * sx0;
           const float ry = (float)(int32_t)(pb.y - pa.y) * sx1;
           int64_t fx, fy;  // on a; b receives exactly the negation
@@ -3290,16 +3285,16 @@ template <bool kMulti, bool kWalls, bool kTwoPass = false>
 __device__ __forceinline__ void run_wave_dispatch(const Derived* __restrict__ d, const DevState& st,
                                                   const Scratch& sc, int n_envs, int n_steps,
                                                   uint64_t step0, const float* __restrict__ table,
-                                                  int gw, int lane, uint2* lpos_w,
+                                                  int gw, int lane,
                                                   unsigned long long* lacc_x,
                                                   unsigned long long* lacc_y,
                                                   const PairTables& pt, int par) {
   if (table)
     run_wave<kMulti, true, kWalls, kTwoPass>(d, st, sc, n_envs, n_steps, step0, table, gw, lane,
-                                             lpos_w, lacc_x, lacc_y, pt, par);
+                                             lacc_x, lacc_y, pt, par);
   else
     run_wave<kMulti, false, kWalls, kTwoPass>(d, st, sc, n_envs, n_steps, step0, nullptr, gw, lane,
-                                              lpos_w, lacc_x, lacc_y, pt, par);
+                                              lacc_x, lacc_y, pt, par);
 }
 
 // Launch-duration stamps for measurement (bench.py, swarm_engine_profile
@@ -3343,7 +3338,6 @@ __global__ __launch_bounds__(256, kRunMinBlocks) void k_cluster_run(const Derive
                                                      int xcd_bpe,
                                                      unsigned long long* __restrict__ tstamp) {
   __shared__ PairTables pt;
-  __shared__ uint2 lpos[4][64];                  // positions of the block's 4 waves
   __shared__ unsigned long long lacc[4][2][64];  // int64 force sums (x, y)
   stamp_start(tstamp);
   stage_pair_tables(d, &pt);
@@ -3364,7 +3358,7 @@ __global__ __launch_bounds__(256, kRunMinBlocks) void k_cluster_run(const Derive
   // normally guarantees it) -> the normals are drawn in the kernel
   run_wave_dispatch<kMulti, kWalls>(d, st, sc, n_envs, n_steps, step0,
                                     table_ok ? tables + par * noise_table_words(st.m) : nullptr,
-                                    gw, lane, lpos[wv], lacc[wv][0], lacc[wv][1], pt, par);
+                                    gw, lane, lacc[wv][0], lacc[wv][1], pt, par);
   stamp_end(tstamp);
 }
 
@@ -3385,7 +3379,6 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
                                                            int n_cand_blocks, int lxb, int lyb,
                                                            unsigned long long* __restrict__ tstamp) {
   __shared__ PairTables pt;
-  __shared__ uint2 lpos[4][64];
   __shared__ unsigned long long lacc[4][2][64];
   stamp_start(tstamp);
   stage_pair_tables(d, &pt);
@@ -3427,7 +3420,7 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
   // 65-128 pairs (a cluster denser than two pairs per particle) runs its own
   // unrolled two-pass sub-step instead of the general pass loop
   run_wave_dispatch<kMulti, kWalls, true>(d, st, sc, n_envs, n_steps, step0, table, gw, lane,
-                                          lpos[wv], lacc[wv][0], lacc[wv][1], pt, par);
+                                          lacc[wv][0], lacc[wv][1], pt, par);
   stamp_end(tstamp);
 }
 

@@ -252,30 +252,39 @@ __global__ __launch_bounds__(256) void k_rnd_env(const float* __restrict__ x, in
   __shared__ int last;
   const int e = blockIdx.y, kb = gridDim.x, tid = threadIdx.x;
   const int sub = tid & (kRndLanes - 1), grp = tid / kRndLanes;
-  const int k = blockIdx.x * kRndObsPerBlock + grp;
-  const bool valid = k < per_env;
-  const size_t a = (size_t)e * per_env + (valid ? k : 0);
-  float xi[D];
-#pragma unroll
-  for (int i = 0; i < D; ++i) xi[i] = i < d_in ? x[a * d_in + i] : 0.0f;
   rnd_stage_rows<D>(&tnet, tp.w, d_in);
   rnd_stage_rows<D>(&pnet, pp.w, d_in);
   __syncthreads();
-  float t[kRndOut], p[kRndOut];
-  rnd_forward_lanes<D>(tnet, xi, sub, rows[grp], t);
-  rnd_forward_lanes<D>(pnet, xi, sub, rows[grp], p);
-  float acc = 0.0f;
+  // the block's groups of 32 observations (blockIdx.x, + gridDim.x, ...):
+  // the networks are staged once per block, not once per 32 observations;
+  // each group's metric sum in a fixed order per thread
+  double own = 0.0;
+  for (int k0 = blockIdx.x * kRndObsPerBlock; k0 < per_env; k0 += kb * kRndObsPerBlock) {
+    const int k = k0 + grp;
+    const bool valid = k < per_env;
+    const size_t a = (size_t)e * per_env + (valid ? k : 0);
+    float xi[D];
 #pragma unroll
-  for (int r = 0; r < kRndOut; ++r) {
-    const float dlt = fabsf(t[r] - p[r]);
-    acc += order == 2 ? dlt * dlt : powf(dlt, (float)order);
+    for (int i = 0; i < D; ++i) xi[i] = i < d_in ? x[a * d_in + i] : 0.0f;
+    float t[kRndOut], p[kRndOut];
+    rnd_forward_lanes<D>(tnet, xi, sub, rows[grp], t);
+    rnd_forward_lanes<D>(pnet, xi, sub, rows[grp], p);
+    float acc = 0.0f;
+#pragma unroll
+    for (int r = 0; r < kRndOut; ++r) {
+      const float dlt = fabsf(t[r] - p[r]);
+      acc += order == 2 ? dlt * dlt : powf(dlt, (float)order);
+    }
+#pragma unroll
+    for (int o = 1; o < kRndLanes; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    const float m = order == 2 ? sqrtf(acc) : powf(acc, 1.0f / (float)order);
+    if (valid && sub == 0) {
+      metric[a] = m;
+      own += (double)m;
+    }
   }
-#pragma unroll
-  for (int o = 1; o < kRndLanes; o <<= 1) acc += __shfl_xor(acc, o, 64);
-  const float m = order == 2 ? sqrtf(acc) : powf(acc, 1.0f / (float)order);
-  if (valid && sub == 0) metric[a] = m;
-  // the block's sum of its (up to 32) metrics: fixed tree over the groups
-  red[tid] = valid && sub == 0 ? (double)m : 0.0;
+  // the block's sum: fixed tree over its threads
+  red[tid] = own;
   __syncthreads();
   for (int w = 128; w >= 1; w >>= 1) {
     if (tid < w) red[tid] += red[tid + w];

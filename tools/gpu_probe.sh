@@ -22,6 +22,9 @@ fi
 if [ -n "$SCHED_LINE" ]; then  # schedule A/B: SCHED_LINE=c5 SCHEDS="default obs_side"
   timeout -k 10 900 python3 tools/sched_ab.py "$SCHED_LINE" $SCHEDS > "$out/sched.txt" 2>&1 || exit $?
 fi
+if [ -n "$EXTRA" ]; then  # one more command (e.g. a rocprofv3 run of a tool), 300 s
+  timeout -k 10 300 bash -c "$EXTRA" > "$out/extra.txt" 2>&1 || exit $?
+fi
 prof() {  # prof <dir> <name>
   (cd "$1" && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
      -d "$out/prof_$2" -o run -- python3 bench.py --only "$PROF_LINE" --no-cpu-baseline \
