@@ -521,6 +521,33 @@ int swarm_ppo_epoch_grad(const float *x, int32_t T, int32_t S, int32_t d_in,
                          float gamma, float lambda, float clip_eps, float entropy_coef,
                          void *workspace, int64_t workspace_bytes, float *grad, void *stream);
 
+/* The optimizer of the PPO update (torch.optim.Adam as TorchModel builds it
+ * for the optax optimizer of swarmrl/networks/flax_network.py:42-79): the six tensors
+ * w1 | b1 | wa | ba | wc | bc of swarm_ppo_epoch_grad, updated in place with
+ * their first / second moments and per-tensor step counts (device fp32, as
+ * torch's capturable Adam keeps them).  weight_decay 0, no amsgrad. */
+typedef struct {
+  float lr, beta1, beta2, eps;
+  float *param[6];
+  float *exp_avg[6];
+  float *exp_avg_sq[6];
+  float *step[6];
+} swarm_adam_t;
+
+/* One PPO epoch with the optimizer step fused into its last launch: the
+ * gradient of swarm_ppo_epoch_grad (written to grad, the parameters read
+ * from adam->param) followed by the Adam step of torch's fused Adam
+ * (step += 1; m = b1 m + (1 - b1) g; v = b2 v + (1 - b2) g^2;
+ * p -= lr / (1 - b1^step) * m / (sqrt(v) / sqrt(1 - b2^step) + eps), fp32).
+ * Replaces swarm_ppo_epoch_grad + optimizer.step() (three launches fewer per
+ * epoch).  The workspace must be zero-filled before its first use (the
+ * kernel leaves its ticket at zero after each call). */
+int swarm_ppo_epoch_step(const float *x, int32_t T, int32_t S, int32_t d_in,
+                         const int64_t *actions, const float *old_logp, const float *rewards,
+                         int32_t hidden, int32_t k, float gamma, float lambda, float clip_eps,
+                         float entropy_coef, const swarm_adam_t *adam, void *workspace,
+                         int64_t workspace_bytes, float *grad, void *stream);
+
 /* Random Network Distillation distance (the intrinsic reward of
  * swarmrl/intrinsic_reward/random_network_distillation.py:126-143 with the
  * networks of rnd_configs.py:17-38): for every observation a < n of x

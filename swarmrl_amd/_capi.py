@@ -98,6 +98,21 @@ class SwarmVisionParams(ctypes.Structure):
     ]
 
 
+class SwarmAdam(ctypes.Structure):
+    """swarm_adam_t: torch Adam's hyper-parameters and the device tensors
+    of the six PPO layers (w1 | b1 | wa | ba | wc | bc)."""
+    _fields_ = [
+        ("lr", ctypes.c_float),
+        ("beta1", ctypes.c_float),
+        ("beta2", ctypes.c_float),
+        ("eps", ctypes.c_float),
+        ("param", ctypes.c_void_p * 6),
+        ("exp_avg", ctypes.c_void_p * 6),
+        ("exp_avg_sq", ctypes.c_void_p * 6),
+        ("step", ctypes.c_void_p * 6),
+    ]
+
+
 # name -> (restype, argtypes)
 _P = ctypes.c_void_p
 _SIGNATURES = {
@@ -161,6 +176,12 @@ _SIGNATURES = {
         [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, _P, _P, _P, ctypes.c_int32,
          _P, _P, ctypes.c_int32, _P, _P, ctypes.c_float, ctypes.c_float, ctypes.c_float,
          ctypes.c_float, _P, ctypes.c_int64, _P, _P],
+    ),
+    "swarm_ppo_epoch_step": (
+        ctypes.c_int,
+        [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, _P, ctypes.c_int32,
+         ctypes.c_int32, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+         ctypes.POINTER(SwarmAdam), _P, ctypes.c_int64, _P, _P],
     ),
     "swarm_ppo_profile": (ctypes.c_int, [ctypes.c_int32, _P, _P]),
     "swarm_engine_step_count": (ctypes.c_int64, [_P]),

@@ -47,12 +47,15 @@ class ActorCriticAgent(Agent):
 
     def absorbs_build(self) -> bool:
         """True when this agent's device calc_action launches the engine-bound
-        kernels a deferred cluster build rides along in (the vision cone, then
-        the one-kernel policy): SwarmEngine then defers the build instead of
-        forking it onto a second stream."""
+        kernels a deferred cluster build rides along in (the vision cone, or
+        with a concentration field the field reward, then the one-kernel
+        policy): SwarmEngine then defers the build instead of forking it onto
+        a second stream.  Engines that cannot carry it decline the deferral
+        (swarm_engine_defer_build) and fork as before."""
+        from swarmrl_amd.observables.concentration_field import ConcentrationField
         from swarmrl_amd.observables.subdivided_vision_cones import SubdividedVisionCones
 
-        return (isinstance(self.observable, SubdividedVisionCones)
+        return (isinstance(self.observable, (SubdividedVisionCones, ConcentrationField))
                 and getattr(self.network, "accepts_engine", False))
 
     def supports_device(self) -> bool:

@@ -1080,11 +1080,14 @@ __global__ __launch_bounds__(256) void k_field(DevState st, FieldArgs f) {
 // so the observable launch only runs the cone (beside stage 2).
 // l1_pairs (n_fb > 0): the next window's pair search rides here too,
 // n_fb blocks per env after the grid workgroups (l1_pairs_role).
+// with_grid = 0 (a field observable, l1_pairs): no vision grid, the reward
+// carries the sort and the pair search only (its grid workgroups return).
 template <int CH>
 __global__ __launch_bounds__(1024) void k_field_vgrid_sort(FieldArgs f, int n_fblocks, DevState st,
                                                            VisionArgs va, Scratch sc, int lxb,
                                                            int lyb, const Derived* __restrict__ d,
-                                                           int n_fb, const uint64_t* __restrict__ ctl) {
+                                                           int n_fb, const uint64_t* __restrict__ ctl,
+                                                           int with_grid) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int b = fused_block(2 * va.n_envs);
   const int E = va.n_envs, npb = n_fb * E;
@@ -1092,6 +1095,7 @@ __global__ __launch_bounds__(1024) void k_field_vgrid_sort(FieldArgs f, int n_fb
     l1_pairs_role(d, st, sc, lxb, lyb, b - 2 * E, n_fb, ctl, smem);
     return;
   }
+  if (!with_grid && b >= E && b < 2 * E) return;
   const int role = b < E ? swarm::kRoleSort : b < 2 * E ? swarm::kRoleVgrid : swarm::kRoleField;
   swarm::role_begin(sc, role);
   if (b < E)
@@ -3087,9 +3091,16 @@ namespace {
 // along in the reward launch).
 int launch_field(swarm_engine* e, const FieldArgs& f) {
   const int total = f.n_agents * e->n_envs;
-  if (e->spec_ok && e->ride_stage == 1) {
-    const VisionArgs& va = e->spec_va;
-    const size_t glds = vision_grid_lds_bytes(va.lx, va.ly, e->n, va.staged != 0);
+  // the reward launch of a slice with a deferred build carries stage 1 (and
+  // the l1_pairs pair search), and for a persistent vision cone the next
+  // observable's grid; without a vision cone only with l1_pairs (the
+  // cluster build then rides in the policy launch: k_policy_cbuild)
+  const bool grid_too = e->spec_ok;
+  if (e->ride_stage == 1 && (grid_too || e->sc.l1_pairs)) {
+    VisionArgs none{};
+    none.n_envs = e->n_envs;
+    const VisionArgs& va = grid_too ? e->spec_va : none;
+    const size_t glds = grid_too ? vision_grid_lds_bytes(va.lx, va.ly, e->n, va.staged != 0) : 0;
     const size_t slds = sort_lds_bytes(e);
     const int nfb = (total + 1023) / 1024;
     const int npf = l1_blocks_per_env(e);  // l1_pairs: the pair search rides here too
@@ -3097,13 +3108,15 @@ int launch_field(swarm_engine* e, const FieldArgs& f) {
     const size_t lds = l1_launch_lds(e, std::max(glds, slds));
     if (e->n > 4096)
       hipLaunchKernelGGL((k_field_vgrid_sort<16>), grid, dim3(1024), lds, e->stream, f, nfb,
-                         e->st, va, e->sc, e->lxb, e->lyb, e->d_derived, npf, e->d_step);
+                         e->st, va, e->sc, e->lxb, e->lyb, e->d_derived, npf, e->d_step,
+                         grid_too ? 1 : 0);
     else
       hipLaunchKernelGGL((k_field_vgrid_sort<4>), grid, dim3(1024), lds, e->stream, f, nfb,
-                         e->st, va, e->sc, e->lxb, e->lyb, e->d_derived, npf, e->d_step);
+                         e->st, va, e->sc, e->lxb, e->lyb, e->d_derived, npf, e->d_step,
+                         grid_too ? 1 : 0);
     HIP_TRY(hipGetLastError());
     e->ride_stage = e->sc.l1_pairs ? 3 : 2;
-    e->vgrid_ready = true;
+    e->vgrid_ready = grid_too;
     return SWARM_OK;
   }
   hipLaunchKernelGGL(k_field, dim3((total + 255) / 256), dim3(256), 0, e->stream, e->st, f);
@@ -3401,7 +3414,7 @@ int swarm_engine_defer_build(swarm_engine_t* e, int32_t* deferred) {
 
 namespace {
 struct PpoWorkspace {
-  size_t values, adv, dv, spart, table, partial, total;
+  size_t values, adv, dv, spart, table, partial, ticket, total;
 };
 PpoWorkspace ppo_workspace(long n, long S, int d, int hidden, int k) {
   PpoWorkspace w;
@@ -3413,7 +3426,8 @@ PpoWorkspace ppo_workspace(long n, long S, int d, int hidden, int k) {
   w.table = up(w.spart + (size_t)((S + 255) / 256) * 2 * sizeof(double));
   // unit rows: at most 256 units x PpoTable<32, 16>::kStride floats
   w.partial = up(w.table + (size_t)swarm::kPpoMaxHidden * swarm::PpoTable<32, 16>::kStride * 4);
-  w.total = up(w.partial + (size_t)swarm::kPpoBlocks * swarm::ppo_grad_size(d, hidden, k) * 4);
+  w.ticket = up(w.partial + (size_t)swarm::kPpoBlocks * swarm::ppo_grad_size(d, hidden, k) * 4);
+  w.total = up(w.ticket + 4);
   return w;
 }
 }  // namespace
@@ -3461,12 +3475,13 @@ int ppo_resident_blocks(const void* fn, int threads, size_t lds) {
 }
 }  // namespace
 
-int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
-                         const int64_t* actions, const float* old_logp, const float* rewards,
-                         const float* w1, const float* b1, int32_t hidden, const float* wa,
-                         const float* ba, int32_t k, const float* wc, const float* bc,
-                         float gamma, float lambda, float clip_eps, float entropy_coef,
-                         void* workspace, int64_t workspace_bytes, float* grad, void* stream) {
+namespace {
+int ppo_epoch(const float* x, int32_t T, int32_t S, int32_t d_in, const int64_t* actions,
+              const float* old_logp, const float* rewards, const float* w1, const float* b1,
+              int32_t hidden, const float* wa, const float* ba, int32_t k, const float* wc,
+              const float* bc, float gamma, float lambda, float clip_eps, float entropy_coef,
+              void* workspace, int64_t workspace_bytes, float* grad, void* stream,
+              const swarm_adam_t* adam) {
   if (!x || !actions || !old_logp || !rewards || !w1 || !b1 || !wa || !ba || !wc || !bc ||
       !workspace || !grad)
     return fail(SWARM_EINVAL, "null argument");
@@ -3573,10 +3588,58 @@ int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
 #undef SWARM_PPO_GRADS
 #undef SWARM_PPO
   const int size = swarm::ppo_grad_size(d_in, hidden, k);
-  hipLaunchKernelGGL(swarm::k_ppo_reduce, dim3((unsigned)((size + 63) / 64)), dim3(1024), 0, s,
-                     partial, blocks, size, grad);
+  if (adam) {  // the optimizer step fused into the reduce
+    swarm::AdamArgs a;
+    a.lr = adam->lr;
+    a.beta1 = adam->beta1;
+    a.beta2 = adam->beta2;
+    a.eps = adam->eps;
+    const int sizes[6] = {hidden * d_in, hidden, k * hidden, k, hidden, 1};
+    a.seg[0] = 0;
+    for (int t = 0; t < 6; ++t) {
+      if (!adam->param[t] || !adam->exp_avg[t] || !adam->exp_avg_sq[t] || !adam->step[t])
+        return fail(SWARM_EINVAL, "null Adam tensor");
+      a.param[t] = adam->param[t];
+      a.m[t] = adam->exp_avg[t];
+      a.v[t] = adam->exp_avg_sq[t];
+      a.step[t] = adam->step[t];
+      a.seg[t + 1] = a.seg[t] + sizes[t];
+    }
+    uint32_t* ticket = reinterpret_cast<uint32_t*>(base + ws.ticket);
+    hipLaunchKernelGGL(swarm::k_ppo_reduce_adam, dim3((unsigned)((size + 63) / 64)), dim3(1024), 0,
+                       s, partial, blocks, size, grad, a, ticket);
+  } else {
+    hipLaunchKernelGGL(swarm::k_ppo_reduce, dim3((unsigned)((size + 63) / 64)), dim3(1024), 0, s,
+                       partial, blocks, size, grad);
+  }
   HIP_TRY(hipGetLastError());
   return SWARM_OK;
+}
+}  // namespace
+
+int swarm_ppo_epoch_grad(const float* x, int32_t T, int32_t S, int32_t d_in,
+                         const int64_t* actions, const float* old_logp, const float* rewards,
+                         const float* w1, const float* b1, int32_t hidden, const float* wa,
+                         const float* ba, int32_t k, const float* wc, const float* bc,
+                         float gamma, float lambda, float clip_eps, float entropy_coef,
+                         void* workspace, int64_t workspace_bytes, float* grad, void* stream) {
+  return ppo_epoch(x, T, S, d_in, actions, old_logp, rewards, w1, b1, hidden, wa, ba, k, wc, bc,
+                   gamma, lambda, clip_eps, entropy_coef, workspace, workspace_bytes, grad, stream,
+                   nullptr);
+}
+
+int swarm_ppo_epoch_step(const float* x, int32_t T, int32_t S, int32_t d_in,
+                         const int64_t* actions, const float* old_logp, const float* rewards,
+                         int32_t hidden, int32_t k, float gamma, float lambda, float clip_eps,
+                         float entropy_coef, const swarm_adam_t* adam, void* workspace,
+                         int64_t workspace_bytes, float* grad, void* stream) {
+  if (!adam) return fail(SWARM_EINVAL, "null argument");
+  if (!(adam->beta1 >= 0.0f && adam->beta1 < 1.0f && adam->beta2 >= 0.0f && adam->beta2 < 1.0f))
+    return fail(SWARM_EINVAL, "Adam betas must be in [0, 1)");
+  return ppo_epoch(x, T, S, d_in, actions, old_logp, rewards, adam->param[0], adam->param[1],
+                   hidden, adam->param[2], adam->param[3], k, adam->param[4], adam->param[5],
+                   gamma, lambda, clip_eps, entropy_coef, workspace, workspace_bytes, grad, stream,
+                   adam);
 }
 
 int swarm_neighbor_reduce(const double* pos, const double* dir, const double* vel,

@@ -680,4 +680,67 @@ __global__ __launch_bounds__(1024) void k_ppo_reduce(const float* __restrict__ p
   }
 }
 
+// The optimizer step fused into the reduce (swarm_ppo_epoch_step): torch
+// Adam (torch.optim.Adam, weight_decay 0, no amsgrad / maximize) on the six
+// tensors w1 | b1 | wa | ba | wc | bc, their moments and per-tensor step
+// counts in place -- the sequence of torch's fused Adam: step + 1,
+// m = b1 m + (1 - b1) g, v = b2 v + (1 - b2) g^2, p -= lr / (1 - b1^step) * m
+// / (sqrt(v) / sqrt(1 - b2^step) + eps), in fp32.
+struct AdamArgs {
+  float lr, beta1, beta2, eps;
+  float* param[6];
+  float* m[6];
+  float* v[6];
+  float* step[6];
+  int seg[7];  // parameter index ranges of the six tensors
+};
+
+__global__ __launch_bounds__(1024) void k_ppo_reduce_adam(const float* __restrict__ partial,
+                                                          int n_blocks, int size,
+                                                          float* __restrict__ grad, AdamArgs a,
+                                                          uint32_t* __restrict__ ticket) {
+  __shared__ double red[16][64];
+  __shared__ int last;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int p = blockIdx.x * 64 + lane;
+  double acc = 0.0;
+  if (p < size) {
+#pragma unroll 8
+    for (int b = w; b < n_blocks; b += 16) acc += (double)partial[(size_t)b * size + p];
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && p < size) {
+    double t = 0.0;
+    for (int i = 0; i < 16; ++i) t += red[i][lane];
+    const float g = (float)t;
+    grad[p] = g;
+    int sg = 0;
+    while (sg < 5 && p >= a.seg[sg + 1]) ++sg;
+    const int off = p - a.seg[sg];
+    // the step count before this step: every workgroup reads it before its
+    // ticket, the last one writes step + 1
+    const float step = *a.step[sg] + 1.0f;
+    const float bc1 = 1.0f - powf(a.beta1, step);
+    const float bc2 = 1.0f - powf(a.beta2, step);
+    const float bc2s = sqrtf(bc2);
+    float m = a.m[sg][off], v = a.v[sg][off];
+    m = a.beta1 * m + (1.0f - a.beta1) * g;
+    v = a.beta2 * v + (1.0f - a.beta2) * g * g;
+    const float step_size = a.lr / bc1;
+    const float denom = sqrtf(v) / bc2s + a.eps;
+    a.param[sg][off] = a.param[sg][off] - step_size * m / denom;
+    a.m[sg][off] = m;
+    a.v[sg][off] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t tk = atomicAdd(ticket, 1u);
+    last = tk == gridDim.x - 1;
+    if (last) *ticket = 0u;  // the next step's count (graph replays)
+  }
+  __syncthreads();
+  if (last && threadIdx.x < 6) *a.step[threadIdx.x] = *a.step[threadIdx.x] + 1.0f;
+}
+
 }  // namespace swarm

@@ -165,23 +165,60 @@ struct RndRows {
   float b3[kRndWidth];
 };
 
+// Both networks' weights into LDS (torch layouts, w1 zero-padded to D
+// inputs).  Every load of the block's share of BOTH networks is issued
+// before any LDS store: one memory latency (a load -> store -> load chain
+// per loop trip took ~14 us per workgroup, SQ_WAIT_ANY 62 % of its wave
+// cycles).  blockDim = 256.
 template <int D>
-__device__ __forceinline__ void rnd_stage_rows(RndRows<D>* net, const float* const* w, int d_in) {
-  constexpr int W = kRndWidth;
-  for (int k = threadIdx.x; k < W * D; k += blockDim.x) {
-    const int j = k / D, i = k - j * D;
-    net->w1[j][i] = i < d_in ? w[0][j * d_in + i] : 0.0f;
+__device__ __forceinline__ void rnd_stage_rows(RndRows<D>* tnet, RndRows<D>* pnet,
+                                               const float* const* tw, const float* const* pw,
+                                               int d_in) {
+  constexpr int W = kRndWidth, T = 256;
+  constexpr int N1 = (W * D + T - 1) / T, N2 = W * W / T;
+  const int tid = threadIdx.x;
+  RndRows<D>* nets[2] = {tnet, pnet};
+  const float* const* ws[2] = {tw, pw};
+  float v1[2][N1], v2[2][N2], v3[2][N2], bb[2][3];
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const float* const* w = ws[n];
+#pragma unroll
+    for (int u = 0; u < N1; ++u) {
+      const int k = tid + u * T, j = k / D, i = k - j * D;
+      v1[n][u] = k < W * D && i < d_in ? w[0][j * d_in + i] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < N2; ++u) {
+      v2[n][u] = w[2][tid + u * T];
+      v3[n][u] = w[4][tid + u * T];
+    }
+    if (tid < W) {
+      bb[n][0] = w[1][tid];
+      bb[n][1] = w[3][tid];
+      bb[n][2] = w[5][tid];
+    }
   }
-  float* w2 = reinterpret_cast<float*>(net->w2);
-  float* w3 = reinterpret_cast<float*>(net->w3);
-  for (int k = threadIdx.x; k < W * W; k += blockDim.x) {
-    w2[k] = w[2][k];
-    w3[k] = w[4][k];
-  }
-  for (int k = threadIdx.x; k < W; k += blockDim.x) {
-    net->b1[k] = w[1][k];
-    net->b2[k] = w[3][k];
-    net->b3[k] = w[5][k];
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    RndRows<D>* net = nets[n];
+#pragma unroll
+    for (int u = 0; u < N1; ++u) {
+      const int k = tid + u * T;
+      if (k < W * D) net->w1[k / D][k % D] = v1[n][u];
+    }
+    float* w2 = reinterpret_cast<float*>(net->w2);
+    float* w3 = reinterpret_cast<float*>(net->w3);
+#pragma unroll
+    for (int u = 0; u < N2; ++u) {
+      w2[tid + u * T] = v2[n][u];
+      w3[tid + u * T] = v3[n][u];
+    }
+    if (tid < W) {
+      net->b1[tid] = bb[n][0];
+      net->b2[tid] = bb[n][1];
+      net->b3[tid] = bb[n][2];
+    }
   }
 }
 
@@ -252,8 +289,7 @@ __global__ __launch_bounds__(256) void k_rnd_env(const float* __restrict__ x, in
   __shared__ int last;
   const int e = blockIdx.y, kb = gridDim.x, tid = threadIdx.x;
   const int sub = tid & (kRndLanes - 1), grp = tid / kRndLanes;
-  rnd_stage_rows<D>(&tnet, tp.w, d_in);
-  rnd_stage_rows<D>(&pnet, pp.w, d_in);
+  rnd_stage_rows<D>(&tnet, &pnet, tp.w, pp.w, d_in);
   __syncthreads();
   // the block's groups of 32 observations (blockIdx.x, + gridDim.x, ...):
   // the networks are staged once per block, not once per 32 observations;

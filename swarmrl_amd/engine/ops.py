@@ -404,9 +404,42 @@ def policy_mlp_sample(obs: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2:
 _PPO_WS: Dict[Tuple[int, int], torch.Tensor] = {}
 
 
+def adam_args(optimizer, layers):
+    """swarm_adam_t for a torch Adam whose only parameters are the six PPO
+    layers, or None when the fused step does not apply (another optimizer,
+    weight decay, amsgrad / maximize, several groups, state not on the
+    device yet).  Holds device pointers: valid while the tensors live."""
+    if type(optimizer) is not torch.optim.Adam or len(optimizer.param_groups) != 1:
+        return None
+    g = optimizer.param_groups[0]
+    if (g.get("weight_decay", 0) != 0 or g.get("amsgrad") or g.get("maximize")
+            or not g.get("capturable") or g.get("differentiable")
+            or isinstance(g["lr"], torch.Tensor)):
+        return None
+    if len(g["params"]) != 6 or {id(p) for p in g["params"]} != {id(t) for t in layers}:
+        return None
+    a = _capi.SwarmAdam()
+    a.lr, a.beta1, a.beta2, a.eps = float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]), \
+        float(g["eps"])
+    for k, t in enumerate(layers):
+        st = optimizer.state.get(t, {})
+        need = ("exp_avg", "exp_avg_sq", "step")
+        if not all(isinstance(st.get(n), torch.Tensor) and st[n].is_cuda for n in need):
+            return None
+        if (st["step"].dtype != torch.float32 or st["exp_avg"].dtype != torch.float32
+                or not t.is_contiguous() or t.dtype != torch.float32):
+            return None
+        a.param[k] = t.data_ptr()
+        a.exp_avg[k] = st["exp_avg"].data_ptr()
+        a.exp_avg_sq[k] = st["exp_avg_sq"].data_ptr()
+        a.step[k] = st["step"].data_ptr()
+    return a
+
+
 def ppo_epoch_grad(features: torch.Tensor, actions: torch.Tensor, old_logp: torch.Tensor,
                    rewards: torch.Tensor, layers, gamma: float, lambda_: float,
-                   clip_eps: float, entropy_coef: float, out: torch.Tensor = None) -> torch.Tensor:
+                   clip_eps: float, entropy_coef: float, out: torch.Tensor = None,
+                   adam=None) -> torch.Tensor:
     """
     The gradient of one PPO epoch (swarm_ppo_epoch_grad): features [T, S, d]
     fp32, actions [T, S] int64, old_logp / rewards [T, S] fp32 (all device),
@@ -414,6 +447,8 @@ def ppo_epoch_grad(features: torch.Tensor, actions: torch.Tensor, old_logp: torc
     layouts.  Returns the flat gradient w1 | b1 | wa | ba | wc | bc (fp32),
     written into `out` when given.  Inputs already fp32/int64 and contiguous
     are used in place (no copies: the launches can be graph-captured).
+    adam: a swarm_adam_t (adam_args) -- the optimizer's step then runs in the
+    epoch's last launch (swarm_ppo_epoch_step) and updates the layers.
     """
     T, S = int(actions.shape[0]), int(actions.shape[1])
     x = features.reshape(T * S, -1).to(torch.float32).contiguous()
@@ -427,9 +462,9 @@ def ppo_epoch_grad(features: torch.Tensor, actions: torch.Tensor, old_logp: torc
         raise ValueError("bad PPO sizes")
     key = (dev.index or 0, nbytes)
     ws = _PPO_WS.get(key)
-    if ws is None:
+    if ws is None:  # zeroed once: the fused Adam's ticket is left at zero after use
         _PPO_WS.clear()
-        ws = _PPO_WS[key] = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        ws = _PPO_WS[key] = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
     size = hidden * d_in + hidden + k * hidden + k + hidden + 1
     grad = out if out is not None else torch.empty(size, dtype=torch.float32, device=dev)
     if grad.numel() != size or grad.dtype != torch.float32 or not grad.is_contiguous():
@@ -438,6 +473,13 @@ def ppo_epoch_grad(features: torch.Tensor, actions: torch.Tensor, old_logp: torc
     olp = old_logp.to(torch.float32).contiguous()
     rew = rewards.to(torch.float32).contiguous()
     stream = torch.cuda.current_stream(dev).cuda_stream
+    if adam is not None:  # the optimizer step fused into the epoch (swarm_ppo_epoch_step)
+        _capi.check(lib.swarm_ppo_epoch_step(
+            x.data_ptr(), T, S, d_in, acts.data_ptr(), olp.data_ptr(), rew.data_ptr(), hidden, k,
+            ctypes.c_float(gamma), ctypes.c_float(lambda_), ctypes.c_float(clip_eps),
+            ctypes.c_float(entropy_coef), ctypes.byref(adam), ws.data_ptr(), nbytes,
+            grad.data_ptr(), ctypes.c_void_p(stream)))
+        return grad
     _capi.check(lib.swarm_ppo_epoch_grad(
         x.data_ptr(), T, S, d_in, acts.data_ptr(), olp.data_ptr(), rew.data_ptr(),
         w1.data_ptr(), b1.data_ptr(), hidden, wa.data_ptr(), ba.data_ptr(), k, wc.data_ptr(),

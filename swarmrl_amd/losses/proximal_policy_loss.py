@@ -113,7 +113,13 @@ class ProximalPolicyLoss(Loss):
         states = [opt.state.get(p, {}) for p in layers]
         if not all(states) or any(p.grad is None for p in layers):
             return False  # optimizer state not initialised yet: first episode is eager
-        sig = (id(network), id(opt), tuple(features.shape), tuple(actions.shape),
+        # torch Adam on exactly these layers: its step fused into each epoch's
+        # last launch (swarm_ppo_epoch_step; SWARMRL_AMD_FUSED_ADAM=0: the
+        # optimizer's own step after the gradient)
+        adam = (ops.adam_args(opt, layers)
+                if os.environ.get("SWARMRL_AMD_FUSED_ADAM", "1") != "0" else None)
+        sig = (adam is not None, id(network), id(opt), tuple(features.shape),
+               tuple(actions.shape),
                tuple(float(g["lr"]) for g in opt.param_groups),
                tuple(t.data_ptr() for st in states for t in st.values()
                      if isinstance(t, torch.Tensor)),
@@ -141,8 +147,11 @@ class ProximalPolicyLoss(Loss):
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
                 for _ in range(self.n_epochs):
-                    ops.ppo_epoch_grad(*args, out=grad)
-                    opt.step()
+                    if adam is not None:
+                        ops.ppo_epoch_grad(*args, out=grad, adam=adam)
+                    else:
+                        ops.ppo_epoch_grad(*args, out=grad)
+                        opt.step()
             cache = self._ppo_graph = {"sig": sig, "graph": graph, "inputs": (x, act, olp, rew),
                                        "grad": grad}
         x, act, olp, rew = cache["inputs"]

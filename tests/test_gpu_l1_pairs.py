@@ -126,3 +126,70 @@ def test_l1_pairs_and_fused_policy_match_oracle(force):
         assert waited <= 1 and filtered >= step - 1, (moved, list(stats))
     else:
         assert max(moved) > 1.5 and waited > 0, (moved, list(stats))
+
+
+def test_field_observable_rides_the_build_and_matches_oracle():
+    """The same schedule with a concentration-field observable (BASELINE C3's
+    find-centre workload, bench.build_c3_workload): the deferred build rides
+    in the reward launch (sort + pair search, no vision grid) and the policy
+    launch (cluster build), no side stream.  Features (the field observable,
+    its own history), rewards, the final state and the window statistics
+    against the oracle's replay of the recorded actions."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    N, T = 4096, 6
+    ns = argparse.Namespace(colloids=N, envs_per_gpu=1, write_interval=1.0)
+    eng, ff, agent = bench.build_c3_workload(ns, 42, dev)
+    assert ff.absorbs_build()
+    pos0 = np.stack(eng._pos[0])
+    dir0 = np.stack(eng._dir[0])
+    eng.integrate(1, ff)
+    _, episode_graph, warm = bench.capture_episode(eng, ff, agent, T)
+    slices = [_host(warm)]
+    episode_graph.replay()
+    torch.cuda.synchronize()
+    slices.append(_host(agent.trajectory))
+    eng.drain_trajectory(block=True)
+    got = eng.get_raw_state()
+    del episode_graph
+    stats = (ctypes.c_uint64 * 4)()
+    eng._native.call("swarm_engine_build_stats", stats, 0)
+    filtered, waited, reruns, windows = list(stats)
+
+    L = float(eng._box[0])
+    box = np.array([L, L, L])
+    src = np.array([L / 2, L / 2, 0.0])
+    p = oracle.make_params(eng._box, eng._time_step, eng._kT(),
+                           eng.params.WCA_epsilon.m_as("sim_energy"), 42, [eng._species_keys[0]])
+    agents = np.arange(N)
+    ftab = np.array([0.0, 10.0, 0.0, 0.0], np.float32)
+    ttab = np.array([10.0, 0.0, -10.0, 0.0], np.float32)
+    sp = np.zeros(N, np.uint8)
+    st = oracle.state_from_positions(pos0, dir0, eng._box)
+    hist_task = oracle.history_from_state(st, agents)
+    hist_obs = oracle.history_from_state(st, agents)
+    st, _ = oracle.sd_run(p, st, sp, 1000)
+    prev = {"f": np.zeros(N, np.float32), "t": np.zeros(N, np.float32), "ang": st["ang"].copy()}
+    f32 = np.float32
+    step = 0
+    for block in slices:
+        for s in range(len(block["actions"])):
+            dc, dp = oracle.field_distance(p, st, agents, src, box, hist_obs, update=True)
+            obs = (f32(10000.0) * ((f32(1.0) - dc) - (f32(1.0) - dp))).astype(np.float32)
+            assert np.array_equal(block["features"][s].reshape(-1), obs), (step, "field")
+            idx = block["actions"][s].reshape(-1)
+            f, t = ftab[idx], ttab[idx]
+            st, _, _ = oracle.bd_run(p, st, sp, f, t, 100, step0=100 * step, prev=prev)
+            prev = {"f": f, "t": t, "ang": st["ang"].copy()}
+            rew = _reward(p, st, agents, src, box, hist_task)
+            assert np.array_equal(block["rewards"][s].reshape(-1), rew), (step, "reward")
+            step += 1
+    assert step == 3 + T
+    for k in ("q", "img", "ang"):
+        assert np.array_equal(got[k], st[k]), k
+    # every window's pair search ran in the reward launch (lists or the
+    # fresh sort), none re-ran
+    assert windows == step and filtered + waited == step and reruns == 0, list(stats)

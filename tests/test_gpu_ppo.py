@@ -149,8 +149,10 @@ def test_compute_loss_fused_equals_torch_path(monkeypatch):
 
 def test_graph_epochs_equal_eager(monkeypatch):
     """Three episodes of compute_loss with the default (fused, capturable)
-    Adam: the captured-graph epochs (episode 1 eager, 2 captured + replayed,
-    3 replayed) end on bit-identical parameters to the eager loop."""
+    Adam, the optimizer's own step (SWARMRL_AMD_FUSED_ADAM=0): the
+    captured-graph epochs (episode 1 eager, 2 captured + replayed, 3
+    replayed) end on bit-identical parameters to the eager loop."""
+    monkeypatch.setenv("SWARMRL_AMD_FUSED_ADAM", "0")
     from swarmrl_amd.losses.proximal_policy_loss import ProximalPolicyLoss
     from swarmrl_amd.networks.torch_network import ActorCriticMLP, TorchModel
 
@@ -180,3 +182,50 @@ def test_graph_epochs_equal_eager(monkeypatch):
         finals.append([p.detach().clone() for p in model.model.ppo_layers()])
     for a, b in zip(*finals):
         assert torch.equal(a, b)
+
+
+def test_fused_adam_step_matches_torch_adam(monkeypatch):
+    """The Adam step fused into each epoch's last launch (swarm_ppo_epoch_step,
+    the default for torch Adam on the six layers) against torch's fused Adam
+    after the same gradients: parameters, moments and step counts of three
+    episodes x 5 epochs (episode 1 eager with torch's step, 2-3 captured),
+    fp32 rounding apart (another operation order); and run to run the fused
+    path is bit-identical."""
+    from swarmrl_amd.losses.proximal_policy_loss import ProximalPolicyLoss
+    from swarmrl_amd.networks.torch_network import ActorCriticMLP, TorchModel
+
+    dev = torch.device("cuda", 0)
+    T, E, A, d = 20, 1, 300, 1
+
+    def episode(seed):
+        g = torch.Generator().manual_seed(seed)
+
+        class Episode:
+            features = [f.to(dev) for f in torch.randn(T, E, A, d, generator=g)]
+            actions = [a.to(dev) for a in torch.randint(0, 4, (T, E, A), generator=g)]
+            rewards = [r.to(dev) for r in torch.randn(T, E, A, generator=g)]
+            log_probs = [lp.to(dev) for lp in -1.386 + 0.3 * torch.randn(T, E, A, generator=g)]
+        return Episode()
+
+    runs = {}
+    for tag, fused in (("fused", "1"), ("fused2", "1"), ("torch", "0")):
+        monkeypatch.setenv("SWARMRL_AMD_FUSED_ADAM", fused)
+        torch.manual_seed(0)
+        model = TorchModel(ActorCriticMLP(d, 4, 128), input_shape=(d,), device=dev)
+        loss = ProximalPolicyLoss(n_epochs=5)
+        for ep in range(3):
+            loss.compute_loss(model, episode(200 + ep))
+        assert loss._ppo_graph["sig"][0] == (fused == "1")
+        layers = model.model.ppo_layers()
+        st = [model.optimizer.state[p] for p in layers]
+        runs[tag] = ([p.detach().clone() for p in layers],
+                     [s["exp_avg"].clone() for s in st], [s["exp_avg_sq"].clone() for s in st],
+                     [float(s["step"]) for s in st])
+    for a, b in zip(runs["fused"][0] + runs["fused"][1] + runs["fused"][2],
+                    runs["fused2"][0] + runs["fused2"][1] + runs["fused2"][2]):
+        assert torch.equal(a, b)
+    assert runs["fused"][3] == runs["torch"][3] == [15.0] * 6
+    for a, b in zip(runs["fused"][0], runs["torch"][0]):
+        torch.testing.assert_close(a, b, rtol=2e-5, atol=2e-6)
+    for a, b in zip(runs["fused"][1] + runs["fused"][2], runs["torch"][1] + runs["torch"][2]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-7)
