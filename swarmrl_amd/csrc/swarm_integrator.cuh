@@ -1329,25 +1329,25 @@ __global__ __launch_bounds__(1024) void k_sort_scan(Scratch sc, int lx, int ly) 
   int32_t* g = sc.gcnt + ((size_t)e << (lx + ly));
   // the counts into LDS, kB loads in flight per thread (one memory latency
   // per kB cells, not per cell), then the next build's counters zeroed
+  // (the counters are zeroed again by k_sort_scatter, the slots reset here
+  // or -- multi-workgroup builds -- by k_mwb_size: this one workgroup only
+  // moves the counts)
   constexpr int kB = 16;
   for (int c0 = tid; c0 < ncell; c0 += kB * T) {
     int32_t v[kB];
 #pragma unroll
     for (int u = 0; u < kB; ++u) v[u] = c0 + u * T < ncell ? g[c0 + u * T] : 0;
 #pragma unroll
-    for (int u = 0; u < kB; ++u) {
-      if (c0 + u * T < ncell) {
-        cnt[c0 + u * T] = v[u];
-        g[c0 + u * T] = 0;
-      }
-    }
+    for (int u = 0; u < kB; ++u)
+      if (c0 + u * T < ncell) cnt[c0 + u * T] = v[u];
   }
   if (tid == 0) {
     sc.gnpairs[e] = 0;
     sc.gnx[e] = 0;
     sc.fallback[e] = 0;  // the neighbour-list build sets it on overflow
   }
-  for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
+  if (!sc.bmisc)
+    for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
   __syncthreads();
   block_exclusive_scan(cnt, ncell, wave_sums);
   __syncthreads();
@@ -1360,7 +1360,9 @@ __global__ __launch_bounds__(256) void k_sort_scatter(DevState st, Scratch sc, i
   if (i >= N) return;
   const size_t M = (size_t)st.m, base = (size_t)e * N, gi = base + i;
   const int ncell = 1 << (lx + ly);
-  const size_t pos = base + sc.bcstart[(size_t)e * (ncell + 1) + sc.gcell[gi]] + sc.grank[gi];
+  const int c = sc.gcell[gi];
+  const size_t pos = base + sc.bcstart[(size_t)e * (ncell + 1) + c] + sc.grank[gi];
+  sc.gcnt[((size_t)e << (lx + ly)) + c] = 0;  // the next build's counter (k_sort_scan read it)
   sc.bsq[pos] = st.q[gi];
   sc.bsq[M + pos] = st.q[M + gi];
   sc.bsid[pos] = i | (sc.multi_species ? (int32_t)st.species[i] << 24 : 0);
@@ -2537,6 +2539,9 @@ __global__ __launch_bounds__(256) void k_mwb_size(DevState st, Scratch sc) {
   const int np_i = sc.one_pass ? (int)((uint32_t)sc.lroot[base + i] >> 16) : 0;
   const uint32_t rank = (uint32_t)atomicAdd(&B[r], 1 + (np_i << 16)) & 0xffffu;
   sc.gclus[2 * M + base + i] = r | (int32_t)(rank << 16);
+  // the env's slots, idle until k_mwb_slots places the colloids (spread over
+  // this launch instead of k_sort_scan's one workgroup)
+  for (int k = i; k < sc.S; k += N) sc.perm[(size_t)e * sc.S + k] = -1;
 }
 
 // k_mwb_class: every root's packing class and rank in it, counted per
