@@ -2922,9 +2922,11 @@ int vision_cone_impl(swarm_engine_t* e, const swarm_vision_params_t* vp, const i
     HIP_TRY(hipGetLastError());
   }
   if (pol && ride_ok && e->ride_stage == 3) {  // cluster build | cone + policy (l1_pairs)
-    // 16 lanes per agent (32 measured: the cone's bins summed ~2 us sooner,
-    // the MLP tail ~2 us longer, no change)
-    constexpr int GC = 16;
+    // 32 lanes per agent: with the actor rows staged in LDS the cone's bins
+    // are summed ~1.5 us sooner and the MLP tail no longer outweighs it
+    // (same box: head 53.1 -> 53.3 M, C2 14.5 -> 14.8 M; with the rows read
+    // from L2 the tail took ~2 us longer and 16 lanes won)
+    constexpr int GC = 32;
     const int ncb = (int)((total * GC + 1023) / 1024);
     const size_t rows = ((size_t)pol->hidden * swarm::MlpRow<4, 4>::kStride + 4) * sizeof(float);
     const size_t lds = std::max(build_lds_bytes(e->n, e->sc.pair_cap),

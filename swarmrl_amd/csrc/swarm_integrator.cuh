@@ -1756,10 +1756,12 @@ __device__ __forceinline__ void pair_filter_body(const Derived* __restrict__ d, 
   const int nc = valid ? sc.ncand[gi] : 0;
   const uint32_t qx = st.q[gi], qy = st.q[M + gi];
   // the first eight list entries load with the count (one memory latency,
-  // not two; entries past the count are never used)
-  int c0[8];
+  // not two; entries past the count are never used); sixteen in flight
+  // measured no different
+  constexpr int kFly = 8;
+  int c0[kFly];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) c0[u] = sc.cand[(size_t)u * M + gi];
+  for (int u = 0; u < kFly; ++u) c0[u] = sc.cand[(size_t)u * M + gi];
   const bool multi = sc.multi_species != 0;
   const int si = multi && valid ? (int)st.species[i] : 0;
   const float sx0 = d->sx[0], sx1 = d->sx[1];
@@ -1773,20 +1775,20 @@ __device__ __forceinline__ void pair_filter_body(const Derived* __restrict__ d, 
     const float ry = (float)(int32_t)(yj - qy) * sx1;
     return rx * rx + ry * ry < nb2_row[multi ? ((uint32_t)c >> 24) : 0];
   };
-  for (int k0 = 0; k0 < nc; k0 += 8) {  // eight candidates in flight per round
-    int cj[8];
-    uint32_t xj[8], yj[8];
+  for (int k0 = 0; k0 < nc; k0 += kFly) {  // eight candidates in flight per round
+    int cj[kFly];
+    uint32_t xj[kFly], yj[kFly];
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+    for (int u = 0; u < kFly; ++u)
       cj[u] = k0 + u < nc ? (k0 == 0 ? c0[u] : sc.cand[(size_t)(k0 + u) * M + gi]) : -1;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < kFly; ++u) {
       const size_t gj = base + (cj[u] < 0 ? 0 : (cj[u] & 0xffffff));
       xj[u] = st.q[gj];
       yj[u] = st.q[M + gj];
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < kFly; ++u) {
       if (cj[u] >= 0 && test(cj[u], xj[u], yj[u])) {
         const uint32_t kv = (uint32_t)(cj[u] & 0xffffff);
 #pragma unroll
@@ -3147,12 +3149,23 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
           } else {
             pair_fix_sel(cut2_0, sig6_0, eps24, rx, ry, fx, fy);
           }
+#ifdef SWARM_EXP_NEG_FIRST
+          // b: the exact negation, formed before the first atomic so that no
+          // hazard wait sits between the negation and its ds_add_u64
+          const unsigned long long nfx = 0ull - (unsigned long long)fx;
+          const unsigned long long nfy = 0ull - (unsigned long long)fy;
+          atomicAdd(&lacc_x[a], (unsigned long long)fx);
+          atomicAdd(&lacc_y[a], (unsigned long long)fy);
+          atomicAdd(&lacc_x[b], nfx);
+          atomicAdd(&lacc_y[b], nfy);
+#else
           atomicAdd(&lacc_x[a], (unsigned long long)fx);
           atomicAdd(&lacc_y[a], (unsigned long long)fy);
           // b: the exact negation (written as a subtract; the compiler still
           // emits ds_add_u64 of the negated value)
           atomicSub(&lacc_x[b], (unsigned long long)fx);
           atomicSub(&lacc_y[b], (unsigned long long)fy);
+#endif
         }
       }
     }

@@ -154,14 +154,20 @@ constexpr int kRndLanes = 8;                      // lanes per observation
 constexpr int kRndObsPerBlock = 256 / kRndLanes;  // 32
 constexpr int kRndOut = kRndWidth / kRndLanes;    // outputs per lane and layer
 
-// One network's weights in LDS, torch layouts (rows = outputs).
+// One network's weights in LDS, torch layouts (rows = outputs), the square
+// layers' rows padded to kRndStride floats: lane `sub` of a group takes the
+// outputs j = sub + 8 r, so the eight lanes of a group read rows 8 r .. 8 r
+// + 7 together, which start 36 floats (= 36 banks mod 64) apart and cover
+// disjoint bank quads -- no LDS bank conflict (unpadded rows 4 apart put all
+// eight in one quad: an 8-way conflict on every float4 read).
+constexpr int kRndStride = kRndWidth + 4;  // floats per padded row (16-B aligned)
 template <int D>
 struct RndRows {
   float w1[kRndWidth][D];
   float b1[kRndWidth];
-  float4 w2[kRndWidth][kRndWidth / 4];
+  float4 w2[kRndWidth][kRndStride / 4];
   float b2[kRndWidth];
-  float4 w3[kRndWidth][kRndWidth / 4];
+  float4 w3[kRndWidth][kRndStride / 4];
   float b3[kRndWidth];
 };
 
@@ -211,8 +217,9 @@ __device__ __forceinline__ void rnd_stage_rows(RndRows<D>* tnet, RndRows<D>* pne
     float* w3 = reinterpret_cast<float*>(net->w3);
 #pragma unroll
     for (int u = 0; u < N2; ++u) {
-      w2[tid + u * T] = v2[n][u];
-      w3[tid + u * T] = v3[n][u];
+      const int t = tid + u * T, j = t / W, c = t - j * W;
+      w2[j * kRndStride + c] = v2[n][u];
+      w3[j * kRndStride + c] = v3[n][u];
     }
     if (tid < W) {
       net->b1[tid] = bb[n][0];
@@ -222,18 +229,18 @@ __device__ __forceinline__ void rnd_stage_rows(RndRows<D>* tnet, RndRows<D>* pne
   }
 }
 
-// A square layer: the lane's outputs j = 4 sub + r, a[r] = b[j] + sum_k
+// A square layer: the lane's outputs j = sub + 8 r, a[r] = b[j] + sum_k
 // w[j][k] h[k] over the group's activations h (LDS row, float4 reads).
-__device__ __forceinline__ void rnd_square_lanes(const float4 (*w)[kRndWidth / 4], const float* b,
+__device__ __forceinline__ void rnd_square_lanes(const float4 (*w)[kRndStride / 4], const float* b,
                                                  const float4* h, int sub, float* a) {
 #pragma unroll
-  for (int r = 0; r < kRndOut; ++r) a[r] = b[kRndOut * sub + r];
+  for (int r = 0; r < kRndOut; ++r) a[r] = b[sub + kRndLanes * r];
 #pragma unroll
   for (int q = 0; q < kRndWidth / 4; ++q) {
     const float4 hv = h[q];
 #pragma unroll
     for (int r = 0; r < kRndOut; ++r) {
-      const float4 wv = w[kRndOut * sub + r][q];
+      const float4 wv = w[sub + kRndLanes * r][q];
       a[r] = __builtin_fmaf(wv.x, hv.x, a[r]);
       a[r] = __builtin_fmaf(wv.y, hv.y, a[r]);
       a[r] = __builtin_fmaf(wv.z, hv.z, a[r]);
@@ -243,14 +250,14 @@ __device__ __forceinline__ void rnd_square_lanes(const float4 (*w)[kRndWidth / 4
 }
 
 // The lane's four outputs of one network for the group's observation x;
-// row: the group's LDS activation row (kRndWidth floats, float4-aligned).
+// row: the group's LDS activation row (kRndStride floats, float4-aligned).
 template <int D>
 __device__ __forceinline__ void rnd_forward_lanes(const RndRows<D>& net, const float* x, int sub,
-                                                  float4* row, float* out) {
+                                                  float* row, float* out) {
   float a[kRndOut];
 #pragma unroll
   for (int r = 0; r < kRndOut; ++r) {
-    const int j = kRndOut * sub + r;
+    const int j = sub + kRndLanes * r;
     float v = net.b1[j];
 #pragma unroll
     for (int i = 0; i < D; ++i) v = __builtin_fmaf(net.w1[j][i], x[i], v);
@@ -259,17 +266,19 @@ __device__ __forceinline__ void rnd_forward_lanes(const RndRows<D>& net, const f
   auto publish = [&](const float* v) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();  // the group's previous reads of the row are done
-    row[sub] = make_float4(v[0], v[1], v[2], v[3]);
+#pragma unroll
+    for (int r = 0; r < kRndOut; ++r) row[sub + kRndLanes * r] = v[r];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
+  const float4* h = reinterpret_cast<const float4*>(row);
   publish(a);
-  rnd_square_lanes(net.w2, net.b2, row, sub, a);
+  rnd_square_lanes(net.w2, net.b2, h, sub, a);
 #pragma unroll
   for (int r = 0; r < kRndOut; ++r) a[r] = fmaxf(a[r], 0.0f);
   publish(a);
-  rnd_square_lanes(net.w3, net.b3, row, sub, out);
+  rnd_square_lanes(net.w3, net.b3, h, sub, out);
 }
 
 template <int D>
@@ -284,7 +293,7 @@ __global__ __launch_bounds__(256) void k_rnd_env(const float* __restrict__ x, in
                                                  uint32_t* __restrict__ tickets) {
   static_assert(kRndOut == 4, "float4 activation rows");
   __shared__ RndRows<D> tnet, pnet;
-  __shared__ float4 rows[kRndObsPerBlock][kRndWidth / 4];
+  __shared__ __align__(16) float rows[kRndObsPerBlock][kRndStride];
   __shared__ double red[256];
   __shared__ int last;
   const int e = blockIdx.y, kb = gridDim.x, tid = threadIdx.x;
