@@ -3149,23 +3149,12 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
           } else {
             pair_fix_sel(cut2_0, sig6_0, eps24, rx, ry, fx, fy);
           }
-#ifdef SWARM_EXP_NEG_FIRST
-          // b: the exact negation, formed before the first atomic so that no
-          // hazard wait sits between the negation and its ds_add_u64
-          const unsigned long long nfx = 0ull - (unsigned long long)fx;
-          const unsigned long long nfy = 0ull - (unsigned long long)fy;
-          atomicAdd(&lacc_x[a], (unsigned long long)fx);
-          atomicAdd(&lacc_y[a], (unsigned long long)fy);
-          atomicAdd(&lacc_x[b], nfx);
-          atomicAdd(&lacc_y[b], nfy);
-#else
           atomicAdd(&lacc_x[a], (unsigned long long)fx);
           atomicAdd(&lacc_y[a], (unsigned long long)fy);
           // b: the exact negation (written as a subtract; the compiler still
           // emits ds_add_u64 of the negated value)
           atomicSub(&lacc_x[b], (unsigned long long)fx);
           atomicSub(&lacc_y[b], (unsigned long long)fy);
-#endif
         }
       }
     }

@@ -11,6 +11,7 @@ pids=()
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off \
+    -fno-slp-vectorize \
     $flags swarmrl_amd/csrc/swarm_engine.hip -o tools/_variants/lib_${name}.so &
   pids+=($!)
 done
