@@ -2109,13 +2109,9 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     // particles, 64 CUs produce the next window's table in its shadow (C5:
     // no k_noise launch between the policy and the run)
     e->wide_run = e->noise_table;
-#ifdef SWARM_EXP_NB32
-    // above one 4096-colloid env, 32 noise workgroups (a few us of work each
-    // beside a ~45 us run) leave room for one run wave per CU
-    e->noise_blocks = e->wide_run && M <= 16384 ? (M <= 4096 ? 64 : 32) : 0;
-#else
+    // (32 noise workgroups above 4096 colloids, so that C4's 8 x 1024 gets one
+    // run wave per CU, measured slower: C4 81.1 -> 72.9 M, same box)
     e->noise_blocks = e->wide_run && M <= 16384 ? 64 : 0;
-#endif
     const char* ow = std::getenv("SWARMRL_AMD_WIDE_RUN");
     if (ow && ow[0] == '0') e->wide_run = false, e->noise_blocks = 0;
     // run waves per CU: a wave alone on its CU does not share the CU's
