@@ -1609,16 +1609,17 @@ int launch_run(swarm_engine* e, int n_steps, unsigned long long* tstamp = nullpt
 }
 
 // The 2-D cluster window's exact check (and re-run on failure).
-// The window's cell-sorted snapshot is in global memory unless the build
-// was k_build_env (LDS-resident): k_check then takes each mover's
-// candidates from its cells (-1: every colloid).
+// k_check takes each mover's candidates from the cells of the window's
+// cell-sorted snapshot in global memory.
 size_t sort_lds_bytes(const swarm_engine* e) {
   const size_t ncb = (size_t)1 << (e->lxb + e->lyb + e->lzb);
   return (16 + ((ncb + 4) & ~(size_t)3) + 3 * (size_t)e->sc.sort_stage_k) * 4;
 }
 
-int check_cell_lx(const swarm_engine* e) { return e->env_build ? -1 : e->lxb; }
-int check_cell_ly(const swarm_engine* e) { return e->env_build ? -1 : e->lyb; }
+// every 2-D build leaves its cell-sorted snapshot in global memory (k_build_env
+// too), so the check searches the movers' candidate cells
+int check_cell_lx(const swarm_engine* e) { return e->lxb; }
+int check_cell_ly(const swarm_engine* e) { return e->lyb; }
 
 int launch_check(swarm_engine* e, int n_steps) {
   hipLaunchKernelGGL(swarm::k_check, dim3(e->n_envs), dim3(1024),

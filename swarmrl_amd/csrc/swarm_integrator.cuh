@@ -2814,6 +2814,19 @@ __global__ __launch_bounds__(1024) void k_build_env(const Derived* __restrict__ 
   // idle wave slots of the next run (the packing writes the used ones)
   for (int k = tid; k < sc.S; k += T) sc.perm[(size_t)e * sc.S + k] = -1;
   __syncthreads();  // cnt[c] = end of cell c = start of cell c + 1
+  // the window-start cell-sorted snapshot in global memory too, for
+  // k_check's cell-based exact test (without it the check tested every mover
+  // against every colloid: 23.6 us per launch at E = 64)
+  for (int t = tid; t < N; t += T) {
+    const uint2 v = lq[t];
+    sc.bsq[base + t] = v.x;
+    sc.bsq[M + base + t] = v.y;
+    sc.bsid[base + t] = lid[t];
+  }
+  {
+    int32_t* cs = sc.bcstart + (size_t)e * (ncell + 1);
+    for (int c = tid; c <= ncell; c += T) cs[c] = c == 0 ? 0 : cnt[c - 1];
+  }
   SWARM_STAMP(1);
   // pair search: a stencil row (cells x-1..x+1) is one contiguous sorted
   // range, plus a wrap range at the grid edge
@@ -3490,6 +3503,8 @@ __device__ void run_big_clusters(const Derived* __restrict__ d, const DevState& 
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
+      // (wave-uniform: a wave whose slots all lie past the list skips them)
+      if (u * T + (tid & ~63) >= np) break;
       const int a = (int)(pr[u] & 1023u), b = (int)((pr[u] >> 10) & 1023u);
       const int sp = (int)(pr[u] >> 20);
       const uint2 pa = lp[a], pb = lp[b];
@@ -3752,9 +3767,32 @@ __global__ __launch_bounds__(256) void k_nl_step2(const Derived* __restrict__ d,
 }
 
 // ---------------------------------------------------------------- check
-// cell_lx, cell_ly: the window's build grid when its counting sort left the
-// cell-sorted snapshot in global memory (sc.bsq / bsid / bcstart: the
-// three-launch build, not k_build_env); -1: scan every colloid per mover.
+// Whether the first n entries of a pair list (16-byte aligned, readable in
+// whole 16-entry rounds) hold k1 or k2 under mask: 16 entries per round of
+// loads.
+__device__ __forceinline__ bool list_holds(const uint4* __restrict__ l, int n, uint32_t mask,
+                                           uint32_t k1, uint32_t k2) {
+  bool hit = false;
+  for (int k = 0; k < n && !hit; k += 16) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = l[(k >> 2) + u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t x = w[c] & mask;
+        hit |= k + 4 * u + c < n && (x == k1 || x == k2);
+      }
+    }
+  }
+  return hit;
+}
+
+// cell_lx, cell_ly: the window's build grid, whose counting sort left the
+// cell-sorted snapshot in global memory (sc.bsq / bsid / bcstart: every 2-D
+// build, k_build_env included); -1: scan every colloid per mover.
 __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, DevState st,
                                                 Scratch sc, int n_steps,
                                                 uint64_t* __restrict__ step_ctr,
@@ -3769,6 +3807,10 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
   const int e = blockIdx.x, T = blockDim.x, tid = threadIdx.x, N = st.n;
   const size_t M = (size_t)st.m, base = (size_t)e * N;
   role_begin(sc, kRoleCheck);
+#ifdef SWARM_CHECK_TIMING
+  uint64_t ct0 = __builtin_amdgcn_s_memrealtime(), ct1 = 0, ct2 = 0;
+  int ckc = -1;
+#endif
   // every load the test starts from is issued here together -- the window
   // counters, the build's flags, the mover count and list (written by the
   // run kernel) and the pair tables: one memory latency, not a chain
@@ -3789,6 +3831,9 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
   const bool flagged_build = fb == 1;
   if (!flagged_build && bign > 0)
     run_big_clusters(d, st, sc, e, n_steps, step0, cnt, &pt, par);
+#ifdef SWARM_CHECK_TIMING
+  ct1 = __builtin_amdgcn_s_memrealtime();
+#endif
   int nm = 0;  // movers of the window (listed in LDS below)
   bool kc_dmax = false;  // misc[7] holds the movers' largest displacement
   if (!flagged_build) {
@@ -3821,42 +3866,90 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
       const float rc0 = sqrtf(pt.cut2[0]);
       const float sx0 = d->sx[0], sx1 = d->sx[1];
       const bool per = d->periodic != 0;
-      auto test_pair = [&](int m, int j) {
+      // Each global load of the test is a round trip to another XCD's
+      // writes (~1 us): the mover's own state and the first 16 entries of its
+      // wave's pair list are loaded once per mover, the candidate's four
+      // words together, so a mover costs four rounds (its state; cell
+      // ranges and list; candidate ids; candidate state), not seven.
+      struct MoverCtx {
+        uint32_t qx, qy;
+        int32_t ix, iy;
+        float disp;
+        int sm, root, np;
+        uint4 l[4];  // the first 16 entries of the mover's wave pair list
+      };
+      auto mover_ctx = [&](int m) {
+        MoverCtx c;
+        c.qx = sc.bq[base + m];
+        c.qy = sc.bq[M + base + m];
+        c.ix = per ? 0 : sc.bimg[base + m];
+        c.iy = per ? 0 : sc.bimg[M + base + m];
+        c.disp = sc.disp[base + m];
+        c.sm = nlist ? 0 : sc.slot_of[base + m];
+        c.root = nlist ? 0 : sc.root[base + m];
+        c.np = 0;
+        if (!nlist && c.sm >= 0) {
+          const size_t wl = (size_t)e * sc.wmax + (c.sm >> 6);
+          const uint4* pw = reinterpret_cast<const uint4*>(sc.pairs + wl * kPairsPerWave);
+          c.np = sc.wave_npairs[wl];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) c.l[u] = pw[u];
+        }
+        return c;
+      };
+      auto test_pair = [&](int m, int j, const MoverCtx& c) {
+        const uint32_t jqx = sc.bq[base + j], jqy = sc.bq[M + base + j];
+        const int32_t jix = per ? 0 : sc.bimg[base + j], jiy = per ? 0 : sc.bimg[M + base + j];
+        const float jd = sc.disp[base + j];
+        const int sj = nlist ? 0 : sc.slot_of[base + j];
+        const int rj = nlist ? 0 : sc.root[base + j];
         // (non-periodic box: the unwrapped separation; the folded one would
         // only make the test stricter)
-        const float rx = per ? (float)(int32_t)(sc.bq[base + j] - sc.bq[base + m]) * sx0
-                             : pair_disp(sc.bq[base + j], sc.bimg[base + j], sc.bq[base + m],
-                                         sc.bimg[base + m], sx0, false);
-        const float ry = per ? (float)(int32_t)(sc.bq[M + base + j] - sc.bq[M + base + m]) * sx1
-                             : pair_disp(sc.bq[M + base + j], sc.bimg[M + base + j],
-                                         sc.bq[M + base + m], sc.bimg[M + base + m], sx1, false);
+        const float rx = per ? (float)(int32_t)(jqx - c.qx) * sx0
+                             : pair_disp(jqx, jix, c.qx, c.ix, sx0, false);
+        const float ry = per ? (float)(int32_t)(jqy - c.qy) * sx1
+                             : pair_disp(jqy, jiy, c.qy, c.iy, sx1, false);
         // the pair's own WCA cutoff r_m + r_j (not the largest one: a dense
         // mixture would fail the test for pairs that cannot interact)
         const float rc = multi ? sqrtf(pt.cut2[st.species[m] * kMaxSpecies + st.species[j]]) : rc0;
-        const float lim = rc + sc.disp[base + m] + sc.disp[base + j] + 1e-3f;
+        const float lim = rc + c.disp + jd + 1e-3f;
         if (rx * rx + ry * ry < lim * lim) {
+          // the lists are scanned 16 entries per round of loads (an
+          // entry-by-entry loop waited one round trip per entry)
           bool listed = false;
-          const int sm = sc.slot_of[base + m], sj = sc.slot_of[base + j];
+          const int sm = c.sm;
           if (nlist) {  // j among m's listed neighbours
             const int nn = sc.nn[base + m];
-            for (int k = 0; k < nn; ++k)
-              listed |= (sc.nl[(size_t)k * M + base + m] & 0xffffff) == j;
-          } else if (sc.root[base + j] == sc.root[base + m] && sm < 0) {  // same big cluster
-            const uint32_t bm = (uint32_t)(-1 - sm), bj = (uint32_t)(-1 - sj);
-            const uint32_t* bp = sc.big_pairs + (size_t)e * kBigPairs;
-            const int np = min(sc.big_np[e], kBigPairs);
-            for (int k = 0; k < np; ++k) {
-              const uint32_t a = bp[k] & 1023u, b = (bp[k] >> 10) & 1023u;
-              listed |= (a == bm && b == bj) || (a == bj && b == bm);
+            for (int k = 0; k < nn && !listed; k += 8) {
+              int32_t v[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u)
+                v[u] = k + u < nn ? sc.nl[(size_t)(k + u) * M + base + m] : -1;
+#pragma unroll
+              for (int u = 0; u < 8; ++u) listed |= (v[u] & 0xffffff) == j;
             }
-          } else if (sc.root[base + j] == sc.root[base + m]) {  // same wave: its pairs
-            const int wv = sm >> 6;
+          } else if (rj == c.root && sm < 0) {  // same big cluster
+            const uint32_t bm = (uint32_t)(-1 - sm), bj = (uint32_t)(-1 - sj);
+            const uint32_t k1 = bm | bj << 10, k2 = bj | bm << 10;
+            const uint4* bp = reinterpret_cast<const uint4*>(sc.big_pairs + (size_t)e * kBigPairs);
+            const int np = min(sc.big_np[e], kBigPairs);
+            listed = list_holds(bp, np, 0xfffffu, k1, k2);
+          } else if (rj == c.root) {  // same wave: its pairs
             const uint32_t lm = (uint32_t)(sm & 63), lj = (uint32_t)(sj & 63);
-            const uint32_t* pw = sc.pairs + ((size_t)e * sc.wmax + wv) * kPairsPerWave;
-            const int np = sc.wave_npairs[(size_t)e * sc.wmax + wv];
-            for (int k = 0; k < np; ++k) {
-              const uint32_t a = pw[k] & 63u, b = (pw[k] >> 6) & 63u;
-              listed |= (a == lm && b == lj) || (a == lj && b == lm);
+            const uint32_t k1 = lm | lj << 6, k2 = lj | lm << 6;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const uint32_t w[4] = {c.l[u].x, c.l[u].y, c.l[u].z, c.l[u].w};
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const uint32_t x = w[q] & 0xfffu;
+                listed |= 4 * u + q < c.np && (x == k1 || x == k2);
+              }
+            }
+            if (!listed && c.np > 16) {
+              const uint4* pw = reinterpret_cast<const uint4*>(
+                  sc.pairs + ((size_t)e * sc.wmax + (sm >> 6)) * kPairsPerWave);
+              listed = list_holds(pw + 4, c.np - 16, 0xfffu, k1, k2);
             }
           }
           if (!listed) misc[1] = 1;
@@ -3885,18 +3978,23 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
         kc = (int)ceilf(lim_max / side);
         if (kc > 2 || ncx < 2 * kc + 1 || ncy < 2 * kc + 1) kc = 99;
       }
+#ifdef SWARM_CHECK_TIMING
+      ckc = kc;
+#endif
       if (kc <= 2) {
         const int32_t* cs = sc.bcstart + (size_t)e * ((size_t)ncx * ncy + 1);
-        const int lane = tid & 63, nwv = T >> 6;
-        for (int k = tid >> 6; k < nm; k += nwv) {  // wave-uniform mover
+        // G lanes per mover, G = 64 / 2^k with every mover in flight at once
+        // when they fit in the workgroup (a wave per mover took one chain of
+        // memory latencies per 16 movers: the 9-16 us checks of the windows
+        // with many movers)
+        int G = 64;
+        while (G > 4 && nm * G > T) G >>= 1;
+        const int lane = tid & (G - 1), ng = T / G;
+        for (int k = tid / G; k < nm; k += ng) {
           const int m = movers[k];
-          const uint32_t qx = sc.bq[base + m], qy = sc.bq[M + base + m];
-          const int cx = per ? (int)(qx >> (32 - cell_lx))
-                             : cell_coord(qx, sc.bimg[base + m], cell_lx, false);
-          const int cy = per ? (int)(qy >> (32 - cell_ly))
-                             : cell_coord(qy, sc.bimg[M + base + m], cell_ly, false);
-          // up to two ranges per row (a periodic row wraps once)
-          int rb[10], rl[10], nr = 0;
+          const MoverCtx c = mover_ctx(m);
+          const int cx = per ? (int)(c.qx >> (32 - cell_lx)) : cell_coord(c.qx, c.ix, cell_lx, false);
+          const int cy = per ? (int)(c.qy >> (32 - cell_ly)) : cell_coord(c.qy, c.iy, cell_ly, false);
           for (int oy = -kc; oy <= kc; ++oy) {
             int y = cy + oy;
             if (!per && (y < 0 || y >= ncy)) continue;
@@ -3907,43 +4005,40 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
               x0 = max(x0, 0);
               x1 = min(x1, ncx - 1);
             }
-            if (x0 < 0) {  // periodic wrap on the left
-              rb[nr] = cs[row | (ncx + x0)];
-              rl[nr] = cs[(row | (ncx - 1)) + 1] - rb[nr];
-              ++nr;
+            // the row's cells as up to two sorted ranges (a periodic row
+            // wraps at one end at most: ncx >= 2 kc + 1)
+            int b1 = 0, l1 = 0;
+            if (x0 < 0) {
+              b1 = cs[row | (ncx + x0)];
+              l1 = cs[(row | (ncx - 1)) + 1] - b1;
               x0 = 0;
-            }
-            if (x1 > ncx - 1) {  // periodic wrap on the right
-              rb[nr] = cs[row];
-              rl[nr] = cs[(row | (x1 - ncx)) + 1] - rb[nr];
-              ++nr;
+            } else if (x1 > ncx - 1) {
+              b1 = cs[row];
+              l1 = cs[(row | (x1 - ncx)) + 1] - b1;
               x1 = ncx - 1;
             }
-            rb[nr] = cs[row | x0];
-            rl[nr] = cs[(row | x1) + 1] - rb[nr];
-            ++nr;
-          }
-          int total = 0;
-          for (int r = 0; r < nr; ++r) total += rl[r];
-          for (int f = lane; f < total; f += 64) {
-            int jj = f, r = 0;
-            while (jj >= rl[r]) jj -= rl[r++];
-            const int j = sc.bsid[base + rb[r] + jj] & 0xffffff;
-            if (j != m) test_pair(m, j);
+            const int b0 = cs[row | x0], l0 = cs[(row | x1) + 1] - b0;
+            for (int f = lane; f < l0 + l1; f += G) {
+              const int j = sc.bsid[base + (f < l0 ? b0 + f : b1 + f - l0)] & 0xffffff;
+              if (j != m) test_pair(m, j, c);
+            }
           }
         }
       } else {
-        const long total = (long)nm * N;
-        for (long t = tid; t < total; t += T) {
-          const int m = movers[t / N];
-          const int j = (int)(t % N);
-          if (j != m) test_pair(m, j);
+        for (int k = 0; k < nm; ++k) {  // every colloid against each mover
+          const int m = movers[k];
+          const MoverCtx c = mover_ctx(m);
+          for (int j = tid; j < N; j += T)
+            if (j != m) test_pair(m, j, c);
         }
       }
     }
     __syncthreads();
   }
   const bool rerun = flagged_build || misc[1] != 0;
+#ifdef SWARM_CHECK_TIMING
+  ct2 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (sc.l1_pairs) {
     // the candidate lists the run's extra workgroups built from this
     // window's start positions hold every pair of the next window's start
@@ -4001,6 +4096,13 @@ __global__ __launch_bounds__(1024) void k_check(const Derived* __restrict__ d, D
     sc.gnx[e] = 0;
   }
   advance_counter(step_ctr, arrive, step0, n_steps);
+#ifdef SWARM_CHECK_TIMING
+  if (tid == 0) {
+    uint64_t* cw = sc.phase + 32 + 8 * (size_t)e;
+    cw[0] = ct0; cw[1] = ct1; cw[2] = ct2; cw[3] = __builtin_amdgcn_s_memrealtime();
+    cw[4] = (uint64_t)nm; cw[5] = (uint64_t)bign; cw[6] = (uint64_t)(int64_t)ckc; cw[7] = rerun;
+  }
+#endif
   role_end(sc, kRoleCheck);
 }
 

@@ -255,11 +255,16 @@ def _disc(rng, n, L):
     return pos, dirs
 
 
+@pytest.mark.parametrize("env_build", ["0", "1"])
 @pytest.mark.parametrize("force", [40.0, 400.0])
-def test_fast_swimmers_cross_skin_bit_exact(force):
+def test_fast_swimmers_cross_skin_bit_exact(force, env_build, monkeypatch):
     """Swimmers faster than skin / window exercise the decomposition check and
-    the global-path re-run; results must stay bit-exact."""
+    the global-path re-run; results must stay bit-exact.  env_build = "1":
+    the one-launch LDS build (k_build_env), whose cell-sorted snapshot the
+    check's cell-based exact test reads from global memory."""
     from gpu_harness import Harness, random_state, species_list
+
+    monkeypatch.setenv("SWARMRL_AMD_ENV_BUILD", env_build)
 
     rng = np.random.default_rng(9)
     box = [150.0, 150.0, 150.0]
