@@ -144,18 +144,17 @@ __device__ __forceinline__ float asinf_small(float a) {
   return __builtin_fmaf(p, a, a);
 }
 
+// acos by the three-range asin reduction, branch-free: the outer ranges'
+// 0.5 (1 + x) for x < -0.5 is 0.5 (1 - |x|) bit for bit (a + (-b) = a - b),
+// so one correctly rounded sqrt (t >= 2^-25 or 0: sqrt_pos holds) and one
+// asin polynomial serve every lane (a divergent wave ran all three ranges).
 __device__ __forceinline__ float acosf_fixed(float x) {
-  if (x < -0.5f) {
-    float t = 1.0f + x;
-    t = 0.5f * t;
-    return 3.14159265358979323846f - 2.0f * asinf_small(sqrt_rn(t));
-  }
-  if (x > 0.5f) {
-    float t = 1.0f - x;
-    t = 0.5f * t;
-    return 2.0f * asinf_small(sqrt_rn(t));
-  }
-  return 1.57079632679489661923f - asinf_small(x);
+  const bool outer = x < -0.5f || x > 0.5f;
+  const float t = 0.5f * (1.0f - fabsf(x));
+  const float a = asinf_small(outer ? sqrt_pos(t) : x);
+  const float two_a = 2.0f * a;
+  if (!outer) return 1.57079632679489661923f - a;
+  return x < 0.0f ? 3.14159265358979323846f - two_a : two_a;
 }
 
 // Three standard normals from one Philox block: a full Box-Muller pair from

@@ -417,7 +417,8 @@ __device__ __forceinline__ void vision_hit(const VisionLane& L, const swarm_visi
   if (!vision_offsets<kAny>(L, c0, &dx, &dy)) return;
   const int ti = vision_rec_type(c1.y);
   if (ti < 0 || vision_rec_id(c1.y) == L.i) return;
-  const float dist = swarm::sqrt_rn(dx * dx + dy * dy);
+  // (dist^2 >= sx0^2 ~ 1e-14: positive and normal, no special cases)
+  const float dist = swarm::sqrt_pos(dx * dx + dy * dy);
   if (!(dist < L.R)) return;
   float amp = (2.0f * __uint_as_float(c1.x)) / dist;
   amp = fminf(1.0f, amp);
@@ -616,7 +617,7 @@ __device__ __forceinline__ void vision_body(const DevState& st, const Derived* _
   L.iyi = (int32_t)own0.w;
   float sn, cs;
   swarm::sincos_turn(own1.z, &sn, &cs);
-  const float nm = swarm::sqrt_rn(cs * cs + sn * sn);
+  const float nm = swarm::sqrt_pos(cs * cs + sn * sn);  // ~1
   L.mx = cs / nm;
   L.my = sn / nm;
   L.sx0 = d->sx[0];
