@@ -71,6 +71,67 @@ __global__ __launch_bounds__(256) void k_valu(const float* __restrict__ rows_g,
   if (lane == 0) cyc[blockIdx.x * 4 + wv] = t1 - t0;
 }
 
+// The VALU phase B with the rows of the next FOUR samples read while these
+// four are used (one LDS wait per four samples instead of one per sample).
+__global__ __launch_bounds__(256) void k_valu4(const float* __restrict__ rows_g,
+                                               const float* __restrict__ par,
+                                               float* __restrict__ out,
+                                               unsigned long long* __restrict__ cyc) {
+  __shared__ __align__(16) float rows[4][128 * kRow];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int k = lane; k < 128 * kRow; k += 64) rows[wv][k] = rows_g[k];
+  __syncthreads();
+  const f2 w1p{par[lane], par[lane + 64]}, b1p{par[128 + lane], par[192 + lane]};
+  f2 wop[5];
+  for (int q = 0; q < 5; ++q) wop[q] = f2{par[256 + q * 128 + lane], par[256 + q * 128 + 64 + lane]};
+  f2 gwop[5], gb1 = splat(0.0f), gw1 = splat(0.0f);
+  for (int q = 0; q < 5; ++q) gwop[q] = splat(0.0f);
+  const float* srow = rows[wv];
+  __builtin_amdgcn_s_waitcnt(0);
+  const unsigned long long t0 = __builtin_readcyclecounter();
+  f4 na[4], nb[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    na[u] = *reinterpret_cast<const f4*>(srow + u * kRow);
+    nb[u] = *reinterpret_cast<const f4*>(srow + u * kRow + 4);
+  }
+  for (int tile = 0; tile < kTiles; ++tile) {
+    for (int s0 = 0; s0 < 128; s0 += 4) {
+      f4 a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] = na[u];
+        b[u] = nb[u];
+        const int sn = (s0 + 4 + u) & 127;
+        na[u] = *reinterpret_cast<const f4*>(srow + sn * kRow);
+        nb[u] = *reinterpret_cast<const f4*>(srow + sn * kRow + 4);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float g[5] = {a[u].x, a[u].y, a[u].z, a[u].w, b[u].x};
+        const float x = b[u].y;
+        f2 h = __builtin_elementwise_fma(w1p, splat(x), b1p);
+        h = __builtin_elementwise_max(h, splat(0.0f));
+        f2 dh = splat(0.0f);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+          gwop[q] = __builtin_elementwise_fma(splat(g[q]), h, gwop[q]);
+          dh = __builtin_elementwise_fma(wop[q], splat(g[q]), dh);
+        }
+        dh.x = h.x > 0.0f ? dh.x : 0.0f;
+        dh.y = h.y > 0.0f ? dh.y : 0.0f;
+        gb1 += dh;
+        gw1 = __builtin_elementwise_fma(dh, splat(x), gw1);
+      }
+    }
+  }
+  const unsigned long long t1 = __builtin_readcyclecounter();
+  float acc = gb1.x + gb1.y + gw1.x + gw1.y;
+  for (int q = 0; q < 5; ++q) acc += gwop[q].x + gwop[q].y;
+  out[blockIdx.x * 256 + threadIdx.x] = acc;
+  if (lane == 0) cyc[blockIdx.x * 4 + wv] = t1 - t0;
+}
+
 __global__ __launch_bounds__(256) void k_mfma(const float* __restrict__ rows_g,
                                               const float* __restrict__ par,
                                               float* __restrict__ out,
@@ -128,7 +189,7 @@ int main() {
   hipMemcpy(d_rows, rows.data(), rows.size() * 4, hipMemcpyHostToDevice);
   hipMemcpy(d_par, par.data(), par.size() * 4, hipMemcpyHostToDevice);
   std::vector<unsigned long long> cyc(blocks * 4);
-  for (int v = 0; v < 2; ++v) {
+  for (int v = 0; v < 3; ++v) {
     for (int rep = 0; rep < 3; ++rep) {
       hipEvent_t e0, e1;
       hipEventCreate(&e0);
@@ -136,6 +197,8 @@ int main() {
       hipEventRecord(e0);
       if (v == 0)
         hipLaunchKernelGGL(k_valu, dim3(blocks), dim3(256), 0, 0, d_rows, d_par, d_out, d_cyc);
+      else if (v == 2)
+        hipLaunchKernelGGL(k_valu4, dim3(blocks), dim3(256), 0, 0, d_rows, d_par, d_out, d_cyc);
       else
         hipLaunchKernelGGL(k_mfma, dim3(blocks), dim3(256), 0, 0, d_rows, d_par, d_out, d_cyc);
       hipEventRecord(e1);
@@ -147,7 +210,9 @@ int main() {
       for (auto c : cyc) mean += (double)c;
       mean /= (double)cyc.size();
       printf("%s rep %d: %.1f cycles per 128-sample tile per wave (128 units), launch %.3f ms\n",
-             v == 0 ? "VALU phase B (all of it)" : "MFMA dWo only          ", rep,
+             v == 0 ? "VALU phase B (all of it)       "
+                    : (v == 2 ? "VALU phase B, rows 4 ahead     " : "MFMA dWo only                  "),
+             rep,
              mean / kTiles, ms);
     }
   }
