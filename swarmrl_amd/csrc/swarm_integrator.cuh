@@ -3476,11 +3476,17 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
     return;
   }
   const int lane = tid & 63, wv = tid >> 6;
-  const int gw0 = (b - n_noise_blocks - n_cand_blocks) * run_wpb;
+  // wave-major over the envs (slot t: wave t / E of env t % E): every env's
+  // low waves -- the ones that exist -- come in the first blocks, the slots
+  // past an env's wave count (they exit at once) last, so no live wave waits
+  // for a CU behind them (C4, 8 x 1024: start skew up to 19 us env-major)
+  const int t0 = (b - n_noise_blocks - n_cand_blocks) * run_wpb;
   const bool table_ok = ctl[kCtlTStep + par] == step0 && (uint64_t)n_steps <= ctl[kCtlTLen + par];
   const float* table = table_ok ? tables + par * noise_table_words(M) : nullptr;
   if (wv >= run_wpb) return;
-  const int gw = gw0 + wv;
+  const int t = t0 + wv;
+  if (t >= n_envs * sc.wmax) return;  // the last block's padding
+  const int gw = (t % n_envs) * sc.wmax + t / n_envs;
   // latency-bound launches last as long as their slowest wave: one with
   // 65-128 pairs (a cluster denser than two pairs per particle) runs its own
   // unrolled two-pass sub-step instead of the general pass loop

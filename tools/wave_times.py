@@ -17,8 +17,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("envs", nargs="?", type=int, default=1)
 ap.add_argument("slices", nargs="?", type=int, default=30)
 ap.add_argument("--c5", action="store_true", help="the C5 workload (16384 colloids, field + RND)")
+ap.add_argument("--colloids", type=int, default=0, help="colloids per env (C4: 1024 with E = 8)")
 a = ap.parse_args()
-n = 16384 if a.c5 else 4096
+n = a.colloids or (16384 if a.c5 else 4096)
 ns = bench.argparse.Namespace(colloids=n, envs_per_gpu=a.envs)
 torch.cuda.set_device(0)
 eng, ff, agent = (bench.build_c5_workload if a.c5 else bench.build_workload)(
