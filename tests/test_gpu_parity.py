@@ -88,6 +88,36 @@ def test_bd_parity_dense_wca_multi_env():
     assert len(oracle.neighbor_pairs(h.op, got[0], 2.0)) > 10
 
 
+@pytest.mark.parametrize("E", [8, 16])
+def test_bd_parity_throughput_kernel_xcd_envs(E, monkeypatch):
+    """The throughput run kernel (SWARMRL_AMD_WIDE_RUN=0) at E = 8 and 16 envs:
+    its XCD-aware block placement (env e on XCD e mod 8, block-major over
+    each XCD's envs, blocks past an env's wave count leaving before they
+    stage anything) on dilute swimmers, against the oracle env by env."""
+    from gpu_harness import Harness, random_state, species_list
+
+    monkeypatch.setenv("SWARMRL_AMD_WIDE_RUN", "0")
+    rng = np.random.default_rng(11)
+    n = 512
+    L = float(np.sqrt(n * np.pi / 0.1))  # area fraction 0.1
+    box = [L, L, L]
+    sp = np.zeros(n, int)
+    h = Harness(box, 1e-3, 1.0239, 1.0239, 5, species_list()[:1], sp, n_envs=E)
+    states = [random_state(rng, n, box) for _ in range(E)]
+    sd_states = [oracle.sd_run(h.op, s, sp, 100)[0] for s in states]
+    h.upload(states)
+    h.sd(100)
+    f = rng.choice([0.0, 10.0], n * E).astype(np.float32)
+    t = rng.choice([-10.0, 0.0, 10.0], n * E).astype(np.float32)
+    h.set_actions(f, t)
+    h.integrate(100)
+    got = h.download()
+    for e in range(E):
+        ref, _, _ = oracle.bd_run(h.op, sd_states[e], sp, f[e * n:(e + 1) * n],
+                                  t[e * n:(e + 1) * n], 100, step0=0, env=e)
+        _eq(got[e], ref)
+
+
 def test_bd_parity_kt0_deterministic():
     from gpu_harness import Harness, random_state, species_list
 
