@@ -1400,7 +1400,7 @@ int launch_global(swarm_engine* e, int n_steps, int sd_mode, float g, float md) 
 // step counter.
 int launch_noise(swarm_engine* e, hipStream_t stream, int n) {
   const long M = (long)e->n_envs * e->n;
-  const long items = M * (long)swarm::noise_groups(n);
+  const long items = M * (long)swarm::noise_items(n);
   hipLaunchKernelGGL(swarm::k_noise, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, stream,
                      e->d_derived, e->st, e->d_step, e->d_noise, n);
   HIP_TRY(hipGetLastError());

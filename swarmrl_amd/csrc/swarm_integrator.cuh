@@ -37,6 +37,12 @@
 #include "../../include/swarmrl_amd.h"
 #include "swarm_device.cuh"
 
+// Sub-step schedule of the run kernels (round 6): off-chain work placed in
+// the latency windows of the position exchange and the force-sum round trip.
+#ifndef SWARM_RUN_SCHED
+#define SWARM_RUN_SCHED 2
+#endif
+
 namespace swarm {
 
 constexpr int kMaxSpecies = SWARM_MAX_SPECIES;
@@ -3008,45 +3014,51 @@ __host__ __device__ inline size_t noise_index(size_t M, size_t gi, int s, int c)
 __host__ __device__ inline size_t noise_step_stride(size_t) { return 3; }
 __host__ __device__ inline size_t noise_comp_stride(size_t) { return 1; }
 
-// Group k of a table starting at step_start: sub-steps t = 4 (g0 + k) + j
-// (g0 = step_start / 4) of particle gi, those within [start, start + len).
-// One thread draws the group's three Philox blocks (StepNoise).
-__device__ __forceinline__ void noise_group(const Derived* __restrict__ d, const DevState& st,
+// Item (k, b) of a table starting at step_start: Philox block b (0..2) of
+// group g = g0 + k (g0 = step_start / 4), i.e. normals n[4b..4b+3] of
+// sub-steps t = 4 g .. 4 g + 3 (StepNoise's numbers), stored where they
+// fall in particle gi's records: element u of the block is word
+// f + u = 12 k + 4 b - 3 (step_start mod 4) + u of the particle's run of
+// 12-B records, kept when it lies within [0, 3 len).  One block per lane and
+// consecutive items at consecutive 16-B words: with an aligned start a wave's
+// stores are one float4 per lane over 1 KiB of whole lines (three scalar
+// stores per normal at a 48-B lane stride left lines partially written, and
+// WRITE_SIZE at 2-3.5x the table).
+__device__ __forceinline__ void noise_block(const Derived* __restrict__ d, const DevState& st,
                                             uint64_t step_start, int len,
-                                            float* __restrict__ table, long gi, int k) {
-  const long M = st.m;
+                                            float* __restrict__ table, long gi, int k, int b) {
   const int e = (int)(gi / st.n);
   const int i = (int)(gi - (long)e * st.n);
-  const uint64_t t0 = (step_start & ~3ull) + 4ull * (uint64_t)k;
-  const size_t cs = noise_comp_stride((size_t)M);
-  StepNoise sn;
+  float n[4];
+  group_block(d->key0, d->key1 ^ (uint32_t)e, (uint32_t)i, (step_start >> 2) + (uint64_t)k,
+              (uint32_t)b, n);
+  const int f = 12 * k + 4 * b - 3 * (int)(step_start & 3u);
+  float* o = table + noise_index((size_t)st.m, (size_t)gi, 0, 0);
+  // streaming stores: the table is read by the next window's run only
+  // (same-box A/B, E = 1: the launch ends ~1.1 us sooner, the next
+  // window's gathers cost ~0.6 us; head line 51.8 -> 52.5 M)
+  if ((f & 3) == 0 && f >= 0 && f + 4 <= 3 * len) {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    const f32x4 v = {n[0], n[1], n[2], n[3]};
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(o + f));
+  } else {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float g[3];
-    sn.next(d->key0, d->key1 ^ (uint32_t)e, (uint32_t)i, t0 + (uint64_t)j, j == 0, g);
-    const long s = (long)(t0 + (uint64_t)j) - (long)step_start;
-    if (s >= 0 && s < len) {
-      float* o = table + noise_index((size_t)M, (size_t)gi, (int)s, 0);
-      // streaming stores: the table is read by the next window's run only
-      // (same-box A/B, E = 1: the launch ends ~1.1 us sooner, the next
-      // window's gathers cost ~0.6 us; head line 51.8 -> 52.5 M)
-      __builtin_nontemporal_store(g[0], o);
-      __builtin_nontemporal_store(g[1], o + cs);
-      __builtin_nontemporal_store(g[2], o + 2 * cs);
-    }
+    for (int u = 0; u < 4; ++u)
+      if (f + u >= 0 && f + u < 3 * len) __builtin_nontemporal_store(n[u], o + f + u);
   }
 }
 
-// Work item k of a table fill over M particles x G groups: consecutive
-// items are the consecutive groups of one particle (the stores of a wave
-// then cover contiguous records).
-__device__ __forceinline__ void noise_item(long k, long M, int G, long* gi, int* grp) {
-  (void)M;
-  *gi = k / G;
-  *grp = (int)(k - *gi * G);
-}
-
+// Work item k of a table fill over M particles: noise_items(len) per
+// particle, (group, block) in order, so consecutive lanes store consecutive
+// 16-B words of one particle's records.
 __host__ __device__ inline int noise_groups(int len) { return len / 4 + 2; }  // any alignment
+__host__ __device__ inline int noise_items(int len) { return 3 * noise_groups(len); }
+__device__ __forceinline__ void noise_item(long k, int per, long* gi, int* grp, int* blk) {
+  *gi = k / per;
+  const int r = (int)(k - *gi * per);
+  *grp = r / 3;
+  *blk = r - 3 * *grp;
+}
 
 // This window's table of len sub-steps (grid.y = noise_groups(len)) from the
 // current step counter.
@@ -3060,13 +3072,13 @@ __global__ __launch_bounds__(256) void k_noise(const Derived* __restrict__ d, De
     ctl[kCtlTStep + par] = step0;
     ctl[kCtlTLen + par] = (uint64_t)len;
   }
-  const int G = noise_groups(len);
+  const int per = noise_items(len);
   const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= M * G) return;
+  if (k >= M * per) return;
   long gi;
-  int grp;
-  noise_item(k, M, G, &gi, &grp);
-  noise_group(d, st, step0, len, tables + par * noise_table_words(M), gi, grp);
+  int grp, blk;
+  noise_item(k, per, &gi, &grp, &blk);
+  noise_block(d, st, step0, len, tables + par * noise_table_words(M), gi, grp, blk);
 }
 
 // One wave of the cluster run: all n_steps sub-steps of the particles in
@@ -3182,6 +3194,32 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     }
     if (!kTable && pc.noisy) noise.next(k0, k1, (uint32_t)i, step0 + (uint64_t)s, s == 0, gt);
     int64_t ax = 0, ay = 0;
+    float dnext[2] = {dir[0], dir[1]};
+    uint32_t an_next;
+    // rotation (bd_step's sequence): off the force chain
+    auto rotate = [&]() __attribute__((always_inline)) {
+      float dth = tz * pc.rot_dt;
+      if (pc.noisy) dth = dth + pc.sig_r * gt[2];
+      an_next = p.an + (uint32_t)f2i32(dth * kAngInvScale);
+    };
+    // the previous sub-step's displacement (max is order-free)
+    auto prev_disp = [&]() __attribute__((always_inline)) {
+      if (SWARM_RUN_SCHED && s > 0) {
+        const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
+        const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
+        dmax2 = __uint_as_float(max(__float_as_uint(dmax2), __float_as_uint(ddx * ddx + ddy * ddy)));
+      }
+    };
+    // the next sub-step's director, pinned where it is computed: without a
+    // use there the compiler sinks it past the read-back's vote branch into
+    // the next sub-step's translation, onto the force chain
+    auto director = [&]() __attribute__((always_inline)) {
+      if (!kLast) sincos_turn(an_next, &dnext[0], &dnext[1]);
+      if (SWARM_RUN_SCHED) __asm__ volatile("" : "+v"(dnext[0]), "+v"(dnext[1]));
+    };
+    if (kPass == 0 || SWARM_RUN_SCHED < 2) {
+      if (SWARM_RUN_SCHED) prev_disp();
+    }
     if (kPass > 0) {
       for (int q = 0; q < (kPass == 1 ? 1 : (kPass == 2 ? 2 : npass)); ++q) {
         {  // wave-uniform; an empty slot names the lane twice
@@ -3198,6 +3236,15 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
                                       (uint32_t)__builtin_amdgcn_ds_bpermute(a << 2, (int)p.qy));
           const uint2 pb = make_uint2((uint32_t)__builtin_amdgcn_ds_bpermute(b << 2, (int)p.qx),
                                       (uint32_t)__builtin_amdgcn_ds_bpermute(b << 2, (int)p.qy));
+          if (SWARM_RUN_SCHED >= 2 && q == 0) {
+            // the exchange's latency window: rotation and displacement
+            __builtin_amdgcn_sched_barrier(0);
+            rotate();
+            prev_disp();
+            // pinned here (the compiler would sink both behind the vote branch)
+            __asm__ volatile("" : "+v"(an_next), "+v"(dmax2));
+            __builtin_amdgcn_sched_barrier(0);
+          }
           const float rx = (float)(int32_t)(pb.x - pa.x) * sx0;
           const float ry = (float)(int32_t)(pb.y - pa.y) * sx1;
           int64_t fx, fy;  // on a; b receives exactly the negation
@@ -3216,35 +3263,45 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
         }
       }
     }
-    // rotation (bd_step's sequence) and the next director, between the
-    // force-sum atomics and their read-back
-    __builtin_amdgcn_sched_barrier(0);
-    float dnext[2] = {dir[0], dir[1]};
-    float dth = tz * pc.rot_dt;
-    if (pc.noisy) dth = dth + pc.sig_r * gt[2];
-    const uint32_t an_next = p.an + (uint32_t)f2i32(dth * kAngInvScale);
-    if (!kLast) sincos_turn(an_next, &dnext[0], &dnext[1]);
-    __builtin_amdgcn_sched_barrier(0);
-    __asm__ volatile("" ::: "memory");  // keep the read-back after the director
-    if (kPass > 0) {
+    if (SWARM_RUN_SCHED >= 2 && kPass > 0) {
+      // the read-back issued right behind the atomics (a wave's DS operations
+      // execute in order), the director computed in its latency window
       wave_lds_sync();
-#ifdef SWARM_PHASE_TIMING
-      if (stamp) {
-        t1s = __builtin_amdgcn_s_memtime();
-        t_pairs += t1s - t0s;
-      }
-#endif
       ax = (int64_t)lacc_x[lane];
       ay = (int64_t)lacc_y[lane];
       lacc_x[lane] = 0ull;
       lacc_y[lane] = 0ull;
+      __builtin_amdgcn_sched_barrier(0);
+      director();
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      // rotation (bd_step's sequence) and the next director, between the
+      // force-sum atomics and their read-back
+      __builtin_amdgcn_sched_barrier(0);
+      rotate();
+      director();
+      __builtin_amdgcn_sched_barrier(0);
+      __asm__ volatile("" ::: "memory");  // keep the read-back after the director
+      if (kPass > 0) {
+        wave_lds_sync();
 #ifdef SWARM_PHASE_TIMING
-      if (stamp) {
-        const uint64_t t2 = __builtin_amdgcn_s_memtime();
-        t_read += t2 - t1s;
-        t1s = t2;
-      }
+        if (stamp) {
+          t1s = __builtin_amdgcn_s_memtime();
+          t_pairs += t1s - t0s;
+        }
 #endif
+        ax = (int64_t)lacc_x[lane];
+        ay = (int64_t)lacc_y[lane];
+        lacc_x[lane] = 0ull;
+        lacc_y[lane] = 0ull;
+#ifdef SWARM_PHASE_TIMING
+        if (stamp) {
+          const uint64_t t2 = __builtin_amdgcn_s_memtime();
+          t_read += t2 - t1s;
+          t1s = t2;
+        }
+#endif
+      }
     }
     if (kWalls && active) {  // contacts of real particles only
       int64_t az = 0;
@@ -3253,11 +3310,13 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     }
     bd_translate(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
                  kLast, &vx, &vy, &om, gt, dir[0], dir[1]);
-    const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
-    const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
-    // non-negative floats order like their bit patterns: one v_max_u32
-    // (fmaxf adds a canonicalising max)
-    dmax2 = __uint_as_float(max(__float_as_uint(dmax2), __float_as_uint(ddx * ddx + ddy * ddy)));
+    if (!SWARM_RUN_SCHED || kLast) {  // (else the next sub-step's prev_disp)
+      const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
+      const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
+      // non-negative floats order like their bit patterns: one v_max_u32
+      // (fmaxf adds a canonicalising max)
+      dmax2 = __uint_as_float(max(__float_as_uint(dmax2), __float_as_uint(ddx * ddx + ddy * ddy)));
+    }
     p.an = an_next;
     if (!kLast) {
       dir[0] = dnext[0];
@@ -3458,13 +3517,13 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
       ctl[kCtlTLen + (par ^ 1)] = (uint64_t)kMaxWindow;
     }
     float* t = tables + (par ^ 1) * noise_table_words(M);
-    const int G = noise_groups(kMaxWindow);
-    const long total = (long)G * (long)M;
+    const int per = noise_items(kMaxWindow);
+    const long total = (long)per * (long)M;
     for (long k = (long)b * blockDim.x + tid; k < total; k += (long)n_noise_blocks * blockDim.x) {
       long gi;
-      int grp;
-      noise_item(k, (long)M, G, &gi, &grp);
-      noise_group(d, st, start, kMaxWindow, t, gi, grp);
+      int grp, blk;
+      noise_item(k, per, &gi, &grp, &blk);
+      noise_block(d, st, start, kMaxWindow, t, gi, grp, blk);
     }
     stamp_end(tstamp);
     return;

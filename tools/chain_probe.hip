@@ -1,0 +1,168 @@
+// Dependent-chain latencies of one lone wave on gfx950 (round 6): the
+// E = 1 run kernel is one wave per CU running a 100-sub-step recurrence, so
+// what a sub-step costs is the latency of its dependency chain, not the
+// issue rate.  Each test runs a chain of kIters dependent operations in one
+// 64-thread block and reports shader cycles (s_memtime) per operation.
+// Measurement only; not part of the library.
+//   hipcc --offload-arch=gfx950 -O3 tools/chain_probe.hip -o tools/_variants/chain_probe
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+constexpr int kIters = 512;
+
+#define PIN(x) __asm__ volatile("" : "+v"(x))
+
+__device__ __forceinline__ unsigned long long now() {
+  __builtin_amdgcn_s_waitcnt(0);
+  return __builtin_amdgcn_s_memtime();
+}
+
+__global__ void k_probe(int test, float fa, float fb, unsigned long long* out, float* sink,
+                        const int* chase) {
+  __shared__ unsigned long long lds[128];
+  const int lane = threadIdx.x;
+  lds[lane] = 0;
+  lds[lane + 64] = 0;
+  __syncthreads();
+  float x = fa + (float)lane * 1e-7f, y = fb, z = fa * 0.5f, w = fb * 0.25f;
+  double dx = (double)x;
+  int ix = lane;
+  unsigned long long t0 = now(), t1 = 0;
+  switch (test) {
+    case 0:  // dependent v_fma_f32
+      for (int k = 0; k < kIters; ++k) {
+        x = __builtin_fmaf(x, fa, fb);
+        PIN(x);
+      }
+      break;
+    case 1:  // four independent fma chains interleaved (issue rate)
+      for (int k = 0; k < kIters / 4; ++k) {
+        x = __builtin_fmaf(x, fa, fb);
+        y = __builtin_fmaf(y, fa, fb);
+        z = __builtin_fmaf(z, fa, fb);
+        w = __builtin_fmaf(w, fa, fb);
+        PIN(x);
+        PIN(y);
+        PIN(z);
+        PIN(w);
+      }
+      break;
+    case 2:  // dependent v_rcp_f32
+      for (int k = 0; k < kIters; ++k) {
+        x = __builtin_amdgcn_rcpf(x);
+        PIN(x);
+      }
+      break;
+    case 3:  // dependent ds_bpermute (lane ^ 1)
+      for (int k = 0; k < kIters; ++k) {
+        ix = __builtin_amdgcn_ds_bpermute((lane ^ 1) << 2, ix);
+        PIN(ix);
+      }
+      break;
+    case 4:  // ds_add_u64 x4 then ds_read_b64 of the sum (the run's force round trip)
+      for (int k = 0; k < kIters; ++k) {
+        const unsigned long long v = (unsigned long long)(unsigned)ix;
+        __hip_atomic_fetch_add(&lds[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(&lds[lane + 64], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(&lds[lane ^ 1], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(&lds[(lane ^ 1) + 64], v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        ix = (int)lds[lane];
+        PIN(ix);
+      }
+      break;
+    case 5:  // wave vote through SALU into a uniform branch, dependent
+      for (int k = 0; k < kIters; ++k) {
+        const bool all = __builtin_amdgcn_ballot_w64(x < 1e30f) == __builtin_amdgcn_read_exec();
+        if (all)
+          x = x + 1.0f;
+        else
+          x = x * 0.5f;
+        PIN(x);
+      }
+      break;
+    case 6:  // dependent v_fma_f64
+      for (int k = 0; k < kIters; ++k) {
+        dx = __builtin_fma(dx, (double)fa, (double)fb);
+        __asm__ volatile("" : "+v"(dx));
+      }
+      break;
+    case 7:  // f32 -> i32 -> f32 (v_cvt pair), dependent
+      for (int k = 0; k < kIters; ++k) {
+        x = (float)__float2int_rn(x);
+        PIN(x);
+      }
+      break;
+    case 8:  // dependent global loads (L2-resident pointer chase)
+      for (int k = 0; k < kIters; ++k) {
+        ix = chase[ix];
+        PIN(ix);
+      }
+      break;
+    case 9:  // dependent v_add_u32
+      for (int k = 0; k < kIters; ++k) {
+        ix = ix + 3;
+        PIN(ix);
+      }
+      break;
+    case 10:  // dependent v_mul_f32
+      for (int k = 0; k < kIters; ++k) {
+        x = x * fa;
+        PIN(x);
+      }
+      break;
+    case 11:  // ds_write_b64 then ds_read_b64 of another lane's word (LDS publish round trip)
+      for (int k = 0; k < kIters; ++k) {
+        lds[lane] = (unsigned long long)(unsigned)ix;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        ix = (int)lds[lane ^ 1];
+        PIN(ix);
+      }
+      break;
+    case 12:  // DPP row swap (quad_perm [1,0,3,2]) dependent
+      for (int k = 0; k < kIters; ++k) {
+        ix = __builtin_amdgcn_mov_dpp(ix, 0xB1, 0xF, 0xF, false);
+        PIN(ix);
+      }
+      break;
+  }
+  t1 = now();
+  if (lane == 0) out[test] = t1 - t0;
+  sink[lane] = x + y + z + w + (float)dx + (float)ix;
+}
+
+int main() {
+  const char* names[] = {"v_fma_f32 dependent",   "v_fma_f32 4 chains",   "v_rcp_f32 dependent",
+                         "ds_bpermute dependent", "4 ds_add_u64 + read",  "ballot vote + branch",
+                         "v_fma_f64 dependent",   "cvt f32->i32->f32",    "global load chase (L2)",
+                         "v_add_u32 dependent",   "v_mul_f32 dependent",  "ds_write + ds_read other lane",
+                         "DPP quad swap dependent"};
+  const int ntest = 13;
+  unsigned long long* d_out;
+  float* d_sink;
+  int* d_chase;
+  hipMalloc(&d_out, 64 * sizeof(unsigned long long));
+  hipMalloc(&d_sink, 64 * sizeof(float));
+  int h_chase[4096];
+  for (int k = 0; k < 4096; ++k) h_chase[k] = (k * 37 + 11) & 4095;
+  hipMalloc(&d_chase, sizeof(h_chase));
+  hipMemcpy(d_chase, h_chase, sizeof(h_chase), hipMemcpyHostToDevice);
+  for (int rep = 0; rep < 3; ++rep) {
+    for (int t = 0; t < ntest; ++t)
+      hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 0, 0, t, 1.0000001f, 1e-7f, d_out, d_sink,
+                         d_chase);
+    hipDeviceSynchronize();
+    unsigned long long h[64];
+    hipMemcpy(h, d_out, sizeof(h), hipMemcpyDeviceToHost);
+    if (rep == 2)
+      for (int t = 0; t < ntest; ++t)
+        printf("%-32s %7.1f cycles/op\n", names[t], (double)h[t] / kIters);
+  }
+  return 0;
+}
