@@ -98,6 +98,10 @@ def parse_args():
     ap.add_argument("--c4-colloids", type=int, default=1024)
     ap.add_argument("--train-episodes", type=int, default=4,
                     help="timed episodes of the 'c3train' line (rollout + PPO update)")
+    ap.add_argument("--force-collective", action="store_true",
+                    help="at --gpus 1: a world-size-1 RCCL group, and the episode-parallel "
+                         "collectives (broadcast, packed trajectory all-gather, replicated "
+                         "update) run through it as at N GPUs (rollout.force_collectives)")
     ap.add_argument("--stub", action="store_true",
                     help="CPU plumbing test: no GPU, gloo, synthetic trajectories")
     return ap.parse_args()
@@ -746,7 +750,9 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
     # env g is placed with default_rng(42 + g) (swarm_engine.add_colloids)
     envs = shard_envs(world * E, rank, world)
     eng, ff, agent = (builder or build_workload)(args_e, 42 + envs[0], device)
-    if train and world > 1:
+    # the collectives run at world > 1, or through a world-1 group when forced
+    coll = world > 1 or getattr(args, "force_collective", False)
+    if train and coll:
         broadcast_agent(agent)  # rank 0's replica everywhere (EpisodeParallelTrainer)
     eng.integrate(1, ff)  # setup, overlap removal, first slice (eager)
 
@@ -770,15 +776,15 @@ def measure(args, E, rank, world, device, builder=None, colloids=None, line="hea
         the gathered [T, world E, ...] episode (rollout.replicated_update,
         SURVEY 8(e)); at world 1 the update runs on the local episode."""
         traj = agent.trajectory  # in graph mode: the episode graph's output tensors
-        st = {} if (timed and world > 1 and len(gstats) < 4) else None
+        st = {} if (timed and coll and len(gstats) < 4) else None
         if train:
             n_updates[0] += 1
-            if world > 1:
+            if coll:
                 episode = gather_episode(traj, stats=st)
                 replicated_update(agent, episode, seed=1000 + n_updates[0])
             else:
                 agent.loss.compute_loss(network=agent.network, episode_data=traj)
-        elif timed and world > 1:
+        elif timed and coll:
             gather_trajectory(traj, stats=st)
         if st:
             gstats.append(st)
@@ -1059,6 +1065,19 @@ def main():
     else:
         if world > 1:
             dist.init_process_group("nccl", init_method="env://")
+        elif args.force_collective:
+            # one rank, one GPU: a world-size-1 RCCL group on a free local port
+            import socket
+
+            from swarmrl_amd.rollout import force_collectives
+
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                port = sk.getsockname()[1]
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                                    world_size=1, device_id=torch.device("cuda", local_rank))
+            force_collectives(True)
         torch.cuda.set_device(local_rank)
         device = torch.device("cuda", local_rank)
         res = run_lines(args, lines, rank, world, device)
@@ -1121,9 +1140,11 @@ def main():
             line["cpu_baseline_all_cores"] = cpu_baseline_all_cores(args)
         if args.cpu_all_pairs_slices > 0:
             line["cpu_baseline_all_pairs_vision"] = cpu_baseline_all_pairs(args)
+    if args.force_collective and world == 1:
+        line["config"]["parallelism"] += " (forced through a world-size-1 RCCL group)"
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if world > 1 or (args.force_collective and dist.is_initialized()):
         dist.destroy_process_group()
 
 

@@ -401,9 +401,6 @@ def policy_mlp_sample(obs: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2:
     return idx, logp, f, t
 
 
-_PPO_WS: Dict[Tuple[int, int], torch.Tensor] = {}
-
-
 def adam_args(optimizer, layers):
     """swarm_adam_t for a torch Adam whose only parameters are the six PPO
     layers, or None when the fused step does not apply (another optimizer,
@@ -439,7 +436,7 @@ def adam_args(optimizer, layers):
 def ppo_epoch_grad(features: torch.Tensor, actions: torch.Tensor, old_logp: torch.Tensor,
                    rewards: torch.Tensor, layers, gamma: float, lambda_: float,
                    clip_eps: float, entropy_coef: float, out: torch.Tensor = None,
-                   adam=None) -> torch.Tensor:
+                   adam=None, workspaces: dict = None) -> torch.Tensor:
     """
     The gradient of one PPO epoch (swarm_ppo_epoch_grad): features [T, S, d]
     fp32, actions [T, S] int64, old_logp / rewards [T, S] fp32 (all device),
@@ -449,6 +446,11 @@ def ppo_epoch_grad(features: torch.Tensor, actions: torch.Tensor, old_logp: torc
     are used in place (no copies: the launches can be graph-captured).
     adam: a swarm_adam_t (adam_args) -- the optimizer's step then runs in the
     epoch's last launch (swarm_ppo_epoch_step) and updates the layers.
+    workspaces: the caller's own cache of workspaces (one per device and
+    size, never dropped while the caller lives, so a captured graph that
+    holds a workspace's pointer never replays into freed memory); without
+    one every call takes a fresh zeroed buffer (a module-wide
+    single-entry cache freed a buffer another loss's graph still used).
     """
     T, S = int(actions.shape[0]), int(actions.shape[1])
     x = features.reshape(T * S, -1).to(torch.float32).contiguous()
@@ -461,10 +463,11 @@ def ppo_epoch_grad(features: torch.Tensor, actions: torch.Tensor, old_logp: torc
     if nbytes < 0:
         raise ValueError("bad PPO sizes")
     key = (dev.index or 0, nbytes)
-    ws = _PPO_WS.get(key)
+    ws = workspaces.get(key) if workspaces is not None else None
     if ws is None:  # zeroed once: the fused Adam's ticket is left at zero after use
-        _PPO_WS.clear()
-        ws = _PPO_WS[key] = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+        ws = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+        if workspaces is not None:
+            workspaces[key] = ws
     size = hidden * d_in + hidden + k * hidden + k + hidden + 1
     grad = out if out is not None else torch.empty(size, dtype=torch.float32, device=dev)
     if grad.numel() != size or grad.dtype != torch.float32 or not grad.is_contiguous():

@@ -87,7 +87,8 @@ class ProximalPolicyLoss(Loss):
                 grad = ops.ppo_epoch_grad(features, actions, old_log_probs, rewards, layers,
                                           self.value_function.gamma,
                                           self.value_function.lambda_, self.epsilon,
-                                          self.entropy_coefficient)
+                                          self.entropy_coefficient,
+                                          workspaces=self._workspaces())
                 network.apply_gradients(layers, grad)
                 continue
             loss = self._calculate_loss(network, features, actions, rewards, old_log_probs)
@@ -118,9 +119,14 @@ class ProximalPolicyLoss(Loss):
         # optimizer's own step after the gradient)
         adam = (ops.adam_args(opt, layers)
                 if os.environ.get("SWARMRL_AMD_FUSED_ADAM", "1") != "0" else None)
+        # every hyper-parameter the fused step bakes into its captured
+        # arguments (betas / eps were missing)
         sig = (adam is not None, id(network), id(opt), tuple(features.shape),
                tuple(actions.shape),
-               tuple(float(g["lr"]) for g in opt.param_groups),
+               tuple((float(g["lr"]), tuple(float(b) for b in g.get("betas", ())),
+                      float(g.get("eps", 0.0)), float(g.get("weight_decay", 0.0)),
+                      bool(g.get("amsgrad", False)), bool(g.get("maximize", False)))
+                     for g in opt.param_groups),
                tuple(t.data_ptr() for st in states for t in st.values()
                      if isinstance(t, torch.Tensor)),
                tuple(p.data_ptr() for p in layers), self.n_epochs,
@@ -142,15 +148,17 @@ class ProximalPolicyLoss(Loss):
                 off += p.numel()
             args = (x, act, olp, rew, layers, self.value_function.gamma,
                     self.value_function.lambda_, self.epsilon, self.entropy_coefficient)
-            ops.ppo_epoch_grad(*args, out=grad)  # sizes the workspace outside the capture
+            ws = self._workspaces()
+            # sizes the workspace outside the capture
+            ops.ppo_epoch_grad(*args, out=grad, workspaces=ws)
             torch.cuda.synchronize(features.device)
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
                 for _ in range(self.n_epochs):
                     if adam is not None:
-                        ops.ppo_epoch_grad(*args, out=grad, adam=adam)
+                        ops.ppo_epoch_grad(*args, out=grad, adam=adam, workspaces=ws)
                     else:
-                        ops.ppo_epoch_grad(*args, out=grad)
+                        ops.ppo_epoch_grad(*args, out=grad, workspaces=ws)
                         opt.step()
             cache = self._ppo_graph = {"sig": sig, "graph": graph, "inputs": (x, act, olp, rew),
                                        "grad": grad}
@@ -163,6 +171,14 @@ class ProximalPolicyLoss(Loss):
         if hasattr(network, "epoch_count"):
             network.epoch_count += self.n_epochs
         return True
+
+    def _workspaces(self):
+        """This loss's fused-PPO workspaces (one per device and size), kept
+        for its lifetime: its captured epoch graph reads them in place."""
+        ws = getattr(self, "_ppo_ws", None)
+        if ws is None:
+            ws = self._ppo_ws = {}
+        return ws
 
     def _fused_layers(self, network, features, actions):
         """The network's layers when the epoch gradient runs as the fused

@@ -179,7 +179,11 @@ class TorchModel:
             if st is not None and st.device == device:
                 grown[: st.numel()] = st
             self._agent_state = st = grown
-        return (*layers, self._fused_seed, st, float(self.exploration_policy.probability))
+        # a key of its own: the group counters of compute_action_fused also
+        # start at zero, so one network serving both paths would otherwise
+        # replay the same Gumbel noise on them
+        return (*layers, self._fused_seed ^ 0x2545F4914F6CDD1D, st,
+                float(self.exploration_policy.probability))
 
     def _mlp_layers(self, d_in: int, k: int):
         """The actor weights when the one-kernel policy applies (fp32 device

@@ -23,6 +23,7 @@ beats five small ones.
 
 from __future__ import annotations
 
+import os
 import time
 from typing import Dict, Optional, Sequence
 
@@ -50,8 +51,24 @@ def shard_envs(total_envs: int, rank: int, world: int):
     return list(range(lo, lo + per + (1 if rank < extra else 0)))
 
 
+_FORCE_COLLECTIVE = [False]
+
+
+def force_collectives(flag: bool = True) -> None:
+    """Run every collective of this module even in a world of one process
+    (a world-size-1 RCCL group then executes the real device-tensor
+    all-gather, broadcast and all-reduce on one GPU: the path N GPUs take,
+    minus the transfers; tests/test_gpu_rccl.py, bench.py
+    --force-collective).  Also on with SWARMRL_AMD_FORCE_COLLECTIVE=1."""
+    _FORCE_COLLECTIVE[0] = bool(flag)
+
+
 def _is_distributed(group=None) -> bool:
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    if dist.get_world_size(group) > 1:
+        return True
+    return _FORCE_COLLECTIVE[0] or os.environ.get("SWARMRL_AMD_FORCE_COLLECTIVE", "0") == "1"
 
 
 def _as_tensor(x, device) -> torch.Tensor:

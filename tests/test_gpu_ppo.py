@@ -232,3 +232,84 @@ def test_fused_adam_step_matches_torch_adam(monkeypatch):
     # differences, which moves a few moment entries by ~1e-5 (absolute)
     for a, b in zip(runs["fused"][1] + runs["fused"][2], runs["torch"][1] + runs["torch"][2]):
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4)
+
+
+def _random_episode(dev, T, E, A, d, seed):
+    g = torch.Generator().manual_seed(seed)
+
+    class Episode:
+        features = [f.to(dev) for f in torch.randn(T, E, A, d, generator=g)]
+        actions = [a.to(dev) for a in torch.randint(0, 4, (T, E, A), generator=g)]
+        rewards = [r.to(dev) for r in torch.randn(T, E, A, generator=g)]
+        log_probs = [lp.to(dev) for lp in -1.386 + 0.3 * torch.randn(T, E, A, generator=g)]
+    return Episode()
+
+
+def _train(monkeypatch, fused, epsilon, episodes=3, n_epochs=5, d=1, A=300, seed0=200):
+    from swarmrl_amd.losses.proximal_policy_loss import ProximalPolicyLoss
+    from swarmrl_amd.networks.torch_network import ActorCriticMLP, TorchModel
+
+    dev = torch.device("cuda", 0)
+    monkeypatch.setenv("SWARMRL_AMD_FUSED_ADAM", fused)
+    torch.manual_seed(0)
+    model = TorchModel(ActorCriticMLP(d, 4, 128), input_shape=(d,), device=dev)
+    loss = ProximalPolicyLoss(n_epochs=n_epochs, epsilon=epsilon)
+    for ep in range(episodes):
+        loss.compute_loss(model, _random_episode(dev, 20, 1, A, d, seed0 + ep))
+    layers = model.model.ppo_layers()
+    st = [model.optimizer.state[p] for p in layers]
+    return ([p.detach().clone() for p in layers],
+            [s["exp_avg"].clone() for s in st] + [s["exp_avg_sq"].clone() for s in st])
+
+
+def test_fused_adam_moments_tight_without_clip_boundaries(monkeypatch):
+    """The looser moment tolerance of test_fused_adam_step_matches_torch_adam
+    is due to the clipped surrogate, measured: with epsilon so large that no
+    probability ratio reaches a clip boundary, the fused Adam step and
+    torch's agree on parameters AND moments at the parameters' tolerance
+    (rtol 2e-5) after the same three episodes x 5 epochs; and one fused epoch
+    from identical states differs from torch's by fp32 rounding only."""
+    fused = _train(monkeypatch, "1", epsilon=1e6)
+    ref = _train(monkeypatch, "0", epsilon=1e6)
+    for a, b in zip(fused[0] + fused[1], ref[0] + ref[1]):
+        torch.testing.assert_close(a, b, rtol=2e-5, atol=2e-6)
+    # one captured epoch (episode 1 eager with torch's step on both sides, so
+    # both start episode 2 from bit-identical states)
+    f1 = _train(monkeypatch, "1", epsilon=0.2, episodes=2, n_epochs=1)
+    r1 = _train(monkeypatch, "0", epsilon=0.2, episodes=2, n_epochs=1)
+    for a, b in zip(f1[0] + f1[1], r1[0] + r1[1]):
+        torch.testing.assert_close(a, b, rtol=2e-6, atol=1e-8)
+
+
+def test_two_losses_of_different_sizes_share_a_device(monkeypatch):
+    """Two PPO losses whose episodes have different T*S on one device
+    (ADVICE r5): each keeps its own fused-PPO workspace, so interleaving
+    their captured epoch graphs ends on exactly the parameters each reaches
+    alone."""
+    from swarmrl_amd.losses.proximal_policy_loss import ProximalPolicyLoss
+    from swarmrl_amd.networks.torch_network import ActorCriticMLP, TorchModel
+
+    dev = torch.device("cuda", 0)
+    monkeypatch.setenv("SWARMRL_AMD_FUSED_ADAM", "1")
+
+    def make(seed):
+        torch.manual_seed(seed)
+        return (TorchModel(ActorCriticMLP(2, 4, 64), input_shape=(2,), device=dev),
+                ProximalPolicyLoss(n_epochs=3))
+
+    sizes = {0: 300, 1: 700}
+    alone = {}
+    for k, A in sizes.items():
+        model, loss = make(k)
+        for ep in range(3):
+            loss.compute_loss(model, _random_episode(dev, 20, 1, A, 2, 50 * k + ep))
+        alone[k] = [p.detach().clone() for p in model.model.ppo_layers()]
+    pairs = {k: make(k) for k in sizes}
+    for ep in range(3):
+        for k, A in sizes.items():
+            model, loss = pairs[k]
+            loss.compute_loss(model, _random_episode(dev, 20, 1, A, 2, 50 * k + ep))
+    for k in sizes:
+        assert pairs[k][1]._ppo_graph is not None
+        for a, b in zip(alone[k], pairs[k][0].model.ppo_layers()):
+            assert torch.equal(a, b.detach())
