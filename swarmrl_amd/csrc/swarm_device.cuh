@@ -340,29 +340,33 @@ __device__ __forceinline__ void i64x2_to_f32(int64_t ax, int64_t ay, float* fx, 
 }
 
 // 1 / x correctly rounded, for x in [2^-96, 2^96] (every in-range squared
-// pair distance: the fixed-point grid step is >= 2^-48).  It is the
-// compiler's IEEE division sequence for 1.0f / x (v_rcp_f32, a Newton step,
-// then two residual corrections) without the v_div_scale / v_div_fmas /
-// v_div_fixup range handling, which is the identity on this range (no
-// scaling: the exponents of 1 and x differ by < 96, neither is denormal).
-// Bit-identical to 1.0f / x over the whole range: tests/test_gpu_rcp.py
-// checks every float in it on the GPU.
+// pair distance: the fixed-point grid step is >= 2^-48): the hardware
+// estimate v_rcp_f32 and ONE residual correction -- r = 1 - x y exactly
+// (fma), then y + r y rounded once.  No v_div_scale / v_div_fixup range
+// handling is needed on this range (no scaling: the exponents of 1 and x
+// differ by < 96, neither is denormal).  Bit-identical to the IEEE division
+// 1.0f / x for every float in the range on gfx950 (1.6e9 values, checked
+// exhaustively on the GPU by tests/test_gpu_devmath.py::
+// test_rcp_rn_exhaustive).  Round 6: three dependent operations where the
+// compiler's division sequence (a Newton step, then two corrections) takes
+// seven, on the run kernels' force chain, where a dependent VALU operation
+// of a lone wave costs ~11 cycles (tools/chain_probe.hip).
 __device__ __forceinline__ float rcp_rn(float x) {
-  float y = __builtin_amdgcn_rcpf(x);
-  const float e = __builtin_fmaf(-x, y, 1.0f);
-  y = __builtin_fmaf(e, y, y);
-  float r = __builtin_fmaf(-x, y, 1.0f);
-  const float q = __builtin_fmaf(r, y, y);
-  r = __builtin_fmaf(-x, q, 1.0f);
-  return __builtin_fmaf(r, y, q);
+  const float y = __builtin_amdgcn_rcpf(x);
+  const float r = __builtin_fmaf(-x, y, 1.0f);
+  return __builtin_fmaf(r, y, y);
 }
 
 // q + dq with the box crossing carried into the image counter: the high
 // word of the 64-bit sum (q zero-extended, dq sign-extended) is -1, 0 or +1.
+// The new q is one 32-bit add (the next sub-step's position exchange waits
+// on it); the carry comes from comparing it with the old q, off that chain:
+// dq >= 0 wrapped past 2^32 iff the sum is below q, dq < 0 wrapped below 0
+// iff it is above q.
 __device__ __forceinline__ void advance(uint32_t& q, int32_t& img, int32_t dq) {
-  const int64_t sum = (int64_t)(uint64_t)q + (int64_t)dq;
-  img += (int32_t)(sum >> 32);
-  q = (uint32_t)sum;
+  const uint32_t qn = q + (uint32_t)dq;
+  img += dq >= 0 ? (qn < q ? 1 : 0) : (qn > q ? -1 : 0);
+  q = qn;
 }
 
 }  // namespace swarm

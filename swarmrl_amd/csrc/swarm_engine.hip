@@ -1265,6 +1265,9 @@ struct swarm_engine {
   // length are checked on the device, this flag only skips k_noise).
   bool wide_run = false;
   int run_wpb = 4;  // run waves per block (= per CU) of k_cluster_run_wide
+  // a rotation helper wave beside each run wave of k_cluster_run_wide
+  // (swarm::rot_helper; run_wpb <= 2)
+  bool rot_helper = true;
   // k_build_env: the whole build in one LDS-resident workgroup per env
   bool env_build = false;
   int noise_blocks = 0;
@@ -1553,11 +1556,15 @@ int launch_run(swarm_engine* e, int n_steps, unsigned long long* tstamp = nullpt
     // l1_pairs: the next window's candidate lists built beside the run
     const int ncb = e->sc.l1_pairs ? e->n_envs * ((e->n + 1023) / 1024) : 0;
     const dim3 grid((unsigned)(e->noise_blocks + ncb + (waves + R - 1) / R));
-    const size_t lds = 96 * 1024;  // one block per CU
+    // one block per CU; with rotation helpers (run_wpb <= 2, round 6) their
+    // director tables in the dynamic LDS
+    const int helpers = e->rot_helper && R <= 2 ? 1 : 0;
+    const size_t lds = helpers ? std::max<size_t>(96 * 1024, R * swarm::helper_lds_bytes())
+                               : 96 * 1024;
 #define SWARM_WIDE(MULTI, WALLS)                                                             \
   hipLaunchKernelGGL((swarm::k_cluster_run_wide<MULTI, WALLS>), grid, dim3(1024), lds, e->stream, \
                      e->d_derived, e->st, e->sc, e->n_envs, n_steps, e->d_step, e->d_noise,      \
-                     e->noise_blocks, R, ncb, e->lxb, e->lyb, tstamp)
+                     e->noise_blocks, R, ncb, e->lxb, e->lyb, tstamp, helpers)
     if (walls) {
       if (multi)
         SWARM_WIDE(true, true);
@@ -2114,6 +2121,8 @@ int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_
     // (32 noise workgroups above 4096 colloids, so that C4's 8 x 1024 gets one
     // run wave per CU, measured slower: C4 81.1 -> 72.9 M, same box)
     e->noise_blocks = e->wide_run && M <= 16384 ? 64 : 0;
+    const char* orh = std::getenv("SWARMRL_AMD_ROT_HELPER");
+    if (orh && orh[0] == '0') e->rot_helper = false;
     const char* ow = std::getenv("SWARMRL_AMD_WIDE_RUN");
     if (ow && ow[0] == '0') e->wide_run = false, e->noise_blocks = 0;
     // run waves per CU: a wave alone on its CU does not share the CU's

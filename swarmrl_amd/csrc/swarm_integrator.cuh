@@ -40,7 +40,7 @@
 // Sub-step schedule of the run kernels (round 6): off-chain work placed in
 // the latency windows of the position exchange and the force-sum round trip.
 #ifndef SWARM_RUN_SCHED
-#define SWARM_RUN_SCHED 2
+#define SWARM_RUN_SCHED 3
 #endif
 
 namespace swarm {
@@ -498,21 +498,35 @@ __device__ __forceinline__ void pair_force(float cut2, float sig6, float eps24, 
 // first particle in 2^-24 fixed point, or zero out of range (r2 = 0 for an
 // empty slot that names one particle twice).  In-range values equal
 // pair_force's; the int32 conversion is taken when every lane fits.
-__device__ __forceinline__ void pair_fix_sel(float cut2, float sig6, float eps24, float rx,
-                                             float ry, int64_t& fx, int64_t& fy) {
+// pair_force's force on the first particle scaled by 2^24 (fp32), zero out
+// of range, with a short dependency chain and the same values:
+//  * no select before the reciprocal: an out-of-range lane's value is
+//    discarded by the final select (in range r2 >= 2^-96, rcp_rn's range);
+//  * 2 s6 - 1 as one fma (2 s6 is exact, so one rounding either way);
+//  * (-fr rx) 2^24 = fr (-rx 2^24): scaling by 2^24 commutes with the
+//    rounding (no overflow or subnormal here), and -rx 2^24 is ready before
+//    fr.
+__device__ __forceinline__ void pair_vals(float cut2, float sig6, float eps24, float rx, float ry,
+                                          float& vx, float& vy) {
   const float r2 = rx * rx + ry * ry;
   const bool in = r2 < cut2 && r2 > 0.0f;
-  const float ir2 = rcp_rn(in ? r2 : 1.0f);  // = 1.0f / r2 (in range: r2 >= 2^-96)
+  const float ir2 = rcp_rn(r2);  // = 1.0f / r2 on every in-range lane
+  const float rxs = rx * -16777216.0f, rys = ry * -16777216.0f;
   float ir6 = ir2 * ir2;
   ir6 = ir6 * ir2;
   const float s6 = sig6 * ir6;
-  float t = 2.0f * s6;
-  t = t - 1.0f;
+  const float t = __builtin_fmaf(s6, 2.0f, -1.0f);
   float fr = eps24 * s6;
   fr = fr * t;
   fr = fr * ir2;
-  const float vx = (in ? -fr * rx : 0.0f) * 16777216.0f;
-  const float vy = (in ? -fr * ry : 0.0f) * 16777216.0f;
+  vx = in ? fr * rxs : 0.0f;
+  vy = in ? fr * rys : 0.0f;
+}
+
+__device__ __forceinline__ void pair_fix_sel(float cut2, float sig6, float eps24, float rx,
+                                             float ry, int64_t& fx, int64_t& fy) {
+  float vx, vy;
+  pair_vals(cut2, sig6, eps24, rx, ry, vx, vy);
   if (__builtin_expect(wave_all2(fabsf(vx) < 2147483520.0f, fabsf(vy) < 2147483520.0f), 1)) {
     fx = (int64_t)__float2int_rn(vx);
     fy = (int64_t)__float2int_rn(vy);
@@ -678,27 +692,47 @@ __device__ __forceinline__ void bd_step(const PConst& c, PState& p, int64_t ax, 
 // bd_step without the rotation, for the cluster run (which updates the
 // angle, and the next sub-step's director, while the force sums are in
 // flight): same operation sequence for the translation and velocities.
-__device__ __forceinline__ void bd_translate(const PConst& c, PState& p, int64_t ax, int64_t ay,
-                                             float fs, float tz, float fex, float fey,
-                                             uint32_t k0, uint32_t k1, uint32_t id, uint64_t step,
-                                             bool last, float* vx, float* vy, float* w,
-                                             const float* g, float sn, float cs) {
-  float fx, fy;
-  i64x2_to_f32(ax, ay, &fx, &fy);
-  fx = fx * 5.9604644775390625e-08f;
-  fy = fy * 5.9604644775390625e-08f;
-  fx = fx + fex;
-  fy = fy + fey;
+// from the force sums already converted to fp32 (2^24 fixed-point units):
+// F 2^-24 + f_ext as one fma (F 2^-24 is exact, so the same single rounding)
+// kNoiseAlways: the translation noise is added unconditionally; the caller
+// passes sig_t = 0 for a noiseless engine (dx + 0 g rounds to the same
+// integer displacement as dx, g being finite), so no select sits on the chain.
+// Carry: with a Carry record the image counters are left to the caller
+// (apply_carry, off the next sub-step's chain); q is updated here.
+struct Carry {
+  uint32_t qx0, qy0;
+  int32_t dqx, dqy;
+};
+__device__ __forceinline__ void apply_carry(PState& p, const Carry& c) {
+  p.ix += (int32_t)(((int64_t)(uint64_t)c.qx0 + (int64_t)c.dqx) >> 32);
+  p.iy += (int32_t)(((int64_t)(uint64_t)c.qy0 + (int64_t)c.dqy) >> 32);
+}
+template <bool kNoiseAlways = false>
+__device__ __forceinline__ void bd_translate_f(const PConst& c, PState& p, float fx, float fy,
+                                               float fs, float tz, float fex, float fey,
+                                               uint32_t k0, uint32_t k1, uint32_t id,
+                                               uint64_t step, bool last, float* vx, float* vy,
+                                               float* w, const float* g, float sn, float cs,
+                                               Carry* carry = nullptr) {
+  fx = __builtin_fmaf(fx, 5.9604644775390625e-08f, fex);
+  fy = __builtin_fmaf(fy, 5.9604644775390625e-08f, fey);
   fx = fx + fs * cs;
   fy = fy + fs * sn;
   float dx = fx * c.mob_dt;
   float dy = fy * c.mob_dt;
-  if (c.noisy) {
+  if (kNoiseAlways || c.noisy) {
     dx = dx + c.sig_t * g[0];
     dy = dy + c.sig_t * g[1];
   }
-  advance(p.qx, p.ix, f2i32(dx * c.inv_sx0));
-  advance(p.qy, p.iy, f2i32(dy * c.inv_sx1));
+  const int32_t dqx = f2i32(dx * c.inv_sx0), dqy = f2i32(dy * c.inv_sx1);
+  if (carry) {
+    *carry = Carry{p.qx, p.qy, dqx, dqy};
+    p.qx += (uint32_t)dqx;
+    p.qy += (uint32_t)dqy;
+  } else {
+    advance(p.qx, p.ix, dqx);
+    advance(p.qy, p.iy, dqy);
+  }
   if (last) {
     float v0 = fx * c.inv_gt, v1 = fy * c.inv_gt;
     float om = tz * c.inv_gr;
@@ -713,6 +747,16 @@ __device__ __forceinline__ void bd_translate(const PConst& c, PState& p, int64_t
     *vy = v1;
     *w = om;
   }
+}
+
+__device__ __forceinline__ void bd_translate(const PConst& c, PState& p, int64_t ax, int64_t ay,
+                                             float fs, float tz, float fex, float fey,
+                                             uint32_t k0, uint32_t k1, uint32_t id, uint64_t step,
+                                             bool last, float* vx, float* vy, float* w,
+                                             const float* g, float sn, float cs) {
+  float fx, fy;
+  i64x2_to_f32(ax, ay, &fx, &fy);
+  bd_translate_f(c, p, fx, fy, fs, tz, fex, fey, k0, k1, id, step, last, vx, vy, w, g, sn, cs);
 }
 
 // One steepest-descent step of one particle (espresso.py:1163-1168).
@@ -3081,19 +3125,119 @@ __global__ __launch_bounds__(256) void k_noise(const Derived* __restrict__ d, De
   noise_block(d, st, step0, len, tables + par * noise_table_words(M), gi, grp, blk);
 }
 
+// Rotation helper (round 6, latency-bound runs).  A particle's orientation
+// never depends on positions or forces: sub-step s turns it by
+// f2i32((tz tau + sig_r g2_s) 2^32 / 2 pi), so the whole window's directors
+// can be computed apart from the force chain.  In k_cluster_run_wide a
+// second wave of the block (another SIMD of the CU: waves are dealt to the
+// SIMDs in turn) runs the rotation of a run wave's 64 slots and writes each
+// sub-step's director (sin, cos) to LDS ahead of it; the run wave reads them
+// in its force round trip's latency window instead of issuing the ~35
+// rotation and sin/cos instructions itself (a lone wave's sub-step is
+// bounded by its own issue and dependency chain).  Same operation sequence
+// as the run wave's own rotation, so the same bits.  The run wave never
+// waits: a director the helper has not published yet is computed from the
+// window start (helper_director_at), so no wave depends on another's
+// progress.
+constexpr int32_t kHelpDone = 0x40000000;
+struct HelperLds {
+  float2* dir;       // [kMaxWindow][64] director of sub-step s (s >= 1)
+  uint32_t* an_end;  // [64] orientation after the window
+  int32_t* prog;     // directors [0, prog) published; kHelpDone: an_end too
+};
+__host__ __device__ constexpr size_t helper_lds_bytes() {
+  return (size_t)kMaxWindow * 64 * 8 + 64 * 4 + 64;
+}
+__device__ __forceinline__ HelperLds helper_lds(unsigned char* base, int slot) {
+  unsigned char* b = base + (size_t)slot * helper_lds_bytes();
+  HelperLds h;
+  h.dir = reinterpret_cast<float2*>(b);
+  h.an_end = reinterpret_cast<uint32_t*>(b + (size_t)kMaxWindow * 64 * 8);
+  h.prog = reinterpret_cast<int32_t*>(b + (size_t)kMaxWindow * 64 * 8 + 256);
+  return h;
+}
+
+// the orientation increment of sub-step s (bd_step's rotation sequence)
+__device__ __forceinline__ uint32_t rot_increment(const PConst& pc, float tzs, float g2) {
+  float dth = tzs * pc.rot_dt;
+  if (pc.noisy) dth = dth + pc.sig_r * g2;
+  return (uint32_t)f2i32(dth * kAngInvScale);
+}
+
+// The helper wave of run wave gw: publishes the directors of sub-steps
+// 1 .. n_steps - 1 and the final orientation.  Table normals only (the
+// latency-bound path); g2 loaded eight sub-steps ahead.
+template <bool kMulti>
+__device__ __forceinline__ void rot_helper(const Derived* __restrict__ d, const DevState& st,
+                                           const Scratch& sc, int n_envs, int n_steps,
+                                           const float* __restrict__ table, int gw, int lane,
+                                           const HelperLds& h, int par) {
+  const int e = gw / sc.wmax;
+  const int w = gw - e * sc.wmax;
+  if (e >= n_envs) return;
+  if (sc.fallback[e] != 0 || w >= sc.env_waves[e]) return;
+  const int N = st.n;
+  const size_t M = (size_t)st.m, base = (size_t)e * N;
+  const int i = sc.perm[(size_t)e * sc.S + w * 64 + lane];
+  const bool active = i >= 0;
+  const size_t gi = base + (active ? i : 0);
+  uint32_t an = 0u;
+  float tz0 = 0.0f, tzc = 0.0f;
+  int si = 0;
+  if (active) {
+    an = st.ang[gi];
+    si = st.species[i];
+    const PrevSlot prv = prev_slot(st, par);
+    tzc = st.torque_z[gi];
+    tz0 = st.reuse ? prv.tz[gi] : tzc;
+  }
+  const PConst pc = load_pconst(d, kMulti ? si : 0);
+  const float* tg = table + noise_index(M, gi, 0, 2);  // g2 of sub-step 0; stride 3
+  float gb[8], gx[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) gb[k] = k < n_steps ? tg[3 * k] : 0.0f;
+  for (int s0 = 0; s0 < n_steps; s0 += 8) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gx[k] = s0 + 8 + k < n_steps ? tg[3 * (s0 + 8 + k)] : 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int s = s0 + k;
+      if (s < n_steps) {
+        an = an + rot_increment(pc, s == 0 ? tz0 : tzc, gb[k]);
+        if (s + 1 < n_steps) {
+          float sn, cs;
+          sincos_turn(an, &sn, &cs);
+          h.dir[(size_t)(s + 1) * 64 + lane] = make_float2(sn, cs);
+          // publish (a wave's LDS writes complete in order: a reader that
+          // sees the count sees the directors)
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0)
+            __hip_atomic_store(h.prog, s + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gb[k] = gx[k];
+  }
+  h.an_end[lane] = an;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane == 0) __hip_atomic_store(h.prog, kHelpDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // One wave of the cluster run: all n_steps sub-steps of the particles in
 // its 64 slots.  kTable: the normals come from this window's noise table
 // (prefetched one sub-step ahead), else they are drawn here.
 // kMulti = false: one species, so the pair constants are wave-uniform scalars.
 // kTwoPass: waves with 65-128 pairs get their own unrolled two-pass variant
 // (else the general up-to-four-pass loop).
-template <bool kMulti, bool kTable, bool kWalls, bool kTwoPass = false>
+template <bool kMulti, bool kTable, bool kWalls, bool kTwoPass = false, bool kHelper = false>
 __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const DevState& st,
                                          const Scratch& sc, int n_envs, int n_steps,
                                          uint64_t step0, const float* __restrict__ table,
                                          int gw, int lane,
                                          unsigned long long* lacc_x, unsigned long long* lacc_y,
-                                         const PairTables& pt, int par) {
+                                         const PairTables& pt, int par,
+                                         HelperLds hl = HelperLds{}) {
   const int e = gw / sc.wmax;
   const int w = gw - e * sc.wmax;
   if (e >= n_envs) return;
@@ -3154,6 +3298,13 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
   const float eps24 = d->eps24;
   // one species: its constants are wave-uniform (scalar registers)
   const PConst pc = load_pconst(d, kMulti ? si : 0);
+  // helper mode: the window-start orientation and torques, for a director
+  // the helper has not published yet (helper_director_at)
+  const uint32_t an_start = p.an;
+  const float tz0 = tz, tzc = (kHelper && active) ? st.torque_z[gi] : 0.0f;
+  PConst pcn = pc;  // sig_t = 0 without noise (bd_translate_f<true>)
+  if (!pc.noisy) pcn.sig_t = 0.0f;
+  Carry carry = {0u, 0u, 0, 0};  // the previous sub-step's image carries, pending
   const float cut2_0 = d->cut2[0], sig6_0 = d->sig6[0];
   const uint32_t q0x = p.qx, q0y = p.qy;
   float dmax2 = 0.0f;
@@ -3177,6 +3328,13 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
   // A lone wave pays for every taken branch, so the sub-step is branch-lean:
   // the pass count (0, 1 or up to 4) and the last sub-step (velocities) are
   // compile-time variants, and idle lanes compute along (never stored).
+  // the orientation after j sub-steps, from the window start (helper mode:
+  // what the helper has not published yet)
+  auto helper_angle_at = [&](int j) __attribute__((always_inline)) {
+    uint32_t a = an_start;
+    for (int k = 0; k < j; ++k) a = a + rot_increment(pc, k == 0 ? tz0 : tzc, tcol[3 * k + 2]);
+    return a;
+  };
   float dir[2];
   sincos_turn(an0, &dir[0], &dir[1]);
   auto substep = [&](const int s, auto last_t, auto pass_t) __attribute__((always_inline)) {
@@ -3198,6 +3356,10 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     uint32_t an_next;
     // rotation (bd_step's sequence): off the force chain
     auto rotate = [&]() __attribute__((always_inline)) {
+      if (kHelper) {
+        an_next = p.an;  // the helper wave turns the directors
+        return;
+      }
       float dth = tz * pc.rot_dt;
       if (pc.noisy) dth = dth + pc.sig_r * gt[2];
       an_next = p.an + (uint32_t)f2i32(dth * kAngInvScale);
@@ -3213,13 +3375,32 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     // the next sub-step's director, pinned where it is computed: without a
     // use there the compiler sinks it past the read-back's vote branch into
     // the next sub-step's translation, onto the force chain
+    int hprog = 0;  // helper mode: the published count read with the director
     auto director = [&]() __attribute__((always_inline)) {
+      if constexpr (kHelper) {
+        if (!kLast) {  // the count first, then the director (LDS order)
+          hprog = __hip_atomic_load(hl.prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          const float2 dv = hl.dir[(size_t)(s + 1) * 64 + lane];
+          dnext[0] = dv.x;
+          dnext[1] = dv.y;
+        }
+        return;
+      }
       if (!kLast) sincos_turn(an_next, &dnext[0], &dnext[1]);
       if (SWARM_RUN_SCHED) __asm__ volatile("" : "+v"(dnext[0]), "+v"(dnext[1]));
     };
     if (kPass == 0 || SWARM_RUN_SCHED < 2) {
       if (SWARM_RUN_SCHED) prev_disp();
     }
+    // one-pass waves convert speculatively (see below); sa, sb, sv_*: the
+    // lane's pair for the rare fix-up
+    constexpr bool kSpec = SWARM_RUN_SCHED >= 3 && kPass == 1;
+    // speculative read-back conversion, image carries deferred (any pass count)
+    constexpr bool kDefer = SWARM_RUN_SCHED >= 3 && kPass > 0 && !kWalls;
+    float sv_x = 0.0f, sv_y = 0.0f;
+    int sa = lane, sb = lane;
+    bool spec_ok = true;
     if (kPass > 0) {
       for (int q = 0; q < (kPass == 1 ? 1 : (kPass == 2 ? 2 : npass)); ++q) {
         {  // wave-uniform; an empty slot names the lane twice
@@ -3241,14 +3422,30 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
             __builtin_amdgcn_sched_barrier(0);
             rotate();
             prev_disp();
-            // pinned here (the compiler would sink both behind the vote branch)
-            __asm__ volatile("" : "+v"(an_next), "+v"(dmax2));
+            if (kDefer) apply_carry(p, carry);
+            // pinned here (the compiler would sink them behind the vote branch)
+            __asm__ volatile("" : "+v"(an_next), "+v"(dmax2), "+v"(p.ix), "+v"(p.iy));
             __builtin_amdgcn_sched_barrier(0);
           }
           const float rx = (float)(int32_t)(pb.x - pa.x) * sx0;
           const float ry = (float)(int32_t)(pb.y - pa.y) * sx1;
           int64_t fx, fy;  // on a; b receives exactly the negation
-          if (kMulti) {
+          if (kSpec) {
+            // speculative int32 conversion: the atomics do not wait for the
+            // wave vote; a wave whose vote fails adds the exact remainder
+            // after them (spec_fix below), so the sums are the same integers
+            if (kMulti) {
+              const int sp = (int)((e_ >> 12) & 255u);
+              pair_vals(pt.cut2[sp], pt.sig6[sp], eps24, rx, ry, sv_x, sv_y);
+            } else {
+              pair_vals(cut2_0, sig6_0, eps24, rx, ry, sv_x, sv_y);
+            }
+            spec_ok = wave_all2(fabsf(sv_x) < 2147483520.0f, fabsf(sv_y) < 2147483520.0f);
+            fx = (int64_t)__float2int_rn(sv_x);
+            fy = (int64_t)__float2int_rn(sv_y);
+            sa = a;
+            sb = b;
+          } else if (kMulti) {
             const int sp = (int)((e_ >> 12) & 255u);
             pair_fix_sel(pt.cut2[sp], pt.sig6[sp], eps24, rx, ry, fx, fy);
           } else {
@@ -3271,6 +3468,26 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
       ay = (int64_t)lacc_y[lane];
       lacc_x[lane] = 0ull;
       lacc_y[lane] = 0ull;
+      if (kSpec && __builtin_expect(!spec_ok, 0)) {
+        // a pair force beyond 2^31 fixed-point units on some lane: the
+        // exact int64 values' remainders over the speculative int32 ones go
+        // through the (zeroed) sums once more
+        auto wide = [](float v) __attribute__((always_inline)) {
+          return __float2ll_rn(
+              fminf(fmaxf(v, -4.611686018427387904e18f), 4.611686018427387904e18f));
+        };
+        const int64_t rx_ = wide(sv_x) - (int64_t)__float2int_rn(sv_x);
+        const int64_t ry_ = wide(sv_y) - (int64_t)__float2int_rn(sv_y);
+        atomicAdd(&lacc_x[sa], (unsigned long long)rx_);
+        atomicAdd(&lacc_y[sa], (unsigned long long)ry_);
+        atomicSub(&lacc_x[sb], (unsigned long long)rx_);
+        atomicSub(&lacc_y[sb], (unsigned long long)ry_);
+        wave_lds_sync();
+        ax += (int64_t)lacc_x[lane];
+        ay += (int64_t)lacc_y[lane];
+        lacc_x[lane] = 0ull;
+        lacc_y[lane] = 0ull;
+      }
       __builtin_amdgcn_sched_barrier(0);
       director();
       __builtin_amdgcn_sched_barrier(0);
@@ -3308,8 +3525,30 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
       wall_forces<2>(d, si, (float)p.qx * sx0, (float)p.qy * sx1, 0.0f, ax, ay, az,
                      st.wall_viol);
     }
-    bd_translate(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
-                 kLast, &vx, &vy, &om, gt, dir[0], dir[1]);
+    if (kDefer) {
+      // speculative read-back conversion: the translation runs from the
+      // int32 view of the sums while the wave vote resolves; the rare wave
+      // with a sum beyond int32 redoes it from the exact conversion
+      // the image carries are applied in the next sub-step's exchange window
+      // (the last sub-step applies its own)
+      const PState p0 = p;
+      const bool fits = wave_all2(fits_i32(ax), fits_i32(ay));
+      bd_translate_f<true>(pcn, p, (float)(int32_t)ax, (float)(int32_t)ay, fs, tz, fex, fey, k0,
+                           k1, (uint32_t)i, step0 + (uint64_t)s, kLast, &vx, &vy, &om, gt, dir[0],
+                           dir[1], kLast ? nullptr : &carry);
+      // computed before the vote's branch (else the compiler moves the
+      // translation behind it, back onto the chain)
+      __asm__ volatile("" : "+v"(p.qx), "+v"(p.qy));
+      if (__builtin_expect(!fits, 0)) {
+        p = p0;
+        bd_translate_f<true>(pcn, p, i64_to_f32_wide(ax), i64_to_f32_wide(ay), fs, tz, fex, fey,
+                             k0, k1, (uint32_t)i, step0 + (uint64_t)s, kLast, &vx, &vy, &om, gt,
+                             dir[0], dir[1], kLast ? nullptr : &carry);
+      }
+    } else {
+      bd_translate(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
+                   kLast, &vx, &vy, &om, gt, dir[0], dir[1]);
+    }
     if (!SWARM_RUN_SCHED || kLast) {  // (else the next sub-step's prev_disp)
       const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
       const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
@@ -3318,6 +3557,11 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
       dmax2 = __uint_as_float(max(__float_as_uint(dmax2), __float_as_uint(ddx * ddx + ddy * ddy)));
     }
     p.an = an_next;
+    if (kHelper && !kLast && __builtin_amdgcn_readfirstlane(hprog) <= s + 1) {
+      // not published yet (the window's first sub-steps): from the start
+      const uint32_t a = helper_angle_at(s + 1);
+      sincos_turn(a, &dnext[0], &dnext[1]);
+    }
     if (!kLast) {
       dir[0] = dnext[0];
       dir[1] = dnext[1];
@@ -3361,6 +3605,12 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     run_steps(std::integral_constant<int, 2>{});
   else
     run_steps(std::integral_constant<int, 4>{});
+  if constexpr (kHelper) {  // the window's final orientation
+    const int pg = __hip_atomic_load(hl.prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t ae = hl.an_end[lane];
+    p.an = __builtin_amdgcn_readfirstlane(pg) == kHelpDone ? ae : helper_angle_at(n_steps);
+  }
 #ifdef SWARM_PHASE_TIMING
   if (stamp) {
     sc.phase[16] = t_pairs;
@@ -3412,8 +3662,12 @@ __device__ __forceinline__ void run_wave_dispatch(const Derived* __restrict__ d,
                                                   int gw, int lane,
                                                   unsigned long long* lacc_x,
                                                   unsigned long long* lacc_y,
-                                                  const PairTables& pt, int par) {
-  if (table)
+                                                  const PairTables& pt, int par,
+                                                  bool help = false, HelperLds hl = HelperLds{}) {
+  if (table && help)
+    run_wave<kMulti, true, kWalls, kTwoPass, true>(d, st, sc, n_envs, n_steps, step0, table, gw,
+                                                   lane, lacc_x, lacc_y, pt, par, hl);
+  else if (table)
     run_wave<kMulti, true, kWalls, kTwoPass>(d, st, sc, n_envs, n_steps, step0, table, gw, lane,
                                              lacc_x, lacc_y, pt, par);
   else
@@ -3501,10 +3755,17 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
                                                            float* __restrict__ tables,
                                                            int n_noise_blocks, int run_wpb,
                                                            int n_cand_blocks, int lxb, int lyb,
-                                                           unsigned long long* __restrict__ tstamp) {
+                                                           unsigned long long* __restrict__ tstamp,
+                                                           int helpers) {
   __shared__ PairTables pt;
   __shared__ unsigned long long lacc[4][2][64];
+  extern __shared__ __align__(16) unsigned char dyn_lds[];  // rotation helpers' tables
   stamp_start(tstamp);
+  // helpers != 0 (host: run_wpb <= 2 and the dynamic LDS holds run_wpb
+  // helper tables): the published counts start at zero before any wave of
+  // the block reads them (ordered by stage_pair_tables' barrier)
+  if (helpers && threadIdx.x < (unsigned)run_wpb)
+    *helper_lds(dyn_lds, (int)threadIdx.x).prog = 0;
   stage_pair_tables(d, &pt);
   const int par = window_parity(ctl);
   const uint64_t step0 = ctl[kCtlStep];
@@ -3542,15 +3803,24 @@ __global__ __launch_bounds__(1024) void k_cluster_run_wide(const Derived* __rest
   const int t0 = (b - n_noise_blocks - n_cand_blocks) * run_wpb;
   const bool table_ok = ctl[kCtlTStep + par] == step0 && (uint64_t)n_steps <= ctl[kCtlTLen + par];
   const float* table = table_ok ? tables + par * noise_table_words(M) : nullptr;
-  if (wv >= run_wpb) return;
-  const int t = t0 + wv;
+  // waves [run_wpb, 2 run_wpb): the rotation helpers of waves [0, run_wpb)
+  // (on other SIMDs of the CU), with the table normals only
+  const bool help = helpers && table != nullptr;
+  const int slot = wv >= run_wpb ? wv - run_wpb : wv;
+  if (wv >= (help ? 2 * run_wpb : run_wpb)) return;
+  const int t = t0 + slot;
   if (t >= n_envs * sc.wmax) return;  // the last block's padding
   const int gw = (t % n_envs) * sc.wmax + t / n_envs;
+  if (wv >= run_wpb) {
+    rot_helper<kMulti>(d, st, sc, n_envs, n_steps, table, gw, lane, helper_lds(dyn_lds, slot), par);
+    return;
+  }
+  const HelperLds hl = helper_lds(dyn_lds, slot);
   // latency-bound launches last as long as their slowest wave: one with
   // 65-128 pairs (a cluster denser than two pairs per particle) runs its own
   // unrolled two-pass sub-step instead of the general pass loop
   run_wave_dispatch<kMulti, kWalls, true>(d, st, sc, n_envs, n_steps, step0, table, gw, lane,
-                                          lacc[wv][0], lacc[wv][1], pt, par);
+                                          lacc[wv][0], lacc[wv][1], pt, par, help, hl);
   stamp_end(tstamp);
 }
 

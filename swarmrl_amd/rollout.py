@@ -176,7 +176,11 @@ def gather_trajectory(trajectory, group=None, stats: Optional[dict] = None,
     off = 0
     for name, sz in zip(_NAMES, sizes):
         src = padded[name]
-        chunk = per_rank[:, off:off + sz].contiguous().view(src.dtype)
+        # a fresh copy: .contiguous() keeps a one-rank slice as a view with
+        # the packed row's stride, which cannot be reinterpreted as src.dtype
+        # (found by the world-1 RCCL test, tests/test_gpu_rccl.py)
+        chunk = per_rank[:, off:off + sz].clone(memory_format=torch.contiguous_format)
+        chunk = chunk.view(src.dtype)
         chunk = chunk.view(world, *src.shape)  # [world, T, Emax, ...]
         if all(c == emax for c in counts):
             result[name] = chunk.transpose(0, 1).reshape(src.shape[0], world * emax,

@@ -137,6 +137,30 @@ __global__ void k_probe(int test, float fa, float fb, unsigned long long* out, f
   sink[lane] = x + y + z + w + (float)dx + (float)ix;
 }
 
+// Shorter correctly rounded reciprocals for the pair force's 1/r^2: every
+// float in [2^-96, 2^96] against 1.0f / x.  variant 0: rcp + one residual
+// correction (3 dependent ops); 1: rcp + Newton step + correction (5).
+__global__ void k_rcp_variants(int variant, unsigned long long* bad, unsigned* first) {
+  const uint32_t lo = 31u << 23, hi = 223u << 23;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  unsigned long long nb = 0;
+  for (uint32_t b = lo + blockIdx.x * blockDim.x + threadIdx.x; b < hi; b += stride) {
+    const float x = __uint_as_float(b);
+    float y = __builtin_amdgcn_rcpf(x);
+    if (variant == 1) {
+      const float e = __builtin_fmaf(-x, y, 1.0f);
+      y = __builtin_fmaf(e, y, y);
+    }
+    const float r = __builtin_fmaf(-x, y, 1.0f);
+    const float res = __builtin_fmaf(r, y, y);
+    if (__float_as_uint(res) != __float_as_uint(1.0f / x)) {
+      ++nb;
+      atomicCAS(first, 0u, b);
+    }
+  }
+  if (nb) atomicAdd(bad, nb);
+}
+
 int main() {
   const char* names[] = {"v_fma_f32 dependent",   "v_fma_f32 4 chains",   "v_rcp_f32 dependent",
                          "ds_bpermute dependent", "4 ds_add_u64 + read",  "ballot vote + branch",
@@ -163,6 +187,19 @@ int main() {
     if (rep == 2)
       for (int t = 0; t < ntest; ++t)
         printf("%-32s %7.1f cycles/op\n", names[t], (double)h[t] / kIters);
+  }
+  for (int v = 0; v < 2; ++v) {
+    unsigned long long* d;
+    hipMalloc(&d, 16);
+    hipMemset(d, 0, 16);
+    hipLaunchKernelGGL(k_rcp_variants, dim3(8192), dim3(256), 0, 0, v, d,
+                       reinterpret_cast<unsigned*>(d + 1));
+    hipDeviceSynchronize();
+    unsigned long long h[2];
+    hipMemcpy(h, d, 16, hipMemcpyDeviceToHost);
+    printf("rcp variant %d: %llu mismatches over [2^-96, 2^96] (first 0x%08x)\n", v, h[0],
+           (unsigned)h[1]);
+    hipFree(d);
   }
   return 0;
 }
