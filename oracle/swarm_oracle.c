@@ -395,23 +395,44 @@ static float pair_disp(const swarm_params_t *p, const derived_t *d,
   return (float)dq * d->sx[a];
 }
 
-/* WCA force on i from j accumulated in 2^-24 fixed point */
+/* a 2^24-scaled force value to int64 fixed point (round to nearest even,
+ * clamped to +-2^62) */
+static int64_t fix_scaled(float v) {
+  v = fminf(fmaxf(v, -4.611686018427387904e18f), 4.611686018427387904e18f);
+  return (int64_t)llrintf(v);
+}
+
+/* WCA force on i from j accumulated in 2^-24 fixed point (2-D).  The
+ * engine's round-6 operation sequence (swarm_integrator.cuh:pair_vals, chosen
+ * for a short dependency chain on the GPU), the WCA law of
+ * espresso.py:802-832 (pinned by refsem.wca_force in fp64):
+ *   r2 = fma(rx, rx, ry ry); ir2 = 1 / r2
+ *   s6 = (ir2 ir2)(sig6 ir2); t = fma(s6, 2, -1)
+ *   v  = ((eps24 s6) t)(ir2 (-rx 2^24)) */
 static void wca_pair(const derived_t *d, int si, int sj, float rx, float ry,
                      int64_t *ax, int64_t *ay) {
-  float r2 = rx * rx + ry * ry;
+  float r2 = fmaf(rx, rx, ry * ry);
   if (r2 < d->cut2[si][sj] && r2 > 0.0f) {
     float ir2 = 1.0f / r2;
-    float ir6 = ir2 * ir2;
-    ir6 = ir6 * ir2;
-    float s6 = d->sig6[si][sj] * ir6;
-    float t = 2.0f * s6;
-    t = t - 1.0f;
-    float fr = d->eps24 * s6;
-    fr = fr * t;
-    fr = fr * ir2;
-    *ax += f2fix24(-fr * rx);
-    *ay += f2fix24(-fr * ry);
+    float s6 = (ir2 * ir2) * (d->sig6[si][sj] * ir2);
+    float t = fmaf(s6, 2.0f, -1.0f);
+    float fr = (d->eps24 * s6) * t;
+    *ax += fix_scaled(fr * (ir2 * (rx * -16777216.0f)));
+    *ay += fix_scaled(fr * (ir2 * (ry * -16777216.0f)));
   }
+}
+
+/* round to nearest even, then saturate to the int32 range (NaN -> 0): the
+ * GPU's v_rndne_f32 + v_cvt_i32_f32 (swarm_integrator.cuh:f2i32_sat) */
+static int32_t f2i32_sat(float v) {
+  float r = rintf(v);
+  if (r != r)
+    return 0;
+  if (r >= 2147483648.0f)
+    return INT32_MAX;
+  if (r <= -2147483648.0f)
+    return INT32_MIN;
+  return (int32_t)r;
 }
 
 /* WCA force of every wall on a particle of species sp at the folded
@@ -656,26 +677,24 @@ int or_bd_run_walls(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
       const float fs = first && f_swim0 ? f_swim0[i] : f_swim[i];
       const float tz = first && torque0 ? torque0[i] : torque_z[i];
       or_sincos_turn(first && ang0 ? ang0[i] : ang[i], &sn, &cs);
-      float fx = (float)acc[i] * 5.9604644775390625e-08f;
-      float fy = (float)acc[n + i] * 5.9604644775390625e-08f;
-      if (f_ext) {
-        fx = fx + f_ext[i];
-        fy = fy + f_ext[n + i];
-      }
-      fx = fx + fs * cs;
-      fy = fy + fs * sn;
-      float dx = fx * d.mob_dt[sp];
-      float dy = fy * d.mob_dt[sp];
+      /* translation in fixed-point units, the engine's round-6 sequence
+       * (swarm_integrator.cuh:bd_dq): f = fma(F, 2^-24, f_ext + f_swim d),
+       * dq = f2i32_sat(fma(f, mob_dt / sx, (sig_t / sx) g)) */
+      float g[3] = {0.0f, 0.0f, 0.0f};
       float dth = tz * d.rot_dt[sp];
       if (noisy) {
-        float g[3];
         or_step_normals(p->seed, env, (uint32_t)i, step, g);
-        dx = dx + d.sig_t[sp] * g[0];
-        dy = dy + d.sig_t[sp] * g[1];
         dth = dth + d.sig_r[sp] * g[2];
       }
-      advance(&q[i], &img[i], f2i32(dx * d.inv_sx[0]));
-      advance(&q[n + i], &img[n + i], f2i32(dy * d.inv_sx[1]));
+      const float c1x = (f_ext ? f_ext[i] : 0.0f) + fs * cs;
+      const float c1y = (f_ext ? f_ext[n + i] : 0.0f) + fs * sn;
+      float fx = fmaf((float)acc[i], 5.9604644775390625e-08f, c1x);
+      float fy = fmaf((float)acc[n + i], 5.9604644775390625e-08f, c1y);
+      const float mobx = d.mob_dt[sp] * d.inv_sx[0], moby = d.mob_dt[sp] * d.inv_sx[1];
+      const float sigx = noisy ? d.sig_t[sp] * d.inv_sx[0] : 0.0f;
+      const float sigy = noisy ? d.sig_t[sp] * d.inv_sx[1] : 0.0f;
+      advance(&q[i], &img[i], f2i32_sat(fmaf(fx, mobx, sigx * g[0])));
+      advance(&q[n + i], &img[n + i], f2i32_sat(fmaf(fy, moby, sigy * g[1])));
       ang[i] = ang[i] + (uint32_t)f2i32(dth * ANG_INV_SCALE);
       if (s == n_steps - 1) {
         float vx = fx * d.inv_gt[sp], vy = fy * d.inv_gt[sp];

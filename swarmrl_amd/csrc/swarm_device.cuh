@@ -281,6 +281,18 @@ __device__ __forceinline__ int32_t f2i32(float v) {
   return __float2int_rn(v);
 }
 
+// f2i32 for the 2-D translation (round 6): round to nearest even, then
+// v_cvt_i32_f32's saturation to the int32 range (NaN -> 0) instead of a
+// clamp before it -- one dependent operation fewer on the run kernels'
+// chain (oracle/swarm_oracle.c:f2i32_sat; tests/test_gpu_devmath.py checks
+// the edge values).  The conversion is written as the instruction itself:
+// the compiler's fptosi leaves out-of-range values undefined.
+__device__ __forceinline__ int32_t f2i32_sat(float v) {
+  int32_t r;
+  __asm__("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(__builtin_rintf(v)));
+  return r;
+}
+
 __device__ __forceinline__ int64_t f2fix24(float v) {
   v = v * 16777216.0f;
   // |v| < 2^31 (force below 128): one int32 conversion, same value

@@ -474,55 +474,49 @@ __device__ inline void block_exclusive_scan(int32_t* data, int n, int32_t* wave_
   if (tid == T - 1) data[n] = wave_sums[nw - 1];
 }
 
-// WCA force on i from j (r = x_j - x_i), accumulated in 2^-24 fixed point.
+// WCA pair force of the 2-D paths (round 6 operation sequence, restated in
+// oracle/swarm_oracle.c:wca_pair): the force on the first particle scaled
+// by 2^24 (fp32), zero out of range.  The sequence is chosen for a short
+// dependency chain in the run kernels (a dependent VALU operation of a lone
+// wave costs ~11 cycles):
+//   r2 = fma(rx, rx, ry ry); ir2 = 1 / r2 (rcp_rn)
+//   s6 = (ir2 ir2) (sig6 ir2); t = fma(s6, 2, -1)
+//   v  = ((eps24 s6) t) (ir2 (-rx 2^24))
+// No select before the reciprocal: an out-of-range lane's value is
+// discarded by the final select (in range r2 >= 2^-96, rcp_rn's range).
 // cut2 = (r_i + r_j)^2, sig6 = sigma^6, eps24 = 24 epsilon (Derived tables).
-__device__ __forceinline__ void pair_force(float cut2, float sig6, float eps24, float rx,
-                                           float ry, int64_t& ax, int64_t& ay) {
-  const float r2 = rx * rx + ry * ry;
-  if (r2 < cut2 && r2 > 0.0f) {
-    const float ir2 = 1.0f / r2;
-    float ir6 = ir2 * ir2;
-    ir6 = ir6 * ir2;
-    const float s6 = sig6 * ir6;
-    float t = 2.0f * s6;
-    t = t - 1.0f;
-    float fr = eps24 * s6;
-    fr = fr * t;
-    fr = fr * ir2;
-    ax += f2fix24(-fr * rx);
-    ay += f2fix24(-fr * ry);
-  }
-}
-
-// Branch-free pair_force for the run kernel's pair passes: the force on the
-// first particle in 2^-24 fixed point, or zero out of range (r2 = 0 for an
-// empty slot that names one particle twice).  In-range values equal
-// pair_force's; the int32 conversion is taken when every lane fits.
-// pair_force's force on the first particle scaled by 2^24 (fp32), zero out
-// of range, with a short dependency chain and the same values:
-//  * no select before the reciprocal: an out-of-range lane's value is
-//    discarded by the final select (in range r2 >= 2^-96, rcp_rn's range);
-//  * 2 s6 - 1 as one fma (2 s6 is exact, so one rounding either way);
-//  * (-fr rx) 2^24 = fr (-rx 2^24): scaling by 2^24 commutes with the
-//    rounding (no overflow or subnormal here), and -rx 2^24 is ready before
-//    fr.
 __device__ __forceinline__ void pair_vals(float cut2, float sig6, float eps24, float rx, float ry,
                                           float& vx, float& vy) {
-  const float r2 = rx * rx + ry * ry;
+  const float r2 = __builtin_fmaf(rx, rx, ry * ry);
   const bool in = r2 < cut2 && r2 > 0.0f;
   const float ir2 = rcp_rn(r2);  // = 1.0f / r2 on every in-range lane
-  const float rxs = rx * -16777216.0f, rys = ry * -16777216.0f;
-  float ir6 = ir2 * ir2;
-  ir6 = ir6 * ir2;
-  const float s6 = sig6 * ir6;
+  const float s6 = (ir2 * ir2) * (sig6 * ir2);
   const float t = __builtin_fmaf(s6, 2.0f, -1.0f);
-  float fr = eps24 * s6;
-  fr = fr * t;
-  fr = fr * ir2;
-  vx = in ? fr * rxs : 0.0f;
-  vy = in ? fr * rys : 0.0f;
+  const float fr = (eps24 * s6) * t;
+  const float gx = ir2 * (rx * -16777216.0f), gy = ir2 * (ry * -16777216.0f);
+  vx = in ? fr * gx : 0.0f;
+  vy = in ? fr * gy : 0.0f;
 }
 
+// a 2^24-scaled force value to int64 fixed point: round to nearest even,
+// clamped to +-2^62 (one int32 conversion below 2^31, the same value)
+__device__ __forceinline__ int64_t fix_scaled(float v) {
+  if (__builtin_expect(fabsf(v) < 2147483520.0f, 1)) return (int64_t)__float2int_rn(v);
+  return __float2ll_rn(fminf(fmaxf(v, -4.611686018427387904e18f), 4.611686018427387904e18f));
+}
+
+// WCA force on i from j (r = x_j - x_i), accumulated in 2^-24 fixed point.
+__device__ __forceinline__ void pair_force(float cut2, float sig6, float eps24, float rx,
+                                           float ry, int64_t& ax, int64_t& ay) {
+  float vx, vy;
+  pair_vals(cut2, sig6, eps24, rx, ry, vx, vy);
+  ax += fix_scaled(vx);
+  ay += fix_scaled(vy);
+}
+
+// pair_force's fixed-point values for the run kernel's pair passes (every
+// lane: zero out of range, and for an empty slot that names one particle
+// twice); the int32 conversion is taken when every lane fits.
 __device__ __forceinline__ void pair_fix_sel(float cut2, float sig6, float eps24, float rx,
                                              float ry, int64_t& fx, int64_t& fy) {
   float vx, vy;
@@ -600,6 +594,9 @@ struct PState {
 struct PConst {
   float mob_dt, sig_t, rot_dt, sig_r, inv_gt, inv_gr, sig_v, sig_w;
   float inv_sx0, inv_sx1;
+  // the translation in fixed-point units per axis (2-D, round 6):
+  // mob_dt / sx and sig_t / sx (0 without noise) as fp32 products
+  float mobx, moby, sigx, sigy;
   bool noisy;
 };
 
@@ -616,6 +613,10 @@ __device__ __forceinline__ PConst load_pconst(const Derived* __restrict__ d, int
   c.inv_sx0 = d->inv_sx[0];
   c.inv_sx1 = d->inv_sx[1];
   c.noisy = d->noisy != 0;
+  c.mobx = c.mob_dt * c.inv_sx0;
+  c.moby = c.mob_dt * c.inv_sx1;
+  c.sigx = c.noisy ? c.sig_t * c.inv_sx0 : 0.0f;
+  c.sigy = c.noisy ? c.sig_t * c.inv_sx1 : 0.0f;
   return c;
 }
 
@@ -633,6 +634,22 @@ __device__ __forceinline__ void stage_pair_tables(const Derived* __restrict__ d,
   __syncthreads();
 }
 
+// The translation of one BD sub-step in fixed-point units (2-D, round 6
+// sequence; oracle/swarm_oracle.c:or_bd_run_walls): from the WCA sum F
+// (fp32, 2^24 units),
+//   f  = fma(F, 2^-24, f_ext + f_swim d)      (the force, d the director)
+//   dq = f2i32_sat(fma(f, mob_dt / sx, (sig_t / sx) g))
+// (F 2^-24 is exact; the per-axis constants are PConst's fp32 products).
+__device__ __forceinline__ void bd_dq(const PConst& c, float Fx, float Fy, float fs, float fex,
+                                      float fey, float sn, float cs, const float* g, float* fx,
+                                      float* fy, int32_t* dqx, int32_t* dqy) {
+  const float c1x = fex + fs * cs, c1y = fey + fs * sn;
+  *fx = __builtin_fmaf(Fx, 5.9604644775390625e-08f, c1x);
+  *fy = __builtin_fmaf(Fy, 5.9604644775390625e-08f, c1y);
+  *dqx = f2i32_sat(__builtin_fmaf(*fx, c.mobx, c.sigx * g[0]));
+  *dqy = f2i32_sat(__builtin_fmaf(*fy, c.moby, c.sigy * g[1]));
+}
+
 // One Brownian-dynamics sub-step of one particle from its summed WCA force.
 // an_swim: the orientation the swim force points along (p.an, or with
 // reuse_forces at sub-step 0 the previous run's last one).
@@ -646,17 +663,9 @@ __device__ __forceinline__ void bd_step(const PConst& c, PState& p, int64_t ax, 
                                         bool fresh = true) {
   float sn, cs;
   sincos_turn(an_swim, &sn, &cs);
-  float fx = i64_to_f32(ax) * 5.9604644775390625e-08f;
-  float fy = i64_to_f32(ay) * 5.9604644775390625e-08f;
-  fx = fx + fex;
-  fy = fy + fey;
-  fx = fx + fs * cs;
-  fy = fy + fs * sn;
-  float dx = fx * c.mob_dt;
-  float dy = fy * c.mob_dt;
+  float g[3] = {0.0f, 0.0f, 0.0f};
   float dth = tz * c.rot_dt;
   if (c.noisy) {
-    float g[3];
     if (kTable) {
       g[0] = gt[0];
       g[1] = gt[1];
@@ -666,12 +675,13 @@ __device__ __forceinline__ void bd_step(const PConst& c, PState& p, int64_t ax, 
     } else {
       step_normals(k0, k1, id, step, g);
     }
-    dx = dx + c.sig_t * g[0];
-    dy = dy + c.sig_t * g[1];
     dth = dth + c.sig_r * g[2];
   }
-  advance(p.qx, p.ix, f2i32(dx * c.inv_sx0));
-  advance(p.qy, p.iy, f2i32(dy * c.inv_sx1));
+  float fx, fy;
+  int32_t dqx, dqy;
+  bd_dq(c, i64_to_f32(ax), i64_to_f32(ay), fs, fex, fey, sn, cs, g, &fx, &fy, &dqx, &dqy);
+  advance(p.qx, p.ix, dqx);
+  advance(p.qy, p.iy, dqy);
   p.an = p.an + (uint32_t)f2i32(dth * kAngInvScale);
   if (last) {
     float v0 = fx * c.inv_gt, v1 = fy * c.inv_gt;
@@ -689,14 +699,9 @@ __device__ __forceinline__ void bd_step(const PConst& c, PState& p, int64_t ax, 
   }
 }
 
-// bd_step without the rotation, for the cluster run (which updates the
-// angle, and the next sub-step's director, while the force sums are in
-// flight): same operation sequence for the translation and velocities.
-// from the force sums already converted to fp32 (2^24 fixed-point units):
-// F 2^-24 + f_ext as one fma (F 2^-24 is exact, so the same single rounding)
-// kNoiseAlways: the translation noise is added unconditionally; the caller
-// passes sig_t = 0 for a noiseless engine (dx + 0 g rounds to the same
-// integer displacement as dx, g being finite), so no select sits on the chain.
+// bd_step without the rotation, for the cluster run (which turns the
+// director apart from the force chain): the same translation (bd_dq) and
+// velocities, from the force sums already converted to fp32 (2^24 units).
 // Carry: with a Carry record the image counters are left to the caller
 // (apply_carry, off the next sub-step's chain); q is updated here.
 struct Carry {
@@ -707,24 +712,17 @@ __device__ __forceinline__ void apply_carry(PState& p, const Carry& c) {
   p.ix += (int32_t)(((int64_t)(uint64_t)c.qx0 + (int64_t)c.dqx) >> 32);
   p.iy += (int32_t)(((int64_t)(uint64_t)c.qy0 + (int64_t)c.dqy) >> 32);
 }
-template <bool kNoiseAlways = false>
 __device__ __forceinline__ void bd_translate_f(const PConst& c, PState& p, float fx, float fy,
                                                float fs, float tz, float fex, float fey,
                                                uint32_t k0, uint32_t k1, uint32_t id,
                                                uint64_t step, bool last, float* vx, float* vy,
                                                float* w, const float* g, float sn, float cs,
                                                Carry* carry = nullptr) {
-  fx = __builtin_fmaf(fx, 5.9604644775390625e-08f, fex);
-  fy = __builtin_fmaf(fy, 5.9604644775390625e-08f, fey);
-  fx = fx + fs * cs;
-  fy = fy + fs * sn;
-  float dx = fx * c.mob_dt;
-  float dy = fy * c.mob_dt;
-  if (kNoiseAlways || c.noisy) {
-    dx = dx + c.sig_t * g[0];
-    dy = dy + c.sig_t * g[1];
-  }
-  const int32_t dqx = f2i32(dx * c.inv_sx0), dqy = f2i32(dy * c.inv_sx1);
+  const float F[2] = {fx, fy};
+  int32_t dqx, dqy;
+  // (without noise sigx = sigy = 0: g is finite, so sig g = +-0 changes no
+  // displacement)
+  bd_dq(c, F[0], F[1], fs, fex, fey, sn, cs, g, &fx, &fy, &dqx, &dqy);
   if (carry) {
     *carry = Carry{p.qx, p.qy, dqx, dqy};
     p.qx += (uint32_t)dqx;
@@ -3302,8 +3300,6 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
   // the helper has not published yet (helper_director_at)
   const uint32_t an_start = p.an;
   const float tz0 = tz, tzc = (kHelper && active) ? st.torque_z[gi] : 0.0f;
-  PConst pcn = pc;  // sig_t = 0 without noise (bd_translate_f<true>)
-  if (!pc.noisy) pcn.sig_t = 0.0f;
   Carry carry = {0u, 0u, 0, 0};  // the previous sub-step's image carries, pending
   const float cut2_0 = d->cut2[0], sig6_0 = d->sig6[0];
   const uint32_t q0x = p.qx, q0y = p.qy;
@@ -3533,7 +3529,7 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
       // (the last sub-step applies its own)
       const PState p0 = p;
       const bool fits = wave_all2(fits_i32(ax), fits_i32(ay));
-      bd_translate_f<true>(pcn, p, (float)(int32_t)ax, (float)(int32_t)ay, fs, tz, fex, fey, k0,
+      bd_translate_f(pc, p, (float)(int32_t)ax, (float)(int32_t)ay, fs, tz, fex, fey, k0,
                            k1, (uint32_t)i, step0 + (uint64_t)s, kLast, &vx, &vy, &om, gt, dir[0],
                            dir[1], kLast ? nullptr : &carry);
       // computed before the vote's branch (else the compiler moves the
@@ -3541,7 +3537,7 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
       __asm__ volatile("" : "+v"(p.qx), "+v"(p.qy));
       if (__builtin_expect(!fits, 0)) {
         p = p0;
-        bd_translate_f<true>(pcn, p, i64_to_f32_wide(ax), i64_to_f32_wide(ay), fs, tz, fex, fey,
+        bd_translate_f(pc, p, i64_to_f32_wide(ax), i64_to_f32_wide(ay), fs, tz, fex, fey,
                              k0, k1, (uint32_t)i, step0 + (uint64_t)s, kLast, &vx, &vy, &om, gt,
                              dir[0], dir[1], kLast ? nullptr : &carry);
       }

@@ -111,3 +111,22 @@ extern "C" int devmath_i64_to_f32(const int64_t* v, int n, float* out) {
   (void)hipFree(dout);
   return 0;
 }
+
+// f2i32_sat (the 2-D translation's conversion) on host-supplied values
+__global__ void k_f2i32_sat(const float* v, int n, int32_t* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = swarm::f2i32_sat(v[i]);
+}
+
+extern "C" int devmath_f2i32_sat(const float* v, int n, int32_t* out) {
+  float* dv;
+  int32_t* dout;
+  if (hipMalloc(&dv, n * 4) || hipMalloc(&dout, n * 4)) return 1;
+  (void)hipMemcpy(dv, v, n * 4, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(k_f2i32_sat, dim3((n + 255) / 256), dim3(256), 0, 0, dv, n, dout);
+  if (hipDeviceSynchronize() != hipSuccess) return 2;
+  (void)hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost);
+  (void)hipFree(dv);
+  (void)hipFree(dout);
+  return 0;
+}

@@ -113,3 +113,30 @@ def test_i64_to_f32_paths():
         assert np.array_equal(out[0::3], ref)
         assert np.array_equal(out[1::3], np.roll(ref, -1))
         assert np.array_equal(out[2::3], ref)
+
+
+def test_f2i32_sat_rounds_and_saturates():
+    """f2i32_sat (the 2-D translation's fp32 -> int32, round 6) rounds to
+    nearest even and saturates to the int32 range, NaN -> 0: the oracle's
+    f2i32_sat (oracle/swarm_oracle.c) on halves, the range edges and
+    beyond, infinities and NaN."""
+    lib_path = ROOT / "tests" / "csrc" / "libdevmath.so"
+    import torch  # noqa: F401  (HIP runtime first)
+
+    lib = ctypes.CDLL(str(lib_path))
+    rng = np.random.default_rng(5)
+    v = np.concatenate([
+        np.array([0.5, 1.5, 2.5, -0.5, -1.5, -2.5, 0.0, -0.0, 2147483520.0, 2147483648.0,
+                  -2147483648.0, -2147483904.0, 3.0e9, -3.0e9, 1e30, -1e30, np.inf, -np.inf,
+                  np.nan], np.float32),
+        (rng.standard_normal(1 << 16) * 10.0 ** rng.uniform(-3, 10, 1 << 16)).astype(np.float32),
+    ])
+    v = np.ascontiguousarray(v)
+    out = np.zeros(len(v), np.int32)
+    rc = lib.devmath_f2i32_sat(v.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(len(v)),
+                               out.ctypes.data_as(ctypes.c_void_p))
+    assert rc == 0
+    r = np.rint(v.astype(np.float64))
+    want = np.where(np.isnan(r), 0, np.clip(np.nan_to_num(r, posinf=2**31, neginf=-2**31),
+                                            -2**31, 2**31 - 1)).astype(np.int64)
+    assert np.array_equal(out.astype(np.int64), want)
