@@ -44,19 +44,20 @@ LINES = ("head", "batched", "c2", "c4", "c5", "c3train", "dims3", "dense2d")
 
 
 def source_sha() -> str:
-    """Hash of the HIP sources and the C-ABI header the library is built from:
-    profiles/<tag>_traffic.json rows carry it, so a kernel change is not
-    reported with stale counter numbers."""
-    import glob
+    """Hash of the HIP sources and the C-ABI header the library is built from
+    (swarmrl_amd._capi.source_hash, compiled into the library as
+    swarm_build_id): profiles/<tag>_traffic.json rows carry it, so a kernel
+    change is not reported with stale counter numbers."""
     import hashlib
+    import pathlib
 
+    root = pathlib.Path(ROOT)
     h = hashlib.sha256()
-    files = sorted(glob.glob(os.path.join(ROOT, "swarmrl_amd", "csrc", "*")) +
-                   glob.glob(os.path.join(ROOT, "include", "*.h")))
+    files = sorted([*(root / "swarmrl_amd" / "csrc").glob("*"), *(root / "include").glob("*.h")],
+                   key=os.fspath)
     for path in files:
-        h.update(os.path.basename(path).encode())
-        with open(path, "rb") as f:
-            h.update(f.read())
+        h.update(path.name.encode())
+        h.update(path.read_bytes())
     return h.hexdigest()[:12]
 
 

@@ -133,6 +133,12 @@ typedef struct swarm_engine swarm_engine_t;
 /* Thread-local message of the last failing call. */
 const char *swarm_last_error(void);
 
+/* Build provenance (no reference counterpart): the 12-hex-digit hash of the
+ * HIP sources and this header the library was compiled from
+ * (__graft_entry__.build, swarmrl_amd._capi.source_hash); swarmrl_amd._capi
+ * warns when it differs from the checkout it runs in. */
+const char *swarm_build_id(void);
+
 /* Engine construction: replaces espressomd.System(...) + _init_system +
  * part.add for all particles (espresso.py:192-196, 236-288, 415-441).
  * `species` is [n_particles]: index into the per-species arrays of params. */

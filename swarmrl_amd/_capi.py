@@ -117,6 +117,7 @@ class SwarmAdam(ctypes.Structure):
 _P = ctypes.c_void_p
 _SIGNATURES = {
     "swarm_last_error": (ctypes.c_char_p, []),
+    "swarm_build_id": (ctypes.c_char_p, []),
     "swarm_engine_create": (
         ctypes.c_int,
         [ctypes.POINTER(SwarmParams), ctypes.c_int32, ctypes.c_int32, _P, ctypes.POINTER(_P)],
@@ -248,8 +249,30 @@ def library_path() -> pathlib.Path:
     return _LIB_PATH
 
 
+def source_hash(root: pathlib.Path = None) -> str:
+    """12-hex-digit hash of the HIP sources (swarmrl_amd/csrc/*) and the
+    C-ABI header the library is built from: compiled into the library
+    (swarm_build_id) and carried by the profiles' rows (bench.py)."""
+    import hashlib
+
+    root = pathlib.Path(root) if root is not None else pathlib.Path(__file__).resolve().parents[1]
+    h = hashlib.sha256()
+    files = sorted([*(root / "swarmrl_amd" / "csrc").glob("*"), *(root / "include").glob("*.h")],
+                   key=os.fspath)
+    for path in files:
+        h.update(path.name.encode())
+        h.update(path.read_bytes())
+    return h.hexdigest()[:12]
+
+
+def build_id() -> str:
+    """The source hash the loaded library was compiled from."""
+    return lib().swarm_build_id().decode()
+
+
 def lib() -> ctypes.CDLL:
-    """Load the HIP engine library (raises if it was not built)."""
+    """Load the HIP engine library (raises if it was not built).  Warns when
+    the library was built from other sources than the checkout's."""
     global _lib
     if _lib is not None:
         return _lib
@@ -264,6 +287,15 @@ def lib() -> ctypes.CDLL:
         fn.restype = res
         fn.argtypes = args
     _lib = handle
+    try:
+        built, here = handle.swarm_build_id().decode(), source_hash()
+    except OSError:  # sources not shipped beside the library
+        built, here = None, None
+    if built is not None and built != here:
+        import warnings
+
+        warnings.warn(f"{_LIB_PATH} was built from sources {built}, the checkout has {here}: "
+                      "rebuild (__graft_entry__.build())", RuntimeWarning, stacklevel=2)
     return _lib
 
 

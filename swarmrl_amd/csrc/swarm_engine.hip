@@ -1879,6 +1879,11 @@ extern "C" {
 
 const char* swarm_last_error(void) { return g_err.c_str(); }
 
+#ifndef SWARM_BUILD_ID
+#define SWARM_BUILD_ID "unknown"
+#endif
+const char* swarm_build_id(void) { return SWARM_BUILD_ID; }
+
 int swarm_engine_create(const swarm_params_t* params, int32_t n_envs, int32_t n_particles,
                         const int32_t* species, swarm_engine_t** out) {
   if (!params || !out) return fail(SWARM_EINVAL, "null argument");

@@ -3236,6 +3236,10 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
                                          unsigned long long* lacc_x, unsigned long long* lacc_y,
                                          const PairTables& pt, int par,
                                          HelperLds hl = HelperLds{}) {
+  // the sub-step schedule for latency-bound waves (the wide kernel, which
+  // also takes the two-pass variant); the throughput kernel, bound by VALU
+  // issue over many waves, keeps the plain one (fewer registers, no spill)
+  constexpr int kSched = kTwoPass ? SWARM_RUN_SCHED : 0;
   const int e = gw / sc.wmax;
   const int w = gw - e * sc.wmax;
   if (e >= n_envs) return;
@@ -3362,7 +3366,7 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     };
     // the previous sub-step's displacement (max is order-free)
     auto prev_disp = [&]() __attribute__((always_inline)) {
-      if (SWARM_RUN_SCHED && s > 0) {
+      if (kSched && s > 0) {
         const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
         const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
         dmax2 = __uint_as_float(max(__float_as_uint(dmax2), __float_as_uint(ddx * ddx + ddy * ddy)));
@@ -3384,18 +3388,18 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
         return;
       }
       if (!kLast) sincos_turn(an_next, &dnext[0], &dnext[1]);
-      if (SWARM_RUN_SCHED) __asm__ volatile("" : "+v"(dnext[0]), "+v"(dnext[1]));
+      if (kSched) __asm__ volatile("" : "+v"(dnext[0]), "+v"(dnext[1]));
     };
-    if (kPass == 0 || SWARM_RUN_SCHED < 2) {
-      if (SWARM_RUN_SCHED) prev_disp();
+    if (kPass == 0 || kSched < 2) {
+      if (kSched) prev_disp();
     }
     // one-pass waves convert speculatively (see below); sa, sb, sv_*: the
     // lane's pair for the rare fix-up
-    constexpr bool kSpec = SWARM_RUN_SCHED >= 3 && kPass == 1;
+    constexpr bool kSpec = kSched >= 3 && (kPass == 1 || kPass == 2);
     // speculative read-back conversion, image carries deferred (any pass count)
-    constexpr bool kDefer = SWARM_RUN_SCHED >= 3 && kPass > 0 && !kWalls;
-    float sv_x = 0.0f, sv_y = 0.0f;
-    int sa = lane, sb = lane;
+    constexpr bool kDefer = kSched >= 3 && kPass > 0 && !kWalls;
+    float sv_x[2] = {0.0f, 0.0f}, sv_y[2] = {0.0f, 0.0f};
+    int sa[2] = {lane, lane}, sb[2] = {lane, lane};
     bool spec_ok = true;
     if (kPass > 0) {
       for (int q = 0; q < (kPass == 1 ? 1 : (kPass == 2 ? 2 : npass)); ++q) {
@@ -3413,12 +3417,14 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
                                       (uint32_t)__builtin_amdgcn_ds_bpermute(a << 2, (int)p.qy));
           const uint2 pb = make_uint2((uint32_t)__builtin_amdgcn_ds_bpermute(b << 2, (int)p.qx),
                                       (uint32_t)__builtin_amdgcn_ds_bpermute(b << 2, (int)p.qy));
-          if (SWARM_RUN_SCHED >= 2 && q == 0) {
+          if (kSched >= 2 && q == 0) {
             // the exchange's latency window: rotation and displacement
             __builtin_amdgcn_sched_barrier(0);
             rotate();
-            prev_disp();
-            if (kDefer) apply_carry(p, carry);
+            if (!kHelper) {  // (helper mode: in the force round trip's window)
+              prev_disp();
+              if (kDefer) apply_carry(p, carry);
+            }
             // pinned here (the compiler would sink them behind the vote branch)
             __asm__ volatile("" : "+v"(an_next), "+v"(dmax2), "+v"(p.ix), "+v"(p.iy));
             __builtin_amdgcn_sched_barrier(0);
@@ -3430,17 +3436,19 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
             // speculative int32 conversion: the atomics do not wait for the
             // wave vote; a wave whose vote fails adds the exact remainder
             // after them (spec_fix below), so the sums are the same integers
+            const int qq = q & 1;  // (kSpec: q < 2, unrolled)
             if (kMulti) {
               const int sp = (int)((e_ >> 12) & 255u);
-              pair_vals(pt.cut2[sp], pt.sig6[sp], eps24, rx, ry, sv_x, sv_y);
+              pair_vals(pt.cut2[sp], pt.sig6[sp], eps24, rx, ry, sv_x[qq], sv_y[qq]);
             } else {
-              pair_vals(cut2_0, sig6_0, eps24, rx, ry, sv_x, sv_y);
+              pair_vals(cut2_0, sig6_0, eps24, rx, ry, sv_x[qq], sv_y[qq]);
             }
-            spec_ok = wave_all2(fabsf(sv_x) < 2147483520.0f, fabsf(sv_y) < 2147483520.0f);
-            fx = (int64_t)__float2int_rn(sv_x);
-            fy = (int64_t)__float2int_rn(sv_y);
-            sa = a;
-            sb = b;
+            spec_ok = spec_ok && wave_all2(fabsf(sv_x[qq]) < 2147483520.0f,
+                                           fabsf(sv_y[qq]) < 2147483520.0f);
+            fx = (int64_t)__float2int_rn(sv_x[qq]);
+            fy = (int64_t)__float2int_rn(sv_y[qq]);
+            sa[qq] = a;
+            sb[qq] = b;
           } else if (kMulti) {
             const int sp = (int)((e_ >> 12) & 255u);
             pair_fix_sel(pt.cut2[sp], pt.sig6[sp], eps24, rx, ry, fx, fy);
@@ -3456,7 +3464,7 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
         }
       }
     }
-    if (SWARM_RUN_SCHED >= 2 && kPass > 0) {
+    if (kSched >= 2 && kPass > 0) {
       // the read-back issued right behind the atomics (a wave's DS operations
       // execute in order), the director computed in its latency window
       wave_lds_sync();
@@ -3472,12 +3480,15 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
           return __float2ll_rn(
               fminf(fmaxf(v, -4.611686018427387904e18f), 4.611686018427387904e18f));
         };
-        const int64_t rx_ = wide(sv_x) - (int64_t)__float2int_rn(sv_x);
-        const int64_t ry_ = wide(sv_y) - (int64_t)__float2int_rn(sv_y);
-        atomicAdd(&lacc_x[sa], (unsigned long long)rx_);
-        atomicAdd(&lacc_y[sa], (unsigned long long)ry_);
-        atomicSub(&lacc_x[sb], (unsigned long long)rx_);
-        atomicSub(&lacc_y[sb], (unsigned long long)ry_);
+#pragma unroll
+        for (int qq = 0; qq < kPass; ++qq) {
+          const int64_t rx_ = wide(sv_x[qq]) - (int64_t)__float2int_rn(sv_x[qq]);
+          const int64_t ry_ = wide(sv_y[qq]) - (int64_t)__float2int_rn(sv_y[qq]);
+          atomicAdd(&lacc_x[sa[qq]], (unsigned long long)rx_);
+          atomicAdd(&lacc_y[sa[qq]], (unsigned long long)ry_);
+          atomicSub(&lacc_x[sb[qq]], (unsigned long long)rx_);
+          atomicSub(&lacc_y[sb[qq]], (unsigned long long)ry_);
+        }
         wave_lds_sync();
         ax += (int64_t)lacc_x[lane];
         ay += (int64_t)lacc_y[lane];
@@ -3486,6 +3497,13 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
       }
       __builtin_amdgcn_sched_barrier(0);
       director();
+      if (kHelper) {
+        // the round trip's latency window holds no rotation in helper mode:
+        // the previous sub-step's displacement and image carries go here
+        prev_disp();
+        if (kDefer) apply_carry(p, carry);
+        __asm__ volatile("" : "+v"(dmax2), "+v"(p.ix), "+v"(p.iy));
+      }
       __builtin_amdgcn_sched_barrier(0);
     } else {
       // rotation (bd_step's sequence) and the next director, between the
@@ -3545,7 +3563,7 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
       bd_translate(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
                    kLast, &vx, &vy, &om, gt, dir[0], dir[1]);
     }
-    if (!SWARM_RUN_SCHED || kLast) {  // (else the next sub-step's prev_disp)
+    if (!kSched || kLast) {  // (else the next sub-step's prev_disp)
       const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
       const float ddy = (float)(int32_t)(p.qy - q0y) * sx1;
       // non-negative floats order like their bit patterns: one v_max_u32

@@ -94,3 +94,17 @@ def test_lib_env_selects_the_library(tmp_path):
     out = subprocess.run([sys.executable, "-c", code], env=env, cwd=str(ROOT),
                          capture_output=True, text=True, check=True).stdout
     assert out == str(alt)
+
+
+def test_library_build_id_matches_the_sources():
+    """swarm_build_id: the library was compiled from the checkout's HIP
+    sources and header (the hash __graft_entry__.build compiles in)."""
+    import __graft_entry__ as g
+
+    if not g.HIP_LIB.exists():
+        g.build()
+    lib = ctypes.CDLL(str(g.HIP_LIB))
+    lib.swarm_build_id.restype = ctypes.c_char_p
+    from swarmrl_amd import _capi
+
+    assert lib.swarm_build_id().decode() == _capi.source_hash() == g._source_hash()

@@ -7,12 +7,13 @@
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p tools/_variants
+bid=$(python3 -c "import __graft_entry__ as g; print(g._source_hash())")
 pids=()
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off \
     -fno-slp-vectorize \
-    $flags swarmrl_amd/csrc/swarm_engine.hip -o tools/_variants/lib_${name}.so &
+    -DSWARM_BUILD_ID=\"$bid\" $flags swarmrl_amd/csrc/swarm_engine.hip -o tools/_variants/lib_${name}.so &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p; done
