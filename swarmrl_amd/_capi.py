@@ -283,13 +283,15 @@ def lib() -> ctypes.CDLL:
         )
     handle = ctypes.CDLL(os.fspath(_LIB_PATH), mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in _SIGNATURES.items():
+        if name == "swarm_build_id" and not hasattr(handle, name):
+            continue  # a library from before round 6 (A/B variants): no provenance
         fn = getattr(handle, name)
         fn.restype = res
         fn.argtypes = args
     _lib = handle
     try:
         built, here = handle.swarm_build_id().decode(), source_hash()
-    except OSError:  # sources not shipped beside the library
+    except (OSError, AttributeError):  # no sources beside the library / an old library
         built, here = None, None
     if built is not None and built != here:
         import warnings

@@ -42,6 +42,12 @@
 #ifndef SWARM_RUN_SCHED
 #define SWARM_RUN_SCHED 3
 #endif
+// helper mode: the displacement and carries in the exchange window (0,
+// measured faster: head 62.4 / 61.8 vs 60.0 / 60.5 M with them in the force
+// round trip's window, same box) or in the round trip's window (1)
+#ifndef SWARM_HELPER_WIN2
+#define SWARM_HELPER_WIN2 0
+#endif
 
 namespace swarm {
 
@@ -3421,7 +3427,7 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
             // the exchange's latency window: rotation and displacement
             __builtin_amdgcn_sched_barrier(0);
             rotate();
-            if (!kHelper) {  // (helper mode: in the force round trip's window)
+            if (!kHelper || !SWARM_HELPER_WIN2) {  // (helper: the round trip's window)
               prev_disp();
               if (kDefer) apply_carry(p, carry);
             }
@@ -3497,7 +3503,7 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
       }
       __builtin_amdgcn_sched_barrier(0);
       director();
-      if (kHelper) {
+      if (kHelper && SWARM_HELPER_WIN2) {
         // the round trip's latency window holds no rotation in helper mode:
         // the previous sub-step's displacement and image carries go here
         prev_disp();
