@@ -102,6 +102,8 @@ def lib():
         L.or_sincos_turn.argtypes = [ctypes.c_uint32, _P, _P]
         L.or_signed_angle.restype = ctypes.c_float
         L.or_signed_angle.argtypes = [_P, _P]
+        L.or_normal_from_word.restype = ctypes.c_float
+        L.or_normal_from_word.argtypes = [ctypes.c_uint32]
         L.or_normals3.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_uint64, ctypes.c_uint32, _P]
         L.or_step_normals.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
@@ -441,6 +443,11 @@ def step_normals(seed, env, pid, t):
     out = np.zeros(3, np.float32)
     lib().or_step_normals(int(seed), int(env), int(pid), int(t), _ptr(out))
     return out
+
+
+def normal_from_word(r):
+    """The standard normal of one 32-bit Philox word (or_normal_from_word)."""
+    return lib().or_normal_from_word(int(r) & 0xFFFFFFFF)
 
 
 def normals3(seed, env, pid, step, tag):

@@ -46,6 +46,7 @@
 #include <string.h>
 
 #include "../include/swarmrl_amd.h"
+#include "../include/swarm_normal_table.h"
 
 #ifdef _OPENMP
 #include <omp.h>
@@ -227,50 +228,53 @@ float or_signed_angle(const float my[3], const float other[3]) {
   return orth >= 0.0f ? ang : -ang;
 }
 
-/* Three standard normals for (seed, env, particle id, step, tag): a full
- * Box-Muller pair from Philox words 0/1, the cosine leg of words 2/3. */
-static float bm_radius(uint32_t r) {
-  float u = (float)(r >> 9) + 0.5f;
-  u = u * 1.1920928955078125e-07f; /* 2^-23 : u in (0, 1) */
-  return sqrtf(-2.0f * or_logf(u));
+/* One standard normal from one 32-bit Philox word: the engine's
+ * piecewise-linear inverse normal CDF (swarm_device.cuh:normal_from_word,
+ * table include/swarm_normal_table.h from tools/make_normal_table.py):
+ * t = r < 2^31 ? r : 2^32 - 1 - r, x = fp32(t) + 0.5, bin k from x's
+ * exponent and top 6 mantissa bits, f the next 17 bits, z = fma(d, f, a),
+ * the sign r's top bit.  The reference's thermostat draws ESPResSo's own
+ * Gaussian stream (espresso.py:1179-1186), unknowable here: noisy
+ * trajectories are pinned statistically. */
+static const float ntab[2 * SWARM_NTAB_BINS] = {SWARM_NTAB_DATA};
+
+float or_normal_from_word(uint32_t r) {
+  uint32_t m = (uint32_t)((int32_t)r >> 31);
+  uint32_t t = (r ^ m) & 0x7FFFFFFFu;
+  float x = (float)t + 0.5f;
+  uint32_t b = bits_from_f(x);
+  uint32_t k = (b >> 17) - (126u << 6);
+  float f = f_from_bits(((b & 0x1FFFFu) << 6) | 0x3F800000u) - 1.0f;
+  float z = fmaf(ntab[2 * k + 1], f, ntab[2 * k]);
+  return f_from_bits(bits_from_f(z) ^ (~m & 0x80000000u));
 }
 
+/* Three standard normals for (seed, env, particle id, step, tag): Philox
+ * words 0, 1, 2. */
 void or_normals3(uint64_t seed, uint32_t env, uint32_t id, uint64_t step,
                  uint32_t tag, float out[3]) {
   uint32_t ctr[4] = {id, (uint32_t)step, (uint32_t)(step >> 32), tag};
   uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32) ^ env};
   uint32_t r[4];
   or_philox4x32_10(ctr, key, r);
-  float rad0 = bm_radius(r[0]);
-  float rad1 = bm_radius(r[2]);
-  float s0, c0, s1, c1;
-  or_sincos_turn(r[1], &s0, &c0);
-  or_sincos_turn(r[3], &s1, &c1);
-  out[0] = rad0 * c0;
-  out[1] = rad0 * s0;
-  out[2] = rad1 * c1;
+  out[0] = or_normal_from_word(r[0]);
+  out[1] = or_normal_from_word(r[1]);
+  out[2] = or_normal_from_word(r[2]);
 }
 
 /* Translation/rotation normals of sub-step t (the tag-0 stream; the
  * engine's swarm_device.cuh StepNoise): sub-steps 4g..4g+3 take the twelve
  * normals of three Philox blocks with counter (id, g lo, g hi, 0x10 + b),
- * block b giving two full Box-Muller pairs (words 0/1, then 2/3: cosine
- * leg, sine leg); sub-step t takes normals 3j..3j+2 of its group, j = t & 3. */
+ * block b giving one normal per word; sub-step t takes normals 3j..3j+2 of
+ * its group, j = t & 3. */
 static void group_block(uint64_t seed, uint32_t env, uint32_t id, uint64_t g,
                         uint32_t b, float n[4]) {
   uint32_t ctr[4] = {id, (uint32_t)g, (uint32_t)(g >> 32), 0x10u + b};
   uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32) ^ env};
   uint32_t r[4];
   or_philox4x32_10(ctr, key, r);
-  float rad0 = bm_radius(r[0]);
-  float rad1 = bm_radius(r[2]);
-  float s0, c0, s1, c1;
-  or_sincos_turn(r[1], &s0, &c0);
-  or_sincos_turn(r[3], &s1, &c1);
-  n[0] = rad0 * c0;
-  n[1] = rad0 * s0;
-  n[2] = rad1 * c1;
-  n[3] = rad1 * s1;
+  for (int w = 0; w < 4; ++w)
+    n[w] = or_normal_from_word(r[w]);
 }
 
 void or_step_normals(uint64_t seed, uint32_t env, uint32_t id, uint64_t t,

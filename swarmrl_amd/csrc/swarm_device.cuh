@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/swarm_normal_table.h"
+
 namespace swarm {
 
 // ---------------------------------------------------------------- Philox
@@ -157,14 +159,34 @@ __device__ __forceinline__ float acosf_fixed(float x) {
   return x < 0.0f ? 3.14159265358979323846f - two_a : two_a;
 }
 
-// Three standard normals from one Philox block: a full Box-Muller pair from
-// words (x, y) and the cosine leg of a second pair from (z, w).
-__device__ __forceinline__ float bm_radius(uint32_t r) {
-  float u = (float)(r >> 9) + 0.5f;
-  u = u * 1.1920928955078125e-07f;  // 2^-23: u in (0, 1)
-  return sqrt_pos(-2.0f * logf_fixed(u));
+// One standard normal from one 32-bit Philox word (round 6): a
+// piecewise-linear inverse normal CDF over 2112 bins (64 per octave of the
+// word's distance from the middle), tabulated by tools/make_normal_table.py
+// into include/swarm_normal_table.h and shared with the oracle
+// (oracle/swarm_oracle.c:normal_from_word): |z - Phi^-1(u)| <= 1.3e-5,
+// tails to 6.4 sigma.  ~11 instructions and one cached table load per
+// normal, where Box-Muller took a fixed-polynomial log, a correctly rounded
+// sqrt and a sin/cos polynomial per pair (~32 instructions per normal; 41 %
+// of the throughput run kernel's sub-step).
+//   t = r < 2^31 ? r : 2^32 - 1 - r    (r's top bit is the sign)
+//   x = fp32(t) + 0.5                  (in (0, 2^31])
+//   bin k from x's exponent and top 6 mantissa bits, f the next 17 bits
+//   z = fma(d_k, f, a_k)
+__constant__ float kNtab[2 * SWARM_NTAB_BINS] = {SWARM_NTAB_DATA};
+
+__device__ __forceinline__ float normal_from_word(uint32_t r) {
+  const uint32_t m = (uint32_t)((int32_t)r >> 31);
+  const uint32_t t = (r ^ m) & 0x7FFFFFFFu;
+  const float x = __uint2float_rn(t) + 0.5f;
+  const uint32_t b = __float_as_uint(x);
+  const uint32_t k = (b >> 17) - (126u << 6);
+  const float f = __uint_as_float(((b & 0x1FFFFu) << 6) | 0x3F800000u) - 1.0f;
+  const float2 ad = reinterpret_cast<const float2*>(kNtab)[k];
+  const float z = __builtin_fmaf(ad.y, f, ad.x);
+  return __uint_as_float(__float_as_uint(z) ^ (~m & 0x80000000u));
 }
 
+// Three standard normals from one Philox block (words x, y, z).
 __device__ __forceinline__ void normals3(uint32_t k0, uint32_t k1, uint32_t id,
                                          uint64_t step, uint32_t tag, float g[3]) {
   u32x4 c;
@@ -173,23 +195,17 @@ __device__ __forceinline__ void normals3(uint32_t k0, uint32_t k1, uint32_t id,
   c.z = (uint32_t)(step >> 32);
   c.w = tag;
   const u32x4 r = philox4x32_10(c, k0, k1);
-  const float rad0 = bm_radius(r.x);
-  const float rad1 = bm_radius(r.z);
-  float s0, c0, s1, c1;
-  sincos_turn(r.y, &s0, &c0);
-  sincos_turn(r.w, &s1, &c1);
-  g[0] = rad0 * c0;
-  g[1] = rad0 * s0;
-  g[2] = rad1 * c1;
+  g[0] = normal_from_word(r.x);
+  g[1] = normal_from_word(r.y);
+  g[2] = normal_from_word(r.z);
 }
 
 // Translation/rotation normals of the Brownian step (tag 0 stream), all
 // four Philox words used: sub-steps t = 4 g .. 4 g + 3 ("group" g) take the
 // twelve normals n[0..11] of three Philox blocks with counter (id, g lo,
-// g hi, kGroupTag + b), b = 0, 1, 2; block b gives n[4b..4b+3] as two full
-// Box-Muller pairs (words x/y, then z/w: cosine leg, sine leg).  Sub-step t
-// takes n[3j..3j+2], j = t & 3.  Per sub-step 0.75 Philox blocks and 1.5
-// Box-Muller pairs (three normals per block before: one block, two pairs).
+// g hi, kGroupTag + b), b = 0, 1, 2; block b gives n[4b..4b+3], one per
+// word.  Sub-step t takes n[3j..3j+2], j = t & 3.  Per sub-step 0.75 Philox
+// blocks.
 constexpr uint32_t kGroupTag = 0x10u;
 
 // the four normals of block b of group g
@@ -201,15 +217,10 @@ __device__ __forceinline__ void group_block(uint32_t k0, uint32_t k1, uint32_t i
   c.z = (uint32_t)(g >> 32);
   c.w = kGroupTag + b;
   const u32x4 r = philox4x32_10(c, k0, k1);
-  const float rad0 = bm_radius(r.x);
-  const float rad1 = bm_radius(r.z);
-  float s0, c0, s1, c1;
-  sincos_turn(r.y, &s0, &c0);
-  sincos_turn(r.w, &s1, &c1);
-  n[0] = rad0 * c0;
-  n[1] = rad0 * s0;
-  n[2] = rad1 * c1;
-  n[3] = rad1 * s1;
+  n[0] = normal_from_word(r.x);
+  n[1] = normal_from_word(r.y);
+  n[2] = normal_from_word(r.z);
+  n[3] = normal_from_word(r.w);
 }
 
 // The normals of consecutive sub-steps: next(t) returns sub-step t's three,

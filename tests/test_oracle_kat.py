@@ -430,3 +430,42 @@ def test_oracle_threads_do_not_change_dynamics(oracle_mod):
     oracle_mod.set_threads(1)
     for k in ("q", "img", "ang"):
         assert np.array_equal(outs[0][k], outs[1][k])
+
+
+def test_normal_from_word_is_the_inverse_cdf(oracle_mod):
+    """The word -> normal transform (round 6, tools/make_normal_table.py)
+    is the inverse normal CDF of the word's centre to 2e-5, antisymmetric
+    (the top bit is the sign), monotone in the word, and its tails reach
+    6.3 sigma at the extreme words."""
+    from scipy.special import ndtri
+
+    rng = np.random.default_rng(11)
+    r = np.concatenate([rng.integers(0, 2**32, 20000, dtype=np.uint64),
+                        np.array([0, 1, 2, 2**31 - 1, 2**31, 2**32 - 2, 2**32 - 1], np.uint64)])
+    z = np.array([oracle_mod.normal_from_word(int(w)) for w in r])
+    u = (r.astype(np.float64) + 0.5) / 2.0**32
+    assert np.max(np.abs(z - ndtri(u))) < 2e-5
+    for w in (0, 5, 12345, 2**20, 2**31 - 1):  # w and its mirror 2^32 - 1 - w
+        assert oracle_mod.normal_from_word(w) == -oracle_mod.normal_from_word(2**32 - 1 - w)
+    srt = np.sort(r)
+    zs = np.array([oracle_mod.normal_from_word(int(w)) for w in srt])
+    assert np.all(np.diff(zs) >= 0)
+    assert oracle_mod.normal_from_word(0) < -6.3 and oracle_mod.normal_from_word(2**32 - 1) > 6.3
+
+
+def test_normal_table_header_is_generated():
+    """include/swarm_normal_table.h is what tools/make_normal_table.py
+    writes (the table the engine and the oracle share)."""
+    import importlib.util
+
+    from conftest import ROOT
+
+    spec = importlib.util.spec_from_file_location("mnt", ROOT / "tools" / "make_normal_table.py")
+    mnt = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mnt)
+    a, d = mnt.table()
+    text = (ROOT / "include" / "swarm_normal_table.h").read_text()
+    body = text.split("#define SWARM_NTAB_DATA", 1)[1].replace("\\", " ")
+    vals = np.array([float.fromhex(v.strip()[:-1]) for v in body.split(",") if v.strip()],
+                    np.float32)
+    assert np.array_equal(vals[0::2], a) and np.array_equal(vals[1::2], d)
