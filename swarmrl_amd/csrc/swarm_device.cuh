@@ -174,14 +174,19 @@ __device__ __forceinline__ float acosf_fixed(float x) {
 //   z = fma(d_k, f, a_k)
 __constant__ float kNtab[2 * SWARM_NTAB_BINS] = {SWARM_NTAB_DATA};
 
-__device__ __forceinline__ float normal_from_word(uint32_t r) {
+__device__ __forceinline__ const float2* ntab_global() {
+  return reinterpret_cast<const float2*>(kNtab);
+}
+
+// tab: the table (kNtab, or a copy in the caller's LDS)
+__device__ __forceinline__ float normal_from_word(uint32_t r, const float2* tab = ntab_global()) {
   const uint32_t m = (uint32_t)((int32_t)r >> 31);
   const uint32_t t = (r ^ m) & 0x7FFFFFFFu;
   const float x = __uint2float_rn(t) + 0.5f;
   const uint32_t b = __float_as_uint(x);
   const uint32_t k = (b >> 17) - (126u << 6);
   const float f = __uint_as_float(((b & 0x1FFFFu) << 6) | 0x3F800000u) - 1.0f;
-  const float2 ad = reinterpret_cast<const float2*>(kNtab)[k];
+  const float2 ad = tab[k];
   const float z = __builtin_fmaf(ad.y, f, ad.x);
   return __uint_as_float(__float_as_uint(z) ^ (~m & 0x80000000u));
 }
@@ -210,42 +215,45 @@ constexpr uint32_t kGroupTag = 0x10u;
 
 // the four normals of block b of group g
 __device__ __forceinline__ void group_block(uint32_t k0, uint32_t k1, uint32_t id, uint64_t g,
-                                            uint32_t b, float n[4]) {
+                                            uint32_t b, float n[4],
+                                            const float2* tab = ntab_global()) {
   u32x4 c;
   c.x = id;
   c.y = (uint32_t)g;
   c.z = (uint32_t)(g >> 32);
   c.w = kGroupTag + b;
   const u32x4 r = philox4x32_10(c, k0, k1);
-  n[0] = normal_from_word(r.x);
-  n[1] = normal_from_word(r.y);
-  n[2] = normal_from_word(r.z);
-  n[3] = normal_from_word(r.w);
+  n[0] = normal_from_word(r.x, tab);
+  n[1] = normal_from_word(r.y, tab);
+  n[2] = normal_from_word(r.z, tab);
+  n[3] = normal_from_word(r.w, tab);
 }
 
 // The normals of consecutive sub-steps: next(t) returns sub-step t's three,
 // generating a block only when the group reaches it and carrying the rest
 // (at most three floats).  fresh: t does not follow the previous call (the
 // first sub-step of a window), so the blocks it shares are drawn again.
+// tab: the normal table (global, or the throughput run kernel's LDS copy).
 struct StepNoise {
   float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f;
+  const float2* tab = ntab_global();
   __device__ __forceinline__ void next(uint32_t k0, uint32_t k1, uint32_t id, uint64_t t,
                                        bool fresh, float g[3]) {
     const uint32_t j = (uint32_t)t & 3u;
     const uint64_t grp = t >> 2;
     float n[4];
     if (j == 0u) {
-      group_block(k0, k1, id, grp, 0u, n);
+      group_block(k0, k1, id, grp, 0u, n, tab);
       g[0] = n[0];
       g[1] = n[1];
       g[2] = n[2];
       c0 = n[3];
     } else if (j == 1u) {
       if (fresh) {
-        group_block(k0, k1, id, grp, 0u, n);
+        group_block(k0, k1, id, grp, 0u, n, tab);
         c0 = n[3];
       }
-      group_block(k0, k1, id, grp, 1u, n);
+      group_block(k0, k1, id, grp, 1u, n, tab);
       g[0] = c0;
       g[1] = n[0];
       g[2] = n[1];
@@ -253,11 +261,11 @@ struct StepNoise {
       c1 = n[3];
     } else if (j == 2u) {
       if (fresh) {
-        group_block(k0, k1, id, grp, 1u, n);
+        group_block(k0, k1, id, grp, 1u, n, tab);
         c0 = n[2];
         c1 = n[3];
       }
-      group_block(k0, k1, id, grp, 2u, n);
+      group_block(k0, k1, id, grp, 2u, n, tab);
       g[0] = c0;
       g[1] = c1;
       g[2] = n[0];
@@ -266,7 +274,7 @@ struct StepNoise {
       c2 = n[3];
     } else {
       if (fresh) {
-        group_block(k0, k1, id, grp, 2u, n);
+        group_block(k0, k1, id, grp, 2u, n, tab);
         c0 = n[1];
         c1 = n[2];
         c2 = n[3];

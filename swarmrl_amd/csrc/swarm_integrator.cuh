@@ -3241,7 +3241,8 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
                                          int gw, int lane,
                                          unsigned long long* lacc_x, unsigned long long* lacc_y,
                                          const PairTables& pt, int par,
-                                         HelperLds hl = HelperLds{}) {
+                                         HelperLds hl = HelperLds{},
+                                         const float2* ntab = ntab_global()) {
   // the sub-step schedule for latency-bound waves (the wide kernel, which
   // also takes the two-pass variant); the throughput kernel, bound by VALU
   // issue over many waves, keeps the plain one (fewer registers, no spill)
@@ -3319,6 +3320,7 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
   const float* tcol = kTable ? table + noise_index(M, gi, 0, 0) : nullptr;
   float gn[3] = {0.0f, 0.0f, 0.0f};
   StepNoise noise;  // !kTable: the window's normals drawn here, group by group
+  noise.tab = ntab;
   if (kTable) {  // idle lanes read particle 0's (never stored)
     gn[0] = tcol[0];
     gn[1] = tcol[ts];
@@ -3683,16 +3685,17 @@ __device__ __forceinline__ void run_wave_dispatch(const Derived* __restrict__ d,
                                                   unsigned long long* lacc_x,
                                                   unsigned long long* lacc_y,
                                                   const PairTables& pt, int par,
-                                                  bool help = false, HelperLds hl = HelperLds{}) {
+                                                  bool help = false, HelperLds hl = HelperLds{},
+                                                  const float2* ntab = ntab_global()) {
   if (table && help)
     run_wave<kMulti, true, kWalls, kTwoPass, true>(d, st, sc, n_envs, n_steps, step0, table, gw,
                                                    lane, lacc_x, lacc_y, pt, par, hl);
   else if (table)
     run_wave<kMulti, true, kWalls, kTwoPass>(d, st, sc, n_envs, n_steps, step0, table, gw, lane,
-                                             lacc_x, lacc_y, pt, par);
+                                             lacc_x, lacc_y, pt, par, HelperLds{}, ntab);
   else
     run_wave<kMulti, false, kWalls, kTwoPass>(d, st, sc, n_envs, n_steps, step0, nullptr, gw, lane,
-                                              lacc_x, lacc_y, pt, par);
+                                              lacc_x, lacc_y, pt, par, HelperLds{}, ntab);
 }
 
 // Launch-duration stamps for measurement (bench.py, swarm_engine_profile
@@ -3737,7 +3740,12 @@ __global__ __launch_bounds__(256, kRunMinBlocks) void k_cluster_run(const Derive
                                                      unsigned long long* __restrict__ tstamp) {
   __shared__ PairTables pt;
   __shared__ unsigned long long lacc[4][2][64];  // int64 force sums (x, y)
+  // the normal table in LDS (16.9 KB): the in-kernel normals' lookups are
+  // scattered 8-byte reads, one per normal (ordered by stage_pair_tables'
+  // barrier)
+  __shared__ float2 ntab_lds[SWARM_NTAB_BINS];
   stamp_start(tstamp);
+  for (int k = threadIdx.x; k < SWARM_NTAB_BINS; k += blockDim.x) ntab_lds[k] = ntab_global()[k];
   stage_pair_tables(d, &pt);
   const int par = window_parity(ctl);
   const uint64_t step0 = ctl[kCtlStep];
@@ -3756,7 +3764,8 @@ __global__ __launch_bounds__(256, kRunMinBlocks) void k_cluster_run(const Derive
   // normally guarantees it) -> the normals are drawn in the kernel
   run_wave_dispatch<kMulti, kWalls>(d, st, sc, n_envs, n_steps, step0,
                                     table_ok ? tables + par * noise_table_words(st.m) : nullptr,
-                                    gw, lane, lacc[wv][0], lacc[wv][1], pt, par);
+                                    gw, lane, lacc[wv][0], lacc[wv][1], pt, par, false,
+                                    HelperLds{}, ntab_lds);
   stamp_end(tstamp);
 }
 
