@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <string>
 
 constexpr int kIters = 512;
 
@@ -161,7 +162,50 @@ __global__ void k_rcp_variants(int variant, unsigned long long* bad, unsigned* f
   if (nb) atomicAdd(bad, nb);
 }
 
-int main() {
+// WRITE_SIZE calibration: the noise table's store
+// patterns over a known byte count.  k_write_f4: one streaming 16-B store
+// per lane at consecutive 16-B addresses (the round-6 fill); k_write_3x4:
+// three streaming 4-B stores per lane at a 48-B lane stride (round 5's).
+// Each writes `bytes` bytes exactly once; rocprofv3 --pmc WRITE_SIZE on
+// `chain_probe --write-cal` gives the counter's reading of each.
+__global__ void k_write_f4(float* __restrict__ out, size_t n4) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n4) {
+    const f32x4 v = {(float)i, 1.0f, 2.0f, 3.0f};
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out) + i);
+  }
+}
+__global__ void k_write_3x4(float* __restrict__ out, size_t n12) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n12) {
+    float* o = out + 12 * i;  // 48-B record group; stores at words 0, 1, 2 (x 4 sub-steps)
+    for (int j = 0; j < 4; ++j) {
+      __builtin_nontemporal_store((float)i, o + 3 * j);
+      __builtin_nontemporal_store(1.0f, o + 3 * j + 1);
+      __builtin_nontemporal_store(2.0f, o + 3 * j + 2);
+    }
+  }
+}
+
+static int write_cal() {
+  const size_t bytes = (size_t)24 << 20;  // C5's table size
+  float* d;
+  if (hipMalloc(&d, bytes)) return 1;
+  for (int rep = 0; rep < 3; ++rep) {
+    hipLaunchKernelGGL(k_write_f4, dim3((unsigned)(bytes / 16 / 256)), dim3(256), 0, 0, d,
+                       bytes / 16);
+    hipLaunchKernelGGL(k_write_3x4, dim3((unsigned)(bytes / 48 / 256)), dim3(256), 0, 0, d,
+                       bytes / 48);
+  }
+  hipDeviceSynchronize();
+  printf("write calibration: %zu bytes per launch of k_write_f4 and k_write_3x4\n", bytes);
+  hipFree(d);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && std::string(argv[1]) == "--write-cal") return write_cal();
   const char* names[] = {"v_fma_f32 dependent",   "v_fma_f32 4 chains",   "v_rcp_f32 dependent",
                          "ds_bpermute dependent", "4 ds_add_u64 + read",  "ballot vote + branch",
                          "v_fma_f64 dependent",   "cvt f32->i32->f32",    "global load chase (L2)",
