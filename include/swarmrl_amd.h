@@ -299,8 +299,10 @@ int swarm_engine_profile_stamps(swarm_engine_t *e, int32_t reset, void *stream, 
  * stamped the same way while profiling (stamp slot k: the k_check after the
  * k-th run node and the next window's build / observable / policy launches
  * up to the next run).  Writes, for slot k and role q (k_check, build sort,
- * vision grid, field, pair search, vision cone, cluster build, policy MLP;
- * *n_roles = 8), us_out[2 (k n_roles + q) + 0 / 1] = the role's earliest
+ * vision grid, field, pair search, vision cone, cluster build, policy MLP,
+ * then three progress marks: pair filter lists tested, pair filter output
+ * reserved, vision-cone bins summed; *n_roles = 11, swarm::kRoles),
+ * us_out[2 (k n_roles + q) + 0 / 1] = the role's earliest
  * start / latest end in microseconds after the k-th run node's end (NaN
  * where the role did not run), for entries below cap.  Waits for the
  * device; reset with swarm_engine_profile_stamps. */
