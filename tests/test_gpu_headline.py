@@ -49,11 +49,13 @@ def _host(traj):
             for k in ("features", "actions", "rewards")}
 
 
-# build-mode switches read at engine creation: the default and the pair
-# search's block-local union-find (SWARMRL_AMD_LOCAL_UF); every mode
-# integrates the same bits
-@pytest.mark.parametrize("mode", [{}, {"SWARMRL_AMD_LOCAL_UF": "1"}],
-                         ids=["default", "local_uf"])
+# switches read at engine creation: the default, the pair search's
+# block-local union-find (SWARMRL_AMD_LOCAL_UF) and the run without its
+# rotation helper waves (SWARMRL_AMD_ROT_HELPER=0: each run wave turns its
+# own directors); every mode integrates the same bits
+@pytest.mark.parametrize("mode", [{}, {"SWARMRL_AMD_LOCAL_UF": "1"},
+                                  {"SWARMRL_AMD_ROT_HELPER": "0"}],
+                         ids=["default", "local_uf", "no_rot_helper"])
 def test_headline_episode_graph_replays_match_oracle(tmp_path, monkeypatch, mode):
     for k, v in mode.items():
         monkeypatch.setenv(k, v)
