@@ -275,7 +275,7 @@ def measure_dims3(args, E, reps, global_reps=0, dims=3, fraction=0.04):
             eng._run(100)
         torch.cuda.current_stream().wait_stream(side)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             eng._run(100)
         graph.replay()
         torch.cuda.synchronize()
@@ -339,7 +339,7 @@ def time_run_kernel(eng, ff, agent, episode_length, replays=3):
     graph = None
     try:
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             eng.integrate(episode_length, ff)
     except RuntimeError as err:  # no event nodes in this HIP: eager episodes instead
         graph = None
@@ -717,11 +717,15 @@ def capture_episode(eng, ff, agent, T):
     warm = agent.trajectory
     agent.reset_trajectory()
     slice_graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(slice_graph):
+    # thread-local capture: a process group's watchdog thread polls its
+    # collectives' events during the capture (global mode fails those
+    # queries: hipErrorStreamCaptureUnsupported, seen on a world-1 RCCL group)
+    with torch.cuda.graph(slice_graph, capture_error_mode="thread_local"):
         eng.integrate(1, ff)
     agent.reset_trajectory()
     episode_graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(episode_graph, pool=slice_graph.pool()):
+    with torch.cuda.graph(episode_graph, pool=slice_graph.pool(),
+                          capture_error_mode="thread_local"):
         # one episode as the trainers run it (episodic_trainer.py:35 ->
         # engine.integrate(episode_length, force_fn))
         eng.integrate(T, ff)

@@ -231,22 +231,20 @@ float or_signed_angle(const float my[3], const float other[3]) {
 /* One standard normal from one 32-bit Philox word: the engine's
  * piecewise-linear inverse normal CDF (swarm_device.cuh:normal_from_word,
  * table include/swarm_normal_table.h from tools/make_normal_table.py):
- * t = r < 2^31 ? r : 2^32 - 1 - r, x = fp32(t) + 0.5, bin k from x's
- * exponent and top 6 mantissa bits, f the next 17 bits, z = fma(d, f, a),
+ * y = fp32(2 t + 1) for t = r's low 31 bits, bin k from y's exponent and
+ * top 6 mantissa bits, m = y's mantissa in [1, 2), |z| = fma(D_k, m, A_k),
  * the sign r's top bit.  The reference's thermostat draws ESPResSo's own
  * Gaussian stream (espresso.py:1179-1186), unknowable here: noisy
  * trajectories are pinned statistically. */
 static const float ntab[2 * SWARM_NTAB_BINS] = {SWARM_NTAB_DATA};
 
 float or_normal_from_word(uint32_t r) {
-  uint32_t m = (uint32_t)((int32_t)r >> 31);
-  uint32_t t = (r ^ m) & 0x7FFFFFFFu;
-  float x = (float)t + 0.5f;
-  uint32_t b = bits_from_f(x);
-  uint32_t k = (b >> 17) - (126u << 6);
-  float f = f_from_bits(((b & 0x1FFFFu) << 6) | 0x3F800000u) - 1.0f;
-  float z = fmaf(ntab[2 * k + 1], f, ntab[2 * k]);
-  return f_from_bits(bits_from_f(z) ^ (~m & 0x80000000u));
+  float y = (float)((r << 1) | 1u);
+  uint32_t b = bits_from_f(y);
+  uint32_t k = (b >> 17) - (127u << 6);
+  float m = f_from_bits((b & 0x007FFFFFu) | 0x3F800000u);
+  float z = fmaf(ntab[2 * k + 1], m, ntab[2 * k]);
+  return f_from_bits((bits_from_f(z) & 0x7FFFFFFFu) | (r & 0x80000000u));
 }
 
 /* Three standard normals for (seed, env, particle id, step, tag): Philox
@@ -699,7 +697,9 @@ int or_bd_run_walls(const swarm_params_t *p, int n, uint32_t *q, int32_t *img,
       const float sigy = noisy ? d.sig_t[sp] * d.inv_sx[1] : 0.0f;
       advance(&q[i], &img[i], f2i32_sat(fmaf(fx, mobx, sigx * g[0])));
       advance(&q[n + i], &img[n + i], f2i32_sat(fmaf(fy, moby, sigy * g[1])));
-      ang[i] = ang[i] + (uint32_t)f2i32(dth * ANG_INV_SCALE);
+      /* the rotation's increment saturates like the translation's
+       * (swarm_integrator.cuh:bd_step, f2i32_sat) */
+      ang[i] = ang[i] + (uint32_t)f2i32_sat(dth * ANG_INV_SCALE);
       if (s == n_steps - 1) {
         float vx = fx * d.inv_gt[sp], vy = fy * d.inv_gt[sp];
         float w = tz * d.inv_gr[sp];

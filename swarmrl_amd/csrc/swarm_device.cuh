@@ -31,9 +31,14 @@ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1
     const uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c.x;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c.z;
     u32x4 n;
-    n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+    if (r == 0) {  // (the first round's x word is wave-uniform: scalar ALU)
+      n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+      n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+    } else {  // three-input XOR in one v_bitop3_b32 (gfx950; two v_xor_b32 otherwise)
+      n.x = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c.y, k0, 0x96);
+      n.z = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c.w, k1, 0x96);
+    }
     n.y = (uint32_t)p1;
-    n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
     n.w = (uint32_t)p0;
     c = n;
   }
@@ -160,18 +165,18 @@ __device__ __forceinline__ float acosf_fixed(float x) {
 }
 
 // One standard normal from one 32-bit Philox word (round 6): a
-// piecewise-linear inverse normal CDF over 2112 bins (64 per octave of the
-// word's distance from the middle), tabulated by tools/make_normal_table.py
-// into include/swarm_normal_table.h and shared with the oracle
-// (oracle/swarm_oracle.c:normal_from_word): |z - Phi^-1(u)| <= 1.3e-5,
-// tails to 6.4 sigma.  ~11 instructions and one cached table load per
-// normal, where Box-Muller took a fixed-polynomial log, a correctly rounded
-// sqrt and a sin/cos polynomial per pair (~32 instructions per normal; 41 %
-// of the throughput run kernel's sub-step).
-//   t = r < 2^31 ? r : 2^32 - 1 - r    (r's top bit is the sign)
-//   x = fp32(t) + 0.5                  (in (0, 2^31])
-//   bin k from x's exponent and top 6 mantissa bits, f the next 17 bits
-//   z = fma(d_k, f, a_k)
+// piecewise-linear inverse normal CDF over 2112 bins (64 per octave),
+// tabulated by tools/make_normal_table.py into include/swarm_normal_table.h
+// and shared with the oracle (oracle/swarm_oracle.c:or_normal_from_word):
+// |z - Phi^-1(u)| <= 1.3e-5, tails to 6.4 sigma.  7 VALU instructions and
+// one table load per normal, where Box-Muller took a fixed-polynomial log, a
+// correctly rounded sqrt and a sin/cos polynomial per pair (~32 per normal;
+// 41 % of the throughput run kernel's sub-step).
+//   y = fp32(2 t + 1), t = r's low 31 bits  (in [1, 2^32]; one v_lshl_or_b32)
+//   bin k from y's exponent and top 6 mantissa bits
+//   m = y's mantissa as a float in [1, 2)   (one v_and_or_b32)
+//   z = fma(D_k, m, A_k) = |Phi^-1((t + 0.5) / 2^32)|, linear within the bin
+//   the sign is r's top bit                  (one v_bfi_b32)
 __constant__ float kNtab[2 * SWARM_NTAB_BINS] = {SWARM_NTAB_DATA};
 
 __device__ __forceinline__ const float2* ntab_global() {
@@ -180,15 +185,13 @@ __device__ __forceinline__ const float2* ntab_global() {
 
 // tab: the table (kNtab, or a copy in the caller's LDS)
 __device__ __forceinline__ float normal_from_word(uint32_t r, const float2* tab = ntab_global()) {
-  const uint32_t m = (uint32_t)((int32_t)r >> 31);
-  const uint32_t t = (r ^ m) & 0x7FFFFFFFu;
-  const float x = __uint2float_rn(t) + 0.5f;
-  const uint32_t b = __float_as_uint(x);
-  const uint32_t k = (b >> 17) - (126u << 6);
-  const float f = __uint_as_float(((b & 0x1FFFFu) << 6) | 0x3F800000u) - 1.0f;
+  const float y = __uint2float_rn((r << 1) | 1u);
+  const uint32_t b = __float_as_uint(y);
+  const uint32_t k = (b >> 17) - (127u << 6);
+  const float m = __uint_as_float((b & 0x007FFFFFu) | 0x3F800000u);
   const float2 ad = tab[k];
-  const float z = __builtin_fmaf(ad.y, f, ad.x);
-  return __uint_as_float(__float_as_uint(z) ^ (~m & 0x80000000u));
+  const float z = __builtin_fmaf(ad.y, m, ad.x);
+  return __uint_as_float((__float_as_uint(z) & 0x7FFFFFFFu) | (r & 0x80000000u));
 }
 
 // Three standard normals from one Philox block (words x, y, z).
@@ -398,6 +401,17 @@ __device__ __forceinline__ void advance(uint32_t& q, int32_t& img, int32_t dq) {
   const uint32_t qn = q + (uint32_t)dq;
   img += dq >= 0 ? (qn < q ? 1 : 0) : (qn > q ? -1 : 0);
   q = qn;
+}
+
+// The same update as one 64-bit add of (img, q) and dq sign-extended:
+// v_add_co_u32 + v_addc_co_u32 and the sign word, three VALU operations
+// where advance takes seven.  For the throughput run kernel, bound by VALU
+// issue (E = 64 run 176 -> 172 us); the latency-bound run keeps advance
+// (E = 1 run 33.9 vs 34.9 us with this form, same box, round 6).
+__device__ __forceinline__ void advance_adc(uint32_t& q, int32_t& img, int32_t dq) {
+  const uint64_t v = (((uint64_t)(uint32_t)img << 32) | q) + (uint64_t)(int64_t)dq;
+  q = (uint32_t)v;
+  img = (int32_t)(uint32_t)(v >> 32);
 }
 
 }  // namespace swarm

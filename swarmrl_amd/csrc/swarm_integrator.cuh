@@ -603,6 +603,7 @@ struct PConst {
   // the translation in fixed-point units per axis (2-D, round 6):
   // mob_dt / sx and sig_t / sx (0 without noise) as fp32 products
   float mobx, moby, sigx, sigy;
+  float sigr;  // sig_r, 0 without noise (the rotation adds sigr g unconditionally)
   bool noisy;
 };
 
@@ -623,6 +624,7 @@ __device__ __forceinline__ PConst load_pconst(const Derived* __restrict__ d, int
   c.moby = c.mob_dt * c.inv_sx1;
   c.sigx = c.noisy ? c.sig_t * c.inv_sx0 : 0.0f;
   c.sigy = c.noisy ? c.sig_t * c.inv_sx1 : 0.0f;
+  c.sigr = c.noisy ? c.sig_r : 0.0f;
   return c;
 }
 
@@ -688,7 +690,7 @@ __device__ __forceinline__ void bd_step(const PConst& c, PState& p, int64_t ax, 
   bd_dq(c, i64_to_f32(ax), i64_to_f32(ay), fs, fex, fey, sn, cs, g, &fx, &fy, &dqx, &dqy);
   advance(p.qx, p.ix, dqx);
   advance(p.qy, p.iy, dqy);
-  p.an = p.an + (uint32_t)f2i32(dth * kAngInvScale);
+  p.an = p.an + (uint32_t)f2i32_sat(dth * kAngInvScale);
   if (last) {
     float v0 = fx * c.inv_gt, v1 = fy * c.inv_gt;
     float om = tz * c.inv_gr;
@@ -723,7 +725,7 @@ __device__ __forceinline__ void bd_translate_f(const PConst& c, PState& p, float
                                                uint32_t k0, uint32_t k1, uint32_t id,
                                                uint64_t step, bool last, float* vx, float* vy,
                                                float* w, const float* g, float sn, float cs,
-                                               Carry* carry = nullptr) {
+                                               Carry* carry = nullptr, bool adc = false) {
   const float F[2] = {fx, fy};
   int32_t dqx, dqy;
   // (without noise sigx = sigy = 0: g is finite, so sig g = +-0 changes no
@@ -733,6 +735,9 @@ __device__ __forceinline__ void bd_translate_f(const PConst& c, PState& p, float
     *carry = Carry{p.qx, p.qy, dqx, dqy};
     p.qx += (uint32_t)dqx;
     p.qy += (uint32_t)dqy;
+  } else if (adc) {  // (a compile-time constant at every call)
+    advance_adc(p.qx, p.ix, dqx);
+    advance_adc(p.qy, p.iy, dqy);
   } else {
     advance(p.qx, p.ix, dqx);
     advance(p.qy, p.iy, dqy);
@@ -757,10 +762,12 @@ __device__ __forceinline__ void bd_translate(const PConst& c, PState& p, int64_t
                                              float fs, float tz, float fex, float fey,
                                              uint32_t k0, uint32_t k1, uint32_t id, uint64_t step,
                                              bool last, float* vx, float* vy, float* w,
-                                             const float* g, float sn, float cs) {
+                                             const float* g, float sn, float cs,
+                                             bool adc = false) {
   float fx, fy;
   i64x2_to_f32(ax, ay, &fx, &fy);
-  bd_translate_f(c, p, fx, fy, fs, tz, fex, fey, k0, k1, id, step, last, vx, vy, w, g, sn, cs);
+  bd_translate_f(c, p, fx, fy, fs, tz, fex, fey, k0, k1, id, step, last, vx, vy, w, g, sn, cs,
+                 nullptr, adc);
 }
 
 // One steepest-descent step of one particle (espresso.py:1163-1168).
@@ -3131,7 +3138,7 @@ __global__ __launch_bounds__(256) void k_noise(const Derived* __restrict__ d, De
 
 // Rotation helper (round 6, latency-bound runs).  A particle's orientation
 // never depends on positions or forces: sub-step s turns it by
-// f2i32((tz tau + sig_r g2_s) 2^32 / 2 pi), so the whole window's directors
+// f2i32_sat((tz tau + sig_r g2_s) 2^32 / 2 pi), so the whole window's directors
 // can be computed apart from the force chain.  In k_cluster_run_wide a
 // second wave of the block (another SIMD of the CU: waves are dealt to the
 // SIMDs in turn) runs the rotation of a run wave's 64 slots and writes each
@@ -3164,8 +3171,8 @@ __device__ __forceinline__ HelperLds helper_lds(unsigned char* base, int slot) {
 // the orientation increment of sub-step s (bd_step's rotation sequence)
 __device__ __forceinline__ uint32_t rot_increment(const PConst& pc, float tzs, float g2) {
   float dth = tzs * pc.rot_dt;
-  if (pc.noisy) dth = dth + pc.sig_r * g2;
-  return (uint32_t)f2i32(dth * kAngInvScale);
+  dth = dth + pc.sigr * g2;  // (+0 without noise: the same increment)
+  return (uint32_t)f2i32_sat(dth * kAngInvScale);
 }
 
 // The helper wave of run wave gw: publishes the directors of sub-steps
@@ -3368,9 +3375,11 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
         an_next = p.an;  // the helper wave turns the directors
         return;
       }
+      // (without noise gt is zero and sigr 0: dth + 0 is the same increment,
+      // and no select)
       float dth = tz * pc.rot_dt;
-      if (pc.noisy) dth = dth + pc.sig_r * gt[2];
-      an_next = p.an + (uint32_t)f2i32(dth * kAngInvScale);
+      dth = dth + pc.sigr * gt[2];
+      an_next = p.an + (uint32_t)f2i32_sat(dth * kAngInvScale);
     };
     // the previous sub-step's displacement (max is order-free)
     auto prev_disp = [&]() __attribute__((always_inline)) {
@@ -3568,8 +3577,9 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
                              dir[0], dir[1], kLast ? nullptr : &carry);
       }
     } else {
+      // (the throughput kernel: the three-operation carry, advance_adc)
       bd_translate(pc, p, ax, ay, fs, tz, fex, fey, k0, k1, (uint32_t)i, step0 + (uint64_t)s,
-                   kLast, &vx, &vy, &om, gt, dir[0], dir[1]);
+                   kLast, &vx, &vy, &om, gt, dir[0], dir[1], kSched == 0);
     }
     if (!kSched || kLast) {  // (else the next sub-step's prev_disp)
       const float ddx = (float)(int32_t)(p.qx - q0x) * sx0;
@@ -3642,10 +3652,13 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
     sc.phase[20] = (uint64_t)npass;
   }
   if (lane == 0) {  // per-wave realtime stamps (100 MHz): entry, end, passes, pairs
+    // (passes | XCC_ID << 16 | HW_ID << 32: which XCD, CU and SIMD ran the wave)
     uint64_t* ws = sc.phase + 32 + 4 * (size_t)gw;
+    const uint32_t hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const uint32_t xcc_id = __builtin_amdgcn_s_getreg((15 << 11) | 20);
     ws[0] = t_wave0;
     ws[1] = __builtin_amdgcn_s_memrealtime();
-    ws[2] = (uint64_t)npass;
+    ws[2] = (uint64_t)npass | ((uint64_t)(xcc_id & 0xffu) << 16) | ((uint64_t)hw_id << 32);
     ws[3] = (uint64_t)np;
   }
 #endif

@@ -153,7 +153,9 @@ class ProximalPolicyLoss(Loss):
             ops.ppo_epoch_grad(*args, out=grad, workspaces=ws)
             torch.cuda.synchronize(features.device)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
+            # (thread-local: a process group's watchdog thread may query
+            # events while this thread captures)
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 for _ in range(self.n_epochs):
                     if adam is not None:
                         ops.ppo_epoch_grad(*args, out=grad, adam=adam, workspaces=ws)

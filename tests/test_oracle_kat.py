@@ -433,24 +433,25 @@ def test_oracle_threads_do_not_change_dynamics(oracle_mod):
 
 
 def test_normal_from_word_is_the_inverse_cdf(oracle_mod):
-    """The word -> normal transform (round 6, tools/make_normal_table.py)
-    is the inverse normal CDF of the word's centre to 2e-5, antisymmetric
-    (the top bit is the sign), monotone in the word, and its tails reach
-    6.3 sigma at the extreme words."""
+    """The word -> normal transform (round 6, tools/make_normal_table.py):
+    the sign is the word's top bit and the magnitude the inverse normal CDF
+    of the low 31 bits' centre, -Phi^-1((t + 0.5) / 2^32), to 2e-5; flipping
+    the top bit negates the normal exactly, the magnitude falls as t grows,
+    and the tails reach 6.3 sigma at t = 0."""
     from scipy.special import ndtri
 
     rng = np.random.default_rng(11)
     r = np.concatenate([rng.integers(0, 2**32, 20000, dtype=np.uint64),
                         np.array([0, 1, 2, 2**31 - 1, 2**31, 2**32 - 2, 2**32 - 1], np.uint64)])
     z = np.array([oracle_mod.normal_from_word(int(w)) for w in r])
-    u = (r.astype(np.float64) + 0.5) / 2.0**32
-    assert np.max(np.abs(z - ndtri(u))) < 2e-5
-    for w in (0, 5, 12345, 2**20, 2**31 - 1):  # w and its mirror 2^32 - 1 - w
-        assert oracle_mod.normal_from_word(w) == -oracle_mod.normal_from_word(2**32 - 1 - w)
-    srt = np.sort(r)
-    zs = np.array([oracle_mod.normal_from_word(int(w)) for w in srt])
-    assert np.all(np.diff(zs) >= 0)
-    assert oracle_mod.normal_from_word(0) < -6.3 and oracle_mod.normal_from_word(2**32 - 1) > 6.3
+    g = -ndtri(((r & 0x7FFFFFFF).astype(np.float64) + 0.5) / 2.0**32)
+    assert np.max(np.abs(z - np.where(r >> 31 != 0, -g, g))) < 2e-5
+    for w in (0, 5, 12345, 2**20, 2**31 - 1):  # w and w with the top bit set
+        assert oracle_mod.normal_from_word(w) == -oracle_mod.normal_from_word(w | 2**31)
+    low = np.sort(r & 0x7FFFFFFF)
+    zs = np.array([oracle_mod.normal_from_word(int(w)) for w in low])
+    assert np.all(zs >= 0) and np.all(np.diff(zs) <= 0)
+    assert oracle_mod.normal_from_word(0) > 6.3 and oracle_mod.normal_from_word(2**31) < -6.3
 
 
 def test_normal_table_header_is_generated():

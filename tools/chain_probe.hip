@@ -126,6 +126,35 @@ __global__ void k_probe(int test, float fa, float fb, unsigned long long* out, f
         PIN(ix);
       }
       break;
+#define FOUR_CHAINS(CASE, ASM)                                   \
+    case CASE: {                                                 \
+      uint32_t a0 = lane, a1 = lane + 1, a2 = lane + 2, a3 = lane + 3; \
+      const uint32_t m = 0xD2511F53u;                            \
+      for (int k = 0; k < kIters / 4; ++k) {                     \
+        ASM(a0);                                                 \
+        ASM(a1);                                                 \
+        ASM(a2);                                                 \
+        ASM(a3);                                                 \
+      }                                                          \
+      ix = (int)(a0 ^ a1 ^ a2 ^ a3);                             \
+      break;                                                     \
+    }
+#define MAD64(a)                                                                         \
+  {                                                                                      \
+    uint64_t r_, c_;                                                                     \
+    __asm__ volatile("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r_), "=s"(c_) : "v"(a), "v"(m)); \
+    a = (uint32_t)r_;                                                                    \
+  }
+#define MULHI(a) __asm__ volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a) : "v"(m))
+#define MULLO(a) __asm__ volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a) : "v"(m))
+#define XOR(a) __asm__ volatile("v_xor_b32 %0, %0, %1" : "+v"(a) : "v"(m))
+#define CVT(a) __asm__ volatile("v_cvt_f32_u32 %0, %0" : "+v"(a))
+    // issue rates of Philox's and the table normals' integer operations
+    FOUR_CHAINS(13, MAD64)
+    FOUR_CHAINS(14, MULHI)
+    FOUR_CHAINS(15, MULLO)
+    FOUR_CHAINS(16, XOR)
+    FOUR_CHAINS(17, CVT)
     case 12:  // DPP row swap (quad_perm [1,0,3,2]) dependent
       for (int k = 0; k < kIters; ++k) {
         ix = __builtin_amdgcn_mov_dpp(ix, 0xB1, 0xF, 0xF, false);
@@ -210,8 +239,10 @@ int main(int argc, char** argv) {
                          "ds_bpermute dependent", "4 ds_add_u64 + read",  "ballot vote + branch",
                          "v_fma_f64 dependent",   "cvt f32->i32->f32",    "global load chase (L2)",
                          "v_add_u32 dependent",   "v_mul_f32 dependent",  "ds_write + ds_read other lane",
-                         "DPP quad swap dependent"};
-  const int ntest = 13;
+                         "DPP quad swap dependent", "v_mad_u64_u32 4 chains",
+                         "v_mul_hi_u32 4 chains",   "v_mul_lo_u32 4 chains", "v_xor_b32 4 chains",
+                         "v_cvt_f32_u32 4 chains"};
+  const int ntest = 18;
   unsigned long long* d_out;
   float* d_sink;
   int* d_chase;

@@ -39,11 +39,24 @@ for rep in range(4):
     dur = (w[:, 1] - w[:, 0]) / 100.0  # us (100 MHz realtime)
     start = (w[:, 0] - t0) / 100.0
     end = (w[:, 1] - t0) / 100.0
+    npass = w[:, 2] & 0xFF
+    xcc = (w[:, 2] >> 16) & 0xFF
+    hw = w[:, 2] >> 32
+    # the SIMD a wave ran on: XCD, shader engine, array, CU, SIMD (HW_ID fields)
+    simd_key = (xcc << 16) | (((hw >> 13) & 7) << 8) | (((hw >> 12) & 1) << 7) | \
+        (((hw >> 8) & 15) << 3) | ((hw >> 4) & 3)
     order = np.argsort(-dur)
     print(f"rep {rep}: {len(w)} waves, span {end.max():.1f} us; duration p50 {np.median(dur):.1f} "
           f"p90 {np.percentile(dur, 90):.1f} max {dur.max():.1f}; start skew max {start.max():.1f}")
     for k in order[:6]:
-        print(f"   wave: start {start[k]:6.1f} dur {dur[k]:6.1f} npass {w[k, 2]} pairs {w[k, 3]}")
-    for p in sorted(set(w[:, 2].tolist())):
-        m = w[:, 2] == p
+        print(f"   wave: start {start[k]:6.1f} dur {dur[k]:6.1f} npass {npass[k]} pairs {w[k, 3]}")
+    keys, inv, cnt = np.unique(simd_key, return_inverse=True, return_counts=True)
+    simd_end = np.zeros(len(keys))
+    np.maximum.at(simd_end, inv, end)
+    print(f"   {len(keys)} SIMDs in {len(np.unique(simd_key >> 2))} CUs; waves per SIMD: " +
+          ", ".join(f"{c}: {n} SIMDs (last end mean {simd_end[cnt == c].mean():.1f} max "
+                    f"{simd_end[cnt == c].max():.1f} us)"
+                    for c, n in zip(*np.unique(cnt, return_counts=True))))
+    for p in sorted(set(npass.tolist())):
+        m = npass == p
         print(f"   npass {p}: {m.sum()} waves, mean {dur[m].mean():.1f} max {dur[m].max():.1f}")
