@@ -149,6 +149,23 @@ __global__ void k_probe(int test, float fa, float fb, unsigned long long* out, f
 #define MULLO(a) __asm__ volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a) : "v"(m))
 #define XOR(a) __asm__ volatile("v_xor_b32 %0, %0, %1" : "+v"(a) : "v"(m))
 #define CVT(a) __asm__ volatile("v_cvt_f32_u32 %0, %0" : "+v"(a))
+#define PK_CHAINS(CASE, INSN)                                              \
+    case CASE: {                                                           \
+      typedef float f2 __attribute__((ext_vector_type(2)));               \
+      f2 a0 = {x, y}, a1 = {z, w}, a2 = {x, w}, a3 = {z, y};               \
+      const f2 m = {fa, fb};                                               \
+      for (int k = 0; k < kIters / 4; ++k) {                               \
+        __asm__ volatile(INSN : "+v"(a0) : "v"(m));                        \
+        __asm__ volatile(INSN : "+v"(a1) : "v"(m));                        \
+        __asm__ volatile(INSN : "+v"(a2) : "v"(m));                        \
+        __asm__ volatile(INSN : "+v"(a3) : "v"(m));                        \
+      }                                                                    \
+      x = a0.x + a1.y + a2.x + a3.y;                                       \
+      break;                                                               \
+    }
+    // packed fp32 (two floats per lane per instruction)
+    PK_CHAINS(18, "v_pk_fma_f32 %0, %0, %1, %1")
+    PK_CHAINS(19, "v_pk_mul_f32 %0, %0, %1")
     // issue rates of Philox's and the table normals' integer operations
     FOUR_CHAINS(13, MAD64)
     FOUR_CHAINS(14, MULHI)
@@ -241,8 +258,9 @@ int main(int argc, char** argv) {
                          "v_add_u32 dependent",   "v_mul_f32 dependent",  "ds_write + ds_read other lane",
                          "DPP quad swap dependent", "v_mad_u64_u32 4 chains",
                          "v_mul_hi_u32 4 chains",   "v_mul_lo_u32 4 chains", "v_xor_b32 4 chains",
-                         "v_cvt_f32_u32 4 chains"};
-  const int ntest = 18;
+                         "v_cvt_f32_u32 4 chains", "v_pk_fma_f32 4 chains",
+                         "v_pk_mul_f32 4 chains"};
+  const int ntest = 20;
   unsigned long long* d_out;
   float* d_sink;
   int* d_chase;
