@@ -113,10 +113,14 @@ __device__ __forceinline__ float logf_fixed(float x) {
 }
 
 // sin/cos of a * 2 pi / 2^32
+// (quadrant q = (a + 2^29) >> 30; the reduced angle is a's low 30 bits
+// sign-extended -- one v_bfe_i32 -- and the quadrant's swap and sign bits
+// are read off a + 2^29 and a + 3 2^29 directly: the same values as the
+// quad arithmetic for every a, checked exhaustively; oracle/swarm_oracle.c
+// or_sincos_turn keeps the quad form)
 __device__ __forceinline__ void sincos_turn(uint32_t a, float* s_out, float* c_out) {
   const uint32_t b = a + 0x20000000u;
-  const uint32_t quad = b >> 30;
-  const int32_t rem = (int32_t)(b & 0x3FFFFFFFu) - 0x20000000;
+  const int32_t rem = ((int32_t)(a << 2)) >> 2;
   const float x = (float)rem * 1.46291807926715968e-09f;
   const float z = x * x;
   float sp = -1.9515295891e-4f;
@@ -131,11 +135,11 @@ __device__ __forceinline__ void sincos_turn(uint32_t a, float* s_out, float* c_o
   const float h = __builtin_fmaf(-0.5f, z, 1.0f);
   const float c = __builtin_fmaf(cp, z, h);
   // quadrant rotation: a swap and two sign flips on the float bits (exact)
-  const bool swap = (quad & 1u) != 0u;
+  const bool swap = (b & 0x40000000u) != 0u;
   const float so0 = swap ? c : s;
   const float co0 = swap ? s : c;
-  const float so = __uint_as_float(__float_as_uint(so0) ^ ((quad >> 1) << 31));
-  const float co = __uint_as_float(__float_as_uint(co0) ^ (((quad ^ (quad >> 1)) & 1u) << 31));
+  const float so = __uint_as_float(__float_as_uint(so0) ^ (b & 0x80000000u));
+  const float co = __uint_as_float(__float_as_uint(co0) ^ ((a + 0x60000000u) & 0x80000000u));
   *s_out = so;
   *c_out = co;
 }

@@ -3241,6 +3241,21 @@ __device__ __forceinline__ void rot_helper(const Derived* __restrict__ d, const 
 // kMulti = false: one species, so the pair constants are wave-uniform scalars.
 // kTwoPass: waves with 65-128 pairs get their own unrolled two-pass variant
 // (else the general up-to-four-pass loop).
+// *p -= v on LDS words, no return (ds_sub_u64).  Ordering: a wave's LDS
+// instructions execute in issue order (one instruction for all 64 lanes), so
+// the force sums' read-back issued after it sees it; the memory clobber keeps
+// the compiler from moving LDS accesses across it.
+// px[0] -= vx and px[64] -= vy: the x and y force sums of one slot (the
+// run kernels' lacc[wave][2][64] rows, y 512 bytes after x).
+__device__ __forceinline__ void lds_sub_u64_xy(unsigned long long* px, unsigned long long vx,
+                                               unsigned long long vy) {
+  const uint32_t addr = (uint32_t)(uintptr_t)px;  // the LDS offset (low word of the flat address)
+  __asm__ volatile("ds_sub_u64 %0, %1\n\tds_sub_u64 %0, %2 offset:512"
+                   :
+                   : "v"(addr), "v"(vx), "v"(vy)
+                   : "memory");
+}
+
 template <bool kMulti, bool kTable, bool kWalls, bool kTwoPass = false, bool kHelper = false>
 __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const DevState& st,
                                          const Scratch& sc, int n_envs, int n_steps,
@@ -3474,10 +3489,16 @@ __device__ __forceinline__ void run_wave(const Derived* __restrict__ d, const De
           }
           atomicAdd(&lacc_x[a], (unsigned long long)fx);
           atomicAdd(&lacc_y[a], (unsigned long long)fy);
-          // b: the exact negation (written as a subtract; the compiler still
-          // emits ds_add_u64 of the negated value)
-          atomicSub(&lacc_x[b], (unsigned long long)fx);
-          atomicSub(&lacc_y[b], (unsigned long long)fy);
+          // b: the exact negation.  The throughput kernel issues ds_sub_u64
+          // itself (lds_sub_u64); atomicSub compiles to ds_add_u64 of the
+          // negated value, a 64-bit negation (two VALU operations and a
+          // hazard wait) per component and pass
+          if (kSched == 0) {
+            lds_sub_u64_xy(&lacc_x[b], (unsigned long long)fx, (unsigned long long)fy);
+          } else {
+            atomicSub(&lacc_x[b], (unsigned long long)fx);
+            atomicSub(&lacc_y[b], (unsigned long long)fy);
+          }
         }
       }
     }
