@@ -470,3 +470,24 @@ def test_normal_table_header_is_generated():
     vals = np.array([float.fromhex(v.strip()[:-1]) for v in body.split(",") if v.strip()],
                     np.float32)
     assert np.array_equal(vals[0::2], a) and np.array_equal(vals[1::2], d)
+
+
+def test_normal_table_numpy_restatement_matches_oracle(oracle_mod):
+    """tools/make_normal_table.py's numpy transform (the generator's own
+    accuracy check) and the C oracle's or_normal_from_word give the same
+    fp32 bits for the same words (edge words included)."""
+    import importlib.util
+
+    from conftest import ROOT
+
+    spec = importlib.util.spec_from_file_location("mnt", ROOT / "tools" / "make_normal_table.py")
+    mnt = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mnt)
+    a, d = mnt.table()
+    rng = np.random.default_rng(5)
+    r = np.concatenate([rng.integers(0, 2**32, 4000, dtype=np.uint64),
+                        np.array([0, 1, 2**31 - 1, 2**31, 2**31 + 1, 2**32 - 1], np.uint64)])
+    z_np = mnt.transform(r.astype(np.uint32), a, d)
+    z_c = np.array([oracle_mod.normal_from_word(int(w)) for w in r], np.float32)
+    assert np.array_equal(z_np.view(np.uint32), z_c.view(np.uint32))
+
