@@ -23,7 +23,8 @@ SRC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "swarmrl_am
 COMPONENT = {
     "philox4x32_10": "philox",
     "bm_radius": "box_muller", "logf_fixed": "box_muller", "sqrt_pos": "box_muller",
-    "group_block": "box_muller", "normals3": "box_muller", "next": "noise_select",
+    "group_block": "normals", "normals3": "normals", "normal_from_word": "normals",
+    "next": "noise_select",
     "sincos_turn": "sincos",
     "pair_force": "pair_force", "pair_fix_sel": "pair_force", "f2fix24": "pair_force",
     "bd_translate": "bd_update", "bd_step": "bd_update", "advance": "bd_update",
